@@ -1,0 +1,317 @@
+// bf16 GEMM on gfx950 MFMA with fused epilogues.
+//
+//   C[M, N] = epi( A[M, K] · W[N, K]^T )       (nn.Linear layout: both operands K-contiguous)
+//
+// Design (MI355X-first, see /opt/skills/guides/cdna_hip_programming.md §5):
+//  * v_mfma_f32_16x16x32_bf16, 4 waves per workgroup, each wave owns a (BM/WM)x(BN/WN) sub-tile
+//    indexed by fragment repeat (acc[FM][FN]), never by wave position.
+//  * BK = 64, double-buffered LDS with register-staged prefetch (issue global loads for tile t+1
+//    before the MFMAs of tile t, write them to the other LDS buffer after: Guideline 15 / T14).
+//  * LDS rows are 128 B; 16-B chunks XOR-swizzled by ((row>>1)&7) so the 16 rows read by one
+//    ds_read_b128 lane group land on 16 distinct slots of the 256-B bank row (conflict-free).
+//  * bijective XCD remap + grouped-M tile order so neighbouring tiles share an XCD L2 (T1).
+//  * epilogue staged through LDS in fp32, then 16-B coalesced stores with bias / GELU / SwiGLU /
+//    residual fused (the reference outsources all of this to OpenAI).
+//  * split-K writes fp32 partials; gemm_splitk_reduce applies the same epilogue.
+#include "common.h"
+
+enum Epi : int {
+  EPI_NONE = 0,
+  EPI_BIAS = 1,
+  EPI_GELU = 2,       // bias (optional) + exact GELU (BERT)
+  EPI_SWIGLU = 3,     // W rows interleaved in 16-row (gate, up) groups; out N/2 = silu(g)*u
+  EPI_RESID = 4,      // bias (optional) + residual add
+  EPI_PARTIAL = 5,    // fp32 split-K partial to workspace
+};
+
+struct GemmArgs {
+  const bf16_t* A; const bf16_t* W; bf16_t* C;
+  const bf16_t* bias; const bf16_t* resid; float* ws;
+  int M, N, K, lda, ldc, ldr, k_per_split;
+};
+
+template <int BM, int BN, int WM, int WN, int EPI>
+__global__ void __launch_bounds__(256)
+gemm_bf16_kernel(GemmArgs p) {
+  constexpr int BK = 64;
+  constexpr int TM = BM / WM, TN = BN / WN;
+  constexpr int FM = TM / 16, FN = TN / 16;
+  constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2;
+  constexpr int LA = BM * 8 / 256, LB = BN * 8 / 256;  // 16-B loads per thread per tile
+  static_assert(WM * WN == 4, "4 waves");
+  static_assert(LA >= 1 && LB >= 1, "tile too small");
+  constexpr int STAGE_FLOATS = 4 * TM * (TN + 4);
+  constexpr int LDS_MAIN = 2 * (A_BYTES + B_BYTES);
+  constexpr int LDS_BYTES = LDS_MAIN > STAGE_FLOATS * 4 ? LDS_MAIN : STAGE_FLOATS * 4;
+  __shared__ __attribute__((aligned(16))) char smem[LDS_BYTES];
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid / WN, wn = wid % WN;
+
+  // ---- tile scheduling: XCD remap, then grouped-M ordering ----
+  const int ntm = (p.M + BM - 1) / BM, ntn = (p.N + BN - 1) / BN;
+  const int nwg = ntm * ntn;
+  const int t = xcd_remap(blockIdx.x, nwg);
+  constexpr int GROUP = 8;
+  const int gid = t / (GROUP * ntn);
+  const int first_m = gid * GROUP;
+  const int gsz = min(ntm - first_m, GROUP);
+  const int tin = t % (GROUP * ntn);
+  const int tm = first_m + tin % gsz, tn = tin / gsz;
+  const int m0 = tm * BM, n0 = tn * BN;
+
+  const int kbeg = blockIdx.z * p.k_per_split;
+  const int nk = p.k_per_split / BK;
+
+  // ---- global -> register staging ----
+  u32x4_t ra[LA], rb[LB];
+  auto gload = [&](int kt) {
+    const int k0 = kbeg + kt * BK;
+#pragma unroll
+    for (int i = 0; i < LA; ++i) {
+      const int idx = tid + 256 * i, r = idx >> 3, c = idx & 7;
+      const int gm = m0 + r;
+      if (gm < p.M) ra[i] = *(const u32x4_t*)(p.A + (size_t)gm * p.lda + k0 + c * 8);
+      else ra[i] = u32x4_t{0, 0, 0, 0};
+    }
+#pragma unroll
+    for (int i = 0; i < LB; ++i) {
+      const int idx = tid + 256 * i, r = idx >> 3, c = idx & 7;
+      const int gn = n0 + r;
+      if (gn < p.N) rb[i] = *(const u32x4_t*)(p.W + (size_t)gn * p.K + k0 + c * 8);
+      else rb[i] = u32x4_t{0, 0, 0, 0};
+    }
+  };
+  auto lstore = [&](int buf) {
+    char* sa = smem + buf * (A_BYTES + B_BYTES);
+    char* sb = sa + A_BYTES;
+#pragma unroll
+    for (int i = 0; i < LA; ++i) {
+      const int idx = tid + 256 * i, r = idx >> 3, c = idx & 7;
+      *(u32x4_t*)(sa + r * 128 + ((c ^ ((r >> 1) & 7)) << 4)) = ra[i];
+    }
+#pragma unroll
+    for (int i = 0; i < LB; ++i) {
+      const int idx = tid + 256 * i, r = idx >> 3, c = idx & 7;
+      *(u32x4_t*)(sb + r * 128 + ((c ^ ((r >> 1) & 7)) << 4)) = rb[i];
+    }
+  };
+
+  f32x4_t acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  if (nk > 0) {
+    gload(0);
+    lstore(0);
+  }
+  __syncthreads();
+
+  const int fr = lane & 15, fg = lane >> 4;
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) gload(kt + 1);
+    const char* sa = smem + cur * (A_BYTES + B_BYTES);
+    const char* sb = sa + A_BYTES;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const int c = kk * 4 + fg;
+      bf16x8_t af[FM], bfr[FN];
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+        const int r = wm * TM + i * 16 + fr;
+        af[i] = *(const bf16x8_t*)(sa + r * 128 + ((c ^ ((r >> 1) & 7)) << 4));
+      }
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int r = wn * TN + j * 16 + fr;
+        bfr[j] = *(const bf16x8_t*)(sb + r * 128 + ((c ^ ((r >> 1) & 7)) << 4));
+      }
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) acc[i][j] = mfma16(af[i], bfr[j], acc[i][j]);
+    }
+    if (kt + 1 < nk) lstore(cur ^ 1);
+    __syncthreads();
+  }
+
+  // ---- epilogue: stage fp32 tile of this wave in LDS, then coalesced 16-B stores ----
+  float* st = (float*)smem + wid * TM * (TN + 4);
+  constexpr int SLD = TN + 4;
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) st[(i * 16 + fg * 4 + q) * SLD + j * 16 + fr] = acc[i][j][q];
+  __syncthreads();
+
+  const int row0 = m0 + wm * TM, col0 = n0 + wn * TN;
+  if constexpr (EPI == EPI_SWIGLU) {
+    // output tile TM x TN/2; chunk of 8 outputs; TN/16 chunks per row
+    constexpr int CPR = TN / 16;
+    constexpr int RPI = 64 / CPR;
+    const int oc = (lane % CPR) * 8;          // output col within wave tile
+    const int grp = oc / 16, within = oc % 16;  // gate cols 32*grp+within.., up cols +16
+    const int ncols_out = p.N / 2;
+    const int gout = col0 / 2 + oc;
+    for (int rr = lane / CPR; rr < TM; rr += RPI) {
+      const int gm = row0 + rr;
+      if (gm >= p.M || gout >= ncols_out) continue;
+      const float* srow = st + rr * SLD + grp * 32 + within;
+      unsigned packed[4];
+#pragma unroll
+      for (int e = 0; e < 8; e += 2) {
+        float g0 = srow[e], g1 = srow[e + 1], u0 = srow[16 + e], u1 = srow[16 + e + 1];
+        packed[e / 2] = pack_bf2(silu(g0) * u0, silu(g1) * u1);
+      }
+      *(u32x4_t*)(p.C + (size_t)gm * p.ldc + gout) = u32x4_t{packed[0], packed[1], packed[2], packed[3]};
+    }
+  } else {
+    constexpr int CPR = TN / 8;
+    constexpr int RPI = 64 / CPR;
+    const int cc = (lane % CPR) * 8;
+    const int gn = col0 + cc;
+    for (int rr = lane / CPR; rr < TM; rr += RPI) {
+      const int gm = row0 + rr;
+      if (gm >= p.M || gn >= p.N) continue;
+      const float* srow = st + rr * SLD + cc;
+      float v[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = srow[e];
+      if constexpr (EPI == EPI_PARTIAL) {
+        float* dst = p.ws + ((size_t)blockIdx.z * p.M + gm) * p.N + gn;
+        *(f32x4_t*)dst = f32x4_t{v[0], v[1], v[2], v[3]};
+        *(f32x4_t*)(dst + 4) = f32x4_t{v[4], v[5], v[6], v[7]};
+        continue;
+      }
+      if (p.bias) {
+        u32x4_t b = *(const u32x4_t*)(p.bias + gn);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          v[2 * e] += bf2f((bf16_t)(b[e] & 0xffff));
+          v[2 * e + 1] += bf2f((bf16_t)(b[e] >> 16));
+        }
+      }
+      if constexpr (EPI == EPI_GELU) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = gelu_erf(v[e]);
+      }
+      if constexpr (EPI == EPI_RESID) {
+        u32x4_t r = *(const u32x4_t*)(p.resid + (size_t)gm * p.ldr + gn);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          v[2 * e] += bf2f((bf16_t)(r[e] & 0xffff));
+          v[2 * e + 1] += bf2f((bf16_t)(r[e] >> 16));
+        }
+      }
+      *(u32x4_t*)(p.C + (size_t)gm * p.ldc + gn) =
+          u32x4_t{pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3]), pack_bf2(v[4], v[5]), pack_bf2(v[6], v[7])};
+    }
+  }
+}
+
+// Split-K reduction + epilogue. One thread per 8 output elements (16-B stores).
+__global__ void __launch_bounds__(256)
+gemm_splitk_reduce(const float* __restrict__ ws, int splits, int M, int N, int epi,
+                   const bf16_t* __restrict__ bias, const bf16_t* __restrict__ resid, int ldr,
+                   bf16_t* __restrict__ C, int ldc) {
+  const int nout = (epi == EPI_SWIGLU) ? N / 2 : N;
+  const int chunks = nout / 8;
+  const size_t total = (size_t)M * chunks;
+  for (size_t idx = blockIdx.x * (size_t)blockDim.x + threadIdx.x; idx < total;
+       idx += (size_t)gridDim.x * blockDim.x) {
+    const int m = (int)(idx / chunks), oc = (int)(idx % chunks) * 8;
+    float v[8];
+    if (epi == EPI_SWIGLU) {
+      const int grp = oc / 16, within = oc % 16;
+      const int gc = grp * 32 + within;
+      float g[8], u[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) { g[e] = 0.f; u[e] = 0.f; }
+      for (int s = 0; s < splits; ++s) {
+        const float* row = ws + ((size_t)s * M + m) * N;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) { g[e] += row[gc + e]; u[e] += row[gc + 16 + e]; }
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = silu(g[e]) * u[e];
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = 0.f;
+      for (int s = 0; s < splits; ++s) {
+        const float* row = ws + ((size_t)s * M + m) * N + oc;
+        f32x4_t a = *(const f32x4_t*)row, b = *(const f32x4_t*)(row + 4);
+        v[0] += a[0]; v[1] += a[1]; v[2] += a[2]; v[3] += a[3];
+        v[4] += b[0]; v[5] += b[1]; v[6] += b[2]; v[7] += b[3];
+      }
+      if (bias) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] += bf2f(bias[oc + e]);
+      }
+      if (epi == EPI_GELU) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = gelu_erf(v[e]);
+      }
+      if (epi == EPI_RESID) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] += bf2f(resid[(size_t)m * ldr + oc + e]);
+      }
+    }
+    *(u32x4_t*)(C + (size_t)m * ldc + oc) =
+        u32x4_t{pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3]), pack_bf2(v[4], v[5]), pack_bf2(v[6], v[7])};
+  }
+}
+
+template <int BM, int BN, int WM, int WN>
+static int launch_tile(const GemmArgs& a, int epi, int splits, hipStream_t s) {
+  const int ntm = (a.M + BM - 1) / BM, ntn = (a.N + BN - 1) / BN;
+  dim3 grid(ntm * ntn, 1, splits), block(256);
+  switch (splits > 1 ? (int)EPI_PARTIAL : epi) {
+    case EPI_NONE: gemm_bf16_kernel<BM, BN, WM, WN, EPI_NONE><<<grid, block, 0, s>>>(a); break;
+    case EPI_BIAS: gemm_bf16_kernel<BM, BN, WM, WN, EPI_BIAS><<<grid, block, 0, s>>>(a); break;
+    case EPI_GELU: gemm_bf16_kernel<BM, BN, WM, WN, EPI_GELU><<<grid, block, 0, s>>>(a); break;
+    case EPI_SWIGLU: gemm_bf16_kernel<BM, BN, WM, WN, EPI_SWIGLU><<<grid, block, 0, s>>>(a); break;
+    case EPI_RESID: gemm_bf16_kernel<BM, BN, WM, WN, EPI_RESID><<<grid, block, 0, s>>>(a); break;
+    case EPI_PARTIAL: gemm_bf16_kernel<BM, BN, WM, WN, EPI_PARTIAL><<<grid, block, 0, s>>>(a); break;
+    default: return (int)hipErrorInvalidValue;
+  }
+  return (int)hipGetLastError();
+}
+
+// Tile selection: big tiles when the grid fills 256 CUs, skinny tiles (+ split-K) for decode-sized M.
+// tile: 0 = auto, 1 = 128x128, 2 = 64x128, 3 = 32x128.
+DA_EXPORT int da_gemm_bf16(const void* A, int lda, const void* W, void* C, int ldc,
+                           const void* bias, const void* resid, int ldr,
+                           int M, int N, int K, int epi, int tile, int splits, void* ws,
+                           void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  if (K % 64 || N % 8 || lda % 8 || ldc % 8) return (int)hipErrorInvalidValue;
+  if (epi == EPI_SWIGLU && N % 32) return (int)hipErrorInvalidValue;
+  if (splits < 1) splits = 1;
+  if ((K / 64) % splits) return (int)hipErrorInvalidValue;
+  if (splits > 1 && ws == nullptr) return (int)hipErrorInvalidValue;
+  GemmArgs a;
+  a.A = (const bf16_t*)A; a.W = (const bf16_t*)W; a.C = (bf16_t*)C;
+  a.bias = (const bf16_t*)bias; a.resid = (const bf16_t*)resid; a.ws = (float*)ws;
+  a.M = M; a.N = N; a.K = K; a.lda = lda; a.ldc = ldc; a.ldr = ldr; a.k_per_split = K / splits;
+  if (tile == 0) tile = (M <= 32) ? 3 : (M <= 64 ? 2 : 1);
+  int err;
+  switch (tile) {
+    case 1: err = launch_tile<128, 128, 2, 2>(a, epi, splits, s); break;
+    case 2: err = launch_tile<64, 128, 1, 4>(a, epi, splits, s); break;
+    case 3: err = launch_tile<32, 128, 1, 4>(a, epi, splits, s); break;
+    default: return (int)hipErrorInvalidValue;
+  }
+  if (err || splits == 1) return err;
+  const int nout = (epi == EPI_SWIGLU) ? N / 2 : N;
+  const size_t work = (size_t)M * (nout / 8);
+  int blocks = (int)((work + 255) / 256);
+  if (blocks > 4096) blocks = 4096;
+  gemm_splitk_reduce<<<blocks, 256, 0, s>>>((const float*)ws, splits, M, N, epi, a.bias, a.resid, ldr,
+                                             a.C, ldc);
+  DA_LAUNCH_CHECK();
+}

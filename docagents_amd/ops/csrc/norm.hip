@@ -1,0 +1,283 @@
+// Normalisation / embedding / pooling kernels (memory-bound: 16-B vector loads everywhere,
+// Guideline 13). One workgroup per row, values kept in registers between the two passes so each
+// row is read from HBM exactly once.
+//
+// Reference compute sites replaced: N1 (encoder LayerNorm / embeddings),
+// N3 (`normalize`, internal/embeddings/openai.go:146-158 -> fused pooling + L2 norm), N6 (RMSNorm).
+#include "common.h"
+
+#define MAXCH 8  // max 8-element chunks per thread (D <= 8 * 8 * 256 = 16384)
+
+__device__ __forceinline__ void load8(const bf16_t* p, float* v) {
+  u32x4_t u = *(const u32x4_t*)p;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    v[2 * e] = bf2f((bf16_t)(u[e] & 0xffff));
+    v[2 * e + 1] = bf2f((bf16_t)(u[e] >> 16));
+  }
+}
+__device__ __forceinline__ void store8(bf16_t* p, const float* v) {
+  *(u32x4_t*)p = u32x4_t{pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3]), pack_bf2(v[4], v[5]), pack_bf2(v[6], v[7])};
+}
+
+// RMSNorm with optional fused residual add:
+//   if resid: h = x + resid; resid <- h (residual stream updated in place); y = rms(h) * w
+//   else:     y = rms(x) * w
+__global__ void rmsnorm_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ resid,
+                               const bf16_t* __restrict__ w, bf16_t* __restrict__ y, int D, float eps,
+                               int ldx, int ldy) {
+  __shared__ float red[16];
+  const int row = blockIdx.x;
+  const bf16_t* xr = x + (size_t)row * ldx;
+  bf16_t* rr = resid ? resid + (size_t)row * D : nullptr;
+  const int nch = D / 8;
+  float v[MAXCH][8];
+  float ss = 0.f;
+#pragma unroll
+  for (int i = 0; i < MAXCH; ++i) {
+    const int c = threadIdx.x + i * blockDim.x;
+    if (c < nch) {
+      load8(xr + c * 8, v[i]);
+      if (rr) {
+        float r[8];
+        load8(rr + c * 8, r);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[i][e] += r[e];
+        store8(rr + c * 8, v[i]);
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) ss += v[i][e] * v[i][e];
+    }
+  }
+  ss = block_sum(ss, red);
+  const float inv = rsqrtf(ss / D + eps);
+#pragma unroll
+  for (int i = 0; i < MAXCH; ++i) {
+    const int c = threadIdx.x + i * blockDim.x;
+    if (c < nch) {
+      float wv[8];
+      load8(w + c * 8, wv);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[i][e] = v[i][e] * inv * wv[e];
+      store8(y + (size_t)row * ldy + c * 8, v[i]);
+    }
+  }
+}
+
+// LayerNorm (BERT), optional residual input added first (x + resid), bias optional.
+__global__ void layernorm_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ resid,
+                                 const bf16_t* __restrict__ g, const bf16_t* __restrict__ b,
+                                 bf16_t* __restrict__ y, int D, float eps) {
+  __shared__ float red[16];
+  const int row = blockIdx.x;
+  const int nch = D / 8;
+  float v[MAXCH][8];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < MAXCH; ++i) {
+    const int c = threadIdx.x + i * blockDim.x;
+    if (c < nch) {
+      load8(x + (size_t)row * D + c * 8, v[i]);
+      if (resid) {
+        float r[8];
+        load8(resid + (size_t)row * D + c * 8, r);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[i][e] += r[e];
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) s += v[i][e];
+    }
+  }
+  const float mean = block_sum(s, red) / D;
+  float var = 0.f;
+#pragma unroll
+  for (int i = 0; i < MAXCH; ++i) {
+    const int c = threadIdx.x + i * blockDim.x;
+    if (c < nch) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) { float d = v[i][e] - mean; var += d * d; }
+    }
+  }
+  var = block_sum(var, red) / D;
+  const float inv = rsqrtf(var + eps);
+#pragma unroll
+  for (int i = 0; i < MAXCH; ++i) {
+    const int c = threadIdx.x + i * blockDim.x;
+    if (c < nch) {
+      float gv[8], bv[8];
+      load8(g + c * 8, gv);
+      if (b) load8(b + c * 8, bv);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[i][e] = (v[i][e] - mean) * inv * gv[e] + (b ? bv[e] : 0.f);
+      store8(y + (size_t)row * D + c * 8, v[i]);
+    }
+  }
+}
+
+// BERT embeddings: y = LN(word[ids[t]] + pos[positions[t]] + type[types ? types[t] : 0])
+__global__ void bert_embed_ln_kernel(const int* __restrict__ ids, const int* __restrict__ positions,
+                                     const int* __restrict__ types, const bf16_t* __restrict__ word,
+                                     const bf16_t* __restrict__ pos, const bf16_t* __restrict__ type,
+                                     const bf16_t* __restrict__ g, const bf16_t* __restrict__ b,
+                                     bf16_t* __restrict__ y, int D, float eps) {
+  __shared__ float red[16];
+  const int row = blockIdx.x;
+  const size_t wi = (size_t)ids[row], pi = (size_t)positions[row], ti = types ? (size_t)types[row] : 0;
+  const int nch = D / 8;
+  float v[MAXCH][8];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < MAXCH; ++i) {
+    const int c = threadIdx.x + i * blockDim.x;
+    if (c < nch) {
+      float a[8], p[8], t[8];
+      load8(word + wi * D + c * 8, a);
+      load8(pos + pi * D + c * 8, p);
+      load8(type + ti * D + c * 8, t);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) { v[i][e] = a[e] + p[e] + t[e]; s += v[i][e]; }
+    }
+  }
+  const float mean = block_sum(s, red) / D;
+  float var = 0.f;
+#pragma unroll
+  for (int i = 0; i < MAXCH; ++i) {
+    const int c = threadIdx.x + i * blockDim.x;
+    if (c < nch) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) { float d = v[i][e] - mean; var += d * d; }
+    }
+  }
+  var = block_sum(var, red) / D;
+  const float inv = rsqrtf(var + eps);
+#pragma unroll
+  for (int i = 0; i < MAXCH; ++i) {
+    const int c = threadIdx.x + i * blockDim.x;
+    if (c < nch) {
+      float gv[8], bv[8];
+      load8(g + c * 8, gv);
+      load8(b + c * 8, bv);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[i][e] = (v[i][e] - mean) * inv * gv[e] + bv[e];
+      store8(y + (size_t)row * D + c * 8, v[i]);
+    }
+  }
+}
+
+// Token embedding gather (decoder): y[t] = table[ids[t]]
+__global__ void embed_kernel(const int* __restrict__ ids, const bf16_t* __restrict__ table,
+                             bf16_t* __restrict__ y, int D) {
+  const int row = blockIdx.x;
+  const size_t id = (size_t)ids[row];
+  for (int c = threadIdx.x; c < D / 8; c += blockDim.x)
+    *(u32x4_t*)(y + (size_t)row * D + c * 8) = *(const u32x4_t*)(table + id * D + c * 8);
+}
+
+// Pooling + L2 normalisation (fp32 accumulate; zero vector left unchanged like the reference's
+// `normalize`). mode 0 = CLS (first token), 1 = mean over the sequence's tokens.
+// Output fp32 [B, D] and/or bf16 [B, D] (the index stores bf16).
+__global__ void pool_l2norm_kernel(const bf16_t* __restrict__ h, const int* __restrict__ cu_seqlens,
+                                   int D, int mode, float* __restrict__ out32,
+                                   bf16_t* __restrict__ out16) {
+  __shared__ float red[16];
+  const int b = blockIdx.x;
+  const int s0 = cu_seqlens[b], s1 = cu_seqlens[b + 1];
+  const int nch = D / 8;
+  float v[MAXCH][8];
+  float ss = 0.f;
+#pragma unroll
+  for (int i = 0; i < MAXCH; ++i) {
+    const int c = threadIdx.x + i * blockDim.x;
+    if (c < nch) {
+      if (mode == 0 || s1 <= s0) {
+        load8(h + (size_t)s0 * D + c * 8, v[i]);
+      } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[i][e] = 0.f;
+        for (int t = s0; t < s1; ++t) {
+          float a[8];
+          load8(h + (size_t)t * D + c * 8, a);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[i][e] += a[e];
+        }
+        const float invn = 1.f / (float)(s1 - s0);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[i][e] *= invn;
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) ss += v[i][e] * v[i][e];
+    }
+  }
+  ss = block_sum(ss, red);
+  const float inv = ss > 0.f ? rsqrtf(ss) : 1.f;
+#pragma unroll
+  for (int i = 0; i < MAXCH; ++i) {
+    const int c = threadIdx.x + i * blockDim.x;
+    if (c < nch) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[i][e] *= inv;
+      if (out32) {
+        float* o = out32 + (size_t)b * D + c * 8;
+        *(f32x4_t*)o = f32x4_t{v[i][0], v[i][1], v[i][2], v[i][3]};
+        *(f32x4_t*)(o + 4) = f32x4_t{v[i][4], v[i][5], v[i][6], v[i][7]};
+      }
+      if (out16) store8(out16 + (size_t)b * D + c * 8, v[i]);
+    }
+  }
+}
+
+static inline int row_threads(int D) {
+  int ch = D / 8;
+  int t = ((ch + 63) / 64) * 64;
+  if (t > 256) t = 256;
+  if (t < 64) t = 64;
+  return t;
+}
+static inline bool d_ok(int D) { return D % 8 == 0 && D / 8 <= MAXCH * 256; }
+
+DA_EXPORT int da_rmsnorm(const void* x, int ldx, void* resid, const void* w, void* y, int ldy, int M, int D,
+                         float eps, void* stream) {
+  if (!d_ok(D) || ldx % 8 || ldy % 8) return (int)hipErrorInvalidValue;
+  if (M == 0) return 0;
+  rmsnorm_kernel<<<M, row_threads(D), 0, (hipStream_t)stream>>>((const bf16_t*)x, (bf16_t*)resid,
+                                                                 (const bf16_t*)w, (bf16_t*)y, D, eps, ldx, ldy);
+  DA_LAUNCH_CHECK();
+}
+
+DA_EXPORT int da_layernorm(const void* x, const void* resid, const void* g, const void* b, void* y, int M, int D,
+                           float eps, void* stream) {
+  if (!d_ok(D)) return (int)hipErrorInvalidValue;
+  if (M == 0) return 0;
+  layernorm_kernel<<<M, row_threads(D), 0, (hipStream_t)stream>>>((const bf16_t*)x, (const bf16_t*)resid,
+                                                                   (const bf16_t*)g, (const bf16_t*)b,
+                                                                   (bf16_t*)y, D, eps);
+  DA_LAUNCH_CHECK();
+}
+
+DA_EXPORT int da_bert_embed_ln(const void* ids, const void* positions, const void* types, const void* word,
+                               const void* pos, const void* type, const void* g, const void* b, void* y, int T,
+                               int D, float eps, void* stream) {
+  if (!d_ok(D)) return (int)hipErrorInvalidValue;
+  if (T == 0) return 0;
+  bert_embed_ln_kernel<<<T, row_threads(D), 0, (hipStream_t)stream>>>(
+      (const int*)ids, (const int*)positions, (const int*)types, (const bf16_t*)word, (const bf16_t*)pos,
+      (const bf16_t*)type, (const bf16_t*)g, (const bf16_t*)b, (bf16_t*)y, D, eps);
+  DA_LAUNCH_CHECK();
+}
+
+DA_EXPORT int da_embed(const void* ids, const void* table, void* y, int T, int D, void* stream) {
+  if (D % 8) return (int)hipErrorInvalidValue;
+  if (T == 0) return 0;
+  embed_kernel<<<T, row_threads(D), 0, (hipStream_t)stream>>>((const int*)ids, (const bf16_t*)table,
+                                                               (bf16_t*)y, D);
+  DA_LAUNCH_CHECK();
+}
+
+DA_EXPORT int da_pool_l2norm(const void* h, const void* cu_seqlens, int B, int D, int mode, void* out32,
+                             void* out16, void* stream) {
+  if (!d_ok(D)) return (int)hipErrorInvalidValue;
+  if (B == 0) return 0;
+  pool_l2norm_kernel<<<B, row_threads(D), 0, (hipStream_t)stream>>>((const bf16_t*)h, (const int*)cu_seqlens, D,
+                                                                     mode, (float*)out32, (bf16_t*)out16);
+  DA_LAUNCH_CHECK();
+}

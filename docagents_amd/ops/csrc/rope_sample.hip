@@ -1,0 +1,150 @@
+// RoPE + KV-cache write, and the fused temperature sampler with chosen-token logprob.
+//
+// RoPE (NeoX / HF rotate_half layout, Llama-3 & Phi-3): pairs (i, i + D/2) rotated by
+// theta_i * pos. cos/sin come from a host-built fp32 table [max_pos, D/2, 2] so the kernel stays
+// memory-bound (Appendix B: trig tables on the host, not sinf/cosf per element).
+//
+// The sampler replaces OpenAI's `logprobs=true, top_logprobs=1` + `calculateLLMConfidence`
+// (internal/llm/openai.go:84-90,149-164): Gumbel-max sampling at
+// temperature T (0.2 in the reference, openai.go:22) with an in-kernel counter-based hash RNG, and
+// the chosen token's log-probability under the untempered distribution.
+#include "common.h"
+
+// qkv: [T, (H + 2*Hkv) * D] row-major (q heads, then k heads, then v heads)
+// k_cache / v_cache: [num_slots, Hkv, max_seq, D]; slot[t], pos[t] give where token t goes.
+__global__ void rope_cache_kernel(bf16_t* __restrict__ qkv, const int* __restrict__ pos,
+                                  const int* __restrict__ slot, const float* __restrict__ cs,
+                                  bf16_t* __restrict__ kc, bf16_t* __restrict__ vc, int H, int Hkv, int D,
+                                  int max_seq, int rotate_q) {
+  const int t = blockIdx.x;
+  const int p = pos[t];
+  const int half = D / 2;
+  const int ld = (H + 2 * Hkv) * D;
+  bf16_t* row = qkv + (size_t)t * ld;
+  const float* cst = cs + (size_t)p * half * 2;
+  const int groups = half / 4;  // 4 consecutive rotary pairs per work item
+  const int nheads = (rotate_q ? H : 0) + Hkv;
+  const int s = slot ? slot[t] : 0;
+  for (int w = threadIdx.x; w < nheads * groups; w += blockDim.x) {
+    const int hh = w / groups, gq = w % groups;
+    const int head = rotate_q ? hh : H + hh;  // head index within q|k region
+    bf16_t* hp = row + head * D;
+    const int i0 = gq * 4;
+    u32x2_t a = *(const u32x2_t*)(hp + i0);
+    u32x2_t b = *(const u32x2_t*)(hp + half + i0);
+    float x1[4] = {bf2f(a[0] & 0xffff), bf2f(a[0] >> 16), bf2f(a[1] & 0xffff), bf2f(a[1] >> 16)};
+    float x2[4] = {bf2f(b[0] & 0xffff), bf2f(b[0] >> 16), bf2f(b[1] & 0xffff), bf2f(b[1] >> 16)};
+    float o1[4], o2[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float c = cst[(i0 + e) * 2], sn = cst[(i0 + e) * 2 + 1];
+      o1[e] = x1[e] * c - x2[e] * sn;
+      o2[e] = x2[e] * c + x1[e] * sn;
+    }
+    u32x2_t ra = u32x2_t{pack_bf2(o1[0], o1[1]), pack_bf2(o1[2], o1[3])};
+    u32x2_t rb = u32x2_t{pack_bf2(o2[0], o2[1]), pack_bf2(o2[2], o2[3])};
+    *(u32x2_t*)(hp + i0) = ra;
+    *(u32x2_t*)(hp + half + i0) = rb;
+    if (kc && head >= H) {
+      const int hk = head - H;
+      bf16_t* dst = kc + (((size_t)s * Hkv + hk) * max_seq + p) * D;
+      *(u32x2_t*)(dst + i0) = ra;
+      *(u32x2_t*)(dst + half + i0) = rb;
+    }
+  }
+  if (vc) {
+    const bf16_t* vrow = row + (H + Hkv) * D;
+    for (int w = threadIdx.x; w < Hkv * D / 8; w += blockDim.x) {
+      const int hk = w / (D / 8), c = w % (D / 8);
+      bf16_t* dst = vc + (((size_t)s * Hkv + hk) * max_seq + p) * D + c * 8;
+      *(u32x4_t*)dst = *(const u32x4_t*)(vrow + hk * D + c * 8);
+    }
+  }
+}
+
+// One workgroup per row of logits [B, V] (bf16). temperature <= 0 -> greedy.
+// out_tok[b], out_lp[b] = log softmax(logits)[tok]; optional running confidence accumulators
+// conf_sum[b] += exp(lp), conf_cnt[b] += 1 (mean token probability, llm/openai.go:149-164).
+__global__ void __launch_bounds__(1024)
+sample_kernel(const bf16_t* __restrict__ logits, int V, int ld, float temperature, unsigned seed,
+              unsigned step, int* __restrict__ out_tok, float* __restrict__ out_lp,
+              float* __restrict__ conf_sum, const int* __restrict__ active) {
+  __shared__ float redf[16];
+  __shared__ float bestv[16];
+  __shared__ int besti[16];
+  const int b = blockIdx.x;
+  const bf16_t* row = logits + (size_t)b * ld;
+  const float invT = temperature > 0.f ? 1.f / temperature : 0.f;
+  float mx = -INFINITY, bv = -INFINITY;
+  int bi = 0;
+  for (int c = threadIdx.x; c < V / 8; c += blockDim.x) {
+    u32x4_t u = *(const u32x4_t*)(row + c * 8);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float x = bf2f((bf16_t)((e & 1) ? (u[e >> 1] >> 16) : (u[e >> 1] & 0xffff)));
+      const int v = c * 8 + e;
+      mx = fmaxf(mx, x);
+      float score;
+      if (temperature > 0.f) {
+        const float uu = u01(seed, step * 131071u + (unsigned)b, (unsigned)v);
+        score = x * invT - __logf(-__logf(uu));
+      } else {
+        score = x;
+      }
+      if (score > bv) { bv = score; bi = v; }
+    }
+  }
+  for (int v = (V / 8) * 8 + threadIdx.x; v < V; v += blockDim.x) {  // tail
+    const float x = bf2f(row[v]);
+    mx = fmaxf(mx, x);
+    float score = x;
+    if (temperature > 0.f) score = x * invT - __logf(-__logf(u01(seed, step * 131071u + (unsigned)b, (unsigned)v)));
+    if (score > bv) { bv = score; bi = v; }
+  }
+  // argmax reduction (ties -> smallest index)
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float ov = __shfl_xor(bv, o, 64);
+    const int oi = __shfl_xor(bi, o, 64);
+    if (ov > bv || (ov == bv && oi < bi)) { bv = ov; bi = oi; }
+  }
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  if (lane == 0) { bestv[wid] = bv; besti[wid] = bi; }
+  const float gmax = block_max(mx, redf);  // contains __syncthreads
+  float s = 0.f;
+  for (int v = threadIdx.x; v < V; v += blockDim.x) s += __expf(bf2f(row[v]) - gmax);
+  s = block_sum(s, redf);
+  if (threadIdx.x == 0) {
+    float fv = bestv[0];
+    int fi = besti[0];
+    for (int i = 1; i < nw; ++i)
+      if (bestv[i] > fv || (bestv[i] == fv && besti[i] < fi)) { fv = bestv[i]; fi = besti[i]; }
+    const float lp = bf2f(row[fi]) - gmax - __logf(s);
+    const bool on = active ? active[b] != 0 : true;
+    if (on) {
+      out_tok[b] = fi;
+      if (out_lp) out_lp[b] = lp;
+      if (conf_sum) { conf_sum[2 * b] += __expf(lp); conf_sum[2 * b + 1] += 1.f; }
+    }
+  }
+}
+
+DA_EXPORT int da_rope_cache(void* qkv, const void* pos, const void* slot, const void* cos_sin, void* k_cache,
+                            void* v_cache, int T, int H, int Hkv, int D, int max_seq, int rotate_q, void* stream) {
+  if (D % 8 || (D / 2) % 4) return (int)hipErrorInvalidValue;
+  if (T == 0) return 0;
+  rope_cache_kernel<<<T, 256, 0, (hipStream_t)stream>>>((bf16_t*)qkv, (const int*)pos, (const int*)slot,
+                                                         (const float*)cos_sin, (bf16_t*)k_cache,
+                                                         (bf16_t*)v_cache, H, Hkv, D, max_seq, rotate_q);
+  DA_LAUNCH_CHECK();
+}
+
+DA_EXPORT int da_sample(const void* logits, int B, int V, int ld, float temperature, unsigned seed, unsigned step,
+                        void* out_tok, void* out_lp, void* conf, const void* active, void* stream) {
+  if (ld % 8) return (int)hipErrorInvalidValue;
+  if (B == 0) return 0;
+  sample_kernel<<<B, 1024, 0, (hipStream_t)stream>>>((const bf16_t*)logits, V, ld, temperature, seed, step,
+                                                      (int*)out_tok, (float*)out_lp, (float*)conf,
+                                                      (const int*)active);
+  DA_LAUNCH_CHECK();
+}

@@ -1,0 +1,395 @@
+"""ctypes bindings for the gfx950 kernel library (``_da_kernels.so``).
+
+Every wrapper validates shapes / dtypes / contiguity / device on the host BEFORE launching (a
+mis-shaped launch of a hand-written kernel can fault the GPU), launches on PyTorch's current HIP
+stream, and raises on any launch error. There is deliberately no silent fallback: on a GPU box,
+if the library is missing the import fails loudly (``KernelLibraryMissing``). The fp32 PyTorch
+oracles for tests live in ``docagents_amd.ops.reference``.
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+import os
+import threading
+from pathlib import Path
+
+import torch
+
+_LIB = None
+_LOCK = threading.Lock()
+_LIB_PATH = Path(__file__).resolve().parent / "_da_kernels.so"
+
+EPI_NONE, EPI_BIAS, EPI_GELU, EPI_SWIGLU, EPI_RESID = 0, 1, 2, 3, 4
+
+c_void_p, c_int, c_float, c_uint, c_size_t = (ctypes.c_void_p, ctypes.c_int, ctypes.c_float,
+                                             ctypes.c_uint, ctypes.c_size_t)
+
+_SIGS = {
+    "da_gemm_bf16": [c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int,
+                     c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p],
+    "da_rmsnorm": [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_float, c_void_p],
+    "da_layernorm": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_float, c_void_p],
+    "da_bert_embed_ln": [c_void_p] * 9 + [c_int, c_int, c_float, c_void_p],
+    "da_embed": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p],
+    "da_pool_l2norm": [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p],
+    "da_rope_cache": [c_void_p] * 6 + [c_int] * 7 + [c_void_p],
+    "da_sample": [c_void_p, c_int, c_int, c_int, c_float, c_uint, c_uint, c_void_p, c_void_p, c_void_p,
+                  c_void_p, c_void_p],
+    "da_flash_attn_varlen": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_int,
+                             c_int, c_int, c_int, c_int, c_float, c_void_p, c_int, c_void_p],
+    "da_decode_attn": [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
+                       c_int, c_int, c_int, c_float, c_void_p, c_void_p, c_int, c_void_p],
+    "da_topk_dense": [c_void_p, c_int, c_int, c_void_p, c_void_p, c_int, c_void_p, c_int, c_float, c_int,
+                      c_int, c_void_p, c_void_p, c_void_p, c_void_p],
+    "da_topk_ranges": [c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int,
+                       c_float, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p],
+    "da_topk_merge": [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p],
+    "da_kmeans_accum": [c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p],
+}
+
+
+class KernelLibraryMissing(RuntimeError):
+    pass
+
+
+class KernelError(RuntimeError):
+    pass
+
+
+def lib() -> ctypes.CDLL:
+    """Load (building on first use if sources are newer) the kernel library."""
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    with _LOCK:
+        if _LIB is not None:
+            return _LIB
+        if os.environ.get("DA_BUILD_ON_IMPORT", "1") == "1":
+            try:
+                from .build import build
+                build()
+            except Exception as e:  # noqa: BLE001 - fall through to the explicit check below
+                if not _LIB_PATH.exists():
+                    raise KernelLibraryMissing(f"cannot build {_LIB_PATH}: {e}") from e
+        if not _LIB_PATH.exists():
+            raise KernelLibraryMissing(f"{_LIB_PATH} not built; run python -m docagents_amd.ops.build")
+        import torch.cuda  # noqa: F401 - make sure torch's HIP runtime is loaded first
+        L = ctypes.CDLL(str(_LIB_PATH))
+        for name, argt in _SIGS.items():
+            fn = getattr(L, name)
+            fn.argtypes = argt
+            fn.restype = c_int
+        L.da_topk_dense_ws.argtypes = [c_int, c_int, c_int, c_int]
+        L.da_topk_dense_ws.restype = c_size_t
+        _LIB = L
+        return L
+
+
+def available() -> bool:
+    return torch.cuda.is_available() and _LIB_PATH.exists()
+
+
+def _ptr(t):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def _stream():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def _check(rc: int, name: str):
+    if rc != 0:
+        raise KernelError(f"{name} failed with hipError {rc}")
+
+
+def _req(cond: bool, msg: str):
+    if not cond:
+        raise ValueError(msg)
+
+
+def _bf16_cuda(t, name):
+    _req(t.is_cuda, f"{name} must be on GPU")
+    _req(t.dtype == torch.bfloat16, f"{name} must be bf16, got {t.dtype}")
+
+
+def _i32(t, name):
+    _req(t.is_cuda and t.dtype == torch.int32 and t.is_contiguous(), f"{name} must be contiguous int32 on GPU")
+
+
+# ----------------------------------------------------------------------------------- GEMM
+_WS = {}
+
+
+def _workspace(nbytes: int, device) -> torch.Tensor:
+    key = (device.index if device.index is not None else torch.cuda.current_device())
+    buf = _WS.get(key)
+    if buf is None or buf.numel() < nbytes:
+        buf = torch.empty(max(nbytes, 1 << 20), dtype=torch.uint8, device=device)
+        _WS[key] = buf
+    return buf
+
+
+def gemm(a: torch.Tensor, w: torch.Tensor, bias=None, epi: int = EPI_NONE, resid=None, out=None,
+         tile: int = 0, splits: int = 0) -> torch.Tensor:
+    """out[M, N'] = epi(a[M, K] @ w[N, K]^T). N' = N/2 for EPI_SWIGLU (w rows interleaved by 16)."""
+    _bf16_cuda(a, "a"); _bf16_cuda(w, "w")
+    _req(a.dim() == 2 and w.dim() == 2, "gemm expects 2-D operands")
+    M, K = a.shape
+    N, K2 = w.shape
+    _req(K == K2, f"K mismatch {K} vs {K2}")
+    _req(K % 64 == 0, f"K={K} must be a multiple of 64")
+    _req(N % 8 == 0, f"N={N} must be a multiple of 8")
+    _req(a.stride(1) == 1 and a.stride(0) % 8 == 0 and a.stride(0) >= K, "a must be row-major, 16-B aligned rows")
+    _req(w.is_contiguous(), "w must be contiguous")
+    _req(a.data_ptr() % 16 == 0 and w.data_ptr() % 16 == 0, "operands must be 16-B aligned")
+    nout = N // 2 if epi == EPI_SWIGLU else N
+    if epi == EPI_SWIGLU:
+        _req(N % 32 == 0, "SwiGLU needs N % 32 == 0")
+    if out is None:
+        out = torch.empty((M, nout), dtype=torch.bfloat16, device=a.device)
+    _bf16_cuda(out, "out")
+    _req(out.shape == (M, nout) and out.stride(1) == 1 and out.stride(0) % 8 == 0, "bad out")
+    if bias is not None:
+        _bf16_cuda(bias, "bias"); _req(bias.numel() == N and bias.is_contiguous(), "bias must be [N]")
+        _req(epi in (EPI_BIAS, EPI_GELU, EPI_RESID), "bias only with BIAS/GELU/RESID epilogues")
+    ldr = 0
+    if epi == EPI_RESID:
+        _req(resid is not None, "EPI_RESID needs resid")
+        _bf16_cuda(resid, "resid")
+        _req(resid.shape == (M, N) and resid.stride(1) == 1 and resid.stride(0) % 8 == 0, "bad resid")
+        ldr = resid.stride(0)
+    if M == 0:
+        return out
+    if splits <= 0:
+        splits = _auto_splits(M, N, K)
+    ws = None
+    if splits > 1:
+        ws = _workspace(splits * M * N * 4, a.device)
+    rc = lib().da_gemm_bf16(_ptr(a), a.stride(0), _ptr(w), _ptr(out), out.stride(0), _ptr(bias), _ptr(resid), ldr,
+                            M, N, K, epi, tile, splits, _ptr(ws), _stream())
+    _check(rc, "gemm")
+    return out
+
+
+def _auto_splits(M: int, N: int, K: int) -> int:
+    """Split-K so skinny (decode-sized) GEMMs put >= ~512 workgroups on the 256 CUs."""
+    if M > 64:
+        return 1
+    bm, bn = (32, 128) if M <= 32 else (64, 128)
+    tiles = math.ceil(M / bm) * math.ceil(N / bn)
+    ksteps = K // 64
+    s = 1
+    while tiles * s < 512 and ksteps % (s * 2) == 0 and ksteps // (s * 2) >= 4:
+        s *= 2
+    return s
+
+
+# ------------------------------------------------------------------------------ norms etc.
+def rmsnorm(x, w, eps: float, resid=None, out=None):
+    _bf16_cuda(x, "x"); _bf16_cuda(w, "w")
+    M, D = x.shape
+    _req(x.stride(1) == 1 and x.stride(0) % 8 == 0 and D % 8 == 0, "x must be row-major, D % 8 == 0")
+    _req(w.numel() == D, "w must be [D]")
+    if resid is not None:
+        _bf16_cuda(resid, "resid"); _req(resid.is_contiguous() and resid.shape == (M, D), "resid must be [M, D]")
+    if out is None:
+        out = torch.empty((M, D), dtype=torch.bfloat16, device=x.device)
+    _req(out.stride(1) == 1 and out.stride(0) % 8 == 0, "bad out")
+    _check(lib().da_rmsnorm(_ptr(x), x.stride(0), _ptr(resid), _ptr(w), _ptr(out), out.stride(0), M, D,
+                            float(eps), _stream()), "rmsnorm")
+    return out
+
+
+def layernorm(x, g, b, eps: float, resid=None, out=None):
+    _bf16_cuda(x, "x")
+    M, D = x.shape
+    _req(x.is_contiguous() and D % 8 == 0, "x must be contiguous, D % 8 == 0")
+    if resid is not None:
+        _req(resid.is_contiguous() and resid.shape == x.shape, "bad resid")
+    if out is None:
+        out = torch.empty_like(x)
+    _check(lib().da_layernorm(_ptr(x), _ptr(resid), _ptr(g), _ptr(b), _ptr(out), M, D, float(eps), _stream()),
+           "layernorm")
+    return out
+
+
+def bert_embed_ln(ids, positions, types, word, pos, type_, g, b, eps: float, out=None):
+    _i32(ids, "ids"); _i32(positions, "positions")
+    if types is not None:
+        _i32(types, "types")
+    T = ids.numel()
+    D = word.shape[1]
+    _req(positions.numel() == T, "positions length")
+    if out is None:
+        out = torch.empty((T, D), dtype=torch.bfloat16, device=ids.device)
+    _check(lib().da_bert_embed_ln(_ptr(ids), _ptr(positions), _ptr(types), _ptr(word), _ptr(pos), _ptr(type_),
+                                  _ptr(g), _ptr(b), _ptr(out), T, D, float(eps), _stream()), "bert_embed_ln")
+    return out
+
+
+def embed(ids, table, out=None):
+    _i32(ids, "ids"); _bf16_cuda(table, "table")
+    T, D = ids.numel(), table.shape[1]
+    if out is None:
+        out = torch.empty((T, D), dtype=torch.bfloat16, device=ids.device)
+    _check(lib().da_embed(_ptr(ids), _ptr(table), _ptr(out), T, D, _stream()), "embed")
+    return out
+
+
+def pool_l2norm(h, cu_seqlens, mode: int = 0, out32=None, out16=None):
+    _bf16_cuda(h, "h"); _i32(cu_seqlens, "cu_seqlens")
+    B = cu_seqlens.numel() - 1
+    D = h.shape[1]
+    _req(h.is_contiguous(), "h contiguous")
+    if out32 is None and out16 is None:
+        out32 = torch.empty((B, D), dtype=torch.float32, device=h.device)
+    _check(lib().da_pool_l2norm(_ptr(h), _ptr(cu_seqlens), B, D, mode, _ptr(out32), _ptr(out16), _stream()),
+           "pool_l2norm")
+    return out32 if out32 is not None else out16
+
+
+def rope_cache(qkv, pos, cos_sin, H, Hkv, D, slot=None, k_cache=None, v_cache=None, rotate_q=True):
+    """In-place RoPE on q and k heads of qkv [T, (H+2Hkv)*D]; optionally writes k/v into the cache."""
+    _bf16_cuda(qkv, "qkv"); _i32(pos, "pos")
+    T = qkv.shape[0]
+    _req(qkv.is_contiguous() and qkv.shape[1] == (H + 2 * Hkv) * D, "qkv shape")
+    _req(cos_sin.dtype == torch.float32 and cos_sin.is_contiguous() and cos_sin.shape[-1] == 2
+         and cos_sin.shape[1] == D // 2, "cos_sin must be fp32 [max_pos, D/2, 2]")
+    max_seq = 0
+    if k_cache is not None:
+        _i32(slot, "slot")
+        _req(k_cache.is_contiguous() and v_cache.is_contiguous() and k_cache.shape == v_cache.shape, "caches")
+        _req(k_cache.dim() == 4 and k_cache.shape[1] == Hkv and k_cache.shape[3] == D, "cache [S, Hkv, max_seq, D]")
+        max_seq = k_cache.shape[2]
+    _check(lib().da_rope_cache(_ptr(qkv), _ptr(pos), _ptr(slot), _ptr(cos_sin), _ptr(k_cache), _ptr(v_cache),
+                               T, H, Hkv, D, max_seq, 1 if rotate_q else 0, _stream()), "rope_cache")
+    return qkv
+
+
+def flash_attn_varlen(q, k, v, cu_seqlens, max_seqlen: int, H: int, Hkv: int, D: int, causal: bool,
+                      scale: float | None = None, out=None):
+    """q/k/v: 2-D [T, *] views with head h at columns h*D (strided views into a packed qkv are fine)."""
+    for t, n in ((q, "q"), (k, "k"), (v, "v")):
+        _bf16_cuda(t, n)
+        _req(t.dim() == 2 and t.stride(1) == 1 and t.stride(0) % 8 == 0 and t.data_ptr() % 16 == 0, f"{n} layout")
+    _i32(cu_seqlens, "cu_seqlens")
+    _req(D in (64, 96, 128), f"head dim {D} unsupported")
+    _req(H % Hkv == 0, "H % Hkv")
+    T = q.shape[0]
+    if out is None:
+        out = torch.empty((T, H * D), dtype=torch.bfloat16, device=q.device)
+    scale = scale if scale is not None else 1.0 / math.sqrt(D)
+    B = cu_seqlens.numel() - 1
+    _check(lib().da_flash_attn_varlen(_ptr(q), _ptr(k), _ptr(v), q.stride(0), k.stride(0), v.stride(0),
+                                      _ptr(cu_seqlens), B, int(max_seqlen), H, Hkv, D, int(causal), float(scale),
+                                      _ptr(out), out.stride(0), _stream()), "flash_attn_varlen")
+    return out
+
+
+def decode_attn(q, k_cache, v_cache, lens, slot, H, Hkv, D, max_len: int, chunk: int = 256, scale=None, out=None):
+    """q [B, >=H*D] (row stride any multiple of 8); lens/slot int32 [B]; max_len = max(lens) (host int)."""
+    _bf16_cuda(q, "q"); _i32(lens, "lens"); _i32(slot, "slot")
+    _req(D in (64, 96, 128), "head dim")
+    _req((H // Hkv) in (1, 2, 4, 8) and H % Hkv == 0, "GQA group must be 1/2/4/8")
+    B = q.shape[0]
+    _req(k_cache.dim() == 4 and k_cache.shape[1] == Hkv and k_cache.shape[3] == D, "cache shape")
+    max_seq = k_cache.shape[2]
+    _req(max_len <= max_seq, "max_len > cache capacity")
+    nsplit = max(1, math.ceil(max_len / chunk))
+    ws = _workspace(B * H * nsplit * (D + 2) * 4, q.device)
+    if out is None:
+        out = torch.empty((B, H * D), dtype=torch.bfloat16, device=q.device)
+    scale = scale if scale is not None else 1.0 / math.sqrt(D)
+    _check(lib().da_decode_attn(_ptr(q), q.stride(0), _ptr(k_cache), _ptr(v_cache), _ptr(lens), _ptr(slot), B, H,
+                                Hkv, D, max_seq, chunk, nsplit, float(scale), _ptr(ws), _ptr(out), out.stride(0),
+                                _stream()), "decode_attn")
+    return out
+
+
+def sample(logits, temperature: float, seed: int, step: int, out_tok=None, out_lp=None, conf=None, active=None):
+    _bf16_cuda(logits, "logits")
+    B, V = logits.shape
+    _req(logits.stride(1) == 1 and logits.stride(0) % 8 == 0, "logits layout")
+    dev = logits.device
+    if out_tok is None:
+        out_tok = torch.empty(B, dtype=torch.int32, device=dev)
+    if out_lp is None:
+        out_lp = torch.empty(B, dtype=torch.float32, device=dev)
+    if conf is not None:
+        _req(conf.dtype == torch.float32 and conf.shape == (B, 2), "conf must be fp32 [B, 2]")
+    _check(lib().da_sample(_ptr(logits), B, V, logits.stride(0), float(temperature), seed & 0xffffffff,
+                           step & 0xffffffff, _ptr(out_tok), _ptr(out_lp), _ptr(conf), _ptr(active), _stream()),
+           "sample")
+    return out_tok, out_lp
+
+
+# --------------------------------------------------------------------------- vector search
+def topk_dense(X, Qv, K: int, thr: float, slots=None, bitmap=None, rows_per_block: int | None = None):
+    """Exact top-K of Qv @ X^T per query with threshold and optional doc-slot bitmap [Q, W] int32."""
+    _bf16_cuda(X, "X"); _bf16_cuda(Qv, "Qv")
+    N, d = X.shape
+    Q = Qv.shape[0]
+    _req(X.is_contiguous() and Qv.is_contiguous() and Qv.shape[1] == d, "X/Qv layout")
+    _req(d % 32 == 0 and 1 <= K <= 32, "d % 32 and 1 <= K <= 32")
+    W = 0
+    if bitmap is not None:
+        _req(slots is not None, "bitmap needs slots")
+        _i32(slots, "slots")
+        _req(bitmap.dtype == torch.int32 and bitmap.is_contiguous() and bitmap.shape[0] == Q, "bitmap [Q, W] int32")
+        W = bitmap.shape[1]
+    if rows_per_block is None:
+        qt = math.ceil(Q / 16)
+        nblk = max(1, min(math.ceil(N / 256), max(1, 1024 // qt)))
+        rows_per_block = max(64, math.ceil(math.ceil(N / nblk) / 64) * 64)
+    nblk = max(1, math.ceil(N / rows_per_block))
+    ws = _workspace(nblk * Q * K * 8, X.device)
+    out_s = torch.empty((Q, K), dtype=torch.float32, device=X.device)
+    out_i = torch.empty((Q, K), dtype=torch.int32, device=X.device)
+    _check(lib().da_topk_dense(_ptr(X), N, d, _ptr(slots), _ptr(Qv), Q, _ptr(bitmap), W, float(thr), K,
+                               rows_per_block, _ptr(ws), _ptr(out_s), _ptr(out_i), _stream()), "topk_dense")
+    return out_s, out_i
+
+
+def topk_ranges(X, Qv, ranges, range_off, K: int, thr: float, max_rows: int, slots=None, bitmap=None,
+                rows_per_split: int = 512):
+    """Top-K per query over its own row ranges. ranges int32 [R, 2], range_off int32 [Q+1];
+    max_rows = max total rows of any query (host int) — sets the split count."""
+    _bf16_cuda(X, "X"); _bf16_cuda(Qv, "Qv")
+    N, d = X.shape
+    Q = Qv.shape[0]
+    _req(d % 8 == 0 and d <= 4096 and 1 <= K <= 32, "d / K limits")
+    _i32(ranges, "ranges"); _i32(range_off, "range_off")
+    _req(range_off.numel() == Q + 1, "range_off length")
+    W = 0
+    if bitmap is not None:
+        _i32(slots, "slots")
+        _req(bitmap.dtype == torch.int32 and bitmap.shape[0] == Q, "bitmap")
+        W = bitmap.shape[1]
+    splits = max(1, math.ceil(max_rows / rows_per_split))
+    ws = _workspace(splits * Q * K * 8, X.device)
+    out_s = torch.empty((Q, K), dtype=torch.float32, device=X.device)
+    out_i = torch.empty((Q, K), dtype=torch.int32, device=X.device)
+    _check(lib().da_topk_ranges(_ptr(X), d, _ptr(slots), _ptr(Qv), Q, _ptr(ranges), _ptr(range_off), _ptr(bitmap),
+                                W, float(thr), K, splits, rows_per_split, _ptr(ws), _ptr(out_s), _ptr(out_i),
+                                _stream()), "topk_ranges")
+    return out_s, out_i
+
+
+def topk_merge(cand_s, cand_i, K: int):
+    """cand [P, Q, K] (consumed) -> [Q, K]."""
+    _req(cand_s.dtype == torch.float32 and cand_i.dtype == torch.int32, "dtypes")
+    P, Q, K2 = cand_s.shape
+    _req(K2 == K, "K mismatch")
+    cs, ci = cand_s.contiguous().clone(), cand_i.contiguous().clone()
+    out_s = torch.empty((Q, K), dtype=torch.float32, device=cs.device)
+    out_i = torch.empty((Q, K), dtype=torch.int32, device=cs.device)
+    _check(lib().da_topk_merge(_ptr(cs), _ptr(ci), P, Q, K, _ptr(out_s), _ptr(out_i), _stream()), "topk_merge")
+    return out_s, out_i
+
+
+def kmeans_accum(X, assign, sums, counts):
+    _bf16_cuda(X, "X"); _i32(assign, "assign")
+    N, d = X.shape
+    _req(sums.dtype == torch.float32 and sums.shape[1] == d and counts.dtype == torch.float32, "sums/counts fp32")
+    _check(lib().da_kmeans_accum(_ptr(X), N, d, _ptr(assign), _ptr(sums), _ptr(counts), _stream()), "kmeans_accum")

@@ -1,0 +1,276 @@
+"""Plain-PyTorch fp32 reference implementations of every kernel in ``kernels.py``.
+
+Used as the numerics oracle in tests (HIP kernel vs fp32 PyTorch of the same op) and as the
+CPU execution path of the models (the container running CPU tests has no GPU). They are NOT a
+GPU fallback: on a GPU device the models always call the HIP kernels.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.nn.functional as F
+
+EPI_NONE, EPI_BIAS, EPI_GELU, EPI_SWIGLU, EPI_RESID = 0, 1, 2, 3, 4
+
+
+def gemm(a, w, bias=None, epi=EPI_NONE, resid=None, out=None, **_):
+    y = a.float() @ w.float().t()
+    if bias is not None:
+        y = y + bias.float()
+    if epi == EPI_GELU:
+        y = F.gelu(y)
+    elif epi == EPI_SWIGLU:
+        N = w.shape[0]
+        yy = y.view(y.shape[0], N // 32, 2, 16)
+        g, u = yy[:, :, 0, :], yy[:, :, 1, :]
+        y = (F.silu(g) * u).reshape(y.shape[0], N // 2)
+    elif epi == EPI_RESID:
+        y = y + resid.float()
+    y = y.to(a.dtype)
+    if out is not None:
+        out.copy_(y)
+        return out
+    return y
+
+
+def interleave_gate_up(gate: torch.Tensor, up: torch.Tensor) -> torch.Tensor:
+    """[F, K] gate + [F, K] up -> [2F, K] rows interleaved in 16-row groups (EPI_SWIGLU layout)."""
+    Fd, K = gate.shape
+    assert Fd % 16 == 0
+    g = gate.view(Fd // 16, 16, K)
+    u = up.view(Fd // 16, 16, K)
+    return torch.stack([g, u], dim=1).reshape(2 * Fd, K).contiguous()
+
+
+def rmsnorm(x, w, eps, resid=None, out=None):
+    xf = x.float()
+    if resid is not None:
+        xf = xf + resid.float()
+        resid.copy_(xf.to(resid.dtype))
+    y = xf * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + eps) * w.float()
+    y = y.to(x.dtype)
+    if out is not None:
+        out.copy_(y)
+        return out
+    return y
+
+
+def layernorm(x, g, b, eps, resid=None, out=None):
+    xf = x.float()
+    if resid is not None:
+        xf = xf + resid.float()
+    y = F.layer_norm(xf, (xf.shape[-1],), g.float(), None if b is None else b.float(), eps).to(x.dtype)
+    if out is not None:
+        out.copy_(y)
+        return out
+    return y
+
+
+def bert_embed_ln(ids, positions, types, word, pos, type_, g, b, eps, out=None):
+    t = type_[types.long()] if types is not None else type_[0]
+    x = word[ids.long()].float() + pos[positions.long()].float() + t.float()
+    return layernorm(x.to(word.dtype), g, b, eps, out=out)
+
+
+def embed(ids, table, out=None):
+    y = table[ids.long()]
+    if out is not None:
+        out.copy_(y)
+        return out
+    return y
+
+
+def pool_l2norm(h, cu_seqlens, mode=0, out32=None, out16=None):
+    cu = cu_seqlens.tolist()
+    rows = []
+    for i in range(len(cu) - 1):
+        s0, s1 = cu[i], cu[i + 1]
+        if mode == 0 or s1 <= s0:
+            rows.append(h[s0].float())
+        else:
+            rows.append(h[s0:s1].float().mean(0))
+    v = torch.stack(rows) if rows else torch.zeros((0, h.shape[1]))
+    n = v.norm(dim=-1, keepdim=True)
+    v = torch.where(n > 0, v / n.clamp_min(1e-30), v)
+    if out16 is not None:
+        out16.copy_(v.to(out16.dtype))
+    if out32 is not None:
+        out32.copy_(v)
+        return out32
+    return v if out16 is None else out16
+
+
+def rope_table(max_pos: int, D: int, theta: float, device=None) -> torch.Tensor:
+    inv = 1.0 / (theta ** (torch.arange(0, D, 2, dtype=torch.float64) / D))
+    t = torch.arange(max_pos, dtype=torch.float64)
+    ang = torch.outer(t, inv)
+    return torch.stack([ang.cos(), ang.sin()], dim=-1).float().contiguous().to(device)
+
+
+def _rope_rows(x, cs):  # x [T, nh, D], cs [T, D/2, 2]
+    half = x.shape[-1] // 2
+    x1, x2 = x[..., :half].float(), x[..., half:].float()
+    c, s = cs[:, None, :, 0], cs[:, None, :, 1]
+    return torch.cat([x1 * c - x2 * s, x2 * c + x1 * s], dim=-1)
+
+
+def rope_cache(qkv, pos, cos_sin, H, Hkv, D, slot=None, k_cache=None, v_cache=None, rotate_q=True):
+    T = qkv.shape[0]
+    x = qkv.view(T, H + 2 * Hkv, D)
+    cs = cos_sin[pos.long()]
+    if rotate_q:
+        x[:, :H] = _rope_rows(x[:, :H], cs).to(qkv.dtype)
+    x[:, H:H + Hkv] = _rope_rows(x[:, H:H + Hkv], cs).to(qkv.dtype)
+    if k_cache is not None:
+        sl, ps = slot.long(), pos.long()
+        k_cache[sl, :, ps] = x[:, H:H + Hkv]
+        v_cache[sl, :, ps] = x[:, H + Hkv:]
+    return qkv
+
+
+def flash_attn_varlen(q, k, v, cu_seqlens, max_seqlen, H, Hkv, D, causal, scale=None, out=None):
+    scale = scale if scale is not None else 1.0 / math.sqrt(D)
+    T = q.shape[0]
+    res = torch.empty((T, H * D), dtype=q.dtype, device=q.device)
+    cu = cu_seqlens.tolist()
+    G = H // Hkv
+    for b in range(len(cu) - 1):
+        s0, s1 = cu[b], cu[b + 1]
+        L = s1 - s0
+        if L == 0:
+            continue
+        qq = q[s0:s1, :H * D].float().view(L, H, D).transpose(0, 1)
+        kk = k[s0:s1, :Hkv * D].float().view(L, Hkv, D).transpose(0, 1).repeat_interleave(G, 0)
+        vv = v[s0:s1, :Hkv * D].float().view(L, Hkv, D).transpose(0, 1).repeat_interleave(G, 0)
+        s = (qq @ kk.transpose(1, 2)) * scale
+        if causal:
+            m = torch.ones(L, L, dtype=torch.bool, device=q.device).triu(1)
+            s = s.masked_fill(m, float("-inf"))
+        p = s.softmax(-1)
+        res[s0:s1] = (p @ vv).transpose(0, 1).reshape(L, H * D).to(q.dtype)
+    if out is not None:
+        out.copy_(res)
+        return out
+    return res
+
+
+def decode_attn(q, k_cache, v_cache, lens, slot, H, Hkv, D, max_len=None, chunk=256, scale=None, out=None):
+    scale = scale if scale is not None else 1.0 / math.sqrt(D)
+    B = q.shape[0]
+    G = H // Hkv
+    res = torch.empty((B, H * D), dtype=q.dtype, device=q.device)
+    for b in range(B):
+        L, s = int(lens[b]), int(slot[b])
+        qq = q[b, :H * D].float().view(H, 1, D)
+        kk = k_cache[s, :, :L].float().repeat_interleave(G, 0)
+        vv = v_cache[s, :, :L].float().repeat_interleave(G, 0)
+        p = ((qq @ kk.transpose(1, 2)) * scale).softmax(-1)
+        res[b] = (p @ vv).reshape(H * D).to(q.dtype)
+    if out is not None:
+        out.copy_(res)
+        return out
+    return res
+
+
+def log_softmax_rows(logits):
+    return torch.log_softmax(logits.float(), dim=-1)
+
+
+def sample(logits, temperature, seed, step, out_tok=None, out_lp=None, conf=None, active=None):
+    """Reference sampler: greedy when temperature <= 0, else torch multinomial (a different RNG
+    stream than the kernel's hash RNG, so only greedy is bit-comparable)."""
+    lp = log_softmax_rows(logits)
+    if temperature > 0:
+        g = torch.Generator(device="cpu").manual_seed((seed * 1000003 + step) & 0x7FFFFFFF)
+        probs = torch.softmax(logits.float().cpu() / temperature, -1)
+        tok = torch.multinomial(probs, 1, generator=g).squeeze(1).to(logits.device)
+    else:
+        tok = logits.float().argmax(-1)
+    chosen = lp.gather(1, tok.view(-1, 1)).squeeze(1)
+    tok = tok.int()
+    if active is not None:
+        keep = active.bool()
+        if out_tok is not None:
+            tok = torch.where(keep, tok, out_tok)
+    if conf is not None:
+        m = active.bool() if active is not None else torch.ones_like(chosen, dtype=torch.bool)
+        conf[:, 0] += torch.where(m, chosen.exp(), torch.zeros_like(chosen))
+        conf[:, 1] += m.float()
+    if out_tok is not None:
+        out_tok.copy_(tok)
+    if out_lp is not None:
+        out_lp.copy_(chosen)
+    return tok, chosen
+
+
+def topk_dense(X, Qv, K, thr, slots=None, bitmap=None, **_):
+    s = Qv.float() @ X.float().t()  # [Q, N]
+    valid = s >= thr
+    if bitmap is not None:
+        sl = slots.long()
+        words = bitmap[:, (sl >> 5)]  # [Q, N]
+        bits = (words >> (sl & 31).view(1, -1)) & 1
+        valid &= bits.bool()
+    s = s.masked_fill(~valid, float("-inf"))
+    return _topk_with_ties(s, K)
+
+
+def _topk_with_ties(s, K):
+    Q, N = s.shape
+    if N == 0:
+        return (torch.full((Q, K), float("-inf")), torch.full((Q, K), -1, dtype=torch.int32))
+    # sort desc by score, asc by index
+    idx = torch.arange(N, device=s.device).expand(Q, N)
+    order = torch.argsort(idx, dim=1, stable=True)
+    vals, perm = torch.sort(s, dim=1, descending=True, stable=True)
+    ids = torch.gather(idx, 1, perm)
+    kk = min(K, N)
+    vs, ii = vals[:, :kk], ids[:, :kk].int()
+    ii = torch.where(torch.isinf(vs), torch.full_like(ii, -1), ii)
+    if kk < K:
+        vs = torch.cat([vs, torch.full((Q, K - kk), float("-inf"), device=s.device)], 1)
+        ii = torch.cat([ii, torch.full((Q, K - kk), -1, dtype=torch.int32, device=s.device)], 1)
+    del order
+    return vs, ii
+
+
+def topk_ranges(X, Qv, ranges, range_off, K, thr, max_rows=None, slots=None, bitmap=None, **_):
+    Q = Qv.shape[0]
+    N = X.shape[0]
+    s = Qv.float() @ X.float().t()
+    allowed = torch.zeros((Q, N), dtype=torch.bool, device=X.device)
+    ro = range_off.tolist()
+    rg = ranges.tolist()
+    for q in range(Q):
+        for r in range(ro[q], ro[q + 1]):
+            a, b = rg[r]
+            allowed[q, a:b] = True
+    valid = allowed & (s >= thr)
+    if bitmap is not None:
+        sl = slots.long()
+        bits = (bitmap[:, (sl >> 5)] >> (sl & 31).view(1, -1)) & 1
+        valid &= bits.bool()
+    s = s.masked_fill(~valid, float("-inf"))
+    return _topk_with_ties(s, K)
+
+
+def topk_merge(cand_s, cand_i, K):
+    P, Q, _ = cand_s.shape
+    s = cand_s.permute(1, 0, 2).reshape(Q, -1)
+    i = cand_i.permute(1, 0, 2).reshape(Q, -1)
+    s = torch.where(i < 0, torch.full_like(s, float("-inf")), s)
+    # sort by score desc, id asc
+    big = i.clamp_min(0).to(torch.float64)
+    key = s.to(torch.float64) * 1e12 - big
+    order = torch.argsort(key, dim=1, descending=True, stable=True)
+    vs, ii = torch.gather(s, 1, order)[:, :K], torch.gather(i, 1, order)[:, :K]
+    ii = torch.where(torch.isinf(vs), torch.full_like(ii, -1), ii)
+    return vs, ii
+
+
+def kmeans_accum(X, assign, sums, counts):
+    a = assign.long()
+    m = a >= 0
+    sums.index_add_(0, a[m], X[m].float())
+    counts.index_add_(0, a[m], torch.ones(int(m.sum()), device=X.device))

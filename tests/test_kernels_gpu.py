@@ -1,0 +1,241 @@
+"""Numerics of every gfx950 HIP kernel vs the plain-PyTorch fp32 reference of the same op."""
+import math
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+from docagents_amd.ops import kernels as K  # noqa: E402
+from docagents_amd.ops import reference as R  # noqa: E402
+
+DEV = "cuda"
+
+
+def _rand(*shape, scale=1.0, dtype=torch.bfloat16):
+    return (torch.randn(*shape, device=DEV) * scale).to(dtype)
+
+
+def _close(a, b, atol, rtol=0.02):
+    a, b = a.float(), b.float()
+    err = (a - b).abs()
+    tol = atol + rtol * b.abs()
+    bad = (err > tol).sum().item()
+    assert bad == 0, f"{bad} / {a.numel()} mismatches, max err {err.max().item():.4g}"
+
+
+@pytest.mark.parametrize("M,N,Kd", [(1, 128, 64), (7, 200, 128), (33, 256, 192), (64, 384, 256),
+                                    (130, 264, 320), (257, 1024, 768), (512, 768, 3072)])
+@pytest.mark.parametrize("epi", [K.EPI_NONE, K.EPI_BIAS, K.EPI_GELU, K.EPI_RESID])
+def test_gemm(M, N, Kd, epi):
+    torch.manual_seed(M * 1000 + N)
+    a, w = _rand(M, Kd), _rand(N, Kd, scale=Kd ** -0.5)
+    bias = _rand(N) if epi != K.EPI_NONE else None
+    resid = _rand(M, N) if epi == K.EPI_RESID else None
+    got = K.gemm(a, w, bias=bias, epi=epi, resid=resid)
+    ref = R.gemm(a, w, bias=bias, epi=epi, resid=resid)
+    _close(got, ref, atol=0.03)
+
+
+@pytest.mark.parametrize("tile", [1, 2, 3])
+@pytest.mark.parametrize("splits", [1, 2, 4])
+def test_gemm_tiles_splitk(tile, splits):
+    torch.manual_seed(tile * 10 + splits)
+    M, N, Kd = 96, 512, 512
+    a, w, bias = _rand(M, Kd), _rand(N, Kd, scale=Kd ** -0.5), _rand(N)
+    got = K.gemm(a, w, bias=bias, epi=K.EPI_BIAS, tile=tile, splits=splits)
+    _close(got, R.gemm(a, w, bias=bias, epi=K.EPI_BIAS), atol=0.03)
+
+
+@pytest.mark.parametrize("M,F,splits", [(5, 256, 1), (64, 512, 2), (300, 1024, 1), (40, 2048, 4)])
+def test_gemm_swiglu(M, F, splits):
+    torch.manual_seed(M)
+    Kd = 256
+    gate, up = _rand(F, Kd, scale=Kd ** -0.5), _rand(F, Kd, scale=Kd ** -0.5)
+    w = R.interleave_gate_up(gate, up)
+    a = _rand(M, Kd)
+    got = K.gemm(a, w, epi=K.EPI_SWIGLU, splits=splits)
+    ref = (torch.nn.functional.silu(a.float() @ gate.float().t()) * (a.float() @ up.float().t()))
+    _close(got, ref, atol=0.03)
+
+
+def test_gemm_strided_a():
+    big = _rand(50, 3 * 256)
+    a = big[:, 256:512]
+    w = _rand(128, 256, scale=1 / 16)
+    _close(K.gemm(a, w), R.gemm(a.contiguous(), w), atol=0.03)
+
+
+@pytest.mark.parametrize("D", [768, 3072, 4096])
+def test_rmsnorm(D):
+    x, w = _rand(37, D), _rand(D)
+    r1 = _rand(37, D)
+    r2 = r1.clone()
+    got = K.rmsnorm(x, w, 1e-5, resid=r1)
+    ref = R.rmsnorm(x, w, 1e-5, resid=r2)
+    _close(got, ref, atol=0.02)
+    _close(r1, r2, atol=0.01)
+    _close(K.rmsnorm(x, w, 1e-5), R.rmsnorm(x, w, 1e-5), atol=0.02)
+
+
+@pytest.mark.parametrize("D", [384, 768, 1024])
+def test_layernorm_and_embed(D):
+    x, g, b = _rand(19, D), _rand(D), _rand(D)
+    _close(K.layernorm(x, g, b, 1e-12), R.layernorm(x, g, b, 1e-12), atol=0.03)
+    res = _rand(19, D)
+    _close(K.layernorm(x, g, b, 1e-12, resid=res), R.layernorm(x, g, b, 1e-12, resid=res), atol=0.03)
+    word, pos, typ = _rand(100, D), _rand(64, D), _rand(2, D)
+    ids = torch.randint(0, 100, (23,), device=DEV, dtype=torch.int32)
+    ps = torch.randint(0, 64, (23,), device=DEV, dtype=torch.int32)
+    _close(K.bert_embed_ln(ids, ps, None, word, pos, typ, g, b, 1e-12),
+           R.bert_embed_ln(ids, ps, None, word, pos, typ, g, b, 1e-12), atol=0.03)
+    _close(K.embed(ids, word), R.embed(ids, word), atol=0)
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+def test_pool_l2norm(mode):
+    h = _rand(50, 768)
+    cu = torch.tensor([0, 5, 5, 20, 50], device=DEV, dtype=torch.int32)
+    got = K.pool_l2norm(h, cu, mode)
+    ref = R.pool_l2norm(h, cu, mode)
+    _close(got, ref, atol=2e-3)
+    n = got.norm(dim=-1)
+    assert torch.allclose(n, torch.ones_like(n), atol=1e-3)
+
+
+@pytest.mark.parametrize("H,Hkv,D", [(4, 4, 96), (8, 2, 128), (4, 1, 64)])
+def test_rope_cache(H, Hkv, D):
+    T = 21
+    qkv = _rand(T, (H + 2 * Hkv) * D)
+    pos = torch.randint(0, 100, (T,), device=DEV, dtype=torch.int32)
+    slot = torch.randint(0, 3, (T,), device=DEV, dtype=torch.int32)
+    pos = pos + torch.arange(T, device=DEV, dtype=torch.int32) * 0  # distinct writes not required
+    # make (slot, pos) unique so cache writes are deterministic
+    pos = torch.arange(T, device=DEV, dtype=torch.int32) * 3
+    cs = R.rope_table(128, D, 10000.0, device=DEV)
+    kc1 = torch.zeros(3, Hkv, 128, D, device=DEV, dtype=torch.bfloat16)
+    vc1 = torch.zeros_like(kc1)
+    kc2, vc2 = kc1.clone(), vc1.clone()
+    a, b = qkv.clone(), qkv.clone()
+    K.rope_cache(a, pos, cs, H, Hkv, D, slot=slot, k_cache=kc1, v_cache=vc1)
+    R.rope_cache(b, pos, cs, H, Hkv, D, slot=slot, k_cache=kc2, v_cache=vc2)
+    _close(a, b, atol=0.02)
+    _close(kc1, kc2, atol=0.02)
+    _close(vc1, vc2, atol=0)
+
+
+@pytest.mark.parametrize("D", [64, 96, 128])
+@pytest.mark.parametrize("causal,H,Hkv", [(False, 4, 4), (True, 8, 2), (True, 4, 4)])
+def test_flash_attn(D, causal, H, Hkv):
+    torch.manual_seed(D + H)
+    lens = [1, 63, 64, 65, 200, 7]
+    cu = torch.tensor([0] + list(torch.tensor(lens).cumsum(0)), device=DEV, dtype=torch.int32)
+    T = sum(lens)
+    qkv = _rand(T, (H + 2 * Hkv) * D)
+    q = qkv[:, :H * D]
+    k = qkv[:, H * D:(H + Hkv) * D]
+    v = qkv[:, (H + Hkv) * D:]
+    got = K.flash_attn_varlen(q, k, v, cu, max(lens), H, Hkv, D, causal)
+    ref = R.flash_attn_varlen(q, k, v, cu, max(lens), H, Hkv, D, causal)
+    _close(got, ref, atol=0.02)
+
+
+def test_flash_attn_spike():
+    # force a late rescale: one key dominates one query (online-softmax branch coverage)
+    H, Hkv, D = 2, 2, 64
+    L = 300
+    qkv = _rand(L, 6 * D, scale=0.3)
+    qkv[250, 2 * D:3 * D] = 4.0
+    qkv[10, :D] = 4.0
+    cu = torch.tensor([0, L], device=DEV, dtype=torch.int32)
+    q, k, v = qkv[:, :2 * D], qkv[:, 2 * D:4 * D], qkv[:, 4 * D:]
+    for causal in (False, True):
+        _close(K.flash_attn_varlen(q, k, v, cu, L, H, Hkv, D, causal),
+               R.flash_attn_varlen(q, k, v, cu, L, H, Hkv, D, causal), atol=0.02)
+
+
+@pytest.mark.parametrize("H,Hkv,D", [(32, 32, 96), (32, 8, 128), (8, 1, 128), (12, 6, 64)])
+def test_decode_attn(H, Hkv, D):
+    torch.manual_seed(H * D)
+    B, S = 5, 700
+    kc, vc = _rand(7, Hkv, S, D), _rand(7, Hkv, S, D)
+    lens = torch.tensor([1, 64, 65, 300, 700], device=DEV, dtype=torch.int32)
+    slot = torch.tensor([6, 0, 3, 2, 1], device=DEV, dtype=torch.int32)
+    q = _rand(B, (H + 2 * Hkv) * D)
+    got = K.decode_attn(q, kc, vc, lens, slot, H, Hkv, D, max_len=700, chunk=128)
+    ref = R.decode_attn(q, kc, vc, lens, slot, H, Hkv, D)
+    _close(got, ref, atol=0.02)
+
+
+def test_sample_greedy_and_logprob():
+    torch.manual_seed(0)
+    B, V = 6, 32064
+    logits = _rand(B, V, scale=3.0)
+    conf = torch.zeros(B, 2, device=DEV)
+    tok, lp = K.sample(logits, 0.0, 1, 0, conf=conf)
+    rtok, rlp = R.sample(logits, 0.0, 1, 0)
+    assert torch.equal(tok.cpu(), rtok.cpu())
+    _close(lp, rlp, atol=2e-3)
+    _close(conf[:, 0], rlp.exp(), atol=2e-3)
+    assert torch.all(conf[:, 1] == 1)
+
+
+def test_sample_temperature_distribution():
+    # Gumbel-max with the hash RNG must follow softmax(logits / T)
+    V = 8
+    logits = torch.tensor([[0.0, 0.5, 1.0, 0.2, -1.0, 0.3, 0.1, 0.9]], device=DEV).to(torch.bfloat16)
+    logits = logits.repeat(4096, 1).contiguous()
+    tok, _ = K.sample(logits, 0.7, 1234, 5)
+    counts = torch.bincount(tok.long().cpu(), minlength=V).float() / 4096
+    p = torch.softmax(logits[0].float().cpu() / 0.7, -1)
+    assert (counts - p).abs().max() < 0.03
+
+
+@pytest.mark.parametrize("N,d,Q,Kk", [(1000, 768, 5, 5), (5000, 1024, 37, 20), (63, 768, 1, 3), (20000, 768, 16, 1)])
+def test_topk_dense(N, d, Q, Kk):
+    torch.manual_seed(N)
+    X = torch.nn.functional.normalize(torch.randn(N, d, device=DEV), dim=-1).to(torch.bfloat16)
+    Qv = torch.nn.functional.normalize(torch.randn(Q, d, device=DEV), dim=-1).to(torch.bfloat16)
+    Qv[0] = X[N // 2]
+    s, i = K.topk_dense(X, Qv, Kk, -1.0)
+    rs, ri = R.topk_dense(X, Qv, Kk, -1.0)
+    _close(s, rs, atol=2e-3)
+    assert (i == ri).float().mean() > 0.97
+    assert int(i[0, 0]) == N // 2
+    # filter + threshold
+    slots = (torch.arange(N, device=DEV, dtype=torch.int32) // 10).contiguous()
+    W = (N // 10 + 32) // 32
+    bitmap = torch.zeros(Q, W, dtype=torch.int32, device=DEV)
+    bitmap[:, 0] = 0b1011
+    bitmap[0, (N // 2 // 10) >> 5] |= (1 << ((N // 2 // 10) & 31))
+    s, i = K.topk_dense(X, Qv, Kk, 0.0, slots=slots, bitmap=bitmap)
+    rs, ri = R.topk_dense(X, Qv, Kk, 0.0, slots=slots, bitmap=bitmap)
+    _close(s, rs, atol=2e-3)
+    assert torch.equal(i.cpu(), ri.cpu()) or (s - rs).abs().max() < 2e-3
+
+
+def test_topk_ranges():
+    torch.manual_seed(1)
+    N, d, Q, Kk = 3000, 768, 4, 6
+    X = torch.nn.functional.normalize(torch.randn(N, d, device=DEV), dim=-1).to(torch.bfloat16)
+    Qv = torch.nn.functional.normalize(torch.randn(Q, d, device=DEV), dim=-1).to(torch.bfloat16)
+    rg = [[0, 10], [100, 700], [2990, 3000], [5, 6], [0, 3000], [1000, 1001]]
+    ro = [0, 3, 4, 5, 6]
+    ranges = torch.tensor(rg, dtype=torch.int32, device=DEV)
+    roff = torch.tensor(ro, dtype=torch.int32, device=DEV)
+    s, i = K.topk_ranges(X, Qv, ranges, roff, Kk, -1.0, max_rows=3000, rows_per_split=256)
+    rs, ri = R.topk_ranges(X, Qv, ranges, roff, Kk, -1.0)
+    _close(s, rs, atol=2e-3)
+    assert (i == ri).float().mean() > 0.95
+    assert int(i[1, 0]) == 5 and int(i[1, 1]) == -1  # single-row range
+
+
+def test_kmeans_accum():
+    X = _rand(500, 256)
+    assign = torch.randint(-1, 10, (500,), device=DEV, dtype=torch.int32)
+    s1, c1 = torch.zeros(10, 256, device=DEV), torch.zeros(10, device=DEV)
+    s2, c2 = s1.clone(), c1.clone()
+    K.kmeans_accum(X, assign, s1, c1)
+    R.kmeans_accum(X, assign, s2, c2)
+    _close(s1, s2, atol=1e-3)
+    assert torch.equal(c1, c2)
