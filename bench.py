@@ -1,0 +1,219 @@
+"""Headline benchmark: RAG QA queries/sec (+ p50 cache-miss latency, ingest docs/min) on MI355X.
+
+Metric / config from BASELINE.json: "QA queries/sec + p50 cache-miss latency; docs/min ingest at
+1/2/4/8 MI355X" on config 2: "BGE-base embedder + Phi-3-mini QA on 1xMI355X, 100k-chunk brute-force
+cosine in HBM" — here 100k chunks PER GPU (weak scaling: the index grows with N, every query is
+searched against every shard over RCCL/xGMI).
+
+One timed step = every GPU serves B cache-miss queries end to end (the reference's query path,
+cmd/query/main.go:44-136, minus the cache hit): tokenize -> BGE-base encode (HIP kernels) ->
+all-gather query vectors -> fused cosine + doc-filter + threshold + top-k on every shard ->
+all-gather + merge top-k -> build the Answer prompt from the top-k chunks (pre-tokenized at ingest)
+-> Phi-3-mini prefill (~2.8k tokens/query) + decode MAX_NEW tokens at T=0.2 (HIP kernels, HIP
+graphs) -> confidence = avg similarity x mean token probability -> detokenize.
+
+Synthetic data (no network): random-init weights of the named architectures, random unit vectors
+for the 100k background chunks per GPU (their token ids drawn from the locally trained BPE vocab),
+synthetic questions; each query filters on `--docs-per-query` random documents spread over all
+shards. MIN_SIMILARITY is set to -1 so every query retrieves exactly top_k chunks (random weights
+make the reference's 0.7 floor meaningless; -1 is the MOST work per query, never less).
+
+Launch: python bench.py [--gpus 1 --steps 3 --warmup 1]  or, for N GPUs,
+        python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+from docagents_amd.engine.engine import Engine  # noqa: E402
+from docagents_amd.parallel.dist import (all_reduce_max, all_reduce_sum, barrier, init_from_env,  # noqa: E402
+                                         shutdown)
+from docagents_amd.parallel.sharded_index import ShardedIndex  # noqa: E402
+from docagents_amd.text.chunker import Options, chunk_text  # noqa: E402
+from docagents_amd.text.synthetic import TextGen  # noqa: E402
+
+METRIC = "QA queries/sec + p50 cache-miss latency; docs/min ingest at 1/2/4/8 MI355X"
+REFERENCE_CACHE_MISS_MS = 2500.0  # README.md:590 "~2-3 seconds" (midpoint); no QPS is published
+
+
+def log(info, *a):
+    if info.rank == 0:
+        print("[bench]", *a, file=sys.stderr, flush=True)
+
+
+class ChunkTokens:
+    """Token ids of the synthetic background chunks (what ingest would have cached per chunk)."""
+
+    def __init__(self, vocab_lo: int, vocab_hi: int, seed: int = 1234, pool: int = 1 << 20):
+        rng = np.random.default_rng(seed)
+        self.pool = rng.integers(vocab_lo, vocab_hi, size=pool, dtype=np.int32)
+        self.lens = rng.integers(500, 561, size=4096)
+
+    def get(self, cid: int) -> list[int]:
+        n = int(self.lens[cid % 4096])
+        o = (cid * 7919) % (len(self.pool) - n)
+        return self.pool[o:o + n].tolist()
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--batch", type=int, default=64, help="cache-miss queries per GPU per step")
+    ap.add_argument("--index-rows", type=int, default=100_000, help="chunks per GPU shard")
+    ap.add_argument("--chunks-per-doc", type=int, default=10)
+    ap.add_argument("--docs-per-query", type=int, default=8)
+    ap.add_argument("--top-k", type=int, default=5)
+    ap.add_argument("--max-new", type=int, default=64)
+    ap.add_argument("--min-sim", type=float, default=-1.0)
+    ap.add_argument("--enc", default="bge-base")
+    ap.add_argument("--llm", default="phi3-mini")
+    ap.add_argument("--latency-reps", type=int, default=5)
+    ap.add_argument("--ingest-docs", type=int, default=16, help="docs per GPU for the ingest measurement")
+    ap.add_argument("--ingest-words", type=int, default=2000)
+    ap.add_argument("--no-graphs", action="store_true")
+    ap.add_argument("--seed", type=int, default=0)
+    a = ap.parse_args()
+
+    info = init_from_env()
+    W, R = info.world, info.rank
+    dev = info.device
+    if dev.type != "cuda":
+        raise SystemExit("bench.py needs a GPU (run it through gpurun)")
+    t_setup = time.perf_counter()
+    eng = Engine(a.enc, a.llm, dev, seed=a.seed, max_batch=a.batch, max_seq=4096, temperature=0.2,
+                 max_new_tokens=a.max_new, summary_max_new=128, use_graphs=not a.no_graphs)
+    shard = ShardedIndex(eng.index, R, W)
+    d = eng.dim
+
+    # ---- synthetic 100k-chunk shard in HBM ----
+    g = torch.Generator(device=dev)
+    g.manual_seed(1000 + R)
+    rows = a.index_rows
+    X = torch.randn((rows, d), device=dev, generator=g)
+    X = torch.nn.functional.normalize(X, dim=-1).to(torch.bfloat16)
+    ndocs = rows // a.chunks_per_doc
+    doc_ids = [f"d{R}-{i}" for i in range(ndocs)]
+    ids = (np.int64(R) * 1_000_000_000 + np.arange(rows, dtype=np.int64))
+    eng.index.add_bulk(doc_ids, [a.chunks_per_doc] * ndocs, ids, X)
+    del X
+    vocab_hi = eng.dec_tok.get_vocab_size()
+    chunks = ChunkTokens(300, vocab_hi)
+    tg = TextGen(seed=77 + R)
+
+    def make_filters(step: int):
+        rng = np.random.default_rng(10_000 + step)
+        out = []
+        for r in range(W):
+            for _ in range(B_cur):
+                rr = rng.integers(0, W, size=a.docs_per_query)
+                ii = rng.integers(0, ndocs, size=a.docs_per_query)
+                out.append([f"d{x}-{y}" for x, y in zip(rr, ii)])
+        return out
+
+    def qa_step(step: int, B: int):
+        qs = [tg.question() for _ in range(B)]
+        filters = make_filters(step)
+        qv = eng.embed(qs)
+        s, gid = shard.search(qv, a.top_k, a.min_sim, filters)
+        s_h, id_h = s.cpu().numpy(), gid.cpu().numpy()
+        items = []
+        for b in range(B):
+            valid = id_h[b] >= 0
+            sc = s_h[b][valid]
+            quality = float(sc.mean()) if len(sc) else 0.0
+            items.append((qs[b], [chunks.get(int(c)) for c in id_h[b][valid]], quality))
+        res = eng.answer_many(items, a.max_new)
+        return res, items
+
+    # ---- QA throughput ----
+    B_cur = a.batch
+    log(info, f"setup {time.perf_counter() - t_setup:.1f}s; warmup {a.warmup} steps (B={a.batch}/GPU, W={W})")
+    for i in range(a.warmup):
+        qa_step(i, a.batch)
+    barrier(); torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    plen = []
+    for i in range(a.steps):
+        res, items = qa_step(100 + i, a.batch)
+        plen.extend(len(eng.answer_prompt_ids(q, ch, a.max_new)) for q, ch, _ in items[:4])
+    torch.cuda.synchronize(); barrier()
+    dt = time.perf_counter() - t0
+    dt_max = all_reduce_max(dt, dev)
+    qps = W * a.batch * a.steps / dt_max
+
+    # ---- p50 cache-miss latency (one query per GPU, end to end) ----
+    lat = []
+    if a.latency_reps > 0:
+        B_cur = 1
+        qa_step(900, 1)  # warm the batch-1 graph
+        for i in range(a.latency_reps):
+            barrier(); torch.cuda.synchronize()
+            t1 = time.perf_counter()
+            qa_step(1000 + i, 1)
+            torch.cuda.synchronize()
+            lat.append(all_reduce_max(time.perf_counter() - t1, dev) * 1000)
+    p50 = statistics.median(lat) if lat else None
+
+    # ---- ingest docs/min: chunk -> enrich+embed -> summarize -> index (per GPU, batched) ----
+    docs_per_min = None
+    if a.ingest_docs > 0:
+        dg = TextGen(seed=500 + R)
+        texts = [dg.document(a.ingest_words) for _ in range(a.ingest_docs)]
+
+        def ingest(texts, tag):
+            all_chunks, owners = [], []
+            for j, t in enumerate(texts):
+                cs = chunk_text(t, Options(400, 80))
+                all_chunks.extend(f"Document: doc{j}.txt\n\n{c.text}" for c in cs)
+                owners.append(len(cs))
+            vec = eng.embed(all_chunks)
+            summaries = eng.summarize_many(["".join(c.text + "\n" for c in chunk_text(t, Options(400, 80))) for t in texts])
+            o = 0
+            for j, n in enumerate(owners):
+                eng.index.add(f"ing{tag}-{R}-{j}", np.arange(n) + 5_000_000_000 + o, vec[o:o + n])
+                o += n
+            return summaries
+
+        ingest(texts[:2], "w")
+        barrier(); torch.cuda.synchronize()
+        t2 = time.perf_counter()
+        ingest(texts, "t")
+        torch.cuda.synchronize(); barrier()
+        di = all_reduce_max(time.perf_counter() - t2, dev)
+        docs_per_min = W * a.ingest_docs / di * 60.0
+
+    gen = eng.gen.stats
+    out = {
+        "metric": METRIC, "value": round(qps, 3), "unit": "queries/s", "n_gpus": W, "steps": a.steps,
+        "warmup": a.warmup, "ms_per_step": round(dt_max / a.steps * 1000, 2), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
+        "data": "synthetic (random-init weights; random unit vectors for the background chunks; synthetic questions)",
+        "config": {"model": f"{a.enc} embedder + {a.llm} QA", "global_batch": W * a.batch,
+                   "seq_len": int(np.mean(plen)) if plen else None, "parallelism": f"dp{W} + {W}-way sharded index",
+                   "index_rows_per_gpu": a.index_rows, "top_k": a.top_k, "max_new_tokens": a.max_new,
+                   "temperature": 0.2, "min_similarity": a.min_sim, "docs_per_query": a.docs_per_query},
+        "p50_cache_miss_ms": round(p50, 2) if p50 else None,
+        "reference_cache_miss_ms": REFERENCE_CACHE_MISS_MS,
+        "cache_miss_speedup_vs_reference": round(REFERENCE_CACHE_MISS_MS / p50, 2) if p50 else None,
+        "ingest_docs_per_min": round(docs_per_min, 1) if docs_per_min else None,
+        "prefill_tokens": gen["prefill_tokens"], "decode_steps": gen["decode_steps"],
+    }
+    if R == 0:
+        print(json.dumps(out), flush=True)
+    shutdown()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,109 @@
+"""Environment configuration.
+
+Accepts every key of the reference (internal/config/config.go:11-42) with the same defaults, plus
+the keys of the MI355X engine. Like the reference's ``Load`` (config.go:45-51), a
+value that fails to parse is logged and the default is kept.
+"""
+from __future__ import annotations
+
+import dataclasses
+import logging
+import os
+from dataclasses import dataclass, field, fields
+
+_log = logging.getLogger("docagents.config")
+
+
+def _env(name: str):
+    return os.environ.get(name)
+
+
+@dataclass
+class Config:
+    # --- reference keys (config.go:13-41) ---
+    port: int = field(default=8080, metadata={"env": "PORT"})
+    log_level: str = field(default="info", metadata={"env": "LOG_LEVEL"})
+    max_upload_size: int = field(default=10485760, metadata={"env": "MAX_UPLOAD_SIZE"})
+    store_provider: str = field(default="sqlite", metadata={"env": "STORE_PROVIDER"})
+    db_host: str = field(default="localhost", metadata={"env": "DB_HOST"})
+    db_port: int = field(default=5432, metadata={"env": "DB_PORT"})
+    db_user: str = field(default="", metadata={"env": "DB_USER"})
+    db_password: str = field(default="", metadata={"env": "DB_PASSWORD"})
+    db_name: str = field(default="", metadata={"env": "DB_NAME"})
+    queue_provider: str = field(default="broker", metadata={"env": "QUEUE_PROVIDER"})
+    queue_url: str = field(default="", metadata={"env": "QUEUE_URL"})
+    llm_provider: str = field(default="local", metadata={"env": "LLM_PROVIDER"})
+    openai_api_key: str = field(default="", metadata={"env": "OPENAI_API_KEY"})
+    llm_model: str = field(default="phi3-mini", metadata={"env": "LLM_MODEL"})
+    embedding_model: str = field(default="bge-base", metadata={"env": "EMBEDDING_MODEL"})
+    cache_provider: str = field(default="kv", metadata={"env": "CACHE_PROVIDER"})
+    redis_addr: str = field(default="localhost:6379", metadata={"env": "REDIS_ADDR"})
+    redis_password: str = field(default="", metadata={"env": "REDIS_PASSWORD"})
+    cache_ttl: int = field(default=86400, metadata={"env": "CACHE_TTL"})
+    # --- new keys: storage / providers ---
+    data_dir: str = field(default="./data", metadata={"env": "DATA_DIR"})
+    db_path: str = field(default="", metadata={"env": "DB_PATH"})
+    embedder_provider: str = field(default="", metadata={"env": "EMBEDDER_PROVIDER"})  # "" -> follow LLM_PROVIDER
+    engine_url: str = field(default="", metadata={"env": "ENGINE_URL"})
+    query_service_url: str = field(default="http://127.0.0.1:8081/api/query", metadata={"env": "QUERY_SERVICE_URL"})
+    # --- new keys: models / numerics ---
+    embed_arch: str = field(default="bge-base", metadata={"env": "EMBED_ARCH"})
+    llm_arch: str = field(default="phi3-mini", metadata={"env": "LLM_ARCH"})
+    embed_dim: int = field(default=0, metadata={"env": "EMBED_DIM"})  # 0 -> encoder hidden size
+    dtype: str = field(default="bf16", metadata={"env": "DTYPE"})
+    tp_size: int = field(default=1, metadata={"env": "TP_SIZE"})
+    index_shards: int = field(default=1, metadata={"env": "INDEX_SHARDS"})
+    index_kind: str = field(default="flat", metadata={"env": "INDEX_KIND"})
+    ivf_lists: int = field(default=100, metadata={"env": "IVF_LISTS"})
+    ivf_probes: int = field(default=1, metadata={"env": "IVF_PROBES"})
+    min_similarity: float = field(default=0.7, metadata={"env": "MIN_SIMILARITY"})
+    chunk_max_tokens: int = field(default=400, metadata={"env": "CHUNK_MAX_TOKENS"})
+    chunk_overlap: int = field(default=80, metadata={"env": "CHUNK_OVERLAP"})
+    max_new_tokens: int = field(default=64, metadata={"env": "MAX_NEW_TOKENS"})
+    summary_max_new_tokens: int = field(default=128, metadata={"env": "SUMMARY_MAX_NEW_TOKENS"})
+    temperature: float = field(default=0.2, metadata={"env": "LLM_TEMPERATURE"})
+    weights_path: str = field(default="", metadata={"env": "WEIGHTS_PATH"})
+    seed: int = field(default=0, metadata={"env": "SEED"})
+    max_batch: int = field(default=64, metadata={"env": "ENGINE_MAX_BATCH"})
+    kv_cache_gb: float = field(default=0.0, metadata={"env": "KV_CACHE_GB"})  # 0 -> auto
+    fault_spec: str = field(default="", metadata={"env": "DA_FAULT"})
+
+    def database_url(self) -> str:
+        """config.go:56-64 (kept for parity; the sqlite store uses db_path)."""
+        return (f"postgres://{self.db_user}:{self.db_password}@{self.db_host}:{self.db_port}/"
+                f"{self.db_name}?sslmode=disable")
+
+    def sqlite_path(self) -> str:
+        if self.db_path:
+            return self.db_path
+        return os.path.join(self.data_dir, "docagents.sqlite3")
+
+    def effective_embedder_provider(self) -> str:
+        # reference quirk: embedder chosen by LLM_PROVIDER (internal/app/deps.go:239); an explicit
+        # EMBEDDER_PROVIDER overrides it here.
+        return self.embedder_provider or self.llm_provider
+
+    def replace(self, **kw) -> "Config":
+        return dataclasses.replace(self, **kw)
+
+
+def load(environ: dict | None = None) -> Config:
+    env = os.environ if environ is None else environ
+    cfg = Config()
+    for f in fields(Config):
+        key = f.metadata.get("env")
+        if not key or key not in env:
+            continue
+        raw = env[key]
+        try:
+            if f.type in ("int", int):
+                val = int(raw)
+            elif f.type in ("float", float):
+                val = float(raw)
+            else:
+                val = raw
+        except ValueError as e:
+            _log.warning("failed to parse env; using defaults where set", extra={"key": key, "err": str(e)})
+            continue
+        setattr(cfg, f.name, val)
+    return cfg

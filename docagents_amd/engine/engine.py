@@ -1,0 +1,195 @@
+"""The per-GPU inference engine: encoder + decoder + vector index shard.
+
+Implements the reference's outsourced compute contracts on-node:
+  * ``Embedder.Embed / EmbedBatch`` (internal/embeddings/embeddings.go:7-10, openai.go:38-127)
+    -> ``embed`` (preprocess identically, keep a 1:1 text->vector mapping, unit-norm output);
+  * ``llm.Client.Summarize`` (internal/llm/openai.go:40-62) -> ``summarize_many`` with map-reduce over
+    the decoder context and the same ``extractSummary`` parsing;
+  * ``llm.Client.Answer`` (openai.go:64-105) -> ``answer_many``: confidence = context quality x mean
+    token probability of the generated tokens (openai.go:101-102,149-164);
+  * ``Store.TopK``'s vector part (internal/store/postgres.go:218-285) -> ``index`` (flat / IVFFlat).
+Batching is across requests: texts are packed by tokens, prompts are generated together.
+"""
+from __future__ import annotations
+
+import threading
+import time
+
+import numpy as np
+import torch
+
+from ..models.bert import BertEncoder, pack_for_encoder
+from ..models.configs import decoder_config, encoder_config
+from ..models.llama import LlamaDecoder, TPContext
+from ..models.tokenizer import ChatFormat, decoder_tokenizer, encoder_tokenizer
+from ..text.preprocess import extract_summary, preprocess_text
+from . import prompts as P
+from .generator import Generator
+
+
+class Engine:
+    def __init__(self, embed_arch: str = "bge-base", llm_arch: str = "phi3-mini", device="cuda", seed: int = 0,
+                 tp: TPContext | None = None, max_batch: int = 64, max_seq: int = 4096, temperature: float = 0.2,
+                 max_new_tokens: int = 64, summary_max_new: int = 128, index_kind: str = "flat",
+                 ivf_lists: int = 100, ivf_probes: int = 1, load_llm: bool = True, load_encoder: bool = True,
+                 use_graphs: bool = True, embed_max_tokens: int = 65536):
+        self.device = torch.device(device)
+        self.lock = threading.RLock()
+        self.enc_cfg = encoder_config(embed_arch)
+        self.dec_cfg = decoder_config(llm_arch)
+        self.enc_tok = encoder_tokenizer(self.enc_cfg.vocab)
+        self.dec_tok = decoder_tokenizer(self.dec_cfg.vocab)
+        self.chat = ChatFormat(self.dec_tok)
+        self.temperature = temperature
+        self.max_new_tokens = max_new_tokens
+        self.summary_max_new = summary_max_new
+        self.embed_max_tokens = embed_max_tokens
+        self.encoder = BertEncoder(self.enc_cfg, self.device, seed=seed) if load_encoder else None
+        self.decoder = None
+        self.gen = None
+        if load_llm:
+            self.decoder = LlamaDecoder(self.dec_cfg, self.device, seed=seed, tp=tp)
+            self.decoder.alloc_cache(max_batch + 1, max_seq)
+            self.gen = Generator(self.decoder, max_batch=max_batch, max_seq=max_seq, temperature=temperature,
+                                 seed=seed, eos=sorted(self.chat.eos_ids), use_graphs=use_graphs)
+        from ..index import make_index
+        self.index = make_index(index_kind, self.enc_cfg.hidden, self.device, lists=ivf_lists, probes=ivf_probes)
+        self._prefix_cache: dict[str, list[int]] = {}
+        self.stats = {"embed_texts": 0, "embed_tokens": 0, "embed_s": 0.0}
+
+    @property
+    def dim(self) -> int:
+        return self.enc_cfg.hidden
+
+    # ------------------------------------------------------------------ embeddings
+    def embed(self, texts: list[str], preprocess: bool = True, out_dtype=torch.bfloat16) -> torch.Tensor:
+        """Unit-norm embeddings [n, d] on the engine device (1:1 with ``texts``)."""
+        if self.encoder is None:
+            raise RuntimeError("encoder not loaded")
+        if preprocess:
+            texts = [preprocess_text(t) for t in texts]
+        n = len(texts)
+        out = torch.empty((n, self.dim), dtype=out_dtype, device=self.device)
+        if n == 0:
+            return out
+        t0 = time.perf_counter()
+        seqs = pack_for_encoder(self.enc_tok, texts, self.enc_cfg.max_pos)
+        order = np.argsort([-len(s) for s in seqs], kind="stable")
+        with self.lock:
+            i = 0
+            while i < n:
+                j, tot = i, 0
+                while j < n and (j == i or tot + len(seqs[order[j]]) <= self.embed_max_tokens):
+                    tot += len(seqs[order[j]])
+                    j += 1
+                idx = order[i:j]
+                vec = self.encoder.encode_packed([seqs[k] for k in idx])
+                out[torch.from_numpy(idx).to(self.device)] = vec.to(out_dtype)
+                self.stats["embed_tokens"] += tot
+                i = j
+        self.stats["embed_texts"] += n
+        self.stats["embed_s"] += time.perf_counter() - t0
+        return out
+
+    def embed_one(self, text: str) -> torch.Tensor:
+        """Embed(text): error on empty-after-preprocessing input (openai.go:44-47)."""
+        t = preprocess_text(text)
+        if not t:
+            raise ValueError("text is empty after preprocessing")
+        return self.embed([t], preprocess=False, out_dtype=torch.float32)[0]
+
+    # ------------------------------------------------------------------ generation
+    def _ids(self, s: str) -> list[int]:
+        return self.dec_tok.encode(s, add_special_tokens=False).ids
+
+    def _cached_ids(self, s: str) -> list[int]:
+        v = self._prefix_cache.get(s)
+        if v is None:
+            v = self._ids(s)
+            self._prefix_cache[s] = v
+        return v
+
+    def context_budget(self, max_new: int) -> int:
+        return self.gen.cache.max_seq - max_new - 8
+
+    def answer_prompt_ids(self, question: str, chunk_ids: list[list[int]], max_new: int) -> list[int]:
+        """Chat prompt for Answer with pre-tokenized chunks (tokenized once at ingest). Drops the
+        lowest-ranked chunks first when the prompt would not fit the context."""
+        head = self._cached_ids(f"<|system|>\n{P.ANSWER_SYSTEM}<|end|>\n<|user|>\nContext:\n")
+        nl = self._cached_ids("\n")
+        tail = self._ids(f"\nQuestion: {question}<|end|>\n<|assistant|>\n")
+        budget = self.context_budget(max_new) - len(head) - len(tail)
+        ctx: list[int] = []
+        for c in chunk_ids:
+            if len(ctx) + len(c) + len(nl) > budget:
+                break
+            ctx.extend(c)
+            ctx.extend(nl)
+        return head + ctx + tail
+
+    def answer_many(self, items, max_new: int | None = None):
+        """items: (question, [chunk token-id lists ranked by score], context_quality) ->
+        [(answer, confidence)] with confidence = quality * mean token probability."""
+        max_new = max_new or self.max_new_tokens
+        prompts = [self.answer_prompt_ids(q, ch, max_new) for q, ch, _ in items]
+        with self.lock:
+            res = self.gen.generate(prompts, max_new)
+        out = []
+        for (q, ch, quality), r in zip(items, res):
+            out.append((self.chat.decode(r.tokens), float(quality) * r.mean_prob))
+        return out
+
+    def answer_text(self, question: str, context: str, quality: float, max_new: int | None = None):
+        """Answer(ctx, question, contextText, contextQuality) with an untokenized context string."""
+        max_new = max_new or self.max_new_tokens
+        ids = self._ids(context)
+        return self.answer_many([(question, [ids], quality)], max_new)[0] if ids else \
+            self.answer_many([(question, [], quality)], max_new)[0]
+
+    def summarize_many(self, texts: list[str], max_new: int | None = None) -> list[tuple[str, list[str]]]:
+        """Summarize each text; texts longer than the decoder context are summarized map-reduce:
+        window summaries (batched) then one reduce summary over them."""
+        max_new = max_new or self.summary_max_new
+        head = self._cached_ids(f"<|system|>\n{P.SUMMARIZE_SYSTEM}<|end|>\n<|user|>\n")
+        tail = self._cached_ids("<|end|>\n<|assistant|>\n")
+        budget = self.context_budget(max_new) - len(head) - len(tail)
+        all_ids = [self._ids(t) for t in texts]
+        windows, owner = [], []
+        for i, ids in enumerate(all_ids):
+            if len(ids) <= budget:
+                windows.append(head + ids + tail)
+                owner.append((i, False))
+            else:
+                for s in range(0, len(ids), budget):
+                    windows.append(head + ids[s:s + budget] + tail)
+                    owner.append((i, True))
+        with self.lock:
+            res = self.gen.generate(windows, max_new)
+        partial: dict[int, list[str]] = {}
+        final: dict[int, str] = {}
+        for (i, is_part), r in zip(owner, res):
+            txt = self.chat.decode(r.tokens)
+            if is_part:
+                partial.setdefault(i, []).append(txt)
+            else:
+                final[i] = txt
+        if partial:
+            red_ids, red_owner = [], []
+            for i, parts in partial.items():
+                joined = self._ids("\n".join(parts))[:budget]
+                red_ids.append(head + joined + tail)
+                red_owner.append(i)
+            with self.lock:
+                rres = self.gen.generate(red_ids, max_new)
+            for i, r in zip(red_owner, rres):
+                final[i] = self.chat.decode(r.tokens)
+        return [extract_summary(final[i]) for i in range(len(texts))]
+
+    # ------------------------------------------------------------------ introspection
+    def describe(self) -> dict:
+        d = {"encoder": self.enc_cfg.name, "decoder": self.dec_cfg.name, "device": str(self.device),
+             "dim": self.dim, "index": self.index.kind, "index_rows": len(self.index)}
+        if self.gen is not None:
+            d["gen"] = dict(self.gen.stats)
+        d["embed"] = dict(self.stats)
+        return d

@@ -1,0 +1,222 @@
+"""In-HBM flat (brute-force) vector index shard.
+
+Replaces the pgvector ``embeddings`` table + cosine search (internal/store/postgres.go:84,176-201,
+218-285). Rows are unit-norm bf16 vectors stored contiguously in HBM; all rows
+of one document are appended together, so a document filter becomes a list of row ranges and a
+filtered query reads only the rows it can match (exact, filter-before-top-k semantics — pgvector
+post-filters). Unfiltered / wide queries run the MFMA dense scan with a doc bitmap.
+
+Capacity grows geometrically; at 288 GB per GPU a 768-d bf16 shard holds ~180M rows.
+"""
+from __future__ import annotations
+
+import math
+import threading
+from dataclasses import dataclass, field
+
+import numpy as np
+import torch
+
+from ..ops import get_ops
+
+
+@dataclass
+class DocEntry:
+    slot: int
+    ranges: list = field(default_factory=list)  # [(start, end)]
+    rows: int = 0
+
+
+class FlatIndex:
+    kind = "flat"
+
+    def __init__(self, dim: int, device="cuda", capacity: int = 1024, dtype=torch.bfloat16):
+        self.dim = dim
+        self.device = torch.device(device)
+        self.ops = get_ops(self.device)
+        self.X = torch.zeros((max(64, capacity), dim), dtype=dtype, device=self.device)
+        self.slots_t = torch.full((self.X.shape[0],), -1, dtype=torch.int32, device=self.device)
+        self.n = 0
+        self.ids = np.zeros(self.X.shape[0], dtype=np.int64)     # external chunk id per row
+        self.ids_t = torch.zeros(self.X.shape[0], dtype=torch.int64, device=self.device)  # device mirror
+        self.docs: dict[str, DocEntry] = {}
+        self.slot_docs: list[str | None] = []
+        self.lock = threading.RLock()
+
+    # ----------------------------------------------------------------- mutation
+    def _grow(self, need: int):
+        cap = self.X.shape[0]
+        if need <= cap:
+            return
+        new = max(need, int(cap * 1.5) + 64)
+        X = torch.zeros((new, self.dim), dtype=self.X.dtype, device=self.device)
+        X[:self.n] = self.X[:self.n]
+        s = torch.full((new,), -1, dtype=torch.int32, device=self.device)
+        s[:self.n] = self.slots_t[:self.n]
+        ids = np.zeros(new, dtype=np.int64)
+        ids[:self.n] = self.ids[:self.n]
+        ids_t = torch.zeros(new, dtype=torch.int64, device=self.device)
+        ids_t[:self.n] = self.ids_t[:self.n]
+        self.X, self.slots_t, self.ids, self.ids_t = X, s, ids, ids_t
+
+    def doc_slot(self, doc_id: str) -> int:
+        e = self.docs.get(doc_id)
+        if e is None:
+            e = DocEntry(slot=len(self.slot_docs))
+            self.docs[doc_id] = e
+            self.slot_docs.append(doc_id)
+        return e.slot
+
+    def add(self, doc_id: str, ids: np.ndarray, vecs: torch.Tensor) -> tuple[int, int]:
+        """Append the vectors of one document. ``vecs`` [n, d] (unit norm), any float dtype/device."""
+        n = int(vecs.shape[0])
+        if n == 0:
+            self.doc_slot(doc_id)
+            return (self.n, self.n)
+        if vecs.shape[1] != self.dim:
+            raise ValueError(f"vector dim {vecs.shape[1]} != index dim {self.dim}")
+        with self.lock:
+            slot = self.doc_slot(doc_id)
+            s0 = self.n
+            self._grow(s0 + n)
+            self.X[s0:s0 + n] = vecs.to(device=self.device, dtype=self.X.dtype)
+            self.slots_t[s0:s0 + n] = slot
+            self.ids[s0:s0 + n] = np.asarray(ids, dtype=np.int64)
+            self.ids_t[s0:s0 + n] = torch.from_numpy(self.ids[s0:s0 + n].copy()).to(self.device)
+            self.n = s0 + n
+            e = self.docs[doc_id]
+            e.ranges.append((s0, s0 + n))
+            e.rows += n
+            return (s0, s0 + n)
+
+    def add_bulk(self, doc_ids: list[str], rows_per_doc: list[int], ids: np.ndarray, vecs: torch.Tensor):
+        """Bulk load (benchmarks / snapshot restore): documents laid out back to back."""
+        with self.lock:
+            n = int(vecs.shape[0])
+            s0 = self.n
+            self._grow(s0 + n)
+            self.X[s0:s0 + n] = vecs.to(device=self.device, dtype=self.X.dtype)
+            self.ids[s0:s0 + n] = ids
+            self.ids_t[s0:s0 + n] = torch.from_numpy(np.asarray(ids, dtype=np.int64)).to(self.device)
+            slots = np.empty(n, dtype=np.int32)
+            r = s0
+            for d, k in zip(doc_ids, rows_per_doc):
+                sl = self.doc_slot(d)
+                slots[r - s0:r - s0 + k] = sl
+                e = self.docs[d]
+                e.ranges.append((r, r + k))
+                e.rows += k
+                r += k
+            self.slots_t[s0:s0 + n] = torch.from_numpy(slots).to(self.device)
+            self.n = s0 + n
+
+    def remove_doc(self, doc_id: str) -> int:
+        """Drop a document's rows from search (rows become unreachable; compacted on snapshot)."""
+        with self.lock:
+            e = self.docs.get(doc_id)
+            if e is None:
+                return 0
+            for a, b in e.ranges:
+                self.slots_t[a:b] = -1
+            n = e.rows
+            e.ranges, e.rows = [], 0
+            return n
+
+    def __len__(self):
+        return self.n
+
+    # ----------------------------------------------------------------- search
+    def _ranges_for(self, doc_filters):
+        ranges, off, maxrows = [], [0], 0
+        for f in doc_filters:
+            tot = 0
+            for d in f:
+                e = self.docs.get(d)
+                if e is None:
+                    continue
+                for a, b in e.ranges:
+                    ranges.append((a, b))
+                    tot += b - a
+            off.append(len(ranges))
+            maxrows = max(maxrows, tot)
+        return ranges, off, maxrows
+
+    def search(self, q: torch.Tensor, k: int, min_sim: float, doc_filters: list[list[str]] | None = None):
+        """q [Q, d] unit-norm -> (scores fp32 [Q, k], row idx int32 [Q, k]) on device; -inf / -1 padding.
+        doc_filters: per-query list of document ids (None = all documents)."""
+        Q = q.shape[0]
+        q = q.to(device=self.device, dtype=self.X.dtype).contiguous()
+        with self.lock:
+            if self.n == 0 or Q == 0:
+                return (torch.full((Q, k), float("-inf"), device=self.device),
+                        torch.full((Q, k), -1, dtype=torch.int32, device=self.device))
+            X = self.X[:self.n]
+            if doc_filters is None:
+                return self._dense(X, q, k, min_sim, self.slots_t[:self.n])
+            ranges, off, maxrows = self._ranges_for(doc_filters)
+            if maxrows == 0:
+                return (torch.full((Q, k), float("-inf"), device=self.device),
+                        torch.full((Q, k), -1, dtype=torch.int32, device=self.device))
+            if maxrows * Q > 4 * self.n and self.dim % 32 == 0:
+                # wide filters: one MFMA dense scan + bitmap beats per-query range scans
+                return self._dense(X, q, k, min_sim, self.slots_t[:self.n], doc_filters)
+            rt = torch.tensor(ranges, dtype=torch.int32, device=self.device).view(-1, 2)
+            ot = torch.tensor(off, dtype=torch.int32, device=self.device)
+            return self.ops.topk_ranges(X, q, rt, ot, k, min_sim, max_rows=maxrows)
+
+    def _dense(self, X, q, k, min_sim, slots, doc_filters=None):
+        """MFMA dense scan; doc filter as a bitmap over local doc slots. Removed rows (slot -1) map to
+        a guard slot whose bit is never set."""
+        Q = q.shape[0]
+        nslots = len(self.slot_docs)
+        guard = nslots
+        W = (nslots + 1 + 31) // 32
+        bm = np.zeros((Q, W), dtype=np.uint32)
+        if doc_filters is None:
+            full, rem = divmod(nslots, 32)
+            bm[:, :full] = 0xFFFFFFFF
+            if rem:
+                bm[:, full] = (1 << rem) - 1
+        else:
+            for i, f in enumerate(doc_filters):
+                for d in f:
+                    e = self.docs.get(d)
+                    if e is not None and e.rows:
+                        bm[i, e.slot >> 5] |= np.uint32(1 << (e.slot & 31))
+        bitmap = torch.from_numpy(bm.view(np.int32)).to(self.device)
+        slots = torch.where(slots < 0, torch.full_like(slots, guard), slots).contiguous()
+        return self.ops.topk_dense(X, q, k, min_sim, slots=slots, bitmap=bitmap)
+
+    def gather_ids(self, rows: torch.Tensor) -> torch.Tensor:
+        """Device: row indices (int32, -1 = none) -> external ids (int64, -1 = none)."""
+        r = rows.long()
+        return torch.where(r >= 0, self.ids_t[r.clamp_min(0)], torch.full_like(r, -1))
+
+    def row_ids(self, rows: np.ndarray) -> np.ndarray:
+        out = np.full(rows.shape, -1, dtype=np.int64)
+        m = rows >= 0
+        out[m] = self.ids[rows[m]]
+        return out
+
+    # ----------------------------------------------------------------- snapshot
+    def state_dict(self) -> dict:
+        live = []
+        for d, e in self.docs.items():
+            for a, b in e.ranges:
+                live.append((d, a, b))
+        return {"dim": self.dim, "live": live, "X": self.X[:self.n].cpu(), "ids": self.ids[:self.n].copy()}
+
+    def nbytes(self) -> int:
+        return self.n * self.dim * self.X.element_size()
+
+
+def bytes_per_row(dim: int) -> int:
+    return dim * 2 + 4
+
+
+def rows_for_budget(dim: int, gbytes: float) -> int:
+    return int(gbytes * 1e9 // bytes_per_row(dim))
+
+
+def _pad64(n: int) -> int:
+    return int(math.ceil(n / 64) * 64)

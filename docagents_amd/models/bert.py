@@ -1,0 +1,141 @@
+"""BERT-family sentence encoder (BGE / E5) on the gfx950 kernels.
+
+Replaces the OpenAI embeddings client (internal/embeddings/openai.go:38-127):
+packed variable-length batches (no padding), fused embeddings+LayerNorm, GEMMs with fused
+bias / GELU / residual epilogues, bidirectional varlen flash attention, and CLS (BGE) or mean (E5)
+pooling fused with the L2 normalisation. Output vectors are unit-norm like the reference's
+``normalize`` (openai.go:146-158).
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+import torch
+
+from ..ops import get_ops
+from .configs import EncoderConfig
+
+EPI_BIAS, EPI_GELU, EPI_RESID = 1, 2, 4
+
+
+def _randn(shape, gen, device, std=0.02, dtype=torch.bfloat16):
+    t = torch.empty(shape, dtype=torch.float32, device=device)
+    t.normal_(0.0, std, generator=gen)
+    return t.to(dtype)
+
+
+class BertEncoder:
+    def __init__(self, cfg: EncoderConfig, device="cuda", seed: int = 0, weights: dict | None = None):
+        self.cfg = cfg
+        self.device = torch.device(device)
+        self.ops = get_ops(self.device)
+        self.w = weights if weights is not None else self._random_init(seed)
+
+    # ------------------------------------------------------------------ weights
+    def _random_init(self, seed: int) -> dict:
+        c, dev = self.cfg, self.device
+        gen = torch.Generator(device=dev)
+        gen.manual_seed(seed * 7919 + 17)
+        h, f = c.hidden, c.ffn
+        ones = lambda n: torch.ones(n, dtype=torch.bfloat16, device=dev)  # noqa: E731
+        zeros = lambda n: torch.zeros(n, dtype=torch.bfloat16, device=dev)  # noqa: E731
+        w = {
+            "word": _randn((c.vocab, h), gen, dev), "pos": _randn((c.max_pos, h), gen, dev),
+            "type": _randn((c.type_vocab, h), gen, dev), "emb_ln_g": ones(h), "emb_ln_b": zeros(h),
+            "layers": [],
+        }
+        for _ in range(c.layers):
+            w["layers"].append({
+                "wqkv": _randn((3 * h, h), gen, dev), "bqkv": zeros(3 * h),
+                "wo": _randn((h, h), gen, dev), "bo": zeros(h),
+                "ln1_g": ones(h), "ln1_b": zeros(h),
+                "w1": _randn((f, h), gen, dev), "b1": zeros(f),
+                "w2": _randn((h, f), gen, dev), "b2": zeros(h),
+                "ln2_g": ones(h), "ln2_b": zeros(h),
+            })
+        return w
+
+    @classmethod
+    def from_hf_state_dict(cls, cfg: EncoderConfig, sd: dict, device="cuda"):
+        """Map a HF BertModel state dict (e.g. BGE safetensors) onto our packed layout."""
+        dev = torch.device(device)
+        g = lambda k: sd[k].to(device=dev, dtype=torch.bfloat16).contiguous()  # noqa: E731
+        pre = "bert." if any(k.startswith("bert.") for k in sd) else ""
+        w = {"word": g(pre + "embeddings.word_embeddings.weight"), "pos": g(pre + "embeddings.position_embeddings.weight"),
+             "type": g(pre + "embeddings.token_type_embeddings.weight"),
+             "emb_ln_g": g(pre + "embeddings.LayerNorm.weight"), "emb_ln_b": g(pre + "embeddings.LayerNorm.bias"),
+             "layers": []}
+        for i in range(cfg.layers):
+            p = f"{pre}encoder.layer.{i}."
+            w["layers"].append({
+                "wqkv": torch.cat([g(p + f"attention.self.{n}.weight") for n in ("query", "key", "value")]).contiguous(),
+                "bqkv": torch.cat([g(p + f"attention.self.{n}.bias") for n in ("query", "key", "value")]).contiguous(),
+                "wo": g(p + "attention.output.dense.weight"), "bo": g(p + "attention.output.dense.bias"),
+                "ln1_g": g(p + "attention.output.LayerNorm.weight"), "ln1_b": g(p + "attention.output.LayerNorm.bias"),
+                "w1": g(p + "intermediate.dense.weight"), "b1": g(p + "intermediate.dense.bias"),
+                "w2": g(p + "output.dense.weight"), "b2": g(p + "output.dense.bias"),
+                "ln2_g": g(p + "output.LayerNorm.weight"), "ln2_b": g(p + "output.LayerNorm.bias"),
+            })
+        return cls(cfg, device, weights=w)
+
+    # ------------------------------------------------------------------ forward
+    def forward(self, ids: torch.Tensor, positions: torch.Tensor, cu_seqlens: torch.Tensor, max_seqlen: int):
+        """ids/positions int32 [T] (packed), cu_seqlens int32 [B+1] -> hidden bf16 [T, H]."""
+        c, o, w = self.cfg, self.ops, self.w
+        h, nh, hd = c.hidden, c.heads, c.head_dim
+        x = o.bert_embed_ln(ids, positions, None, w["word"], w["pos"], w["type"], w["emb_ln_g"], w["emb_ln_b"], c.eps)
+        for L in w["layers"]:
+            qkv = o.gemm(x, L["wqkv"], bias=L["bqkv"], epi=EPI_BIAS)
+            a = o.flash_attn_varlen(qkv[:, :h], qkv[:, h:2 * h], qkv[:, 2 * h:], cu_seqlens, max_seqlen, nh, nh, hd,
+                                    causal=False)
+            x1 = o.gemm(a, L["wo"], bias=L["bo"], epi=EPI_RESID, resid=x)
+            x = o.layernorm(x1, L["ln1_g"], L["ln1_b"], c.eps)
+            f = o.gemm(x, L["w1"], bias=L["b1"], epi=EPI_GELU)
+            x2 = o.gemm(f, L["w2"], bias=L["b2"], epi=EPI_RESID, resid=x)
+            x = o.layernorm(x2, L["ln2_g"], L["ln2_b"], c.eps)
+        return x
+
+    def encode_packed(self, seqs: list[list[int]], out16: torch.Tensor | None = None) -> torch.Tensor:
+        """Token-id sequences -> unit-norm embeddings. Returns bf16 [B, H] if out16 given else fp32."""
+        lens = np.fromiter((len(s) for s in seqs), dtype=np.int64, count=len(seqs))
+        if len(seqs) == 0:
+            return torch.empty((0, self.cfg.hidden), dtype=torch.float32, device=self.device)
+        cu = np.zeros(len(seqs) + 1, dtype=np.int32)
+        np.cumsum(lens, out=cu[1:])
+        flat = np.fromiter((t for s in seqs for t in s), dtype=np.int32, count=int(cu[-1]))
+        pos = np.arange(int(cu[-1]), dtype=np.int32) - np.repeat(cu[:-1], lens)
+        dev = self.device
+        ids_t = torch.from_numpy(flat).to(dev, non_blocking=True)
+        pos_t = torch.from_numpy(pos).to(dev, non_blocking=True)
+        cu_t = torch.from_numpy(cu).to(dev, non_blocking=True)
+        hid = self.forward(ids_t, pos_t, cu_t, int(lens.max()))
+        mode = 0 if self.cfg.pooling == "cls" else 1
+        if out16 is not None:
+            return self.ops.pool_l2norm(hid, cu_t, mode, out16=out16)
+        return self.ops.pool_l2norm(hid, cu_t, mode)
+
+    def flops_per_token(self, seqlen: int) -> float:
+        c = self.cfg
+        lin = 2 * (4 * c.hidden * c.hidden + 2 * c.hidden * c.ffn)
+        return c.layers * (lin + 4 * seqlen * c.hidden)
+
+    def param_bytes(self) -> int:
+        return 2 * self.cfg.param_count()
+
+
+def pack_for_encoder(tok, texts: list[str], max_len: int) -> list[list[int]]:
+    """Tokenize with [CLS]/[SEP] and truncate to the encoder's max positions (BERT max 512,
+    SURVEY.md §5.7)."""
+    encs = tok.encode_batch(texts, add_special_tokens=True)
+    out = []
+    for e in encs:
+        ids = e.ids
+        if len(ids) > max_len:
+            ids = ids[:max_len - 1] + [ids[-1]]
+        out.append(ids)
+    return out
+
+
+def est_tokens(texts: list[str]) -> int:
+    return int(math.fsum(len(t) for t in texts) / 4) + 2 * len(texts)

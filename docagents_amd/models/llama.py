@@ -1,0 +1,262 @@
+"""Llama-3 / Phi-3 decoder on the gfx950 kernels, with Megatron-style tensor parallelism over RCCL.
+
+Replaces gpt-4o-mini for ``Summarize`` and ``Answer`` (internal/llm/openai.go:40-105; SURVEY.md §2.4
+N6-N8). Per layer (hidden state x is the residual stream, updated in place):
+
+    h   = RMSNorm(x)                                   rmsnorm kernel
+    qkv = h @ Wqkv^T                                   MFMA GEMM   (column-parallel: local heads)
+    RoPE(q, k) + write k, v to the KV cache            rope_cache kernel
+    a   = attention(q, K, V)                           varlen flash prefill / split-KV decode
+    x   = x + a @ Wo^T                                 GEMM + fused residual epilogue (row-parallel
+                                                       -> RCCL all-reduce over xGMI when TP > 1)
+    h   = RMSNorm(x)
+    g   = silu(h Wg^T) * (h Wu^T)                      ONE GEMM with the fused SwiGLU epilogue
+    x   = x + g @ Wdown^T                              GEMM + residual (row-parallel + all-reduce)
+
+TP layout (rank r of t): local q/k/v heads, F/t FFN features, vocab-parallel lm_head whose [B, V/t]
+logits are all-gathered before the (replicated, identically seeded) sampler. With TP the residual
+is added by rank 0's epilogue only, so a single in-place all-reduce yields x + sum of partials.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from ..ops import get_ops
+from ..ops.reference import interleave_gate_up, rope_table
+from .configs import DecoderConfig
+
+EPI_NONE, EPI_SWIGLU, EPI_RESID = 0, 3, 4
+
+
+class TPContext:
+    """Tensor-parallel process group (identity when size == 1)."""
+
+    def __init__(self, rank: int = 0, size: int = 1, group=None):
+        self.rank, self.size, self.group = rank, size, group
+
+    def all_reduce_(self, t: torch.Tensor) -> torch.Tensor:
+        if self.size > 1:
+            import torch.distributed as dist
+            dist.all_reduce(t, group=self.group)
+        return t
+
+    def all_gather_cols(self, t: torch.Tensor) -> torch.Tensor:
+        """[B, n] on every rank -> [B, n * size] (rank-major columns)."""
+        if self.size == 1:
+            return t
+        import torch.distributed as dist
+        out = torch.empty((self.size,) + tuple(t.shape), dtype=t.dtype, device=t.device)
+        dist.all_gather_into_tensor(out, t.contiguous(), group=self.group)
+        return out.permute(1, 0, 2).reshape(t.shape[0], -1)
+
+
+def _randn(shape, gen, device, std=0.02):
+    t = torch.empty(shape, dtype=torch.float32, device=device)
+    t.normal_(0.0, std, generator=gen)
+    return t.to(torch.bfloat16)
+
+
+def shard_weights(cfg: DecoderConfig, full: dict, rank: int, size: int) -> dict:
+    """Slice a full (unsharded) weight dict for TP rank ``rank`` of ``size``."""
+    if size == 1:
+        return full
+    H, Hkv, D, F, V = cfg.heads, cfg.kv_heads, cfg.head_dim, cfg.ffn, cfg.vocab
+    assert H % size == 0 and Hkv % size == 0 and F % (16 * size) == 0 and V % size == 0
+    hl, kl, fl, vl = H // size, Hkv // size, F // size, V // size
+    out = {"embed": full["embed"], "norm": full["norm"],
+           "lm_head": full["lm_head"][rank * vl:(rank + 1) * vl].contiguous(), "layers": []}
+    for L in full["layers"]:
+        q = L["wqkv"][:H * D].view(H, D, -1)[rank * hl:(rank + 1) * hl].reshape(hl * D, -1)
+        k = L["wqkv"][H * D:(H + Hkv) * D].view(Hkv, D, -1)[rank * kl:(rank + 1) * kl].reshape(kl * D, -1)
+        v = L["wqkv"][(H + Hkv) * D:].view(Hkv, D, -1)[rank * kl:(rank + 1) * kl].reshape(kl * D, -1)
+        out["layers"].append({
+            "wqkv": torch.cat([q, k, v]).contiguous(),
+            "wo": L["wo"][:, rank * hl * D:(rank + 1) * hl * D].contiguous(),
+            "w_gu": L["w_gu"][2 * rank * fl:2 * (rank + 1) * fl].contiguous(),
+            "w_down": L["w_down"][:, rank * fl:(rank + 1) * fl].contiguous(),
+            "ln_attn": L["ln_attn"], "ln_mlp": L["ln_mlp"],
+        })
+    return out
+
+
+def random_weights(cfg: DecoderConfig, device, seed: int = 0, tp_rank: int = 0, tp_size: int = 1,
+                   full_then_shard: bool = False) -> dict:
+    """Seeded random init. Large models generate only the local TP shard (seeded per shard);
+    ``full_then_shard`` builds the full model first (tests: TP result == unsharded result)."""
+    dev = torch.device(device)
+    if full_then_shard and tp_size > 1:
+        return shard_weights(cfg, random_weights(cfg, device, seed), tp_rank, tp_size)
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(seed * 1_000_003 + 101)  # shared part (embedding, norms) identical on all ranks
+    h, D, F, V = cfg.hidden, cfg.head_dim, cfg.ffn, cfg.vocab
+    hl, kl, fl, vl = cfg.heads // tp_size, cfg.kv_heads // tp_size, F // tp_size, V // tp_size
+    w = {"embed": _randn((V, h), gen, dev), "norm": torch.ones(h, dtype=torch.bfloat16, device=dev), "layers": []}
+    gen.manual_seed(seed * 1_000_003 + 7 * tp_rank + 1)
+    std_o = 0.02 / (2 * cfg.layers) ** 0.5
+    for _ in range(cfg.layers):
+        gate = _randn((fl, h), gen, dev)
+        up = _randn((fl, h), gen, dev)
+        w["layers"].append({
+            "wqkv": _randn(((hl + 2 * kl) * D, h), gen, dev),
+            "wo": _randn((h, hl * D), gen, dev, std_o),
+            "w_gu": interleave_gate_up(gate, up),
+            "w_down": _randn((h, fl), gen, dev, std_o),
+            "ln_attn": torch.ones(h, dtype=torch.bfloat16, device=dev),
+            "ln_mlp": torch.ones(h, dtype=torch.bfloat16, device=dev),
+        })
+        del gate, up
+    w["lm_head"] = _randn((vl, h), gen, dev)
+    return w
+
+
+class KVCache:
+    """Contiguous per-slot KV cache: k/v [layers][slots, Hkv_local, max_seq, D] (one allocation)."""
+
+    def __init__(self, cfg: DecoderConfig, slots: int, max_seq: int, tp_size: int, device):
+        self.slots, self.max_seq = slots, max_seq
+        self.hkv = cfg.kv_heads // tp_size
+        self.buf = torch.zeros((cfg.layers, 2, slots, self.hkv, max_seq, cfg.head_dim), dtype=torch.bfloat16,
+                               device=device)
+        self.free = list(range(slots - 1, -1, -1))
+
+    def k(self, layer):
+        return self.buf[layer, 0]
+
+    def v(self, layer):
+        return self.buf[layer, 1]
+
+    def acquire(self, n: int) -> list[int]:
+        if n > len(self.free):
+            raise RuntimeError(f"KV cache exhausted: want {n} slots, {len(self.free)} free")
+        return [self.free.pop() for _ in range(n)]
+
+    def release(self, ids):
+        self.free.extend(ids)
+
+    @staticmethod
+    def bytes_for(cfg: DecoderConfig, slots: int, max_seq: int, tp_size: int = 1) -> int:
+        return cfg.layers * 2 * slots * (cfg.kv_heads // tp_size) * max_seq * cfg.head_dim * 2
+
+
+class LlamaDecoder:
+    def __init__(self, cfg: DecoderConfig, device="cuda", seed: int = 0, tp: TPContext | None = None,
+                 weights: dict | None = None):
+        self.cfg = cfg
+        self.device = torch.device(device)
+        self.ops = get_ops(self.device)
+        self.tp = tp or TPContext()
+        t = self.tp.size
+        if cfg.heads % t or cfg.kv_heads % t:
+            raise ValueError(f"TP={t} must divide heads={cfg.heads} and kv_heads={cfg.kv_heads}")
+        self.hl, self.kl = cfg.heads // t, cfg.kv_heads // t
+        self.w = weights if weights is not None else random_weights(cfg, self.device, seed, self.tp.rank, t)
+        self.cos_sin = rope_table(cfg.max_pos, cfg.head_dim, cfg.rope_theta, self.device)
+        self.cache: KVCache | None = None
+
+    def alloc_cache(self, slots: int, max_seq: int) -> KVCache:
+        max_seq = min(max_seq, self.cfg.max_pos)
+        self.cache = KVCache(self.cfg, slots, max_seq, self.tp.size, self.device)
+        return self.cache
+
+    # ------------------------------------------------------------- shared layer body
+    def _attn_out_and_mlp(self, L, a, x):
+        o, tp = self.ops, self.tp
+        if tp.size == 1 or tp.rank == 0:
+            o.gemm(a, L["wo"], epi=EPI_RESID, resid=x, out=x)
+        else:
+            o.gemm(a, L["wo"], out=x)
+        tp.all_reduce_(x)
+        h = o.rmsnorm(x, L["ln_mlp"], self.cfg.eps)
+        g = o.gemm(h, L["w_gu"], epi=EPI_SWIGLU)
+        if tp.size == 1 or tp.rank == 0:
+            o.gemm(g, L["w_down"], epi=EPI_RESID, resid=x, out=x)
+        else:
+            o.gemm(g, L["w_down"], out=x)
+        tp.all_reduce_(x)
+        return x
+
+    def _logits(self, hlast):
+        o = self.ops
+        h = o.rmsnorm(hlast, self.w["norm"], self.cfg.eps)
+        logits = o.gemm(h, self.w["lm_head"])
+        return self.tp.all_gather_cols(logits)
+
+    # ------------------------------------------------------------- prefill
+    def prefill(self, ids: torch.Tensor, pos: torch.Tensor, slot_tok: torch.Tensor, cu: torch.Tensor,
+                max_seqlen: int, last_idx: torch.Tensor) -> torch.Tensor:
+        """Packed causal prefill; writes the KV cache; returns logits [B, V] of each sequence's last token."""
+        c, o, cache = self.cfg, self.ops, self.cache
+        D, hl, kl = c.head_dim, self.hl, self.kl
+        x = o.embed(ids, self.w["embed"])
+        for li, L in enumerate(self.w["layers"]):
+            h = o.rmsnorm(x, L["ln_attn"], c.eps)
+            qkv = o.gemm(h, L["wqkv"])
+            o.rope_cache(qkv, pos, self.cos_sin, hl, kl, D, slot=slot_tok, k_cache=cache.k(li), v_cache=cache.v(li))
+            a = o.flash_attn_varlen(qkv[:, :hl * D], qkv[:, hl * D:(hl + kl) * D], qkv[:, (hl + kl) * D:], cu,
+                                    max_seqlen, hl, kl, D, causal=True)
+            del qkv, h
+            x = self._attn_out_and_mlp(L, a, x)
+        return self._logits(x.index_select(0, last_idx))
+
+    # ------------------------------------------------------------- decode (graph-capturable)
+    def decode_step(self, st: "DecodeState") -> torch.Tensor:
+        c, o, cache = self.cfg, self.ops, self.cache
+        D, hl, kl = c.head_dim, self.hl, self.kl
+        x = o.embed(st.tokens, self.w["embed"], out=st.x)
+        for li, L in enumerate(self.w["layers"]):
+            h = o.rmsnorm(x, L["ln_attn"], c.eps, out=st.h)
+            qkv = o.gemm(h, L["wqkv"], out=st.qkv)
+            o.rope_cache(qkv, st.pos, self.cos_sin, hl, kl, D, slot=st.slot, k_cache=cache.k(li), v_cache=cache.v(li))
+            a = o.decode_attn(qkv, cache.k(li), cache.v(li), st.lens, st.slot, hl, kl, D, max_len=cache.max_seq,
+                              out=st.attn)
+            self._attn_out_and_mlp(L, a, x)
+        logits = self._logits(x)
+        st.logits.copy_(logits)
+        o.sample(st.logits, st.temperature, st.seed, 0, out_tok=st.tokens, out_lp=st.lp, conf=st.conf,
+                 active=st.active, ctr=st.pos, pos=st.pos, lens=st.lens, hist=st.hist, start=st.start, eos=st.eos)
+        return st.tokens
+
+    def prefill_flops(self, lens) -> float:
+        c = self.cfg
+        h, D = c.hidden, c.head_dim
+        lin = 2 * (h * (c.heads + 2 * c.kv_heads) * D + c.heads * D * h + 3 * h * c.ffn)
+        tot = 0.0
+        for L in lens:
+            tot += c.layers * (L * lin + 2 * c.heads * D * L * L) + 2 * h * c.vocab
+        return tot
+
+
+class DecodeState:
+    """Static device buffers for a batch bucket of B sequences (HIP-graph friendly)."""
+
+    def __init__(self, model: LlamaDecoder, B: int, max_new: int, temperature: float, seed: int, eos=()):
+        c, dev = model.cfg, model.device
+        i32 = dict(dtype=torch.int32, device=dev)
+        self.B = B
+        self.tokens = torch.zeros(B, **i32)
+        self.pos = torch.zeros(B, **i32)
+        self.lens = torch.ones(B, **i32)
+        self.slot = torch.zeros(B, **i32)
+        self.active = torch.zeros(B, **i32)
+        self.start = torch.zeros(B, **i32)
+        self.hist = torch.full((B, max(1, max_new)), -1, **i32)
+        self.conf = torch.zeros(B, 2, dtype=torch.float32, device=dev)
+        self.lp = torch.zeros(B, dtype=torch.float32, device=dev)
+        h = c.hidden
+        self.x = torch.zeros(B, h, dtype=torch.bfloat16, device=dev)
+        self.h = torch.zeros(B, h, dtype=torch.bfloat16, device=dev)
+        self.qkv = torch.zeros(B, (model.hl + 2 * model.kl) * c.head_dim, dtype=torch.bfloat16, device=dev)
+        self.attn = torch.zeros(B, model.hl * c.head_dim, dtype=torch.bfloat16, device=dev)
+        self.logits = torch.zeros(B, c.vocab, dtype=torch.bfloat16, device=dev)
+        self.temperature, self.seed, self.eos = temperature, seed, tuple(eos)[:4]
+        self.graph = None
+
+
+def pack_prompts(prompts: list[list[int]]):
+    lens = np.fromiter((len(p) for p in prompts), dtype=np.int64, count=len(prompts))
+    cu = np.zeros(len(prompts) + 1, dtype=np.int32)
+    np.cumsum(lens, out=cu[1:])
+    flat = np.fromiter((t for p in prompts for t in p), dtype=np.int32, count=int(cu[-1]))
+    pos = (np.arange(int(cu[-1]), dtype=np.int64) - np.repeat(cu[:-1], lens)).astype(np.int32)
+    return flat, pos, cu, lens

@@ -63,18 +63,32 @@ __global__ void rope_cache_kernel(bf16_t* __restrict__ qkv, const int* __restric
 }
 
 // One workgroup per row of logits [B, V] (bf16). temperature <= 0 -> greedy.
-// out_tok[b], out_lp[b] = log softmax(logits)[tok]; optional running confidence accumulators
-// conf_sum[b] += exp(lp), conf_cnt[b] += 1 (mean token probability, llm/openai.go:149-164).
+// Device-side decode bookkeeping so one decode step is graph-capturable (no host round trip):
+//   ctr[b]   : per-row RNG counter (the row's position); null -> `step`
+//   out_tok  : sampled token (also the next step's input token)
+//   out_lp   : log softmax(logits)[tok] under the untempered distribution
+//   conf     : [B, 2] running (sum exp(lp), count) -> mean token probability (llm/openai.go:149-164)
+//   active   : rows still generating; cleared on EOS or when the history is full
+//   pos/lens : advanced by one for active rows
+//   hist     : hist[b * hist_ld + (pos[b] - start[b])] = tok (generation history)
+struct SampleArgs {
+  const bf16_t* logits; int V, ld; float temperature; unsigned seed, step;
+  const int* ctr; int* out_tok; float* out_lp; float* conf; int* active; int* pos; int* lens;
+  int* hist; const int* start; int hist_ld; int eos0, eos1, eos2, eos3;
+};
+
 __global__ void __launch_bounds__(1024)
-sample_kernel(const bf16_t* __restrict__ logits, int V, int ld, float temperature, unsigned seed,
-              unsigned step, int* __restrict__ out_tok, float* __restrict__ out_lp,
-              float* __restrict__ conf_sum, const int* __restrict__ active) {
+sample_kernel(SampleArgs a) {
   __shared__ float redf[16];
   __shared__ float bestv[16];
   __shared__ int besti[16];
   const int b = blockIdx.x;
-  const bf16_t* row = logits + (size_t)b * ld;
+  const bf16_t* row = a.logits + (size_t)b * a.ld;
+  const int V = a.V;
+  const float temperature = a.temperature;
   const float invT = temperature > 0.f ? 1.f / temperature : 0.f;
+  const unsigned rs = a.ctr ? (unsigned)a.ctr[b] : a.step;
+  const unsigned rkey = rs * 131071u + (unsigned)b;
   float mx = -INFINITY, bv = -INFINITY;
   int bi = 0;
   for (int c = threadIdx.x; c < V / 8; c += blockDim.x) {
@@ -84,13 +98,8 @@ sample_kernel(const bf16_t* __restrict__ logits, int V, int ld, float temperatur
       const float x = bf2f((bf16_t)((e & 1) ? (u[e >> 1] >> 16) : (u[e >> 1] & 0xffff)));
       const int v = c * 8 + e;
       mx = fmaxf(mx, x);
-      float score;
-      if (temperature > 0.f) {
-        const float uu = u01(seed, step * 131071u + (unsigned)b, (unsigned)v);
-        score = x * invT - __logf(-__logf(uu));
-      } else {
-        score = x;
-      }
+      float score = x;
+      if (temperature > 0.f) score = x * invT - __logf(-__logf(u01(a.seed, rkey, (unsigned)v)));
       if (score > bv) { bv = score; bi = v; }
     }
   }
@@ -98,10 +107,9 @@ sample_kernel(const bf16_t* __restrict__ logits, int V, int ld, float temperatur
     const float x = bf2f(row[v]);
     mx = fmaxf(mx, x);
     float score = x;
-    if (temperature > 0.f) score = x * invT - __logf(-__logf(u01(seed, step * 131071u + (unsigned)b, (unsigned)v)));
+    if (temperature > 0.f) score = x * invT - __logf(-__logf(u01(a.seed, rkey, (unsigned)v)));
     if (score > bv) { bv = score; bi = v; }
   }
-  // argmax reduction (ties -> smallest index)
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
     const float ov = __shfl_xor(bv, o, 64);
@@ -120,11 +128,20 @@ sample_kernel(const bf16_t* __restrict__ logits, int V, int ld, float temperatur
     for (int i = 1; i < nw; ++i)
       if (bestv[i] > fv || (bestv[i] == fv && besti[i] < fi)) { fv = bestv[i]; fi = besti[i]; }
     const float lp = bf2f(row[fi]) - gmax - __logf(s);
-    const bool on = active ? active[b] != 0 : true;
+    const bool on = a.active ? a.active[b] != 0 : true;
     if (on) {
-      out_tok[b] = fi;
-      if (out_lp) out_lp[b] = lp;
-      if (conf_sum) { conf_sum[2 * b] += __expf(lp); conf_sum[2 * b + 1] += 1.f; }
+      a.out_tok[b] = fi;
+      if (a.out_lp) a.out_lp[b] = lp;
+      if (a.conf) { a.conf[2 * b] += __expf(lp); a.conf[2 * b + 1] += 1.f; }
+      bool stop = (fi == a.eos0 || fi == a.eos1 || fi == a.eos2 || fi == a.eos3);
+      if (a.hist) {
+        const int gi = a.pos[b] - a.start[b];
+        if (gi >= 0 && gi < a.hist_ld) a.hist[(size_t)b * a.hist_ld + gi] = fi;
+        if (gi + 1 >= a.hist_ld) stop = true;
+      }
+      if (a.pos) a.pos[b] += 1;
+      if (a.lens) a.lens[b] += 1;
+      if (stop && a.active) a.active[b] = 0;
     }
   }
 }
@@ -140,11 +157,17 @@ DA_EXPORT int da_rope_cache(void* qkv, const void* pos, const void* slot, const 
 }
 
 DA_EXPORT int da_sample(const void* logits, int B, int V, int ld, float temperature, unsigned seed, unsigned step,
-                        void* out_tok, void* out_lp, void* conf, const void* active, void* stream) {
+                        const void* ctr, void* out_tok, void* out_lp, void* conf, void* active, void* pos, void* lens,
+                        void* hist, const void* start, int hist_ld, int eos0, int eos1, int eos2, int eos3,
+                        void* stream) {
   if (ld % 8) return (int)hipErrorInvalidValue;
+  if (hist && (!pos || !start)) return (int)hipErrorInvalidValue;
   if (B == 0) return 0;
-  sample_kernel<<<B, 1024, 0, (hipStream_t)stream>>>((const bf16_t*)logits, V, ld, temperature, seed, step,
-                                                      (int*)out_tok, (float*)out_lp, (float*)conf,
-                                                      (const int*)active);
+  SampleArgs a;
+  a.logits = (const bf16_t*)logits; a.V = V; a.ld = ld; a.temperature = temperature; a.seed = seed; a.step = step;
+  a.ctr = (const int*)ctr; a.out_tok = (int*)out_tok; a.out_lp = (float*)out_lp; a.conf = (float*)conf;
+  a.active = (int*)active; a.pos = (int*)pos; a.lens = (int*)lens; a.hist = (int*)hist; a.start = (const int*)start;
+  a.hist_ld = hist_ld; a.eos0 = eos0; a.eos1 = eos1; a.eos2 = eos2; a.eos3 = eos3;
+  sample_kernel<<<B, 1024, 0, (hipStream_t)stream>>>(a);
   DA_LAUNCH_CHECK();
 }

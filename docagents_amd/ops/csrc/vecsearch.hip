@@ -101,7 +101,7 @@ topk_dense_kernel(const bf16_t* __restrict__ X, int N, int d, const int* __restr
       bool ok = row < rend && q < nq && s >= thr;
       if (ok && bitmap) {
         const int sl = slots[row];
-        ok = (bitmap[(size_t)(qbase + q) * W + (sl >> 5)] >> (sl & 31)) & 1u;
+        ok = sl >= 0 && (sl >> 5) < W && ((bitmap[(size_t)(qbase + q) * W + (sl >> 5)] >> (sl & 31)) & 1u);
       }
       sc[q * 65 + rl] = ok ? s : -INFINITY;
     }
@@ -184,7 +184,7 @@ topk_ranges_kernel(const bf16_t* __restrict__ X, int d, const int* __restrict__ 
           bool ok = p < hi && dot >= thr;
           if (ok && bitmap) {
             const int sl = slots[row];
-            ok = (bitmap[(size_t)q * W + (sl >> 5)] >> (sl & 31)) & 1u;
+            ok = sl >= 0 && (sl >> 5) < W && ((bitmap[(size_t)q * W + (sl >> 5)] >> (sl & 31)) & 1u);
           }
           sc[rl] = ok ? dot : -INFINITY;
           sr[rl] = ok ? row : -1;

@@ -33,9 +33,9 @@ _SIGS = {
     "da_bert_embed_ln": [c_void_p] * 9 + [c_int, c_int, c_float, c_void_p],
     "da_embed": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p],
     "da_pool_l2norm": [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p],
-    "da_rope_cache": [c_void_p] * 6 + [c_int] * 7 + [c_void_p],
-    "da_sample": [c_void_p, c_int, c_int, c_int, c_float, c_uint, c_uint, c_void_p, c_void_p, c_void_p,
-                  c_void_p, c_void_p],
+    "da_rope_cache": [c_void_p] * 6 + [c_int] * 6 + [c_void_p],
+    "da_sample": [c_void_p, c_int, c_int, c_int, c_float, c_uint, c_uint] + [c_void_p] * 9
+                 + [c_int] * 5 + [c_void_p],
     "da_flash_attn_varlen": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_int,
                              c_int, c_int, c_int, c_int, c_float, c_void_p, c_int, c_void_p],
     "da_decode_attn": [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
@@ -307,7 +307,9 @@ def decode_attn(q, k_cache, v_cache, lens, slot, H, Hkv, D, max_len: int, chunk:
     return out
 
 
-def sample(logits, temperature: float, seed: int, step: int, out_tok=None, out_lp=None, conf=None, active=None):
+def sample(logits, temperature: float, seed: int, step: int = 0, out_tok=None, out_lp=None, conf=None,
+           active=None, ctr=None, pos=None, lens=None, hist=None, start=None, eos=()):
+    """Fused temperature sampler (see rope_sample.hip). Returns (tokens, logprobs)."""
     _bf16_cuda(logits, "logits")
     B, V = logits.shape
     _req(logits.stride(1) == 1 and logits.stride(0) % 8 == 0, "logits layout")
@@ -318,9 +320,19 @@ def sample(logits, temperature: float, seed: int, step: int, out_tok=None, out_l
         out_lp = torch.empty(B, dtype=torch.float32, device=dev)
     if conf is not None:
         _req(conf.dtype == torch.float32 and conf.shape == (B, 2), "conf must be fp32 [B, 2]")
+    for t, n in ((active, "active"), (ctr, "ctr"), (pos, "pos"), (lens, "lens"), (start, "start")):
+        if t is not None:
+            _i32(t, n); _req(t.numel() >= B, f"{n} too short")
+    hist_ld = 0
+    if hist is not None:
+        _i32(hist, "hist"); _req(hist.dim() == 2 and hist.shape[0] >= B, "hist [B, n]")
+        _req(pos is not None and start is not None, "hist needs pos and start")
+        hist_ld = hist.shape[1]
+    e = list(eos)[:4] + [-1] * (4 - min(4, len(eos)))
     _check(lib().da_sample(_ptr(logits), B, V, logits.stride(0), float(temperature), seed & 0xffffffff,
-                           step & 0xffffffff, _ptr(out_tok), _ptr(out_lp), _ptr(conf), _ptr(active), _stream()),
-           "sample")
+                           step & 0xffffffff, _ptr(ctr), _ptr(out_tok), _ptr(out_lp), _ptr(conf), _ptr(active),
+                           _ptr(pos), _ptr(lens), _ptr(hist), _ptr(start), hist_ld, e[0], e[1], e[2], e[3],
+                           _stream()), "sample")
     return out_tok, out_lp
 
 
@@ -393,3 +405,10 @@ def kmeans_accum(X, assign, sums, counts):
     N, d = X.shape
     _req(sums.dtype == torch.float32 and sums.shape[1] == d and counts.dtype == torch.float32, "sums/counts fp32")
     _check(lib().da_kmeans_accum(_ptr(X), N, d, _ptr(assign), _ptr(sums), _ptr(counts), _stream()), "kmeans_accum")
+
+
+def reserve_workspace(nbytes: int, device=None) -> None:
+    """Pre-size the shared split-K / decode workspace. Must be called before capturing HIP graphs
+    so the captured kernels keep pointing at a live buffer."""
+    dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+    _workspace(nbytes, dev)

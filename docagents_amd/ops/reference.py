@@ -177,9 +177,12 @@ def log_softmax_rows(logits):
     return torch.log_softmax(logits.float(), dim=-1)
 
 
-def sample(logits, temperature, seed, step, out_tok=None, out_lp=None, conf=None, active=None):
-    """Reference sampler: greedy when temperature <= 0, else torch multinomial (a different RNG
-    stream than the kernel's hash RNG, so only greedy is bit-comparable)."""
+def sample(logits, temperature, seed, step=0, out_tok=None, out_lp=None, conf=None, active=None, ctr=None,
+           pos=None, lens=None, hist=None, start=None, eos=()):
+    """Reference sampler with the kernel's bookkeeping semantics. Greedy when temperature <= 0;
+    otherwise torch multinomial (a different RNG stream than the kernel's hash RNG, so only greedy
+    is bit-comparable)."""
+    B = logits.shape[0]
     lp = log_softmax_rows(logits)
     if temperature > 0:
         g = torch.Generator(device="cpu").manual_seed((seed * 1000003 + step) & 0x7FFFFFFF)
@@ -189,19 +192,31 @@ def sample(logits, temperature, seed, step, out_tok=None, out_lp=None, conf=None
         tok = logits.float().argmax(-1)
     chosen = lp.gather(1, tok.view(-1, 1)).squeeze(1)
     tok = tok.int()
-    if active is not None:
-        keep = active.bool()
-        if out_tok is not None:
-            tok = torch.where(keep, tok, out_tok)
-    if conf is not None:
-        m = active.bool() if active is not None else torch.ones_like(chosen, dtype=torch.bool)
-        conf[:, 0] += torch.where(m, chosen.exp(), torch.zeros_like(chosen))
-        conf[:, 1] += m.float()
-    if out_tok is not None:
-        out_tok.copy_(tok)
+    on = active.bool().clone() if active is not None else torch.ones(B, dtype=torch.bool, device=logits.device)
+    if out_tok is None:
+        out_tok = torch.zeros(B, dtype=torch.int32, device=logits.device)
+    out_tok.copy_(torch.where(on, tok, out_tok))
     if out_lp is not None:
-        out_lp.copy_(chosen)
-    return tok, chosen
+        out_lp.copy_(torch.where(on, chosen, out_lp))
+    if conf is not None:
+        conf[:, 0] += torch.where(on, chosen.exp(), torch.zeros_like(chosen))
+        conf[:, 1] += on.float()
+    stop = torch.zeros(B, dtype=torch.bool, device=logits.device)
+    for e in list(eos)[:4]:
+        stop |= tok == e
+    if hist is not None:
+        gi = (pos - start).long()
+        for b in range(B):
+            if on[b] and 0 <= gi[b] < hist.shape[1]:
+                hist[b, gi[b]] = tok[b]
+        stop |= (gi + 1) >= hist.shape[1]
+    if pos is not None:
+        pos += on.int()
+    if lens is not None:
+        lens += on.int()
+    if active is not None:
+        active.copy_(torch.where(on & stop, torch.zeros_like(active), active))
+    return out_tok, chosen
 
 
 def topk_dense(X, Qv, K, thr, slots=None, bitmap=None, **_):

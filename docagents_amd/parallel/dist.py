@@ -1,0 +1,104 @@
+"""Process-group plumbing: one process per GPU, ``torch.distributed`` over RCCL ("nccl" backend on
+ROCm) on the GPUs, gloo on CPU (tests). Reads RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* from the
+environment (torchrun). Collectives used by the framework:
+
+  C1 all-gather of per-shard top-k          -> ``ShardedIndex.search``
+  C2 all-gather of query embeddings         -> ``ShardedIndex.search``
+  C3 all-reduce of row-parallel outputs     -> ``LlamaDecoder`` (TP)
+  C4 all-gather of vocab-parallel logits    -> ``LlamaDecoder`` (TP)
+  C6 all-reduce of k-means statistics       -> ``IVFFlatIndex.train``
+  C7 barrier / liveness all-reduce          -> ``liveness_check``
+"""
+from __future__ import annotations
+
+import datetime
+import os
+from dataclasses import dataclass
+
+import torch
+import torch.distributed as dist
+
+
+@dataclass
+class DistInfo:
+    rank: int = 0
+    world: int = 1
+    local_rank: int = 0
+    backend: str = "none"
+    device: torch.device = torch.device("cpu")
+
+    @property
+    def is_main(self) -> bool:
+        return self.rank == 0
+
+
+def init_from_env(prefer_gpu: bool = True, timeout_s: int = 600) -> DistInfo:
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", str(rank)))
+    use_gpu = prefer_gpu and torch.cuda.is_available()
+    if use_gpu:
+        torch.cuda.set_device(local)
+        device = torch.device("cuda", local)
+    else:
+        device = torch.device("cpu")
+    backend = "none"
+    if world > 1 and not dist.is_initialized():
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29511")
+        backend = "nccl" if use_gpu else "gloo"
+        kw = dict(backend=backend, rank=rank, world_size=world, timeout=datetime.timedelta(seconds=timeout_s))
+        if use_gpu:
+            kw["device_id"] = device
+        dist.init_process_group(**kw)
+    elif dist.is_initialized():
+        backend = dist.get_backend()
+    return DistInfo(rank, world, local, backend, device)
+
+
+def barrier():
+    if dist.is_initialized():
+        dist.barrier()
+
+
+def all_reduce_max(x: float, device) -> float:
+    if not dist.is_initialized():
+        return x
+    t = torch.tensor([x], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def all_reduce_sum(x: float, device) -> float:
+    if not dist.is_initialized():
+        return x
+    t = torch.tensor([x], dtype=torch.float64, device=device)
+    dist.all_reduce(t)
+    return float(t.item())
+
+
+def all_gather_rows(t: torch.Tensor, group=None) -> torch.Tensor:
+    """[n, ...] per rank (same n on every rank) -> [world * n, ...] in rank order."""
+    if not dist.is_initialized() or dist.get_world_size(group) == 1:
+        return t
+    w = dist.get_world_size(group)
+    out = torch.empty((w * t.shape[0],) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
+    dist.all_gather_into_tensor(out, t.contiguous(), group=group)
+    return out
+
+
+def liveness_check(device, timeout_ok: bool = True) -> int:
+    """C7: every rank contributes 1; returns the number of live ranks (== world when healthy)."""
+    if not dist.is_initialized():
+        return 1
+    t = torch.ones(1, dtype=torch.int32, device=device)
+    dist.all_reduce(t)
+    return int(t.item())
+
+
+def shutdown():
+    if dist.is_initialized():
+        try:
+            dist.barrier()
+        finally:
+            dist.destroy_process_group()
