@@ -1,0 +1,236 @@
+"""Metadata in SQLite (WAL) + vectors in the HBM index: the Postgres/pgvector replacement.
+
+Schema mirrors internal/store/postgres.go:63-87 (documents / chunks / summaries / embedding model),
+plus an integer ``key`` per chunk (the vector id in the HBM index), a dense integer ``seq`` per
+document, and the chunk's decoder token ids (tokenized once at analysis, reused for every Answer
+prompt). Fixes carried over from SURVEY.md Appendix B: ``list_chunks`` orders by ``ord`` (#7),
+``save_chunks`` replaces a document's chunks in one transaction so a parse retry is idempotent
+(#17), migrations take an exclusive lock and non-holders WAIT instead of skipping (§5.2).
+
+Vectors go to a ``VectorBackend`` (in-process HBM index, or the engine server over RPC).
+"""
+from __future__ import annotations
+
+import asyncio
+import datetime as dt
+import json
+import os
+import sqlite3
+import threading
+import uuid
+
+import numpy as np
+
+from ..utils import faults
+from .base import (STATUS_PROCESSING, Chunk, Document, DocumentNotFound, Embedding, SearchResult, Summary,
+                   SummaryNotFound)
+
+SCHEMA = [
+    """CREATE TABLE IF NOT EXISTS documents (
+        id TEXT PRIMARY KEY, seq INTEGER UNIQUE, filename TEXT, status TEXT,
+        created_at TEXT DEFAULT (strftime('%Y-%m-%dT%H:%M:%fZ','now')))""",
+    """CREATE TABLE IF NOT EXISTS chunks (
+        key INTEGER PRIMARY KEY AUTOINCREMENT, id TEXT UNIQUE, document_id TEXT REFERENCES documents(id)
+        ON DELETE CASCADE, ord INTEGER, text TEXT, token_count INTEGER, dec_tokens BLOB)""",
+    "CREATE INDEX IF NOT EXISTS chunks_doc ON chunks(document_id, ord)",
+    """CREATE TABLE IF NOT EXISTS summaries (
+        document_id TEXT PRIMARY KEY REFERENCES documents(id) ON DELETE CASCADE, summary TEXT, key_points TEXT)""",
+    """CREATE TABLE IF NOT EXISTS embeddings (
+        chunk_id TEXT PRIMARY KEY REFERENCES chunks(id) ON DELETE CASCADE, model TEXT, dim INTEGER)""",
+]
+
+
+class SqliteMeta:
+    def __init__(self, path: str):
+        self.path = path
+        if path != ":memory:":
+            os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
+        self.conn = sqlite3.connect(path, check_same_thread=False, timeout=30.0, isolation_level=None)
+        self.conn.execute("PRAGMA journal_mode=WAL")
+        self.conn.execute("PRAGMA synchronous=NORMAL")
+        self.conn.execute("PRAGMA foreign_keys=ON")
+        self.lock = threading.RLock()
+        self._migrate()
+
+    def _migrate(self):
+        with self.lock:
+            # BEGIN EXCLUSIVE blocks concurrent migrators until the holder commits (no skip-and-race)
+            self.conn.execute("BEGIN EXCLUSIVE")
+            try:
+                for s in SCHEMA:
+                    self.conn.execute(s)
+                self.conn.execute("COMMIT")
+            except Exception:
+                self.conn.execute("ROLLBACK")
+                raise
+
+    def q(self, sql, args=()):
+        with self.lock:
+            return self.conn.execute(sql, args).fetchall()
+
+    def x(self, sql, args=()):
+        with self.lock:
+            return self.conn.execute(sql, args)
+
+    def close(self):
+        with self.lock:
+            self.conn.close()
+
+
+def _parse_ts(s):
+    if not s:
+        return None
+    try:
+        return dt.datetime.fromisoformat(s.replace("Z", "+00:00"))
+    except ValueError:
+        return None
+
+
+class CompositeStore:
+    """Store implementation: SQLite metadata + a vector backend (see vectors.py)."""
+
+    def __init__(self, meta: SqliteMeta, vectors, min_similarity: float = 0.7, dec_tokenizer=None):
+        self.meta, self.vectors = meta, vectors
+        self.min_similarity = min_similarity
+        self.dec_tokenizer = dec_tokenizer
+
+    async def _run(self, fn, *a):
+        return await asyncio.to_thread(fn, *a)
+
+    # -------------------------------------------------------------------- documents
+    async def create_document(self, filename: str) -> Document:
+        def f():
+            did = str(uuid.uuid4())
+            with self.meta.lock:
+                row = self.meta.conn.execute("SELECT COALESCE(MAX(seq), -1) + 1 FROM documents").fetchone()
+                self.meta.conn.execute("INSERT INTO documents(id, seq, filename, status) VALUES(?,?,?,?)",
+                                       (did, row[0], filename, STATUS_PROCESSING))
+            return Document(did, filename, STATUS_PROCESSING, dt.datetime.now(dt.timezone.utc), row[0])
+        return await self._run(f)
+
+    async def get_document(self, doc_id: str) -> Document:
+        rows = await self._run(self.meta.q, "SELECT id, filename, status, created_at, seq FROM documents WHERE id=?",
+                               (doc_id,))
+        if not rows:
+            raise DocumentNotFound()
+        r = rows[0]
+        return Document(r[0], r[1], r[2], _parse_ts(r[3]), r[4])
+
+    async def update_document_status(self, doc_id: str, status: str) -> None:
+        cur = await self._run(self.meta.x, "UPDATE documents SET status=? WHERE id=?", (status, doc_id))
+        if cur.rowcount == 0:
+            raise DocumentNotFound()
+
+    async def list_documents(self, status: str | None = None) -> list[Document]:
+        sql = "SELECT id, filename, status, created_at, seq FROM documents"
+        args = ()
+        if status:
+            sql += " WHERE status=?"
+            args = (status,)
+        rows = await self._run(self.meta.q, sql, args)
+        return [Document(r[0], r[1], r[2], _parse_ts(r[3]), r[4]) for r in rows]
+
+    # -------------------------------------------------------------------- chunks
+    async def save_chunks(self, doc_id: str, chunks: list[Chunk]) -> list[Chunk]:
+        faults.maybe_fail("store.save_chunks")
+
+        def f():
+            out = []
+            with self.meta.lock:
+                c = self.meta.conn
+                c.execute("BEGIN IMMEDIATE")
+                try:
+                    c.execute("DELETE FROM chunks WHERE document_id=?", (doc_id,))
+                    for ch in chunks:
+                        cid = str(uuid.uuid4())
+                        cur = c.execute("INSERT INTO chunks(id, document_id, ord, text, token_count) VALUES(?,?,?,?,?)",
+                                        (cid, doc_id, ch.index, ch.text, ch.token_count))
+                        out.append(Chunk(cid, doc_id, ch.index, ch.text, ch.token_count, cur.lastrowid))
+                    c.execute("COMMIT")
+                except Exception:
+                    c.execute("ROLLBACK")
+                    raise
+            return out
+        return await self._run(f)
+
+    async def list_chunks(self, doc_id: str) -> list[Chunk]:
+        rows = await self._run(self.meta.q, "SELECT id, ord, text, token_count, key FROM chunks WHERE document_id=? "
+                                            "ORDER BY ord", (doc_id,))
+        return [Chunk(r[0], doc_id, r[1], r[2], r[3], r[4]) for r in rows]
+
+    async def chunks_by_keys(self, keys: list[int]) -> dict[int, tuple[Chunk, bytes | None]]:
+        if not keys:
+            return {}
+        qs = ",".join("?" * len(keys))
+        rows = await self._run(self.meta.q, f"SELECT key, id, document_id, ord, text, token_count, dec_tokens FROM chunks "
+                                            f"WHERE key IN ({qs})", tuple(int(k) for k in keys))
+        return {r[0]: (Chunk(r[1], r[2], r[3], r[4], r[5], r[0]), r[6]) for r in rows}
+
+    async def save_chunk_tokens(self, pairs: list[tuple[str, list[int]]]):
+        def f():
+            with self.meta.lock:
+                self.meta.conn.executemany("UPDATE chunks SET dec_tokens=? WHERE id=?",
+                                           [(np.asarray(t, dtype=np.int32).tobytes(), cid) for cid, t in pairs])
+        await self._run(f)
+
+    # -------------------------------------------------------------------- summaries
+    async def save_summary(self, doc_id: str, summary: Summary) -> None:
+        await self._run(self.meta.x, "INSERT INTO summaries(document_id, summary, key_points) VALUES(?,?,?) "
+                                     "ON CONFLICT(document_id) DO UPDATE SET summary=excluded.summary, "
+                                     "key_points=excluded.key_points",
+                        (doc_id, summary.summary, json.dumps(list(summary.key_points or []))))
+
+    async def get_summary(self, doc_id: str) -> Summary:
+        rows = await self._run(self.meta.q, "SELECT summary, key_points FROM summaries WHERE document_id=?", (doc_id,))
+        if not rows:
+            raise SummaryNotFound()
+        return Summary(doc_id, rows[0][0], json.loads(rows[0][1] or "[]"))
+
+    # -------------------------------------------------------------------- vectors
+    async def save_embeddings(self, embs: list[Embedding]) -> None:
+        if not embs:
+            return
+        ids = [e.chunk_id for e in embs]
+        qs = ",".join("?" * len(ids))
+        rows = await self._run(self.meta.q, f"SELECT id, key, document_id FROM chunks WHERE id IN ({qs})", tuple(ids))
+        info = {r[0]: (r[1], r[2]) for r in rows}
+        by_doc: dict[str, list] = {}
+        for e in embs:
+            if e.chunk_id not in info:
+                raise LookupError(f"unknown chunk {e.chunk_id}")
+            key, doc = info[e.chunk_id]
+            by_doc.setdefault(doc, []).append((key, e.vector))
+        for doc, items in by_doc.items():
+            keys = np.asarray([k for k, _ in items], dtype=np.int64)
+            vecs = np.stack([np.asarray(v, dtype=np.float32) for _, v in items])
+            await self.vectors.add(doc, keys, vecs)
+
+        def f():
+            with self.meta.lock:
+                self.meta.conn.executemany(
+                    "INSERT INTO embeddings(chunk_id, model, dim) VALUES(?,?,?) ON CONFLICT(chunk_id) DO UPDATE SET "
+                    "model=excluded.model, dim=excluded.dim",
+                    [(e.chunk_id, e.model, int(np.asarray(e.vector).shape[-1])) for e in embs])
+        await self._run(f)
+
+    async def top_k(self, doc_ids: list[str], vector, k: int, min_similarity: float | None = None) -> list[SearchResult]:
+        thr = self.min_similarity if min_similarity is None else min_similarity
+        hits = await self.vectors.search(np.asarray(vector, dtype=np.float32), list(doc_ids), k, thr)
+        keys = [kk for kk, _ in hits]
+        found = await self.chunks_by_keys(keys)
+        sums: dict[str, Summary] = {}
+        out = []
+        for key, score in hits:
+            if key not in found:
+                continue
+            ch, _ = found[key]
+            if ch.document_id not in sums:
+                try:
+                    sums[ch.document_id] = await self.get_summary(ch.document_id)
+                except SummaryNotFound:
+                    sums[ch.document_id] = Summary(ch.document_id, "", [])
+            out.append(SearchResult(ch, float(score), sums[ch.document_id]))
+        return out
+
+    async def close(self):
+        self.meta.close()
