@@ -1,0 +1,299 @@
+"""Engine server: owns the GPU(s); serves embed / summarize / answer / index RPCs to the agents.
+
+Micro-batching: every method has a queue; while the GPU executes one batch, newly arriving
+requests accumulate and are run together as the next batch (one encoder launch for all queued
+embeddings, one ``Generator.generate`` for all queued answers/summaries). This is the cross-request
+batching the reference cannot do (it issues one OpenAI call per request).
+
+Multi-GPU (``torchrun --nproc-per-node N``): rank 0 serves RPCs and drives the group; ranks 1..N-1
+run ``follower_loop``. A command is broadcast as a small object over a gloo group; bulk work is
+split data-parallel (each rank embeds / generates a slice, results gathered to rank 0); the vector
+index is sharded (documents routed to rank = hash(doc_id) % N, inserts stay local to the owner's
+HBM, searches fan out with the query matrix broadcast over RCCL and top-k merged on rank 0).
+"""
+from __future__ import annotations
+
+import asyncio
+import concurrent.futures as cf
+import hashlib
+import time
+import traceback
+
+import numpy as np
+import torch
+
+from ..utils import faults
+from .rpc import pack, parse_url, read_frame
+
+
+def owner_of(doc_id: str, world: int) -> int:
+    return int.from_bytes(hashlib.blake2b(doc_id.encode(), digest_size=8).digest(), "little") % max(1, world)
+
+
+class EngineGroup:
+    """Executes engine commands on one rank or on all ranks of a torch.distributed group."""
+
+    def __init__(self, engine, rank: int = 0, world: int = 1, ctrl_group=None, data_group=None):
+        self.engine, self.rank, self.world = engine, rank, world
+        self.ctrl_group, self.data_group = ctrl_group, data_group
+
+    # ---------------------------------------------------------------- collectives (control plane)
+    def _bcast(self, obj):
+        if self.world == 1:
+            return obj
+        import torch.distributed as dist
+        lst = [obj]
+        dist.broadcast_object_list(lst, src=0, group=self.ctrl_group)
+        return lst[0]
+
+    def _gather(self, obj):
+        if self.world == 1:
+            return [obj]
+        import torch.distributed as dist
+        out = [None] * self.world
+        dist.all_gather_object(out, obj, group=self.ctrl_group)
+        return out
+
+    def run(self, cmd: str, args: dict):
+        """Rank 0: broadcast the command, execute collectively, return rank 0's result."""
+        if self.world > 1:
+            self._bcast((cmd, args))
+        return self.execute(cmd, args)
+
+    def follower_loop(self):
+        while True:
+            cmd, args = self._bcast(None)
+            if cmd == "shutdown":
+                return
+            try:
+                self.execute(cmd, args)
+            except Exception:  # noqa: BLE001 - keep the group alive; rank 0 reports errors
+                traceback.print_exc()
+
+    # ---------------------------------------------------------------- commands
+    def _slice(self, n: int):
+        per = (n + self.world - 1) // self.world
+        a = min(n, self.rank * per)
+        return a, min(n, a + per)
+
+    def execute(self, cmd: str, a: dict):
+        e = self.engine
+        if cmd == "embed":
+            texts = a["texts"]
+            lo, hi = self._slice(len(texts))
+            faults.maybe_fail("engine.embed")
+            v = e.embed(texts[lo:hi], a.get("preprocess", True), out_dtype=torch.float32).cpu().numpy()
+            parts = self._gather(v)
+            return np.concatenate(parts, axis=0) if parts else v
+        if cmd in ("answer", "summarize"):
+            items = a["items"]
+            lo, hi = self._slice(len(items))
+            faults.maybe_fail("engine.generate")
+            mine = items[lo:hi]
+            if cmd == "summarize":
+                res = e.summarize_many(mine) if mine else []
+            else:
+                batch = []
+                for it in mine:
+                    if it.get("chunks") is not None:
+                        ids = [(c["tokens"].tolist() if c.get("tokens") is not None else e._ids(c["text"]))
+                               for c in it["chunks"]]
+                    else:
+                        ids = [e._ids(it.get("context", ""))] if it.get("context") else []
+                    batch.append((it["question"], ids, it.get("quality", 0.0)))
+                res = e.answer_many(batch) if batch else []
+            out = []
+            for r in self._gather(res):
+                out.extend(r)
+            return out
+        if cmd == "index_add":
+            if owner_of(a["doc_id"], self.world) == self.rank:
+                e.index.add(a["doc_id"], a["keys"], torch.from_numpy(np.ascontiguousarray(a["vecs"], dtype=np.float32)))
+            return True
+        if cmd == "index_remove":
+            n = e.index.remove_doc(a["doc_id"])
+            return sum(self._gather(n))
+        if cmd == "search":
+            return self._search(a)
+        if cmd == "stats":
+            return self._gather(e.describe())
+        if cmd == "snapshot":
+            from ..index.snapshot import save_index
+            save_index(e.index, f"{a['path']}.shard{self.rank}")
+            return True
+        if cmd == "restore":
+            from ..index.snapshot import load_index
+            load_index(e.index, f"{a['path']}.shard{self.rank}")
+            return len(e.index)
+        if cmd == "ping":
+            return self._gather(self.rank)
+        raise ValueError(f"unknown engine command {cmd!r}")
+
+    def _search(self, a):
+        e = self.engine
+        k, thr, filters = int(a["k"]), float(a["min_sim"]), a.get("filters")
+        if self.world == 1:
+            q = torch.from_numpy(np.ascontiguousarray(a["vecs"], dtype=np.float32))
+            s, rows = e.index.search(q, k, thr, filters)
+            ids = e.index.gather_ids(rows)
+            return s.cpu().numpy(), ids.cpu().numpy()
+        import torch.distributed as dist
+        dev = e.device
+        Q = self._bcast(a["vecs"].shape[0] if self.rank == 0 else None)
+        d = e.dim
+        q = (torch.from_numpy(np.ascontiguousarray(a["vecs"], dtype=np.float32)).to(dev) if self.rank == 0
+             else torch.empty((Q, d), dtype=torch.float32, device=dev))
+        dist.broadcast(q, src=0, group=self.data_group)                     # C2 (broadcast form)
+        s, rows = e.index.search(q, k, thr, filters)
+        gid = e.index.gather_ids(rows)
+        S = torch.empty((self.world,) + tuple(s.shape), dtype=s.dtype, device=dev)
+        G = torch.empty((self.world,) + tuple(gid.shape), dtype=gid.dtype, device=dev)
+        dist.all_gather_into_tensor(S, s.contiguous(), group=self.data_group)    # C1
+        dist.all_gather_into_tensor(G, gid.contiguous(), group=self.data_group)
+        flatS = S.permute(1, 0, 2).reshape(Q, -1)
+        flatG = G.permute(1, 0, 2).reshape(Q, -1)
+        flatS = torch.where(flatG >= 0, flatS, torch.full_like(flatS, float("-inf")))
+        ms, mi = torch.sort(flatS, dim=1, descending=True, stable=True)
+        ms, mi = ms[:, :k], mi[:, :k]
+        mid = torch.where(torch.isfinite(ms), flatG.gather(1, mi), torch.full_like(mi, -1))
+        return ms.cpu().numpy(), mid.cpu().numpy()
+
+
+class EngineServer:
+    """asyncio RPC front end with per-method micro-batch queues."""
+
+    BATCHED = ("embed", "answer", "summarize")
+
+    def __init__(self, group: EngineGroup, log, max_batch_items: int = 256):
+        self.group, self.log = group, log
+        self.gpu = cf.ThreadPoolExecutor(max_workers=1, thread_name_prefix="gpu")
+        self.queues: dict[str, asyncio.Queue] = {}
+        self.max_batch_items = max_batch_items
+        self.stats = {m: {"batches": 0, "items": 0, "busy_s": 0.0} for m in self.BATCHED}
+        self.server = None
+
+    async def _gpu(self, cmd, args):
+        loop = asyncio.get_running_loop()
+        return await loop.run_in_executor(self.gpu, self.group.run, cmd, args)
+
+    async def _batcher(self, method: str):
+        q = self.queues[method]
+        while True:
+            first = await q.get()
+            reqs = [first]
+            n = len(first[0])
+            while not q.empty() and n < self.max_batch_items:
+                r = q.get_nowait()
+                reqs.append(r)
+                n += len(r[0])
+            items = [x for r in reqs for x in r[0]]
+            t0 = time.perf_counter()
+            try:
+                if method == "embed":
+                    pre = reqs[0][2]
+                    res = await self._gpu("embed", {"texts": items, "preprocess": pre})
+                else:
+                    res = await self._gpu(method, {"items": items})
+                st = self.stats[method]
+                st["batches"] += 1
+                st["items"] += len(items)
+                st["busy_s"] += time.perf_counter() - t0
+                o = 0
+                for its, fut, _ in reqs:
+                    if not fut.done():
+                        fut.set_result(res[o:o + len(its)])
+                    o += len(its)
+            except Exception as e:  # noqa: BLE001
+                for _, fut, _ in reqs:
+                    if not fut.done():
+                        fut.set_exception(e)
+
+    async def _enqueue(self, method, items, extra=None):
+        fut = asyncio.get_running_loop().create_future()
+        await self.queues[method].put((items, fut, extra))
+        return await fut
+
+    async def dispatch(self, method: str, args: dict):
+        if method == "embed":
+            # batches of the same preprocess flag only
+            key = "embed" if args.get("preprocess", True) else "embed_raw"
+            vecs = await self._enqueue(key, list(args["texts"]), args.get("preprocess", True))
+            return {"vecs": np.asarray(vecs, dtype=np.float32)}
+        if method == "summarize":
+            res = await self._enqueue("summarize", list(args["texts"]))
+            return {"results": [[s, list(kp)] for s, kp in res]}
+        if method == "answer":
+            res = await self._enqueue("answer", list(args["items"]))
+            return {"results": [[a, float(c)] for a, c in res]}
+        if method == "search":
+            s, ids = await self._gpu("search", args)
+            return {"scores": s, "keys": ids}
+        if method in ("index_add", "index_remove", "snapshot", "restore", "ping"):
+            return await self._gpu(method, args)
+        if method == "stats":
+            st = await self._gpu("stats", {})
+            return {"ranks": st, "batching": self.stats}
+        if method == "health":
+            return {"ok": True}
+        raise ValueError(f"unknown method {method!r}")
+
+    async def _client(self, reader, writer):
+        lock = asyncio.Lock()
+
+        async def handle(msg):
+            rid = msg.get("id")
+            try:
+                res = await self.dispatch(msg.get("method"), msg.get("args") or {})
+                out = {"id": rid, "result": res}
+            except Exception as e:  # noqa: BLE001
+                self.log.error("engine rpc failed", "method", msg.get("method"), "err", repr(e),
+                               "trace_id", msg.get("trace", ""))
+                out = {"id": rid, "error": f"{type(e).__name__}: {e}"}
+            async with lock:
+                writer.write(pack(out))
+                await writer.drain()
+
+        try:
+            while True:
+                msg = await read_frame(reader)
+                asyncio.ensure_future(handle(msg))
+        except (asyncio.IncompleteReadError, ConnectionError):
+            pass
+        finally:
+            writer.close()
+
+    async def start(self, url: str):
+        for m in ("embed", "embed_raw", "answer", "summarize"):
+            self.queues[m] = asyncio.Queue()
+        for m in ("embed", "answer", "summarize"):
+            asyncio.ensure_future(self._batcher(m))
+        self.queues_raw_task = asyncio.ensure_future(self._batcher_raw())
+        kind, addr = parse_url(url)
+        if kind == "unix":
+            self.server = await asyncio.start_unix_server(self._client, path=addr)
+        else:
+            self.server = await asyncio.start_server(self._client, addr[0], addr[1])
+        return self.server
+
+    async def _batcher_raw(self):
+        # raw (already preprocessed) embeddings share the embed batcher logic
+        self.stats.setdefault("embed_raw", {"batches": 0, "items": 0, "busy_s": 0.0})
+        self.BATCHED = self.BATCHED + ("embed_raw",)
+        q = self.queues["embed_raw"]
+        while True:
+            first = await q.get()
+            reqs = [first]
+            while not q.empty():
+                reqs.append(q.get_nowait())
+            items = [x for r in reqs for x in r[0]]
+            try:
+                res = await self._gpu("embed", {"texts": items, "preprocess": False})
+                o = 0
+                for its, fut, _ in reqs:
+                    if not fut.done():
+                        fut.set_result(res[o:o + len(its)])
+                    o += len(its)
+            except Exception as e:  # noqa: BLE001
+                for _, fut, _ in reqs:
+                    if not fut.done():
+                        fut.set_exception(e)

@@ -155,7 +155,16 @@ flash_attn_varlen_kernel(const bf16_t* __restrict__ q, const bf16_t* __restrict_
 // ------------------------------------------------------------------------------------------
 // Decode attention: q [B, ldq] (head h at h*D), caches [slots, Hkv, max_seq, D],
 // lens[b] = tokens in cache for b (current token included), slot[b] = cache slot of b.
-// Partials: po [B, H, nsplit, D] fp32, pm/pl [B, H, nsplit].
+// Partials: po [B, H, nsplit, D] fp32 (unnormalised, relative to pm), pm/pl [B, H, nsplit].
+//
+// Memory-bound streaming design: for a fixed (slot, kv head) the keys of a 64-key tile are one
+// contiguous [64 x D] bf16 block, so each wave loads it as a flat byte array with fully coalesced
+// 16-B-per-lane loads (1 KiB per wave-instruction) — chunk c = 64*i + lane holds key c / (D/8),
+// dims 8*(c % (D/8)) .. +7. Partial dot products are reduced per key with lane shuffles when a key's
+// chunks sit in one wave-instruction (D = 64, 128) or through a small per-wave LDS buffer (D = 96).
+// The P*V accumulation uses the same flat chunks: lane's dim-slot for chunk i is static given
+// i mod NSET, so accumulators stay in registers. Each of the 4 waves streams its own tiles with its
+// own online softmax (no block barriers in the loop); the waves are merged once at the end.
 template <int D, int G>
 __global__ void __launch_bounds__(256)
 decode_attn_kernel(const bf16_t* __restrict__ q, int ldq, const bf16_t* __restrict__ kc,
@@ -163,115 +172,165 @@ decode_attn_kernel(const bf16_t* __restrict__ q, int ldq, const bf16_t* __restri
                    int H, int Hkv, int max_seq, int chunk, int nsplit, float scale_log2e,
                    float* __restrict__ po, float* __restrict__ pm, float* __restrict__ pl) {
   constexpr int KT = 64;
-  constexpr int PART = D / 4;            // dims per thread in the score phase
-  constexpr int NP = D / 2;              // d-pairs
-  constexpr int KG = 256 / NP;           // key groups in the PV phase
+  constexpr int CPR = D / 8;                       // 16-B chunks per key row
+  constexpr int GCD = (CPR % 16 == 0) ? 16 : ((CPR % 8 == 0) ? 8 : ((CPR % 4 == 0) ? 4 : 2));
+  constexpr int NSET = CPR / GCD;                  // distinct dim-slots per lane
+  constexpr bool SHFL = (64 % CPR) == 0;           // a key's chunks live in one wave-instruction
   __shared__ float sq[G][D];
-  __shared__ float sp[G][KT];
-  __shared__ float salpha[G], sm[G], sl[G];
-  __shared__ float sred[KG > 0 ? KG : 1][G][D];
+  __shared__ float sp[4][G][KT];
+  __shared__ float spart[SHFL ? 1 : 4][SHFL ? 1 : G * KT * CPR];
+  __shared__ float so[4][G][D];
+  __shared__ float swm[4][G], swl[4][G];
 
   const int split = blockIdx.x, hk = blockIdx.y, b = blockIdx.z;
   const int L = lens[b];
   const int kstart = split * chunk;
   const int kend = min(L, kstart + chunk);
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const size_t cbase = ((size_t)slot[b] * Hkv + hk) * (size_t)max_seq * D;
 
   for (int i = tid; i < G * D; i += 256) {
     const int g = i / D, d = i % D;
     sq[g][d] = bf2f(q[(size_t)b * ldq + (hk * G + g) * D + d]) * scale_log2e;
   }
-  if (tid < G) { sm[tid] = -INFINITY; sl[tid] = 0.f; }
-  const int dp = tid % NP, kg = tid / NP;
-  float oacc[G][2];
-#pragma unroll
-  for (int g = 0; g < G; ++g) { oacc[g][0] = 0.f; oacc[g][1] = 0.f; }
+  for (int i = tid; i < 4 * G * D; i += 256) (&so[0][0][0])[i] = 0.f;
   __syncthreads();
 
-  for (int kb = kstart; kb < kend; kb += KT) {
-    // ---- scores: 4 lanes per key, each PART dims ----
-    {
-      const int key = kb + (tid >> 2), part = tid & 3;
-      float dots[G];
+  float m[G], l[G], acc[G][NSET][8];
 #pragma unroll
-      for (int g = 0; g < G; ++g) dots[g] = 0.f;
-      if (key < kend) {
-        const bf16_t* kr = kc + cbase + (size_t)key * D + part * PART;
+  for (int g = 0; g < G; ++g) {
+    m[g] = -INFINITY; l[g] = 0.f;
 #pragma unroll
-        for (int c = 0; c < PART / 8; ++c) {
-          u32x4_t u = *(const u32x4_t*)(kr + c * 8);
+    for (int s = 0; s < NSET; ++s)
 #pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            const float kv = bf2f((bf16_t)((e & 1) ? (u[e >> 1] >> 16) : (u[e >> 1] & 0xffff)));
+      for (int e = 0; e < 8; ++e) acc[g][s][e] = 0.f;
+  }
+
+  for (int t0 = kstart + w * KT; t0 < kend; t0 += 4 * KT) {
+    const int nk = min(KT, kend - t0);
+    const bf16_t* kb = kc + cbase + (size_t)t0 * D;
+    const bf16_t* vb = vc + cbase + (size_t)t0 * D;
+    // K first (V is loaded after the scores: keeps ~100 VGPRs live instead of ~200, so 4-5
+    // waves per SIMD hide the HBM latency instead of 2)
+    u32x4_t kv[CPR];
 #pragma unroll
-            for (int g = 0; g < G; ++g) dots[g] += kv * sq[g][part * PART + c * 8 + e];
-          }
-        }
+    for (int i = 0; i < CPR; ++i) {
+      const int c = i * 64 + lane;
+      kv[i] = (c < nk * CPR) ? *(const u32x4_t*)(kb + c * 8) : u32x4_t{0, 0, 0, 0};
+    }
+    // ---- scores ----
+#pragma unroll
+    for (int i = 0; i < CPR; ++i) {
+      const int c = i * 64 + lane;
+      const int dp = c % CPR;
+      float kf[8];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        kf[2 * e] = bf2f((bf16_t)(kv[i][e] & 0xffff));
+        kf[2 * e + 1] = bf2f((bf16_t)(kv[i][e] >> 16));
       }
 #pragma unroll
       for (int g = 0; g < G; ++g) {
-        float d2 = dots[g] + __shfl_xor(dots[g], 1, 64);
-        d2 += __shfl_xor(d2, 2, 64);
-        if (part == 0) sp[g][tid >> 2] = (key < kend) ? d2 : -INFINITY;
-      }
-    }
-    __syncthreads();
-    // ---- online softmax per head (one wave per head) ----
-    for (int g = wid; g < G; g += 4) {
-      const float s = sp[g][lane];
-      const float tmax = wave_max(s);
-      const float m_old = sm[g];
-      const float m_new = fmaxf(m_old, tmax);
-      const float m_use = (m_new == -INFINITY) ? 0.f : m_new;
-      const float p = exp2f(s - m_use);
-      const float psum = wave_sum(p);
-      sp[g][lane] = p;
-      if (lane == 0) {
-        const float a = exp2f(m_old - m_use);
-        salpha[g] = a;
-        sl[g] = sl[g] * a + psum;
-        sm[g] = m_new;
-      }
-    }
-    __syncthreads();
-    // ---- PV: thread = (d-pair, key group) ----
-    if (kg < KG) {
+        const f32x4_t q0 = *(const f32x4_t*)&sq[g][dp * 8];
+        const f32x4_t q1 = *(const f32x4_t*)&sq[g][dp * 8 + 4];
+        float part = kf[0] * q0[0] + kf[1] * q0[1] + kf[2] * q0[2] + kf[3] * q0[3] +
+                     kf[4] * q1[0] + kf[5] * q1[1] + kf[6] * q1[2] + kf[7] * q1[3];
+        if constexpr (SHFL) {
 #pragma unroll
-      for (int g = 0; g < G; ++g) { oacc[g][0] *= salpha[g]; oacc[g][1] *= salpha[g]; }
-      for (int kk = kg; kk < KT; kk += KG) {
-        const int key = kb + kk;
-        if (key >= kend) break;
-        const unsigned u = *(const unsigned*)(vc + cbase + (size_t)key * D + 2 * dp);
-        const float v0 = bf2f((bf16_t)(u & 0xffff)), v1 = bf2f((bf16_t)(u >> 16));
-#pragma unroll
-        for (int g = 0; g < G; ++g) {
-          const float p = sp[g][kk];
-          oacc[g][0] += p * v0;
-          oacc[g][1] += p * v1;
+          for (int o = 1; o < CPR; o <<= 1) part += __shfl_xor(part, o, 64);
+          if (dp == 0) sp[w][g][c / CPR] = part;
+        } else {
+          spart[w][g * KT * CPR + c] = part;
         }
       }
     }
-    __syncthreads();
-  }
-  // ---- reduce key groups, write partials ----
-  if (kg < KG) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    // ---- online softmax; lane = key ----
 #pragma unroll
-    for (int g = 0; g < G; ++g) { sred[kg][g][2 * dp] = oacc[g][0]; sred[kg][g][2 * dp + 1] = oacc[g][1]; }
+    for (int g = 0; g < G; ++g) {
+      float s;
+      if constexpr (SHFL) {
+        s = sp[w][g][lane];
+      } else {
+        s = 0.f;
+#pragma unroll
+        for (int j = 0; j < CPR; ++j) s += spart[w][g * KT * CPR + lane * CPR + j];
+      }
+      if (lane >= nk) s = -INFINITY;
+      const float tmax = wave_max(s);
+      const float m_new = fmaxf(m[g], tmax);
+      const float m_use = (m_new == -INFINITY) ? 0.f : m_new;
+      const float alpha = exp2f(m[g] - m_use);
+      const float p = exp2f(s - m_use);
+      l[g] = l[g] * alpha + wave_sum(p);
+      m[g] = m_new;
+      sp[w][g][lane] = p;
+#pragma unroll
+      for (int st = 0; st < NSET; ++st)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) acc[g][st][e] *= alpha;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    // ---- P * V ----
+    asm volatile("" ::: "memory");
+    u32x4_t vv[CPR];
+#pragma unroll
+    for (int i = 0; i < CPR; ++i) {
+      const int c = i * 64 + lane;
+      vv[i] = (c < nk * CPR) ? *(const u32x4_t*)(vb + c * 8) : u32x4_t{0, 0, 0, 0};
+    }
+#pragma unroll
+    for (int i = 0; i < CPR; ++i) {
+      const int c = i * 64 + lane;
+      const int key = c / CPR;
+      float vf[8];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        vf[2 * e] = bf2f((bf16_t)(vv[i][e] & 0xffff));
+        vf[2 * e + 1] = bf2f((bf16_t)(vv[i][e] >> 16));
+      }
+#pragma unroll
+      for (int g = 0; g < G; ++g) {
+        const float p = sp[w][g][key];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) acc[g][i % NSET][e] += p * vf[e];
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
+  // ---- merge lanes -> per-wave O (LDS atomics), then waves -> block partial ----
+#pragma unroll
+  for (int g = 0; g < G; ++g)
+#pragma unroll
+    for (int st = 0; st < NSET; ++st) {
+      const int dp = (lane + 64 * st) % CPR;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) atomicAdd(&so[w][g][dp * 8 + e], acc[g][st][e]);
+    }
+  if (lane == 0) {
+#pragma unroll
+    for (int g = 0; g < G; ++g) { swm[w][g] = m[g]; swl[w][g] = l[g]; }
   }
   __syncthreads();
   for (int i = tid; i < G * D; i += 256) {
     const int g = i / D, d = i % D;
-    float s = 0.f;
+    float M = fmaxf(fmaxf(swm[0][g], swm[1][g]), fmaxf(swm[2][g], swm[3][g]));
+    const float Mu = (M == -INFINITY) ? 0.f : M;
+    float o = 0.f, ls = 0.f;
 #pragma unroll
-    for (int j = 0; j < KG; ++j) s += sred[j][g][d];
+    for (int ww = 0; ww < 4; ++ww) {
+      const float f = exp2f(swm[ww][g] - Mu);
+      o += so[ww][g][d] * f;
+      ls += swl[ww][g] * f;
+    }
     const int h = hk * G + g;
-    po[(((size_t)b * H + h) * nsplit + split) * D + d] = s;
-  }
-  if (tid < G) {
-    const int h = hk * G + tid;
-    pm[((size_t)b * H + h) * nsplit + split] = sm[tid];
-    pl[((size_t)b * H + h) * nsplit + split] = sl[tid];
+    const size_t pidx = ((size_t)b * H + h) * nsplit + split;
+    po[pidx * D + d] = o;
+    if (d == 0) { pm[pidx] = M; pl[pidx] = ls; }
   }
 }
 

@@ -287,8 +287,17 @@ def flash_attn_varlen(q, k, v, cu_seqlens, max_seqlen: int, H: int, Hkv: int, D:
     return out
 
 
-def decode_attn(q, k_cache, v_cache, lens, slot, H, Hkv, D, max_len: int, chunk: int = 256, scale=None, out=None):
-    """q [B, >=H*D] (row stride any multiple of 8); lens/slot int32 [B]; max_len = max(lens) (host int)."""
+def decode_attn(q, k_cache, v_cache, lens, slot, H, Hkv, D, max_len: int, chunk: int = 0, scale=None, out=None):
+    """q [B, >=H*D] (row stride any multiple of 8); lens/slot int32 [B]; max_len = max(lens) or the
+    cache capacity (host int, fixes the split count so the launch is graph-capturable).
+    chunk = keys per workgroup (0 = auto: enough workgroups to fill 256 CUs, 4 waves x 64-key tiles)."""
+    if chunk <= 0:
+        # measured on MI355X (profiles/decode_attn_chunks_r1.txt): per-workgroup overhead dominates
+        # small chunks; aim for ~768 workgroups, 512..4096 keys each
+        want = max_len * q.shape[0] * Hkv / 768
+        chunk = 512
+        while chunk < want and chunk < 4096:
+            chunk *= 2
     _bf16_cuda(q, "q"); _i32(lens, "lens"); _i32(slot, "slot")
     _req(D in (64, 96, 128), "head dim")
     _req((H // Hkv) in (1, 2, 4, 8) and H % Hkv == 0, "GQA group must be 1/2/4/8")
