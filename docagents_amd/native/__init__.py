@@ -1,0 +1,101 @@
+"""Native (C++) runtime components and their build/launch helpers.
+
+* ``da-broker``   — NATS-protocol task broker with durable buffering + ack/redelivery/DLQ
+* ``da-kvserver`` — RESP key-value cache (query-result / embedding caches)
+* ``libda_text``  — text fast path (chunker word spans), loaded with ctypes
+
+Built with g++ into ``native/bin`` (``python -m docagents_amd.native`` or on first use).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import shutil
+import subprocess
+import sys
+import threading
+from pathlib import Path
+
+HERE = Path(__file__).resolve().parent
+BIN = HERE / "bin"
+_lock = threading.Lock()
+_TARGETS = {
+    "da-broker": (["broker.cpp"], ["-O2"]),
+    "da-kvserver": (["kvserver.cpp"], ["-O2"]),
+    "libda_text.so": (["textfast.cpp"], ["-O3", "-shared", "-fPIC"]),
+}
+
+
+def _cxx() -> str:
+    return os.environ.get("CXX") or shutil.which("g++") or shutil.which("c++") or "g++"
+
+
+def build(target: str | None = None, force: bool = False) -> dict:
+    out = {}
+    BIN.mkdir(exist_ok=True)
+    with _lock:
+        for name, (srcs, flags) in _TARGETS.items():
+            if target and name != target:
+                continue
+            dst = BIN / name
+            src_paths = [HERE / s for s in srcs]
+            newest = max(p.stat().st_mtime for p in src_paths + [HERE / "netloop.h"])
+            if dst.exists() and dst.stat().st_mtime >= newest and not force:
+                out[name] = dst
+                continue
+            tmp = dst.with_name(dst.name + ".tmp")
+            cmd = [_cxx(), "-std=c++17", *flags, "-I", str(HERE), *map(str, src_paths), "-o", str(tmp)]
+            r = subprocess.run(cmd, capture_output=True, text=True)
+            if r.returncode != 0:
+                raise RuntimeError(f"native build of {name} failed:\n{r.stderr}")
+            os.replace(tmp, dst)
+            out[name] = dst
+    return out
+
+
+def binary(name: str) -> Path:
+    return build(name)[name]
+
+
+def run_broker(args: list[str]) -> int:
+    """Exec the broker (CPU-only process: never touches the GPU)."""
+    from ..config import load
+    exe = str(binary("da-broker"))
+    if not any(a.startswith("--listen") for a in args):
+        url = load().queue_url or "nats://0.0.0.0:4222"
+        args = ["--listen", url] + args
+    os.execv(exe, [exe, *args])
+    return 0
+
+
+def run_kvserver(args: list[str]) -> int:
+    from ..config import load
+    exe = str(binary("da-kvserver"))
+    cfg = load()
+    if not any(a.startswith("--listen") for a in args):
+        args = ["--listen", cfg.redis_addr.replace("localhost", "0.0.0.0")] + args
+    if cfg.redis_password and "--requirepass" not in args:
+        args += ["--requirepass", cfg.redis_password]
+    os.execv(exe, [exe, *args])
+    return 0
+
+
+_TEXT = None
+
+
+def textlib():
+    global _TEXT
+    if _TEXT is None:
+        L = ctypes.CDLL(str(binary("libda_text.so")))
+        L.da_word_offsets.argtypes = [ctypes.c_char_p, ctypes.c_long, ctypes.c_void_p, ctypes.c_long]
+        L.da_word_offsets.restype = ctypes.c_long
+        L.da_chunk.argtypes = [ctypes.c_char_p, ctypes.c_void_p, ctypes.c_long, ctypes.c_long, ctypes.c_long,
+                               ctypes.c_void_p, ctypes.c_long, ctypes.c_void_p, ctypes.c_long]
+        L.da_chunk.restype = ctypes.c_long
+        _TEXT = L
+    return _TEXT
+
+
+if __name__ == "__main__":
+    for k, v in build(force="--force" in sys.argv).items():
+        print(k, v)

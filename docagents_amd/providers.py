@@ -102,6 +102,8 @@ class StubLLM:
 
 
 class LocalLLM:
+    supports_chunks = True  # Answer from chunk token ids cached at ingest
+
     def __init__(self, engine):
         self.engine = engine
 
@@ -117,6 +119,8 @@ class LocalLLM:
 
 
 class RemoteLLM:
+    supports_chunks = True
+
     def __init__(self, client):
         self.client = client
 

@@ -122,7 +122,7 @@ async def query_handler(deps, body: bytes) -> Response:
     quality = calculate_avg_similarity(results)
     t3 = time.perf_counter()
     try:
-        if hasattr(deps.llm, "answer_chunks") and hasattr(deps.store, "chunks_by_keys") and results:
+        if getattr(deps.llm, "supports_chunks", False) and hasattr(deps.store, "chunks_by_keys") and results:
             toks = await deps.store.chunks_by_keys([r.chunk.key for r in results])
             chunks = []
             for r in results:

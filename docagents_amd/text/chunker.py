@@ -54,6 +54,44 @@ def fields(text: str) -> list[str]:
 
 def chunk_text(text: str, opts: Options | None = None) -> list[Chunk]:
     opts = opts or Options()
+    if len(text) > 65536 and text.isascii():
+        try:
+            return chunk_text_native(text, opts)
+        except Exception:  # noqa: BLE001 - native library unavailable: pure-Python path below
+            pass
     words = fields(text)
     return [Chunk(index=i, text=" ".join(words[s:e]), token_count=e - s)
             for i, (s, e) in enumerate(chunk_spans(len(words), opts.max_tokens, opts.overlap))]
+
+
+def chunk_text_native(text: str, opts: Options | None = None) -> list[Chunk]:
+    """C++ fast path (docagents_amd/native/textfast.cpp) for ASCII text; identical output."""
+    import ctypes
+
+    import numpy as np
+
+    from ..native import textlib
+    opts = opts or Options()
+    if not text.isascii():
+        return chunk_text(text, opts)
+    L = textlib()
+    b = text.encode("ascii")
+    cap = len(b) // 2 + 1
+    words = np.empty(2 * cap, dtype=np.int64)
+    nw = L.da_word_offsets(b, len(b), words.ctypes.data, cap)
+    if nw == 0:
+        return []
+    mx = opts.max_tokens if opts.max_tokens > 0 else 400
+    step = mx - max(0, opts.overlap)
+    if step <= 0:
+        step = mx
+    nchunks = (max(0, nw - mx) + step - 1) // step + 1
+    out = ctypes.create_string_buffer(len(b) * (mx // step + 2) + 16)
+    meta = np.empty(3 * nchunks + 3, dtype=np.int64)
+    nc = L.da_chunk(b, words.ctypes.data, nw, opts.max_tokens, opts.overlap, out, len(out), meta.ctypes.data,
+                    nchunks + 1)
+    if nc < 0:
+        raise RuntimeError("native chunker buffer too small")
+    raw = out.raw
+    return [Chunk(index=i, text=raw[meta[3 * i]:meta[3 * i] + meta[3 * i + 1]].decode("ascii"),
+                  token_count=int(meta[3 * i + 2])) for i in range(nc)]
