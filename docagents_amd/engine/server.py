@@ -146,12 +146,12 @@ class EngineGroup:
         dist.broadcast(q, src=0, group=self.data_group)                     # C2 (broadcast form)
         s, rows = e.index.search(q, k, thr, filters)
         gid = e.index.gather_ids(rows)
-        S = torch.empty((self.world,) + tuple(s.shape), dtype=s.dtype, device=dev)
-        G = torch.empty((self.world,) + tuple(gid.shape), dtype=gid.dtype, device=dev)
+        S = torch.empty((self.world * Q, k), dtype=s.dtype, device=dev)
+        G = torch.empty((self.world * Q, k), dtype=gid.dtype, device=dev)
         dist.all_gather_into_tensor(S, s.contiguous(), group=self.data_group)    # C1
         dist.all_gather_into_tensor(G, gid.contiguous(), group=self.data_group)
-        flatS = S.permute(1, 0, 2).reshape(Q, -1)
-        flatG = G.permute(1, 0, 2).reshape(Q, -1)
+        flatS = S.view(self.world, Q, k).permute(1, 0, 2).reshape(Q, -1)
+        flatG = G.view(self.world, Q, k).permute(1, 0, 2).reshape(Q, -1)
         flatS = torch.where(flatG >= 0, flatS, torch.full_like(flatS, float("-inf")))
         ms, mi = torch.sort(flatS, dim=1, descending=True, stable=True)
         ms, mi = ms[:, :k], mi[:, :k]

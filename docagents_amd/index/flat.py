@@ -130,7 +130,7 @@ class FlatIndex:
         ranges, off, maxrows = [], [0], 0
         for f in doc_filters:
             tot = 0
-            for d in f:
+            for d in (self.docs if f is None else f):  # None = every document
                 e = self.docs.get(d)
                 if e is None:
                     continue
@@ -178,7 +178,13 @@ class FlatIndex:
             if rem:
                 bm[:, full] = (1 << rem) - 1
         else:
+            full, rem = divmod(nslots, 32)
             for i, f in enumerate(doc_filters):
+                if f is None:
+                    bm[i, :full] = 0xFFFFFFFF
+                    if rem:
+                        bm[i, full] = (1 << rem) - 1
+                    continue
                 for d in f:
                     e = self.docs.get(d)
                     if e is not None and e.rows:

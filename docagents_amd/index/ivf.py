@@ -150,7 +150,13 @@ class IVFFlatIndex(FlatIndex):
             if rem:
                 bm[:, full] = (1 << rem) - 1
         else:
+            full, rem = divmod(nslots, 32)
             for i, f in enumerate(doc_filters):
+                if f is None:
+                    bm[i, :full] = 0xFFFFFFFF
+                    if rem:
+                        bm[i, full] = (1 << rem) - 1
+                    continue
                 for d in f:
                     e = self.docs.get(d)
                     if e is not None and e.rows:

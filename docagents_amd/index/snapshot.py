@@ -1,0 +1,51 @@
+"""Index shard snapshot / restore: safetensors with the live rows (removed
+documents compacted away), their external ids and doc slots, plus a JSON doc table in the metadata
+header. IVF shards also store centroids; lists are rebuilt on load."""
+from __future__ import annotations
+
+import json
+import os
+
+import numpy as np
+import torch
+from safetensors.torch import load_file, save_file
+
+
+def save_index(index, path: str) -> str:
+    with index.lock:
+        docs, rows = [], []
+        for d, e in index.docs.items():
+            n = 0
+            for a, b in e.ranges:
+                rows.append((a, b))
+                n += b - a
+            docs.append([d, n])
+        sel = np.concatenate([np.arange(a, b) for a, b in rows]) if rows else np.zeros(0, dtype=np.int64)
+        selt = torch.from_numpy(sel.astype(np.int64)).to(index.device)
+        tensors = {"X": index.X.index_select(0, selt).cpu().contiguous(),
+                   "ids": torch.from_numpy(index.ids[sel].copy())}
+        if getattr(index, "centroids", None) is not None:
+            tensors["centroids"] = index.centroids.cpu().contiguous()
+        meta = {"dim": str(index.dim), "kind": index.kind, "docs": json.dumps(docs)}
+    tmp = path + ".tmp"
+    os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
+    save_file(tensors, tmp, metadata=meta)
+    os.replace(tmp, path)
+    return path
+
+
+def load_index(index, path: str) -> int:
+    from safetensors import safe_open
+    with safe_open(path, framework="pt") as f:
+        meta = f.metadata()
+    t = load_file(path)
+    if int(meta["dim"]) != index.dim:
+        raise ValueError(f"snapshot dim {meta['dim']} != index dim {index.dim}")
+    docs = json.loads(meta["docs"])
+    X, ids = t["X"], t["ids"].numpy()
+    with index.lock:
+        index.add_bulk([d for d, _ in docs], [n for _, n in docs], ids, X)
+        if "centroids" in t and hasattr(index, "_build_lists"):
+            index.centroids = t["centroids"].to(index.device)
+            index._build_lists()
+    return len(index)

@@ -46,9 +46,9 @@ class TPContext:
         if self.size == 1:
             return t
         import torch.distributed as dist
-        out = torch.empty((self.size,) + tuple(t.shape), dtype=t.dtype, device=t.device)
+        out = torch.empty((self.size * t.shape[0],) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
         dist.all_gather_into_tensor(out, t.contiguous(), group=self.group)
-        return out.permute(1, 0, 2).reshape(t.shape[0], -1)
+        return out.view(self.size, t.shape[0], -1).permute(1, 0, 2).reshape(t.shape[0], -1)
 
 
 def _randn(shape, gen, device, std=0.02):

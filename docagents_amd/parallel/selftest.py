@@ -1,0 +1,169 @@
+"""Multi-process correctness checks for the distributed paths (run with gloo on CPU in tests, or
+with RCCL on GPUs). Each ``check_*`` is a ``torch.multiprocessing.spawn`` target; rank 0 writes a
+JSON verdict to ``out_path``.
+
+  check_tp_decoder      TP=world LlamaDecoder (column/row-parallel + all-reduce, vocab-parallel
+                        lm_head + all-gather) == the unsharded decoder (prefill logits, greedy tokens)
+  check_sharded_index   W-way sharded flat index (C2 all-gather queries, C1 all-gather top-k, merge)
+                        == exact single-index search over all rows, with doc filters and threshold
+  check_engine_group    EngineGroup command fan-out: embed (DP), search (broadcast + gather), index
+                        routing by document owner, answer (DP generate)
+  check_ivf_kmeans      IVFFlat with cross-shard k-means statistics all-reduce (C6)
+"""
+from __future__ import annotations
+
+import json
+import os
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+
+def _init(rank, world, port):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+
+
+def _done(rank, out_path, verdict):
+    if rank == 0:
+        with open(out_path, "w") as f:
+            json.dump(verdict, f)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def check_tp_decoder(rank, world, port, out_path):
+    _init(rank, world, port)
+    from ..models.configs import decoder_config
+    from ..models.llama import LlamaDecoder, TPContext, random_weights
+    from ..engine.generator import Generator
+    cfg = decoder_config("tiny-dec")
+    full = random_weights(cfg, "cpu", seed=5)
+    ref = LlamaDecoder(cfg, "cpu", weights=full)
+    tp = LlamaDecoder(cfg, "cpu", tp=TPContext(rank, world, None),
+                      weights=random_weights(cfg, "cpu", seed=5, tp_rank=rank, tp_size=world, full_then_shard=True))
+    prompts = [list(range(30, 30 + n)) for n in (9, 33, 4)]
+    g_ref = Generator(ref, max_batch=4, max_seq=256, temperature=0.0, use_graphs=False)
+    g_tp = Generator(tp, max_batch=4, max_seq=256, temperature=0.0, use_graphs=False)
+    a = g_ref.generate(prompts, 6)
+    b = g_tp.generate(prompts, 6)
+    same = all(x.tokens == y.tokens for x, y in zip(a, b))
+    probs = max(abs(x.mean_prob - y.mean_prob) for x, y in zip(a, b))
+    _done(rank, out_path, {"same_tokens": same, "max_prob_diff": probs, "tokens": [x.tokens for x in b]})
+
+
+def check_sharded_index(rank, world, port, out_path):
+    _init(rank, world, port)
+    from ..index.flat import FlatIndex
+    from .sharded_index import ShardedIndex
+    d, per, B, k = 64, 120, 5, 7
+    rng = np.random.default_rng(0)  # identical global data on every rank
+    X = rng.standard_normal((world * per, d)).astype(np.float32)
+    X /= np.linalg.norm(X, axis=1, keepdims=True)
+    docs = [f"doc{i // 10}" for i in range(world * per)]
+    local = FlatIndex(d, "cpu")
+    for r0 in range(rank * per, (rank + 1) * per, 10):
+        local.add(docs[r0], np.arange(r0, r0 + 10), torch.from_numpy(X[r0:r0 + 10]))
+    sh = ShardedIndex(local, rank, world)
+    Q = rng.standard_normal((world * B, d)).astype(np.float32)
+    Q /= np.linalg.norm(Q, axis=1, keepdims=True)
+    filters = [[f"doc{j}" for j in rng.choice(world * per // 10, size=4, replace=False)] for _ in range(world * B)]
+    filters[0] = [docs[-1], docs[0]]
+    s, ids = sh.search(torch.from_numpy(Q[rank * B:(rank + 1) * B]), k, 0.0, filters)
+    # exact reference over all rows (bf16-rounded operands, like the index); ids must match except
+    # where two candidates tie within bf16 rounding
+    Xb = torch.from_numpy(X).bfloat16().float().numpy()
+    Qb = torch.from_numpy(Q).bfloat16().float().numpy()
+    ok = True
+    s = s.numpy()
+    for b in range(B):
+        qi = rank * B + b
+        allowed = np.array([docs[i] in filters[qi] for i in range(len(docs))])
+        sc = Xb @ Qb[qi]
+        m = allowed & (sc >= 0.0)
+        idx = np.where(m)[0]
+        order = idx[np.lexsort((idx, -sc[idx]))][:k]
+        got = [int(i) for i in ids[b].tolist() if i >= 0]
+        if len(got) != len(order) or not np.allclose(np.sort(s[b][:len(got)]), np.sort(sc[order]), atol=2e-3):
+            ok = False
+        if any(not allowed[i] for i in got):
+            ok = False
+        if sum(1 for x, y in zip(got, order.tolist()) if x != y) > 1:
+            ok = False
+    oks = [None] * world
+    dist.all_gather_object(oks, ok)
+    _done(rank, out_path, {"exact": all(oks)})
+
+
+def check_engine_group(rank, world, port, out_path):
+    _init(rank, world, port)
+    from ..engine.engine import Engine
+    from ..engine.server import EngineGroup, owner_of
+    eng = Engine("tiny-enc", "tiny-dec", "cpu", max_batch=4, max_seq=512, max_new_tokens=5, summary_max_new=5,
+                 use_graphs=False)
+    grp = EngineGroup(eng, rank, world, ctrl_group=None, data_group=None)
+    if rank != 0:
+        grp.follower_loop()
+        dist.barrier()
+        dist.destroy_process_group()
+        return
+    texts = [f"text number {i} about topic {i % 3}" for i in range(7)]
+    vecs = grp.run("embed", {"texts": texts})
+    solo = eng.embed(texts, out_dtype=torch.float32).numpy()
+    embed_ok = vecs.shape == (7, eng.dim) and np.allclose(vecs, solo, atol=1e-4)
+    owners = set()
+    # distinct random unit vectors for the routing check (a random-init encoder maps all texts to
+    # nearly the same direction, which would make the top-1 expectation a bf16 coin flip)
+    vecs = np.random.default_rng(3).standard_normal((7, eng.dim)).astype(np.float32)
+    vecs /= np.linalg.norm(vecs, axis=1, keepdims=True)
+    for i in range(6):
+        doc = f"doc-{i}"
+        owners.add(owner_of(doc, world))
+        grp.run("index_add", {"doc_id": doc, "keys": np.array([100 + i]), "vecs": vecs[i:i + 1]})
+    s, keys = grp.run("search", {"vecs": vecs[:3], "k": 2, "min_sim": -1.0, "filters": [["doc-0"], ["doc-1", "doc-2"], None]})
+    search_ok = int(keys[0][0]) == 100 and int(keys[1][0]) == 101 and int(keys[2][0]) == 102
+    res = grp.run("answer", {"items": [{"question": "q?", "context": "some context", "quality": 0.5}] * 3})
+    answer_ok = len(res) == 3 and all(0 <= c <= 0.5 + 1e-6 for _, c in res)
+    stats = grp.run("stats", {})
+    grp.run("shutdown", {}) if False else grp._bcast(("shutdown", {}))
+    verdict = {"embed_ok": bool(embed_ok), "search_ok": bool(search_ok), "answer_ok": bool(answer_ok),
+               "owners": sorted(owners), "ranks": len(stats)}
+    with open(out_path, "w") as f:
+        json.dump(verdict, f)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def check_ivf_kmeans(rank, world, port, out_path):
+    _init(rank, world, port)
+    from ..index.ivf import IVFFlatIndex
+    from .sharded_index import ShardedIndex
+    d, per = 32, 600
+    rng = np.random.default_rng(1)
+    centers = rng.standard_normal((8, d)).astype(np.float32)
+    lab = rng.integers(0, 8, size=world * per)
+    X = centers[lab] + 0.15 * rng.standard_normal((world * per, d)).astype(np.float32)
+    X /= np.linalg.norm(X, axis=1, keepdims=True)
+    ix = IVFFlatIndex(d, "cpu", lists=8, probes=2)
+    lo = rank * per
+    for r0 in range(lo, lo + per, 50):
+        ix.add(f"d{r0}", np.arange(r0, r0 + 50), torch.from_numpy(X[r0:r0 + 50]))
+    sh = ShardedIndex(ix, rank, world)
+    sh.train(iters=8)
+    Q = X[rng.choice(world * per, 20, replace=False)] + 0.01
+    Q /= np.linalg.norm(Q, axis=1, keepdims=True)
+    s, ids = sh.search(torch.from_numpy(Q[rank * 10:(rank + 1) * 10] if rank < 2 else Q[:10]), 5, -1.0, None)
+    # recall@5 vs exact
+    rec = []
+    for b in range(ids.shape[0]):
+        qi = rank * 10 + b if rank < 2 else b
+        exact = set(np.argsort(-(X @ Q[qi]))[:5].tolist())
+        rec.append(len(exact & set(ids[b].tolist())) / 5)
+    allrec = [None] * world
+    dist.all_gather_object(allrec, float(np.mean(rec)))
+    C = ix.centroids.float()
+    C0 = C.clone()
+    dist.broadcast(C0, 0)
+    _done(rank, out_path, {"recall": float(np.mean(allrec)), "centroids_equal": bool(torch.allclose(C, C0))})

@@ -1,0 +1,128 @@
+"""Engine / model / index behaviour on CPU (the fp32 reference op path) with tiny configs:
+encoder normalisation, generation bookkeeping, map-reduce summarisation, index semantics
+(filters, threshold, removal, snapshot), IVF recall and the engine RPC server with micro-batching."""
+import asyncio
+import socket
+
+import numpy as np
+import pytest
+import torch
+
+from docagents_amd.engine.engine import Engine
+from docagents_amd.index.flat import FlatIndex
+from docagents_amd.index.ivf import IVFFlatIndex
+from docagents_amd.index.snapshot import load_index, save_index
+
+
+@pytest.fixture(scope="module")
+def eng():
+    return Engine("tiny-enc", "tiny-dec", "cpu", max_batch=4, max_seq=512, max_new_tokens=6, summary_max_new=6,
+                  use_graphs=False)
+
+
+def test_embed_unit_norm_and_one_to_one(eng):
+    v = eng.embed(["hello world", "", "  \x00 ", "Document: a.txt\n\nbody"])
+    assert v.shape == (4, eng.dim)
+    assert torch.allclose(v.float().norm(dim=-1), torch.ones(4), atol=1e-2)
+    with pytest.raises(ValueError):
+        eng.embed_one("  \x01  ")
+
+
+def test_generation_confidence_and_lengths(eng):
+    out = eng.answer_many([("q?", [[10, 11, 12] * 30], 0.8), ("q2?", [], 0.0)], 6)
+    assert len(out) == 2
+    (a1, c1), (a2, c2) = out
+    assert 0 < c1 <= 0.8 and c2 == 0.0
+    r = eng.gen.generate([[5, 6, 7], [8] * 40], 6)
+    assert all(len(x.tokens) <= 6 and x.n_tokens >= 1 for x in r)
+
+
+def test_summarize_map_reduce_long_input(eng):
+    long_text = "alpha beta gamma delta " * 400  # > the tiny decoder's 512-token context
+    s = eng.summarize_many([long_text, "short text"])
+    assert len(s) == 2 and all(isinstance(x[0], str) and isinstance(x[1], list) for x in s)
+
+
+def _unit(n, d, seed=0):
+    x = np.random.default_rng(seed).standard_normal((n, d)).astype(np.float32)
+    return torch.from_numpy(x / np.linalg.norm(x, axis=1, keepdims=True))
+
+
+def test_flat_index_filters_threshold_removal_snapshot(tmp_path):
+    X = _unit(40, 32)
+    ix = FlatIndex(32, "cpu")
+    for i in range(4):
+        ix.add(f"d{i}", np.arange(10 * i, 10 * i + 10) + 1000, X[10 * i:10 * i + 10])
+    s, r = ix.search(X[[3, 25]], 3, -1.0, [["d0"], ["d2", "d3"]])
+    assert int(ix.row_ids(r[0].numpy())[0]) == 1003 and int(ix.row_ids(r[1].numpy())[0]) == 1025
+    s, r = ix.search(X[[3]], 5, 0.99, [["d0", "d1"]])  # only the self-match passes the floor
+    assert (r[0] >= 0).sum() == 1
+    assert ix.remove_doc("d0") == 10
+    s, r = ix.search(X[[3]], 3, -1.0, None)
+    assert all(int(x) >= 10 for x in r[0] if x >= 0)
+    p = save_index(ix, str(tmp_path / "shard0.safetensors"))
+    ix2 = FlatIndex(32, "cpu")
+    assert load_index(ix2, p) == 30
+    s2, r2 = ix2.search(X[[25]], 3, -1.0, [["d2"]])
+    assert int(ix2.row_ids(r2[0].numpy())[0]) == 1025
+
+
+def test_ivf_recall_and_delta_rows():
+    rng = np.random.default_rng(2)
+    centers = rng.standard_normal((10, 48)).astype(np.float32)
+    lab = rng.integers(0, 10, 2000)
+    X = centers[lab] + 0.2 * rng.standard_normal((2000, 48)).astype(np.float32)
+    X = torch.from_numpy(X / np.linalg.norm(X, axis=1, keepdims=True))
+    ix = IVFFlatIndex(48, "cpu", lists=10, probes=3)
+    for i in range(0, 1800, 100):
+        ix.add(f"d{i}", np.arange(i, i + 100), X[i:i + 100])
+    assert ix.train(iters=6)
+    ix.add("late", np.arange(1800, 2000), X[1800:])  # delta region, scanned exactly
+    Q = X[rng.choice(2000, 30, replace=False)]
+    s, r = ix.search(Q, 5, -1.0, None)
+    rec = np.mean([len(set(np.argsort(-(X @ Q[i]).numpy())[:5]) & set(r[i].tolist())) / 5 for i in range(30)])
+    assert rec > 0.8
+    s, r = ix.search(X[[1900]], 1, -1.0, [["late"]])
+    assert int(r[0, 0]) == 1900
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def test_engine_rpc_server_microbatching(eng):
+    from docagents_amd.engine.rpc import EngineClient
+    from docagents_amd.engine.server import EngineGroup, EngineServer
+    from docagents_amd.providers import RemoteEmbedder, RemoteLLM
+    from docagents_amd.store.vectors import EngineVectors
+    from docagents_amd.utils.log import discard
+
+    async def go():
+        srv = EngineServer(EngineGroup(eng), discard())
+        port = _port()
+        await srv.start(f"tcp://127.0.0.1:{port}")
+        cl = await EngineClient(f"tcp://127.0.0.1:{port}").connect()
+        emb, llm, vec = RemoteEmbedder(cl), RemoteLLM(cl), EngineVectors(cl)
+        # 8 concurrent single-text embeds -> coalesced into fewer encoder batches
+        outs = await asyncio.gather(*[emb.embed(f"question {i}") for i in range(8)])
+        assert all(o.shape == (eng.dim,) for o in outs)
+        assert srv.stats["embed_raw"]["batches"] < 8
+        vs = await emb.embed_batch(["a b", "c d", ""])
+        assert len(vs) == 3
+        u = _unit(3, eng.dim, 5).numpy()
+        await vec.add("docX", np.array([7, 8, 9]), u)
+        hits = await vec.search(u[1], ["docX"], 2, -1.0)
+        assert hits[0][0] == 8
+        s, kp = await llm.summarize("some text to summarize")
+        a, c = await llm.answer("q?", "ctx text", 0.5)
+        a2, c2 = await llm.answer_chunks("q?", [("ctx", [5, 6, 7]), ("other", None)], 0.5)
+        assert isinstance(s, str) and isinstance(kp, list) and 0 <= c <= 0.5 and 0 <= c2 <= 0.5
+        st = await cl.call("stats")
+        assert st["ranks"][0]["index_rows"] >= 3
+        await cl.close()
+        srv.server.close()
+    asyncio.run(go())

@@ -1,0 +1,135 @@
+"""End-to-end: native broker + native KV cache + gateway + parser + analysis + query as separate
+processes on localhost (BASELINE.json config 1: stub embeddings, CPU brute-force cosine, stub LLM).
+Drives upload -> poll summary -> query -> cached query, like a real client."""
+import json
+import os
+import signal
+import socket
+import subprocess
+import sys
+import time
+
+import httpx
+import pytest
+
+from docagents_amd.text import multipart
+from docagents_amd.text.pdf import make_pdf
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def wait_http(url, timeout=60):
+    t0 = time.time()
+    while time.time() - t0 < timeout:
+        try:
+            if httpx.get(url, timeout=1).status_code == 200:
+                return
+        except Exception:  # noqa: BLE001
+            time.sleep(0.1)
+    raise TimeoutError(url)
+
+
+@pytest.fixture(scope="module")
+def stack(tmp_path_factory):
+    from docagents_amd.native import binary
+    tmp = tmp_path_factory.mktemp("stack")
+    bport, kport = free_port(), free_port()
+    gport, qport, pport, aport = free_port(), free_port(), free_port(), free_port()
+    env = dict(os.environ, PYTHONPATH=ROOT, LLM_PROVIDER="stub", STORE_PROVIDER="sqlite",
+               DB_PATH=str(tmp / "meta.sqlite3"), QUEUE_PROVIDER="broker", QUEUE_URL=f"nats://127.0.0.1:{bport}",
+               CACHE_PROVIDER="kv", REDIS_ADDR=f"127.0.0.1:{kport}", REDIS_PASSWORD="secret", MIN_SIMILARITY="-1",
+               QUERY_SERVICE_URL=f"http://127.0.0.1:{qport}/api/query", LOG_LEVEL="warn", EMBED_DIM="64")
+    procs = [subprocess.Popen([str(binary("da-broker")), "--listen", f"127.0.0.1:{bport}"], stderr=subprocess.DEVNULL),
+             subprocess.Popen([str(binary("da-kvserver")), "--listen", f"127.0.0.1:{kport}", "--requirepass", "secret"],
+                              stderr=subprocess.DEVNULL)]
+    time.sleep(0.3)
+    logs = []
+    for name, port in (("query", qport), ("gateway", gport), ("parser", pport), ("analysis", aport)):
+        lf = open(tmp / f"{name}.log", "w")
+        logs.append(lf)
+        procs.append(subprocess.Popen([sys.executable, "-m", "docagents_amd.services", name],
+                                      env=dict(env, PORT=str(port)), stdout=lf, stderr=subprocess.STDOUT))
+    try:
+        for port in (qport, gport, pport, aport):
+            wait_http(f"http://127.0.0.1:{port}/healthz")
+        yield {"gateway": f"http://127.0.0.1:{gport}", "tmp": tmp}
+    finally:
+        for p in procs:
+            p.send_signal(signal.SIGTERM)
+        for p in procs:
+            try:
+                p.wait(5)
+            except subprocess.TimeoutExpired:
+                p.kill()
+        for lf in logs:
+            lf.close()
+
+
+def _upload(gw, name, data, ct):
+    body, ctype = multipart.build({}, {"file": (name, data, ct)})
+    return httpx.post(gw + "/api/documents/upload", content=body, headers={"content-type": ctype}, timeout=30)
+
+
+def _wait_summary(gw, doc, timeout=30):
+    t0 = time.time()
+    while time.time() - t0 < timeout:
+        r = httpx.get(f"{gw}/api/documents/{doc}/summary", timeout=10)
+        if r.status_code == 200:
+            return r.json()
+        assert r.status_code == 404 and r.text == "summary not ready\n"
+        time.sleep(0.1)
+    raise TimeoutError("summary")
+
+
+def test_upload_summary_query_cache(stack):
+    gw = stack["gateway"]
+    text = ("The MI355X accelerator has 256 compute units and 288 GB of HBM3E memory. " * 60).strip()
+    r = _upload(gw, "gpu.txt", text.encode(), "text/plain")
+    assert r.status_code == 202, r.text
+    doc = r.json()["document_id"]
+    assert r.json()["status"] == "processing"
+    s = _wait_summary(gw, doc)
+    assert s["summary"].startswith("Summary of") and len(s["key_points"]) == 2 and s["documentId"] == doc
+    # the summary is written before the embeddings: wait for status ready via a successful query
+    # (a query before the embeddings land is answered — and cached — with no sources, exactly like
+    # the reference; probe with distinct questions so the real one is a fresh cache miss)
+    for i in range(200):
+        p = httpx.post(gw + "/api/query", json={"question": f"probe {i}", "document_ids": [doc]}, timeout=30)
+        assert p.status_code == 200, p.text
+        if p.json()["sources"]:
+            break
+        time.sleep(0.1)
+    body = {"question": "How much memory does the MI355X have?", "document_ids": [doc], "top_k": 3}
+    q = httpx.post(gw + "/api/query", json=body, timeout=30)
+    assert q.status_code == 200, q.text
+    j = q.json()
+    assert j["cached"] is False and len(j["sources"]) == 3  # 840 words -> 3 chunks of 400/80
+    assert j["answer"].startswith("According to the documentation")
+    assert all(set(x) == {"chunk_id", "score", "preview"} for x in j["sources"])
+    assert all(len(x["preview"].encode()) <= 153 for x in j["sources"])
+    q2 = httpx.post(gw + "/api/query", json=body, timeout=30)
+    assert q2.json()["cached"] is True and q2.json()["answer"] == j["answer"]
+
+
+def test_pdf_upload_and_errors(stack):
+    gw = stack["gateway"]
+    r = _upload(gw, "paper.pdf", make_pdf(["Attention is all you need. " * 30, "Second page words."]), None)
+    assert r.status_code == 202
+    s = _wait_summary(gw, r.json()["document_id"])
+    assert "Attention" in s["summary"]
+    bad = _upload(gw, "x.docx", b"zzz", None)
+    assert bad.status_code == 400 and bad.text == "unsupported file type (only PDF and TXT allowed)\n"
+    q = httpx.post(gw + "/api/query", content=b"{invalid json}", timeout=10)
+    assert q.status_code == 400 and q.text == "invalid payload\n"
+    q = httpx.post(gw + "/api/query", json={"question": "Hi", "document_ids": []}, timeout=10)
+    assert q.status_code == 400 and q.text == "Question must be at least 3; DocumentIDs must be at least 1\n"
+    m = httpx.get(gw + "/metrics", timeout=10)
+    assert m.status_code == 200 and "da_http_request_seconds" in m.text
