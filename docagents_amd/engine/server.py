@@ -87,7 +87,8 @@ class EngineGroup:
             return np.concatenate(parts, axis=0) if parts else v
         if cmd in ("answer", "summarize"):
             items = a["items"]
-            lo, hi = self._slice(len(items))
+            # tensor-parallel decoder: every rank runs every generation on its weight shard
+            lo, hi = (0, len(items)) if getattr(self, "tensor_parallel", False) else self._slice(len(items))
             faults.maybe_fail("engine.generate")
             mine = items[lo:hi]
             if cmd == "summarize":
@@ -102,6 +103,8 @@ class EngineGroup:
                         ids = [e._ids(it.get("context", ""))] if it.get("context") else []
                     batch.append((it["question"], ids, it.get("quality", 0.0)))
                 res = e.answer_many(batch) if batch else []
+            if getattr(self, "tensor_parallel", False):
+                return res
             out = []
             for r in self._gather(res):
                 out.extend(r)

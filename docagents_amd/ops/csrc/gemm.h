@@ -1,0 +1,21 @@
+// Shared GEMM declarations (epilogue codes and launch arguments).
+#pragma once
+#include "common.h"
+
+enum Epi : int {
+  EPI_NONE = 0,
+  EPI_BIAS = 1,
+  EPI_GELU = 2,       // bias (optional) + exact GELU (BERT)
+  EPI_SWIGLU = 3,     // W rows interleaved in 16-row (gate, up) groups; out N/2 = silu(g)*u
+  EPI_RESID = 4,      // bias (optional) + residual add
+  EPI_PARTIAL = 5,    // fp32 split-K partial to workspace
+};
+
+struct GemmArgs {
+  const bf16_t* A; const bf16_t* W; bf16_t* C;
+  const bf16_t* bias; const bf16_t* resid; float* ws;
+  int M, N, K, lda, ldc, ldr, k_per_split;
+};
+
+// large-tile (256x256, 8 waves, LDS-DMA staged) path; returns hipError_t
+int launch_gemm256(const GemmArgs& a, int epi, hipStream_t s);

@@ -13,22 +13,7 @@
 //  * epilogue staged through LDS in fp32, then 16-B coalesced stores with bias / GELU / SwiGLU /
 //    residual fused (the reference outsources all of this to OpenAI).
 //  * split-K writes fp32 partials; gemm_splitk_reduce applies the same epilogue.
-#include "common.h"
-
-enum Epi : int {
-  EPI_NONE = 0,
-  EPI_BIAS = 1,
-  EPI_GELU = 2,       // bias (optional) + exact GELU (BERT)
-  EPI_SWIGLU = 3,     // W rows interleaved in 16-row (gate, up) groups; out N/2 = silu(g)*u
-  EPI_RESID = 4,      // bias (optional) + residual add
-  EPI_PARTIAL = 5,    // fp32 split-K partial to workspace
-};
-
-struct GemmArgs {
-  const bf16_t* A; const bf16_t* W; bf16_t* C;
-  const bf16_t* bias; const bf16_t* resid; float* ws;
-  int M, N, K, lda, ldc, ldr, k_per_split;
-};
+#include "gemm.h"
 
 template <int BM, int BN, int WM, int WN, int EPI>
 __global__ void __launch_bounds__(256)
@@ -298,7 +283,14 @@ DA_EXPORT int da_gemm_bf16(const void* A, int lda, const void* W, void* C, int l
   a.A = (const bf16_t*)A; a.W = (const bf16_t*)W; a.C = (bf16_t*)C;
   a.bias = (const bf16_t*)bias; a.resid = (const bf16_t*)resid; a.ws = (float*)ws;
   a.M = M; a.N = N; a.K = K; a.lda = lda; a.ldc = ldc; a.ldr = ldr; a.k_per_split = K / splits;
-  if (tile == 0) tile = (M <= 32) ? 3 : (M <= 64 ? 2 : 1);
+  if (tile == 0) {
+    const long t256 = (long)((M + 255) / 256) * ((N + 255) / 256);
+    tile = (M <= 32) ? 3 : (M <= 64 ? 2 : (t256 >= 256 && splits == 1 ? 4 : 1));
+  }
+  if (tile == 4) {
+    if (splits != 1) return (int)hipErrorInvalidValue;
+    return launch_gemm256(a, epi, s);
+  }
   int err;
   switch (tile) {
     case 1: err = launch_tile<128, 128, 2, 2>(a, epi, splits, s); break;

@@ -1,0 +1,179 @@
+// 256x256-tile bf16 GEMM for prefill-sized M (C[M,N] = epi(A[M,K] . W[N,K]^T)).
+//
+// MI355X-first structure (cdna_hip_programming.md §5 "glds vs register staging", T1, T2):
+//  * 512 threads = 8 waves as 2 (M) x 4 (N); each wave owns a 128 x 64 output block
+//    (8 x 4 fragments of v_mfma_f32_16x16x32_bf16, 128 accumulator registers).
+//  * operands staged global -> LDS with LDS-DMA (`global_load_lds_dwordx4`: 1 KiB per
+//    wave-instruction, no VGPR round trip), two 64-KiB stages (A 256x64 + W 256x64 bf16).
+//    The LDS image is lane-linear, so the bank-conflict XOR swizzle (16-B chunk c of row r stored
+//    at chunk c ^ ((r >> 1) & 7)) is applied on the per-lane SOURCE address and undone on the
+//    ds_read_b128 address (rule 21: same involution both sides).
+//  * one barrier per K-step: the barrier that publishes stage kt also proves every wave finished
+//    reading stage kt-1, so the LDS-DMA for tile kt+1 is issued right after it and flies under the
+//    64 MFMAs per wave of tile kt. Fragment reads for the whole K-step are issued BEFORE the DMA so
+//    the compiler never has to order a ds_read behind a pending LDS-DMA.
+//  * bijective XCD remap + grouped-M tile order (L2 reuse of A panels / W panels per XCD).
+//  * epilogue: bias / GELU / SwiGLU applied in registers, bf16 tile staged through LDS, then
+//    16-B coalesced row stores with the residual add fused.
+#include "gemm.h"
+
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+typedef __attribute__((address_space(1))) const void* gptr_t;
+
+namespace {
+constexpr int BM = 256, BN = 256, BK = 64;
+constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2, STAGE = A_BYTES + B_BYTES;  // 64 KiB
+constexpr int TM = 128, TN = 64;                      // per-wave output block
+constexpr int SROW = TN * 2 + 16;                     // staging row stride (bytes)
+constexpr int STAGING = 8 * TM * SROW;                // 144 KiB
+constexpr int SMEM = (2 * STAGE > STAGING) ? 2 * STAGE : STAGING;
+}  // namespace
+
+__device__ __forceinline__ int swz(int r) { return (r >> 1) & 7; }
+
+template <int EPI>
+__global__ void __launch_bounds__(512)
+gemm256_kernel(GemmArgs p) {
+  __shared__ __attribute__((aligned(16))) char smem[SMEM];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid >> 2, wn = wid & 3;
+  const int fr = lane & 15, fg = lane >> 4;
+
+  const int ntm = (p.M + BM - 1) / BM, ntn = (p.N + BN - 1) / BN;
+  const int t = xcd_remap(blockIdx.x, ntm * ntn);
+  constexpr int GROUP = 4;
+  const int gid = t / (GROUP * ntn);
+  const int first_m = gid * GROUP;
+  const int gsz = min(ntm - first_m, GROUP);
+  const int tin = t % (GROUP * ntn);
+  const int m0 = (first_m + tin % gsz) * BM, n0 = (tin / gsz) * BN;
+
+  // ---- per-lane LDS-DMA source pointers (rows clamped into range; clamped rows only feed
+  //      outputs that are never stored) ----
+  const bf16_t* asrc[4];
+  const bf16_t* bsrc[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int r = (wid * 4 + j) * 8 + (lane >> 3);
+    const int c = (lane & 7) ^ swz(r);
+    asrc[j] = p.A + (size_t)min(m0 + r, p.M - 1) * p.lda + c * 8;
+    bsrc[j] = p.W + (size_t)min(n0 + r, p.N - 1) * p.K + c * 8;
+  }
+  auto issue = [&](int kt, int buf) {
+    char* sa = smem + buf * STAGE;
+    char* sb = sa + A_BYTES;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      __builtin_amdgcn_global_load_lds((gptr_t)(asrc[j] + kt * BK), (lds_ptr_t)(sa + (wid * 4 + j) * 1024), 16, 0, 0);
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      __builtin_amdgcn_global_load_lds((gptr_t)(bsrc[j] + kt * BK), (lds_ptr_t)(sb + (wid * 4 + j) * 1024), 16, 0, 0);
+  };
+
+  f32x4_t acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = p.K / BK;
+  issue(0, 0);
+  for (int kt = 0; kt < nk; ++kt) {
+    __syncthreads();  // vmcnt(0) + barrier: stage kt landed for every wave; stage kt-1 fully read
+    const char* sa = smem + (kt & 1) * STAGE;
+    const char* sb = sa + A_BYTES;
+    bf16x8_t af[2][8], bfr[2][4];
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const int c = kk * 4 + fg;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int r = wm * TM + i * 16 + fr;
+        af[kk][i] = *(const bf16x8_t*)(sa + r * 128 + ((c ^ swz(r)) << 4));
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int r = wn * TN + j * 16 + fr;
+        bfr[kk][j] = *(const bf16x8_t*)(sb + r * 128 + ((c ^ swz(r)) << 4));
+      }
+    }
+    if (kt + 1 < nk) issue(kt + 1, (kt + 1) & 1);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(af[kk][i], bfr[kk][j], acc[i][j]);
+  }
+  __syncthreads();
+
+  // ---- epilogue: registers -> (bias / GELU / SwiGLU) -> bf16 staging -> coalesced stores ----
+  char* st = smem + wid * TM * SROW;
+  const int row0 = m0 + wm * TM, col0 = n0 + wn * TN;
+  if constexpr (EPI == EPI_SWIGLU) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int pq = 0; pq < 2; ++pq)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const float v = silu(acc[i][2 * pq][q]) * acc[i][2 * pq + 1][q];
+          *(bf16_t*)(st + (i * 16 + fg * 4 + q) * SROW + (pq * 16 + fr) * 2) = f2bf(v);
+        }
+  } else {
+    float bv[4] = {0.f, 0.f, 0.f, 0.f};
+    if (p.bias) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int gc = col0 + j * 16 + fr;
+        bv[j] = gc < p.N ? bf2f(p.bias[gc]) : 0.f;
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          float v = acc[i][j][q] + bv[j];
+          if constexpr (EPI == EPI_GELU) v = gelu_erf(v);
+          *(bf16_t*)(st + (i * 16 + fg * 4 + q) * SROW + (j * 16 + fr) * 2) = f2bf(v);
+        }
+  }
+  __syncthreads();
+  constexpr int OC = (EPI == EPI_SWIGLU) ? TN / 2 : TN;  // output columns of this wave
+  constexpr int CPR = OC / 8;                            // 16-B chunks per staged row
+  constexpr int RPI = 64 / CPR;
+  const int cc = (lane % CPR) * 8;
+  const int gcol = ((EPI == EPI_SWIGLU) ? col0 / 2 : col0) + cc;
+  const int ncols = (EPI == EPI_SWIGLU) ? p.N / 2 : p.N;
+  for (int rr = lane / CPR; rr < TM; rr += RPI) {
+    const int gm = row0 + rr;
+    if (gm >= p.M || gcol >= ncols) continue;
+    u32x4_t v = *(const u32x4_t*)(st + rr * SROW + cc * 2);
+    if constexpr (EPI == EPI_RESID) {
+      const u32x4_t r = *(const u32x4_t*)(p.resid + (size_t)gm * p.ldr + gcol);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float lo = bf2f((bf16_t)(v[e] & 0xffff)) + bf2f((bf16_t)(r[e] & 0xffff));
+        const float hi = bf2f((bf16_t)(v[e] >> 16)) + bf2f((bf16_t)(r[e] >> 16));
+        v[e] = pack_bf2(lo, hi);
+      }
+    }
+    *(u32x4_t*)(p.C + (size_t)gm * p.ldc + gcol) = v;
+  }
+}
+
+int launch_gemm256(const GemmArgs& a, int epi, hipStream_t s) {
+  const int ntm = (a.M + BM - 1) / BM, ntn = (a.N + BN - 1) / BN;
+  dim3 grid(ntm * ntn), block(512);
+  switch (epi) {
+    case EPI_NONE: gemm256_kernel<EPI_NONE><<<grid, block, 0, s>>>(a); break;
+    case EPI_BIAS: gemm256_kernel<EPI_BIAS><<<grid, block, 0, s>>>(a); break;
+    case EPI_GELU: gemm256_kernel<EPI_GELU><<<grid, block, 0, s>>>(a); break;
+    case EPI_SWIGLU: gemm256_kernel<EPI_SWIGLU><<<grid, block, 0, s>>>(a); break;
+    case EPI_RESID: gemm256_kernel<EPI_RESID><<<grid, block, 0, s>>>(a); break;
+    default: return (int)hipErrorInvalidValue;
+  }
+  return (int)hipGetLastError();
+}

@@ -1,0 +1,86 @@
+"""Engine server process: ``python -m docagents_amd.services engine [--listen tcp://0.0.0.0:9090]``.
+
+Multi-GPU: ``python -m torch.distributed.run --nproc-per-node 8 --master-addr 127.0.0.1 -m
+docagents_amd.services engine``. One process per GPU; RCCL ("nccl" backend) carries the data-plane
+collectives over xGMI, a gloo group carries the small control messages. Rank 0 serves the RPCs.
+
+  TP_SIZE=1 (default)  data parallel: embeddings / generations split across ranks, index sharded
+  TP_SIZE=world        the decoder is tensor-parallel across all ranks (Llama-3-70B class); every
+                       rank runs every generation on its shard, index still sharded
+Index snapshot: ``--snapshot PATH`` restores each rank's shard on start and saves on SIGTERM.
+"""
+from __future__ import annotations
+
+import argparse
+import asyncio
+import os
+import signal
+
+import torch
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser("engine")
+    ap.add_argument("--listen", default=os.environ.get("ENGINE_LISTEN", "tcp://0.0.0.0:9090"))
+    ap.add_argument("--snapshot", default=os.environ.get("INDEX_SNAPSHOT", ""))
+    a = ap.parse_args(argv)
+
+    from ..config import load
+    from ..engine.engine import Engine
+    from ..engine.server import EngineGroup, EngineServer
+    from ..models.llama import TPContext
+    from ..parallel.dist import init_from_env
+    from ..utils.log import new as new_logger
+
+    cfg = load()
+    log = new_logger(cfg.log_level)
+    info = init_from_env()
+    ctrl = data = None
+    tp = None
+    if info.world > 1:
+        import torch.distributed as dist
+        ctrl = dist.new_group(backend="gloo")
+        data = dist.group.WORLD
+        if cfg.tp_size > 1:
+            if cfg.tp_size != info.world:
+                raise SystemExit("TP_SIZE must be 1 or the world size")
+            tp = TPContext(info.rank, info.world, data)
+    dev = info.device
+    eng = Engine(cfg.embed_arch, cfg.llm_arch, dev, seed=cfg.seed, tp=tp, max_batch=cfg.max_batch,
+                 temperature=cfg.temperature, max_new_tokens=cfg.max_new_tokens,
+                 summary_max_new=cfg.summary_max_new_tokens, index_kind=cfg.index_kind, ivf_lists=cfg.ivf_lists,
+                 ivf_probes=cfg.ivf_probes, max_seq=4096 if dev.type == "cuda" else 1024)
+    grp = EngineGroup(eng, info.rank, info.world, ctrl, data)
+    grp.tensor_parallel = tp is not None
+    if a.snapshot and os.path.exists(f"{a.snapshot}.shard{info.rank}"):
+        from ..index.snapshot import load_index
+        n = load_index(eng.index, f"{a.snapshot}.shard{info.rank}")
+        log.info("restored index shard", "rank", info.rank, "rows", n)
+    if info.rank != 0:
+        grp.follower_loop()
+        return 0
+
+    async def serve():
+        srv = EngineServer(grp, log, max_batch_items=cfg.max_batch * 4)
+        server = await srv.start(a.listen)
+        log.info("engine listening", "addr", a.listen, "world", info.world, "device", str(dev),
+                 "encoder", cfg.embed_arch, "decoder", cfg.llm_arch, "tp", cfg.tp_size)
+        stop = asyncio.Event()
+        loop = asyncio.get_running_loop()
+        for sgn in (signal.SIGINT, signal.SIGTERM):
+            try:
+                loop.add_signal_handler(sgn, stop.set)
+            except (NotImplementedError, RuntimeError):
+                pass
+        await stop.wait()
+        server.close()
+        if a.snapshot:
+            await srv._gpu("snapshot", {"path": a.snapshot})
+            log.info("index snapshot saved", "path", a.snapshot)
+        if info.world > 1:
+            grp._bcast(("shutdown", {}))
+
+    asyncio.run(serve())
+    if torch.distributed.is_initialized():
+        torch.distributed.destroy_process_group()
+    return 0

@@ -59,6 +59,20 @@ def test_gemm_swiglu(M, F, splits):
     _close(got, ref, atol=0.03)
 
 
+@pytest.mark.parametrize("M,N,Kd", [(256, 256, 64), (300, 520, 192), (1000, 1032, 768), (2048, 3072, 3072)])
+@pytest.mark.parametrize("epi", [K.EPI_NONE, K.EPI_BIAS, K.EPI_GELU, K.EPI_RESID, K.EPI_SWIGLU])
+def test_gemm256_tile(M, N, Kd, epi):
+    torch.manual_seed(M + N + epi)
+    if epi == K.EPI_SWIGLU:
+        N = (N // 32) * 32
+    a, w = _rand(M, Kd), _rand(N, Kd, scale=Kd ** -0.5)
+    bias = _rand(N) if epi in (K.EPI_BIAS, K.EPI_GELU, K.EPI_RESID) else None
+    resid = _rand(M, N) if epi == K.EPI_RESID else None
+    got = K.gemm(a, w, bias=bias, epi=epi, resid=resid, tile=4, splits=1)
+    ref = R.gemm(a, w, bias=bias, epi=epi, resid=resid)
+    _close(got, ref, atol=0.04)
+
+
 def test_gemm_strided_a():
     big = _rand(50, 3 * 256)
     a = big[:, 256:512]
