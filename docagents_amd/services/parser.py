@@ -30,3 +30,16 @@ def make_handler(deps):
         payload = json.loads(task.payload or b"{}")
         await handle_parse(deps, payload, task.trace_id)
     return handler
+
+
+def make_failure_hook(deps):
+    """A parse task that exhausted its retries marks the document 'failed' (the reference leaves
+    it 'processing' forever)."""
+    async def on_fail(task: Task, err):
+        try:
+            doc_id = json.loads(task.payload or b"{}").get("document_id")
+            if doc_id:
+                await deps.store.update_document_status(str(uuid.UUID(doc_id)), "failed")
+        except Exception:  # noqa: BLE001
+            pass
+    return on_fail

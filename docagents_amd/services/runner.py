@@ -63,7 +63,8 @@ async def run_worker_service(name: str):
     stop = await _stop_event()
     deps.log.info(f"{name} worker starting")
     if name == "parser":
-        worker = deps.queue.worker("parse", parser.make_handler(deps), stop)
+        worker = deps.queue.worker("parse", parser.make_handler(deps), stop,
+                                   on_permanent_failure=parser.make_failure_hook(deps))
     else:
         await startup_sweep(deps)
         worker = deps.queue.worker("analyze", analysis.make_handler(deps), stop,
@@ -134,7 +135,8 @@ async def run_all():
     await asyncio.gather(
         _serve_http(gateway.build_app(deps), cfg.port),
         _serve_http(query.build_app(deps), qport),
-        deps.queue.worker("parse", parser.make_handler(deps), stop),
+        deps.queue.worker("parse", parser.make_handler(deps), stop,
+                          on_permanent_failure=parser.make_failure_hook(deps)),
         deps.queue.worker("analyze", analysis.make_handler(deps), stop,
                           on_permanent_failure=analysis.make_failure_hook(deps)),
     )

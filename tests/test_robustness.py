@@ -1,0 +1,130 @@
+"""Robustness: many concurrent uploads through competing parser/analysis workers (every document
+processed exactly once, chunks never duplicated by a retried parse), injected faults
+(DA_FAULT sites) recovered by the retry machinery, and permanent failure -> status 'failed'
+(the reference leaves such documents 'processing' forever)."""
+import asyncio
+import datetime as dt
+import json
+import uuid
+
+from docagents_amd.app import Deps
+from docagents_amd.config import Config
+from docagents_amd.providers import StubEmbedder, StubLLM
+from docagents_amd.queue import inproc as inproc_mod
+from docagents_amd.queue.inproc import InProcBus, InProcQueue
+from docagents_amd.queue.task import TASK_PARSE, Task
+from docagents_amd.services import analysis, parser
+from docagents_amd.store.sqlite_store import CompositeStore, SqliteMeta
+from docagents_amd.store.sqlite_vectors import SqliteVectors
+from docagents_amd.utils import faults
+from docagents_amd.utils.log import discard
+
+
+def _fast_retry(t, now=None):
+    t.attempts += 1
+    if t.max_attempts == 0:
+        t.max_attempts = 5
+    if t.attempts < t.max_attempts:
+        t.not_before = dt.datetime.now(dt.timezone.utc) + dt.timedelta(milliseconds=2)
+        return t
+    return None
+
+
+def _stack(tmp_path):
+    meta = SqliteMeta(str(tmp_path / "m.sqlite3"))
+    store = CompositeStore(meta, SqliteVectors(meta), min_similarity=-1.0)
+    bus = InProcBus()
+    d = Deps(Config(), discard(), store=store, queue=InProcQueue(bus, discard()), llm=StubLLM(),
+             embedder=StubEmbedder(32))
+    return d, bus
+
+
+async def _run_workers(d, bus, n_workers, stop):
+    ws = []
+    for _ in range(n_workers):
+        qp = InProcQueue(bus, discard())
+        qa = InProcQueue(bus, discard())
+        ws.append(asyncio.ensure_future(qp.worker("parse", parser.make_handler(d), stop,
+                                                  on_permanent_failure=parser.make_failure_hook(d))))
+        ws.append(asyncio.ensure_future(qa.worker("analyze", analysis.make_handler(d), stop,
+                                                  on_permanent_failure=analysis.make_failure_hook(d))))
+    return ws
+
+
+def test_concurrent_uploads_exactly_once_with_faults(tmp_path, monkeypatch):
+    monkeypatch.setattr(inproc_mod, "next_retry", _fast_retry)
+    faults.configure({"handler.parse": 0.3, "handler.analyze": 0.3, "store.save_chunks": 0.2})
+    try:
+        async def go():
+            d, bus = _stack(tmp_path)
+            stop = asyncio.Event()
+            ws = await _run_workers(d, bus, 3, stop)
+            docs = []
+            for i in range(40):
+                doc = await d.store.create_document(f"f{i}.txt")
+                docs.append(doc.id)
+                body = json.dumps({"document_id": doc.id, "filename": f"f{i}.txt",
+                                   "content": " ".join(f"w{i}_{j}" for j in range(900))}).encode()
+                await d.queue.enqueue(Task(type=TASK_PARSE, payload=body))
+            for _ in range(400):
+                st = [(await d.store.get_document(x)).status for x in docs]
+                if all(s != "processing" for s in st):
+                    break
+                await asyncio.sleep(0.05)
+            stop.set()
+            await asyncio.gather(*ws)
+            return d, docs, st
+        d, docs, statuses = asyncio.run(go())
+    finally:
+        faults.configure(None)
+
+    async def check():
+        n_ready = 0
+        for x, s in zip(docs, statuses):
+            chunks = await d.store.list_chunks(x)
+            if s == "ready":
+                n_ready += 1
+                assert [c.index for c in chunks] == [0, 1, 2]  # 900 words -> 3 chunks, never duplicated
+            else:
+                assert s == "failed"
+        return n_ready
+    n_ready = asyncio.run(check())
+    assert n_ready >= 36  # with 30% fault rates and 5 attempts almost every document succeeds
+
+
+def test_permanent_failure_marks_document_failed(tmp_path, monkeypatch):
+    monkeypatch.setattr(inproc_mod, "next_retry", _fast_retry)
+    faults.configure({"handler.analyze": 100})  # fail the first 100 calls
+    try:
+        async def go():
+            d, bus = _stack(tmp_path)
+            stop = asyncio.Event()
+            ws = await _run_workers(d, bus, 1, stop)
+            doc = await d.store.create_document("x.txt")
+            await d.queue.enqueue(Task(type=TASK_PARSE, payload=json.dumps(
+                {"document_id": doc.id, "filename": "x.txt", "content": "a b c"}).encode()))
+            for _ in range(200):
+                if (await d.store.get_document(doc.id)).status == "failed":
+                    break
+                await asyncio.sleep(0.02)
+            stop.set()
+            await asyncio.gather(*ws)
+            return (await d.store.get_document(doc.id)).status
+        assert asyncio.run(go()) == "failed"
+    finally:
+        faults.configure(None)
+
+
+def test_fault_spec_parsing():
+    faults.configure("queue.enqueue:2,cache.get:0")
+    try:
+        n = 0
+        for _ in range(5):
+            try:
+                faults.maybe_fail("queue.enqueue")
+            except faults.InjectedFault:
+                n += 1
+        assert n == 2
+        faults.maybe_fail("cache.get")
+    finally:
+        faults.configure(None)
