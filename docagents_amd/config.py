@@ -67,6 +67,11 @@ class Config:
     max_batch: int = field(default=64, metadata={"env": "ENGINE_MAX_BATCH"})
     kv_cache_gb: float = field(default=0.0, metadata={"env": "KV_CACHE_GB"})  # 0 -> auto
     fault_spec: str = field(default="", metadata={"env": "DA_FAULT"})
+    # --- new keys: engine supervision / observability ---
+    engine_step_timeout: float = field(default=300.0, metadata={"env": "ENGINE_STEP_TIMEOUT"})
+    engine_hard_timeout: float = field(default=0.0, metadata={"env": "ENGINE_HARD_TIMEOUT"})  # 0 -> never exit
+    engine_liveness_s: float = field(default=30.0, metadata={"env": "ENGINE_LIVENESS_INTERVAL"})
+    engine_metrics_port: int = field(default=0, metadata={"env": "ENGINE_METRICS_PORT"})  # 0 -> off
 
     def database_url(self) -> str:
         """config.go:56-64 (kept for parity; the sqlite store uses db_path)."""

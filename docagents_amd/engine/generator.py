@@ -50,7 +50,8 @@ class Generator:
         self.cache = model.cache
         self.dummy_slot = self.cache.acquire(1)[0]
         self.states: dict[tuple, DecodeState] = {}
-        self.stats = {"prefill_s": 0.0, "decode_s": 0.0, "prefill_tokens": 0, "decode_steps": 0, "calls": 0}
+        self.stats = {"prefill_s": 0.0, "decode_s": 0.0, "prefill_tokens": 0, "decode_steps": 0, "decode_tokens": 0,
+                      "calls": 0}
         if self.is_cuda:
             from ..ops import kernels
             c = model.cfg
@@ -180,4 +181,5 @@ class Generator:
             toks = [t for t in toks if t not in self.eos]
             cnt = float(conf[b, 1])
             res.append(GenResult(toks, float(conf[b, 0] / cnt) if cnt > 0 else 1.0, int(cnt)))
+            self.stats["decode_tokens"] += int(cnt)
         return res

@@ -22,7 +22,8 @@ import traceback
 import numpy as np
 import torch
 
-from ..utils import faults
+from ..utils import faults, metrics
+from .observe import StepProfiler, Watchdog, device_memory
 from .rpc import pack, parse_url, read_frame
 
 
@@ -51,7 +52,9 @@ class EngineGroup:
             return [obj]
         import torch.distributed as dist
         out = [None] * self.world
+        t0 = time.perf_counter()
         dist.all_gather_object(out, obj, group=self.ctrl_group)
+        metrics.ENGINE_COLLECTIVE.labels("all_gather_object").inc(time.perf_counter() - t0)
         return out
 
     def run(self, cmd: str, args: dict):
@@ -151,8 +154,10 @@ class EngineGroup:
         gid = e.index.gather_ids(rows)
         S = torch.empty((self.world * Q, k), dtype=s.dtype, device=dev)
         G = torch.empty((self.world * Q, k), dtype=gid.dtype, device=dev)
+        t1 = time.perf_counter()
         dist.all_gather_into_tensor(S, s.contiguous(), group=self.data_group)    # C1
         dist.all_gather_into_tensor(G, gid.contiguous(), group=self.data_group)
+        metrics.ENGINE_COLLECTIVE.labels("search_all_gather").inc(time.perf_counter() - t1)
         flatS = S.view(self.world, Q, k).permute(1, 0, 2).reshape(Q, -1)
         flatG = G.view(self.world, Q, k).permute(1, 0, 2).reshape(Q, -1)
         flatS = torch.where(flatG >= 0, flatS, torch.full_like(flatS, float("-inf")))
@@ -167,17 +172,68 @@ class EngineServer:
 
     BATCHED = ("embed", "answer", "summarize")
 
-    def __init__(self, group: EngineGroup, log, max_batch_items: int = 256):
+    def __init__(self, group: EngineGroup, log, max_batch_items: int = 256, step_timeout_s: float = 300.0,
+                 hard_timeout_s: float = 0.0, liveness_s: float = 30.0, profiler: StepProfiler | None = None):
         self.group, self.log = group, log
         self.gpu = cf.ThreadPoolExecutor(max_workers=1, thread_name_prefix="gpu")
         self.queues: dict[str, asyncio.Queue] = {}
         self.max_batch_items = max_batch_items
         self.stats = {m: {"batches": 0, "items": 0, "busy_s": 0.0} for m in self.BATCHED}
         self.server = None
+        self.watchdog = Watchdog(step_timeout_s, hard_timeout_s, log)
+        self.profiler = profiler or StepProfiler(rank=group.rank)
+        self.liveness_s = liveness_s
+        self.live_ranks = group.world
+        self._busy = 0
+        self._tok = {"prefill": 0, "decode": 0}
+
+    def _run_step(self, cmd, args):
+        """Executed on the GPU thread: watchdog + optional torch.profiler + step metrics."""
+        self.watchdog.begin(cmd)
+        t0 = time.perf_counter()
+        try:
+            return self.profiler.run(cmd, self.group.run, cmd, args)
+        finally:
+            metrics.ENGINE_STEP.labels(cmd).observe(time.perf_counter() - t0)
+            self.watchdog.end()
+            self._account(cmd)
+
+    def _account(self, cmd):
+        e = self.group.engine
+        if cmd in ("answer", "summarize") and getattr(e, "gen", None) is not None:
+            st = e.gen.stats
+            for ph, key in (("prefill", "prefill_tokens"), ("decode", "decode_tokens")):
+                v = int(st.get(key, 0))
+                if v > self._tok[ph]:
+                    metrics.ENGINE_TOKENS.labels(ph).inc(v - self._tok[ph])
+                    self._tok[ph] = v
+        elif cmd in ("index_add", "index_remove", "restore", "stats"):
+            metrics.ENGINE_INDEX_ROWS.labels(str(self.group.rank)).set(len(e.index))
+            for k, v in device_memory(getattr(e, "device", None)).items():
+                metrics.ENGINE_HBM.labels(str(self.group.rank), k).set(v)
 
     async def _gpu(self, cmd, args):
+        if not self.watchdog.healthy and cmd not in ("stats", "ping"):
+            raise RuntimeError(f"engine unhealthy: step {self.watchdog.stuck!r} exceeded the watchdog timeout")
         loop = asyncio.get_running_loop()
-        return await loop.run_in_executor(self.gpu, self.group.run, cmd, args)
+        self._busy += 1
+        try:
+            return await loop.run_in_executor(self.gpu, self._run_step, cmd, args)
+        finally:
+            self._busy -= 1
+
+    async def _liveness_loop(self):
+        """C7: periodic rank-liveness all-reduce while idle (a dead follower hangs it -> watchdog)."""
+        while True:
+            await asyncio.sleep(self.liveness_s)
+            if self._busy or self.group.world == 1:
+                continue
+            try:
+                ranks = await self._gpu("ping", {})
+                self.live_ranks = len(ranks)
+                metrics.ENGINE_LIVE_RANKS.set(self.live_ranks)
+            except Exception as e:  # noqa: BLE001
+                self.log.error("engine liveness check failed", "err", repr(e))
 
     async def _batcher(self, method: str):
         q = self.queues[method]
@@ -201,6 +257,9 @@ class EngineServer:
                 st["batches"] += 1
                 st["items"] += len(items)
                 st["busy_s"] += time.perf_counter() - t0
+                metrics.ENGINE_BATCHES.labels(method).inc()
+                metrics.ENGINE_ITEMS.labels(method).inc(len(items))
+                metrics.ENGINE_BATCH_SIZE.labels(method).observe(len(items))
                 o = 0
                 for its, fut, _ in reqs:
                     if not fut.done():
@@ -237,7 +296,7 @@ class EngineServer:
             st = await self._gpu("stats", {})
             return {"ranks": st, "batching": self.stats}
         if method == "health":
-            return {"ok": True}
+            return dict(self.watchdog.state(), live_ranks=self.live_ranks, world=self.group.world)
         raise ValueError(f"unknown method {method!r}")
 
     async def _client(self, reader, writer):
@@ -271,6 +330,9 @@ class EngineServer:
         for m in ("embed", "answer", "summarize"):
             asyncio.ensure_future(self._batcher(m))
         self.queues_raw_task = asyncio.ensure_future(self._batcher_raw())
+        self.watchdog.start()
+        if self.liveness_s > 0 and self.group.world > 1:
+            self.liveness_task = asyncio.ensure_future(self._liveness_loop())
         kind, addr = parse_url(url)
         if kind == "unix":
             self.server = await asyncio.start_unix_server(self._client, path=addr)

@@ -153,6 +153,192 @@ flash_attn_varlen_kernel(const bf16_t* __restrict__ q, const bf16_t* __restrict_
 }
 
 // ------------------------------------------------------------------------------------------
+// flash_attn_v2: 32x32x16 MFMA, 4 waves x 32 queries (128 queries per workgroup), 64-key tiles
+// double-buffered in LDS with register staging (tile t+1's global loads are in flight while tile t
+// is computed; one barrier per tile).
+//   S^T[key][q] = K·Q^T : A = K rows from LDS (16-B pad per row -> conflict-free ds_read_b128),
+//                         B = Q^T from registers (loaded once per wave).
+//   lane l owns query l&31; its 32 keys of a 64-key tile sit in the two S^T accumulators, the
+//   other 32 in lane l^32 -> row max / row sum need ONE v_permlane32_swap each.
+//   O^T[d][q] += V^T·P^T : B = P^T straight from the S^T registers (k index permuted), A = V^T
+//                         fetched from the row-major V tile with ds_read_b64_tr_b16 (hardware
+//                         transpose; row stride chosen so the 4-row x 2-group reads are
+//                         bank-conflict-free).
+//   scale·log2(e) is folded into the exp2 argument (one FMA per score); the O rescale is skipped
+//   when no lane's running max moved; causal tiles past a wave's last query are skipped by that
+//   wave (it still stages tiles and joins the barrier).
+template <int D>
+struct FA2Cfg {
+  static constexpr int KT = 64, QW = 32, QB = 128;
+  static constexpr int KSTR = D * 2 + 16;                                         // bytes
+  static constexpr int VSTR = (D == 64) ? 192 : (D == 128) ? 320 : D * 2;         // bytes
+  static constexpr int KBUF = KT * KSTR, VBUF = KT * VSTR;
+  static constexpr int CPR = D / 8, LPT = KT * CPR / 256;
+  static constexpr int SMEM = 2 * (KBUF + VBUF);
+};
+
+template <int D>
+__global__ void __launch_bounds__(256, 2)
+flash_attn_v2_kernel(const bf16_t* __restrict__ q, const bf16_t* __restrict__ k, const bf16_t* __restrict__ v,
+                     int ldq, int ldk, int ldv, const int* __restrict__ cu, int H, int Hkv, int causal,
+                     float c, bf16_t* __restrict__ o, int ldo) {
+  using C = FA2Cfg<D>;
+  constexpr int KT = C::KT, NDS = D / 16, NDB = D / 32, CPR = C::CPR, LPT = C::LPT;
+  static_assert(LPT * 256 == KT * CPR, "tile chunks must split evenly over 256 threads");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int b = blockIdx.z, h = blockIdx.y;
+  const int s0 = cu[b], L = cu[b + 1] - s0;
+  const int q0 = blockIdx.x * C::QB;
+  if (q0 >= L) return;
+  const int hk = h / (H / Hkv);
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int qr = lane & 31, hi = lane >> 5;
+  const int wq0 = q0 + wid * C::QW;
+  const int qi = wq0 + qr;
+  const bool qvalid = qi < L;
+
+  bf16x8_t qf[NDS];
+#pragma unroll
+  for (int ds = 0; ds < NDS; ++ds) {
+    if (qvalid) qf[ds] = *(const bf16x8_t*)(q + (size_t)(s0 + qi) * ldq + h * D + ds * 16 + hi * 8);
+    else qf[ds] = bf16x8_t{0, 0, 0, 0, 0, 0, 0, 0};
+  }
+  f32x16_t oacc[NDB];
+#pragma unroll
+  for (int i = 0; i < NDB; ++i)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) oacc[i][r] = 0.f;
+  float m_run = -INFINITY, l_part = 0.f;
+
+  const int kv_end = causal ? min(L, q0 + C::QB) : L;
+  const int wave_end = causal ? min(L, wq0 + C::QW) : L;
+  const int ntiles = (kv_end + KT - 1) / KT;
+
+  const bf16_t* kbase_p = k + (size_t)s0 * ldk + hk * D;
+  const bf16_t* vbase_p = v + (size_t)s0 * ldv + hk * D;
+  u32x4_t kst[LPT], vst[LPT];
+  auto load_tile = [&](int t) {
+#pragma unroll
+    for (int i = 0; i < LPT; ++i) {
+      const int idx = tid + 256 * i, r = idx / CPR, cc = idx % CPR, key = t * KT + r;
+      if (key < L) {
+        kst[i] = *(const u32x4_t*)(kbase_p + (size_t)key * ldk + cc * 8);
+        vst[i] = *(const u32x4_t*)(vbase_p + (size_t)key * ldv + cc * 8);
+      } else {
+        kst[i] = u32x4_t{0, 0, 0, 0};
+        vst[i] = u32x4_t{0, 0, 0, 0};
+      }
+    }
+  };
+  auto store_tile = [&](int buf) {
+    char* sK = smem + buf * (C::KBUF + C::VBUF);
+    char* sV = sK + C::KBUF;
+#pragma unroll
+    for (int i = 0; i < LPT; ++i) {
+      const int idx = tid + 256 * i, r = idx / CPR, cc = idx % CPR;
+      *(u32x4_t*)(sK + r * C::KSTR + cc * 16) = kst[i];
+      *(u32x4_t*)(sV + r * C::VSTR + cc * 16) = vst[i];
+    }
+  };
+
+  load_tile(0);
+  store_tile(0);
+  __syncthreads();
+
+  for (int t = 0; t < ntiles; ++t) {
+    const int cur = t & 1;
+    if (t + 1 < ntiles) load_tile(t + 1);
+    const int kb = t * KT;
+    if (kb < wave_end) {
+      const char* sK = smem + cur * (C::KBUF + C::VBUF);
+      const char* sV = sK + C::KBUF;
+      f32x16_t sacc[2];
+#pragma unroll
+      for (int hh = 0; hh < 2; ++hh) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) sacc[hh][r] = 0.f;
+#pragma unroll
+        for (int ds = 0; ds < NDS; ++ds) {
+          const bf16x8_t a = *(const bf16x8_t*)(sK + (hh * 32 + qr) * C::KSTR + ds * 32 + hi * 16);
+          sacc[hh] = mfma32(a, qf[ds], sacc[hh]);
+        }
+      }
+      if (kb + KT > L || (causal && kb + KT - 1 > wq0)) {
+#pragma unroll
+        for (int hh = 0; hh < 2; ++hh)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int key = kb + hh * 32 + 8 * (r >> 2) + 4 * hi + (r & 3);
+            if (key >= L || (causal && key > qi)) sacc[hh][r] = -INFINITY;
+          }
+      }
+      float mx = sacc[0][0];
+#pragma unroll
+      for (int r = 1; r < 16; ++r) mx = fmaxf(mx, sacc[0][r]);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) mx = fmaxf(mx, sacc[1][r]);
+      mx = max_xhalf(mx);
+      const float m_new = fmaxf(m_run, mx);
+      const float m_use = (m_new == -INFINITY) ? 0.f : m_new;
+      if (__any(m_new > m_run)) {
+        const float alpha = exp2f((m_run - m_use) * c);
+        l_part *= alpha;
+#pragma unroll
+        for (int i = 0; i < NDB; ++i) oacc[i] *= alpha;
+      }
+      m_run = m_new;
+      const float mc = -m_use * c;
+      float psum = 0.f;
+#pragma unroll
+      for (int hh = 0; hh < 2; ++hh)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float p = __builtin_amdgcn_exp2f(fmaf(sacc[hh][r], c, mc));  // raw v_exp_f32
+          sacc[hh][r] = p;
+          psum += p;
+        }
+      l_part += psum;
+
+      // O^T += V^T P^T over 4 k-steps of 16 keys: slot (hi, j) -> key 16kc + 8(j>>2) + 4hi + (j&3)
+#pragma unroll
+      for (int kc = 0; kc < 4; ++kc) {
+        const int hh = kc >> 1, cb = (kc & 1) * 8;
+        const u32x4_t pw = u32x4_t{pack_bf2(sacc[hh][cb], sacc[hh][cb + 1]), pack_bf2(sacc[hh][cb + 2], sacc[hh][cb + 3]),
+                                   pack_bf2(sacc[hh][cb + 4], sacc[hh][cb + 5]), pack_bf2(sacc[hh][cb + 6], sacc[hh][cb + 7])};
+        const bf16x8_t pb = __builtin_bit_cast(bf16x8_t, pw);
+        const int g = lane >> 4, li = lane & 15;
+        const int row0 = kc * 16 + 4 * (g >> 1) + (li >> 2);
+#pragma unroll
+        for (int db = 0; db < NDB; ++db) {
+          const int col = db * 32 + 16 * (g & 1) + 4 * (li & 3);
+          const s16x4_t lo = lds_read_tr16(sV + row0 * C::VSTR + col * 2);
+          const s16x4_t hi8 = lds_read_tr16(sV + (row0 + 8) * C::VSTR + col * 2);
+          const bf16x8_t va = bf16x8_t{lo[0], lo[1], lo[2], lo[3], hi8[0], hi8[1], hi8[2], hi8[3]};
+          oacc[db] = mfma32(va, pb, oacc[db]);
+        }
+      }
+    }
+    if (t + 1 < ntiles) store_tile(cur ^ 1);
+    __syncthreads();
+  }
+
+  const float l_tot = sum_xhalf(l_part);
+  const float inv = l_tot > 0.f ? 1.f / l_tot : 0.f;
+  if (qvalid) {
+    bf16_t* orow = o + (size_t)(s0 + qi) * ldo + h * D;
+#pragma unroll
+    for (int db = 0; db < NDB; ++db)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int d = db * 32 + 8 * g + 4 * hi;
+        *(u32x2_t*)(orow + d) = u32x2_t{pack_bf2(oacc[db][4 * g] * inv, oacc[db][4 * g + 1] * inv),
+                                        pack_bf2(oacc[db][4 * g + 2] * inv, oacc[db][4 * g + 3] * inv)};
+      }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
 // Decode attention: q [B, ldq] (head h at h*D), caches [slots, Hkv, max_seq, D],
 // lens[b] = tokens in cache for b (current token included), slot[b] = cache slot of b.
 // Partials: po [B, H, nsplit, D] fp32 (unnormalised, relative to pm), pm/pl [B, H, nsplit].
@@ -364,6 +550,7 @@ DA_EXPORT int da_flash_attn_varlen(const void* q, const void* k, const void* v, 
 #define FA_ARGS (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, ldq, ldk, ldv, (const int*)cu_seqlens, H, Hkv, \
                 causal, sl2e, (bf16_t*)o, ldo
   switch (D) {
+    case 32: flash_attn_varlen_kernel<32><<<grid, 256, 0, s>>>(FA_ARGS); break;
     case 64: flash_attn_varlen_kernel<64><<<grid, 256, 0, s>>>(FA_ARGS); break;
     case 96: flash_attn_varlen_kernel<96><<<grid, 256, 0, s>>>(FA_ARGS); break;
     case 128: flash_attn_varlen_kernel<128><<<grid, 256, 0, s>>>(FA_ARGS); break;
@@ -423,5 +610,32 @@ DA_EXPORT int da_decode_attn(const void* q, int ldq, const void* k_cache, const 
     case 96: decode_combine_kernel<96><<<cgrid, 128, 0, s>>>(po, pm, pl, H, nsplit, (bf16_t*)o, ldo); break;
     case 128: decode_combine_kernel<128><<<cgrid, 128, 0, s>>>(po, pm, pl, H, nsplit, (bf16_t*)o, ldo); break;
   }
+  DA_LAUNCH_CHECK();
+}
+
+DA_EXPORT int da_flash_attn_v2(const void* q, const void* k, const void* v, int ldq, int ldk, int ldv,
+                               const void* cu_seqlens, int B, int max_seqlen, int H, int Hkv, int D, int causal,
+                               float scale, void* o, int ldo, void* stream) {
+  if (H % Hkv || ldq % 8 || ldk % 8 || ldv % 8 || ldo % 4) return (int)hipErrorInvalidValue;
+  if (B == 0 || max_seqlen == 0) return 0;
+  dim3 grid((max_seqlen + 127) / 128, H, B);
+  const float sl2e = scale * 1.4426950408889634f;
+  hipStream_t s = (hipStream_t)stream;
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute((const void*)flash_attn_v2_kernel<128>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                        FA2Cfg<128>::SMEM);
+    attr_set = true;
+  }
+#define FA_ARGS (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, ldq, ldk, ldv, (const int*)cu_seqlens, H, Hkv, \
+                causal, sl2e, (bf16_t*)o, ldo
+  switch (D) {
+    case 32: flash_attn_v2_kernel<32><<<grid, 256, FA2Cfg<32>::SMEM, s>>>(FA_ARGS); break;
+    case 64: flash_attn_v2_kernel<64><<<grid, 256, FA2Cfg<64>::SMEM, s>>>(FA_ARGS); break;
+    case 96: flash_attn_v2_kernel<96><<<grid, 256, FA2Cfg<96>::SMEM, s>>>(FA_ARGS); break;
+    case 128: flash_attn_v2_kernel<128><<<grid, 256, FA2Cfg<128>::SMEM, s>>>(FA_ARGS); break;
+    default: return (int)hipErrorInvalidValue;
+  }
+#undef FA_ARGS
   DA_LAUNCH_CHECK();
 }

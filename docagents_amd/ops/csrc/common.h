@@ -4,6 +4,8 @@
 // operand layouts documented in /opt/skills/guides/cdna_hip_programming.md §3:
 //   mfma_f32_16x16x32_bf16:  A lane l -> A[l&15][8*(l>>4)+j],  B lane l -> B[8*(l>>4)+j][l&15]
 //                            C lane l -> C[4*(l>>4)+i][l&15]   (i = 0..3)
+//   mfma_f32_32x32x16_bf16:  A lane l -> A[l&31][8*(l>>5)+j],  B lane l -> B[8*(l>>5)+j][l&31]
+//                            C lane l, reg r -> C[8*(r>>2)+4*(l>>5)+(r&3)][l&31]   (r = 0..15)
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -18,6 +20,8 @@
 
 typedef __attribute__((ext_vector_type(8))) short bf16x8_t;   // 8 bf16 = one MFMA A/B fragment
 typedef __attribute__((ext_vector_type(4))) float f32x4_t;    // 16x16 accumulator fragment
+typedef __attribute__((ext_vector_type(16))) float f32x16_t;  // 32x32 accumulator fragment
+typedef __attribute__((ext_vector_type(4))) short s16x4_t;    // ds_read_b64_tr_b16 result
 typedef __attribute__((ext_vector_type(4))) unsigned u32x4_t; // 16-byte vector memory op
 typedef __attribute__((ext_vector_type(2))) unsigned u32x2_t;
 
@@ -27,20 +31,42 @@ __device__ __forceinline__ float bf2f(bf16_t v) {
   return __uint_as_float(((unsigned)v) << 16);
 }
 
-// Round-to-nearest-even f32 -> bf16; NaN kept NaN.
+// f32 -> bf16, round-to-nearest-even (NaN stays NaN): gfx950 has a hardware conversion
+// (v_cvt_pk_bf16_f32, two values per instruction), which clang emits for __bf16 casts.
+typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2_hw_t;
+
 __device__ __forceinline__ bf16_t f2bf(float f) {
-  unsigned u = __float_as_uint(f);
-  if ((u & 0x7fffffffu) > 0x7f800000u) return (bf16_t)((u >> 16) | 0x40);
-  u += 0x7fffu + ((u >> 16) & 1u);
-  return (bf16_t)(u >> 16);
+  return __builtin_bit_cast(bf16_t, (__bf16)f);
 }
 
 __device__ __forceinline__ unsigned pack_bf2(float lo, float hi) {
-  return (unsigned)f2bf(lo) | ((unsigned)f2bf(hi) << 16);
+  const bf16x2_hw_t r = {(__bf16)lo, (__bf16)hi};
+  return __builtin_bit_cast(unsigned, r);
 }
 
 __device__ __forceinline__ f32x4_t mfma16(const bf16x8_t& a, const bf16x8_t& b, const f32x4_t& c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ f32x16_t mfma32(const bf16x8_t& a, const bf16x8_t& b, const f32x16_t& c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
+// Exchange with lane l^32 (v_permlane32_swap, a VALU op — no LDS crossbar). Returns {own, partner}
+// in some order, so callers combine both halves symmetrically (max / sum).
+__device__ __forceinline__ float max_xhalf(float x) {
+  auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+__device__ __forceinline__ float sum_xhalf(float x) {
+  auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+
+// gfx950 ds_read_b64_tr_b16: per 16-lane group, lane 4q+p addresses row q / columns 4p..4p+3 of a
+// 4x16 block of 16-bit values; lane i receives column i (row q in element q).
+__device__ __forceinline__ s16x4_t lds_read_tr16(const void* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4_t*)(p));
 }
 
 __device__ __forceinline__ float wave_sum(float v) {

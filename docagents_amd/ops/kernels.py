@@ -38,6 +38,8 @@ _SIGS = {
                  + [c_int] * 5 + [c_void_p],
     "da_flash_attn_varlen": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_int,
                              c_int, c_int, c_int, c_int, c_float, c_void_p, c_int, c_void_p],
+    "da_flash_attn_v2": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_int,
+                             c_int, c_int, c_int, c_int, c_float, c_void_p, c_int, c_void_p],
     "da_decode_attn": [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
                        c_int, c_int, c_int, c_float, c_void_p, c_void_p, c_int, c_void_p],
     "da_topk_dense": [c_void_p, c_int, c_int, c_void_p, c_void_p, c_int, c_void_p, c_int, c_float, c_int,
@@ -267,23 +269,27 @@ def rope_cache(qkv, pos, cos_sin, H, Hkv, D, slot=None, k_cache=None, v_cache=No
     return qkv
 
 
+FLASH_IMPL = "v2"  # "v1" (16x16 MFMA, 64 queries/workgroup) kept for A/B measurements
+
+
 def flash_attn_varlen(q, k, v, cu_seqlens, max_seqlen: int, H: int, Hkv: int, D: int, causal: bool,
-                      scale: float | None = None, out=None):
+                      scale: float | None = None, out=None, impl: str | None = None):
     """q/k/v: 2-D [T, *] views with head h at columns h*D (strided views into a packed qkv are fine)."""
     for t, n in ((q, "q"), (k, "k"), (v, "v")):
         _bf16_cuda(t, n)
         _req(t.dim() == 2 and t.stride(1) == 1 and t.stride(0) % 8 == 0 and t.data_ptr() % 16 == 0, f"{n} layout")
     _i32(cu_seqlens, "cu_seqlens")
-    _req(D in (64, 96, 128), f"head dim {D} unsupported")
+    _req(D in (32, 64, 96, 128), f"head dim {D} unsupported")
     _req(H % Hkv == 0, "H % Hkv")
     T = q.shape[0]
     if out is None:
         out = torch.empty((T, H * D), dtype=torch.bfloat16, device=q.device)
     scale = scale if scale is not None else 1.0 / math.sqrt(D)
     B = cu_seqlens.numel() - 1
-    _check(lib().da_flash_attn_varlen(_ptr(q), _ptr(k), _ptr(v), q.stride(0), k.stride(0), v.stride(0),
-                                      _ptr(cu_seqlens), B, int(max_seqlen), H, Hkv, D, int(causal), float(scale),
-                                      _ptr(out), out.stride(0), _stream()), "flash_attn_varlen")
+    fn = lib().da_flash_attn_v2 if (impl or FLASH_IMPL) == "v2" else lib().da_flash_attn_varlen
+    _check(fn(_ptr(q), _ptr(k), _ptr(v), q.stride(0), k.stride(0), v.stride(0),
+              _ptr(cu_seqlens), B, int(max_seqlen), H, Hkv, D, int(causal), float(scale),
+              _ptr(out), out.stride(0), _stream()), "flash_attn_varlen")
     return out
 
 

@@ -14,9 +14,10 @@ from __future__ import annotations
 import asyncio
 import datetime as dt
 import itertools
+import time
 from collections import defaultdict
 
-from ..utils import faults
+from ..utils import faults, metrics
 from .task import Handler, Task, group_for, next_retry, prepare_for_publish, subject_for
 
 
@@ -71,11 +72,15 @@ async def run_task(q, task: Task, handler: Handler, log, on_permanent_failure=No
         delay = (task.not_before - dt.datetime.now(dt.timezone.utc)).total_seconds()
         if delay > 0:
             await asyncio.sleep(delay)
+    t0 = time.perf_counter()
     try:
         faults.maybe_fail(f"handler.{task.type}")
         await handler(task)
+        metrics.TASKS.labels(task.type, "ok").inc()
+        metrics.TASK_ATTEMPTS.labels(task.type).observe(task.attempts + 1)
     except Exception as err:  # noqa: BLE001
         nxt = next_retry(task)
+        metrics.TASKS.labels(task.type, "retry" if nxt is not None else "permanent_failure").inc()
         if nxt is not None:
             try:
                 await q.enqueue(nxt)
@@ -89,6 +94,8 @@ async def run_task(q, task: Task, handler: Handler, log, on_permanent_failure=No
                     await on_permanent_failure(task, err)
                 except Exception as e3:  # noqa: BLE001
                     log.error("permanent-failure hook failed", "err", e3)
+    finally:
+        metrics.TASK_SECONDS.labels(task.type).observe(time.perf_counter() - t0)
 
 
 class InProcQueue:

@@ -61,7 +61,12 @@ def main(argv=None) -> int:
         return 0
 
     async def serve():
-        srv = EngineServer(grp, log, max_batch_items=cfg.max_batch * 4)
+        srv = EngineServer(grp, log, max_batch_items=cfg.max_batch * 4, step_timeout_s=cfg.engine_step_timeout,
+                           hard_timeout_s=cfg.engine_hard_timeout, liveness_s=cfg.engine_liveness_s)
+        if cfg.engine_metrics_port:
+            import prometheus_client
+            prometheus_client.start_http_server(cfg.engine_metrics_port)
+            log.info("engine metrics listening", "port", cfg.engine_metrics_port)
         server = await srv.start(a.listen)
         log.info("engine listening", "addr", a.listen, "world", info.world, "device", str(dev),
                  "encoder", cfg.embed_arch, "decoder", cfg.llm_arch, "tp", cfg.tp_size)

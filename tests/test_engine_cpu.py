@@ -126,3 +126,73 @@ def test_engine_rpc_server_microbatching(eng):
         await cl.close()
         srv.server.close()
     asyncio.run(go())
+
+
+def test_engine_health_and_metrics(eng):
+    from prometheus_client import generate_latest
+
+    from docagents_amd.engine.rpc import EngineClient
+    from docagents_amd.engine.server import EngineGroup, EngineServer
+    from docagents_amd.utils.log import discard
+
+    async def go():
+        srv = EngineServer(EngineGroup(eng), discard())
+        port = _port()
+        await srv.start(f"tcp://127.0.0.1:{port}")
+        cl = await EngineClient(f"tcp://127.0.0.1:{port}").connect()
+        await cl.call("embed", texts=["x y z"], preprocess=True)
+        await cl.call("answer", items=[{"question": "q?", "context": "c", "quality": 1.0}])
+        await cl.call("stats")
+        h = await cl.call("health")
+        assert h["ok"] is True and h["steps"] >= 3 and h["world"] == 1
+        await cl.close()
+        srv.server.close()
+    asyncio.run(go())
+    text = generate_latest().decode()
+    for name in ("da_engine_step_seconds", "da_engine_batches_total", "da_engine_tokens_total",
+                 "da_engine_index_rows"):
+        assert name in text, name
+
+
+def test_watchdog_flags_and_recovers():
+    from docagents_amd.engine.observe import Watchdog
+    hard = []
+    w = Watchdog(soft_s=5.0, hard_s=10.0, on_hard=lambda c, e: hard.append(c))
+    w.begin("answer")
+    t0 = w._cur[1]
+    w.check(t0 + 1.0)
+    assert w.healthy
+    w.check(t0 + 6.0)
+    assert not w.healthy and w.state()["stuck"] == "answer" and not hard
+    w.check(t0 + 11.0)
+    assert hard == ["answer"]
+    w.end()
+    assert w.healthy and w.steps == 1
+
+
+def test_unhealthy_engine_fails_fast(eng):
+    from docagents_amd.engine.server import EngineGroup, EngineServer
+    from docagents_amd.utils.log import discard
+
+    async def go():
+        srv = EngineServer(EngineGroup(eng), discard())
+        srv.watchdog.stuck = "answer"
+        try:
+            await srv._gpu("embed", {"texts": ["a"]})
+        except RuntimeError as e:
+            assert "unhealthy" in str(e)
+        else:
+            raise AssertionError("expected fail-fast")
+        assert (await srv._gpu("ping", {})) == [0]
+    asyncio.run(go())
+
+
+def test_step_profiler_writes_trace(tmp_path):
+    from docagents_amd.engine.observe import StepProfiler
+    p = StepProfiler(f"{tmp_path}:1")
+    import torch
+    assert p.run("embed", lambda a: torch.ones(8).sum() + a, 1) == 9
+    assert not p.active
+    files = sorted(x.name for x in tmp_path.iterdir())
+    assert files == ["rank0_001_embed.json", "rank0_001_embed.txt"]
+    assert p.run("embed", lambda: 3) == 3  # exhausted -> passthrough

@@ -138,7 +138,7 @@ def test_rope_cache(H, Hkv, D):
     _close(vc1, vc2, atol=0)
 
 
-@pytest.mark.parametrize("D", [64, 96, 128])
+@pytest.mark.parametrize("D", [32, 64, 96, 128])
 @pytest.mark.parametrize("causal,H,Hkv", [(False, 4, 4), (True, 8, 2), (True, 4, 4)])
 def test_flash_attn(D, causal, H, Hkv):
     torch.manual_seed(D + H)
