@@ -72,6 +72,8 @@ class Config:
     engine_hard_timeout: float = field(default=0.0, metadata={"env": "ENGINE_HARD_TIMEOUT"})  # 0 -> never exit
     engine_liveness_s: float = field(default=30.0, metadata={"env": "ENGINE_LIVENESS_INTERVAL"})
     engine_metrics_port: int = field(default=0, metadata={"env": "ENGINE_METRICS_PORT"})  # 0 -> off
+    engine_continuous: bool = field(default=True, metadata={"env": "ENGINE_CONTINUOUS"})
+    engine_cb_steps: int = field(default=8, metadata={"env": "ENGINE_CB_STEPS"})
 
     def database_url(self) -> str:
         """config.go:56-64 (kept for parity; the sqlite store uses db_path)."""
@@ -105,6 +107,11 @@ def load(environ: dict | None = None) -> Config:
                 val = int(raw)
             elif f.type in ("float", float):
                 val = float(raw)
+            elif f.type in ("bool", bool):  # caarlos0/env uses strconv.ParseBool
+                lo = raw.strip().lower()
+                if lo not in ("1", "t", "true", "0", "f", "false"):
+                    raise ValueError(f"invalid bool {raw!r}")
+                val = lo in ("1", "t", "true")
             else:
                 val = raw
         except ValueError as e:

@@ -139,6 +139,27 @@ class Engine:
             out.append((self.chat.decode(r.tokens), float(quality) * r.mean_prob))
         return out
 
+    # ------------------------------------------------------------------ continuous batching
+    @property
+    def scheduler(self):
+        """Lazily built ContinuousScheduler sharing this engine's generator and KV cache."""
+        if getattr(self, "_sched", None) is None:
+            from .generator import ContinuousScheduler
+            self._sched = ContinuousScheduler(self.gen, B=self.gen.max_batch,
+                                              max_new_cap=max(self.max_new_tokens, self.summary_max_new))
+        return self._sched
+
+    def cb_tick(self, new_items, steps: int | None = None):
+        """Submit [(tag, (question, chunk_ids, quality))] and run one scheduler tick.
+        Returns ([(tag, answer, confidence)], still_busy)."""
+        sch = self.scheduler
+        for tag, (q, ch, quality) in new_items:
+            sch.submit(self.answer_prompt_ids(q, ch, self.max_new_tokens), self.max_new_tokens, (tag, quality))
+        with self.lock:
+            done = sch.tick(steps)
+        out = [(tag, self.chat.decode(r.tokens), float(quality) * r.mean_prob) for (tag, quality), r in done]
+        return out, sch.busy()
+
     def answer_text(self, question: str, context: str, quality: float, max_new: int | None = None):
         """Answer(ctx, question, contextText, contextQuality) with an untokenized context string."""
         max_new = max_new or self.max_new_tokens

@@ -9,8 +9,10 @@ every few steps. The reference's equivalent is one OpenAI chat call per request
 """
 from __future__ import annotations
 
+import collections
 import math
 import time
+from types import SimpleNamespace
 
 import numpy as np
 import torch
@@ -183,3 +185,158 @@ class Generator:
             res.append(GenResult(toks, float(conf[b, 0] / cnt) if cnt > 0 else 1.0, int(cnt)))
             self.stats["decode_tokens"] += int(cnt)
         return res
+
+
+class ContinuousScheduler:
+    """Continuous batching over one HIP-graph-captured decode bucket of ``B`` rows.
+
+    Requests are admitted into free rows between decode chunks (prefill of the new prompts runs
+    as one packed varlen batch, then their rows join the running graph), and a row is reaped and
+    reused as soon as its sequence hits EOS or its token budget — so a short answer never waits
+    for the longest one in its batch, and requests arriving mid-generation do not wait for the
+    whole batch to drain (SURVEY.md §2.5 "continuous batching for the decoder"; the reference
+    makes one blocking OpenAI call per request, internal/llm/openai.go:64-105).
+
+    Per-row token budgets share one history buffer of ``max_new_cap`` columns: a row with budget m
+    starts writing at column cap - m (``start`` shifted back), so the sampler's "history full"
+    stop fires after exactly m tokens with no kernel change. Free rows point at the generator's
+    dummy KV slot and stay inactive (the sampler never advances them).
+
+    Not thread-safe: ``submit`` and ``tick`` are called from the engine's single GPU thread.
+    """
+
+    def __init__(self, gen: "Generator", B: int | None = None, max_new_cap: int = 256, chunk_steps: int = 8,
+                 max_admit_tokens: int | None = None):
+        self.gen, self.m = gen, gen.model
+        self.B = B or gen.max_batch
+        self.cap = max(1, max_new_cap)
+        self.chunk_steps = chunk_steps
+        self.max_admit_tokens = max_admit_tokens or gen.max_prefill_tokens
+        self.st = DecodeState(self.m, self.B, self.cap, gen.temperature, gen.seed, gen.eos)
+        self.rows: list = [None] * self.B        # row -> (tag, slot, budget)
+        self.pending: collections.deque = collections.deque()
+        self._reset_rows(list(range(self.B)))
+        self.stats = {"admitted": 0, "finished": 0, "ticks": 0, "steps": 0}
+
+    # -------------------------------------------------------------------------------- public
+    def submit(self, prompt: list[int], max_new: int, tag=None):
+        max_new = max(1, min(int(max_new), self.cap))
+        if not prompt:
+            raise ValueError("empty prompt")
+        if len(prompt) + max_new > self.gen.cache.max_seq:
+            raise ValueError(f"prompt of {len(prompt)} tokens + {max_new} new exceeds the context "
+                             f"({self.gen.cache.max_seq})")
+        self.pending.append((list(prompt), max_new, tag))
+
+    def busy(self) -> bool:
+        return bool(self.pending) or any(r is not None for r in self.rows)
+
+    @property
+    def n_active(self) -> int:
+        return sum(r is not None for r in self.rows)
+
+    def tick(self, steps: int | None = None) -> list:
+        """Admit what fits, run ``steps`` decode steps, return [(tag, GenResult)] of finished rows."""
+        self.stats["ticks"] += 1
+        done = self._admit()
+        if self.n_active:
+            st, k = self.st, steps or self.chunk_steps
+            if self.gen.use_graphs and st.graph is None:
+                self.gen._capture(st)
+            t0 = time.perf_counter()
+            for _ in range(k):
+                if st.graph is not None:
+                    st.graph.replay()
+                else:
+                    self.m.decode_step(st)
+            self.stats["steps"] += k
+            self.gen.stats["decode_steps"] += k
+            done += self._reap()
+            self.gen.stats["decode_s"] += time.perf_counter() - t0
+        return done
+
+    def run_all(self, prompts, max_new: int) -> list["GenResult"]:
+        """Convenience: submit everything and tick until drained (results in submission order)."""
+        for i, p in enumerate(prompts):
+            self.submit(p, max_new, i)
+        out: dict = {}
+        while self.busy():
+            for tag, r in self.tick():
+                out[tag] = r
+        return [out[i] for i in range(len(prompts))]
+
+    # -------------------------------------------------------------------------------- internals
+    def _reset_rows(self, rows):
+        if not rows:
+            return
+        st, dev = self.st, self.m.device
+        idx = torch.as_tensor(rows, dtype=torch.long, device=dev)
+        st.slot.index_fill_(0, idx, self.gen.dummy_slot)
+        st.pos.index_fill_(0, idx, 0)
+        st.lens.index_fill_(0, idx, 1)
+        st.active.index_fill_(0, idx, 0)
+        st.start.index_fill_(0, idx, 0)
+
+    def _admit(self) -> list:
+        free = [i for i, r in enumerate(self.rows) if r is None]
+        take, tot = [], 0
+        while self.pending and len(take) < len(free):
+            p = self.pending[0]
+            if take and tot + len(p[0]) > self.max_admit_tokens:
+                break
+            take.append(self.pending.popleft())
+            tot += len(p[0])
+        if not take:
+            return []
+        n, rows = len(take), free[:len(take)]
+        slots = self.gen.cache.acquire(n)
+        prompts = [t[0] for t in take]
+        plen = np.asarray([len(p) for p in prompts], dtype=np.int32)
+        budget = np.asarray([t[1] for t in take], dtype=np.int32)
+        dev, i32 = self.m.device, dict(dtype=torch.int32, device=self.m.device)
+        tmp = SimpleNamespace(
+            tokens=torch.zeros(n, **i32), lp=torch.zeros(n, dtype=torch.float32, device=dev),
+            conf=torch.zeros(n, 2, dtype=torch.float32, device=dev), active=torch.ones(n, **i32),
+            pos=torch.from_numpy(plen - 1).to(dev), lens=torch.from_numpy(plen.copy()).to(dev),
+            hist=torch.full((n, self.cap), -1, **i32),
+            start=torch.from_numpy(plen - 1 - (self.cap - budget)).to(dev),
+            slot=torch.as_tensor(slots, dtype=torch.int32, device=dev))
+        self.gen._prefill_into(tmp, prompts, slots, 0)
+        st = self.st
+        idx = torch.as_tensor(rows, dtype=torch.long, device=dev)
+        for name in ("tokens", "lp", "conf", "active", "pos", "lens", "hist", "start", "slot"):
+            getattr(st, name).index_copy_(0, idx, getattr(tmp, name))
+        for r, (p, b, tag), sl in zip(rows, take, slots):
+            self.rows[r] = (tag, sl, int(b))
+        self.stats["admitted"] += n
+        # a budget of one token (or an immediate EOS) finishes at prefill
+        return self._reap(rows)
+
+    def _reap(self, rows=None) -> list:
+        rows = [i for i, r in enumerate(self.rows) if r is not None] if rows is None else rows
+        if not rows:
+            return []
+        st = self.st
+        act = st.active.cpu().numpy()
+        fin = [r for r in rows if self.rows[r] is not None and act[r] == 0]
+        if not fin:
+            return []
+        idx = torch.as_tensor(fin, dtype=torch.long, device=self.m.device)
+        hist = st.hist.index_select(0, idx).cpu().numpy()
+        conf = st.conf.index_select(0, idx).cpu().numpy()
+        out, slots = [], []
+        eos = set(self.gen.eos)
+        for k, r in enumerate(fin):
+            tag, sl, b = self.rows[r]
+            toks = [int(t) for t in hist[k, self.cap - b:] if t >= 0 and int(t) not in eos]
+            cnt = float(conf[k, 1])
+            out.append((tag, GenResult(toks, float(conf[k, 0] / cnt) if cnt > 0 else 1.0, int(cnt))))
+            self.gen.stats["decode_tokens"] += int(cnt)
+            self.rows[r] = None
+            slots.append(sl)
+        self._reset_rows(fin)
+        st.hist.index_fill_(0, idx, -1)
+        st.conf.index_fill_(0, idx, 0.0)
+        self.gen.cache.release(slots)
+        self.stats["finished"] += len(fin)
+        return out

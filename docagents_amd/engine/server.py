@@ -97,14 +97,7 @@ class EngineGroup:
             if cmd == "summarize":
                 res = e.summarize_many(mine) if mine else []
             else:
-                batch = []
-                for it in mine:
-                    if it.get("chunks") is not None:
-                        ids = [(c["tokens"].tolist() if c.get("tokens") is not None else e._ids(c["text"]))
-                               for c in it["chunks"]]
-                    else:
-                        ids = [e._ids(it.get("context", ""))] if it.get("context") else []
-                    batch.append((it["question"], ids, it.get("quality", 0.0)))
+                batch = [self._answer_item(it) for it in mine]
                 res = e.answer_many(batch) if batch else []
             if getattr(self, "tensor_parallel", False):
                 return res
@@ -112,6 +105,18 @@ class EngineGroup:
             for r in self._gather(res):
                 out.extend(r)
             return out
+        if cmd == "cb_tick":
+            # continuous batching: TP ranks all run every sequence (identical schedulers); DP
+            # ranks take the new items round-robin by tag and run their own schedulers
+            tp = getattr(self, "tensor_parallel", False)
+            mine = [(t, self._answer_item(it)) for t, it in a["items"] if tp or t % self.world == self.rank]
+            if mine:
+                faults.maybe_fail("engine.generate")
+            done, busy = e.cb_tick(mine, a.get("steps"))
+            if tp or self.world == 1:
+                return done, busy
+            parts = self._gather((done, busy))
+            return [d for p in parts for d in p[0]], any(p[1] for p in parts)
         if cmd == "index_add":
             if owner_of(a["doc_id"], self.world) == self.rank:
                 e.index.add(a["doc_id"], a["keys"], torch.from_numpy(np.ascontiguousarray(a["vecs"], dtype=np.float32)))
@@ -134,6 +139,15 @@ class EngineGroup:
         if cmd == "ping":
             return self._gather(self.rank)
         raise ValueError(f"unknown engine command {cmd!r}")
+
+    def _answer_item(self, it):
+        e = self.engine
+        if it.get("chunks") is not None:
+            ids = [(c["tokens"].tolist() if c.get("tokens") is not None else e._ids(c["text"]))
+                   for c in it["chunks"]]
+        else:
+            ids = [e._ids(it.get("context", ""))] if it.get("context") else []
+        return it["question"], ids, it.get("quality", 0.0)
 
     def _search(self, a):
         e = self.engine
@@ -173,7 +187,8 @@ class EngineServer:
     BATCHED = ("embed", "answer", "summarize")
 
     def __init__(self, group: EngineGroup, log, max_batch_items: int = 256, step_timeout_s: float = 300.0,
-                 hard_timeout_s: float = 0.0, liveness_s: float = 30.0, profiler: StepProfiler | None = None):
+                 hard_timeout_s: float = 0.0, liveness_s: float = 30.0, profiler: StepProfiler | None = None,
+                 continuous: bool = False, cb_steps: int = 8):
         self.group, self.log = group, log
         self.gpu = cf.ThreadPoolExecutor(max_workers=1, thread_name_prefix="gpu")
         self.queues: dict[str, asyncio.Queue] = {}
@@ -186,6 +201,13 @@ class EngineServer:
         self.live_ranks = group.world
         self._busy = 0
         self._tok = {"prefill": 0, "decode": 0}
+        # continuous batching of answers (a decode tick loop instead of whole-batch waves)
+        self.continuous = continuous and getattr(group.engine, "gen", None) is not None
+        self.cb_steps = cb_steps
+        self._cb_new: list = []
+        self._cb_futs: dict = {}
+        self._cb_tag = 0
+        self._cb_wake = asyncio.Event()
 
     def _run_step(self, cmd, args):
         """Executed on the GPU thread: watchdog + optional torch.profiler + step metrics."""
@@ -221,6 +243,48 @@ class EngineServer:
             return await loop.run_in_executor(self.gpu, self._run_step, cmd, args)
         finally:
             self._busy -= 1
+
+    async def _cb_submit(self, items):
+        futs = []
+        loop = asyncio.get_running_loop()
+        for it in items:
+            self._cb_tag += 1
+            f = loop.create_future()
+            self._cb_futs[self._cb_tag] = f
+            self._cb_new.append((self._cb_tag, it))
+            futs.append(f)
+        self._cb_wake.set()
+        return await asyncio.gather(*futs)
+
+    async def _cb_loop(self):
+        """Tick the decode scheduler while it has work; new answers join at the next tick."""
+        busy = False
+        while True:
+            if not busy and not self._cb_new:
+                self._cb_wake.clear()
+                await self._cb_wake.wait()
+            new, self._cb_new = self._cb_new, []
+            t0 = time.perf_counter()
+            try:
+                done, busy = await self._gpu("cb_tick", {"items": new, "steps": self.cb_steps})
+            except Exception as e:  # noqa: BLE001 - fail the requests of this tick, keep serving
+                for tag, _ in new:
+                    f = self._cb_futs.pop(tag, None)
+                    if f is not None and not f.done():
+                        f.set_exception(e)
+                busy = False
+                continue
+            st = self.stats.setdefault("answer_cb", {"ticks": 0, "items": 0, "busy_s": 0.0})
+            st["ticks"] += 1
+            st["items"] += len(done)
+            st["busy_s"] += time.perf_counter() - t0
+            if new:
+                metrics.ENGINE_BATCH_SIZE.labels("answer_cb_admit").observe(len(new))
+            for tag, ans, conf in done:
+                f = self._cb_futs.pop(tag, None)
+                if f is not None and not f.done():
+                    f.set_result((ans, conf))
+            metrics.ENGINE_ITEMS.labels("answer").inc(len(done))
 
     async def _liveness_loop(self):
         """C7: periodic rank-liveness all-reduce while idle (a dead follower hangs it -> watchdog)."""
@@ -285,7 +349,10 @@ class EngineServer:
             res = await self._enqueue("summarize", list(args["texts"]))
             return {"results": [[s, list(kp)] for s, kp in res]}
         if method == "answer":
-            res = await self._enqueue("answer", list(args["items"]))
+            if self.continuous:
+                res = await self._cb_submit(list(args["items"]))
+            else:
+                res = await self._enqueue("answer", list(args["items"]))
             return {"results": [[a, float(c)] for a, c in res]}
         if method == "search":
             s, ids = await self._gpu("search", args)
@@ -331,6 +398,8 @@ class EngineServer:
             asyncio.ensure_future(self._batcher(m))
         self.queues_raw_task = asyncio.ensure_future(self._batcher_raw())
         self.watchdog.start()
+        if self.continuous:
+            self.cb_task = asyncio.ensure_future(self._cb_loop())
         if self.liveness_s > 0 and self.group.world > 1:
             self.liveness_task = asyncio.ensure_future(self._liveness_loop())
         kind, addr = parse_url(url)

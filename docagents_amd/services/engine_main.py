@@ -62,7 +62,8 @@ def main(argv=None) -> int:
 
     async def serve():
         srv = EngineServer(grp, log, max_batch_items=cfg.max_batch * 4, step_timeout_s=cfg.engine_step_timeout,
-                           hard_timeout_s=cfg.engine_hard_timeout, liveness_s=cfg.engine_liveness_s)
+                           hard_timeout_s=cfg.engine_hard_timeout, liveness_s=cfg.engine_liveness_s,
+                           continuous=cfg.engine_continuous, cb_steps=cfg.engine_cb_steps)
         if cfg.engine_metrics_port:
             import prometheus_client
             prometheus_client.start_http_server(cfg.engine_metrics_port)

@@ -196,3 +196,60 @@ def test_step_profiler_writes_trace(tmp_path):
     files = sorted(x.name for x in tmp_path.iterdir())
     assert files == ["rank0_001_embed.json", "rank0_001_embed.txt"]
     assert p.run("embed", lambda: 3) == 3  # exhausted -> passthrough
+
+
+def test_continuous_batching_matches_waves_greedy():
+    from docagents_amd.engine.generator import ContinuousScheduler
+    e = Engine("tiny-enc", "tiny-dec", "cpu", max_batch=4, max_seq=256, max_new_tokens=6, temperature=0.0,
+               use_graphs=False)
+    rng = np.random.default_rng(1)
+    prompts = [list(rng.integers(5, 3000, size=n)) for n in (7, 30, 3, 12, 50, 9)]
+    budgets = [3, 6, 1, 5, 2, 6]
+    want = [e.gen.generate([p], b)[0].tokens for p, b in zip(prompts, budgets)]
+    sched = ContinuousScheduler(e.gen, B=4, max_new_cap=8, chunk_steps=2)
+    got = {}
+    for i in range(2):
+        sched.submit(prompts[i], budgets[i], i)
+    for tag, r in sched.tick():
+        got[tag] = r.tokens
+    for i in range(2, 6):  # arrive mid-generation; more requests than rows -> queueing
+        sched.submit(prompts[i], budgets[i], i)
+    while sched.busy():
+        for tag, r in sched.tick():
+            got[tag] = r.tokens
+    assert [got[i] for i in range(6)] == want
+    assert [len(t) for t in want] == budgets
+    assert sched.stats["admitted"] == sched.stats["finished"] == 6
+    assert len(e.gen.cache.free) == e.gen.cache.slots - 1  # only the dummy slot stays taken
+
+
+def test_engine_server_continuous_batching(eng):
+    from docagents_amd.engine.rpc import EngineClient
+    from docagents_amd.engine.server import EngineGroup, EngineServer
+    from docagents_amd.providers import RemoteLLM
+    from docagents_amd.utils.log import discard
+
+    async def go():
+        srv = EngineServer(EngineGroup(eng), discard(), continuous=True, cb_steps=2)
+        port = _port()
+        await srv.start(f"tcp://127.0.0.1:{port}")
+        cl = await EngineClient(f"tcp://127.0.0.1:{port}").connect()
+        llm = RemoteLLM(cl)
+        # 7 concurrent answers through a 4-row scheduler, plus an embed interleaved between ticks
+        outs = await asyncio.gather(*[llm.answer(f"question {i}?", "context words " * (i + 1), 0.5) for i in range(7)],
+                                    cl.call("embed", texts=["x"], preprocess=True))
+        answers = outs[:7]
+        assert all(isinstance(a, str) and 0 <= c <= 0.5 for a, c in answers)
+        st = srv.stats["answer_cb"]
+        assert st["items"] == 7 and st["ticks"] >= 2
+        assert eng.scheduler.stats["finished"] >= 7 and not eng.scheduler.busy()
+        await cl.close()
+        srv.server.close()
+    asyncio.run(go())
+
+
+def test_config_bool_parsing():
+    from docagents_amd.config import load
+    assert load({"ENGINE_CONTINUOUS": "false"}).engine_continuous is False
+    assert load({"ENGINE_CONTINUOUS": "1"}).engine_continuous is True
+    assert load({"ENGINE_CONTINUOUS": "maybe"}).engine_continuous is True  # parse error -> default
