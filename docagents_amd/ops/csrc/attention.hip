@@ -351,7 +351,7 @@ flash_attn_v2_kernel(const bf16_t* __restrict__ q, const bf16_t* __restrict__ k,
 // The P*V accumulation uses the same flat chunks: lane's dim-slot for chunk i is static given
 // i mod NSET, so accumulators stay in registers. Each of the 4 waves streams its own tiles with its
 // own online softmax (no block barriers in the loop); the waves are merged once at the end.
-template <int D, int G>
+template <int D, int G, int VAR>
 __global__ void __launch_bounds__(256)
 decode_attn_kernel(const bf16_t* __restrict__ q, int ldq, const bf16_t* __restrict__ kc,
                    const bf16_t* __restrict__ vc, const int* __restrict__ lens, const int* __restrict__ slot,
@@ -397,12 +397,26 @@ decode_attn_kernel(const bf16_t* __restrict__ q, int ldq, const bf16_t* __restri
     const bf16_t* kb = kc + cbase + (size_t)t0 * D;
     const bf16_t* vb = vc + cbase + (size_t)t0 * D;
     // K first (V is loaded after the scores: keeps ~100 VGPRs live instead of ~200, so 4-5
-    // waves per SIMD hide the HBM latency instead of 2)
+    // waves per SIMD hide the HBM latency instead of 2). VAR bit0: non-temporal loads (the KV
+    // stream is read once per step); bit1: issue V together with K.
+    constexpr bool NT = VAR & 1, VEARLY = (VAR & 2) != 0;
+    auto ld16 = [&](const bf16_t* p) -> u32x4_t {
+      if constexpr (NT) return __builtin_nontemporal_load((const u32x4_t*)p);
+      else return *(const u32x4_t*)p;
+    };
     u32x4_t kv[CPR];
+    u32x4_t vv[CPR];
 #pragma unroll
     for (int i = 0; i < CPR; ++i) {
       const int c = i * 64 + lane;
-      kv[i] = (c < nk * CPR) ? *(const u32x4_t*)(kb + c * 8) : u32x4_t{0, 0, 0, 0};
+      kv[i] = (c < nk * CPR) ? ld16(kb + c * 8) : u32x4_t{0, 0, 0, 0};
+    }
+    if constexpr (VEARLY) {
+#pragma unroll
+      for (int i = 0; i < CPR; ++i) {
+        const int c = i * 64 + lane;
+        vv[i] = (c < nk * CPR) ? ld16(vb + c * 8) : u32x4_t{0, 0, 0, 0};
+      }
     }
     // ---- scores ----
 #pragma unroll
@@ -463,11 +477,12 @@ decode_attn_kernel(const bf16_t* __restrict__ q, int ldq, const bf16_t* __restri
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     // ---- P * V ----
     asm volatile("" ::: "memory");
-    u32x4_t vv[CPR];
+    if constexpr (!VEARLY) {
 #pragma unroll
-    for (int i = 0; i < CPR; ++i) {
-      const int c = i * 64 + lane;
-      vv[i] = (c < nk * CPR) ? *(const u32x4_t*)(vb + c * 8) : u32x4_t{0, 0, 0, 0};
+      for (int i = 0; i < CPR; ++i) {
+        const int c = i * 64 + lane;
+        vv[i] = (c < nk * CPR) ? ld16(vb + c * 8) : u32x4_t{0, 0, 0, 0};
+      }
     }
 #pragma unroll
     for (int i = 0; i < CPR; ++i) {
@@ -560,12 +575,12 @@ DA_EXPORT int da_flash_attn_varlen(const void* q, const void* k, const void* v, 
   DA_LAUNCH_CHECK();
 }
 
-template <int D>
-static int launch_decode(int G, dim3 grid, hipStream_t s, const bf16_t* q, int ldq, const bf16_t* kc,
-                         const bf16_t* vc, const int* lens, const int* slot, int H, int Hkv, int max_seq, int chunk,
-                         int nsplit, float sl2e, float* po, float* pm, float* pl) {
-#define DEC(GG) decode_attn_kernel<D, GG><<<grid, 256, 0, s>>>(q, ldq, kc, vc, lens, slot, H, Hkv, max_seq, chunk, \
-                                                                nsplit, sl2e, po, pm, pl)
+template <int D, int VAR>
+static int launch_decode_v(int G, dim3 grid, hipStream_t s, const bf16_t* q, int ldq, const bf16_t* kc,
+                           const bf16_t* vc, const int* lens, const int* slot, int H, int Hkv, int max_seq, int chunk,
+                           int nsplit, float sl2e, float* po, float* pm, float* pl) {
+#define DEC(GG) decode_attn_kernel<D, GG, VAR><<<grid, 256, 0, s>>>(q, ldq, kc, vc, lens, slot, H, Hkv, max_seq, \
+                                                                     chunk, nsplit, sl2e, po, pm, pl)
   switch (G) {
     case 1: DEC(1); break;
     case 2: DEC(2); break;
@@ -575,6 +590,18 @@ static int launch_decode(int G, dim3 grid, hipStream_t s, const bf16_t* q, int l
   }
 #undef DEC
   return (int)hipGetLastError();
+}
+
+// Measured on MI355X (profiles/decode_attn_variants_r1.json): non-temporal K/V loads + V issued with
+// K reach 6.5 TB/s for MHA (G = 1, Phi-3); with G >= 2 the extra V registers cost more occupancy
+// than they buy, so those keep V after the scores (nt loads only).
+template <int D>
+static int launch_decode(int G, dim3 grid, hipStream_t s, const bf16_t* q, int ldq, const bf16_t* kc,
+                         const bf16_t* vc, const int* lens, const int* slot, int H, int Hkv, int max_seq, int chunk,
+                         int nsplit, float sl2e, float* po, float* pm, float* pl) {
+  if (G == 1)
+    return launch_decode_v<D, 3>(G, grid, s, q, ldq, kc, vc, lens, slot, H, Hkv, max_seq, chunk, nsplit, sl2e, po, pm, pl);
+  return launch_decode_v<D, 1>(G, grid, s, q, ldq, kc, vc, lens, slot, H, Hkv, max_seq, chunk, nsplit, sl2e, po, pm, pl);
 }
 
 // ws must hold B*H*nsplit*(D+2) floats. chunk = keys per split (multiple of 64).

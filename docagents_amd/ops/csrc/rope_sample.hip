@@ -12,37 +12,44 @@
 
 // qkv: [T, (H + 2*Hkv) * D] row-major (q heads, then k heads, then v heads)
 // k_cache / v_cache: [num_slots, Hkv, max_seq, D]; slot[t], pos[t] give where token t goes.
-__global__ void rope_cache_kernel(bf16_t* __restrict__ qkv, const int* __restrict__ pos,
-                                  const int* __restrict__ slot, const float* __restrict__ cs,
-                                  bf16_t* __restrict__ kc, bf16_t* __restrict__ vc, int H, int Hkv, int D,
-                                  int max_seq, int rotate_q) {
+// One work item per (token, 4 rotary pairs of one head) plus one per (token, 16-B chunk of V):
+// grid (T, ceil(items / 256)) so a decode step's handful of tokens still spreads over many CUs.
+__global__ void __launch_bounds__(256)
+rope_cache_kernel(bf16_t* __restrict__ qkv, const int* __restrict__ pos, const int* __restrict__ slot,
+                  const float* __restrict__ cs, bf16_t* __restrict__ kc, bf16_t* __restrict__ vc, int H, int Hkv,
+                  int D, int max_seq, int rotate_q) {
   const int t = blockIdx.x;
-  const int p = pos[t];
+  const int w = blockIdx.y * blockDim.x + threadIdx.x;
   const int half = D / 2;
-  const int ld = (H + 2 * Hkv) * D;
-  bf16_t* row = qkv + (size_t)t * ld;
-  const float* cst = cs + (size_t)p * half * 2;
   const int groups = half / 4;  // 4 consecutive rotary pairs per work item
   const int nheads = (rotate_q ? H : 0) + Hkv;
+  const int nrot = nheads * groups;
+  const int nv = vc ? Hkv * (D / 8) : 0;
+  if (w >= nrot + nv) return;
+  const int p = pos[t];
+  const int ld = (H + 2 * Hkv) * D;
+  bf16_t* row = qkv + (size_t)t * ld;
   const int s = slot ? slot[t] : 0;
-  for (int w = threadIdx.x; w < nheads * groups; w += blockDim.x) {
+  if (w < nrot) {
     const int hh = w / groups, gq = w % groups;
     const int head = rotate_q ? hh : H + hh;  // head index within q|k region
     bf16_t* hp = row + head * D;
     const int i0 = gq * 4;
-    u32x2_t a = *(const u32x2_t*)(hp + i0);
-    u32x2_t b = *(const u32x2_t*)(hp + half + i0);
-    float x1[4] = {bf2f(a[0] & 0xffff), bf2f(a[0] >> 16), bf2f(a[1] & 0xffff), bf2f(a[1] >> 16)};
-    float x2[4] = {bf2f(b[0] & 0xffff), bf2f(b[0] >> 16), bf2f(b[1] & 0xffff), bf2f(b[1] >> 16)};
+    const u32x2_t a = *(const u32x2_t*)(hp + i0);
+    const u32x2_t b = *(const u32x2_t*)(hp + half + i0);
+    const f32x4_t c01 = *(const f32x4_t*)(cs + ((size_t)p * half + i0) * 2);
+    const f32x4_t c23 = *(const f32x4_t*)(cs + ((size_t)p * half + i0) * 2 + 4);
+    const float cc[4] = {c01[0], c01[2], c23[0], c23[2]}, sn[4] = {c01[1], c01[3], c23[1], c23[3]};
+    const float x1[4] = {bf2f(a[0] & 0xffff), bf2f(a[0] >> 16), bf2f(a[1] & 0xffff), bf2f(a[1] >> 16)};
+    const float x2[4] = {bf2f(b[0] & 0xffff), bf2f(b[0] >> 16), bf2f(b[1] & 0xffff), bf2f(b[1] >> 16)};
     float o1[4], o2[4];
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-      const float c = cst[(i0 + e) * 2], sn = cst[(i0 + e) * 2 + 1];
-      o1[e] = x1[e] * c - x2[e] * sn;
-      o2[e] = x2[e] * c + x1[e] * sn;
+      o1[e] = x1[e] * cc[e] - x2[e] * sn[e];
+      o2[e] = x2[e] * cc[e] + x1[e] * sn[e];
     }
-    u32x2_t ra = u32x2_t{pack_bf2(o1[0], o1[1]), pack_bf2(o1[2], o1[3])};
-    u32x2_t rb = u32x2_t{pack_bf2(o2[0], o2[1]), pack_bf2(o2[2], o2[3])};
+    const u32x2_t ra = u32x2_t{pack_bf2(o1[0], o1[1]), pack_bf2(o1[2], o1[3])};
+    const u32x2_t rb = u32x2_t{pack_bf2(o2[0], o2[1]), pack_bf2(o2[2], o2[3])};
     *(u32x2_t*)(hp + i0) = ra;
     *(u32x2_t*)(hp + half + i0) = rb;
     if (kc && head >= H) {
@@ -51,14 +58,12 @@ __global__ void rope_cache_kernel(bf16_t* __restrict__ qkv, const int* __restric
       *(u32x2_t*)(dst + i0) = ra;
       *(u32x2_t*)(dst + half + i0) = rb;
     }
-  }
-  if (vc) {
+  } else {
+    const int wv = w - nrot;
+    const int hk = wv / (D / 8), c = wv % (D / 8);
     const bf16_t* vrow = row + (H + Hkv) * D;
-    for (int w = threadIdx.x; w < Hkv * D / 8; w += blockDim.x) {
-      const int hk = w / (D / 8), c = w % (D / 8);
-      bf16_t* dst = vc + (((size_t)s * Hkv + hk) * max_seq + p) * D + c * 8;
-      *(u32x4_t*)dst = *(const u32x4_t*)(vrow + hk * D + c * 8);
-    }
+    bf16_t* dst = vc + (((size_t)s * Hkv + hk) * max_seq + p) * D + c * 8;
+    *(u32x4_t*)dst = *(const u32x4_t*)(vrow + hk * D + c * 8);
   }
 }
 
@@ -150,7 +155,9 @@ DA_EXPORT int da_rope_cache(void* qkv, const void* pos, const void* slot, const 
                             void* v_cache, int T, int H, int Hkv, int D, int max_seq, int rotate_q, void* stream) {
   if (D % 8 || (D / 2) % 4) return (int)hipErrorInvalidValue;
   if (T == 0) return 0;
-  rope_cache_kernel<<<T, 256, 0, (hipStream_t)stream>>>((bf16_t*)qkv, (const int*)pos, (const int*)slot,
+  const int items = ((rotate_q ? H : 0) + Hkv) * (D / 8) + (v_cache ? Hkv * (D / 8) : 0);
+  const dim3 grid(T, (items + 255) / 256);
+  rope_cache_kernel<<<grid, 256, 0, (hipStream_t)stream>>>((bf16_t*)qkv, (const int*)pos, (const int*)slot,
                                                          (const float*)cos_sin, (bf16_t*)k_cache,
                                                          (bf16_t*)v_cache, H, Hkv, D, max_seq, rotate_q);
   DA_LAUNCH_CHECK();
