@@ -83,8 +83,7 @@ gemm256_kernel(GemmArgs p) {
     const char* sa = smem + (kt & 1) * STAGE;
     const char* sb = sa + A_BYTES;
     bf16x8_t af[2][8], bfr[2][4];
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
+    auto read_frags = [&](int kk) {
       const int c = kk * 4 + fg;
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
@@ -96,8 +95,16 @@ gemm256_kernel(GemmArgs p) {
         const int r = wn * TN + j * 16 + fr;
         bfr[kk][j] = *(const bf16x8_t*)(sb + r * 128 + ((c ^ swz(r)) << 4));
       }
-    }
-    if (kt + 1 < nk) issue(kt + 1, (kt + 1) & 1);
+    };
+    // DMA for the next stage first (branch-free: the last K-step re-stages tile nk-1 into the idle
+    // buffer), so it gets the whole K-step of MFMAs to land; then all 24 fragment reads, then the
+    // 64 MFMAs (measured on MI355X: ~+3 % over reads-first / compiler-interleaved orders,
+    // profiles/gemm256_sched_variants_r1.txt).
+    issue(min(kt + 1, nk - 1), (kt + 1) & 1);
+    __builtin_amdgcn_sched_barrier(0);
+    read_frags(0);
+    read_frags(1);
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
