@@ -1,0 +1,177 @@
+"""HTTP load generator for the full agent stack (SURVEY.md §7.1 "bench/").
+
+Drives the public API exactly like a client of the reference would (README.md of the reference:
+upload -> poll summary -> query), through the gateway:
+
+  1. ingest: upload ``--docs`` synthetic documents (``--concurrency`` in flight), poll each
+     summary until it is ready -> docs/min from the first upload to the last ready summary;
+  2. cache-miss queries: ``--queries`` unique questions over the ingested documents -> QPS and
+     p50/p99 latency (embed + search + answer inside the stack);
+  3. cache-hit queries: the same questions again -> p50/p99 (served from the query cache; the
+     reference promises "sub-millisecond" server-side, README.md:588).
+
+``--spawn`` starts an all-in-one stack (``python -m docagents_amd.services all``) on a free port
+with the current environment (``LLM_PROVIDER=stub`` on CPU, ``engine`` with ``ENGINE_URL`` set for
+the GPU engine); otherwise ``--gateway URL`` targets a running deployment. Prints one JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import asyncio
+import json
+import os
+import socket
+import statistics
+import subprocess
+import sys
+import time
+
+import httpx
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from docagents_amd.text import multipart  # noqa: E402
+from docagents_amd.text.synthetic import TextGen  # noqa: E402
+
+
+def _pct(xs, q):
+    if not xs:
+        return None
+    xs = sorted(xs)
+    return xs[min(len(xs) - 1, int(round(q / 100.0 * (len(xs) - 1))))]
+
+
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+async def _wait_ready(client, url, timeout=120.0):
+    t0 = time.time()
+    while time.time() - t0 < timeout:
+        try:
+            if (await client.get(url, timeout=2.0)).status_code == 200:
+                return
+        except Exception:  # noqa: BLE001
+            pass
+        await asyncio.sleep(0.2)
+    raise TimeoutError(url)
+
+
+async def run(gw: str, docs: int, words: int, queries: int, concurrency: int, top_k: int, seed: int,
+              poll_s: float = 0.1, ingest_timeout: float = 600.0) -> dict:
+    tg = TextGen(seed=seed)
+    texts = [tg.document(words) for _ in range(docs)]
+    sem = asyncio.Semaphore(concurrency)
+    limits = httpx.Limits(max_connections=concurrency * 2, max_keepalive_connections=concurrency * 2)
+    async with httpx.AsyncClient(timeout=120.0, limits=limits) as client:
+        await _wait_ready(client, gw + "/healthz")
+
+        # ---- ingest ----
+        ids: list[str] = []
+        ready_at: dict[str, float] = {}
+
+        async def upload(i):
+            body, ctype = multipart.build({}, {"file": (f"doc{i}.txt", texts[i].encode(), "text/plain")})
+            async with sem:
+                r = await client.post(gw + "/api/documents/upload", content=body, headers={"content-type": ctype})
+            r.raise_for_status()
+            return r.json()["document_id"]
+
+        t0 = time.perf_counter()
+        ids = list(await asyncio.gather(*[upload(i) for i in range(docs)]))
+
+        async def poll(doc_id):
+            while time.perf_counter() - t0 < ingest_timeout:
+                r = await client.get(f"{gw}/api/documents/{doc_id}/summary")
+                if r.status_code == 200:
+                    ready_at[doc_id] = time.perf_counter()
+                    return True
+                await asyncio.sleep(poll_s)
+            return False
+
+        ok = await asyncio.gather(*[poll(d) for d in ids])
+        t_ingest = (max(ready_at.values()) - t0) if ready_at else None
+        ready = [d for d, o in zip(ids, ok) if o]
+
+        # ---- queries ----
+        qs = [f"What does {tg.word()} say about {tg.word()} and {tg.word()}?" for _ in range(queries)]
+        bodies = []
+        for i, q in enumerate(qs):
+            pick = [ready[(i + j) % len(ready)] for j in range(min(3, len(ready)))] if ready else []
+            bodies.append(json.dumps({"question": q, "document_ids": pick, "top_k": top_k}))
+
+        async def ask(body):
+            async with sem:
+                t = time.perf_counter()
+                r = await client.post(gw + "/api/query", content=body, headers={"content-type": "application/json"})
+                dt = (time.perf_counter() - t) * 1000.0
+            return r.status_code, dt
+
+        t1 = time.perf_counter()
+        miss = await asyncio.gather(*[ask(b) for b in bodies])
+        t_miss = time.perf_counter() - t1
+        hit = []
+        for b in bodies:  # sequential: per-request latency of a cache hit, not throughput
+            hit.append(await ask(b))
+
+    miss_ok = [dt for st, dt in miss if st == 200]
+    hit_ok = [dt for st, dt in hit if st == 200]
+    return {
+        "metric": "http_stack", "docs": docs, "docs_ready": len(ready), "words_per_doc": words,
+        "ingest_docs_per_min": round(len(ready) / t_ingest * 60.0, 1) if t_ingest else None,
+        "queries": queries, "query_errors": sum(1 for st, _ in miss if st != 200),
+        "qa_qps": round(len(miss_ok) / t_miss, 2) if t_miss > 0 else None,
+        "cache_miss_p50_ms": _r(statistics.median(miss_ok) if miss_ok else None),
+        "cache_miss_p99_ms": _r(_pct(miss_ok, 99)),
+        "cache_hit_p50_ms": _r(statistics.median(hit_ok) if hit_ok else None),
+        "cache_hit_p99_ms": _r(_pct(hit_ok, 99)),
+        "concurrency": concurrency, "top_k": top_k,
+    }
+
+
+def _r(x):
+    return None if x is None else round(x, 3)
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser("loadgen")
+    ap.add_argument("--gateway", default="")
+    ap.add_argument("--spawn", action="store_true", help="start `services all` for the run")
+    ap.add_argument("--docs", type=int, default=32)
+    ap.add_argument("--words", type=int, default=2000)
+    ap.add_argument("--queries", type=int, default=64)
+    ap.add_argument("--concurrency", type=int, default=16)
+    ap.add_argument("--top-k", type=int, default=5)
+    ap.add_argument("--seed", type=int, default=7)
+    a = ap.parse_args(argv)
+    proc = None
+    gw = a.gateway
+    if a.spawn or not gw:
+        port = _free_port()
+        root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+        env = dict(os.environ, PORT=str(port),
+                   PYTHONPATH=os.pathsep.join(x for x in (root, os.environ.get("PYTHONPATH", "")) if x))
+        env.setdefault("MIN_SIMILARITY", "-1")
+        env.setdefault("DB_PATH", os.path.join(os.environ.get("TMPDIR", "/tmp"), f"loadgen-{port}.sqlite3"))
+        proc = subprocess.Popen([sys.executable, "-m", "docagents_amd.services", "all"], env=env,
+                                stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
+        gw = f"http://127.0.0.1:{port}"
+    try:
+        out = asyncio.run(run(gw, a.docs, a.words, a.queries, a.concurrency, a.top_k, a.seed))
+    finally:
+        if proc is not None:
+            proc.terminate()
+            try:
+                proc.wait(10)
+            except subprocess.TimeoutExpired:
+                proc.kill()
+    print(json.dumps(out), flush=True)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -133,3 +133,15 @@ def test_pdf_upload_and_errors(stack):
     assert q.status_code == 400 and q.text == "Question must be at least 3; DocumentIDs must be at least 1\n"
     m = httpx.get(gw + "/metrics", timeout=10)
     assert m.status_code == 200 and "da_http_request_seconds" in m.text
+
+
+def test_loadgen_against_spawned_stack(tmp_path):
+    """bench/loadgen.py end to end on CPU with stub models (the same tool drives the GPU stack)."""
+    env = dict(os.environ, LLM_PROVIDER="stub", EMBED_DIM="64", TMPDIR=str(tmp_path), LOG_LEVEL="error")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench", "loadgen.py"), "--spawn", "--docs", "4",
+                        "--words", "500", "--queries", "6", "--concurrency", "3"],
+                       env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-2000:]
+    out = json.loads(r.stdout.strip().splitlines()[-1])
+    assert out["docs_ready"] == 4 and out["query_errors"] == 0
+    assert out["cache_hit_p50_ms"] < out["cache_miss_p99_ms"] + 1000
