@@ -87,16 +87,25 @@ async def build_store(cfg: Config, log: Logger, deps: Deps):
     return CompositeStore(meta, vectors, min_similarity=cfg.min_similarity)
 
 
+def worker_concurrency(cfg: Config) -> int:
+    """Tasks one worker runs at once. The reference handles one message at a time per replica
+    (internal/queue/nats.go:43-45); with the GPU engine behind the agents, concurrent tasks are
+    what lets the engine batch summaries/embeddings across documents, so the default is 32 there."""
+    if cfg.worker_concurrency > 0:
+        return cfg.worker_concurrency
+    return 32 if cfg.llm_provider in ("engine", "openai", "local") else 1
+
+
 async def build_queue(cfg: Config, log: Logger, bus=None):
     p = cfg.queue_provider
     if p == "inproc":
         from .queue.inproc import InProcBus, InProcQueue
-        return InProcQueue(bus or InProcBus(), log)
+        return InProcQueue(bus or InProcBus(), log, concurrency=worker_concurrency(cfg))
     if p in ("broker", "nats"):
         if not cfg.queue_url:
             raise ValueError(f"QUEUE_URL is required when QUEUE_PROVIDER={p}")
         from .queue.broker_client import BrokerQueue
-        q = BrokerQueue(cfg.queue_url, log)
+        q = BrokerQueue(cfg.queue_url, log, concurrency=worker_concurrency(cfg))
         await q.connect()
         log.info("using broker queue", "url", cfg.queue_url)
         return q

@@ -72,6 +72,7 @@ class Config:
     engine_hard_timeout: float = field(default=0.0, metadata={"env": "ENGINE_HARD_TIMEOUT"})  # 0 -> never exit
     engine_liveness_s: float = field(default=30.0, metadata={"env": "ENGINE_LIVENESS_INTERVAL"})
     engine_metrics_port: int = field(default=0, metadata={"env": "ENGINE_METRICS_PORT"})  # 0 -> off
+    worker_concurrency: int = field(default=0, metadata={"env": "WORKER_CONCURRENCY"})  # 0 -> auto
     engine_continuous: bool = field(default=True, metadata={"env": "ENGINE_CONTINUOUS"})
     engine_cb_steps: int = field(default=8, metadata={"env": "ENGINE_CB_STEPS"})
 

@@ -16,7 +16,7 @@ for i in $(seq 1 240); do
 done
 if [ $ok -ne 1 ]; then echo "engine did not start"; tail -30 gpurun_out/stack_engine.log; kill $EPID 2>/dev/null; exit 1; fi
 echo "engine up after ${i}s"
-LLM_PROVIDER=engine ENGINE_URL=tcp://127.0.0.1:19090 timeout -k 10 600 python bench/loadgen.py --spawn --docs 64 --words 2000 --queries 256 --concurrency 64 > gpurun_out/loadgen.json 2> gpurun_out/loadgen.err
+LLM_PROVIDER=engine ENGINE_URL=tcp://127.0.0.1:19090 timeout -k 10 600 python bench/loadgen.py --spawn --docs 128 --words 2000 --queries 256 --concurrency 64 > gpurun_out/loadgen.json 2> gpurun_out/loadgen.err
 rc=$?
 echo "loadgen rc=$rc"; cat gpurun_out/loadgen.json; tail -5 gpurun_out/loadgen.err
 kill $EPID 2>/dev/null
