@@ -32,7 +32,9 @@ def main():
     torch.manual_seed(0)
     res = {}
     for name, B, L, H, Hkv, D in [("phi3_b64", 64, 2944, 32, 32, 96), ("llama3_b64", 64, 4096, 32, 8, 128),
-                                  ("phi3_b32", 32, 2944, 32, 32, 96)]:
+                                  ("phi3_b32", 32, 2944, 32, 32, 96),
+                                  ("llama70b_tp8_b64", 64, 4096, 8, 1, 128), ("llama3_b16_short", 16, 512, 32, 8, 128),
+                                  ("gqa2_d64", 32, 2048, 8, 4, 64)]:
         S = L + 64
         kc = torch.randn(B, Hkv, S, D, device=dev, dtype=torch.bfloat16)
         vc = torch.randn(B, Hkv, S, D, device=dev, dtype=torch.bfloat16)
@@ -40,8 +42,15 @@ def main():
         lens = torch.full((B,), L, device=dev, dtype=torch.int32)
         slot = torch.arange(B, device=dev, dtype=torch.int32)
         by = 2 * B * Hkv * L * D * 2
-        t = timeit(lambda: K.decode_attn(q, kc, vc, lens, slot, H, Hkv, D, max_len=S))
-        r = dict(ms=t, tbps=by / t / 1e9)
+        r = {}
+        outs = []
+        for mf in (0, 1):
+            K.lib().da_set_gqa_mfma(mf)
+            t = timeit(lambda: K.decode_attn(q, kc, vc, lens, slot, H, Hkv, D, max_len=S))
+            outs.append(K.decode_attn(q, kc, vc, lens, slot, H, Hkv, D, max_len=S).float())
+            r[f"mfma{mf}"] = dict(ms=t, tbps=by / t / 1e9)
+        r["maxdiff"] = (outs[0] - outs[1]).abs().max().item()
+        K.lib().da_set_gqa_mfma(1)
         res[f"decode_attn/{name}"] = r
         print(name, json.dumps(r), flush=True)
     # rope + cache write at decode size

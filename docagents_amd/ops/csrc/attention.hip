@@ -535,6 +535,165 @@ decode_attn_kernel(const bf16_t* __restrict__ q, int ldq, const bf16_t* __restri
   }
 }
 
+// ------------------------------------------------------------------------------------------
+// GQA decode attention on MFMA (G = H/Hkv query heads share one KV head: Llama-3-8B G=4,
+// Llama-3-70B at TP=8 G=8). The G queries of a KV head form the N=16 side of
+// v_mfma_f32_16x16x32_bf16 (zero-padded), so K and V are read once per KV head instead of being
+// multiplied against each query on the VALU (the G >= 2 path of decode_attn_kernel is VALU-bound).
+// Per wave and 64-key tile:
+//   S^T[key][g] = K·Q^T : A = K rows straight from HBM into registers (non-temporal 16-B loads),
+//                         B = Q^T (registers, loaded once);
+//   softmax over the 64 keys of each query column: 16 values per lane + two cross-lane steps;
+//   O^T[d][g] += V^T·P^T : B = P^T from the S^T registers (k index permuted), A = V^T read from the
+//                         wave's private LDS copy of the V tile with ds_read_b64_tr_b16. The V tile
+//                         is a contiguous [64 x D] block of the cache, so it is copied by LDS-DMA
+//                         (global_load_lds, 1 KiB per wave-instruction) with an XOR chunk swizzle
+//                         on the source address that makes the transposed reads conflict-free.
+template <int D>
+__device__ __forceinline__ int vswz(int r) {
+  return D == 128 ? ((r & 7) << 1) : (((r >> 1) & 3) << 1);
+}
+
+template <int D, int G>
+__global__ void __launch_bounds__(256)
+decode_attn_gqa_kernel(const bf16_t* __restrict__ q, int ldq, const bf16_t* __restrict__ kc,
+                       const bf16_t* __restrict__ vc, const int* __restrict__ lens, const int* __restrict__ slot,
+                       int H, int Hkv, int max_seq, int chunk, int nsplit, float scale_log2e,
+                       float* __restrict__ po, float* __restrict__ pm, float* __restrict__ pl) {
+  static_assert(D == 64 || D == 128, "GQA MFMA decode supports head dims 64 and 128");
+  constexpr int KT = 64, NDS = D / 32, NDT = D / 16, NS = D / 8;   // d-steps (S), d-tiles (O), 16-B chunks/row
+  constexpr int VBYTES = KT * D * 2, NDMA = VBYTES / 1024;
+  typedef __attribute__((address_space(3))) void* lds_ptr_t;
+  typedef __attribute__((address_space(1))) const void* gptr_t;
+  __shared__ __attribute__((aligned(16))) char sv[4 * VBYTES];
+  __shared__ float swm[4][16], swl[4][16];
+
+  const int split = blockIdx.x, hk = blockIdx.y, b = blockIdx.z;
+  const int L = lens[b];
+  const int kstart = split * chunk;
+  const int kend = min(L, kstart + chunk);
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int fr = lane & 15, fg = lane >> 4;
+  const size_t cbase = ((size_t)slot[b] * Hkv + hk) * (size_t)max_seq * D;
+  char* myv = sv + w * VBYTES;
+
+  bf16x8_t qf[NDS];
+#pragma unroll
+  for (int ds = 0; ds < NDS; ++ds) {
+    if (fr < G) qf[ds] = *(const bf16x8_t*)(q + (size_t)b * ldq + (hk * G + fr) * D + ds * 32 + fg * 8);
+    else qf[ds] = bf16x8_t{0, 0, 0, 0, 0, 0, 0, 0};
+  }
+  f32x4_t oacc[NDT];
+#pragma unroll
+  for (int i = 0; i < NDT; ++i) oacc[i] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  float m_run = -INFINITY, l_part = 0.f;
+
+  for (int t0 = kstart + w * KT; t0 < kend; t0 += 4 * KT) {
+    const int nk = min(KT, kend - t0);
+    const bf16_t* kb = kc + cbase + (size_t)t0 * D;
+    const bf16_t* vb = vc + cbase + (size_t)t0 * D;
+    // ---- K straight to registers (A operand rows = keys), then the V tile by LDS-DMA ----
+    u32x4_t kr[4][NDS];
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int ds = 0; ds < NDS; ++ds) {
+        const int key = min(16 * t + fr, nk - 1);
+        kr[t][ds] = __builtin_nontemporal_load((const u32x4_t*)(kb + (size_t)key * D + ds * 32 + fg * 8));
+      }
+#pragma unroll
+    for (int i = 0; i < NDMA; ++i) {
+      const int P = i * 64 + lane, row = P / NS, sl = P % NS;
+      const int c = sl ^ vswz<D>(row);
+      const int key = min(row, nk - 1);
+      __builtin_amdgcn_global_load_lds((gptr_t)(vb + (size_t)key * D + c * 8), (lds_ptr_t)(myv + i * 1024), 16, 0, 0);
+    }
+    // ---- S^T = K Q^T ----
+    f32x4_t sacc[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      sacc[t] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ds = 0; ds < NDS; ++ds) sacc[t] = mfma16(__builtin_bit_cast(bf16x8_t, kr[t][ds]), qf[ds], sacc[t]);
+    }
+    float mx = -INFINITY;
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int key = 16 * t + 4 * fg + i;
+        const float sc = key < nk ? sacc[t][i] * scale_log2e : -INFINITY;
+        sacc[t][i] = sc;
+        mx = fmaxf(mx, sc);
+      }
+    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+    mx = max_xhalf(mx);
+    const float m_new = fmaxf(m_run, mx);
+    const float m_use = (m_new == -INFINITY) ? 0.f : m_new;
+    const float alpha = exp2f(m_run - m_use);
+    m_run = m_new;
+    float psum = 0.f;
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float p = __builtin_amdgcn_exp2f(sacc[t][i] - m_use);
+        sacc[t][i] = p;
+        psum += p;
+      }
+    l_part = l_part * alpha + psum;
+#pragma unroll
+    for (int i = 0; i < NDT; ++i) oacc[i] *= alpha;
+    // ---- O^T += V^T P^T: k-step c covers keys 32c..32c+31; slot j -> key 32c + 16(j>>2) + 4fg + (j&3) ----
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's V DMA landed (wave-private LDS)
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      const u32x4_t pw = u32x4_t{pack_bf2(sacc[2 * c][0], sacc[2 * c][1]), pack_bf2(sacc[2 * c][2], sacc[2 * c][3]),
+                                 pack_bf2(sacc[2 * c + 1][0], sacc[2 * c + 1][1]),
+                                 pack_bf2(sacc[2 * c + 1][2], sacc[2 * c + 1][3])};
+      const bf16x8_t pb = __builtin_bit_cast(bf16x8_t, pw);
+      const int q4 = fr >> 2, p4 = fr & 3;
+#pragma unroll
+      for (int dt = 0; dt < NDT; ++dt) {
+        const int col = dt * 16 + 4 * p4;                      // 4 columns of this lane's address
+        const int r0 = 32 * c + 4 * fg + q4, r1 = r0 + 16;
+        const s16x4_t lo = lds_read_tr16(myv + r0 * (D * 2) + (((col >> 3) ^ vswz<D>(r0)) << 4) + (col & 7) * 2);
+        const s16x4_t hi = lds_read_tr16(myv + r1 * (D * 2) + (((col >> 3) ^ vswz<D>(r1)) << 4) + (col & 7) * 2);
+        const bf16x8_t va = bf16x8_t{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        oacc[dt] = mfma16(va, pb, oacc[dt]);
+      }
+    }
+    // the next tile's DMA rewrites this wave's V region: finish the tr-reads first
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  }
+  // ---- merge the 4 waves: per-query (m, l) and O^T partials through LDS ----
+  float l_tot = l_part + __shfl_xor(l_part, 16, 64);
+  l_tot = sum_xhalf(l_tot);
+  if (fg == 0) { swm[w][fr] = m_run; swl[w][fr] = l_tot; }
+  __syncthreads();  // every wave is done with its V region
+  float* so = (float*)sv;  // [4][16][D]
+#pragma unroll
+  for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) so[(w * 16 + fr) * D + dt * 16 + 4 * fg + i] = oacc[dt][i];
+  __syncthreads();
+  for (int i = tid; i < G * D; i += 256) {
+    const int g = i / D, d = i % D;
+    const float M = fmaxf(fmaxf(swm[0][g], swm[1][g]), fmaxf(swm[2][g], swm[3][g]));
+    const float Mu = (M == -INFINITY) ? 0.f : M;
+    float o = 0.f, ls = 0.f;
+#pragma unroll
+    for (int ww = 0; ww < 4; ++ww) {
+      const float f = exp2f(swm[ww][g] - Mu);
+      o += so[(ww * 16 + g) * D + d] * f;
+      ls += swl[ww][g] * f;
+    }
+    const size_t pidx = ((size_t)b * H + hk * G + g) * nsplit + split;
+    po[pidx * D + d] = o;
+    if (d == 0) { pm[pidx] = M; pl[pidx] = ls; }
+  }
+}
+
 template <int D>
 __global__ void decode_combine_kernel(const float* __restrict__ po, const float* __restrict__ pm,
                                       const float* __restrict__ pl, int H, int nsplit, bf16_t* __restrict__ o,
@@ -592,6 +751,12 @@ static int launch_decode_v(int G, dim3 grid, hipStream_t s, const bf16_t* q, int
   return (int)hipGetLastError();
 }
 
+// GQA groups (G >= 2) take the MFMA kernel: 1.8x (Llama-3-8B, G=4) to 5x (Llama-3-70B TP=8, G=8)
+// over the VALU path (profiles/decode_attn_gqa_mfma_r1.json). da_set_gqa_mfma(0) selects the VALU
+// path (kept for A/B measurements and as the numerics cross-check in tests).
+static int g_gqa_mfma = 1;
+DA_EXPORT void da_set_gqa_mfma(int v) { g_gqa_mfma = v; }
+
 // Measured on MI355X (profiles/decode_attn_variants_r1.json): non-temporal K/V loads + V issued with
 // K reach 6.5 TB/s for MHA (G = 1, Phi-3); with G >= 2 the extra V registers cost more occupancy
 // than they buy, so those keep V after the scores (nt loads only).
@@ -601,6 +766,17 @@ static int launch_decode(int G, dim3 grid, hipStream_t s, const bf16_t* q, int l
                          int nsplit, float sl2e, float* po, float* pm, float* pl) {
   if (G == 1)
     return launch_decode_v<D, 3>(G, grid, s, q, ldq, kc, vc, lens, slot, H, Hkv, max_seq, chunk, nsplit, sl2e, po, pm, pl);
+  if constexpr (D == 64 || D == 128) {
+    if (g_gqa_mfma) {
+      switch (G) {
+        case 2: decode_attn_gqa_kernel<D, 2><<<grid, 256, 0, s>>>(q, ldq, kc, vc, lens, slot, H, Hkv, max_seq, chunk, nsplit, sl2e, po, pm, pl); break;
+        case 4: decode_attn_gqa_kernel<D, 4><<<grid, 256, 0, s>>>(q, ldq, kc, vc, lens, slot, H, Hkv, max_seq, chunk, nsplit, sl2e, po, pm, pl); break;
+        case 8: decode_attn_gqa_kernel<D, 8><<<grid, 256, 0, s>>>(q, ldq, kc, vc, lens, slot, H, Hkv, max_seq, chunk, nsplit, sl2e, po, pm, pl); break;
+        default: return (int)hipErrorInvalidValue;
+      }
+      return (int)hipGetLastError();
+    }
+  }
   return launch_decode_v<D, 1>(G, grid, s, q, ldq, kc, vc, lens, slot, H, Hkv, max_seq, chunk, nsplit, sl2e, po, pm, pl);
 }
 

@@ -253,3 +253,21 @@ def test_kmeans_accum():
     R.kmeans_accum(X, assign, s2, c2)
     _close(s1, s2, atol=1e-3)
     assert torch.equal(c1, c2)
+
+
+@pytest.mark.parametrize("H,Hkv,D", [(32, 8, 128), (8, 1, 128), (16, 8, 64)])
+def test_decode_attn_gqa_mfma_matches_valu_path(H, Hkv, D):
+    torch.manual_seed(7)
+    B, S = 4, 1500
+    kc, vc = _rand(4, Hkv, S, D), _rand(4, Hkv, S, D)
+    lens = torch.tensor([3, 129, 1000, 1500], device=DEV, dtype=torch.int32)
+    slot = torch.tensor([3, 1, 0, 2], device=DEV, dtype=torch.int32)
+    q = _rand(B, (H + 2 * Hkv) * D)
+    a = K.decode_attn(q, kc, vc, lens, slot, H, Hkv, D, max_len=S)
+    K.lib().da_set_gqa_mfma(0)
+    try:
+        b = K.decode_attn(q, kc, vc, lens, slot, H, Hkv, D, max_len=S)
+    finally:
+        K.lib().da_set_gqa_mfma(1)
+    _close(a, b, atol=0.01)
+    _close(a, R.decode_attn(q, kc, vc, lens, slot, H, Hkv, D), atol=0.02)
