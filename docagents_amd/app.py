@@ -48,6 +48,7 @@ def local_engine(cfg: Config):
                                temperature=cfg.temperature, max_new_tokens=cfg.max_new_tokens,
                                summary_max_new=cfg.summary_max_new_tokens, index_kind=cfg.index_kind,
                                ivf_lists=cfg.ivf_lists, ivf_probes=cfg.ivf_probes,
+                               enc_dtype="fp8" if cfg.dtype == "fp8" else "bf16",
                                max_seq=4096 if dev == "cuda" else 1024)
     return _ENGINES[key]
 

@@ -32,7 +32,7 @@ class Engine:
                  tp: TPContext | None = None, max_batch: int = 64, max_seq: int = 4096, temperature: float = 0.2,
                  max_new_tokens: int = 64, summary_max_new: int = 128, index_kind: str = "flat",
                  ivf_lists: int = 100, ivf_probes: int = 1, load_llm: bool = True, load_encoder: bool = True,
-                 use_graphs: bool = True, embed_max_tokens: int = 65536):
+                 use_graphs: bool = True, embed_max_tokens: int = 65536, enc_dtype: str = "bf16"):
         self.device = torch.device(device)
         self.lock = threading.RLock()
         self.enc_cfg = encoder_config(embed_arch)
@@ -44,7 +44,7 @@ class Engine:
         self.max_new_tokens = max_new_tokens
         self.summary_max_new = summary_max_new
         self.embed_max_tokens = embed_max_tokens
-        self.encoder = BertEncoder(self.enc_cfg, self.device, seed=seed) if load_encoder else None
+        self.encoder = BertEncoder(self.enc_cfg, self.device, seed=seed, dtype=enc_dtype) if load_encoder else None
         self.decoder = None
         self.gen = None
         if load_llm:

@@ -26,11 +26,37 @@ def _randn(shape, gen, device, std=0.02, dtype=torch.bfloat16):
 
 
 class BertEncoder:
-    def __init__(self, cfg: EncoderConfig, device="cuda", seed: int = 0, weights: dict | None = None):
+    """``dtype="fp8"``: the QKV and FFN-up projections run on e4m3 operands (SURVEY.md §7.2 step 7,
+    BASELINE config 5 "fp8 MFMA embeddings"): weights quantised once per output channel, the
+    LayerNorm kernels emit the per-token-quantised activations next to the bf16 rows, and the
+    dequantisation is fused into the GEMM epilogue. Attention, the O / FFN-down projections
+    (whose inputs would need a separate quantisation pass), pooling and the residual stream
+    stay bf16."""
+
+    LINEAR = ("wqkv", "w1")
+
+    def __init__(self, cfg: EncoderConfig, device="cuda", seed: int = 0, weights: dict | None = None,
+                 dtype: str = "bf16"):
+        if dtype not in ("bf16", "fp8"):
+            raise ValueError(f"encoder dtype must be bf16 or fp8, got {dtype!r}")
         self.cfg = cfg
         self.device = torch.device(device)
         self.ops = get_ops(self.device)
         self.w = weights if weights is not None else self._random_init(seed)
+        self.fp8 = dtype == "fp8"
+        if self.fp8:
+            for L in self.w["layers"]:
+                for n in self.LINEAR:
+                    L[n + "_q"], L[n + "_s"] = self.ops.quant_weight_fp8(L[n])
+
+    def _linear(self, x, L, name, bias, epi, resid=None, xq=None):
+        """fp8 path: ``xq = (q, scale)`` when the producer (a LayerNorm) already emitted the
+        quantised rows; otherwise the layer stays bf16 (a standalone quantisation pass would cost
+        more than the fp8 MFMA saves at these K, profiles/fp8_gemm_r1.txt)."""
+        o = self.ops
+        if xq is not None:
+            return o.gemm_fp8(xq[0], xq[1], L[name + "_q"], L[name + "_s"], bias=bias, epi=epi, resid=resid)
+        return o.gemm(x, L[name], bias=bias, epi=epi, resid=resid)
 
     # ------------------------------------------------------------------ weights
     def _random_init(self, seed: int) -> dict:
@@ -57,7 +83,7 @@ class BertEncoder:
         return w
 
     @classmethod
-    def from_hf_state_dict(cls, cfg: EncoderConfig, sd: dict, device="cuda"):
+    def from_hf_state_dict(cls, cfg: EncoderConfig, sd: dict, device="cuda", dtype: str = "bf16"):
         """Map a HF BertModel state dict (e.g. BGE safetensors) onto our packed layout."""
         dev = torch.device(device)
         g = lambda k: sd[k].to(device=dev, dtype=torch.bfloat16).contiguous()  # noqa: E731
@@ -77,23 +103,32 @@ class BertEncoder:
                 "w2": g(p + "output.dense.weight"), "b2": g(p + "output.dense.bias"),
                 "ln2_g": g(p + "output.LayerNorm.weight"), "ln2_b": g(p + "output.LayerNorm.bias"),
             })
-        return cls(cfg, device, weights=w)
+        return cls(cfg, device, weights=w, dtype=dtype)
 
     # ------------------------------------------------------------------ forward
     def forward(self, ids: torch.Tensor, positions: torch.Tensor, cu_seqlens: torch.Tensor, max_seqlen: int):
         """ids/positions int32 [T] (packed), cu_seqlens int32 [B+1] -> hidden bf16 [T, H]."""
         c, o, w = self.cfg, self.ops, self.w
         h, nh, hd = c.hidden, c.heads, c.head_dim
-        x = o.bert_embed_ln(ids, positions, None, w["word"], w["pos"], w["type"], w["emb_ln_g"], w["emb_ln_b"], c.eps)
+        q8 = self.fp8
+        xq = None
+        x = o.bert_embed_ln(ids, positions, None, w["word"], w["pos"], w["type"], w["emb_ln_g"], w["emb_ln_b"], c.eps,
+                            fp8_out=q8)
+        if q8:
+            x, *xq = x
         for L in w["layers"]:
-            qkv = o.gemm(x, L["wqkv"], bias=L["bqkv"], epi=EPI_BIAS)
+            qkv = self._linear(x, L, "wqkv", L["bqkv"], EPI_BIAS, xq=xq)
             a = o.flash_attn_varlen(qkv[:, :h], qkv[:, h:2 * h], qkv[:, 2 * h:], cu_seqlens, max_seqlen, nh, nh, hd,
                                     causal=False)
-            x1 = o.gemm(a, L["wo"], bias=L["bo"], epi=EPI_RESID, resid=x)
-            x = o.layernorm(x1, L["ln1_g"], L["ln1_b"], c.eps)
-            f = o.gemm(x, L["w1"], bias=L["b1"], epi=EPI_GELU)
-            x2 = o.gemm(f, L["w2"], bias=L["b2"], epi=EPI_RESID, resid=x)
-            x = o.layernorm(x2, L["ln2_g"], L["ln2_b"], c.eps)
+            x1 = self._linear(a, L, "wo", L["bo"], EPI_RESID, resid=x)
+            x = o.layernorm(x1, L["ln1_g"], L["ln1_b"], c.eps, fp8_out=q8)
+            if q8:
+                x, *xq = x
+            f = self._linear(x, L, "w1", L["b1"], EPI_GELU, xq=xq)
+            x2 = self._linear(f, L, "w2", L["b2"], EPI_RESID, resid=x)
+            x = o.layernorm(x2, L["ln2_g"], L["ln2_b"], c.eps, fp8_out=q8)
+            if q8:
+                x, *xq = x
         return x
 
     def encode_packed(self, seqs: list[list[int]], out16: torch.Tensor | None = None) -> torch.Tensor:

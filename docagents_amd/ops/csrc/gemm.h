@@ -15,7 +15,9 @@ struct GemmArgs {
   const bf16_t* A; const bf16_t* W; bf16_t* C;
   const bf16_t* bias; const bf16_t* resid; float* ws;
   int M, N, K, lda, ldc, ldr, k_per_split;
+  const float* sa; const float* sw;  // fp8 path: per-row (A) and per-output-channel (W) scales
 };
 
-// large-tile (256x256, 8 waves, LDS-DMA staged) path; returns hipError_t
-int launch_gemm256(const GemmArgs& a, int epi, hipStream_t s);
+// large-tile (256x256, 8 waves, LDS-DMA staged) path; returns hipError_t.
+// fp8 = 1: A and W hold OCP e4m3 bytes (lda / K in elements = bytes), C = (A.W^T) * sa[m] * sw[n].
+int launch_gemm256(const GemmArgs& a, int epi, hipStream_t s, int fp8 = 0);

@@ -279,7 +279,7 @@ DA_EXPORT int da_gemm_bf16(const void* A, int lda, const void* W, void* C, int l
   if (splits < 1) splits = 1;
   if ((K / 64) % splits) return (int)hipErrorInvalidValue;
   if (splits > 1 && ws == nullptr) return (int)hipErrorInvalidValue;
-  GemmArgs a;
+  GemmArgs a{};
   a.A = (const bf16_t*)A; a.W = (const bf16_t*)W; a.C = (bf16_t*)C;
   a.bias = (const bf16_t*)bias; a.resid = (const bf16_t*)resid; a.ws = (float*)ws;
   a.M = M; a.N = N; a.K = K; a.lda = lda; a.ldc = ldc; a.ldr = ldr; a.k_per_split = K / splits;

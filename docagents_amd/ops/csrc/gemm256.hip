@@ -1,4 +1,10 @@
-// 256x256-tile bf16 GEMM for prefill-sized M (C[M,N] = epi(A[M,K] . W[N,K]^T)).
+// 256x256-tile GEMM for prefill-sized M (C[M,N] = epi(A[M,K] . W[N,K]^T)), bf16 or fp8 operands.
+//
+// fp8 (OCP e4m3): the same 128-byte K-step and LDS image (BK = 128 fp8), one
+// v_mfma_scale_f32_16x16x128_f8f6f4 per fragment pair instead of two bf16 16x16x32 (2x the bf16
+// MFMA rate); each lane feeds the same 32 contiguous k-bytes of its A row and W row, so the
+// instruction's internal k order pairs them consistently. Dequantisation (per-token activation
+// scale x per-output-channel weight scale) is applied to the fp32 accumulators in the epilogue.
 //
 // MI355X-first structure (cdna_hip_programming.md §5 "glds vs register staging", T1, T2):
 //  * 512 threads = 8 waves as 2 (M) x 4 (N); each wave owns a 128 x 64 output block
@@ -31,9 +37,10 @@ constexpr int SMEM = (2 * STAGE > STAGING) ? 2 * STAGE : STAGING;
 
 __device__ __forceinline__ int swz(int r) { return (r >> 1) & 7; }
 
-template <int EPI>
+template <int EPI, int FP8>
 __global__ void __launch_bounds__(512)
 gemm256_kernel(GemmArgs p) {
+  constexpr int ES = FP8 ? 1 : 2;  // bytes per element
   __shared__ __attribute__((aligned(16))) char smem[SMEM];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid >> 2, wn = wid & 3;
@@ -50,24 +57,24 @@ gemm256_kernel(GemmArgs p) {
 
   // ---- per-lane LDS-DMA source pointers (rows clamped into range; clamped rows only feed
   //      outputs that are never stored) ----
-  const bf16_t* asrc[4];
-  const bf16_t* bsrc[4];
+  const char* asrc[4];
+  const char* bsrc[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const int r = (wid * 4 + j) * 8 + (lane >> 3);
     const int c = (lane & 7) ^ swz(r);
-    asrc[j] = p.A + (size_t)min(m0 + r, p.M - 1) * p.lda + c * 8;
-    bsrc[j] = p.W + (size_t)min(n0 + r, p.N - 1) * p.K + c * 8;
+    asrc[j] = (const char*)p.A + ((size_t)min(m0 + r, p.M - 1) * p.lda) * ES + c * 16;
+    bsrc[j] = (const char*)p.W + ((size_t)min(n0 + r, p.N - 1) * p.K) * ES + c * 16;
   }
   auto issue = [&](int kt, int buf) {
     char* sa = smem + buf * STAGE;
     char* sb = sa + A_BYTES;
 #pragma unroll
     for (int j = 0; j < 4; ++j)
-      __builtin_amdgcn_global_load_lds((gptr_t)(asrc[j] + kt * BK), (lds_ptr_t)(sa + (wid * 4 + j) * 1024), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((gptr_t)(asrc[j] + kt * 128), (lds_ptr_t)(sa + (wid * 4 + j) * 1024), 16, 0, 0);
 #pragma unroll
     for (int j = 0; j < 4; ++j)
-      __builtin_amdgcn_global_load_lds((gptr_t)(bsrc[j] + kt * BK), (lds_ptr_t)(sb + (wid * 4 + j) * 1024), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((gptr_t)(bsrc[j] + kt * 128), (lds_ptr_t)(sb + (wid * 4 + j) * 1024), 16, 0, 0);
   };
 
   f32x4_t acc[8][4];
@@ -76,7 +83,7 @@ gemm256_kernel(GemmArgs p) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
-  const int nk = p.K / BK;
+  const int nk = p.K * ES / 128;  // 128-byte K-steps (64 bf16 or 128 fp8)
   issue(0, 0);
   for (int kt = 0; kt < nk; ++kt) {
     __syncthreads();  // vmcnt(0) + barrier: stage kt landed for every wave; stage kt-1 fully read
@@ -84,7 +91,7 @@ gemm256_kernel(GemmArgs p) {
     const char* sb = sa + A_BYTES;
     bf16x8_t af[2][8], bfr[2][4];
     auto read_frags = [&](int kk) {
-      const int c = kk * 4 + fg;
+      const int c = FP8 ? 2 * fg + kk : kk * 4 + fg;
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
         const int r = wm * TM + i * 16 + fr;
@@ -105,18 +112,47 @@ gemm256_kernel(GemmArgs p) {
     read_frags(0);
     read_frags(1);
     __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk)
+    if constexpr (FP8) {
+      // lane group fg owns k-bytes 32fg..32fg+31 = chunks 2fg, 2fg+1 (read as "k-halves" 0 and 1
+      // by read_frags with c = kk*4 + fg -> re-read here with the fp8 chunk pairing)
+      typedef __attribute__((ext_vector_type(8))) int i32x8_t;
 #pragma unroll
       for (int i = 0; i < 8; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(af[kk][i], bfr[kk][j], acc[i][j]);
+        for (int j = 0; j < 4; ++j) {
+          const i32x8_t a8 = __builtin_bit_cast(i32x8_t, __builtin_shufflevector(af[0][i], af[1][i], 0, 1, 2, 3, 4, 5, 6, 7,
+                                                                                  8, 9, 10, 11, 12, 13, 14, 15));
+          const i32x8_t b8 = __builtin_bit_cast(i32x8_t, __builtin_shufflevector(bfr[0][j], bfr[1][j], 0, 1, 2, 3, 4, 5, 6, 7,
+                                                                                  8, 9, 10, 11, 12, 13, 14, 15));
+          acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a8, b8, acc[i][j], 0, 0, 0, 127, 0, 127);
+        }
+    } else {
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(af[kk][i], bfr[kk][j], acc[i][j]);
+    }
   }
   __syncthreads();
 
   // ---- epilogue: registers -> (bias / GELU / SwiGLU) -> bf16 staging -> coalesced stores ----
   char* st = smem + wid * TM * SROW;
   const int row0 = m0 + wm * TM, col0 = n0 + wn * TN;
+  if constexpr (FP8) {
+    float swv[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) swv[j] = p.sw[min(col0 + j * 16 + fr, p.N - 1)];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float sav = p.sa[min(row0 + i * 16 + fg * 4 + q, p.M - 1)];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j][q] *= sav * swv[j];
+      }
+  }
   if constexpr (EPI == EPI_SWIGLU) {
 #pragma unroll
     for (int i = 0; i < 8; ++i)
@@ -171,16 +207,35 @@ gemm256_kernel(GemmArgs p) {
   }
 }
 
-int launch_gemm256(const GemmArgs& a, int epi, hipStream_t s) {
-  const int ntm = (a.M + BM - 1) / BM, ntn = (a.N + BN - 1) / BN;
-  dim3 grid(ntm * ntn), block(512);
+template <int FP8>
+static int launch256(const GemmArgs& a, int epi, hipStream_t s, dim3 grid, dim3 block) {
   switch (epi) {
-    case EPI_NONE: gemm256_kernel<EPI_NONE><<<grid, block, 0, s>>>(a); break;
-    case EPI_BIAS: gemm256_kernel<EPI_BIAS><<<grid, block, 0, s>>>(a); break;
-    case EPI_GELU: gemm256_kernel<EPI_GELU><<<grid, block, 0, s>>>(a); break;
-    case EPI_SWIGLU: gemm256_kernel<EPI_SWIGLU><<<grid, block, 0, s>>>(a); break;
-    case EPI_RESID: gemm256_kernel<EPI_RESID><<<grid, block, 0, s>>>(a); break;
+    case EPI_NONE: gemm256_kernel<EPI_NONE, FP8><<<grid, block, 0, s>>>(a); break;
+    case EPI_BIAS: gemm256_kernel<EPI_BIAS, FP8><<<grid, block, 0, s>>>(a); break;
+    case EPI_GELU: gemm256_kernel<EPI_GELU, FP8><<<grid, block, 0, s>>>(a); break;
+    case EPI_SWIGLU: gemm256_kernel<EPI_SWIGLU, FP8><<<grid, block, 0, s>>>(a); break;
+    case EPI_RESID: gemm256_kernel<EPI_RESID, FP8><<<grid, block, 0, s>>>(a); break;
     default: return (int)hipErrorInvalidValue;
   }
   return (int)hipGetLastError();
+}
+
+int launch_gemm256(const GemmArgs& a, int epi, hipStream_t s, int fp8) {
+  const int ntm = (a.M + BM - 1) / BM, ntn = (a.N + BN - 1) / BN;
+  dim3 grid(ntm * ntn), block(512);
+  return fp8 ? launch256<1>(a, epi, s, grid, block) : launch256<0>(a, epi, s, grid, block);
+}
+
+// fp8 GEMM entry: A [M, lda] e4m3 (row-major), W [N, K] e4m3, sa [M], sw [N] fp32 dequant scales.
+DA_EXPORT int da_gemm_fp8(const void* A, int lda, const void* W, const void* sa, const void* sw, void* C, int ldc,
+                          const void* bias, const void* resid, int ldr, int M, int N, int K, int epi, void* stream) {
+  if (K % 128 || N % 8 || lda % 16 || ldc % 8 || !sa || !sw) return (int)hipErrorInvalidValue;
+  if (epi == EPI_SWIGLU && N % 32) return (int)hipErrorInvalidValue;
+  if (M == 0) return 0;
+  GemmArgs a{};
+  a.A = (const bf16_t*)A; a.W = (const bf16_t*)W; a.C = (bf16_t*)C;
+  a.bias = (const bf16_t*)bias; a.resid = (const bf16_t*)resid; a.ws = nullptr;
+  a.M = M; a.N = N; a.K = K; a.lda = lda; a.ldc = ldc; a.ldr = ldr; a.k_per_split = K;
+  a.sa = (const float*)sa; a.sw = (const float*)sw;
+  return launch_gemm256(a, epi, (hipStream_t)stream, 1);
 }

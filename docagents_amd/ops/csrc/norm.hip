@@ -64,10 +64,42 @@ __global__ void rmsnorm_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict_
   }
 }
 
+// Optional fused fp8 output of a normalised row held in registers (v[i] = chunk threadIdx.x + i*blockDim):
+// per-row e4m3 quantisation exactly like quant_fp8_rows_kernel, so the next GEMM can run on fp8
+// without a separate quantisation pass over the activations.
+__device__ __forceinline__ void store_row_fp8(float (&v)[MAXCH][8], int nch, int row, unsigned char* yq, int ldq,
+                                              float* yscale, float* red) {
+  float amax = 0.f;
+#pragma unroll
+  for (int i = 0; i < MAXCH; ++i) {
+    const int c = threadIdx.x + i * blockDim.x;
+    if (c < nch) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) amax = fmaxf(amax, fabsf(v[i][e]));
+    }
+  }
+  amax = block_max(amax, red);
+  const float sc = amax > 0.f ? amax / 448.f : 1.f;
+  const float inv = 1.f / sc;
+  if (threadIdx.x == 0) yscale[row] = sc;
+#pragma unroll
+  for (int i = 0; i < MAXCH; ++i) {
+    const int c = threadIdx.x + i * blockDim.x;
+    if (c < nch) {
+      int lo = __builtin_amdgcn_cvt_pk_fp8_f32(v[i][0] * inv, v[i][1] * inv, 0, false);
+      lo = __builtin_amdgcn_cvt_pk_fp8_f32(v[i][2] * inv, v[i][3] * inv, lo, true);
+      int hi = __builtin_amdgcn_cvt_pk_fp8_f32(v[i][4] * inv, v[i][5] * inv, 0, false);
+      hi = __builtin_amdgcn_cvt_pk_fp8_f32(v[i][6] * inv, v[i][7] * inv, hi, true);
+      *(u32x2_t*)(yq + (size_t)row * ldq + c * 8) = u32x2_t{(unsigned)lo, (unsigned)hi};
+    }
+  }
+}
+
 // LayerNorm (BERT), optional residual input added first (x + resid), bias optional.
 __global__ void layernorm_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ resid,
                                  const bf16_t* __restrict__ g, const bf16_t* __restrict__ b,
-                                 bf16_t* __restrict__ y, int D, float eps) {
+                                 bf16_t* __restrict__ y, int D, float eps, unsigned char* __restrict__ yq = nullptr,
+                                 float* __restrict__ yscale = nullptr) {
   __shared__ float red[16];
   const int row = blockIdx.x;
   const int nch = D / 8;
@@ -112,6 +144,7 @@ __global__ void layernorm_kernel(const bf16_t* __restrict__ x, const bf16_t* __r
       store8(y + (size_t)row * D + c * 8, v[i]);
     }
   }
+  if (yq) store_row_fp8(v, nch, row, yq, D, yscale, red);
 }
 
 // BERT embeddings: y = LN(word[ids[t]] + pos[positions[t]] + type[types ? types[t] : 0])
@@ -119,7 +152,8 @@ __global__ void bert_embed_ln_kernel(const int* __restrict__ ids, const int* __r
                                      const int* __restrict__ types, const bf16_t* __restrict__ word,
                                      const bf16_t* __restrict__ pos, const bf16_t* __restrict__ type,
                                      const bf16_t* __restrict__ g, const bf16_t* __restrict__ b,
-                                     bf16_t* __restrict__ y, int D, float eps) {
+                                     bf16_t* __restrict__ y, int D, float eps, unsigned char* __restrict__ yq = nullptr,
+                                     float* __restrict__ yscale = nullptr) {
   __shared__ float red[16];
   const int row = blockIdx.x;
   const size_t wi = (size_t)ids[row], pi = (size_t)positions[row], ti = types ? (size_t)types[row] : 0;
@@ -162,6 +196,7 @@ __global__ void bert_embed_ln_kernel(const int* __restrict__ ids, const int* __r
       store8(y + (size_t)row * D + c * 8, v[i]);
     }
   }
+  if (yq) store_row_fp8(v, nch, row, yq, D, yscale, red);
 }
 
 // Token embedding gather (decoder): y[t] = table[ids[t]]
@@ -226,6 +261,43 @@ __global__ void pool_l2norm_kernel(const bf16_t* __restrict__ h, const int* __re
   }
 }
 
+// Per-row dynamic fp8 (OCP e4m3) quantisation for the fp8 GEMM path: scale[m] = amax(|x[m,:]|)/448,
+// q = rne(x / scale) (v_cvt_pk_fp8_f32, saturating at +-448). One workgroup per row, the row kept
+// in registers between the amax and the conversion pass.
+__global__ void quant_fp8_rows_kernel(const bf16_t* __restrict__ x, int ldx, int K, unsigned char* __restrict__ out,
+                                      int ldo, float* __restrict__ scale) {
+  __shared__ float red[16];
+  const int row = blockIdx.x;
+  const bf16_t* xr = x + (size_t)row * ldx;
+  const int nch = K / 8;
+  float v[MAXCH][8];
+  float amax = 0.f;
+#pragma unroll
+  for (int i = 0; i < MAXCH; ++i) {
+    const int c = threadIdx.x + i * blockDim.x;
+    if (c < nch) {
+      load8(xr + c * 8, v[i]);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) amax = fmaxf(amax, fabsf(v[i][e]));
+    }
+  }
+  amax = block_max(amax, red);
+  const float sc = amax > 0.f ? amax / 448.f : 1.f;
+  const float inv = 1.f / sc;
+  if (threadIdx.x == 0) scale[row] = sc;
+#pragma unroll
+  for (int i = 0; i < MAXCH; ++i) {
+    const int c = threadIdx.x + i * blockDim.x;
+    if (c < nch) {
+      int lo = __builtin_amdgcn_cvt_pk_fp8_f32(v[i][0] * inv, v[i][1] * inv, 0, false);
+      lo = __builtin_amdgcn_cvt_pk_fp8_f32(v[i][2] * inv, v[i][3] * inv, lo, true);
+      int hi = __builtin_amdgcn_cvt_pk_fp8_f32(v[i][4] * inv, v[i][5] * inv, 0, false);
+      hi = __builtin_amdgcn_cvt_pk_fp8_f32(v[i][6] * inv, v[i][7] * inv, hi, true);
+      *(u32x2_t*)(out + (size_t)row * ldo + c * 8) = u32x2_t{(unsigned)lo, (unsigned)hi};
+    }
+  }
+}
+
 static inline int row_threads(int D) {
   int ch = D / 8;
   int t = ((ch + 63) / 64) * 64;
@@ -279,5 +351,35 @@ DA_EXPORT int da_pool_l2norm(const void* h, const void* cu_seqlens, int B, int D
   if (B == 0) return 0;
   pool_l2norm_kernel<<<B, row_threads(D), 0, (hipStream_t)stream>>>((const bf16_t*)h, (const int*)cu_seqlens, D,
                                                                      mode, (float*)out32, (bf16_t*)out16);
+  DA_LAUNCH_CHECK();
+}
+
+DA_EXPORT int da_quant_fp8_rows(const void* x, int ldx, int M, int K, void* out, int ldo, void* scale, void* stream) {
+  if (!d_ok(K) || ldx % 8 || ldo % 8) return (int)hipErrorInvalidValue;
+  if (M == 0) return 0;
+  quant_fp8_rows_kernel<<<M, row_threads(K), 0, (hipStream_t)stream>>>((const bf16_t*)x, ldx, K, (unsigned char*)out,
+                                                                       ldo, (float*)scale);
+  DA_LAUNCH_CHECK();
+}
+
+// LayerNorm / BERT embeddings + LayerNorm with an additional fused fp8 (e4m3, per-row scale) output.
+DA_EXPORT int da_layernorm_q(const void* x, const void* resid, const void* g, const void* b, void* y, void* yq,
+                             void* yscale, int M, int D, float eps, void* stream) {
+  if (!d_ok(D) || !yq || !yscale) return (int)hipErrorInvalidValue;
+  if (M == 0) return 0;
+  layernorm_kernel<<<M, row_threads(D), 0, (hipStream_t)stream>>>((const bf16_t*)x, (const bf16_t*)resid,
+                                                                   (const bf16_t*)g, (const bf16_t*)b, (bf16_t*)y, D,
+                                                                   eps, (unsigned char*)yq, (float*)yscale);
+  DA_LAUNCH_CHECK();
+}
+
+DA_EXPORT int da_bert_embed_ln_q(const void* ids, const void* positions, const void* types, const void* word,
+                                 const void* pos, const void* type, const void* g, const void* b, void* y, void* yq,
+                                 void* yscale, int T, int D, float eps, void* stream) {
+  if (!d_ok(D) || !yq || !yscale) return (int)hipErrorInvalidValue;
+  if (T == 0) return 0;
+  bert_embed_ln_kernel<<<T, row_threads(D), 0, (hipStream_t)stream>>>(
+      (const int*)ids, (const int*)positions, (const int*)types, (const bf16_t*)word, (const bf16_t*)pos,
+      (const bf16_t*)type, (const bf16_t*)g, (const bf16_t*)b, (bf16_t*)y, D, eps, (unsigned char*)yq, (float*)yscale);
   DA_LAUNCH_CHECK();
 }

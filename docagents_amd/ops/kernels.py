@@ -28,6 +28,11 @@ c_void_p, c_int, c_float, c_uint, c_size_t = (ctypes.c_void_p, ctypes.c_int, cty
 _SIGS = {
     "da_gemm_bf16": [c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int,
                      c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p],
+    "da_gemm_fp8": [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int,
+                    c_int, c_int, c_int, c_int, c_void_p],
+    "da_quant_fp8_rows": [c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p],
+    "da_layernorm_q": [c_void_p] * 7 + [c_int, c_int, c_float, c_void_p],
+    "da_bert_embed_ln_q": [c_void_p] * 11 + [c_int, c_int, c_float, c_void_p],
     "da_rmsnorm": [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_float, c_void_p],
     "da_layernorm": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_float, c_void_p],
     "da_bert_embed_ln": [c_void_p] * 9 + [c_int, c_int, c_float, c_void_p],
@@ -175,6 +180,59 @@ def gemm(a: torch.Tensor, w: torch.Tensor, bias=None, epi: int = EPI_NONE, resid
     return out
 
 
+FP8 = torch.float8_e4m3fn  # OCP e4m3 (gfx950), not the MI300 fnuz variant
+
+
+def quant_fp8(x: torch.Tensor, out=None, scale=None):
+    """Per-row dynamic e4m3 quantisation: returns (q [M, K] float8_e4m3fn, scale [M] fp32)."""
+    _bf16_cuda(x, "x")
+    _req(x.dim() == 2 and x.stride(1) == 1 and x.stride(0) % 8 == 0 and x.shape[1] % 8 == 0, "x layout")
+    M, K = x.shape
+    if out is None:
+        out = torch.empty((M, K), dtype=FP8, device=x.device)
+    if scale is None:
+        scale = torch.empty(M, dtype=torch.float32, device=x.device)
+    _req(out.dtype == FP8 and out.shape == (M, K) and out.stride(1) == 1 and out.stride(0) % 16 == 0, "bad out")
+    _req(scale.dtype == torch.float32 and scale.numel() >= M, "bad scale")
+    _check(lib().da_quant_fp8_rows(_ptr(x), x.stride(0), M, K, _ptr(out), out.stride(0), _ptr(scale), _stream()),
+           "quant_fp8")
+    return out, scale
+
+
+def quant_weight_fp8(w: torch.Tensor):
+    """Per-output-channel e4m3 weight quantisation (host-side torch; done once at load)."""
+    wf = w.float()
+    sw = (wf.abs().amax(dim=1) / 448.0).clamp_min(1e-30)
+    return (wf / sw[:, None]).clamp(-448, 448).to(FP8).contiguous(), sw.contiguous()
+
+
+def gemm_fp8(aq, sa, wq, sw, bias=None, epi: int = EPI_NONE, resid=None, out=None) -> torch.Tensor:
+    """out[M, N] = epi((aq . wq^T) * sa[:, None] * sw[None, :]) with e4m3 operands (256x256 MFMA tile)."""
+    _req(aq.is_cuda and aq.dtype == FP8 and wq.dtype == FP8, "fp8 operands expected")
+    M, K = aq.shape
+    N, K2 = wq.shape
+    _req(K == K2 and K % 128 == 0 and N % 8 == 0, f"fp8 gemm shape M={M} N={N} K={K}")
+    _req(aq.stride(1) == 1 and aq.stride(0) % 16 == 0 and wq.is_contiguous(), "fp8 operand layout")
+    _req(aq.data_ptr() % 16 == 0 and wq.data_ptr() % 16 == 0, "operands must be 16-B aligned")
+    _req(sa.dtype == torch.float32 and sa.numel() >= M and sw.dtype == torch.float32 and sw.numel() == N, "scales")
+    nout = N // 2 if epi == EPI_SWIGLU else N
+    if out is None:
+        out = torch.empty((M, nout), dtype=torch.bfloat16, device=aq.device)
+    _bf16_cuda(out, "out")
+    _req(out.shape == (M, nout) and out.stride(1) == 1 and out.stride(0) % 8 == 0, "bad out")
+    if bias is not None:
+        _bf16_cuda(bias, "bias"); _req(bias.numel() == N, "bias must be [N]")
+    ldr = 0
+    if epi == EPI_RESID:
+        _req(resid is not None and resid.shape == (M, N) and resid.stride(1) == 1, "bad resid")
+        ldr = resid.stride(0)
+    if M == 0:
+        return out
+    _check(lib().da_gemm_fp8(_ptr(aq), aq.stride(0), _ptr(wq), _ptr(sa), _ptr(sw), _ptr(out), out.stride(0),
+                             _ptr(bias), _ptr(resid), ldr, M, N, K, epi, _stream()), "gemm_fp8")
+    return out
+
+
 def _auto_splits(M: int, N: int, K: int) -> int:
     """Split-K so skinny (decode-sized) GEMMs put >= ~512 workgroups on the 256 CUs."""
     if M > 64:
@@ -204,7 +262,9 @@ def rmsnorm(x, w, eps: float, resid=None, out=None):
     return out
 
 
-def layernorm(x, g, b, eps: float, resid=None, out=None):
+def layernorm(x, g, b, eps: float, resid=None, out=None, fp8_out: bool = False):
+    """LayerNorm; with ``fp8_out`` also returns the row-quantised e4m3 copy and its scales
+    (fused: the row is quantised from registers) -> (y, yq, yscale)."""
     _bf16_cuda(x, "x")
     M, D = x.shape
     _req(x.is_contiguous() and D % 8 == 0, "x must be contiguous, D % 8 == 0")
@@ -212,12 +272,18 @@ def layernorm(x, g, b, eps: float, resid=None, out=None):
         _req(resid.is_contiguous() and resid.shape == x.shape, "bad resid")
     if out is None:
         out = torch.empty_like(x)
+    if fp8_out:
+        yq = torch.empty((M, D), dtype=FP8, device=x.device)
+        ys = torch.empty(M, dtype=torch.float32, device=x.device)
+        _check(lib().da_layernorm_q(_ptr(x), _ptr(resid), _ptr(g), _ptr(b), _ptr(out), _ptr(yq), _ptr(ys), M, D,
+                                    float(eps), _stream()), "layernorm_q")
+        return out, yq, ys
     _check(lib().da_layernorm(_ptr(x), _ptr(resid), _ptr(g), _ptr(b), _ptr(out), M, D, float(eps), _stream()),
            "layernorm")
     return out
 
 
-def bert_embed_ln(ids, positions, types, word, pos, type_, g, b, eps: float, out=None):
+def bert_embed_ln(ids, positions, types, word, pos, type_, g, b, eps: float, out=None, fp8_out: bool = False):
     _i32(ids, "ids"); _i32(positions, "positions")
     if types is not None:
         _i32(types, "types")
@@ -226,6 +292,13 @@ def bert_embed_ln(ids, positions, types, word, pos, type_, g, b, eps: float, out
     _req(positions.numel() == T, "positions length")
     if out is None:
         out = torch.empty((T, D), dtype=torch.bfloat16, device=ids.device)
+    if fp8_out:
+        yq = torch.empty((T, D), dtype=FP8, device=ids.device)
+        ys = torch.empty(T, dtype=torch.float32, device=ids.device)
+        _check(lib().da_bert_embed_ln_q(_ptr(ids), _ptr(positions), _ptr(types), _ptr(word), _ptr(pos), _ptr(type_),
+                                        _ptr(g), _ptr(b), _ptr(out), _ptr(yq), _ptr(ys), T, D, float(eps), _stream()),
+               "bert_embed_ln_q")
+        return out, yq, ys
     _check(lib().da_bert_embed_ln(_ptr(ids), _ptr(positions), _ptr(types), _ptr(word), _ptr(pos), _ptr(type_),
                                   _ptr(g), _ptr(b), _ptr(out), T, D, float(eps), _stream()), "bert_embed_ln")
     return out

@@ -15,19 +15,21 @@ EPI_NONE, EPI_BIAS, EPI_GELU, EPI_SWIGLU, EPI_RESID = 0, 1, 2, 3, 4
 
 
 def gemm(a, w, bias=None, epi=EPI_NONE, resid=None, out=None, **_):
-    y = a.float() @ w.float().t()
+    return _epilogue(a.float() @ w.float().t(), w.shape[0], bias, epi, resid, out)
+
+
+def _epilogue(y, N, bias, epi, resid, out):
     if bias is not None:
         y = y + bias.float()
     if epi == EPI_GELU:
         y = F.gelu(y)
     elif epi == EPI_SWIGLU:
-        N = w.shape[0]
         yy = y.view(y.shape[0], N // 32, 2, 16)
         g, u = yy[:, :, 0, :], yy[:, :, 1, :]
         y = (F.silu(g) * u).reshape(y.shape[0], N // 2)
     elif epi == EPI_RESID:
         y = y + resid.float()
-    y = y.to(a.dtype)
+    y = y.to(torch.bfloat16)
     if out is not None:
         out.copy_(y)
         return out
@@ -56,21 +58,25 @@ def rmsnorm(x, w, eps, resid=None, out=None):
     return y
 
 
-def layernorm(x, g, b, eps, resid=None, out=None):
+def layernorm(x, g, b, eps, resid=None, out=None, fp8_out=False):
     xf = x.float()
     if resid is not None:
         xf = xf + resid.float()
-    y = F.layer_norm(xf, (xf.shape[-1],), g.float(), None if b is None else b.float(), eps).to(x.dtype)
+    yf = F.layer_norm(xf, (xf.shape[-1],), g.float(), None if b is None else b.float(), eps)
+    y = yf.to(x.dtype)
     if out is not None:
         out.copy_(y)
-        return out
+        y = out
+    if fp8_out:
+        yq, ys = quant_fp8(yf)
+        return y, yq, ys
     return y
 
 
-def bert_embed_ln(ids, positions, types, word, pos, type_, g, b, eps, out=None):
+def bert_embed_ln(ids, positions, types, word, pos, type_, g, b, eps, out=None, fp8_out=False):
     t = type_[types.long()] if types is not None else type_[0]
     x = word[ids.long()].float() + pos[positions.long()].float() + t.float()
-    return layernorm(x.to(word.dtype), g, b, eps, out=out)
+    return layernorm(x.to(word.dtype), g, b, eps, out=out, fp8_out=fp8_out)
 
 
 def embed(ids, table, out=None):
@@ -289,3 +295,29 @@ def kmeans_accum(X, assign, sums, counts):
     m = a >= 0
     sums.index_add_(0, a[m], X[m].float())
     counts.index_add_(0, a[m], torch.ones(int(m.sum()), device=X.device))
+
+
+# ----------------------------------------------------------------------------------- fp8 path
+def quant_fp8(x, out=None, scale=None):
+    xf = x.float()
+    sc = xf.abs().amax(dim=1) / 448.0
+    sc = torch.where(sc > 0, sc, torch.ones_like(sc))
+    q = (xf / sc[:, None]).clamp(-448, 448).to(torch.float8_e4m3fn)
+    if out is not None:
+        out.copy_(q)
+        q = out
+    if scale is not None:
+        scale[:sc.numel()].copy_(sc)
+        sc = scale
+    return q, sc
+
+
+def gemm_fp8(aq, sa, wq, sw, bias=None, epi=EPI_NONE, resid=None, out=None):
+    y = (aq.float() * sa[:aq.shape[0], None].float()) @ (wq.float() * sw[:, None].float()).t()
+    return _epilogue(y, wq.shape[0], bias, epi, resid, out)
+
+
+def quant_weight_fp8(w):
+    wf = w.float()
+    sw = (wf.abs().amax(dim=1) / 448.0).clamp_min(1e-30)
+    return (wf / sw[:, None]).clamp(-448, 448).to(torch.float8_e4m3fn).contiguous(), sw.contiguous()

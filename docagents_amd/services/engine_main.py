@@ -49,7 +49,8 @@ def main(argv=None) -> int:
     eng = Engine(cfg.embed_arch, cfg.llm_arch, dev, seed=cfg.seed, tp=tp, max_batch=cfg.max_batch,
                  temperature=cfg.temperature, max_new_tokens=cfg.max_new_tokens,
                  summary_max_new=cfg.summary_max_new_tokens, index_kind=cfg.index_kind, ivf_lists=cfg.ivf_lists,
-                 ivf_probes=cfg.ivf_probes, max_seq=4096 if dev.type == "cuda" else 1024)
+                 ivf_probes=cfg.ivf_probes, max_seq=4096 if dev.type == "cuda" else 1024,
+                 enc_dtype="fp8" if cfg.dtype == "fp8" else "bf16")
     grp = EngineGroup(eng, info.rank, info.world, ctrl, data)
     grp.tensor_parallel = tp is not None
     if a.snapshot and os.path.exists(f"{a.snapshot}.shard{info.rank}"):

@@ -253,3 +253,15 @@ def test_config_bool_parsing():
     assert load({"ENGINE_CONTINUOUS": "false"}).engine_continuous is False
     assert load({"ENGINE_CONTINUOUS": "1"}).engine_continuous is True
     assert load({"ENGINE_CONTINUOUS": "maybe"}).engine_continuous is True  # parse error -> default
+
+
+def test_encoder_fp8_close_to_bf16_reference_path():
+    from docagents_amd.models.bert import BertEncoder
+    from docagents_amd.models.configs import encoder_config
+    cfg = encoder_config("tiny-enc")
+    a = BertEncoder(cfg, "cpu", seed=3)
+    b = BertEncoder(cfg, "cpu", weights=a.w, dtype="fp8")
+    seqs = [[101, 7, 8, 9, 102], [101] + list(range(200, 260)) + [102]]
+    va, vb = a.encode_packed(seqs), b.encode_packed(seqs)
+    cos = (va * vb).sum(-1)
+    assert torch.all(cos > 0.98), cos

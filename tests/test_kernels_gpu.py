@@ -271,3 +271,50 @@ def test_decode_attn_gqa_mfma_matches_valu_path(H, Hkv, D):
         K.lib().da_set_gqa_mfma(1)
     _close(a, b, atol=0.01)
     _close(a, R.decode_attn(q, kc, vc, lens, slot, H, Hkv, D), atol=0.02)
+
+
+@pytest.mark.parametrize("M,N,Kd,epi", [(300, 768, 768, 0), (512, 3072, 768, 2), (1000, 768, 3072, 4),
+                                         (256, 2304, 1024, 1)])
+def test_gemm_fp8_matches_dequantized_reference(M, N, Kd, epi):
+    torch.manual_seed(M + N)
+    x = _rand(M, Kd)
+    w = _rand(N, Kd, scale=Kd ** -0.5)
+    bias = _rand(N) if epi in (1, 2, 4) else None
+    resid = _rand(M, N) if epi == 4 else None
+    xq, sa = K.quant_fp8(x)
+    rq, rsa = R.quant_fp8(x)
+    assert torch.allclose(sa, rsa, rtol=1e-6)
+    # both round to nearest even; x*(1/s) vs x/s may land on opposite sides of a rounding boundary
+    d = (xq.float() - rq.float()).abs()
+    assert (d > 0).float().mean().item() < 1e-2
+    assert torch.all(d <= 0.126 * rq.float().abs() + 2 ** -9)
+    wq, sw = K.quant_weight_fp8(w)
+    got = K.gemm_fp8(xq, sa, wq, sw, bias=bias, epi=epi, resid=resid)
+    ref = R.gemm_fp8(xq, sa, wq, sw, bias=bias, epi=epi, resid=resid)
+    _close(got, ref, atol=0.03)
+    full = R.gemm(x, w, bias=bias, epi=epi, resid=resid)
+    rel = (got.float() - full.float()).norm() / full.float().norm()
+    assert rel < 0.06, rel
+
+
+def test_encoder_fp8_vs_bf16_gpu():
+    from docagents_amd.models.bert import BertEncoder
+    from docagents_amd.models.configs import encoder_config
+    cfg = encoder_config("bge-small")
+    a = BertEncoder(cfg, DEV, seed=5)
+    b = BertEncoder(cfg, DEV, weights=a.w, dtype="fp8")
+    seqs = [[101] + list(range(1000, 1000 + n)) + [102] for n in (5, 60, 300)]
+    cos = (a.encode_packed(seqs) * b.encode_packed(seqs)).sum(-1)
+    assert torch.all(cos > 0.97), cos
+
+
+def test_layernorm_fused_fp8_output():
+    torch.manual_seed(11)
+    x, r = _rand(333, 768), _rand(333, 768)
+    g, b = _rand(768) + 1, _rand(768)
+    y, yq, ys = K.layernorm(x, g, b, 1e-12, resid=r, fp8_out=True)
+    ry, rq, rs = R.layernorm(x, g, b, 1e-12, resid=r, fp8_out=True)
+    _close(y, ry, atol=0.03)
+    assert torch.allclose(ys, rs, rtol=1e-3)
+    d = (yq.float() * ys[:, None] - rq.float() * rs[:, None]).abs()
+    assert torch.all(d <= 0.13 * (rq.float() * rs[:, None]).abs() + 1e-3)
