@@ -38,17 +38,20 @@ def init_from_env(prefer_gpu: bool = True, timeout_s: int = 600) -> DistInfo:
     local = int(os.environ.get("LOCAL_RANK", str(rank)))
     use_gpu = prefer_gpu and torch.cuda.is_available()
     if use_gpu:
-        torch.cuda.set_device(local)
-        device = torch.device("cuda", local)
+        # one rank per GPU; more ranks than GPUs (a rehearsal of the multi-rank path on a 1-GPU box,
+        # DA_DIST_BACKEND=gloo) wrap around
+        idx = local % max(1, torch.cuda.device_count())
+        torch.cuda.set_device(idx)
+        device = torch.device("cuda", idx)
     else:
         device = torch.device("cpu")
     backend = "none"
     if world > 1 and not dist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29511")
-        backend = "nccl" if use_gpu else "gloo"
+        backend = os.environ.get("DA_DIST_BACKEND") or ("nccl" if use_gpu else "gloo")
         kw = dict(backend=backend, rank=rank, world_size=world, timeout=datetime.timedelta(seconds=timeout_s))
-        if use_gpu:
+        if use_gpu and backend == "nccl":
             kw["device_id"] = device
         dist.init_process_group(**kw)
     elif dist.is_initialized():
@@ -64,6 +67,8 @@ def barrier():
 def all_reduce_max(x: float, device) -> float:
     if not dist.is_initialized():
         return x
+    if dist.get_backend() == "gloo":
+        device = "cpu"
     t = torch.tensor([x], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
@@ -72,6 +77,8 @@ def all_reduce_max(x: float, device) -> float:
 def all_reduce_sum(x: float, device) -> float:
     if not dist.is_initialized():
         return x
+    if dist.get_backend() == "gloo":
+        device = "cpu"
     t = torch.tensor([x], dtype=torch.float64, device=device)
     dist.all_reduce(t)
     return float(t.item())
@@ -82,6 +89,8 @@ def all_gather_rows(t: torch.Tensor, group=None) -> torch.Tensor:
     if not dist.is_initialized() or dist.get_world_size(group) == 1:
         return t
     w = dist.get_world_size(group)
+    if t.is_cuda and dist.get_backend(group) == "gloo":  # gloo rehearsal of GPU ranks: stage on the host
+        return all_gather_rows(t.cpu(), group).to(t.device)
     out = torch.empty((w * t.shape[0],) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
     dist.all_gather_into_tensor(out, t.contiguous(), group=group)
     return out
