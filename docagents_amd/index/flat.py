@@ -205,6 +205,18 @@ class FlatIndex:
         return out
 
     # ----------------------------------------------------------------- snapshot
+    def live_rows_by_doc(self):
+        """(rows grouped by document, [(doc_id, n_rows)]) for snapshots (removed docs dropped)."""
+        docs, rows = [], []
+        for d, e in self.docs.items():
+            n = 0
+            for a, b in e.ranges:
+                rows.append((a, b))
+                n += b - a
+            docs.append((d, n))
+        sel = np.concatenate([np.arange(a, b) for a, b in rows]) if rows else np.zeros(0, dtype=np.int64)
+        return sel.astype(np.int64), docs
+
     def state_dict(self) -> dict:
         live = []
         for d, e in self.docs.items():

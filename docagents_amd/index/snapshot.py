@@ -13,14 +13,8 @@ from safetensors.torch import load_file, save_file
 
 def save_index(index, path: str) -> str:
     with index.lock:
-        docs, rows = [], []
-        for d, e in index.docs.items():
-            n = 0
-            for a, b in e.ranges:
-                rows.append((a, b))
-                n += b - a
-            docs.append([d, n])
-        sel = np.concatenate([np.arange(a, b) for a, b in rows]) if rows else np.zeros(0, dtype=np.int64)
+        sel, docs = index.live_rows_by_doc()
+        docs = [[d, n] for d, n in docs]
         selt = torch.from_numpy(sel.astype(np.int64)).to(index.device)
         tensors = {"X": index.X.index_select(0, selt).cpu().contiguous(),
                    "ids": torch.from_numpy(index.ids[sel].copy())}

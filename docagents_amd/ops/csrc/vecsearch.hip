@@ -99,9 +99,9 @@ topk_dense_kernel(const bf16_t* __restrict__ X, int N, int d, const int* __restr
       const int row = r0 + rl;
       float s = acc[i];
       bool ok = row < rend && q < nq && s >= thr;
-      if (ok && bitmap) {
+      if (ok && slots) {  // removed rows (slot -1) never match; the bitmap (if any) filters documents
         const int sl = slots[row];
-        ok = sl >= 0 && (sl >> 5) < W && ((bitmap[(size_t)(qbase + q) * W + (sl >> 5)] >> (sl & 31)) & 1u);
+        ok = sl >= 0 && (!bitmap || ((sl >> 5) < W && ((bitmap[(size_t)(qbase + q) * W + (sl >> 5)] >> (sl & 31)) & 1u)));
       }
       sc[q * 65 + rl] = ok ? s : -INFINITY;
     }
@@ -182,9 +182,9 @@ topk_ranges_kernel(const bf16_t* __restrict__ X, int d, const int* __restrict__ 
         for (int o = 16; o > 0; o >>= 1) dot += __shfl_xor(dot, o, 64);
         if (l32 == 0) {
           bool ok = p < hi && dot >= thr;
-          if (ok && bitmap) {
+          if (ok && slots) {
             const int sl = slots[row];
-            ok = sl >= 0 && (sl >> 5) < W && ((bitmap[(size_t)q * W + (sl >> 5)] >> (sl & 31)) & 1u);
+            ok = sl >= 0 && (!bitmap || ((sl >> 5) < W && ((bitmap[(size_t)q * W + (sl >> 5)] >> (sl & 31)) & 1u)));
           }
           sc[rl] = ok ? dot : -INFINITY;
           sr[rl] = ok ? row : -1;

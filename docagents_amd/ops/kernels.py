@@ -434,9 +434,11 @@ def topk_dense(X, Qv, K: int, thr: float, slots=None, bitmap=None, rows_per_bloc
     _req(X.is_contiguous() and Qv.is_contiguous() and Qv.shape[1] == d, "X/Qv layout")
     _req(d % 32 == 0 and 1 <= K <= 32, "d % 32 and 1 <= K <= 32")
     W = 0
+    if slots is not None:
+        _i32(slots, "slots")
+        _req(slots.numel() >= N, "slots length")
     if bitmap is not None:
         _req(slots is not None, "bitmap needs slots")
-        _i32(slots, "slots")
         _req(bitmap.dtype == torch.int32 and bitmap.is_contiguous() and bitmap.shape[0] == Q, "bitmap [Q, W] int32")
         W = bitmap.shape[1]
     if rows_per_block is None:
@@ -463,8 +465,11 @@ def topk_ranges(X, Qv, ranges, range_off, K: int, thr: float, max_rows: int, slo
     _i32(ranges, "ranges"); _i32(range_off, "range_off")
     _req(range_off.numel() == Q + 1, "range_off length")
     W = 0
-    if bitmap is not None:
+    if slots is not None:
         _i32(slots, "slots")
+        _req(slots.numel() >= N, "slots length")
+    if bitmap is not None:
+        _req(slots is not None, "bitmap needs slots")
         _req(bitmap.dtype == torch.int32 and bitmap.shape[0] == Q, "bitmap")
         W = bitmap.shape[1]
     splits = max(1, math.ceil(max_rows / rows_per_split))

@@ -228,8 +228,10 @@ def sample(logits, temperature, seed, step=0, out_tok=None, out_lp=None, conf=No
 def topk_dense(X, Qv, K, thr, slots=None, bitmap=None, **_):
     s = Qv.float() @ X.float().t()  # [Q, N]
     valid = s >= thr
+    if slots is not None:
+        valid &= (slots[:X.shape[0]] >= 0).view(1, -1)
     if bitmap is not None:
-        sl = slots.long()
+        sl = slots[:X.shape[0]].long().clamp_min(0)
         words = bitmap[:, (sl >> 5)]  # [Q, N]
         bits = (words >> (sl & 31).view(1, -1)) & 1
         valid &= bits.bool()
@@ -268,8 +270,10 @@ def topk_ranges(X, Qv, ranges, range_off, K, thr, max_rows=None, slots=None, bit
             a, b = rg[r]
             allowed[q, a:b] = True
     valid = allowed & (s >= thr)
+    if slots is not None:
+        valid &= (slots[:N] >= 0).view(1, -1)
     if bitmap is not None:
-        sl = slots.long()
+        sl = slots[:N].long().clamp_min(0)
         bits = (bitmap[:, (sl >> 5)] >> (sl & 31).view(1, -1)) & 1
         valid &= bits.bool()
     s = s.masked_fill(~valid, float("-inf"))

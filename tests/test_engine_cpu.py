@@ -80,10 +80,41 @@ def test_ivf_recall_and_delta_rows():
     ix.add("late", np.arange(1800, 2000), X[1800:])  # delta region, scanned exactly
     Q = X[rng.choice(2000, 30, replace=False)]
     s, r = ix.search(Q, 5, -1.0, None)
-    rec = np.mean([len(set(np.argsort(-(X @ Q[i]).numpy())[:5]) & set(r[i].tolist())) / 5 for i in range(30)])
+    # rows are list-major after training: compare external ids
+    rec = np.mean([len(set(np.argsort(-(X @ Q[i]).numpy())[:5]) & set(ix.row_ids(r[i].numpy()).tolist())) / 5
+                   for i in range(30)])
     assert rec > 0.8
     s, r = ix.search(X[[1900]], 1, -1.0, [["late"]])
-    assert int(r[0, 0]) == 1900
+    assert int(ix.row_ids(r[0].numpy())[0]) == 1900
+    assert ix.remove_doc("d0") == 100
+    s, r = ix.search(X[:100], 5, -1.0, None)
+    assert all(i >= 100 for i in ix.row_ids(r.numpy().ravel()) if i >= 0)  # removed rows never match
+    rows, docs = ix.live_rows_by_doc()
+    assert len(rows) == 1900 and dict(docs)["late"] == 200 and "d0" not in dict(docs)
+
+
+def test_ivf_streaming_build_matches_exact_search():
+    dim, n = 64, 6000
+    cent = torch.nn.functional.normalize(torch.randn(40, dim, generator=torch.Generator().manual_seed(0)), dim=-1)
+
+    def gen(c, rows=1000):
+        g = torch.Generator().manual_seed(100 + c)
+        lab = torch.randint(0, 40, (rows,), generator=g)
+        x = cent[lab] + 0.15 * torch.randn(rows, dim, generator=g)
+        return torch.nn.functional.normalize(x, dim=-1).to(torch.bfloat16)
+
+    ix = IVFFlatIndex(dim, "cpu", lists=40, probes=6).build_streaming(gen, n, 1000, rows_per_doc=50, iters=5,
+                                                                      sample=4000)
+    assert len(ix) == n and int(ix.list_off[-1]) == n
+    Xall = torch.cat([gen(c) for c in range(6)]).float()
+    Q = Xall[torch.arange(0, n, 97)]
+    s, r = ix.search(Q, 10, -1.0, None)
+    rec = np.mean([len(set(torch.topk(Xall @ Q[i], 10).indices.tolist()) & set(ix.row_ids(r[i].numpy()).tolist()))
+                   / 10 for i in range(Q.shape[0])])
+    assert rec > 0.9, rec
+    s, r = ix.search(Q[:3], 5, -1.0, [["d7"]] * 3)  # doc filter: rows 350..399
+    ids = ix.row_ids(r.numpy().ravel())
+    assert all(350 <= i < 400 for i in ids if i >= 0) and (ids >= 0).sum() == 15
 
 
 def _port():
