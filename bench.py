@@ -82,6 +82,8 @@ def main():
     ap.add_argument("--latency-reps", type=int, default=5)
     ap.add_argument("--ingest-docs", type=int, default=16, help="docs per GPU for the ingest measurement")
     ap.add_argument("--ingest-words", type=int, default=2000)
+    ap.add_argument("--pdf-ingest", action="store_true",
+                    help="ingest synthetic PDFs (gateway PDF extraction in the timed path; BASELINE config 3)")
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--seed", type=int, default=0)
     a = ap.parse_args()
@@ -171,8 +173,18 @@ def main():
     if a.ingest_docs > 0:
         dg = TextGen(seed=500 + R)
         texts = [dg.document(a.ingest_words) for _ in range(a.ingest_docs)]
+        if a.pdf_ingest:
+            from docagents_amd.text.pdf import extract_text as pdf_text
+            from docagents_amd.text.pdf import make_pdf
+
+            def _pages(t, per=400):
+                w = t.split()
+                return [" ".join(w[i:i + per]) for i in range(0, len(w), per)]
+            texts = [make_pdf(_pages(t)) for t in texts]
 
         def ingest(texts, tag):
+            if a.pdf_ingest:
+                texts = [pdf_text(b) for b in texts]  # the gateway's PDF extraction (cmd/gateway/main.go:223-249)
             all_chunks, owners = [], []
             for j, t in enumerate(texts):
                 cs = chunk_text(t, Options(400, 80))
@@ -208,6 +220,7 @@ def main():
         "reference_cache_miss_ms": REFERENCE_CACHE_MISS_MS,
         "cache_miss_speedup_vs_reference": round(REFERENCE_CACHE_MISS_MS / p50, 2) if p50 else None,
         "ingest_docs_per_min": round(docs_per_min, 1) if docs_per_min else None,
+        "ingest_format": "pdf" if a.pdf_ingest else "txt",
         "prefill_tokens": gen["prefill_tokens"], "decode_steps": gen["decode_steps"],
     }
     if R == 0:
