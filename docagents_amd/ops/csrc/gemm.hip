@@ -251,6 +251,117 @@ gemm_splitk_reduce(const float* __restrict__ ws, int splits, int M, int N, int e
   }
 }
 
+// ------------------------------------------------------------------------------------------
+// GEMV (M = 1: the batch-1 decode step that sets cache-miss latency). Pure weight streaming:
+// every wave instruction loads 1 KiB of ONE weight row (64 lanes x 16 B, fully coalesced,
+// non-temporal), R rows x U k-blocks of loads are in flight per wave before any FMA, the 8-wide
+// dot products accumulate in fp32 per lane and each row is reduced across the wave once.
+// The activation row (K bf16) is read through the caches (every wave reads the same vector).
+// EPI_SWIGLU: a wave owns 2 gate rows and their 2 up rows (16-row interleave) -> 2 outputs.
+template <int EPI, int R>
+__global__ void __launch_bounds__(256)
+gemv_kernel(GemmArgs p) {
+  constexpr int U = 4;
+  static_assert(EPI != EPI_SWIGLU || R == 4, "SwiGLU waves own 2 gate + 2 up rows");
+  const int lane = threadIdx.x & 63;
+  const int wg = blockIdx.x * 4 + (threadIdx.x >> 6);  // global wave index
+  int rows[R];
+  if constexpr (EPI == EPI_SWIGLU) {
+    const int g = wg >> 3, t = wg & 7;
+#pragma unroll
+    for (int r = 0; r < R; ++r) rows[r] = g * 32 + 2 * t + (r & 1) + (r >> 1) * 16;
+  } else {
+#pragma unroll
+    for (int r = 0; r < R; ++r) rows[r] = wg * R + r;
+  }
+  if (rows[0] >= p.N) return;
+  const bf16_t* wr[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) wr[r] = p.W + (size_t)min(rows[r], p.N - 1) * p.K + lane * 8;
+  const bf16_t* ar = p.A + lane * 8;
+  const int nkb = p.K / 512;
+  float acc[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) acc[r] = 0.f;
+  for (int kb = 0; kb < nkb; kb += U) {
+    u32x4_t wv[U][R], av[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int k = min(kb + u, nkb - 1) * 512;
+#pragma unroll
+      for (int r = 0; r < R; ++r) wv[u][r] = __builtin_nontemporal_load((const u32x4_t*)(wr[r] + k));
+      av[u] = *(const u32x4_t*)(ar + k);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (kb + u >= nkb) break;
+      float a[8];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        a[2 * e] = bf2f((bf16_t)(av[u][e] & 0xffff));
+        a[2 * e + 1] = bf2f((bf16_t)(av[u][e] >> 16));
+      }
+#pragma unroll
+      for (int r = 0; r < R; ++r)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          acc[r] = fmaf(bf2f((bf16_t)(wv[u][r][e] & 0xffff)), a[2 * e], acc[r]);
+          acc[r] = fmaf(bf2f((bf16_t)(wv[u][r][e] >> 16)), a[2 * e + 1], acc[r]);
+        }
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < R; ++r) acc[r] = wave_sum(acc[r]);
+  if (lane != 0) return;
+  if constexpr (EPI == EPI_SWIGLU) {
+    const int g = wg >> 3, t = wg & 7;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int o = g * 16 + 2 * t + j;
+      if (o < p.N / 2) p.C[o] = f2bf(silu(acc[j]) * acc[2 + j]);
+    }
+  } else {
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const int n = rows[r];
+      if (n >= p.N) continue;
+      float v = acc[r];
+      if (p.bias) v += bf2f(p.bias[n]);
+      if constexpr (EPI == EPI_GELU) v = gelu_erf(v);
+      if constexpr (EPI == EPI_RESID) v += bf2f(p.resid[n]);
+      p.C[n] = f2bf(v);
+    }
+  }
+}
+
+template <int R>
+static int launch_gemv_r(const GemmArgs& a, int epi, hipStream_t s) {
+  const int waves = (a.N + R - 1) / R;
+  dim3 grid((waves + 3) / 4), block(256);
+  switch (epi) {
+    case EPI_NONE: gemv_kernel<EPI_NONE, R><<<grid, block, 0, s>>>(a); break;
+    case EPI_BIAS: gemv_kernel<EPI_BIAS, R><<<grid, block, 0, s>>>(a); break;
+    case EPI_GELU: gemv_kernel<EPI_GELU, R><<<grid, block, 0, s>>>(a); break;
+    case EPI_RESID: gemv_kernel<EPI_RESID, R><<<grid, block, 0, s>>>(a); break;
+    default: return (int)hipErrorInvalidValue;
+  }
+  return (int)hipGetLastError();
+}
+
+// Rows per wave: enough waves (>= ~4 per SIMD) that the loads in flight cover HBM latency on
+// narrow matrices, 4 rows per wave (more bytes per wave) on wide ones.
+static int launch_gemv(const GemmArgs& a, int epi, hipStream_t s) {
+  if (a.M != 1 || a.K % 512 || a.N % 4) return (int)hipErrorInvalidValue;
+  if (epi == EPI_SWIGLU) {
+    dim3 grid((a.N / 4 + 3) / 4), block(256);
+    gemv_kernel<EPI_SWIGLU, 4><<<grid, block, 0, s>>>(a);
+    return (int)hipGetLastError();
+  }
+  if (a.N >= 16384) return launch_gemv_r<4>(a, epi, s);
+  if (a.N >= 8192) return launch_gemv_r<2>(a, epi, s);
+  return launch_gemv_r<1>(a, epi, s);
+}
+
 template <int BM, int BN, int WM, int WN>
 static int launch_tile(const GemmArgs& a, int epi, int splits, hipStream_t s) {
   const int ntm = (a.M + BM - 1) / BM, ntn = (a.N + BN - 1) / BN;
@@ -268,7 +379,7 @@ static int launch_tile(const GemmArgs& a, int epi, int splits, hipStream_t s) {
 }
 
 // Tile selection: big tiles when the grid fills 256 CUs, skinny tiles (+ split-K) for decode-sized M.
-// tile: 0 = auto, 1 = 128x128, 2 = 64x128, 3 = 32x128.
+// tile: 0 = auto, 1 = 128x128, 2 = 64x128, 3 = 32x128, 4 = 256x256, 6 = GEMV (M = 1).
 DA_EXPORT int da_gemm_bf16(const void* A, int lda, const void* W, void* C, int ldc,
                            const void* bias, const void* resid, int ldr,
                            int M, int N, int K, int epi, int tile, int splits, void* ws,
@@ -291,6 +402,7 @@ DA_EXPORT int da_gemm_bf16(const void* A, int lda, const void* W, void* C, int l
     if (splits != 1) return (int)hipErrorInvalidValue;
     return launch_gemm256(a, epi, s);
   }
+  if (tile == 6) return launch_gemv(a, epi, s);
   int err;
   switch (tile) {
     case 1: err = launch_tile<128, 128, 2, 2>(a, epi, splits, s); break;

@@ -169,6 +169,8 @@ def gemm(a: torch.Tensor, w: torch.Tensor, bias=None, epi: int = EPI_NONE, resid
         ldr = resid.stride(0)
     if M == 0:
         return out
+    if tile == 0 and splits <= 0 and M == 1 and K % 512 == 0 and N % 4 == 0 and (epi != EPI_SWIGLU or N % 32 == 0):
+        tile, splits = 6, 1  # batch-1 decode: weight-streaming GEMV, one launch, no split-K workspace
     if splits <= 0:
         splits = _auto_splits(M, N, K)
     ws = None

@@ -318,3 +318,19 @@ def test_layernorm_fused_fp8_output():
     assert torch.allclose(ys, rs, rtol=1e-3)
     d = (yq.float() * ys[:, None] - rq.float() * rs[:, None]).abs()
     assert torch.all(d <= 0.13 * (rq.float() * rs[:, None]).abs() + 1e-3)
+
+
+@pytest.mark.parametrize("N,Kd", [(96, 512), (544, 3072), (1024, 8192), (32064, 3072)])
+@pytest.mark.parametrize("epi", [K.EPI_NONE, K.EPI_BIAS, K.EPI_RESID, K.EPI_SWIGLU])
+def test_gemv_batch1_decode(N, Kd, epi):
+    torch.manual_seed(N + Kd + epi)
+    if epi == K.EPI_SWIGLU:
+        N = (N // 32) * 32
+    a, w = _rand(1, Kd), _rand(N, Kd, scale=Kd ** -0.5)
+    bias = _rand(N) if epi in (K.EPI_BIAS, K.EPI_RESID) else None
+    resid = _rand(1, N) if epi == K.EPI_RESID else None
+    got = K.gemm(a, w, bias=bias, epi=epi, resid=resid, tile=6, splits=1)
+    ref = R.gemm(a, w, bias=bias, epi=epi, resid=resid)
+    _close(got, ref, atol=0.03)
+    auto = K.gemm(a, w, bias=bias, epi=epi, resid=resid)  # M = 1 auto-selects the GEMV
+    assert torch.equal(auto, got)
