@@ -167,8 +167,11 @@ class LlamaDecoder:
         else:
             o.gemm(a, L["wo"], out=x)
         tp.all_reduce_(x)
-        h = o.rmsnorm(x, L["ln_mlp"], self.cfg.eps)
-        g = o.gemm(h, L["w_gu"], epi=EPI_SWIGLU)
+        if o.gemv_fusable(x.shape[0], L["w_gu"].shape[0], x.shape[1], EPI_SWIGLU):  # batch 1: norm fused
+            g = o.gemm(x, L["w_gu"], epi=EPI_SWIGLU, rms=(L["ln_mlp"], self.cfg.eps))
+        else:
+            h = o.rmsnorm(x, L["ln_mlp"], self.cfg.eps)
+            g = o.gemm(h, L["w_gu"], epi=EPI_SWIGLU)
         if tp.size == 1 or tp.rank == 0:
             o.gemm(g, L["w_down"], epi=EPI_RESID, resid=x, out=x)
         else:
@@ -178,8 +181,11 @@ class LlamaDecoder:
 
     def _logits(self, hlast):
         o = self.ops
-        h = o.rmsnorm(hlast, self.w["norm"], self.cfg.eps)
-        logits = o.gemm(h, self.w["lm_head"])
+        if o.gemv_fusable(hlast.shape[0], self.w["lm_head"].shape[0], hlast.shape[1]):
+            logits = o.gemm(hlast.contiguous(), self.w["lm_head"], rms=(self.w["norm"], self.cfg.eps))
+        else:
+            h = o.rmsnorm(hlast, self.w["norm"], self.cfg.eps)
+            logits = o.gemm(h, self.w["lm_head"])
         return self.tp.all_gather_cols(logits)
 
     # ------------------------------------------------------------- prefill
@@ -204,9 +210,13 @@ class LlamaDecoder:
         c, o, cache = self.cfg, self.ops, self.cache
         D, hl, kl = c.head_dim, self.hl, self.kl
         x = o.embed(st.tokens, self.w["embed"], out=st.x)
+        fuse = o.gemv_fusable(x.shape[0], self.w["layers"][0]["wqkv"].shape[0], x.shape[1])
         for li, L in enumerate(self.w["layers"]):
-            h = o.rmsnorm(x, L["ln_attn"], c.eps, out=st.h)
-            qkv = o.gemm(h, L["wqkv"], out=st.qkv)
+            if fuse:  # batch 1: RMSNorm folded into the QKV GEMV (no separate norm launch)
+                qkv = o.gemm(x, L["wqkv"], out=st.qkv, rms=(L["ln_attn"], c.eps))
+            else:
+                h = o.rmsnorm(x, L["ln_attn"], c.eps, out=st.h)
+                qkv = o.gemm(h, L["wqkv"], out=st.qkv)
             o.rope_cache(qkv, st.pos, self.cos_sin, hl, kl, D, slot=st.slot, k_cache=cache.k(li), v_cache=cache.v(li))
             a = o.decode_attn(qkv, cache.k(li), cache.v(li), st.lens, st.slot, hl, kl, D, max_len=cache.max_seq,
                               out=st.attn)

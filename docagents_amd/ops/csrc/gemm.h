@@ -16,6 +16,7 @@ struct GemmArgs {
   const bf16_t* bias; const bf16_t* resid; float* ws;
   int M, N, K, lda, ldc, ldr, k_per_split;
   const float* sa; const float* sw;  // fp8 path: per-row (A) and per-output-channel (W) scales
+  const bf16_t* gamma; float eps;    // GEMV only: fused RMSNorm of the input row (gamma != null)
 };
 
 // large-tile (256x256, 8 waves, LDS-DMA staged) path; returns hipError_t.

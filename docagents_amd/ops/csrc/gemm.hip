@@ -279,18 +279,21 @@ gemv_kernel(GemmArgs p) {
 #pragma unroll
   for (int r = 0; r < R; ++r) wr[r] = p.W + (size_t)min(rows[r], p.N - 1) * p.K + lane * 8;
   const bf16_t* ar = p.A + lane * 8;
+  const bf16_t* gr = p.gamma ? p.gamma + lane * 8 : nullptr;
   const int nkb = p.K / 512;
   float acc[R];
 #pragma unroll
   for (int r = 0; r < R; ++r) acc[r] = 0.f;
+  float ss = 0.f;  // fused RMSNorm: sum of squares of the raw input row (every wave sees all of it)
   for (int kb = 0; kb < nkb; kb += U) {
-    u32x4_t wv[U][R], av[U];
+    u32x4_t wv[U][R], av[U], gv[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int k = min(kb + u, nkb - 1) * 512;
 #pragma unroll
       for (int r = 0; r < R; ++r) wv[u][r] = __builtin_nontemporal_load((const u32x4_t*)(wr[r] + k));
       av[u] = *(const u32x4_t*)(ar + k);
+      if (gr) gv[u] = *(const u32x4_t*)(gr + k);
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -300,6 +303,14 @@ gemv_kernel(GemmArgs p) {
       for (int e = 0; e < 4; ++e) {
         a[2 * e] = bf2f((bf16_t)(av[u][e] & 0xffff));
         a[2 * e + 1] = bf2f((bf16_t)(av[u][e] >> 16));
+      }
+      if (gr) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          ss = fmaf(a[2 * e], a[2 * e], fmaf(a[2 * e + 1], a[2 * e + 1], ss));
+          a[2 * e] *= bf2f((bf16_t)(gv[u][e] & 0xffff));
+          a[2 * e + 1] *= bf2f((bf16_t)(gv[u][e] >> 16));
+        }
       }
 #pragma unroll
       for (int r = 0; r < R; ++r)
@@ -312,6 +323,11 @@ gemv_kernel(GemmArgs p) {
   }
 #pragma unroll
   for (int r = 0; r < R; ++r) acc[r] = wave_sum(acc[r]);
+  if (gr) {
+    const float inv = rsqrtf(wave_sum(ss) / p.K + p.eps);
+#pragma unroll
+    for (int r = 0; r < R; ++r) acc[r] *= inv;
+  }
   if (lane != 0) return;
   if constexpr (EPI == EPI_SWIGLU) {
     const int g = wg >> 3, t = wg & 7;
@@ -383,7 +399,7 @@ static int launch_tile(const GemmArgs& a, int epi, int splits, hipStream_t s) {
 DA_EXPORT int da_gemm_bf16(const void* A, int lda, const void* W, void* C, int ldc,
                            const void* bias, const void* resid, int ldr,
                            int M, int N, int K, int epi, int tile, int splits, void* ws,
-                           void* stream) {
+                           const void* rms_gamma, float rms_eps, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   if (K % 64 || N % 8 || lda % 8 || ldc % 8) return (int)hipErrorInvalidValue;
   if (epi == EPI_SWIGLU && N % 32) return (int)hipErrorInvalidValue;
@@ -394,6 +410,8 @@ DA_EXPORT int da_gemm_bf16(const void* A, int lda, const void* W, void* C, int l
   a.A = (const bf16_t*)A; a.W = (const bf16_t*)W; a.C = (bf16_t*)C;
   a.bias = (const bf16_t*)bias; a.resid = (const bf16_t*)resid; a.ws = (float*)ws;
   a.M = M; a.N = N; a.K = K; a.lda = lda; a.ldc = ldc; a.ldr = ldr; a.k_per_split = K / splits;
+  a.gamma = (const bf16_t*)rms_gamma; a.eps = rms_eps;
+  if (rms_gamma && tile != 6) return (int)hipErrorInvalidValue;  // fused RMSNorm: GEMV path only
   if (tile == 0) {
     const long t256 = (long)((M + 255) / 256) * ((N + 255) / 256);
     tile = (M <= 32) ? 3 : (M <= 64 ? 2 : (t256 >= 256 && splits == 1 ? 4 : 1));

@@ -27,7 +27,7 @@ c_void_p, c_int, c_float, c_uint, c_size_t = (ctypes.c_void_p, ctypes.c_int, cty
 
 _SIGS = {
     "da_gemm_bf16": [c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int,
-                     c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p],
+                     c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_float, c_void_p],
     "da_gemm_fp8": [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int,
                     c_int, c_int, c_int, c_int, c_void_p],
     "da_quant_fp8_rows": [c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p],
@@ -138,9 +138,16 @@ def _workspace(nbytes: int, device) -> torch.Tensor:
     return buf
 
 
+def gemv_fusable(M: int, N: int, K: int, epi: int = EPI_NONE) -> bool:
+    """True when gemm() runs the batch-1 GEMV (which can also fuse the input RMSNorm)."""
+    return M == 1 and K % 512 == 0 and N % 4 == 0 and (epi != EPI_SWIGLU or N % 32 == 0)
+
+
 def gemm(a: torch.Tensor, w: torch.Tensor, bias=None, epi: int = EPI_NONE, resid=None, out=None,
-         tile: int = 0, splits: int = 0) -> torch.Tensor:
-    """out[M, N'] = epi(a[M, K] @ w[N, K]^T). N' = N/2 for EPI_SWIGLU (w rows interleaved by 16)."""
+         tile: int = 0, splits: int = 0, rms=None) -> torch.Tensor:
+    """out[M, N'] = epi(a[M, K] @ w[N, K]^T). N' = N/2 for EPI_SWIGLU (w rows interleaved by 16).
+    rms = (gamma, eps): ``a`` is the raw residual stream and RMSNorm(a) * gamma is fused into the
+    GEMV (M == 1 only, see gemv_fusable)."""
     _bf16_cuda(a, "a"); _bf16_cuda(w, "w")
     _req(a.dim() == 2 and w.dim() == 2, "gemm expects 2-D operands")
     M, K = a.shape
@@ -169,15 +176,19 @@ def gemm(a: torch.Tensor, w: torch.Tensor, bias=None, epi: int = EPI_NONE, resid
         ldr = resid.stride(0)
     if M == 0:
         return out
-    if tile == 0 and splits <= 0 and M == 1 and K % 512 == 0 and N % 4 == 0 and (epi != EPI_SWIGLU or N % 32 == 0):
+    if tile == 0 and splits <= 0 and gemv_fusable(M, N, K, epi):
         tile, splits = 6, 1  # batch-1 decode: weight-streaming GEMV, one launch, no split-K workspace
+    gamma, eps = (None, 0.0) if rms is None else rms
+    if gamma is not None:
+        _req(tile == 6, "fused RMSNorm needs the M == 1 GEMV path")
+        _bf16_cuda(gamma, "gamma"); _req(gamma.numel() == K, "gamma must be [K]")
     if splits <= 0:
         splits = _auto_splits(M, N, K)
     ws = None
     if splits > 1:
         ws = _workspace(splits * M * N * 4, a.device)
     rc = lib().da_gemm_bf16(_ptr(a), a.stride(0), _ptr(w), _ptr(out), out.stride(0), _ptr(bias), _ptr(resid), ldr,
-                            M, N, K, epi, tile, splits, _ptr(ws), _stream())
+                            M, N, K, epi, tile, splits, _ptr(ws), _ptr(gamma), float(eps), _stream())
     _check(rc, "gemm")
     return out
 

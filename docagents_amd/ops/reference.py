@@ -14,7 +14,13 @@ import torch.nn.functional as F
 EPI_NONE, EPI_BIAS, EPI_GELU, EPI_SWIGLU, EPI_RESID = 0, 1, 2, 3, 4
 
 
-def gemm(a, w, bias=None, epi=EPI_NONE, resid=None, out=None, **_):
+def gemv_fusable(M, N, K, epi=EPI_NONE):
+    return M == 1
+
+
+def gemm(a, w, bias=None, epi=EPI_NONE, resid=None, out=None, rms=None, **_):
+    if rms is not None:  # same numerics as rmsnorm() followed by gemm() (bf16 normalised row)
+        a = rmsnorm(a, rms[0], rms[1])
     return _epilogue(a.float() @ w.float().t(), w.shape[0], bias, epi, resid, out)
 
 

@@ -334,3 +334,15 @@ def test_gemv_batch1_decode(N, Kd, epi):
     _close(got, ref, atol=0.03)
     auto = K.gemm(a, w, bias=bias, epi=epi, resid=resid)  # M = 1 auto-selects the GEMV
     assert torch.equal(auto, got)
+
+
+@pytest.mark.parametrize("N,Kd,epi", [(9216, 3072, K.EPI_NONE), (1024, 3072, K.EPI_SWIGLU), (32064, 3072, K.EPI_NONE)])
+def test_gemv_fused_rmsnorm(N, Kd, epi):
+    torch.manual_seed(N)
+    x = _rand(1, Kd, scale=3.0)
+    g = _rand(Kd) + 1.0
+    w = _rand(N, Kd, scale=Kd ** -0.5)
+    got = K.gemm(x, w, epi=epi, rms=(g, 1e-5))
+    unfused = K.gemm(K.rmsnorm(x, g, 1e-5), w, epi=epi, tile=6, splits=1)
+    _close(got, unfused, atol=0.03)
+    _close(got, R.gemm(x, w, epi=epi, rms=(g, 1e-5)), atol=0.03)
