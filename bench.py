@@ -80,7 +80,8 @@ def main():
     ap.add_argument("--enc", default="bge-base")
     ap.add_argument("--llm", default="phi3-mini")
     ap.add_argument("--latency-reps", type=int, default=5)
-    ap.add_argument("--ingest-docs", type=int, default=16, help="docs per GPU for the ingest measurement")
+    ap.add_argument("--ingest-docs", type=int, default=64,
+                    help="docs per GPU for the ingest measurement (one engine batch, like the QA batch)")
     ap.add_argument("--ingest-words", type=int, default=2000)
     ap.add_argument("--pdf-ingest", action="store_true",
                     help="ingest synthetic PDFs (gateway PDF extraction in the timed path; BASELINE config 3)")

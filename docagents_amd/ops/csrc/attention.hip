@@ -370,6 +370,7 @@ decode_attn_kernel(const bf16_t* __restrict__ q, int ldq, const bf16_t* __restri
 
   const int split = blockIdx.x, hk = blockIdx.y, b = blockIdx.z;
   const int L = lens[b];
+  DA_ASSERT(L >= 0 && L <= max_seq && slot[b] >= 0);
   const int kstart = split * chunk;
   const int kend = min(L, kstart + chunk);
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -570,6 +571,7 @@ decode_attn_gqa_kernel(const bf16_t* __restrict__ q, int ldq, const bf16_t* __re
 
   const int split = blockIdx.x, hk = blockIdx.y, b = blockIdx.z;
   const int L = lens[b];
+  DA_ASSERT(L >= 0 && L <= max_seq && slot[b] >= 0);
   const int kstart = split * chunk;
   const int kend = min(L, kstart + chunk);
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;

@@ -12,9 +12,13 @@
 
 #define DA_WAVE 64
 
+// Debug builds (python -m docagents_amd.ops.build --debug: -O1 -g -DDA_DEBUG) turn DA_ASSERT into
+// device asserts at the kernels' indexing hot spots (cache slots / positions, top-k rows, ranges),
+// for fault isolation together with AMD_SERIALIZE_KERNEL=3.
 #ifndef DA_DEBUG
 #define DA_ASSERT(x) ((void)0)
 #else
+#include <cassert>
 #define DA_ASSERT(x) assert(x)
 #endif
 

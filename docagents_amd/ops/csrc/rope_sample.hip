@@ -30,6 +30,7 @@ rope_cache_kernel(bf16_t* __restrict__ qkv, const int* __restrict__ pos, const i
   const int ld = (H + 2 * Hkv) * D;
   bf16_t* row = qkv + (size_t)t * ld;
   const int s = slot ? slot[t] : 0;
+  DA_ASSERT(p >= 0 && (!kc || p < max_seq) && s >= 0);
   if (w < nrot) {
     const int hh = w / groups, gq = w % groups;
     const int head = rotate_q ? hh : H + hh;  // head index within q|k region

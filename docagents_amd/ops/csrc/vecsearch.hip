@@ -150,6 +150,7 @@ topk_ranges_kernel(const bf16_t* __restrict__ X, int d, const int* __restrict__ 
     }
   }
   const int rb = range_off[q], re = range_off[q + 1];
+  DA_ASSERT(rb >= 0 && re >= rb);
   const int pbeg = split * rows_per_split, pend = pbeg + rows_per_split;
   __syncthreads();
   // walk the concatenated ranges; position p counts rows across this query's ranges

@@ -155,3 +155,20 @@ def test_kvserver_cache_client(kvserver):
         assert await c._cmd("DBSIZE") == 1
         await c.close()
     asyncio.run(go())
+
+
+def test_kernel_debug_build_compiles(tmp_path):
+    """The DA_DEBUG (device-assert) variant of the kernels cross-compiles for gfx950."""
+    import shutil
+    import subprocess
+
+    import pytest
+
+    from docagents_amd.ops import build as B
+    hipcc = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
+    if not os.path.exists(hipcc):
+        pytest.skip("hipcc not available")
+    src = B.CSRC / "rope_sample.hip"
+    r = subprocess.run([hipcc, *B._flags(True), "-c", str(src), "-o", str(tmp_path / "dbg.o")],
+                       capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-2000:]

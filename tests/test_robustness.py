@@ -128,3 +128,34 @@ def test_fault_spec_parsing():
         faults.maybe_fail("cache.get")
     finally:
         faults.configure(None)
+
+
+def test_concurrent_pipeline_under_asyncio_debug(tmp_path, monkeypatch):
+    """the ingest pipeline under asyncio debug mode with coroutine/resource warnings
+    promoted to errors (a never-awaited coroutine or an un-closed resource fails the test)."""
+    import warnings
+    monkeypatch.setattr(inproc_mod, "next_retry", _fast_retry)
+
+    async def go():
+        d, bus = _stack(tmp_path)
+        stop = asyncio.Event()
+        ws = await _run_workers(d, bus, 2, stop)
+        docs = []
+        for i in range(12):
+            doc = await d.store.create_document(f"g{i}.txt")
+            docs.append(doc.id)
+            await d.queue.enqueue(Task(type=TASK_PARSE, payload=json.dumps(
+                {"document_id": doc.id, "filename": f"g{i}.txt", "content": "w " * 500}).encode()))
+        for _ in range(400):
+            st = [(await d.store.get_document(x)).status for x in docs]
+            if all(v == "ready" for v in st):
+                break
+            await asyncio.sleep(0.02)
+        stop.set()
+        await asyncio.gather(*ws)
+        return [(await d.store.get_document(x)).status for x in docs]
+
+    with warnings.catch_warnings():
+        warnings.simplefilter("error", RuntimeWarning)
+        statuses = asyncio.run(go(), debug=True)
+    assert statuses == ["ready"] * 12
