@@ -41,11 +41,15 @@ def main():
         cu = torch.arange(0, T + 1, L, device=dev, dtype=torch.int32)
         fl = 4 * B * L * L * H * D * (0.5 if causal else 1.0)
         r = {}
-        for impl in ("v1", "v2"):
+        for impl in ("v1", "v2", "v2w8"):
             if impl == "v1" and D == 32:
                 continue
-            t = timeit(lambda: K.flash_attn_varlen(q, k, v, cu, L, H, Hkv, D, causal, impl=impl))
+            K.lib().da_set_flash_waves(8 if impl == "v2w8" else 4)
+            t = timeit(lambda: K.flash_attn_varlen(q, k, v, cu, L, H, Hkv, D, causal, impl=impl[:2]))
             r[impl + "_ms"], r[impl + "_tflops"] = t, fl / t / 1e9
+        K.lib().da_set_flash_waves(8)
+        o8 = K.flash_attn_varlen(q, k, v, cu, L, H, Hkv, D, causal, impl="v2").float()
+        K.lib().da_set_flash_waves(0)
         qq = q.reshape(B, L, H, D).transpose(1, 2)
         kk = k.reshape(B, L, Hkv, D).transpose(1, 2).repeat_interleave(H // Hkv, 1)
         vv = v.reshape(B, L, Hkv, D).transpose(1, 2).repeat_interleave(H // Hkv, 1)
@@ -55,6 +59,7 @@ def main():
         o2 = torch.nn.functional.scaled_dot_product_attention(qq, kk, vv, is_causal=causal)
         o2 = o2.transpose(1, 2).reshape(T, H * D).float()
         r["max_err_vs_sdpa"] = (o1 - o2).abs().max().item()
+        r["w8_vs_w4_maxdiff"] = (o8 - o1).abs().max().item()
         res[name] = r
         print(name, json.dumps(r), flush=True)
     if a.out:

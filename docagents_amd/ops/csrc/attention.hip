@@ -167,24 +167,23 @@ flash_attn_varlen_kernel(const bf16_t* __restrict__ q, const bf16_t* __restrict_
 //   scale·log2(e) is folded into the exp2 argument (one FMA per score); the O rescale is skipped
 //   when no lane's running max moved; causal tiles past a wave's last query are skipped by that
 //   wave (it still stages tiles and joins the barrier).
-template <int D>
+template <int D, int NW = 4>
 struct FA2Cfg {
-  static constexpr int KT = 64, QW = 32, QB = 128;
+  static constexpr int KT = 64, QW = 32, QB = 32 * NW, NT = 64 * NW;
   static constexpr int KSTR = D * 2 + 16;                                         // bytes
   static constexpr int VSTR = (D == 64) ? 192 : (D == 128) ? 320 : D * 2;         // bytes
   static constexpr int KBUF = KT * KSTR, VBUF = KT * VSTR;
-  static constexpr int CPR = D / 8, LPT = KT * CPR / 256;
+  static constexpr int CPR = D / 8, LPT = (KT * CPR + NT - 1) / NT;
   static constexpr int SMEM = 2 * (KBUF + VBUF);
 };
 
-template <int D>
-__global__ void __launch_bounds__(256, 2)
+template <int D, int NW>
+__global__ void __launch_bounds__(64 * NW, 8 / NW)
 flash_attn_v2_kernel(const bf16_t* __restrict__ q, const bf16_t* __restrict__ k, const bf16_t* __restrict__ v,
                      int ldq, int ldk, int ldv, const int* __restrict__ cu, int H, int Hkv, int causal,
                      float c, bf16_t* __restrict__ o, int ldo) {
-  using C = FA2Cfg<D>;
-  constexpr int KT = C::KT, NDS = D / 16, NDB = D / 32, CPR = C::CPR, LPT = C::LPT;
-  static_assert(LPT * 256 == KT * CPR, "tile chunks must split evenly over 256 threads");
+  using C = FA2Cfg<D, NW>;
+  constexpr int KT = C::KT, NDS = D / 16, NDB = D / 32, CPR = C::CPR, LPT = C::LPT, NT = C::NT;
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
   const int b = blockIdx.z, h = blockIdx.y;
@@ -221,8 +220,8 @@ flash_attn_v2_kernel(const bf16_t* __restrict__ q, const bf16_t* __restrict__ k,
   auto load_tile = [&](int t) {
 #pragma unroll
     for (int i = 0; i < LPT; ++i) {
-      const int idx = tid + 256 * i, r = idx / CPR, cc = idx % CPR, key = t * KT + r;
-      if (key < L) {
+      const int idx = tid + NT * i, r = idx / CPR, cc = idx % CPR, key = t * KT + r;
+      if (idx < KT * CPR && key < L) {
         kst[i] = *(const u32x4_t*)(kbase_p + (size_t)key * ldk + cc * 8);
         vst[i] = *(const u32x4_t*)(vbase_p + (size_t)key * ldv + cc * 8);
       } else {
@@ -236,9 +235,11 @@ flash_attn_v2_kernel(const bf16_t* __restrict__ q, const bf16_t* __restrict__ k,
     char* sV = sK + C::KBUF;
 #pragma unroll
     for (int i = 0; i < LPT; ++i) {
-      const int idx = tid + 256 * i, r = idx / CPR, cc = idx % CPR;
-      *(u32x4_t*)(sK + r * C::KSTR + cc * 16) = kst[i];
-      *(u32x4_t*)(sV + r * C::VSTR + cc * 16) = vst[i];
+      const int idx = tid + NT * i, r = idx / CPR, cc = idx % CPR;
+      if (idx < KT * CPR) {
+        *(u32x4_t*)(sK + r * C::KSTR + cc * 16) = kst[i];
+        *(u32x4_t*)(sV + r * C::VSTR + cc * 16) = vst[i];
+      }
     }
   };
 
@@ -818,29 +819,44 @@ DA_EXPORT int da_decode_attn(const void* q, int ldq, const void* k_cache, const 
   DA_LAUNCH_CHECK();
 }
 
+// Waves per workgroup: 0 = auto (8 waves x 32 queries for bidirectional encoders, where a K/V tile
+// staged once serves 256 queries; 4 for causal prefill, where a taller query block wastes more
+// work on the diagonal — profiles/attn_v2_waves_r1.json). 4 / 8 force a shape (A/B runs).
+static int g_fa_waves = 0;
+DA_EXPORT void da_set_flash_waves(int nw) { g_fa_waves = nw; }
+
+template <int NW>
+static int launch_fa2(const void* q, const void* k, const void* v, int ldq, int ldk, int ldv, const void* cu_seqlens,
+                      int B, int max_seqlen, int H, int Hkv, int D, int causal, float sl2e, void* o, int ldo,
+                      hipStream_t s) {
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute((const void*)flash_attn_v2_kernel<128, NW>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              FA2Cfg<128, NW>::SMEM);
+    attr_set = true;
+  }
+  dim3 grid((max_seqlen + 32 * NW - 1) / (32 * NW), H, B);
+#define FA_ARGS (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, ldq, ldk, ldv, (const int*)cu_seqlens, H, Hkv, \
+                causal, sl2e, (bf16_t*)o, ldo
+  switch (D) {
+    case 32: flash_attn_v2_kernel<32, NW><<<grid, 64 * NW, FA2Cfg<32, NW>::SMEM, s>>>(FA_ARGS); break;
+    case 64: flash_attn_v2_kernel<64, NW><<<grid, 64 * NW, FA2Cfg<64, NW>::SMEM, s>>>(FA_ARGS); break;
+    case 96: flash_attn_v2_kernel<96, NW><<<grid, 64 * NW, FA2Cfg<96, NW>::SMEM, s>>>(FA_ARGS); break;
+    case 128: flash_attn_v2_kernel<128, NW><<<grid, 64 * NW, FA2Cfg<128, NW>::SMEM, s>>>(FA_ARGS); break;
+    default: return (int)hipErrorInvalidValue;
+  }
+#undef FA_ARGS
+  return (int)hipGetLastError();
+}
+
 DA_EXPORT int da_flash_attn_v2(const void* q, const void* k, const void* v, int ldq, int ldk, int ldv,
                                const void* cu_seqlens, int B, int max_seqlen, int H, int Hkv, int D, int causal,
                                float scale, void* o, int ldo, void* stream) {
   if (H % Hkv || ldq % 8 || ldk % 8 || ldv % 8 || ldo % 4) return (int)hipErrorInvalidValue;
   if (B == 0 || max_seqlen == 0) return 0;
-  dim3 grid((max_seqlen + 127) / 128, H, B);
   const float sl2e = scale * 1.4426950408889634f;
   hipStream_t s = (hipStream_t)stream;
-  static bool attr_set = false;
-  if (!attr_set) {
-    (void)hipFuncSetAttribute((const void*)flash_attn_v2_kernel<128>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                        FA2Cfg<128>::SMEM);
-    attr_set = true;
-  }
-#define FA_ARGS (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, ldq, ldk, ldv, (const int*)cu_seqlens, H, Hkv, \
-                causal, sl2e, (bf16_t*)o, ldo
-  switch (D) {
-    case 32: flash_attn_v2_kernel<32><<<grid, 256, FA2Cfg<32>::SMEM, s>>>(FA_ARGS); break;
-    case 64: flash_attn_v2_kernel<64><<<grid, 256, FA2Cfg<64>::SMEM, s>>>(FA_ARGS); break;
-    case 96: flash_attn_v2_kernel<96><<<grid, 256, FA2Cfg<96>::SMEM, s>>>(FA_ARGS); break;
-    case 128: flash_attn_v2_kernel<128><<<grid, 256, FA2Cfg<128>::SMEM, s>>>(FA_ARGS); break;
-    default: return (int)hipErrorInvalidValue;
-  }
-#undef FA_ARGS
-  DA_LAUNCH_CHECK();
+  if (g_fa_waves == 8 || (g_fa_waves == 0 && !causal))
+    return launch_fa2<8>(q, k, v, ldq, ldk, ldv, cu_seqlens, B, max_seqlen, H, Hkv, D, causal, sl2e, o, ldo, s);
+  return launch_fa2<4>(q, k, v, ldq, ldk, ldv, cu_seqlens, B, max_seqlen, H, Hkv, D, causal, sl2e, o, ldo, s);
 }

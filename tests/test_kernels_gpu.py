@@ -1,6 +1,8 @@
 """Numerics of every gfx950 HIP kernel vs the plain-PyTorch fp32 reference of the same op."""
 import math
 
+import numpy as np
+
 import pytest
 import torch
 
@@ -346,3 +348,20 @@ def test_gemv_fused_rmsnorm(N, Kd, epi):
     unfused = K.gemm(K.rmsnorm(x, g, 1e-5), w, epi=epi, tile=6, splits=1)
     _close(got, unfused, atol=0.03)
     _close(got, R.gemm(x, w, epi=epi, rms=(g, 1e-5)), atol=0.03)
+
+
+@pytest.mark.parametrize("nw", [4, 8])
+@pytest.mark.parametrize("D,causal", [(64, False), (96, True), (128, True), (32, False)])
+def test_flash_attn_wave_shapes(nw, D, causal):
+    torch.manual_seed(D + nw)
+    lens = [1, 77, 300, 513]
+    H, Hkv = 4, 2
+    T = sum(lens)
+    q, k, v = _rand(T, H * D), _rand(T, Hkv * D), _rand(T, Hkv * D)
+    cu = torch.tensor([0] + list(np.cumsum(lens)), device=DEV, dtype=torch.int32)
+    K.lib().da_set_flash_waves(nw)
+    try:
+        got = K.flash_attn_varlen(q, k, v, cu, max(lens), H, Hkv, D, causal)
+    finally:
+        K.lib().da_set_flash_waves(0)
+    _close(got, R.flash_attn_varlen(q, k, v, cu, max(lens), H, Hkv, D, causal), atol=0.02)
