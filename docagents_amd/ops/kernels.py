@@ -47,6 +47,7 @@ _SIGS = {
                              c_int, c_int, c_int, c_int, c_float, c_void_p, c_int, c_void_p],
     "da_set_gqa_mfma": [c_int],
     "da_set_flash_waves": [c_int],
+    "da_set_gemm_pingpong": [c_int],
     "da_decode_attn": [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
                        c_int, c_int, c_int, c_float, c_void_p, c_void_p, c_int, c_void_p],
     "da_topk_dense": [c_void_p, c_int, c_int, c_void_p, c_void_p, c_int, c_void_p, c_int, c_float, c_int,

@@ -22,14 +22,14 @@ for M,N,Kd in [(4096,9216,3072),(32768,9216,3072),(32768,16384,3072),(32768,3072
     out=[]
     ref=None
     for sch in range(2):
-        K.lib().da_set_gemm_ring(sch)
+        K.lib().da_set_gemm_pingpong(sch)
         tf=fl/t(lambda: K.gemm(x,w,tile=4,splits=1))/1e9
         o=K.gemm(x,w,tile=4,splits=1).float()
         ref = o if ref is None else ref
         out.append(f"s{sch}={tf:.0f}({(o-ref).abs().max().item():.1g})")
         tf=fl/t(lambda: K.gemm(x,w,epi=K.EPI_SWIGLU,tile=4,splits=1))/1e9
         out.append(f"sw{sch}={tf:.0f}")
-    K.lib().da_set_gemm_ring(0)
+    K.lib().da_set_gemm_pingpong(0)
     tt=fl/t(lambda: torch.matmul(x,w.t()))/1e9
     print(f"M={M} N={N} K={Kd} " + " ".join(out) + f" hipblaslt={tt:.0f}", flush=True)
 PY

@@ -365,3 +365,22 @@ def test_flash_attn_wave_shapes(nw, D, causal):
     finally:
         K.lib().da_set_flash_waves(0)
     _close(got, R.flash_attn_varlen(q, k, v, cu, max(lens), H, Hkv, D, causal), atol=0.02)
+
+
+@pytest.mark.parametrize("M,N,Kd", [(256, 256, 64), (300, 520, 192), (1000, 1032, 768), (2048, 3072, 3072)])
+@pytest.mark.parametrize("epi", [K.EPI_NONE, K.EPI_BIAS, K.EPI_RESID, K.EPI_SWIGLU])
+def test_gemm256_pingpong(M, N, Kd, epi):
+    torch.manual_seed(M * 3 + N + epi)
+    if epi == K.EPI_SWIGLU:
+        N = (N // 32) * 32
+    a, w = _rand(M, Kd), _rand(N, Kd, scale=Kd ** -0.5)
+    bias = _rand(N) if epi in (K.EPI_BIAS, K.EPI_RESID) else None
+    resid = _rand(M, N) if epi == K.EPI_RESID else None
+    K.lib().da_set_gemm_pingpong(0)
+    try:
+        lockstep = K.gemm(a, w, bias=bias, epi=epi, resid=resid, tile=4, splits=1)
+    finally:
+        K.lib().da_set_gemm_pingpong(1)
+    got = K.gemm(a, w, bias=bias, epi=epi, resid=resid, tile=4, splits=1)
+    _close(got, R.gemm(a, w, bias=bias, epi=epi, resid=resid), atol=0.04)
+    assert torch.equal(got, lockstep)  # same K order -> bit-identical
