@@ -184,6 +184,7 @@ flash_attn_v2_kernel(const bf16_t* __restrict__ q, const bf16_t* __restrict__ k,
                      float c, bf16_t* __restrict__ o, int ldo) {
   using C = FA2Cfg<D, NW>;
   constexpr int KT = C::KT, NDS = D / 16, NDB = D / 32, CPR = C::CPR, LPT = C::LPT, NT = C::NT;
+  constexpr bool EVEN = (KT * CPR) % NT == 0;  // every thread stages exactly LPT chunks
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
   const int b = blockIdx.z, h = blockIdx.y;
@@ -221,7 +222,7 @@ flash_attn_v2_kernel(const bf16_t* __restrict__ q, const bf16_t* __restrict__ k,
 #pragma unroll
     for (int i = 0; i < LPT; ++i) {
       const int idx = tid + NT * i, r = idx / CPR, cc = idx % CPR, key = t * KT + r;
-      if (idx < KT * CPR && key < L) {
+      if ((EVEN || idx < KT * CPR) && key < L) {
         kst[i] = *(const u32x4_t*)(kbase_p + (size_t)key * ldk + cc * 8);
         vst[i] = *(const u32x4_t*)(vbase_p + (size_t)key * ldv + cc * 8);
       } else {
@@ -236,7 +237,7 @@ flash_attn_v2_kernel(const bf16_t* __restrict__ q, const bf16_t* __restrict__ k,
 #pragma unroll
     for (int i = 0; i < LPT; ++i) {
       const int idx = tid + NT * i, r = idx / CPR, cc = idx % CPR;
-      if (idx < KT * CPR) {
+      if (EVEN || idx < KT * CPR) {
         *(u32x4_t*)(sK + r * C::KSTR + cc * 16) = kst[i];
         *(u32x4_t*)(sV + r * C::VSTR + cc * 16) = vst[i];
       }

@@ -281,9 +281,11 @@ gemm256_kernel(GemmArgs p) {
   }
 }
 
-// bf16 default: the ping-pong schedule (+2-14 % over the lock-step one, bit-identical results,
-// profiles/gemm256_pingpong_r1.txt); da_set_gemm_pingpong(0) selects the lock-step kernel.
-static int g_gemm_pp = 1;
+// The ping-pong schedule is +2-14 % on repeated (L2/MALL-warm) GEMMs but ~0.8 % slower in the
+// flagship bench, where every projection streams cold weights (same-box A/B,
+// profiles/gemm256_pingpong_r1.txt), so the lock-step kernel stays the default;
+// da_set_gemm_pingpong(1) / DA_GEMM_PINGPONG=1 selects ping-pong. Results are bit-identical.
+static int g_gemm_pp = 0;
 DA_EXPORT void da_set_gemm_pingpong(int v) { g_gemm_pp = v; }
 
 template <int FP8, int PP>

@@ -92,6 +92,11 @@ def lib() -> ctypes.CDLL:
             fn.restype = c_int
         L.da_topk_dense_ws.argtypes = [c_int, c_int, c_int, c_int]
         L.da_topk_dense_ws.restype = c_size_t
+        # schedule overrides for A/B measurements (defaults are the measured-best variants)
+        if os.environ.get("DA_GEMM_PINGPONG") is not None:
+            L.da_set_gemm_pingpong(int(os.environ["DA_GEMM_PINGPONG"]))
+        if os.environ.get("DA_FLASH_WAVES") is not None:
+            L.da_set_flash_waves(int(os.environ["DA_FLASH_WAVES"]))
         _LIB = L
         return L
 

@@ -376,11 +376,11 @@ def test_gemm256_pingpong(M, N, Kd, epi):
     a, w = _rand(M, Kd), _rand(N, Kd, scale=Kd ** -0.5)
     bias = _rand(N) if epi in (K.EPI_BIAS, K.EPI_RESID) else None
     resid = _rand(M, N) if epi == K.EPI_RESID else None
-    K.lib().da_set_gemm_pingpong(0)
+    lockstep = K.gemm(a, w, bias=bias, epi=epi, resid=resid, tile=4, splits=1)
+    K.lib().da_set_gemm_pingpong(1)
     try:
-        lockstep = K.gemm(a, w, bias=bias, epi=epi, resid=resid, tile=4, splits=1)
+        got = K.gemm(a, w, bias=bias, epi=epi, resid=resid, tile=4, splits=1)
     finally:
-        K.lib().da_set_gemm_pingpong(1)
-    got = K.gemm(a, w, bias=bias, epi=epi, resid=resid, tile=4, splits=1)
+        K.lib().da_set_gemm_pingpong(0)
     _close(got, R.gemm(a, w, bias=bias, epi=epi, resid=resid), atol=0.04)
     assert torch.equal(got, lockstep)  # same K order -> bit-identical
