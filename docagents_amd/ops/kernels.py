@@ -191,6 +191,8 @@ def gemm(a: torch.Tensor, w: torch.Tensor, bias=None, epi: int = EPI_NONE, resid
         _bf16_cuda(gamma, "gamma"); _req(gamma.numel() == K, "gamma must be [K]")
     if splits <= 0:
         splits = _auto_splits(M, N, K)
+        if tile == 0 and M <= 64:
+            tile = 3  # 32-row tiles beat 64-row ones at every decode shape measured
     ws = None
     if splits > 1:
         ws = _workspace(splits * M * N * 4, a.device)
@@ -254,14 +256,14 @@ def gemm_fp8(aq, sa, wq, sw, bias=None, epi: int = EPI_NONE, resid=None, out=Non
 
 
 def _auto_splits(M: int, N: int, K: int) -> int:
-    """Split-K so skinny (decode-sized) GEMMs put >= ~512 workgroups on the 256 CUs."""
+    """Split-K for decode-sized M (32-row tiles): the largest power of two keeping <= ~640
+    workgroups and >= 8 K-steps per workgroup (measured sweep, profiles/splitk_sweep_r1.txt)."""
     if M > 64:
         return 1
-    bm, bn = (32, 128) if M <= 32 else (64, 128)
-    tiles = math.ceil(M / bm) * math.ceil(N / bn)
+    tiles = math.ceil(M / 32) * math.ceil(N / 128)
     ksteps = K // 64
     s = 1
-    while tiles * s < 512 and ksteps % (s * 2) == 0 and ksteps // (s * 2) >= 4:
+    while tiles * s * 2 <= 640 and ksteps % (s * 2) == 0 and ksteps // (s * 2) >= 8:
         s *= 2
     return s
 
