@@ -210,6 +210,8 @@ class LlamaDecoder:
         c, o, cache = self.cfg, self.ops, self.cache
         D, hl, kl = c.head_dim, self.hl, self.kl
         x = o.embed(st.tokens, self.w["embed"], out=st.x)
+        if self._norm_fusable(x.shape[0]):
+            return self._decode_step_fused_norms(st, x)
         fuse = o.gemv_fusable(x.shape[0], self.w["layers"][0]["wqkv"].shape[0], x.shape[1])
         for li, L in enumerate(self.w["layers"]):
             if fuse:  # batch 1: RMSNorm folded into the QKV GEMV (no separate norm launch)
@@ -223,6 +225,31 @@ class LlamaDecoder:
             self._attn_out_and_mlp(L, a, x)
         logits = self._logits(x)
         st.logits.copy_(logits)
+        o.sample(st.logits, st.temperature, st.seed, 0, out_tok=st.tokens, out_lp=st.lp, conf=st.conf,
+                 active=st.active, ctr=st.pos, pos=st.pos, lens=st.lens, hist=st.hist, start=st.start, eos=st.eos)
+        return st.tokens
+
+    def _norm_fusable(self, B: int) -> bool:
+        """Batched decode (1 < B <= 64, no TP): every RMSNorm rides on the split-K reduction of the
+        projection before it (gemm_resid_norm), so a layer is 2 GEMM+reduce pairs, 2 plain GEMMs,
+        RoPE/cache and attention — no standalone norm launches."""
+        return self.tp.size == 1 and 1 < B <= 64 and self.cfg.hidden <= 8192 and self.cfg.hidden % 8 == 0
+
+    def _decode_step_fused_norms(self, st: "DecodeState", x: torch.Tensor) -> torch.Tensor:
+        c, o, cache = self.cfg, self.ops, self.cache
+        D, hl, kl = c.head_dim, self.hl, self.kl
+        layers = self.w["layers"]
+        h = o.rmsnorm(x, layers[0]["ln_attn"], c.eps, out=st.h)
+        for li, L in enumerate(layers):
+            qkv = o.gemm(h, L["wqkv"], out=st.qkv)
+            o.rope_cache(qkv, st.pos, self.cos_sin, hl, kl, D, slot=st.slot, k_cache=cache.k(li), v_cache=cache.v(li))
+            a = o.decode_attn(qkv, cache.k(li), cache.v(li), st.lens, st.slot, hl, kl, D, max_len=cache.max_seq,
+                              out=st.attn)
+            h = o.gemm_resid_norm(a, L["wo"], x, L["ln_mlp"], c.eps, out=x, h_out=st.h)      # x += o; h = norm(x)
+            g = o.gemm(h, L["w_gu"], epi=EPI_SWIGLU)
+            nxt = layers[li + 1]["ln_attn"] if li + 1 < len(layers) else self.w["norm"]
+            h = o.gemm_resid_norm(g, L["w_down"], x, nxt, c.eps, out=x, h_out=st.h)       # x += mlp; h = norm(x)
+        st.logits.copy_(o.gemm(h, self.w["lm_head"]))  # h already carries the final norm
         o.sample(st.logits, st.temperature, st.seed, 0, out_tok=st.tokens, out_lp=st.lp, conf=st.conf,
                  active=st.active, ctr=st.pos, pos=st.pos, lens=st.lens, hist=st.hist, start=st.start, eos=st.eos)
         return st.tokens

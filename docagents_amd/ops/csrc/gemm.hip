@@ -394,6 +394,94 @@ static int launch_tile(const GemmArgs& a, int epi, int splits, hipStream_t s) {
   return (int)hipGetLastError();
 }
 
+// Split-K reduction fused with the residual add AND the next RMSNorm (decode layers, M <= 64):
+// one workgroup per row sums the fp32 partials, adds bias + residual, writes the new residual
+// stream row C, then normalises that (bf16-rounded) row: H = C * rsqrt(mean(C^2) + eps) * gamma.
+// Replaces reduce + rmsnorm (two launches, two passes over the row) with one.
+__global__ void __launch_bounds__(256)
+splitk_reduce_resid_rmsnorm(const float* __restrict__ ws, int splits, int M, int N, const bf16_t* __restrict__ bias,
+                            const bf16_t* __restrict__ resid, int ldr, bf16_t* __restrict__ C, int ldc,
+                            const bf16_t* __restrict__ gamma, float eps, bf16_t* __restrict__ H, int ldh) {
+  constexpr int MAXC = 4;  // N <= 8 * 256 * 4 = 8192
+  __shared__ float red[16];
+  const int m = blockIdx.x;
+  const int nch = N / 8;
+  float v[MAXC][8];
+  float ss = 0.f;
+#pragma unroll
+  for (int i = 0; i < MAXC; ++i) {
+    const int c = threadIdx.x + 256 * i;
+    if (c >= nch) continue;
+    const int oc = c * 8;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[i][e] = 0.f;
+    for (int sp = 0; sp < splits; ++sp) {
+      const float* row = ws + ((size_t)sp * M + m) * N + oc;
+      const f32x4_t a = *(const f32x4_t*)row, b = *(const f32x4_t*)(row + 4);
+      v[i][0] += a[0]; v[i][1] += a[1]; v[i][2] += a[2]; v[i][3] += a[3];
+      v[i][4] += b[0]; v[i][5] += b[1]; v[i][6] += b[2]; v[i][7] += b[3];
+    }
+    const u32x4_t r = *(const u32x4_t*)(resid + (size_t)m * ldr + oc);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      v[i][2 * e] += bf2f((bf16_t)(r[e] & 0xffff)) + (bias ? bf2f(bias[oc + 2 * e]) : 0.f);
+      v[i][2 * e + 1] += bf2f((bf16_t)(r[e] >> 16)) + (bias ? bf2f(bias[oc + 2 * e + 1]) : 0.f);
+    }
+    u32x4_t o;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      o[e] = pack_bf2(v[i][2 * e], v[i][2 * e + 1]);
+      v[i][2 * e] = bf2f((bf16_t)(o[e] & 0xffff));       // normalise what the stream holds (bf16)
+      v[i][2 * e + 1] = bf2f((bf16_t)(o[e] >> 16));
+      ss += v[i][2 * e] * v[i][2 * e] + v[i][2 * e + 1] * v[i][2 * e + 1];
+    }
+    *(u32x4_t*)(C + (size_t)m * ldc + oc) = o;
+  }
+  const float inv = rsqrtf(block_sum(ss, red) / N + eps);
+#pragma unroll
+  for (int i = 0; i < MAXC; ++i) {
+    const int c = threadIdx.x + 256 * i;
+    if (c >= nch) continue;
+    const u32x4_t g = *(const u32x4_t*)(gamma + c * 8);
+    u32x4_t o;
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+      o[e] = pack_bf2(v[i][2 * e] * inv * bf2f((bf16_t)(g[e] & 0xffff)),
+                      v[i][2 * e + 1] * inv * bf2f((bf16_t)(g[e] >> 16)));
+    *(u32x4_t*)(H + (size_t)m * ldh + c * 8) = o;
+  }
+}
+
+// C = resid + A.W^T (+ bias) and H = RMSNorm(C) * gamma in two launches (split-K GEMM + fused
+// reduce). M <= 64 (decode), N % 8 == 0, N <= 8192. ws holds splits * M * N floats.
+DA_EXPORT int da_gemm_resid_rmsnorm(const void* A, int lda, const void* W, void* C, int ldc, const void* bias,
+                                    const void* resid, int ldr, int M, int N, int K, int tile, int splits, void* ws,
+                                    const void* gamma, float eps, void* Hout, int ldh, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  if (K % 64 || N % 8 || N > 8192 || lda % 8 || ldc % 8 || ldh % 8 || !ws || !gamma || !resid || !Hout)
+    return (int)hipErrorInvalidValue;
+  if (splits < 1 || (K / 64) % splits || M > 64) return (int)hipErrorInvalidValue;
+  if (M == 0) return 0;
+  GemmArgs a{};
+  a.A = (const bf16_t*)A; a.W = (const bf16_t*)W; a.C = (bf16_t*)C;
+  a.bias = nullptr; a.resid = nullptr; a.ws = (float*)ws;
+  a.M = M; a.N = N; a.K = K; a.lda = lda; a.ldc = ldc; a.ldr = ldr; a.k_per_split = K / splits;
+  const int ntm = (M + 31) / 32, ntn = (N + 127) / 128;
+  dim3 grid(ntm * ntn, 1, splits), block(256);
+  if (tile == 2) {
+    dim3 g2(((M + 63) / 64) * ntn, 1, splits);
+    gemm_bf16_kernel<64, 128, 1, 4, EPI_PARTIAL><<<g2, block, 0, s>>>(a);
+  } else {
+    gemm_bf16_kernel<32, 128, 1, 4, EPI_PARTIAL><<<grid, block, 0, s>>>(a);
+  }
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return (int)e;
+  splitk_reduce_resid_rmsnorm<<<M, 256, 0, s>>>((const float*)ws, splits, M, N, (const bf16_t*)bias,
+                                                (const bf16_t*)resid, ldr, (bf16_t*)C, ldc, (const bf16_t*)gamma, eps,
+                                                (bf16_t*)Hout, ldh);
+  DA_LAUNCH_CHECK();
+}
+
 // Tile selection: big tiles when the grid fills 256 CUs, skinny tiles (+ split-K) for decode-sized M.
 // tile: 0 = auto, 1 = 128x128, 2 = 64x128, 3 = 32x128, 4 = 256x256, 6 = GEMV (M = 1).
 DA_EXPORT int da_gemm_bf16(const void* A, int lda, const void* W, void* C, int ldc,

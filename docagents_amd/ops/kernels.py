@@ -33,6 +33,8 @@ _SIGS = {
     "da_quant_fp8_rows": [c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p],
     "da_layernorm_q": [c_void_p] * 7 + [c_int, c_int, c_float, c_void_p],
     "da_bert_embed_ln_q": [c_void_p] * 11 + [c_int, c_int, c_float, c_void_p],
+    "da_gemm_resid_rmsnorm": [c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_int, c_int,
+                              c_int, c_int, c_int, c_void_p, c_void_p, c_float, c_void_p, c_int, c_void_p],
     "da_rmsnorm": [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_float, c_void_p],
     "da_layernorm": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_float, c_void_p],
     "da_bert_embed_ln": [c_void_p] * 9 + [c_int, c_int, c_float, c_void_p],
@@ -190,9 +192,9 @@ def gemm(a: torch.Tensor, w: torch.Tensor, bias=None, epi: int = EPI_NONE, resid
         _req(tile == 6, "fused RMSNorm needs the M == 1 GEMV path")
         _bf16_cuda(gamma, "gamma"); _req(gamma.numel() == K, "gamma must be [K]")
     if splits <= 0:
-        splits = _auto_splits(M, N, K)
         if tile == 0 and M <= 64:
-            tile = 3  # 32-row tiles beat 64-row ones at every decode shape measured
+            tile = _decode_tile(M)
+        splits = _auto_splits(M, N, K)
     ws = None
     if splits > 1:
         ws = _workspace(splits * M * N * 4, a.device)
@@ -255,15 +257,44 @@ def gemm_fp8(aq, sa, wq, sw, bias=None, epi: int = EPI_NONE, resid=None, out=Non
     return out
 
 
+def gemm_resid_norm(a, w, resid, gamma, eps: float, out=None, h_out=None, bias=None):
+    """Decode layer tail (M <= 64): out = resid + a @ w^T (+ bias) — the new residual stream — and
+    h_out = RMSNorm(out) * gamma, with the norm fused into the split-K reduction. Returns h_out."""
+    _bf16_cuda(a, "a"); _bf16_cuda(w, "w"); _bf16_cuda(resid, "resid"); _bf16_cuda(gamma, "gamma")
+    M, K = a.shape
+    N = w.shape[0]
+    _req(M <= 64 and K % 64 == 0 and N % 8 == 0 and N <= 8192 and w.shape[1] == K, "gemm_resid_norm shape")
+    _req(a.stride(1) == 1 and a.stride(0) % 8 == 0 and w.is_contiguous() and gamma.numel() == N, "layout")
+    _req(resid.shape == (M, N) and resid.stride(1) == 1, "bad resid")
+    out = resid if out is None else out
+    if h_out is None:
+        h_out = torch.empty((M, N), dtype=torch.bfloat16, device=a.device)
+    if M == 0:
+        return h_out
+    splits = _auto_splits(M, N, K)
+    ws = _workspace(splits * M * N * 4, a.device)
+    _check(lib().da_gemm_resid_rmsnorm(_ptr(a), a.stride(0), _ptr(w), _ptr(out), out.stride(0), _ptr(bias),
+                                       _ptr(resid), resid.stride(0), M, N, K, _decode_tile(M), splits, _ptr(ws), _ptr(gamma),
+                                       float(eps), _ptr(h_out), h_out.stride(0), _stream()), "gemm_resid_norm")
+    return h_out
+
+
+def _decode_tile(M: int) -> int:
+    """Decode-sized M: 32x128 tiles up to 32 rows, 64x128 above (no wasted MFMA rows either way)."""
+    return 3 if M <= 32 else 2
+
+
 def _auto_splits(M: int, N: int, K: int) -> int:
-    """Split-K for decode-sized M (32-row tiles): the largest power of two keeping <= ~640
-    workgroups and >= 8 K-steps per workgroup (measured sweep, profiles/splitk_sweep_r1.txt)."""
+    """Split-K for decode-sized M: the largest power of two keeping <= 512 workgroups and >= 6
+    K-steps per workgroup. Chosen from a sweep with weights streamed cold from HBM, as in a real
+    decode step (profiles/splitk_sweep_cold_r1.txt); a warm-MALL sweep favours fewer splits and
+    mis-predicts the in-graph timings."""
     if M > 64:
         return 1
-    tiles = math.ceil(M / 32) * math.ceil(N / 128)
+    tiles = math.ceil(M / (32 if _decode_tile(M) == 3 else 64)) * math.ceil(N / 128)
     ksteps = K // 64
     s = 1
-    while tiles * s * 2 <= 640 and ksteps % (s * 2) == 0 and ksteps // (s * 2) >= 8:
+    while tiles * s * 2 <= 512 and ksteps % (s * 2) == 0 and ksteps // (s * 2) >= 6:
         s *= 2
     return s
 

@@ -331,3 +331,13 @@ def quant_weight_fp8(w):
     wf = w.float()
     sw = (wf.abs().amax(dim=1) / 448.0).clamp_min(1e-30)
     return (wf / sw[:, None]).clamp(-448, 448).to(torch.float8_e4m3fn).contiguous(), sw.contiguous()
+
+
+def gemm_resid_norm(a, w, resid, gamma, eps, out=None, h_out=None, bias=None):
+    y = gemm(a, w, bias=bias, epi=EPI_RESID, resid=resid)
+    (resid if out is None else out).copy_(y)
+    h = rmsnorm(y, gamma, eps)
+    if h_out is not None:
+        h_out.copy_(h)
+        return h_out
+    return h

@@ -384,3 +384,16 @@ def test_gemm256_pingpong(M, N, Kd, epi):
         K.lib().da_set_gemm_pingpong(0)
     _close(got, R.gemm(a, w, bias=bias, epi=epi, resid=resid), atol=0.04)
     assert torch.equal(got, lockstep)  # same K order -> bit-identical
+
+
+@pytest.mark.parametrize("M,N,Kd", [(2, 3072, 3072), (17, 3072, 8192), (64, 4096, 1024), (64, 8192, 512)])
+def test_gemm_resid_rmsnorm_fused(M, N, Kd):
+    torch.manual_seed(M + N)
+    a, w = _rand(M, Kd), _rand(N, Kd, scale=Kd ** -0.5)
+    x = _rand(M, N)
+    g = _rand(N) + 1.0
+    x_ref = x.clone()
+    h = K.gemm_resid_norm(a, w, x, g, 1e-5, out=x)
+    h_ref = R.gemm_resid_norm(a, w, x_ref, g, 1e-5, out=x_ref)
+    _close(x, x_ref, atol=0.03)
+    _close(h, h_ref, atol=0.05)
