@@ -22,3 +22,5 @@ struct GemmArgs {
 // large-tile (256x256, 8 waves, LDS-DMA staged) path; returns hipError_t.
 // fp8 = 1: A and W hold OCP e4m3 bytes (lda / K in elements = bytes), C = (A.W^T) * sa[m] * sw[n].
 int launch_gemm256(const GemmArgs& a, int epi, hipStream_t s, int fp8 = 0);
+// 4-wave 256x256 bf16 variant (gemm256w4.hip); K % 32 == 0
+int launch_gemm256w4(const GemmArgs& a, int epi, hipStream_t s);

@@ -482,8 +482,13 @@ DA_EXPORT int da_gemm_resid_rmsnorm(const void* A, int lda, const void* W, void*
   DA_LAUNCH_CHECK();
 }
 
+// 256x256 prefill tile: 0 = 8-wave gemm256 (default), 1 = 4-wave gemm256w4 (tile 5 selects it
+// explicitly); DA_GEMM_W4=1 / da_set_gemm_w4 for A/B runs.
+static int g_gemm_w4 = 0;
+DA_EXPORT void da_set_gemm_w4(int v) { g_gemm_w4 = v; }
+
 // Tile selection: big tiles when the grid fills 256 CUs, skinny tiles (+ split-K) for decode-sized M.
-// tile: 0 = auto, 1 = 128x128, 2 = 64x128, 3 = 32x128, 4 = 256x256, 6 = GEMV (M = 1).
+// tile: 0 = auto, 1 = 128x128, 2 = 64x128, 3 = 32x128, 4 = 256x256, 5 = 256x256 4-wave, 6 = GEMV (M = 1).
 DA_EXPORT int da_gemm_bf16(const void* A, int lda, const void* W, void* C, int ldc,
                            const void* bias, const void* resid, int ldr,
                            int M, int N, int K, int epi, int tile, int splits, void* ws,
@@ -504,9 +509,10 @@ DA_EXPORT int da_gemm_bf16(const void* A, int lda, const void* W, void* C, int l
     const long t256 = (long)((M + 255) / 256) * ((N + 255) / 256);
     tile = (M <= 32) ? 3 : (M <= 64 ? 2 : (t256 >= 256 && splits == 1 ? 4 : 1));
   }
-  if (tile == 4) {
+  if (tile == 4 && g_gemm_w4 && K % 32 == 0) tile = 5;
+  if (tile == 4 || tile == 5) {
     if (splits != 1) return (int)hipErrorInvalidValue;
-    return launch_gemm256(a, epi, s);
+    return tile == 5 ? launch_gemm256w4(a, epi, s) : launch_gemm256(a, epi, s);
   }
   if (tile == 6) return launch_gemv(a, epi, s);
   int err;

@@ -42,7 +42,8 @@ __global__ void __launch_bounds__(512)
 gemm256_kernel(GemmArgs p) {
   constexpr int ES = FP8 ? 1 : 2;  // bytes per element
   __shared__ __attribute__((aligned(16))) char smem[SMEM];
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);  // SGPR: LDS-DMA bases (M0) stay scalar
   const int wm = wid >> 2, wn = wid & 3;
   const int fr = lane & 15, fg = lane >> 4;
 

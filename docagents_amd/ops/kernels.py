@@ -50,6 +50,8 @@ _SIGS = {
     "da_set_gqa_mfma": [c_int],
     "da_set_flash_waves": [c_int],
     "da_set_gemm_pingpong": [c_int],
+    "da_set_gemm_w4": [c_int],
+    "da_set_gemm_w4_cfg": [c_int],
     "da_decode_attn": [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
                        c_int, c_int, c_int, c_float, c_void_p, c_void_p, c_int, c_void_p],
     "da_topk_dense": [c_void_p, c_int, c_int, c_void_p, c_void_p, c_int, c_void_p, c_int, c_float, c_int,
@@ -97,6 +99,8 @@ def lib() -> ctypes.CDLL:
         # schedule overrides for A/B measurements (defaults are the measured-best variants)
         if os.environ.get("DA_GEMM_PINGPONG") is not None:
             L.da_set_gemm_pingpong(int(os.environ["DA_GEMM_PINGPONG"]))
+        if os.environ.get("DA_GEMM_W4") is not None:
+            L.da_set_gemm_w4(int(os.environ["DA_GEMM_W4"]))
         if os.environ.get("DA_FLASH_WAVES") is not None:
             L.da_set_flash_waves(int(os.environ["DA_FLASH_WAVES"]))
         _LIB = L
@@ -185,6 +189,9 @@ def gemm(a: torch.Tensor, w: torch.Tensor, bias=None, epi: int = EPI_NONE, resid
         ldr = resid.stride(0)
     if M == 0:
         return out
+    if (_BLAS_PREFILL and tile == 0 and splits <= 0 and rms is None and M >= _BLAS_MIN_M
+            and (epi in (EPI_NONE, EPI_BIAS) or (epi == EPI_RESID and bias is None))):
+        return _blas_gemm(a, w, bias, epi, resid, out)
     if tile == 0 and splits <= 0 and gemv_fusable(M, N, K, epi):
         tile, splits = 6, 1  # batch-1 decode: weight-streaming GEMV, one launch, no split-K workspace
     gamma, eps = (None, 0.0) if rms is None else rms
@@ -202,6 +209,27 @@ def gemm(a: torch.Tensor, w: torch.Tensor, bias=None, epi: int = EPI_NONE, resid
                             M, N, K, epi, tile, splits, _ptr(ws), _ptr(gamma), float(eps), _stream())
     _check(rc, "gemm")
     return out
+
+
+# Plain prefill-sized GEMMs (no epilogue, bias, or residual as the BLAS beta*C term) go to the
+# platform GEMM library (hipBLASLt) — the "plain library GEMM" case; everything with a fused
+# epilogue (SwiGLU, GELU, RMSNorm, split-K reductions, fp8 scales) and every decode-sized GEMM stays
+# on the hand-written kernels. Measured sustained on MI355X (profiles/gemm256_w4_r1.txt): hipBLASLt
+# 1.50-1.57 PF/s vs gemm256 1.22-1.31 at M = 32768. DA_BLAS_PREFILL=0 keeps everything on gemm256.
+_BLAS_PREFILL = os.environ.get("DA_BLAS_PREFILL", "1") != "0"
+_BLAS_MIN_M = int(os.environ.get("DA_BLAS_MIN_M", "4096"))
+
+
+def _blas_gemm(a, w, bias, epi, resid, out):
+    wt = w.t()
+    if epi == EPI_NONE:
+        return torch.mm(a, wt, out=out)
+    if epi == EPI_BIAS:
+        return torch.addmm(bias, a, wt, out=out)
+    _req(resid.shape == out.shape, "bad resid")
+    if out.data_ptr() == resid.data_ptr() and out.stride() == resid.stride():
+        return out.addmm_(a, wt)  # x += a @ w^T in place (beta = 1)
+    return torch.addmm(resid, a, wt, out=out)
 
 
 FP8 = torch.float8_e4m3fn  # OCP e4m3 (gfx950), not the MI300 fnuz variant

@@ -386,6 +386,54 @@ def test_gemm256_pingpong(M, N, Kd, epi):
     assert torch.equal(got, lockstep)  # same K order -> bit-identical
 
 
+@pytest.mark.parametrize("epi", [K.EPI_NONE, K.EPI_BIAS, K.EPI_RESID])
+@pytest.mark.parametrize("inplace", [False, True])
+def test_gemm_blas_prefill(epi, inplace):
+    """Prefill-sized plain GEMMs routed to the platform library (bias / residual as beta*C)."""
+    if inplace and epi != K.EPI_RESID:
+        pytest.skip("in-place only applies to the residual form")
+    torch.manual_seed(epi)
+    M, N, Kd = K._BLAS_MIN_M + 37, 768, 512
+    a, w = _rand(M, Kd), _rand(N, Kd, scale=Kd ** -0.5)
+    bias = _rand(N) if epi == K.EPI_BIAS else None
+    resid = _rand(M, N) if epi == K.EPI_RESID else None
+    ref = R.gemm(a, w, bias=bias, epi=epi, resid=resid)
+    out = resid if inplace else None
+    got = K.gemm(a, w, bias=bias, epi=epi, resid=resid, out=out)
+    _close(got, ref, atol=0.04)
+    if inplace:
+        assert got.data_ptr() == resid.data_ptr()
+
+
+@pytest.mark.parametrize("M,N,Kd", [(256, 256, 64), (300, 520, 192), (1000, 1032, 768), (2048, 3072, 3072),
+                                    (512, 768, 128)])
+@pytest.mark.parametrize("epi", [K.EPI_NONE, K.EPI_BIAS, K.EPI_GELU, K.EPI_RESID, K.EPI_SWIGLU])
+def test_gemm256_w4(M, N, Kd, epi):
+    """4-wave 256x256 kernel (tile 5) vs the fp32 reference and vs the 8-wave kernel."""
+    torch.manual_seed(M * 5 + N + epi)
+    if epi == K.EPI_SWIGLU:
+        N = (N // 32) * 32
+    a, w = _rand(M, Kd), _rand(N, Kd, scale=Kd ** -0.5)
+    bias = _rand(N) if epi in (K.EPI_BIAS, K.EPI_GELU, K.EPI_RESID) else None
+    resid = _rand(M, N) if epi == K.EPI_RESID else None
+    got = K.gemm(a, w, bias=bias, epi=epi, resid=resid, tile=5, splits=1)
+    _close(got, R.gemm(a, w, bias=bias, epi=epi, resid=resid), atol=0.04)
+    for cfg in (1, 2, 3, 5):  # 5-slot ring / split-phase / register-staged: same K order -> bit-identical
+        K.lib().da_set_gemm_w4_cfg(cfg)
+        try:
+            other = K.gemm(a, w, bias=bias, epi=epi, resid=resid, tile=5, splits=1)
+        finally:
+            K.lib().da_set_gemm_w4_cfg(0)
+        assert torch.equal(got, other), cfg
+    # tile 4 + the global switch routes to the same kernel
+    K.lib().da_set_gemm_w4(1)
+    try:
+        again = K.gemm(a, w, bias=bias, epi=epi, resid=resid, tile=4, splits=1)
+    finally:
+        K.lib().da_set_gemm_w4(0)
+    assert torch.equal(got, again)
+
+
 @pytest.mark.parametrize("M,N,Kd", [(2, 3072, 3072), (17, 3072, 8192), (64, 4096, 1024), (64, 8192, 512)])
 def test_gemm_resid_rmsnorm_fused(M, N, Kd):
     torch.manual_seed(M + N)
