@@ -4,7 +4,7 @@ R=$GRAFT_REPO_ROOT
 cd $R
 mkdir -p gpurun_out/prof3
 python -m docagents_amd.ops.build > gpurun_out/build.log 2>&1 || { cat gpurun_out/build.log; exit 3; }
-timeout -k 10 900 python -m pytest tests -m gpu -q -x -p no:cacheprovider > gpurun_out/t_all.log 2>&1
+timeout -k 10 900 python -u -m pytest tests -m gpu -q -x -p no:cacheprovider --timeout 180 --timeout-method thread > gpurun_out/t_all.log 2>&1
 rc=$?
 echo "pytest rc=$rc"; tail -5 gpurun_out/t_all.log
 if [ $rc -ne 0 ]; then exit $rc; fi
