@@ -34,20 +34,35 @@ class TPContext:
 
     def __init__(self, rank: int = 0, size: int = 1, group=None):
         self.rank, self.size, self.group = rank, size, group
+        self.xgmi = None  # XgmiAllReduce once setup_device() ran on a GPU
+
+    def setup_device(self, device: torch.device) -> None:
+        """Collective (every TP rank): map the peers' all-reduce buffers over xGMI (GPU only).
+        Decode-sized row-parallel outputs then take the one-/two-shot IPC kernel; anything else
+        (and every CPU run) uses torch.distributed (RCCL / gloo)."""
+        if self.size > 1 and device.type == "cuda" and self.xgmi is None:
+            from ..parallel.xgmi_allreduce import XgmiAllReduce
+            self.xgmi = XgmiAllReduce.create(self.group, device)
 
     def all_reduce_(self, t: torch.Tensor) -> torch.Tensor:
         if self.size > 1:
+            if self.xgmi is not None and self.xgmi.takes(t):
+                return self.xgmi.all_reduce_(t)
             import torch.distributed as dist
-            dist.all_reduce(t, group=self.group)
+            if t.is_cuda and dist.get_backend(self.group) == "gloo":  # 1-GPU multi-rank rehearsal
+                h = t.cpu()
+                dist.all_reduce(h, group=self.group)
+                t.copy_(h)
+            else:
+                dist.all_reduce(t, group=self.group)
         return t
 
     def all_gather_cols(self, t: torch.Tensor) -> torch.Tensor:
         """[B, n] on every rank -> [B, n * size] (rank-major columns)."""
         if self.size == 1:
             return t
-        import torch.distributed as dist
-        out = torch.empty((self.size * t.shape[0],) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
-        dist.all_gather_into_tensor(out, t.contiguous(), group=self.group)
+        from ..parallel.dist import all_gather_rows
+        out = all_gather_rows(t.contiguous(), self.group)
         return out.view(self.size, t.shape[0], -1).permute(1, 0, 2).reshape(t.shape[0], -1)
 
 
@@ -146,6 +161,7 @@ class LlamaDecoder:
         self.device = torch.device(device)
         self.ops = get_ops(self.device)
         self.tp = tp or TPContext()
+        self.tp.setup_device(self.device)
         t = self.tp.size
         if cfg.heads % t or cfg.kv_heads % t:
             raise ValueError(f"TP={t} must divide heads={cfg.heads} and kv_heads={cfg.kv_heads}")

@@ -1,0 +1,220 @@
+// Custom all-reduce over xGMI for tensor-parallel decoding.
+//
+// MI355X nodes connect the 8 GPUs as a full mesh (7 xGMI links x ~153 GB/s per GPU). RCCL's ring
+// uses one link per neighbour and pays a multi-microsecond protocol latency per call, which dominates
+// the 2 x 80 small all-reduces of every Llama-3-70B TP=8 decode step. Here every rank exposes one
+// registered buffer (hipIpcGetMemHandle, opened by every peer), so a kernel reads all 7 peers at once
+// over all 7 links:
+//
+//   one-shot (latency path, decode-sized messages):
+//     stage own input -> [flag barrier] -> every rank sums all W buffers in rank order -> out
+//   two-shot (bandwidth path, prefill-sized messages):
+//     stage -> [barrier] -> reduce own 1/W slice in place -> [barrier] -> gather all slices -> out
+//
+// Synchronisation is per workgroup, not grid-wide: 16-byte vector v belongs to row v / AR_TPB and
+// row r is always handled by workgroup r % gridDim.x, in every phase of every call (the grid size
+// is fixed per communicator). So a workgroup only waits for the same workgroup index on its peers.
+// Each workgroup keeps its own call counter k in its rank's signal block (device-resident, so the
+// launch is HIP-graph capturable with constant arguments); barrier values are 2k+1 / 2k+2
+// (monotonic, no reset) and the staging buffer alternates by k's parity, which makes call k+2's
+// writes wait for every peer to have finished reading call k.
+//
+// Memory ordering: staged data is made visible with a system-scope fence (L2 write-back) before the
+// flag store (release, system scope) to each peer; waiting threads use system-scope acquire loads,
+// then every thread issues a system-scope acquire fence before reading peer memory.
+// Every wait is bounded (wall clock): a missing peer sets an error bit and the kernel finishes
+// instead of hanging the GPU; the host checks the bit (XgmiAllReduce.check()).
+#include <cstring>
+
+#include "common.h"
+
+#define AR_MAX_RANKS 8
+#define AR_MAX_BLOCKS 80
+#define AR_TPB 256
+
+struct ArPtrs {
+  char* p[AR_MAX_RANKS];
+};
+
+struct ArSignal {
+  uint32_t flags[AR_MAX_BLOCKS][AR_MAX_RANKS];  // flags[b][w]: last barrier value peer w reached
+  uint32_t cnt[AR_MAX_BLOCKS];                   // per-workgroup call counter (local only)
+  uint32_t err;                                  // bit 0: a barrier timed out
+  uint32_t pad[15];
+};
+
+__device__ __forceinline__ void ar_barrier(const ArPtrs& sig, ArSignal* self, int rank, int world, int b,
+                                           uint32_t val, long long timeout) {
+  __threadfence_system();  // this workgroup's staged writes -> memory, before any flag goes out
+  __syncthreads();
+  if ((int)threadIdx.x < world) {
+    ArSignal* peer = (ArSignal*)sig.p[threadIdx.x];
+    __hip_atomic_store(&peer->flags[b][rank], val, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    uint32_t* mine = &self->flags[b][threadIdx.x];
+    const long long t0 = wall_clock64();
+    while ((int)(__hip_atomic_load(mine, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) - val) < 0) {
+      if (wall_clock64() - t0 > timeout) {
+        __hip_atomic_fetch_or(&self->err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+  }
+  __syncthreads();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope: drop stale cached peer lines
+}
+
+template <bool BF16>
+__device__ __forceinline__ void acc_add(float (&a)[8], const u32x4_t& x) {
+  if (BF16) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      a[2 * i] += __uint_as_float(x[i] << 16);
+      a[2 * i + 1] += __uint_as_float(x[i] & 0xffff0000u);
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) a[i] += __uint_as_float(x[i]);
+  }
+}
+
+template <bool BF16>
+__device__ __forceinline__ u32x4_t acc_pack(const float (&a)[8]) {
+  u32x4_t r;
+  if (BF16) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) r[i] = pack_bf2(a[2 * i], a[2 * i + 1]);
+  } else {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) r[i] = __float_as_uint(a[i]);
+  }
+  return r;
+}
+
+// Sum vector v over all ranks' staging buffers, in rank order (bit-identical on every rank).
+template <bool BF16>
+__device__ __forceinline__ u32x4_t ar_sum(const ArPtrs& data, long long poff, long long v, int world) {
+  float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  u32x4_t x[AR_MAX_RANKS];
+#pragma unroll
+  for (int w = 0; w < AR_MAX_RANKS; ++w)
+    if (w < world) x[w] = ((const u32x4_t*)data.p[w])[poff + v];  // all loads in flight at once
+#pragma unroll
+  for (int w = 0; w < AR_MAX_RANKS; ++w)
+    if (w < world) acc_add<BF16>(a, x[w]);
+  return acc_pack<BF16>(a);
+}
+
+template <bool BF16>
+__global__ __launch_bounds__(AR_TPB) void allreduce_kernel(ArPtrs data, ArPtrs sig, const u32x4_t* __restrict__ in,
+                                                           u32x4_t* __restrict__ out, long long nvec,
+                                                           long long slice, long long parity_vec, int rank,
+                                                           int world, int twoshot, long long timeout) {
+  const int b = blockIdx.x, G = gridDim.x, t = threadIdx.x;
+  ArSignal* self = (ArSignal*)sig.p[rank];
+  __shared__ uint32_t s_k;
+  if (t == 0) s_k = self->cnt[b];
+  __syncthreads();
+  const uint32_t k = s_k;
+  const long long poff = (k & 1) ? parity_vec : 0;
+  u32x4_t* mine = (u32x4_t*)data.p[rank] + poff;
+  const long long rows = (nvec + AR_TPB - 1) / AR_TPB;
+
+  for (long long r = b; r < rows; r += G) {  // phase 1: stage
+    const long long v = r * AR_TPB + t;
+    if (v < nvec) mine[v] = in[v];
+  }
+  ar_barrier(sig, self, rank, world, b, 2u * k + 1u, timeout);
+
+  if (!twoshot) {
+    for (long long r = b; r < rows; r += G) {
+      const long long v = r * AR_TPB + t;
+      if (v < nvec) out[v] = ar_sum<BF16>(data, poff, v, world);
+    }
+  } else {
+    const long long lo = (long long)rank * slice, hi = lo + slice < nvec ? lo + slice : nvec;
+    for (long long r = b; r < rows; r += G) {  // phase 2: reduce own slice in place
+      const long long v = r * AR_TPB + t;
+      if (v >= lo && v < hi) {
+        const u32x4_t s = ar_sum<BF16>(data, poff, v, world);
+        mine[v] = s;
+      }
+    }
+    ar_barrier(sig, self, rank, world, b, 2u * k + 2u, timeout);
+    for (long long r = b; r < rows; r += G) {  // phase 3: gather every slice
+      const long long v = r * AR_TPB + t;
+      if (v < nvec) out[v] = ((const u32x4_t*)data.p[v / slice])[poff + v];
+    }
+  }
+  if (t == 0) self->cnt[b] = k + 1u;
+}
+
+DA_EXPORT int da_ar_signal_bytes() { return (int)sizeof(ArSignal); }
+DA_EXPORT int da_ar_max_blocks() { return AR_MAX_BLOCKS; }
+DA_EXPORT int da_ar_block_vecs() { return AR_TPB; }
+
+DA_EXPORT int da_ar_malloc(long long bytes, void** out) {
+  hipError_t e = hipMalloc(out, (size_t)bytes);
+  if (e != hipSuccess) return (int)e;
+  e = hipMemset(*out, 0, (size_t)bytes);
+  if (e != hipSuccess) return (int)e;
+  return (int)hipDeviceSynchronize();
+}
+
+DA_EXPORT int da_ar_free(void* p) { return (int)hipFree(p); }
+
+DA_EXPORT int da_ar_ipc_handle(void* p, void* handle_out) {
+  return (int)hipIpcGetMemHandle((hipIpcMemHandle_t*)handle_out, p);
+}
+
+DA_EXPORT int da_ar_ipc_handle_bytes() { return (int)sizeof(hipIpcMemHandle_t); }
+
+DA_EXPORT int da_ar_ipc_open(const void* handle, void** out) {
+  hipIpcMemHandle_t h;
+  memcpy(&h, handle, sizeof(h));
+  return (int)hipIpcOpenMemHandle(out, h, hipIpcMemLazyEnablePeerAccess);
+}
+
+DA_EXPORT int da_ar_ipc_close(void* p) { return (int)hipIpcCloseMemHandle(p); }
+
+DA_EXPORT int da_ar_read_err(void* own_sig, unsigned* out) {
+  return (int)hipMemcpy(out, &((ArSignal*)own_sig)->err, sizeof(unsigned), hipMemcpyDeviceToHost);
+}
+
+// wall_clock64() ticks per millisecond (the timeout unit of da_ar_allreduce).
+DA_EXPORT long long da_ar_clock_khz() {
+  int dev = 0, khz = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return 100000;
+  if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev) != hipSuccess || khz <= 0) return 100000;
+  return khz;
+}
+
+// in/out: nbytes (multiple of 16) on this rank; data/sig: host arrays of `world` device pointers
+// (own + IPC-opened peers); parity_bytes: offset of the second staging half (>= nbytes);
+// grid: fixed per communicator (<= AR_MAX_BLOCKS); dtype 0 = bf16, 1 = fp32.
+DA_EXPORT int da_ar_allreduce(const void* in, void* out, long long nbytes, int dtype, int rank, int world,
+                              void* const* data, void* const* sig, long long parity_bytes, int twoshot, int grid,
+                              long long timeout_ticks, hipStream_t stream) {
+  if (world < 2 || world > AR_MAX_RANKS || rank < 0 || rank >= world) return (int)hipErrorInvalidValue;
+  if (nbytes <= 0 || nbytes % 16 || nbytes > parity_bytes || parity_bytes % 16) return (int)hipErrorInvalidValue;
+  if (grid < 1 || grid > AR_MAX_BLOCKS) return (int)hipErrorInvalidValue;
+  ArPtrs d{}, s{};
+  for (int w = 0; w < world; ++w) {
+    d.p[w] = (char*)data[w];
+    s.p[w] = (char*)sig[w];
+  }
+  const long long nvec = nbytes / 16, rows = (nvec + AR_TPB - 1) / AR_TPB;
+  // two-shot: whole rows per slice so every slice boundary is a row boundary
+  const long long slice = twoshot ? (rows + world - 1) / world * AR_TPB : nvec;
+  // Row r always belongs to workgroup r % grid. A message with fewer rows than `grid` launches only
+  // workgroups 0..rows-1 (one row each, no wrap), which keeps that mapping, and every rank makes the
+  // same choice, so the skipped workgroups' counters stay in step across ranks.
+  if (rows < grid) grid = (int)rows;
+  if (dtype == 0)
+    allreduce_kernel<true><<<grid, AR_TPB, 0, stream>>>(d, s, (const u32x4_t*)in, (u32x4_t*)out, nvec, slice,
+                                                        parity_bytes / 16, rank, world, twoshot, timeout_ticks);
+  else
+    allreduce_kernel<false><<<grid, AR_TPB, 0, stream>>>(d, s, (const u32x4_t*)in, (u32x4_t*)out, nvec, slice,
+                                                         parity_bytes / 16, rank, world, twoshot, timeout_ticks);
+  DA_LAUNCH_CHECK();
+}

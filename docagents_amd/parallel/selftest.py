@@ -9,6 +9,8 @@ JSON verdict to ``out_path``.
   check_engine_group    EngineGroup command fan-out: embed (DP), search (broadcast + gather), index
                         routing by document owner, answer (DP generate)
   check_ivf_kmeans      IVFFlat with cross-shard k-means statistics all-reduce (C6)
+  check_xgmi_allreduce  IPC peer-buffer all-reduce kernel == fp32 rank-order sum (GPU ranks)
+  check_tp_decoder_gpu  TP=world decoder on GPU ranks (xGMI all-reduce in every layer) vs unsharded
 """
 from __future__ import annotations
 
@@ -167,3 +169,101 @@ def check_ivf_kmeans(rank, world, port, out_path):
     C0 = C.clone()
     dist.broadcast(C0, 0)
     _done(rank, out_path, {"recall": float(np.mean(allrec)), "centroids_equal": bool(torch.allclose(C, C0))})
+
+
+def check_xgmi_allreduce(rank, world, port, out_path):
+    """XgmiAllReduce (IPC peer buffers, ops/csrc/allreduce.hip) == the fp32 rank-order sum, for
+    one-shot and two-shot sizes, bf16 and fp32, eager and HIP-graph replay, with back-to-back calls
+    of different sizes (exercises the per-workgroup counters and the staging parity). GPU ranks;
+    the handle exchange rides a gloo group, so several ranks may share one GPU (1-GPU rehearsal)."""
+    _init(rank, world, port)
+    from .xgmi_allreduce import XgmiAllReduce
+    dev = torch.device("cuda", rank % torch.cuda.device_count())
+    torch.cuda.set_device(dev)
+    ar = XgmiAllReduce(None, dev, max_bytes=8 << 20, oneshot_max=256 << 10)
+    verdict = {"cases": [], "ok": True}
+
+    def inputs(n, dtype, salt):
+        xs = []
+        for r in range(world):
+            g = torch.Generator(device="cpu").manual_seed(1000 * salt + r)
+            xs.append(torch.randn(n, generator=g).to(dtype))
+        return xs
+
+    def ref_sum(xs, dtype):
+        acc = torch.zeros_like(xs[0], dtype=torch.float32)
+        for x in xs:
+            acc += x.float()
+        return acc.to(dtype)
+
+    sizes = [8, 4096, 8192 * 3, 131072, 8192 * 64, 1_000_000, (8 << 20) // 2]
+    salt = 0
+    for dtype in (torch.bfloat16, torch.float32):
+        for n in sizes:
+            if n * (2 if dtype == torch.bfloat16 else 4) > (8 << 20):
+                continue
+            salt += 1
+            xs = inputs(n, dtype, salt)
+            t = xs[rank].to(dev)
+            ar.all_reduce_(t)
+            torch.cuda.synchronize()
+            ref = ref_sum(xs, dtype)
+            err = float((t.cpu().float() - ref.float()).abs().max())
+            ok = err == 0.0
+            verdict["cases"].append({"n": n, "dtype": str(dtype), "max_err": err, "ok": ok})
+            verdict["ok"] &= ok
+    # graph capture: three calls (one-shot, two-shot, one-shot) replayed twice with fresh inputs
+    bufs = [torch.empty(n, dtype=torch.bfloat16, device=dev) for n in (8192, 400_000, 16384)]
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        for b in bufs:  # warm-up outside capture
+            b.zero_()
+            ar.all_reduce_(b)
+    torch.cuda.current_stream().wait_stream(s)
+    torch.cuda.synchronize()
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        for b in bufs:
+            ar.all_reduce_(b)
+    for rep in range(2):
+        refs = []
+        for i, b in enumerate(bufs):
+            salt += 1
+            xs = inputs(b.numel(), torch.bfloat16, salt)
+            b.copy_(xs[rank].to(dev))
+            refs.append(ref_sum(xs, torch.bfloat16))
+        graph.replay()
+        torch.cuda.synchronize()
+        for b, ref in zip(bufs, refs):
+            err = float((b.cpu().float() - ref.float()).abs().max())
+            verdict["cases"].append({"n": b.numel(), "graph_replay": rep, "max_err": err, "ok": err == 0.0})
+            verdict["ok"] &= err == 0.0
+    ar.check()
+    verdict["calls"] = ar.calls
+    ar.close()
+    _done(rank, out_path, verdict)
+
+
+def check_tp_decoder_gpu(rank, world, port, out_path):
+    """TP=world LlamaDecoder on GPU ranks: row-parallel outputs summed by the xGMI all-reduce
+    kernel, vocab-parallel logits all-gathered; compared with the unsharded decoder on the same
+    device (bf16 partial sums round differently, so: close logits, mostly identical tokens)."""
+    _init(rank, world, port)
+    from ..engine.generator import Generator
+    from ..models.configs import decoder_config
+    from ..models.llama import LlamaDecoder, TPContext, random_weights
+    dev = torch.device("cuda", rank % torch.cuda.device_count())
+    torch.cuda.set_device(dev)
+    cfg = decoder_config("tiny-dec")
+    ref = LlamaDecoder(cfg, dev, weights=random_weights(cfg, dev, seed=5))
+    tp = LlamaDecoder(cfg, dev, tp=TPContext(rank, world, None),
+                      weights=random_weights(cfg, dev, seed=5, tp_rank=rank, tp_size=world, full_then_shard=True))
+    prompts = [list(range(30, 30 + n)) for n in (9, 33, 4, 120)]
+    a = Generator(ref, max_batch=4, max_seq=256, temperature=0.0, use_graphs=False).generate(prompts, 8)
+    b = Generator(tp, max_batch=4, max_seq=256, temperature=0.0, use_graphs=False).generate(prompts, 8)
+    agree = [sum(x == y for x, y in zip(p.tokens, q.tokens)) / max(1, len(p.tokens)) for p, q in zip(a, b)]
+    first = [p.tokens[:1] == q.tokens[:1] for p, q in zip(a, b)]
+    _done(rank, out_path, {"xgmi": tp.tp.xgmi is not None, "xgmi_calls": tp.tp.xgmi.calls if tp.tp.xgmi else 0,
+                           "agree": agree, "first_equal": first,
+                           "max_prob_diff": max(abs(p.mean_prob - q.mean_prob) for p, q in zip(a, b))})
