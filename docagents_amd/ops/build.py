@@ -61,6 +61,16 @@ def build(force: bool = False, debug: bool = False, verbose: bool = False) -> Pa
     fp = _fingerprint(debug)
     if LIB.exists() and stamp.exists() and stamp.read_text() == fp and not force:
         return LIB
+    # N ranks of one job import the package at once: one builds, the others wait and reuse it
+    import fcntl
+    with open(HERE / "_da_kernels.lock", "w") as lk:
+        fcntl.flock(lk, fcntl.LOCK_EX)
+        if LIB.exists() and stamp.exists() and stamp.read_text() == fp and not force:
+            return LIB
+        return _build_locked(stamp, fp, debug, verbose)
+
+
+def _build_locked(stamp: Path, fp: str, debug: bool, verbose: bool) -> Path:
     hipcc = _hipcc()
     objdir = HERE / "_build"
     objdir.mkdir(exist_ok=True)
@@ -79,7 +89,7 @@ def build(force: bool = False, debug: bool = False, verbose: bool = False) -> Pa
     workers = min(len(_sources()), int(os.environ.get("MAX_JOBS", "8")), 16)
     with cf.ThreadPoolExecutor(max_workers=max(1, workers)) as ex:
         objs = list(ex.map(compile_one, _sources()))
-    tmp = LIB.with_suffix(".so.tmp")
+    tmp = LIB.with_suffix(f".so.tmp{os.getpid()}")
     cmd = [hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", *map(str, objs), "-o", str(tmp)]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:

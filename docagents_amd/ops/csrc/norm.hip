@@ -383,3 +383,40 @@ DA_EXPORT int da_bert_embed_ln_q(const void* ids, const void* positions, const v
       (const bf16_t*)type, (const bf16_t*)g, (const bf16_t*)b, (bf16_t*)y, D, eps, (unsigned char*)yq, (float*)yscale);
   DA_LAUNCH_CHECK();
 }
+
+// SwiGLU on a [M, 2F] projection whose columns are gate/up interleaved in 16-column groups (the
+// w_gu row order of EPI_SWIGLU): out[m, 16j + i] = silu(g[m, 32j + i]) * u[m, 32j + 16 + i].
+// Used when the gate/up GEMM runs on hipBLASLt (no SwiGLU epilogue there); one thread = 8 outputs,
+// 16-B loads/stores, grid-stride over M * F / 8 chunks.
+__global__ void __launch_bounds__(256)
+swiglu_interleaved_kernel(const bf16_t* __restrict__ x, int ldx, bf16_t* __restrict__ y, int ldy, int M, int F) {
+  const long long chunks = (long long)M * (F / 8);
+  const int cpr = F / 8;
+  for (long long c = (long long)blockIdx.x * blockDim.x + threadIdx.x; c < chunks;
+       c += (long long)gridDim.x * blockDim.x) {
+    const int m = (int)(c / cpr), o = (int)(c % cpr) * 8;  // output column o .. o+7 (same 16-group)
+    const int j = o >> 4, i = o & 15;
+    const bf16_t* row = x + (size_t)m * ldx + 32 * j + i;
+    const u32x4_t g = __builtin_nontemporal_load((const u32x4_t*)row);
+    const u32x4_t u = __builtin_nontemporal_load((const u32x4_t*)(row + 16));
+    u32x4_t r;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float g0 = __uint_as_float(g[q] << 16), g1 = __uint_as_float(g[q] & 0xffff0000u);
+      const float u0 = __uint_as_float(u[q] << 16), u1 = __uint_as_float(u[q] & 0xffff0000u);
+      r[q] = pack_bf2(silu(g0) * u0, silu(g1) * u1);
+    }
+    *(u32x4_t*)(y + (size_t)m * ldy + o) = r;
+  }
+}
+
+DA_EXPORT int da_swiglu_interleaved(const void* x, int ldx, void* y, int ldy, int M, int F, void* stream) {
+  if (F % 16 || ldx % 8 || ldy % 8 || ldx < 2 * F || ldy < F) return (int)hipErrorInvalidValue;
+  if (M == 0) return 0;
+  const long long chunks = (long long)M * (F / 8);
+  long long blocks = (chunks + 255) / 256;
+  if (blocks > 256 * 32) blocks = 256 * 32;
+  swiglu_interleaved_kernel<<<(int)blocks, 256, 0, (hipStream_t)stream>>>((const bf16_t*)x, ldx, (bf16_t*)y, ldy,
+                                                                          M, F);
+  DA_LAUNCH_CHECK();
+}

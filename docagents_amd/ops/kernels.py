@@ -36,6 +36,7 @@ _SIGS = {
     "da_gemm_resid_rmsnorm": [c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_int, c_int,
                               c_int, c_int, c_int, c_void_p, c_void_p, c_float, c_void_p, c_int, c_void_p],
     "da_rmsnorm": [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_float, c_void_p],
+    "da_swiglu_interleaved": [c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_void_p],
     "da_layernorm": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_float, c_void_p],
     "da_bert_embed_ln": [c_void_p] * 9 + [c_int, c_int, c_float, c_void_p],
     "da_embed": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p],
@@ -192,6 +193,8 @@ def gemm(a: torch.Tensor, w: torch.Tensor, bias=None, epi: int = EPI_NONE, resid
     if (_BLAS_PREFILL and tile == 0 and splits <= 0 and rms is None and M >= _BLAS_MIN_M
             and (epi in (EPI_NONE, EPI_BIAS) or (epi == EPI_RESID and bias is None))):
         return _blas_gemm(a, w, bias, epi, resid, out)
+    if _BLAS_SWIGLU and epi == EPI_SWIGLU and tile == 0 and splits <= 0 and rms is None and M >= _BLAS_MIN_M:
+        return swiglu_interleaved(torch.mm(a, w.t()), out)
     if tile == 0 and splits <= 0 and gemv_fusable(M, N, K, epi):
         tile, splits = 6, 1  # batch-1 decode: weight-streaming GEMV, one launch, no split-K workspace
     gamma, eps = (None, 0.0) if rms is None else rms
@@ -217,7 +220,24 @@ def gemm(a: torch.Tensor, w: torch.Tensor, bias=None, epi: int = EPI_NONE, resid
 # on the hand-written kernels. Measured sustained on MI355X (profiles/gemm256_w4_r1.txt): hipBLASLt
 # 1.50-1.57 PF/s vs gemm256 1.22-1.31 at M = 32768. DA_BLAS_PREFILL=0 keeps everything on gemm256.
 _BLAS_PREFILL = os.environ.get("DA_BLAS_PREFILL", "1") != "0"
+# Gate/up projection on hipBLASLt + a separate SwiGLU pass (DA_BLAS_SWIGLU=1) instead of gemm256
+# with the fused epilogue: trades 1.5x the output bytes for hipBLASLt's faster main loop. Same-box
+# A/B (profiles/ab_blas_swiglu_r1.txt): +0.3% flagship; DA_BLAS_SWIGLU=0 keeps the fused gemm256.
+_BLAS_SWIGLU = os.environ.get("DA_BLAS_SWIGLU", "1") == "1"
 _BLAS_MIN_M = int(os.environ.get("DA_BLAS_MIN_M", "4096"))
+
+
+def swiglu_interleaved(x: torch.Tensor, out=None) -> torch.Tensor:
+    """[M, 2F] gate/up (16-column interleave, the EPI_SWIGLU weight order) -> silu(gate) * up [M, F]."""
+    _bf16_cuda(x, "x")
+    M, N2 = x.shape
+    _req(N2 % 32 == 0 and x.stride(1) == 1 and x.stride(0) % 8 == 0, "x must be [M, 2F] row-major, F % 16 == 0")
+    if out is None:
+        out = torch.empty((M, N2 // 2), dtype=torch.bfloat16, device=x.device)
+    _req(out.shape == (M, N2 // 2) and out.stride(1) == 1 and out.stride(0) % 8 == 0, "bad out")
+    _check(lib().da_swiglu_interleaved(_ptr(x), x.stride(0), _ptr(out), out.stride(0), M, N2 // 2, _stream()),
+           "swiglu_interleaved")
+    return out
 
 
 def _blas_gemm(a, w, bias, epi, resid, out):

@@ -445,3 +445,25 @@ def test_gemm_resid_rmsnorm_fused(M, N, Kd):
     h_ref = R.gemm_resid_norm(a, w, x_ref, g, 1e-5, out=x_ref)
     _close(x, x_ref, atol=0.03)
     _close(h, h_ref, atol=0.05)
+
+
+@pytest.mark.parametrize("M,F", [(1, 32), (7, 256), (300, 1024), (4097, 8192)])
+def test_swiglu_interleaved(M, F):
+    torch.manual_seed(M + F)
+    x = _rand(M, 2 * F, scale=2.0)
+    got = K.swiglu_interleaved(x)
+    xg = x.float().view(M, F // 16, 2, 16)
+    ref = (torch.nn.functional.silu(xg[:, :, 0]) * xg[:, :, 1]).reshape(M, F)
+    _close(got, ref, atol=0.02)
+
+
+def test_gemm_swiglu_blas_route(monkeypatch):
+    """DA_BLAS_SWIGLU path: hipBLASLt gate/up GEMM + interleaved SwiGLU == fused-epilogue reference."""
+    monkeypatch.setattr(K, "_BLAS_SWIGLU", True)
+    torch.manual_seed(3)
+    M, F, Kd = 4096, 1024, 512
+    gate, up = _rand(F, Kd, scale=Kd ** -0.5), _rand(F, Kd, scale=Kd ** -0.5)
+    a = _rand(M, Kd)
+    got = K.gemm(a, R.interleave_gate_up(gate, up), epi=K.EPI_SWIGLU)
+    ref = torch.nn.functional.silu(a.float() @ gate.float().t()) * (a.float() @ up.float().t())
+    _close(got, ref, atol=0.03)
