@@ -12,6 +12,8 @@ Batching is across requests: texts are packed by tokens, prompts are generated t
 """
 from __future__ import annotations
 
+import os
+
 import threading
 import time
 
@@ -51,7 +53,8 @@ class Engine:
             self.decoder = LlamaDecoder(self.dec_cfg, self.device, seed=seed, tp=tp)
             self.decoder.alloc_cache(max_batch + 1, max_seq)
             self.gen = Generator(self.decoder, max_batch=max_batch, max_seq=max_seq, temperature=temperature,
-                                 seed=seed, eos=sorted(self.chat.eos_ids), use_graphs=use_graphs)
+                                 seed=seed, eos=sorted(self.chat.eos_ids), use_graphs=use_graphs,
+                                 share_prefix=os.environ.get("DA_SHARE_PREFIX", "1") != "0")
         from ..index import make_index
         self.index = make_index(index_kind, self.enc_cfg.hidden, self.device, lists=ivf_lists, probes=ivf_probes)
         self._prefix_cache: dict[str, list[int]] = {}

@@ -37,8 +37,11 @@ class GenResult:
 class Generator:
     def __init__(self, model: LlamaDecoder, max_batch: int = 64, max_seq: int = 4096, temperature: float = 0.2,
                  seed: int = 0, eos=(), use_graphs: bool = True, max_prefill_tokens: int = 32768,
-                 check_every: int = 16):
+                 check_every: int = 16, share_prefix: bool = True, min_shared_prefix: int = 64):
         self.model = model
+        # prompts of one wave that start with the same tokens (the Answer / Summarize system prompt:
+        # ~260 tokens of every QA prompt) prefill that head once; see _generate_wave
+        self.share_prefix, self.min_shared_prefix = share_prefix, min_shared_prefix
         self.max_batch = max_batch
         self.temperature, self.seed = temperature, seed
         self.eos = tuple(e for e in eos if e is not None)[:4]
@@ -53,7 +56,7 @@ class Generator:
         self.dummy_slot = self.cache.acquire(1)[0]
         self.states: dict[tuple, DecodeState] = {}
         self.stats = {"prefill_s": 0.0, "decode_s": 0.0, "prefill_tokens": 0, "decode_steps": 0, "decode_tokens": 0,
-                      "calls": 0}
+                      "calls": 0, "shared_prefix_tokens": 0}
         if self.is_cuda:
             from ..ops import kernels
             c = model.cfg
@@ -87,9 +90,31 @@ class Generator:
             t.copy_(v)
         st.graph = g
 
-    def _prefill_into(self, st: DecodeState, prompts, slots, row0: int):
-        """Prefill prompts (rows row0..) in token-bounded chunks; sample each first token."""
+    def shared_prefix_len(self, prompts) -> int:
+        """Tokens every prompt of the wave starts with (0 when sharing does not pay: fewer than 2
+        prompts or a head shorter than min_shared_prefix); at least one token of each prompt stays
+        in its own prefill, which produces that prompt's first-token logits."""
+        if not self.share_prefix or len(prompts) < 2:
+            return 0
+        first = prompts[0]
+        n = min(len(p) for p in prompts) - 1
+        if n < self.min_shared_prefix:
+            return 0
+        for p in prompts[1:]:
+            if p[:n] != first[:n]:
+                k = 0
+                while k < n and p[k] == first[k]:
+                    k += 1
+                n = k
+                if n < self.min_shared_prefix:
+                    return 0
+        return n
+
+    def _prefill_into(self, st: DecodeState, prompts, slots, row0: int, prefix: tuple[int, int] | None = None):
+        """Prefill prompts (rows row0..) in token-bounded chunks; sample each first token.
+        prefix = (slot, P): the prompts are suffixes of a P-token head already in ``slot``."""
         m, dev = self.model, self.model.device
+        P = 0 if prefix is None else prefix[1]
         i = 0
         n = len(prompts)
         while i < n:
@@ -99,11 +124,13 @@ class Generator:
                 j += 1
             chunk = prompts[i:j]
             flat, pos, cu, lens = pack_prompts(chunk)
+            if P:
+                pos += P
             slot_tok = np.repeat(np.asarray(slots[i:j], dtype=np.int32), lens)
             last = (cu[1:] - 1).astype(np.int64)
             t0 = time.perf_counter()
             to = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev, non_blocking=True)  # noqa: E731
-            logits = m.prefill(to(flat), to(pos), to(slot_tok), to(cu), int(lens.max()), to(last))
+            logits = m.prefill(to(flat), to(pos), to(slot_tok), to(cu), int(lens.max()), to(last), prefix=prefix)
             r0, r1 = row0 + i, row0 + j
             m.ops.sample(logits, self.temperature, self.seed, 0, out_tok=st.tokens[r0:r1], out_lp=st.lp[r0:r1],
                          conf=st.conf[r0:r1], active=st.active[r0:r1], ctr=st.pos[r0:r1], pos=st.pos[r0:r1],
@@ -147,7 +174,23 @@ class Generator:
             st.pos.copy_(ht[0]); st.lens.copy_(ht[1]); st.slot.copy_(ht[2]); st.active.copy_(ht[3])
             st.start.copy_(ht[4])
             st.tokens.zero_(); st.hist.fill_(-1); st.conf.zero_()
-            self._prefill_into(st, prompts, slots, 0)
+            P = self.shared_prefix_len(prompts)
+            if P:
+                # the shared head once (into row 0's slot), then only the suffixes, attending to the
+                # head's keys in that slot; finally the head's K/V are copied into every other slot
+                # so decode sees ordinary per-sequence caches
+                t0 = time.perf_counter()
+                to = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev, non_blocking=True)  # noqa: E731
+                m.prefill(to(np.asarray(prompts[0][:P], dtype=np.int32)), to(np.arange(P, dtype=np.int32)),
+                          to(np.full(P, slots[0], dtype=np.int32)), to(np.array([0, P], dtype=np.int32)), P,
+                          to(np.array([P - 1], dtype=np.int64)))
+                self.stats["prefill_tokens"] += P
+                self.stats["shared_prefix_tokens"] += P * (n - 1)
+                self.stats["prefill_s"] += time.perf_counter() - t0
+                self._prefill_into(st, [p[P:] for p in prompts], slots, 0, prefix=(slots[0], P))
+                self.cache.copy_prefix(slots[0], slots[1:], P)
+            else:
+                self._prefill_into(st, prompts, slots, 0)
             # padded rows: keep them inside the dummy slot's first positions
             if B > n:
                 st.pos[n:].zero_(); st.lens[n:].fill_(1)

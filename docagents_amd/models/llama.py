@@ -149,6 +149,15 @@ class KVCache:
     def release(self, ids):
         self.free.extend(ids)
 
+    def copy_prefix(self, src: int, dst: list[int], n: int) -> None:
+        """Positions [0, n) of slot ``src`` (every layer, K and V) -> the same positions of ``dst``:
+        the shared prompt head prefilled once becomes part of every sequence's own cache."""
+        if not dst or n <= 0:
+            return
+        idx = torch.as_tensor(dst, dtype=torch.long, device=self.buf.device)
+        head = self.buf[:, :, src:src + 1, :, :n]
+        self.buf[:, :, idx, :, :n] = head.expand(-1, -1, len(dst), -1, -1, -1)
+
     @staticmethod
     def bytes_for(cfg: DecoderConfig, slots: int, max_seq: int, tp_size: int = 1) -> int:
         return cfg.layers * 2 * slots * (cfg.kv_heads // tp_size) * max_seq * cfg.head_dim * 2
@@ -206,8 +215,10 @@ class LlamaDecoder:
 
     # ------------------------------------------------------------- prefill
     def prefill(self, ids: torch.Tensor, pos: torch.Tensor, slot_tok: torch.Tensor, cu: torch.Tensor,
-                max_seqlen: int, last_idx: torch.Tensor) -> torch.Tensor:
-        """Packed causal prefill; writes the KV cache; returns logits [B, V] of each sequence's last token."""
+                max_seqlen: int, last_idx: torch.Tensor, prefix: tuple[int, int] | None = None) -> torch.Tensor:
+        """Packed causal prefill; writes the KV cache; returns logits [B, V] of each sequence's last token.
+        prefix = (slot, P): every sequence continues a shared P-token head already in ``slot``'s cache
+        (``pos`` then starts at P); attention reads those keys from the cache."""
         c, o, cache = self.cfg, self.ops, self.cache
         D, hl, kl = c.head_dim, self.hl, self.kl
         x = o.embed(ids, self.w["embed"])
@@ -215,8 +226,9 @@ class LlamaDecoder:
             h = o.rmsnorm(x, L["ln_attn"], c.eps)
             qkv = o.gemm(h, L["wqkv"])
             o.rope_cache(qkv, pos, self.cos_sin, hl, kl, D, slot=slot_tok, k_cache=cache.k(li), v_cache=cache.v(li))
+            pre = None if prefix is None else (cache.k(li)[prefix[0]], cache.v(li)[prefix[0]], prefix[1])
             a = o.flash_attn_varlen(qkv[:, :hl * D], qkv[:, hl * D:(hl + kl) * D], qkv[:, (hl + kl) * D:], cu,
-                                    max_seqlen, hl, kl, D, causal=True)
+                                    max_seqlen, hl, kl, D, causal=True, prefix=pre)
             del qkv, h
             x = self._attn_out_and_mlp(L, a, x)
         return self._logits(x.index_select(0, last_idx))

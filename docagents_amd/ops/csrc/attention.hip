@@ -177,11 +177,23 @@ struct FA2Cfg {
   static constexpr int SMEM = 2 * (KBUF + VBUF);
 };
 
+// Shared-prefix keys (pre.len > 0): every sequence's keys are [pre.len prefix keys | its own keys];
+// the prefix K/V live once in a KV-cache slot ([Hkv][max_seq][D]: head stride pre.hstride, row
+// stride D), RoPE already applied. Query i of a sequence sits at key position pre.len + i (causal
+// mask bottom-right aligned), so a batch whose prompts share a system-prompt head prefills that
+// head once and only the suffixes here.
+struct FaPrefix {
+  const bf16_t* k;
+  const bf16_t* v;
+  long long hstride;
+  int len;
+};
+
 template <int D, int NW>
 __global__ void __launch_bounds__(64 * NW, 8 / NW)
 flash_attn_v2_kernel(const bf16_t* __restrict__ q, const bf16_t* __restrict__ k, const bf16_t* __restrict__ v,
                      int ldq, int ldk, int ldv, const int* __restrict__ cu, int H, int Hkv, int causal,
-                     float c, bf16_t* __restrict__ o, int ldo) {
+                     float c, bf16_t* __restrict__ o, int ldo, FaPrefix pre) {
   using C = FA2Cfg<D, NW>;
   constexpr int KT = C::KT, NDS = D / 16, NDB = D / 32, CPR = C::CPR, LPT = C::LPT, NT = C::NT;
   constexpr bool EVEN = (KT * CPR) % NT == 0;  // every thread stages exactly LPT chunks
@@ -211,20 +223,28 @@ flash_attn_v2_kernel(const bf16_t* __restrict__ q, const bf16_t* __restrict__ k,
     for (int r = 0; r < 16; ++r) oacc[i][r] = 0.f;
   float m_run = -INFINITY, l_part = 0.f;
 
-  const int kv_end = causal ? min(L, q0 + C::QB) : L;
-  const int wave_end = causal ? min(L, wq0 + C::QW) : L;
+  const int P = pre.len, Lk = P + L;  // keys: [prefix | own]; own query i is key P + i
+  const int kv_end = causal ? min(Lk, P + q0 + C::QB) : Lk;
+  const int wave_end = causal ? min(Lk, P + wq0 + C::QW) : Lk;
   const int ntiles = (kv_end + KT - 1) / KT;
 
   const bf16_t* kbase_p = k + (size_t)s0 * ldk + hk * D;
   const bf16_t* vbase_p = v + (size_t)s0 * ldv + hk * D;
+  const bf16_t* kpre = pre.k + hk * pre.hstride;
+  const bf16_t* vpre = pre.v + hk * pre.hstride;
   u32x4_t kst[LPT], vst[LPT];
   auto load_tile = [&](int t) {
 #pragma unroll
     for (int i = 0; i < LPT; ++i) {
       const int idx = tid + NT * i, r = idx / CPR, cc = idx % CPR, key = t * KT + r;
-      if ((EVEN || idx < KT * CPR) && key < L) {
-        kst[i] = *(const u32x4_t*)(kbase_p + (size_t)key * ldk + cc * 8);
-        vst[i] = *(const u32x4_t*)(vbase_p + (size_t)key * ldv + cc * 8);
+      if ((EVEN || idx < KT * CPR) && key < Lk) {
+        if (key >= P) {
+          kst[i] = *(const u32x4_t*)(kbase_p + (size_t)(key - P) * ldk + cc * 8);
+          vst[i] = *(const u32x4_t*)(vbase_p + (size_t)(key - P) * ldv + cc * 8);
+        } else {
+          kst[i] = *(const u32x4_t*)(kpre + (size_t)key * D + cc * 8);
+          vst[i] = *(const u32x4_t*)(vpre + (size_t)key * D + cc * 8);
+        }
       } else {
         kst[i] = u32x4_t{0, 0, 0, 0};
         vst[i] = u32x4_t{0, 0, 0, 0};
@@ -266,13 +286,13 @@ flash_attn_v2_kernel(const bf16_t* __restrict__ q, const bf16_t* __restrict__ k,
           sacc[hh] = mfma32(a, qf[ds], sacc[hh]);
         }
       }
-      if (kb + KT > L || (causal && kb + KT - 1 > wq0)) {
+      if (kb + KT > Lk || (causal && kb + KT - 1 > P + wq0)) {
 #pragma unroll
         for (int hh = 0; hh < 2; ++hh)
 #pragma unroll
           for (int r = 0; r < 16; ++r) {
             const int key = kb + hh * 32 + 8 * (r >> 2) + 4 * hi + (r & 3);
-            if (key >= L || (causal && key > qi)) sacc[hh][r] = -INFINITY;
+            if (key >= Lk || (causal && key > P + qi)) sacc[hh][r] = -INFINITY;
           }
       }
       float mx = sacc[0][0];
@@ -829,7 +849,7 @@ DA_EXPORT void da_set_flash_waves(int nw) { g_fa_waves = nw; }
 template <int NW>
 static int launch_fa2(const void* q, const void* k, const void* v, int ldq, int ldk, int ldv, const void* cu_seqlens,
                       int B, int max_seqlen, int H, int Hkv, int D, int causal, float sl2e, void* o, int ldo,
-                      hipStream_t s) {
+                      FaPrefix pre, hipStream_t s) {
   static bool attr_set = false;
   if (!attr_set) {
     (void)hipFuncSetAttribute((const void*)flash_attn_v2_kernel<128, NW>, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -838,7 +858,7 @@ static int launch_fa2(const void* q, const void* k, const void* v, int ldq, int 
   }
   dim3 grid((max_seqlen + 32 * NW - 1) / (32 * NW), H, B);
 #define FA_ARGS (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, ldq, ldk, ldv, (const int*)cu_seqlens, H, Hkv, \
-                causal, sl2e, (bf16_t*)o, ldo
+                causal, sl2e, (bf16_t*)o, ldo, pre
   switch (D) {
     case 32: flash_attn_v2_kernel<32, NW><<<grid, 64 * NW, FA2Cfg<32, NW>::SMEM, s>>>(FA_ARGS); break;
     case 64: flash_attn_v2_kernel<64, NW><<<grid, 64 * NW, FA2Cfg<64, NW>::SMEM, s>>>(FA_ARGS); break;
@@ -850,14 +870,20 @@ static int launch_fa2(const void* q, const void* k, const void* v, int ldq, int 
   return (int)hipGetLastError();
 }
 
+// pre_k / pre_v: shared-prefix K/V of KV head 0 in a cache slot (nullptr / pre_len 0: none),
+// pre_hstride: elements between KV heads there (max_seq * D).
 DA_EXPORT int da_flash_attn_v2(const void* q, const void* k, const void* v, int ldq, int ldk, int ldv,
                                const void* cu_seqlens, int B, int max_seqlen, int H, int Hkv, int D, int causal,
-                               float scale, void* o, int ldo, void* stream) {
+                               float scale, void* o, int ldo, const void* pre_k, const void* pre_v,
+                               long long pre_hstride, int pre_len, void* stream) {
   if (H % Hkv || ldq % 8 || ldk % 8 || ldv % 8 || ldo % 4) return (int)hipErrorInvalidValue;
+  if (pre_len < 0 || (pre_len > 0 && (!pre_k || !pre_v || pre_hstride < (long long)pre_len * D)))
+    return (int)hipErrorInvalidValue;
   if (B == 0 || max_seqlen == 0) return 0;
   const float sl2e = scale * 1.4426950408889634f;
   hipStream_t s = (hipStream_t)stream;
+  const FaPrefix pre{(const bf16_t*)pre_k, (const bf16_t*)pre_v, pre_hstride, pre_len};
   if (g_fa_waves == 8 || (g_fa_waves == 0 && !causal))
-    return launch_fa2<8>(q, k, v, ldq, ldk, ldv, cu_seqlens, B, max_seqlen, H, Hkv, D, causal, sl2e, o, ldo, s);
-  return launch_fa2<4>(q, k, v, ldq, ldk, ldv, cu_seqlens, B, max_seqlen, H, Hkv, D, causal, sl2e, o, ldo, s);
+    return launch_fa2<8>(q, k, v, ldq, ldk, ldv, cu_seqlens, B, max_seqlen, H, Hkv, D, causal, sl2e, o, ldo, pre, s);
+  return launch_fa2<4>(q, k, v, ldq, ldk, ldv, cu_seqlens, B, max_seqlen, H, Hkv, D, causal, sl2e, o, ldo, pre, s);
 }

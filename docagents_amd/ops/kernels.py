@@ -22,6 +22,7 @@ _LIB_PATH = Path(__file__).resolve().parent / "_da_kernels.so"
 
 EPI_NONE, EPI_BIAS, EPI_GELU, EPI_SWIGLU, EPI_RESID = 0, 1, 2, 3, 4
 
+c_longlong = ctypes.c_longlong
 c_void_p, c_int, c_float, c_uint, c_size_t = (ctypes.c_void_p, ctypes.c_int, ctypes.c_float,
                                              ctypes.c_uint, ctypes.c_size_t)
 
@@ -47,7 +48,8 @@ _SIGS = {
     "da_flash_attn_varlen": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_int,
                              c_int, c_int, c_int, c_int, c_float, c_void_p, c_int, c_void_p],
     "da_flash_attn_v2": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_int,
-                             c_int, c_int, c_int, c_int, c_float, c_void_p, c_int, c_void_p],
+                         c_int, c_int, c_int, c_int, c_float, c_void_p, c_int, c_void_p, c_void_p, c_longlong,
+                         c_int, c_void_p],
     "da_set_gqa_mfma": [c_int],
     "da_set_flash_waves": [c_int],
     "da_set_gemm_pingpong": [c_int],
@@ -448,8 +450,10 @@ FLASH_IMPL = "v2"  # "v1" (16x16 MFMA, 64 queries/workgroup) kept for A/B measur
 
 
 def flash_attn_varlen(q, k, v, cu_seqlens, max_seqlen: int, H: int, Hkv: int, D: int, causal: bool,
-                      scale: float | None = None, out=None, impl: str | None = None):
-    """q/k/v: 2-D [T, *] views with head h at columns h*D (strided views into a packed qkv are fine)."""
+                      scale: float | None = None, out=None, impl: str | None = None, prefix=None):
+    """q/k/v: 2-D [T, *] views with head h at columns h*D (strided views into a packed qkv are fine).
+    prefix = (k_pre, v_pre, P): shared-prefix keys of every sequence, one KV-cache slot's
+    [Hkv, max_seq, D] K and V (RoPE applied); query i of a sequence is key P + i."""
     for t, n in ((q, "q"), (k, "k"), (v, "v")):
         _bf16_cuda(t, n)
         _req(t.dim() == 2 and t.stride(1) == 1 and t.stride(0) % 8 == 0 and t.data_ptr() % 16 == 0, f"{n} layout")
@@ -461,10 +465,25 @@ def flash_attn_varlen(q, k, v, cu_seqlens, max_seqlen: int, H: int, Hkv: int, D:
         out = torch.empty((T, H * D), dtype=torch.bfloat16, device=q.device)
     scale = scale if scale is not None else 1.0 / math.sqrt(D)
     B = cu_seqlens.numel() - 1
-    fn = lib().da_flash_attn_v2 if (impl or FLASH_IMPL) == "v2" else lib().da_flash_attn_varlen
-    _check(fn(_ptr(q), _ptr(k), _ptr(v), q.stride(0), k.stride(0), v.stride(0),
-              _ptr(cu_seqlens), B, int(max_seqlen), H, Hkv, D, int(causal), float(scale),
-              _ptr(out), out.stride(0), _stream()), "flash_attn_varlen")
+    if (impl or FLASH_IMPL) != "v2":
+        _req(prefix is None, "shared-prefix attention needs the v2 kernel")
+        _check(lib().da_flash_attn_varlen(_ptr(q), _ptr(k), _ptr(v), q.stride(0), k.stride(0), v.stride(0),
+                                          _ptr(cu_seqlens), B, int(max_seqlen), H, Hkv, D, int(causal), float(scale),
+                                          _ptr(out), out.stride(0), _stream()), "flash_attn_varlen")
+        return out
+    kp = vp = None
+    hstride, P = 0, 0
+    if prefix is not None:
+        kp, vp, P = prefix
+        P = int(P)
+        _bf16_cuda(kp, "k_pre"); _bf16_cuda(vp, "v_pre")
+        _req(kp.dim() == 3 and kp.shape == vp.shape and kp.shape[0] == Hkv and kp.shape[2] == D
+             and kp.is_contiguous() and vp.is_contiguous() and 0 <= P <= kp.shape[1], "prefix K/V [Hkv, max_seq, D]")
+        hstride = kp.shape[1] * D
+    _check(lib().da_flash_attn_v2(_ptr(q), _ptr(k), _ptr(v), q.stride(0), k.stride(0), v.stride(0),
+                                  _ptr(cu_seqlens), B, int(max_seqlen), H, Hkv, D, int(causal), float(scale),
+                                  _ptr(out), out.stride(0), _ptr(kp), _ptr(vp), hstride, P, _stream()),
+           "flash_attn_varlen")
     return out
 
 

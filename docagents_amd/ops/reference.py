@@ -141,12 +141,18 @@ def rope_cache(qkv, pos, cos_sin, H, Hkv, D, slot=None, k_cache=None, v_cache=No
     return qkv
 
 
-def flash_attn_varlen(q, k, v, cu_seqlens, max_seqlen, H, Hkv, D, causal, scale=None, out=None):
+def flash_attn_varlen(q, k, v, cu_seqlens, max_seqlen, H, Hkv, D, causal, scale=None, out=None, prefix=None):
+    """prefix = (k_pre [Hkv, >=P, D], v_pre, P): every sequence's keys are the P shared prefix keys
+    followed by its own; query i sits at key position P + i (bottom-right causal)."""
     scale = scale if scale is not None else 1.0 / math.sqrt(D)
     T = q.shape[0]
     res = torch.empty((T, H * D), dtype=q.dtype, device=q.device)
     cu = cu_seqlens.tolist()
     G = H // Hkv
+    P = 0 if prefix is None else int(prefix[2])
+    if P:
+        kp = prefix[0][:, :P].float().repeat_interleave(G, 0)   # [H, P, D]
+        vp = prefix[1][:, :P].float().repeat_interleave(G, 0)
     for b in range(len(cu) - 1):
         s0, s1 = cu[b], cu[b + 1]
         L = s1 - s0
@@ -155,9 +161,11 @@ def flash_attn_varlen(q, k, v, cu_seqlens, max_seqlen, H, Hkv, D, causal, scale=
         qq = q[s0:s1, :H * D].float().view(L, H, D).transpose(0, 1)
         kk = k[s0:s1, :Hkv * D].float().view(L, Hkv, D).transpose(0, 1).repeat_interleave(G, 0)
         vv = v[s0:s1, :Hkv * D].float().view(L, Hkv, D).transpose(0, 1).repeat_interleave(G, 0)
+        if P:
+            kk, vv = torch.cat([kp, kk], 1), torch.cat([vp, vv], 1)
         s = (qq @ kk.transpose(1, 2)) * scale
         if causal:
-            m = torch.ones(L, L, dtype=torch.bool, device=q.device).triu(1)
+            m = torch.ones(L, P + L, dtype=torch.bool, device=q.device).triu(P + 1)
             s = s.masked_fill(m, float("-inf"))
         p = s.softmax(-1)
         res[s0:s1] = (p @ vv).transpose(0, 1).reshape(L, H * D).to(q.dtype)

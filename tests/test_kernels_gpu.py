@@ -467,3 +467,24 @@ def test_gemm_swiglu_blas_route(monkeypatch):
     got = K.gemm(a, R.interleave_gate_up(gate, up), epi=K.EPI_SWIGLU)
     ref = torch.nn.functional.silu(a.float() @ gate.float().t()) * (a.float() @ up.float().t())
     _close(got, ref, atol=0.03)
+
+
+@pytest.mark.parametrize("H,Hkv,D,P", [(32, 32, 96, 261), (8, 2, 128, 64), (4, 4, 64, 1), (4, 2, 96, 130)])
+@pytest.mark.parametrize("nw", [4, 8])
+def test_flash_attn_shared_prefix(H, Hkv, D, P, nw):
+    """Suffix queries attend to P shared-prefix keys held in a KV-cache slot + their own keys."""
+    torch.manual_seed(H + D + P)
+    lens = [1, 63, 64, 200, 7]
+    T = sum(lens)
+    qkv = _rand(T, (H + 2 * Hkv) * D)
+    q, k, v = qkv[:, :H * D], qkv[:, H * D:(H + Hkv) * D], qkv[:, (H + Hkv) * D:]
+    cu = torch.tensor([0] + list(np.cumsum(lens)), device=DEV, dtype=torch.int32)
+    kc, vc = _rand(3, Hkv, 512, D), _rand(3, Hkv, 512, D)
+    pre = (kc[1], vc[1], P)
+    K.lib().da_set_flash_waves(nw)
+    try:
+        got = K.flash_attn_varlen(q, k, v, cu, max(lens), H, Hkv, D, True, prefix=pre)
+    finally:
+        K.lib().da_set_flash_waves(0)
+    ref = R.flash_attn_varlen(q, k, v, cu, max(lens), H, Hkv, D, True, prefix=pre)
+    _close(got, ref, atol=0.02)
