@@ -91,9 +91,10 @@ class Generator:
         st.graph = g
 
     def shared_prefix_len(self, prompts) -> int:
-        """Tokens every prompt of the wave starts with (0 when sharing does not pay: fewer than 2
-        prompts or a head shorter than min_shared_prefix); at least one token of each prompt stays
-        in its own prefill, which produces that prompt's first-token logits."""
+        """Tokens every prompt of the wave starts with, rounded down to a multiple of 64 (the decode
+        attention's key tile), or 0 when sharing does not pay (fewer than 2 prompts or a head
+        shorter than min_shared_prefix); at least one token of each prompt stays in its own
+        prefill, which produces that prompt's first-token logits."""
         if not self.share_prefix or len(prompts) < 2:
             return 0
         first = prompts[0]
@@ -108,7 +109,8 @@ class Generator:
                 n = k
                 if n < self.min_shared_prefix:
                     return 0
-        return n
+        n -= n % 64
+        return n if n >= self.min_shared_prefix else 0
 
     def _prefill_into(self, st: DecodeState, prompts, slots, row0: int, prefix: tuple[int, int] | None = None):
         """Prefill prompts (rows row0..) in token-bounded chunks; sample each first token.
@@ -177,8 +179,8 @@ class Generator:
             P = self.shared_prefix_len(prompts)
             if P:
                 # the shared head once (into row 0's slot), then only the suffixes, attending to the
-                # head's keys in that slot; finally the head's K/V are copied into every other slot
-                # so decode sees ordinary per-sequence caches
+                # head's keys in that slot; decode reads keys [0, P) of every row from that slot too
+                # (st.pre), so the head's K/V exist once: prefilled once, read from L2/MALL by all rows
                 t0 = time.perf_counter()
                 to = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev, non_blocking=True)  # noqa: E731
                 m.prefill(to(np.asarray(prompts[0][:P], dtype=np.int32)), to(np.arange(P, dtype=np.int32)),
@@ -188,8 +190,11 @@ class Generator:
                 self.stats["shared_prefix_tokens"] += P * (n - 1)
                 self.stats["prefill_s"] += time.perf_counter() - t0
                 self._prefill_into(st, [p[P:] for p in prompts], slots, 0, prefix=(slots[0], P))
-                self.cache.copy_prefix(slots[0], slots[1:], P)
+                pre = np.zeros((B, 2), dtype=np.int32)
+                pre[:n] = (P, slots[0])
+                st.pre.copy_(torch.from_numpy(pre).to(dev))
             else:
+                st.pre.zero_()
                 self._prefill_into(st, prompts, slots, 0)
             # padded rows: keep them inside the dummy slot's first positions
             if B > n:

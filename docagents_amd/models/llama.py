@@ -149,15 +149,6 @@ class KVCache:
     def release(self, ids):
         self.free.extend(ids)
 
-    def copy_prefix(self, src: int, dst: list[int], n: int) -> None:
-        """Positions [0, n) of slot ``src`` (every layer, K and V) -> the same positions of ``dst``:
-        the shared prompt head prefilled once becomes part of every sequence's own cache."""
-        if not dst or n <= 0:
-            return
-        idx = torch.as_tensor(dst, dtype=torch.long, device=self.buf.device)
-        head = self.buf[:, :, src:src + 1, :, :n]
-        self.buf[:, :, idx, :, :n] = head.expand(-1, -1, len(dst), -1, -1, -1)
-
     @staticmethod
     def bytes_for(cfg: DecoderConfig, slots: int, max_seq: int, tp_size: int = 1) -> int:
         return cfg.layers * 2 * slots * (cfg.kv_heads // tp_size) * max_seq * cfg.head_dim * 2
@@ -249,7 +240,7 @@ class LlamaDecoder:
                 qkv = o.gemm(h, L["wqkv"], out=st.qkv)
             o.rope_cache(qkv, st.pos, self.cos_sin, hl, kl, D, slot=st.slot, k_cache=cache.k(li), v_cache=cache.v(li))
             a = o.decode_attn(qkv, cache.k(li), cache.v(li), st.lens, st.slot, hl, kl, D, max_len=cache.max_seq,
-                              out=st.attn)
+                              out=st.attn, pre=st.pre)
             self._attn_out_and_mlp(L, a, x)
         logits = self._logits(x)
         st.logits.copy_(logits)
@@ -272,7 +263,7 @@ class LlamaDecoder:
             qkv = o.gemm(h, L["wqkv"], out=st.qkv)
             o.rope_cache(qkv, st.pos, self.cos_sin, hl, kl, D, slot=st.slot, k_cache=cache.k(li), v_cache=cache.v(li))
             a = o.decode_attn(qkv, cache.k(li), cache.v(li), st.lens, st.slot, hl, kl, D, max_len=cache.max_seq,
-                              out=st.attn)
+                              out=st.attn, pre=st.pre)
             h = o.gemm_resid_norm(a, L["wo"], x, L["ln_mlp"], c.eps, out=x, h_out=st.h)      # x += o; h = norm(x)
             g = o.gemm(h, L["w_gu"], epi=EPI_SWIGLU)
             nxt = layers[li + 1]["ln_attn"] if li + 1 < len(layers) else self.w["norm"]
@@ -305,6 +296,7 @@ class DecodeState:
         self.slot = torch.zeros(B, **i32)
         self.active = torch.zeros(B, **i32)
         self.start = torch.zeros(B, **i32)
+        self.pre = torch.zeros(B, 2, **i32)  # (P, slot): shared prompt head of row b (decode_attn pre)
         self.hist = torch.full((B, max(1, max_new)), -1, **i32)
         self.conf = torch.zeros(B, 2, dtype=torch.float32, device=dev)
         self.lp = torch.zeros(B, dtype=torch.float32, device=dev)

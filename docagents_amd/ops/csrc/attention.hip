@@ -377,6 +377,7 @@ template <int D, int G, int VAR>
 __global__ void __launch_bounds__(256)
 decode_attn_kernel(const bf16_t* __restrict__ q, int ldq, const bf16_t* __restrict__ kc,
                    const bf16_t* __restrict__ vc, const int* __restrict__ lens, const int* __restrict__ slot,
+                   const int* __restrict__ pre,
                    int H, int Hkv, int max_seq, int chunk, int nsplit, float scale_log2e,
                    float* __restrict__ po, float* __restrict__ pm, float* __restrict__ pl) {
   constexpr int KT = 64;
@@ -397,6 +398,9 @@ decode_attn_kernel(const bf16_t* __restrict__ q, int ldq, const bf16_t* __restri
   const int kend = min(L, kstart + chunk);
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const size_t cbase = ((size_t)slot[b] * Hkv + hk) * (size_t)max_seq * D;
+  const int P = pre ? pre[2 * b] : 0;  // shared-prefix keys [0, P) live in slot pre[2b + 1]
+  const size_t pbase = P ? ((size_t)pre[2 * b + 1] * Hkv + hk) * (size_t)max_seq * D : cbase;
+  DA_ASSERT(P % 64 == 0 && P <= L);
 
   for (int i = tid; i < G * D; i += 256) {
     const int g = i / D, d = i % D;
@@ -417,8 +421,9 @@ decode_attn_kernel(const bf16_t* __restrict__ q, int ldq, const bf16_t* __restri
 
   for (int t0 = kstart + w * KT; t0 < kend; t0 += 4 * KT) {
     const int nk = min(KT, kend - t0);
-    const bf16_t* kb = kc + cbase + (size_t)t0 * D;
-    const bf16_t* vb = vc + cbase + (size_t)t0 * D;
+    const bool shared = t0 < P;
+    const bf16_t* kb = kc + (shared ? pbase : cbase) + (size_t)t0 * D;
+    const bf16_t* vb = vc + (shared ? pbase : cbase) + (size_t)t0 * D;
     // K first (V is loaded after the scores: keeps ~100 VGPRs live instead of ~200, so 4-5
     // waves per SIMD hide the HBM latency instead of 2). VAR bit0: non-temporal loads (the KV
     // stream is read once per step); bit1: issue V together with K.
@@ -581,6 +586,7 @@ template <int D, int G>
 __global__ void __launch_bounds__(256)
 decode_attn_gqa_kernel(const bf16_t* __restrict__ q, int ldq, const bf16_t* __restrict__ kc,
                        const bf16_t* __restrict__ vc, const int* __restrict__ lens, const int* __restrict__ slot,
+                   const int* __restrict__ pre,
                        int H, int Hkv, int max_seq, int chunk, int nsplit, float scale_log2e,
                        float* __restrict__ po, float* __restrict__ pm, float* __restrict__ pl) {
   static_assert(D == 64 || D == 128, "GQA MFMA decode supports head dims 64 and 128");
@@ -599,6 +605,9 @@ decode_attn_gqa_kernel(const bf16_t* __restrict__ q, int ldq, const bf16_t* __re
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int fr = lane & 15, fg = lane >> 4;
   const size_t cbase = ((size_t)slot[b] * Hkv + hk) * (size_t)max_seq * D;
+  const int P = pre ? pre[2 * b] : 0;  // shared-prefix keys [0, P) live in slot pre[2b + 1]
+  const size_t pbase = P ? ((size_t)pre[2 * b + 1] * Hkv + hk) * (size_t)max_seq * D : cbase;
+  DA_ASSERT(P % 64 == 0 && P <= L);
   char* myv = sv + w * VBYTES;
 
   bf16x8_t qf[NDS];
@@ -614,8 +623,9 @@ decode_attn_gqa_kernel(const bf16_t* __restrict__ q, int ldq, const bf16_t* __re
 
   for (int t0 = kstart + w * KT; t0 < kend; t0 += 4 * KT) {
     const int nk = min(KT, kend - t0);
-    const bf16_t* kb = kc + cbase + (size_t)t0 * D;
-    const bf16_t* vb = vc + cbase + (size_t)t0 * D;
+    const bool shared = t0 < P;
+    const bf16_t* kb = kc + (shared ? pbase : cbase) + (size_t)t0 * D;
+    const bf16_t* vb = vc + (shared ? pbase : cbase) + (size_t)t0 * D;
     // ---- K straight to registers (A operand rows = keys), then the V tile by LDS-DMA ----
     u32x4_t kr[4][NDS];
 #pragma unroll
@@ -623,7 +633,8 @@ decode_attn_gqa_kernel(const bf16_t* __restrict__ q, int ldq, const bf16_t* __re
 #pragma unroll
       for (int ds = 0; ds < NDS; ++ds) {
         const int key = min(16 * t + fr, nk - 1);
-        kr[t][ds] = __builtin_nontemporal_load((const u32x4_t*)(kb + (size_t)key * D + ds * 32 + fg * 8));
+        const u32x4_t* src = (const u32x4_t*)(kb + (size_t)key * D + ds * 32 + fg * 8);
+        kr[t][ds] = __builtin_nontemporal_load(src);
       }
 #pragma unroll
     for (int i = 0; i < NDMA; ++i) {
@@ -760,9 +771,9 @@ DA_EXPORT int da_flash_attn_varlen(const void* q, const void* k, const void* v, 
 
 template <int D, int VAR>
 static int launch_decode_v(int G, dim3 grid, hipStream_t s, const bf16_t* q, int ldq, const bf16_t* kc,
-                           const bf16_t* vc, const int* lens, const int* slot, int H, int Hkv, int max_seq, int chunk,
+                           const bf16_t* vc, const int* lens, const int* slot, const int* pre, int H, int Hkv, int max_seq, int chunk,
                            int nsplit, float sl2e, float* po, float* pm, float* pl) {
-#define DEC(GG) decode_attn_kernel<D, GG, VAR><<<grid, 256, 0, s>>>(q, ldq, kc, vc, lens, slot, H, Hkv, max_seq, \
+#define DEC(GG) decode_attn_kernel<D, GG, VAR><<<grid, 256, 0, s>>>(q, ldq, kc, vc, lens, slot, pre, H, Hkv, max_seq, \
                                                                      chunk, nsplit, sl2e, po, pm, pl)
   switch (G) {
     case 1: DEC(1); break;
@@ -786,28 +797,32 @@ DA_EXPORT void da_set_gqa_mfma(int v) { g_gqa_mfma = v; }
 // than they buy, so those keep V after the scores (nt loads only).
 template <int D>
 static int launch_decode(int G, dim3 grid, hipStream_t s, const bf16_t* q, int ldq, const bf16_t* kc,
-                         const bf16_t* vc, const int* lens, const int* slot, int H, int Hkv, int max_seq, int chunk,
+                         const bf16_t* vc, const int* lens, const int* slot, const int* pre, int H, int Hkv, int max_seq, int chunk,
                          int nsplit, float sl2e, float* po, float* pm, float* pl) {
   if (G == 1)
-    return launch_decode_v<D, 3>(G, grid, s, q, ldq, kc, vc, lens, slot, H, Hkv, max_seq, chunk, nsplit, sl2e, po, pm, pl);
+    return launch_decode_v<D, 3>(G, grid, s, q, ldq, kc, vc, lens, slot, pre, H, Hkv, max_seq, chunk, nsplit, sl2e, po, pm, pl);
   if constexpr (D == 64 || D == 128) {
     if (g_gqa_mfma) {
       switch (G) {
-        case 2: decode_attn_gqa_kernel<D, 2><<<grid, 256, 0, s>>>(q, ldq, kc, vc, lens, slot, H, Hkv, max_seq, chunk, nsplit, sl2e, po, pm, pl); break;
-        case 4: decode_attn_gqa_kernel<D, 4><<<grid, 256, 0, s>>>(q, ldq, kc, vc, lens, slot, H, Hkv, max_seq, chunk, nsplit, sl2e, po, pm, pl); break;
-        case 8: decode_attn_gqa_kernel<D, 8><<<grid, 256, 0, s>>>(q, ldq, kc, vc, lens, slot, H, Hkv, max_seq, chunk, nsplit, sl2e, po, pm, pl); break;
+        case 2: decode_attn_gqa_kernel<D, 2><<<grid, 256, 0, s>>>(q, ldq, kc, vc, lens, slot, pre, H, Hkv, max_seq, chunk, nsplit, sl2e, po, pm, pl); break;
+        case 4: decode_attn_gqa_kernel<D, 4><<<grid, 256, 0, s>>>(q, ldq, kc, vc, lens, slot, pre, H, Hkv, max_seq, chunk, nsplit, sl2e, po, pm, pl); break;
+        case 8: decode_attn_gqa_kernel<D, 8><<<grid, 256, 0, s>>>(q, ldq, kc, vc, lens, slot, pre, H, Hkv, max_seq, chunk, nsplit, sl2e, po, pm, pl); break;
         default: return (int)hipErrorInvalidValue;
       }
       return (int)hipGetLastError();
     }
   }
-  return launch_decode_v<D, 1>(G, grid, s, q, ldq, kc, vc, lens, slot, H, Hkv, max_seq, chunk, nsplit, sl2e, po, pm, pl);
+  return launch_decode_v<D, 1>(G, grid, s, q, ldq, kc, vc, lens, slot, pre, H, Hkv, max_seq, chunk, nsplit, sl2e, po, pm, pl);
 }
 
 // ws must hold B*H*nsplit*(D+2) floats. chunk = keys per split (multiple of 64).
+// pre (nullable): int32 [B][2] = (P, prefix slot) per row — keys [0, P) of row b are read from the
+// prefix slot (a prompt head shared by the whole batch, stored once; P % 64 == 0 so no 64-key tile
+// straddles the two sources). Every row of the batch reads the same prefix lines, so they are served
+// from L2 / MALL instead of HBM.
 DA_EXPORT int da_decode_attn(const void* q, int ldq, const void* k_cache, const void* v_cache, const void* lens,
-                             const void* slot, int B, int H, int Hkv, int D, int max_seq, int chunk, int nsplit,
-                             float scale, void* ws, void* o, int ldo, void* stream) {
+                             const void* slot, const void* pre, int B, int H, int Hkv, int D, int max_seq, int chunk,
+                             int nsplit, float scale, void* ws, void* o, int ldo, void* stream) {
   if (H % Hkv || chunk % 64 || nsplit < 1 || (long)chunk * nsplit < 1) return (int)hipErrorInvalidValue;
   if (B == 0) return 0;
   const int G = H / Hkv;
@@ -820,13 +835,13 @@ DA_EXPORT int da_decode_attn(const void* q, int ldq, const void* k_cache, const 
   int err;
   switch (D) {
     case 64: err = launch_decode<64>(G, grid, s, (const bf16_t*)q, ldq, (const bf16_t*)k_cache, (const bf16_t*)v_cache,
-                                     (const int*)lens, (const int*)slot, H, Hkv, max_seq, chunk, nsplit, sl2e, po, pm, pl);
+                                     (const int*)lens, (const int*)slot, (const int*)pre, H, Hkv, max_seq, chunk, nsplit, sl2e, po, pm, pl);
       break;
     case 96: err = launch_decode<96>(G, grid, s, (const bf16_t*)q, ldq, (const bf16_t*)k_cache, (const bf16_t*)v_cache,
-                                     (const int*)lens, (const int*)slot, H, Hkv, max_seq, chunk, nsplit, sl2e, po, pm, pl);
+                                     (const int*)lens, (const int*)slot, (const int*)pre, H, Hkv, max_seq, chunk, nsplit, sl2e, po, pm, pl);
       break;
     case 128: err = launch_decode<128>(G, grid, s, (const bf16_t*)q, ldq, (const bf16_t*)k_cache, (const bf16_t*)v_cache,
-                                       (const int*)lens, (const int*)slot, H, Hkv, max_seq, chunk, nsplit, sl2e, po, pm, pl);
+                                       (const int*)lens, (const int*)slot, (const int*)pre, H, Hkv, max_seq, chunk, nsplit, sl2e, po, pm, pl);
       break;
     default: return (int)hipErrorInvalidValue;
   }

@@ -55,7 +55,7 @@ _SIGS = {
     "da_set_gemm_pingpong": [c_int],
     "da_set_gemm_w4": [c_int],
     "da_set_gemm_w4_cfg": [c_int],
-    "da_decode_attn": [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
+    "da_decode_attn": [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
                        c_int, c_int, c_int, c_float, c_void_p, c_void_p, c_int, c_void_p],
     "da_topk_dense": [c_void_p, c_int, c_int, c_void_p, c_void_p, c_int, c_void_p, c_int, c_float, c_int,
                       c_int, c_void_p, c_void_p, c_void_p, c_void_p],
@@ -487,10 +487,13 @@ def flash_attn_varlen(q, k, v, cu_seqlens, max_seqlen: int, H: int, Hkv: int, D:
     return out
 
 
-def decode_attn(q, k_cache, v_cache, lens, slot, H, Hkv, D, max_len: int, chunk: int = 0, scale=None, out=None):
+def decode_attn(q, k_cache, v_cache, lens, slot, H, Hkv, D, max_len: int, chunk: int = 0, scale=None, out=None,
+                pre=None):
     """q [B, >=H*D] (row stride any multiple of 8); lens/slot int32 [B]; max_len = max(lens) or the
     cache capacity (host int, fixes the split count so the launch is graph-capturable).
-    chunk = keys per workgroup (0 = auto: enough workgroups to fill 256 CUs, 4 waves x 64-key tiles)."""
+    chunk = keys per workgroup (0 = auto: enough workgroups to fill 256 CUs, 4 waves x 64-key tiles).
+    pre: optional int32 [B, 2] device tensor (P, prefix slot), P % 64 == 0: keys [0, P) of row b
+    are the batch's shared prompt head, stored once in the prefix slot (read through the cache)."""
     if chunk <= 0:
         # measured on MI355X (profiles/decode_attn_chunks_r1.txt): per-workgroup overhead dominates
         # small chunks; aim for ~768 workgroups, 512..4096 keys each
@@ -510,7 +513,9 @@ def decode_attn(q, k_cache, v_cache, lens, slot, H, Hkv, D, max_len: int, chunk:
     if out is None:
         out = torch.empty((B, H * D), dtype=torch.bfloat16, device=q.device)
     scale = scale if scale is not None else 1.0 / math.sqrt(D)
-    _check(lib().da_decode_attn(_ptr(q), q.stride(0), _ptr(k_cache), _ptr(v_cache), _ptr(lens), _ptr(slot), B, H,
+    if pre is not None:
+        _i32(pre, "pre"); _req(pre.shape == (B, 2) and pre.is_contiguous(), "pre must be int32 [B, 2]")
+    _check(lib().da_decode_attn(_ptr(q), q.stride(0), _ptr(k_cache), _ptr(v_cache), _ptr(lens), _ptr(slot), _ptr(pre), B, H,
                                 Hkv, D, max_seq, chunk, nsplit, float(scale), _ptr(ws), _ptr(out), out.stride(0),
                                 _stream()), "decode_attn")
     return out

@@ -175,16 +175,23 @@ def flash_attn_varlen(q, k, v, cu_seqlens, max_seqlen, H, Hkv, D, causal, scale=
     return res
 
 
-def decode_attn(q, k_cache, v_cache, lens, slot, H, Hkv, D, max_len=None, chunk=256, scale=None, out=None):
+def decode_attn(q, k_cache, v_cache, lens, slot, H, Hkv, D, max_len=None, chunk=256, scale=None, out=None, pre=None):
+    """pre: optional int32 [B, 2] = (P, prefix slot): keys [0, P) of row b come from the prefix slot."""
     scale = scale if scale is not None else 1.0 / math.sqrt(D)
     B = q.shape[0]
     G = H // Hkv
     res = torch.empty((B, H * D), dtype=q.dtype, device=q.device)
+    pre_h = None if pre is None else pre.tolist()
     for b in range(B):
         L, s = int(lens[b]), int(slot[b])
         qq = q[b, :H * D].float().view(H, 1, D)
-        kk = k_cache[s, :, :L].float().repeat_interleave(G, 0)
-        vv = v_cache[s, :, :L].float().repeat_interleave(G, 0)
+        kk = k_cache[s, :, :L].float()
+        vv = v_cache[s, :, :L].float()
+        if pre_h is not None and pre_h[b][0] > 0:
+            P, ps = pre_h[b]
+            kk = torch.cat([k_cache[ps, :, :P].float(), kk[:, P:]], 1)
+            vv = torch.cat([v_cache[ps, :, :P].float(), vv[:, P:]], 1)
+        kk, vv = kk.repeat_interleave(G, 0), vv.repeat_interleave(G, 0)
         p = ((qq @ kk.transpose(1, 2)) * scale).softmax(-1)
         res[b] = (p @ vv).reshape(H * D).to(q.dtype)
     if out is not None:

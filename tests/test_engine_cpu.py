@@ -304,10 +304,10 @@ def test_shared_prompt_head_prefilled_once_same_tokens():
     e = Engine("tiny-enc", "tiny-dec", "cpu", max_batch=4, max_seq=512, max_new_tokens=6, temperature=0.0,
                use_graphs=False)
     rng = np.random.default_rng(7)
-    head = list(rng.integers(5, 3000, size=90))
+    head = list(rng.integers(5, 3000, size=130))
     prompts = [head + list(rng.integers(5, 3000, size=n)) for n in (1, 17, 40, 5)]
     g = e.gen
-    assert g.shared_prefix_len(prompts) == 90
+    assert g.shared_prefix_len(prompts) == 128  # rounded down to the 64-key decode tile
     assert g.shared_prefix_len(prompts[:1]) == 0 and g.shared_prefix_len([head[:20] + [1], head[:20] + [2]]) == 0
     g.share_prefix = False
     want = g.generate(prompts, 6)
@@ -316,6 +316,6 @@ def test_shared_prompt_head_prefilled_once_same_tokens():
     got = g.generate(prompts, 6)
     assert [r.tokens for r in got] == [r.tokens for r in want]
     assert all(abs(a.mean_prob - b.mean_prob) < 1e-3 for a, b in zip(got, want))
-    assert g.stats["shared_prefix_tokens"] == 90 * 3
-    assert g.stats["prefill_tokens"] - t_plain == t_plain - 90 * 3
+    assert g.stats["shared_prefix_tokens"] == 128 * 3
+    assert g.stats["prefill_tokens"] - t_plain == t_plain - 128 * 3
     assert len(g.cache.free) == g.cache.slots - 1

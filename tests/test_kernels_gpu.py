@@ -488,3 +488,18 @@ def test_flash_attn_shared_prefix(H, Hkv, D, P, nw):
         K.lib().da_set_flash_waves(0)
     ref = R.flash_attn_varlen(q, k, v, cu, max(lens), H, Hkv, D, True, prefix=pre)
     _close(got, ref, atol=0.02)
+
+
+@pytest.mark.parametrize("H,Hkv,D", [(32, 32, 96), (32, 8, 128), (8, 1, 128), (12, 6, 64)])
+def test_decode_attn_shared_prefix(H, Hkv, D):
+    """Rows whose keys [0, P) live in a shared prefix slot (pre = (P, slot)) vs the fp32 reference."""
+    torch.manual_seed(H + D)
+    B, S = 5, 700
+    kc, vc = _rand(7, Hkv, S, D), _rand(7, Hkv, S, D)
+    lens = torch.tensor([64, 65, 300, 700, 129], device=DEV, dtype=torch.int32)
+    slot = torch.tensor([6, 0, 3, 2, 1], device=DEV, dtype=torch.int32)
+    pre = torch.tensor([[64, 5], [64, 5], [256, 5], [0, 0], [128, 4]], device=DEV, dtype=torch.int32)
+    q = _rand(B, (H + 2 * Hkv) * D)
+    got = K.decode_attn(q, kc, vc, lens, slot, H, Hkv, D, max_len=700, chunk=128, pre=pre)
+    ref = R.decode_attn(q, kc, vc, lens, slot, H, Hkv, D, pre=pre)
+    _close(got, ref, atol=0.02)
