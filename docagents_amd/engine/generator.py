@@ -254,8 +254,15 @@ class ContinuousScheduler:
     """
 
     def __init__(self, gen: "Generator", B: int | None = None, max_new_cap: int = 256, chunk_steps: int = 8,
-                 max_admit_tokens: int | None = None):
+                 max_admit_tokens: int | None = None, max_heads: int = 2):
         self.gen, self.m = gen, gen.model
+        # Prompt-head cache (automatic prefix caching): a head shared by the prompts of one admission
+        # (the Answer system prompt) is prefilled once into a slot of its own and kept; later prompts
+        # starting with it prefill only their suffix, and their decode reads the head's keys from
+        # that slot (DecodeState.pre). Entries: {"tokens", "P", "slot", "refs", "used"}; LRU among
+        # unreferenced entries when a new head needs a slot.
+        self.heads: list[dict] = []
+        self.max_heads = max_heads if gen.share_prefix else 0
         self.B = B or gen.max_batch
         self.cap = max(1, max_new_cap)
         self.chunk_steps = chunk_steps
@@ -264,7 +271,7 @@ class ContinuousScheduler:
         self.rows: list = [None] * self.B        # row -> (tag, slot, budget)
         self.pending: collections.deque = collections.deque()
         self._reset_rows(list(range(self.B)))
-        self.stats = {"admitted": 0, "finished": 0, "ticks": 0, "steps": 0}
+        self.stats = {"admitted": 0, "finished": 0, "ticks": 0, "steps": 0, "head_hits": 0, "heads_built": 0}
 
     # -------------------------------------------------------------------------------- public
     def submit(self, prompt: list[int], max_new: int, tag=None):
@@ -324,6 +331,44 @@ class ContinuousScheduler:
         st.lens.index_fill_(0, idx, 1)
         st.active.index_fill_(0, idx, 0)
         st.start.index_fill_(0, idx, 0)
+        st.pre.index_fill_(0, idx, 0)
+
+    def _match_head(self, prompt):
+        for h in self.heads:
+            if len(prompt) > h["P"] and prompt[:h["P"]] == h["tokens"]:
+                return h
+        return None
+
+    def _build_head(self, prompts):
+        """Cache the head shared by ``prompts`` (>= 2 of them, >= min_shared_prefix tokens) in a
+        slot of its own; None when there is no such head or no slot to spare."""
+        P = self.gen.shared_prefix_len(prompts)
+        if not P:
+            return None
+        cache = self.gen.cache
+        if len(self.heads) >= self.max_heads:
+            idle = [h for h in self.heads if h["refs"] == 0]
+            if not idle:
+                return None
+            old = min(idle, key=lambda h: h["used"])
+            self.heads.remove(old)
+            cache.release([old["slot"]])
+        if not cache.free:
+            return None
+        slot = cache.acquire(1)[0]
+        head = list(prompts[0][:P])
+        dev = self.m.device
+        to = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev, non_blocking=True)  # noqa: E731
+        t0 = time.perf_counter()
+        self.m.prefill(to(np.asarray(head, dtype=np.int32)), to(np.arange(P, dtype=np.int32)),
+                       to(np.full(P, slot, dtype=np.int32)), to(np.array([0, P], dtype=np.int32)), P,
+                       to(np.array([P - 1], dtype=np.int64)))
+        self.gen.stats["prefill_tokens"] += P
+        self.gen.stats["prefill_s"] += time.perf_counter() - t0
+        h = {"tokens": head, "P": P, "slot": slot, "refs": 0, "used": self.stats["ticks"]}
+        self.heads.append(h)
+        self.stats["heads_built"] += 1
+        return h
 
     def _admit(self) -> list:
         free = [i for i, r in enumerate(self.rows) if r is None]
@@ -336,6 +381,18 @@ class ContinuousScheduler:
             tot += len(p[0])
         if not take:
             return []
+        # prompt heads: reuse a cached one, or cache the head this admission's prompts share
+        hs = [self._match_head(t[0]) for t in take] if self.max_heads else [None] * len(take)
+        if self.max_heads:
+            miss = [t[0] for t, h in zip(take, hs) if h is None]
+            if len(miss) >= 2:
+                h = self._build_head(miss)
+                if h is not None:
+                    hs = [hh if hh is not None else (h if self._match_head(t[0]) is h else None)
+                          for t, hh in zip(take, hs)]
+        # rows using the same head are prefilled together (suffixes only), plain prompts last
+        order = sorted(range(len(take)), key=lambda i: (hs[i] is None, id(hs[i])))
+        take, hs = [take[i] for i in order], [hs[i] for i in order]
         n, rows = len(take), free[:len(take)]
         slots = self.gen.cache.acquire(n)
         prompts = [t[0] for t in take]
@@ -349,13 +406,29 @@ class ContinuousScheduler:
             hist=torch.full((n, self.cap), -1, **i32),
             start=torch.from_numpy(plen - 1 - (self.cap - budget)).to(dev),
             slot=torch.as_tensor(slots, dtype=torch.int32, device=dev))
-        self.gen._prefill_into(tmp, prompts, slots, 0)
+        i = 0
+        pre = np.zeros((n, 2), dtype=np.int32)
+        while i < n:
+            h, j = hs[i], i
+            while j < n and hs[j] is h:
+                j += 1
+            if h is None:
+                self.gen._prefill_into(tmp, prompts[i:j], slots[i:j], i)
+            else:
+                self.gen._prefill_into(tmp, [p[h["P"]:] for p in prompts[i:j]], slots[i:j], i, prefix=(h["slot"], h["P"]))
+                pre[i:j] = (h["P"], h["slot"])
+                h["refs"] += j - i
+                h["used"] = self.stats["ticks"]
+                self.stats["head_hits"] += j - i
+                self.gen.stats["shared_prefix_tokens"] += h["P"] * (j - i)
+            i = j
         st = self.st
         idx = torch.as_tensor(rows, dtype=torch.long, device=dev)
         for name in ("tokens", "lp", "conf", "active", "pos", "lens", "hist", "start", "slot"):
             getattr(st, name).index_copy_(0, idx, getattr(tmp, name))
-        for r, (p, b, tag), sl in zip(rows, take, slots):
-            self.rows[r] = (tag, sl, int(b))
+        st.pre.index_copy_(0, idx, torch.from_numpy(pre).to(dev))
+        for r, (p, b, tag), sl, h in zip(rows, take, slots, hs):
+            self.rows[r] = (tag, sl, int(b), h)
         self.stats["admitted"] += n
         # a budget of one token (or an immediate EOS) finishes at prefill
         return self._reap(rows)
@@ -375,7 +448,9 @@ class ContinuousScheduler:
         out, slots = [], []
         eos = set(self.gen.eos)
         for k, r in enumerate(fin):
-            tag, sl, b = self.rows[r]
+            tag, sl, b, h = self.rows[r]
+            if h is not None:
+                h["refs"] -= 1
             toks = [int(t) for t in hist[k, self.cap - b:] if t >= 0 and int(t) not in eos]
             cnt = float(conf[k, 1])
             out.append((tag, GenResult(toks, float(conf[k, 0] / cnt) if cnt > 0 else 1.0, int(cnt))))

@@ -319,3 +319,36 @@ def test_shared_prompt_head_prefilled_once_same_tokens():
     assert g.stats["shared_prefix_tokens"] == 128 * 3
     assert g.stats["prefill_tokens"] - t_plain == t_plain - 128 * 3
     assert len(g.cache.free) == g.cache.slots - 1
+
+
+def test_continuous_batching_caches_prompt_head():
+    """ContinuousScheduler keeps the head shared by an admission's prompts in a slot of its own;
+    later prompts with that head (even alone) prefill only their suffix; generations equal the
+    per-prompt greedy path; the head slot stays reserved, every row slot is returned."""
+    from docagents_amd.engine.generator import ContinuousScheduler
+    e = Engine("tiny-enc", "tiny-dec", "cpu", max_batch=4, max_seq=512, max_new_tokens=6, temperature=0.0,
+               use_graphs=False)
+    rng = np.random.default_rng(5)
+    head = [int(t) for t in rng.integers(5, 3000, size=150)]
+    prompts = [head + [int(t) for t in rng.integers(5, 3000, size=n)] for n in (3, 40, 11, 7, 25)]
+    other = [int(t) for t in rng.integers(5, 3000, size=30)]
+    e.gen.share_prefix = False
+    want = [e.gen.generate([p], 5)[0].tokens for p in prompts + [other]]
+    e.gen.share_prefix = True
+    sched = ContinuousScheduler(e.gen, B=4, max_new_cap=8, chunk_steps=2)
+    got = {}
+    for i in range(3):
+        sched.submit(prompts[i], 5, i)
+    for tag, r in sched.tick():
+        got[tag] = r.tokens
+    assert sched.stats["heads_built"] == 1 and sched.heads[0]["P"] == 128
+    for i in (3, 4):
+        sched.submit(prompts[i], 5, i)
+    sched.submit(other, 5, 5)
+    while sched.busy():
+        for tag, r in sched.tick():
+            got[tag] = r.tokens
+    assert [got[i] for i in range(6)] == want
+    assert sched.stats["heads_built"] == 1 and sched.stats["head_hits"] == 5
+    assert sched.heads[0]["refs"] == 0
+    assert len(e.gen.cache.free) == e.gen.cache.slots - 2  # dummy slot + the cached head's slot

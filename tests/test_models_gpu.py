@@ -103,3 +103,22 @@ def test_generate_shared_prompt_head_matches_unshared():
     agree = np.mean([np.mean([x == y for x, y in zip(a.tokens, b.tokens)]) for a, b in zip(got, want)])
     assert agree >= 0.75, agree
     assert max(abs(a.mean_prob - b.mean_prob) for a, b in zip(got, want)) < 0.02
+
+
+def test_continuous_scheduler_prompt_head_cache_graphs():
+    """Graph-replayed continuous batching with a cached prompt head: same tokens as per-prompt runs."""
+    from docagents_amd.engine.generator import ContinuousScheduler
+    m = LlamaDecoder(decoder_config("tiny-dec"), "cuda", seed=8)
+    m.alloc_cache(8, 1024)
+    g = Generator(m, max_batch=4, max_seq=1024, temperature=0.0, use_graphs=True)
+    rng = np.random.default_rng(12)
+    head = [int(t) for t in rng.integers(5, 3000, size=300)]
+    prompts = [head + [int(t) for t in rng.integers(5, 3000, size=n)] for n in (5, 64, 200, 17, 90)]
+    g.share_prefix = False
+    want = [g.generate([p], 8)[0] for p in prompts]
+    g.share_prefix = True
+    sched = ContinuousScheduler(g, B=4, max_new_cap=8, chunk_steps=4)
+    res = sched.run_all(prompts, 8)
+    assert sched.stats["heads_built"] == 1 and sched.stats["head_hits"] == 5
+    agree = np.mean([np.mean([x == y for x, y in zip(a.tokens, b.tokens)]) for a, b in zip(res, want)])
+    assert agree >= 0.75, agree
