@@ -61,8 +61,39 @@ async def _wait_ready(client, url, timeout=120.0):
     raise TimeoutError(url)
 
 
+def _raw_hits(url: str, bodies: list[str]) -> list[float]:
+    """Sequential POST /api/query over one keep-alive socket with no client library in the way:
+    the latency a cache hit costs the stack itself (the httpx client adds ~1 ms per request)."""
+    import socket
+    from urllib.parse import urlsplit
+    u = urlsplit(url)
+    s = socket.create_connection((u.hostname, u.port))
+    s.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
+    out = []
+    try:
+        for b in bodies:
+            data = b.encode()
+            req = (f"POST /api/query HTTP/1.1\r\nHost: {u.hostname}\r\nContent-Type: application/json\r\n"
+                   f"Content-Length: {len(data)}\r\n\r\n").encode() + data
+            t = time.perf_counter()
+            s.sendall(req)
+            buf = b""
+            while True:
+                buf += s.recv(65536)
+                head, sep, rest = buf.partition(b"\r\n\r\n")
+                if not sep:
+                    continue
+                n = next(int(ln.split(b":")[1]) for ln in head.split(b"\r\n") if ln.lower().startswith(b"content-length"))
+                if len(rest) >= n:
+                    break
+            out.append((time.perf_counter() - t) * 1000.0)
+    finally:
+        s.close()
+    return out
+
+
 async def run(gw: str, docs: int, words: int, queries: int, concurrency: int, top_k: int, seed: int,
-              poll_s: float = 0.1, ingest_timeout: float = 600.0) -> dict:
+              poll_s: float = 0.1, ingest_timeout: float = 600.0, query_url: str = "") -> dict:
     tg = TextGen(seed=seed)
     texts = [tg.document(words) for _ in range(docs)]
     sem = asyncio.Semaphore(concurrency)
@@ -117,6 +148,15 @@ async def run(gw: str, docs: int, words: int, queries: int, concurrency: int, to
         hit = []
         for b in bodies:  # sequential: per-request latency of a cache hit, not throughput
             hit.append(await ask(b))
+        raw_gw = await asyncio.to_thread(_raw_hits, gw, bodies)
+        raw_q = await asyncio.to_thread(_raw_hits, query_url, bodies) if query_url else []
+        handler_ms = None
+        if query_url:
+            m = (await client.get(query_url.rsplit("/api/", 1)[0] + "/metrics")).text
+            vals = {ln.split("{")[0]: float(ln.split()[-1]) for ln in m.splitlines()
+                    if ln.startswith("da_query_stage_seconds_") and 'stage="cache_hit"' in ln}
+            if vals.get("da_query_stage_seconds_count"):
+                handler_ms = vals["da_query_stage_seconds_sum"] / vals["da_query_stage_seconds_count"] * 1000.0
 
     miss_ok = [dt for st, dt in miss if st == 200]
     hit_ok = [dt for st, dt in hit if st == 200]
@@ -129,6 +169,9 @@ async def run(gw: str, docs: int, words: int, queries: int, concurrency: int, to
         "cache_miss_p99_ms": _r(_pct(miss_ok, 99)),
         "cache_hit_p50_ms": _r(statistics.median(hit_ok) if hit_ok else None),
         "cache_hit_p99_ms": _r(_pct(hit_ok, 99)),
+        "cache_hit_gateway_raw_p50_ms": _r(statistics.median(raw_gw) if raw_gw else None),
+        "cache_hit_query_service_raw_p50_ms": _r(statistics.median(raw_q) if raw_q else None),
+        "cache_hit_handler_mean_ms": _r(handler_ms),
         "concurrency": concurrency, "top_k": top_k,
     }
 
@@ -147,6 +190,7 @@ def main(argv=None):
     ap.add_argument("--concurrency", type=int, default=16)
     ap.add_argument("--top-k", type=int, default=5)
     ap.add_argument("--seed", type=int, default=7)
+    ap.add_argument("--query-url", default="", help="query service URL (direct cache-hit timing)")
     a = ap.parse_args(argv)
     proc = None
     gw = a.gateway
@@ -161,7 +205,8 @@ def main(argv=None):
                                 stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
         gw = f"http://127.0.0.1:{port}"
     try:
-        out = asyncio.run(run(gw, a.docs, a.words, a.queries, a.concurrency, a.top_k, a.seed))
+        qurl = f"http://127.0.0.1:{int(gw.rsplit(':', 1)[1]) + 1}/api/query" if proc is not None else a.query_url
+        out = asyncio.run(run(gw, a.docs, a.words, a.queries, a.concurrency, a.top_k, a.seed, query_url=qurl))
     finally:
         if proc is not None:
             proc.terminate()

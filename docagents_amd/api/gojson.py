@@ -8,7 +8,13 @@ U+2028, U+2029), float32 values in Go's shortest float32 representation (``strco
 from __future__ import annotations
 
 import math
+import re
 import struct
+from json.encoder import encode_basestring as _encode_basestring
+
+import numpy as _np
+
+_SURR = re.compile("[\ud800-\udfff]")
 
 
 class F32(float):
@@ -34,6 +40,17 @@ def _fmt_float(x: float, bits: int) -> str:
         raise ValueError(f"json: unsupported value: {x}")
     if x == 0:
         return "-0" if math.copysign(1.0, x) < 0 else "0"
+    a = abs(x)
+    if 1e-6 <= a < 1e21:  # Go's 'f' form: numpy's shortest round-trip digits, positional (fast path)
+        v = _np.float32(x) if bits == 32 else _np.float64(x)
+        if 1e-6 <= abs(float(v)) < 1e21:
+            return _np.format_float_positional(v, unique=True, trim="-")
+    return _fmt_float_slow(x, bits)
+
+
+def _fmt_float_slow(x: float, bits: int) -> str:
+    if x == 0:
+        return "-0" if math.copysign(1.0, x) < 0 else "0"
     s = _shortest_f32(x) if bits == 32 else repr(float(x))
     from decimal import Decimal
     d = Decimal(s)
@@ -56,7 +73,22 @@ _ESC = {'"': '\\"', "\\": "\\\\", "\n": "\\n", "\r": "\\r", "\t": "\\t", "<": "\
         "&": "\\u0026", "\u2028": "\\u2028", "\u2029": "\\u2029", "\b": "\\b", "\f": "\\f"}
 
 
+_HTML = ("<", ">", "&", "\u2028", "\u2029")
+
+
 def _str(s: str) -> str:
+    """C-accelerated JSON string escaping plus Go's HTML-safe escapes; lone surrogates (invalid
+    UTF-8 in Go) take the slow path, which writes U+FFFD like Go."""
+    if _SURR.search(s):
+        return _str_slow(s)
+    out = _encode_basestring(s)
+    if any(c in out for c in _HTML):
+        out = (out.replace("<", "\\u003c").replace(">", "\\u003e").replace("&", "\\u0026")
+               .replace("\u2028", "\\u2028").replace("\u2029", "\\u2029"))
+    return out
+
+
+def _str_slow(s: str) -> str:
     out = ['"']
     for ch in s:
         e = _ESC.get(ch)

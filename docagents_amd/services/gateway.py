@@ -128,18 +128,18 @@ async def summary_handler(deps, id_str: str) -> Response:
 
 async def query_proxy(deps, request: Request) -> Response:
     """main.go:180-207: forward the body verbatim; status + body back, Content-Type forced."""
-    import httpx
+    from ..api.proxy import PooledHTTPClient
     body = await request.body()
     client = deps.extras.get("http")
     if client is None:
-        client = httpx.AsyncClient(timeout=60.0)
+        client = PooledHTTPClient(timeout=60.0)
         deps.extras["http"] = client
     try:
-        r = await client.post(deps.config.query_service_url, content=body,
-                              headers={"Content-Type": "application/json", "X-Request-Id": request_id(request)})
+        status, content = await client.post(deps.config.query_service_url, body,
+                                            {"Content-Type": "application/json", "X-Request-Id": request_id(request)})
     except Exception as e:  # noqa: BLE001
         return fail(deps.log, "query service unavailable", e, 503)
-    return Response(r.content, status_code=r.status_code, media_type="application/json")
+    return Response(content, status_code=status, media_type="application/json")
 
 
 def build_app(deps) -> Middleware:

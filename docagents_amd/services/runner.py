@@ -21,6 +21,9 @@ from ..config import load
 
 
 async def _serve_http(app, port: int, host: str = "0.0.0.0"):
+    if os.environ.get("DA_HTTP_SERVER", "native") != "uvicorn":
+        from ..api.server import serve
+        return await serve(app, host, port)
     import uvicorn
     cfg = uvicorn.Config(app, host=host, port=port, log_level="warning", access_log=False, lifespan="off")
     server = uvicorn.Server(cfg)
