@@ -373,13 +373,66 @@ flash_attn_v2_kernel(const bf16_t* __restrict__ q, const bf16_t* __restrict__ k,
 // The P*V accumulation uses the same flat chunks: lane's dim-slot for chunk i is static given
 // i mod NSET, so accumulators stay in registers. Each of the 4 waves streams its own tiles with its
 // own online softmax (no block barriers in the loop); the waves are merged once at the end.
+// Split-KV epilogue shared by the decode kernels. A split's merged (over its 4 waves) result for
+// query head h: unnormalised O row `o`, running max M (log2 domain), sum ls. With one split the
+// normalised bf16 output is written directly; otherwise the fp32 partial, and the LAST split of
+// (b, kv head) to finish (atomic ticket in cnt[b * Hkv + hk], reset by that split so the counters
+// are zero again for the next launch / graph replay) merges all splits of its G heads — the
+// separate combine launch (~5 us per layer, most of a batch-1 decode attention) is gone.
+__device__ __forceinline__ void dec_store(float o, float M, float ls, int b, int h, int d, int H, int nsplit,
+                                          int split, int D, float* po, float* pm, float* pl, bf16_t* out,
+                                          int ldo) {
+  if (nsplit == 1) {
+    out[(size_t)b * ldo + h * D + d] = f2bf(ls > 0.f ? o / ls : 0.f);
+    return;
+  }
+  const size_t pidx = ((size_t)b * H + h) * nsplit + split;
+  po[pidx * D + d] = o;
+  if (d == 0) { pm[pidx] = M; pl[pidx] = ls; }
+}
+
+template <int D, int G>
+__device__ __forceinline__ void dec_finish(const float* po, const float* pm, const float* pl, int H, int Hkv,
+                                           int nsplit, int b, int hk, int* cnt, bf16_t* out, int ldo, int* s_last) {
+  if (nsplit == 1 || cnt == nullptr) return;  // no counters: the host launches decode_combine_kernel
+  const int tid = threadIdx.x;
+  // Partials and tickets live in UNCACHED memory (da_malloc_uncached: MTYPE UC, L2 bypassed), so
+  // device-wide visibility needs only this workgroup's stores to have completed — no
+  // __threadfence(), whose L2 write-back + invalidate of the whole cache costs more than the
+  // combine launch it replaces (measured: 24.6 -> 48.4 us at batch 1).
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0) {
+    const int old = atomicAdd(&cnt[b * Hkv + hk], 1);
+    *s_last = old == nsplit - 1;
+    if (*s_last) cnt[b * Hkv + hk] = 0;
+  }
+  __syncthreads();
+  if (!*s_last) return;
+  for (int i = tid; i < G * D; i += blockDim.x) {
+    const int g = i / D, d = i % D, h = hk * G + g;
+    const size_t base = ((size_t)b * H + h) * nsplit;
+    float M = -INFINITY;
+    for (int s = 0; s < nsplit; ++s) M = fmaxf(M, pm[base + s]);
+    const float Mu = (M == -INFINITY) ? 0.f : M;
+    float lsum = 0.f, acc = 0.f;
+    for (int s = 0; s < nsplit; ++s) {
+      const float f = exp2f(pm[base + s] - Mu);
+      lsum += pl[base + s] * f;
+      acc += po[(base + s) * D + d] * f;
+    }
+    out[(size_t)b * ldo + h * D + d] = f2bf(lsum > 0.f ? acc / lsum : 0.f);
+  }
+}
+
 template <int D, int G, int VAR>
 __global__ void __launch_bounds__(256)
 decode_attn_kernel(const bf16_t* __restrict__ q, int ldq, const bf16_t* __restrict__ kc,
                    const bf16_t* __restrict__ vc, const int* __restrict__ lens, const int* __restrict__ slot,
                    const int* __restrict__ pre,
                    int H, int Hkv, int max_seq, int chunk, int nsplit, float scale_log2e,
-                   float* __restrict__ po, float* __restrict__ pm, float* __restrict__ pl) {
+                   float* __restrict__ po, float* __restrict__ pm, float* __restrict__ pl,
+                   bf16_t* __restrict__ out, int ldo, int* __restrict__ cnt) {
   constexpr int KT = 64;
   constexpr int CPR = D / 8;                       // 16-B chunks per key row
   constexpr int GCD = (CPR % 16 == 0) ? 16 : ((CPR % 8 == 0) ? 8 : ((CPR % 4 == 0) ? 4 : 2));
@@ -556,11 +609,10 @@ decode_attn_kernel(const bf16_t* __restrict__ q, int ldq, const bf16_t* __restri
       o += so[ww][g][d] * f;
       ls += swl[ww][g] * f;
     }
-    const int h = hk * G + g;
-    const size_t pidx = ((size_t)b * H + h) * nsplit + split;
-    po[pidx * D + d] = o;
-    if (d == 0) { pm[pidx] = M; pl[pidx] = ls; }
+    dec_store(o, M, ls, b, hk * G + g, d, H, nsplit, split, D, po, pm, pl, out, ldo);
   }
+  __shared__ int s_last;
+  dec_finish<D, G>(po, pm, pl, H, Hkv, nsplit, b, hk, cnt, out, ldo, &s_last);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -588,7 +640,8 @@ decode_attn_gqa_kernel(const bf16_t* __restrict__ q, int ldq, const bf16_t* __re
                        const bf16_t* __restrict__ vc, const int* __restrict__ lens, const int* __restrict__ slot,
                    const int* __restrict__ pre,
                        int H, int Hkv, int max_seq, int chunk, int nsplit, float scale_log2e,
-                       float* __restrict__ po, float* __restrict__ pm, float* __restrict__ pl) {
+                       float* __restrict__ po, float* __restrict__ pm, float* __restrict__ pl,
+                       bf16_t* __restrict__ out, int ldo, int* __restrict__ cnt) {
   static_assert(D == 64 || D == 128, "GQA MFMA decode supports head dims 64 and 128");
   constexpr int KT = 64, NDS = D / 32, NDT = D / 16, NS = D / 8;   // d-steps (S), d-tiles (O), 16-B chunks/row
   constexpr int VBYTES = KT * D * 2, NDMA = VBYTES / 1024;
@@ -723,10 +776,10 @@ decode_attn_gqa_kernel(const bf16_t* __restrict__ q, int ldq, const bf16_t* __re
       o += so[(ww * 16 + g) * D + d] * f;
       ls += swl[ww][g] * f;
     }
-    const size_t pidx = ((size_t)b * H + hk * G + g) * nsplit + split;
-    po[pidx * D + d] = o;
-    if (d == 0) { pm[pidx] = M; pl[pidx] = ls; }
+    dec_store(o, M, ls, b, hk * G + g, d, H, nsplit, split, D, po, pm, pl, out, ldo);
   }
+  __shared__ int s_last;
+  dec_finish<D, G>(po, pm, pl, H, Hkv, nsplit, b, hk, cnt, out, ldo, &s_last);
 }
 
 template <int D>
@@ -772,9 +825,10 @@ DA_EXPORT int da_flash_attn_varlen(const void* q, const void* k, const void* v, 
 template <int D, int VAR>
 static int launch_decode_v(int G, dim3 grid, hipStream_t s, const bf16_t* q, int ldq, const bf16_t* kc,
                            const bf16_t* vc, const int* lens, const int* slot, const int* pre, int H, int Hkv, int max_seq, int chunk,
-                           int nsplit, float sl2e, float* po, float* pm, float* pl) {
+                           int nsplit, float sl2e, float* po, float* pm, float* pl, bf16_t* out, int ldo,
+                           int* cnt) {
 #define DEC(GG) decode_attn_kernel<D, GG, VAR><<<grid, 256, 0, s>>>(q, ldq, kc, vc, lens, slot, pre, H, Hkv, max_seq, \
-                                                                     chunk, nsplit, sl2e, po, pm, pl)
+                                                                     chunk, nsplit, sl2e, po, pm, pl, out, ldo, cnt)
   switch (G) {
     case 1: DEC(1); break;
     case 2: DEC(2); break;
@@ -798,21 +852,22 @@ DA_EXPORT void da_set_gqa_mfma(int v) { g_gqa_mfma = v; }
 template <int D>
 static int launch_decode(int G, dim3 grid, hipStream_t s, const bf16_t* q, int ldq, const bf16_t* kc,
                          const bf16_t* vc, const int* lens, const int* slot, const int* pre, int H, int Hkv, int max_seq, int chunk,
-                         int nsplit, float sl2e, float* po, float* pm, float* pl) {
+                         int nsplit, float sl2e, float* po, float* pm, float* pl, bf16_t* out, int ldo,
+                           int* cnt) {
   if (G == 1)
-    return launch_decode_v<D, 3>(G, grid, s, q, ldq, kc, vc, lens, slot, pre, H, Hkv, max_seq, chunk, nsplit, sl2e, po, pm, pl);
+    return launch_decode_v<D, 3>(G, grid, s, q, ldq, kc, vc, lens, slot, pre, H, Hkv, max_seq, chunk, nsplit, sl2e, po, pm, pl, out, ldo, cnt);
   if constexpr (D == 64 || D == 128) {
     if (g_gqa_mfma) {
       switch (G) {
-        case 2: decode_attn_gqa_kernel<D, 2><<<grid, 256, 0, s>>>(q, ldq, kc, vc, lens, slot, pre, H, Hkv, max_seq, chunk, nsplit, sl2e, po, pm, pl); break;
-        case 4: decode_attn_gqa_kernel<D, 4><<<grid, 256, 0, s>>>(q, ldq, kc, vc, lens, slot, pre, H, Hkv, max_seq, chunk, nsplit, sl2e, po, pm, pl); break;
-        case 8: decode_attn_gqa_kernel<D, 8><<<grid, 256, 0, s>>>(q, ldq, kc, vc, lens, slot, pre, H, Hkv, max_seq, chunk, nsplit, sl2e, po, pm, pl); break;
+        case 2: decode_attn_gqa_kernel<D, 2><<<grid, 256, 0, s>>>(q, ldq, kc, vc, lens, slot, pre, H, Hkv, max_seq, chunk, nsplit, sl2e, po, pm, pl, out, ldo, cnt); break;
+        case 4: decode_attn_gqa_kernel<D, 4><<<grid, 256, 0, s>>>(q, ldq, kc, vc, lens, slot, pre, H, Hkv, max_seq, chunk, nsplit, sl2e, po, pm, pl, out, ldo, cnt); break;
+        case 8: decode_attn_gqa_kernel<D, 8><<<grid, 256, 0, s>>>(q, ldq, kc, vc, lens, slot, pre, H, Hkv, max_seq, chunk, nsplit, sl2e, po, pm, pl, out, ldo, cnt); break;
         default: return (int)hipErrorInvalidValue;
       }
       return (int)hipGetLastError();
     }
   }
-  return launch_decode_v<D, 1>(G, grid, s, q, ldq, kc, vc, lens, slot, pre, H, Hkv, max_seq, chunk, nsplit, sl2e, po, pm, pl);
+  return launch_decode_v<D, 1>(G, grid, s, q, ldq, kc, vc, lens, slot, pre, H, Hkv, max_seq, chunk, nsplit, sl2e, po, pm, pl, out, ldo, cnt);
 }
 
 // ws must hold B*H*nsplit*(D+2) floats. chunk = keys per split (multiple of 64).
@@ -820,9 +875,22 @@ static int launch_decode(int G, dim3 grid, hipStream_t s, const bf16_t* q, int l
 // prefix slot (a prompt head shared by the whole batch, stored once; P % 64 == 0 so no 64-key tile
 // straddles the two sources). Every row of the batch reads the same prefix lines, so they are served
 // from L2 / MALL instead of HBM.
+// counters (nullable): int32 [B * Hkv], all zero, left zero by every launch -> the splits are merged
+// inside the attention kernel (last split per (b, kv head)); null -> separate combine launch. With
+// counters, ws and counters must be uncached allocations (da_malloc_uncached).
+DA_EXPORT int da_malloc_uncached(long long bytes, void** out) {
+  hipError_t e = hipExtMallocWithFlags(out, (size_t)bytes, hipDeviceMallocUncached);
+  if (e != hipSuccess) return (int)e;
+  e = hipMemset(*out, 0, (size_t)bytes);
+  if (e != hipSuccess) return (int)e;
+  return (int)hipDeviceSynchronize();
+}
+
 DA_EXPORT int da_decode_attn(const void* q, int ldq, const void* k_cache, const void* v_cache, const void* lens,
                              const void* slot, const void* pre, int B, int H, int Hkv, int D, int max_seq, int chunk,
-                             int nsplit, float scale, void* ws, void* o, int ldo, void* stream) {
+                             int nsplit, float scale, void* ws, void* o, int ldo, void* counters, void* stream) {
+  bf16_t* out = (bf16_t*)o;
+  int* cnt = (int*)counters;
   if (H % Hkv || chunk % 64 || nsplit < 1 || (long)chunk * nsplit < 1) return (int)hipErrorInvalidValue;
   if (B == 0) return 0;
   const int G = H / Hkv;
@@ -835,17 +903,18 @@ DA_EXPORT int da_decode_attn(const void* q, int ldq, const void* k_cache, const 
   int err;
   switch (D) {
     case 64: err = launch_decode<64>(G, grid, s, (const bf16_t*)q, ldq, (const bf16_t*)k_cache, (const bf16_t*)v_cache,
-                                     (const int*)lens, (const int*)slot, (const int*)pre, H, Hkv, max_seq, chunk, nsplit, sl2e, po, pm, pl);
+                                     (const int*)lens, (const int*)slot, (const int*)pre, H, Hkv, max_seq, chunk, nsplit, sl2e, po, pm, pl, out, ldo, cnt);
       break;
     case 96: err = launch_decode<96>(G, grid, s, (const bf16_t*)q, ldq, (const bf16_t*)k_cache, (const bf16_t*)v_cache,
-                                     (const int*)lens, (const int*)slot, (const int*)pre, H, Hkv, max_seq, chunk, nsplit, sl2e, po, pm, pl);
+                                     (const int*)lens, (const int*)slot, (const int*)pre, H, Hkv, max_seq, chunk, nsplit, sl2e, po, pm, pl, out, ldo, cnt);
       break;
     case 128: err = launch_decode<128>(G, grid, s, (const bf16_t*)q, ldq, (const bf16_t*)k_cache, (const bf16_t*)v_cache,
-                                       (const int*)lens, (const int*)slot, (const int*)pre, H, Hkv, max_seq, chunk, nsplit, sl2e, po, pm, pl);
+                                       (const int*)lens, (const int*)slot, (const int*)pre, H, Hkv, max_seq, chunk, nsplit, sl2e, po, pm, pl, out, ldo, cnt);
       break;
     default: return (int)hipErrorInvalidValue;
   }
   if (err) return err;
+  if (nsplit == 1 || cnt) return 0;
   dim3 cgrid(H, B);
   switch (D) {
     case 64: decode_combine_kernel<64><<<cgrid, 64, 0, s>>>(po, pm, pl, H, nsplit, (bf16_t*)o, ldo); break;

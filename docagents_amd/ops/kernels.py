@@ -51,12 +51,13 @@ _SIGS = {
                          c_int, c_int, c_int, c_int, c_float, c_void_p, c_int, c_void_p, c_void_p, c_longlong,
                          c_int, c_void_p],
     "da_set_gqa_mfma": [c_int],
+    "da_malloc_uncached": [c_longlong, ctypes.POINTER(c_void_p)],
     "da_set_flash_waves": [c_int],
     "da_set_gemm_pingpong": [c_int],
     "da_set_gemm_w4": [c_int],
     "da_set_gemm_w4_cfg": [c_int],
     "da_decode_attn": [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
-                       c_int, c_int, c_int, c_float, c_void_p, c_void_p, c_int, c_void_p],
+                       c_int, c_int, c_int, c_float, c_void_p, c_void_p, c_int, c_void_p, c_void_p],
     "da_topk_dense": [c_void_p, c_int, c_int, c_void_p, c_void_p, c_int, c_void_p, c_int, c_float, c_int,
                       c_int, c_void_p, c_void_p, c_void_p, c_void_p],
     "da_topk_ranges": [c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int,
@@ -487,6 +488,37 @@ def flash_attn_varlen(q, k, v, cu_seqlens, max_seqlen: int, H: int, Hkv: int, D:
     return out
 
 
+# Split-KV partials merged inside the decode kernel by the last split of each (row, kv head)
+# (DA_FUSED_COMBINE=0: separate combine launch, for A/B). The ticket counters stay zero between
+# launches; buffers are only ever added, never freed, so a captured graph's pointer stays valid.
+_FUSED_COMBINE = os.environ.get("DA_FUSED_COMBINE", "1") != "0"
+_UC: dict = {}
+
+
+class _RawBuf:
+    """A device allocation outside PyTorch's allocator (uncached memory), as a ``_ptr``-able object."""
+
+    def __init__(self, ptr: int, nbytes: int):
+        self.ptr, self.nbytes = ptr, nbytes
+
+    def data_ptr(self) -> int:
+        return self.ptr
+
+
+def _uncached(tag: str, nbytes: int, device) -> _RawBuf:
+    """Zeroed uncached (L2-bypassing) device memory for cross-workgroup hand-offs (decode split
+    partials + tickets). Grows by adding buffers, never frees: captured graphs keep their pointers."""
+    key = (tag, device.index if device.index is not None else torch.cuda.current_device())
+    bufs = _UC.setdefault(key, [])
+    if not bufs or bufs[-1].nbytes < nbytes:
+        n = max(nbytes, 1 << 20)
+        p = ctypes.c_void_p()
+        with torch.cuda.device(device):
+            _check(lib().da_malloc_uncached(n, ctypes.byref(p)), "hipExtMallocWithFlags(uncached)")
+        bufs.append(_RawBuf(p.value, n))
+    return bufs[-1]
+
+
 def decode_attn(q, k_cache, v_cache, lens, slot, H, Hkv, D, max_len: int, chunk: int = 0, scale=None, out=None,
                 pre=None):
     """q [B, >=H*D] (row stride any multiple of 8); lens/slot int32 [B]; max_len = max(lens) or the
@@ -515,8 +547,12 @@ def decode_attn(q, k_cache, v_cache, lens, slot, H, Hkv, D, max_len: int, chunk:
     scale = scale if scale is not None else 1.0 / math.sqrt(D)
     if pre is not None:
         _i32(pre, "pre"); _req(pre.shape == (B, 2) and pre.is_contiguous(), "pre must be int32 [B, 2]")
+    cnt = None
+    if _FUSED_COMBINE and nsplit > 1:
+        cnt = _uncached("decode_cnt", B * Hkv * 4, q.device)
+        ws = _uncached("decode_ws", B * H * nsplit * (D + 2) * 4, q.device)
     _check(lib().da_decode_attn(_ptr(q), q.stride(0), _ptr(k_cache), _ptr(v_cache), _ptr(lens), _ptr(slot), _ptr(pre), B, H,
-                                Hkv, D, max_seq, chunk, nsplit, float(scale), _ptr(ws), _ptr(out), out.stride(0),
+                                Hkv, D, max_seq, chunk, nsplit, float(scale), _ptr(ws), _ptr(out), out.stride(0), _ptr(cnt),
                                 _stream()), "decode_attn")
     return out
 

@@ -1,0 +1,8 @@
+# Decode attention with the in-kernel split merge: numerics tests, then the chunk sweep.
+set -u
+cd $GRAFT_REPO_ROOT
+mkdir -p gpurun_out
+timeout -k 10 300 python -u -m pytest tests/test_kernels_gpu.py -q -x -p no:cacheprovider -k "decode" --timeout 120 --timeout-method thread > gpurun_out/t_dec.log 2>&1 || { tail -30 gpurun_out/t_dec.log; exit 1; }
+tail -1 gpurun_out/t_dec.log
+timeout -k 10 300 python bench/decode_chunk_sweep.py > gpurun_out/dec_sweep.txt 2>&1 || { tail -20 gpurun_out/dec_sweep.txt; exit 1; }
+cat gpurun_out/dec_sweep.txt
