@@ -503,3 +503,19 @@ def test_decode_attn_shared_prefix(H, Hkv, D):
     got = K.decode_attn(q, kc, vc, lens, slot, H, Hkv, D, max_len=700, chunk=128, pre=pre)
     ref = R.decode_attn(q, kc, vc, lens, slot, H, Hkv, D, pre=pre)
     _close(got, ref, atol=0.02)
+
+
+@pytest.mark.parametrize("fused", [False, True])
+def test_decode_attn_split_merge(fused, monkeypatch):
+    """In-kernel (last split merges, uncached partials) and separate-launch split merge vs reference."""
+    monkeypatch.setattr(K, "_FUSED_COMBINE", fused)
+    torch.manual_seed(3)
+    H = Hkv = 32
+    D, B, S = 96, 3, 1100
+    kc, vc = _rand(4, Hkv, S, D), _rand(4, Hkv, S, D)
+    lens = torch.tensor([1, 513, 1100], device=DEV, dtype=torch.int32)
+    slot = torch.tensor([3, 0, 2], device=DEV, dtype=torch.int32)
+    q = _rand(B, (H + 2 * Hkv) * D)
+    ref = R.decode_attn(q, kc, vc, lens, slot, H, Hkv, D)
+    for ch in (64, 512, 1152):
+        _close(K.decode_attn(q, kc, vc, lens, slot, H, Hkv, D, max_len=S, chunk=ch), ref, atol=0.02)
