@@ -85,6 +85,14 @@ def main():
     ap.add_argument("--ingest-words", type=int, default=2000)
     ap.add_argument("--pdf-ingest", action="store_true",
                     help="ingest synthetic PDFs (gateway PDF extraction in the timed path; BASELINE config 3)")
+    ap.add_argument("--tp", type=int, default=1,
+                    help="tensor-parallel degree of the QA decoder (BASELINE config 5: Llama-3-70B TP=8); "
+                         "the world splits into world/tp data-parallel groups, the index stays world-way sharded")
+    ap.add_argument("--index-kind", default="flat", choices=["flat", "ivfflat"])
+    ap.add_argument("--ivf-lists", type=int, default=1024)
+    ap.add_argument("--ivf-probes", type=int, default=16)
+    ap.add_argument("--enc-dtype", default="bf16", choices=["bf16", "fp8"],
+                    help="encoder GEMM dtype (fp8 = OCP e4m3 MFMA, BASELINE config 5)")
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--seed", type=int, default=0)
     a = ap.parse_args()
@@ -95,8 +103,19 @@ def main():
     if dev.type != "cuda":
         raise SystemExit("bench.py needs a GPU (run it through gpurun)")
     t_setup = time.perf_counter()
-    eng = Engine(a.enc, a.llm, dev, seed=a.seed, max_batch=a.batch, max_seq=4096, temperature=0.2,
-                 max_new_tokens=a.max_new, summary_max_new=128, use_graphs=not a.no_graphs)
+    TP = a.tp
+    if TP < 1 or W % TP:
+        raise SystemExit(f"--tp {TP} must divide the world size {W}")
+    DP, dp_rank = W // TP, R // TP
+    tp_ctx = None
+    if TP > 1:
+        import torch.distributed as dist
+        from docagents_amd.models.llama import TPContext
+        groups = [dist.new_group(list(range(g * TP, (g + 1) * TP))) for g in range(DP)]  # every rank creates every group
+        tp_ctx = TPContext(R % TP, TP, groups[dp_rank])
+    eng = Engine(a.enc, a.llm, dev, seed=a.seed, tp=tp_ctx, max_batch=a.batch, max_seq=4096, temperature=0.2,
+                 max_new_tokens=a.max_new, summary_max_new=128, use_graphs=not a.no_graphs,
+                 index_kind=a.index_kind, ivf_lists=a.ivf_lists, ivf_probes=a.ivf_probes, enc_dtype=a.enc_dtype)
     shard = ShardedIndex(eng.index, R, W)
     d = eng.dim
 
@@ -111,19 +130,23 @@ def main():
     ids = (np.int64(R) * 1_000_000_000 + np.arange(rows, dtype=np.int64))
     eng.index.add_bulk(doc_ids, [a.chunks_per_doc] * ndocs, ids, X)
     del X
+    if a.index_kind == "ivfflat":
+        shard.train(iters=10, sample=min(rows, 1 << 20))  # shared centroids: k-means stats all-reduced (C6)
     vocab_hi = eng.dec_tok.get_vocab_size()
     chunks = ChunkTokens(300, vocab_hi)
-    tg = TextGen(seed=77 + R)
+    tg = TextGen(seed=77 + dp_rank)  # the ranks of one TP group serve the same queries
 
     def make_filters(step: int):
         rng = np.random.default_rng(10_000 + step)
-        out = []
-        for r in range(W):
+        per_dp = []
+        for _ in range(DP):
+            fs = []
             for _ in range(B_cur):
                 rr = rng.integers(0, W, size=a.docs_per_query)
                 ii = rng.integers(0, ndocs, size=a.docs_per_query)
-                out.append([f"d{x}-{y}" for x, y in zip(rr, ii)])
-        return out
+                fs.append([f"d{x}-{y}" for x, y in zip(rr, ii)])
+            per_dp.append(fs)
+        return [f for r in range(W) for f in per_dp[r // TP]]  # rank order, identical within a TP group
 
     def qa_step(step: int, B: int):
         qs = [tg.question() for _ in range(B)]
@@ -145,6 +168,7 @@ def main():
     log(info, f"setup {time.perf_counter() - t_setup:.1f}s; warmup {a.warmup} steps (B={a.batch}/GPU, W={W})")
     for i in range(a.warmup):
         qa_step(i, a.batch)
+        log(info, f"warmup step {i + 1}/{a.warmup} done")
     barrier(); torch.cuda.synchronize()
     t0 = time.perf_counter()
     plen = []
@@ -154,7 +178,7 @@ def main():
     torch.cuda.synchronize(); barrier()
     dt = time.perf_counter() - t0
     dt_max = all_reduce_max(dt, dev)
-    qps = W * a.batch * a.steps / dt_max
+    qps = DP * a.batch * a.steps / dt_max
 
     # ---- p50 cache-miss latency (one query per GPU, end to end) ----
     lat = []
@@ -172,7 +196,7 @@ def main():
     # ---- ingest docs/min: chunk -> enrich+embed -> summarize -> index (per GPU, batched) ----
     docs_per_min = None
     if a.ingest_docs > 0:
-        dg = TextGen(seed=500 + R)
+        dg = TextGen(seed=500 + dp_rank)
         texts = [dg.document(a.ingest_words) for _ in range(a.ingest_docs)]
         if a.pdf_ingest:
             from docagents_amd.text.pdf import extract_text as pdf_text
@@ -205,16 +229,20 @@ def main():
         ingest(texts, "t")
         torch.cuda.synchronize(); barrier()
         di = all_reduce_max(time.perf_counter() - t2, dev)
-        docs_per_min = W * a.ingest_docs / di * 60.0
+        docs_per_min = DP * a.ingest_docs / di * 60.0
 
     gen = eng.gen.stats
     out = {
         "metric": METRIC, "value": round(qps, 3), "unit": "queries/s", "n_gpus": W, "steps": a.steps,
         "warmup": a.warmup, "ms_per_step": round(dt_max / a.steps * 1000, 2), "higher_is_better": True,
-        "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
+        "scaling": "weak", "vs_baseline": None,
+        "dtype": "bf16" if a.enc_dtype == "bf16" else "bf16 (fp8 e4m3 encoder GEMMs)",
         "data": "synthetic (random-init weights; random unit vectors for the background chunks; synthetic questions)",
-        "config": {"model": f"{a.enc} embedder + {a.llm} QA", "global_batch": W * a.batch,
-                   "seq_len": int(np.mean(plen)) if plen else None, "parallelism": f"dp{W} + {W}-way sharded index",
+        "config": {"model": f"{a.enc} embedder + {a.llm} QA", "global_batch": DP * a.batch,
+                   "seq_len": int(np.mean(plen)) if plen else None,
+                   "parallelism": (f"tp{TP} x dp{DP}" if TP > 1 else f"dp{W}") + f" + {W}-way sharded index",
+                   "index_kind": a.index_kind if a.index_kind == "flat" else
+                   f"ivfflat(lists={a.ivf_lists}, probes={a.ivf_probes})",
                    "index_rows_per_gpu": a.index_rows, "top_k": a.top_k, "max_new_tokens": a.max_new,
                    "temperature": 0.2, "min_similarity": a.min_sim, "docs_per_query": a.docs_per_query},
         "p50_cache_miss_ms": round(p50, 2) if p50 else None,

@@ -50,6 +50,14 @@ class TPContext:
                 return self.xgmi.all_reduce_(t)
             import torch.distributed as dist
             if t.is_cuda and dist.get_backend(self.group) == "gloo":  # 1-GPU multi-rank rehearsal
+                if self.xgmi is not None and t.is_contiguous() and t.dtype in (torch.bfloat16, torch.float32):
+                    # prefill-sized sums: max_bytes pieces through the peer buffers, not the host
+                    flat = t.view(-1)
+                    step = self.xgmi.max_bytes // t.element_size() // 8 * 8
+                    if (flat.numel() * t.element_size()) % 16 == 0:
+                        for a in range(0, flat.numel(), step):
+                            self.xgmi.all_reduce_(flat[a:a + step])
+                        return t
                 h = t.cpu()
                 dist.all_reduce(h, group=self.group)
                 t.copy_(h)
@@ -61,6 +69,15 @@ class TPContext:
         """[B, n] on every rank -> [B, n * size] (rank-major columns)."""
         if self.size == 1:
             return t
+        if self.xgmi is not None:
+            # over the peer-mapped xGMI buffers (graph-capturable, unlike a host-staged gather):
+            # every rank contributes its columns into a zero [B, n * size] row block and the
+            # one-shot all-reduce sums them; x + 0 is exact, so this IS the all-gather
+            B, n = t.shape
+            full = torch.zeros((B, n * self.size), dtype=t.dtype, device=t.device)
+            full[:, self.rank * n:(self.rank + 1) * n] = t
+            if self.xgmi.takes(full):
+                return self.xgmi.all_reduce_(full)
         from ..parallel.dist import all_gather_rows
         out = all_gather_rows(t.contiguous(), self.group)
         return out.view(self.size, t.shape[0], -1).permute(1, 0, 2).reshape(t.shape[0], -1)

@@ -15,9 +15,13 @@
 //  * split-K writes fp32 partials; gemm_splitk_reduce applies the same epilogue.
 #include "gemm.h"
 
-template <int BM, int BN, int WM, int WN, int EPI>
+template <int BM, int BN, int WM, int WN, int EPI, int PF = 1>
 __global__ void __launch_bounds__(256)
 gemm_bf16_kernel(GemmArgs p) {
+  // PF = k-tiles in flight in registers. PF = 1: the classic register-staged double buffer (one
+  // tile ahead). Decode-sized tiles (M <= 64) stream weights and are latency-bound at PF = 1 —
+  // one 16-KB W tile per workgroup in flight, ~6 dependent HBM round trips per split — so they
+  // keep PF tiles (up to 72 KB per workgroup) requested ahead of the MFMAs (Little's law).
   constexpr int BK = 64;
   constexpr int TM = BM / WM, TN = BN / WN;
   constexpr int FM = TM / 16, FN = TN / 16;
@@ -48,37 +52,36 @@ gemm_bf16_kernel(GemmArgs p) {
   const int kbeg = blockIdx.z * p.k_per_split;
   const int nk = p.k_per_split / BK;
 
-  // ---- global -> register staging ----
-  u32x4_t ra[LA], rb[LB];
-  auto gload = [&](int kt) {
+  // ---- global -> register staging (PF slots) ----
+  u32x4_t ra[PF][LA], rb[PF][LB];
+  // Rows past M / N are clamped, not branched around: they only feed accumulators whose outputs
+  // are never stored, and branch-free loads keep the compiler's vmcnt waits counted (a load
+  // under a divergent branch makes every later wait a full vmcnt(0) drain).
+  auto gload = [&](u32x4_t (&xa)[LA], u32x4_t (&xb)[LB], int kt) {
     const int k0 = kbeg + kt * BK;
 #pragma unroll
     for (int i = 0; i < LA; ++i) {
       const int idx = tid + 256 * i, r = idx >> 3, c = idx & 7;
-      const int gm = m0 + r;
-      if (gm < p.M) ra[i] = *(const u32x4_t*)(p.A + (size_t)gm * p.lda + k0 + c * 8);
-      else ra[i] = u32x4_t{0, 0, 0, 0};
+      xa[i] = *(const u32x4_t*)(p.A + (size_t)min(m0 + r, p.M - 1) * p.lda + k0 + c * 8);
     }
 #pragma unroll
     for (int i = 0; i < LB; ++i) {
       const int idx = tid + 256 * i, r = idx >> 3, c = idx & 7;
-      const int gn = n0 + r;
-      if (gn < p.N) rb[i] = *(const u32x4_t*)(p.W + (size_t)gn * p.K + k0 + c * 8);
-      else rb[i] = u32x4_t{0, 0, 0, 0};
+      xb[i] = *(const u32x4_t*)(p.W + (size_t)min(n0 + r, p.N - 1) * p.K + k0 + c * 8);
     }
   };
-  auto lstore = [&](int buf) {
+  auto lstore = [&](const u32x4_t (&xa)[LA], const u32x4_t (&xb)[LB], int buf) {
     char* sa = smem + buf * (A_BYTES + B_BYTES);
     char* sb = sa + A_BYTES;
 #pragma unroll
     for (int i = 0; i < LA; ++i) {
       const int idx = tid + 256 * i, r = idx >> 3, c = idx & 7;
-      *(u32x4_t*)(sa + r * 128 + ((c ^ ((r >> 1) & 7)) << 4)) = ra[i];
+      *(u32x4_t*)(sa + r * 128 + ((c ^ ((r >> 1) & 7)) << 4)) = xa[i];
     }
 #pragma unroll
     for (int i = 0; i < LB; ++i) {
       const int idx = tid + 256 * i, r = idx >> 3, c = idx & 7;
-      *(u32x4_t*)(sb + r * 128 + ((c ^ ((r >> 1) & 7)) << 4)) = rb[i];
+      *(u32x4_t*)(sb + r * 128 + ((c ^ ((r >> 1) & 7)) << 4)) = xb[i];
     }
   };
 
@@ -88,39 +91,53 @@ gemm_bf16_kernel(GemmArgs p) {
 #pragma unroll
     for (int j = 0; j < FN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
-  if (nk > 0) {
-    gload(0);
-    lstore(0);
+  // Loads are issued unconditionally (tile index clamped to nk - 1: the redundant tail loads hit
+  // L2) so every vmcnt wait below stays counted; compute / LDS stores sit under uniform branches.
+  const int kl = nk > 0 ? nk - 1 : 0;
+#pragma unroll
+  for (int u = 0; u < PF; ++u) {
+    gload(ra[u], rb[u], min(u, kl));
+    asm volatile("" ::: "memory");  // keep issue order = tile order (counted waits stay short)
   }
+  if (nk > 0) lstore(ra[0], rb[0], 0);
   __syncthreads();
 
   const int fr = lane & 15, fg = lane >> 4;
-  for (int kt = 0; kt < nk; ++kt) {
-    const int cur = kt & 1;
-    if (kt + 1 < nk) gload(kt + 1);
-    const char* sa = smem + cur * (A_BYTES + B_BYTES);
-    const char* sb = sa + A_BYTES;
+  for (int kt0 = 0; kt0 < nk; kt0 += PF) {
 #pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      const int c = kk * 4 + fg;
-      bf16x8_t af[FM], bfr[FN];
+    for (int u = 0; u < PF; ++u) {
+      const int kt = kt0 + u;
+      const int cur = kt & 1;
+      // slot u held tile kt, already copied to LDS: refill it PF tiles ahead
+      if (PF > 1 || kt + 1 < nk) gload(ra[u], rb[u], min(kt + PF, kl));
+      if (kt >= nk) continue;
+      const char* sa = smem + cur * (A_BYTES + B_BYTES);
+      const char* sb = sa + A_BYTES;
 #pragma unroll
-      for (int i = 0; i < FM; ++i) {
-        const int r = wm * TM + i * 16 + fr;
-        af[i] = *(const bf16x8_t*)(sa + r * 128 + ((c ^ ((r >> 1) & 7)) << 4));
+      for (int kk = 0; kk < 2; ++kk) {
+        const int c = kk * 4 + fg;
+        bf16x8_t af[FM], bfr[FN];
+#pragma unroll
+        for (int i = 0; i < FM; ++i) {
+          const int r = wm * TM + i * 16 + fr;
+          af[i] = *(const bf16x8_t*)(sa + r * 128 + ((c ^ ((r >> 1) & 7)) << 4));
+        }
+#pragma unroll
+        for (int j = 0; j < FN; ++j) {
+          const int r = wn * TN + j * 16 + fr;
+          bfr[j] = *(const bf16x8_t*)(sb + r * 128 + ((c ^ ((r >> 1) & 7)) << 4));
+        }
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j) acc[i][j] = mfma16(af[i], bfr[j], acc[i][j]);
       }
-#pragma unroll
-      for (int j = 0; j < FN; ++j) {
-        const int r = wn * TN + j * 16 + fr;
-        bfr[j] = *(const bf16x8_t*)(sb + r * 128 + ((c ^ ((r >> 1) & 7)) << 4));
-      }
-#pragma unroll
-      for (int i = 0; i < FM; ++i)
-#pragma unroll
-        for (int j = 0; j < FN; ++j) acc[i][j] = mfma16(af[i], bfr[j], acc[i][j]);
+      if (kt + 1 < nk) lstore(ra[(u + 1) % PF], rb[(u + 1) % PF], cur ^ 1);
+      // LDS writes visible + buffer reads done; a raw barrier, NOT __syncthreads(): its fence
+      // drains vmcnt and would cancel the PF - 1 tiles still in flight
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
     }
-    if (kt + 1 < nk) lstore(cur ^ 1);
-    __syncthreads();
   }
 
   // ---- epilogue: stage fp32 tile of this wave in LDS, then coalesced 16-B stores ----
@@ -217,6 +234,7 @@ gemm_splitk_reduce(const float* __restrict__ ws, int splits, int M, int N, int e
       float g[8], u[8];
 #pragma unroll
       for (int e = 0; e < 8; ++e) { g[e] = 0.f; u[e] = 0.f; }
+#pragma unroll 4
       for (int s = 0; s < splits; ++s) {
         const float* row = ws + ((size_t)s * M + m) * N;
 #pragma unroll
@@ -227,6 +245,7 @@ gemm_splitk_reduce(const float* __restrict__ ws, int splits, int M, int N, int e
     } else {
 #pragma unroll
       for (int e = 0; e < 8; ++e) v[e] = 0.f;
+#pragma unroll 8
       for (int s = 0; s < splits; ++s) {
         const float* row = ws + ((size_t)s * M + m) * N + oc;
         f32x4_t a = *(const f32x4_t*)row, b = *(const f32x4_t*)(row + 4);
@@ -378,20 +397,34 @@ static int launch_gemv(const GemmArgs& a, int epi, hipStream_t s) {
   return launch_gemv_r<1>(a, epi, s);
 }
 
-template <int BM, int BN, int WM, int WN>
+template <int BM, int BN, int WM, int WN, int PF = 1>
 static int launch_tile(const GemmArgs& a, int epi, int splits, hipStream_t s) {
   const int ntm = (a.M + BM - 1) / BM, ntn = (a.N + BN - 1) / BN;
   dim3 grid(ntm * ntn, 1, splits), block(256);
   switch (splits > 1 ? (int)EPI_PARTIAL : epi) {
-    case EPI_NONE: gemm_bf16_kernel<BM, BN, WM, WN, EPI_NONE><<<grid, block, 0, s>>>(a); break;
-    case EPI_BIAS: gemm_bf16_kernel<BM, BN, WM, WN, EPI_BIAS><<<grid, block, 0, s>>>(a); break;
-    case EPI_GELU: gemm_bf16_kernel<BM, BN, WM, WN, EPI_GELU><<<grid, block, 0, s>>>(a); break;
-    case EPI_SWIGLU: gemm_bf16_kernel<BM, BN, WM, WN, EPI_SWIGLU><<<grid, block, 0, s>>>(a); break;
-    case EPI_RESID: gemm_bf16_kernel<BM, BN, WM, WN, EPI_RESID><<<grid, block, 0, s>>>(a); break;
-    case EPI_PARTIAL: gemm_bf16_kernel<BM, BN, WM, WN, EPI_PARTIAL><<<grid, block, 0, s>>>(a); break;
+    case EPI_NONE: gemm_bf16_kernel<BM, BN, WM, WN, EPI_NONE, PF><<<grid, block, 0, s>>>(a); break;
+    case EPI_BIAS: gemm_bf16_kernel<BM, BN, WM, WN, EPI_BIAS, PF><<<grid, block, 0, s>>>(a); break;
+    case EPI_GELU: gemm_bf16_kernel<BM, BN, WM, WN, EPI_GELU, PF><<<grid, block, 0, s>>>(a); break;
+    case EPI_SWIGLU: gemm_bf16_kernel<BM, BN, WM, WN, EPI_SWIGLU, PF><<<grid, block, 0, s>>>(a); break;
+    case EPI_RESID: gemm_bf16_kernel<BM, BN, WM, WN, EPI_RESID, PF><<<grid, block, 0, s>>>(a); break;
+    case EPI_PARTIAL: gemm_bf16_kernel<BM, BN, WM, WN, EPI_PARTIAL, PF><<<grid, block, 0, s>>>(a); break;
     default: return (int)hipErrorInvalidValue;
   }
   return (int)hipGetLastError();
+}
+
+// Register prefetch depth of the decode tiles (64x128 / 32x128): 1, 2 or 4 (default 4);
+// da_set_gemm_pf for A/B runs.
+static int g_gemm_pf = 4;
+DA_EXPORT void da_set_gemm_pf(int v) { g_gemm_pf = (v == 1 || v == 2) ? v : 4; }
+
+template <int BM, int BN>
+static int launch_decode_tile(const GemmArgs& a, int epi, int splits, hipStream_t s) {
+  switch (g_gemm_pf) {
+    case 1: return launch_tile<BM, BN, 1, 4, 1>(a, epi, splits, s);
+    case 2: return launch_tile<BM, BN, 1, 4, 2>(a, epi, splits, s);
+    default: return launch_tile<BM, BN, 1, 4, 4>(a, epi, splits, s);
+  }
 }
 
 // Split-K reduction fused with the residual add AND the next RMSNorm (decode layers, M <= 64):
@@ -415,7 +448,8 @@ splitk_reduce_resid_rmsnorm(const float* __restrict__ ws, int splits, int M, int
     const int oc = c * 8;
 #pragma unroll
     for (int e = 0; e < 8; ++e) v[i][e] = 0.f;
-    for (int sp = 0; sp < splits; ++sp) {
+#pragma unroll 8
+    for (int sp = 0; sp < splits; ++sp) {  // unrolled: 8 splits' loads in flight, not one at a time
       const float* row = ws + ((size_t)sp * M + m) * N + oc;
       const f32x4_t a = *(const f32x4_t*)row, b = *(const f32x4_t*)(row + 4);
       v[i][0] += a[0]; v[i][1] += a[1]; v[i][2] += a[2]; v[i][3] += a[3];
@@ -466,16 +500,9 @@ DA_EXPORT int da_gemm_resid_rmsnorm(const void* A, int lda, const void* W, void*
   a.A = (const bf16_t*)A; a.W = (const bf16_t*)W; a.C = (bf16_t*)C;
   a.bias = nullptr; a.resid = nullptr; a.ws = (float*)ws;
   a.M = M; a.N = N; a.K = K; a.lda = lda; a.ldc = ldc; a.ldr = ldr; a.k_per_split = K / splits;
-  const int ntm = (M + 31) / 32, ntn = (N + 127) / 128;
-  dim3 grid(ntm * ntn, 1, splits), block(256);
-  if (tile == 2) {
-    dim3 g2(((M + 63) / 64) * ntn, 1, splits);
-    gemm_bf16_kernel<64, 128, 1, 4, EPI_PARTIAL><<<g2, block, 0, s>>>(a);
-  } else {
-    gemm_bf16_kernel<32, 128, 1, 4, EPI_PARTIAL><<<grid, block, 0, s>>>(a);
-  }
-  const hipError_t e = hipGetLastError();
-  if (e != hipSuccess) return (int)e;
+  const int err = tile == 2 ? launch_decode_tile<64, 128>(a, EPI_PARTIAL, splits, s)
+                            : launch_decode_tile<32, 128>(a, EPI_PARTIAL, splits, s);
+  if (err) return err;
   splitk_reduce_resid_rmsnorm<<<M, 256, 0, s>>>((const float*)ws, splits, M, N, (const bf16_t*)bias,
                                                 (const bf16_t*)resid, ldr, (bf16_t*)C, ldc, (const bf16_t*)gamma, eps,
                                                 (bf16_t*)Hout, ldh);
@@ -518,8 +545,8 @@ DA_EXPORT int da_gemm_bf16(const void* A, int lda, const void* W, void* C, int l
   int err;
   switch (tile) {
     case 1: err = launch_tile<128, 128, 2, 2>(a, epi, splits, s); break;
-    case 2: err = launch_tile<64, 128, 1, 4>(a, epi, splits, s); break;
-    case 3: err = launch_tile<32, 128, 1, 4>(a, epi, splits, s); break;
+    case 2: err = launch_decode_tile<64, 128>(a, epi, splits, s); break;
+    case 3: err = launch_decode_tile<32, 128>(a, epi, splits, s); break;
     default: return (int)hipErrorInvalidValue;
   }
   if (err || splits == 1) return err;

@@ -55,6 +55,7 @@ _SIGS = {
     "da_set_flash_waves": [c_int],
     "da_set_gemm_pingpong": [c_int],
     "da_set_gemm_w4": [c_int],
+    "da_set_gemm_pf": [c_int],
     "da_set_gemm_w4_cfg": [c_int],
     "da_decode_attn": [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
                        c_int, c_int, c_int, c_float, c_void_p, c_void_p, c_int, c_void_p, c_void_p],
@@ -105,6 +106,8 @@ def lib() -> ctypes.CDLL:
             L.da_set_gemm_pingpong(int(os.environ["DA_GEMM_PINGPONG"]))
         if os.environ.get("DA_GEMM_W4") is not None:
             L.da_set_gemm_w4(int(os.environ["DA_GEMM_W4"]))
+        if os.environ.get("DA_GEMM_PF") is not None:  # decode-tile register prefetch depth (A/B)
+            L.da_set_gemm_pf(int(os.environ["DA_GEMM_PF"]))
         if os.environ.get("DA_FLASH_WAVES") is not None:
             L.da_set_flash_waves(int(os.environ["DA_FLASH_WAVES"]))
         _LIB = L
@@ -308,7 +311,7 @@ def gemm_fp8(aq, sa, wq, sw, bias=None, epi: int = EPI_NONE, resid=None, out=Non
     return out
 
 
-def gemm_resid_norm(a, w, resid, gamma, eps: float, out=None, h_out=None, bias=None):
+def gemm_resid_norm(a, w, resid, gamma, eps: float, out=None, h_out=None, bias=None, tile: int = 0, splits: int = 0):
     """Decode layer tail (M <= 64): out = resid + a @ w^T (+ bias) — the new residual stream — and
     h_out = RMSNorm(out) * gamma, with the norm fused into the split-K reduction. Returns h_out."""
     _bf16_cuda(a, "a"); _bf16_cuda(w, "w"); _bf16_cuda(resid, "resid"); _bf16_cuda(gamma, "gamma")
@@ -322,10 +325,12 @@ def gemm_resid_norm(a, w, resid, gamma, eps: float, out=None, h_out=None, bias=N
         h_out = torch.empty((M, N), dtype=torch.bfloat16, device=a.device)
     if M == 0:
         return h_out
-    splits = _auto_splits(M, N, K)
+    tile = tile or _decode_tile(M)
+    if splits <= 0:
+        splits = _auto_splits(M, N, K)
     ws = _workspace(splits * M * N * 4, a.device)
     _check(lib().da_gemm_resid_rmsnorm(_ptr(a), a.stride(0), _ptr(w), _ptr(out), out.stride(0), _ptr(bias),
-                                       _ptr(resid), resid.stride(0), M, N, K, _decode_tile(M), splits, _ptr(ws), _ptr(gamma),
+                                       _ptr(resid), resid.stride(0), M, N, K, tile, splits, _ptr(ws), _ptr(gamma),
                                        float(eps), _ptr(h_out), h_out.stride(0), _stream()), "gemm_resid_norm")
     return h_out
 
@@ -336,16 +341,18 @@ def _decode_tile(M: int) -> int:
 
 
 def _auto_splits(M: int, N: int, K: int) -> int:
-    """Split-K for decode-sized M: the largest power of two keeping <= 512 workgroups and >= 6
-    K-steps per workgroup. Chosen from a sweep with weights streamed cold from HBM, as in a real
-    decode step (profiles/splitk_sweep_cold_r1.txt); a warm-MALL sweep favours fewer splits and
-    mis-predicts the in-graph timings."""
+    """Split-K for decode-sized M: the largest power of two keeping <= 256 workgroups (one per CU)
+    and >= 4 K-steps per split. With 4 k-tiles in flight per workgroup (gemm.hip PF) a tile needs
+    fewer splits to cover HBM latency, and fewer splits = fewer partial bytes to reduce. From a
+    graph-replayed sweep with weights streamed cold from HBM, as in a real decode step
+    (profiles/decode_gemm_prefetch_sweep_r1.jsonl: matches the best split on 17 of 20 Phi-3 /
+    Llama-3-8B shapes at M = 16 / 64, within 0.7 us on the rest)."""
     if M > 64:
         return 1
     tiles = math.ceil(M / (32 if _decode_tile(M) == 3 else 64)) * math.ceil(N / 128)
     ksteps = K // 64
     s = 1
-    while tiles * s * 2 <= 512 and ksteps % (s * 2) == 0 and ksteps // (s * 2) >= 6:
+    while tiles * s * 2 <= 256 and ksteps % (s * 2) == 0 and ksteps // (s * 2) >= 4:
         s *= 2
     return s
 

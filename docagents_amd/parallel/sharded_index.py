@@ -53,6 +53,13 @@ class ShardedIndex:
     def train(self, **kw):
         if hasattr(self.local, "train"):
             if self.world > 1:
-                self.local.allreduce = lambda t: dist.all_reduce(t, group=self.group)
+                def allreduce(t):
+                    if t.is_cuda and dist.get_backend(self.group) == "gloo":  # 1-GPU multi-rank rehearsal
+                        h = t.cpu()
+                        dist.all_reduce(h, group=self.group)
+                        t.copy_(h)
+                    else:
+                        dist.all_reduce(t, group=self.group)
+                self.local.allreduce = allreduce
             return self.local.train(**kw)
         return False

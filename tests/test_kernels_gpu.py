@@ -447,6 +447,22 @@ def test_gemm_resid_rmsnorm_fused(M, N, Kd):
     _close(h, h_ref, atol=0.05)
 
 
+@pytest.mark.parametrize("pf", [1, 2, 4])
+@pytest.mark.parametrize("tile,M", [(2, 64), (2, 40), (3, 17)])
+@pytest.mark.parametrize("splits,Kd", [(1, 64), (1, 448), (2, 768), (4, 3072), (3, 576)])
+def test_gemm_decode_tile_prefetch(pf, tile, M, splits, Kd):
+    """Decode tiles with PF k-tiles in flight (incl. nk < PF and nk % PF != 0) match PF = 1."""
+    torch.manual_seed(pf * 100 + M + Kd)
+    N = 392
+    a, w, r = _rand(M, Kd), _rand(N, Kd, scale=Kd ** -0.5), _rand(M, N)
+    K.lib().da_set_gemm_pf(pf)
+    try:
+        got = K.gemm(a, w, epi=K.EPI_RESID, resid=r, tile=tile, splits=splits)
+    finally:
+        K.lib().da_set_gemm_pf(4)
+    _close(got, R.gemm(a, w, epi=K.EPI_RESID, resid=r), atol=0.03)
+
+
 @pytest.mark.parametrize("M,F", [(1, 32), (7, 256), (300, 1024), (4097, 8192)])
 def test_swiglu_interleaved(M, F):
     torch.manual_seed(M + F)
