@@ -50,14 +50,6 @@ class TPContext:
                 return self.xgmi.all_reduce_(t)
             import torch.distributed as dist
             if t.is_cuda and dist.get_backend(self.group) == "gloo":  # 1-GPU multi-rank rehearsal
-                if self.xgmi is not None and t.is_contiguous() and t.dtype in (torch.bfloat16, torch.float32):
-                    # prefill-sized sums: max_bytes pieces through the peer buffers, not the host
-                    flat = t.view(-1)
-                    step = self.xgmi.max_bytes // t.element_size() // 8 * 8
-                    if (flat.numel() * t.element_size()) % 16 == 0:
-                        for a in range(0, flat.numel(), step):
-                            self.xgmi.all_reduce_(flat[a:a + step])
-                        return t
                 h = t.cpu()
                 dist.all_reduce(h, group=self.group)
                 t.copy_(h)
