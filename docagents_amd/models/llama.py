@@ -19,6 +19,8 @@ is added by rank 0's epilogue only, so a single in-place all-reduce yields x + s
 """
 from __future__ import annotations
 
+import os
+
 import numpy as np
 import torch
 
@@ -27,6 +29,9 @@ from ..ops.reference import interleave_gate_up, rope_table
 from .configs import DecoderConfig
 
 EPI_NONE, EPI_SWIGLU, EPI_RESID = 0, 3, 4
+# Decode step of MHA models: RoPE + KV-cache write folded into the attention kernel (DA_FUSED_ROPE=0:
+# separate rope_cache launch, for A/B runs).
+_FUSED_ROPE_DECODE = os.environ.get("DA_FUSED_ROPE", "1") != "0"
 
 
 class TPContext:
@@ -247,15 +252,26 @@ class LlamaDecoder:
             else:
                 h = o.rmsnorm(x, L["ln_attn"], c.eps, out=st.h)
                 qkv = o.gemm(h, L["wqkv"], out=st.qkv)
-            o.rope_cache(qkv, st.pos, self.cos_sin, hl, kl, D, slot=st.slot, k_cache=cache.k(li), v_cache=cache.v(li))
-            a = o.decode_attn(qkv, cache.k(li), cache.v(li), st.lens, st.slot, hl, kl, D, max_len=cache.max_seq,
-                              out=st.attn, pre=st.pre)
+            a = self._decode_attn(qkv, li, st)
             self._attn_out_and_mlp(L, a, x)
         logits = self._logits(x)
         st.logits.copy_(logits)
         o.sample(st.logits, st.temperature, st.seed, 0, out_tok=st.tokens, out_lp=st.lp, conf=st.conf,
                  active=st.active, ctr=st.pos, pos=st.pos, lens=st.lens, hist=st.hist, start=st.start, eos=st.eos)
         return st.tokens
+
+    def _decode_attn(self, qkv, li: int, st: "DecodeState"):
+        """RoPE + new-token cache write + decode attention. MHA (Phi-3): one launch — the attention
+        kernel rotates q / the new k itself and writes the new k / v to the cache; GQA: rope_cache,
+        then the MFMA decode kernel."""
+        c, o, cache = self.cfg, self.ops, self.cache
+        D, hl, kl = c.head_dim, self.hl, self.kl
+        if hl == kl and _FUSED_ROPE_DECODE:
+            return o.decode_attn(qkv, cache.k(li), cache.v(li), st.lens, st.slot, hl, kl, D, max_len=cache.max_seq,
+                                 out=st.attn, pre=st.pre, rope=(self.cos_sin, st.pos))
+        o.rope_cache(qkv, st.pos, self.cos_sin, hl, kl, D, slot=st.slot, k_cache=cache.k(li), v_cache=cache.v(li))
+        return o.decode_attn(qkv, cache.k(li), cache.v(li), st.lens, st.slot, hl, kl, D, max_len=cache.max_seq,
+                             out=st.attn, pre=st.pre)
 
     def _norm_fusable(self, B: int) -> bool:
         """Batched decode (1 < B <= 64, no TP): every RMSNorm rides on the split-K reduction of the
@@ -270,9 +286,7 @@ class LlamaDecoder:
         h = o.rmsnorm(x, layers[0]["ln_attn"], c.eps, out=st.h)
         for li, L in enumerate(layers):
             qkv = o.gemm(h, L["wqkv"], out=st.qkv)
-            o.rope_cache(qkv, st.pos, self.cos_sin, hl, kl, D, slot=st.slot, k_cache=cache.k(li), v_cache=cache.v(li))
-            a = o.decode_attn(qkv, cache.k(li), cache.v(li), st.lens, st.slot, hl, kl, D, max_len=cache.max_seq,
-                              out=st.attn, pre=st.pre)
+            a = self._decode_attn(qkv, li, st)
             h = o.gemm_resid_norm(a, L["wo"], x, L["ln_mlp"], c.eps, out=x, h_out=st.h)      # x += o; h = norm(x)
             g = o.gemm(h, L["w_gu"], epi=EPI_SWIGLU)
             nxt = layers[li + 1]["ln_attn"] if li + 1 < len(layers) else self.w["norm"]

@@ -409,21 +409,55 @@ __device__ __forceinline__ void dec_finish(const float* po, const float* pm, con
   }
   __syncthreads();
   if (!*s_last) return;
+  // One online pass over the splits, 8 splits' (m, l, o) loads issued per step: the partials sit in
+  // uncached memory (~1-2 us per round trip), so a max pass + a sum pass that each walk the splits
+  // one dependent load at a time cost ~2 x nsplit round trips — most of a batch-1 decode attention.
   for (int i = tid; i < G * D; i += blockDim.x) {
     const int g = i / D, d = i % D, h = hk * G + g;
     const size_t base = ((size_t)b * H + h) * nsplit;
-    float M = -INFINITY;
-    for (int s = 0; s < nsplit; ++s) M = fmaxf(M, pm[base + s]);
-    const float Mu = (M == -INFINITY) ? 0.f : M;
-    float lsum = 0.f, acc = 0.f;
-    for (int s = 0; s < nsplit; ++s) {
-      const float f = exp2f(pm[base + s] - Mu);
-      lsum += pl[base + s] * f;
-      acc += po[(base + s) * D + d] * f;
+    float M = -INFINITY, lsum = 0.f, acc = 0.f;
+    for (int s0 = 0; s0 < nsplit; s0 += 8) {
+      float ms[8], ls[8], os[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int s = min(s0 + j, nsplit - 1);
+        ms[j] = pm[base + s];
+        ls[j] = pl[base + s];
+        os[j] = po[(base + s) * D + d];
+      }
+      float mx = M;
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if (s0 + j < nsplit) mx = fmaxf(mx, ms[j]);
+      const float mu = (mx == -INFINITY) ? 0.f : mx;
+      const float r = (M == -INFINITY) ? 0.f : exp2f(M - mu);
+      lsum *= r;
+      acc *= r;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        if (s0 + j >= nsplit) continue;
+        const float f = exp2f(ms[j] - mu);
+        lsum += ls[j] * f;
+        acc += os[j] * f;
+      }
+      M = mx;
     }
     out[(size_t)b * ldo + h * D + d] = f2bf(lsum > 0.f ? acc / lsum : 0.f);
   }
 }
+
+// Fused RoPE + KV-cache write for the decode step (cs != null; MHA kernel): q is the raw qkv row
+// ([q heads | k heads | v heads], row stride ldq). The kernel rotates q on its way into LDS, and
+// the split holding the new token (key L-1, rope position pos[b] == L-1) takes that key's rotated
+// k and v straight from the qkv row — as one extra online-softmax term, never read back from the
+// cache — and writes them into the cache slot for later steps. Replaces the per-layer
+// rope_cache launch of the decode step (bit-identical: the same bf16 roundings).
+struct DecRope {
+  bf16_t* kc;           // cache bases (writable) for the new token's k / v
+  bf16_t* vc;
+  const float* cs;      // [max_pos][D/2][2] (cos, sin)
+  const int* pos;       // [B]
+};
 
 template <int D, int G, int VAR>
 __global__ void __launch_bounds__(256)
@@ -432,7 +466,7 @@ decode_attn_kernel(const bf16_t* __restrict__ q, int ldq, const bf16_t* __restri
                    const int* __restrict__ pre,
                    int H, int Hkv, int max_seq, int chunk, int nsplit, float scale_log2e,
                    float* __restrict__ po, float* __restrict__ pm, float* __restrict__ pl,
-                   bf16_t* __restrict__ out, int ldo, int* __restrict__ cnt) {
+                   bf16_t* __restrict__ out, int ldo, int* __restrict__ cnt, DecRope rope) {
   constexpr int KT = 64;
   constexpr int CPR = D / 8;                       // 16-B chunks per key row
   constexpr int GCD = (CPR % 16 == 0) ? 16 : ((CPR % 8 == 0) ? 8 : ((CPR % 4 == 0) ? 4 : 2));
@@ -448,19 +482,54 @@ decode_attn_kernel(const bf16_t* __restrict__ q, int ldq, const bf16_t* __restri
   const int L = lens[b];
   DA_ASSERT(L >= 0 && L <= max_seq && slot[b] >= 0);
   const int kstart = split * chunk;
-  const int kend = min(L, kstart + chunk);
+  const bool fr = rope.cs != nullptr;
+  const bool own_new = fr && kstart <= L - 1 && L - 1 < kstart + chunk;  // this split holds key L-1
+  const int kend = min(fr ? L - 1 : L, kstart + chunk);                  // fused: key L-1 comes from qkv
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const size_t cbase = ((size_t)slot[b] * Hkv + hk) * (size_t)max_seq * D;
   const int P = pre ? pre[2 * b] : 0;  // shared-prefix keys [0, P) live in slot pre[2b + 1]
   const size_t pbase = P ? ((size_t)pre[2 * b + 1] * Hkv + hk) * (size_t)max_seq * D : cbase;
   DA_ASSERT(P % 64 == 0 && P <= L);
+  DA_ASSERT(!fr || rope.pos[b] == L - 1);
+  __shared__ float skn[D], svn[D], ssn[G];
 
+  // RoPE (rotate-half pairs (i, i + D/2)) of one element of a head row, rounded to bf16 like the
+  // rope_cache kernel that this path replaces
+  auto rot = [&](const bf16_t* hp, int d, int p) -> float {
+    constexpr int HALF = D / 2;
+    const int i = d % HALF;
+    const float x1 = bf2f(hp[i]), x2 = bf2f(hp[i + HALF]);
+    const float c = rope.cs[((size_t)p * HALF + i) * 2], sn = rope.cs[((size_t)p * HALF + i) * 2 + 1];
+    return bf2f(f2bf(d < HALF ? x1 * c - x2 * sn : x2 * c + x1 * sn));
+  };
   for (int i = tid; i < G * D; i += 256) {
     const int g = i / D, d = i % D;
-    sq[g][d] = bf2f(q[(size_t)b * ldq + (hk * G + g) * D + d]) * scale_log2e;
+    const bf16_t* hp = q + (size_t)b * ldq + (hk * G + g) * D;
+    sq[g][d] = (fr ? rot(hp, d, L - 1) : bf2f(hp[d])) * scale_log2e;
+  }
+  if (own_new) {
+    const bf16_t* kr = q + (size_t)b * ldq + (size_t)(H + hk) * D;
+    const bf16_t* vr = q + (size_t)b * ldq + (size_t)(H + Hkv + hk) * D;
+    const size_t crow = cbase + (size_t)(L - 1) * D;
+    for (int d = tid; d < D; d += 256) {
+      const float kv = rot(kr, d, L - 1);
+      skn[d] = kv;
+      svn[d] = bf2f(vr[d]);
+      rope.kc[crow + d] = f2bf(kv);  // for later steps (read back only after this launch)
+      rope.vc[crow + d] = vr[d];
+    }
   }
   for (int i = tid; i < 4 * G * D; i += 256) (&so[0][0][0])[i] = 0.f;
   __syncthreads();
+  if (own_new && w == 0) {  // score of the new key for each query head of this kv head
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      float part = 0.f;
+      for (int d = lane; d < D; d += 64) part += sq[g][d] * skn[d];
+      part = wave_sum(part);
+      if (lane == 0) ssn[g] = part;
+    }
+  }
 
   float m[G], l[G], acc[G][NSET][8];
 #pragma unroll
@@ -472,33 +541,42 @@ decode_attn_kernel(const bf16_t* __restrict__ q, int ldq, const bf16_t* __restri
       for (int e = 0; e < 8; ++e) acc[g][s][e] = 0.f;
   }
 
-  for (int t0 = kstart + w * KT; t0 < kend; t0 += 4 * KT) {
-    const int nk = min(KT, kend - t0);
-    const bool shared = t0 < P;
-    const bf16_t* kb = kc + (shared ? pbase : cbase) + (size_t)t0 * D;
-    const bf16_t* vb = vc + (shared ? pbase : cbase) + (size_t)t0 * D;
-    // K first (V is loaded after the scores: keeps ~100 VGPRs live instead of ~200, so 4-5
-    // waves per SIMD hide the HBM latency instead of 2). VAR bit0: non-temporal loads (the KV
-    // stream is read once per step); bit1: issue V together with K.
-    constexpr bool NT = VAR & 1, VEARLY = (VAR & 2) != 0;
-    auto ld16 = [&](const bf16_t* p) -> u32x4_t {
-      if constexpr (NT) return __builtin_nontemporal_load((const u32x4_t*)p);
-      else return *(const u32x4_t*)p;
-    };
-    u32x4_t kv[CPR];
-    u32x4_t vv[CPR];
+  // VAR bit0: non-temporal loads (the KV stream is read once per step); bit1: V issued together
+  // with K (else after the scores: ~100 VGPRs live instead of ~200, so 4-5 waves per SIMD hide the
+  // HBM latency instead of 2); bit2 (small batches, implies bit1): the wave's NEXT tile is loaded
+  // before the current one is computed — at batch 1 a workgroup's few tiles are latency-bound, one
+  // HBM round trip each, and occupancy buys nothing. Loads are branch-free (chunk index clamped
+  // into the tile; keys >= nk get p = 0) so the compiler's vmcnt waits stay counted.
+  constexpr bool NT = VAR & 1, PFT = (VAR & 4) != 0, VEARLY = PFT || (VAR & 2) != 0;
+  auto ld16 = [&](const bf16_t* p) -> u32x4_t {
+    if constexpr (NT) return __builtin_nontemporal_load((const u32x4_t*)p);
+    else return *(const u32x4_t*)p;
+  };
+  auto tile_base = [&](const bf16_t* c, int t0) {
+    return c + (t0 < P ? pbase : cbase) + (size_t)t0 * D;
+  };
+  auto load_k = [&](u32x4_t (&kv)[CPR], int t0) {
+    const int last = min(KT, kend - t0) * CPR - 1;
+    const bf16_t* kb = tile_base(kc, t0);
 #pragma unroll
     for (int i = 0; i < CPR; ++i) {
       const int c = i * 64 + lane;
-      kv[i] = (c < nk * CPR) ? ld16(kb + c * 8) : u32x4_t{0, 0, 0, 0};
+      if constexpr (PFT) kv[i] = ld16(kb + min(c, last) * 8);
+      else kv[i] = (c <= last) ? ld16(kb + c * 8) : u32x4_t{0, 0, 0, 0};
     }
-    if constexpr (VEARLY) {
+  };
+  auto load_v = [&](u32x4_t (&vv)[CPR], int t0) {
+    const int last = min(KT, kend - t0) * CPR - 1;
+    const bf16_t* vb = tile_base(vc, t0);
 #pragma unroll
-      for (int i = 0; i < CPR; ++i) {
-        const int c = i * 64 + lane;
-        vv[i] = (c < nk * CPR) ? ld16(vb + c * 8) : u32x4_t{0, 0, 0, 0};
-      }
+    for (int i = 0; i < CPR; ++i) {
+      const int c = i * 64 + lane;
+      if constexpr (PFT) vv[i] = ld16(vb + min(c, last) * 8);
+      else vv[i] = (c <= last) ? ld16(vb + c * 8) : u32x4_t{0, 0, 0, 0};
     }
+  };
+  auto process = [&](const u32x4_t (&kv)[CPR], u32x4_t (&vv)[CPR], int t0) {
+    const int nk = min(KT, kend - t0);
     // ---- scores ----
 #pragma unroll
     for (int i = 0; i < CPR; ++i) {
@@ -531,20 +609,20 @@ decode_attn_kernel(const bf16_t* __restrict__ q, int ldq, const bf16_t* __restri
     // ---- online softmax; lane = key ----
 #pragma unroll
     for (int g = 0; g < G; ++g) {
-      float s;
+      float sc;
       if constexpr (SHFL) {
-        s = sp[w][g][lane];
+        sc = sp[w][g][lane];
       } else {
-        s = 0.f;
+        sc = 0.f;
 #pragma unroll
-        for (int j = 0; j < CPR; ++j) s += spart[w][g * KT * CPR + lane * CPR + j];
+        for (int j = 0; j < CPR; ++j) sc += spart[w][g * KT * CPR + lane * CPR + j];
       }
-      if (lane >= nk) s = -INFINITY;
-      const float tmax = wave_max(s);
+      if (lane >= nk) sc = -INFINITY;
+      const float tmax = wave_max(sc);
       const float m_new = fmaxf(m[g], tmax);
       const float m_use = (m_new == -INFINITY) ? 0.f : m_new;
       const float alpha = exp2f(m[g] - m_use);
-      const float p = exp2f(s - m_use);
+      const float p = exp2f(sc - m_use);
       l[g] = l[g] * alpha + wave_sum(p);
       m[g] = m_new;
       sp[w][g][lane] = p;
@@ -558,13 +636,7 @@ decode_attn_kernel(const bf16_t* __restrict__ q, int ldq, const bf16_t* __restri
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     // ---- P * V ----
     asm volatile("" ::: "memory");
-    if constexpr (!VEARLY) {
-#pragma unroll
-      for (int i = 0; i < CPR; ++i) {
-        const int c = i * 64 + lane;
-        vv[i] = (c < nk * CPR) ? ld16(vb + c * 8) : u32x4_t{0, 0, 0, 0};
-      }
-    }
+    if constexpr (!VEARLY) load_v(vv, t0);
 #pragma unroll
     for (int i = 0; i < CPR; ++i) {
       const int c = i * 64 + lane;
@@ -577,12 +649,35 @@ decode_attn_kernel(const bf16_t* __restrict__ q, int ldq, const bf16_t* __restri
       }
 #pragma unroll
       for (int g = 0; g < G; ++g) {
-        const float p = sp[w][g][key];
+        const float pk = sp[w][g][key];
 #pragma unroll
-        for (int e = 0; e < 8; ++e) acc[g][i % NSET][e] += p * vf[e];
+        for (int e = 0; e < 8; ++e) acc[g][i % NSET][e] += pk * vf[e];
       }
     }
     __builtin_amdgcn_wave_barrier();
+  };
+
+  if constexpr (PFT) {
+    u32x4_t ka[CPR], va[CPR], kb2[CPR], vb2[CPR];
+    int t0 = kstart + w * KT;
+    if (t0 < kend) { load_k(ka, t0); load_v(va, t0); }
+    while (t0 < kend) {
+      const int t1 = t0 + 4 * KT;
+      if (t1 < kend) { load_k(kb2, t1); load_v(vb2, t1); }
+      process(ka, va, t0);
+      if (t1 >= kend) break;
+      const int t2 = t1 + 4 * KT;
+      if (t2 < kend) { load_k(ka, t2); load_v(va, t2); }
+      process(kb2, vb2, t1);
+      t0 = t2;
+    }
+  } else {
+    for (int t0 = kstart + w * KT; t0 < kend; t0 += 4 * KT) {
+      u32x4_t kv[CPR], vv[CPR];
+      load_k(kv, t0);
+      if constexpr (VEARLY) load_v(vv, t0);
+      process(kv, vv, t0);
+    }
   }
   // ---- merge lanes -> per-wave O (LDS atomics), then waves -> block partial ----
 #pragma unroll
@@ -601,6 +696,7 @@ decode_attn_kernel(const bf16_t* __restrict__ q, int ldq, const bf16_t* __restri
   for (int i = tid; i < G * D; i += 256) {
     const int g = i / D, d = i % D;
     float M = fmaxf(fmaxf(swm[0][g], swm[1][g]), fmaxf(swm[2][g], swm[3][g]));
+    if (own_new) M = fmaxf(M, ssn[g]);
     const float Mu = (M == -INFINITY) ? 0.f : M;
     float o = 0.f, ls = 0.f;
 #pragma unroll
@@ -608,6 +704,11 @@ decode_attn_kernel(const bf16_t* __restrict__ q, int ldq, const bf16_t* __restri
       const float f = exp2f(swm[ww][g] - Mu);
       o += so[ww][g][d] * f;
       ls += swl[ww][g] * f;
+    }
+    if (own_new) {  // the new token's key: weight exp2(s - M), value straight from the qkv row
+      const float f = exp2f(ssn[g] - Mu);
+      o += svn[d] * f;
+      ls += f;
     }
     dec_store(o, M, ls, b, hk * G + g, d, H, nsplit, split, D, po, pm, pl, out, ldo);
   }
@@ -826,9 +927,9 @@ template <int D, int VAR>
 static int launch_decode_v(int G, dim3 grid, hipStream_t s, const bf16_t* q, int ldq, const bf16_t* kc,
                            const bf16_t* vc, const int* lens, const int* slot, const int* pre, int H, int Hkv, int max_seq, int chunk,
                            int nsplit, float sl2e, float* po, float* pm, float* pl, bf16_t* out, int ldo,
-                           int* cnt) {
+                           int* cnt, DecRope rope) {
 #define DEC(GG) decode_attn_kernel<D, GG, VAR><<<grid, 256, 0, s>>>(q, ldq, kc, vc, lens, slot, pre, H, Hkv, max_seq, \
-                                                                     chunk, nsplit, sl2e, po, pm, pl, out, ldo, cnt)
+                                                                     chunk, nsplit, sl2e, po, pm, pl, out, ldo, cnt, rope)
   switch (G) {
     case 1: DEC(1); break;
     case 2: DEC(2); break;
@@ -845,6 +946,9 @@ static int launch_decode_v(int G, dim3 grid, hipStream_t s, const bf16_t* q, int
 // path (kept for A/B measurements and as the numerics cross-check in tests).
 static int g_gqa_mfma = 1;
 DA_EXPORT void da_set_gqa_mfma(int v) { g_gqa_mfma = v; }
+// MHA decode with the next tile prefetched (VAR bit 2) when B * Hkv <= this (0 = never).
+static int g_dec_pft = 32;
+DA_EXPORT void da_set_decode_pft(int v) { g_dec_pft = v; }
 
 // Measured on MI355X (profiles/decode_attn_variants_r1.json): non-temporal K/V loads + V issued with
 // K reach 6.5 TB/s for MHA (G = 1, Phi-3); with G >= 2 the extra V registers cost more occupancy
@@ -853,9 +957,13 @@ template <int D>
 static int launch_decode(int G, dim3 grid, hipStream_t s, const bf16_t* q, int ldq, const bf16_t* kc,
                          const bf16_t* vc, const int* lens, const int* slot, const int* pre, int H, int Hkv, int max_seq, int chunk,
                          int nsplit, float sl2e, float* po, float* pm, float* pl, bf16_t* out, int ldo,
-                           int* cnt) {
-  if (G == 1)
-    return launch_decode_v<D, 3>(G, grid, s, q, ldq, kc, vc, lens, slot, pre, H, Hkv, max_seq, chunk, nsplit, sl2e, po, pm, pl, out, ldo, cnt);
+                         int* cnt, DecRope rope) {
+  if (G == 1) {
+    if (g_dec_pft && (int)(grid.y * grid.z) <= g_dec_pft)  // few (row, kv head) pairs: latency-bound
+      return launch_decode_v<D, 7>(G, grid, s, q, ldq, kc, vc, lens, slot, pre, H, Hkv, max_seq, chunk, nsplit, sl2e, po, pm, pl, out, ldo, cnt, rope);
+    return launch_decode_v<D, 3>(G, grid, s, q, ldq, kc, vc, lens, slot, pre, H, Hkv, max_seq, chunk, nsplit, sl2e, po, pm, pl, out, ldo, cnt, rope);
+  }
+  if (rope.cs) return (int)hipErrorInvalidValue;  // fused RoPE: MHA kernel only
   if constexpr (D == 64 || D == 128) {
     if (g_gqa_mfma) {
       switch (G) {
@@ -867,7 +975,7 @@ static int launch_decode(int G, dim3 grid, hipStream_t s, const bf16_t* q, int l
       return (int)hipGetLastError();
     }
   }
-  return launch_decode_v<D, 1>(G, grid, s, q, ldq, kc, vc, lens, slot, pre, H, Hkv, max_seq, chunk, nsplit, sl2e, po, pm, pl, out, ldo, cnt);
+  return launch_decode_v<D, 1>(G, grid, s, q, ldq, kc, vc, lens, slot, pre, H, Hkv, max_seq, chunk, nsplit, sl2e, po, pm, pl, out, ldo, cnt, rope);
 }
 
 // ws must hold B*H*nsplit*(D+2) floats. chunk = keys per split (multiple of 64).
@@ -886,12 +994,18 @@ DA_EXPORT int da_malloc_uncached(long long bytes, void** out) {
   return (int)hipDeviceSynchronize();
 }
 
+// cos_sin / pos (both null, or both set): fused RoPE + new-token KV-cache write (MHA only; q is
+// then the raw qkv row, see DecRope).
 DA_EXPORT int da_decode_attn(const void* q, int ldq, const void* k_cache, const void* v_cache, const void* lens,
                              const void* slot, const void* pre, int B, int H, int Hkv, int D, int max_seq, int chunk,
-                             int nsplit, float scale, void* ws, void* o, int ldo, void* counters, void* stream) {
+                             int nsplit, float scale, void* ws, void* o, int ldo, void* counters, const void* cos_sin,
+                             const void* pos, void* stream) {
   bf16_t* out = (bf16_t*)o;
   int* cnt = (int*)counters;
   if (H % Hkv || chunk % 64 || nsplit < 1 || (long)chunk * nsplit < 1) return (int)hipErrorInvalidValue;
+  if ((cos_sin == nullptr) != (pos == nullptr) || (cos_sin && (H != Hkv || ldq < (H + 2 * Hkv) * D)))
+    return (int)hipErrorInvalidValue;
+  const DecRope rope{(bf16_t*)k_cache, (bf16_t*)v_cache, (const float*)cos_sin, (const int*)pos};
   if (B == 0) return 0;
   const int G = H / Hkv;
   float* po = (float*)ws;
@@ -903,13 +1017,13 @@ DA_EXPORT int da_decode_attn(const void* q, int ldq, const void* k_cache, const 
   int err;
   switch (D) {
     case 64: err = launch_decode<64>(G, grid, s, (const bf16_t*)q, ldq, (const bf16_t*)k_cache, (const bf16_t*)v_cache,
-                                     (const int*)lens, (const int*)slot, (const int*)pre, H, Hkv, max_seq, chunk, nsplit, sl2e, po, pm, pl, out, ldo, cnt);
+                                     (const int*)lens, (const int*)slot, (const int*)pre, H, Hkv, max_seq, chunk, nsplit, sl2e, po, pm, pl, out, ldo, cnt, rope);
       break;
     case 96: err = launch_decode<96>(G, grid, s, (const bf16_t*)q, ldq, (const bf16_t*)k_cache, (const bf16_t*)v_cache,
-                                     (const int*)lens, (const int*)slot, (const int*)pre, H, Hkv, max_seq, chunk, nsplit, sl2e, po, pm, pl, out, ldo, cnt);
+                                     (const int*)lens, (const int*)slot, (const int*)pre, H, Hkv, max_seq, chunk, nsplit, sl2e, po, pm, pl, out, ldo, cnt, rope);
       break;
     case 128: err = launch_decode<128>(G, grid, s, (const bf16_t*)q, ldq, (const bf16_t*)k_cache, (const bf16_t*)v_cache,
-                                       (const int*)lens, (const int*)slot, (const int*)pre, H, Hkv, max_seq, chunk, nsplit, sl2e, po, pm, pl, out, ldo, cnt);
+                                       (const int*)lens, (const int*)slot, (const int*)pre, H, Hkv, max_seq, chunk, nsplit, sl2e, po, pm, pl, out, ldo, cnt, rope);
       break;
     default: return (int)hipErrorInvalidValue;
   }

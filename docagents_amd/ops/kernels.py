@@ -56,9 +56,11 @@ _SIGS = {
     "da_set_gemm_pingpong": [c_int],
     "da_set_gemm_w4": [c_int],
     "da_set_gemm_pf": [c_int],
+    "da_set_decode_pft": [c_int],
     "da_set_gemm_w4_cfg": [c_int],
     "da_decode_attn": [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
-                       c_int, c_int, c_int, c_float, c_void_p, c_void_p, c_int, c_void_p, c_void_p],
+                       c_int, c_int, c_int, c_float, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p,
+                       c_void_p],
     "da_topk_dense": [c_void_p, c_int, c_int, c_void_p, c_void_p, c_int, c_void_p, c_int, c_float, c_int,
                       c_int, c_void_p, c_void_p, c_void_p, c_void_p],
     "da_topk_ranges": [c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int,
@@ -108,6 +110,8 @@ def lib() -> ctypes.CDLL:
             L.da_set_gemm_w4(int(os.environ["DA_GEMM_W4"]))
         if os.environ.get("DA_GEMM_PF") is not None:  # decode-tile register prefetch depth (A/B)
             L.da_set_gemm_pf(int(os.environ["DA_GEMM_PF"]))
+        if os.environ.get("DA_DECODE_PFT") is not None:  # MHA decode next-tile prefetch below B*Hkv (A/B)
+            L.da_set_decode_pft(int(os.environ["DA_DECODE_PFT"]))
         if os.environ.get("DA_FLASH_WAVES") is not None:
             L.da_set_flash_waves(int(os.environ["DA_FLASH_WAVES"]))
         _LIB = L
@@ -527,12 +531,15 @@ def _uncached(tag: str, nbytes: int, device) -> _RawBuf:
 
 
 def decode_attn(q, k_cache, v_cache, lens, slot, H, Hkv, D, max_len: int, chunk: int = 0, scale=None, out=None,
-                pre=None):
+                pre=None, rope=None):
     """q [B, >=H*D] (row stride any multiple of 8); lens/slot int32 [B]; max_len = max(lens) or the
     cache capacity (host int, fixes the split count so the launch is graph-capturable).
     chunk = keys per workgroup (0 = auto: enough workgroups to fill 256 CUs, 4 waves x 64-key tiles).
     pre: optional int32 [B, 2] device tensor (P, prefix slot), P % 64 == 0: keys [0, P) of row b
-    are the batch's shared prompt head, stored once in the prefix slot (read through the cache)."""
+    are the batch's shared prompt head, stored once in the prefix slot (read through the cache).
+    rope = (cos_sin fp32 [max_pos, D/2, 2], pos int32 [B]), MHA only: q is the raw qkv row
+    [B, (H + 2 Hkv) D]; the kernel applies RoPE to q and the new token's k and writes that token's
+    k / v into the cache at pos (== lens - 1) — the decode step's rope_cache launch folded in."""
     if chunk <= 0:
         # measured on MI355X (profiles/decode_attn_chunks_r1.txt): per-workgroup overhead dominates
         # small chunks; aim for ~768 workgroups, 512..4096 keys each
@@ -554,13 +561,21 @@ def decode_attn(q, k_cache, v_cache, lens, slot, H, Hkv, D, max_len: int, chunk:
     scale = scale if scale is not None else 1.0 / math.sqrt(D)
     if pre is not None:
         _i32(pre, "pre"); _req(pre.shape == (B, 2) and pre.is_contiguous(), "pre must be int32 [B, 2]")
+    cs = ps = None
+    if rope is not None:
+        cs, ps = rope
+        _req(H == Hkv and D % 8 == 0, "fused RoPE decode: MHA only")
+        _i32(ps, "pos")
+        _req(cs.dtype == torch.float32 and cs.is_contiguous() and cs.shape[1] == D // 2 and cs.shape[2] == 2, "cos_sin")
+        _req(q.stride(1) == 1 and q.shape[1] >= (H + 2 * Hkv) * D, "fused RoPE decode needs the qkv row")
+        _req(k_cache.is_contiguous() and v_cache.is_contiguous(), "caches must be contiguous")
     cnt = None
     if _FUSED_COMBINE and nsplit > 1:
         cnt = _uncached("decode_cnt", B * Hkv * 4, q.device)
         ws = _uncached("decode_ws", B * H * nsplit * (D + 2) * 4, q.device)
     _check(lib().da_decode_attn(_ptr(q), q.stride(0), _ptr(k_cache), _ptr(v_cache), _ptr(lens), _ptr(slot), _ptr(pre), B, H,
                                 Hkv, D, max_seq, chunk, nsplit, float(scale), _ptr(ws), _ptr(out), out.stride(0), _ptr(cnt),
-                                _stream()), "decode_attn")
+                                _ptr(cs), _ptr(ps), _stream()), "decode_attn")
     return out
 
 

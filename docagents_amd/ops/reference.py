@@ -175,8 +175,13 @@ def flash_attn_varlen(q, k, v, cu_seqlens, max_seqlen, H, Hkv, D, causal, scale=
     return res
 
 
-def decode_attn(q, k_cache, v_cache, lens, slot, H, Hkv, D, max_len=None, chunk=256, scale=None, out=None, pre=None):
-    """pre: optional int32 [B, 2] = (P, prefix slot): keys [0, P) of row b come from the prefix slot."""
+def decode_attn(q, k_cache, v_cache, lens, slot, H, Hkv, D, max_len=None, chunk=256, scale=None, out=None, pre=None,
+                rope=None):
+    """pre: optional int32 [B, 2] = (P, prefix slot): keys [0, P) of row b come from the prefix slot.
+    rope = (cos_sin, pos): q is the raw qkv row; RoPE + the new token's cache write happen here
+    (rope_cache on a copy of the rows, then attention)."""
+    if rope is not None:
+        q = rope_cache(q.clone(), rope[1], rope[0], H, Hkv, D, slot=slot, k_cache=k_cache, v_cache=v_cache)
     scale = scale if scale is not None else 1.0 / math.sqrt(D)
     B = q.shape[0]
     G = H // Hkv

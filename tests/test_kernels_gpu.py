@@ -170,6 +170,60 @@ def test_flash_attn_spike():
                R.flash_attn_varlen(q, k, v, cu, L, H, Hkv, D, causal), atol=0.02)
 
 
+@pytest.mark.parametrize("D", [64, 96, 128])
+@pytest.mark.parametrize("lens,chunk,pft", [([1000], 512, 32), ([1], 256, 32), ([513, 257, 64], 256, 0),
+                                            ([2944] * 5, 0, 0), ([65, 1024, 700], 64, 1024)])
+def test_decode_attn_fused_rope(D, lens, chunk, pft):
+    """Decode attention with RoPE + the new token's cache write folded in == rope_cache + attention."""
+    torch.manual_seed(D + len(lens) + chunk)
+    H, slots, max_seq = 4, 6, 4096
+    B = len(lens)
+    kc, vc = _rand(slots, H, max_seq, D), _rand(slots, H, max_seq, D)
+    qkv = _rand(B, 3 * H * D)
+    L = torch.tensor(lens, dtype=torch.int32, device=DEV)
+    pos = L - 1
+    slot = torch.arange(B, dtype=torch.int32, device=DEV) + 1
+    cs = R.rope_table(max_seq, D, 10000.0, device=DEV)
+    kc2, vc2, qkv2, qkv0 = kc.clone(), vc.clone(), qkv.clone(), qkv.clone()
+    K.rope_cache(qkv2, pos, cs, H, H, D, slot=slot, k_cache=kc2, v_cache=vc2)
+    want = K.decode_attn(qkv2, kc2, vc2, L, slot, H, H, D, max_seq, chunk=chunk)
+    K.lib().da_set_decode_pft(pft)
+    try:
+        got = K.decode_attn(qkv, kc, vc, L, slot, H, H, D, max_seq, chunk=chunk, rope=(cs, pos))
+    finally:
+        K.lib().da_set_decode_pft(32)
+    _close(got, want, atol=0.01)
+    for b in range(B):
+        s_, p_ = int(slot[b]), int(pos[b])
+        _close(kc[s_, :, p_], kc2[s_, :, p_], atol=0.01)
+        assert torch.equal(vc[s_, :, p_], vc2[s_, :, p_])
+    assert torch.equal(qkv, qkv0)  # q / k rows untouched (the kernel rotates on the fly)
+    ref = R.decode_attn(qkv.clone(), kc.clone(), vc.clone(), L, slot, H, H, D, rope=(cs, pos))
+    _close(got, ref, atol=0.02)
+
+
+@pytest.mark.parametrize("D", [64, 96, 128])
+@pytest.mark.parametrize("B,chunk", [(1, 512), (2, 256), (3, 1024), (1, 64)])
+def test_decode_attn_prefetch_variant(D, B, chunk):
+    """MHA decode with the next tile prefetched (small batches) == the plain variant."""
+    torch.manual_seed(D + B)
+    H, slots, max_seq = 8, 4, 2048
+    kc, vc = _rand(slots, H, max_seq, D), _rand(slots, H, max_seq, D)
+    q = _rand(B, H * D)
+    lens = torch.tensor([1000, 1537, 63][:B], dtype=torch.int32, device=DEV)
+    slot = torch.tensor([2, 0, 3][:B], dtype=torch.int32, device=DEV)
+    outs = []
+    for pft in (0, 1024):
+        K.lib().da_set_decode_pft(pft)
+        try:
+            outs.append(K.decode_attn(q, kc, vc, lens, slot, H, H, D, max_seq, chunk=chunk))
+        finally:
+            K.lib().da_set_decode_pft(32)
+    ref = R.decode_attn(q, kc, vc, lens, slot, H, H, D, max_seq)
+    _close(outs[1], ref, atol=0.02)
+    _close(outs[1], outs[0], atol=0.01)
+
+
 @pytest.mark.parametrize("H,Hkv,D", [(32, 32, 96), (32, 8, 128), (8, 1, 128), (12, 6, 64)])
 def test_decode_attn(H, Hkv, D):
     torch.manual_seed(H * D)
