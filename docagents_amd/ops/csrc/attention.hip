@@ -187,6 +187,7 @@ struct FaPrefix {
   const bf16_t* v;
   long long hstride;
   int len;
+  int rev;  // causal: dispatch query blocks longest-first (set by the launcher)
 };
 
 template <int D, int NW>
@@ -201,7 +202,10 @@ flash_attn_v2_kernel(const bf16_t* __restrict__ q, const bf16_t* __restrict__ k,
 
   const int b = blockIdx.z, h = blockIdx.y;
   const int s0 = cu[b], L = cu[b + 1] - s0;
-  const int q0 = blockIdx.x * C::QB;
+  // causal: the longest query blocks (most keys) are dispatched first, so the kernel's tail is
+  // made of short blocks (longest-processing-time-first packing); pre.rev = 0 keeps grid order
+  const int qb = (causal && pre.rev) ? (int)gridDim.x - 1 - (int)blockIdx.x : (int)blockIdx.x;
+  const int q0 = qb * C::QB;
   if (q0 >= L) return;
   const int hk = h / (H / Hkv);
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -1043,6 +1047,9 @@ DA_EXPORT int da_decode_attn(const void* q, int ldq, const void* k_cache, const 
 // work on the diagonal — profiles/attn_v2_waves_r1.json). 4 / 8 force a shape (A/B runs).
 static int g_fa_waves = 0;
 DA_EXPORT void da_set_flash_waves(int nw) { g_fa_waves = nw; }
+// causal flash: longest query blocks first (1, default) or grid order (0); A/B runs
+static int g_fa_rev = 1;
+DA_EXPORT void da_set_flash_rev(int v) { g_fa_rev = v ? 1 : 0; }
 
 template <int NW>
 static int launch_fa2(const void* q, const void* k, const void* v, int ldq, int ldk, int ldv, const void* cu_seqlens,
@@ -1080,7 +1087,7 @@ DA_EXPORT int da_flash_attn_v2(const void* q, const void* k, const void* v, int 
   if (B == 0 || max_seqlen == 0) return 0;
   const float sl2e = scale * 1.4426950408889634f;
   hipStream_t s = (hipStream_t)stream;
-  const FaPrefix pre{(const bf16_t*)pre_k, (const bf16_t*)pre_v, pre_hstride, pre_len};
+  const FaPrefix pre{(const bf16_t*)pre_k, (const bf16_t*)pre_v, pre_hstride, pre_len, g_fa_rev};
   if (g_fa_waves == 8 || (g_fa_waves == 0 && !causal))
     return launch_fa2<8>(q, k, v, ldq, ldk, ldv, cu_seqlens, B, max_seqlen, H, Hkv, D, causal, sl2e, o, ldo, pre, s);
   return launch_fa2<4>(q, k, v, ldq, ldk, ldv, cu_seqlens, B, max_seqlen, H, Hkv, D, causal, sl2e, o, ldo, pre, s);

@@ -57,6 +57,7 @@ _SIGS = {
     "da_set_gemm_w4": [c_int],
     "da_set_gemm_pf": [c_int],
     "da_set_decode_pft": [c_int],
+    "da_set_flash_rev": [c_int],
     "da_set_gemm_w4_cfg": [c_int],
     "da_decode_attn": [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
                        c_int, c_int, c_int, c_float, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p,
@@ -110,6 +111,8 @@ def lib() -> ctypes.CDLL:
             L.da_set_gemm_w4(int(os.environ["DA_GEMM_W4"]))
         if os.environ.get("DA_GEMM_PF") is not None:  # decode-tile register prefetch depth (A/B)
             L.da_set_gemm_pf(int(os.environ["DA_GEMM_PF"]))
+        if os.environ.get("DA_FLASH_REV") is not None:  # causal flash longest-first dispatch (A/B)
+            L.da_set_flash_rev(int(os.environ["DA_FLASH_REV"]))
         if os.environ.get("DA_DECODE_PFT") is not None:  # MHA decode next-tile prefetch below B*Hkv (A/B)
             L.da_set_decode_pft(int(os.environ["DA_DECODE_PFT"]))
         if os.environ.get("DA_FLASH_WAVES") is not None:
