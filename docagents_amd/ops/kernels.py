@@ -203,7 +203,7 @@ def gemm(a: torch.Tensor, w: torch.Tensor, bias=None, epi: int = EPI_NONE, resid
         ldr = resid.stride(0)
     if M == 0:
         return out
-    if (_BLAS_PREFILL and tile == 0 and splits <= 0 and rms is None and M >= _BLAS_MIN_M
+    if (_BLAS_PREFILL and tile == 0 and splits <= 0 and rms is None and _blas_size_ok(M, N)
             and (epi in (EPI_NONE, EPI_BIAS) or (epi == EPI_RESID and bias is None))):
         return _blas_gemm(a, w, bias, epi, resid, out)
     if _BLAS_SWIGLU and epi == EPI_SWIGLU and tile == 0 and splits <= 0 and rms is None and M >= _BLAS_MIN_M:
@@ -238,6 +238,16 @@ _BLAS_PREFILL = os.environ.get("DA_BLAS_PREFILL", "1") != "0"
 # A/B (profiles/ab_blas_swiglu_r1.txt): +0.3% flagship; DA_BLAS_SWIGLU=0 keeps the fused gemm256.
 _BLAS_SWIGLU = os.environ.get("DA_BLAS_SWIGLU", "1") == "1"
 _BLAS_MIN_M = int(os.environ.get("DA_BLAS_MIN_M", "4096"))
+# Between 1024 rows and _BLAS_MIN_M a plain GEMM also goes to hipBLASLt when the 256x256 tile would
+# leave CUs idle (< 256 tiles, e.g. the o / down projections of a batch-1 ~2.9k-token prefill, N =
+# 3072: 144 tiles; the 128x128 fallback reached only ~0.6 PF/s there). DA_BLAS_UNDERFILL=0: off.
+_BLAS_UNDERFILL = os.environ.get("DA_BLAS_UNDERFILL", "1") != "0"
+
+
+def _blas_size_ok(M: int, N: int) -> bool:
+    if M >= _BLAS_MIN_M:
+        return True
+    return _BLAS_UNDERFILL and M >= 1024 and math.ceil(M / 256) * math.ceil(N / 256) < 256
 
 
 def swiglu_interleaved(x: torch.Tensor, out=None) -> torch.Tensor:
