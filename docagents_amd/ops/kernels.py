@@ -68,6 +68,7 @@ _SIGS = {
                        c_float, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p],
     "da_topk_merge": [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p],
     "da_kmeans_accum": [c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p],
+    "da_mall_prefetch": [c_void_p, ctypes.c_long, c_int, c_void_p, c_void_p],
 }
 
 
@@ -165,6 +166,15 @@ def _workspace(nbytes: int, device) -> torch.Tensor:
     return buf
 
 
+def mall_prefetch(t: torch.Tensor, nwg: int = 32) -> None:
+    """Read ``t`` with ``nwg`` workgroups on the current stream so a later consumer finds it in the
+    memory-side Infinity Cache (loads only; see csrc/prefetch.hip)."""
+    _req(t.is_cuda and t.is_contiguous() and t.data_ptr() % 16 == 0, "prefetch needs a contiguous 16-B aligned tensor")
+    sink = _workspace(256, t.device)
+    _check(lib().da_mall_prefetch(_ptr(t), t.numel() * t.element_size(), nwg, _ptr(sink), _stream()),
+           "da_mall_prefetch")
+
+
 def gemv_fusable(M: int, N: int, K: int, epi: int = EPI_NONE) -> bool:
     """True when gemm() runs the batch-1 GEMV (which can also fuse the input RMSNorm)."""
     return M == 1 and K % 512 == 0 and N % 4 == 0 and (epi != EPI_SWIGLU or N % 32 == 0)
@@ -206,7 +216,8 @@ def gemm(a: torch.Tensor, w: torch.Tensor, bias=None, epi: int = EPI_NONE, resid
     if (_BLAS_PREFILL and tile == 0 and splits <= 0 and rms is None and _blas_size_ok(M, N)
             and (epi in (EPI_NONE, EPI_BIAS) or (epi == EPI_RESID and bias is None))):
         return _blas_gemm(a, w, bias, epi, resid, out)
-    if _BLAS_SWIGLU and epi == EPI_SWIGLU and tile == 0 and splits <= 0 and rms is None and M >= _BLAS_MIN_M:
+    if (_BLAS_SWIGLU and epi == EPI_SWIGLU and tile == 0 and splits <= 0 and rms is None
+            and (M >= _BLAS_MIN_M or _blas_mid(M))):
         return swiglu_interleaved(torch.mm(a, w.t()), out)
     if tile == 0 and splits <= 0 and gemv_fusable(M, N, K, epi):
         tile, splits = 6, 1  # batch-1 decode: weight-streaming GEMV, one launch, no split-K workspace
@@ -244,8 +255,20 @@ _BLAS_MIN_M = int(os.environ.get("DA_BLAS_MIN_M", "4096"))
 _BLAS_UNDERFILL = os.environ.get("DA_BLAS_UNDERFILL", "1") != "0"
 
 
+# 65..1023 rows (decode batches above 64, shared-prompt-head and short prefills): too many rows for
+# the 64-row decode tiles, too few to fill the 128x128 / 256x256 tiles with split-K off. Measured on
+# a 32-layer Phi-3 GEMM chain in one HIP graph (profiles/decode_gemm_mid_m_r1.jsonl): hipBLASLt
+# 3.2-7.6 ms vs 8.4-10.5 ms in-tree for M = 80..1023 (plain and gate/up + separate SwiGLU alike);
+# M <= 64 stays on the decode tiles (2.54 vs 2.61 ms at M = 64). DA_BLAS_MID=0: off.
+_BLAS_MID = os.environ.get("DA_BLAS_MID", "1") != "0"
+
+
+def _blas_mid(M: int) -> bool:
+    return _BLAS_MID and 64 < M < 1024
+
+
 def _blas_size_ok(M: int, N: int) -> bool:
-    if M >= _BLAS_MIN_M:
+    if M >= _BLAS_MIN_M or _blas_mid(M):
         return True
     return _BLAS_UNDERFILL and M >= 1024 and math.ceil(M / 256) * math.ceil(N / 256) < 256
 

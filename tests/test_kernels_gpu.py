@@ -539,6 +539,37 @@ def test_gemm_swiglu_blas_route(monkeypatch):
     _close(got, ref, atol=0.03)
 
 
+@pytest.mark.parametrize("M", [65, 128, 261, 1023])
+def test_gemm_mid_m_blas_route(M):
+    """65..1023 rows go to hipBLASLt (plain, residual, gate/up + SwiGLU) and match the fp32 reference;
+    the in-tree 128x128 tile (explicit tile) still computes the same product."""
+    assert K._blas_mid(M)
+    torch.manual_seed(M)
+    N, F, Kd = 384, 256, 512
+    a, w = _rand(M, Kd), _rand(N, Kd, scale=Kd ** -0.5)
+    ref = a.float() @ w.float().t()
+    _close(K.gemm(a, w), ref, atol=0.03)
+    resid = _rand(M, N)
+    _close(K.gemm(a, w, epi=K.EPI_RESID, resid=resid.clone(), out=None), ref + resid.float(), atol=0.05)
+    x = resid.clone()
+    K.gemm(a, w, epi=K.EPI_RESID, resid=x, out=x)  # in-place residual add (beta = 1)
+    _close(x, ref + resid.float(), atol=0.05)
+    gate, up = _rand(F, Kd, scale=Kd ** -0.5), _rand(F, Kd, scale=Kd ** -0.5)
+    got = K.gemm(a, R.interleave_gate_up(gate, up), epi=K.EPI_SWIGLU)
+    _close(got, torch.nn.functional.silu(a.float() @ gate.float().t()) * (a.float() @ up.float().t()), atol=0.03)
+    _close(K.gemm(a, w, tile=1), ref, atol=0.03)
+
+
+def test_mall_prefetch_reads_only():
+    """The side-stream weight prefetch kernel (bench/prefetch_probe.py) leaves its input unchanged."""
+    w = _rand(4099, 256)
+    before = w.clone()
+    K.mall_prefetch(w, 64)
+    K.mall_prefetch(w[:3], 1)
+    torch.cuda.synchronize()
+    assert torch.equal(w, before)
+
+
 @pytest.mark.parametrize("H,Hkv,D,P", [(32, 32, 96, 261), (8, 2, 128, 64), (4, 4, 64, 1), (4, 2, 96, 130)])
 @pytest.mark.parametrize("nw", [4, 8])
 def test_flash_attn_shared_prefix(H, Hkv, D, P, nw):
