@@ -1,4 +1,6 @@
-"""One prefill-shaped GEMM repeated (for rocprofv3 counter collection)."""
+"""One prefill-shaped GEMM repeated (for rocprofv3 counter collection).
+
+python bench/gemm_one.py [M N K]; env ARM = tile[:sched] of the in-tree kernel (default 7) or "blas"."""
 import os
 import sys
 
@@ -8,9 +10,17 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from docagents_amd.ops import kernels as K  # noqa: E402
 
 M, N, Kd = (int(v) for v in (sys.argv[1:4] if len(sys.argv) > 3 else (32768, 9216, 3072)))
+arm = os.environ.get("ARM", "7")
 x = (torch.rand(M, Kd, device="cuda") * 2 - 1).bfloat16()
 w = ((torch.rand(N, Kd, device="cuda") * 2 - 1) * Kd ** -0.5).bfloat16()
+out = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+tile, _, sched = arm.partition(":")
+if sched:
+    K.lib().da_set_gemm8p_sched(int(sched))
 for _ in range(5):
-    K.gemm(x, w, tile=int(os.environ.get("TILE", "4")), splits=1)
+    if arm == "blas":
+        torch.mm(x, w.t(), out=out)
+    else:
+        K.gemm(x, w, tile=int(tile), splits=1, out=out)
 torch.cuda.synchronize()
 print("ok")

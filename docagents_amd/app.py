@@ -85,7 +85,8 @@ async def build_store(cfg: Config, log: Logger, deps: Deps):
         from .store.sqlite_vectors import SqliteVectors
         vectors = SqliteVectors(meta)
     log.info("using store", "metadata", path, "vectors", vp)
-    return CompositeStore(meta, vectors, min_similarity=cfg.min_similarity)
+    direct = vp == "engine" and cfg.effective_embedder_provider() in ("engine", "openai")
+    return CompositeStore(meta, vectors, min_similarity=cfg.min_similarity, direct_embed=direct)
 
 
 def worker_concurrency(cfg: Config) -> int:

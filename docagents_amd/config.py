@@ -75,6 +75,10 @@ class Config:
     worker_concurrency: int = field(default=0, metadata={"env": "WORKER_CONCURRENCY"})  # 0 -> auto
     engine_continuous: bool = field(default=True, metadata={"env": "ENGINE_CONTINUOUS"})
     engine_cb_steps: int = field(default=8, metadata={"env": "ENGINE_CB_STEPS"})
+    # --- new keys: durable vector shards (index/wal.py) ---
+    index_dir: str = field(default="", metadata={"env": "INDEX_DIR"})  # "" -> DATA_DIR/index; "none" -> off
+    index_checkpoint_s: float = field(default=300.0, metadata={"env": "INDEX_CHECKPOINT_S"})
+    index_fsync: bool = field(default=True, metadata={"env": "INDEX_FSYNC"})
 
     def database_url(self) -> str:
         """config.go:56-64 (kept for parity; the sqlite store uses db_path)."""
@@ -85,6 +89,9 @@ class Config:
         if self.db_path:
             return self.db_path
         return os.path.join(self.data_dir, "docagents.sqlite3")
+
+    def index_dir_path(self) -> str:
+        return self.index_dir or os.path.join(self.data_dir, "index")
 
     def effective_embedder_provider(self) -> str:
         # reference quirk: embedder chosen by LLM_PROVIDER (internal/app/deps.go:239); an explicit

@@ -34,9 +34,21 @@ def owner_of(doc_id: str, world: int) -> int:
 class EngineGroup:
     """Executes engine commands on one rank or on all ranks of a torch.distributed group."""
 
-    def __init__(self, engine, rank: int = 0, world: int = 1, ctrl_group=None, data_group=None):
+    def __init__(self, engine, rank: int = 0, world: int = 1, ctrl_group=None, data_group=None, shard_log=None):
         self.engine, self.rank, self.world = engine, rank, world
         self.ctrl_group, self.data_group = ctrl_group, data_group
+        # durable shard (index/wal.py): every mutation of this rank's rows is logged before it is
+        # applied; None = HBM only (tests, benchmarks)
+        self.shard_log = shard_log
+
+    def _put(self, doc_id, keys, vecs):
+        """Replace ``doc_id``'s rows in this rank's shard (logged first when durable)."""
+        idx = self.engine.index
+        if self.shard_log is not None:
+            self.shard_log.put(idx, doc_id, keys, vecs)
+        else:
+            idx.remove_doc(doc_id)
+            idx.add(doc_id, keys, vecs)
 
     # ---------------------------------------------------------------- collectives (control plane)
     def _bcast(self, obj):
@@ -119,11 +131,45 @@ class EngineGroup:
             return [d for p in parts for d in p[0]], any(p[1] for p in parts)
         if cmd == "index_add":
             if owner_of(a["doc_id"], self.world) == self.rank:
-                e.index.add(a["doc_id"], a["keys"], torch.from_numpy(np.ascontiguousarray(a["vecs"], dtype=np.float32)))
+                self._put(a["doc_id"], np.asarray(a["keys"], dtype=np.int64),
+                          torch.from_numpy(np.ascontiguousarray(a["vecs"], dtype=np.float32)))
             return True
+        if cmd == "embed_index":
+            # ingest without a vector round trip: the owner rank of each document
+            # embeds its chunks and writes the unit-norm rows straight into its HBM shard; only the
+            # row counts travel back
+            mine = [it for it in a["items"] if owner_of(it[0], self.world) == self.rank]
+            counts = {}
+            if mine:
+                faults.maybe_fail("engine.embed")
+                texts = [t for _, _, ts in mine for t in ts]
+                v = e.embed(texts, True)
+                o = 0
+                for doc_id, keys, ts in mine:
+                    self._put(doc_id, np.asarray(keys, dtype=np.int64), v[o:o + len(ts)])
+                    counts[doc_id] = len(ts)
+                    o += len(ts)
+            merged = {}
+            for part in self._gather(counts):
+                merged.update(part)
+            return [merged.get(it[0], 0) for it in a["items"]]
         if cmd == "index_remove":
-            n = e.index.remove_doc(a["doc_id"])
+            if self.shard_log is not None:
+                n = self.shard_log.remove(e.index, a["doc_id"])
+            else:
+                n = e.index.remove_doc(a["doc_id"])
             return sum(self._gather(n))
+        if cmd == "index_docs":
+            rows = {d: en.rows for d, en in e.index.docs.items() if en.rows}
+            merged = {}
+            for part in self._gather(rows):
+                for d, n in part.items():
+                    merged[d] = merged.get(d, 0) + n
+            return merged
+        if cmd == "checkpoint":
+            if self.shard_log is not None:
+                self.shard_log.checkpoint(e.index)
+            return sum(self._gather(len(e.index)))
         if cmd == "search":
             return self._search(a)
         if cmd == "stats":
@@ -184,12 +230,13 @@ class EngineGroup:
 class EngineServer:
     """asyncio RPC front end with per-method micro-batch queues."""
 
-    BATCHED = ("embed", "answer", "summarize")
+    BATCHED = ("embed", "answer", "summarize", "embed_index")
 
     def __init__(self, group: EngineGroup, log, max_batch_items: int = 256, step_timeout_s: float = 300.0,
                  hard_timeout_s: float = 0.0, liveness_s: float = 30.0, profiler: StepProfiler | None = None,
-                 continuous: bool = False, cb_steps: int = 8):
+                 continuous: bool = False, cb_steps: int = 8, checkpoint_s: float = 0.0):
         self.group, self.log = group, log
+        self.checkpoint_s = checkpoint_s  # periodic shard snapshots when the shard is durable (0 = off)
         self.gpu = cf.ThreadPoolExecutor(max_workers=1, thread_name_prefix="gpu")
         self.queues: dict[str, asyncio.Queue] = {}
         self.max_batch_items = max_batch_items
@@ -286,6 +333,17 @@ class EngineServer:
                     f.set_result((ans, conf))
             metrics.ENGINE_ITEMS.labels("answer").inc(len(done))
 
+    async def _checkpoint_loop(self):
+        """Periodic shard snapshot + log rotation (bounds replay time after a crash)."""
+        while True:
+            await asyncio.sleep(self.checkpoint_s)
+            if self.group.shard_log.stats["rows_since_ckpt"] == 0:
+                continue
+            try:
+                await self._gpu("checkpoint", {})
+            except Exception as e:  # noqa: BLE001
+                self.log.error("index checkpoint failed", "err", repr(e))
+
     async def _liveness_loop(self):
         """C7: periodic rank-liveness all-reduce while idle (a dead follower hangs it -> watchdog)."""
         while True:
@@ -357,7 +415,11 @@ class EngineServer:
         if method == "search":
             s, ids = await self._gpu("search", args)
             return {"scores": s, "keys": ids}
-        if method in ("index_add", "index_remove", "snapshot", "restore", "ping"):
+        if method == "embed_index":
+            res = await self._enqueue("embed_index", [(str(args["doc_id"]), np.asarray(args["keys"], dtype=np.int64),
+                                                       list(args["texts"]))])
+            return {"rows": int(res[0]), "dim": int(self.group.engine.dim)}
+        if method in ("index_add", "index_remove", "snapshot", "restore", "ping", "index_docs", "checkpoint"):
             return await self._gpu(method, args)
         if method == "stats":
             st = await self._gpu("stats", {})
@@ -392,10 +454,12 @@ class EngineServer:
             writer.close()
 
     async def start(self, url: str):
-        for m in ("embed", "embed_raw", "answer", "summarize"):
+        for m in ("embed", "embed_raw", "answer", "summarize", "embed_index"):
             self.queues[m] = asyncio.Queue()
-        for m in ("embed", "answer", "summarize"):
+        for m in ("embed", "answer", "summarize", "embed_index"):
             asyncio.ensure_future(self._batcher(m))
+        if self.checkpoint_s > 0 and self.group.shard_log is not None:
+            self.checkpoint_task = asyncio.ensure_future(self._checkpoint_loop())
         self.queues_raw_task = asyncio.ensure_future(self._batcher_raw())
         self.watchdog.start()
         if self.continuous:

@@ -11,7 +11,7 @@ import torch
 from safetensors.torch import load_file, save_file
 
 
-def save_index(index, path: str) -> str:
+def save_index(index, path: str, extra_meta: dict | None = None) -> str:
     with index.lock:
         sel, docs = index.live_rows_by_doc()
         docs = [[d, n] for d, n in docs]
@@ -21,11 +21,18 @@ def save_index(index, path: str) -> str:
         if getattr(index, "centroids", None) is not None:
             tensors["centroids"] = index.centroids.cpu().contiguous()
         meta = {"dim": str(index.dim), "kind": index.kind, "docs": json.dumps(docs)}
+        meta.update({k: str(v) for k, v in (extra_meta or {}).items()})
     tmp = path + ".tmp"
     os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
     save_file(tensors, tmp, metadata=meta)
     os.replace(tmp, path)
     return path
+
+
+def snapshot_meta(path: str) -> dict:
+    from safetensors import safe_open
+    with safe_open(path, framework="pt") as f:
+        return dict(f.metadata() or {})
 
 
 def load_index(index, path: str) -> int:

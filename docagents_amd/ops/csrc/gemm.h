@@ -24,3 +24,5 @@ struct GemmArgs {
 int launch_gemm256(const GemmArgs& a, int epi, hipStream_t s, int fp8 = 0);
 // 4-wave 256x256 bf16 variant (gemm256w4.hip); K % 32 == 0
 int launch_gemm256w4(const GemmArgs& a, int epi, hipStream_t s);
+// phase-split 256x256 bf16 kernel (gemm8p.hip); K % 64 == 0, K >= 128
+int launch_gemm8p(const GemmArgs& a, int epi, hipStream_t s);

@@ -534,9 +534,13 @@ DA_EXPORT int da_gemm_bf16(const void* A, int lda, const void* W, void* C, int l
   if (rms_gamma && tile != 6) return (int)hipErrorInvalidValue;  // fused RMSNorm: GEMV path only
   if (tile == 0) {
     const long t256 = (long)((M + 255) / 256) * ((N + 255) / 256);
-    tile = (M <= 32) ? 3 : (M <= 64 ? 2 : (t256 >= 256 && splits == 1 ? 4 : 1));
+    tile = (M <= 32) ? 3 : (M <= 64 ? 2 : (t256 >= 256 && splits == 1 && K >= 128 ? 7 : 1));
   }
   if (tile == 4 && g_gemm_w4 && K % 32 == 0) tile = 5;
+  if (tile == 7) {
+    if (splits != 1 || K < 128) return (int)hipErrorInvalidValue;
+    return launch_gemm8p(a, epi, s);
+  }
   if (tile == 4 || tile == 5) {
     if (splits != 1) return (int)hipErrorInvalidValue;
     return tile == 5 ? launch_gemm256w4(a, epi, s) : launch_gemm256(a, epi, s);

@@ -54,6 +54,7 @@ _SIGS = {
     "da_malloc_uncached": [c_longlong, ctypes.POINTER(c_void_p)],
     "da_set_flash_waves": [c_int],
     "da_set_gemm_pingpong": [c_int],
+    "da_set_gemm8p_sched": [c_int],
     "da_set_gemm_w4": [c_int],
     "da_set_gemm_pf": [c_int],
     "da_set_decode_pft": [c_int],
@@ -108,6 +109,8 @@ def lib() -> ctypes.CDLL:
         # schedule overrides for A/B measurements (defaults are the measured-best variants)
         if os.environ.get("DA_GEMM_PINGPONG") is not None:
             L.da_set_gemm_pingpong(int(os.environ["DA_GEMM_PINGPONG"]))
+        if os.environ.get("DA_GEMM8P_SCHED") is not None:
+            L.da_set_gemm8p_sched(int(os.environ["DA_GEMM8P_SCHED"]))
         if os.environ.get("DA_GEMM_W4") is not None:
             L.da_set_gemm_w4(int(os.environ["DA_GEMM_W4"]))
         if os.environ.get("DA_GEMM_PF") is not None:  # decode-tile register prefetch depth (A/B)
@@ -243,11 +246,11 @@ def gemm(a: torch.Tensor, w: torch.Tensor, bias=None, epi: int = EPI_NONE, resid
 # epilogue (SwiGLU, GELU, RMSNorm, split-K reductions, fp8 scales) and every decode-sized GEMM stays
 # on the hand-written kernels. Measured sustained on MI355X (profiles/gemm256_w4_r1.txt): hipBLASLt
 # 1.50-1.57 PF/s vs gemm256 1.22-1.31 at M = 32768. DA_BLAS_PREFILL=0 keeps everything on gemm256.
-_BLAS_PREFILL = os.environ.get("DA_BLAS_PREFILL", "1") != "0"
+_BLAS_PREFILL = os.environ.get("DA_BLAS_PREFILL", "0") == "1"
 # Gate/up projection on hipBLASLt + a separate SwiGLU pass (DA_BLAS_SWIGLU=1) instead of gemm256
 # with the fused epilogue: trades 1.5x the output bytes for hipBLASLt's faster main loop. Same-box
 # A/B (profiles/ab_blas_swiglu_r1.txt): +0.3% flagship; DA_BLAS_SWIGLU=0 keeps the fused gemm256.
-_BLAS_SWIGLU = os.environ.get("DA_BLAS_SWIGLU", "1") == "1"
+_BLAS_SWIGLU = os.environ.get("DA_BLAS_SWIGLU", "0") == "1"
 _BLAS_MIN_M = int(os.environ.get("DA_BLAS_MIN_M", "4096"))
 # Between 1024 rows and _BLAS_MIN_M a plain GEMM also goes to hipBLASLt when the 256x256 tile would
 # leave CUs idle (< 256 tiles, e.g. the o / down projections of a batch-1 ~2.9k-token prefill, N =

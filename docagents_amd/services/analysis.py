@@ -2,6 +2,8 @@
 
 Order kept exactly: ListChunks -> concatenate -> LLM.Summarize -> SaveSummary -> GetDocument ->
 enrich "Document: {filename}\\n\\n{chunk}" -> Embedder.EmbedBatch -> SaveEmbeddings -> status ready.
+With the engine as both embedder and vector store, EmbedBatch + SaveEmbeddings are one engine step
+(``embed_index``: vectors written into the owner shard's HBM, durably logged there).
 Extras: the chunks' decoder token ids are cached for Answer prompts when the LLM runs on this
 node, the 1:1 embedding mapping is enforced (the reference can index past the end, §5.3), and a
 permanently failed analyze marks the document ``failed`` (the reference leaves it processing).
@@ -27,14 +29,24 @@ async def handle_analyze(deps, payload: dict) -> None:
     except Exception as e:  # noqa: BLE001
         raise RuntimeError(f"failed to get document: {e}") from e
     texts = [enrich_for_embedding(doc.filename, c.text) for c in chunks]
-    try:
-        vectors = await deps.embedder.embed_batch(texts)
-    except Exception as e:  # noqa: BLE001
-        raise RuntimeError(f"failed to generate embeddings: {e}") from e
-    if len(vectors) != len(chunks):
-        raise RuntimeError(f"expected {len(chunks)} embeddings, got {len(vectors)}")
-    embs = [Embedding(c.id, v, deps.config.embedding_model) for c, v in zip(chunks, vectors)]
-    await deps.store.save_embeddings(embs)
+    if getattr(deps.store, "direct_embed", False) is True:
+        # engine embedder + engine vector shards: EmbedBatch and SaveEmbeddings in one engine step,
+        # the vectors go from the encoder straight into the owner shard's HBM (no round trip)
+        try:
+            n = await deps.store.embed_and_save(doc_id, chunks, texts, deps.config.embedding_model)
+        except Exception as e:  # noqa: BLE001
+            raise RuntimeError(f"failed to generate embeddings: {e}") from e
+        if n != len(chunks):
+            raise RuntimeError(f"expected {len(chunks)} embeddings, got {n}")
+    else:
+        try:
+            vectors = await deps.embedder.embed_batch(texts)
+        except Exception as e:  # noqa: BLE001
+            raise RuntimeError(f"failed to generate embeddings: {e}") from e
+        if len(vectors) != len(chunks):
+            raise RuntimeError(f"expected {len(chunks)} embeddings, got {len(vectors)}")
+        embs = [Embedding(c.id, v, deps.config.embedding_model) for c, v in zip(chunks, vectors)]
+        await deps.store.save_embeddings(embs)
     tok = deps.extras.get("dec_tokenizer")
     if tok is not None and chunks and hasattr(deps.store, "save_chunk_tokens"):
         enc = tok.encode_batch([c.text for c in chunks], add_special_tokens=False)

@@ -7,7 +7,10 @@ collectives over xGMI, a gloo group carries the small control messages. Rank 0 s
   TP_SIZE=1 (default)  data parallel: embeddings / generations split across ranks, index sharded
   TP_SIZE=world        the decoder is tensor-parallel across all ranks (Llama-3-70B class); every
                        rank runs every generation on its shard, index still sharded
-Index snapshot: ``--snapshot PATH`` restores each rank's shard on start and saves on SIGTERM.
+Durable shards (default): ``--index-dir DIR`` (INDEX_DIR, default DATA_DIR/index) holds each rank's
+vector log + snapshot (index/wal.py); a restarted engine recovers every row it acknowledged, after
+SIGKILL too. Checkpoints every INDEX_CHECKPOINT_S seconds and on SIGTERM. INDEX_DIR=none: HBM only.
+Legacy ``--snapshot PATH``: restore each rank's shard from PATH.shard{rank} on start, save on SIGTERM.
 """
 from __future__ import annotations
 
@@ -23,6 +26,7 @@ def main(argv=None) -> int:
     ap = argparse.ArgumentParser("engine")
     ap.add_argument("--listen", default=os.environ.get("ENGINE_LISTEN", "tcp://0.0.0.0:9090"))
     ap.add_argument("--snapshot", default=os.environ.get("INDEX_SNAPSHOT", ""))
+    ap.add_argument("--index-dir", default=None)
     a = ap.parse_args(argv)
 
     from ..config import load
@@ -51,7 +55,14 @@ def main(argv=None) -> int:
                  summary_max_new=cfg.summary_max_new_tokens, index_kind=cfg.index_kind, ivf_lists=cfg.ivf_lists,
                  ivf_probes=cfg.ivf_probes, max_seq=4096 if dev.type == "cuda" else 1024,
                  enc_dtype="fp8" if cfg.dtype == "fp8" else "bf16")
-    grp = EngineGroup(eng, info.rank, info.world, ctrl, data)
+    index_dir = a.index_dir if a.index_dir is not None else cfg.index_dir_path()
+    shard_log = None
+    if index_dir and index_dir != "none":
+        from ..index.wal import ShardLog
+        shard_log = ShardLog(index_dir, info.rank, fsync=cfg.index_fsync)
+        rec = shard_log.recover(eng.index)
+        log.info("recovered index shard", "rank", info.rank, "dir", index_dir, **rec)
+    grp = EngineGroup(eng, info.rank, info.world, ctrl, data, shard_log=shard_log)
     grp.tensor_parallel = tp is not None
     if a.snapshot and os.path.exists(f"{a.snapshot}.shard{info.rank}"):
         from ..index.snapshot import load_index
@@ -64,7 +75,8 @@ def main(argv=None) -> int:
     async def serve():
         srv = EngineServer(grp, log, max_batch_items=cfg.max_batch * 4, step_timeout_s=cfg.engine_step_timeout,
                            hard_timeout_s=cfg.engine_hard_timeout, liveness_s=cfg.engine_liveness_s,
-                           continuous=cfg.engine_continuous, cb_steps=cfg.engine_cb_steps)
+                           continuous=cfg.engine_continuous, cb_steps=cfg.engine_cb_steps,
+                           checkpoint_s=cfg.index_checkpoint_s)
         if cfg.engine_metrics_port:
             import prometheus_client
             prometheus_client.start_http_server(cfg.engine_metrics_port)
@@ -81,6 +93,9 @@ def main(argv=None) -> int:
                 pass
         await stop.wait()
         server.close()
+        if shard_log is not None:
+            await srv._gpu("checkpoint", {})
+            log.info("index checkpoint saved", "dir", index_dir)
         if a.snapshot:
             await srv._gpu("snapshot", {"path": a.snapshot})
             log.info("index snapshot saved", "path", a.snapshot)

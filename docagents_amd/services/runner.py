@@ -87,7 +87,9 @@ def _attach_tokenizer(deps):
 
 
 async def startup_sweep(deps):
-    """Re-drive documents stuck in 'processing' with no chunks (their parse task was lost)."""
+    """Re-drive documents stuck in 'processing' (their analyze task was lost), and 'ready' documents
+    whose vectors are missing from the engine's shards (e.g. an engine restarted without its
+    index directory): both get a fresh analyze task."""
     if not hasattr(deps.store, "list_documents") or deps.queue is None:
         return
     import json
@@ -101,6 +103,16 @@ async def startup_sweep(deps):
                 body = json.dumps({"document_id": d.id, "chunk_ids": [c.id for c in chunks]}).encode()
                 await enqueue_with_retry(deps.queue, Task(type=TASK_ANALYZE, payload=body), 3, 0.2)
                 deps.log.info("re-enqueued stuck document", "document_id", d.id)
+        vec = getattr(deps.store, "vectors", None)
+        if hasattr(vec, "doc_rows"):
+            have = await vec.doc_rows()
+            for d in await deps.store.list_documents("ready"):
+                chunks = await deps.store.list_chunks(d.id)
+                if chunks and have.get(d.id, 0) < len(chunks):
+                    body = json.dumps({"document_id": d.id, "chunk_ids": [c.id for c in chunks]}).encode()
+                    await enqueue_with_retry(deps.queue, Task(type=TASK_ANALYZE, payload=body), 3, 0.2)
+                    deps.log.info("re-enqueued document with missing vectors", "document_id", d.id,
+                                  "indexed", have.get(d.id, 0), "chunks", len(chunks))
     except Exception as e:  # noqa: BLE001
         deps.log.warn("startup sweep failed", "err", e)
 

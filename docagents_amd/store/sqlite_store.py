@@ -89,10 +89,14 @@ def _parse_ts(s):
 class CompositeStore:
     """Store implementation: SQLite metadata + a vector backend (see vectors.py)."""
 
-    def __init__(self, meta: SqliteMeta, vectors, min_similarity: float = 0.7, dec_tokenizer=None):
+    def __init__(self, meta: SqliteMeta, vectors, min_similarity: float = 0.7, dec_tokenizer=None,
+                 direct_embed: bool = False):
         self.meta, self.vectors = meta, vectors
         self.min_similarity = min_similarity
         self.dec_tokenizer = dec_tokenizer
+        # the embedder and the vector shards are the same engine: EmbedBatch + SaveEmbeddings run as
+        # one engine step that writes the rows into HBM directly (embed_and_save)
+        self.direct_embed = direct_embed and hasattr(vectors, "embed_index")
 
     async def _run(self, fn, *a):
         return await asyncio.to_thread(fn, *a)
@@ -212,6 +216,19 @@ class CompositeStore:
                     "model=excluded.model, dim=excluded.dim",
                     [(e.chunk_id, e.model, int(np.asarray(e.vector).shape[-1])) for e in embs])
         await self._run(f)
+
+    async def embed_and_save(self, doc_id: str, chunks: list[Chunk], texts: list[str], model: str) -> int:
+        """EmbedBatch + SaveEmbeddings in one engine call (the vectors are written into the owner
+        shard's HBM, durably logged there); records the embeddings metadata rows here."""
+        rows, dim = await self.vectors.embed_index(doc_id, np.asarray([c.key for c in chunks], dtype=np.int64), texts)
+
+        def f():
+            with self.meta.lock:
+                self.meta.conn.executemany(
+                    "INSERT INTO embeddings(chunk_id, model, dim) VALUES(?,?,?) ON CONFLICT(chunk_id) DO UPDATE SET "
+                    "model=excluded.model, dim=excluded.dim", [(c.id, model, dim) for c in chunks])
+        await self._run(f)
+        return rows
 
     async def top_k(self, doc_ids: list[str], vector, k: int, min_similarity: float | None = None) -> list[SearchResult]:
         thr = self.min_similarity if min_similarity is None else min_similarity

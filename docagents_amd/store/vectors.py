@@ -56,3 +56,14 @@ class EngineVectors:
 
     async def remove_doc(self, doc_id: str):
         return await self.client.call("index_remove", doc_id=doc_id)
+
+    async def embed_index(self, doc_id: str, keys: np.ndarray, texts: list[str]) -> tuple[int, int]:
+        """Embed ``texts`` on the engine and write the rows straight into the owner shard (no vector
+        bytes leave the GPU). Returns (rows written, dim)."""
+        r = await self.client.call("embed_index", doc_id=doc_id, keys=np.asarray(keys, dtype=np.int64),
+                                   texts=list(texts))
+        return int(r["rows"]), int(r["dim"])
+
+    async def doc_rows(self) -> dict[str, int]:
+        """{document id: indexed rows} over every shard (startup sweep)."""
+        return dict(await self.client.call("index_docs"))
