@@ -1,4 +1,4 @@
-"""Prefill attention microbenchmark: flash v1 vs v2 vs torch SDPA on MI355X shapes."""
+"""Prefill attention microbenchmark: flash_attn_v2 (4- and 8-wave workgroups) vs torch SDPA on MI355X shapes."""
 import argparse
 import os
 import sys
@@ -41,21 +41,19 @@ def main():
         cu = torch.arange(0, T + 1, L, device=dev, dtype=torch.int32)
         fl = 4 * B * L * L * H * D * (0.5 if causal else 1.0)
         r = {}
-        for impl in ("v1", "v2", "v2w8"):
-            if impl == "v1" and D == 32:
-                continue
+        for impl in ("v2", "v2w8"):
             K.lib().da_set_flash_waves(8 if impl == "v2w8" else 4)
-            t = timeit(lambda: K.flash_attn_varlen(q, k, v, cu, L, H, Hkv, D, causal, impl=impl[:2]))
+            t = timeit(lambda: K.flash_attn_varlen(q, k, v, cu, L, H, Hkv, D, causal))
             r[impl + "_ms"], r[impl + "_tflops"] = t, fl / t / 1e9
         K.lib().da_set_flash_waves(8)
-        o8 = K.flash_attn_varlen(q, k, v, cu, L, H, Hkv, D, causal, impl="v2").float()
+        o8 = K.flash_attn_varlen(q, k, v, cu, L, H, Hkv, D, causal).float()
         K.lib().da_set_flash_waves(0)
         qq = q.reshape(B, L, H, D).transpose(1, 2)
         kk = k.reshape(B, L, Hkv, D).transpose(1, 2).repeat_interleave(H // Hkv, 1)
         vv = v.reshape(B, L, Hkv, D).transpose(1, 2).repeat_interleave(H // Hkv, 1)
         t = timeit(lambda: torch.nn.functional.scaled_dot_product_attention(qq, kk, vv, is_causal=causal))
         r["sdpa_ms"], r["sdpa_tflops"] = t, fl / t / 1e9
-        o1 = K.flash_attn_varlen(q, k, v, cu, L, H, Hkv, D, causal, impl="v2").float()
+        o1 = K.flash_attn_varlen(q, k, v, cu, L, H, Hkv, D, causal).float()
         o2 = torch.nn.functional.scaled_dot_product_attention(qq, kk, vv, is_causal=causal)
         o2 = o2.transpose(1, 2).reshape(T, H * D).float()
         r["max_err_vs_sdpa"] = (o1 - o2).abs().max().item()

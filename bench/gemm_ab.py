@@ -25,9 +25,7 @@ def call(arm, x, w, out, epi, bias=None, resid=None):
         if epi == K.EPI_SWIGLU:
             return K.swiglu_interleaved(torch.mm(x, w.t()), out)
         return torch.mm(x, w.t(), out=out)
-    tile, _, sched = arm.partition(":")
-    if sched:
-        K.lib().da_set_gemm8p_sched(int(sched))
+    tile = arm
     return K.gemm(x, w, bias=bias, epi=epi, resid=resid, out=out, tile=int(tile), splits=1)
 
 
@@ -87,10 +85,13 @@ def rate(fn, flop):
 def perf():
     shapes = [(32768, 9216, 3072, "none"), (32768, 16384, 3072, "swiglu"), (32768, 3072, 8192, "none"),
               (32768, 3072, 3072, "none"), (8192, 8192, 8192, "none"), (29440, 9216, 3072, "none"),
-              (65536, 768, 3072, "none"), (65536, 3072, 768, "none")]
+              (65536, 768, 3072, "none"), (65536, 3072, 768, "none"),
+              # batch-1 prefill (~2.9k tokens): 256-row tiles underfill the chip at N = 3072
+              (2930, 3072, 3072, "none"), (2930, 3072, 8192, "none"), (2930, 9216, 3072, "none"),
+              (2930, 16384, 3072, "swiglu"), (512, 9216, 3072, "none"), (256, 9216, 3072, "none")]
     only = os.environ.get("SHAPES")
     if only:
-        shapes = [s for i, s in enumerate(shapes) if str(i) in only.split(",")]
+        shapes = [shapes[int(i)] for i in only.split(",")]
     for (M, N, Kd, epi) in shapes:
         x = (torch.rand(M, Kd, device="cuda") * 2 - 1).bfloat16()
         w = ((torch.rand(N, Kd, device="cuda") * 2 - 1) * Kd ** -0.5).bfloat16()

@@ -1,6 +1,6 @@
 """One prefill-shaped GEMM repeated (for rocprofv3 counter collection).
 
-python bench/gemm_one.py [M N K]; env ARM = tile[:sched] of the in-tree kernel (default 7) or "blas"."""
+python bench/gemm_one.py [M N K]; env ARM = tile id of the in-tree kernel (default 7 = gemm8p) or "blas"."""
 import os
 import sys
 
@@ -14,9 +14,7 @@ arm = os.environ.get("ARM", "7")
 x = (torch.rand(M, Kd, device="cuda") * 2 - 1).bfloat16()
 w = ((torch.rand(N, Kd, device="cuda") * 2 - 1) * Kd ** -0.5).bfloat16()
 out = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
-tile, _, sched = arm.partition(":")
-if sched:
-    K.lib().da_set_gemm8p_sched(int(sched))
+tile = arm
 for _ in range(5):
     if arm == "blas":
         torch.mm(x, w.t(), out=out)

@@ -10,7 +10,8 @@ upload -> poll summary -> query), through the gateway:
   3. cache-hit queries: the same questions again -> p50/p99 (served from the query cache; the
      reference promises "sub-millisecond" server-side, README.md:588).
 
-``--spawn`` starts an all-in-one stack (``python -m docagents_amd.services all``) on a free port
+``--spawn`` starts the multi-process deploy.py stack (``--topology deploy``, default) or the all-in-one
+process (``--topology all``) on free ports
 with the current environment (``LLM_PROVIDER=stub`` on CPU, ``engine`` with ``ENGINE_URL`` set for
 the GPU engine); otherwise ``--gateway URL`` targets a running deployment. Prints one JSON line.
 """
@@ -39,6 +40,28 @@ def _pct(xs, q):
         return None
     xs = sorted(xs)
     return xs[min(len(xs) - 1, int(round(q / 100.0 * (len(xs) - 1))))]
+
+
+def _free_block(n: int = 40) -> int:
+    """A base port with [base, base + n) free (the deploy topology's port plan)."""
+    for _ in range(50):
+        base = _free_port()
+        if base + n >= 65000:
+            continue
+        ok = True
+        for p in range(base, base + n):
+            t = socket.socket()
+            try:
+                t.bind(("127.0.0.1", p))
+            except OSError:
+                ok = False
+            finally:
+                t.close()
+            if not ok:
+                break
+        if ok:
+            return base
+    raise RuntimeError("no free port block")
 
 
 def _free_port() -> int:
@@ -183,7 +206,11 @@ def _r(x):
 def main(argv=None):
     ap = argparse.ArgumentParser("loadgen")
     ap.add_argument("--gateway", default="")
-    ap.add_argument("--spawn", action="store_true", help="start `services all` for the run")
+    ap.add_argument("--spawn", action="store_true", help="start a stack for the run (see --topology)")
+    ap.add_argument("--topology", default="deploy", choices=["deploy", "all"],
+                    help="deploy: the compose-equivalent multi-process stack (native broker + KV cache, engine "
+                         "server when LLM_PROVIDER=engine, query, gateway, 2 parsers, 2 analyzers); all: every "
+                         "agent in one process with the in-process bus")
     ap.add_argument("--docs", type=int, default=32)
     ap.add_argument("--words", type=int, default=2000)
     ap.add_argument("--queries", type=int, default=64)
@@ -194,24 +221,37 @@ def main(argv=None):
     a = ap.parse_args(argv)
     proc = None
     gw = a.gateway
+    sup_log = None
     if a.spawn or not gw:
-        port = _free_port()
+        port = _free_port() if a.topology == "all" else _free_block()
         root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
         env = dict(os.environ, PORT=str(port),
                    PYTHONPATH=os.pathsep.join(x for x in (root, os.environ.get("PYTHONPATH", "")) if x))
         env.setdefault("MIN_SIMILARITY", "-1")
-        env.setdefault("DB_PATH", os.path.join(os.environ.get("TMPDIR", "/tmp"), f"loadgen-{port}.sqlite3"))
-        proc = subprocess.Popen([sys.executable, "-m", "docagents_amd.services", "all"], env=env,
-                                stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
+        tmp = os.environ.get("TMPDIR", "/tmp")
+        env.setdefault("DB_PATH", os.path.join(tmp, f"loadgen-{port}.sqlite3"))
+        if a.topology == "all":
+            proc = subprocess.Popen([sys.executable, "-m", "docagents_amd.services", "all"], env=env,
+                                    stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
+        else:
+            env.setdefault("QUEUE_URL", f"nats://127.0.0.1:{port + 30}")
+            env.setdefault("REDIS_ADDR", f"127.0.0.1:{port + 31}")
+            env.setdefault("ENGINE_URL", f"tcp://127.0.0.1:{port + 32}")
+            env.setdefault("DATA_DIR", os.path.join(tmp, f"loadgen-{port}"))
+            sup_log = os.path.join(tmp, f"loadgen-{port}-logs")
+            proc = subprocess.Popen([sys.executable, "-m", "docagents_amd.deploy", "--base-port", str(port),
+                                     "--log-dir", sup_log], env=env, stdout=subprocess.DEVNULL,
+                                    stderr=subprocess.DEVNULL, start_new_session=True)
         gw = f"http://127.0.0.1:{port}"
     try:
         qurl = f"http://127.0.0.1:{int(gw.rsplit(':', 1)[1]) + 1}/api/query" if proc is not None else a.query_url
         out = asyncio.run(run(gw, a.docs, a.words, a.queries, a.concurrency, a.top_k, a.seed, query_url=qurl))
+        out["topology"] = a.topology if proc is not None else "external"
     finally:
         if proc is not None:
             proc.terminate()
             try:
-                proc.wait(10)
+                proc.wait(120 if sup_log else 10)
             except subprocess.TimeoutExpired:
                 proc.kill()
     print(json.dumps(out), flush=True)

@@ -41,6 +41,15 @@ def _ext_hook(code, data):
     return msgpack.ExtType(code, data)
 
 
+def dumps(obj) -> bytes:
+    """msgpack with numpy arrays as ext type 1 (the engine's data-plane payload encoding)."""
+    return msgpack.packb(obj, default=_default, use_bin_type=True)
+
+
+def loads(b: bytes):
+    return msgpack.unpackb(b, ext_hook=_ext_hook, raw=False, strict_map_key=False)
+
+
 def pack(obj) -> bytes:
     b = msgpack.packb(obj, default=_default, use_bin_type=True)
     return struct.pack(">I", len(b)) + b

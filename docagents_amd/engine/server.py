@@ -60,14 +60,16 @@ class EngineGroup:
         return lst[0]
 
     def _gather(self, obj):
+        """Every rank's ``obj`` (msgpack-encoded) gathered as tensors over the data group (RCCL on GPU
+        ranks): answers, summaries, stats. Embeddings and search results use typed tensor gathers."""
         if self.world == 1:
             return [obj]
-        import torch.distributed as dist
-        out = [None] * self.world
+        from ..parallel.dist import all_gather_bytes
+        from .rpc import dumps, loads
         t0 = time.perf_counter()
-        dist.all_gather_object(out, obj, group=self.ctrl_group)
-        metrics.ENGINE_COLLECTIVE.labels("all_gather_object").inc(time.perf_counter() - t0)
-        return out
+        parts = all_gather_bytes(dumps(obj), self.engine.device, self.data_group)
+        metrics.ENGINE_COLLECTIVE.labels("all_gather_bytes").inc(time.perf_counter() - t0)
+        return [loads(p) for p in parts]
 
     def run(self, cmd: str, args: dict):
         """Rank 0: broadcast the command, execute collectively, return rank 0's result."""
@@ -97,9 +99,13 @@ class EngineGroup:
             texts = a["texts"]
             lo, hi = self._slice(len(texts))
             faults.maybe_fail("engine.embed")
-            v = e.embed(texts[lo:hi], a.get("preprocess", True), out_dtype=torch.float32).cpu().numpy()
-            parts = self._gather(v)
-            return np.concatenate(parts, axis=0) if parts else v
+            v = e.embed(texts[lo:hi], a.get("preprocess", True), out_dtype=torch.float32)
+            if self.world > 1:  # the slices as one tensor all-gather (RCCL on GPU ranks)
+                from ..parallel.dist import all_gather_padded_rows
+                t0 = time.perf_counter()
+                v = all_gather_padded_rows(v, len(texts), self.data_group)
+                metrics.ENGINE_COLLECTIVE.labels("embed_all_gather").inc(time.perf_counter() - t0)
+            return v.cpu().numpy()
         if cmd in ("answer", "summarize"):
             items = a["items"]
             # tensor-parallel decoder: every rank runs every generation on its weight shard
@@ -149,10 +155,13 @@ class EngineGroup:
                     self._put(doc_id, np.asarray(keys, dtype=np.int64), v[o:o + len(ts)])
                     counts[doc_id] = len(ts)
                     o += len(ts)
-            merged = {}
-            for part in self._gather(counts):
-                merged.update(part)
-            return [merged.get(it[0], 0) for it in a["items"]]
+            n = torch.tensor([counts.get(it[0], 0) for it in a["items"]], dtype=torch.int64)
+            if self.world > 1:  # each document has one owner: the sum is its row count
+                import torch.distributed as dist
+                dev = e.device if dist.get_backend(self.data_group) != "gloo" else torch.device("cpu")
+                n = n.to(dev)
+                dist.all_reduce(n, group=self.data_group)
+            return [int(x) for x in n.cpu().tolist()]
         if cmd == "index_remove":
             if self.shard_log is not None:
                 n = self.shard_log.remove(e.index, a["doc_id"])
@@ -212,12 +221,12 @@ class EngineGroup:
         dist.broadcast(q, src=0, group=self.data_group)                     # C2 (broadcast form)
         s, rows = e.index.search(q, k, thr, filters)
         gid = e.index.gather_ids(rows)
-        S = torch.empty((self.world * Q, k), dtype=s.dtype, device=dev)
-        G = torch.empty((self.world * Q, k), dtype=gid.dtype, device=dev)
+        # C1: scores (fp32 bits) and ids packed into ONE int64 buffer -> one all-gather per search
+        from ..parallel.dist import all_gather_rows, pack_scores_ids, unpack_scores_ids
         t1 = time.perf_counter()
-        dist.all_gather_into_tensor(S, s.contiguous(), group=self.data_group)    # C1
-        dist.all_gather_into_tensor(G, gid.contiguous(), group=self.data_group)
+        P = all_gather_rows(pack_scores_ids(s, gid), self.data_group)
         metrics.ENGINE_COLLECTIVE.labels("search_all_gather").inc(time.perf_counter() - t1)
+        S, G = unpack_scores_ids(P)
         flatS = S.view(self.world, Q, k).permute(1, 0, 2).reshape(Q, -1)
         flatG = G.view(self.world, Q, k).permute(1, 0, 2).reshape(Q, -1)
         flatS = torch.where(flatG >= 0, flatS, torch.full_like(flatS, float("-inf")))

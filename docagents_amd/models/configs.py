@@ -78,6 +78,10 @@ DECODERS = {
                                 ffn=28672, max_pos=8192, rope_theta=500000.0),
     "tiny-dec": DecoderConfig("tiny-dec", vocab=32064, hidden=256, layers=2, heads=4, kv_heads=2, ffn=512,
                               max_pos=4096, rope_theta=10000.0),
+    # Llama-3-70B's TP=8 layout in miniature: 8 KV heads (one per rank), GQA group 2, FFN / vocab
+    # divisible by 8 ranks (distributed tests)
+    "tiny-dec-tp8": DecoderConfig("tiny-dec-tp8", vocab=32064, hidden=512, layers=2, heads=16, kv_heads=8,
+                                  ffn=1024, max_pos=4096, rope_theta=500000.0),
 }
 
 ALIASES = {"text-embedding-3-large": "bge-large", "text-embedding-3-small": "bge-base",

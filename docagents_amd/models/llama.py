@@ -5,7 +5,8 @@ N6-N8). Per layer (hidden state x is the residual stream, updated in place):
 
     h   = RMSNorm(x)                                   rmsnorm kernel
     qkv = h @ Wqkv^T                                   MFMA GEMM   (column-parallel: local heads)
-    RoPE(q, k) + write k, v to the KV cache            rope_cache kernel
+    RoPE(q, k) + write k, v to the KV cache            prefill: the GEMM's epilogue; decode: the
+                                                       attention kernel (MHA) / rope_cache (GQA)
     a   = attention(q, K, V)                           varlen flash prefill / split-KV decode
     x   = x + a @ Wo^T                                 GEMM + fused residual epilogue (row-parallel
                                                        -> RCCL all-reduce over xGMI when TP > 1)
@@ -78,6 +79,15 @@ class TPContext:
         from ..parallel.dist import all_gather_rows
         out = all_gather_rows(t.contiguous(), self.group)
         return out.view(self.size, t.shape[0], -1).permute(1, 0, 2).reshape(t.shape[0], -1)
+
+
+def to_interleaved_rope(wqkv: torch.Tensor, H: int, Hkv: int, D: int) -> torch.Tensor:
+    """Convert an HF (rotate_half: pairs (i, i + D/2)) QKV weight to this engine's interleaved RoPE
+    layout (pairs (2i, 2i + 1)) by permuting the rows of every q and k head; v rows are unchanged.
+    q.k is invariant under the same permutation of both, so attention outputs are identical."""
+    perm = torch.stack([torch.arange(D // 2), torch.arange(D // 2) + D // 2], dim=1).flatten()
+    qk = wqkv[:(H + Hkv) * D].view(H + Hkv, D, -1)[:, perm.to(wqkv.device)].reshape((H + Hkv) * D, -1)
+    return torch.cat([qk, wqkv[(H + Hkv) * D:]]).contiguous()
 
 
 def _randn(shape, gen, device, std=0.02):
@@ -229,8 +239,8 @@ class LlamaDecoder:
         x = o.embed(ids, self.w["embed"])
         for li, L in enumerate(self.w["layers"]):
             h = o.rmsnorm(x, L["ln_attn"], c.eps)
-            qkv = o.gemm(h, L["wqkv"])
-            o.rope_cache(qkv, pos, self.cos_sin, hl, kl, D, slot=slot_tok, k_cache=cache.k(li), v_cache=cache.v(li))
+            # QKV projection + RoPE + KV-cache write in one kernel (gemm8p EPI_ROPE epilogue)
+            qkv = o.gemm_rope(h, L["wqkv"], pos, self.cos_sin, hl, kl, D, slot_tok, cache.k(li), cache.v(li))
             pre = None if prefix is None else (cache.k(li)[prefix[0]], cache.v(li)[prefix[0]], prefix[1])
             a = o.flash_attn_varlen(qkv[:, :hl * D], qkv[:, hl * D:(hl + kl) * D], qkv[:, (hl + kl) * D:], cu,
                                     max_seqlen, hl, kl, D, causal=True, prefix=pre)

@@ -57,15 +57,31 @@ def binary(name: str) -> Path:
     return build(name)[name]
 
 
+def _run_child(cmd: list[str]) -> int:
+    """Run a native server as a child process and return its exit code (forwarding SIGINT/SIGTERM).
+    The Python process is never replaced by the binary (no exec)."""
+    import signal
+    p = subprocess.Popen(cmd)
+
+    def fwd(sig, _frame):
+        if p.poll() is None:
+            p.send_signal(sig)
+    old = {s: signal.signal(s, fwd) for s in (signal.SIGINT, signal.SIGTERM)}
+    try:
+        return p.wait()
+    finally:
+        for s, h in old.items():
+            signal.signal(s, h)
+
+
 def run_broker(args: list[str]) -> int:
-    """Exec the broker (CPU-only process: never touches the GPU)."""
+    """Run the broker (CPU-only process: never touches the GPU)."""
     from ..config import load
     exe = str(binary("da-broker"))
     if not any(a.startswith("--listen") for a in args):
         url = load().queue_url or "nats://0.0.0.0:4222"
         args = ["--listen", url] + args
-    os.execv(exe, [exe, *args])
-    return 0
+    return _run_child([exe, *args])
 
 
 def run_kvserver(args: list[str]) -> int:
@@ -76,8 +92,7 @@ def run_kvserver(args: list[str]) -> int:
         args = ["--listen", cfg.redis_addr.replace("localhost", "0.0.0.0")] + args
     if cfg.redis_password and "--requirepass" not in args:
         args += ["--requirepass", cfg.redis_password]
-    os.execv(exe, [exe, *args])
-    return 0
+    return _run_child([exe, *args])
 
 
 _TEXT = None

@@ -1,156 +1,14 @@
 // Attention kernels for gfx950.
 //
-// 1) flash_attn_varlen: packed (varlen) prefill attention, bidirectional (BERT encoder, SURVEY
-//    §2.4 N1) or causal with GQA (Llama-3 / Phi-3 prefill, N6/N7). Online softmax in fp32, bf16
-//    MFMA (v_mfma_f32_16x16x32_bf16). "Swapped" formulation (cdna_hip_programming.md T12 / §3):
-//    S^T = K·Q^T puts the query on the MFMA lane, so every softmax statistic and the O^T rescale
-//    are lane-local, and the S^T accumulator registers ARE the B operand of O^T += V^T·P^T once
-//    the k index is permuted consistently on both operands (no LDS round trip for P).
-//    One workgroup = 4 waves x 16 queries; K tile in LDS with a 16-B row pad (conflict-free
-//    ds_read_b128), V tile stored transposed in LDS for the V^T operand.
+// 1) flash_attn_v2: packed (varlen) prefill attention, bidirectional (BERT encoder)
+//    or causal with GQA (Llama-3 / Phi-3 prefill, N6/N7), optionally over a shared-prefix head in
+//    the KV cache. Online softmax in fp32, bf16 MFMA 32x32x16, "swapped" S^T = K.Q^T formulation
+//    (details above the kernel).
 //
 // 2) decode attention (one new token per sequence) over the KV cache [slot, Hkv, max_seq, D]:
 //    split-KV ("flash-decoding") so a batch of long contexts fills all 256 CUs; fp32 partials
 //    (unnormalised O, running max, running sum) merged by decode_combine.
 #include "common.h"
-
-template <int D>
-__global__ void __launch_bounds__(256)
-flash_attn_varlen_kernel(const bf16_t* __restrict__ q, const bf16_t* __restrict__ k, const bf16_t* __restrict__ v,
-                         int ldq, int ldk, int ldv, const int* __restrict__ cu, int H, int Hkv, int causal,
-                         float scale_log2e, bf16_t* __restrict__ o, int ldo) {
-  constexpr int KT = 64;                 // keys per tile
-  constexpr int KSTR = D * 2 + 16;       // K row stride (bytes) in LDS
-  constexpr int VSTR = KT * 2 + 8;       // V^T row stride (bytes)
-  constexpr int NKK = D / 32;            // k-steps for S (over d)
-  constexpr int NDT = D / 16;            // d tiles for O
-  constexpr int CPR = D / 8;             // 16-B chunks per row
-  __shared__ __attribute__((aligned(16))) char sK[KT * KSTR];
-  __shared__ __attribute__((aligned(16))) char sVt[D * VSTR];
-
-  const int b = blockIdx.z, h = blockIdx.y;
-  const int s0 = cu[b], L = cu[b + 1] - s0;
-  const int q0 = blockIdx.x * 64;
-  if (q0 >= L) return;
-  const int hk = h / (H / Hkv);
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int fr = lane & 15, fg = lane >> 4;
-  const int qi = q0 + wid * 16 + fr;  // this lane's query (MFMA column)
-  const bool qvalid = qi < L;
-
-  bf16x8_t qf[NKK];
-#pragma unroll
-  for (int kk = 0; kk < NKK; ++kk) {
-    if (qvalid) qf[kk] = *(const bf16x8_t*)(q + (size_t)(s0 + qi) * ldq + h * D + kk * 32 + fg * 8);
-    else qf[kk] = bf16x8_t{0, 0, 0, 0, 0, 0, 0, 0};
-  }
-
-  f32x4_t oacc[NDT];
-#pragma unroll
-  for (int i = 0; i < NDT; ++i) oacc[i] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-  float m_run = -INFINITY, l_part = 0.f;
-
-  const int kv_end = causal ? min(L, q0 + 64) : L;
-  const int ntiles = (kv_end + KT - 1) / KT;
-  for (int kt = 0; kt < ntiles; ++kt) {
-    const int kbase = kt * KT;
-    // ---- stage K (row-major, padded) and V^T into LDS ----
-    for (int idx = tid; idx < KT * CPR; idx += 256) {
-      const int r = idx / CPR, c = idx % CPR;
-      const int key = kbase + r;
-      u32x4_t kvv = u32x4_t{0, 0, 0, 0}, vvv = u32x4_t{0, 0, 0, 0};
-      if (key < L) {
-        kvv = *(const u32x4_t*)(k + (size_t)(s0 + key) * ldk + hk * D + c * 8);
-        vvv = *(const u32x4_t*)(v + (size_t)(s0 + key) * ldv + hk * D + c * 8);
-      }
-      *(u32x4_t*)(sK + r * KSTR + c * 16) = kvv;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        *(bf16_t*)(sVt + (c * 8 + 2 * e) * VSTR + r * 2) = (bf16_t)(vvv[e] & 0xffff);
-        *(bf16_t*)(sVt + (c * 8 + 2 * e + 1) * VSTR + r * 2) = (bf16_t)(vvv[e] >> 16);
-      }
-    }
-    __syncthreads();
-
-    // ---- S^T[key][q] for 4 key tiles of 16 ----
-    f32x4_t sacc[4];
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      sacc[t] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int kk = 0; kk < NKK; ++kk) {
-        const bf16x8_t a = *(const bf16x8_t*)(sK + (t * 16 + fr) * KSTR + kk * 64 + fg * 16);
-        sacc[t] = mfma16(a, qf[kk], sacc[t]);
-      }
-    }
-    // ---- mask + online softmax (per query = per lane column) ----
-    float tmax = -INFINITY;
-#pragma unroll
-    for (int t = 0; t < 4; ++t)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int key = kbase + t * 16 + fg * 4 + i;
-        float s = sacc[t][i] * scale_log2e;
-        if (key >= L || (causal && key > qi)) s = -INFINITY;
-        sacc[t][i] = s;
-        tmax = fmaxf(tmax, s);
-      }
-    tmax = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
-    tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
-    const float m_new = fmaxf(m_run, tmax);
-    const float m_use = (m_new == -INFINITY) ? 0.f : m_new;
-    const float alpha = exp2f(m_run - m_use);
-    m_run = m_new;
-    float psum = 0.f;
-#pragma unroll
-    for (int t = 0; t < 4; ++t)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const float p = exp2f(sacc[t][i] - m_use);
-        sacc[t][i] = p;
-        psum += p;
-      }
-    l_part = l_part * alpha + psum;
-#pragma unroll
-    for (int i = 0; i < NDT; ++i) oacc[i] *= alpha;
-
-    // ---- O^T[d][q] += V^T[d][key] · P^T[key][q]; k permuted: j -> key 32c + 16(j>>2) + 4g + (j&3) ----
-#pragma unroll
-    for (int c = 0; c < 2; ++c) {
-      bf16x8_t pb;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        pb[j] = (short)f2bf(sacc[2 * c][j]);
-        pb[4 + j] = (short)f2bf(sacc[2 * c + 1][j]);
-      }
-#pragma unroll
-      for (int dt = 0; dt < NDT; ++dt) {
-        const char* rowp = sVt + (dt * 16 + fr) * VSTR;
-        const u32x2_t lo = *(const u32x2_t*)(rowp + (32 * c + 4 * fg) * 2);
-        const u32x2_t hi = *(const u32x2_t*)(rowp + (32 * c + 16 + 4 * fg) * 2);
-        bf16x8_t va;
-        va[0] = (short)(lo[0] & 0xffff); va[1] = (short)(lo[0] >> 16);
-        va[2] = (short)(lo[1] & 0xffff); va[3] = (short)(lo[1] >> 16);
-        va[4] = (short)(hi[0] & 0xffff); va[5] = (short)(hi[0] >> 16);
-        va[6] = (short)(hi[1] & 0xffff); va[7] = (short)(hi[1] >> 16);
-        oacc[dt] = mfma16(va, pb, oacc[dt]);
-      }
-    }
-    __syncthreads();
-  }
-
-  float l_tot = l_part + __shfl_xor(l_part, 16, 64);
-  l_tot += __shfl_xor(l_tot, 32, 64);
-  const float inv = l_tot > 0.f ? 1.f / l_tot : 0.f;
-  if (qvalid) {
-    bf16_t* orow = o + (size_t)(s0 + qi) * ldo + h * D;
-#pragma unroll
-    for (int dt = 0; dt < NDT; ++dt) {
-      *(u32x2_t*)(orow + dt * 16 + fg * 4) =
-          u32x2_t{pack_bf2(oacc[dt][0] * inv, oacc[dt][1] * inv), pack_bf2(oacc[dt][2] * inv, oacc[dt][3] * inv)};
-    }
-  }
-}
 
 // ------------------------------------------------------------------------------------------
 // flash_attn_v2: 32x32x16 MFMA, 4 waves x 32 queries (128 queries per workgroup), 64-key tiles
@@ -497,14 +355,14 @@ decode_attn_kernel(const bf16_t* __restrict__ q, int ldq, const bf16_t* __restri
   DA_ASSERT(!fr || rope.pos[b] == L - 1);
   __shared__ float skn[D], svn[D], ssn[G];
 
-  // RoPE (rotate-half pairs (i, i + D/2)) of one element of a head row, rounded to bf16 like the
-  // rope_cache kernel that this path replaces
+  // RoPE (interleaved pairs (2i, 2i+1)) of one element of a head row, rounded to bf16 like the
+  // rope_cache kernel / the QKV GEMM epilogue that this path replaces
   auto rot = [&](const bf16_t* hp, int d, int p) -> float {
     constexpr int HALF = D / 2;
-    const int i = d % HALF;
-    const float x1 = bf2f(hp[i]), x2 = bf2f(hp[i + HALF]);
+    const int i = d >> 1;
+    const float x1 = bf2f(hp[d & ~1]), x2 = bf2f(hp[d | 1]);
     const float c = rope.cs[((size_t)p * HALF + i) * 2], sn = rope.cs[((size_t)p * HALF + i) * 2 + 1];
-    return bf2f(f2bf(d < HALF ? x1 * c - x2 * sn : x2 * c + x1 * sn));
+    return bf2f(f2bf((d & 1) ? x2 * c + x1 * sn : x1 * c - x2 * sn));
   };
   for (int i = tid; i < G * D; i += 256) {
     const int g = i / D, d = i % D;
@@ -904,27 +762,6 @@ __global__ void decode_combine_kernel(const float* __restrict__ po, const float*
     for (int s = 0; s < nsplit; ++s) acc += po[(base + s) * D + d] * exp2f(pm[base + s] - Mu);
     o[(size_t)b * ldo + h * D + d] = f2bf(acc * inv);
   }
-}
-
-DA_EXPORT int da_flash_attn_varlen(const void* q, const void* k, const void* v, int ldq, int ldk, int ldv,
-                                   const void* cu_seqlens, int B, int max_seqlen, int H, int Hkv, int D, int causal,
-                                   float scale, void* o, int ldo, void* stream) {
-  if (H % Hkv || ldq % 8 || ldk % 8 || ldv % 8 || ldo % 4) return (int)hipErrorInvalidValue;
-  if (B == 0 || max_seqlen == 0) return 0;
-  dim3 grid((max_seqlen + 63) / 64, H, B);
-  const float sl2e = scale * 1.4426950408889634f;
-  hipStream_t s = (hipStream_t)stream;
-#define FA_ARGS (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, ldq, ldk, ldv, (const int*)cu_seqlens, H, Hkv, \
-                causal, sl2e, (bf16_t*)o, ldo
-  switch (D) {
-    case 32: flash_attn_varlen_kernel<32><<<grid, 256, 0, s>>>(FA_ARGS); break;
-    case 64: flash_attn_varlen_kernel<64><<<grid, 256, 0, s>>>(FA_ARGS); break;
-    case 96: flash_attn_varlen_kernel<96><<<grid, 256, 0, s>>>(FA_ARGS); break;
-    case 128: flash_attn_varlen_kernel<128><<<grid, 256, 0, s>>>(FA_ARGS); break;
-    default: return (int)hipErrorInvalidValue;
-  }
-#undef FA_ARGS
-  DA_LAUNCH_CHECK();
 }
 
 template <int D, int VAR>

@@ -9,6 +9,15 @@ enum Epi : int {
   EPI_SWIGLU = 3,     // W rows interleaved in 16-row (gate, up) groups; out N/2 = silu(g)*u
   EPI_RESID = 4,      // bias (optional) + residual add
   EPI_PARTIAL = 5,    // fp32 split-K partial to workspace
+  EPI_ROPE = 6,       // QKV projection: RoPE (interleaved pairs) on q / k, k / v written to the KV cache
+};
+
+// EPI_ROPE operands: output columns [H q heads | Hkv k heads | Hkv v heads] of D; token row m goes to
+// cache slot slot[m] at position pos[m] (caches [slots, Hkv, max_seq, D]); cs = [max_pos, D/2, 2].
+struct RopeArgs {
+  const int* pos; const int* slot; const float* cs;
+  bf16_t* kc; bf16_t* vc;
+  int H, Hkv, D, max_seq;
 };
 
 struct GemmArgs {
@@ -17,12 +26,11 @@ struct GemmArgs {
   int M, N, K, lda, ldc, ldr, k_per_split;
   const float* sa; const float* sw;  // fp8 path: per-row (A) and per-output-channel (W) scales
   const bf16_t* gamma; float eps;    // GEMV only: fused RMSNorm of the input row (gamma != null)
+  RopeArgs rope;                     // EPI_ROPE only
 };
 
-// large-tile (256x256, 8 waves, LDS-DMA staged) path; returns hipError_t.
-// fp8 = 1: A and W hold OCP e4m3 bytes (lda / K in elements = bytes), C = (A.W^T) * sa[m] * sw[n].
-int launch_gemm256(const GemmArgs& a, int epi, hipStream_t s, int fp8 = 0);
-// 4-wave 256x256 bf16 variant (gemm256w4.hip); K % 32 == 0
-int launch_gemm256w4(const GemmArgs& a, int epi, hipStream_t s);
-// phase-split 256x256 bf16 kernel (gemm8p.hip); K % 64 == 0, K >= 128
-int launch_gemm8p(const GemmArgs& a, int epi, hipStream_t s);
+// 256x256 fp8 tile (gemm256.hip): A and W hold OCP e4m3 bytes (lda / K in elements = bytes),
+// C = (A.W^T) * sa[m] * sw[n]; returns hipError_t.
+int launch_gemm256(const GemmArgs& a, int epi, hipStream_t s, int fp8 = 1);
+// phase-split BMx256 bf16 kernel (gemm8p.hip), bm = 256 or 128; K % 64 == 0, K >= 128
+int launch_gemm8p(const GemmArgs& a, int epi, hipStream_t s, int bm = 256);

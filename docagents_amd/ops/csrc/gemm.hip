@@ -509,13 +509,25 @@ DA_EXPORT int da_gemm_resid_rmsnorm(const void* A, int lda, const void* W, void*
   DA_LAUNCH_CHECK();
 }
 
-// 256x256 prefill tile: 0 = 8-wave gemm256 (default), 1 = 4-wave gemm256w4 (tile 5 selects it
-// explicitly); DA_GEMM_W4=1 / da_set_gemm_w4 for A/B runs.
-static int g_gemm_w4 = 0;
-DA_EXPORT void da_set_gemm_w4(int v) { g_gemm_w4 = v; }
+// Prefill QKV projection with RoPE + KV-cache write fused into the epilogue (gemm8p EPI_ROPE);
+// M >= 256 (the phase-split kernel), N == (H + 2 Hkv) * D, D % 8 == 0.
+DA_EXPORT int da_gemm_rope(const void* A, int lda, const void* W, void* C, int ldc, int M, int N, int K,
+                           const void* pos, const void* slot, const void* cos_sin, void* k_cache, void* v_cache,
+                           int H, int Hkv, int D, int max_seq, void* stream) {
+  if (K % 64 || K < 128 || N % 8 || lda % 8 || ldc % 8 || D % 8 || M < 256) return (int)hipErrorInvalidValue;
+  if (N != (H + 2 * Hkv) * D || !pos || !slot || !cos_sin || !k_cache || !v_cache) return (int)hipErrorInvalidValue;
+  GemmArgs a{};
+  a.A = (const bf16_t*)A; a.W = (const bf16_t*)W; a.C = (bf16_t*)C;
+  a.M = M; a.N = N; a.K = K; a.lda = lda; a.ldc = ldc; a.k_per_split = K;
+  a.rope = RopeArgs{(const int*)pos, (const int*)slot, (const float*)cos_sin, (bf16_t*)k_cache, (bf16_t*)v_cache,
+                    H, Hkv, D, max_seq};
+  const long t256 = (long)((M + 255) / 256) * ((N + 255) / 256);
+  return launch_gemm8p(a, EPI_ROPE, (hipStream_t)stream, t256 >= 256 ? 256 : 128);
+}
 
 // Tile selection: big tiles when the grid fills 256 CUs, skinny tiles (+ split-K) for decode-sized M.
-// tile: 0 = auto, 1 = 128x128, 2 = 64x128, 3 = 32x128, 4 = 256x256, 5 = 256x256 4-wave, 6 = GEMV (M = 1).
+// tile: 0 = auto, 1 = 128x128, 2 = 64x128, 3 = 32x128, 4 / 7 = 256x256 phase-split (gemm8p),
+// 6 = GEMV (M = 1), 8 = 128x128 PF4, 9 = 128x64 PF4, 10 = 128x256 phase-split (gemm8p).
 DA_EXPORT int da_gemm_bf16(const void* A, int lda, const void* W, void* C, int ldc,
                            const void* bias, const void* resid, int ldr,
                            int M, int N, int K, int epi, int tile, int splits, void* ws,
@@ -534,16 +546,18 @@ DA_EXPORT int da_gemm_bf16(const void* A, int lda, const void* W, void* C, int l
   if (rms_gamma && tile != 6) return (int)hipErrorInvalidValue;  // fused RMSNorm: GEMV path only
   if (tile == 0) {
     const long t256 = (long)((M + 255) / 256) * ((N + 255) / 256);
-    tile = (M <= 32) ? 3 : (M <= 64 ? 2 : (t256 >= 256 && splits == 1 && K >= 128 ? 7 : 1));
+    // decode-sized M: 32x128 / 64x128 weight-streaming tiles (+ split-K, chosen by the caller);
+    // 65..639 rows: the 64x128 tile over ceil(M/64) row blocks; from 640 rows the phase-split
+    // kernel: 256-row tiles unless the grid is below half the chip, then 128-row tiles (32-layer
+    // Phi-3 chain and single-GEMM sweeps: bench/midm_chain.py, bench/gemm_ab.py, profiles/r2)
+    if (M <= 32) tile = 3;
+    else if (M < 640 || splits > 1) tile = 2;
+    else if (K < 128) tile = 1;
+    else tile = (t256 >= 128) ? 7 : 10;
   }
-  if (tile == 4 && g_gemm_w4 && K % 32 == 0) tile = 5;
-  if (tile == 7) {
+  if (tile == 4 || tile == 7 || tile == 10) {
     if (splits != 1 || K < 128) return (int)hipErrorInvalidValue;
-    return launch_gemm8p(a, epi, s);
-  }
-  if (tile == 4 || tile == 5) {
-    if (splits != 1) return (int)hipErrorInvalidValue;
-    return tile == 5 ? launch_gemm256w4(a, epi, s) : launch_gemm256(a, epi, s);
+    return launch_gemm8p(a, epi, s, tile == 10 ? 128 : 256);
   }
   if (tile == 6) return launch_gemv(a, epi, s);
   int err;
@@ -551,6 +565,8 @@ DA_EXPORT int da_gemm_bf16(const void* A, int lda, const void* W, void* C, int l
     case 1: err = launch_tile<128, 128, 2, 2>(a, epi, splits, s); break;
     case 2: err = launch_decode_tile<64, 128>(a, epi, splits, s); break;
     case 3: err = launch_decode_tile<32, 128>(a, epi, splits, s); break;
+    case 8: err = launch_tile<128, 128, 2, 2, 4>(a, epi, splits, s); break;   // mid-M weight streaming
+    case 9: err = launch_tile<128, 64, 2, 2, 4>(a, epi, splits, s); break;
     default: return (int)hipErrorInvalidValue;
   }
   if (err || splits == 1) return err;

@@ -1,4 +1,6 @@
-// 256x256-tile GEMM for prefill-sized M (C[M,N] = epi(A[M,K] . W[N,K]^T)), bf16 or fp8 operands.
+// 256x256-tile fp8 GEMM for prefill-sized M (C[M,N] = epi(A[M,K] . W[N,K]^T)): the encoder's fp8
+// path (BASELINE config 5). bf16 prefill GEMMs run the phase-split gemm8p.hip kernel, which
+// replaced this kernel's bf16 instantiation (1.42-1.51 vs 1.23-1.33 PF/s, profiles/r2).
 //
 // fp8 (OCP e4m3): the same 128-byte K-step and LDS image (BK = 128 fp8), one
 // v_mfma_scale_f32_16x16x128_f8f6f4 per fragment pair instead of two bf16 16x16x32 (2x the bf16
@@ -37,7 +39,7 @@ constexpr int SMEM = (2 * STAGE > STAGING) ? 2 * STAGE : STAGING;
 
 __device__ __forceinline__ int swz(int r) { return (r >> 1) & 7; }
 
-template <int EPI, int FP8, int PP = 0>
+template <int EPI, int FP8>
 __global__ void __launch_bounds__(512)
 gemm256_kernel(GemmArgs p) {
   constexpr int ES = FP8 ? 1 : 2;  // bytes per element
@@ -84,79 +86,7 @@ gemm256_kernel(GemmArgs p) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
-  if constexpr (!FP8 && PP) {
-    // ---- ping-pong schedule (bf16): the two 4-wave groups (wm = 0 / 1; every SIMD hosts one wave
-    // of each) are offset by one phase with ONE extra s_barrier, so on every SIMD one wave issues its
-    // LDS fragment reads + LDS-DMA while the other runs its MFMAs — the read bubble after each
-    // barrier that idles the MFMA pipe in the lock-step schedule (SQ_WAIT_ANY 25 %,
-    // profiles/gemm256_pmc_r1) is filled by the partner group. 32-deep K-steps in a 4-slot LDS ring
-    // (4 x 32 KiB), tiles issued 3 steps ahead; waits are counted (vmcnt(8) = two newer tiles of 4
-    // DMAs per wave stay in flight) and every barrier is a raw s_barrier (no vmcnt drain).
-    // Schedule per wave:  [G1: barrier]  for t: { X: barrier; issue(t+3 -> slot (t-1)%4); R(t);
-    //                      vmcnt(tile t+1); Y: barrier; M(t) }  [G0: barrier]
-    // Global barrier 2t is G0's X_t = G1's Y_{t-1}; 2t+1 is G0's Y_t = G1's X_t. RAW: every wave
-    // waits for tile t before global barrier 2t (G1 at the end of its R(t-1)); WAR: slot (t-1)%4 is
-    // refilled only after the barrier that ends the later group's R(t-1).
-    constexpr int HK = 32, SLOT = (BM + BN) * HK * 2;
-    const int g1 = wm;
-    const char* ra[2];
-    const char* rb[2];
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int r = (wid * 2 + j) * 16 + (lane >> 2);
-      const int c = (lane & 3) ^ (((r >> 3) & 1) << 1);
-      ra[j] = (const char*)p.A + ((size_t)min(m0 + r, p.M - 1) * p.lda) * 2 + c * 16;
-      rb[j] = (const char*)p.W + ((size_t)min(n0 + r, p.N - 1) * p.K) * 2 + c * 16;
-    }
-    const int nh = p.K / HK;
-    auto fill = [&](int h, int slot) {
-      char* sa = smem + slot * SLOT;
-      char* sb = sa + BM * HK * 2;
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-        __builtin_amdgcn_global_load_lds((gptr_t)(ra[j] + h * 64), (lds_ptr_t)(sa + (wid * 2 + j) * 1024), 16, 0, 0);
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-        __builtin_amdgcn_global_load_lds((gptr_t)(rb[j] + h * 64), (lds_ptr_t)(sb + (wid * 2 + j) * 1024), 16, 0, 0);
-    };
-    auto bar = [&]() {
-      __builtin_amdgcn_sched_barrier(0);
-      __builtin_amdgcn_s_barrier();
-      __builtin_amdgcn_sched_barrier(0);
-    };
-    fill(0, 0);
-    fill(min(1, nh - 1), 1);
-    fill(min(2, nh - 1), 2);
-    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-    if (g1) bar();
-    for (int h = 0; h < nh; ++h) {
-      bar();                                            // X_h
-      fill(min(h + 3, nh - 1), (h + 3) & 3);
-      const char* sa = smem + (h & 3) * SLOT;
-      const char* sb = sa + BM * HK * 2;
-      bf16x8_t af[8], bfr[4];
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const int r = wm * TM + i * 16 + fr;
-        af[i] = *(const bf16x8_t*)(sa + r * 64 + ((fg ^ (((r >> 3) & 1) << 1)) << 4));
-      }
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int r = wn * TN + j * 16 + fr;
-        bfr[j] = *(const bf16x8_t*)(sb + r * 64 + ((fg ^ (((r >> 3) & 1) << 1)) << 4));
-      }
-      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // tile h+1 landed (h+2, h+3 in flight)
-      bar();                                            // Y_h
-      __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-      for (int i = 0; i < 8; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(af[i], bfr[j], acc[i][j]);
-      __builtin_amdgcn_s_setprio(0);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (!g1) bar();
-  } else {
+  {
   const int nk = p.K * ES / 128;  // 128-byte K-steps (64 bf16 or 128 fp8)
   issue(0, 0);
   for (int kt = 0; kt < nk; ++kt) {
@@ -282,32 +212,24 @@ gemm256_kernel(GemmArgs p) {
   }
 }
 
-// The ping-pong schedule is +2-14 % on repeated (L2/MALL-warm) GEMMs but ~0.8 % slower in the
-// flagship bench, where every projection streams cold weights (same-box A/B,
-// profiles/gemm256_pingpong_r1.txt), so the lock-step kernel stays the default;
-// da_set_gemm_pingpong(1) / DA_GEMM_PINGPONG=1 selects ping-pong. Results are bit-identical.
-static int g_gemm_pp = 0;
-DA_EXPORT void da_set_gemm_pingpong(int v) { g_gemm_pp = v; }
-
-template <int FP8, int PP>
+template <int FP8>
 static int launch256(const GemmArgs& a, int epi, hipStream_t s, dim3 grid, dim3 block) {
   switch (epi) {
-    case EPI_NONE: gemm256_kernel<EPI_NONE, FP8, PP><<<grid, block, 0, s>>>(a); break;
-    case EPI_BIAS: gemm256_kernel<EPI_BIAS, FP8, PP><<<grid, block, 0, s>>>(a); break;
-    case EPI_GELU: gemm256_kernel<EPI_GELU, FP8, PP><<<grid, block, 0, s>>>(a); break;
-    case EPI_SWIGLU: gemm256_kernel<EPI_SWIGLU, FP8, PP><<<grid, block, 0, s>>>(a); break;
-    case EPI_RESID: gemm256_kernel<EPI_RESID, FP8, PP><<<grid, block, 0, s>>>(a); break;
+    case EPI_NONE: gemm256_kernel<EPI_NONE, FP8><<<grid, block, 0, s>>>(a); break;
+    case EPI_BIAS: gemm256_kernel<EPI_BIAS, FP8><<<grid, block, 0, s>>>(a); break;
+    case EPI_GELU: gemm256_kernel<EPI_GELU, FP8><<<grid, block, 0, s>>>(a); break;
+    case EPI_SWIGLU: gemm256_kernel<EPI_SWIGLU, FP8><<<grid, block, 0, s>>>(a); break;
+    case EPI_RESID: gemm256_kernel<EPI_RESID, FP8><<<grid, block, 0, s>>>(a); break;
     default: return (int)hipErrorInvalidValue;
   }
   return (int)hipGetLastError();
 }
 
 int launch_gemm256(const GemmArgs& a, int epi, hipStream_t s, int fp8) {
+  if (!fp8) return (int)hipErrorInvalidValue;  // bf16: gemm8p
   const int ntm = (a.M + BM - 1) / BM, ntn = (a.N + BN - 1) / BN;
   dim3 grid(ntm * ntn), block(512);
-  if (fp8) return launch256<1, 0>(a, epi, s, grid, block);
-  if (g_gemm_pp && a.K % 32 == 0) return launch256<0, 1>(a, epi, s, grid, block);
-  return launch256<0, 0>(a, epi, s, grid, block);
+  return launch256<1>(a, epi, s, grid, block);
 }
 
 // fp8 GEMM entry: A [M, lda] e4m3 (row-major), W [N, K] e4m3, sa [M], sw [N] fp32 dequant scales.

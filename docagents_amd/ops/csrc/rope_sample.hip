@@ -1,8 +1,11 @@
 // RoPE + KV-cache write, and the fused temperature sampler with chosen-token logprob.
 //
-// RoPE (NeoX / HF rotate_half layout, Llama-3 & Phi-3): pairs (i, i + D/2) rotated by
-// theta_i * pos. cos/sin come from a host-built fp32 table [max_pos, D/2, 2] so the kernel stays
-// memory-bound (Appendix B: trig tables on the host, not sinf/cosf per element).
+// RoPE, interleaved pairs (2i, 2i+1) rotated by theta_i * pos (the original Llama / GPT-J layout; an
+// HF rotate_half checkpoint is converted by permuting the q / k rows of each head at load,
+// models/llama.py to_interleaved_rope — q.k is invariant under the same permutation of both). With
+// adjacent pairs a rotation never leaves a 16-B chunk, so the prefill QKV GEMM applies it in its
+// epilogue (gemm8p EPI_ROPE). cos/sin come from a host-built fp32 table [max_pos, D/2, 2] so the
+// kernels stay memory-bound (Appendix B: trig tables on the host, not sinf/cosf per element).
 //
 // The sampler replaces OpenAI's `logprobs=true, top_logprobs=1` + `calculateLLMConfidence`
 // (internal/llm/openai.go:84-90,149-164): Gumbel-max sampling at
@@ -21,7 +24,7 @@ rope_cache_kernel(bf16_t* __restrict__ qkv, const int* __restrict__ pos, const i
   const int t = blockIdx.x;
   const int w = blockIdx.y * blockDim.x + threadIdx.x;
   const int half = D / 2;
-  const int groups = half / 4;  // 4 consecutive rotary pairs per work item
+  const int groups = D / 8;  // one 16-B chunk = 4 consecutive rotary pairs per work item
   const int nheads = (rotate_q ? H : 0) + Hkv;
   const int nrot = nheads * groups;
   const int nv = vc ? Hkv * (D / 8) : 0;
@@ -34,30 +37,24 @@ rope_cache_kernel(bf16_t* __restrict__ qkv, const int* __restrict__ pos, const i
   if (w < nrot) {
     const int hh = w / groups, gq = w % groups;
     const int head = rotate_q ? hh : H + hh;  // head index within q|k region
-    bf16_t* hp = row + head * D;
+    bf16_t* hp = row + head * D + gq * 8;
     const int i0 = gq * 4;
-    const u32x2_t a = *(const u32x2_t*)(hp + i0);
-    const u32x2_t b = *(const u32x2_t*)(hp + half + i0);
+    const u32x4_t a = *(const u32x4_t*)hp;
     const f32x4_t c01 = *(const f32x4_t*)(cs + ((size_t)p * half + i0) * 2);
     const f32x4_t c23 = *(const f32x4_t*)(cs + ((size_t)p * half + i0) * 2 + 4);
     const float cc[4] = {c01[0], c01[2], c23[0], c23[2]}, sn[4] = {c01[1], c01[3], c23[1], c23[3]};
-    const float x1[4] = {bf2f(a[0] & 0xffff), bf2f(a[0] >> 16), bf2f(a[1] & 0xffff), bf2f(a[1] >> 16)};
-    const float x2[4] = {bf2f(b[0] & 0xffff), bf2f(b[0] >> 16), bf2f(b[1] & 0xffff), bf2f(b[1] >> 16)};
-    float o1[4], o2[4];
+    u32x4_t r;
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-      o1[e] = x1[e] * cc[e] - x2[e] * sn[e];
-      o2[e] = x2[e] * cc[e] + x1[e] * sn[e];
+      const float x1 = bf2f(a[e] & 0xffff), x2 = bf2f(a[e] >> 16);
+      const float o1 = x1 * cc[e] - x2 * sn[e];
+      const float o2 = x2 * cc[e] + x1 * sn[e];
+      r[e] = pack_bf2(o1, o2);
     }
-    const u32x2_t ra = u32x2_t{pack_bf2(o1[0], o1[1]), pack_bf2(o1[2], o1[3])};
-    const u32x2_t rb = u32x2_t{pack_bf2(o2[0], o2[1]), pack_bf2(o2[2], o2[3])};
-    *(u32x2_t*)(hp + i0) = ra;
-    *(u32x2_t*)(hp + half + i0) = rb;
+    *(u32x4_t*)hp = r;
     if (kc && head >= H) {
       const int hk = head - H;
-      bf16_t* dst = kc + (((size_t)s * Hkv + hk) * max_seq + p) * D;
-      *(u32x2_t*)(dst + i0) = ra;
-      *(u32x2_t*)(dst + half + i0) = rb;
+      *(u32x4_t*)(kc + (((size_t)s * Hkv + hk) * max_seq + p) * D + gq * 8) = r;
     }
   } else {
     const int wv = w - nrot;

@@ -29,6 +29,8 @@ c_void_p, c_int, c_float, c_uint, c_size_t = (ctypes.c_void_p, ctypes.c_int, cty
 _SIGS = {
     "da_gemm_bf16": [c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int,
                      c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_float, c_void_p],
+    "da_gemm_rope": [c_void_p, c_int, c_void_p, c_void_p, c_int, c_int, c_int, c_int] + [c_void_p] * 5
+                    + [c_int] * 4 + [c_void_p],
     "da_gemm_fp8": [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int,
                     c_int, c_int, c_int, c_int, c_void_p],
     "da_quant_fp8_rows": [c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p],
@@ -45,21 +47,15 @@ _SIGS = {
     "da_rope_cache": [c_void_p] * 6 + [c_int] * 6 + [c_void_p],
     "da_sample": [c_void_p, c_int, c_int, c_int, c_float, c_uint, c_uint] + [c_void_p] * 9
                  + [c_int] * 5 + [c_void_p],
-    "da_flash_attn_varlen": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_int,
-                             c_int, c_int, c_int, c_int, c_float, c_void_p, c_int, c_void_p],
     "da_flash_attn_v2": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_int,
                          c_int, c_int, c_int, c_int, c_float, c_void_p, c_int, c_void_p, c_void_p, c_longlong,
                          c_int, c_void_p],
     "da_set_gqa_mfma": [c_int],
     "da_malloc_uncached": [c_longlong, ctypes.POINTER(c_void_p)],
     "da_set_flash_waves": [c_int],
-    "da_set_gemm_pingpong": [c_int],
-    "da_set_gemm8p_sched": [c_int],
-    "da_set_gemm_w4": [c_int],
     "da_set_gemm_pf": [c_int],
     "da_set_decode_pft": [c_int],
     "da_set_flash_rev": [c_int],
-    "da_set_gemm_w4_cfg": [c_int],
     "da_decode_attn": [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
                        c_int, c_int, c_int, c_float, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p,
                        c_void_p],
@@ -69,7 +65,6 @@ _SIGS = {
                        c_float, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p],
     "da_topk_merge": [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p],
     "da_kmeans_accum": [c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p],
-    "da_mall_prefetch": [c_void_p, ctypes.c_long, c_int, c_void_p, c_void_p],
 }
 
 
@@ -107,12 +102,6 @@ def lib() -> ctypes.CDLL:
         L.da_topk_dense_ws.argtypes = [c_int, c_int, c_int, c_int]
         L.da_topk_dense_ws.restype = c_size_t
         # schedule overrides for A/B measurements (defaults are the measured-best variants)
-        if os.environ.get("DA_GEMM_PINGPONG") is not None:
-            L.da_set_gemm_pingpong(int(os.environ["DA_GEMM_PINGPONG"]))
-        if os.environ.get("DA_GEMM8P_SCHED") is not None:
-            L.da_set_gemm8p_sched(int(os.environ["DA_GEMM8P_SCHED"]))
-        if os.environ.get("DA_GEMM_W4") is not None:
-            L.da_set_gemm_w4(int(os.environ["DA_GEMM_W4"]))
         if os.environ.get("DA_GEMM_PF") is not None:  # decode-tile register prefetch depth (A/B)
             L.da_set_gemm_pf(int(os.environ["DA_GEMM_PF"]))
         if os.environ.get("DA_FLASH_REV") is not None:  # causal flash longest-first dispatch (A/B)
@@ -169,15 +158,6 @@ def _workspace(nbytes: int, device) -> torch.Tensor:
     return buf
 
 
-def mall_prefetch(t: torch.Tensor, nwg: int = 32) -> None:
-    """Read ``t`` with ``nwg`` workgroups on the current stream so a later consumer finds it in the
-    memory-side Infinity Cache (loads only; see csrc/prefetch.hip)."""
-    _req(t.is_cuda and t.is_contiguous() and t.data_ptr() % 16 == 0, "prefetch needs a contiguous 16-B aligned tensor")
-    sink = _workspace(256, t.device)
-    _check(lib().da_mall_prefetch(_ptr(t), t.numel() * t.element_size(), nwg, _ptr(sink), _stream()),
-           "da_mall_prefetch")
-
-
 def gemv_fusable(M: int, N: int, K: int, epi: int = EPI_NONE) -> bool:
     """True when gemm() runs the batch-1 GEMV (which can also fuse the input RMSNorm)."""
     return M == 1 and K % 512 == 0 and N % 4 == 0 and (epi != EPI_SWIGLU or N % 32 == 0)
@@ -229,9 +209,9 @@ def gemm(a: torch.Tensor, w: torch.Tensor, bias=None, epi: int = EPI_NONE, resid
         _req(tile == 6, "fused RMSNorm needs the M == 1 GEMV path")
         _bf16_cuda(gamma, "gamma"); _req(gamma.numel() == K, "gamma must be [K]")
     if splits <= 0:
-        if tile == 0 and M <= 64:
+        if tile == 0 and M < 640:
             tile = _decode_tile(M)
-        splits = _auto_splits(M, N, K)
+        splits = _auto_splits(M, N, K) if tile in (0, 2, 3) else 1
     ws = None
     if splits > 1:
         ws = _workspace(splits * M * N * 4, a.device)
@@ -241,29 +221,20 @@ def gemm(a: torch.Tensor, w: torch.Tensor, bias=None, epi: int = EPI_NONE, resid
     return out
 
 
-# Plain prefill-sized GEMMs (no epilogue, bias, or residual as the BLAS beta*C term) go to the
-# platform GEMM library (hipBLASLt) — the "plain library GEMM" case; everything with a fused
-# epilogue (SwiGLU, GELU, RMSNorm, split-K reductions, fp8 scales) and every decode-sized GEMM stays
-# on the hand-written kernels. Measured sustained on MI355X (profiles/gemm256_w4_r1.txt): hipBLASLt
-# 1.50-1.57 PF/s vs gemm256 1.22-1.31 at M = 32768. DA_BLAS_PREFILL=0 keeps everything on gemm256.
+# Every GEMM runs on the in-tree kernels by default: gemm8p (phase-split BMx256, csrc/gemm8p.hip)
+# from 256 rows, the 64x128 / 32x128 weight-streaming tiles below. Same-box measurements
+# (profiles/r2/ab_gemm8p_vs_hipblaslt.txt): gemm8p 1.42-1.51 PF/s vs hipBLASLt 1.43-1.56 on the
+# Phi-3 prefill shapes and +9 % on gate/up with the fused SwiGLU (hipBLASLt needs a separate pass);
+# flagship 31.0 vs 30.6 QA q/s. The hipBLASLt routes below stay only as opt-in A/B arms:
+#   DA_BLAS_PREFILL=1   plain / bias / residual GEMMs with M >= DA_BLAS_MIN_M
+#   DA_BLAS_SWIGLU=1    gate/up on hipBLASLt + swiglu_interleaved
+#   DA_BLAS_UNDERFILL=1 1024..DA_BLAS_MIN_M rows when 256x256 tiles underfill the chip
+#   DA_BLAS_MID=1       65..1023 rows
 _BLAS_PREFILL = os.environ.get("DA_BLAS_PREFILL", "0") == "1"
-# Gate/up projection on hipBLASLt + a separate SwiGLU pass (DA_BLAS_SWIGLU=1) instead of gemm256
-# with the fused epilogue: trades 1.5x the output bytes for hipBLASLt's faster main loop. Same-box
-# A/B (profiles/ab_blas_swiglu_r1.txt): +0.3% flagship; DA_BLAS_SWIGLU=0 keeps the fused gemm256.
 _BLAS_SWIGLU = os.environ.get("DA_BLAS_SWIGLU", "0") == "1"
 _BLAS_MIN_M = int(os.environ.get("DA_BLAS_MIN_M", "4096"))
-# Between 1024 rows and _BLAS_MIN_M a plain GEMM also goes to hipBLASLt when the 256x256 tile would
-# leave CUs idle (< 256 tiles, e.g. the o / down projections of a batch-1 ~2.9k-token prefill, N =
-# 3072: 144 tiles; the 128x128 fallback reached only ~0.6 PF/s there). DA_BLAS_UNDERFILL=0: off.
-_BLAS_UNDERFILL = os.environ.get("DA_BLAS_UNDERFILL", "1") != "0"
-
-
-# 65..1023 rows (decode batches above 64, shared-prompt-head and short prefills): too many rows for
-# the 64-row decode tiles, too few to fill the 128x128 / 256x256 tiles with split-K off. Measured on
-# a 32-layer Phi-3 GEMM chain in one HIP graph (profiles/decode_gemm_mid_m_r1.jsonl): hipBLASLt
-# 3.2-7.6 ms vs 8.4-10.5 ms in-tree for M = 80..1023 (plain and gate/up + separate SwiGLU alike);
-# M <= 64 stays on the decode tiles (2.54 vs 2.61 ms at M = 64). DA_BLAS_MID=0: off.
-_BLAS_MID = os.environ.get("DA_BLAS_MID", "1") != "0"
+_BLAS_UNDERFILL = os.environ.get("DA_BLAS_UNDERFILL", "0") == "1"
+_BLAS_MID = os.environ.get("DA_BLAS_MID", "0") == "1"
 
 
 def _blas_mid(M: int) -> bool:
@@ -274,6 +245,30 @@ def _blas_size_ok(M: int, N: int) -> bool:
     if M >= _BLAS_MIN_M or _blas_mid(M):
         return True
     return _BLAS_UNDERFILL and M >= 1024 and math.ceil(M / 256) * math.ceil(N / 256) < 256
+
+
+def gemm_rope(a, w, pos, cos_sin, H: int, Hkv: int, D: int, slot, k_cache, v_cache, out=None) -> torch.Tensor:
+    """Prefill QKV projection: qkv = a @ w^T with RoPE applied to the q / k heads and the token's
+    k / v written to the KV cache (cache [slots, Hkv, max_seq, D]) — one kernel (gemm8p EPI_ROPE)
+    from 256 rows; shorter prefills run gemm + rope_cache (identical roundings)."""
+    _bf16_cuda(a, "a"); _bf16_cuda(w, "w"); _i32(pos, "pos"); _i32(slot, "slot")
+    M, K = a.shape
+    N = w.shape[0]
+    _req(N == (H + 2 * Hkv) * D and w.shape[1] == K and D % 8 == 0, "qkv weight shape")
+    _req(pos.numel() >= M and slot.numel() >= M, "pos / slot length")
+    _req(cos_sin.dtype == torch.float32 and cos_sin.is_contiguous() and cos_sin.shape[1] == D // 2, "cos_sin")
+    _req(k_cache.is_contiguous() and v_cache.is_contiguous() and k_cache.shape == v_cache.shape
+         and k_cache.dim() == 4 and k_cache.shape[1] == Hkv and k_cache.shape[3] == D, "caches")
+    if M < 256 or K % 64 or K < 128 or a.stride(1) != 1 or a.stride(0) % 8 or not w.is_contiguous():
+        qkv = gemm(a, w, out=out)
+        return rope_cache(qkv, pos, cos_sin, H, Hkv, D, slot=slot, k_cache=k_cache, v_cache=v_cache)
+    if out is None:
+        out = torch.empty((M, N), dtype=torch.bfloat16, device=a.device)
+    _req(out.shape == (M, N) and out.stride(1) == 1 and out.stride(0) % 8 == 0, "bad out")
+    _check(lib().da_gemm_rope(_ptr(a), a.stride(0), _ptr(w), _ptr(out), out.stride(0), M, N, K, _ptr(pos), _ptr(slot),
+                              _ptr(cos_sin), _ptr(k_cache), _ptr(v_cache), H, Hkv, D, k_cache.shape[2], _stream()),
+           "gemm_rope")
+    return out
 
 
 def swiglu_interleaved(x: torch.Tensor, out=None) -> torch.Tensor:
@@ -379,7 +374,8 @@ def gemm_resid_norm(a, w, resid, gamma, eps: float, out=None, h_out=None, bias=N
 
 
 def _decode_tile(M: int) -> int:
-    """Decode-sized M: 32x128 tiles up to 32 rows, 64x128 above (no wasted MFMA rows either way)."""
+    """Decode-sized M: 32x128 tiles up to 32 rows, 64x128 above (no wasted MFMA rows either way;
+    65..255 rows run the 64x128 tile over ceil(M/64) row blocks)."""
     return 3 if M <= 32 else 2
 
 
@@ -390,12 +386,17 @@ def _auto_splits(M: int, N: int, K: int) -> int:
     graph-replayed sweep with weights streamed cold from HBM, as in a real decode step
     (profiles/decode_gemm_prefetch_sweep_r1.jsonl: matches the best split on 17 of 20 Phi-3 /
     Llama-3-8B shapes at M = 16 / 64, within 0.7 us on the rest)."""
-    if M > 64:
+    if M >= 640:
         return 1
     tiles = math.ceil(M / (32 if _decode_tile(M) == 3 else 64)) * math.ceil(N / 128)
     ksteps = K // 64
+    # 65..639 rows run the 64x128 tile over ceil(M/64) row blocks (the row blocks of one weight tile
+    # share it through L2): up to 4 workgroups per CU below 256 rows, 2.5 from 256 (32-layer Phi-3
+    # chain, bench/midm_chain.py, profiles/r2/midm_chain.txt: split 4 best at M = 65 / 128, 2 at 192 /
+    # 256, 1 from 384)
+    cap = 256 if M <= 64 else (1024 if M < 256 else 640)
     s = 1
-    while tiles * s * 2 <= 256 and ksteps % (s * 2) == 0 and ksteps // (s * 2) >= 4:
+    while tiles * s * 2 <= cap and ksteps % (s * 2) == 0 and ksteps // (s * 2) >= 4:
         s *= 2
     return s
 
@@ -497,11 +498,8 @@ def rope_cache(qkv, pos, cos_sin, H, Hkv, D, slot=None, k_cache=None, v_cache=No
     return qkv
 
 
-FLASH_IMPL = "v2"  # "v1" (16x16 MFMA, 64 queries/workgroup) kept for A/B measurements
-
-
 def flash_attn_varlen(q, k, v, cu_seqlens, max_seqlen: int, H: int, Hkv: int, D: int, causal: bool,
-                      scale: float | None = None, out=None, impl: str | None = None, prefix=None):
+                      scale: float | None = None, out=None, prefix=None):
     """q/k/v: 2-D [T, *] views with head h at columns h*D (strided views into a packed qkv are fine).
     prefix = (k_pre, v_pre, P): shared-prefix keys of every sequence, one KV-cache slot's
     [Hkv, max_seq, D] K and V (RoPE applied); query i of a sequence is key P + i."""
@@ -516,12 +514,6 @@ def flash_attn_varlen(q, k, v, cu_seqlens, max_seqlen: int, H: int, Hkv: int, D:
         out = torch.empty((T, H * D), dtype=torch.bfloat16, device=q.device)
     scale = scale if scale is not None else 1.0 / math.sqrt(D)
     B = cu_seqlens.numel() - 1
-    if (impl or FLASH_IMPL) != "v2":
-        _req(prefix is None, "shared-prefix attention needs the v2 kernel")
-        _check(lib().da_flash_attn_varlen(_ptr(q), _ptr(k), _ptr(v), q.stride(0), k.stride(0), v.stride(0),
-                                          _ptr(cu_seqlens), B, int(max_seqlen), H, Hkv, D, int(causal), float(scale),
-                                          _ptr(out), out.stride(0), _stream()), "flash_attn_varlen")
-        return out
     kp = vp = None
     hstride, P = 0, 0
     if prefix is not None:

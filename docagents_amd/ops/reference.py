@@ -120,11 +120,16 @@ def rope_table(max_pos: int, D: int, theta: float, device=None) -> torch.Tensor:
     return torch.stack([ang.cos(), ang.sin()], dim=-1).float().contiguous().to(device)
 
 
-def _rope_rows(x, cs):  # x [T, nh, D], cs [T, D/2, 2]
-    half = x.shape[-1] // 2
-    x1, x2 = x[..., :half].float(), x[..., half:].float()
+def _rope_rows(x, cs):  # x [T, nh, D], cs [T, D/2, 2]; pairs (2i, 2i+1) rotated by theta_i * pos
+    x1, x2 = x[..., 0::2].float(), x[..., 1::2].float()
     c, s = cs[:, None, :, 0], cs[:, None, :, 1]
-    return torch.cat([x1 * c - x2 * s, x2 * c + x1 * s], dim=-1)
+    return torch.stack([x1 * c - x2 * s, x2 * c + x1 * s], dim=-1).flatten(-2)
+
+
+def gemm_rope(a, w, pos, cos_sin, H, Hkv, D, slot, k_cache, v_cache, out=None):
+    """QKV projection with RoPE on q / k and the k / v cache write fused (gemm + rope_cache)."""
+    qkv = gemm(a, w, out=out)
+    return rope_cache(qkv, pos, cos_sin, H, Hkv, D, slot=slot, k_cache=k_cache, v_cache=v_cache)
 
 
 def rope_cache(qkv, pos, cos_sin, H, Hkv, D, slot=None, k_cache=None, v_cache=None, rotate_q=True):

@@ -96,6 +96,62 @@ def all_gather_rows(t: torch.Tensor, group=None) -> torch.Tensor:
     return out
 
 
+def _stage(t: torch.Tensor, group) -> torch.Tensor:
+    """gloo cannot all-gather device tensors (1-GPU multi-rank rehearsal): stage on the host."""
+    return t.cpu() if t.is_cuda and dist.get_backend(group) == "gloo" else t
+
+
+def all_gather_padded_rows(t: torch.Tensor, n_total: int, group=None) -> torch.Tensor:
+    """Rank r holds rows [r*per, min(n_total, (r+1)*per)) of an n_total-row result, per =
+    ceil(n_total / world) (the engine's data-parallel slicing). One all_gather_into_tensor of the
+    zero-padded slices (RCCL on GPU ranks) -> the [n_total, ...] result in rank order, on every rank."""
+    if not dist.is_initialized() or dist.get_world_size(group) == 1:
+        return t
+    w = dist.get_world_size(group)
+    per = (n_total + w - 1) // w
+    pad = torch.zeros((per,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
+    pad[:t.shape[0]] = t
+    src = _stage(pad, group)
+    out = torch.empty((w * per,) + tuple(t.shape[1:]), dtype=t.dtype, device=src.device)
+    dist.all_gather_into_tensor(out, src, group=group)
+    return out[:n_total].to(t.device)
+
+
+def pack_scores_ids(scores: torch.Tensor, ids: torch.Tensor) -> torch.Tensor:
+    """fp32 scores + int64 ids [Q, k] -> one int64 [Q, k, 2] buffer (scores as their bit pattern), so
+    a search's top-k lists travel in ONE collective."""
+    bits = scores.float().contiguous().view(torch.int32).to(torch.int64)
+    return torch.stack([ids.to(torch.int64), bits], dim=-1).contiguous()
+
+
+def unpack_scores_ids(p: torch.Tensor):
+    return p[..., 1].to(torch.int32).view(torch.float32), p[..., 0]
+
+
+def all_gather_bytes(payload: bytes, device, group=None) -> list[bytes]:
+    """Variable-length byte payloads from every rank, as tensors (RCCL on GPU ranks, gloo on CPU):
+    one all-gather of the lengths, one of the zero-padded uint8 payloads. The engine's data plane
+    for results that are not plain tensors (answers, summaries) — no pickles."""
+    if not dist.is_initialized() or dist.get_world_size(group) == 1:
+        return [payload]
+    w = dist.get_world_size(group)
+    dev = torch.device(device) if device is not None else torch.device("cpu")
+    if dev.type == "cuda" and dist.get_backend(group) == "gloo":
+        dev = torch.device("cpu")
+    n = torch.tensor([len(payload)], dtype=torch.int64, device=dev)
+    ns = torch.empty(w, dtype=torch.int64, device=dev)
+    dist.all_gather_into_tensor(ns, n, group=group)
+    lens = ns.cpu().tolist()
+    mx = max(1, max(lens))
+    buf = torch.zeros(mx, dtype=torch.uint8, device=dev)
+    if payload:
+        buf[:len(payload)] = torch.frombuffer(bytearray(payload), dtype=torch.uint8).to(dev)
+    out = torch.empty(w * mx, dtype=torch.uint8, device=dev)
+    dist.all_gather_into_tensor(out, buf, group=group)
+    host = out.cpu().numpy()
+    return [host[i * mx:i * mx + lens[i]].tobytes() for i in range(w)]
+
+
 def liveness_check(device, timeout_ok: bool = True) -> int:
     """C7: every rank contributes 1; returns the number of live ranks (== world when healthy)."""
     if not dist.is_initialized():

@@ -4,8 +4,8 @@ Each rank owns one in-HBM shard (flat or IVFFlat). A search is one collective ro
 
     C2  all-gather of the query embeddings  [W*B, d]   (every shard scores every query)
         local fused scan + doc filter + threshold + top-k on the shard
-    C1  all-gather of per-shard (score, id) top-k lists [W, W*B, k]   (a few KB: latency-bound,
-        so all queries of a step share ONE collective instead of one per query)
+    C1  all-gather of per-shard (score, id) top-k lists [W, W*B, k] packed into ONE int64 buffer
+        (a few KB: latency-bound, so all queries of a step share ONE collective)
         device merge (topk_merge kernel) -> each rank keeps its own queries' global top-k
 
 Exactness: the doc filter and the similarity floor are applied inside each shard BEFORE the
@@ -16,7 +16,7 @@ from __future__ import annotations
 import torch
 import torch.distributed as dist
 
-from .dist import all_gather_rows
+from .dist import all_gather_rows, pack_scores_ids, unpack_scores_ids
 
 
 class ShardedIndex:
@@ -37,8 +37,10 @@ class ShardedIndex:
         qs = all_gather_rows(q_local.contiguous(), self.group)                     # C2
         s, rows = self.local.search(qs, k, min_sim, doc_filters_all)
         gid = self.local.gather_ids(rows)                                          # int64 [W*B, k]
-        S = all_gather_rows(s.contiguous(), self.group).view(self.world, self.world * B, k)   # C1
-        G = all_gather_rows(gid.contiguous(), self.group).view(self.world, self.world * B, k)
+        P = all_gather_rows(pack_scores_ids(s, gid), self.group)                    # C1 (one buffer)
+        S, G = unpack_scores_ids(P)
+        S = S.reshape(self.world, self.world * B, k)
+        G = G.reshape(self.world, self.world * B, k)
         mine = slice(self.rank * B, (self.rank + 1) * B)
         S, G = S[:, mine].contiguous(), G[:, mine].contiguous()
         # merge: candidate "ids" for the kernel are positions (shard * k + j) -> deterministic ties

@@ -73,7 +73,16 @@ async def run_worker_service(name: str):
         worker = deps.queue.worker("analyze", analysis.make_handler(deps), stop,
                                    on_permanent_failure=analysis.make_failure_hook(deps))
     deps.log.info(f"{name} health endpoint listening", "addr", f":{deps.config.port}")
-    await asyncio.gather(worker, _serve_http(_health_app(deps, name), deps.config.port))
+    http = asyncio.ensure_future(_serve_http(_health_app(deps, name), deps.config.port))
+    try:
+        await worker  # returns once SIGINT / SIGTERM set ``stop`` and in-flight tasks finished
+    finally:
+        http.cancel()
+        try:
+            await http
+        except (asyncio.CancelledError, Exception):  # noqa: BLE001
+            pass
+    deps.log.info(f"{name} worker stopped")
 
 
 def _attach_tokenizer(deps):
@@ -147,14 +156,19 @@ async def run_all():
     stop = await _stop_event()
     await startup_sweep(deps)
     deps.log.info("all-in-one listening", "gateway", cfg.port, "query", qport)
-    await asyncio.gather(
-        _serve_http(gateway.build_app(deps), cfg.port),
-        _serve_http(query.build_app(deps), qport),
-        deps.queue.worker("parse", parser.make_handler(deps), stop,
-                          on_permanent_failure=parser.make_failure_hook(deps)),
-        deps.queue.worker("analyze", analysis.make_handler(deps), stop,
-                          on_permanent_failure=analysis.make_failure_hook(deps)),
-    )
+    http = [asyncio.ensure_future(_serve_http(gateway.build_app(deps), cfg.port)),
+            asyncio.ensure_future(_serve_http(query.build_app(deps), qport))]
+    try:
+        await asyncio.gather(
+            deps.queue.worker("parse", parser.make_handler(deps), stop,
+                              on_permanent_failure=parser.make_failure_hook(deps)),
+            deps.queue.worker("analyze", analysis.make_handler(deps), stop,
+                              on_permanent_failure=analysis.make_failure_hook(deps)),
+        )
+    finally:
+        for t in http:
+            t.cancel()
+        await asyncio.gather(*http, return_exceptions=True)
 
 
 def main(argv=None):

@@ -352,3 +352,42 @@ def test_continuous_batching_caches_prompt_head():
     assert sched.stats["heads_built"] == 1 and sched.stats["head_hits"] == 5
     assert sched.heads[0]["refs"] == 0
     assert len(e.gen.cache.free) == e.gen.cache.slots - 2  # dummy slot + the cached head's slot
+
+
+def test_interleaved_rope_conversion_preserves_attention_scores():
+    """HF rotate_half checkpoints run on this engine's interleaved-pair RoPE (so the prefill QKV GEMM can
+    rotate inside its epilogue) after to_interleaved_rope permutes the q / k rows of every head:
+    q.k per head and the v rows are unchanged."""
+    from docagents_amd.models.llama import to_interleaved_rope
+    from docagents_amd.ops import reference as R
+    torch.manual_seed(0)
+    H, Hkv, D, hid, T = 4, 2, 96, 64, 9
+    w = torch.randn((H + 2 * Hkv) * D, hid, dtype=torch.float64)
+    x = torch.randn(T, hid, dtype=torch.float64)
+    pos = torch.arange(T) * 7 + 3
+    cs = R.rope_table(128, D, 10000.0).double()[pos]
+
+    def rotate_half_rope(z):  # HF layout: pairs (i, i + D/2)
+        z1, z2 = z[..., :D // 2], z[..., D // 2:]
+        c, s = cs[:, None, :, 0], cs[:, None, :, 1]
+        return torch.cat([z1 * c - z2 * s, z2 * c + z1 * s], dim=-1)
+
+    def interleaved_rope(z):  # this engine: pairs (2i, 2i + 1)
+        z1, z2 = z[..., 0::2], z[..., 1::2]
+        c, s = cs[:, None, :, 0], cs[:, None, :, 1]
+        return torch.stack([z1 * c - z2 * s, z2 * c + z1 * s], dim=-1).flatten(-2)
+
+    def scores(qkv, rope):
+        q = rope(qkv[:, :H * D].view(T, H, D))
+        k = rope(qkv[:, H * D:(H + Hkv) * D].view(T, Hkv, D)).repeat_interleave(H // Hkv, 1)
+        return torch.einsum("qhd,khd->hqk", q, k), qkv[:, (H + Hkv) * D:]
+
+    s_hf, v_hf = scores(x @ w.t(), rotate_half_rope)
+    s_il, v_il = scores(x @ to_interleaved_rope(w, H, Hkv, D).t(), interleaved_rope)
+    torch.testing.assert_close(s_il, s_hf, rtol=1e-10, atol=1e-10)
+    assert torch.equal(v_il, v_hf)
+    # the fp32 reference kernel implements the interleaved layout
+    qkv = (x @ to_interleaved_rope(w, H, Hkv, D).t()).float().to(torch.bfloat16)
+    got = R.rope_cache(qkv.clone(), pos.int(), R.rope_table(128, D, 10000.0), H, Hkv, D)
+    want = interleaved_rope(qkv.double()[:, :(H + Hkv) * D].view(T, H + Hkv, D)).reshape(T, -1)
+    torch.testing.assert_close(got[:, :(H + Hkv) * D].double(), want, rtol=0.02, atol=0.02)

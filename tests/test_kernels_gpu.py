@@ -61,18 +61,69 @@ def test_gemm_swiglu(M, F, splits):
     _close(got, ref, atol=0.03)
 
 
-@pytest.mark.parametrize("M,N,Kd", [(256, 256, 64), (300, 520, 192), (1000, 1032, 768), (2048, 3072, 3072)])
+@pytest.mark.parametrize("M,N,Kd", [(256, 256, 128), (300, 520, 192), (1000, 1032, 768), (2048, 3072, 3072),
+                                    (129, 264, 640), (4100, 776, 256)])
 @pytest.mark.parametrize("epi", [K.EPI_NONE, K.EPI_BIAS, K.EPI_GELU, K.EPI_RESID, K.EPI_SWIGLU])
-def test_gemm256_tile(M, N, Kd, epi):
+@pytest.mark.parametrize("tile", [7, 10])
+def test_gemm8p_tile(M, N, Kd, epi, tile):
+    """Phase-split kernel, 256-row (tile 7) and 128-row (tile 10) tiles, every epilogue, ragged M / N."""
     torch.manual_seed(M + N + epi)
     if epi == K.EPI_SWIGLU:
         N = (N // 32) * 32
     a, w = _rand(M, Kd), _rand(N, Kd, scale=Kd ** -0.5)
     bias = _rand(N) if epi in (K.EPI_BIAS, K.EPI_GELU, K.EPI_RESID) else None
     resid = _rand(M, N) if epi == K.EPI_RESID else None
-    got = K.gemm(a, w, bias=bias, epi=epi, resid=resid, tile=4, splits=1)
+    got = K.gemm(a, w, bias=bias, epi=epi, resid=resid, tile=tile, splits=1)
     ref = R.gemm(a, w, bias=bias, epi=epi, resid=resid)
     _close(got, ref, atol=0.04)
+
+
+@pytest.mark.parametrize("M", [256, 700, 3000])
+@pytest.mark.parametrize("H,Hkv,D", [(32, 32, 96), (8, 2, 128), (4, 4, 64)])
+def test_gemm_rope(M, H, Hkv, D):
+    """QKV projection with RoPE + KV-cache write in the GEMM epilogue == gemm + rope_cache (fp32 ref),
+    and bit-identical to the in-tree gemm -> rope_cache kernels."""
+    torch.manual_seed(M + D)
+    Kd = 256
+    N = (H + 2 * Hkv) * D
+    a, w = _rand(M, Kd), _rand(N, Kd, scale=Kd ** -0.5)
+    S, L = 5, 1024
+    slot = torch.randint(0, S, (M,), device=DEV, dtype=torch.int32)
+    pos = torch.randperm(L, device=DEV)[:M].to(torch.int32) if M <= L else \
+        torch.arange(M, device=DEV, dtype=torch.int32) % L
+    if M > L:  # keep (slot, pos) unique
+        slot = (torch.arange(M, device=DEV, dtype=torch.int32) // L).to(torch.int32)
+        S = int(slot.max()) + 1
+    cs = R.rope_table(L, D, 10000.0, device=DEV)
+    kc = torch.zeros(S, Hkv, L, D, device=DEV, dtype=torch.bfloat16)
+    vc = torch.zeros_like(kc)
+    kc2, vc2, kc3, vc3 = kc.clone(), vc.clone(), kc.clone(), vc.clone()
+    got = K.gemm_rope(a, w, pos, cs, H, Hkv, D, slot, kc, vc)
+    ref = R.gemm_rope(a, w, pos, cs, H, Hkv, D, slot, kc2, vc2)
+    _close(got, ref, atol=0.03)
+    _close(kc, kc2, atol=0.03)
+    _close(vc, vc2, atol=0.03)
+    two = K.rope_cache(K.gemm(a, w), pos, cs, H, Hkv, D, slot=slot, k_cache=kc3, v_cache=vc3)
+    assert torch.equal(got, two) and torch.equal(kc, kc3) and torch.equal(vc, vc3)
+
+
+@pytest.mark.parametrize("M", [65, 128, 200])
+def test_gemm_mid_m_in_tree(M):
+    """65..255 rows: the 64x128 weight-streaming tile over ceil(M/64) row blocks with split-K
+    (auto), plain / SwiGLU / residual epilogues, vs the fp32 reference."""
+    torch.manual_seed(M)
+    N, F, Kd = 3072, 1024, 3072
+    a, w = _rand(M, Kd), _rand(N, Kd, scale=Kd ** -0.5)
+    assert K._auto_splits(M, N, Kd) > 1
+    ref = a.float() @ w.float().t()
+    _close(K.gemm(a, w), ref, atol=0.03)
+    resid = _rand(M, N)
+    x = resid.clone()
+    K.gemm(a, w, epi=K.EPI_RESID, resid=x, out=x)
+    _close(x, ref + resid.float(), atol=0.05)
+    gate, up = _rand(F, Kd, scale=Kd ** -0.5), _rand(F, Kd, scale=Kd ** -0.5)
+    got = K.gemm(a, R.interleave_gate_up(gate, up), epi=K.EPI_SWIGLU)
+    _close(got, torch.nn.functional.silu(a.float() @ gate.float().t()) * (a.float() @ up.float().t()), atol=0.03)
 
 
 def test_gemm_strided_a():
@@ -421,29 +472,11 @@ def test_flash_attn_wave_shapes(nw, D, causal):
     _close(got, R.flash_attn_varlen(q, k, v, cu, max(lens), H, Hkv, D, causal), atol=0.02)
 
 
-@pytest.mark.parametrize("M,N,Kd", [(256, 256, 64), (300, 520, 192), (1000, 1032, 768), (2048, 3072, 3072)])
-@pytest.mark.parametrize("epi", [K.EPI_NONE, K.EPI_BIAS, K.EPI_RESID, K.EPI_SWIGLU])
-def test_gemm256_pingpong(M, N, Kd, epi):
-    torch.manual_seed(M * 3 + N + epi)
-    if epi == K.EPI_SWIGLU:
-        N = (N // 32) * 32
-    a, w = _rand(M, Kd), _rand(N, Kd, scale=Kd ** -0.5)
-    bias = _rand(N) if epi in (K.EPI_BIAS, K.EPI_RESID) else None
-    resid = _rand(M, N) if epi == K.EPI_RESID else None
-    lockstep = K.gemm(a, w, bias=bias, epi=epi, resid=resid, tile=4, splits=1)
-    K.lib().da_set_gemm_pingpong(1)
-    try:
-        got = K.gemm(a, w, bias=bias, epi=epi, resid=resid, tile=4, splits=1)
-    finally:
-        K.lib().da_set_gemm_pingpong(0)
-    _close(got, R.gemm(a, w, bias=bias, epi=epi, resid=resid), atol=0.04)
-    assert torch.equal(got, lockstep)  # same K order -> bit-identical
-
-
 @pytest.mark.parametrize("epi", [K.EPI_NONE, K.EPI_BIAS, K.EPI_RESID])
 @pytest.mark.parametrize("inplace", [False, True])
-def test_gemm_blas_prefill(epi, inplace):
-    """Prefill-sized plain GEMMs routed to the platform library (bias / residual as beta*C)."""
+def test_gemm_blas_prefill(epi, inplace, monkeypatch):
+    """Opt-in A/B arm (DA_BLAS_PREFILL=1): plain GEMMs on the platform library (bias / residual as beta*C)."""
+    monkeypatch.setattr(K, "_BLAS_PREFILL", True)
     if inplace and epi != K.EPI_RESID:
         pytest.skip("in-place only applies to the residual form")
     torch.manual_seed(epi)
@@ -457,35 +490,6 @@ def test_gemm_blas_prefill(epi, inplace):
     _close(got, ref, atol=0.04)
     if inplace:
         assert got.data_ptr() == resid.data_ptr()
-
-
-@pytest.mark.parametrize("M,N,Kd", [(256, 256, 64), (300, 520, 192), (1000, 1032, 768), (2048, 3072, 3072),
-                                    (512, 768, 128)])
-@pytest.mark.parametrize("epi", [K.EPI_NONE, K.EPI_BIAS, K.EPI_GELU, K.EPI_RESID, K.EPI_SWIGLU])
-def test_gemm256_w4(M, N, Kd, epi):
-    """4-wave 256x256 kernel (tile 5) vs the fp32 reference and vs the 8-wave kernel."""
-    torch.manual_seed(M * 5 + N + epi)
-    if epi == K.EPI_SWIGLU:
-        N = (N // 32) * 32
-    a, w = _rand(M, Kd), _rand(N, Kd, scale=Kd ** -0.5)
-    bias = _rand(N) if epi in (K.EPI_BIAS, K.EPI_GELU, K.EPI_RESID) else None
-    resid = _rand(M, N) if epi == K.EPI_RESID else None
-    got = K.gemm(a, w, bias=bias, epi=epi, resid=resid, tile=5, splits=1)
-    _close(got, R.gemm(a, w, bias=bias, epi=epi, resid=resid), atol=0.04)
-    for cfg in (1, 2, 3, 5):  # 5-slot ring / split-phase / register-staged: same K order -> bit-identical
-        K.lib().da_set_gemm_w4_cfg(cfg)
-        try:
-            other = K.gemm(a, w, bias=bias, epi=epi, resid=resid, tile=5, splits=1)
-        finally:
-            K.lib().da_set_gemm_w4_cfg(0)
-        assert torch.equal(got, other), cfg
-    # tile 4 + the global switch routes to the same kernel
-    K.lib().da_set_gemm_w4(1)
-    try:
-        again = K.gemm(a, w, bias=bias, epi=epi, resid=resid, tile=4, splits=1)
-    finally:
-        K.lib().da_set_gemm_w4(0)
-    assert torch.equal(got, again)
 
 
 @pytest.mark.parametrize("M,N,Kd", [(2, 3072, 3072), (17, 3072, 8192), (64, 4096, 1024), (64, 8192, 512)])
@@ -540,9 +544,10 @@ def test_gemm_swiglu_blas_route(monkeypatch):
 
 
 @pytest.mark.parametrize("M", [65, 128, 261, 1023])
-def test_gemm_mid_m_blas_route(M):
-    """65..1023 rows go to hipBLASLt (plain, residual, gate/up + SwiGLU) and match the fp32 reference;
-    the in-tree 128x128 tile (explicit tile) still computes the same product."""
+def test_gemm_mid_m_blas_route(M, monkeypatch):
+    """Opt-in A/B arm (DA_BLAS_MID=1): 65..1023 rows on hipBLASLt (plain, residual, gate/up + SwiGLU)
+    match the fp32 reference; the in-tree 128x128 tile (explicit tile) computes the same product."""
+    monkeypatch.setattr(K, "_BLAS_MID", True)
     assert K._blas_mid(M)
     torch.manual_seed(M)
     N, F, Kd = 384, 256, 512
@@ -558,16 +563,6 @@ def test_gemm_mid_m_blas_route(M):
     got = K.gemm(a, R.interleave_gate_up(gate, up), epi=K.EPI_SWIGLU)
     _close(got, torch.nn.functional.silu(a.float() @ gate.float().t()) * (a.float() @ up.float().t()), atol=0.03)
     _close(K.gemm(a, w, tile=1), ref, atol=0.03)
-
-
-def test_mall_prefetch_reads_only():
-    """The side-stream weight prefetch kernel (bench/prefetch_probe.py) leaves its input unchanged."""
-    w = _rand(4099, 256)
-    before = w.clone()
-    K.mall_prefetch(w, 64)
-    K.mall_prefetch(w[:3], 1)
-    torch.cuda.synchronize()
-    assert torch.equal(w, before)
 
 
 @pytest.mark.parametrize("H,Hkv,D,P", [(32, 32, 96, 261), (8, 2, 128, 64), (4, 4, 64, 1), (4, 2, 96, 130)])
