@@ -59,7 +59,8 @@ class Engine:
         from ..index import make_index
         self.index = make_index(index_kind, self.enc_cfg.hidden, self.device, lists=ivf_lists, probes=ivf_probes)
         self._prefix_cache: dict[str, list[int]] = {}
-        self.stats = {"embed_texts": 0, "embed_tokens": 0, "embed_s": 0.0}
+        self.stats = {"embed_texts": 0, "embed_tokens": 0, "embed_s": 0.0, "embed_truncated_texts": 0,
+                      "embed_truncated_tokens": 0}
 
     @property
     def dim(self) -> int:
@@ -77,7 +78,12 @@ class Engine:
         if n == 0:
             return out
         t0 = time.perf_counter()
-        seqs = pack_for_encoder(self.enc_tok, texts, self.enc_cfg.max_pos)
+        trunc0 = (self.stats["embed_truncated_texts"], self.stats["embed_truncated_tokens"])
+        seqs = pack_for_encoder(self.enc_tok, texts, self.enc_cfg.max_pos, self.stats)
+        if self.stats["embed_truncated_texts"] != trunc0[0]:
+            from ..utils import metrics
+            metrics.ENGINE_EMBED_TRUNCATED.labels("texts").inc(self.stats["embed_truncated_texts"] - trunc0[0])
+            metrics.ENGINE_EMBED_TRUNCATED.labels("tokens").inc(self.stats["embed_truncated_tokens"] - trunc0[1])
         order = np.argsort([-len(s) for s in seqs], kind="stable")
         with self.lock:
             i = 0

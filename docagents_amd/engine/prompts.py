@@ -27,6 +27,29 @@ def concatenate_chunks(chunk_texts: list[str]) -> str:
     return "".join(t + "\n" for t in chunk_texts)
 
 
+def dedup_overlap(chunk_texts: list[str], max_overlap: int) -> list[str]:
+    """Drop from every chunk the leading words it shares with the end of the previous chunk (the
+    chunker's sliding-window overlap, 80 words by default). The reference summarizes the raw
+    concatenation (cmd/analysis/main.go:115-122), i.e. ~25 % duplicated words at 400/80; SURVEY §5.7 /
+    Appendix B #7-8: the summary input carries each word span once, in ``ord`` order. Chunks hold
+    single-space-joined words (text/chunker.py), so the overlap is found by exact word match."""
+    out: list[str] = []
+    prev: list[str] = []
+    for i, t in enumerate(chunk_texts):
+        words = t.split()
+        k = 0
+        if i > 0 and max_overlap > 0:
+            for n in range(min(max_overlap, len(prev), len(words)), 0, -1):
+                if words[:n] == prev[-n:]:
+                    k = n
+                    break
+        rest = words[k:]
+        if rest:
+            out.append(" ".join(rest) if k else t)
+        prev = words
+    return out
+
+
 def enrich_for_embedding(filename: str, text: str) -> str:
     """cmd/analysis/main.go:89-93."""
     return f"Document: {filename}\n\n{text}"

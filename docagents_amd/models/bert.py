@@ -159,14 +159,18 @@ class BertEncoder:
         return 2 * self.cfg.param_count()
 
 
-def pack_for_encoder(tok, texts: list[str], max_len: int) -> list[list[int]]:
+def pack_for_encoder(tok, texts: list[str], max_len: int, stats: dict | None = None) -> list[list[int]]:
     """Tokenize with [CLS]/[SEP] and truncate to the encoder's max positions (BERT max 512,
-    SURVEY.md §5.7)."""
+    SURVEY.md §5.7). Truncations are counted in ``stats`` (embed_truncated_texts / _tokens): a
+    400-word enriched chunk can exceed 512 WordPiece tokens."""
     encs = tok.encode_batch(texts, add_special_tokens=True)
     out = []
     for e in encs:
         ids = e.ids
         if len(ids) > max_len:
+            if stats is not None:
+                stats["embed_truncated_texts"] = stats.get("embed_truncated_texts", 0) + 1
+                stats["embed_truncated_tokens"] = stats.get("embed_truncated_tokens", 0) + len(ids) - max_len
             ids = ids[:max_len - 1] + [ids[-1]]
         out.append(ids)
     return out

@@ -189,6 +189,33 @@ DA_EXPORT long long da_ar_clock_khz() {
   return khz;
 }
 
+// Work partition of one call (host side; the kernel follows it): nvec 16-B vectors in rows of
+// AR_TPB, row r owned by workgroup r % grid on every rank; two-shot slices are whole rows. Exported
+// so the CPU protocol model (tests/test_xgmi_protocol.py) runs the exact partition the kernel runs.
+struct ArPlan {
+  long long nvec, rows, slice;
+  int grid;
+};
+static ArPlan ar_plan(long long nbytes, int world, int grid, int twoshot) {
+  ArPlan p;
+  p.nvec = nbytes / 16;
+  p.rows = (p.nvec + AR_TPB - 1) / AR_TPB;
+  // two-shot: whole rows per slice so every slice boundary is a row boundary
+  p.slice = twoshot ? (p.rows + world - 1) / world * AR_TPB : p.nvec;
+  // A message with fewer rows than `grid` launches only workgroups 0..rows-1 (one row each, no
+  // wrap), which keeps the row -> workgroup mapping, and every rank makes the same choice, so the
+  // skipped workgroups' counters stay in step across ranks.
+  p.grid = p.rows < grid ? (int)p.rows : grid;
+  return p;
+}
+
+DA_EXPORT int da_ar_plan(long long nbytes, int world, int grid, int twoshot, long long* out) {
+  if (nbytes <= 0 || nbytes % 16 || world < 1 || grid < 1) return (int)hipErrorInvalidValue;
+  const ArPlan p = ar_plan(nbytes, world, grid, twoshot);
+  out[0] = p.nvec; out[1] = p.rows; out[2] = p.slice; out[3] = p.grid;
+  return 0;
+}
+
 // in/out: nbytes (multiple of 16) on this rank; data/sig: host arrays of `world` device pointers
 // (own + IPC-opened peers); parity_bytes: offset of the second staging half (>= nbytes);
 // grid: fixed per communicator (<= AR_MAX_BLOCKS); dtype 0 = bf16, 1 = fp32.
@@ -203,13 +230,9 @@ DA_EXPORT int da_ar_allreduce(const void* in, void* out, long long nbytes, int d
     d.p[w] = (char*)data[w];
     s.p[w] = (char*)sig[w];
   }
-  const long long nvec = nbytes / 16, rows = (nvec + AR_TPB - 1) / AR_TPB;
-  // two-shot: whole rows per slice so every slice boundary is a row boundary
-  const long long slice = twoshot ? (rows + world - 1) / world * AR_TPB : nvec;
-  // Row r always belongs to workgroup r % grid. A message with fewer rows than `grid` launches only
-  // workgroups 0..rows-1 (one row each, no wrap), which keeps that mapping, and every rank makes the
-  // same choice, so the skipped workgroups' counters stay in step across ranks.
-  if (rows < grid) grid = (int)rows;
+  const ArPlan pl = ar_plan(nbytes, world, grid, twoshot);
+  const long long nvec = pl.nvec, slice = pl.slice;
+  grid = pl.grid;
   if (dtype == 0)
     allreduce_kernel<true><<<grid, AR_TPB, 0, stream>>>(d, s, (const u32x4_t*)in, (u32x4_t*)out, nvec, slice,
                                                         parity_bytes / 16, rank, world, twoshot, timeout_ticks);

@@ -13,7 +13,7 @@ from __future__ import annotations
 import json
 import uuid
 
-from ..engine.prompts import concatenate_chunks, enrich_for_embedding
+from ..engine.prompts import concatenate_chunks, dedup_overlap, enrich_for_embedding
 from ..queue.task import Task
 from ..store.base import STATUS_FAILED, STATUS_READY, Embedding, Summary
 
@@ -21,7 +21,8 @@ from ..store.base import STATUS_FAILED, STATUS_READY, Embedding, Summary
 async def handle_analyze(deps, payload: dict) -> None:
     doc_id = str(uuid.UUID(payload.get("document_id", "")))
     chunks = await deps.store.list_chunks(doc_id)
-    text = concatenate_chunks([c.text for c in chunks])
+    # ord-ordered chunks with the sliding-window overlap removed: each word span summarized once
+    text = concatenate_chunks(dedup_overlap([c.text for c in chunks], deps.config.chunk_overlap))
     summary, key_points = await deps.llm.summarize(text)
     await deps.store.save_summary(doc_id, Summary(doc_id, summary, key_points))
     try:

@@ -60,6 +60,8 @@ ENGINE_COLLECTIVE = _metric("Counter", "da_engine_collective_seconds_total", "ti
 ENGINE_INDEX_ROWS = _metric("Gauge", "da_engine_index_rows", "vector index rows per shard", ["rank"])
 ENGINE_HBM = _metric("Gauge", "da_engine_hbm_bytes", "device memory in use", ["rank", "kind"])
 ENGINE_HEALTHY = _metric("Gauge", "da_engine_healthy", "1 when the watchdog sees no stuck step", [])
+ENGINE_EMBED_TRUNCATED = _metric("Counter", "da_engine_embed_truncated_total",
+                                 "encoder inputs cut at the max position (512): texts and tokens dropped", ["what"])
 ENGINE_LIVE_RANKS = _metric("Gauge", "da_engine_live_ranks", "ranks answering the last liveness all-reduce", [])
 
 

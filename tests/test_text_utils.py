@@ -174,3 +174,35 @@ def test_extract_summary():
     s, kp = extract_summary("Intro line.\n\n- point one\n* point two\nmore text\n  -  three")
     assert s == "Intro line. more text"
     assert kp == ["point one", "point two", "three"]
+
+
+def test_summary_input_has_each_word_span_once():
+    """the analysis agent summarizes ord-ordered chunks with the 80-word
+    sliding-window overlaps removed (the reference duplicates them, cmd/analysis/main.go:115-122)."""
+    from docagents_amd.engine.prompts import concatenate_chunks, dedup_overlap
+    from docagents_amd.text.chunker import Options, chunk_text
+    words = [f"w{i}" for i in range(1234)]
+    chunks = chunk_text(" ".join(words), Options(400, 80))
+    assert len(chunks) == 4
+    raw = concatenate_chunks([c.text for c in chunks]).split()
+    assert len(raw) == 1234 + 3 * 80  # the reference's input: every overlap twice
+    once = concatenate_chunks(dedup_overlap([c.text for c in chunks], 80)).split()
+    assert once == words
+    # no overlap / mismatched neighbours are left alone
+    assert dedup_overlap(["a b c", "d e f"], 80) == ["a b c", "d e f"]
+    assert dedup_overlap(["a b c"], 80) == ["a b c"]
+
+
+def test_encoder_truncation_is_counted():
+    """An enriched chunk longer than BERT's 512 positions is cut, and the cut is counted (not silent)."""
+    import torch
+    from docagents_amd.engine.engine import Engine
+    from docagents_amd.utils import metrics
+    eng = Engine("tiny-enc", "tiny-dec", "cpu", load_llm=False)
+    long = "Document: big.txt\n\n" + " ".join(f"tokenization{i}x" for i in range(700))
+    before = metrics.ENGINE_EMBED_TRUNCATED.labels("texts")._value.get()
+    v = eng.embed([long, "short text"])
+    assert v.shape[0] == 2 and torch.isfinite(v.float()).all()
+    assert eng.stats["embed_truncated_texts"] == 1 and eng.stats["embed_truncated_tokens"] > 0
+    assert metrics.ENGINE_EMBED_TRUNCATED.labels("texts")._value.get() == before + 1
+    assert eng.describe()["embed"]["embed_truncated_texts"] == 1
