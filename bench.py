@@ -97,6 +97,7 @@ def main():
     ap.add_argument("--enc-dtype", default="bf16", choices=["bf16", "fp8"],
                     help="encoder GEMM dtype (fp8 = OCP e4m3 MFMA, BASELINE config 5)")
     ap.add_argument("--no-graphs", action="store_true")
+    ap.add_argument("--breakdown", type=int, default=1, help="1: one extra untimed QA step with per-phase timing")
     ap.add_argument("--seed", type=int, default=0)
     a = ap.parse_args()
 
@@ -183,6 +184,36 @@ def main():
     dt_max = all_reduce_max(dt, dev)
     qps = DP * a.batch * a.steps / dt_max
 
+    # ---- phase breakdown of one extra (untimed) QA step, device-synchronized at phase boundaries ----
+    phases = {}
+    if a.breakdown:
+        sy = torch.cuda.synchronize
+        qs = [tg.question() for _ in range(a.batch)]
+        filters = make_filters(777)
+        sy(); t = time.perf_counter()
+        qv = eng.embed(qs); sy(); phases["embed"] = time.perf_counter() - t; t = time.perf_counter()
+        s_, gid = shard.search(qv, a.top_k, a.min_sim, filters)
+        s_h, id_h = s_.cpu().numpy(), gid.cpu().numpy(); phases["search"] = time.perf_counter() - t
+        t = time.perf_counter()
+        items = [(qs[b], [chunks.get(int(c)) for c in id_h[b][id_h[b] >= 0]], 0.5) for b in range(a.batch)]
+        prompts = [eng.answer_prompt_ids(q, ch, a.max_new) for q, ch, _ in items]
+        phases["prompt_build"] = time.perf_counter() - t
+        g_ = eng.gen
+        g_.sync_phases = True
+        pw0, d0 = g_.stats.get("prefill_wall_s", 0.0), g_.stats["decode_s"]
+        t = time.perf_counter()
+        res = g_.generate(prompts, a.max_new)
+        sy(); tot = time.perf_counter() - t
+        g_.sync_phases = False
+        phases["prefill"] = g_.stats["prefill_wall_s"] - pw0
+        phases["decode"] = g_.stats["decode_s"] - d0
+        t = time.perf_counter()
+        _ = [eng.chat.decode(r.tokens) for r in res]
+        phases["detokenize"] = time.perf_counter() - t
+        phases["generate_other"] = tot - phases["prefill"] - phases["decode"]
+        phases = {k: round(v * 1000, 2) for k, v in phases.items()}
+        log(info, f"QA step phases (ms): {phases}")
+
     # ---- p50 cache-miss latency (one query per GPU, end to end) ----
     lat = []
     if a.latency_reps > 0:
@@ -260,6 +291,7 @@ def main():
         "ingest_docs_per_min_runs": [round(x, 1) for x in ingest_runs],
         "ingest_format": "pdf" if a.pdf_ingest else "txt",
         "prefill_tokens": gen["prefill_tokens"], "decode_steps": gen["decode_steps"],
+        "qa_step_phase_ms": phases or None,
     }
     if R == 0:
         print(json.dumps(out), flush=True)

@@ -57,6 +57,9 @@ class Generator:
         self.states: dict[tuple, DecodeState] = {}
         self.stats = {"prefill_s": 0.0, "decode_s": 0.0, "prefill_tokens": 0, "decode_steps": 0, "decode_tokens": 0,
                       "calls": 0, "shared_prefix_tokens": 0}
+        # phase timing: synchronize the device around prefill / decode so prefill_s / decode_s are
+        # device time (bench breakdown pass); off in serving (a sync per phase costs overlap)
+        self.sync_phases = False
         if self.is_cuda:
             from ..ops import kernels
             c = model.cfg
@@ -176,6 +179,9 @@ class Generator:
             st.pos.copy_(ht[0]); st.lens.copy_(ht[1]); st.slot.copy_(ht[2]); st.active.copy_(ht[3])
             st.start.copy_(ht[4])
             st.tokens.zero_(); st.hist.fill_(-1); st.conf.zero_()
+            if self.sync_phases:
+                torch.cuda.synchronize(dev)
+            t_pf = time.perf_counter()
             P = self.shared_prefix_len(prompts)
             if P:
                 # the shared head once (into row 0's slot), then only the suffixes, attending to the
@@ -199,6 +205,9 @@ class Generator:
             # padded rows: keep them inside the dummy slot's first positions
             if B > n:
                 st.pos[n:].zero_(); st.lens[n:].fill_(1)
+            if self.sync_phases:
+                torch.cuda.synchronize(dev)
+                self.stats["prefill_wall_s"] = self.stats.get("prefill_wall_s", 0.0) + time.perf_counter() - t_pf
             t0 = time.perf_counter()
             steps = max_new - 1
             if steps > 0:

@@ -114,7 +114,9 @@ gemm8p_kernel(GemmArgs p) {
   } while (0)
 
   // ---- fragment read offsets: row wg*QR + i*16 + fr of an A half (wn*32 + j*16 + fr of a B half),
-  //      16-B chunk kk*4 + fg, swizzled by ((row >> 1) & 7) = fr >> 1 (i*16, wg*QR, wn*32 keep it)
+  //      16-B chunk kk*4 + fg, swizzled by ((row >> 1) & 7) = fr >> 1 (i*16, wg*QR, wn*32 keep it).
+  //      (v_mfma_f32_16x16x32_bf16; the 32x32x16 shape with the same per-wave tile measured 8 %
+  //      slower: the same cycles at a lower clock, profiles/r2/ab_gemm8p_mfma_shape.txt)
   int aoff[2], boff[2];
 #pragma unroll
   for (int kk = 0; kk < 2; ++kk) {
