@@ -137,6 +137,7 @@ async def run(gw: str, docs: int, words: int, queries: int, concurrency: int, to
 
         t0 = time.perf_counter()
         ids = list(await asyncio.gather(*[upload(i) for i in range(docs)]))
+        t_up = time.perf_counter()
 
         async def poll(doc_id):
             while time.perf_counter() - t0 < ingest_timeout:
@@ -150,6 +151,11 @@ async def run(gw: str, docs: int, words: int, queries: int, concurrency: int, to
         ok = await asyncio.gather(*[poll(d) for d in ids])
         t_ingest = (max(ready_at.values()) - t0) if ready_at else None
         ready = [d for d, o in zip(ids, ok) if o]
+        # ingest timeline: when the uploads were all accepted and how the summaries trickled in
+        rt = sorted(v - t0 for v in ready_at.values())
+        timeline = {"uploads_accepted_s": _r(t_up - t0), "first_ready_s": _r(rt[0]) if rt else None,
+                    "median_ready_s": _r(statistics.median(rt)) if rt else None,
+                    "last_ready_s": _r(rt[-1]) if rt else None}
 
         # ---- queries ----
         qs = [f"What does {tg.word()} say about {tg.word()} and {tg.word()}?" for _ in range(queries)]
@@ -195,8 +201,54 @@ async def run(gw: str, docs: int, words: int, queries: int, concurrency: int, to
         "cache_hit_gateway_raw_p50_ms": _r(statistics.median(raw_gw) if raw_gw else None),
         "cache_hit_query_service_raw_p50_ms": _r(statistics.median(raw_q) if raw_q else None),
         "cache_hit_handler_mean_ms": _r(handler_ms),
-        "concurrency": concurrency, "top_k": top_k,
+        "concurrency": concurrency, "top_k": top_k, "ingest_timeline": timeline,
     }
+
+
+def _scrape(url: str, names: tuple[str, ...]) -> dict:
+    """Mean of each Prometheus histogram ``name{label}`` (sum / count) at a /metrics URL."""
+    try:
+        text = httpx.get(url, timeout=5.0).text
+    except Exception as e:  # noqa: BLE001
+        return {"error": repr(e)}
+    acc: dict = {}
+    for ln in text.splitlines():
+        for n in names:
+            for suf in ("_sum", "_count"):
+                if ln.startswith(n + suf):
+                    lab = ln[len(n + suf):].split(" ")[0]
+                    acc.setdefault(n + lab, {})[suf] = float(ln.split()[-1])
+    return {k: {"n": int(v.get("_count", 0)), "mean_ms": _r(v["_sum"] / v["_count"] * 1000.0)}
+            for k, v in acc.items() if v.get("_count")}
+
+
+async def _engine_stats(url: str) -> dict:
+    from docagents_amd.engine.rpc import EngineClient
+    c = EngineClient(url, timeout=30.0)
+    try:
+        await c.connect(retries=2)
+        st = await c.call("stats")
+    finally:
+        await c.close()
+    r0 = st["ranks"][0] if st.get("ranks") else {}
+    return {"exec": st.get("exec"), "batching": st.get("batching"), "gen": r0.get("gen"), "embed": r0.get("embed"),
+            "sched": r0.get("sched")}
+
+
+def diagnostics(base: int, parsers: int = 2, analyzers: int = 2, engine_url: str = "") -> dict:
+    """Where the time went inside the deploy stack: per-service handler latencies (worker /metrics),
+    query stages, and the engine's batching + generator counters."""
+    out = {"query": _scrape(f"http://127.0.0.1:{base + 1}/metrics", ("da_query_stage_seconds",))}
+    for i in range(parsers):
+        out[f"parser-{i}"] = _scrape(f"http://127.0.0.1:{base + 2 + 10 * i}/metrics", ("da_task_seconds",))
+    for i in range(analyzers):
+        out[f"analysis-{i}"] = _scrape(f"http://127.0.0.1:{base + 3 + 10 * i}/metrics", ("da_task_seconds",))
+    if engine_url:
+        try:
+            out["engine"] = asyncio.run(_engine_stats(engine_url))
+        except Exception as e:  # noqa: BLE001
+            out["engine"] = {"error": repr(e)}
+    return out
 
 
 def _r(x):
@@ -243,10 +295,25 @@ def main(argv=None):
                                      "--log-dir", sup_log], env=env, stdout=subprocess.DEVNULL,
                                     stderr=subprocess.DEVNULL, start_new_session=True)
         gw = f"http://127.0.0.1:{port}"
+        if sup_log:  # the whole stack, not just the gateway (workers start after it)
+            t0 = time.time()
+            while True:
+                try:
+                    with open(os.path.join(sup_log, "status.json")) as f:
+                        if json.load(f).get("ready"):
+                            break
+                except (OSError, ValueError):
+                    pass
+                if time.time() - t0 > 900 or proc.poll() is not None:
+                    raise RuntimeError(f"deploy stack did not come up; see {sup_log}")
+                time.sleep(0.25)
     try:
         qurl = f"http://127.0.0.1:{int(gw.rsplit(':', 1)[1]) + 1}/api/query" if proc is not None else a.query_url
         out = asyncio.run(run(gw, a.docs, a.words, a.queries, a.concurrency, a.top_k, a.seed, query_url=qurl))
         out["topology"] = a.topology if proc is not None else "external"
+        if proc is not None and a.topology == "deploy":
+            eng = env.get("ENGINE_URL", "") if env.get("LLM_PROVIDER") == "engine" else ""
+            out["diag"] = diagnostics(port, engine_url=eng)
     finally:
         if proc is not None:
             proc.terminate()

@@ -75,9 +75,12 @@ class Config:
     worker_concurrency: int = field(default=0, metadata={"env": "WORKER_CONCURRENCY"})  # 0 -> auto
     engine_continuous: bool = field(default=True, metadata={"env": "ENGINE_CONTINUOUS"})
     engine_cb_steps: int = field(default=8, metadata={"env": "ENGINE_CB_STEPS"})
+    engine_admit_tokens: int = field(default=0, metadata={"env": "ENGINE_ADMIT_TOKENS"})  # 0 -> 4 prefill chunks
     # --- new keys: durable vector shards (index/wal.py) ---
     index_dir: str = field(default="", metadata={"env": "INDEX_DIR"})  # "" -> DATA_DIR/index; "none" -> off
     index_checkpoint_s: float = field(default=300.0, metadata={"env": "INDEX_CHECKPOINT_S"})
+    # startup sweep: a "processing" document younger than this is in flight, not stuck
+    sweep_stuck_after_s: float = field(default=600.0, metadata={"env": "SWEEP_STUCK_AFTER_S"})
     index_fsync: bool = field(default=True, metadata={"env": "INDEX_FSYNC"})
 
     def database_url(self) -> str:

@@ -130,6 +130,7 @@ class Supervisor:
     def __init__(self, procs: list[Proc], log_dir: str, max_backoff: float = 30.0):
         self.procs, self.log_dir, self.max_backoff = procs, log_dir, max_backoff
         self.stopping = False
+        self.ready = False  # every process started and healthy (clients wait for this, not the gateway)
         os.makedirs(log_dir, exist_ok=True)
 
     def _status(self):
@@ -137,7 +138,7 @@ class Supervisor:
                "restarts": p.restarts} for p in self.procs]
         tmp = os.path.join(self.log_dir, "status.json.tmp")
         with open(tmp, "w") as f:
-            json.dump({"supervisor": os.getpid(), "procs": st}, f)
+            json.dump({"supervisor": os.getpid(), "ready": self.ready, "procs": st}, f)
         os.replace(tmp, os.path.join(self.log_dir, "status.json"))
 
     def start_all(self) -> bool:
@@ -150,6 +151,8 @@ class Supervisor:
                 return False
             print(f"[deploy] {p.name} up", file=sys.stderr, flush=True)
             self._status()
+        self.ready = True
+        self._status()
         return True
 
     def tick(self):

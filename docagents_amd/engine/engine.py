@@ -156,15 +156,22 @@ class Engine:
         if getattr(self, "_sched", None) is None:
             from .generator import ContinuousScheduler
             self._sched = ContinuousScheduler(self.gen, B=self.gen.max_batch,
-                                              max_new_cap=max(self.max_new_tokens, self.summary_max_new))
+                                              max_new_cap=max(self.max_new_tokens, self.summary_max_new),
+                                              max_admit_tokens=getattr(self, "admit_tokens", None))
         return self._sched
 
     def cb_tick(self, new_items, steps: int | None = None):
-        """Submit [(tag, (question, chunk_ids, quality))] and run one scheduler tick.
-        Returns ([(tag, answer, confidence)], still_busy)."""
+        """Submit new work and run one scheduler tick. An item is ``(tag, (question, chunk_ids,
+        quality))`` (an Answer) or ``(tag, {"ids": prompt_ids, "max_new": n})`` (a prebuilt prompt:
+        summary windows). Returns ([(tag, text, confidence)], still_busy); a prompt item's
+        confidence is its mean token probability."""
         sch = self.scheduler
-        for tag, (q, ch, quality) in new_items:
-            sch.submit(self.answer_prompt_ids(q, ch, self.max_new_tokens), self.max_new_tokens, (tag, quality))
+        for tag, it in new_items:
+            if isinstance(it, dict):
+                sch.submit(it["ids"], int(it.get("max_new") or self.summary_max_new), (tag, 1.0))
+            else:
+                q, ch, quality = it
+                sch.submit(self.answer_prompt_ids(q, ch, self.max_new_tokens), self.max_new_tokens, (tag, quality))
         with self.lock:
             done = sch.tick(steps)
         out = [(tag, self.chat.decode(r.tokens), float(quality) * r.mean_prob) for (tag, quality), r in done]
@@ -177,16 +184,19 @@ class Engine:
         return self.answer_many([(question, [ids], quality)], max_new)[0] if ids else \
             self.answer_many([(question, [], quality)], max_new)[0]
 
-    def summarize_many(self, texts: list[str], max_new: int | None = None) -> list[tuple[str, list[str]]]:
-        """Summarize each text; texts longer than the decoder context are summarized map-reduce:
-        window summaries (batched) then one reduce summary over them."""
-        max_new = max_new or self.summary_max_new
+    def _summary_frame(self, max_new: int):
         head = self._cached_ids(f"<|system|>\n{P.SUMMARIZE_SYSTEM}<|end|>\n<|user|>\n")
         tail = self._cached_ids("<|end|>\n<|assistant|>\n")
-        budget = self.context_budget(max_new) - len(head) - len(tail)
-        all_ids = [self._ids(t) for t in texts]
+        return head, tail, self.context_budget(max_new) - len(head) - len(tail)
+
+    def summary_windows(self, texts: list[str], max_new: int | None = None):
+        """Map step of summarize: one prompt per text, or one per context-sized window of a text
+        longer than the decoder context. Returns (prompts, owner) with owner[j] = (text index,
+        is_partial). CPU only (tokenization), so the server runs it off the GPU thread."""
+        head, tail, budget = self._summary_frame(max_new or self.summary_max_new)
         windows, owner = [], []
-        for i, ids in enumerate(all_ids):
+        for i, t in enumerate(texts):
+            ids = self._ids(t)
             if len(ids) <= budget:
                 windows.append(head + ids + tail)
                 owner.append((i, False))
@@ -194,6 +204,18 @@ class Engine:
                 for s in range(0, len(ids), budget):
                     windows.append(head + ids[s:s + budget] + tail)
                     owner.append((i, True))
+        return windows, owner
+
+    def summary_reduce_prompts(self, partial: dict[int, list[str]], max_new: int | None = None):
+        """Reduce step: one prompt over the joined window summaries of each long text."""
+        head, tail, budget = self._summary_frame(max_new or self.summary_max_new)
+        return [(i, head + self._ids("\n".join(parts))[:budget] + tail) for i, parts in partial.items()]
+
+    def summarize_many(self, texts: list[str], max_new: int | None = None) -> list[tuple[str, list[str]]]:
+        """Summarize each text; texts longer than the decoder context are summarized map-reduce:
+        window summaries (batched) then one reduce summary over them."""
+        max_new = max_new or self.summary_max_new
+        windows, owner = self.summary_windows(texts, max_new)
         with self.lock:
             res = self.gen.generate(windows, max_new)
         partial: dict[int, list[str]] = {}
@@ -205,14 +227,10 @@ class Engine:
             else:
                 final[i] = txt
         if partial:
-            red_ids, red_owner = [], []
-            for i, parts in partial.items():
-                joined = self._ids("\n".join(parts))[:budget]
-                red_ids.append(head + joined + tail)
-                red_owner.append(i)
+            red = self.summary_reduce_prompts(partial, max_new)
             with self.lock:
-                rres = self.gen.generate(red_ids, max_new)
-            for i, r in zip(red_owner, rres):
+                rres = self.gen.generate([p for _, p in red], max_new)
+            for (i, _), r in zip(red, rres):
                 final[i] = self.chat.decode(r.tokens)
         return [extract_summary(final[i]) for i in range(len(texts))]
 
@@ -222,5 +240,7 @@ class Engine:
              "dim": self.dim, "index": self.index.kind, "index_rows": len(self.index)}
         if self.gen is not None:
             d["gen"] = dict(self.gen.stats)
+            if getattr(self, "_sched", None) is not None:
+                d["sched"] = dict(self._sched.stats)
         d["embed"] = dict(self.stats)
         return d

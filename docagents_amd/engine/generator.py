@@ -275,7 +275,10 @@ class ContinuousScheduler:
         self.B = B or gen.max_batch
         self.cap = max(1, max_new_cap)
         self.chunk_steps = chunk_steps
-        self.max_admit_tokens = max_admit_tokens or gen.max_prefill_tokens
+        # prompt tokens admitted per tick (prefilled in max_prefill_tokens chunks): a burst of long
+        # prompts (a batch of summaries) joins in one or two ticks instead of trickling in at one
+        # prefill chunk per tick, which would stretch the decode of the last-admitted rows
+        self.max_admit_tokens = max_admit_tokens or 4 * gen.max_prefill_tokens
         self.st = DecodeState(self.m, self.B, self.cap, gen.temperature, gen.seed, gen.eos)
         self.rows: list = [None] * self.B        # row -> (tag, slot, budget)
         self.pending: collections.deque = collections.deque()

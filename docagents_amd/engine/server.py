@@ -22,6 +22,7 @@ import traceback
 import numpy as np
 import torch
 
+from ..text.preprocess import extract_summary
 from ..utils import faults, metrics
 from .observe import StepProfiler, Watchdog, device_memory
 from .rpc import pack, parse_url, read_frame
@@ -127,7 +128,8 @@ class EngineGroup:
             # continuous batching: TP ranks all run every sequence (identical schedulers); DP
             # ranks take the new items round-robin by tag and run their own schedulers
             tp = getattr(self, "tensor_parallel", False)
-            mine = [(t, self._answer_item(it)) for t, it in a["items"] if tp or t % self.world == self.rank]
+            mine = [(t, it if "ids" in it else self._answer_item(it)) for t, it in a["items"]
+                    if tp or t % self.world == self.rank]
             if mine:
                 faults.maybe_fail("engine.generate")
             done, busy = e.cb_tick(mine, a.get("steps"))
@@ -250,6 +252,7 @@ class EngineServer:
         self.queues: dict[str, asyncio.Queue] = {}
         self.max_batch_items = max_batch_items
         self.stats = {m: {"batches": 0, "items": 0, "busy_s": 0.0} for m in self.BATCHED}
+        self.exec_stats: dict[str, list] = {}
         self.server = None
         self.watchdog = Watchdog(step_timeout_s, hard_timeout_s, log)
         self.profiler = profiler or StepProfiler(rank=group.rank)
@@ -264,6 +267,10 @@ class EngineServer:
         self._cb_futs: dict = {}
         self._cb_tag = 0
         self._cb_wake = asyncio.Event()
+        self._search_q: list = []
+        self._search_wake = asyncio.Event()
+        # CPU-side work of a request (prompt tokenization) stays off the GPU thread
+        self.cpu = cf.ThreadPoolExecutor(max_workers=2, thread_name_prefix="engine-cpu")
 
     def _run_step(self, cmd, args):
         """Executed on the GPU thread: watchdog + optional torch.profiler + step metrics."""
@@ -272,7 +279,11 @@ class EngineServer:
         try:
             return self.profiler.run(cmd, self.group.run, cmd, args)
         finally:
-            metrics.ENGINE_STEP.labels(cmd).observe(time.perf_counter() - t0)
+            dt = time.perf_counter() - t0
+            metrics.ENGINE_STEP.labels(cmd).observe(dt)
+            ex = self.exec_stats.setdefault(cmd, [0, 0.0])  # time ON the GPU thread (no queueing)
+            ex[0] += 1
+            ex[1] += dt
             self.watchdog.end()
             self._account(cmd)
 
@@ -311,6 +322,74 @@ class EngineServer:
             futs.append(f)
         self._cb_wake.set()
         return await asyncio.gather(*futs)
+
+    async def _cb_summarize(self, texts):
+        """Summaries through the continuous scheduler (map windows, then reduce prompts for texts
+        longer than the context): a document arriving while others are being summarized or answers
+        are decoding joins the running batch at the next tick instead of waiting for it to drain.
+        Tokenization runs on a CPU thread, not on the GPU thread."""
+        e = self.group.engine
+        loop = asyncio.get_running_loop()
+        windows, owner = await loop.run_in_executor(self.cpu, e.summary_windows, texts)
+        res = await self._cb_submit([{"ids": w, "max_new": e.summary_max_new} for w in windows])
+        partial, final = {}, {}
+        for (i, is_part), (txt, _) in zip(owner, res):
+            if is_part:
+                partial.setdefault(i, []).append(txt)
+            else:
+                final[i] = txt
+        if partial:
+            red = await loop.run_in_executor(self.cpu, e.summary_reduce_prompts, partial)
+            rres = await self._cb_submit([{"ids": p, "max_new": e.summary_max_new} for _, p in red])
+            for (i, _), (txt, _) in zip(red, rres):
+                final[i] = txt
+        metrics.ENGINE_ITEMS.labels("summarize").inc(len(texts))
+        return [extract_summary(final[i]) for i in range(len(texts))]
+
+    async def _search_enqueue(self, args):
+        fut = asyncio.get_running_loop().create_future()
+        self._search_q.append((args, fut))
+        self._search_wake.set()
+        return await fut
+
+    async def _search_loop(self):
+        """Search micro-batching: the queries that queued while the GPU thread was busy run as ONE
+        index scan per (k, min_sim) group, with per-query document filters (the index takes a
+        filter list per query row)."""
+        while True:
+            if not self._search_q:
+                self._search_wake.clear()
+                await self._search_wake.wait()
+            reqs, self._search_q = self._search_q, []
+            groups: dict = {}
+            for a, f in reqs:
+                groups.setdefault((int(a["k"]), float(a["min_sim"]), a.get("filters") is None), []).append((a, f))
+            for (k, thr, nof), g in groups.items():
+                vecs = [np.asarray(a["vecs"], dtype=np.float32).reshape(-1, self.group.engine.dim) for a, _ in g]
+                filters = None
+                if not nof:
+                    filters = [flt for (a, _), v in zip(g, vecs) for flt in (a["filters"] * v.shape[0]
+                                                                             if len(a["filters"]) == 1
+                                                                             else a["filters"])]
+                t0 = time.perf_counter()
+                try:
+                    s, ids = await self._gpu("search", {"vecs": np.concatenate(vecs), "k": k, "min_sim": thr,
+                                                        "filters": filters})
+                except Exception as e:  # noqa: BLE001
+                    for _, f in g:
+                        if not f.done():
+                            f.set_exception(e)
+                    continue
+                st = self.stats.setdefault("search", {"batches": 0, "items": 0, "busy_s": 0.0})
+                st["batches"] += 1
+                st["items"] += len(g)
+                st["busy_s"] += time.perf_counter() - t0
+                metrics.ENGINE_BATCH_SIZE.labels("search").observe(len(g))
+                o = 0
+                for (_, f), v in zip(g, vecs):
+                    if not f.done():
+                        f.set_result((s[o:o + v.shape[0]], ids[o:o + v.shape[0]]))
+                    o += v.shape[0]
 
     async def _cb_loop(self):
         """Tick the decode scheduler while it has work; new answers join at the next tick."""
@@ -413,7 +492,10 @@ class EngineServer:
             vecs = await self._enqueue(key, list(args["texts"]), args.get("preprocess", True))
             return {"vecs": np.asarray(vecs, dtype=np.float32)}
         if method == "summarize":
-            res = await self._enqueue("summarize", list(args["texts"]))
+            if self.continuous:
+                res = await self._cb_summarize(list(args["texts"]))
+            else:
+                res = await self._enqueue("summarize", list(args["texts"]))
             return {"results": [[s, list(kp)] for s, kp in res]}
         if method == "answer":
             if self.continuous:
@@ -422,7 +504,7 @@ class EngineServer:
                 res = await self._enqueue("answer", list(args["items"]))
             return {"results": [[a, float(c)] for a, c in res]}
         if method == "search":
-            s, ids = await self._gpu("search", args)
+            s, ids = await self._search_enqueue(args)
             return {"scores": s, "keys": ids}
         if method == "embed_index":
             res = await self._enqueue("embed_index", [(str(args["doc_id"]), np.asarray(args["keys"], dtype=np.int64),
@@ -432,7 +514,8 @@ class EngineServer:
             return await self._gpu(method, args)
         if method == "stats":
             st = await self._gpu("stats", {})
-            return {"ranks": st, "batching": self.stats}
+            return {"ranks": st, "batching": self.stats,
+                    "exec": {k: {"n": n, "s": round(t, 4)} for k, (n, t) in self.exec_stats.items()}}
         if method == "health":
             return dict(self.watchdog.state(), live_ranks=self.live_ranks, world=self.group.world)
         raise ValueError(f"unknown method {method!r}")
@@ -473,6 +556,7 @@ class EngineServer:
         self.watchdog.start()
         if self.continuous:
             self.cb_task = asyncio.ensure_future(self._cb_loop())
+        self.search_task = asyncio.ensure_future(self._search_loop())
         if self.liveness_s > 0 and self.group.world > 1:
             self.liveness_task = asyncio.ensure_future(self._liveness_loop())
         kind, addr = parse_url(url)

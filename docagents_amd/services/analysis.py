@@ -20,6 +20,13 @@ from ..store.base import STATUS_FAILED, STATUS_READY, Embedding, Summary
 
 async def handle_analyze(deps, payload: dict) -> None:
     doc_id = str(uuid.UUID(payload.get("document_id", "")))
+    if not payload.get("reindex"):
+        # a duplicate delivery (a redelivered or re-driven task) of a finished document is a no-op
+        try:
+            if (await deps.store.get_document(doc_id)).status == STATUS_READY:
+                return
+        except Exception:  # noqa: BLE001 - a missing document fails below, as before
+            pass
     chunks = await deps.store.list_chunks(doc_id)
     # ord-ordered chunks with the sliding-window overlap removed: each word span summarized once
     text = concatenate_chunks(dedup_overlap([c.text for c in chunks], deps.config.chunk_overlap))

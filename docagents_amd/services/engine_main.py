@@ -55,6 +55,8 @@ def main(argv=None) -> int:
                  summary_max_new=cfg.summary_max_new_tokens, index_kind=cfg.index_kind, ivf_lists=cfg.ivf_lists,
                  ivf_probes=cfg.ivf_probes, max_seq=4096 if dev.type == "cuda" else 1024,
                  enc_dtype="fp8" if cfg.dtype == "fp8" else "bf16")
+    if cfg.engine_admit_tokens > 0:
+        eng.admit_tokens = cfg.engine_admit_tokens
     index_dir = a.index_dir if a.index_dir is not None else cfg.index_dir_path()
     shard_log = None
     if index_dir and index_dir != "none":

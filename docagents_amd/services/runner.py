@@ -98,15 +98,23 @@ def _attach_tokenizer(deps):
 async def startup_sweep(deps):
     """Re-drive documents stuck in 'processing' (their analyze task was lost), and 'ready' documents
     whose vectors are missing from the engine's shards (e.g. an engine restarted without its
-    index directory): both get a fresh analyze task."""
+    index directory): both get a fresh analyze task. Only documents older than SWEEP_STUCK_AFTER_S
+    count as stuck: a document uploaded while this worker was starting is in flight, not lost
+    (the broker redelivers an unacked task itself)."""
     if not hasattr(deps.store, "list_documents") or deps.queue is None:
         return
+    import datetime as dt
     import json
 
     from ..queue.task import TASK_ANALYZE, Task, enqueue_with_retry
+    cutoff = dt.datetime.now(dt.timezone.utc) - dt.timedelta(
+        seconds=getattr(getattr(deps, "config", None), "sweep_stuck_after_s", 600.0))
     try:
         docs = await deps.store.list_documents("processing")
         for d in docs:
+            ca = d.created_at
+            if ca is not None and (ca if ca.tzinfo else ca.replace(tzinfo=dt.timezone.utc)) > cutoff:
+                continue
             chunks = await deps.store.list_chunks(d.id)
             if chunks:
                 body = json.dumps({"document_id": d.id, "chunk_ids": [c.id for c in chunks]}).encode()
@@ -118,7 +126,8 @@ async def startup_sweep(deps):
             for d in await deps.store.list_documents("ready"):
                 chunks = await deps.store.list_chunks(d.id)
                 if chunks and have.get(d.id, 0) < len(chunks):
-                    body = json.dumps({"document_id": d.id, "chunk_ids": [c.id for c in chunks]}).encode()
+                    body = json.dumps({"document_id": d.id, "chunk_ids": [c.id for c in chunks],
+                                       "reindex": True}).encode()
                     await enqueue_with_retry(deps.queue, Task(type=TASK_ANALYZE, payload=body), 3, 0.2)
                     deps.log.info("re-enqueued document with missing vectors", "document_id", d.id,
                                   "indexed", have.get(d.id, 0), "chunks", len(chunks))

@@ -181,3 +181,44 @@ def test_startup_sweep_reenqueues_ready_docs_without_vectors(tmp_path):
     import json
     sent = [json.loads(t.payload)["document_id"] for t in deps.queue.sent]
     assert sent == [docs[1]]
+
+
+def test_startup_sweep_skips_in_flight_documents_and_analyze_is_idempotent(tmp_path):
+    """A 'processing' document younger than SWEEP_STUCK_AFTER_S is in flight (a worker starting
+    while uploads arrive must not duplicate its task); an older one is re-driven; a duplicate
+    analyze delivery of a ready document is a no-op."""
+    import types
+
+    from docagents_amd.services.analysis import handle_analyze
+    from docagents_amd.services.runner import startup_sweep
+    from docagents_amd.store.base import STATUS_READY, Chunk
+    from docagents_amd.store.sqlite_store import CompositeStore, SqliteMeta
+    from docagents_amd.utils.log import discard
+
+    class Q:
+        def __init__(self):
+            self.sent = []
+
+        async def enqueue(self, task):
+            self.sent.append(task)
+
+    store = CompositeStore(SqliteMeta(str(tmp_path / "m.sqlite3")), None)
+
+    async def mk():
+        d = await store.create_document("p.txt")
+        await store.save_chunks(d.id, [Chunk(index=0, text="x")])
+        return d.id
+    doc = asyncio.run(mk())
+    import json
+    for grace, want in ((600.0, []), (-1.0, [doc])):
+        deps = types.SimpleNamespace(store=store, queue=Q(), log=discard(),
+                                     config=types.SimpleNamespace(sweep_stuck_after_s=grace))
+        asyncio.run(startup_sweep(deps))
+        assert [json.loads(t.payload)["document_id"] for t in deps.queue.sent] == want
+
+    class Boom:
+        async def summarize(self, text):
+            raise AssertionError("a ready document must not be summarized again")
+    asyncio.run(store.update_document_status(doc, STATUS_READY))
+    deps = types.SimpleNamespace(store=store, llm=Boom(), config=types.SimpleNamespace(chunk_overlap=0))
+    asyncio.run(handle_analyze(deps, {"document_id": doc}))

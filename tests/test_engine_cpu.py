@@ -279,6 +279,67 @@ def test_engine_server_continuous_batching(eng):
     asyncio.run(go())
 
 
+def test_continuous_summaries_match_wave_summaries():
+    """Summaries through the continuous scheduler (map windows + reduce for a text longer than the
+    context) give the same text as the whole-batch path, with answers decoding alongside."""
+    from docagents_amd.engine.rpc import EngineClient
+    from docagents_amd.engine.server import EngineGroup, EngineServer
+    from docagents_amd.providers import RemoteLLM
+    from docagents_amd.utils.log import discard
+    e = Engine("tiny-enc", "tiny-dec", "cpu", max_batch=4, max_seq=512, max_new_tokens=5, summary_max_new=6,
+               temperature=0.0, use_graphs=False)
+    texts = ["alpha beta gamma " * 5, "delta epsilon " * 3, "word " * 1200, "zeta eta theta iota"]
+    want = e.summarize_many(texts)
+    wins, owner = e.summary_windows(texts)
+    assert sum(1 for i, part in owner if part and i == 2) >= 2  # the long text is map-reduced
+
+    async def go():
+        srv = EngineServer(EngineGroup(e), discard(), continuous=True, cb_steps=2)
+        port = _port()
+        await srv.start(f"tcp://127.0.0.1:{port}")
+        cl = await EngineClient(f"tcp://127.0.0.1:{port}").connect()
+        llm = RemoteLLM(cl)
+        outs = await asyncio.gather(*[llm.summarize(t) for t in texts],
+                                    *[llm.answer(f"q{i}?", "ctx " * (i + 2), 1.0) for i in range(3)])
+        await cl.close()
+        srv.server.close()
+        return outs[:len(texts)]
+    got = asyncio.run(go())
+    assert [(s, list(kp)) for s, kp in got] == [(s, list(kp)) for s, kp in want]
+    # every slot is back except the dummy and the cached prompt heads
+    assert not e.scheduler.busy() and len(e.gen.cache.free) == e.gen.cache.slots - 1 - len(e.scheduler.heads)
+
+
+def test_engine_search_microbatch_matches_single_searches(eng):
+    """Concurrent searches (mixed document filters, one without) coalesce into fewer index scans
+    and return exactly what each search returns alone."""
+    from docagents_amd.engine.rpc import EngineClient
+    from docagents_amd.engine.server import EngineGroup, EngineServer
+    from docagents_amd.utils.log import discard
+
+    async def go():
+        srv = EngineServer(EngineGroup(eng), discard())
+        port = _port()
+        await srv.start(f"tcp://127.0.0.1:{port}")
+        cl = await EngineClient(f"tcp://127.0.0.1:{port}").connect()
+        u = _unit(24, eng.dim, 11).numpy()
+        for j, d in enumerate(("sA", "sB", "sC")):
+            await cl.call("index_add", doc_id=d, keys=np.arange(100 * j, 100 * j + 8), vecs=u[8 * j:8 * j + 8])
+        qs = _unit(9, eng.dim, 12).numpy()
+        flt = [["sA"], ["sB", "sC"], None, ["sC"], ["sA", "sB", "sC"], ["sB"], None, ["sA"], ["sC"]]
+        args = [dict(vecs=qs[i:i + 1], filters=None if f is None else [f], k=3, min_sim=-1.0)
+                for i, f in enumerate(flt)]
+        alone = [await cl.call("search", **a) for a in args]
+        b0 = srv.stats["search"]["batches"]
+        together = await asyncio.gather(*[cl.call("search", **a) for a in args])
+        assert srv.stats["search"]["batches"] - b0 < len(args)
+        for x, y in zip(alone, together):
+            assert np.array_equal(x["keys"], y["keys"]) and np.allclose(x["scores"], y["scores"])
+        await cl.close()
+        srv.server.close()
+    asyncio.run(go())
+
+
 def test_config_bool_parsing():
     from docagents_amd.config import load
     assert load({"ENGINE_CONTINUOUS": "false"}).engine_continuous is False
