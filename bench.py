@@ -185,33 +185,41 @@ def main():
     qps = DP * a.batch * a.steps / dt_max
 
     # ---- phase breakdown of one extra (untimed) QA step, device-synchronized at phase boundaries ----
-    phases = {}
-    if a.breakdown:
-        sy = torch.cuda.synchronize
-        qs = [tg.question() for _ in range(a.batch)]
-        filters = make_filters(777)
+    def breakdown(B: int, seed: int) -> dict:
+        sy = torch.cuda.synchronize if dev.type == "cuda" else (lambda: None)
+        ph = {}
+        qs = [tg.question() for _ in range(B)]
+        filters = make_filters(seed)
         sy(); t = time.perf_counter()
-        qv = eng.embed(qs); sy(); phases["embed"] = time.perf_counter() - t; t = time.perf_counter()
+        qv = eng.embed(qs); sy(); ph["embed"] = time.perf_counter() - t; t = time.perf_counter()
         s_, gid = shard.search(qv, a.top_k, a.min_sim, filters)
-        s_h, id_h = s_.cpu().numpy(), gid.cpu().numpy(); phases["search"] = time.perf_counter() - t
+        s_h, id_h = s_.cpu().numpy(), gid.cpu().numpy(); ph["search"] = time.perf_counter() - t
         t = time.perf_counter()
-        items = [(qs[b], [chunks.get(int(c)) for c in id_h[b][id_h[b] >= 0]], 0.5) for b in range(a.batch)]
+        items = [(qs[b], [chunks.get(int(c)) for c in id_h[b][id_h[b] >= 0]], 0.5) for b in range(B)]
         prompts = [eng.answer_prompt_ids(q, ch, a.max_new) for q, ch, _ in items]
-        phases["prompt_build"] = time.perf_counter() - t
+        ph["prompt_build"] = time.perf_counter() - t
         g_ = eng.gen
         g_.sync_phases = True
-        pw0, d0 = g_.stats.get("prefill_wall_s", 0.0), g_.stats["decode_s"]
+        pw0, d0, st0 = g_.stats.get("prefill_wall_s", 0.0), g_.stats["decode_s"], g_.stats["decode_steps"]
         t = time.perf_counter()
         res = g_.generate(prompts, a.max_new)
         sy(); tot = time.perf_counter() - t
         g_.sync_phases = False
-        phases["prefill"] = g_.stats["prefill_wall_s"] - pw0
-        phases["decode"] = g_.stats["decode_s"] - d0
+        ph["prefill"] = g_.stats["prefill_wall_s"] - pw0
+        ph["decode"] = g_.stats["decode_s"] - d0
         t = time.perf_counter()
         _ = [eng.chat.decode(r.tokens) for r in res]
-        phases["detokenize"] = time.perf_counter() - t
-        phases["generate_other"] = tot - phases["prefill"] - phases["decode"]
-        phases = {k: round(v * 1000, 2) for k, v in phases.items()}
+        ph["detokenize"] = time.perf_counter() - t
+        ph["generate_other"] = tot - ph["prefill"] - ph["decode"]
+        out = {k: round(v * 1000, 2) for k, v in ph.items()}
+        steps = g_.stats["decode_steps"] - st0
+        out["decode_ms_per_step"] = round(ph["decode"] * 1000 / max(1, steps), 3)
+        out["prompt_tokens_mean"] = round(float(np.mean([len(p) for p in prompts])), 1)
+        return out
+
+    phases, lat_phases = {}, {}
+    if a.breakdown:
+        phases = breakdown(a.batch, 777)
         log(info, f"QA step phases (ms): {phases}")
 
     # ---- p50 cache-miss latency (one query per GPU, end to end) ----
@@ -226,6 +234,9 @@ def main():
             torch.cuda.synchronize()
             lat.append(all_reduce_max(time.perf_counter() - t1, dev) * 1000)
     p50 = statistics.median(lat) if lat else None
+    if a.breakdown and a.latency_reps > 0:  # after the timed reps: the batch-1 graph is captured
+        lat_phases = breakdown(1, 778)
+        log(info, f"latency query phases (ms): {lat_phases}")
 
     # ---- ingest docs/min: chunk -> enrich+embed -> summarize -> index (per GPU, batched) ----
     docs_per_min = None
@@ -292,6 +303,7 @@ def main():
         "ingest_format": "pdf" if a.pdf_ingest else "txt",
         "prefill_tokens": gen["prefill_tokens"], "decode_steps": gen["decode_steps"],
         "qa_step_phase_ms": phases or None,
+        "latency_phase_ms": lat_phases or None,
     }
     if R == 0:
         print(json.dumps(out), flush=True)

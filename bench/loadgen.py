@@ -116,7 +116,7 @@ def _raw_hits(url: str, bodies: list[str]) -> list[float]:
 
 
 async def run(gw: str, docs: int, words: int, queries: int, concurrency: int, top_k: int, seed: int,
-              poll_s: float = 0.1, ingest_timeout: float = 600.0, query_url: str = "") -> dict:
+              poll_s: float = 0.05, ingest_timeout: float = 600.0, query_url: str = "") -> dict:
     tg = TextGen(seed=seed)
     texts = [tg.document(words) for _ in range(docs)]
     sem = asyncio.Semaphore(concurrency)

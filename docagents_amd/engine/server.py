@@ -245,7 +245,8 @@ class EngineServer:
 
     def __init__(self, group: EngineGroup, log, max_batch_items: int = 256, step_timeout_s: float = 300.0,
                  hard_timeout_s: float = 0.0, liveness_s: float = 30.0, profiler: StepProfiler | None = None,
-                 continuous: bool = False, cb_steps: int = 8, checkpoint_s: float = 0.0):
+                 continuous: bool = False, cb_steps: int = 8, checkpoint_s: float = 0.0,
+                 cb_window_s: float = 0.02):
         self.group, self.log = group, log
         self.checkpoint_s = checkpoint_s  # periodic shard snapshots when the shard is durable (0 = off)
         self.gpu = cf.ThreadPoolExecutor(max_workers=1, thread_name_prefix="gpu")
@@ -263,6 +264,7 @@ class EngineServer:
         # continuous batching of answers (a decode tick loop instead of whole-batch waves)
         self.continuous = continuous and getattr(group.engine, "gen", None) is not None
         self.cb_steps = cb_steps
+        self.cb_window_s = cb_window_s
         self._cb_new: list = []
         self._cb_futs: dict = {}
         self._cb_tag = 0
@@ -398,6 +400,11 @@ class EngineServer:
             if not busy and not self._cb_new:
                 self._cb_wake.clear()
                 await self._cb_wake.wait()
+                if self.cb_window_s > 0:
+                    # idle -> busy: let the rest of a burst arrive so it is admitted (prefilled) in
+                    # one tick and decodes in lockstep, instead of the first request's tick delaying
+                    # everyone else's start by a whole tick
+                    await asyncio.sleep(self.cb_window_s)
             new, self._cb_new = self._cb_new, []
             t0 = time.perf_counter()
             try:

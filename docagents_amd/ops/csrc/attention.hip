@@ -319,6 +319,7 @@ struct DecRope {
   bf16_t* vc;
   const float* cs;      // [max_pos][D/2][2] (cos, sin)
   const int* pos;       // [B]
+  unsigned long long* trace;  // VAR bit 3 only: per-workgroup wall-clock stamps (bench/decode_trace.py)
 };
 
 template <int D, int G, int VAR>
@@ -341,6 +342,15 @@ decode_attn_kernel(const bf16_t* __restrict__ q, int ldq, const bf16_t* __restri
   __shared__ float swm[4][G], swl[4][G];
 
   const int split = blockIdx.x, hk = blockIdx.y, b = blockIdx.z;
+  constexpr bool TRACE = (VAR & 8) != 0;
+  unsigned long long* const trw =
+      TRACE ? rope.trace + ((size_t)(b * gridDim.y + hk) * gridDim.x + split) * 16 : nullptr;
+  auto stamp = [&](int k) {
+    if constexpr (TRACE) {
+      if (threadIdx.x == 0) trw[k] = wall_clock64();
+    }
+  };
+  stamp(0);
   const int L = lens[b];
   DA_ASSERT(L >= 0 && L <= max_seq && slot[b] >= 0);
   const int kstart = split * chunk;
@@ -383,6 +393,7 @@ decode_attn_kernel(const bf16_t* __restrict__ q, int ldq, const bf16_t* __restri
   }
   for (int i = tid; i < 4 * G * D; i += 256) (&so[0][0][0])[i] = 0.f;
   __syncthreads();
+  stamp(1);
   if (own_new && w == 0) {  // score of the new key for each query head of this kv head
 #pragma unroll
     for (int g = 0; g < G; ++g) {
@@ -527,6 +538,7 @@ decode_attn_kernel(const bf16_t* __restrict__ q, int ldq, const bf16_t* __restri
       const int t1 = t0 + 4 * KT;
       if (t1 < kend) { load_k(kb2, t1); load_v(vb2, t1); }
       process(ka, va, t0);
+      if (t0 == kstart + w * KT) stamp(7);
       if (t1 >= kend) break;
       const int t2 = t1 + 4 * KT;
       if (t2 < kend) { load_k(ka, t2); load_v(va, t2); }
@@ -540,6 +552,10 @@ decode_attn_kernel(const bf16_t* __restrict__ q, int ldq, const bf16_t* __restri
       if constexpr (VEARLY) load_v(vv, t0);
       process(kv, vv, t0);
     }
+  }
+  stamp(2);
+  if constexpr (TRACE) {
+    if (lane == 0) trw[8 + w] = wall_clock64();
   }
   // ---- merge lanes -> per-wave O (LDS atomics), then waves -> block partial ----
 #pragma unroll
@@ -555,6 +571,7 @@ decode_attn_kernel(const bf16_t* __restrict__ q, int ldq, const bf16_t* __restri
     for (int g = 0; g < G; ++g) { swm[w][g] = m[g]; swl[w][g] = l[g]; }
   }
   __syncthreads();
+  stamp(12);
   for (int i = tid; i < G * D; i += 256) {
     const int g = i / D, d = i % D;
     float M = fmaxf(fmaxf(swm[0][g], swm[1][g]), fmaxf(swm[2][g], swm[3][g]));
@@ -574,8 +591,17 @@ decode_attn_kernel(const bf16_t* __restrict__ q, int ldq, const bf16_t* __restri
     }
     dec_store(o, M, ls, b, hk * G + g, d, H, nsplit, split, D, po, pm, pl, out, ldo);
   }
+  stamp(3);
   __shared__ int s_last;
   dec_finish<D, G>(po, pm, pl, H, Hkv, nsplit, b, hk, cnt, out, ldo, &s_last);
+  if constexpr (TRACE) {
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      unsigned xcc;
+      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+      trw[4] = wall_clock64(); trw[5] = s_last; trw[6] = __smid() | ((unsigned long long)(xcc & 15) << 32);
+    }
+  }
 }
 
 // ------------------------------------------------------------------------------------------
@@ -790,6 +816,11 @@ DA_EXPORT void da_set_gqa_mfma(int v) { g_gqa_mfma = v; }
 // MHA decode with the next tile prefetched (VAR bit 2) when B * Hkv <= this (0 = never).
 static int g_dec_pft = 32;
 DA_EXPORT void da_set_decode_pft(int v) { g_dec_pft = v; }
+// Timeline probe (bench/decode_trace.py): non-null -> the MHA D=96 prefetch variant writes 8 wall-clock
+// stamps per workgroup here ([B][Hkv][nsplit][8]: start, prologue done, first tile done, tiles done,
+// partial stored, finished, last-split flag, CU id).
+static unsigned long long* g_dec_trace = nullptr;
+DA_EXPORT void da_set_decode_trace(void* p) { g_dec_trace = (unsigned long long*)p; }
 
 // Measured on MI355X (profiles/decode_attn_variants_r1.json): non-temporal K/V loads + V issued with
 // K reach 6.5 TB/s for MHA (G = 1, Phi-3); with G >= 2 the extra V registers cost more occupancy
@@ -800,6 +831,13 @@ static int launch_decode(int G, dim3 grid, hipStream_t s, const bf16_t* q, int l
                          int nsplit, float sl2e, float* po, float* pm, float* pl, bf16_t* out, int ldo,
                          int* cnt, DecRope rope) {
   if (G == 1) {
+    if constexpr (D == 96) {
+      if (g_dec_trace) {
+        DecRope r = rope;
+        r.trace = g_dec_trace;
+        return launch_decode_v<D, 15>(G, grid, s, q, ldq, kc, vc, lens, slot, pre, H, Hkv, max_seq, chunk, nsplit, sl2e, po, pm, pl, out, ldo, cnt, r);
+      }
+    }
     if (g_dec_pft && (int)(grid.y * grid.z) <= g_dec_pft)  // few (row, kv head) pairs: latency-bound
       return launch_decode_v<D, 7>(G, grid, s, q, ldq, kc, vc, lens, slot, pre, H, Hkv, max_seq, chunk, nsplit, sl2e, po, pm, pl, out, ldo, cnt, rope);
     return launch_decode_v<D, 3>(G, grid, s, q, ldq, kc, vc, lens, slot, pre, H, Hkv, max_seq, chunk, nsplit, sl2e, po, pm, pl, out, ldo, cnt, rope);
@@ -846,7 +884,7 @@ DA_EXPORT int da_decode_attn(const void* q, int ldq, const void* k_cache, const 
   if (H % Hkv || chunk % 64 || nsplit < 1 || (long)chunk * nsplit < 1) return (int)hipErrorInvalidValue;
   if ((cos_sin == nullptr) != (pos == nullptr) || (cos_sin && (H != Hkv || ldq < (H + 2 * Hkv) * D)))
     return (int)hipErrorInvalidValue;
-  const DecRope rope{(bf16_t*)k_cache, (bf16_t*)v_cache, (const float*)cos_sin, (const int*)pos};
+  const DecRope rope{(bf16_t*)k_cache, (bf16_t*)v_cache, (const float*)cos_sin, (const int*)pos, nullptr};
   if (B == 0) return 0;
   const int G = H / Hkv;
   float* po = (float*)ws;
