@@ -338,7 +338,8 @@ decode_attn_kernel(const bf16_t* __restrict__ q, int ldq, const bf16_t* __restri
   __shared__ float sq[G][D];
   __shared__ float sp[4][G][KT];
   __shared__ float spart[SHFL ? 1 : 4][SHFL ? 1 : G * KT * CPR];
-  __shared__ float so[4][G][D];
+  __shared__ float so[G == 1 ? 1 : 4][G][D];
+  __shared__ float sacc[G == 1 ? 4 * NSET * 64 * 8 : 1];
   __shared__ float swm[4][G], swl[4][G];
 
   const int split = blockIdx.x, hk = blockIdx.y, b = blockIdx.z;
@@ -365,21 +366,103 @@ decode_attn_kernel(const bf16_t* __restrict__ q, int ldq, const bf16_t* __restri
   DA_ASSERT(!fr || rope.pos[b] == L - 1);
   __shared__ float skn[D], svn[D], ssn[G];
 
+  // VAR bit0: non-temporal loads (the KV stream is read once per step); bit1: V issued together
+  // with K (else after the scores: ~100 VGPRs live instead of ~200, so 4-5 waves per SIMD hide the
+  // HBM latency instead of 2); bit2 (small batches, implies bit1): the wave's NEXT tile is loaded
+  // before the current one is computed — at batch 1 a workgroup's few tiles are latency-bound, one
+  // HBM round trip each, and occupancy buys nothing. Loads are branch-free (chunk index clamped
+  // into the tile; keys >= nk get p = 0) so the compiler's vmcnt waits stay counted.
+  constexpr bool NT = VAR & 1, PFT = (VAR & 4) != 0, VEARLY = PFT || (VAR & 2) != 0;
+  auto ld16 = [&](const bf16_t* p) -> u32x4_t {
+    if constexpr (NT) return __builtin_nontemporal_load((const u32x4_t*)p);
+    else return *(const u32x4_t*)p;
+  };
+  auto tile_base = [&](const bf16_t* c, int t0) {
+    return c + (t0 < P ? pbase : cbase) + (size_t)t0 * D;
+  };
+  // PFT loads are branch-free: a tile past kend reads key 0 of the row's own slot (one line, valid
+  // memory, never used) so the prefetches can be issued unconditionally
+  auto load_k = [&](u32x4_t (&kv)[CPR], int t0) {
+    const int nk = kend - t0;
+    const int last = min(KT, nk) * CPR - 1;
+    const bf16_t* kb = tile_base(kc, t0);
+#pragma unroll
+    for (int i = 0; i < CPR; ++i) {
+      const int c = i * 64 + lane;
+      if constexpr (PFT) kv[i] = ld16(nk > 0 ? kb + min(c, last) * 8 : kc + cbase);
+      else kv[i] = (c <= last) ? ld16(kb + c * 8) : u32x4_t{0, 0, 0, 0};
+    }
+  };
+  auto load_v = [&](u32x4_t (&vv)[CPR], int t0) {
+    const int nk = kend - t0;
+    const int last = min(KT, nk) * CPR - 1;
+    const bf16_t* vb = tile_base(vc, t0);
+#pragma unroll
+    for (int i = 0; i < CPR; ++i) {
+      const int c = i * 64 + lane;
+      if constexpr (PFT) vv[i] = ld16(nk > 0 ? vb + min(c, last) * 8 : vc + cbase);
+      else vv[i] = (c <= last) ? ld16(vb + c * 8) : u32x4_t{0, 0, 0, 0};
+    }
+  };
   // RoPE (interleaved pairs (2i, 2i+1)) of one element of a head row, rounded to bf16 like the
   // rope_cache kernel / the QKV GEMM epilogue that this path replaces
-  auto rot = [&](const bf16_t* hp, int d, int p) -> float {
-    constexpr int HALF = D / 2;
-    const int i = d >> 1;
-    const float x1 = bf2f(hp[d & ~1]), x2 = bf2f(hp[d | 1]);
-    const float c = rope.cs[((size_t)p * HALF + i) * 2], sn = rope.cs[((size_t)p * HALF + i) * 2 + 1];
+  constexpr int HALF = D / 2;
+  auto rot2 = [&](float x1, float x2, float c, float sn, int d) -> float {
     return bf2f(f2bf((d & 1) ? x2 * c + x1 * sn : x1 * c - x2 * sn));
   };
-  for (int i = tid; i < G * D; i += 256) {
-    const int g = i / D, d = i % D;
-    const bf16_t* hp = q + (size_t)b * ldq + (hk * G + g) * D;
-    sq[g][d] = (fr ? rot(hp, d, L - 1) : bf2f(hp[d])) * scale_log2e;
+  auto rot = [&](const bf16_t* hp, int d, int p) -> float {
+    const int i = d >> 1;
+    return rot2(bf2f(hp[d & ~1]), bf2f(hp[d | 1]), rope.cs[((size_t)p * HALF + i) * 2],
+                rope.cs[((size_t)p * HALF + i) * 2 + 1], d);
+  };
+  // PFT (small batches): the prologue's operands (this thread's q element, its RoPE partner and
+  // cos / sin, the new token's k / v element) are loaded FIRST, then the first two K/V tiles of the
+  // wave are requested, unconditionally (an empty tile reads one line), so the compiler's counted
+  // wait for the prologue leaves the K/V stream in flight: its first HBM round trip overlaps the
+  // prologue instead of following it (vmcnt retires loads in order).
+  constexpr bool PRE = PFT && G * D <= 256;
+  u32x4_t ka[PFT ? CPR : 1], va[PFT ? CPR : 1], kb2[PFT ? CPR : 1], vb2[PFT ? CPR : 1];
+  if constexpr (PRE) {
+    // straight-line, clamped loads of raw bits: no branch and no use before the K/V loads below, so
+    // the wait for them is a counted vmcnt(48), not vmcnt(0) (a use inside a branch forces the latter)
+    const int qi = min(tid, G * D - 1), d = qi % D;
+    const bf16_t* hp = q + (size_t)b * ldq + (hk * G + qi / D) * D;
+    const bf16_t rq1 = hp[d & ~1], rq2 = hp[d | 1];
+    const float* csp = fr ? rope.cs + ((size_t)(L - 1) * HALF + (d >> 1)) * 2 : (const float*)hp;
+    const f32x2_t rcs = *(const f32x2_t*)csp;
+    const bf16_t* kr = fr ? q + (size_t)b * ldq + (size_t)(H + hk) * D : hp;
+    const bf16_t* vr = fr ? q + (size_t)b * ldq + (size_t)(H + Hkv + hk) * D : hp;
+    const bf16_t rk1 = kr[d & ~1], rk2 = kr[d | 1], nv = vr[d];
+    const int t0 = kstart + w * KT, t1 = t0 + 4 * KT;
+    load_k(ka, t0); load_v(va, t0);
+    load_k(kb2, t1); load_v(vb2, t1);
+    const float pc = fr ? rcs[0] : 1.f, ps = fr ? rcs[1] : 0.f;
+    if (tid < G * D) {
+      const float px1 = bf2f(rq1), px2 = bf2f(rq2);
+      const float x = fr ? rot2(px1, px2, pc, ps, d) : ((d & 1) ? px2 : px1);
+      sq[tid / D][d] = x * scale_log2e;
+    }
+    if (own_new && tid < D) {
+      const size_t crow = cbase + (size_t)(L - 1) * D;
+      const float kv = rot2(bf2f(rk1), bf2f(rk2), pc, ps, d);  // same position L - 1 -> same cos / sin
+      skn[d] = kv;
+      svn[d] = bf2f(nv);
+      rope.kc[crow + d] = f2bf(kv);  // for later steps (read back only after this launch)
+      rope.vc[crow + d] = nv;
+    }
+  } else {
+    if constexpr (PFT) {
+      const int t0 = kstart + w * KT, t1 = t0 + 4 * KT;
+      load_k(ka, t0); load_v(va, t0);
+      load_k(kb2, t1); load_v(vb2, t1);
+    }
+    for (int i = tid; i < G * D; i += 256) {
+      const int g = i / D, d = i % D;
+      const bf16_t* hp = q + (size_t)b * ldq + (hk * G + g) * D;
+      sq[g][d] = (fr ? rot(hp, d, L - 1) : bf2f(hp[d])) * scale_log2e;
+    }
   }
-  if (own_new) {
+  if (own_new && !PRE) {
     const bf16_t* kr = q + (size_t)b * ldq + (size_t)(H + hk) * D;
     const bf16_t* vr = q + (size_t)b * ldq + (size_t)(H + Hkv + hk) * D;
     const size_t crow = cbase + (size_t)(L - 1) * D;
@@ -391,7 +474,9 @@ decode_attn_kernel(const bf16_t* __restrict__ q, int ldq, const bf16_t* __restri
       rope.vc[crow + d] = vr[d];
     }
   }
-  for (int i = tid; i < 4 * G * D; i += 256) (&so[0][0][0])[i] = 0.f;
+  if constexpr (G > 1) {
+    for (int i = tid; i < 4 * G * D; i += 256) (&so[0][0][0])[i] = 0.f;
+  }
   __syncthreads();
   stamp(1);
   if (own_new && w == 0) {  // score of the new key for each query head of this kv head
@@ -414,40 +499,6 @@ decode_attn_kernel(const bf16_t* __restrict__ q, int ldq, const bf16_t* __restri
       for (int e = 0; e < 8; ++e) acc[g][s][e] = 0.f;
   }
 
-  // VAR bit0: non-temporal loads (the KV stream is read once per step); bit1: V issued together
-  // with K (else after the scores: ~100 VGPRs live instead of ~200, so 4-5 waves per SIMD hide the
-  // HBM latency instead of 2); bit2 (small batches, implies bit1): the wave's NEXT tile is loaded
-  // before the current one is computed — at batch 1 a workgroup's few tiles are latency-bound, one
-  // HBM round trip each, and occupancy buys nothing. Loads are branch-free (chunk index clamped
-  // into the tile; keys >= nk get p = 0) so the compiler's vmcnt waits stay counted.
-  constexpr bool NT = VAR & 1, PFT = (VAR & 4) != 0, VEARLY = PFT || (VAR & 2) != 0;
-  auto ld16 = [&](const bf16_t* p) -> u32x4_t {
-    if constexpr (NT) return __builtin_nontemporal_load((const u32x4_t*)p);
-    else return *(const u32x4_t*)p;
-  };
-  auto tile_base = [&](const bf16_t* c, int t0) {
-    return c + (t0 < P ? pbase : cbase) + (size_t)t0 * D;
-  };
-  auto load_k = [&](u32x4_t (&kv)[CPR], int t0) {
-    const int last = min(KT, kend - t0) * CPR - 1;
-    const bf16_t* kb = tile_base(kc, t0);
-#pragma unroll
-    for (int i = 0; i < CPR; ++i) {
-      const int c = i * 64 + lane;
-      if constexpr (PFT) kv[i] = ld16(kb + min(c, last) * 8);
-      else kv[i] = (c <= last) ? ld16(kb + c * 8) : u32x4_t{0, 0, 0, 0};
-    }
-  };
-  auto load_v = [&](u32x4_t (&vv)[CPR], int t0) {
-    const int last = min(KT, kend - t0) * CPR - 1;
-    const bf16_t* vb = tile_base(vc, t0);
-#pragma unroll
-    for (int i = 0; i < CPR; ++i) {
-      const int c = i * 64 + lane;
-      if constexpr (PFT) vv[i] = ld16(vb + min(c, last) * 8);
-      else vv[i] = (c <= last) ? ld16(vb + c * 8) : u32x4_t{0, 0, 0, 0};
-    }
-  };
   auto process = [&](const u32x4_t (&kv)[CPR], u32x4_t (&vv)[CPR], int t0) {
     const int nk = min(KT, kend - t0);
     // ---- scores ----
@@ -530,19 +581,19 @@ decode_attn_kernel(const bf16_t* __restrict__ q, int ldq, const bf16_t* __restri
     __builtin_amdgcn_wave_barrier();
   };
 
-  if constexpr (PFT) {
-    u32x4_t ka[CPR], va[CPR], kb2[CPR], vb2[CPR];
+  if constexpr (PFT) {  // two tiles in flight per wave: ka/va and kb2/vb2 alternate
     int t0 = kstart + w * KT;
-    if (t0 < kend) { load_k(ka, t0); load_v(va, t0); }
     while (t0 < kend) {
       const int t1 = t0 + 4 * KT;
-      if (t1 < kend) { load_k(kb2, t1); load_v(vb2, t1); }
       process(ka, va, t0);
       if (t0 == kstart + w * KT) stamp(7);
       if (t1 >= kend) break;
       const int t2 = t1 + 4 * KT;
       if (t2 < kend) { load_k(ka, t2); load_v(va, t2); }
       process(kb2, vb2, t1);
+      if (t2 >= kend) break;
+      const int t3 = t2 + 4 * KT;
+      if (t3 < kend) { load_k(kb2, t3); load_v(vb2, t3); }
       t0 = t2;
     }
   } else {
@@ -557,15 +608,27 @@ decode_attn_kernel(const bf16_t* __restrict__ q, int ldq, const bf16_t* __restri
   if constexpr (TRACE) {
     if (lane == 0) trw[8 + w] = wall_clock64();
   }
-  // ---- merge lanes -> per-wave O (LDS atomics), then waves -> block partial ----
-#pragma unroll
-  for (int g = 0; g < G; ++g)
+  // ---- merge lanes -> per-wave O, then waves -> block partial ----
+  // MHA (G = 1): every lane parks its accumulators in LDS with plain 16-B stores and the output
+  // threads sum the (dim-slot, lane) entries that hold their dim. LDS float atomics — 5-6 lanes per
+  // address — took 7.5 us of a 20 us batch-1 launch (bench/decode_trace.py), more than the K/V stream.
+  if constexpr (G == 1) {
 #pragma unroll
     for (int st = 0; st < NSET; ++st) {
-      const int dp = (lane + 64 * st) % CPR;
-#pragma unroll
-      for (int e = 0; e < 8; ++e) atomicAdd(&so[w][g][dp * 8 + e], acc[g][st][e]);
+      float* dst = &sacc[((w * NSET + st) * 64 + lane) * 8];
+      *(f32x4_t*)dst = f32x4_t{acc[0][st][0], acc[0][st][1], acc[0][st][2], acc[0][st][3]};
+      *(f32x4_t*)(dst + 4) = f32x4_t{acc[0][st][4], acc[0][st][5], acc[0][st][6], acc[0][st][7]};
     }
+  } else {
+#pragma unroll
+    for (int g = 0; g < G; ++g)
+#pragma unroll
+      for (int st = 0; st < NSET; ++st) {
+        const int dp = (lane + 64 * st) % CPR;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) atomicAdd(&so[w][g][dp * 8 + e], acc[g][st][e]);
+      }
+  }
   if (lane == 0) {
 #pragma unroll
     for (int g = 0; g < G; ++g) { swm[w][g] = m[g]; swl[w][g] = l[g]; }
@@ -581,7 +644,25 @@ decode_attn_kernel(const bf16_t* __restrict__ q, int ldq, const bf16_t* __restri
 #pragma unroll
     for (int ww = 0; ww < 4; ++ww) {
       const float f = exp2f(swm[ww][g] - Mu);
-      o += so[ww][g][d] * f;
+      float ow;
+      if constexpr (G == 1) {
+        // lane l's slot st holds dims 8 * ((64 st + l) % CPR) .. +7
+        // fixed trip counts: all of a wave's reads are independent and issued back to back
+        ow = 0.f;
+        const int dp = d >> 3, e = d & 7;
+#pragma unroll
+        for (int st = 0; st < NSET; ++st) {
+          const int l0 = ((dp - 64 * st) % CPR + CPR) % CPR;
+#pragma unroll
+          for (int j = 0; j < (64 + CPR - 1) / CPR; ++j) {
+            const int l = l0 + j * CPR;
+            if (l < 64) ow += sacc[((ww * NSET + st) * 64 + l) * 8 + e];
+          }
+        }
+      } else {
+        ow = so[ww][g][d];
+      }
+      o += ow * f;
       ls += swl[ww][g] * f;
     }
     if (own_new) {  // the new token's key: weight exp2(s - M), value straight from the qkv row

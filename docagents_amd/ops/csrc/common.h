@@ -23,6 +23,7 @@
 #endif
 
 typedef __attribute__((ext_vector_type(8))) short bf16x8_t;   // 8 bf16 = one MFMA A/B fragment
+typedef __attribute__((ext_vector_type(2))) float f32x2_t;
 typedef __attribute__((ext_vector_type(4))) float f32x4_t;    // 16x16 accumulator fragment
 typedef __attribute__((ext_vector_type(16))) float f32x16_t;  // 32x32 accumulator fragment
 typedef __attribute__((ext_vector_type(4))) short s16x4_t;    // ds_read_b64_tr_b16 result

@@ -277,10 +277,9 @@ gemm_splitk_reduce(const float* __restrict__ ws, int splits, int M, int N, int e
 // dot products accumulate in fp32 per lane and each row is reduced across the wave once.
 // The activation row (K bf16) is read through the caches (every wave reads the same vector).
 // EPI_SWIGLU: a wave owns 2 gate rows and their 2 up rows (16-row interleave) -> 2 outputs.
-template <int EPI, int R>
+template <int EPI, int R, int U>
 __global__ void __launch_bounds__(256)
 gemv_kernel(GemmArgs p) {
-  constexpr int U = 4;
   static_assert(EPI != EPI_SWIGLU || R == 4, "SwiGLU waves own 2 gate + 2 up rows");
   const int lane = threadIdx.x & 63;
   const int wg = blockIdx.x * 4 + (threadIdx.x >> 6);  // global wave index
@@ -369,18 +368,41 @@ gemv_kernel(GemmArgs p) {
   }
 }
 
-template <int R>
+template <int R, int U>
 static int launch_gemv_r(const GemmArgs& a, int epi, hipStream_t s) {
   const int waves = (a.N + R - 1) / R;
   dim3 grid((waves + 3) / 4), block(256);
   switch (epi) {
-    case EPI_NONE: gemv_kernel<EPI_NONE, R><<<grid, block, 0, s>>>(a); break;
-    case EPI_BIAS: gemv_kernel<EPI_BIAS, R><<<grid, block, 0, s>>>(a); break;
-    case EPI_GELU: gemv_kernel<EPI_GELU, R><<<grid, block, 0, s>>>(a); break;
-    case EPI_RESID: gemv_kernel<EPI_RESID, R><<<grid, block, 0, s>>>(a); break;
+    case EPI_NONE: gemv_kernel<EPI_NONE, R, U><<<grid, block, 0, s>>>(a); break;
+    case EPI_BIAS: gemv_kernel<EPI_BIAS, R, U><<<grid, block, 0, s>>>(a); break;
+    case EPI_GELU: gemv_kernel<EPI_GELU, R, U><<<grid, block, 0, s>>>(a); break;
+    case EPI_RESID: gemv_kernel<EPI_RESID, R, U><<<grid, block, 0, s>>>(a); break;
     default: return (int)hipErrorInvalidValue;
   }
   return (int)hipGetLastError();
+}
+
+// K-blocks (512 elements = 1 KiB per row) in flight per row: the whole row when it is short
+// (K = 3072: 6 blocks, one round of loads and no clamped duplicate loads), 8 per round otherwise.
+static int g_gemv_u = 0;  // 0 = auto; 4 = the fixed round-1 depth (A/B)
+DA_EXPORT void da_set_gemv_u(int v) { g_gemv_u = v; }
+static int gemv_u(int K, int /*R*/) {
+  const int nkb = K / 512;
+  if (g_gemv_u) return g_gemv_u;
+  if (nkb <= 4) return 4;
+  if (nkb == 6) return 6;
+  // 8, not the whole row at K = 8192: at U = 16 the compiler sinks the loads to their uses
+  // (28 VGPRs, one block in flight) and the down projection drops to ~3 TB/s (measured)
+  return 8;
+}
+
+template <int R>
+static int launch_gemv_ru(const GemmArgs& a, int epi, hipStream_t s) {
+  switch (gemv_u(a.K, R)) {
+    case 6: return launch_gemv_r<R, 6>(a, epi, s);
+    case 8: return launch_gemv_r<R, 8>(a, epi, s);
+    default: return launch_gemv_r<R, 4>(a, epi, s);
+  }
 }
 
 // Rows per wave: enough waves (>= ~4 per SIMD) that the loads in flight cover HBM latency on
@@ -389,12 +411,16 @@ static int launch_gemv(const GemmArgs& a, int epi, hipStream_t s) {
   if (a.M != 1 || a.K % 512 || a.N % 4) return (int)hipErrorInvalidValue;
   if (epi == EPI_SWIGLU) {
     dim3 grid((a.N / 4 + 3) / 4), block(256);
-    gemv_kernel<EPI_SWIGLU, 4><<<grid, block, 0, s>>>(a);
+    switch (gemv_u(a.K, 4)) {
+      case 6: gemv_kernel<EPI_SWIGLU, 4, 6><<<grid, block, 0, s>>>(a); break;
+      case 8: gemv_kernel<EPI_SWIGLU, 4, 8><<<grid, block, 0, s>>>(a); break;
+      default: gemv_kernel<EPI_SWIGLU, 4, 4><<<grid, block, 0, s>>>(a); break;
+    }
     return (int)hipGetLastError();
   }
-  if (a.N >= 16384) return launch_gemv_r<4>(a, epi, s);
-  if (a.N >= 8192) return launch_gemv_r<2>(a, epi, s);
-  return launch_gemv_r<1>(a, epi, s);
+  if (a.N >= 16384) return launch_gemv_ru<4>(a, epi, s);
+  if (a.N >= 8192) return launch_gemv_ru<2>(a, epi, s);
+  return launch_gemv_ru<1>(a, epi, s);
 }
 
 template <int BM, int BN, int WM, int WN, int PF = 1>

@@ -427,7 +427,7 @@ def test_layernorm_fused_fp8_output():
     assert torch.all(d <= 0.13 * (rq.float() * rs[:, None]).abs() + 1e-3)
 
 
-@pytest.mark.parametrize("N,Kd", [(96, 512), (544, 3072), (1024, 8192), (32064, 3072)])
+@pytest.mark.parametrize("N,Kd", [(96, 512), (544, 3072), (1024, 8192), (32064, 3072), (256, 2560), (128, 4608)])
 @pytest.mark.parametrize("epi", [K.EPI_NONE, K.EPI_BIAS, K.EPI_RESID, K.EPI_SWIGLU])
 def test_gemv_batch1_decode(N, Kd, epi):
     torch.manual_seed(N + Kd + epi)
