@@ -1,4 +1,5 @@
-"""Prefill attention microbenchmark: flash_attn_v2 (4- and 8-wave workgroups) vs torch SDPA on MI355X shapes."""
+"""Prefill attention microbenchmark: flash_attn_v2 arms (4 / 8 waves per workgroup x 32 / 64 queries per wave)
+vs torch SDPA on MI355X shapes, each arm checked against SDPA."""
 import argparse
 import os
 import sys
@@ -41,23 +42,26 @@ def main():
         cu = torch.arange(0, T + 1, L, device=dev, dtype=torch.int32)
         fl = 4 * B * L * L * H * D * (0.5 if causal else 1.0)
         r = {}
-        for impl in ("v2", "v2w8"):
-            K.lib().da_set_flash_waves(8 if impl == "v2w8" else 4)
-            t = timeit(lambda: K.flash_attn_varlen(q, k, v, cu, L, H, Hkv, D, causal))
-            r[impl + "_ms"], r[impl + "_tflops"] = t, fl / t / 1e9
-        K.lib().da_set_flash_waves(8)
-        o8 = K.flash_attn_varlen(q, k, v, cu, L, H, Hkv, D, causal).float()
-        K.lib().da_set_flash_waves(0)
         qq = q.reshape(B, L, H, D).transpose(1, 2)
         kk = k.reshape(B, L, Hkv, D).transpose(1, 2).repeat_interleave(H // Hkv, 1)
         vv = v.reshape(B, L, Hkv, D).transpose(1, 2).repeat_interleave(H // Hkv, 1)
+        ref = torch.nn.functional.scaled_dot_product_attention(qq, kk, vv, is_causal=causal)
+        ref = ref.transpose(1, 2).reshape(T, H * D).float()
+        # arms: waves per workgroup x 32-query halves per wave
+        for nw, qh in ((4, 1), (8, 1), (4, 2), (8, 2)):
+            if nw * qh > 8 and D > 64:
+                continue
+            K.lib().da_set_flash_waves(nw)
+            K.lib().da_set_flash_qh(qh)
+            arm = f"w{nw}q{qh}"
+            t = timeit(lambda: K.flash_attn_varlen(q, k, v, cu, L, H, Hkv, D, causal))
+            out = K.flash_attn_varlen(q, k, v, cu, L, H, Hkv, D, causal).float()
+            r[arm] = {"ms": round(t, 3), "tflops": round(fl / t / 1e9, 1),
+                      "max_err_vs_sdpa": round((out - ref).abs().max().item(), 4)}
+        K.lib().da_set_flash_waves(0)
+        K.lib().da_set_flash_qh(0)
         t = timeit(lambda: torch.nn.functional.scaled_dot_product_attention(qq, kk, vv, is_causal=causal))
-        r["sdpa_ms"], r["sdpa_tflops"] = t, fl / t / 1e9
-        o1 = K.flash_attn_varlen(q, k, v, cu, L, H, Hkv, D, causal).float()
-        o2 = torch.nn.functional.scaled_dot_product_attention(qq, kk, vv, is_causal=causal)
-        o2 = o2.transpose(1, 2).reshape(T, H * D).float()
-        r["max_err_vs_sdpa"] = (o1 - o2).abs().max().item()
-        r["w8_vs_w4_maxdiff"] = (o8 - o1).abs().max().item()
+        r["sdpa"] = {"ms": round(t, 3), "tflops": round(fl / t / 1e9, 1)}
         res[name] = r
         print(name, json.dumps(r), flush=True)
     if a.out:

@@ -25,9 +25,9 @@
 //   scale·log2(e) is folded into the exp2 argument (one FMA per score); the O rescale is skipped
 //   when no lane's running max moved; causal tiles past a wave's last query are skipped by that
 //   wave (it still stages tiles and joins the barrier).
-template <int D, int NW = 4>
+template <int D, int NW = 4, int QH = 1>
 struct FA2Cfg {
-  static constexpr int KT = 64, QW = 32, QB = 32 * NW, NT = 64 * NW;
+  static constexpr int KT = 64, QW = 32 * QH, QB = QW * NW, NT = 64 * NW;
   static constexpr int KSTR = D * 2 + 16;                                         // bytes
   static constexpr int VSTR = (D == 64) ? 192 : (D == 128) ? 320 : D * 2;         // bytes
   static constexpr int KBUF = KT * KSTR, VBUF = KT * VSTR;
@@ -48,12 +48,16 @@ struct FaPrefix {
   int rev;  // causal: dispatch query blocks longest-first (set by the launcher)
 };
 
-template <int D, int NW>
-__global__ void __launch_bounds__(64 * NW, 8 / NW)
+// QH = 32-query halves per wave. QH = 2: each K fragment read from LDS feeds the S MFMAs of both
+// halves and each transposed V fragment the O MFMAs of both, so LDS read bytes per FLOP halve (at
+// QH = 1 the LDS reads of a tile take as long as its MFMAs); the two halves' softmax VALU work is
+// independent of the other half's MFMAs, so the scheduler overlaps them inside one wave.
+template <int D, int NW, int QH>
+__global__ void __launch_bounds__(64 * NW, QH == 1 ? 8 / NW : 1)
 flash_attn_v2_kernel(const bf16_t* __restrict__ q, const bf16_t* __restrict__ k, const bf16_t* __restrict__ v,
                      int ldq, int ldk, int ldv, const int* __restrict__ cu, int H, int Hkv, int causal,
                      float c, bf16_t* __restrict__ o, int ldo, FaPrefix pre) {
-  using C = FA2Cfg<D, NW>;
+  using C = FA2Cfg<D, NW, QH>;
   constexpr int KT = C::KT, NDS = D / 16, NDB = D / 32, CPR = C::CPR, LPT = C::LPT, NT = C::NT;
   constexpr bool EVEN = (KT * CPR) % NT == 0;  // every thread stages exactly LPT chunks
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -69,21 +73,27 @@ flash_attn_v2_kernel(const bf16_t* __restrict__ q, const bf16_t* __restrict__ k,
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int qr = lane & 31, hi = lane >> 5;
   const int wq0 = q0 + wid * C::QW;
-  const int qi = wq0 + qr;
-  const bool qvalid = qi < L;
-
-  bf16x8_t qf[NDS];
+  int qi[QH];
+  bool qvalid[QH];
+  bf16x8_t qf[QH][NDS];
+  f32x16_t oacc[QH][NDB];
+  float m_run[QH], l_part[QH];
 #pragma unroll
-  for (int ds = 0; ds < NDS; ++ds) {
-    if (qvalid) qf[ds] = *(const bf16x8_t*)(q + (size_t)(s0 + qi) * ldq + h * D + ds * 16 + hi * 8);
-    else qf[ds] = bf16x8_t{0, 0, 0, 0, 0, 0, 0, 0};
+  for (int j = 0; j < QH; ++j) {
+    qi[j] = wq0 + 32 * j + qr;
+    qvalid[j] = qi[j] < L;
+#pragma unroll
+    for (int ds = 0; ds < NDS; ++ds) {
+      if (qvalid[j]) qf[j][ds] = *(const bf16x8_t*)(q + (size_t)(s0 + qi[j]) * ldq + h * D + ds * 16 + hi * 8);
+      else qf[j][ds] = bf16x8_t{0, 0, 0, 0, 0, 0, 0, 0};
+    }
+#pragma unroll
+    for (int i = 0; i < NDB; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) oacc[j][i][r] = 0.f;
+    m_run[j] = -INFINITY;
+    l_part[j] = 0.f;
   }
-  f32x16_t oacc[NDB];
-#pragma unroll
-  for (int i = 0; i < NDB; ++i)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) oacc[i][r] = 0.f;
-  float m_run = -INFINITY, l_part = 0.f;
 
   const int P = pre.len, Lk = P + L;  // keys: [prefix | own]; own query i is key P + i
   const int kv_end = causal ? min(Lk, P + q0 + C::QB) : Lk;
@@ -95,7 +105,33 @@ flash_attn_v2_kernel(const bf16_t* __restrict__ q, const bf16_t* __restrict__ k,
   const bf16_t* kpre = pre.k + hk * pre.hstride;
   const bf16_t* vpre = pre.v + hk * pre.hstride;
   u32x4_t kst[LPT], vst[LPT];
+  // Own-key tiles (all keys >= P) load through buffer resources rebuilt per tile on the scalar unit
+  // (base = the tile's first key, num_records = the bytes left in the sequence: keys past the end
+  // read 0), with fixed per-lane 32-bit offsets: no per-load 64-bit address math, bounds compare or
+  // exec-mask branch (those were ~90 of the ~285 vector instructions of a tile).
+  unsigned koff[LPT], voff[LPT];
+#pragma unroll
+  for (int i = 0; i < LPT; ++i) {
+    const int idx = tid + NT * i, r = idx / CPR, cc = idx % CPR;
+    const bool in = EVEN || idx < KT * CPR;
+    koff[i] = in ? (unsigned)(r * ldk * 2 + cc * 16) : 0x80000000u;
+    voff[i] = in ? (unsigned)(r * ldv * 2 + cc * 16) : 0x80000000u;
+  }
   auto load_tile = [&](int t) {
+    const int k0 = t * KT;
+    if (k0 >= P) {
+      const int o0 = k0 - P;
+      const __amdgpu_buffer_rsrc_t rk = __builtin_amdgcn_make_buffer_rsrc(
+          (void*)(kbase_p + (size_t)o0 * ldk), (short)0, (L - o0) * ldk * 2, 0x00020000);
+      const __amdgpu_buffer_rsrc_t rv = __builtin_amdgcn_make_buffer_rsrc(
+          (void*)(vbase_p + (size_t)o0 * ldv), (short)0, (L - o0) * ldv * 2, 0x00020000);
+#pragma unroll
+      for (int i = 0; i < LPT; ++i) {
+        kst[i] = __builtin_amdgcn_raw_buffer_load_b128(rk, koff[i], 0, 0);
+        vst[i] = __builtin_amdgcn_raw_buffer_load_b128(rv, voff[i], 0, 0);
+      }
+      return;
+    }
 #pragma unroll
     for (int i = 0; i < LPT; ++i) {
       const int idx = tid + NT * i, r = idx / CPR, cc = idx % CPR, key = t * KT + r;
@@ -137,60 +173,100 @@ flash_attn_v2_kernel(const bf16_t* __restrict__ q, const bf16_t* __restrict__ k,
     if (kb < wave_end) {
       const char* sK = smem + cur * (C::KBUF + C::VBUF);
       const char* sV = sK + C::KBUF;
-      f32x16_t sacc[2];
+      f32x16_t sacc[QH][2];
+      // all K fragments of the tile first, then the MFMAs with the two 32-key halves interleaved:
+      // one LDS round trip per tile instead of one per MFMA, and back-to-back MFMAs never depend
+      // on each other (a fragment-at-a-time loop serialises LDS latency + MFMA latency 12 times).
+      // D = 128 (16 fragments) batches per 32-key half, which keeps it within 256 VGPRs.
 #pragma unroll
-      for (int hh = 0; hh < 2; ++hh) {
+      for (int j = 0; j < QH; ++j)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) sacc[hh][r] = 0.f;
+        for (int hh = 0; hh < 2; ++hh)
 #pragma unroll
-        for (int ds = 0; ds < NDS; ++ds) {
-          const bf16x8_t a = *(const bf16x8_t*)(sK + (hh * 32 + qr) * C::KSTR + ds * 32 + hi * 16);
-          sacc[hh] = mfma32(a, qf[ds], sacc[hh]);
+          for (int r = 0; r < 16; ++r) sacc[j][hh][r] = 0.f;
+      if constexpr (NDS <= 6) {
+        bf16x8_t kfr[2][NDS];
+#pragma unroll
+        for (int hh = 0; hh < 2; ++hh)
+#pragma unroll
+          for (int ds = 0; ds < NDS; ++ds)
+            kfr[hh][ds] = *(const bf16x8_t*)(sK + (hh * 32 + qr) * C::KSTR + ds * 32 + hi * 16);
+#pragma unroll
+        for (int ds = 0; ds < NDS; ++ds)
+#pragma unroll
+          for (int hh = 0; hh < 2; ++hh)
+#pragma unroll
+            for (int j = 0; j < QH; ++j) sacc[j][hh] = mfma32(kfr[hh][ds], qf[j][ds], sacc[j][hh]);
+        // pin that order: the register-pressure scheduler otherwise re-serialises read -> MFMA pairs
+        __builtin_amdgcn_sched_group_barrier(0x100, 2 * NDS, 0);       // DS reads
+        __builtin_amdgcn_sched_group_barrier(0x008, 2 * NDS * QH, 0);  // MFMAs
+      } else {
+#pragma unroll
+        for (int hh = 0; hh < 2; ++hh) {
+          bf16x8_t kfr[NDS];
+#pragma unroll
+          for (int ds = 0; ds < NDS; ++ds)
+            kfr[ds] = *(const bf16x8_t*)(sK + (hh * 32 + qr) * C::KSTR + ds * 32 + hi * 16);
+#pragma unroll
+          for (int ds = 0; ds < NDS; ++ds)
+#pragma unroll
+            for (int j = 0; j < QH; ++j) sacc[j][hh] = mfma32(kfr[ds], qf[j][ds], sacc[j][hh]);
+          __builtin_amdgcn_sched_group_barrier(0x100, NDS, 0);
+          __builtin_amdgcn_sched_group_barrier(0x008, NDS * QH, 0);
         }
       }
-      if (kb + KT > Lk || (causal && kb + KT - 1 > P + wq0)) {
+#pragma unroll
+      for (int j = 0; j < QH; ++j) {
+        if (kb + KT > Lk || (causal && kb + KT - 1 > P + wq0 + 32 * j)) {
+#pragma unroll
+          for (int hh = 0; hh < 2; ++hh)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+              const int key = kb + hh * 32 + 8 * (r >> 2) + 4 * hi + (r & 3);
+              if (key >= Lk || (causal && key > P + qi[j])) sacc[j][hh][r] = -INFINITY;
+            }
+        }
+        float mx = sacc[j][0][0];
+#pragma unroll
+        for (int r = 1; r < 16; ++r) mx = fmaxf(mx, sacc[j][0][r]);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) mx = fmaxf(mx, sacc[j][1][r]);
+        mx = max_xhalf(mx);
+        const float m_new = fmaxf(m_run[j], mx);
+        const float m_use = (m_new == -INFINITY) ? 0.f : m_new;
+        if (__any(m_new > m_run[j])) {
+          const float alpha = exp2f((m_run[j] - m_use) * c);
+          l_part[j] *= alpha;
+#pragma unroll
+          for (int i = 0; i < NDB; ++i) oacc[j][i] *= alpha;
+        }
+        m_run[j] = m_new;
+        const float mc = -m_use * c;
+        float psum = 0.f;
 #pragma unroll
         for (int hh = 0; hh < 2; ++hh)
 #pragma unroll
           for (int r = 0; r < 16; ++r) {
-            const int key = kb + hh * 32 + 8 * (r >> 2) + 4 * hi + (r & 3);
-            if (key >= Lk || (causal && key > P + qi)) sacc[hh][r] = -INFINITY;
+            const float p = __builtin_amdgcn_exp2f(fmaf(sacc[j][hh][r], c, mc));  // raw v_exp_f32
+            sacc[j][hh][r] = p;
+            psum += p;
           }
+        l_part[j] += psum;
       }
-      float mx = sacc[0][0];
-#pragma unroll
-      for (int r = 1; r < 16; ++r) mx = fmaxf(mx, sacc[0][r]);
-#pragma unroll
-      for (int r = 0; r < 16; ++r) mx = fmaxf(mx, sacc[1][r]);
-      mx = max_xhalf(mx);
-      const float m_new = fmaxf(m_run, mx);
-      const float m_use = (m_new == -INFINITY) ? 0.f : m_new;
-      if (__any(m_new > m_run)) {
-        const float alpha = exp2f((m_run - m_use) * c);
-        l_part *= alpha;
-#pragma unroll
-        for (int i = 0; i < NDB; ++i) oacc[i] *= alpha;
-      }
-      m_run = m_new;
-      const float mc = -m_use * c;
-      float psum = 0.f;
-#pragma unroll
-      for (int hh = 0; hh < 2; ++hh)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const float p = __builtin_amdgcn_exp2f(fmaf(sacc[hh][r], c, mc));  // raw v_exp_f32
-          sacc[hh][r] = p;
-          psum += p;
-        }
-      l_part += psum;
 
       // O^T += V^T P^T over 4 k-steps of 16 keys: slot (hi, j) -> key 16kc + 8(j>>2) + 4hi + (j&3)
 #pragma unroll
       for (int kc = 0; kc < 4; ++kc) {
         const int hh = kc >> 1, cb = (kc & 1) * 8;
-        const u32x4_t pw = u32x4_t{pack_bf2(sacc[hh][cb], sacc[hh][cb + 1]), pack_bf2(sacc[hh][cb + 2], sacc[hh][cb + 3]),
-                                   pack_bf2(sacc[hh][cb + 4], sacc[hh][cb + 5]), pack_bf2(sacc[hh][cb + 6], sacc[hh][cb + 7])};
-        const bf16x8_t pb = __builtin_bit_cast(bf16x8_t, pw);
+        bf16x8_t pb[QH];
+#pragma unroll
+        for (int j = 0; j < QH; ++j) {
+          const u32x4_t pw = u32x4_t{pack_bf2(sacc[j][hh][cb], sacc[j][hh][cb + 1]),
+                                     pack_bf2(sacc[j][hh][cb + 2], sacc[j][hh][cb + 3]),
+                                     pack_bf2(sacc[j][hh][cb + 4], sacc[j][hh][cb + 5]),
+                                     pack_bf2(sacc[j][hh][cb + 6], sacc[j][hh][cb + 7])};
+          pb[j] = __builtin_bit_cast(bf16x8_t, pw);
+        }
         const int g = lane >> 4, li = lane & 15;
         const int row0 = kc * 16 + 4 * (g >> 1) + (li >> 2);
 #pragma unroll
@@ -199,7 +275,8 @@ flash_attn_v2_kernel(const bf16_t* __restrict__ q, const bf16_t* __restrict__ k,
           const s16x4_t lo = lds_read_tr16(sV + row0 * C::VSTR + col * 2);
           const s16x4_t hi8 = lds_read_tr16(sV + (row0 + 8) * C::VSTR + col * 2);
           const bf16x8_t va = bf16x8_t{lo[0], lo[1], lo[2], lo[3], hi8[0], hi8[1], hi8[2], hi8[3]};
-          oacc[db] = mfma32(va, pb, oacc[db]);
+#pragma unroll
+          for (int j = 0; j < QH; ++j) oacc[j][db] = mfma32(va, pb[j], oacc[j][db]);
         }
       }
     }
@@ -207,18 +284,21 @@ flash_attn_v2_kernel(const bf16_t* __restrict__ q, const bf16_t* __restrict__ k,
     __syncthreads();
   }
 
-  const float l_tot = sum_xhalf(l_part);
-  const float inv = l_tot > 0.f ? 1.f / l_tot : 0.f;
-  if (qvalid) {
-    bf16_t* orow = o + (size_t)(s0 + qi) * ldo + h * D;
 #pragma unroll
-    for (int db = 0; db < NDB; ++db)
+  for (int j = 0; j < QH; ++j) {
+    const float l_tot = sum_xhalf(l_part[j]);
+    const float inv = l_tot > 0.f ? 1.f / l_tot : 0.f;
+    if (qvalid[j]) {
+      bf16_t* orow = o + (size_t)(s0 + qi[j]) * ldo + h * D;
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int d = db * 32 + 8 * g + 4 * hi;
-        *(u32x2_t*)(orow + d) = u32x2_t{pack_bf2(oacc[db][4 * g] * inv, oacc[db][4 * g + 1] * inv),
-                                        pack_bf2(oacc[db][4 * g + 2] * inv, oacc[db][4 * g + 3] * inv)};
-      }
+      for (int db = 0; db < NDB; ++db)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int d = db * 32 + 8 * g + 4 * hi;
+          *(u32x2_t*)(orow + d) = u32x2_t{pack_bf2(oacc[j][db][4 * g] * inv, oacc[j][db][4 * g + 1] * inv),
+                                          pack_bf2(oacc[j][db][4 * g + 2] * inv, oacc[j][db][4 * g + 3] * inv)};
+        }
+    }
   }
 }
 
@@ -998,38 +1078,50 @@ DA_EXPORT int da_decode_attn(const void* q, int ldq, const void* k_cache, const 
   DA_LAUNCH_CHECK();
 }
 
-// Waves per workgroup: 0 = auto (8 waves x 32 queries for bidirectional encoders, where a K/V tile
-// staged once serves 256 queries; 4 for causal prefill, where a taller query block wastes more
-// work on the diagonal — profiles/attn_v2_waves_r1.json). 4 / 8 force a shape (A/B runs).
+// Waves per workgroup: 0 = auto (4; 8 at D = 128), 4 / 8 force a shape (A/B runs). Round 1 picked 8
+// for bidirectional encoders; with the buffer-loaded K/V tiles 4 waves are faster there too.
 static int g_fa_waves = 0;
 DA_EXPORT void da_set_flash_waves(int nw) { g_fa_waves = nw; }
 // causal flash: longest query blocks first (1, default) or grid order (0); A/B runs
 static int g_fa_rev = 1;
 DA_EXPORT void da_set_flash_rev(int v) { g_fa_rev = v ? 1 : 0; }
 
-template <int NW>
+template <int NW, int QH>
 static int launch_fa2(const void* q, const void* k, const void* v, int ldq, int ldk, int ldv, const void* cu_seqlens,
                       int B, int max_seqlen, int H, int Hkv, int D, int causal, float sl2e, void* o, int ldo,
                       FaPrefix pre, hipStream_t s) {
   static bool attr_set = false;
-  if (!attr_set) {
-    (void)hipFuncSetAttribute((const void*)flash_attn_v2_kernel<128, NW>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              FA2Cfg<128, NW>::SMEM);
-    attr_set = true;
+  if constexpr (NW * QH <= 8) {
+    if (!attr_set) {
+      (void)hipFuncSetAttribute((const void*)flash_attn_v2_kernel<128, NW, QH>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                FA2Cfg<128, NW, QH>::SMEM);
+      attr_set = true;
+    }
   }
-  dim3 grid((max_seqlen + 32 * NW - 1) / (32 * NW), H, B);
+  dim3 grid((max_seqlen + 32 * QH * NW - 1) / (32 * QH * NW), H, B);
 #define FA_ARGS (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, ldq, ldk, ldv, (const int*)cu_seqlens, H, Hkv, \
                 causal, sl2e, (bf16_t*)o, ldo, pre
   switch (D) {
-    case 32: flash_attn_v2_kernel<32, NW><<<grid, 64 * NW, FA2Cfg<32, NW>::SMEM, s>>>(FA_ARGS); break;
-    case 64: flash_attn_v2_kernel<64, NW><<<grid, 64 * NW, FA2Cfg<64, NW>::SMEM, s>>>(FA_ARGS); break;
-    case 96: flash_attn_v2_kernel<96, NW><<<grid, 64 * NW, FA2Cfg<96, NW>::SMEM, s>>>(FA_ARGS); break;
-    case 128: flash_attn_v2_kernel<128, NW><<<grid, 64 * NW, FA2Cfg<128, NW>::SMEM, s>>>(FA_ARGS); break;
+    case 32: flash_attn_v2_kernel<32, NW, QH><<<grid, 64 * NW, FA2Cfg<32, NW, QH>::SMEM, s>>>(FA_ARGS); break;
+    case 64: flash_attn_v2_kernel<64, NW, QH><<<grid, 64 * NW, FA2Cfg<64, NW, QH>::SMEM, s>>>(FA_ARGS); break;
+    // 8 waves x 64 queries exceed 256 VGPRs (spills) above D = 64: not instantiated
+    case 96:
+      if constexpr (NW * QH <= 8) flash_attn_v2_kernel<96, NW, QH><<<grid, 64 * NW, FA2Cfg<96, NW, QH>::SMEM, s>>>(FA_ARGS);
+      else return (int)hipErrorInvalidValue;
+      break;
+    case 128:
+      if constexpr (NW * QH <= 8) flash_attn_v2_kernel<128, NW, QH><<<grid, 64 * NW, FA2Cfg<128, NW, QH>::SMEM, s>>>(FA_ARGS);
+      else return (int)hipErrorInvalidValue;
+      break;
     default: return (int)hipErrorInvalidValue;
   }
 #undef FA_ARGS
   return (int)hipGetLastError();
 }
+
+// queries per wave: 0 = auto, 1 = 32 (round-1 shape), 2 = 64 (A/B runs)
+static int g_fa_qh = 0;
+DA_EXPORT void da_set_flash_qh(int v) { g_fa_qh = v; }
 
 // pre_k / pre_v: shared-prefix K/V of KV head 0 in a cache slot (nullptr / pre_len 0: none),
 // pre_hstride: elements between KV heads there (max_seq * D).
@@ -1044,7 +1136,13 @@ DA_EXPORT int da_flash_attn_v2(const void* q, const void* k, const void* v, int 
   const float sl2e = scale * 1.4426950408889634f;
   hipStream_t s = (hipStream_t)stream;
   const FaPrefix pre{(const bf16_t*)pre_k, (const bf16_t*)pre_v, pre_hstride, pre_len, g_fa_rev};
-  if (g_fa_waves == 8 || (g_fa_waves == 0 && !causal))
-    return launch_fa2<8>(q, k, v, ldq, ldk, ldv, cu_seqlens, B, max_seqlen, H, Hkv, D, causal, sl2e, o, ldo, pre, s);
-  return launch_fa2<4>(q, k, v, ldq, ldk, ldv, cu_seqlens, B, max_seqlen, H, Hkv, D, causal, sl2e, o, ldo, pre, s);
+  const int qh = g_fa_qh ? g_fa_qh : 1;
+  // auto: 4 waves, except D = 128 (Llama-3 prefill: 8 waves measured faster, profiles/r2/attn_bench_v4.txt)
+  const bool w8 = g_fa_waves == 8 || (g_fa_waves == 0 && D == 128);
+  if (qh == 2) {
+    if (w8 && D <= 64) return launch_fa2<8, 2>(q, k, v, ldq, ldk, ldv, cu_seqlens, B, max_seqlen, H, Hkv, D, causal, sl2e, o, ldo, pre, s);
+    return launch_fa2<4, 2>(q, k, v, ldq, ldk, ldv, cu_seqlens, B, max_seqlen, H, Hkv, D, causal, sl2e, o, ldo, pre, s);
+  }
+  if (w8) return launch_fa2<8, 1>(q, k, v, ldq, ldk, ldv, cu_seqlens, B, max_seqlen, H, Hkv, D, causal, sl2e, o, ldo, pre, s);
+  return launch_fa2<4, 1>(q, k, v, ldq, ldk, ldv, cu_seqlens, B, max_seqlen, H, Hkv, D, causal, sl2e, o, ldo, pre, s);
 }

@@ -53,6 +53,7 @@ _SIGS = {
     "da_set_gqa_mfma": [c_int],
     "da_malloc_uncached": [c_longlong, ctypes.POINTER(c_void_p)],
     "da_set_flash_waves": [c_int],
+    "da_set_flash_qh": [c_int],
     "da_set_gemm_pf": [c_int],
     "da_set_gemv_u": [c_int],
     "da_set_decode_pft": [c_int],
@@ -105,6 +106,8 @@ def lib() -> ctypes.CDLL:
         # schedule overrides for A/B measurements (defaults are the measured-best variants)
         if os.environ.get("DA_GEMM_PF") is not None:  # decode-tile register prefetch depth (A/B)
             L.da_set_gemm_pf(int(os.environ["DA_GEMM_PF"]))
+        if os.environ.get("DA_FLASH_QH") is not None:  # flash queries per wave: 1 = 32, 2 = 64 (A/B)
+            L.da_set_flash_qh(int(os.environ["DA_FLASH_QH"]))
         if os.environ.get("DA_GEMV_U") is not None:  # batch-1 GEMV K-blocks in flight per row (A/B)
             L.da_set_gemv_u(int(os.environ["DA_GEMV_U"]))
         if os.environ.get("DA_FLASH_REV") is not None:  # causal flash longest-first dispatch (A/B)
