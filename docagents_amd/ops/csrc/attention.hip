@@ -303,6 +303,222 @@ flash_attn_v2_kernel(const bf16_t* __restrict__ q, const bf16_t* __restrict__ k,
 }
 
 // ------------------------------------------------------------------------------------------
+// flash_attn_pipe: the same math and fragment layouts as flash_attn_v2<D, 4, 1>, software-pipelined
+// one tile deep (guide T15): the S MFMAs of tile t + 1 are issued before the softmax + P·V of tile t,
+// so the softmax VALU work never waits on the MFMA results it follows (RAW) and the matrix pipe has
+// independent work while a wave is in its exp/max/pack stretch. Three LDS tile buffers: tile t
+// (P·V), t + 1 (S) and t + 2 (being written); one barrier per tile.
+template <int D>
+__global__ void __launch_bounds__(256, 2)
+flash_attn_pipe_kernel(const bf16_t* __restrict__ q, const bf16_t* __restrict__ k, const bf16_t* __restrict__ v,
+                       int ldq, int ldk, int ldv, const int* __restrict__ cu, int H, int Hkv, int causal,
+                       float c, bf16_t* __restrict__ o, int ldo, FaPrefix pre) {
+  using C = FA2Cfg<D, 4, 1>;
+  constexpr int KT = C::KT, NDS = D / 16, NDB = D / 32, CPR = C::CPR, LPT = C::LPT, NT = C::NT;
+  constexpr bool EVEN = (KT * CPR) % NT == 0;
+  static_assert(NDS <= 6, "pipelined flash: D <= 96");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int b = blockIdx.z, h = blockIdx.y;
+  const int s0 = cu[b], L = cu[b + 1] - s0;
+  const int qb = (causal && pre.rev) ? (int)gridDim.x - 1 - (int)blockIdx.x : (int)blockIdx.x;
+  const int q0 = qb * C::QB;
+  if (q0 >= L) return;
+  const int hk = h / (H / Hkv);
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int qr = lane & 31, hi = lane >> 5;
+  const int wq0 = q0 + wid * C::QW;
+  const int qi = wq0 + qr;
+  const bool qvalid = qi < L;
+  bf16x8_t qf[NDS];
+#pragma unroll
+  for (int ds = 0; ds < NDS; ++ds)
+    qf[ds] = qvalid ? *(const bf16x8_t*)(q + (size_t)(s0 + qi) * ldq + h * D + ds * 16 + hi * 8)
+                    : bf16x8_t{0, 0, 0, 0, 0, 0, 0, 0};
+  f32x16_t oacc[NDB];
+#pragma unroll
+  for (int i = 0; i < NDB; ++i)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) oacc[i][r] = 0.f;
+  float m_run = -INFINITY, l_part = 0.f;
+
+  const int P = pre.len, Lk = P + L;
+  const int kv_end = causal ? min(Lk, P + q0 + C::QB) : Lk;
+  const int wave_end = causal ? min(Lk, P + wq0 + C::QW) : Lk;
+  const int ntiles = (kv_end + KT - 1) / KT;
+
+  const bf16_t* kbase_p = k + (size_t)s0 * ldk + hk * D;
+  const bf16_t* vbase_p = v + (size_t)s0 * ldv + hk * D;
+  const bf16_t* kpre = pre.k + hk * pre.hstride;
+  const bf16_t* vpre = pre.v + hk * pre.hstride;
+  u32x4_t kst[LPT], vst[LPT];
+  unsigned koff[LPT], voff[LPT];
+#pragma unroll
+  for (int i = 0; i < LPT; ++i) {
+    const int idx = tid + NT * i, r = idx / CPR, cc = idx % CPR;
+    const bool in = EVEN || idx < KT * CPR;
+    koff[i] = in ? (unsigned)(r * ldk * 2 + cc * 16) : 0x80000000u;
+    voff[i] = in ? (unsigned)(r * ldv * 2 + cc * 16) : 0x80000000u;
+  }
+  auto load_tile = [&](int t) {
+    const int k0 = t * KT;
+    if (k0 >= P) {
+      const int o0 = k0 - P;
+      const __amdgpu_buffer_rsrc_t rk = __builtin_amdgcn_make_buffer_rsrc(
+          (void*)(kbase_p + (size_t)o0 * ldk), (short)0, (L - o0) * ldk * 2, 0x00020000);
+      const __amdgpu_buffer_rsrc_t rv = __builtin_amdgcn_make_buffer_rsrc(
+          (void*)(vbase_p + (size_t)o0 * ldv), (short)0, (L - o0) * ldv * 2, 0x00020000);
+#pragma unroll
+      for (int i = 0; i < LPT; ++i) {
+        kst[i] = __builtin_amdgcn_raw_buffer_load_b128(rk, koff[i], 0, 0);
+        vst[i] = __builtin_amdgcn_raw_buffer_load_b128(rv, voff[i], 0, 0);
+      }
+      return;
+    }
+#pragma unroll
+    for (int i = 0; i < LPT; ++i) {
+      const int idx = tid + NT * i, r = idx / CPR, cc = idx % CPR, key = t * KT + r;
+      if ((EVEN || idx < KT * CPR) && key < Lk) {
+        if (key >= P) {
+          kst[i] = *(const u32x4_t*)(kbase_p + (size_t)(key - P) * ldk + cc * 8);
+          vst[i] = *(const u32x4_t*)(vbase_p + (size_t)(key - P) * ldv + cc * 8);
+        } else {
+          kst[i] = *(const u32x4_t*)(kpre + (size_t)key * D + cc * 8);
+          vst[i] = *(const u32x4_t*)(vpre + (size_t)key * D + cc * 8);
+        }
+      } else {
+        kst[i] = u32x4_t{0, 0, 0, 0};
+        vst[i] = u32x4_t{0, 0, 0, 0};
+      }
+    }
+  };
+  auto buf_of = [&](int t) { return smem + (t % 3) * (C::KBUF + C::VBUF); };
+  auto store_tile = [&](int t) {
+    char* sK = buf_of(t);
+    char* sV = sK + C::KBUF;
+#pragma unroll
+    for (int i = 0; i < LPT; ++i) {
+      const int idx = tid + NT * i, r = idx / CPR, cc = idx % CPR;
+      if (EVEN || idx < KT * CPR) {
+        *(u32x4_t*)(sK + r * C::KSTR + cc * 16) = kst[i];
+        *(u32x4_t*)(sV + r * C::VSTR + cc * 16) = vst[i];
+      }
+    }
+  };
+  // S^T of tile t: all K fragments, then the MFMAs (two independent accumulation chains)
+  auto s_tile = [&](int t, f32x16_t (&sa)[2]) {
+    const char* sK = buf_of(t);
+    bf16x8_t kfr[2][NDS];
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh)
+#pragma unroll
+      for (int ds = 0; ds < NDS; ++ds)
+        kfr[hh][ds] = *(const bf16x8_t*)(sK + (hh * 32 + qr) * C::KSTR + ds * 32 + hi * 16);
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) sa[hh][r] = 0.f;
+#pragma unroll
+    for (int ds = 0; ds < NDS; ++ds)
+#pragma unroll
+      for (int hh = 0; hh < 2; ++hh) sa[hh] = mfma32(kfr[hh][ds], qf[ds], sa[hh]);
+  };
+  // mask + online softmax + O^T += V^T P^T of tile t
+  auto finish = [&](int t, f32x16_t (&sa)[2]) {
+    const int kb = t * KT;
+    const char* sV = buf_of(t) + C::KBUF;
+    if (kb + KT > Lk || (causal && kb + KT - 1 > P + wq0)) {
+#pragma unroll
+      for (int hh = 0; hh < 2; ++hh)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int key = kb + hh * 32 + 8 * (r >> 2) + 4 * hi + (r & 3);
+          if (key >= Lk || (causal && key > P + qi)) sa[hh][r] = -INFINITY;
+        }
+    }
+    float mx = sa[0][0];
+#pragma unroll
+    for (int r = 1; r < 16; ++r) mx = fmaxf(mx, sa[0][r]);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) mx = fmaxf(mx, sa[1][r]);
+    mx = max_xhalf(mx);
+    const float m_new = fmaxf(m_run, mx);
+    const float m_use = (m_new == -INFINITY) ? 0.f : m_new;
+    if (__any(m_new > m_run)) {
+      const float alpha = exp2f((m_run - m_use) * c);
+      l_part *= alpha;
+#pragma unroll
+      for (int i = 0; i < NDB; ++i) oacc[i] *= alpha;
+    }
+    m_run = m_new;
+    const float mc = -m_use * c;
+    float psum = 0.f;
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float pv = __builtin_amdgcn_exp2f(fmaf(sa[hh][r], c, mc));
+        sa[hh][r] = pv;
+        psum += pv;
+      }
+    l_part += psum;
+#pragma unroll
+    for (int kc = 0; kc < 4; ++kc) {
+      const int hh = kc >> 1, cb = (kc & 1) * 8;
+      const u32x4_t pw = u32x4_t{pack_bf2(sa[hh][cb], sa[hh][cb + 1]), pack_bf2(sa[hh][cb + 2], sa[hh][cb + 3]),
+                                 pack_bf2(sa[hh][cb + 4], sa[hh][cb + 5]), pack_bf2(sa[hh][cb + 6], sa[hh][cb + 7])};
+      const bf16x8_t pb = __builtin_bit_cast(bf16x8_t, pw);
+      const int g = lane >> 4, li = lane & 15;
+      const int row0 = kc * 16 + 4 * (g >> 1) + (li >> 2);
+#pragma unroll
+      for (int db = 0; db < NDB; ++db) {
+        const int col = db * 32 + 16 * (g & 1) + 4 * (li & 3);
+        const s16x4_t lo = lds_read_tr16(sV + row0 * C::VSTR + col * 2);
+        const s16x4_t hi8 = lds_read_tr16(sV + (row0 + 8) * C::VSTR + col * 2);
+        const bf16x8_t va = bf16x8_t{lo[0], lo[1], lo[2], lo[3], hi8[0], hi8[1], hi8[2], hi8[3]};
+        oacc[db] = mfma32(va, pb, oacc[db]);
+      }
+    }
+  };
+
+  load_tile(0);
+  store_tile(0);
+  if (ntiles > 1) {
+    load_tile(1);
+    store_tile(1);
+  }
+  __syncthreads();
+  if (ntiles > 2) load_tile(2);
+  f32x16_t SA[2], SB[2];
+  s_tile(0, SA);
+  auto step = [&](int t, f32x16_t (&cur)[2], f32x16_t (&nxt)[2]) {
+    if (t + 1 < ntiles && (t + 1) * KT < wave_end) s_tile(t + 1, nxt);
+    if (t * KT < wave_end) finish(t, cur);
+    if (t + 2 < ntiles) store_tile(t + 2);   // its buffer (t - 1) % 3 was last read before the previous barrier
+    if (t + 3 < ntiles) load_tile(t + 3);
+    __syncthreads();
+  };
+  for (int t = 0; t < ntiles; t += 2) {
+    step(t, SA, SB);
+    if (t + 1 < ntiles) step(t + 1, SB, SA);
+  }
+
+  const float l_tot = sum_xhalf(l_part);
+  const float inv = l_tot > 0.f ? 1.f / l_tot : 0.f;
+  if (qvalid) {
+    bf16_t* orow = o + (size_t)(s0 + qi) * ldo + h * D;
+#pragma unroll
+    for (int db = 0; db < NDB; ++db)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int d = db * 32 + 8 * g + 4 * hi;
+        *(u32x2_t*)(orow + d) = u32x2_t{pack_bf2(oacc[db][4 * g] * inv, oacc[db][4 * g + 1] * inv),
+                                        pack_bf2(oacc[db][4 * g + 2] * inv, oacc[db][4 * g + 3] * inv)};
+      }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
 // Decode attention: q [B, ldq] (head h at h*D), caches [slots, Hkv, max_seq, D],
 // lens[b] = tokens in cache for b (current token included), slot[b] = cache slot of b.
 // Partials: po [B, H, nsplit, D] fp32 (unnormalised, relative to pm), pm/pl [B, H, nsplit].
@@ -1122,6 +1338,33 @@ static int launch_fa2(const void* q, const void* k, const void* v, int ldq, int 
 // queries per wave: 0 = auto, 1 = 32 (round-1 shape), 2 = 64 (A/B runs)
 static int g_fa_qh = 0;
 DA_EXPORT void da_set_flash_qh(int v) { g_fa_qh = v; }
+// software-pipelined kernel (flash_attn_pipe, D <= 96, 4 waves x 32 queries): 0 = off, 1 = on
+static int g_fa_pipe = 0;
+DA_EXPORT void da_set_flash_pipe(int v) { g_fa_pipe = v; }
+
+static int launch_fa_pipe(const void* q, const void* k, const void* v, int ldq, int ldk, int ldv, const void* cu_seqlens,
+                          int B, int max_seqlen, int H, int Hkv, int D, int causal, float sl2e, void* o, int ldo,
+                          FaPrefix pre, hipStream_t s) {
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute((const void*)flash_attn_pipe_kernel<96>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              3 * (FA2Cfg<96, 4, 1>::KBUF + FA2Cfg<96, 4, 1>::VBUF));
+    (void)hipFuncSetAttribute((const void*)flash_attn_pipe_kernel<64>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              3 * (FA2Cfg<64, 4, 1>::KBUF + FA2Cfg<64, 4, 1>::VBUF));
+    attr_set = true;
+  }
+  dim3 grid((max_seqlen + 127) / 128, H, B);
+#define FA_ARGS (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, ldq, ldk, ldv, (const int*)cu_seqlens, H, Hkv, \
+                causal, sl2e, (bf16_t*)o, ldo, pre
+  switch (D) {
+    case 32: flash_attn_pipe_kernel<32><<<grid, 256, 3 * (FA2Cfg<32, 4, 1>::KBUF + FA2Cfg<32, 4, 1>::VBUF), s>>>(FA_ARGS); break;
+    case 64: flash_attn_pipe_kernel<64><<<grid, 256, 3 * (FA2Cfg<64, 4, 1>::KBUF + FA2Cfg<64, 4, 1>::VBUF), s>>>(FA_ARGS); break;
+    case 96: flash_attn_pipe_kernel<96><<<grid, 256, 3 * (FA2Cfg<96, 4, 1>::KBUF + FA2Cfg<96, 4, 1>::VBUF), s>>>(FA_ARGS); break;
+    default: return (int)hipErrorInvalidValue;
+  }
+#undef FA_ARGS
+  return (int)hipGetLastError();
+}
 
 // pre_k / pre_v: shared-prefix K/V of KV head 0 in a cache slot (nullptr / pre_len 0: none),
 // pre_hstride: elements between KV heads there (max_seq * D).
@@ -1136,6 +1379,8 @@ DA_EXPORT int da_flash_attn_v2(const void* q, const void* k, const void* v, int 
   const float sl2e = scale * 1.4426950408889634f;
   hipStream_t s = (hipStream_t)stream;
   const FaPrefix pre{(const bf16_t*)pre_k, (const bf16_t*)pre_v, pre_hstride, pre_len, g_fa_rev};
+  if (g_fa_pipe && D <= 96 && g_fa_waves != 8 && g_fa_qh != 2)
+    return launch_fa_pipe(q, k, v, ldq, ldk, ldv, cu_seqlens, B, max_seqlen, H, Hkv, D, causal, sl2e, o, ldo, pre, s);
   const int qh = g_fa_qh ? g_fa_qh : 1;
   // auto: 4 waves, except D = 128 (Llama-3 prefill: 8 waves measured faster, profiles/r2/attn_bench_v4.txt)
   const bool w8 = g_fa_waves == 8 || (g_fa_waves == 0 && D == 128);

@@ -21,6 +21,9 @@ _LOCK = threading.Lock()
 _LIB_PATH = Path(__file__).resolve().parent / "_da_kernels.so"
 
 EPI_NONE, EPI_BIAS, EPI_GELU, EPI_SWIGLU, EPI_RESID = 0, 1, 2, 3, 4
+# flash prefill kernel default: the software-pipelined kernel (1) or the round-1 loop (0); must
+# match g_fa_pipe in attention.hip (tests restore it after forcing an arm)
+FLASH_PIPE_DEFAULT = 0
 
 c_longlong = ctypes.c_longlong
 c_void_p, c_int, c_float, c_uint, c_size_t = (ctypes.c_void_p, ctypes.c_int, ctypes.c_float,
@@ -54,6 +57,7 @@ _SIGS = {
     "da_malloc_uncached": [c_longlong, ctypes.POINTER(c_void_p)],
     "da_set_flash_waves": [c_int],
     "da_set_flash_qh": [c_int],
+    "da_set_flash_pipe": [c_int],
     "da_set_gemm_pf": [c_int],
     "da_set_gemv_u": [c_int],
     "da_set_decode_pft": [c_int],
@@ -106,6 +110,8 @@ def lib() -> ctypes.CDLL:
         # schedule overrides for A/B measurements (defaults are the measured-best variants)
         if os.environ.get("DA_GEMM_PF") is not None:  # decode-tile register prefetch depth (A/B)
             L.da_set_gemm_pf(int(os.environ["DA_GEMM_PF"]))
+        if os.environ.get("DA_FLASH_PIPE") is not None:  # software-pipelined flash prefill (A/B)
+            L.da_set_flash_pipe(int(os.environ["DA_FLASH_PIPE"]))
         if os.environ.get("DA_FLASH_QH") is not None:  # flash queries per wave: 1 = 32, 2 = 64 (A/B)
             L.da_set_flash_qh(int(os.environ["DA_FLASH_QH"]))
         if os.environ.get("DA_GEMV_U") is not None:  # batch-1 GEMV K-blocks in flight per row (A/B)

@@ -20,8 +20,9 @@ from ..store.base import STATUS_FAILED, STATUS_READY, Embedding, Summary
 
 async def handle_analyze(deps, payload: dict) -> None:
     doc_id = str(uuid.UUID(payload.get("document_id", "")))
-    if not payload.get("reindex"):
-        # a duplicate delivery (a redelivered or re-driven task) of a finished document is a no-op
+    if payload.get("redrive"):
+        # a startup-sweep re-drive of a document that finished meanwhile is a no-op (plain tasks keep
+        # the reference's exact call order: ListChunks first)
         try:
             if (await deps.store.get_document(doc_id)).status == STATUS_READY:
                 return

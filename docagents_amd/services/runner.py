@@ -117,7 +117,8 @@ async def startup_sweep(deps):
                 continue
             chunks = await deps.store.list_chunks(d.id)
             if chunks:
-                body = json.dumps({"document_id": d.id, "chunk_ids": [c.id for c in chunks]}).encode()
+                body = json.dumps({"document_id": d.id, "chunk_ids": [c.id for c in chunks],
+                                   "redrive": True}).encode()
                 await enqueue_with_retry(deps.queue, Task(type=TASK_ANALYZE, payload=body), 3, 0.2)
                 deps.log.info("re-enqueued stuck document", "document_id", d.id)
         vec = getattr(deps.store, "vectors", None)

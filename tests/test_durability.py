@@ -185,7 +185,7 @@ def test_startup_sweep_reenqueues_ready_docs_without_vectors(tmp_path):
 
 def test_startup_sweep_skips_in_flight_documents_and_analyze_is_idempotent(tmp_path):
     """A 'processing' document younger than SWEEP_STUCK_AFTER_S is in flight (a worker starting
-    while uploads arrive must not duplicate its task); an older one is re-driven; a duplicate
+    while uploads arrive must not duplicate its task); an older one is re-driven (flagged "redrive"); a re-driven
     analyze delivery of a ready document is a no-op."""
     import types
 
@@ -221,4 +221,4 @@ def test_startup_sweep_skips_in_flight_documents_and_analyze_is_idempotent(tmp_p
             raise AssertionError("a ready document must not be summarized again")
     asyncio.run(store.update_document_status(doc, STATUS_READY))
     deps = types.SimpleNamespace(store=store, llm=Boom(), config=types.SimpleNamespace(chunk_overlap=0))
-    asyncio.run(handle_analyze(deps, {"document_id": doc}))
+    asyncio.run(handle_analyze(deps, {"document_id": doc, "redrive": True}))

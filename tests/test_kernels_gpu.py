@@ -455,10 +455,11 @@ def test_gemv_fused_rmsnorm(N, Kd, epi):
     _close(got, R.gemm(x, w, epi=epi, rms=(g, 1e-5)), atol=0.03)
 
 
-@pytest.mark.parametrize("nw,qh", [(4, 1), (8, 1), (4, 2), (8, 2)])
+@pytest.mark.parametrize("nw,qh,pipe", [(4, 1, 0), (8, 1, 0), (4, 2, 0), (8, 2, 0), (4, 1, 1)])
 @pytest.mark.parametrize("D,causal", [(64, False), (96, True), (128, True), (32, False), (64, True), (96, False)])
-def test_flash_attn_wave_shapes(nw, qh, D, causal):
-    """Every workgroup shape (waves x 32-query halves per wave) against the fp32 reference."""
+def test_flash_attn_wave_shapes(nw, qh, pipe, D, causal):
+    """Every workgroup shape (waves x 32-query halves per wave, and the software-pipelined kernel)
+    against the fp32 reference."""
     torch.manual_seed(D + nw + qh)
     lens = [1, 77, 300, 513]
     H, Hkv = 4, 2
@@ -467,11 +468,13 @@ def test_flash_attn_wave_shapes(nw, qh, D, causal):
     cu = torch.tensor([0] + list(np.cumsum(lens)), device=DEV, dtype=torch.int32)
     K.lib().da_set_flash_waves(nw)
     K.lib().da_set_flash_qh(qh)
+    K.lib().da_set_flash_pipe(pipe)
     try:
         got = K.flash_attn_varlen(q, k, v, cu, max(lens), H, Hkv, D, causal)
     finally:
         K.lib().da_set_flash_waves(0)
         K.lib().da_set_flash_qh(0)
+        K.lib().da_set_flash_pipe(K.FLASH_PIPE_DEFAULT)
     _close(got, R.flash_attn_varlen(q, k, v, cu, max(lens), H, Hkv, D, causal), atol=0.02)
 
 
@@ -569,8 +572,8 @@ def test_gemm_mid_m_blas_route(M, monkeypatch):
 
 
 @pytest.mark.parametrize("H,Hkv,D,P", [(32, 32, 96, 261), (8, 2, 128, 64), (4, 4, 64, 1), (4, 2, 96, 130)])
-@pytest.mark.parametrize("nw,qh", [(4, 1), (8, 1), (4, 2)])
-def test_flash_attn_shared_prefix(H, Hkv, D, P, nw, qh):
+@pytest.mark.parametrize("nw,qh,pipe", [(4, 1, 0), (8, 1, 0), (4, 2, 0), (4, 1, 1)])
+def test_flash_attn_shared_prefix(H, Hkv, D, P, nw, qh, pipe):
     """Suffix queries attend to P shared-prefix keys held in a KV-cache slot + their own keys."""
     torch.manual_seed(H + D + P)
     lens = [1, 63, 64, 200, 7]
@@ -582,11 +585,13 @@ def test_flash_attn_shared_prefix(H, Hkv, D, P, nw, qh):
     pre = (kc[1], vc[1], P)
     K.lib().da_set_flash_waves(nw)
     K.lib().da_set_flash_qh(qh)
+    K.lib().da_set_flash_pipe(pipe)
     try:
         got = K.flash_attn_varlen(q, k, v, cu, max(lens), H, Hkv, D, True, prefix=pre)
     finally:
         K.lib().da_set_flash_waves(0)
         K.lib().da_set_flash_qh(0)
+        K.lib().da_set_flash_pipe(K.FLASH_PIPE_DEFAULT)
     ref = R.flash_attn_varlen(q, k, v, cu, max(lens), H, Hkv, D, True, prefix=pre)
     _close(got, ref, atol=0.02)
 
