@@ -1338,8 +1338,10 @@ static int launch_fa2(const void* q, const void* k, const void* v, int ldq, int 
 // queries per wave: 0 = auto, 1 = 32 (round-1 shape), 2 = 64 (A/B runs)
 static int g_fa_qh = 0;
 DA_EXPORT void da_set_flash_qh(int v) { g_fa_qh = v; }
-// software-pipelined kernel (flash_attn_pipe, D <= 96, 4 waves x 32 queries): 0 = off, 1 = on
-static int g_fa_pipe = 0;
+// software-pipelined kernel (flash_attn_pipe, D <= 96, 4 waves x 32 queries): 0 = off, 1 = on,
+// 2 = auto: causal D = 96 (Phi-3 prefill 576 -> 656 TF/s; the short bidirectional BGE sequences,
+// 8 tiles, lose to its longer pipeline fill: 617 -> 531 at D = 64, profiles/r2/attn_bench_v5.txt)
+static int g_fa_pipe = 2;
 DA_EXPORT void da_set_flash_pipe(int v) { g_fa_pipe = v; }
 
 static int launch_fa_pipe(const void* q, const void* k, const void* v, int ldq, int ldk, int ldv, const void* cu_seqlens,
@@ -1379,7 +1381,8 @@ DA_EXPORT int da_flash_attn_v2(const void* q, const void* k, const void* v, int 
   const float sl2e = scale * 1.4426950408889634f;
   hipStream_t s = (hipStream_t)stream;
   const FaPrefix pre{(const bf16_t*)pre_k, (const bf16_t*)pre_v, pre_hstride, pre_len, g_fa_rev};
-  if (g_fa_pipe && D <= 96 && g_fa_waves != 8 && g_fa_qh != 2)
+  const bool pipe = g_fa_pipe == 1 || (g_fa_pipe == 2 && causal && D == 96);
+  if (pipe && D <= 96 && g_fa_waves != 8 && g_fa_qh != 2)
     return launch_fa_pipe(q, k, v, ldq, ldk, ldv, cu_seqlens, B, max_seqlen, H, Hkv, D, causal, sl2e, o, ldo, pre, s);
   const int qh = g_fa_qh ? g_fa_qh : 1;
   // auto: 4 waves, except D = 128 (Llama-3 prefill: 8 waves measured faster, profiles/r2/attn_bench_v4.txt)

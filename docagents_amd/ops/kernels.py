@@ -21,9 +21,9 @@ _LOCK = threading.Lock()
 _LIB_PATH = Path(__file__).resolve().parent / "_da_kernels.so"
 
 EPI_NONE, EPI_BIAS, EPI_GELU, EPI_SWIGLU, EPI_RESID = 0, 1, 2, 3, 4
-# flash prefill kernel default: the software-pipelined kernel (1) or the round-1 loop (0); must
-# match g_fa_pipe in attention.hip (tests restore it after forcing an arm)
-FLASH_PIPE_DEFAULT = 0
+# flash prefill kernel choice: 2 = auto (software-pipelined kernel for causal D = 96), 1 / 0 = force
+# on / off; must match g_fa_pipe's initial value in attention.hip (tests restore it after an A/B arm)
+FLASH_PIPE_DEFAULT = 2
 
 c_longlong = ctypes.c_longlong
 c_void_p, c_int, c_float, c_uint, c_size_t = (ctypes.c_void_p, ctypes.c_int, ctypes.c_float,
