@@ -52,7 +52,8 @@ class Engine:
         if load_llm:
             self.decoder = LlamaDecoder(self.dec_cfg, self.device, seed=seed, tp=tp)
             # + 1 dummy slot (padded graph rows) + 2 prompt-head slots (ContinuousScheduler heads)
-            self.decoder.alloc_cache(max_batch + 3, max_seq)
+            # + 1 for the wave path's kept prompt head (Generator.head)
+            self.decoder.alloc_cache(max_batch + 4, max_seq)
             self.gen = Generator(self.decoder, max_batch=max_batch, max_seq=max_seq, temperature=temperature,
                                  seed=seed, eos=sorted(self.chat.eos_ids), use_graphs=use_graphs,
                                  share_prefix=os.environ.get("DA_SHARE_PREFIX", "1") != "0")

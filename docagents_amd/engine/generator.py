@@ -54,6 +54,7 @@ class Generator:
             model.alloc_cache(max_batch + 1, max_seq)
         self.cache = model.cache
         self.dummy_slot = self.cache.acquire(1)[0]
+        self.head = None  # {"tokens", "P", "slot"}: the last wave's shared prompt head, kept in its own slot
         self.states: dict[tuple, DecodeState] = {}
         self.stats = {"prefill_s": 0.0, "decode_s": 0.0, "prefill_tokens": 0, "decode_steps": 0, "decode_tokens": 0,
                       "calls": 0, "shared_prefix_tokens": 0}
@@ -69,6 +70,17 @@ class Generator:
             kernels.reserve_workspace(need, model.device)
 
     # --------------------------------------------------------------------------------
+    def _persistent_head_slot(self):
+        """The KV slot that keeps the last wave's shared prompt head (taken once, when a slot is
+        spare beyond the ones this call already holds; None when the cache has no slot to spare)."""
+        if self.head is not None:
+            return self.head["slot"]
+        if getattr(self, "_head_slot", None) is None:
+            if not self.cache.free:
+                return None
+            self._head_slot = self.cache.acquire(1)[0]
+        return self._head_slot
+
     def _state(self, B: int, max_new: int) -> DecodeState:
         key = (B, max_new)
         st = self.states.get(key)
@@ -182,22 +194,39 @@ class Generator:
             if self.sync_phases:
                 torch.cuda.synchronize(dev)
             t_pf = time.perf_counter()
-            P = self.shared_prefix_len(prompts)
-            if P:
-                # the shared head once (into row 0's slot), then only the suffixes, attending to the
-                # head's keys in that slot; decode reads keys [0, P) of every row from that slot too
-                # (st.pre), so the head's K/V exist once: prefilled once, read from L2/MALL by all rows
+            h = self.head
+            if h is not None and all(len(p) > h["P"] and p[:h["P"]] == h["tokens"] for p in prompts):
+                # prompt-head cache hit (a batch-1 query after earlier batches): no head prefill
+                P, hslot = h["P"], h["slot"]
+                self.stats["head_cache_hits"] = self.stats.get("head_cache_hits", 0) + n
+                self.stats["shared_prefix_tokens"] += P * n
+            else:
+                P = self.shared_prefix_len(prompts)
+                hslot = None
+            if P and hslot is None:
+                # the shared head once, then only the suffixes, attending to the head's keys in its
+                # slot; decode reads keys [0, P) of every row from that slot too (st.pre), so the
+                # head's K/V exist once: prefilled once, read from L2/MALL by all rows. The head goes
+                # into a slot of its own when one is free and is kept for later calls (a batch-1
+                # query then skips it); otherwise into row 0's slot for this call only.
+                hslot = self._persistent_head_slot()
+                keep = hslot is not None
+                if not keep:
+                    hslot = slots[0]
                 t0 = time.perf_counter()
                 to = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev, non_blocking=True)  # noqa: E731
                 m.prefill(to(np.asarray(prompts[0][:P], dtype=np.int32)), to(np.arange(P, dtype=np.int32)),
-                          to(np.full(P, slots[0], dtype=np.int32)), to(np.array([0, P], dtype=np.int32)), P,
+                          to(np.full(P, hslot, dtype=np.int32)), to(np.array([0, P], dtype=np.int32)), P,
                           to(np.array([P - 1], dtype=np.int64)))
                 self.stats["prefill_tokens"] += P
                 self.stats["shared_prefix_tokens"] += P * (n - 1)
                 self.stats["prefill_s"] += time.perf_counter() - t0
-                self._prefill_into(st, [p[P:] for p in prompts], slots, 0, prefix=(slots[0], P))
+                if keep:
+                    self.head = {"tokens": list(prompts[0][:P]), "P": P, "slot": hslot}
+            if P:
+                self._prefill_into(st, [p[P:] for p in prompts], slots, 0, prefix=(hslot, P))
                 pre = np.zeros((B, 2), dtype=np.int32)
-                pre[:n] = (P, slots[0])
+                pre[:n] = (P, hslot)
                 st.pre.copy_(torch.from_numpy(pre).to(dev))
             else:
                 st.pre.zero_()

@@ -307,7 +307,8 @@ def test_continuous_summaries_match_wave_summaries():
     got = asyncio.run(go())
     assert [(s, list(kp)) for s, kp in got] == [(s, list(kp)) for s, kp in want]
     # every slot is back except the dummy and the cached prompt heads
-    assert not e.scheduler.busy() and len(e.gen.cache.free) == e.gen.cache.slots - 1 - len(e.scheduler.heads)
+    assert not e.scheduler.busy() and len(e.gen.cache.free) == (e.gen.cache.slots - 1 - len(e.scheduler.heads)
+                                                                  - (e.gen.head is not None))
 
 
 def test_engine_search_microbatch_matches_single_searches(eng):
@@ -379,7 +380,19 @@ def test_shared_prompt_head_prefilled_once_same_tokens():
     assert all(abs(a.mean_prob - b.mean_prob) < 1e-3 for a, b in zip(got, want))
     assert g.stats["shared_prefix_tokens"] == 128 * 3
     assert g.stats["prefill_tokens"] - t_plain == t_plain - 128 * 3
-    assert len(g.cache.free) == g.cache.slots - 1
+    # every slot back except the dummy and the kept head
+    assert g.head is not None and g.head["P"] == 128
+    assert len(g.cache.free) == g.cache.slots - 2
+    # a later single prompt with the same head reuses the kept head (no head prefill), same tokens
+    single = head + list(rng.integers(5, 3000, size=9))
+    t0 = g.stats["prefill_tokens"]
+    got1 = g.generate([single], 6)[0]
+    assert g.stats["prefill_tokens"] - t0 == len(single) - 128 and g.stats["head_cache_hits"] == 1
+    g.share_prefix = False
+    h, g.head = g.head, None
+    ref1 = g.generate([single], 6)[0]
+    g.head, g.share_prefix = h, True
+    assert got1.tokens == ref1.tokens and abs(got1.mean_prob - ref1.mean_prob) < 1e-3
 
 
 def test_continuous_batching_caches_prompt_head():
