@@ -194,7 +194,7 @@ class Generator:
             if self.sync_phases:
                 torch.cuda.synchronize(dev)
             t_pf = time.perf_counter()
-            h = self.head
+            h = self.head if self.share_prefix else None
             if h is not None and all(len(p) > h["P"] and p[:h["P"]] == h["tokens"] for p in prompts):
                 # prompt-head cache hit (a batch-1 query after earlier batches): no head prefill
                 P, hslot = h["P"], h["slot"]

@@ -367,14 +367,17 @@ class EngineServer:
             for a, f in reqs:
                 groups.setdefault((int(a["k"]), float(a["min_sim"]), a.get("filters") is None), []).append((a, f))
             for (k, thr, nof), g in groups.items():
-                vecs = [np.asarray(a["vecs"], dtype=np.float32).reshape(-1, self.group.engine.dim) for a, _ in g]
-                filters = None
-                if not nof:
-                    filters = [flt for (a, _), v in zip(g, vecs) for flt in (a["filters"] * v.shape[0]
-                                                                             if len(a["filters"]) == 1
-                                                                             else a["filters"])]
                 t0 = time.perf_counter()
-                try:
+                try:  # a malformed request fails its group, never the loop (later searches would hang)
+                    vecs = [np.asarray(a["vecs"], dtype=np.float32).reshape(-1, self.group.engine.dim)
+                            for a, _ in g]
+                    filters = None
+                    if not nof:
+                        filters = [flt for (a, _), v in zip(g, vecs) for flt in (a["filters"] * v.shape[0]
+                                                                                 if len(a["filters"]) == 1
+                                                                                 else a["filters"])]
+                        if len(filters) != sum(v.shape[0] for v in vecs):
+                            raise ValueError("search: one document filter per query row (or one for all rows)")
                     s, ids = await self._gpu("search", {"vecs": np.concatenate(vecs), "k": k, "min_sim": thr,
                                                         "filters": filters})
                 except Exception as e:  # noqa: BLE001

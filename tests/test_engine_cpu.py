@@ -336,6 +336,15 @@ def test_engine_search_microbatch_matches_single_searches(eng):
         assert srv.stats["search"]["batches"] - b0 < len(args)
         for x, y in zip(alone, together):
             assert np.array_equal(x["keys"], y["keys"]) and np.allclose(x["scores"], y["scores"])
+        # a malformed search fails alone; the batcher keeps serving
+        try:
+            await cl.call("search", vecs=np.zeros((1, 7), dtype=np.float32), filters=None, k=3, min_sim=-1.0)
+        except Exception as e:  # noqa: BLE001
+            assert "reshape" in str(e) or "size" in str(e)
+        else:
+            raise AssertionError("expected a shape error")
+        again = await cl.call("search", **args[0])
+        assert np.array_equal(again["keys"], alone[0]["keys"])
         await cl.close()
         srv.server.close()
     asyncio.run(go())
@@ -388,10 +397,9 @@ def test_shared_prompt_head_prefilled_once_same_tokens():
     t0 = g.stats["prefill_tokens"]
     got1 = g.generate([single], 6)[0]
     assert g.stats["prefill_tokens"] - t0 == len(single) - 128 and g.stats["head_cache_hits"] == 1
-    g.share_prefix = False
-    h, g.head = g.head, None
+    g.share_prefix = False  # the kept head is ignored while sharing is off
     ref1 = g.generate([single], 6)[0]
-    g.head, g.share_prefix = h, True
+    g.share_prefix = True
     assert got1.tokens == ref1.tokens and abs(got1.mean_prob - ref1.mean_prob) < 1e-3
 
 
