@@ -88,7 +88,10 @@ def perf():
               (65536, 768, 3072, "none"), (65536, 3072, 768, "none"),
               # batch-1 prefill (~2.9k tokens): 256-row tiles underfill the chip at N = 3072
               (2930, 3072, 3072, "none"), (2930, 3072, 8192, "none"), (2930, 9216, 3072, "none"),
-              (2930, 16384, 3072, "swiglu"), (512, 9216, 3072, "none"), (256, 9216, 3072, "none")]
+              (2930, 16384, 3072, "swiglu"), (512, 9216, 3072, "none"), (256, 9216, 3072, "none"),
+              # batch-1 prefill after the kept 256-token prompt head (~2.6k suffix tokens)
+              (2614, 3072, 3072, "resid"), (2614, 3072, 8192, "resid"), (2614, 9216, 3072, "none"),
+              (2614, 16384, 3072, "swiglu")]
     only = os.environ.get("SHAPES")
     if only:
         shapes = [shapes[int(i)] for i in only.split(",")]

@@ -179,6 +179,8 @@ class KVCache:
 
 
 class LlamaDecoder:
+    unit_gains = False  # set by _fold_norm_gains
+
     def __init__(self, cfg: DecoderConfig, device="cuda", seed: int = 0, tp: TPContext | None = None,
                  weights: dict | None = None):
         self.cfg = cfg
@@ -191,8 +193,27 @@ class LlamaDecoder:
             raise ValueError(f"TP={t} must divide heads={cfg.heads} and kv_heads={cfg.kv_heads}")
         self.hl, self.kl = cfg.heads // t, cfg.kv_heads // t
         self.w = weights if weights is not None else random_weights(cfg, self.device, seed, self.tp.rank, t)
+        self._fold_norm_gains()
         self.cos_sin = rope_table(cfg.max_pos, cfg.head_dim, cfg.rope_theta, self.device)
         self.cache: KVCache | None = None
+
+    def _fold_norm_gains(self):
+        """Fold every RMSNorm gain into the weights that consume the normalised rows (W -> W diag(g),
+        then g = 1): the same model, and the batch-1 GEMVs fuse the norm without streaming a gain
+        vector next to the weights (rms=(None, eps)). Random-init gains are already 1; converted
+        checkpoints are folded here, once."""
+        pairs = [(L, "ln_attn", "wqkv") for L in self.w["layers"]] + [(L, "ln_mlp", "w_gu") for L in self.w["layers"]]
+        pairs.append((self.w, "norm", "lm_head"))
+        for d, gk, wk in pairs:
+            g = d[gk]
+            if not bool(torch.all(g == 1)):
+                d[wk] = (d[wk].float() * g.float()[None, :]).to(d[wk].dtype).contiguous()
+                d[gk] = torch.ones_like(g)
+        self.unit_gains = True
+
+    def _gain(self, g):
+        """The gain a fused batch-1 GEMV norm streams: none once the gains are folded."""
+        return None if self.unit_gains else g
 
     def alloc_cache(self, slots: int, max_seq: int) -> KVCache:
         max_seq = min(max_seq, self.cfg.max_pos)
@@ -208,7 +229,7 @@ class LlamaDecoder:
             o.gemm(a, L["wo"], out=x)
         tp.all_reduce_(x)
         if o.gemv_fusable(x.shape[0], L["w_gu"].shape[0], x.shape[1], EPI_SWIGLU):  # batch 1: norm fused
-            g = o.gemm(x, L["w_gu"], epi=EPI_SWIGLU, rms=(L["ln_mlp"], self.cfg.eps))
+            g = o.gemm(x, L["w_gu"], epi=EPI_SWIGLU, rms=(self._gain(L["ln_mlp"]), self.cfg.eps))
         else:
             h = o.rmsnorm(x, L["ln_mlp"], self.cfg.eps)
             g = o.gemm(h, L["w_gu"], epi=EPI_SWIGLU)
@@ -222,7 +243,7 @@ class LlamaDecoder:
     def _logits(self, hlast):
         o = self.ops
         if o.gemv_fusable(hlast.shape[0], self.w["lm_head"].shape[0], hlast.shape[1]):
-            logits = o.gemm(hlast.contiguous(), self.w["lm_head"], rms=(self.w["norm"], self.cfg.eps))
+            logits = o.gemm(hlast.contiguous(), self.w["lm_head"], rms=(self._gain(self.w["norm"]), self.cfg.eps))
         else:
             h = o.rmsnorm(hlast, self.w["norm"], self.cfg.eps)
             logits = o.gemm(h, self.w["lm_head"])
@@ -258,7 +279,7 @@ class LlamaDecoder:
         fuse = o.gemv_fusable(x.shape[0], self.w["layers"][0]["wqkv"].shape[0], x.shape[1])
         for li, L in enumerate(self.w["layers"]):
             if fuse:  # batch 1: RMSNorm folded into the QKV GEMV (no separate norm launch)
-                qkv = o.gemm(x, L["wqkv"], out=st.qkv, rms=(L["ln_attn"], c.eps))
+                qkv = o.gemm(x, L["wqkv"], out=st.qkv, rms=(self._gain(L["ln_attn"]), c.eps))
             else:
                 h = o.rmsnorm(x, L["ln_attn"], c.eps, out=st.h)
                 qkv = o.gemm(h, L["wqkv"], out=st.qkv)

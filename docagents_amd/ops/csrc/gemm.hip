@@ -298,6 +298,9 @@ gemv_kernel(GemmArgs p) {
   for (int r = 0; r < R; ++r) wr[r] = p.W + (size_t)min(rows[r], p.N - 1) * p.K + lane * 8;
   const bf16_t* ar = p.A + lane * 8;
   const bf16_t* gr = p.gamma ? p.gamma + lane * 8 : nullptr;
+  // fused RMSNorm: eps > 0 (gamma null = unit gain: the decoder folds RMSNorm gains into the
+  // following weights at load, so the GEMV streams no gain vector)
+  const bool rms = p.eps > 0.f;
   const int nkb = p.K / 512;
   float acc[R];
 #pragma unroll
@@ -322,10 +325,13 @@ gemv_kernel(GemmArgs p) {
         a[2 * e] = bf2f((bf16_t)(av[u][e] & 0xffff));
         a[2 * e + 1] = bf2f((bf16_t)(av[u][e] >> 16));
       }
+      if (rms) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) ss = fmaf(a[2 * e], a[2 * e], fmaf(a[2 * e + 1], a[2 * e + 1], ss));
+      }
       if (gr) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          ss = fmaf(a[2 * e], a[2 * e], fmaf(a[2 * e + 1], a[2 * e + 1], ss));
           a[2 * e] *= bf2f((bf16_t)(gv[u][e] & 0xffff));
           a[2 * e + 1] *= bf2f((bf16_t)(gv[u][e] >> 16));
         }
@@ -341,7 +347,7 @@ gemv_kernel(GemmArgs p) {
   }
 #pragma unroll
   for (int r = 0; r < R; ++r) acc[r] = wave_sum(acc[r]);
-  if (gr) {
+  if (rms) {
     const float inv = rsqrtf(wave_sum(ss) / p.K + p.eps);
 #pragma unroll
     for (int r = 0; r < R; ++r) acc[r] *= inv;
@@ -569,7 +575,7 @@ DA_EXPORT int da_gemm_bf16(const void* A, int lda, const void* W, void* C, int l
   a.bias = (const bf16_t*)bias; a.resid = (const bf16_t*)resid; a.ws = (float*)ws;
   a.M = M; a.N = N; a.K = K; a.lda = lda; a.ldc = ldc; a.ldr = ldr; a.k_per_split = K / splits;
   a.gamma = (const bf16_t*)rms_gamma; a.eps = rms_eps;
-  if (rms_gamma && tile != 6) return (int)hipErrorInvalidValue;  // fused RMSNorm: GEMV path only
+  if ((rms_gamma || rms_eps > 0.f) && tile != 6) return (int)hipErrorInvalidValue;  // fused RMSNorm: GEMV only
   if (tile == 0) {
     const long t256 = (long)((M + 255) / 256) * ((N + 255) / 256);
     // decode-sized M: 32x128 / 64x128 weight-streaming tiles (+ split-K, chosen by the caller);

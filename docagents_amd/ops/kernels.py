@@ -179,7 +179,7 @@ def gemm(a: torch.Tensor, w: torch.Tensor, bias=None, epi: int = EPI_NONE, resid
          tile: int = 0, splits: int = 0, rms=None) -> torch.Tensor:
     """out[M, N'] = epi(a[M, K] @ w[N, K]^T). N' = N/2 for EPI_SWIGLU (w rows interleaved by 16).
     rms = (gamma, eps): ``a`` is the raw residual stream and RMSNorm(a) * gamma is fused into the
-    GEMV (M == 1 only, see gemv_fusable)."""
+    GEMV (M == 1 only, see gemv_fusable); gamma None = unit gain (folded into ``w``)."""
     _bf16_cuda(a, "a"); _bf16_cuda(w, "w")
     _req(a.dim() == 2 and w.dim() == 2, "gemm expects 2-D operands")
     M, K = a.shape
@@ -216,10 +216,12 @@ def gemm(a: torch.Tensor, w: torch.Tensor, bias=None, epi: int = EPI_NONE, resid
         return swiglu_interleaved(torch.mm(a, w.t()), out)
     if tile == 0 and splits <= 0 and gemv_fusable(M, N, K, epi):
         tile, splits = 6, 1  # batch-1 decode: weight-streaming GEMV, one launch, no split-K workspace
-    gamma, eps = (None, 0.0) if rms is None else rms
-    if gamma is not None:
+    gamma, eps = (None, 0.0) if rms is None else rms  # rms = (gain or None for unit gain, eps > 0)
+    if rms is not None:
         _req(tile == 6, "fused RMSNorm needs the M == 1 GEMV path")
-        _bf16_cuda(gamma, "gamma"); _req(gamma.numel() == K, "gamma must be [K]")
+        _req(eps > 0, "fused RMSNorm needs eps > 0")
+        if gamma is not None:
+            _bf16_cuda(gamma, "gamma"); _req(gamma.numel() == K, "gamma must be [K]")
     if splits <= 0:
         if tile == 0 and M < 640:
             tile = _decode_tile(M)

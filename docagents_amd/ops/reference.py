@@ -20,7 +20,8 @@ def gemv_fusable(M, N, K, epi=EPI_NONE):
 
 def gemm(a, w, bias=None, epi=EPI_NONE, resid=None, out=None, rms=None, **_):
     if rms is not None:  # same numerics as rmsnorm() followed by gemm() (bf16 normalised row)
-        a = rmsnorm(a, rms[0], rms[1])
+        g = rms[0] if rms[0] is not None else torch.ones(a.shape[1], dtype=a.dtype, device=a.device)
+        a = rmsnorm(a, g, rms[1])
     return _epilogue(a.float() @ w.float().t(), w.shape[0], bias, epi, resid, out)
 
 

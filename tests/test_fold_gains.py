@@ -1,0 +1,49 @@
+"""RMSNorm-gain folding (LlamaDecoder._fold_norm_gains): W diag(g) with g = 1 is the same model as
+(W, g). A checkpoint's non-unit gains are folded at construction; the folded model's logits must
+match an unfolded model's on the same weights (fp32 reference ops on the CPU; the GPU test in
+test_models_gpu.py covers the fused batch-1 GEMV path that relies on the unit gain)."""
+import copy
+
+import torch
+
+from docagents_amd.models.configs import decoder_config
+from docagents_amd.models.llama import LlamaDecoder, random_weights
+
+
+class _Unfolded(LlamaDecoder):
+    def _fold_norm_gains(self):
+        pass
+
+
+def _gains(w, seed):
+    g = torch.Generator().manual_seed(seed)
+    for L in w["layers"]:
+        for k in ("ln_attn", "ln_mlp"):
+            L[k] = (0.5 + torch.rand(L[k].shape, generator=g)).to(L[k].dtype)
+    w["norm"] = (0.5 + torch.rand(w["norm"].shape, generator=g)).to(w["norm"].dtype)
+    return w
+
+
+def _last_logits(m, seq):
+    t = torch.tensor(seq, dtype=torch.int32)
+    return m.prefill(t, torch.arange(len(seq), dtype=torch.int32), torch.zeros(len(seq), dtype=torch.int32),
+                     torch.tensor([0, len(seq)], dtype=torch.int32), len(seq),
+                     torch.tensor([len(seq) - 1]))[0].float()
+
+
+def test_folded_gains_match_unfolded_model():
+    cfg = decoder_config("tiny-dec")
+    w = _gains(random_weights(cfg, "cpu", seed=11), seed=3)
+    ref = _Unfolded(cfg, "cpu", weights=copy.deepcopy(w))
+    m = LlamaDecoder(cfg, "cpu", weights=copy.deepcopy(w))
+    for L in m.w["layers"]:
+        assert bool((L["ln_attn"] == 1).all()) and bool((L["ln_mlp"] == 1).all())
+    assert bool((m.w["norm"] == 1).all())
+    assert not torch.equal(m.w["lm_head"], w["lm_head"])
+    for mm in (ref, m):
+        mm.alloc_cache(2, 128)
+    seq = list(range(17, 17 + 40))
+    a, b = _last_logits(ref, seq), _last_logits(m, seq)
+    # the folded weights are rounded to bf16 once: noise of a few bf16 ulps on O(1) logits
+    assert float((a - b).abs().max()) < 0.05 * max(1.0, float(a.abs().max()))
+    assert float(torch.nn.functional.cosine_similarity(a, b, dim=0)) > 0.999

@@ -215,3 +215,34 @@ def test_generate_batch_above_64_graph_equals_eager():
     r.alloc_cache(2, 256)
     for i in (0, 57, 99):
         _near_argmax_under_reference(r, prompts[i], out1[i].tokens)
+
+
+def test_batch1_decode_folded_gains_matches_unfolded():
+    """Batch-1 decode fuses RMSNorm into the QKV / gate-up / lm-head GEMVs. With the checkpoint's
+    gains folded into those weights the GEMVs run gain-free (rms=(None, eps)); an unfolded model
+    streams the gains. Both must generate the same greedy tokens."""
+    import copy
+    from docagents_amd.models.llama import random_weights
+
+    class Unfolded(LlamaDecoder):
+        def _fold_norm_gains(self):
+            pass
+
+    cfg = decoder_config("tiny-dec")
+    w = random_weights(cfg, "cuda", seed=12)
+    g = torch.Generator(device="cuda").manual_seed(5)
+    for L in w["layers"]:
+        for k in ("ln_attn", "ln_mlp"):
+            L[k] = (0.5 + torch.rand(L[k].shape, generator=g, device="cuda")).to(torch.bfloat16)
+    w["norm"] = (0.5 + torch.rand(w["norm"].shape, generator=g, device="cuda")).to(torch.bfloat16)
+    m, u = LlamaDecoder(cfg, "cuda", weights=copy.deepcopy(w)), Unfolded(cfg, "cuda", weights=copy.deepcopy(w))
+    assert m.unit_gains and not u.unit_gains
+    assert m.ops.gemv_fusable(1, m.w["layers"][0]["wqkv"].shape[0], cfg.hidden)
+    outs = []
+    for mm in (m, u):
+        mm.alloc_cache(3, 256)
+        outs.append(Generator(mm, max_batch=2, max_seq=256, temperature=0.0, use_graphs=True)
+                    .generate([list(range(50, 83))], 10)[0])
+    a, b = outs
+    assert sum(x == y for x, y in zip(a.tokens, b.tokens)) >= 8, (a.tokens, b.tokens)
+    assert abs(a.mean_prob - b.mean_prob) < 0.05 * max(a.mean_prob, 1e-6) + 1e-4
