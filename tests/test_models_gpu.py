@@ -228,7 +228,10 @@ def test_batch1_decode_folded_gains_matches_unfolded():
         def _fold_norm_gains(self):
             pass
 
-    cfg = decoder_config("tiny-dec")
+    import dataclasses
+    # hidden 512: the GEMV path needs K % 512 == 0 (tiny-dec's 256 would route to the tile GEMM)
+    cfg = dataclasses.replace(decoder_config("tiny-dec"), name="tiny-dec-512", hidden=512, heads=8,
+                              kv_heads=4, ffn=1024)
     w = random_weights(cfg, "cuda", seed=12)
     g = torch.Generator(device="cuda").manual_seed(5)
     for L in w["layers"]:
