@@ -29,6 +29,9 @@ from . import prompts as P
 from .generator import Generator
 
 
+_SERIAL_TOKENIZE = os.environ.get("DA_SERIAL_TOKENIZE", "0") == "1"  # A/B arm: one encode per string
+
+
 class Engine:
     def __init__(self, embed_arch: str = "bge-base", llm_arch: str = "phi3-mini", device="cuda", seed: int = 0,
                  tp: TPContext | None = None, max_batch: int = 64, max_seq: int = 4096, temperature: float = 0.2,
@@ -113,6 +116,14 @@ class Engine:
     def _ids(self, s: str) -> list[int]:
         return self.dec_tok.encode(s, add_special_tokens=False).ids
 
+    def _ids_many(self, texts: list[str]) -> list[list[int]]:
+        """Batch tokenization (the tokenizer's thread pool): 64 2000-word documents take 250 ms
+        one ``encode`` at a time on the GPU box's CPU share, ~10 % of an ingest batch
+        (bench/tok_timing.py)."""
+        if len(texts) <= 1 or _SERIAL_TOKENIZE:
+            return [self._ids(t) for t in texts]
+        return [e.ids for e in self.dec_tok.encode_batch(texts, add_special_tokens=False)]
+
     def _cached_ids(self, s: str) -> list[int]:
         v = self._prefix_cache.get(s)
         if v is None:
@@ -123,12 +134,18 @@ class Engine:
     def context_budget(self, max_new: int) -> int:
         return self.gen.cache.max_seq - max_new - 8
 
-    def answer_prompt_ids(self, question: str, chunk_ids: list[list[int]], max_new: int) -> list[int]:
+    def _answer_tail(self, question: str) -> str:
+        return f"\nQuestion: {question}<|end|>\n<|assistant|>\n"
+
+    def answer_prompt_ids(self, question: str, chunk_ids: list[list[int]], max_new: int,
+                          tail: list[int] | None = None) -> list[int]:
         """Chat prompt for Answer with pre-tokenized chunks (tokenized once at ingest). Drops the
-        lowest-ranked chunks first when the prompt would not fit the context."""
+        lowest-ranked chunks first when the prompt would not fit the context.
+        ``tail``: the question turn already tokenized (answer_many tokenizes a batch at once)."""
         head = self._cached_ids(f"<|system|>\n{P.ANSWER_SYSTEM}<|end|>\n<|user|>\nContext:\n")
         nl = self._cached_ids("\n")
-        tail = self._ids(f"\nQuestion: {question}<|end|>\n<|assistant|>\n")
+        if tail is None:
+            tail = self._ids(self._answer_tail(question))
         budget = self.context_budget(max_new) - len(head) - len(tail)
         ctx: list[int] = []
         for c in chunk_ids:
@@ -142,13 +159,12 @@ class Engine:
         """items: (question, [chunk token-id lists ranked by score], context_quality) ->
         [(answer, confidence)] with confidence = quality * mean token probability."""
         max_new = max_new or self.max_new_tokens
-        prompts = [self.answer_prompt_ids(q, ch, max_new) for q, ch, _ in items]
+        tails = self._ids_many([self._answer_tail(q) for q, _, _ in items])
+        prompts = [self.answer_prompt_ids(q, ch, max_new, tail=t) for (q, ch, _), t in zip(items, tails)]
         with self.lock:
             res = self.gen.generate(prompts, max_new)
-        out = []
-        for (q, ch, quality), r in zip(items, res):
-            out.append((self.chat.decode(r.tokens), float(quality) * r.mean_prob))
-        return out
+        texts = self.chat.decode_many([r.tokens for r in res])
+        return [(txt, float(quality) * r.mean_prob) for (_, _, quality), r, txt in zip(items, res, texts)]
 
     # ------------------------------------------------------------------ continuous batching
     @property
@@ -196,8 +212,7 @@ class Engine:
         is_partial). CPU only (tokenization), so the server runs it off the GPU thread."""
         head, tail, budget = self._summary_frame(max_new or self.summary_max_new)
         windows, owner = [], []
-        for i, t in enumerate(texts):
-            ids = self._ids(t)
+        for i, ids in enumerate(self._ids_many(list(texts))):
             if len(ids) <= budget:
                 windows.append(head + ids + tail)
                 owner.append((i, False))
@@ -210,7 +225,9 @@ class Engine:
     def summary_reduce_prompts(self, partial: dict[int, list[str]], max_new: int | None = None):
         """Reduce step: one prompt over the joined window summaries of each long text."""
         head, tail, budget = self._summary_frame(max_new or self.summary_max_new)
-        return [(i, head + self._ids("\n".join(parts))[:budget] + tail) for i, parts in partial.items()]
+        keys = list(partial)
+        ids = self._ids_many(["\n".join(partial[i]) for i in keys])
+        return [(i, head + x[:budget] + tail) for i, x in zip(keys, ids)]
 
     def summarize_many(self, texts: list[str], max_new: int | None = None) -> list[tuple[str, list[str]]]:
         """Summarize each text; texts longer than the decoder context are summarized map-reduce:
@@ -221,8 +238,7 @@ class Engine:
             res = self.gen.generate(windows, max_new)
         partial: dict[int, list[str]] = {}
         final: dict[int, str] = {}
-        for (i, is_part), r in zip(owner, res):
-            txt = self.chat.decode(r.tokens)
+        for (i, is_part), txt in zip(owner, self.chat.decode_many([r.tokens for r in res])):
             if is_part:
                 partial.setdefault(i, []).append(txt)
             else:
@@ -231,8 +247,8 @@ class Engine:
             red = self.summary_reduce_prompts(partial, max_new)
             with self.lock:
                 rres = self.gen.generate([p for _, p in red], max_new)
-            for (i, _), r in zip(red, rres):
-                final[i] = self.chat.decode(r.tokens)
+            for (i, _), txt in zip(red, self.chat.decode_many([r.tokens for r in rres])):
+                final[i] = txt
         return [extract_summary(final[i]) for i in range(len(texts))]
 
     # ------------------------------------------------------------------ introspection

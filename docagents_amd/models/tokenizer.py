@@ -97,3 +97,7 @@ class ChatFormat:
 
     def decode(self, ids: list[int]) -> str:
         return self.tok.decode(ids, skip_special_tokens=True)
+
+    def decode_many(self, seqs: list[list[int]]) -> list[str]:
+        return self.tok.decode_batch([list(x) for x in seqs], skip_special_tokens=True) if len(seqs) > 1 \
+            else [self.decode(x) for x in seqs]

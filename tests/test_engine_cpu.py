@@ -473,3 +473,23 @@ def test_interleaved_rope_conversion_preserves_attention_scores():
     got = R.rope_cache(qkv.clone(), pos.int(), R.rope_table(128, D, 10000.0), H, Hkv, D)
     want = interleaved_rope(qkv.double()[:, :(H + Hkv) * D].view(T, H + Hkv, D)).reshape(T, -1)
     torch.testing.assert_close(got[:, :(H + Hkv) * D].double(), want, rtol=0.02, atol=0.02)
+
+
+def test_batched_tokenization_matches_serial(eng):
+    """summary windows / reduce prompts / answer tails are tokenized with encode_batch and
+    detokenized with decode_batch: identical ids and texts to one call per string."""
+    texts = ["alpha beta gamma " * 50, "", "delta <|end|> epsilon", "zeta\nêta " * 300]
+    assert eng._ids_many(texts) == [eng._ids(t) for t in texts]
+    seqs = [eng._ids(t) for t in texts]
+    assert eng.chat.decode_many(seqs) == [eng.chat.decode(s) for s in seqs]
+    w, owner = eng.summary_windows(texts, 16)
+    head, tail, budget = eng._summary_frame(16)
+    want = []
+    for t in texts:
+        ids = eng._ids(t)
+        want.extend([head + ids + tail] if len(ids) <= budget else
+                     [head + ids[s:s + budget] + tail for s in range(0, len(ids), budget)])
+    assert w == want
+    q = "what is alpha?"
+    assert eng.answer_prompt_ids(q, [[5, 6]], 16) == \
+        eng.answer_prompt_ids(q, [[5, 6]], 16, tail=eng._ids_many([eng._answer_tail(q)] * 2)[0])
