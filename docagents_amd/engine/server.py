@@ -245,7 +245,7 @@ class EngineServer:
 
     def __init__(self, group: EngineGroup, log, max_batch_items: int = 256, step_timeout_s: float = 300.0,
                  hard_timeout_s: float = 0.0, liveness_s: float = 30.0, profiler: StepProfiler | None = None,
-                 continuous: bool = False, cb_steps: int = 8, checkpoint_s: float = 0.0,
+                 continuous: bool = False, cb_steps: int = 1, checkpoint_s: float = 0.0,
                  cb_window_s: float = 0.02):
         self.group, self.log = group, log
         self.checkpoint_s = checkpoint_s  # periodic shard snapshots when the shard is durable (0 = off)
