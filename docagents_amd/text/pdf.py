@@ -16,6 +16,8 @@ import re
 import zlib
 
 
+_LIT_SPECIAL = re.compile(rb"[\\()]")
+
 class PDFError(ValueError):
     pass
 
@@ -112,6 +114,14 @@ class Lexer:
         out = bytearray()
         depth = 1
         while self.p < n:
+            # copy the run up to the next byte that matters ('\\', '(' or ')') in one slice: a
+            # content stream is mostly long literal strings, byte-at-a-time Python was 70 % of extraction
+            m_ = _LIT_SPECIAL.search(d, self.p)
+            if m_ is None:
+                break
+            if m_.start() > self.p:
+                out += d[self.p:m_.start()]
+                self.p = m_.start()
             c = d[self.p]
             if c == 0x5C:  # backslash
                 self.p += 1
