@@ -241,6 +241,7 @@ def main():
     # ---- ingest docs/min: chunk -> enrich+embed -> summarize -> index (per GPU, batched) ----
     docs_per_min = None
     ingest_runs = []
+    ingest_phases: dict = {}
     if a.ingest_docs > 0:
         dg = TextGen(seed=500 + dp_rank)
         batches = [[dg.document(a.ingest_words) for _ in range(a.ingest_docs)] for _ in range(max(1, a.ingest_batches))]
@@ -253,9 +254,18 @@ def main():
                 return [" ".join(w[i:i + per]) for i in range(0, len(w), per)]
             batches = [[make_pdf(_pages(t)) for t in texts] for texts in batches]
 
-        def ingest(texts, tag):
+        def ingest(texts, tag, ph=None):
+            # ph: dict -> per-phase wall time (ms), device-synchronized at each boundary (untimed run)
+            tp = [time.perf_counter()]
+
+            def mark(name):
+                if ph is not None:
+                    torch.cuda.synchronize()
+                    tp.append(time.perf_counter())
+                    ph[name] = round((tp[-1] - tp[-2]) * 1000, 2)
             if a.pdf_ingest:
                 texts = [pdf_text(b) for b in texts]  # the gateway's PDF extraction (cmd/gateway/main.go:223-249)
+                mark("pdf_extract")
             all_chunks, owners, summ_in = [], [], []
             for j, t in enumerate(texts):
                 cs = chunk_text(t, Options(400, 80))
@@ -263,12 +273,16 @@ def main():
                 owners.append(len(cs))
                 # the analysis agent's summary input: ord-ordered chunks, overlaps removed (§5.7)
                 summ_in.append(concatenate_chunks(dedup_overlap([c.text for c in cs], 80)))
+            mark("chunk")
             vec = eng.embed(all_chunks)
+            mark("embed")
             summaries = eng.summarize_many(summ_in)
+            mark("summarize")
             o = 0
             for j, n in enumerate(owners):
                 eng.index.add(f"ing{tag}-{R}-{j}", np.arange(n) + 5_000_000_000 + o, vec[o:o + n])
                 o += n
+            mark("index_add")
             return summaries
 
         ingest(batches[0][:2], "w")
@@ -280,6 +294,9 @@ def main():
             di = all_reduce_max(time.perf_counter() - t2, dev)
             ingest_runs.append(DP * a.ingest_docs / di * 60.0)
         docs_per_min = statistics.median(ingest_runs)
+        if a.breakdown:
+            ingest(batches[0], "b", ph=ingest_phases)
+            log(info, f"ingest batch phases (ms): {ingest_phases}")
 
     gen = eng.gen.stats
     out = {
@@ -304,6 +321,7 @@ def main():
         "prefill_tokens": gen["prefill_tokens"], "decode_steps": gen["decode_steps"],
         "qa_step_phase_ms": phases or None,
         "latency_phase_ms": lat_phases or None,
+        "ingest_phase_ms": ingest_phases or None,
     }
     if R == 0:
         print(json.dumps(out), flush=True)
