@@ -11,6 +11,7 @@ from __future__ import annotations
 
 import collections
 import math
+import os
 import time
 from types import SimpleNamespace
 
@@ -36,7 +37,7 @@ class GenResult:
 
 class Generator:
     def __init__(self, model: LlamaDecoder, max_batch: int = 64, max_seq: int = 4096, temperature: float = 0.2,
-                 seed: int = 0, eos=(), use_graphs: bool = True, max_prefill_tokens: int = 32768,
+                 seed: int = 0, eos=(), use_graphs: bool = True, max_prefill_tokens: int = 65536,
                  check_every: int = 16, share_prefix: bool = True, min_shared_prefix: int = 64):
         self.model = model
         # prompts of one wave that start with the same tokens (the Answer / Summarize system prompt:
@@ -47,7 +48,9 @@ class Generator:
         self.eos = tuple(e for e in eos if e is not None)[:4]
         self.is_cuda = model.device.type == "cuda"
         self.use_graphs = use_graphs and self.is_cuda
-        self.max_prefill_tokens = max_prefill_tokens
+        # 64k-token chunks: fewer partial tile rounds per GEMM than 32k (same box, 2 rounds each:
+        # QA prefill 1103 vs 1119 ms, profiles/r2/ab_prefill_chunk/); DA_PREFILL_TOKENS overrides (A/B)
+        self.max_prefill_tokens = int(os.environ.get("DA_PREFILL_TOKENS", max_prefill_tokens))
         self.check_every = check_every
         if model.cache is None:
             # one extra slot: the dummy slot for padded rows of a bucket
@@ -307,7 +310,7 @@ class ContinuousScheduler:
         # prompt tokens admitted per tick (prefilled in max_prefill_tokens chunks): a burst of long
         # prompts (a batch of summaries) joins in one or two ticks instead of trickling in at one
         # prefill chunk per tick, which would stretch the decode of the last-admitted rows
-        self.max_admit_tokens = max_admit_tokens or 4 * gen.max_prefill_tokens
+        self.max_admit_tokens = max_admit_tokens or 131072  # 4 x 32k-token chunks (deploy-stack tuning)
         self.st = DecodeState(self.m, self.B, self.cap, gen.temperature, gen.seed, gen.eos)
         self.rows: list = [None] * self.B        # row -> (tag, slot, budget)
         self.pending: collections.deque = collections.deque()
