@@ -277,12 +277,17 @@ gemm_splitk_reduce(const float* __restrict__ ws, int splits, int M, int N, int e
 // dot products accumulate in fp32 per lane and each row is reduced across the wave once.
 // The activation row (K bf16) is read through the caches (every wave reads the same vector).
 // EPI_SWIGLU: a wave owns 2 gate rows and their 2 up rows (16-row interleave) -> 2 outputs.
-template <int EPI, int R, int U>
+// KS = 2: two neighbouring waves of a workgroup split a row's K range (long rows on narrow
+// matrices: the K=8192 down projection has 3072 rows, one 16 KiB row per wave was two dependent
+// HBM round trips at U=8) and combine their partial sums through LDS.
+template <int EPI, int R, int U, int KS = 1>
 __global__ void __launch_bounds__(256)
 gemv_kernel(GemmArgs p) {
   static_assert(EPI != EPI_SWIGLU || R == 4, "SwiGLU waves own 2 gate + 2 up rows");
+  static_assert(KS == 1 || KS == 2, "KS");
   const int lane = threadIdx.x & 63;
-  const int wg = blockIdx.x * 4 + (threadIdx.x >> 6);  // global wave index
+  const int wv = blockIdx.x * 4 + (threadIdx.x >> 6);  // global wave index
+  const int wg = wv / KS, ks = wv % KS;                 // row group, K part
   int rows[R];
   if constexpr (EPI == EPI_SWIGLU) {
     const int g = wg >> 3, t = wg & 7;
@@ -292,7 +297,7 @@ gemv_kernel(GemmArgs p) {
 #pragma unroll
     for (int r = 0; r < R; ++r) rows[r] = wg * R + r;
   }
-  if (rows[0] >= p.N) return;
+  if (KS == 1 && rows[0] >= p.N) return;  // KS = 2: every wave reaches the LDS exchange below
   const bf16_t* wr[R];
 #pragma unroll
   for (int r = 0; r < R; ++r) wr[r] = p.W + (size_t)min(rows[r], p.N - 1) * p.K + lane * 8;
@@ -302,15 +307,16 @@ gemv_kernel(GemmArgs p) {
   // following weights at load, so the GEMV streams no gain vector)
   const bool rms = p.eps > 0.f;
   const int nkb = p.K / 512;
+  const int kb0 = ks * nkb / KS, kb1 = (ks + 1) * nkb / KS;
   float acc[R];
 #pragma unroll
   for (int r = 0; r < R; ++r) acc[r] = 0.f;
-  float ss = 0.f;  // fused RMSNorm: sum of squares of the raw input row (every wave sees all of it)
-  for (int kb = 0; kb < nkb; kb += U) {
+  float ss = 0.f;  // fused RMSNorm: sum of squares of the raw input row (the wave's K range)
+  for (int kb = kb0; kb < kb1; kb += U) {
     u32x4_t wv[U][R], av[U], gv[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const int k = min(kb + u, nkb - 1) * 512;
+      const int k = min(kb + u, kb1 - 1) * 512;
 #pragma unroll
       for (int r = 0; r < R; ++r) wv[u][r] = __builtin_nontemporal_load((const u32x4_t*)(wr[r] + k));
       av[u] = *(const u32x4_t*)(ar + k);
@@ -318,7 +324,7 @@ gemv_kernel(GemmArgs p) {
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      if (kb + u >= nkb) break;
+      if (kb + u >= kb1) break;
       float a[8];
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
@@ -347,8 +353,23 @@ gemv_kernel(GemmArgs p) {
   }
 #pragma unroll
   for (int r = 0; r < R; ++r) acc[r] = wave_sum(acc[r]);
+  if (rms) ss = wave_sum(ss);
+  if constexpr (KS == 2) {
+    __shared__ float xch[4][R + 1];
+    const int w = threadIdx.x >> 6;
+    if (lane == 0) {
+#pragma unroll
+      for (int r = 0; r < R; ++r) xch[w][r] = acc[r];
+      xch[w][R] = ss;
+    }
+    __syncthreads();
+    if (ks != 0 || rows[0] >= p.N) return;
+#pragma unroll
+    for (int r = 0; r < R; ++r) acc[r] += xch[w + 1][r];
+    ss += xch[w + 1][R];
+  }
   if (rms) {
-    const float inv = rsqrtf(wave_sum(ss) / p.K + p.eps);
+    const float inv = rsqrtf(ss / p.K + p.eps);
 #pragma unroll
     for (int r = 0; r < R; ++r) acc[r] *= inv;
   }
@@ -374,15 +395,15 @@ gemv_kernel(GemmArgs p) {
   }
 }
 
-template <int R, int U>
+template <int R, int U, int KS = 1>
 static int launch_gemv_r(const GemmArgs& a, int epi, hipStream_t s) {
-  const int waves = (a.N + R - 1) / R;
+  const int waves = (a.N + R - 1) / R * KS;
   dim3 grid((waves + 3) / 4), block(256);
   switch (epi) {
-    case EPI_NONE: gemv_kernel<EPI_NONE, R, U><<<grid, block, 0, s>>>(a); break;
-    case EPI_BIAS: gemv_kernel<EPI_BIAS, R, U><<<grid, block, 0, s>>>(a); break;
-    case EPI_GELU: gemv_kernel<EPI_GELU, R, U><<<grid, block, 0, s>>>(a); break;
-    case EPI_RESID: gemv_kernel<EPI_RESID, R, U><<<grid, block, 0, s>>>(a); break;
+    case EPI_NONE: gemv_kernel<EPI_NONE, R, U, KS><<<grid, block, 0, s>>>(a); break;
+    case EPI_BIAS: gemv_kernel<EPI_BIAS, R, U, KS><<<grid, block, 0, s>>>(a); break;
+    case EPI_GELU: gemv_kernel<EPI_GELU, R, U, KS><<<grid, block, 0, s>>>(a); break;
+    case EPI_RESID: gemv_kernel<EPI_RESID, R, U, KS><<<grid, block, 0, s>>>(a); break;
     default: return (int)hipErrorInvalidValue;
   }
   return (int)hipGetLastError();
@@ -392,6 +413,8 @@ static int launch_gemv_r(const GemmArgs& a, int epi, hipStream_t s) {
 // (K = 3072: 6 blocks, one round of loads and no clamped duplicate loads), 8 per round otherwise.
 static int g_gemv_u = 0;  // 0 = auto; 4 = the fixed round-1 depth (A/B)
 DA_EXPORT void da_set_gemv_u(int v) { g_gemv_u = v; }
+static int g_gemv_ks = 2;  // K split across 2 waves for long rows on narrow matrices (1 = off, A/B)
+DA_EXPORT void da_set_gemv_ks(int v) { g_gemv_ks = v == 1 ? 1 : 2; }
 static int gemv_u(int K, int /*R*/) {
   const int nkb = K / 512;
   if (g_gemv_u) return g_gemv_u;
@@ -426,6 +449,8 @@ static int launch_gemv(const GemmArgs& a, int epi, hipStream_t s) {
   }
   if (a.N >= 16384) return launch_gemv_ru<4>(a, epi, s);
   if (a.N >= 8192) return launch_gemv_ru<2>(a, epi, s);
+  // long rows on a narrow matrix (down projection, K = 8192): two waves per row, 8 blocks each
+  if (g_gemv_ks == 2 && a.K >= 8192 && a.K % 1024 == 0) return launch_gemv_r<1, 8, 2>(a, epi, s);
   return launch_gemv_ru<1>(a, epi, s);
 }
 

@@ -60,6 +60,7 @@ _SIGS = {
     "da_set_flash_pipe": [c_int],
     "da_set_gemm_pf": [c_int],
     "da_set_gemv_u": [c_int],
+    "da_set_gemv_ks": [c_int],
     "da_set_decode_pft": [c_int],
     "da_set_flash_rev": [c_int],
     "da_decode_attn": [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
@@ -116,6 +117,8 @@ def lib() -> ctypes.CDLL:
             L.da_set_flash_qh(int(os.environ["DA_FLASH_QH"]))
         if os.environ.get("DA_GEMV_U") is not None:  # batch-1 GEMV K-blocks in flight per row (A/B)
             L.da_set_gemv_u(int(os.environ["DA_GEMV_U"]))
+        if os.environ.get("DA_GEMV_KS") is not None:  # batch-1 GEMV waves per long row: 1 or 2 (A/B)
+            L.da_set_gemv_ks(int(os.environ["DA_GEMV_KS"]))
         if os.environ.get("DA_FLASH_REV") is not None:  # causal flash longest-first dispatch (A/B)
             L.da_set_flash_rev(int(os.environ["DA_FLASH_REV"]))
         if os.environ.get("DA_DECODE_PFT") is not None:  # MHA decode next-tile prefetch below B*Hkv (A/B)

@@ -443,6 +443,28 @@ def test_gemv_batch1_decode(N, Kd, epi):
     assert torch.equal(auto, got)
 
 
+@pytest.mark.parametrize("ks", [1, 2])
+@pytest.mark.parametrize("N,Kd", [(3072, 8192), (1000, 16384), (8, 8192), (3072, 9216)])
+@pytest.mark.parametrize("epi", [K.EPI_NONE, K.EPI_BIAS, K.EPI_RESID])
+def test_gemv_long_rows_two_waves(ks, N, Kd, epi):
+    """Batch-1 GEMV on narrow matrices with long rows (the K=8192 down projection): two waves split
+    each row's K range and combine through LDS (ks=2, the default) == one wave per row == fp32."""
+    torch.manual_seed(N + Kd + epi)
+    a, w = _rand(1, Kd), _rand(N, Kd, scale=Kd ** -0.5)
+    bias = _rand(N) if epi in (K.EPI_BIAS, K.EPI_RESID) else None
+    resid = _rand(1, N) if epi == K.EPI_RESID else None
+    K.lib().da_set_gemv_ks(ks)
+    try:
+        got = K.gemm(a, w, bias=bias, epi=epi, resid=resid, tile=6, splits=1)
+        g = _rand(Kd) + 1.0
+        x = _rand(1, Kd, scale=3.0)
+        fused = K.gemm(x, w, epi=epi, bias=bias, resid=resid, rms=(g, 1e-5))
+    finally:
+        K.lib().da_set_gemv_ks(2)
+    _close(got, R.gemm(a, w, bias=bias, epi=epi, resid=resid), atol=0.03)
+    _close(fused, R.gemm(x, w, bias=bias, epi=epi, resid=resid, rms=(g, 1e-5)), atol=0.03)
+
+
 @pytest.mark.parametrize("N,Kd,epi", [(9216, 3072, K.EPI_NONE), (1024, 3072, K.EPI_SWIGLU), (32064, 3072, K.EPI_NONE)])
 def test_gemv_fused_rmsnorm(N, Kd, epi):
     torch.manual_seed(N)
