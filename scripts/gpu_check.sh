@@ -16,7 +16,7 @@ rc=$?; echo "smoke rc=$rc"; tail -1 $OUT/smoke.log
 timeout -k 10 900 python bench.py > $OUT/bench.json 2> $OUT/bench.err
 rc=$?; echo "bench rc=$rc"; cat $OUT/bench.json
 [ $rc -ne 0 ] && { tail -5 $OUT/bench.err; exit $rc; }
-(cd /tmp && export TMPDIR=/tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $R/$OUT/prof -o bench -- python3 $R/bench.py --steps 1 --warmup 1 --latency-reps 1 --ingest-docs 16 > $R/$OUT/prof_bench.json 2> $R/$OUT/prof_bench.err)
+(cd /tmp && export TMPDIR=/tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $R/$OUT/prof -o bench -- python3 $R/bench.py --steps 1 --warmup 1 --latency-reps 1 --ingest-docs 16 --breakdown 0 > $R/$OUT/prof_bench.json 2> $R/$OUT/prof_bench.err)
 rc=$?; echo "prof rc=$rc"
 [ $rc -ne 0 ] && exit $rc
 python - <<PY
@@ -28,4 +28,6 @@ print("Cijk kernels:", sum(1 for r in rows if "Cijk" in r["Name"]))
 for r in sorted(rows, key=lambda r: -float(r["TotalDurationNs"]))[:8]:
     print(f'{float(r["Percentage"]):6.2f}%  {int(r["Calls"]):6d}  {r["Name"][:90]}')
 PY
+# the per-dispatch trace is tens of MB: compressed, so the merged gpurun_out stays under its cap
+gzip -f $OUT/prof/*kernel_trace.csv
 if [ -n "$EXTRA" ]; then eval "$EXTRA"; fi
