@@ -4,6 +4,7 @@
 #   llama70b  Llama-3-70B QA on one GPU (TP=1), BGE-large
 #   rank2     2 ranks sharing the GPU (gloo collectives): the multi-rank bench path
 #   tp2       Phi-3-mini TP=2 + IVFFlat, 2 ranks sharing the GPU (xGMI IPC all-reduce kernel, gloo)
+#   c5        BASELINE config 5 layout: Llama-3-70B TP=8 + fp8 encoder + IVFFlat, 8 ranks sharing the GPU
 #   index     vector index microbenchmarks (flat / IVFFlat, up to 100M x 1024 rows)
 #   xgmi      IPC all-reduce GPU tests (2 ranks sharing the GPU)
 set -u
@@ -28,6 +29,10 @@ case ${1:-c4} in
   tp2) DA_DIST_BACKEND=gloo run tp2 900 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
          --master-addr 127.0.0.1 --master-port 29534 bench.py --gpus 2 --tp 2 --index-kind ivfflat --steps 1 \
          --warmup 1 --batch 8 --latency-reps 1 --ingest-docs 0 ;;
+  c5) DA_DIST_BACKEND=gloo run c5 900 python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 \
+        --master-addr 127.0.0.1 --master-port 29535 bench.py --gpus 8 --llm llama3-70b --tp 8 --enc bge-large \
+        --enc-dtype fp8 --index-kind ivfflat --batch 2 --steps 1 --warmup 1 --latency-reps 1 --ingest-docs 0 \
+        --max-new 8 --breakdown 0 ;;  # gloo TP all-reduces through the host: a path check, not a perf number
   index) run index_flat 600 python bench/index_bench.py --kind flat --rows 10000000 --dim 1024 \
            && run index_ivf 900 python bench/index_bench.py --kind ivfflat --rows 10000000 --dim 1024 --lists 4096 \
               --probes 4,16,64 ;;
