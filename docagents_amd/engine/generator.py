@@ -21,6 +21,18 @@ import torch
 from ..models.llama import DecodeState, LlamaDecoder, pack_prompts
 
 
+def h2d(a, dev) -> torch.Tensor:
+    """Host array -> device tensor without blocking the host: the array is staged in PyTorch's
+    cached pinned-host allocator (which records the copy's stream, so the block is not reused
+    before the copy ran). A pageable-memory copy would make the host wait for the current
+    stream to drain first: fatal for the pipelined path, whose host issues one lane's work while
+    the other lane is still busy."""
+    t = torch.from_numpy(np.ascontiguousarray(a))
+    if dev.type != "cuda":
+        return t.to(dev)
+    return t.pin_memory().to(dev, non_blocking=True)
+
+
 def _bucket(n: int) -> int:
     b = 1
     while b < n:
@@ -149,7 +161,7 @@ class Generator:
             slot_tok = np.repeat(np.asarray(slots[i:j], dtype=np.int32), lens)
             last = (cu[1:] - 1).astype(np.int64)
             t0 = time.perf_counter()
-            to = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev, non_blocking=True)  # noqa: E731
+            to = lambda a: h2d(a, dev)  # noqa: E731
             logits = m.prefill(to(flat), to(pos), to(slot_tok), to(cu), int(lens.max()), to(last), prefix=prefix)
             r0, r1 = row0 + i, row0 + j
             m.ops.sample(logits, self.temperature, self.seed, 0, out_tok=st.tokens[r0:r1], out_lp=st.lp[r0:r1],
@@ -190,7 +202,7 @@ class Generator:
             host[3, :n] = 1                      # active
             host[4, :n] = plen - 1               # start
             dev = m.device
-            ht = torch.from_numpy(host).to(dev)
+            ht = h2d(host, dev)
             st.pos.copy_(ht[0]); st.lens.copy_(ht[1]); st.slot.copy_(ht[2]); st.active.copy_(ht[3])
             st.start.copy_(ht[4])
             st.tokens.zero_(); st.hist.fill_(-1); st.conf.zero_()
@@ -217,7 +229,7 @@ class Generator:
                 if not keep:
                     hslot = slots[0]
                 t0 = time.perf_counter()
-                to = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev, non_blocking=True)  # noqa: E731
+                to = lambda a: h2d(a, dev)  # noqa: E731
                 m.prefill(to(np.asarray(prompts[0][:P], dtype=np.int32)), to(np.arange(P, dtype=np.int32)),
                           to(np.full(P, hslot, dtype=np.int32)), to(np.array([0, P], dtype=np.int32)), P,
                           to(np.array([P - 1], dtype=np.int64)))
@@ -230,7 +242,7 @@ class Generator:
                 self._prefill_into(st, [p[P:] for p in prompts], slots, 0, prefix=(hslot, P))
                 pre = np.zeros((B, 2), dtype=np.int32)
                 pre[:n] = (P, hslot)
-                st.pre.copy_(torch.from_numpy(pre).to(dev))
+                st.pre.copy_(h2d(pre, dev))
             else:
                 st.pre.zero_()
                 self._prefill_into(st, prompts, slots, 0)
@@ -402,7 +414,7 @@ class ContinuousScheduler:
         slot = cache.acquire(1)[0]
         head = list(prompts[0][:P])
         dev = self.m.device
-        to = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev, non_blocking=True)  # noqa: E731
+        to = lambda a: h2d(a, dev)  # noqa: E731
         t0 = time.perf_counter()
         self.m.prefill(to(np.asarray(head, dtype=np.int32)), to(np.arange(P, dtype=np.int32)),
                        to(np.full(P, slot, dtype=np.int32)), to(np.array([0, P], dtype=np.int32)), P,
@@ -446,9 +458,9 @@ class ContinuousScheduler:
         tmp = SimpleNamespace(
             tokens=torch.zeros(n, **i32), lp=torch.zeros(n, dtype=torch.float32, device=dev),
             conf=torch.zeros(n, 2, dtype=torch.float32, device=dev), active=torch.ones(n, **i32),
-            pos=torch.from_numpy(plen - 1).to(dev), lens=torch.from_numpy(plen.copy()).to(dev),
+            pos=h2d(plen - 1, dev), lens=h2d(plen.copy(), dev),
             hist=torch.full((n, self.cap), -1, **i32),
-            start=torch.from_numpy(plen - 1 - (self.cap - budget)).to(dev),
+            start=h2d(plen - 1 - (self.cap - budget), dev),
             slot=torch.as_tensor(slots, dtype=torch.int32, device=dev))
         i = 0
         pre = np.zeros((n, 2), dtype=np.int32)
@@ -470,7 +482,7 @@ class ContinuousScheduler:
         idx = torch.as_tensor(rows, dtype=torch.long, device=dev)
         for name in ("tokens", "lp", "conf", "active", "pos", "lens", "hist", "start", "slot"):
             getattr(st, name).index_copy_(0, idx, getattr(tmp, name))
-        st.pre.index_copy_(0, idx, torch.from_numpy(pre).to(dev))
+        st.pre.index_copy_(0, idx, h2d(pre, dev))
         for r, (p, b, tag), sl, h in zip(rows, take, slots, hs):
             self.rows[r] = (tag, sl, int(b), h)
         self.stats["admitted"] += n

@@ -8,6 +8,7 @@ oracles for tests live in ``docagents_amd.ops.reference``.
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes
 import math
 import os
@@ -72,6 +73,11 @@ _SIGS = {
                        c_float, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p],
     "da_topk_merge": [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p],
     "da_kmeans_accum": [c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p],
+    "da_stream_create_cumask": [c_uint, ctypes.POINTER(c_uint), ctypes.POINTER(c_void_p)],
+    "da_stream_get_cumask": [c_void_p, c_uint, ctypes.POINTER(c_uint)],
+    "da_stream_destroy": [c_void_p],
+    "da_device_cu_count": [c_int, ctypes.POINTER(c_int)],
+    "da_placement_probe": [c_void_p, c_int, c_longlong, c_void_p],
 }
 
 
@@ -162,10 +168,25 @@ def _i32(t, name):
 
 # ----------------------------------------------------------------------------------- GEMM
 _WS = {}
+_ROLE = threading.local()
+
+
+@contextlib.contextmanager
+def workspace_role(name: str):
+    """Kernels launched inside this context use the split-K / decode workspace of ``name``
+    instead of the default one. Two phases that run CONCURRENTLY on different streams (the
+    serving pipeline's prefill lane next to a replaying decode graph) must not share scratch:
+    the decode graph captured the default workspace's pointer."""
+    prev = getattr(_ROLE, "name", "main")
+    _ROLE.name = name
+    try:
+        yield
+    finally:
+        _ROLE.name = prev
 
 
 def _workspace(nbytes: int, device) -> torch.Tensor:
-    key = (device.index if device.index is not None else torch.cuda.current_device())
+    key = (device.index if device.index is not None else torch.cuda.current_device(), getattr(_ROLE, "name", "main"))
     buf = _WS.get(key)
     if buf is None or buf.numel() < nbytes:
         buf = torch.empty(max(nbytes, 1 << 20), dtype=torch.uint8, device=device)
@@ -567,7 +588,8 @@ class _RawBuf:
 def _uncached(tag: str, nbytes: int, device) -> _RawBuf:
     """Zeroed uncached (L2-bypassing) device memory for cross-workgroup hand-offs (decode split
     partials + tickets). Grows by adding buffers, never frees: captured graphs keep their pointers."""
-    key = (tag, device.index if device.index is not None else torch.cuda.current_device())
+    key = (tag, device.index if device.index is not None else torch.cuda.current_device(),
+           getattr(_ROLE, "name", "main"))
     bufs = _UC.setdefault(key, [])
     if not bufs or bufs[-1].nbytes < nbytes:
         n = max(nbytes, 1 << 20)
