@@ -10,6 +10,8 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 from docagents_amd.ops import kernels as K  # noqa: E402
 from docagents_amd.ops import reference as R  # noqa: E402
+from ab_arms import apply_env_overrides  # noqa: E402
+apply_env_overrides()  # DA_* schedule overrides for A/B sweeps
 
 
 def timeit(fn, iters=20):

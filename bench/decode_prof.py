@@ -16,6 +16,8 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from docagents_amd.engine.generator import Generator  # noqa: E402
 from docagents_amd.models.configs import decoder_config  # noqa: E402
 from docagents_amd.models.llama import LlamaDecoder  # noqa: E402
+from ab_arms import apply_env_overrides  # noqa: E402
+apply_env_overrides()  # DA_* schedule overrides for A/B sweeps
 
 
 def main():

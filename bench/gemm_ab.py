@@ -13,6 +13,7 @@ import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from docagents_amd.ops import kernels as K  # noqa: E402
+from ab_arms import blas_gemm  # noqa: E402
 
 ARMS = (sys.argv[1] if len(sys.argv) > 1 else "4,7,blas").split(",")
 SECS = float(os.environ.get("SECS", "0.5"))
@@ -22,9 +23,7 @@ EPI = {"none": K.EPI_NONE, "swiglu": K.EPI_SWIGLU, "resid": K.EPI_RESID, "gelu":
 
 def call(arm, x, w, out, epi, bias=None, resid=None):
     if arm == "blas":
-        if epi == K.EPI_SWIGLU:
-            return K.swiglu_interleaved(torch.mm(x, w.t()), out)
-        return torch.mm(x, w.t(), out=out)
+        return blas_gemm(x, w, epi=epi if epi in (K.EPI_SWIGLU, K.EPI_NONE) else K.EPI_NONE, out=out)
     tile = arm
     return K.gemm(x, w, bias=bias, epi=epi, resid=resid, out=out, tile=int(tile), splits=1)
 

@@ -9,6 +9,8 @@ import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from docagents_amd.ops import kernels as K  # noqa: E402
+from ab_arms import apply_env_overrides  # noqa: E402
+apply_env_overrides()  # DA_* schedule overrides for A/B sweeps
 
 SECS = float(os.environ.get("SECS", "2"))
 only = os.environ.get("ONLY", "")

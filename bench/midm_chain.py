@@ -12,6 +12,7 @@ import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from docagents_amd.ops import kernels as K  # noqa: E402
+from ab_arms import swiglu_interleaved  # noqa: E402
 
 
 def main():
@@ -41,7 +42,7 @@ def main():
                         if arm == "blas":
                             torch.matmul(xi, w.t(), out=outs[j])
                             if j == 2:
-                                K.swiglu_interleaved(outs[j], act)
+                                swiglu_interleaved(outs[j], act)
                         elif arm == "auto":  # the production route (K.gemm defaults)
                             if j == 2:
                                 K.gemm(xi, w, epi=K.EPI_SWIGLU, out=act)

@@ -12,8 +12,6 @@ Batching is across requests: texts are packed by tokens, prompts are generated t
 """
 from __future__ import annotations
 
-import os
-
 import threading
 import time
 
@@ -29,15 +27,13 @@ from . import prompts as P
 from .generator import Generator
 
 
-_SERIAL_TOKENIZE = os.environ.get("DA_SERIAL_TOKENIZE", "0") == "1"  # A/B arm: one encode per string
-
-
 class Engine:
     def __init__(self, embed_arch: str = "bge-base", llm_arch: str = "phi3-mini", device="cuda", seed: int = 0,
                  tp: TPContext | None = None, max_batch: int = 64, max_seq: int = 4096, temperature: float = 0.2,
                  max_new_tokens: int = 64, summary_max_new: int = 128, index_kind: str = "flat",
                  ivf_lists: int = 100, ivf_probes: int = 1, load_llm: bool = True, load_encoder: bool = True,
-                 use_graphs: bool = True, embed_max_tokens: int = 65536, enc_dtype: str = "bf16"):
+                 use_graphs: bool = True, embed_max_tokens: int = 65536, enc_dtype: str = "bf16",
+                 share_prefix: bool = True):
         self.device = torch.device(device)
         self.lock = threading.RLock()
         self.enc_cfg = encoder_config(embed_arch)
@@ -59,7 +55,7 @@ class Engine:
             self.decoder.alloc_cache(max_batch + 4, max_seq)
             self.gen = Generator(self.decoder, max_batch=max_batch, max_seq=max_seq, temperature=temperature,
                                  seed=seed, eos=sorted(self.chat.eos_ids), use_graphs=use_graphs,
-                                 share_prefix=os.environ.get("DA_SHARE_PREFIX", "1") != "0")
+                                 share_prefix=share_prefix)
         from ..index import make_index
         self.index = make_index(index_kind, self.enc_cfg.hidden, self.device, lists=ivf_lists, probes=ivf_probes)
         self._prefix_cache: dict[str, list[int]] = {}
@@ -120,7 +116,7 @@ class Engine:
         """Batch tokenization (the tokenizer's thread pool): 64 2000-word documents take 250 ms
         one ``encode`` at a time on the GPU box's CPU share, ~10 % of an ingest batch
         (bench/tok_timing.py)."""
-        if len(texts) <= 1 or _SERIAL_TOKENIZE:
+        if len(texts) <= 1:
             return [self._ids(t) for t in texts]
         return [e.ids for e in self.dec_tok.encode_batch(texts, add_special_tokens=False)]
 

@@ -11,7 +11,6 @@ from __future__ import annotations
 
 import collections
 import math
-import os
 import time
 from types import SimpleNamespace
 
@@ -61,8 +60,8 @@ class Generator:
         self.is_cuda = model.device.type == "cuda"
         self.use_graphs = use_graphs and self.is_cuda
         # 64k-token chunks: fewer partial tile rounds per GEMM than 32k (same box, 2 rounds each:
-        # QA prefill 1103 vs 1119 ms, profiles/r2/ab_prefill_chunk/); DA_PREFILL_TOKENS overrides (A/B)
-        self.max_prefill_tokens = int(os.environ.get("DA_PREFILL_TOKENS", max_prefill_tokens))
+        # QA prefill 1103 vs 1119 ms, profiles/r2/ab_prefill_chunk/)
+        self.max_prefill_tokens = max_prefill_tokens
         self.check_every = check_every
         if model.cache is None:
             # one extra slot: the dummy slot for padded rows of a bucket
@@ -85,13 +84,15 @@ class Generator:
             kernels.reserve_workspace(need, model.device)
 
     # --------------------------------------------------------------------------------
-    def _persistent_head_slot(self):
-        """The KV slot that keeps the last wave's shared prompt head (taken once, when a slot is
-        spare beyond the ones this call already holds; None when the cache has no slot to spare)."""
+    def _persistent_head_slot(self, held: int):
+        """The KV slot that keeps the last wave's shared prompt head. Taken once, and only when it
+        is a true spare: once this call's ``held`` slots are back, a full wave of max_batch prompts
+        must still find its slots (a head slot taken from a cache sized max_batch + 1 would make
+        the next full wave fail with 'KV cache exhausted'). None when there is no spare slot."""
         if self.head is not None:
             return self.head["slot"]
         if getattr(self, "_head_slot", None) is None:
-            if not self.cache.free:
+            if len(self.cache.free) + held <= self.max_batch:
                 return None
             self._head_slot = self.cache.acquire(1)[0]
         return self._head_slot
@@ -224,7 +225,7 @@ class Generator:
                 # head's K/V exist once: prefilled once, read from L2/MALL by all rows. The head goes
                 # into a slot of its own when one is free and is kept for later calls (a batch-1
                 # query then skips it); otherwise into row 0's slot for this call only.
-                hslot = self._persistent_head_slot()
+                hslot = self._persistent_head_slot(held=n)
                 keep = hslot is not None
                 if not keep:
                     hslot = slots[0]

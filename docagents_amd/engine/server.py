@@ -51,6 +51,18 @@ class EngineGroup:
             idx.remove_doc(doc_id)
             idx.add(doc_id, keys, vecs)
 
+    def _upsert(self, doc_id, keys, vecs):
+        """Per-chunk upsert of ``doc_id``'s rows (index_add = the reference's SaveEmbeddings,
+        ``ON CONFLICT (chunk_id)``, postgres.go:197): rows of other chunks of the document stay."""
+        idx = self.engine.index
+        if self.shard_log is not None:
+            self.shard_log.upsert(idx, doc_id, keys, vecs)
+        else:
+            from ..index.wal import validate
+            validate(idx, keys, vecs)
+            idx.remove_keys(doc_id, keys)
+            idx.add(doc_id, keys, vecs)
+
     # ---------------------------------------------------------------- collectives (control plane)
     def _bcast(self, obj):
         if self.world == 1:
@@ -139,8 +151,8 @@ class EngineGroup:
             return [d for p in parts for d in p[0]], any(p[1] for p in parts)
         if cmd == "index_add":
             if owner_of(a["doc_id"], self.world) == self.rank:
-                self._put(a["doc_id"], np.asarray(a["keys"], dtype=np.int64),
-                          torch.from_numpy(np.ascontiguousarray(a["vecs"], dtype=np.float32)))
+                self._upsert(a["doc_id"], np.asarray(a["keys"], dtype=np.int64),
+                             torch.from_numpy(np.ascontiguousarray(a["vecs"], dtype=np.float32)))
             return True
         if cmd == "embed_index":
             # ingest without a vector round trip: the owner rank of each document

@@ -122,6 +122,37 @@ class FlatIndex:
             e.ranges, e.rows = [], 0
             return n
 
+    def remove_keys(self, doc_id: str, keys) -> int:
+        """Drop the rows of ``doc_id`` whose external ids are in ``keys`` (per-chunk upsert: the
+        reference's ``ON CONFLICT (chunk_id)``, postgres.go:197). Rows tracked by range (flat rows,
+        IVF delta rows) have their ranges split around the dropped rows; rows tracked only by slot
+        (IVF list-major rows) leave search through their slot. Returns the rows dropped."""
+        keys = np.unique(np.asarray(keys, dtype=np.int64))
+        with self.lock:
+            e = self.docs.get(doc_id)
+            if e is None or e.rows == 0 or keys.size == 0 or self.n == 0:
+                return 0
+            n = self.n
+            kt = torch.from_numpy(keys).to(self.device)
+            s = self.slots_t[:n]
+            sel = (s == e.slot) & torch.isin(self.ids_t[:n], kt)
+            removed = int(sel.sum().item())
+            if removed == 0:
+                return 0
+            s.masked_fill_(sel, -1)
+            ranges = []
+            for a, b in e.ranges:
+                keep = ~np.isin(self.ids[a:b], keys)
+                if keep.all():
+                    ranges.append((a, b))
+                    continue
+                # maximal runs of kept rows
+                edges = np.flatnonzero(np.diff(np.concatenate(([0], keep.view(np.int8), [0]))))
+                ranges.extend((a + int(x), a + int(y)) for x, y in zip(edges[::2], edges[1::2]))
+            e.ranges = ranges
+            e.rows -= removed
+            return removed
+
     def __len__(self):
         return self.n
 

@@ -11,7 +11,10 @@ import torch
 from safetensors.torch import load_file, save_file
 
 
-def save_index(index, path: str, extra_meta: dict | None = None) -> str:
+def save_index(index, path: str, extra_meta: dict | None = None, durable: bool = True) -> str:
+    """Write the snapshot to ``path`` atomically (tmp file + rename); ``durable``: fsync the file
+    before the rename and the directory after it, so the snapshot survives a power loss once this
+    returns (the vector log deletes the generations it covers right after)."""
     with index.lock:
         sel, docs = index.live_rows_by_doc()
         docs = [[d, n] for d, n in docs]
@@ -25,7 +28,19 @@ def save_index(index, path: str, extra_meta: dict | None = None) -> str:
     tmp = path + ".tmp"
     os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
     save_file(tensors, tmp, metadata=meta)
+    if durable:
+        fd = os.open(tmp, os.O_RDONLY)
+        try:
+            os.fsync(fd)
+        finally:
+            os.close(fd)
     os.replace(tmp, path)
+    if durable:
+        dfd = os.open(os.path.dirname(os.path.abspath(path)), os.O_RDONLY)
+        try:
+            os.fsync(dfd)
+        finally:
+            os.close(dfd)
     return path
 
 

@@ -15,7 +15,16 @@ process (SIGKILL, watchdog ``os._exit``, a lost box):
 
 Record framing: ``b"DAVL" | u32 payload_len | u32 crc32(payload) | payload``; payload =
 ``u8 op | u16 len(doc) | doc utf-8 | u32 n | u32 dim | i64 keys[n] | bf16 vecs[n, dim]`` with
-op 1 = replace the document's rows by these (index_add / embed_index), op 2 = remove the document.
+op 1 = replace the document's rows by these (embed_index: the engine sees every chunk of the
+document), op 2 = remove the document, op 3 = per-chunk upsert (index_add: drop only the document's
+rows whose keys are in the batch, then add — the reference's ``ON CONFLICT (chunk_id)``,
+postgres.go:197).
+
+A mutation is validated against the index (vector rank / dim, one key per vector) BEFORE it is
+logged, so a bad request is rejected without leaving a record behind; a record that still fails to
+apply on replay (a log written by an older build) is skipped and counted (``quarantined``), never
+allowed to stop the engine from starting. Checkpoint files and the directory are fsync'ed before
+the logs they cover are deleted.
 """
 from __future__ import annotations
 
@@ -29,7 +38,7 @@ import numpy as np
 import torch
 
 MAGIC = b"DAVL"
-OP_PUT, OP_REMOVE = 1, 2
+OP_PUT, OP_REMOVE, OP_UPSERT = 1, 2, 3
 _HDR = struct.Struct("<4sII")
 
 
@@ -62,6 +71,26 @@ def _decode(body: bytes):
     raw = np.frombuffer(body, dtype=np.int16, count=n * dim, offset=o).copy()
     vecs = torch.from_numpy(raw).view(torch.bfloat16).view(n, dim)
     return op, doc, keys, vecs
+
+
+def fsync_dir(path: str) -> None:
+    """Make a rename / create / unlink inside ``path`` durable."""
+    fd = os.open(path, os.O_RDONLY)
+    try:
+        os.fsync(fd)
+    finally:
+        os.close(fd)
+
+
+def validate(index, keys, vecs) -> None:
+    """Raise ValueError for a mutation ``index.add`` would reject (checked before it is logged)."""
+    if vecs.dim() != 2:
+        raise ValueError(f"vectors must be [n, dim], got shape {tuple(vecs.shape)}")
+    n, dim = int(vecs.shape[0]), int(vecs.shape[1])
+    if n and dim != index.dim:
+        raise ValueError(f"vector dim {dim} != index dim {index.dim}")
+    if len(np.asarray(keys).reshape(-1)) != n:
+        raise ValueError(f"{len(np.asarray(keys).reshape(-1))} keys for {n} vectors")
 
 
 def read_records(path: str):
@@ -107,7 +136,11 @@ class ShardLog:
         self.snap_path = os.path.join(self.dir, f"shard{rank}.snap")
         self.gen = 0
         self._f = None
-        self.stats = {"appended": 0, "replayed": 0, "torn_bytes": 0, "checkpoints": 0, "rows_since_ckpt": 0}
+        # rows_since_ckpt counts every logged mutation's rows (removes count 1): the periodic
+        # checkpoint runs when it is non-zero
+        self.stats = {"appended": 0, "replayed": 0, "torn_bytes": 0, "checkpoints": 0, "rows_since_ckpt": 0,
+                      "quarantined": 0}
+        self.quarantine: list[dict] = []
 
     # ------------------------------------------------------------------ files
     def _wal(self, gen: int) -> str:
@@ -124,7 +157,10 @@ class ShardLog:
     def _open(self):
         if self._f is not None:
             self._f.close()
+        new = not os.path.exists(self._wal(self.gen))
         self._f = open(self._wal(self.gen), "ab")
+        if new and self.fsync:
+            fsync_dir(self.dir)  # the new generation's directory entry is durable before anything relies on it
 
     # ------------------------------------------------------------------ recovery
     def recover(self, index) -> dict:
@@ -140,7 +176,12 @@ class ShardLog:
         for g in gens:
             recs, good, total = scan(self._wal(g))
             for op, doc, keys, vecs in recs:
-                self._apply(index, op, doc, keys, vecs)
+                try:
+                    self._apply(index, op, doc, keys, vecs)
+                except Exception as e:  # noqa: BLE001 - a record that cannot apply must not block startup
+                    self.stats["quarantined"] += 1
+                    self.quarantine.append({"gen": g, "op": op, "doc": doc, "err": repr(e)})
+                    continue
                 replayed += 1
             if good < total:  # torn tail: keep the valid prefix so later appends stay readable
                 torn += total - good
@@ -154,15 +195,22 @@ class ShardLog:
         self.stats["replayed"] += replayed
         self.stats["torn_bytes"] += torn
         return {"snapshot_rows": rows, "replayed": replayed, "torn_bytes": torn, "gen": self.gen,
-                "rows": len(index)}
+                "rows": len(index), "quarantined": self.stats["quarantined"]}
 
     @staticmethod
     def _apply(index, op, doc, keys, vecs):
         if op == OP_REMOVE:
             index.remove_doc(doc)
-        else:
+        elif op == OP_UPSERT:
+            validate(index, keys, vecs)
+            index.remove_keys(doc, keys)
+            index.add(doc, keys, vecs)
+        elif op == OP_PUT:
+            validate(index, keys, vecs)
             index.remove_doc(doc)  # put = replace the document's rows (idempotent re-index)
             index.add(doc, keys, vecs)
+        else:
+            raise ValueError(f"unknown log op {op}")
 
     # ------------------------------------------------------------------ mutations
     def _append(self, rec: bytes):
@@ -175,26 +223,39 @@ class ShardLog:
         self.stats["appended"] += 1
 
     def put(self, index, doc_id: str, keys, vecs: torch.Tensor):
-        """Log, then replace ``doc_id``'s rows in ``index`` with ``vecs`` (device or host)."""
-        self._append(_encode(OP_PUT, doc_id, keys, vecs))
-        self._apply(index, OP_PUT, doc_id, np.asarray(keys, dtype=np.int64), vecs)
-        self.stats["rows_since_ckpt"] += int(vecs.shape[0])
+        """Validate, log, then replace ``doc_id``'s rows in ``index`` with ``vecs`` (device or host)."""
+        self._mutate(index, OP_PUT, doc_id, keys, vecs)
+
+    def upsert(self, index, doc_id: str, keys, vecs: torch.Tensor):
+        """Validate, log, then upsert ``doc_id``'s rows by key (rows with other keys are kept)."""
+        self._mutate(index, OP_UPSERT, doc_id, keys, vecs)
+
+    def _mutate(self, index, op, doc_id, keys, vecs):
+        keys = np.asarray(keys, dtype=np.int64).reshape(-1)
+        validate(index, keys, vecs)
+        self._append(_encode(op, doc_id, keys, vecs))
+        self._apply(index, op, doc_id, keys, vecs)
+        self.stats["rows_since_ckpt"] += max(1, int(vecs.shape[0]))
 
     def remove(self, index, doc_id: str) -> int:
         self._append(_encode(OP_REMOVE, doc_id))
+        self.stats["rows_since_ckpt"] += 1
         return index.remove_doc(doc_id)
 
     # ------------------------------------------------------------------ checkpoints
     def checkpoint(self, index) -> str:
         """Snapshot covering every record so far, then rotate to a fresh log generation."""
         from .snapshot import save_index
-        save_index(index, self.snap_path, extra_meta={"wal_gen": str(self.gen)})
+        save_index(index, self.snap_path, extra_meta={"wal_gen": str(self.gen)}, durable=True)
         old = self.gen
         self.gen += 1
         self._open()
+        fsync_dir(self.dir)  # snapshot rename + new generation are on disk before the covered logs go
         for g in self._gens():
             if g <= old:
                 os.remove(self._wal(g))
+        if self.fsync:
+            fsync_dir(self.dir)
         self.stats["checkpoints"] += 1
         self.stats["rows_since_ckpt"] = 0
         return self.snap_path

@@ -20,8 +20,6 @@ is added by rank 0's epilogue only, so a single in-place all-reduce yields x + s
 """
 from __future__ import annotations
 
-import os
-
 import numpy as np
 import torch
 
@@ -30,9 +28,9 @@ from ..ops.reference import interleave_gate_up, rope_table
 from .configs import DecoderConfig
 
 EPI_NONE, EPI_SWIGLU, EPI_RESID = 0, 3, 4
-# Decode step of MHA models: RoPE + KV-cache write folded into the attention kernel (DA_FUSED_ROPE=0:
-# separate rope_cache launch, for A/B runs).
-_FUSED_ROPE_DECODE = os.environ.get("DA_FUSED_ROPE", "1") != "0"
+# Decode step of MHA models: RoPE + KV-cache write folded into the attention kernel (False: separate
+# rope_cache launch; the GPU tests compare both).
+_FUSED_ROPE_DECODE = True
 
 
 class TPContext:

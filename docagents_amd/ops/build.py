@@ -55,19 +55,37 @@ def _flags(debug: bool) -> list[str]:
     return f
 
 
+LAST_BUILD: dict = {}
+
+
+def source_hashes() -> dict:
+    """sha256 (first 16 hex) of every kernel source: what a build compiled."""
+    return {p.name: hashlib.sha256(p.read_bytes()).hexdigest()[:16] for p in sorted(CSRC.glob("*"))}
+
+
 def build(force: bool = False, debug: bool = False, verbose: bool = False) -> Path:
-    """Compile (if stale) and return the path of the shared library."""
+    """Compile (if stale) and return the path of the shared library. ``LAST_BUILD`` records what
+    happened: mode "compiled" (hipcc ran, with the wall time) or "reused" (fingerprint match)."""
+    import time
     stamp = HERE / "_da_kernels.fingerprint"
     fp = _fingerprint(debug)
+    LAST_BUILD.clear()
+    LAST_BUILD.update({"lib": str(LIB), "fingerprint": fp[:16], "arch": ARCH, "debug": debug})
     if LIB.exists() and stamp.exists() and stamp.read_text() == fp and not force:
+        LAST_BUILD["mode"] = "reused"
         return LIB
     # N ranks of one job import the package at once: one builds, the others wait and reuse it
     import fcntl
     with open(HERE / "_da_kernels.lock", "w") as lk:
         fcntl.flock(lk, fcntl.LOCK_EX)
         if LIB.exists() and stamp.exists() and stamp.read_text() == fp and not force:
+            LAST_BUILD["mode"] = "reused"
             return LIB
-        return _build_locked(stamp, fp, debug, verbose)
+        t0 = time.perf_counter()
+        out = _build_locked(stamp, fp, debug, verbose)
+        LAST_BUILD.update({"mode": "compiled", "compile_s": round(time.perf_counter() - t0, 1),
+                           "sources": source_hashes()})
+        return out
 
 
 def _build_locked(stamp: Path, fp: str, debug: bool, verbose: bool) -> Path:

@@ -114,23 +114,6 @@ def lib() -> ctypes.CDLL:
             fn.restype = c_int
         L.da_topk_dense_ws.argtypes = [c_int, c_int, c_int, c_int]
         L.da_topk_dense_ws.restype = c_size_t
-        # schedule overrides for A/B measurements (defaults are the measured-best variants)
-        if os.environ.get("DA_GEMM_PF") is not None:  # decode-tile register prefetch depth (A/B)
-            L.da_set_gemm_pf(int(os.environ["DA_GEMM_PF"]))
-        if os.environ.get("DA_FLASH_PIPE") is not None:  # software-pipelined flash prefill (A/B)
-            L.da_set_flash_pipe(int(os.environ["DA_FLASH_PIPE"]))
-        if os.environ.get("DA_FLASH_QH") is not None:  # flash queries per wave: 1 = 32, 2 = 64 (A/B)
-            L.da_set_flash_qh(int(os.environ["DA_FLASH_QH"]))
-        if os.environ.get("DA_GEMV_U") is not None:  # batch-1 GEMV K-blocks in flight per row (A/B)
-            L.da_set_gemv_u(int(os.environ["DA_GEMV_U"]))
-        if os.environ.get("DA_GEMV_KS") is not None:  # batch-1 GEMV waves per long row: 1 or 2 (A/B)
-            L.da_set_gemv_ks(int(os.environ["DA_GEMV_KS"]))
-        if os.environ.get("DA_FLASH_REV") is not None:  # causal flash longest-first dispatch (A/B)
-            L.da_set_flash_rev(int(os.environ["DA_FLASH_REV"]))
-        if os.environ.get("DA_DECODE_PFT") is not None:  # MHA decode next-tile prefetch below B*Hkv (A/B)
-            L.da_set_decode_pft(int(os.environ["DA_DECODE_PFT"]))
-        if os.environ.get("DA_FLASH_WAVES") is not None:
-            L.da_set_flash_waves(int(os.environ["DA_FLASH_WAVES"]))
         _LIB = L
         return L
 
@@ -232,12 +215,6 @@ def gemm(a: torch.Tensor, w: torch.Tensor, bias=None, epi: int = EPI_NONE, resid
         ldr = resid.stride(0)
     if M == 0:
         return out
-    if (_BLAS_PREFILL and tile == 0 and splits <= 0 and rms is None and _blas_size_ok(M, N)
-            and (epi in (EPI_NONE, EPI_BIAS) or (epi == EPI_RESID and bias is None))):
-        return _blas_gemm(a, w, bias, epi, resid, out)
-    if (_BLAS_SWIGLU and epi == EPI_SWIGLU and tile == 0 and splits <= 0 and rms is None
-            and (M >= _BLAS_MIN_M or _blas_mid(M))):
-        return swiglu_interleaved(torch.mm(a, w.t()), out)
     if tile == 0 and splits <= 0 and gemv_fusable(M, N, K, epi):
         tile, splits = 6, 1  # batch-1 decode: weight-streaming GEMV, one launch, no split-K workspace
     gamma, eps = (None, 0.0) if rms is None else rms  # rms = (gain or None for unit gain, eps > 0)
@@ -259,30 +236,10 @@ def gemm(a: torch.Tensor, w: torch.Tensor, bias=None, epi: int = EPI_NONE, resid
     return out
 
 
-# Every GEMM runs on the in-tree kernels by default: gemm8p (phase-split BMx256, csrc/gemm8p.hip)
-# from 256 rows, the 64x128 / 32x128 weight-streaming tiles below. Same-box measurements
-# (profiles/r2/ab_gemm8p_vs_hipblaslt.txt): gemm8p 1.42-1.51 PF/s vs hipBLASLt 1.43-1.56 on the
-# Phi-3 prefill shapes and +9 % on gate/up with the fused SwiGLU (hipBLASLt needs a separate pass);
-# flagship 31.0 vs 30.6 QA q/s. The hipBLASLt routes below stay only as opt-in A/B arms:
-#   DA_BLAS_PREFILL=1   plain / bias / residual GEMMs with M >= DA_BLAS_MIN_M
-#   DA_BLAS_SWIGLU=1    gate/up on hipBLASLt + swiglu_interleaved
-#   DA_BLAS_UNDERFILL=1 1024..DA_BLAS_MIN_M rows when 256x256 tiles underfill the chip
-#   DA_BLAS_MID=1       65..1023 rows
-_BLAS_PREFILL = os.environ.get("DA_BLAS_PREFILL", "0") == "1"
-_BLAS_SWIGLU = os.environ.get("DA_BLAS_SWIGLU", "0") == "1"
-_BLAS_MIN_M = int(os.environ.get("DA_BLAS_MIN_M", "4096"))
-_BLAS_UNDERFILL = os.environ.get("DA_BLAS_UNDERFILL", "0") == "1"
-_BLAS_MID = os.environ.get("DA_BLAS_MID", "0") == "1"
-
-
-def _blas_mid(M: int) -> bool:
-    return _BLAS_MID and 64 < M < 1024
-
-
-def _blas_size_ok(M: int, N: int) -> bool:
-    if M >= _BLAS_MIN_M or _blas_mid(M):
-        return True
-    return _BLAS_UNDERFILL and M >= 1024 and math.ceil(M / 256) * math.ceil(N / 256) < 256
+# Every GEMM runs on the in-tree kernels: gemm8p (phase-split BMx256, csrc/gemm8p.hip) from 256
+# rows, the 64x128 / 32x128 weight-streaming tiles + split-K below, the GEMV at batch 1. The
+# vendor-library arms used for comparisons live in bench/ab_arms.py (same-box measurements:
+# profiles/r2/ab_gemm8p_vs_hipblaslt.txt).
 
 
 def gemm_rope(a, w, pos, cos_sin, H: int, Hkv: int, D: int, slot, k_cache, v_cache, out=None) -> torch.Tensor:
@@ -307,31 +264,6 @@ def gemm_rope(a, w, pos, cos_sin, H: int, Hkv: int, D: int, slot, k_cache, v_cac
                               _ptr(cos_sin), _ptr(k_cache), _ptr(v_cache), H, Hkv, D, k_cache.shape[2], _stream()),
            "gemm_rope")
     return out
-
-
-def swiglu_interleaved(x: torch.Tensor, out=None) -> torch.Tensor:
-    """[M, 2F] gate/up (16-column interleave, the EPI_SWIGLU weight order) -> silu(gate) * up [M, F]."""
-    _bf16_cuda(x, "x")
-    M, N2 = x.shape
-    _req(N2 % 32 == 0 and x.stride(1) == 1 and x.stride(0) % 8 == 0, "x must be [M, 2F] row-major, F % 16 == 0")
-    if out is None:
-        out = torch.empty((M, N2 // 2), dtype=torch.bfloat16, device=x.device)
-    _req(out.shape == (M, N2 // 2) and out.stride(1) == 1 and out.stride(0) % 8 == 0, "bad out")
-    _check(lib().da_swiglu_interleaved(_ptr(x), x.stride(0), _ptr(out), out.stride(0), M, N2 // 2, _stream()),
-           "swiglu_interleaved")
-    return out
-
-
-def _blas_gemm(a, w, bias, epi, resid, out):
-    wt = w.t()
-    if epi == EPI_NONE:
-        return torch.mm(a, wt, out=out)
-    if epi == EPI_BIAS:
-        return torch.addmm(bias, a, wt, out=out)
-    _req(resid.shape == out.shape, "bad resid")
-    if out.data_ptr() == resid.data_ptr() and out.stride() == resid.stride():
-        return out.addmm_(a, wt)  # x += a @ w^T in place (beta = 1)
-    return torch.addmm(resid, a, wt, out=out)
 
 
 FP8 = torch.float8_e4m3fn  # OCP e4m3 (gfx950), not the MI300 fnuz variant
@@ -569,9 +501,9 @@ def flash_attn_varlen(q, k, v, cu_seqlens, max_seqlen: int, H: int, Hkv: int, D:
 
 
 # Split-KV partials merged inside the decode kernel by the last split of each (row, kv head)
-# (DA_FUSED_COMBINE=0: separate combine launch, for A/B). The ticket counters stay zero between
+# (False: separate combine launch; tests cover both). The ticket counters stay zero between
 # launches; buffers are only ever added, never freed, so a captured graph's pointer stays valid.
-_FUSED_COMBINE = os.environ.get("DA_FUSED_COMBINE", "1") != "0"
+_FUSED_COMBINE = True
 _UC: dict = {}
 
 

@@ -36,14 +36,33 @@ def _done(rank, out_path, verdict):
     dist.destroy_process_group()
 
 
-def check_tp_decoder(rank, world, port, out_path, arch: str = "tiny-dec"):
-    """TP=world decoder vs the unsharded one on the same weights, teacher-forced on the unsharded
-    model's greedy continuation: at every generated step of every prompt the TP model's next-token
-    logits must match (max |diff| = d, bf16 rounding noise only; a wrong-rank / stale-buffer bug is an
-    O(1) error), and free-running greedy tokens must be identical on every prompt whose top-1 / top-2
-    gaps stay above 2 d (where no rounding can flip the argmax). A random-init model's distribution is
-    nearly flat (p ~ 1e-4, bf16 logits within a few ulp of each other), so exact ties exist on some
-    prompts; those are reported, not asserted."""
+def _shuffled_shards(cfg, full, rank, world):
+    """NEGATIVE CONTROL: every rank loads its neighbour's shard (a wrong shard order). The checks
+    below must fail on it — tests assert they do."""
+    from ..models.llama import shard_weights
+    w = shard_weights(cfg, full, (rank + 1) % world, world)
+    return w
+
+
+def check_tp_decoder(rank, world, port, out_path, arch: str = "tiny-dec", wrong_order: bool = False):
+    """TP=world decoder vs the unsharded one on the same weights, per decision.
+
+    Teacher-forced on the unsharded model's greedy continuation, every generated step of every
+    prompt gives (gap = top-1 minus top-2 logit of the unsharded model, its argmax, the TP model's
+    argmax) and d = the max |logit difference| over all steps and the whole vocabulary (bf16
+    rounding noise of the partial sums only; a wrong-rank / stale-buffer bug is an O(1) error). A
+    decision with gap > 2 d cannot be flipped by that noise, so:
+
+    * ``checked`` = decisions with gap > 2 d; every one of them must have the same argmax in both
+      models (``checked_agree``), and they must be most decisions (a random-init model's logits are
+      bf16-quantised: top-1 / top-2 ties of 0-1 ulp exist, those steps are the unchecked ones);
+    * the free-running TP generation must equal the unsharded one up to the first unchecked step
+      of each prompt (``prefix_ok``): identical greedy tokens wherever rounding cannot decide;
+    * ``stable_prompts`` = prompts whose every step is checked (reported).
+
+    Random-init logits are flat AND bf16-quantised, so no weight scale makes every step decidable:
+    an LM-head or embedding scale multiplies gaps and noise alike (measured: stable prompts 0-3 of 8
+    at scales 1-16), hence the per-decision form. ``wrong_order`` runs the negative control."""
     _init(rank, world, port)
     from ..models.configs import decoder_config
     from ..models.llama import LlamaDecoder, TPContext, random_weights, shard_weights
@@ -51,9 +70,10 @@ def check_tp_decoder(rank, world, port, out_path, arch: str = "tiny-dec"):
     cfg = decoder_config(arch)
     full = random_weights(cfg, "cpu", seed=5)
     ref = LlamaDecoder(cfg, "cpu", weights=full)
-    tp = LlamaDecoder(cfg, "cpu", tp=TPContext(rank, world, None), weights=shard_weights(cfg, full, rank, world))
+    shard = (_shuffled_shards if wrong_order else shard_weights)(cfg, full, rank, world)
+    tp = LlamaDecoder(cfg, "cpu", tp=TPContext(rank, world, None), weights=shard)
     prompts = [list(range(30 + 7 * i, 30 + 7 * i + n)) for i, n in enumerate((9, 33, 4, 17, 25, 6, 40, 12))]
-    steps = 6
+    steps = 8
     a = Generator(ref, max_batch=8, max_seq=256, temperature=0.0, use_graphs=False).generate(prompts, steps)
     b = Generator(tp, max_batch=8, max_seq=256, temperature=0.0, use_graphs=False).generate(prompts, steps)
 
@@ -62,25 +82,38 @@ def check_tp_decoder(rank, world, port, out_path, arch: str = "tiny-dec"):
         return m.prefill(t, torch.arange(len(seq), dtype=torch.int32), torch.zeros(len(seq), dtype=torch.int32),
                          torch.tensor([0, len(seq)], dtype=torch.int32), len(seq),
                          torch.tensor([len(seq) - 1]))[0].float()
-    d, gaps = 0.0, []
+    d, dec = 0.0, []  # dec[i] = [(gap, ref argmax, tp argmax)] per step of prompt i
     for p, x in zip(prompts, a):
-        g = float("inf")
+        steps_i = []
         for t in range(len(x.tokens)):
             lr, lt = last_logits(ref, p + x.tokens[:t]), last_logits(tp, p + x.tokens[:t])
             d = max(d, float((lr - lt).abs().max()))
-            top = torch.topk(lr, 2).values
-            g = min(g, float(top[0] - top[1]))
-        gaps.append(g)
-    stable = [i for i, g in enumerate(gaps) if g > 2 * d]
-    same = all(a[i].tokens == b[i].tokens for i in stable)
+            top = torch.topk(lr, 2)
+            steps_i.append((float(top.values[0] - top.values[1]), int(top.indices[0]), int(lt.argmax())))
+        dec.append(steps_i)
+    flat = [s_ for st in dec for s_ in st]
+    checked = [s_ for s_ in flat if s_[0] > 2 * d]
+    checked_agree = sum(1 for g, r_, t_ in checked if r_ == t_)
+    prefix_ok, stable = [], 0
+    for st, x, y in zip(dec, a, b):
+        n = next((j for j, s_ in enumerate(st) if s_[0] <= 2 * d), len(st))  # first undecidable step
+        stable += n == len(st)
+        prefix_ok.append(x.tokens[:n] == y.tokens[:n])  # tokens[t] is the decision of step t
     probs = max(abs(x.mean_prob - y.mean_prob) for x, y in zip(a, b))
-    _done(rank, out_path, {"same_tokens": same, "stable_prompts": len(stable), "max_prob_diff": probs,
-                           "max_logit_diff": d, "gaps": gaps, "tokens": [x.tokens for x in b]})
+    _done(rank, out_path, {"decisions": len(flat), "checked": len(checked), "checked_agree": checked_agree,
+                           "prefix_ok": prefix_ok, "stable_prompts": stable, "max_prob_diff": probs,
+                           "max_logit_diff": d, "gaps": [[round(s_[0], 4) for s_ in st] for st in dec],
+                           "tokens": [x.tokens for x in b]})
 
 
 def check_tp8_decoder(rank, world, port, out_path):
     """TP=world with one KV head per rank (Llama-3-70B's TP=8 layout, tiny-dec-tp8)."""
     check_tp_decoder(rank, world, port, out_path, arch="tiny-dec-tp8")
+
+
+def check_tp_decoder_wrong_order(rank, world, port, out_path):
+    """Negative control of check_tp_decoder: shards loaded in the wrong rank order."""
+    check_tp_decoder(rank, world, port, out_path, wrong_order=True)
 
 
 def check_sharded_index(rank, world, port, out_path):
@@ -280,25 +313,57 @@ def check_xgmi_allreduce(rank, world, port, out_path):
     _done(rank, out_path, verdict)
 
 
-def check_tp_decoder_gpu(rank, world, port, out_path):
-    """TP=world LlamaDecoder on GPU ranks: row-parallel outputs summed by the xGMI all-reduce
-    kernel, vocab-parallel logits all-gathered; compared with the unsharded decoder on the same
-    device (bf16 partial sums round differently, so: close logits, mostly identical tokens)."""
+def check_tp_decoder_gpu(rank, world, port, out_path, wrong_order: bool = False):
+    """TP=world LlamaDecoder on GPU ranks (row-parallel outputs summed by the xGMI all-reduce kernel,
+    vocab-parallel logits gathered over it) vs the unsharded decoder on the same device, with the
+    per-decision verdict of check_tp_decoder: teacher-forced logit bound d, every decision with a
+    top-1 / top-2 gap above 2 d agreeing, identical free-running tokens up to each prompt's first
+    undecidable step. ``wrong_order``: negative control (neighbour's shard)."""
     _init(rank, world, port)
     from ..engine.generator import Generator
     from ..models.configs import decoder_config
-    from ..models.llama import LlamaDecoder, TPContext, random_weights
+    from ..models.llama import LlamaDecoder, TPContext, random_weights, shard_weights
     dev = torch.device("cuda", rank % torch.cuda.device_count())
     torch.cuda.set_device(dev)
     cfg = decoder_config("tiny-dec")
-    ref = LlamaDecoder(cfg, dev, weights=random_weights(cfg, dev, seed=5))
-    tp = LlamaDecoder(cfg, dev, tp=TPContext(rank, world, None),
-                      weights=random_weights(cfg, dev, seed=5, tp_rank=rank, tp_size=world, full_then_shard=True))
-    prompts = [list(range(30, 30 + n)) for n in (9, 33, 4, 120)]
-    a = Generator(ref, max_batch=4, max_seq=256, temperature=0.0, use_graphs=False).generate(prompts, 8)
-    b = Generator(tp, max_batch=4, max_seq=256, temperature=0.0, use_graphs=False).generate(prompts, 8)
-    agree = [sum(x == y for x, y in zip(p.tokens, q.tokens)) / max(1, len(p.tokens)) for p, q in zip(a, b)]
-    first = [p.tokens[:1] == q.tokens[:1] for p, q in zip(a, b)]
+    full = random_weights(cfg, dev, seed=5)
+    ref = LlamaDecoder(cfg, dev, weights=full)
+    src = (rank + 1) % world if wrong_order else rank
+    tp = LlamaDecoder(cfg, dev, tp=TPContext(rank, world, None), weights=shard_weights(cfg, full, src, world))
+    prompts = [list(range(30 + 5 * i, 30 + 5 * i + n)) for i, n in enumerate((9, 33, 4, 120, 17, 64, 25, 7))]
+    steps = 8
+    a = Generator(ref, max_batch=8, max_seq=256, temperature=0.0, use_graphs=False).generate(prompts, steps)
+    b = Generator(tp, max_batch=8, max_seq=256, temperature=0.0, use_graphs=False).generate(prompts, steps)
+
+    def last_logits(m, seq):
+        t = torch.tensor(seq, dtype=torch.int32, device=dev)
+        return m.prefill(t, torch.arange(len(seq), dtype=torch.int32, device=dev),
+                         torch.zeros(len(seq), dtype=torch.int32, device=dev),
+                         torch.tensor([0, len(seq)], dtype=torch.int32, device=dev), len(seq),
+                         torch.tensor([len(seq) - 1], device=dev))[0].float()
+    ref.alloc_cache(1, 256)
+    tp.alloc_cache(1, 256)
+    d, dec = 0.0, []
+    for p, x in zip(prompts, a):
+        st = []
+        for t in range(len(x.tokens)):
+            lr, lt = last_logits(ref, p + x.tokens[:t]), last_logits(tp, p + x.tokens[:t])
+            d = max(d, float((lr - lt).abs().max()))
+            top = torch.topk(lr, 2)
+            st.append((float(top.values[0] - top.values[1]), int(top.indices[0]), int(lt.argmax())))
+        dec.append(st)
+    flat = [s_ for st in dec for s_ in st]
+    checked = [s_ for s_ in flat if s_[0] > 2 * d]
+    prefix_ok = []
+    for st, x, y in zip(dec, a, b):
+        n = next((j for j, s_ in enumerate(st) if s_[0] <= 2 * d), len(st))
+        prefix_ok.append(x.tokens[:n] == y.tokens[:n])
     _done(rank, out_path, {"xgmi": tp.tp.xgmi is not None, "xgmi_calls": tp.tp.xgmi.calls if tp.tp.xgmi else 0,
-                           "agree": agree, "first_equal": first,
+                           "decisions": len(flat), "checked": len(checked),
+                           "checked_agree": sum(1 for _, r_, t_ in checked if r_ == t_), "prefix_ok": prefix_ok,
+                           "max_logit_diff": d,
                            "max_prob_diff": max(abs(p.mean_prob - q.mean_prob) for p, q in zip(a, b))})
+
+
+def check_tp_decoder_gpu_wrong_order(rank, world, port, out_path):
+    check_tp_decoder_gpu(rank, world, port, out_path, wrong_order=True)

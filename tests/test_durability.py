@@ -222,3 +222,91 @@ def test_startup_sweep_skips_in_flight_documents_and_analyze_is_idempotent(tmp_p
     asyncio.run(store.update_document_status(doc, STATUS_READY))
     deps = types.SimpleNamespace(store=store, llm=Boom(), config=types.SimpleNamespace(chunk_overlap=0))
     asyncio.run(handle_analyze(deps, {"document_id": doc, "redrive": True}))
+
+
+def test_bad_mutation_is_rejected_before_it_is_logged_and_restart_works(tmp_path):
+    """A wrong-dim index_add must fail the call without touching the document's rows or the log,
+    and the engine must come back after a restart (round-2 advisor finding, index/wal.py:177)."""
+    d = 32
+    idx = FlatIndex(d, "cpu")
+    log = ShardLog(str(tmp_path), fsync=False)
+    log.recover(idx)
+    log.put(idx, "doc", np.arange(4), _unit(4, d, 1))
+    with pytest.raises(ValueError, match="dim"):
+        log.upsert(idx, "doc", np.arange(2) + 100, _unit(2, d + 8, 2))
+    with pytest.raises(ValueError, match="keys"):
+        log.put(idx, "doc", np.arange(3), _unit(2, d, 3))
+    assert idx.docs["doc"].rows == 4 and log.stats["appended"] == 1
+    log.close()
+    idx2 = FlatIndex(d, "cpu")
+    rec = ShardLog(str(tmp_path), fsync=False).recover(idx2)
+    assert rec["rows"] == 4 and rec["quarantined"] == 0 and idx2.docs["doc"].rows == 4
+
+
+def test_unappliable_record_is_quarantined_not_fatal(tmp_path):
+    """A record that fails to apply on replay (e.g. written by an older build without validation)
+    is skipped and counted; recovery continues with the records after it."""
+    from docagents_amd.index.wal import OP_PUT, _encode
+    d = 16
+    log = ShardLog(str(tmp_path), fsync=False)
+    log.recover(FlatIndex(d, "cpu"))
+    log._append(_encode(OP_PUT, "bad", np.arange(2), _unit(2, d * 2, 5)))  # wrong dim, bypassing validation
+    log.put(FlatIndex(d, "cpu"), "good", np.arange(3), _unit(3, d, 6))
+    log.close()
+    idx = FlatIndex(d, "cpu")
+    log2 = ShardLog(str(tmp_path), fsync=False)
+    rec = log2.recover(idx)
+    assert rec["quarantined"] == 1 and rec["replayed"] == 1 and idx.docs["good"].rows == 3
+    assert log2.quarantine[0]["doc"] == "bad"
+
+
+def test_index_add_is_a_per_chunk_upsert(tmp_path):
+    """SaveEmbeddings parity (postgres.go:197, ON CONFLICT (chunk_id)): saving two chunk subsets of
+    one document keeps both; re-saving a chunk replaces only that chunk's row."""
+    from docagents_amd.engine.engine import Engine
+    from docagents_amd.engine.server import EngineGroup
+    eng = Engine("tiny-enc", "tiny-dec", "cpu", load_llm=False)
+    for durable in (False, True):
+        eng.index = FlatIndex(eng.dim, "cpu")
+        sl = ShardLog(str(tmp_path / f"d{durable}"), fsync=False) if durable else None
+        if sl:
+            sl.recover(eng.index)
+        g = EngineGroup(eng, shard_log=sl)
+        v = _unit(5, eng.dim, 7).numpy()
+        g.execute("index_add", {"doc_id": "doc", "keys": np.array([1, 2, 3]), "vecs": v[:3]})
+        g.execute("index_add", {"doc_id": "doc", "keys": np.array([4, 5]), "vecs": v[3:]})
+        assert eng.index.docs["doc"].rows == 5
+        g.execute("index_add", {"doc_id": "doc", "keys": np.array([2]), "vecs": v[4:5]})  # chunk 2 re-embedded
+        assert eng.index.docs["doc"].rows == 5
+        q = torch.from_numpy(v[4:5])
+        s, rows = eng.index.search(q, 5, -1.0, [["doc"]])
+        keys = eng.index.row_ids(rows.numpy().astype(np.int64))[0]
+        assert sorted(keys.tolist()) == [1, 2, 3, 4, 5]
+        top2 = set(keys[:2].tolist())
+        assert top2 == {2, 5}  # chunk 2 now carries chunk 5's vector: both score 1.0
+        s_all, rows_all = eng.index.search(q, 10, -1.0, None)
+        assert (rows_all >= 0).sum() == 5  # the replaced row is gone from dense scans too
+        if sl:
+            sl.close()
+            idx2 = FlatIndex(eng.dim, "cpu")
+            ShardLog(str(tmp_path / f"d{durable}"), fsync=False).recover(idx2)
+            assert idx2.docs["doc"].rows == 5
+
+
+def test_checkpoint_fsyncs_snapshot_and_directory_before_deleting_logs(tmp_path, monkeypatch):
+    calls = []
+    real_fsync, real_remove = os.fsync, os.remove
+    monkeypatch.setattr(os, "fsync", lambda fd: (calls.append(("fsync", os.readlink(f"/proc/self/fd/{fd}"))),
+                                                 real_fsync(fd))[1])
+    monkeypatch.setattr(os, "remove", lambda p: (calls.append(("remove", p)), real_remove(p))[1])
+    d = 16
+    idx = FlatIndex(d, "cpu")
+    log = ShardLog(str(tmp_path), fsync=True)
+    log.recover(idx)
+    log.put(idx, "doc", np.arange(2), _unit(2, d, 1))
+    calls.clear()
+    log.checkpoint(idx)
+    first_remove = next(i for i, c in enumerate(calls) if c[0] == "remove")
+    synced = [c[1] for c in calls[:first_remove] if c[0] == "fsync"]
+    assert any(p.endswith(".snap.tmp") for p in synced), synced       # snapshot file contents
+    assert synced.count(os.path.abspath(str(tmp_path))) >= 1, synced  # directory (rename + new log)

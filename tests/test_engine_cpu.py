@@ -493,3 +493,21 @@ def test_batched_tokenization_matches_serial(eng):
     q = "what is alpha?"
     assert eng.answer_prompt_ids(q, [[5, 6]], 16) == \
         eng.answer_prompt_ids(q, [[5, 6]], 16, tail=eng._ids_many([eng._answer_tail(q)] * 2)[0])
+
+
+def test_kept_head_slot_never_blocks_a_full_wave():
+    """A Generator that allocates its own cache (max_batch + 1 slots) must not keep a prompt-head
+    slot taken from a full wave's budget: 2 shared-head prompts, then max_batch prompts, both run
+    (round-2 advisor finding, generator.py:76)."""
+    from docagents_amd.engine.generator import Generator
+    from docagents_amd.models.configs import decoder_config
+    from docagents_amd.models.llama import LlamaDecoder
+    m = LlamaDecoder(decoder_config("tiny-dec"), "cpu", seed=0)
+    g = Generator(m, max_batch=4, max_seq=512, temperature=0.0, use_graphs=False)
+    rng = np.random.default_rng(3)
+    head = [int(t) for t in rng.integers(5, 3000, size=130)]
+    two = [head + [int(t) for t in rng.integers(5, 3000, size=n)] for n in (3, 9)]
+    assert len(g.generate(two, 4)) == 2
+    full = [head + [int(t) for t in rng.integers(5, 3000, size=n)] for n in (1, 2, 3, 4)]
+    assert len(g.generate(full, 4)) == 4
+    assert len(g.cache.free) + 1 + (g.head is not None) == g.cache.slots
