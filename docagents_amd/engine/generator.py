@@ -163,11 +163,12 @@ class Generator:
             last = (cu[1:] - 1).astype(np.int64)
             t0 = time.perf_counter()
             to = lambda a: h2d(a, dev)  # noqa: E731
-            logits = m.prefill(to(flat), to(pos), to(slot_tok), to(cu), int(lens.max()), to(last), prefix=prefix)
+            logits = m.prefill(to(flat), to(pos), to(slot_tok), to(cu), int(lens.max()), to(last), prefix=prefix,
+                               local_logits=True)
             r0, r1 = row0 + i, row0 + j
-            m.ops.sample(logits, self.temperature, self.seed, 0, out_tok=st.tokens[r0:r1], out_lp=st.lp[r0:r1],
-                         conf=st.conf[r0:r1], active=st.active[r0:r1], ctr=st.pos[r0:r1], pos=st.pos[r0:r1],
-                         lens=st.lens[r0:r1], hist=st.hist[r0:r1], start=st.start[r0:r1], eos=self.eos)
+            m.sample(logits, self.temperature, self.seed, 0, out_tok=st.tokens[r0:r1], out_lp=st.lp[r0:r1],
+                     conf=st.conf[r0:r1], active=st.active[r0:r1], ctr=st.pos[r0:r1], pos=st.pos[r0:r1],
+                     lens=st.lens[r0:r1], hist=st.hist[r0:r1], start=st.start[r0:r1], eos=self.eos)
             self.stats["prefill_tokens"] += int(tot)
             self.stats["prefill_s"] += time.perf_counter() - t0
             i = j

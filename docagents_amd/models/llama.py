@@ -14,9 +14,12 @@ N6-N8). Per layer (hidden state x is the residual stream, updated in place):
     g   = silu(h Wg^T) * (h Wu^T)                      ONE GEMM with the fused SwiGLU epilogue
     x   = x + g @ Wdown^T                              GEMM + residual (row-parallel + all-reduce)
 
-TP layout (rank r of t): local q/k/v heads, F/t FFN features, vocab-parallel lm_head whose [B, V/t]
-logits are all-gathered before the (replicated, identically seeded) sampler. With TP the residual
-is added by rank 0's epilogue only, so a single in-place all-reduce yields x + sum of partials.
+TP layout (rank r of t): local q/k/v heads, F/t FFN features, vocab-parallel lm_head. Generation
+never gathers the [B, V/t] logits: each rank reduces its slice to 8 floats per row (best Gumbel
+score + its global index, local max, local sum-exp, the best's logit) and one tiny gather of those
+picks the token and its full-vocabulary logprob (distributed sampling, SURVEY §2.4 C4;
+``LlamaDecoder.sample``). With TP the residual is added by rank 0's epilogue only, so a single
+in-place all-reduce yields x + sum of partials.
 """
 from __future__ import annotations
 
@@ -39,6 +42,7 @@ class TPContext:
     def __init__(self, rank: int = 0, size: int = 1, group=None):
         self.rank, self.size, self.group = rank, size, group
         self.xgmi = None  # XgmiAllReduce once setup_device() ran on a GPU
+        self.xgmi_norm = None  # a second communicator for the fused all-reduce + RMSNorm (one row width)
 
     def setup_device(self, device: torch.device) -> None:
         """Collective (every TP rank): map the peers' all-reduce buffers over xGMI (GPU only).
@@ -47,6 +51,9 @@ class TPContext:
         if self.size > 1 and device.type == "cuda" and self.xgmi is None:
             from ..parallel.xgmi_allreduce import XgmiAllReduce
             self.xgmi = XgmiAllReduce.create(self.group, device)
+            if self.xgmi is not None:
+                # decode-sized rows only (one-shot): 512 KB = 32 rows of Llama-3-70B's 8192
+                self.xgmi_norm = XgmiAllReduce.create(self.group, device, max_bytes=512 << 10)
 
     def all_reduce_(self, t: torch.Tensor) -> torch.Tensor:
         if self.size > 1:
@@ -60,6 +67,15 @@ class TPContext:
             else:
                 dist.all_reduce(t, group=self.group)
         return t
+
+    def all_reduce_norm_(self, x: torch.Tensor, gamma, eps: float, h_out: torch.Tensor, ops) -> torch.Tensor:
+        """x <- sum over the group (in place), h_out <- RMSNorm(x) * gamma. One fused launch over
+        the xGMI peer buffers when it takes the rows (C3 with the residual stream's next norm in its
+        epilogue); otherwise the all-reduce and the rmsnorm kernel (CPU / gloo: the same math)."""
+        if self.size > 1 and self.xgmi_norm is not None and self.xgmi_norm.takes_norm(x):
+            return self.xgmi_norm.all_reduce_rmsnorm_(x, gamma, eps, h_out)
+        self.all_reduce_(x)
+        return ops.rmsnorm(x, gamma, eps, out=h_out)
 
     def all_gather_cols(self, t: torch.Tensor) -> torch.Tensor:
         """[B, n] on every rank -> [B, n * size] (rank-major columns)."""
@@ -77,6 +93,17 @@ class TPContext:
         from ..parallel.dist import all_gather_rows
         out = all_gather_rows(t.contiguous(), self.group)
         return out.view(self.size, t.shape[0], -1).permute(1, 0, 2).reshape(t.shape[0], -1)
+
+
+def tp_sample(ops, tp: TPContext, logits, temperature: float, seed: int, step: int = 0, **kw):
+    """Sampling over a vocab-parallel LM head (see LlamaDecoder.sample): partial stats of this rank's
+    slice [B, V/t] (global indices from rank * V/t), one all-gather of [B, 8] fp32, finalize."""
+    if tp.size == 1:
+        return ops.sample(logits, temperature, seed, step, **kw)
+    ctr = kw.pop("ctr", None)
+    stats = ops.sample_partial(logits, temperature, seed, v0=tp.rank * logits.shape[1], step=step, ctr=ctr)
+    gathered = tp.all_gather_cols(stats).contiguous()
+    return ops.sample_finalize(gathered, tp.size, **kw)
 
 
 def to_interleaved_rope(wqkv: torch.Tensor, H: int, Hkv: int, D: int) -> torch.Tensor:
@@ -238,19 +265,31 @@ class LlamaDecoder:
         tp.all_reduce_(x)
         return x
 
-    def _logits(self, hlast):
+    def _logits(self, hlast, gather: bool = True):
+        """Logits of the rows of ``hlast``: the full [B, V] (gather=True; an all-gather of the vocab
+        slices under TP) or this rank's slice [B, V/t] (gather=False: what ``sample`` consumes)."""
         o = self.ops
         if o.gemv_fusable(hlast.shape[0], self.w["lm_head"].shape[0], hlast.shape[1]):
             logits = o.gemm(hlast.contiguous(), self.w["lm_head"], rms=(self._gain(self.w["norm"]), self.cfg.eps))
         else:
             h = o.rmsnorm(hlast, self.w["norm"], self.cfg.eps)
             logits = o.gemm(h, self.w["lm_head"])
-        return self.tp.all_gather_cols(logits)
+        return self.tp.all_gather_cols(logits) if gather else logits
+
+    def sample(self, logits, temperature: float, seed: int, step: int = 0, **kw):
+        """Sample one token per row from this rank's logits (the full row at TP=1, its vocab slice
+        under TP) with the fused sampler's bookkeeping (``ops.sample`` keywords). Under TP: the
+        slice's 8-float summary per row -> ONE all-gather of [B, 8] fp32 per rank (graph-capturable
+        over the xGMI peer buffers) -> the finalize kernel; every rank ends with the same token,
+        logprob and bookkeeping, identical to sampling the gathered row."""
+        return tp_sample(self.ops, self.tp, logits, temperature, seed, step, **kw)
 
     # ------------------------------------------------------------- prefill
     def prefill(self, ids: torch.Tensor, pos: torch.Tensor, slot_tok: torch.Tensor, cu: torch.Tensor,
-                max_seqlen: int, last_idx: torch.Tensor, prefix: tuple[int, int] | None = None) -> torch.Tensor:
-        """Packed causal prefill; writes the KV cache; returns logits [B, V] of each sequence's last token.
+                max_seqlen: int, last_idx: torch.Tensor, prefix: tuple[int, int] | None = None,
+                local_logits: bool = False) -> torch.Tensor:
+        """Packed causal prefill; writes the KV cache; returns logits [B, V] of each sequence's last token
+        (local_logits: this rank's vocab slice [B, V/t], the input of ``sample``).
         prefix = (slot, P): every sequence continues a shared P-token head already in ``slot``'s cache
         (``pos`` then starts at P); attention reads those keys from the cache."""
         c, o, cache = self.cfg, self.ops, self.cache
@@ -265,7 +304,7 @@ class LlamaDecoder:
                                     max_seqlen, hl, kl, D, causal=True, prefix=pre)
             del qkv, h
             x = self._attn_out_and_mlp(L, a, x)
-        return self._logits(x.index_select(0, last_idx))
+        return self._logits(x.index_select(0, last_idx), gather=not local_logits)
 
     # ------------------------------------------------------------- decode (graph-capturable)
     def decode_step(self, st: "DecodeState") -> torch.Tensor:
@@ -274,6 +313,8 @@ class LlamaDecoder:
         x = o.embed(st.tokens, self.w["embed"], out=st.x)
         if self._norm_fusable(x.shape[0]):
             return self._decode_step_fused_norms(st, x)
+        if self.tp.size > 1 and x.shape[0] > 1:
+            return self._decode_step_tp_fused_norms(st, x)
         fuse = o.gemv_fusable(x.shape[0], self.w["layers"][0]["wqkv"].shape[0], x.shape[1])
         for li, L in enumerate(self.w["layers"]):
             if fuse:  # batch 1: RMSNorm folded into the QKV GEMV (no separate norm launch)
@@ -283,10 +324,10 @@ class LlamaDecoder:
                 qkv = o.gemm(h, L["wqkv"], out=st.qkv)
             a = self._decode_attn(qkv, li, st)
             self._attn_out_and_mlp(L, a, x)
-        logits = self._logits(x)
+        logits = self._logits(x, gather=False)
         st.logits.copy_(logits)
-        o.sample(st.logits, st.temperature, st.seed, 0, out_tok=st.tokens, out_lp=st.lp, conf=st.conf,
-                 active=st.active, ctr=st.pos, pos=st.pos, lens=st.lens, hist=st.hist, start=st.start, eos=st.eos)
+        self.sample(st.logits, st.temperature, st.seed, 0, out_tok=st.tokens, out_lp=st.lp, conf=st.conf,
+                    active=st.active, ctr=st.pos, pos=st.pos, lens=st.lens, hist=st.hist, start=st.start, eos=st.eos)
         return st.tokens
 
     def _decode_attn(self, qkv, li: int, st: "DecodeState"):
@@ -325,6 +366,34 @@ class LlamaDecoder:
                  active=st.active, ctr=st.pos, pos=st.pos, lens=st.lens, hist=st.hist, start=st.start, eos=st.eos)
         return st.tokens
 
+    def _decode_step_tp_fused_norms(self, st: "DecodeState", x: torch.Tensor) -> torch.Tensor:
+        """Tensor-parallel decode (B > 1) with the TP=1 fused-norm structure: every RMSNorm rides in
+        the epilogue of the all-reduce before it (the o-proj's sum + ln_mlp, the down-proj's sum +
+        the next layer's ln_attn / the final norm), so a layer is QKV GEMM, attention, o GEMM, fused
+        AR+norm, gate/up GEMM, down GEMM, fused AR+norm — no standalone norm launches."""
+        c, o, tp = self.cfg, self.ops, self.tp
+        layers = self.w["layers"]
+        h = o.rmsnorm(x, layers[0]["ln_attn"], c.eps, out=st.h)
+        for li, L in enumerate(layers):
+            qkv = o.gemm(h, L["wqkv"], out=st.qkv)
+            a = self._decode_attn(qkv, li, st)
+            if tp.rank == 0:
+                o.gemm(a, L["wo"], epi=EPI_RESID, resid=x, out=x)
+            else:
+                o.gemm(a, L["wo"], out=x)
+            h = tp.all_reduce_norm_(x, L["ln_mlp"], c.eps, st.h, o)
+            g = o.gemm(h, L["w_gu"], epi=EPI_SWIGLU)
+            if tp.rank == 0:
+                o.gemm(g, L["w_down"], epi=EPI_RESID, resid=x, out=x)
+            else:
+                o.gemm(g, L["w_down"], out=x)
+            nxt = layers[li + 1]["ln_attn"] if li + 1 < len(layers) else self.w["norm"]
+            h = tp.all_reduce_norm_(x, nxt, c.eps, st.h, o)
+        st.logits.copy_(o.gemm(h, self.w["lm_head"]))  # h already carries the final norm; local vocab slice
+        self.sample(st.logits, st.temperature, st.seed, 0, out_tok=st.tokens, out_lp=st.lp, conf=st.conf,
+                    active=st.active, ctr=st.pos, pos=st.pos, lens=st.lens, hist=st.hist, start=st.start, eos=st.eos)
+        return st.tokens
+
     def prefill_flops(self, lens) -> float:
         c = self.cfg
         h, D = c.hidden, c.head_dim
@@ -357,7 +426,7 @@ class DecodeState:
         self.h = torch.zeros(B, h, dtype=torch.bfloat16, device=dev)
         self.qkv = torch.zeros(B, (model.hl + 2 * model.kl) * c.head_dim, dtype=torch.bfloat16, device=dev)
         self.attn = torch.zeros(B, model.hl * c.head_dim, dtype=torch.bfloat16, device=dev)
-        self.logits = torch.zeros(B, c.vocab, dtype=torch.bfloat16, device=dev)
+        self.logits = torch.zeros(B, c.vocab // model.tp.size, dtype=torch.bfloat16, device=dev)  # this rank's slice
         self.temperature, self.seed, self.eos = temperature, seed, tuple(eos)[:4]
         self.graph = None
 

@@ -149,6 +149,111 @@ __global__ __launch_bounds__(AR_TPB) void allreduce_kernel(ArPtrs data, ArPtrs s
   if (t == 0) self->cnt[b] = k + 1u;
 }
 
+// ---------------------------------------------------------------------------------------------
+// One-shot all-reduce with the residual-stream RMSNorm fused into its epilogue (TP decode: the
+// row-parallel o / down projection's partial sums are reduced AND the next RMSNorm is applied in
+// the same launch, as gemm_resid_norm does at TP = 1). The input rows are this rank's partials,
+// rank 0's already including the residual (models/llama.py), so
+//   x[r] = bf16(sum over ranks in rank order)      (== allreduce_kernel's output, bit for bit)
+//   h[r] = bf16(x[r] * rsqrt(mean(x[r]^2) + eps) * gamma)   (== rmsnorm_kernel on x, bit for bit)
+// Bit-identity with the unfused pair holds because the thread -> chunk map, the per-thread
+// accumulation order and block_sum are rmsnorm_kernel's (launch with blockDim = its row_threads(D)).
+// Partition: whole rows per workgroup (row r -> workgroup r % G) so the norm's reduction stays in
+// one workgroup; the per-workgroup counters / barriers / staging parity are allreduce_kernel's, and
+// every rank uses the same (rows, G) for a call, so the protocol invariants carry over.
+#define ARN_MAXCH 8
+__global__ __launch_bounds__(AR_TPB) void allreduce_rmsnorm_kernel(ArPtrs data, ArPtrs sig, const bf16_t* __restrict__ in,
+                                                                   bf16_t* __restrict__ xout, bf16_t* __restrict__ hout,
+                                                                   const bf16_t* __restrict__ gamma, int rows, int D,
+                                                                   float eps, long long parity_vec, int rank, int world,
+                                                                   long long timeout) {
+  __shared__ float red[16];
+  const int b = blockIdx.x, G = gridDim.x, t = threadIdx.x, bd = blockDim.x;
+  ArSignal* self = (ArSignal*)sig.p[rank];
+  __shared__ uint32_t s_k;
+  if (t == 0) s_k = self->cnt[b];
+  __syncthreads();
+  const uint32_t k = s_k;
+  const long long poff = (k & 1) ? parity_vec : 0;
+  const int nch = D / 8;
+  u32x4_t* mine = (u32x4_t*)data.p[rank] + poff;
+  const u32x4_t* inv4 = (const u32x4_t*)in;
+  for (int r = b; r < rows; r += G) {  // phase 1: stage own rows
+    for (int c = t; c < nch; c += bd) mine[(long long)r * nch + c] = inv4[(long long)r * nch + c];
+  }
+  ar_barrier(sig, self, rank, world, b, 2u * k + 1u, timeout);
+  for (int r = b; r < rows; r += G) {
+    float v[ARN_MAXCH][8];
+    float ss = 0.f;
+#pragma unroll
+    for (int i = 0; i < ARN_MAXCH; ++i) {
+      const int c = t + i * bd;
+      if (c < nch) {
+        const u32x4_t s = ar_sum<true>(data, poff, (long long)r * nch + c, world);
+        *(u32x4_t*)(xout + (size_t)r * D + c * 8) = s;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          v[i][2 * e] = bf2f((bf16_t)(s[e] & 0xffff));
+          v[i][2 * e + 1] = bf2f((bf16_t)(s[e] >> 16));
+        }
+#pragma unroll
+        for (int e = 0; e < 8; ++e) ss += v[i][e] * v[i][e];
+      }
+    }
+    ss = block_sum(ss, red);
+    const float inv = rsqrtf(ss / D + eps);
+#pragma unroll
+    for (int i = 0; i < ARN_MAXCH; ++i) {
+      const int c = t + i * bd;
+      if (c < nch) {
+        float wv[8];
+        if (gamma) {
+          const u32x4_t g = *(const u32x4_t*)(gamma + c * 8);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            wv[2 * e] = bf2f((bf16_t)(g[e] & 0xffff));
+            wv[2 * e + 1] = bf2f((bf16_t)(g[e] >> 16));
+          }
+        } else {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) wv[e] = 1.f;
+        }
+        float y[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) y[e] = v[i][e] * inv * wv[e];
+        *(u32x4_t*)(hout + (size_t)r * D + c * 8) =
+            u32x4_t{pack_bf2(y[0], y[1]), pack_bf2(y[2], y[3]), pack_bf2(y[4], y[5]), pack_bf2(y[6], y[7])};
+      }
+    }
+    __syncthreads();  // `red` is reused by the next row's block_sum
+  }
+  if (t == 0) self->cnt[b] = k + 1u;
+}
+
+// rows x D bf16 (D % 8 == 0, D / 8 <= ARN_MAXCH * 256); threads = the rmsnorm kernel's row_threads(D);
+// grid = min(rows, grid cap). in / xout may alias (in place); gamma may be null (unit gain).
+DA_EXPORT int da_ar_allreduce_rmsnorm(const void* in, void* xout, void* hout, const void* gamma, int rows, int D,
+                                      float eps, int rank, int world, void* const* data, void* const* sig,
+                                      long long parity_bytes, int grid, long long timeout_ticks, hipStream_t stream) {
+  if (world < 2 || world > AR_MAX_RANKS || rank < 0 || rank >= world) return (int)hipErrorInvalidValue;
+  if (rows <= 0 || D % 8 || D / 8 > ARN_MAXCH * AR_TPB) return (int)hipErrorInvalidValue;
+  const long long nbytes = (long long)rows * D * 2;
+  if (nbytes > parity_bytes || parity_bytes % 16) return (int)hipErrorInvalidValue;
+  if (grid < 1 || grid > AR_MAX_BLOCKS) return (int)hipErrorInvalidValue;
+  ArPtrs d{}, s{};
+  for (int w = 0; w < world; ++w) {
+    d.p[w] = (char*)data[w];
+    s.p[w] = (char*)sig[w];
+  }
+  int ch = D / 8, threads = ((ch + 63) / 64) * 64;  // == norm.hip row_threads(D)
+  threads = threads > AR_TPB ? AR_TPB : (threads < 64 ? 64 : threads);
+  const int g = rows < grid ? rows : grid;
+  allreduce_rmsnorm_kernel<<<g, threads, 0, stream>>>(d, s, (const bf16_t*)in, (bf16_t*)xout, (bf16_t*)hout,
+                                                      (const bf16_t*)gamma, rows, D, eps, parity_bytes / 16, rank,
+                                                      world, timeout_ticks);
+  DA_LAUNCH_CHECK();
+}
+
 DA_EXPORT int da_ar_signal_bytes() { return (int)sizeof(ArSignal); }
 DA_EXPORT int da_ar_max_blocks() { return AR_MAX_BLOCKS; }
 DA_EXPORT int da_ar_block_vecs() { return AR_TPB; }

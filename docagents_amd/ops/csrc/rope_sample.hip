@@ -149,6 +149,119 @@ sample_kernel(SampleArgs a) {
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Distributed sampling for a vocab-parallel LM head ("prefer distributed
+// sampling"): each tensor-parallel rank holds logits [B, V/t] of the vocabulary slice
+// [v0, v0 + V/t) and reduces it to 8 floats per row —
+//   {best Gumbel score, its GLOBAL index (int bits), local max, sum exp(x - local max), logit of the
+//    best, 0, 0, 0}
+// — the ranks exchange only those (B x 32 B per rank instead of B x V/t bf16 logits), and
+// sample_finalize_kernel picks the winner (max score, ties to the lower index, i.e. the lower
+// rank), rebuilds the full log-sum-exp and runs sample_kernel's bookkeeping. The Gumbel noise is a
+// function of the global index, so the token is the one sample_kernel draws from the full row.
+__global__ void __launch_bounds__(1024)
+sample_partial_kernel(const bf16_t* __restrict__ logits, int V, int ld, int v0, float temperature, unsigned seed,
+                      unsigned step, const int* __restrict__ ctr, float* __restrict__ stats) {
+  __shared__ float redf[16];
+  __shared__ float bestv[16];
+  __shared__ int besti[16];
+  const int b = blockIdx.x;
+  const bf16_t* row = logits + (size_t)b * ld;
+  const float invT = temperature > 0.f ? 1.f / temperature : 0.f;
+  const unsigned rs = ctr ? (unsigned)ctr[b] : step;
+  const unsigned rkey = rs * 131071u + (unsigned)b;
+  float mx = -INFINITY, bv = -INFINITY;
+  int bi = v0;
+  for (int v = threadIdx.x; v < V; v += blockDim.x) {
+    const float x = bf2f(row[v]);
+    mx = fmaxf(mx, x);
+    float score = x;
+    if (temperature > 0.f) score = x * invT - __logf(-__logf(u01(seed, rkey, (unsigned)(v0 + v))));
+    if (score > bv) { bv = score; bi = v0 + v; }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float ov = __shfl_xor(bv, o, 64);
+    const int oi = __shfl_xor(bi, o, 64);
+    if (ov > bv || (ov == bv && oi < bi)) { bv = ov; bi = oi; }
+  }
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  if (lane == 0) { bestv[wid] = bv; besti[wid] = bi; }
+  const float lmax = block_max(mx, redf);
+  float sacc = 0.f;
+  for (int v = threadIdx.x; v < V; v += blockDim.x) sacc += __expf(bf2f(row[v]) - lmax);
+  sacc = block_sum(sacc, redf);
+  if (threadIdx.x == 0) {
+    float fv = bestv[0];
+    int fi = besti[0];
+    for (int i = 1; i < nw; ++i)
+      if (bestv[i] > fv || (bestv[i] == fv && besti[i] < fi)) { fv = bestv[i]; fi = besti[i]; }
+    float* o = stats + (size_t)b * 8;
+    o[0] = fv;
+    o[1] = __int_as_float(fi);
+    o[2] = lmax;
+    o[3] = sacc;
+    o[4] = bf2f(row[fi - v0]);
+    o[5] = o[6] = o[7] = 0.f;
+  }
+}
+
+// gathered: [B][ranks][8] (the per-rank stats, rank-major within a row). One thread per row.
+__global__ void __launch_bounds__(64)
+sample_finalize_kernel(const float* __restrict__ gathered, int B, int ranks, SampleArgs a) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  const float* g = gathered + (size_t)b * ranks * 8;
+  float fv = g[0], xb = g[4], gmax = g[2];
+  int fi = __float_as_int(g[1]);
+  for (int r = 1; r < ranks; ++r) {
+    const float* q = g + r * 8;
+    const int qi = __float_as_int(q[1]);
+    if (q[0] > fv || (q[0] == fv && qi < fi)) { fv = q[0]; fi = qi; xb = q[4]; }
+    gmax = fmaxf(gmax, q[2]);
+  }
+  float s = 0.f;
+  for (int r = 0; r < ranks; ++r) s += g[r * 8 + 3] * __expf(g[r * 8 + 2] - gmax);
+  const float lp = xb - gmax - __logf(s);
+  const bool on = a.active ? a.active[b] != 0 : true;
+  if (!on) return;
+  a.out_tok[b] = fi;
+  if (a.out_lp) a.out_lp[b] = lp;
+  if (a.conf) { a.conf[2 * b] += __expf(lp); a.conf[2 * b + 1] += 1.f; }
+  bool stop = (fi == a.eos0 || fi == a.eos1 || fi == a.eos2 || fi == a.eos3);
+  if (a.hist) {
+    const int gi = a.pos[b] - a.start[b];
+    if (gi >= 0 && gi < a.hist_ld) a.hist[(size_t)b * a.hist_ld + gi] = fi;
+    if (gi + 1 >= a.hist_ld) stop = true;
+  }
+  if (a.pos) a.pos[b] += 1;
+  if (a.lens) a.lens[b] += 1;
+  if (stop && a.active) a.active[b] = 0;
+}
+
+DA_EXPORT int da_sample_partial(const void* logits, int B, int V, int ld, int v0, float temperature, unsigned seed,
+                                unsigned step, const void* ctr, void* stats, void* stream) {
+  if (B == 0) return 0;
+  if (V <= 0 || ld < V || v0 < 0) return (int)hipErrorInvalidValue;
+  sample_partial_kernel<<<B, 1024, 0, (hipStream_t)stream>>>((const bf16_t*)logits, V, ld, v0, temperature, seed,
+                                                             step, (const int*)ctr, (float*)stats);
+  DA_LAUNCH_CHECK();
+}
+
+DA_EXPORT int da_sample_finalize(const void* gathered, int B, int ranks, void* out_tok, void* out_lp, void* conf,
+                                 void* active, void* pos, void* lens, void* hist, const void* start, int hist_ld,
+                                 int eos0, int eos1, int eos2, int eos3, void* stream) {
+  if (hist && (!pos || !start)) return (int)hipErrorInvalidValue;
+  if (ranks < 1) return (int)hipErrorInvalidValue;
+  if (B == 0) return 0;
+  SampleArgs a{};
+  a.out_tok = (int*)out_tok; a.out_lp = (float*)out_lp; a.conf = (float*)conf;
+  a.active = (int*)active; a.pos = (int*)pos; a.lens = (int*)lens; a.hist = (int*)hist; a.start = (const int*)start;
+  a.hist_ld = hist_ld; a.eos0 = eos0; a.eos1 = eos1; a.eos2 = eos2; a.eos3 = eos3;
+  sample_finalize_kernel<<<(B + 63) / 64, 64, 0, (hipStream_t)stream>>>((const float*)gathered, B, ranks, a);
+  DA_LAUNCH_CHECK();
+}
+
 DA_EXPORT int da_rope_cache(void* qkv, const void* pos, const void* slot, const void* cos_sin, void* k_cache,
                             void* v_cache, int T, int H, int Hkv, int D, int max_seq, int rotate_q, void* stream) {
   if (D % 8 || (D / 2) % 4) return (int)hipErrorInvalidValue;

@@ -73,6 +73,8 @@ _SIGS = {
                        c_float, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p],
     "da_topk_merge": [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p],
     "da_kmeans_accum": [c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p],
+    "da_sample_partial": [c_void_p, c_int, c_int, c_int, c_int, c_float, c_uint, c_uint, c_void_p, c_void_p, c_void_p],
+    "da_sample_finalize": [c_void_p, c_int, c_int] + [c_void_p] * 7 + [c_int] * 5 + [c_void_p],
     "da_stream_create_cumask": [c_uint, ctypes.POINTER(c_uint), ctypes.POINTER(c_void_p)],
     "da_stream_get_cumask": [c_void_p, c_uint, ctypes.POINTER(c_uint)],
     "da_stream_destroy": [c_void_p],
@@ -607,6 +609,53 @@ def sample(logits, temperature: float, seed: int, step: int = 0, out_tok=None, o
                            step & 0xffffffff, _ptr(ctr), _ptr(out_tok), _ptr(out_lp), _ptr(conf), _ptr(active),
                            _ptr(pos), _ptr(lens), _ptr(hist), _ptr(start), hist_ld, e[0], e[1], e[2], e[3],
                            _stream()), "sample")
+    return out_tok, out_lp
+
+
+def sample_partial(logits, temperature: float, seed: int, v0: int, step: int = 0, ctr=None, out=None):
+    """Vocab-parallel sampling, rank side: logits [B, Vl] of the vocabulary slice starting at global
+    index v0 -> stats fp32 [B, 8] = (best Gumbel score, best global index as int bits, local max,
+    local sum exp(x - max), logit of the best, 0, 0, 0). See rope_sample.hip."""
+    _bf16_cuda(logits, "logits")
+    B, V = logits.shape
+    _req(logits.stride(1) == 1, "logits rows must be contiguous")
+    if ctr is not None:
+        _i32(ctr, "ctr"); _req(ctr.numel() >= B, "ctr too short")
+    if out is None:
+        out = torch.empty((B, 8), dtype=torch.float32, device=logits.device)
+    _req(out.dtype == torch.float32 and out.shape == (B, 8) and out.is_contiguous(), "stats must be fp32 [B, 8]")
+    _check(lib().da_sample_partial(_ptr(logits), B, V, logits.stride(0), int(v0), float(temperature),
+                                   seed & 0xffffffff, step & 0xffffffff, _ptr(ctr), _ptr(out), _stream()),
+           "sample_partial")
+    return out
+
+
+def sample_finalize(gathered, ranks: int, out_tok=None, out_lp=None, conf=None, active=None, pos=None, lens=None,
+                    hist=None, start=None, eos=()):
+    """Vocab-parallel sampling, merge side: gathered fp32 [B, ranks * 8] (every rank's stats, rank
+    order) -> the token / logprob / bookkeeping of ``sample`` on the full row."""
+    _req(gathered.is_cuda and gathered.dtype == torch.float32 and gathered.is_contiguous(), "gathered fp32")
+    B = gathered.shape[0]
+    _req(gathered.shape == (B, 8 * ranks), f"gathered must be [B, {8 * ranks}]")
+    dev = gathered.device
+    if out_tok is None:
+        out_tok = torch.empty(B, dtype=torch.int32, device=dev)
+    if out_lp is None:
+        out_lp = torch.empty(B, dtype=torch.float32, device=dev)
+    if conf is not None:
+        _req(conf.dtype == torch.float32 and conf.shape == (B, 2), "conf must be fp32 [B, 2]")
+    for t, n in ((active, "active"), (pos, "pos"), (lens, "lens"), (start, "start")):
+        if t is not None:
+            _i32(t, n); _req(t.numel() >= B, f"{n} too short")
+    hist_ld = 0
+    if hist is not None:
+        _i32(hist, "hist"); _req(hist.dim() == 2 and hist.shape[0] >= B, "hist [B, n]")
+        _req(pos is not None and start is not None, "hist needs pos and start")
+        hist_ld = hist.shape[1]
+    e = list(eos)[:4] + [-1] * (4 - min(4, len(eos)))
+    _check(lib().da_sample_finalize(_ptr(gathered), B, ranks, _ptr(out_tok), _ptr(out_lp), _ptr(conf), _ptr(active),
+                                    _ptr(pos), _ptr(lens), _ptr(hist), _ptr(start), hist_ld, e[0], e[1], e[2], e[3],
+                                    _stream()), "sample_finalize")
     return out_tok, out_lp
 
 

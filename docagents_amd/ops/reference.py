@@ -215,31 +215,56 @@ def log_softmax_rows(logits):
     return torch.log_softmax(logits.float(), dim=-1)
 
 
-def sample(logits, temperature, seed, step=0, out_tok=None, out_lp=None, conf=None, active=None, ctr=None,
-           pos=None, lens=None, hist=None, start=None, eos=()):
-    """Reference sampler with the kernel's bookkeeping semantics. Greedy when temperature <= 0;
-    otherwise torch multinomial (a different RNG stream than the kernel's hash RNG, so only greedy
-    is bit-comparable)."""
-    B = logits.shape[0]
-    lp = log_softmax_rows(logits)
-    if temperature > 0:
-        g = torch.Generator(device="cpu").manual_seed((seed * 1000003 + step) & 0x7FFFFFFF)
-        probs = torch.softmax(logits.float().cpu() / temperature, -1)
-        tok = torch.multinomial(probs, 1, generator=g).squeeze(1).to(logits.device)
-    else:
-        tok = logits.float().argmax(-1)
-    chosen = lp.gather(1, tok.view(-1, 1)).squeeze(1)
-    tok = tok.int()
-    on = active.bool().clone() if active is not None else torch.ones(B, dtype=torch.bool, device=logits.device)
+_M32 = 0xFFFFFFFF
+
+
+def _mul32(x, c: int):
+    """(x * c) mod 2^32 for int64 tensors holding uint32 values (split so nothing overflows)."""
+    return (x * (c & 0xFFFF) + (((x * (c >> 16)) & 0xFFFF) << 16)) & _M32
+
+
+def _hash_u32(x):
+    x = x ^ (x >> 16)
+    x = _mul32(x, 0x7feb352d)
+    x = x ^ (x >> 15)
+    x = _mul32(x, 0x846ca68b)
+    return x ^ (x >> 16)
+
+
+def gumbel_u01(seed: int, rkey, v):
+    """The sampler kernel's counter-based uniform (common.h u01(seed, rkey, v)), bit-exact in int64."""
+    inner = _hash_u32((v + 0x632be5ab) & _M32)
+    h = _hash_u32((seed & _M32) ^ _hash_u32((rkey + _mul32(inner, 0x9e3779b9)) & _M32))
+    return ((h >> 8).double() + 0.5) * (1.0 / 16777216.0)
+
+
+def _gumbel_scores(x, temperature, seed, rkeys, v0=0):
+    """x fp32 [B, V] -> Gumbel-max scores x / T - log(-log u(seed, rkey_b, v0 + v)) (T <= 0: x)."""
+    if temperature <= 0:
+        return x.double()
+    B, V = x.shape
+    v = torch.arange(v0, v0 + V, dtype=torch.int64).view(1, V)
+    u = gumbel_u01(seed, rkeys.view(B, 1).to(torch.int64), v)
+    return x.double().cpu() / temperature - torch.log(-torch.log(u))
+
+
+def _rkeys(B, step, ctr):
+    rs = (ctr.to(torch.int64).cpu() & _M32) if ctr is not None else torch.full((B,), step & _M32, dtype=torch.int64)
+    return (_mul32(rs[:B], 131071) + torch.arange(B, dtype=torch.int64)) & _M32
+
+
+def _bookkeep(B, tok, chosen, device, out_tok=None, out_lp=None, conf=None, active=None, pos=None, lens=None,
+              hist=None, start=None, eos=()):
+    on = active.bool().clone() if active is not None else torch.ones(B, dtype=torch.bool, device=device)
     if out_tok is None:
-        out_tok = torch.zeros(B, dtype=torch.int32, device=logits.device)
+        out_tok = torch.zeros(B, dtype=torch.int32, device=device)
     out_tok.copy_(torch.where(on, tok, out_tok))
     if out_lp is not None:
         out_lp.copy_(torch.where(on, chosen, out_lp))
     if conf is not None:
         conf[:, 0] += torch.where(on, chosen.exp(), torch.zeros_like(chosen))
         conf[:, 1] += on.float()
-    stop = torch.zeros(B, dtype=torch.bool, device=logits.device)
+    stop = torch.zeros(B, dtype=torch.bool, device=device)
     for e in list(eos)[:4]:
         stop |= tok == e
     if hist is not None:
@@ -255,6 +280,57 @@ def sample(logits, temperature, seed, step=0, out_tok=None, out_lp=None, conf=No
     if active is not None:
         active.copy_(torch.where(on & stop, torch.zeros_like(active), active))
     return out_tok, chosen
+
+
+def sample(logits, temperature, seed, step=0, out_tok=None, out_lp=None, conf=None, active=None, ctr=None,
+           pos=None, lens=None, hist=None, start=None, eos=()):
+    """Reference sampler with the kernel's semantics: Gumbel-max at temperature T with the kernel's
+    counter-based hash noise (greedy when T <= 0; ties to the lower index), the chosen token's
+    log-probability under the untempered distribution, and the device-side bookkeeping."""
+    B = logits.shape[0]
+    lp = log_softmax_rows(logits)
+    sc = _gumbel_scores(logits.float().cpu(), temperature, seed, _rkeys(B, step, ctr))
+    tok = sc.argmax(-1).to(logits.device)  # first maximal index = the kernel's lower-index tie rule
+    chosen = lp.gather(1, tok.view(-1, 1)).squeeze(1)
+    return _bookkeep(B, tok.int(), chosen, logits.device, out_tok, out_lp, conf, active, pos, lens, hist, start, eos)
+
+
+def sample_partial(logits, temperature, seed, v0, step=0, ctr=None, out=None):
+    """Vocab-parallel sampling, rank side (see ops.kernels.sample_partial): stats fp32 [B, 8]."""
+    B, V = logits.shape
+    x = logits.float().cpu()
+    sc = _gumbel_scores(x, temperature, seed, _rkeys(B, step, ctr), v0)
+    bi = sc.argmax(-1)
+    mx = x.max(-1).values
+    st = torch.zeros((B, 8), dtype=torch.float32)
+    st[:, 0] = sc.gather(1, bi.view(-1, 1)).squeeze(1).float()
+    st[:, 1] = (bi + v0).to(torch.int32).view(torch.float32)
+    st[:, 2] = mx
+    st[:, 3] = torch.exp(x - mx[:, None]).sum(-1)
+    st[:, 4] = x.gather(1, bi.view(-1, 1)).squeeze(1)
+    st = st.to(logits.device)
+    if out is not None:
+        out.copy_(st)
+        return out
+    return st
+
+
+def sample_finalize(gathered, ranks, out_tok=None, out_lp=None, conf=None, active=None, pos=None, lens=None,
+                    hist=None, start=None, eos=()):
+    """Vocab-parallel sampling, merge side: gathered [B, ranks * 8] -> sample()'s outputs."""
+    B = gathered.shape[0]
+    g = gathered.float().cpu().view(B, ranks, 8)
+    score, idx = g[..., 0], g[..., 1].contiguous().view(torch.int32).long()
+    best = score.max(-1).values
+    cand = torch.where(score == best[:, None], idx, torch.full_like(idx, 1 << 40))
+    r = cand.argmin(-1)  # max score, ties to the lower global index
+    tok = idx.gather(1, r.view(-1, 1)).squeeze(1)
+    xb = g[..., 4].gather(1, r.view(-1, 1)).squeeze(1).double()
+    gmax = g[..., 2].max(-1).values.double()
+    lse = gmax + torch.log((g[..., 3].double() * torch.exp(g[..., 2].double() - gmax[:, None])).sum(-1))
+    chosen = (xb - lse).float().to(gathered.device)
+    return _bookkeep(B, tok.int().to(gathered.device), chosen, gathered.device, out_tok, out_lp, conf, active, pos,
+                     lens, hist, start, eos)
 
 
 def topk_dense(X, Qv, K, thr, slots=None, bitmap=None, **_):

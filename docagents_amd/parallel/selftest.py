@@ -116,6 +116,43 @@ def check_tp_decoder_wrong_order(rank, world, port, out_path):
     check_tp_decoder(rank, world, port, out_path, wrong_order=True)
 
 
+def check_distributed_sampling(rank, world, port, out_path):
+    """C4: sampling over a vocab-parallel LM head (each rank: its [B, V/t] slice -> 8-float row
+    summaries -> one all-gather -> finalize) == the sampler on the full rows: same tokens, same
+    logprobs (to fp32 rounding of the log-sum-exp regrouping), same bookkeeping (pos / hist / conf /
+    active), greedy and at T = 0.2 / 1.0, on every rank."""
+    _init(rank, world, port)
+    from ..models.llama import TPContext, tp_sample
+    from ..ops import reference as R
+    B, V = 6, 32064 // 8 * 8
+    g = torch.Generator().manual_seed(11)
+    logits = (torch.randn(B, V, generator=g) * 3).bfloat16()
+    logits[0, 5] = logits[0, V - 3] = 40.0  # an exact tie across ranks: the lower index must win
+    tp = TPContext(rank, world, None)
+    Vl = V // world
+    ok, worst = True, 0.0
+    for T in (0.0, 0.2, 1.0):
+        def state():
+            return dict(out_tok=torch.zeros(B, dtype=torch.int32), out_lp=torch.zeros(B),
+                        conf=torch.zeros(B, 2), active=torch.tensor([1, 1, 1, 0, 1, 1], dtype=torch.int32),
+                        pos=torch.arange(B, dtype=torch.int32) + 100, lens=torch.arange(B, dtype=torch.int32) + 101,
+                        hist=torch.full((B, 4), -1, dtype=torch.int32), start=torch.full((B,), 99, dtype=torch.int32))
+        a, b = state(), state()
+        R.sample(logits, T, 7, 0, ctr=a["pos"], eos=(3,), **a)
+        tp_sample(R, tp, logits[:, rank * Vl:(rank + 1) * Vl].contiguous(), T, 7, 0, ctr=b["pos"], eos=(3,), **b)
+        for k in a:
+            if k in ("out_lp", "conf"):
+                err = float((a[k] - b[k]).abs().max())
+                worst = max(worst, err)
+                ok &= err < 1e-4
+            else:
+                ok &= bool(torch.equal(a[k], b[k]))
+        ok &= int(a["out_tok"][0]) == 5 if T == 0.0 else True
+    oks = [None] * world
+    dist.all_gather_object(oks, (ok, worst))
+    _done(rank, out_path, {"ok": all(o for o, _ in oks), "max_lp_err": max(w for _, w in oks)})
+
+
 def check_sharded_index(rank, world, port, out_path):
     _init(rank, world, port)
     from ..index.flat import FlatIndex
@@ -310,6 +347,79 @@ def check_xgmi_allreduce(rank, world, port, out_path):
     ar.check()
     verdict["calls"] = ar.calls
     ar.close()
+    _done(rank, out_path, verdict)
+
+
+def check_xgmi_allreduce_norm(rank, world, port, out_path):
+    """C3 with the RMSNorm in the all-reduce's epilogue (one launch) vs the all-reduce kernel
+    followed by the rmsnorm kernel: x and h must be BIT-identical, for several row widths / row
+    counts, gamma given or unit, eager and HIP-graph replay. GPU ranks (may share one GPU)."""
+    _init(rank, world, port)
+    from ..ops import kernels as K
+    from .xgmi_allreduce import XgmiAllReduce
+    dev = torch.device("cuda", rank % torch.cuda.device_count())
+    torch.cuda.set_device(dev)
+    plain = XgmiAllReduce(None, dev, max_bytes=8 << 20)
+    verdict = {"cases": [], "ok": True}
+    salt = 0
+    for D in (256, 3072, 8192):
+        fused = XgmiAllReduce(None, dev, max_bytes=512 << 10)  # one row width per instance
+        for rows in (1, 4, 31):
+            if rows * D * 2 > (512 << 10):
+                continue
+            for with_gamma in (False, True):
+                salt += 1
+                g = torch.Generator().manual_seed(salt)
+                xs = [torch.randn(rows, D, generator=g).bfloat16() for _ in range(world)]
+                gamma = (torch.rand(D, generator=g) + 0.5).bfloat16().to(dev) if with_gamma else None
+                x1 = xs[rank].to(dev)
+                h1 = torch.empty_like(x1)
+                fused.all_reduce_rmsnorm_(x1, gamma, 1e-5, h1)
+                x2 = xs[rank].to(dev)
+                plain.all_reduce_(x2)
+                h2 = K.rmsnorm(x2, gamma if gamma is not None else torch.ones(D, dtype=torch.bfloat16, device=dev),
+                               1e-5)
+                torch.cuda.synchronize()
+                ok = bool(torch.equal(x1, x2) and torch.equal(h1, h2))
+                verdict["cases"].append({"D": D, "rows": rows, "gamma": with_gamma, "ok": ok,
+                                         "max_h_err": float((h1.float() - h2.float()).abs().max())})
+                verdict["ok"] &= ok
+        if D == 3072:  # graph capture of two fused calls, replayed with fresh inputs
+            x = torch.zeros(4, D, dtype=torch.bfloat16, device=dev)
+            h = torch.empty_like(x)
+            s_ = torch.cuda.Stream()
+            s_.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(s_):
+                fused.all_reduce_rmsnorm_(x, None, 1e-5, h)
+            torch.cuda.current_stream().wait_stream(s_)
+            torch.cuda.synchronize()
+            graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(graph):
+                fused.all_reduce_rmsnorm_(x, None, 1e-5, h)
+                fused.all_reduce_rmsnorm_(x, None, 1e-5, h)
+            for rep in range(2):
+                salt += 1
+                g = torch.Generator().manual_seed(salt)
+                xs = [torch.randn(4, D, generator=g).bfloat16() for _ in range(world)]
+                x.copy_(xs[rank].to(dev))
+                graph.replay()
+                torch.cuda.synchronize()
+                acc = torch.zeros(4, D)
+                for xx in xs:
+                    acc += xx.float()
+                once = acc.bfloat16()  # first call: the sum; second: world x the sum
+                acc2 = torch.zeros(4, D)
+                for _ in range(world):
+                    acc2 += once.float()
+                want = acc2.bfloat16().to(dev)
+                hw = K.rmsnorm(want, torch.ones(D, dtype=torch.bfloat16, device=dev), 1e-5)
+                ok = bool(torch.equal(x, want) and torch.equal(h, hw))
+                verdict["cases"].append({"D": D, "graph_replay": rep, "ok": ok})
+                verdict["ok"] &= ok
+        fused.check()
+        fused.close()
+    plain.check()
+    plain.close()
     _done(rank, out_path, verdict)
 
 

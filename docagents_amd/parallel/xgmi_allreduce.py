@@ -43,6 +43,8 @@ def _lib():
             "da_ar_read_err": ([c_void_p, ctypes.POINTER(ctypes.c_uint)], c_int),
             "da_ar_allreduce": ([c_void_p, c_void_p, c_longlong, c_int, c_int, c_int, c_void_p, c_void_p, c_longlong,
                                  c_int, c_int, c_longlong, c_void_p], c_int),
+            "da_ar_allreduce_rmsnorm": ([c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, ctypes.c_float, c_int,
+                                         c_int, c_void_p, c_void_p, c_longlong, c_int, c_longlong, c_void_p], c_int),
         }
         for name, (argt, res) in sigs.items():
             fn = getattr(L, name)
@@ -141,6 +143,36 @@ class XgmiAllReduce:
         _ok(rc, "xgmi all-reduce launch")
         self.calls += 1
         return out
+
+    def takes_norm(self, x: torch.Tensor) -> bool:
+        """Whether ``all_reduce_rmsnorm_`` runs the fused kernel for x [rows, D] (else: the caller
+        falls back to all-reduce + rmsnorm)."""
+        if x.dim() != 2:
+            return False
+        D = x.shape[1]
+        ok = (x.is_cuda and x.dtype == torch.bfloat16 and x.is_contiguous() and D % 8 == 0 and D // 8 <= 2048
+              and 0 < x.numel() * 2 <= self.max_bytes and x.data_ptr() % 16 == 0)
+        return ok and getattr(self, "norm_width", D) == D
+
+    def all_reduce_rmsnorm_(self, x: torch.Tensor, gamma, eps: float, h_out: torch.Tensor) -> torch.Tensor:
+        """x [rows, D] <- sum over the group (in place); h_out <- RMSNorm(x) * gamma, one launch
+        (bit-identical to all_reduce_ then the rmsnorm kernel). The fused kernel partitions by whole
+        rows, so an instance serves ONE row width D (its staging parity protocol assumes a fixed
+        row -> workgroup map); TPContext keeps a dedicated instance for it."""
+        if not self.takes_norm(x):
+            raise ValueError("all_reduce_rmsnorm_: tensor not takeable (check takes_norm)")
+        self.norm_width = x.shape[1]
+        if gamma is not None:
+            K._bf16_cuda(gamma, "gamma")
+            K._req(gamma.is_contiguous() and gamma.numel() == x.shape[1], "gamma must be [D]")
+        K._req(h_out.shape == x.shape and h_out.is_contiguous() and h_out.dtype == torch.bfloat16, "bad h_out")
+        rc = _lib().da_ar_allreduce_rmsnorm(x.data_ptr(), x.data_ptr(), h_out.data_ptr(),
+                                            None if gamma is None else gamma.data_ptr(), x.shape[0], x.shape[1],
+                                            float(eps), self.rank, self.world, self._data, self._sig, self.max_bytes,
+                                            self.grid, self.timeout, torch.cuda.current_stream(x.device).cuda_stream)
+        _ok(rc, "xgmi all-reduce + rmsnorm launch")
+        self.calls += 1
+        return h_out
 
     def check(self) -> None:
         """Raise if any barrier of this communicator timed out (a peer stopped participating)."""

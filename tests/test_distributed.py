@@ -49,6 +49,13 @@ def test_tp_decoder_check_bites_on_wrong_shard_order(tmp_path):
     assert v["checked_agree"] < 0.5 * max(1, v["checked"]) or v["max_logit_diff"] > 0.05, v
 
 
+@pytest.mark.parametrize("world", [2, 8])
+def test_distributed_sampling_matches_full_row_sampler(tmp_path, world):
+    """vocab-parallel sampling (8 floats per row exchanged, not the logits)."""
+    v = _run(selftest.check_distributed_sampling, world, tmp_path)
+    assert v["ok"], v
+
+
 @pytest.mark.parametrize("world", [2, 4, 8])
 def test_sharded_index_exact(tmp_path, world):
     assert _run(selftest.check_sharded_index, world, tmp_path)["exact"]

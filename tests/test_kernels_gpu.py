@@ -312,6 +312,54 @@ def test_sample_temperature_distribution():
     assert (counts - p).abs().max() < 0.03
 
 
+def test_sample_kernel_rng_matches_reference():
+    """The reference sampler reproduces the kernel's counter-based Gumbel noise (bit-exact uniforms;
+    fp32 vs fp64 logs can only flip near-ties), so sampled tokens are comparable at T > 0 too."""
+    torch.manual_seed(1)
+    B, V = 64, 32064
+    logits = _rand(B, V, scale=3.0)
+    ctr = torch.arange(B, dtype=torch.int32, device=DEV) * 7 + 300
+    tok, lp = K.sample(logits, 0.2, 4242, 0, ctr=ctr.clone())
+    rtok, rlp = R.sample(logits, 0.2, 4242, 0, ctr=ctr.clone())
+    assert (tok.cpu() == rtok.cpu()).float().mean() >= 0.95
+    same = tok.cpu() == rtok.cpu()
+    _close(lp.cpu()[same], rlp.cpu()[same], atol=2e-3)
+
+
+@pytest.mark.parametrize("T", [0.0, 0.2, 1.0])
+@pytest.mark.parametrize("ranks", [2, 8])
+def test_sample_partial_finalize_matches_full_row(T, ranks):
+    """Vocab-parallel sampling: per-slice 8-float summaries + finalize == the
+    sampler on the full rows (tokens, logprobs, bookkeeping), including a tie across slices."""
+    torch.manual_seed(ranks)
+    B, V = 48, 128256
+    Vl = V // ranks
+    logits = _rand(B, V, scale=3.0)
+    logits[0, 11] = logits[0, V - 2] = 60.0
+
+    def state():
+        return dict(out_tok=torch.zeros(B, dtype=torch.int32, device=DEV), out_lp=torch.zeros(B, device=DEV),
+                    conf=torch.zeros(B, 2, device=DEV),
+                    active=(torch.arange(B, device=DEV) % 7 != 3).int(),
+                    pos=torch.arange(B, dtype=torch.int32, device=DEV) + 50,
+                    lens=torch.arange(B, dtype=torch.int32, device=DEV) + 51,
+                    hist=torch.full((B, 8), -1, dtype=torch.int32, device=DEV),
+                    start=torch.full((B,), 49, dtype=torch.int32, device=DEV))
+    a, b = state(), state()
+    K.sample(logits, T, 77, 0, ctr=a["pos"], eos=(5,), **a)
+    stats = torch.cat([K.sample_partial(logits[:, r * Vl:(r + 1) * Vl].contiguous(), T, 77, r * Vl, ctr=b["pos"])
+                       for r in range(ranks)], dim=1).contiguous()
+    K.sample_finalize(stats, ranks, eos=(5,), **b)
+    torch.cuda.synchronize()
+    for k in a:
+        if k in ("out_lp", "conf"):
+            _close(a[k], b[k], atol=1e-4)
+        else:
+            assert torch.equal(a[k], b[k]), k
+    if T == 0.0:
+        assert int(b["out_tok"][0]) == 11
+
+
 @pytest.mark.parametrize("N,d,Q,Kk", [(1000, 768, 5, 5), (5000, 1024, 37, 20), (63, 768, 1, 3), (20000, 768, 16, 1)])
 def test_topk_dense(N, d, Q, Kk):
     torch.manual_seed(N)

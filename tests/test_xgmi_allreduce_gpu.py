@@ -29,6 +29,16 @@ def test_xgmi_allreduce_matches_rank_order_sum(tmp_path):
     assert v["calls"] >= 15
 
 
+def test_xgmi_allreduce_rmsnorm_bit_identical_to_unfused(tmp_path):
+    """Fused all-reduce + RMSNorm epilogue == all-reduce kernel then rmsnorm kernel, bit for bit."""
+    out = tmp_path / "arn.json"
+    mp.spawn(selftest.check_xgmi_allreduce_norm, args=(2, _port(), str(out)), nprocs=2, join=True)
+    v = json.loads(out.read_text())
+    bad = [c for c in v["cases"] if not c["ok"]]
+    assert v["ok"] and not bad, bad
+    assert len(v["cases"]) >= 12
+
+
 def _tp_ok(v) -> bool:
     return (v["max_logit_diff"] < 0.05 and v["checked"] >= 0.6 * v["decisions"]
             and v["checked_agree"] == v["checked"] and all(v["prefix_ok"]) and v["max_prob_diff"] < 1e-3)
