@@ -20,7 +20,8 @@ import numpy as np
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-from docagents_amd.engine.generator import Generator, h2d  # noqa: E402
+from docagents_amd.engine.generator import Generator  # noqa: E402
+from docagents_amd.ops import h2d  # noqa: E402
 from docagents_amd.models.configs import decoder_config  # noqa: E402
 from docagents_amd.models.llama import DecodeState, LlamaDecoder  # noqa: E402
 from docagents_amd.ops import kernels as K  # noqa: E402

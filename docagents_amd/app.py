@@ -55,9 +55,9 @@ def local_engine(cfg: Config):
 
 async def engine_client(cfg: Config, deps: Deps):
     if deps.engine_client is None:
-        from .engine.rpc import EngineClient
+        from .engine.rpc import EngineCluster
         url = cfg.engine_url or "tcp://127.0.0.1:9090"
-        deps.engine_client = await EngineClient(url).connect(retries=40, delay=0.25)
+        deps.engine_client = await EngineCluster(url).connect(retries=40, delay=0.25)
     return deps.engine_client
 
 

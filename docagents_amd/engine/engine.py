@@ -22,6 +22,7 @@ from ..models.bert import BertEncoder, pack_for_encoder
 from ..models.configs import decoder_config, encoder_config
 from ..models.llama import LlamaDecoder, TPContext
 from ..models.tokenizer import ChatFormat, decoder_tokenizer, encoder_tokenizer
+from ..ops import h2d
 from ..text.preprocess import extract_summary, preprocess_text
 from . import prompts as P
 from .generator import Generator
@@ -35,7 +36,8 @@ class Engine:
                  use_graphs: bool = True, embed_max_tokens: int = 65536, enc_dtype: str = "bf16",
                  share_prefix: bool = True):
         self.device = torch.device(device)
-        self.lock = threading.RLock()
+        self.lock = threading.RLock()      # the decoder / generator (one GPU thread drives it)
+        self.enc_lock = threading.RLock()  # the encoder: the fast embed lane and the batcher share it
         self.enc_cfg = encoder_config(embed_arch)
         self.dec_cfg = decoder_config(llm_arch)
         self.enc_tok = encoder_tokenizer(self.enc_cfg.vocab)
@@ -85,7 +87,7 @@ class Engine:
             metrics.ENGINE_EMBED_TRUNCATED.labels("texts").inc(self.stats["embed_truncated_texts"] - trunc0[0])
             metrics.ENGINE_EMBED_TRUNCATED.labels("tokens").inc(self.stats["embed_truncated_tokens"] - trunc0[1])
         order = np.argsort([-len(s) for s in seqs], kind="stable")
-        with self.lock:
+        with self.enc_lock:
             i = 0
             while i < n:
                 j, tot = i, 0
@@ -94,7 +96,7 @@ class Engine:
                     j += 1
                 idx = order[i:j]
                 vec = self.encoder.encode_packed([seqs[k] for k in idx])
-                out[torch.from_numpy(idx).to(self.device)] = vec.to(out_dtype)
+                out[h2d(idx, self.device)] = vec.to(out_dtype)
                 self.stats["embed_tokens"] += tot
                 i = j
         self.stats["embed_texts"] += n

@@ -18,18 +18,7 @@ import numpy as np
 import torch
 
 from ..models.llama import DecodeState, LlamaDecoder, pack_prompts
-
-
-def h2d(a, dev) -> torch.Tensor:
-    """Host array -> device tensor without blocking the host: the array is staged in PyTorch's
-    cached pinned-host allocator (which records the copy's stream, so the block is not reused
-    before the copy ran). A pageable-memory copy would make the host wait for the current
-    stream to drain first: fatal for the pipelined path, whose host issues one lane's work while
-    the other lane is still busy."""
-    t = torch.from_numpy(np.ascontiguousarray(a))
-    if dev.type != "cuda":
-        return t.to(dev)
-    return t.pin_memory().to(dev, non_blocking=True)
+from ..ops import h2d
 
 
 def _bucket(n: int) -> int:

@@ -139,3 +139,101 @@ class EngineClient:
         if self.writer:
             self.writer.close()
             self.writer = None
+
+
+def _owner(doc_id: str, world: int) -> int:
+    from .server import owner_of
+    return owner_of(doc_id, world)
+
+
+class EngineCluster:
+    """Client of a replicated engine (``TP_SIZE`` < world): one ``EngineClient`` per replica.
+
+    ``connect`` reaches the configured URL (replica 0), asks it for the topology and connects to
+    every replica. ``call`` keeps the single-client interface:
+      * index mutations (``index_add``, ``embed_index``, ``index_remove``) go to the replica that
+        owns the document's shard (rank hash(doc_id) % world — the engine rejects misrouted ones);
+      * ``index_docs`` / ``stats`` / ``checkpoint`` / ``ping`` fan out to every replica and merge;
+      * everything else (embed, embed_search, search, answer, summarize) goes to the replica with
+        the fewest calls in flight — the reference's queue-group load balancing
+        (internal/queue/nats.go:40-51) for the GPU engine.
+    A one-replica engine behaves exactly like a plain ``EngineClient``."""
+
+    ROUTED = ("index_add", "embed_index", "index_remove")
+    FANOUT = ("index_docs", "stats", "checkpoint", "ping")
+
+    def __init__(self, url: str, timeout: float = 120.0):
+        self.url, self.timeout = url, timeout
+        self.clients: list[EngineClient] = []
+        self.inflight: list[int] = []
+        self.topology: dict = {"replicas": 1, "tp": 1, "world": 1}
+        self._rr = 0
+
+    async def connect(self, retries: int = 1, delay: float = 0.5):
+        first = await EngineClient(self.url, self.timeout).connect(retries, delay)
+        try:
+            topo = await first.call("topology")
+        except RPCError:  # an engine without the topology RPC: a single replica
+            topo = {"replicas": 1, "tp": 1, "world": 1, "urls": [self.url]}
+        self.topology = topo
+        self.clients = [first]
+        kind, addr = parse_url(self.url)
+        for r in range(1, int(topo.get("replicas", 1))):
+            u = topo["urls"][r]
+            if kind == "tcp":  # reach the other replicas on the host this client used for replica 0
+                _, (_, port) = parse_url(u)
+                u = f"tcp://{addr[0]}:{port}"
+            self.clients.append(await EngineClient(u, self.timeout).connect(retries, delay))
+        self.inflight = [0] * len(self.clients)
+        return self
+
+    @property
+    def replicas(self) -> int:
+        return len(self.clients)
+
+    def replica_of(self, doc_id: str) -> int:
+        return _owner(str(doc_id), int(self.topology.get("world", 1))) // int(self.topology.get("tp", 1))
+
+    def _pick(self) -> int:
+        n = len(self.clients)
+        best = min(range(n), key=lambda i: (self.inflight[i], (i - self._rr) % n))
+        self._rr = (best + 1) % n
+        return best
+
+    async def _on(self, i: int, method: str, trace: str, args: dict):
+        self.inflight[i] += 1
+        try:
+            return await self.clients[i].call(method, trace=trace, **args)
+        finally:
+            self.inflight[i] -= 1
+
+    async def call(self, method: str, trace: str = "", **args):
+        if self.writer_missing():
+            await self.connect()
+        if len(self.clients) == 1:
+            return await self._on(0, method, trace, args)
+        if method in self.ROUTED:
+            doc = args["doc_id"] if "doc_id" in args else args["items"][0][0]
+            return await self._on(self.replica_of(doc), method, trace, args)
+        if method in self.FANOUT:
+            parts = await asyncio.gather(*[self._on(i, method, trace, args) for i in range(len(self.clients))])
+            if method == "index_docs":
+                merged: dict = {}
+                for p in parts:
+                    for d, n in p.items():
+                        merged[d] = merged.get(d, 0) + n
+                return merged
+            if method == "checkpoint":
+                return sum(parts)
+            if method == "ping":
+                return [r for p in parts for r in p]
+            return {"replicas": parts}
+        return await self._on(self._pick(), method, trace, args)
+
+    def writer_missing(self) -> bool:
+        return not self.clients
+
+    async def close(self):
+        for c in self.clients:
+            await c.close()
+        self.clients = []

@@ -1,15 +1,20 @@
-"""Engine server: owns the GPU(s); serves embed / summarize / answer / index RPCs to the agents.
+"""Engine server: owns the GPU(s); serves embed / summarize / answer / search / index RPCs.
 
 Micro-batching: every method has a queue; while the GPU executes one batch, newly arriving
 requests accumulate and are run together as the next batch (one encoder launch for all queued
-embeddings, one ``Generator.generate`` for all queued answers/summaries). This is the cross-request
+embeddings; answers and summaries join a continuous decode scheduler). This is the cross-request
 batching the reference cannot do (it issues one OpenAI call per request).
 
-Multi-GPU (``torchrun --nproc-per-node N``): rank 0 serves RPCs and drives the group; ranks 1..N-1
-run ``follower_loop``. A command is broadcast as a small object over a gloo group; bulk work is
-split data-parallel (each rank embeds / generates a slice, results gathered to rank 0); the vector
-index is sharded (documents routed to rank = hash(doc_id) % N, inserts stay local to the owner's
-HBM, searches fan out with the query matrix broadcast over RCCL and top-k merged on rank 0).
+Three lanes per replica, each a thread with its own HIP stream, so latency-critical work never
+queues behind a decode tick or an admission prefill:
+  * the GPU thread: the continuous scheduler's ticks, summaries, ingest embeds, index mutations;
+  * the fast lane: query-sized embeds (the question of ``embed`` / ``embed_search``), on a
+    high-priority stream with its own kernel workspace;
+  * the search plane (parallel/search_plane.py): sharded top-k rounds across every rank.
+
+Multi-GPU (``torchrun --nproc-per-node N``, TP_SIZE = t): N / t independent replicas, replica r =
+ranks [r t, (r + 1) t) served by its leader on port base + r (``EngineGroup``); the vector index is
+sharded over all N ranks (documents routed to rank = hash(doc_id) % N).
 """
 from __future__ import annotations
 
@@ -33,14 +38,41 @@ def owner_of(doc_id: str, world: int) -> int:
 
 
 class EngineGroup:
-    """Executes engine commands on one rank or on all ranks of a torch.distributed group."""
+    """The ranks of ONE engine replica (a tensor-parallel group of ``tp_size`` ranks; one rank when
+    the decoder is not sharded) executing engine commands.
 
-    def __init__(self, engine, rank: int = 0, world: int = 1, ctrl_group=None, data_group=None, shard_log=None):
+    Replicas are independent, like the reference's agent replicas (docker-compose.yml:84-85,105-106):
+    each leader serves its own RPC endpoint with its own micro-batchers and continuous scheduler, and
+    no command crosses replicas — decode ticks, admissions, embeds and ingest never wait for another
+    replica. Within a replica the leader broadcasts each command to its TP followers over a gloo
+    group (the TP ranks step one decoder together). The only cross-replica traffic is the sharded
+    search (parallel/search_plane.py, its own thread and stream on every rank) and ingest routing:
+    a document's vectors live on rank ``owner_of(doc_id, world)``, and clients send its index
+    mutations to that rank's replica (``EngineCluster.call``)."""
+
+    def __init__(self, engine, rank: int = 0, world: int = 1, ctrl_group=None, data_group=None, shard_log=None,
+                 tp_size: int = 1, plane=None):
         self.engine, self.rank, self.world = engine, rank, world
         self.ctrl_group, self.data_group = ctrl_group, data_group
+        self.tp_size = max(1, int(tp_size))
+        if world % self.tp_size:
+            raise ValueError(f"TP size {self.tp_size} must divide the world size {world}")
+        self.replica, self.replicas = rank // self.tp_size, world // self.tp_size
+        self.leader = self.replica * self.tp_size
+        self.is_leader = rank == self.leader
+        self.plane = plane
         # durable shard (index/wal.py): every mutation of this rank's rows is logged before it is
         # applied; None = HBM only (tests, benchmarks)
         self.shard_log = shard_log
+        self.ckpt_at = time.monotonic()
+
+    @property
+    def tensor_parallel(self) -> bool:
+        return self.tp_size > 1
+
+    def _wrote(self):
+        if self.plane is not None:
+            self.plane.note_write()
 
     def _put(self, doc_id, keys, vecs):
         """Replace ``doc_id``'s rows in this rank's shard (logged first when durable)."""
@@ -50,6 +82,7 @@ class EngineGroup:
         else:
             idx.remove_doc(doc_id)
             idx.add(doc_id, keys, vecs)
+        self._wrote()
 
     def _upsert(self, doc_id, keys, vecs):
         """Per-chunk upsert of ``doc_id``'s rows (index_add = the reference's SaveEmbeddings,
@@ -62,20 +95,31 @@ class EngineGroup:
             validate(idx, keys, vecs)
             idx.remove_keys(doc_id, keys)
             idx.add(doc_id, keys, vecs)
+        self._wrote()
 
-    # ---------------------------------------------------------------- collectives (control plane)
+    def owner(self, doc_id: str) -> int:
+        return owner_of(doc_id, self.world)
+
+    def _check_routed(self, doc_id: str) -> int:
+        o = self.owner(doc_id)
+        if o // self.tp_size != self.replica:
+            raise ValueError(f"document {doc_id} lives on rank {o} (replica {o // self.tp_size}); "
+                             f"this is replica {self.replica}: route index calls by owner (EngineCluster)")
+        return o
+
+    # ---------------------------------------------------------------- replica control plane
     def _bcast(self, obj):
-        if self.world == 1:
+        if self.tp_size == 1:
             return obj
         import torch.distributed as dist
         lst = [obj]
-        dist.broadcast_object_list(lst, src=0, group=self.ctrl_group)
+        dist.broadcast_object_list(lst, src=self.leader, group=self.ctrl_group)
         return lst[0]
 
     def _gather(self, obj):
-        """Every rank's ``obj`` (msgpack-encoded) gathered as tensors over the data group (RCCL on GPU
-        ranks): answers, summaries, stats. Embeddings and search results use typed tensor gathers."""
-        if self.world == 1:
+        """Every replica rank's ``obj`` (msgpack-encoded) gathered as tensors over the replica's data
+        group (RCCL on GPU ranks): stats, row counts."""
+        if self.tp_size == 1:
             return [obj]
         from ..parallel.dist import all_gather_bytes
         from .rpc import dumps, loads
@@ -84,73 +128,47 @@ class EngineGroup:
         metrics.ENGINE_COLLECTIVE.labels("all_gather_bytes").inc(time.perf_counter() - t0)
         return [loads(p) for p in parts]
 
+    LOCAL = ("embed",)  # leader-only commands (the encoder is not sharded)
+
     def run(self, cmd: str, args: dict):
-        """Rank 0: broadcast the command, execute collectively, return rank 0's result."""
-        if self.world > 1:
+        """Leader: broadcast the command to the replica's TP followers (when it needs them), execute."""
+        if self.tp_size > 1 and cmd not in self.LOCAL:
             self._bcast((cmd, args))
         return self.execute(cmd, args)
 
-    def follower_loop(self):
+    def follower_loop(self, on_idle=None):
         while True:
             cmd, args = self._bcast(None)
             if cmd == "shutdown":
                 return
             try:
                 self.execute(cmd, args)
-            except Exception:  # noqa: BLE001 - keep the group alive; rank 0 reports errors
+            except Exception:  # noqa: BLE001 - keep the replica alive; the leader reports errors
                 traceback.print_exc()
 
     # ---------------------------------------------------------------- commands
-    def _slice(self, n: int):
-        per = (n + self.world - 1) // self.world
-        a = min(n, self.rank * per)
-        return a, min(n, a + per)
-
     def execute(self, cmd: str, a: dict):
         e = self.engine
         if cmd == "embed":
-            texts = a["texts"]
-            lo, hi = self._slice(len(texts))
             faults.maybe_fail("engine.embed")
-            v = e.embed(texts[lo:hi], a.get("preprocess", True), out_dtype=torch.float32)
-            if self.world > 1:  # the slices as one tensor all-gather (RCCL on GPU ranks)
-                from ..parallel.dist import all_gather_padded_rows
-                t0 = time.perf_counter()
-                v = all_gather_padded_rows(v, len(texts), self.data_group)
-                metrics.ENGINE_COLLECTIVE.labels("embed_all_gather").inc(time.perf_counter() - t0)
-            return v.cpu().numpy()
+            return e.embed(a["texts"], a.get("preprocess", True), out_dtype=torch.float32).cpu().numpy()
         if cmd in ("answer", "summarize"):
+            # every TP rank of the replica runs every generation on its weight shard; the leader's
+            # result is the replica's (identical on all TP ranks)
             items = a["items"]
-            # tensor-parallel decoder: every rank runs every generation on its weight shard
-            lo, hi = (0, len(items)) if getattr(self, "tensor_parallel", False) else self._slice(len(items))
             faults.maybe_fail("engine.generate")
-            mine = items[lo:hi]
             if cmd == "summarize":
-                res = e.summarize_many(mine) if mine else []
-            else:
-                batch = [self._answer_item(it) for it in mine]
-                res = e.answer_many(batch) if batch else []
-            if getattr(self, "tensor_parallel", False):
-                return res
-            out = []
-            for r in self._gather(res):
-                out.extend(r)
-            return out
+                return e.summarize_many(items) if items else []
+            batch = [self._answer_item(it) for it in items]
+            return e.answer_many(batch) if batch else []
         if cmd == "cb_tick":
-            # continuous batching: TP ranks all run every sequence (identical schedulers); DP
-            # ranks take the new items round-robin by tag and run their own schedulers
-            tp = getattr(self, "tensor_parallel", False)
-            mine = [(t, it if "ids" in it else self._answer_item(it)) for t, it in a["items"]
-                    if tp or t % self.world == self.rank]
+            faults.maybe_delay("engine.tick")
+            mine = [(t, it if "ids" in it else self._answer_item(it)) for t, it in a["items"]]
             if mine:
                 faults.maybe_fail("engine.generate")
-            done, busy = e.cb_tick(mine, a.get("steps"))
-            if tp or self.world == 1:
-                return done, busy
-            parts = self._gather((done, busy))
-            return [d for p in parts for d in p[0]], any(p[1] for p in parts)
+            return e.cb_tick(mine, a.get("steps"))
         if cmd == "index_add":
-            if owner_of(a["doc_id"], self.world) == self.rank:
+            if self._check_routed(a["doc_id"]) == self.rank:
                 self._upsert(a["doc_id"], np.asarray(a["keys"], dtype=np.int64),
                              torch.from_numpy(np.ascontiguousarray(a["vecs"], dtype=np.float32)))
             return True
@@ -158,7 +176,9 @@ class EngineGroup:
             # ingest without a vector round trip: the owner rank of each document
             # embeds its chunks and writes the unit-norm rows straight into its HBM shard; only the
             # row counts travel back
-            mine = [it for it in a["items"] if owner_of(it[0], self.world) == self.rank]
+            for it in a["items"]:
+                self._check_routed(it[0])
+            mine = [it for it in a["items"] if self.owner(it[0]) == self.rank]
             counts = {}
             if mine:
                 faults.maybe_fail("engine.embed")
@@ -169,18 +189,18 @@ class EngineGroup:
                     self._put(doc_id, np.asarray(keys, dtype=np.int64), v[o:o + len(ts)])
                     counts[doc_id] = len(ts)
                     o += len(ts)
-            n = torch.tensor([counts.get(it[0], 0) for it in a["items"]], dtype=torch.int64)
-            if self.world > 1:  # each document has one owner: the sum is its row count
-                import torch.distributed as dist
-                dev = e.device if dist.get_backend(self.data_group) != "gloo" else torch.device("cpu")
-                n = n.to(dev)
-                dist.all_reduce(n, group=self.data_group)
-            return [int(x) for x in n.cpu().tolist()]
+            merged = {}
+            for part in self._gather(counts):
+                merged.update(part)
+            return [int(merged.get(it[0], 0)) for it in a["items"]]
         if cmd == "index_remove":
-            if self.shard_log is not None:
-                n = self.shard_log.remove(e.index, a["doc_id"])
-            else:
-                n = e.index.remove_doc(a["doc_id"])
+            n = 0
+            if self._check_routed(a["doc_id"]) == self.rank:
+                if self.shard_log is not None:
+                    n = self.shard_log.remove(e.index, a["doc_id"])
+                else:
+                    n = e.index.remove_doc(a["doc_id"])
+                self._wrote()
             return sum(self._gather(n))
         if cmd == "index_docs":
             rows = {d: en.rows for d, en in e.index.docs.items() if en.rows}
@@ -190,13 +210,17 @@ class EngineGroup:
                     merged[d] = merged.get(d, 0) + n
             return merged
         if cmd == "checkpoint":
-            if self.shard_log is not None:
+            # each rank checkpoints its own shard when its log has anything since the last one
+            if self.shard_log is not None and (a.get("force") or self.shard_log.stats["rows_since_ckpt"] > 0):
                 self.shard_log.checkpoint(e.index)
+                self.ckpt_at = time.monotonic()
             return sum(self._gather(len(e.index)))
-        if cmd == "search":
-            return self._search(a)
         if cmd == "stats":
-            return self._gather(e.describe())
+            d = e.describe()
+            d["rank"], d["replica"] = self.rank, self.replica
+            if self.plane is not None:
+                d["search_plane"] = dict(self.plane.stats, healthy=self.plane.healthy)
+            return self._gather(d)
         if cmd == "snapshot":
             from ..index.snapshot import save_index
             save_index(e.index, f"{a['path']}.shard{self.rank}")
@@ -204,6 +228,7 @@ class EngineGroup:
         if cmd == "restore":
             from ..index.snapshot import load_index
             load_index(e.index, f"{a['path']}.shard{self.rank}")
+            self._wrote()
             return len(e.index)
         if cmd == "ping":
             return self._gather(self.rank)
@@ -218,37 +243,6 @@ class EngineGroup:
             ids = [e._ids(it.get("context", ""))] if it.get("context") else []
         return it["question"], ids, it.get("quality", 0.0)
 
-    def _search(self, a):
-        e = self.engine
-        k, thr, filters = int(a["k"]), float(a["min_sim"]), a.get("filters")
-        if self.world == 1:
-            q = torch.from_numpy(np.ascontiguousarray(a["vecs"], dtype=np.float32))
-            s, rows = e.index.search(q, k, thr, filters)
-            ids = e.index.gather_ids(rows)
-            return s.cpu().numpy(), ids.cpu().numpy()
-        import torch.distributed as dist
-        dev = e.device
-        Q = self._bcast(a["vecs"].shape[0] if self.rank == 0 else None)
-        d = e.dim
-        q = (torch.from_numpy(np.ascontiguousarray(a["vecs"], dtype=np.float32)).to(dev) if self.rank == 0
-             else torch.empty((Q, d), dtype=torch.float32, device=dev))
-        dist.broadcast(q, src=0, group=self.data_group)                     # C2 (broadcast form)
-        s, rows = e.index.search(q, k, thr, filters)
-        gid = e.index.gather_ids(rows)
-        # C1: scores (fp32 bits) and ids packed into ONE int64 buffer -> one all-gather per search
-        from ..parallel.dist import all_gather_rows, pack_scores_ids, unpack_scores_ids
-        t1 = time.perf_counter()
-        P = all_gather_rows(pack_scores_ids(s, gid), self.data_group)
-        metrics.ENGINE_COLLECTIVE.labels("search_all_gather").inc(time.perf_counter() - t1)
-        S, G = unpack_scores_ids(P)
-        flatS = S.view(self.world, Q, k).permute(1, 0, 2).reshape(Q, -1)
-        flatG = G.view(self.world, Q, k).permute(1, 0, 2).reshape(Q, -1)
-        flatS = torch.where(flatG >= 0, flatS, torch.full_like(flatS, float("-inf")))
-        ms, mi = torch.sort(flatS, dim=1, descending=True, stable=True)
-        ms, mi = ms[:, :k], mi[:, :k]
-        mid = torch.where(torch.isfinite(ms), flatG.gather(1, mi), torch.full_like(mi, -1))
-        return ms.cpu().numpy(), mid.cpu().numpy()
-
 
 class EngineServer:
     """asyncio RPC front end with per-method micro-batch queues."""
@@ -258,8 +252,13 @@ class EngineServer:
     def __init__(self, group: EngineGroup, log, max_batch_items: int = 256, step_timeout_s: float = 300.0,
                  hard_timeout_s: float = 0.0, liveness_s: float = 30.0, profiler: StepProfiler | None = None,
                  continuous: bool = False, cb_steps: int = 1, checkpoint_s: float = 0.0,
-                 cb_window_s: float = 0.02):
+                 cb_window_s: float = 0.02, fast_embed_max: int = 8, urls: list[str] | None = None):
         self.group, self.log = group, log
+        self.urls = urls or []  # every replica's listen URL (topology RPC), replica order
+        # the fast lane: query-sized embeds on their own thread / high-priority stream / workspace
+        self.fast_embed_max = fast_embed_max
+        self.fast = cf.ThreadPoolExecutor(max_workers=1, thread_name_prefix="fast-embed")
+        self._fast_stream = None
         self.checkpoint_s = checkpoint_s  # periodic shard snapshots when the shard is durable (0 = off)
         self.gpu = cf.ThreadPoolExecutor(max_workers=1, thread_name_prefix="gpu")
         self.queues: dict[str, asyncio.Queue] = {}
@@ -281,8 +280,9 @@ class EngineServer:
         self._cb_futs: dict = {}
         self._cb_tag = 0
         self._cb_wake = asyncio.Event()
-        self._search_q: list = []
-        self._search_wake = asyncio.Event()
+        if group.plane is None:  # a replica always searches through a plane (one rank: a local one)
+            from ..parallel.search_plane import SearchPlane
+            group.plane = SearchPlane(group.engine.index, 0, 1, device=group.engine.device).start()
         # CPU-side work of a request (prompt tokenization) stays off the GPU thread
         self.cpu = cf.ThreadPoolExecutor(max_workers=2, thread_name_prefix="engine-cpu")
 
@@ -360,53 +360,40 @@ class EngineServer:
         metrics.ENGINE_ITEMS.labels("summarize").inc(len(texts))
         return [extract_summary(final[i]) for i in range(len(texts))]
 
-    async def _search_enqueue(self, args):
-        fut = asyncio.get_running_loop().create_future()
-        self._search_q.append((args, fut))
-        self._search_wake.set()
-        return await fut
+    def _fast_embed(self, texts, preprocess: bool) -> np.ndarray:
+        """Runs on the fast-lane thread: the encoder on a high-priority stream with its own kernel
+        workspace, so it co-runs with the GPU thread's decode tick instead of queueing behind it."""
+        e = self.group.engine
+        faults.maybe_fail("engine.embed")
+        if e.device.type != "cuda":
+            return e.embed(texts, preprocess, out_dtype=torch.float32).cpu().numpy()
+        from ..ops import kernels as K
+        if self._fast_stream is None:
+            torch.cuda.set_device(e.device)
+            self._fast_stream = torch.cuda.Stream(device=e.device, priority=-1)
+        with torch.cuda.stream(self._fast_stream), K.workspace_role("fast"):
+            return e.embed(texts, preprocess, out_dtype=torch.float32).cpu().numpy()
 
-    async def _search_loop(self):
-        """Search micro-batching: the queries that queued while the GPU thread was busy run as ONE
-        index scan per (k, min_sim) group, with per-query document filters (the index takes a
-        filter list per query row)."""
-        while True:
-            if not self._search_q:
-                self._search_wake.clear()
-                await self._search_wake.wait()
-            reqs, self._search_q = self._search_q, []
-            groups: dict = {}
-            for a, f in reqs:
-                groups.setdefault((int(a["k"]), float(a["min_sim"]), a.get("filters") is None), []).append((a, f))
-            for (k, thr, nof), g in groups.items():
-                t0 = time.perf_counter()
-                try:  # a malformed request fails its group, never the loop (later searches would hang)
-                    vecs = [np.asarray(a["vecs"], dtype=np.float32).reshape(-1, self.group.engine.dim)
-                            for a, _ in g]
-                    filters = None
-                    if not nof:
-                        filters = [flt for (a, _), v in zip(g, vecs) for flt in (a["filters"] * v.shape[0]
-                                                                                 if len(a["filters"]) == 1
-                                                                                 else a["filters"])]
-                        if len(filters) != sum(v.shape[0] for v in vecs):
-                            raise ValueError("search: one document filter per query row (or one for all rows)")
-                    s, ids = await self._gpu("search", {"vecs": np.concatenate(vecs), "k": k, "min_sim": thr,
-                                                        "filters": filters})
-                except Exception as e:  # noqa: BLE001
-                    for _, f in g:
-                        if not f.done():
-                            f.set_exception(e)
-                    continue
-                st = self.stats.setdefault("search", {"batches": 0, "items": 0, "busy_s": 0.0})
-                st["batches"] += 1
-                st["items"] += len(g)
-                st["busy_s"] += time.perf_counter() - t0
-                metrics.ENGINE_BATCH_SIZE.labels("search").observe(len(g))
-                o = 0
-                for (_, f), v in zip(g, vecs):
-                    if not f.done():
-                        f.set_result((s[o:o + v.shape[0]], ids[o:o + v.shape[0]]))
-                    o += v.shape[0]
+    async def _embed_fast(self, texts, preprocess: bool):
+        t0 = time.perf_counter()
+        v = await asyncio.get_running_loop().run_in_executor(self.fast, self._fast_embed, list(texts), preprocess)
+        st = self.stats.setdefault("embed_fast", {"batches": 0, "items": 0, "busy_s": 0.0})
+        st["batches"] += 1
+        st["items"] += len(texts)
+        st["busy_s"] += time.perf_counter() - t0
+        metrics.ENGINE_ITEMS.labels("embed").inc(len(texts))
+        return v
+
+    async def _search(self, vecs, k, min_sim, filters):
+        """Sharded top-k through the search plane (its own thread + stream on every rank)."""
+        t0 = time.perf_counter()
+        fut = self.group.plane.submit(np.asarray(vecs, dtype=np.float32), int(k), float(min_sim), filters)
+        s, ids = await asyncio.wrap_future(fut)
+        st = self.stats.setdefault("search", {"batches": 0, "items": 0, "busy_s": 0.0})
+        st["batches"] += 1
+        st["items"] += int(np.asarray(vecs).reshape(-1, self.group.engine.dim).shape[0])
+        st["busy_s"] += time.perf_counter() - t0
+        return s, ids
 
     async def _cb_loop(self):
         """Tick the decode scheduler while it has work; new answers join at the next tick."""
@@ -444,21 +431,22 @@ class EngineServer:
             metrics.ENGINE_ITEMS.labels("answer").inc(len(done))
 
     async def _checkpoint_loop(self):
-        """Periodic shard snapshot + log rotation (bounds replay time after a crash)."""
+        """Periodic shard snapshot + log rotation (bounds replay time after a crash). Every rank of
+        the replica checkpoints its own shard when its log has records since the last checkpoint
+        (removes count), whichever rank the documents hashed to."""
         while True:
             await asyncio.sleep(self.checkpoint_s)
-            if self.group.shard_log.stats["rows_since_ckpt"] == 0:
-                continue
             try:
                 await self._gpu("checkpoint", {})
             except Exception as e:  # noqa: BLE001
                 self.log.error("index checkpoint failed", "err", repr(e))
 
     async def _liveness_loop(self):
-        """C7: periodic rank-liveness all-reduce while idle (a dead follower hangs it -> watchdog)."""
+        """C7: periodic replica-liveness gather while idle (a dead TP follower hangs it -> watchdog);
+        cross-replica liveness is the search plane's round (health: ``search_plane``)."""
         while True:
             await asyncio.sleep(self.liveness_s)
-            if self._busy or self.group.world == 1:
+            if self._busy or self.group.tp_size == 1:
                 continue
             try:
                 ranks = await self._gpu("ping", {})
@@ -508,11 +496,31 @@ class EngineServer:
         return await fut
 
     async def dispatch(self, method: str, args: dict):
+        if method == "topology":
+            g = self.group
+            return {"replica": g.replica, "replicas": g.replicas, "tp": g.tp_size, "world": g.world,
+                    "urls": list(self.urls), "dim": int(g.engine.dim)}
         if method == "embed":
+            texts = list(args["texts"])
+            pre = args.get("preprocess", True)
+            if len(texts) <= self.fast_embed_max:  # the query path: the fast lane
+                return {"vecs": np.asarray(await self._embed_fast(texts, pre), dtype=np.float32)}
             # batches of the same preprocess flag only
-            key = "embed" if args.get("preprocess", True) else "embed_raw"
-            vecs = await self._enqueue(key, list(args["texts"]), args.get("preprocess", True))
+            vecs = await self._enqueue("embed" if pre else "embed_raw", texts, pre)
             return {"vecs": np.asarray(vecs, dtype=np.float32)}
+        if method == "embed_search":
+            # the query path in one call (cmd/query/main.go:87-105): embed the question on the fast
+            # lane, search every shard through the plane; the vector comes back for the embedding
+            # cache. texts: already preprocessed (the client checked they are non-empty).
+            try:
+                v = await self._embed_fast(list(args["texts"]), bool(args.get("preprocess", False)))
+            except Exception as e:  # noqa: BLE001 - the client maps the tag to the reference's message
+                raise RuntimeError(f"embed_search/embed: {e}") from e
+            try:
+                s, ids = await self._search(v, args["k"], args["min_sim"], args.get("filters"))
+            except Exception as e:  # noqa: BLE001
+                raise RuntimeError(f"embed_search/search: {e}") from e
+            return {"vecs": np.asarray(v, dtype=np.float32), "scores": s, "keys": ids}
         if method == "summarize":
             if self.continuous:
                 res = await self._cb_summarize(list(args["texts"]))
@@ -526,7 +534,7 @@ class EngineServer:
                 res = await self._enqueue("answer", list(args["items"]))
             return {"results": [[a, float(c)] for a, c in res]}
         if method == "search":
-            s, ids = await self._search_enqueue(args)
+            s, ids = await self._search(args["vecs"], args["k"], args["min_sim"], args.get("filters"))
             return {"scores": s, "keys": ids}
         if method == "embed_index":
             res = await self._enqueue("embed_index", [(str(args["doc_id"]), np.asarray(args["keys"], dtype=np.int64),
@@ -539,7 +547,9 @@ class EngineServer:
             return {"ranks": st, "batching": self.stats,
                     "exec": {k: {"n": n, "s": round(t, 4)} for k, (n, t) in self.exec_stats.items()}}
         if method == "health":
-            return dict(self.watchdog.state(), live_ranks=self.live_ranks, world=self.group.world)
+            pl = self.group.plane
+            return dict(self.watchdog.state(), live_ranks=self.live_ranks, world=self.group.world,
+                        replica=self.group.replica, search_plane=bool(pl is None or pl.healthy))
         raise ValueError(f"unknown method {method!r}")
 
     async def _client(self, reader, writer):
@@ -578,8 +588,7 @@ class EngineServer:
         self.watchdog.start()
         if self.continuous:
             self.cb_task = asyncio.ensure_future(self._cb_loop())
-        self.search_task = asyncio.ensure_future(self._search_loop())
-        if self.liveness_s > 0 and self.group.world > 1:
+        if self.liveness_s > 0 and self.group.tp_size > 1:
             self.liveness_task = asyncio.ensure_future(self._liveness_loop())
         kind, addr = parse_url(url)
         if kind == "unix":

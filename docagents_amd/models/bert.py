@@ -13,7 +13,7 @@ import math
 import numpy as np
 import torch
 
-from ..ops import get_ops
+from ..ops import get_ops, h2d
 from .configs import EncoderConfig
 
 EPI_BIAS, EPI_GELU, EPI_RESID = 1, 2, 4
@@ -141,9 +141,7 @@ class BertEncoder:
         flat = np.fromiter((t for s in seqs for t in s), dtype=np.int32, count=int(cu[-1]))
         pos = np.arange(int(cu[-1]), dtype=np.int32) - np.repeat(cu[:-1], lens)
         dev = self.device
-        ids_t = torch.from_numpy(flat).to(dev, non_blocking=True)
-        pos_t = torch.from_numpy(pos).to(dev, non_blocking=True)
-        cu_t = torch.from_numpy(cu).to(dev, non_blocking=True)
+        ids_t, pos_t, cu_t = h2d(flat, dev), h2d(pos, dev), h2d(cu, dev)
         hid = self.forward(ids_t, pos_t, cu_t, int(lens.max()))
         mode = 0 if self.cfg.pooling == "cls" else 1
         if out16 is not None:

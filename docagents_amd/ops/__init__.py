@@ -3,7 +3,21 @@
 module for CPU tensors — never a silent fallback on a GPU device."""
 from __future__ import annotations
 
+import numpy as np
 import torch
+
+
+def h2d(a, dev) -> torch.Tensor:
+    """Host array -> device tensor without blocking the host: the array is staged in PyTorch's
+    cached pinned-host allocator (which records the copy's stream, so the block is not reused
+    before the copy ran). A pageable-memory copy would make the host wait for the current stream
+    to drain first, which serialises work the host issues to several streams (the search plane,
+    the fast embed lane and the decode thread each run on a stream of their own)."""
+    t = torch.from_numpy(np.ascontiguousarray(a))
+    dev = torch.device(dev)
+    if dev.type != "cuda":
+        return t.to(dev)
+    return t.pin_memory().to(dev, non_blocking=True)
 
 
 def get_ops(device):

@@ -74,7 +74,7 @@ _SIGS = {
     "da_topk_merge": [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p],
     "da_kmeans_accum": [c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p],
     "da_sample_partial": [c_void_p, c_int, c_int, c_int, c_int, c_float, c_uint, c_uint, c_void_p, c_void_p, c_void_p],
-    "da_sample_finalize": [c_void_p, c_int, c_int] + [c_void_p] * 7 + [c_int] * 5 + [c_void_p],
+    "da_sample_finalize": [c_void_p, c_int, c_int] + [c_void_p] * 8 + [c_int] * 5 + [c_void_p],
     "da_stream_create_cumask": [c_uint, ctypes.POINTER(c_uint), ctypes.POINTER(c_void_p)],
     "da_stream_get_cumask": [c_void_p, c_uint, ctypes.POINTER(c_uint)],
     "da_stream_destroy": [c_void_p],

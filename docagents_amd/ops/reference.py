@@ -8,6 +8,7 @@ from __future__ import annotations
 
 import math
 
+import numpy as np
 import torch
 import torch.nn.functional as F
 
@@ -218,24 +219,24 @@ def log_softmax_rows(logits):
 _M32 = 0xFFFFFFFF
 
 
-def _mul32(x, c: int):
-    """(x * c) mod 2^32 for int64 tensors holding uint32 values (split so nothing overflows)."""
-    return (x * (c & 0xFFFF) + (((x * (c >> 16)) & 0xFFFF) << 16)) & _M32
+def _hash_u32(x: np.ndarray) -> np.ndarray:
+    """common.h hash_u32 on uint32 arrays (numpy uint32 arithmetic wraps mod 2^32, like the kernel)."""
+    x = x ^ (x >> np.uint32(16))
+    x = x * np.uint32(0x7feb352d)
+    x = x ^ (x >> np.uint32(15))
+    x = x * np.uint32(0x846ca68b)
+    return x ^ (x >> np.uint32(16))
 
 
-def _hash_u32(x):
-    x = x ^ (x >> 16)
-    x = _mul32(x, 0x7feb352d)
-    x = x ^ (x >> 15)
-    x = _mul32(x, 0x846ca68b)
-    return x ^ (x >> 16)
-
-
-def gumbel_u01(seed: int, rkey, v):
-    """The sampler kernel's counter-based uniform (common.h u01(seed, rkey, v)), bit-exact in int64."""
-    inner = _hash_u32((v + 0x632be5ab) & _M32)
-    h = _hash_u32((seed & _M32) ^ _hash_u32((rkey + _mul32(inner, 0x9e3779b9)) & _M32))
-    return ((h >> 8).double() + 0.5) * (1.0 / 16777216.0)
+def gumbel_u01(seed: int, rkey, v) -> np.ndarray:
+    """The sampler kernel's counter-based uniform (common.h u01(seed, rkey, v)), bit-exact; rkey and
+    v broadcast (uint32-valued integer arrays)."""
+    with np.errstate(over="ignore"):
+        rk = np.asarray(rkey, dtype=np.uint32)
+        vv = np.asarray(v, dtype=np.uint32)
+        inner = _hash_u32(vv + np.uint32(0x632be5ab))
+        h = _hash_u32(np.uint32(seed & _M32) ^ _hash_u32(rk + np.uint32(0x9e3779b9) * inner))
+    return ((h >> np.uint32(8)).astype(np.float64) + 0.5) * (1.0 / 16777216.0)
 
 
 def _gumbel_scores(x, temperature, seed, rkeys, v0=0):
@@ -243,14 +244,14 @@ def _gumbel_scores(x, temperature, seed, rkeys, v0=0):
     if temperature <= 0:
         return x.double()
     B, V = x.shape
-    v = torch.arange(v0, v0 + V, dtype=torch.int64).view(1, V)
-    u = gumbel_u01(seed, rkeys.view(B, 1).to(torch.int64), v)
-    return x.double().cpu() / temperature - torch.log(-torch.log(u))
+    u = gumbel_u01(seed, rkeys.reshape(B, 1), np.arange(v0, v0 + V, dtype=np.int64).reshape(1, V))
+    return x.double().cpu() / temperature - torch.from_numpy(np.log(-np.log(u)))
 
 
-def _rkeys(B, step, ctr):
-    rs = (ctr.to(torch.int64).cpu() & _M32) if ctr is not None else torch.full((B,), step & _M32, dtype=torch.int64)
-    return (_mul32(rs[:B], 131071) + torch.arange(B, dtype=torch.int64)) & _M32
+def _rkeys(B, step, ctr) -> np.ndarray:
+    rs = (ctr.cpu().numpy()[:B].astype(np.int64) if ctr is not None else np.full(B, step, dtype=np.int64))
+    with np.errstate(over="ignore"):
+        return rs.astype(np.uint32) * np.uint32(131071) + np.arange(B, dtype=np.uint32)
 
 
 def _bookkeep(B, tok, chosen, device, out_tok=None, out_lp=None, conf=None, active=None, pos=None, lens=None,

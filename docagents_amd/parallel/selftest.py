@@ -6,8 +6,8 @@ JSON verdict to ``out_path``.
                         lm_head + all-gather) == the unsharded decoder (prefill logits, greedy tokens)
   check_sharded_index   W-way sharded flat index (C2 all-gather queries, C1 all-gather top-k, merge)
                         == exact single-index search over all rows, with doc filters and threshold
-  check_engine_group    EngineGroup command fan-out: embed (DP), search (broadcast + gather), index
-                        routing by document owner, answer (DP generate)
+  check_replicas        independent replicas (DP or TP x DP) + the search plane: a slow replica
+                        blocks nobody, owner-routed ingest, exact sharded search, load balancing
   check_ivf_kmeans      IVFFlat with cross-shard k-means statistics all-reduce (C6)
   check_xgmi_allreduce  IPC peer-buffer all-reduce kernel == fp32 rank-order sum (GPU ranks)
   check_tp_decoder_gpu  TP=world decoder on GPU ranks (xGMI all-reduce in every layer) vs unsharded
@@ -25,6 +25,8 @@ import torch.distributed as dist
 def _init(rank, world, port):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
+    # world processes share the machine's cores: no intra-op thread oversubscription
+    torch.set_num_threads(max(1, (os.cpu_count() or 1) // world))
     dist.init_process_group("gloo", rank=rank, world_size=world)
 
 
@@ -196,49 +198,151 @@ def check_sharded_index(rank, world, port, out_path):
     _done(rank, out_path, {"exact": all(oks)})
 
 
-def check_engine_group(rank, world, port, out_path):
+def check_replicas(rank, world, port, out_path, tp: int = 1):
+    """Independent engine replicas (engine/server.py EngineGroup) + the cross-rank search plane,
+    the whole serving stack per rank as engine_main builds it: world / tp replicas, each leader an
+    RPC endpoint on base + replica, TP followers stepping with their leader, every rank one index
+    shard. Replica 1's decode ticks are slowed to 3 s each (fault hook); while one of its answers
+    is in flight, the other replicas must serve answers, embeds, searches (which need every rank's
+    shard, replica 1's included) and fused embed+search well inside that time, and ingest routed
+    by document owner must land on the owner's shard (followers included). Rank 0 drives through
+    ``EngineCluster`` (topology discovery, least-loaded balancing, owner routing)."""
+    import asyncio
+    import time as _t
     _init(rank, world, port)
     from ..engine.engine import Engine
-    from ..engine.server import EngineGroup, owner_of
-    eng = Engine("tiny-enc", "tiny-dec", "cpu", max_batch=4, max_seq=512, max_new_tokens=5, summary_max_new=5,
-                 use_graphs=False)
-    grp = EngineGroup(eng, rank, world, ctrl_group=None, data_group=None)
-    if rank != 0:
+    from ..engine.rpc import EngineClient, EngineCluster
+    from ..engine.server import EngineGroup, EngineServer, owner_of
+    from ..models.llama import TPContext
+    from ..utils import faults
+    from ..utils.log import discard
+    from .search_plane import SearchPlane
+    replicas, replica = world // tp, rank // tp
+    rep_ctrl = rep_data = None
+    for r in range(replicas):
+        ranks = list(range(r * tp, (r + 1) * tp))
+        c = dist.new_group(ranks, backend="gloo") if tp > 1 else None
+        d = dist.new_group(ranks, backend="gloo") if tp > 1 else None
+        if r == replica:
+            rep_ctrl, rep_data = c, d
+    plane_ctrl = dist.new_group(backend="gloo")
+    plane_data = dist.new_group(backend="gloo")
+    tpc = TPContext(rank % tp, tp, rep_data) if tp > 1 else None
+    eng = Engine("tiny-enc", "tiny-dec-tp8" if tp > 1 else "tiny-dec", "cpu", tp=tpc, max_batch=4, max_seq=512,
+                 max_new_tokens=4, summary_max_new=4, use_graphs=False)
+    if replica == 1:
+        faults.configure_delay({"engine.tick": float(os.environ.get("DA_TEST_SLOW_TICK", "3.0"))})
+    plane = SearchPlane(eng.index, rank, world, plane_ctrl, plane_data).start()
+    grp = EngineGroup(eng, rank, world, rep_ctrl, rep_data, tp_size=tp, plane=plane)
+    base = port + 1
+    urls = [f"tcp://127.0.0.1:{base + r}" for r in range(replicas)]
+    done_flag = out_path + ".done"
+    if not grp.is_leader:
         grp.follower_loop()
+        plane.stop()
         dist.barrier()
         dist.destroy_process_group()
         return
-    texts = [f"text number {i} about topic {i % 3}" for i in range(7)]
-    vecs = grp.run("embed", {"texts": texts})
-    solo = eng.embed(texts, out_dtype=torch.float32).numpy()
-    embed_ok = vecs.shape == (7, eng.dim) and np.allclose(vecs, solo, atol=1e-4)
-    owners = set()
-    # distinct random unit vectors for the routing check (a random-init encoder maps all texts to
-    # nearly the same direction, which would make the top-1 expectation a bf16 coin flip)
-    vecs = np.random.default_rng(3).standard_normal((7, eng.dim)).astype(np.float32)
-    vecs /= np.linalg.norm(vecs, axis=1, keepdims=True)
-    for i in range(6):
-        doc = f"doc-{i}"
-        owners.add(owner_of(doc, world))
-        grp.run("index_add", {"doc_id": doc, "keys": np.array([100 + i]), "vecs": vecs[i:i + 1]})
-    # ingest without a vector round trip: each document embedded and indexed by its owner rank
-    items = [(f"ing-{i}", np.arange(3, dtype=np.int64) + 1000 + 10 * i, [f"chunk {j} of doc {i}" for j in range(3)])
-             for i in range(4 * world)]
-    for d, _, _ in items:
-        owners.add(owner_of(d, world))
-    counts = grp.run("embed_index", {"items": items})
-    have = grp.run("index_docs", {})
-    embed_index_ok = counts == [3] * len(items) and all(have.get(d) == 3 for d, _, _ in items)
-    s, keys = grp.run("search", {"vecs": vecs[:3], "k": 2, "min_sim": -1.0, "filters": [["doc-0"], ["doc-1", "doc-2"], None]})
-    search_ok = int(keys[0][0]) == 100 and int(keys[1][0]) == 101 and int(keys[2][0]) == 102
-    res = grp.run("answer", {"items": [{"question": "q?", "context": "some context", "quality": 0.5}] * 3})
-    answer_ok = len(res) == 3 and all(0 <= c <= 0.5 + 1e-6 for _, c in res)
-    stats = grp.run("stats", {})
-    grp.run("shutdown", {}) if False else grp._bcast(("shutdown", {}))
-    verdict = {"embed_ok": bool(embed_ok), "search_ok": bool(search_ok), "answer_ok": bool(answer_ok),
-               "embed_index_ok": bool(embed_index_ok), "owners": sorted(owners), "ranks": len(stats)}
-    with open(out_path, "w") as f:
-        json.dump(verdict, f)
+
+    async def serve():
+        srv = EngineServer(grp, discard(), continuous=True, cb_window_s=0.0, urls=urls, liveness_s=0)
+        await srv.start(urls[replica])
+        if rank == 0:
+            verdict = await drive()
+            with open(out_path, "w") as f:
+                json.dump(verdict, f)
+            open(done_flag, "w").close()
+        else:
+            while not os.path.exists(done_flag):
+                await asyncio.sleep(0.05)
+        srv.server.close()
+        if tp > 1:
+            grp._bcast(("shutdown", {}))
+
+    async def drive():
+        v = {}
+        cl = await EngineCluster(urls[0]).connect(retries=200, delay=0.05)
+        v["replicas"] = cl.replicas
+        # ingest routed by owner (followers own shards too under TP)
+        docs, per = [], {}
+        i = 0
+        while len(docs) < 4 * world or min(per.get(r, 0) for r in range(world)) < 2:  # every shard owns docs
+            d = f"doc-{i}"
+            i += 1
+            o = owner_of(d, world)
+            if per.get(o, 0) < 4:
+                docs.append(d)
+                per[o] = per.get(o, 0) + 1
+        texts = {d: [f"chunk {j} of {d} about subject {i * 3 + j}" for j in range(3)] for i, d in enumerate(docs)}
+        counts = await asyncio.gather(*[cl.call("embed_index", doc_id=d, keys=np.arange(3, dtype=np.int64) + 10 * i,
+                                                texts=texts[d]) for i, d in enumerate(docs)])
+        have = await cl.call("index_docs")
+        v["ingest_ok"] = [int(r["rows"]) for r in counts] == [3] * len(docs) and all(have.get(d) == 3 for d in docs)
+        v["owners"] = sorted({owner_of(d, world) for d in docs})
+        # misrouted index mutation is rejected
+        wrong = next(d for d in docs if owner_of(d, world) // tp != 0)
+        try:
+            await cl.clients[0].call("index_add", doc_id=wrong, keys=np.array([1]),
+                                     vecs=np.ones((1, eng.dim), dtype=np.float32))
+            v["misroute_rejected"] = False
+        except Exception as e:  # noqa: BLE001
+            v["misroute_rejected"] = "route index calls by owner" in str(e)
+        # exact reference for searches: every chunk's vector (the fast-lane embed == the ingest embed)
+        allt = [t for d in docs for t in texts[d]]
+        allv = (await cl.clients[2 % cl.replicas].call("embed", texts=allt, preprocess=True))["vecs"]
+        keys = [10 * i + j for i, _ in enumerate(docs) for j in range(3)]
+        # slow replica 1: an answer that takes >= 3 s per tick
+        slow = asyncio.ensure_future(cl.clients[1].call("answer", items=[{"question": "slow?", "context": "c",
+                                                                             "quality": 1.0}]))
+        await asyncio.sleep(0.3)
+        t0 = _t.perf_counter()
+        q = allv[[1, 7]].copy()
+        flt = [[docs[0], docs[2]], docs[:]]
+        others = [r for r in range(cl.replicas) if r != 1]
+        jobs = [cl.clients[others[0]].call("search", vecs=q, filters=flt, k=4, min_sim=-1.0),
+                cl.clients[others[-1]].call("embed_search", texts=[allt[7]], filters=[docs], k=3, min_sim=-1.0),
+                cl.clients[others[-1]].call("embed", texts=["a question"], preprocess=True)]
+        jobs += [cl.clients[r].call("answer", items=[{"question": f"q{r}?", "context": "ctx", "quality": 0.5}])
+                 for r in others]
+        async def timed(j):
+            r_ = await j
+            return r_, _t.perf_counter() - t0
+        out = await asyncio.gather(*[timed(j) for j in jobs])
+        res = [r_ for r_, _ in out]
+        v["job_s"] = [round(x, 3) for _, x in out]
+        v["others_s"] = _t.perf_counter() - t0
+        v["slow_pending"] = not slow.done()
+        def matches(qv, allowed_docs, k, s_row, k_row):
+            """Exact brute-force top-k over every chunk (the random-init encoder maps all texts to
+            nearby directions, so ids may swap only where scores tie within bf16 rounding)."""
+            allowed = np.array([d in allowed_docs for d in docs for _ in range(3)])
+            sc = allv @ qv
+            idx = np.where(allowed)[0]
+            order = idx[np.lexsort((idx, -sc[idx]))][:k]
+            got = [int(x) for x in k_row if x >= 0]
+            if len(got) != len(order) or not np.allclose(np.sort(s_row[:len(got)]), np.sort(sc[order]), atol=1e-2):
+                return False
+            pos = {kk: j for j, kk in enumerate(keys)}
+            return all(abs(sc[pos[g]] - sc[order[j]]) <= 1e-2 for j, g in enumerate(got))
+        s, ks = res[0]["scores"], res[0]["keys"]
+        v["search_ok"] = bool(all(matches(q[b], flt[b], 4, s[b], ks[b]) for b in range(2)))
+        es = res[1]
+        v["embed_search_ok"] = bool(es["vecs"].shape == (1, eng.dim) and np.allclose(es["vecs"][0], allv[7], atol=1e-5)
+                                    and matches(es["vecs"][0], docs, 3, es["scores"][0], es["keys"][0]))
+        v["answers_ok"] = all(0.0 <= r["results"][0][1] <= 0.5 + 1e-6 for r in res[3:])
+        await slow
+        v["slow_done"] = True
+        # load balancing: concurrent answers spread over the replicas
+        await asyncio.gather(*[cl.call("answer", items=[{"question": f"lb{i}", "context": "c", "quality": 1.0}])
+                               for i in range(2 * cl.replicas)])
+        st = await cl.call("stats")
+        v["answered_per_replica"] = [sum(r.get("gen", {}).get("calls", 0) + r.get("sched", {}).get("admitted", 0)
+                                         for r in part["ranks"][:1]) for part in st["replicas"]]
+        await cl.close()
+        return v
+
+    asyncio.run(serve())
+    plane.stop()
     dist.barrier()
     dist.destroy_process_group()
 

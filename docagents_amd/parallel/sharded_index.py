@@ -17,6 +17,7 @@ import torch
 import torch.distributed as dist
 
 from .dist import all_gather_rows, pack_scores_ids, unpack_scores_ids
+from .search_plane import merge_shard_topk
 
 
 class ShardedIndex:
@@ -42,15 +43,7 @@ class ShardedIndex:
         S = S.reshape(self.world, self.world * B, k)
         G = G.reshape(self.world, self.world * B, k)
         mine = slice(self.rank * B, (self.rank + 1) * B)
-        S, G = S[:, mine].contiguous(), G[:, mine].contiguous()
-        # merge: candidate "ids" for the kernel are positions (shard * k + j) -> deterministic ties
-        pos = torch.arange(self.world * k, dtype=torch.int32, device=S.device).view(self.world, 1, k).expand(
-            self.world, B, k).contiguous()
-        pos = torch.where(G >= 0, pos, torch.full_like(pos, -1))
-        ms, mp = self.ops.topk_merge(S, pos, k)
-        flatG = G.permute(1, 0, 2).reshape(B, self.world * k)
-        mid = torch.where(mp >= 0, flatG.gather(1, mp.clamp_min(0).long()), torch.full_like(flatG[:, :k], -1))
-        return ms, mid
+        return merge_shard_topk(self.ops, S[:, mine].contiguous(), G[:, mine].contiguous(), k)
 
     def train(self, **kw):
         if hasattr(self.local, "train"):

@@ -2,11 +2,14 @@
 
 Multi-GPU: ``python -m torch.distributed.run --nproc-per-node 8 --master-addr 127.0.0.1 -m
 docagents_amd.services engine``. One process per GPU; RCCL ("nccl" backend) carries the data-plane
-collectives over xGMI, a gloo group carries the small control messages. Rank 0 serves the RPCs.
+collectives over xGMI, gloo groups carry the small control messages.
 
-  TP_SIZE=1 (default)  data parallel: embeddings / generations split across ranks, index sharded
-  TP_SIZE=world        the decoder is tensor-parallel across all ranks (Llama-3-70B class); every
-                       rank runs every generation on its shard, index still sharded
+  TP_SIZE=t (divides the world; default 1): world / t independent replicas. Replica r = ranks
+  [r t, (r + 1) t), served by its leader on port base + r (unix: path.r<r> for r > 0) with its own
+  micro-batchers and continuous scheduler; TP followers step the decoder with their leader. The
+  vector index is sharded over every rank and searched through the search plane (all ranks).
+  Agents connect to the base URL; ``EngineCluster`` discovers the other replicas (topology RPC),
+  load-balances generation / embedding over them and routes index calls to the owner's replica.
 Durable shards (default): ``--index-dir DIR`` (INDEX_DIR, default DATA_DIR/index) holds each rank's
 vector log + snapshot (index/wal.py); a restarted engine recovers every row it acknowledged, after
 SIGKILL too. Checkpoints every INDEX_CHECKPOINT_S seconds and on SIGTERM. INDEX_DIR=none: HBM only.
@@ -20,6 +23,17 @@ import os
 import signal
 
 import torch
+
+
+def replica_url(base: str, r: int) -> str:
+    """Listen URL of replica r: base port + r for tcp, path.r<r> for unix sockets (r > 0)."""
+    if r == 0:
+        return base
+    if base.startswith("unix://"):
+        return f"{base}.r{r}"
+    from ..engine.rpc import parse_url
+    _, (host, port) = parse_url(base)
+    return f"tcp://{host}:{port + r}"
 
 
 def main(argv=None) -> int:
@@ -39,17 +53,30 @@ def main(argv=None) -> int:
     cfg = load()
     log = new_logger(cfg.log_level)
     info = init_from_env()
-    ctrl = data = None
+    world, rank = info.world, info.rank
+    t = max(1, cfg.tp_size)
+    if world % t:
+        raise SystemExit(f"TP_SIZE={t} must divide the world size {world}")
+    replicas, replica = world // t, rank // t
+    rep_ctrl = rep_data = plane_ctrl = plane_data = None
     tp = None
-    if info.world > 1:
-        import torch.distributed as dist
-        ctrl = dist.new_group(backend="gloo")
-        data = dist.group.WORLD
-        if cfg.tp_size > 1:
-            if cfg.tp_size != info.world:
-                raise SystemExit("TP_SIZE must be 1 or the world size")
-            tp = TPContext(info.rank, info.world, data)
     dev = info.device
+    if world > 1:
+        import datetime
+
+        import torch.distributed as dist
+        # every rank creates every group, in the same order
+        for r in range(replicas):
+            ranks = list(range(r * t, (r + 1) * t))
+            c = dist.new_group(ranks, backend="gloo") if t > 1 else None
+            d = dist.new_group(ranks) if t > 1 else None
+            if r == replica:
+                rep_ctrl, rep_data = c, d
+        to = datetime.timedelta(seconds=max(60.0, cfg.engine_step_timeout))
+        plane_ctrl = dist.new_group(backend="gloo", timeout=to)
+        plane_data = dist.new_group(timeout=to)
+        if t > 1:
+            tp = TPContext(rank % t, t, rep_data)
     eng = Engine(cfg.embed_arch, cfg.llm_arch, dev, seed=cfg.seed, tp=tp, max_batch=cfg.max_batch,
                  temperature=cfg.temperature, max_new_tokens=cfg.max_new_tokens,
                  summary_max_new=cfg.summary_max_new_tokens, index_kind=cfg.index_kind, ivf_lists=cfg.ivf_lists,
@@ -61,31 +88,36 @@ def main(argv=None) -> int:
     shard_log = None
     if index_dir and index_dir != "none":
         from ..index.wal import ShardLog
-        shard_log = ShardLog(index_dir, info.rank, fsync=cfg.index_fsync)
+        shard_log = ShardLog(index_dir, rank, fsync=cfg.index_fsync)
         rec = shard_log.recover(eng.index)
-        log.info("recovered index shard", "rank", info.rank, "dir", index_dir, **rec)
-    grp = EngineGroup(eng, info.rank, info.world, ctrl, data, shard_log=shard_log)
-    grp.tensor_parallel = tp is not None
-    if a.snapshot and os.path.exists(f"{a.snapshot}.shard{info.rank}"):
+        log.info("recovered index shard", "rank", rank, "dir", index_dir, **rec)
+    if a.snapshot and os.path.exists(f"{a.snapshot}.shard{rank}"):
         from ..index.snapshot import load_index
-        n = load_index(eng.index, f"{a.snapshot}.shard{info.rank}")
-        log.info("restored index shard", "rank", info.rank, "rows", n)
-    if info.rank != 0:
+        n = load_index(eng.index, f"{a.snapshot}.shard{rank}")
+        log.info("restored index shard", "rank", rank, "rows", n)
+    from ..parallel.search_plane import SearchPlane
+    plane = SearchPlane(eng.index, rank, world, plane_ctrl, plane_data, device=dev).start()
+    grp = EngineGroup(eng, rank, world, rep_ctrl, rep_data, shard_log=shard_log, tp_size=t, plane=plane)
+    if not grp.is_leader:
         grp.follower_loop()
+        plane.stop()
+        if torch.distributed.is_initialized():
+            torch.distributed.destroy_process_group()
         return 0
+    urls = [replica_url(a.listen, r) for r in range(replicas)]
 
     async def serve():
         srv = EngineServer(grp, log, max_batch_items=cfg.max_batch * 4, step_timeout_s=cfg.engine_step_timeout,
                            hard_timeout_s=cfg.engine_hard_timeout, liveness_s=cfg.engine_liveness_s,
                            continuous=cfg.engine_continuous, cb_steps=cfg.engine_cb_steps,
-                           checkpoint_s=cfg.index_checkpoint_s)
+                           checkpoint_s=cfg.index_checkpoint_s, urls=urls)
         if cfg.engine_metrics_port:
             import prometheus_client
             prometheus_client.start_http_server(cfg.engine_metrics_port)
             log.info("engine metrics listening", "port", cfg.engine_metrics_port)
-        server = await srv.start(a.listen)
-        log.info("engine listening", "addr", a.listen, "world", info.world, "device", str(dev),
-                 "encoder", cfg.embed_arch, "decoder", cfg.llm_arch, "tp", cfg.tp_size)
+        server = await srv.start(urls[replica])
+        log.info("engine listening", "addr", urls[replica], "replica", replica, "replicas", replicas,
+                 "world", world, "device", str(dev), "encoder", cfg.embed_arch, "decoder", cfg.llm_arch, "tp", t)
         stop = asyncio.Event()
         loop = asyncio.get_running_loop()
         for sgn in (signal.SIGINT, signal.SIGTERM):
@@ -96,13 +128,14 @@ def main(argv=None) -> int:
         await stop.wait()
         server.close()
         if shard_log is not None:
-            await srv._gpu("checkpoint", {})
+            await srv._gpu("checkpoint", {"force": True})
             log.info("index checkpoint saved", "dir", index_dir)
         if a.snapshot:
             await srv._gpu("snapshot", {"path": a.snapshot})
             log.info("index snapshot saved", "path", a.snapshot)
-        if info.world > 1:
+        if t > 1:
             grp._bcast(("shutdown", {}))
+        plane.stop()
 
     asyncio.run(serve())
     if torch.distributed.is_initialized():

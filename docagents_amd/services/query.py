@@ -21,7 +21,8 @@ from ..api.http import Middleware, fail, metrics_response, write_json
 from ..api.validation import PayloadError, decode_query_request, validate_query_request
 from ..cache.cache import QueryResult, Source
 from ..cache.keys import generate_cache_key
-from ..text.preprocess import truncate_preview
+from ..providers import EmbedError
+from ..text.preprocess import preprocess_text, truncate_preview
 
 try:
     from prometheus_client import Counter, Histogram
@@ -101,6 +102,24 @@ async def query_handler(deps, body: bytes) -> Response:
     except Exception as e:  # noqa: BLE001
         log.warn("failed to get cached embedding", "err", e)
     ttl = deps.config.cache_ttl
+    results = None
+    if vec is None and getattr(deps.store, "fused_query", False) is True:
+        # embed + search in one engine call (the reference's two calls, main.go:88 + :101)
+        text = preprocess_text(req.question)
+        if not text:
+            return fail(log, "failed to embed question", EmbedError("text is empty after preprocessing"), 500)
+        t1 = time.perf_counter()
+        try:
+            vec, results = await deps.store.embed_top_k(ids, text, req.top_k)
+        except Exception as e:  # noqa: BLE001
+            # the engine tags which half failed (engine/server.py embed_search)
+            msg = "search failed" if "embed_search/search:" in str(e) else "failed to embed question"
+            return fail(log, msg, e, 500)
+        _obs("embed_search", t1)
+        try:
+            await deps.cache.set_embedding(req.question, vec, ttl)
+        except Exception as e:  # noqa: BLE001
+            log.warn("failed to cache embedding", "err", e)
     if vec is None:
         t1 = time.perf_counter()
         try:
@@ -112,12 +131,13 @@ async def query_handler(deps, body: bytes) -> Response:
             await deps.cache.set_embedding(req.question, vec, ttl)
         except Exception as e:  # noqa: BLE001
             log.warn("failed to cache embedding", "err", e)
-    t2 = time.perf_counter()
-    try:
-        results = await deps.store.top_k(ids, vec, req.top_k)
-    except Exception as e:  # noqa: BLE001
-        return fail(log, "search failed", e, 500)
-    _obs("search", t2)
+    if results is None:
+        t2 = time.perf_counter()
+        try:
+            results = await deps.store.top_k(ids, vec, req.top_k)
+        except Exception as e:  # noqa: BLE001
+            return fail(log, "search failed", e, 500)
+        _obs("search", t2)
     context = build_context(results)
     quality = calculate_avg_similarity(results)
     t3 = time.perf_counter()

@@ -233,6 +233,21 @@ class CompositeStore:
     async def top_k(self, doc_ids: list[str], vector, k: int, min_similarity: float | None = None) -> list[SearchResult]:
         thr = self.min_similarity if min_similarity is None else min_similarity
         hits = await self.vectors.search(np.asarray(vector, dtype=np.float32), list(doc_ids), k, thr)
+        return await self._results(hits)
+
+    @property
+    def fused_query(self) -> bool:
+        """Whether ``embed_top_k`` is available: the engine both embeds and holds the vectors."""
+        return self.direct_embed and hasattr(self.vectors, "embed_search")
+
+    async def embed_top_k(self, doc_ids: list[str], text: str, k: int, min_similarity: float | None = None):
+        """Embed the (preprocessed) question AND search in ONE engine call (the question vector never
+        leaves the engine between the two; cmd/query/main.go:87-105). Returns (vector, results)."""
+        thr = self.min_similarity if min_similarity is None else min_similarity
+        vec, hits = await self.vectors.embed_search(text, list(doc_ids), k, thr)
+        return vec, await self._results(hits)
+
+    async def _results(self, hits) -> list[SearchResult]:
         keys = [kk for kk, _ in hits]
         found = await self.chunks_by_keys(keys)
         sums: dict[str, Summary] = {}

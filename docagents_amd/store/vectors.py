@@ -54,6 +54,14 @@ class EngineVectors:
         keys, scores = r["keys"][0], r["scores"][0]
         return [(int(kk), float(sc)) for kk, sc in zip(keys, scores) if kk >= 0]
 
+    async def embed_search(self, text: str, doc_ids: list[str], k: int, min_sim: float):
+        """(question vector, [(chunk_key, score)]) from ONE engine RPC: the engine embeds the text on
+        its fast lane and searches every shard through the search plane."""
+        r = await self.client.call("embed_search", texts=[text], filters=[list(doc_ids)], k=int(k),
+                                   min_sim=float(min_sim), preprocess=False)
+        keys, scores = r["keys"][0], r["scores"][0]
+        return r["vecs"][0], [(int(kk), float(sc)) for kk, sc in zip(keys, scores) if kk >= 0]
+
     async def remove_doc(self, doc_id: str):
         return await self.client.call("index_remove", doc_id=doc_id)
 

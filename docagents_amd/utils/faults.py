@@ -48,6 +48,23 @@ def configure(spec: str | dict | None):
         _counts.clear()
 
 
+_delays: dict[str, float] = {}
+
+
+def configure_delay(spec: dict | None):
+    """Test hook: ``maybe_delay(site)`` sleeps ``spec[site]`` seconds (a slow replica / GPU thread)."""
+    with _lock:
+        _delays.clear()
+        _delays.update(spec or {})
+
+
+def maybe_delay(site: str):
+    d = _delays.get(site)
+    if d:
+        import time
+        time.sleep(d)
+
+
 def maybe_fail(site: str):
     spec = _load()
     if not spec:

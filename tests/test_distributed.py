@@ -61,11 +61,28 @@ def test_sharded_index_exact(tmp_path, world):
     assert _run(selftest.check_sharded_index, world, tmp_path)["exact"]
 
 
-@pytest.mark.parametrize("world", [2, 4])
-def test_engine_group_fanout(tmp_path, world):
-    v = _run(selftest.check_engine_group, world, tmp_path)
-    assert v["embed_ok"] and v["search_ok"] and v["answer_ok"] and v["embed_index_ok"], v
-    assert v["owners"] == list(range(world)) and v["ranks"] == world
+def _replicas_ok(v, world, replicas):
+    assert v["replicas"] == replicas, v
+    assert v["ingest_ok"] and v["owners"] == list(range(world)) and v["misroute_rejected"], v
+    assert v["search_ok"] and v["embed_search_ok"] and v["answers_ok"] and v["slow_done"], v
+    # replica 1 ticks once per 3 s; everything else finished while its answer was still pending
+    assert v["slow_pending"] and v["others_s"] < 2.5, v
+    assert all(n >= 1 for n in v["answered_per_replica"]), v
+
+
+def test_eight_dp_replicas_never_block_on_each_other(tmp_path):
+    """8 DP replicas (TP_SIZE=1): interleaved answer / embed / search / embed_search RPCs while one
+    replica is stuck in slow decode ticks; searches still cover every shard through the plane."""
+    _replicas_ok(_run(selftest.check_replicas, 8, tmp_path), 8, 8)
+
+
+def _check_replicas_tp2(rank, world, port, out_path):
+    selftest.check_replicas(rank, world, port, out_path, tp=2)
+
+
+def test_tp2_x_dp4_serving(tmp_path):
+    """TP=2 x DP=4: four replicas of a tensor-parallel decoder, index sharded over all 8 ranks."""
+    _replicas_ok(_run(_check_replicas_tp2, 8, tmp_path), 8, 4)
 
 
 @pytest.mark.parametrize("world", [2, 8])

@@ -173,9 +173,11 @@ def test_engine_health_and_metrics(eng):
         cl = await EngineClient(f"tcp://127.0.0.1:{port}").connect()
         await cl.call("embed", texts=["x y z"], preprocess=True)
         await cl.call("answer", items=[{"question": "q?", "context": "c", "quality": 1.0}])
-        await cl.call("stats")
+        st = await cl.call("stats")
         h = await cl.call("health")
-        assert h["ok"] is True and h["steps"] >= 3 and h["world"] == 1
+        # answer + stats ran on the GPU thread; the query-sized embed on the fast lane
+        assert h["ok"] is True and h["steps"] >= 2 and h["world"] == 1 and h["search_plane"] is True
+        assert st["batching"]["embed_fast"]["items"] == 1
         await cl.close()
         srv.server.close()
     asyncio.run(go())
@@ -331,9 +333,9 @@ def test_engine_search_microbatch_matches_single_searches(eng):
         args = [dict(vecs=qs[i:i + 1], filters=None if f is None else [f], k=3, min_sim=-1.0)
                 for i, f in enumerate(flt)]
         alone = [await cl.call("search", **a) for a in args]
-        b0 = srv.stats["search"]["batches"]
+        b0 = srv.group.plane.stats["rounds"]
         together = await asyncio.gather(*[cl.call("search", **a) for a in args])
-        assert srv.stats["search"]["batches"] - b0 < len(args)
+        assert srv.group.plane.stats["rounds"] - b0 < len(args)  # coalesced into plane rounds
         for x, y in zip(alone, together):
             assert np.array_equal(x["keys"], y["keys"]) and np.allclose(x["scores"], y["scores"])
         # a malformed search fails alone; the batcher keeps serving

@@ -363,3 +363,35 @@ def test_parse_empty_content_still_enqueues():
     d, store, q = p_deps()
     asyncio.run(parser.handle_parse(d, {"document_id": DOC, "content": ""}))
     assert len(q.calls) == 1
+
+
+def test_query_fused_embed_search_one_engine_call():
+    """With the engine behind both the embedder and the vectors, a cache miss embeds and searches
+    in ONE call (embed_top_k); the vector still lands in the embedding cache, and the next query
+    with the same question (another document set) searches with the cached vector."""
+    cid = str(uuid.uuid4())
+    res = [SearchResult(Chunk(cid, DOC, 0, "Go is a programming language", 5), 0.9, Summary())]
+
+    class Store(Spy):
+        fused_query = True
+    store = Store(embed_top_k=(np.array([0.6, 0.8], dtype=np.float32), res), top_k=res)
+    emb = Spy(embed=np.array([0.1, 0.2], dtype=np.float32))
+    llm = Spy(answer=("an answer", 0.9))
+    cache = MemoryCache()
+    c = TestClient(query.build_app(deps_for(embedder=emb, store=store, llm=llm, cache=cache)))
+    r = _q(c, {"question": "  What\tis Go? ", "document_ids": [DOC], "top_k": 2})
+    assert r.status_code == 200 and r.json()["sources"][0]["chunk_id"] == cid
+    assert store.names() == ["embed_top_k"] and emb.calls == []
+    assert store.calls[0][1] == ([DOC], "What is Go?", 2)  # preprocessed text, reference order of args
+    other = str(uuid.uuid4())
+    r2 = _q(c, {"question": "  What\tis Go? ", "document_ids": [other], "top_k": 2})
+    assert r2.status_code == 200 and store.names() == ["embed_top_k", "top_k"]
+    np.testing.assert_allclose(store.calls[1][1][1], [0.6, 0.8])
+    # the engine's tag decides the reference's error message
+    bad = Store(embed_top_k=RuntimeError("RPCError: RuntimeError: embed_search/search: shard down"))
+    c2 = TestClient(query.build_app(deps_for(embedder=emb, store=bad, llm=llm, cache=MemoryCache())))
+    r3 = _q(c2, {"question": "What is Go?", "document_ids": [DOC]})
+    assert r3.status_code == 500 and r3.text == "search failed\n"
+    bad2 = Store(embed_top_k=RuntimeError("RPCError: RuntimeError: embed_search/embed: boom"))
+    c3 = TestClient(query.build_app(deps_for(embedder=emb, store=bad2, llm=llm, cache=MemoryCache())))
+    assert _q(c3, {"question": "What is Go?", "document_ids": [DOC]}).text == "failed to embed question\n"
