@@ -5,9 +5,12 @@ upload -> poll summary -> query), through the gateway:
 
   1. ingest: upload ``--docs`` synthetic documents (``--concurrency`` in flight), poll each
      summary until it is ready -> docs/min from the first upload to the last ready summary;
-  2. cache-miss queries: ``--queries`` unique questions over the ingested documents -> QPS and
-     p50/p99 latency (embed + search + answer inside the stack);
-  3. cache-hit queries: the same questions again -> p50/p99 (served from the query cache; the
+  2. unloaded cache-miss latency: ``--serial-queries`` unique questions sent one at a time
+     (concurrency 1) -> p50 / p90 / p99 through gateway proxy -> query service -> engine, the
+     number the reference publishes ("~2-3 seconds", README.md:590);
+  3. cache-miss queries: ``--queries`` unique questions over the ingested documents -> QPS and
+     p50/p99 latency (embed + search + answer inside the stack) at ``--concurrency`` in flight;
+  4. cache-hit queries: the same questions again -> p50/p99 (served from the query cache; the
      reference promises "sub-millisecond" server-side, README.md:588).
 
 ``--spawn`` starts the multi-process deploy.py stack (``--topology deploy``, default) or the all-in-one
@@ -116,7 +119,7 @@ def _raw_hits(url: str, bodies: list[str]) -> list[float]:
 
 
 async def run(gw: str, docs: int, words: int, queries: int, concurrency: int, top_k: int, seed: int,
-              poll_s: float = 0.05, ingest_timeout: float = 600.0, query_url: str = "") -> dict:
+              poll_s: float = 0.05, ingest_timeout: float = 600.0, query_url: str = "", serial: int = 50) -> dict:
     tg = TextGen(seed=seed)
     texts = [tg.document(words) for _ in range(docs)]
     sem = asyncio.Semaphore(concurrency)
@@ -171,6 +174,14 @@ async def run(gw: str, docs: int, words: int, queries: int, concurrency: int, to
                 dt = (time.perf_counter() - t) * 1000.0
             return r.status_code, dt
 
+        # ---- unloaded cache misses: one request in flight ----
+        sq = [json.dumps({"question": f"Serial question {i}: what about {tg.word()} and {tg.word()}?",
+                          "document_ids": [ready[(7 * i + j) % len(ready)] for j in range(min(3, len(ready)))],
+                          "top_k": top_k}) for i in range(serial)] if ready else []
+        for b in sq[:2]:  # warm the batch-1 paths (graph capture) before timing
+            await ask(b.replace("Serial question", "Warm-up question"))
+        serial_res = [await ask(b) for b in sq]
+
         t1 = time.perf_counter()
         miss = await asyncio.gather(*[ask(b) for b in bodies])
         t_miss = time.perf_counter() - t1
@@ -188,10 +199,15 @@ async def run(gw: str, docs: int, words: int, queries: int, concurrency: int, to
                 handler_ms = vals["da_query_stage_seconds_sum"] / vals["da_query_stage_seconds_count"] * 1000.0
 
     miss_ok = [dt for st, dt in miss if st == 200]
+    serial_ok = [dt for st, dt in serial_res if st == 200]
     hit_ok = [dt for st, dt in hit if st == 200]
     return {
         "metric": "http_stack", "docs": docs, "docs_ready": len(ready), "words_per_doc": words,
         "ingest_docs_per_min": round(len(ready) / t_ingest * 60.0, 1) if t_ingest else None,
+        "serial_queries": len(serial_res), "serial_errors": sum(1 for st, _ in serial_res if st != 200),
+        "serial_cache_miss_p50_ms": _r(statistics.median(serial_ok) if serial_ok else None),
+        "serial_cache_miss_p90_ms": _r(_pct(serial_ok, 90)),
+        "serial_cache_miss_p99_ms": _r(_pct(serial_ok, 99)),
         "queries": queries, "query_errors": sum(1 for st, _ in miss if st != 200),
         "qa_qps": round(len(miss_ok) / t_miss, 2) if t_miss > 0 else None,
         "cache_miss_p50_ms": _r(statistics.median(miss_ok) if miss_ok else None),
@@ -223,13 +239,15 @@ def _scrape(url: str, names: tuple[str, ...]) -> dict:
 
 
 async def _engine_stats(url: str) -> dict:
-    from docagents_amd.engine.rpc import EngineClient
-    c = EngineClient(url, timeout=30.0)
+    from docagents_amd.engine.rpc import EngineCluster
+    c = EngineCluster(url, timeout=30.0)
     try:
         await c.connect(retries=2)
         st = await c.call("stats")
     finally:
         await c.close()
+    if "replicas" in st:  # several replicas: report replica 0's view (plus the count)
+        st = dict(st["replicas"][0], replicas=len(st["replicas"]))
     r0 = st["ranks"][0] if st.get("ranks") else {}
     return {"exec": st.get("exec"), "batching": st.get("batching"), "gen": r0.get("gen"), "embed": r0.get("embed"),
             "sched": r0.get("sched")}
@@ -266,6 +284,7 @@ def main(argv=None):
     ap.add_argument("--docs", type=int, default=32)
     ap.add_argument("--words", type=int, default=2000)
     ap.add_argument("--queries", type=int, default=64)
+    ap.add_argument("--serial-queries", type=int, default=50, help="unloaded (concurrency 1) cache-miss queries")
     ap.add_argument("--concurrency", type=int, default=16)
     ap.add_argument("--top-k", type=int, default=5)
     ap.add_argument("--seed", type=int, default=7)
@@ -309,7 +328,8 @@ def main(argv=None):
                 time.sleep(0.25)
     try:
         qurl = f"http://127.0.0.1:{int(gw.rsplit(':', 1)[1]) + 1}/api/query" if proc is not None else a.query_url
-        out = asyncio.run(run(gw, a.docs, a.words, a.queries, a.concurrency, a.top_k, a.seed, query_url=qurl))
+        out = asyncio.run(run(gw, a.docs, a.words, a.queries, a.concurrency, a.top_k, a.seed, query_url=qurl,
+                              serial=a.serial_queries))
         out["topology"] = a.topology if proc is not None else "external"
         if proc is not None and a.topology == "deploy":
             eng = env.get("ENGINE_URL", "") if env.get("LLM_PROVIDER") == "engine" else ""
