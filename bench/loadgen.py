@@ -180,7 +180,10 @@ async def run(gw: str, docs: int, words: int, queries: int, concurrency: int, to
                           "top_k": top_k}) for i in range(serial)] if ready else []
         for b in sq[:2]:  # warm the batch-1 paths (graph capture) before timing
             await ask(b.replace("Serial question", "Warm-up question"))
+        mbase = query_url.rsplit("/api/", 1)[0] + "/metrics" if query_url else ""
+        before = _stage_sums(mbase) if mbase else {}
         serial_res = [await ask(b) for b in sq]
+        serial_stages = _stage_delta(before, _stage_sums(mbase)) if mbase else {}
 
         t1 = time.perf_counter()
         miss = await asyncio.gather(*[ask(b) for b in bodies])
@@ -208,6 +211,7 @@ async def run(gw: str, docs: int, words: int, queries: int, concurrency: int, to
         "serial_cache_miss_p50_ms": _r(statistics.median(serial_ok) if serial_ok else None),
         "serial_cache_miss_p90_ms": _r(_pct(serial_ok, 90)),
         "serial_cache_miss_p99_ms": _r(_pct(serial_ok, 99)),
+        "serial_stage_mean_ms": serial_stages,
         "queries": queries, "query_errors": sum(1 for st, _ in miss if st != 200),
         "qa_qps": round(len(miss_ok) / t_miss, 2) if t_miss > 0 else None,
         "cache_miss_p50_ms": _r(statistics.median(miss_ok) if miss_ok else None),
@@ -219,6 +223,31 @@ async def run(gw: str, docs: int, words: int, queries: int, concurrency: int, to
         "cache_hit_handler_mean_ms": _r(handler_ms),
         "concurrency": concurrency, "top_k": top_k, "ingest_timeline": timeline,
     }
+
+
+def _stage_sums(url: str) -> dict:
+    """{stage: (sum_s, count)} of the query service's da_query_stage_seconds histogram."""
+    out = {}
+    try:
+        text = httpx.get(url, timeout=5.0).text
+    except Exception:  # noqa: BLE001
+        return out
+    for ln in text.splitlines():
+        for suf, i in (("_sum", 0), ("_count", 1)):
+            pre = "da_query_stage_seconds" + suf + "{"
+            if ln.startswith(pre):
+                st = ln.split('stage="', 1)[1].split('"', 1)[0]
+                out.setdefault(st, [0.0, 0.0])[i] = float(ln.split()[-1])
+    return out
+
+
+def _stage_delta(a: dict, b: dict) -> dict:
+    res = {}
+    for st, (s1, c1) in b.items():
+        s0, c0 = a.get(st, (0.0, 0.0))
+        if c1 > c0:
+            res[st] = round((s1 - s0) / (c1 - c0) * 1000.0, 3)
+    return res
 
 
 def _scrape(url: str, names: tuple[str, ...]) -> dict:

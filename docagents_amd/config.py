@@ -77,6 +77,8 @@ class Config:
     # decode steps per scheduler tick: 1 lets queued embeds / searches / admissions in between every
     # step (deploy stack, 64 in flight: 35.0 / 34.7 / 33.5 / 32.0 q/s at 1 / 2 / 4 / 8, profiles/r2/stack)
     engine_cb_steps: int = field(default=1, metadata={"env": "ENGINE_CB_STEPS"})
+    # decode steps per tick when no request waits for admission (latency of an unloaded request)
+    engine_cb_max_steps: int = field(default=16, metadata={"env": "ENGINE_CB_MAX_STEPS"})
     engine_admit_tokens: int = field(default=0, metadata={"env": "ENGINE_ADMIT_TOKENS"})  # 0 -> 4 prefill chunks
     # --- new keys: durable vector shards (index/wal.py) ---
     index_dir: str = field(default="", metadata={"env": "INDEX_DIR"})  # "" -> DATA_DIR/index; "none" -> off

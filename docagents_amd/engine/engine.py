@@ -175,7 +175,7 @@ class Engine:
                                               max_admit_tokens=getattr(self, "admit_tokens", None))
         return self._sched
 
-    def cb_tick(self, new_items, steps: int | None = None):
+    def cb_tick(self, new_items, steps: int | None = None, stop=None):
         """Submit new work and run one scheduler tick. An item is ``(tag, (question, chunk_ids,
         quality))`` (an Answer) or ``(tag, {"ids": prompt_ids, "max_new": n})`` (a prebuilt prompt:
         summary windows). Returns ([(tag, text, confidence)], still_busy); a prompt item's
@@ -188,7 +188,7 @@ class Engine:
                 q, ch, quality = it
                 sch.submit(self.answer_prompt_ids(q, ch, self.max_new_tokens), self.max_new_tokens, (tag, quality))
         with self.lock:
-            done = sch.tick(steps)
+            done = sch.tick(steps, stop)
         out = [(tag, self.chat.decode(r.tokens), float(quality) * r.mean_prob) for (tag, quality), r in done]
         return out, sch.busy()
 

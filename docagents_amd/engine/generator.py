@@ -316,6 +316,7 @@ class ContinuousScheduler:
         self.max_admit_tokens = max_admit_tokens or 131072  # 4 x 32k-token chunks (deploy-stack tuning)
         self.st = DecodeState(self.m, self.B, self.cap, gen.temperature, gen.seed, gen.eos)
         self.rows: list = [None] * self.B        # row -> (tag, slot, budget)
+        self.left: list = [None] * self.B        # row -> decode steps it may still need (budget - 1 - steps run)
         self.pending: collections.deque = collections.deque()
         self._reset_rows(list(range(self.B)))
         self.stats = {"admitted": 0, "finished": 0, "ticks": 0, "steps": 0, "head_hits": 0, "heads_built": 0}
@@ -337,22 +338,34 @@ class ContinuousScheduler:
     def n_active(self) -> int:
         return sum(r is not None for r in self.rows)
 
-    def tick(self, steps: int | None = None) -> list:
-        """Admit what fits, run ``steps`` decode steps, return [(tag, GenResult)] of finished rows."""
+    def tick(self, steps: int | None = None, stop=None) -> list:
+        """Admit what fits, run up to ``steps`` decode steps, return [(tag, GenResult)] of finished
+        rows. The steps are capped by the largest remaining token budget of the running rows (no
+        replays after every row is done), and ``stop()`` (checked between steps, host-side, no
+        device sync) ends the tick early — the server passes "new requests are waiting" so an
+        arrival waits for at most one step while an unloaded request runs many steps per tick."""
         self.stats["ticks"] += 1
         done = self._admit()
         if self.n_active:
             st, k = self.st, steps or self.chunk_steps
+            k = max(1, min(k, max(left for left in self.left if left is not None)))
             if self.gen.use_graphs and st.graph is None:
                 self.gen._capture(st)
             t0 = time.perf_counter()
-            for _ in range(k):
+            ran = 0
+            while ran < k:
                 if st.graph is not None:
                     st.graph.replay()
                 else:
                     self.m.decode_step(st)
-            self.stats["steps"] += k
-            self.gen.stats["decode_steps"] += k
+                ran += 1
+                if stop is not None and ran < k and stop():
+                    break
+            for r, left in enumerate(self.left):
+                if left is not None:
+                    self.left[r] = max(0, left - ran)
+            self.stats["steps"] += ran
+            self.gen.stats["decode_steps"] += ran
             done += self._reap()
             self.gen.stats["decode_s"] += time.perf_counter() - t0
         return done
@@ -476,6 +489,7 @@ class ContinuousScheduler:
         st.pre.index_copy_(0, idx, h2d(pre, dev))
         for r, (p, b, tag), sl, h in zip(rows, take, slots, hs):
             self.rows[r] = (tag, sl, int(b), h)
+            self.left[r] = int(b) - 1  # the first token came from the prefill
         self.stats["admitted"] += n
         # a budget of one token (or an immediate EOS) finishes at prefill
         return self._reap(rows)
@@ -503,6 +517,7 @@ class ContinuousScheduler:
             out.append((tag, GenResult(toks, float(conf[k, 0] / cnt) if cnt > 0 else 1.0, int(cnt))))
             self.gen.stats["decode_tokens"] += int(cnt)
             self.rows[r] = None
+            self.left[r] = None
             slots.append(sl)
         self._reset_rows(fin)
         st.hist.index_fill_(0, idx, -1)

@@ -65,6 +65,7 @@ class EngineGroup:
         # applied; None = HBM only (tests, benchmarks)
         self.shard_log = shard_log
         self.ckpt_at = time.monotonic()
+        self.tick_stop = None  # set by the server: "requests are waiting for admission"
 
     @property
     def tensor_parallel(self) -> bool:
@@ -166,7 +167,10 @@ class EngineGroup:
             mine = [(t, it if "ids" in it else self._answer_item(it)) for t, it in a["items"]]
             if mine:
                 faults.maybe_fail("engine.generate")
-            return e.cb_tick(mine, a.get("steps"))
+            # an early stop decided by the leader alone would desynchronise the TP ranks' decode
+            # steps: only a one-rank replica stops a tick when new work arrives
+            stop = self.tick_stop if self.tp_size == 1 else None
+            return e.cb_tick(mine, a.get("steps"), stop)
         if cmd == "index_add":
             if self._check_routed(a["doc_id"]) == self.rank:
                 self._upsert(a["doc_id"], np.asarray(a["keys"], dtype=np.int64),
@@ -252,7 +256,8 @@ class EngineServer:
     def __init__(self, group: EngineGroup, log, max_batch_items: int = 256, step_timeout_s: float = 300.0,
                  hard_timeout_s: float = 0.0, liveness_s: float = 30.0, profiler: StepProfiler | None = None,
                  continuous: bool = False, cb_steps: int = 1, checkpoint_s: float = 0.0,
-                 cb_window_s: float = 0.02, fast_embed_max: int = 8, urls: list[str] | None = None):
+                 cb_window_s: float = 0.003, fast_embed_max: int = 8, urls: list[str] | None = None,
+                 cb_max_steps: int = 16):
         self.group, self.log = group, log
         self.urls = urls or []  # every replica's listen URL (topology RPC), replica order
         # the fast lane: query-sized embeds on their own thread / high-priority stream / workspace
@@ -274,7 +279,10 @@ class EngineServer:
         self._tok = {"prefill": 0, "decode": 0}
         # continuous batching of answers (a decode tick loop instead of whole-batch waves)
         self.continuous = continuous and getattr(group.engine, "gen", None) is not None
-        self.cb_steps = cb_steps
+        # decode steps per scheduler tick: cb_steps while requests wait for admission, up to
+        # cb_max_steps otherwise (a one-rank replica also ends a long tick as soon as one arrives)
+        self.cb_steps, self.cb_max_steps = cb_steps, max(cb_steps, cb_max_steps)
+        group.tick_stop = lambda: bool(self._cb_new)
         self.cb_window_s = cb_window_s
         self._cb_new: list = []
         self._cb_futs: dict = {}
@@ -410,7 +418,8 @@ class EngineServer:
             new, self._cb_new = self._cb_new, []
             t0 = time.perf_counter()
             try:
-                done, busy = await self._gpu("cb_tick", {"items": new, "steps": self.cb_steps})
+                steps = self.cb_steps if self._cb_new else self.cb_max_steps
+                done, busy = await self._gpu("cb_tick", {"items": new, "steps": steps})
             except Exception as e:  # noqa: BLE001 - fail the requests of this tick, keep serving
                 for tag, _ in new:
                     f = self._cb_futs.pop(tag, None)

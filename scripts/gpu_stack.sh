@@ -9,7 +9,9 @@ cd $R
 mkdir -p gpurun_out
 python -m docagents_amd.ops.build > gpurun_out/build.log 2>&1 || { tail -30 gpurun_out/build.log; exit 3; }
 python -m docagents_amd.native > gpurun_out/native.log 2>&1 || { tail -30 gpurun_out/native.log; exit 3; }
-export LLM_PROVIDER=engine MIN_SIMILARITY=-1 LOG_LEVEL=warn TMPDIR=${TMPDIR:-/tmp} INDEX_FSYNC=1
+mkdir -p gpurun_out/stack_tmp
+# the stack's sqlite / index / supervisor logs land under gpurun_out so a failing service's log comes back
+export LLM_PROVIDER=engine MIN_SIMILARITY=-1 LOG_LEVEL=warn TMPDIR=$R/gpurun_out/stack_tmp INDEX_FSYNC=1
 for C in ${3:-64}; do
   timeout -k 10 ${STACK_TIMEOUT:-600} python -u bench/loadgen.py --spawn --topology deploy --docs ${1:-64} \
     --words 2000 --queries ${2:-256} --concurrency $C > gpurun_out/stack_c$C.json 2> gpurun_out/stack_c$C.err
