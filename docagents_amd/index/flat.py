@@ -225,9 +225,11 @@ class FlatIndex:
         return self.ops.topk_dense(X, q, k, min_sim, slots=slots, bitmap=bitmap)
 
     def gather_ids(self, rows: torch.Tensor) -> torch.Tensor:
-        """Device: row indices (int32, -1 = none) -> external ids (int64, -1 = none)."""
+        """Device: row indices (int32, -1 = none) -> external ids (int64, -1 = none). Indices are
+        clamped into the id table before the gather (a bad row index must never read outside it)."""
         r = rows.long()
-        return torch.where(r >= 0, self.ids_t[r.clamp_min(0)], torch.full_like(r, -1))
+        ok = (r >= 0) & (r < self.n)
+        return torch.where(ok, self.ids_t[r.clamp(0, max(0, self.n - 1))], torch.full_like(r, -1))
 
     def row_ids(self, rows: np.ndarray) -> np.ndarray:
         out = np.full(rows.shape, -1, dtype=np.int64)

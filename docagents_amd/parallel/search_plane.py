@@ -185,7 +185,13 @@ class SearchPlane:
         idx, dev = self.index, self.index.device
         d = idx.dim
         stream_ctx = torch.cuda.stream(self.stream) if self.stream is not None else _nullctx()
-        with stream_ctx:
+        # the scan kernels' scratch must not be the GPU thread's: its decode graph captured that
+        # workspace's pointer and runs concurrently with this thread (ops/kernels.py workspace_role)
+        ws_ctx = _nullctx()
+        if dev.type == "cuda":
+            from ..ops.kernels import workspace_role
+            ws_ctx = workspace_role("search")
+        with stream_ctx, ws_ctx:
             if self.write_event is not None and self.stream is not None:
                 self.stream.wait_event(self.write_event)
             rows = [r.vecs.shape[0] for r in take]
