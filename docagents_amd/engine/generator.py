@@ -315,6 +315,10 @@ class ContinuousScheduler:
         # prefill chunk per tick, which would stretch the decode of the last-admitted rows
         self.max_admit_tokens = max_admit_tokens or 131072  # 4 x 32k-token chunks (deploy-stack tuning)
         self.st = DecodeState(self.m, self.B, self.cap, gen.temperature, gen.seed, gen.eos)
+        # row buckets (powers of two up to B): a tick replays the graph of the smallest bucket that
+        # holds every occupied row — an unloaded request decodes at batch-1 cost (the GEMV path), not
+        # in the full B-row graph. Admission fills the lowest free rows, so occupancy stays compact.
+        self.buckets: dict[int, DecodeState] = {self.B: self.st}
         self.rows: list = [None] * self.B        # row -> (tag, slot, budget)
         self.left: list = [None] * self.B        # row -> decode steps it may still need (budget - 1 - steps run)
         self.pending: collections.deque = collections.deque()
@@ -347,7 +351,7 @@ class ContinuousScheduler:
         self.stats["ticks"] += 1
         done = self._admit()
         if self.n_active:
-            st, k = self.st, steps or self.chunk_steps
+            st, k = self._bucket_state(), steps or self.chunk_steps
             k = max(1, min(k, max(left for left in self.left if left is not None)))
             if self.gen.use_graphs and st.graph is None:
                 self.gen._capture(st)
@@ -365,6 +369,8 @@ class ContinuousScheduler:
                 if left is not None:
                     self.left[r] = max(0, left - ran)
             self.stats["steps"] += ran
+            sb = self.stats.setdefault("steps_by_bucket", {})
+            sb[st.B] = sb.get(st.B, 0) + ran
             self.gen.stats["decode_steps"] += ran
             done += self._reap()
             self.gen.stats["decode_s"] += time.perf_counter() - t0
@@ -380,7 +386,29 @@ class ContinuousScheduler:
                 out[tag] = r
         return [out[i] for i in range(len(prompts))]
 
+    def warmup(self):
+        """Capture every bucket's decode graph now (serving startup), not on a request's path."""
+        if not self.gen.use_graphs:
+            return
+        b = 1
+        while b <= self.B:
+            st = self._state_for(b)
+            if st.graph is None:
+                self.gen._capture(st)
+            b *= 2
+
     # -------------------------------------------------------------------------------- internals
+    def _state_for(self, b: int) -> DecodeState:
+        st = self.buckets.get(b)
+        if st is None:
+            st = self.buckets[b] = self.st.rows(b)
+        return st
+
+    def _bucket_state(self) -> DecodeState:
+        top = max(i for i, r in enumerate(self.rows) if r is not None) + 1
+        b = _bucket(top) if top < self.B else self.B
+        return self._state_for(min(b, self.B))
+
     def _reset_rows(self, rows):
         if not rows:
             return

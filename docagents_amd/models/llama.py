@@ -430,6 +430,15 @@ class DecodeState:
         self.temperature, self.seed, self.eos = temperature, seed, tuple(eos)[:4]
         self.graph = None
 
+    def rows(self, b: int) -> "DecodeState":
+        """A state over the first ``b`` rows of this one (views of the same buffers, its own graph):
+        a decode step on it advances rows [0, b) exactly as the full state would, at batch-b cost."""
+        v = object.__new__(DecodeState)
+        for k, t in self.__dict__.items():
+            v.__dict__[k] = t[:b] if isinstance(t, torch.Tensor) else t
+        v.B, v.graph = b, None
+        return v
+
 
 def pack_prompts(prompts: list[list[int]]):
     lens = np.fromiter((len(p) for p in prompts), dtype=np.int64, count=len(prompts))

@@ -84,6 +84,8 @@ def main(argv=None) -> int:
                  enc_dtype="fp8" if cfg.dtype == "fp8" else "bf16")
     if cfg.engine_admit_tokens > 0:
         eng.admit_tokens = cfg.engine_admit_tokens
+    if cfg.engine_continuous and dev.type == "cuda" and eng.gen is not None:
+        eng.scheduler.warmup()  # every row bucket's decode graph, before the first request (all TP ranks)
     index_dir = a.index_dir if a.index_dir is not None else cfg.index_dir_path()
     shard_log = None
     if index_dir and index_dir != "none":

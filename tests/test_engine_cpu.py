@@ -513,3 +513,21 @@ def test_kept_head_slot_never_blocks_a_full_wave():
     full = [head + [int(t) for t in rng.integers(5, 3000, size=n)] for n in (1, 2, 3, 4)]
     assert len(g.generate(full, 4)) == 4
     assert len(g.cache.free) + 1 + (g.head is not None) == g.cache.slots
+
+
+def test_continuous_scheduler_runs_the_smallest_row_bucket():
+    """An unloaded request decodes in the 1-row bucket (batch-1 cost), three in the 4-row bucket;
+    the tokens equal the wave path's either way."""
+    from docagents_amd.engine.generator import ContinuousScheduler
+    e = Engine("tiny-enc", "tiny-dec", "cpu", max_batch=8, max_seq=512, max_new_tokens=6, temperature=0.0,
+               use_graphs=False)
+    rng = np.random.default_rng(9)
+    prompts = [[int(t) for t in rng.integers(5, 3000, size=n)] for n in (12, 40, 7)]
+    e.gen.share_prefix = False
+    want = [e.gen.generate([p], 6)[0].tokens for p in prompts]
+    sched = ContinuousScheduler(e.gen, B=8, max_new_cap=8, chunk_steps=4)
+    got1 = sched.run_all(prompts[:1], 6)
+    assert got1[0].tokens == want[0] and set(sched.stats["steps_by_bucket"]) == {1}
+    got3 = sched.run_all(prompts, 6)
+    assert [r.tokens for r in got3] == want
+    assert sched.stats["steps_by_bucket"].get(4, 0) > 0 and 8 not in sched.stats["steps_by_bucket"]
