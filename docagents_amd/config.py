@@ -79,6 +79,8 @@ class Config:
     engine_cb_steps: int = field(default=1, metadata={"env": "ENGINE_CB_STEPS"})
     # decode steps per tick when no request waits for admission (latency of an unloaded request)
     engine_cb_max_steps: int = field(default=16, metadata={"env": "ENGINE_CB_MAX_STEPS"})
+    # CUs reserved for the latency lanes (query embeds + search plane); 0 = no partition
+    engine_latency_cus: int = field(default=0, metadata={"env": "ENGINE_LATENCY_CUS"})
     engine_admit_tokens: int = field(default=0, metadata={"env": "ENGINE_ADMIT_TOKENS"})  # 0 -> 4 prefill chunks
     # --- new keys: durable vector shards (index/wal.py) ---
     index_dir: str = field(default="", metadata={"env": "INDEX_DIR"})  # "" -> DATA_DIR/index; "none" -> off

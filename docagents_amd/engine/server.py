@@ -257,15 +257,20 @@ class EngineServer:
                  hard_timeout_s: float = 0.0, liveness_s: float = 30.0, profiler: StepProfiler | None = None,
                  continuous: bool = False, cb_steps: int = 1, checkpoint_s: float = 0.0,
                  cb_window_s: float = 0.003, fast_embed_max: int = 8, urls: list[str] | None = None,
-                 cb_max_steps: int = 16):
+                 cb_max_steps: int = 16, lanes=None):
         self.group, self.log = group, log
         self.urls = urls or []  # every replica's listen URL (topology RPC), replica order
         # the fast lane: query-sized embeds on their own thread / high-priority stream / workspace
         self.fast_embed_max = fast_embed_max
+        # lanes = (main, fast) streams of a CU partition (ops/streams.py serving_lanes), or None
+        main_stream, fast_stream = (lanes or (None, None))[:2]
         self.fast = cf.ThreadPoolExecutor(max_workers=1, thread_name_prefix="fast-embed")
-        self._fast_stream = None
+        self._fast_q: list = []
+        self._fast_wake = asyncio.Event()
+        self._fast_stream = fast_stream
         self.checkpoint_s = checkpoint_s  # periodic shard snapshots when the shard is durable (0 = off)
-        self.gpu = cf.ThreadPoolExecutor(max_workers=1, thread_name_prefix="gpu")
+        init = (lambda: torch.cuda.set_stream(main_stream)) if main_stream is not None else None
+        self.gpu = cf.ThreadPoolExecutor(max_workers=1, thread_name_prefix="gpu", initializer=init)
         self.queues: dict[str, asyncio.Queue] = {}
         self.max_batch_items = max_batch_items
         self.stats = {m: {"batches": 0, "items": 0, "busy_s": 0.0} for m in self.BATCHED}
@@ -383,14 +388,43 @@ class EngineServer:
             return e.embed(texts, preprocess, out_dtype=torch.float32).cpu().numpy()
 
     async def _embed_fast(self, texts, preprocess: bool):
-        t0 = time.perf_counter()
-        v = await asyncio.get_running_loop().run_in_executor(self.fast, self._fast_embed, list(texts), preprocess)
-        st = self.stats.setdefault("embed_fast", {"batches": 0, "items": 0, "busy_s": 0.0})
-        st["batches"] += 1
-        st["items"] += len(texts)
-        st["busy_s"] += time.perf_counter() - t0
-        metrics.ENGINE_ITEMS.labels("embed").inc(len(texts))
-        return v
+        """Queue query-sized texts for the fast lane; the lane runs every text queued while its
+        previous encoder call was in flight as ONE call (micro-batching), so under load the lane's
+        throughput scales with the burst instead of one encoder pass per question."""
+        fut = asyncio.get_running_loop().create_future()
+        self._fast_q.append((list(texts), bool(preprocess), fut))
+        self._fast_wake.set()
+        return await fut
+
+    async def _fast_loop(self):
+        loop = asyncio.get_running_loop()
+        while True:
+            if not self._fast_q:
+                self._fast_wake.clear()
+                await self._fast_wake.wait()
+            pre = self._fast_q[0][1]
+            take = [r for r in self._fast_q if r[1] == pre][:64]
+            self._fast_q = [r for r in self._fast_q if all(r is not t for t in take)]
+            texts = [t for r in take for t in r[0]]
+            t0 = time.perf_counter()
+            try:
+                v = await loop.run_in_executor(self.fast, self._fast_embed, texts, pre)
+            except Exception as e:  # noqa: BLE001 - fail this batch, keep the lane serving
+                for _, _, f in take:
+                    if not f.done():
+                        f.set_exception(e)
+                continue
+            st = self.stats.setdefault("embed_fast", {"batches": 0, "items": 0, "busy_s": 0.0})
+            st["batches"] += 1
+            st["items"] += len(texts)
+            st["busy_s"] += time.perf_counter() - t0
+            metrics.ENGINE_ITEMS.labels("embed").inc(len(texts))
+            metrics.ENGINE_BATCH_SIZE.labels("embed_fast").observe(len(texts))
+            o = 0
+            for ts, _, f in take:
+                if not f.done():
+                    f.set_result(v[o:o + len(ts)])
+                o += len(ts)
 
     async def _search(self, vecs, k, min_sim, filters):
         """Sharded top-k through the search plane (its own thread + stream on every rank)."""
@@ -597,6 +631,7 @@ class EngineServer:
         self.watchdog.start()
         if self.continuous:
             self.cb_task = asyncio.ensure_future(self._cb_loop())
+        self.fast_task = asyncio.ensure_future(self._fast_loop())
         if self.liveness_s > 0 and self.group.tp_size > 1:
             self.liveness_task = asyncio.ensure_future(self._liveness_loop())
         kind, addr = parse_url(url)

@@ -1,12 +1,15 @@
-"""CU-masked HIP streams: spatial partitioning of one MI355X between two co-running phases.
+"""CU-masked HIP streams: spatial partitioning of one MI355X (``hipExtStreamCreateWithCUMask``,
+csrc/runtime.hip).
 
-The serving pipeline runs the MFMA-bound prefill of one wave next to the HBM-bound decode of the
-previous wave. Two plain streams barely overlap (each kernel's grid covers every CU, so the
-dispatcher time-slices them: bench/overlap_probe.py, 2-25 %); two streams whose hardware queues
-are restricted to complementary CU sets (``hipExtStreamCreateWithCUMask``, csrc/runtime.hip)
-really co-run. Masks are chosen in groups of eight consecutive CU bits, spread evenly over the
-mask, so a lane's CUs are spread over all eight XCDs whether the bit -> XCD mapping is round
-robin or blocked (``probe_placement`` reports the mapping on a GPU).
+Two uses were measured:
+* co-running the MFMA-bound prefill of one wave with the HBM-bound decode of the previous one on
+  complementary CU sets (bench/cumask_probe.py, profiles/r3/cumask_probe.jsonl): NOT kept — decode
+  attention on a quarter of the CUs runs at half speed (its per-CU memory parallelism, not HBM,
+  limits it), and the co-run was never faster than running the two back to back;
+* isolating the serving latency lanes (query embeds, search plane) on a few CUs from the
+  throughput lane (decode replays, admission prefills): ``serving_lanes``.
+Masks are chosen in groups of eight consecutive CU bits, spread evenly over the mask; the
+placement probe shows a lane's CUs spread over all eight XCDs (8 of 32 per XCD at a quarter).
 """
 from __future__ import annotations
 
@@ -45,11 +48,12 @@ def mask_words(bits: list[int], n_cus: int) -> list[int]:
     return words
 
 
-def masked_stream(bits: list[int], device=None) -> torch.cuda.ExternalStream:
-    """A stream restricted to the CU bits ``bits`` (cached per (device, bits); never destroyed:
-    captured graphs and pending work may still reference it)."""
+def masked_stream(bits: list[int], device=None, tag: str = "") -> torch.cuda.ExternalStream:
+    """A stream restricted to the CU bits ``bits`` (cached per (device, bits, tag); never destroyed:
+    captured graphs and pending work may still reference it). Different tags give distinct streams
+    (hardware queues) on the same CUs."""
     dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
-    key = (dev.index or 0, tuple(sorted(bits)))
+    key = (dev.index or 0, tuple(sorted(bits)), tag)
     s = _STREAMS.get(key)
     if s is not None:
         return s
@@ -71,6 +75,20 @@ def lane_streams(frac_a: float, device=None) -> tuple[torch.cuda.ExternalStream,
     n = cu_count(device)
     a, b = split_groups(n, frac_a)
     return masked_stream(a, device), masked_stream(b, device)
+
+
+def serving_lanes(latency_cus: int, device=None):
+    """Spatial partition of one GPU for serving: ``latency_cus`` CUs (rounded to groups of 8) for
+    the latency lanes — the fast embed lane and the search plane, one stream each — and the rest for
+    the GPU thread's decode replays and admission prefills. Big prefill GEMMs occupy every CU they
+    can reach for milliseconds; a question's ~100-kernel encoder chain queued behind them on the
+    same CUs waits for each kernel's slot (measured: 218 ms per query embed at 128 requests in
+    flight). Returns (main, fast, search) streams, or (None, None, None) when latency_cus <= 0."""
+    if latency_cus <= 0:
+        return None, None, None
+    n = cu_count(device)
+    a, b = split_groups(n, latency_cus / n)
+    return (masked_stream(b, device, "main"), masked_stream(a, device, "fast"), masked_stream(a, device, "search"))
 
 
 def probe_placement(stream, blocks: int = 512, spin: int = 20000) -> list[tuple[int, int, int, int]]:

@@ -59,14 +59,14 @@ class SearchPlane:
     """One per rank. ``submit`` from any thread; results arrive as concurrent futures."""
 
     def __init__(self, index, rank: int = 0, world: int = 1, ctrl_group=None, data_group=None, device=None,
-                 poll_s: float = 0.001, idle_poll_s: float = 0.005, max_rows: int = 1024):
+                 poll_s: float = 0.001, idle_poll_s: float = 0.005, max_rows: int = 1024, stream=None):
         self.index, self.rank, self.world = index, rank, world
         self.ctrl_group, self.data_group = ctrl_group, data_group
         self.device = torch.device(device) if device is not None else torch.device("cpu")
         self.poll_s, self.idle_poll_s, self.max_rows = poll_s, idle_poll_s, max_rows
         self.q: collections.deque = collections.deque()
         self.cv = threading.Condition()
-        self.stream = None
+        self.stream = stream  # None: a high-priority stream created by the plane thread
         self.write_event = None
         self._stop = False
         self._thread = None
@@ -121,7 +121,8 @@ class SearchPlane:
     def _run(self):
         if self.device.type == "cuda":
             torch.cuda.set_device(self.device)
-            self.stream = torch.cuda.Stream(device=self.device, priority=-1)
+            if self.stream is None:
+                self.stream = torch.cuda.Stream(device=self.device, priority=-1)
         try:
             while self._round():
                 pass

@@ -98,7 +98,12 @@ def main(argv=None) -> int:
         n = load_index(eng.index, f"{a.snapshot}.shard{rank}")
         log.info("restored index shard", "rank", rank, "rows", n)
     from ..parallel.search_plane import SearchPlane
-    plane = SearchPlane(eng.index, rank, world, plane_ctrl, plane_data, device=dev).start()
+    lanes = (None, None, None)
+    if dev.type == "cuda" and cfg.engine_latency_cus > 0:
+        from ..ops.streams import serving_lanes
+        lanes = serving_lanes(cfg.engine_latency_cus, dev)
+        log.info("cu partition", "latency_cus", cfg.engine_latency_cus)
+    plane = SearchPlane(eng.index, rank, world, plane_ctrl, plane_data, device=dev, stream=lanes[2]).start()
     grp = EngineGroup(eng, rank, world, rep_ctrl, rep_data, shard_log=shard_log, tp_size=t, plane=plane)
     if not grp.is_leader:
         grp.follower_loop()
@@ -112,7 +117,7 @@ def main(argv=None) -> int:
         srv = EngineServer(grp, log, max_batch_items=cfg.max_batch * 4, step_timeout_s=cfg.engine_step_timeout,
                            hard_timeout_s=cfg.engine_hard_timeout, liveness_s=cfg.engine_liveness_s,
                            continuous=cfg.engine_continuous, cb_steps=cfg.engine_cb_steps,
-                           cb_max_steps=cfg.engine_cb_max_steps,
+                           cb_max_steps=cfg.engine_cb_max_steps, lanes=lanes,
                            checkpoint_s=cfg.index_checkpoint_s, urls=urls)
         if cfg.engine_metrics_port:
             import prometheus_client
