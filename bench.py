@@ -299,6 +299,17 @@ def main():
             ingest(batches[0], "b", ph=ingest_phases)
             log(info, f"ingest batch phases (ms): {ingest_phases}")
 
+    xgmi = None
+    if W > 1 and dev.type == "cuda" and os.environ.get("DA_BENCH_XGMI_CHECK", "1") != "0":
+        # C3 across real devices (outside the timed steps): bounded-wait kernels, so a peer that
+        # cannot be reached ends in an error here, never a hang
+        try:
+            from docagents_amd.parallel.xgmi_allreduce import verify_and_time
+            xgmi = verify_and_time(None, dev)
+        except Exception as e:  # noqa: BLE001 - reported in the JSON line, the bench result stands
+            xgmi = {"ok": False, "error": repr(e)[:200]}
+        log(info, f"xgmi all-reduce check: {xgmi}")
+
     gen = eng.gen.stats
     out = {
         "metric": METRIC, "value": round(qps, 3), "unit": "queries/s", "n_gpus": W, "steps": a.steps,
@@ -325,6 +336,8 @@ def main():
         "latency_phase_ms": lat_phases or None,
         "ingest_phase_ms": ingest_phases or None,
     }
+    if xgmi is not None:
+        out["xgmi_allreduce_check"] = xgmi
     if R == 0:
         print(json.dumps(out), flush=True)
     shutdown()

@@ -23,6 +23,7 @@ from docagents_amd.ops import kernels as K  # noqa: E402
 
 ENV_SETTERS = {
     "DA_GEMM_PF": "da_set_gemm_pf",          # decode-tile k-tiles in flight
+    "DA_GEMM_DB": "da_set_gemm_db",          # decode tiles load W fragments straight to registers
     "DA_FLASH_PIPE": "da_set_flash_pipe",    # software-pipelined flash prefill on / off / auto
     "DA_FLASH_QH": "da_set_flash_qh",        # flash queries per wave: 1 = 32, 2 = 64
     "DA_FLASH_WAVES": "da_set_flash_waves",  # flash waves per workgroup

@@ -12,7 +12,8 @@ import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from docagents_amd.ops import kernels as K  # noqa: E402
-from ab_arms import swiglu_interleaved  # noqa: E402
+from ab_arms import apply_env_overrides, swiglu_interleaved  # noqa: E402
+apply_env_overrides()  # DA_* schedule overrides for A/B sweeps (DA_GEMM_DB, DA_GEMM_PF, ...)
 
 
 def main():

@@ -15,20 +15,26 @@
 //  * split-K writes fp32 partials; gemm_splitk_reduce applies the same epilogue.
 #include "gemm.h"
 
-template <int BM, int BN, int WM, int WN, int EPI, int PF = 1>
+template <int BM, int BN, int WM, int WN, int EPI, int PF = 1, bool DB = false>
 __global__ void __launch_bounds__(256)
 gemm_bf16_kernel(GemmArgs p) {
   // PF = k-tiles in flight in registers. PF = 1: the classic register-staged double buffer (one
   // tile ahead). Decode-sized tiles (M <= 64) stream weights and are latency-bound at PF = 1 —
   // one 16-KB W tile per workgroup in flight, ~6 dependent HBM round trips per split — so they
   // keep PF tiles (up to 72 KB per workgroup) requested ahead of the MFMAs (Little's law).
+  // DB (direct B, decode tiles with WM = 1): each weight row is consumed by exactly one wave, so
+  // the wave loads its W fragments straight into the MFMA B-operand registers (lane l: row
+  // n0 + 16 j + (l & 15), k + 8 (l >> 4); 64 contiguous bytes per row per instruction) — no LDS
+  // write + read of the 16 KB W tile per k-tile; only the activation tile (shared by the 4 waves)
+  // goes through LDS.
   constexpr int BK = 64;
   constexpr int TM = BM / WM, TN = BN / WN;
   constexpr int FM = TM / 16, FN = TN / 16;
-  constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2;
-  constexpr int LA = BM * 8 / 256, LB = BN * 8 / 256;  // 16-B loads per thread per tile
+  constexpr int A_BYTES = BM * BK * 2, B_BYTES = DB ? 0 : BN * BK * 2;
+  constexpr int LA = BM * 8 / 256, LB = DB ? 1 : BN * 8 / 256;  // 16-B loads per thread per tile
   static_assert(WM * WN == 4, "4 waves");
   static_assert(LA >= 1 && LB >= 1, "tile too small");
+  static_assert(!DB || WM == 1, "direct B: one wave per weight column block");
   constexpr int STAGE_FLOATS = 4 * TM * (TN + 4);
   constexpr int LDS_MAIN = 2 * (A_BYTES + B_BYTES);
   constexpr int LDS_BYTES = LDS_MAIN > STAGE_FLOATS * 4 ? LDS_MAIN : STAGE_FLOATS * 4;
@@ -54,6 +60,8 @@ gemm_bf16_kernel(GemmArgs p) {
 
   // ---- global -> register staging (PF slots) ----
   u32x4_t ra[PF][LA], rb[PF][LB];
+  bf16x8_t rd[DB ? PF : 1][DB ? 2 : 1][DB ? FN : 1];  // DB: W fragments [slot][k half][n tile]
+  const int fr = lane & 15, fg = lane >> 4;
   // Rows past M / N are clamped, not branched around: they only feed accumulators whose outputs
   // are never stored, and branch-free loads keep the compiler's vmcnt waits counted (a load
   // under a divergent branch makes every later wait a full vmcnt(0) drain).
@@ -64,10 +72,24 @@ gemm_bf16_kernel(GemmArgs p) {
       const int idx = tid + 256 * i, r = idx >> 3, c = idx & 7;
       xa[i] = *(const u32x4_t*)(p.A + (size_t)min(m0 + r, p.M - 1) * p.lda + k0 + c * 8);
     }
+    if constexpr (!DB) {
 #pragma unroll
-    for (int i = 0; i < LB; ++i) {
-      const int idx = tid + 256 * i, r = idx >> 3, c = idx & 7;
-      xb[i] = *(const u32x4_t*)(p.W + (size_t)min(n0 + r, p.N - 1) * p.K + k0 + c * 8);
+      for (int i = 0; i < LB; ++i) {
+        const int idx = tid + 256 * i, r = idx >> 3, c = idx & 7;
+        xb[i] = *(const u32x4_t*)(p.W + (size_t)min(n0 + r, p.N - 1) * p.K + k0 + c * 8);
+      }
+    }
+  };
+  auto dload = [&](bf16x8_t (&xd)[DB ? 2 : 1][DB ? FN : 1], int kt) {
+    if constexpr (DB) {
+      const int k0 = kbeg + kt * BK + fg * 8;
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) {
+          const int n = min(n0 + wn * TN + j * 16 + fr, p.N - 1);
+          xd[kk][j] = __builtin_nontemporal_load((const bf16x8_t*)(p.W + (size_t)n * p.K + k0 + kk * 32));
+        }
     }
   };
   auto lstore = [&](const u32x4_t (&xa)[LA], const u32x4_t (&xb)[LB], int buf) {
@@ -78,10 +100,12 @@ gemm_bf16_kernel(GemmArgs p) {
       const int idx = tid + 256 * i, r = idx >> 3, c = idx & 7;
       *(u32x4_t*)(sa + r * 128 + ((c ^ ((r >> 1) & 7)) << 4)) = xa[i];
     }
+    if constexpr (!DB) {
 #pragma unroll
-    for (int i = 0; i < LB; ++i) {
-      const int idx = tid + 256 * i, r = idx >> 3, c = idx & 7;
-      *(u32x4_t*)(sb + r * 128 + ((c ^ ((r >> 1) & 7)) << 4)) = xb[i];
+      for (int i = 0; i < LB; ++i) {
+        const int idx = tid + 256 * i, r = idx >> 3, c = idx & 7;
+        *(u32x4_t*)(sb + r * 128 + ((c ^ ((r >> 1) & 7)) << 4)) = xb[i];
+      }
     }
   };
 
@@ -97,41 +121,56 @@ gemm_bf16_kernel(GemmArgs p) {
 #pragma unroll
   for (int u = 0; u < PF; ++u) {
     gload(ra[u], rb[u], min(u, kl));
+    dload(rd[DB ? u : 0], min(u, kl));
     asm volatile("" ::: "memory");  // keep issue order = tile order (counted waits stay short)
   }
   if (nk > 0) lstore(ra[0], rb[0], 0);
   __syncthreads();
 
-  const int fr = lane & 15, fg = lane >> 4;
   for (int kt0 = 0; kt0 < nk; kt0 += PF) {
 #pragma unroll
     for (int u = 0; u < PF; ++u) {
       const int kt = kt0 + u;
       const int cur = kt & 1;
-      // slot u held tile kt, already copied to LDS: refill it PF tiles ahead
-      if (PF > 1 || kt + 1 < nk) gload(ra[u], rb[u], min(kt + PF, kl));
-      if (kt >= nk) continue;
-      const char* sa = smem + cur * (A_BYTES + B_BYTES);
-      const char* sb = sa + A_BYTES;
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk) {
-        const int c = kk * 4 + fg;
-        bf16x8_t af[FM], bfr[FN];
-#pragma unroll
-        for (int i = 0; i < FM; ++i) {
-          const int r = wm * TM + i * 16 + fr;
-          af[i] = *(const bf16x8_t*)(sa + r * 128 + ((c ^ ((r >> 1) & 7)) << 4));
-        }
-#pragma unroll
-        for (int j = 0; j < FN; ++j) {
-          const int r = wn * TN + j * 16 + fr;
-          bfr[j] = *(const bf16x8_t*)(sb + r * 128 + ((c ^ ((r >> 1) & 7)) << 4));
-        }
-#pragma unroll
-        for (int i = 0; i < FM; ++i)
-#pragma unroll
-          for (int j = 0; j < FN; ++j) acc[i][j] = mfma16(af[i], bfr[j], acc[i][j]);
+      // slot u held tile kt, already copied to LDS: refill it PF tiles ahead (DB: the W fragments
+      // of slot u are the MFMA operands of tile kt, refilled after the MFMAs below)
+      if constexpr (!DB) {
+        if (PF > 1 || kt + 1 < nk) gload(ra[u], rb[u], min(kt + PF, kl));
       }
+      if (kt < nk) {
+        const char* sa = smem + cur * (A_BYTES + B_BYTES);
+        const char* sb = sa + A_BYTES;
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) {
+          const int c = kk * 4 + fg;
+          bf16x8_t af[FM], bfr[FN];
+#pragma unroll
+          for (int i = 0; i < FM; ++i) {
+            const int r = wm * TM + i * 16 + fr;
+            af[i] = *(const bf16x8_t*)(sa + r * 128 + ((c ^ ((r >> 1) & 7)) << 4));
+          }
+#pragma unroll
+          for (int j = 0; j < FN; ++j) {
+            if constexpr (DB) {
+              bfr[j] = rd[DB ? u : 0][DB ? kk : 0][DB ? j : 0];
+            } else {
+              const int r = wn * TN + j * 16 + fr;
+              bfr[j] = *(const bf16x8_t*)(sb + r * 128 + ((c ^ ((r >> 1) & 7)) << 4));
+            }
+          }
+#pragma unroll
+          for (int i = 0; i < FM; ++i)
+#pragma unroll
+            for (int j = 0; j < FN; ++j) acc[i][j] = mfma16(af[i], bfr[j], acc[i][j]);
+        }
+      }
+      if constexpr (DB) {
+        if (PF > 1 || kt + 1 < nk) {
+          gload(ra[u], rb[u], min(kt + PF, kl));
+          dload(rd[DB ? u : 0], min(kt + PF, kl));
+        }
+      }
+      if (kt >= nk) continue;
       if (kt + 1 < nk) lstore(ra[(u + 1) % PF], rb[(u + 1) % PF], cur ^ 1);
       // LDS writes visible + buffer reads done; a raw barrier, NOT __syncthreads(): its fence
       // drains vmcnt and would cancel the PF - 1 tiles still in flight
@@ -454,17 +493,17 @@ static int launch_gemv(const GemmArgs& a, int epi, hipStream_t s) {
   return launch_gemv_ru<1>(a, epi, s);
 }
 
-template <int BM, int BN, int WM, int WN, int PF = 1>
+template <int BM, int BN, int WM, int WN, int PF = 1, bool DB = false>
 static int launch_tile(const GemmArgs& a, int epi, int splits, hipStream_t s) {
   const int ntm = (a.M + BM - 1) / BM, ntn = (a.N + BN - 1) / BN;
   dim3 grid(ntm * ntn, 1, splits), block(256);
   switch (splits > 1 ? (int)EPI_PARTIAL : epi) {
-    case EPI_NONE: gemm_bf16_kernel<BM, BN, WM, WN, EPI_NONE, PF><<<grid, block, 0, s>>>(a); break;
-    case EPI_BIAS: gemm_bf16_kernel<BM, BN, WM, WN, EPI_BIAS, PF><<<grid, block, 0, s>>>(a); break;
-    case EPI_GELU: gemm_bf16_kernel<BM, BN, WM, WN, EPI_GELU, PF><<<grid, block, 0, s>>>(a); break;
-    case EPI_SWIGLU: gemm_bf16_kernel<BM, BN, WM, WN, EPI_SWIGLU, PF><<<grid, block, 0, s>>>(a); break;
-    case EPI_RESID: gemm_bf16_kernel<BM, BN, WM, WN, EPI_RESID, PF><<<grid, block, 0, s>>>(a); break;
-    case EPI_PARTIAL: gemm_bf16_kernel<BM, BN, WM, WN, EPI_PARTIAL, PF><<<grid, block, 0, s>>>(a); break;
+    case EPI_NONE: gemm_bf16_kernel<BM, BN, WM, WN, EPI_NONE, PF, DB><<<grid, block, 0, s>>>(a); break;
+    case EPI_BIAS: gemm_bf16_kernel<BM, BN, WM, WN, EPI_BIAS, PF, DB><<<grid, block, 0, s>>>(a); break;
+    case EPI_GELU: gemm_bf16_kernel<BM, BN, WM, WN, EPI_GELU, PF, DB><<<grid, block, 0, s>>>(a); break;
+    case EPI_SWIGLU: gemm_bf16_kernel<BM, BN, WM, WN, EPI_SWIGLU, PF, DB><<<grid, block, 0, s>>>(a); break;
+    case EPI_RESID: gemm_bf16_kernel<BM, BN, WM, WN, EPI_RESID, PF, DB><<<grid, block, 0, s>>>(a); break;
+    case EPI_PARTIAL: gemm_bf16_kernel<BM, BN, WM, WN, EPI_PARTIAL, PF, DB><<<grid, block, 0, s>>>(a); break;
     default: return (int)hipErrorInvalidValue;
   }
   return (int)hipGetLastError();
@@ -473,10 +512,20 @@ static int launch_tile(const GemmArgs& a, int epi, int splits, hipStream_t s) {
 // Register prefetch depth of the decode tiles (64x128 / 32x128): 1, 2 or 4 (default 4);
 // da_set_gemm_pf for A/B runs.
 static int g_gemm_pf = 4;
-DA_EXPORT void da_set_gemm_pf(int v) { g_gemm_pf = (v == 1 || v == 2) ? v : 4; }
+DA_EXPORT void da_set_gemm_pf(int v) { g_gemm_pf = (v == 1 || v == 2 || v == 8) ? v : 4; }
+// Direct-B decode tiles (W fragments straight to registers, gemm_bf16_kernel DB): A/B switch.
+static int g_gemm_db = 0;
+DA_EXPORT void da_set_gemm_db(int v) { g_gemm_db = v; }
 
 template <int BM, int BN>
 static int launch_decode_tile(const GemmArgs& a, int epi, int splits, hipStream_t s) {
+  if (g_gemm_db) {
+    switch (g_gemm_pf) {
+      case 2: return launch_tile<BM, BN, 1, 4, 2, true>(a, epi, splits, s);
+      case 8: return launch_tile<BM, BN, 1, 4, 8, true>(a, epi, splits, s);
+      default: return launch_tile<BM, BN, 1, 4, 4, true>(a, epi, splits, s);
+    }
+  }
   switch (g_gemm_pf) {
     case 1: return launch_tile<BM, BN, 1, 4, 1>(a, epi, splits, s);
     case 2: return launch_tile<BM, BN, 1, 4, 2>(a, epi, splits, s);

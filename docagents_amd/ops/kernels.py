@@ -60,6 +60,7 @@ _SIGS = {
     "da_set_flash_qh": [c_int],
     "da_set_flash_pipe": [c_int],
     "da_set_gemm_pf": [c_int],
+    "da_set_gemm_db": [c_int],
     "da_set_gemv_u": [c_int],
     "da_set_gemv_ks": [c_int],
     "da_set_decode_pft": [c_int],

@@ -454,6 +454,16 @@ def check_xgmi_allreduce(rank, world, port, out_path):
     _done(rank, out_path, verdict)
 
 
+def check_xgmi_verify_and_time(rank, world, port, out_path):
+    """The cross-device check bench.py runs on multi-GPU nodes (xgmi_allreduce.verify_and_time),
+    rehearsed with ranks that may share one GPU."""
+    _init(rank, world, port)
+    from .xgmi_allreduce import verify_and_time
+    dev = torch.device("cuda", rank % torch.cuda.device_count())
+    torch.cuda.set_device(dev)
+    _done(rank, out_path, verify_and_time(None, dev, iters=10))
+
+
 def check_xgmi_allreduce_norm(rank, world, port, out_path):
     """C3 with the RMSNorm in the all-reduce's epilogue (one launch) vs the all-reduce kernel
     followed by the rmsnorm kernel: x and h must be BIT-identical, for several row widths / row

@@ -577,6 +577,39 @@ def test_gemm_decode_tile_prefetch(pf, tile, M, splits, Kd):
     _close(got, R.gemm(a, w, epi=K.EPI_RESID, resid=r), atol=0.03)
 
 
+@pytest.mark.parametrize("pf", [2, 4, 8])
+@pytest.mark.parametrize("tile,M", [(2, 64), (2, 40), (3, 17), (2, 130)])
+@pytest.mark.parametrize("splits,Kd,N", [(1, 64, 392), (1, 448, 392), (2, 768, 392), (4, 3072, 392), (3, 576, 392),
+                                         (2, 3072, 9216)])
+def test_gemm_decode_tile_direct_b(pf, tile, M, splits, Kd, N):
+    """Direct-B decode tiles (W fragments loaded straight into MFMA registers, no LDS hop) are
+    bit-identical to the LDS-staged tiles (same fragments, same MFMA order) for every epilogue
+    route (plain, residual, SwiGLU, split-K partials + reduce, the fused reduce + RMSNorm)."""
+    torch.manual_seed(pf * 100 + M + Kd)
+    a, w, r = _rand(M, Kd), _rand(N, Kd, scale=Kd ** -0.5), _rand(M, N)
+    g = _rand(N) + 1.0
+
+    def run():
+        o1 = K.gemm(a, w, epi=K.EPI_RESID, resid=r, tile=tile, splits=splits)
+        o2 = K.gemm(a, w, epi=K.EPI_SWIGLU, tile=tile, splits=splits) if N % 32 == 0 else None
+        x = r.clone()
+        h = K.gemm_resid_norm(a, w, x, g, 1e-5, out=x, tile=tile, splits=splits) if M <= 64 and N <= 8192 else None
+        return o1, o2, x, h
+
+    K.lib().da_set_gemm_pf(pf)
+    try:
+        base = run()
+        K.lib().da_set_gemm_db(1)
+        got = run()
+    finally:
+        K.lib().da_set_gemm_db(0)
+        K.lib().da_set_gemm_pf(4)
+    for b, o in zip(base, got):
+        if b is not None:
+            assert torch.equal(b, o)
+    _close(got[0], R.gemm(a, w, epi=K.EPI_RESID, resid=r), atol=0.03)
+
+
 @pytest.mark.parametrize("M", [65, 128, 261, 1023])
 def test_gemm_mid_m(M):
     """65..1023 rows (mid-size decode batches, short prefills) on the in-tree tiles (plain, residual

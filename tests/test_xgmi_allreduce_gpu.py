@@ -39,6 +39,15 @@ def test_xgmi_allreduce_rmsnorm_bit_identical_to_unfused(tmp_path):
     assert len(v["cases"]) >= 12
 
 
+def test_bench_xgmi_cross_device_check_passes(tmp_path):
+    """bench.py's multi-GPU C3 check (exact sums one-/two-shot, fused norm bit identity, timing)."""
+    out = tmp_path / "vt.json"
+    mp.spawn(selftest.check_xgmi_verify_and_time, args=(2, _port(), str(out)), nprocs=2, join=True)
+    v = json.loads(out.read_text())
+    assert v["ok"] and v["fused_norm_bit_identical"] and len(v["cases"]) == 3, v
+    assert any(c["twoshot"] for c in v["cases"]) and v["us_per_call_64x3072_xgmi"] > 0
+
+
 def _tp_ok(v) -> bool:
     return (v["max_logit_diff"] < 0.05 and v["checked"] >= 0.6 * v["decisions"]
             and v["checked_agree"] == v["checked"] and all(v["prefix_ok"]) and v["max_prob_diff"] < 1e-3)
