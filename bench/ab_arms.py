@@ -23,7 +23,10 @@ from docagents_amd.ops import kernels as K  # noqa: E402
 
 ENV_SETTERS = {
     "DA_GEMM_PF": "da_set_gemm_pf",          # decode-tile k-tiles in flight
+    "DA_DK_RB": "da_set_dk_rb",              # gemm_dk 33..64 rows: two 32-row blocks (1) / one 64-row block (0)
     "DA_GEMM_DB": "da_set_gemm_db",          # decode tiles load W fragments straight to registers
+    "DA_DECODE_BALANCE": "da_set_decode_balance",  # decode attention: balanced vs fixed keys per split
+    "DA_DECODE_QFIRST": "da_set_decode_qfirst",    # batch-1 decode attention: prologue loads before K/V
     "DA_FLASH_PIPE": "da_set_flash_pipe",    # software-pipelined flash prefill on / off / auto
     "DA_FLASH_QH": "da_set_flash_qh",        # flash queries per wave: 1 = 32, 2 = 64
     "DA_FLASH_WAVES": "da_set_flash_waves",  # flash waves per workgroup
@@ -38,6 +41,9 @@ def apply_env_overrides() -> dict:
     """Push every DA_* schedule override present in the environment into the library."""
     L = K.lib()
     done = {}
+    if os.environ.get("DA_DECODE_DK") is not None:  # decode GEMMs: gemm_dk (1) vs split-K tiles (0)
+        K.DECODE_DK = os.environ["DA_DECODE_DK"] != "0"
+        done["DA_DECODE_DK"] = int(K.DECODE_DK)
     for env, fn in ENV_SETTERS.items():
         v = os.environ.get(env)
         if v is not None:

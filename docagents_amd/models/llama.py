@@ -311,6 +311,8 @@ class LlamaDecoder:
         c, o, cache = self.cfg, self.ops, self.cache
         D, hl, kl = c.head_dim, self.hl, self.kl
         x = o.embed(st.tokens, self.w["embed"], out=st.x)
+        if self._dk_decode(x.shape[0]):
+            return self._decode_step_dk(st, x)
         if self._norm_fusable(x.shape[0]):
             return self._decode_step_fused_norms(st, x)
         if self.tp.size > 1 and x.shape[0] > 1:
@@ -348,6 +350,39 @@ class LlamaDecoder:
         projection before it (gemm_resid_norm), so a layer is 2 GEMM+reduce pairs, 2 plain GEMMs,
         RoPE/cache and attention — no standalone norm launches."""
         return self.tp.size == 1 and 1 < B <= 64 and self.cfg.hidden <= 8192 and self.cfg.hidden % 8 == 0
+
+    def _dk_decode(self, B: int) -> bool:
+        """Batched decode (2 <= B <= 64, no TP) on gemm_dk: every projection one launch without
+        split-K partials, the RMSNorms deferred into the consuming GEMM (needs folded gains)."""
+        o, c = self.ops, self.cfg
+        f = getattr(o, "dk_fusable", None)
+        if f is None or self.tp.size != 1 or not self.unit_gains or not 2 <= B <= 64:
+            return False
+        L = self.w["layers"][0]
+        shapes = [(L["wqkv"], EPI_NONE), (L["wo"], EPI_RESID), (L["w_gu"], EPI_SWIGLU), (L["w_down"], EPI_RESID),
+                  (self.w["lm_head"], EPI_NONE)]
+        return all(f(B, w.shape[0], w.shape[1], e) for w, e in shapes) and o.dk_parts(c.hidden) <= 512
+
+    def _decode_step_dk(self, st: "DecodeState", x: torch.Tensor) -> torch.Tensor:
+        """A layer = QKV, attention, O (+ residual, row sums of squares), gate/up + SwiGLU (norm
+        deferred from those sums), down (+ residual, sums): 5 launches, no reduce launches, no
+        standalone norms after layer 0's input norm."""
+        c, o = self.cfg, self.ops
+        layers = self.w["layers"]
+        sa, sb = st.ssq
+        parts = o.dk_parts(c.hidden)
+        a_in, norm = o.rmsnorm(x, layers[0]["ln_attn"], c.eps, out=st.h), None
+        for li, L in enumerate(layers):
+            qkv = o.gemm_dk(a_in, L["wqkv"], out=st.qkv, norm_in=norm)
+            a = self._decode_attn(qkv, li, st)
+            o.gemm_dk(a, L["wo"], epi=EPI_RESID, resid=x, out=x, ssq_out=sa)               # x += o
+            g = o.gemm_dk(x, L["w_gu"], epi=EPI_SWIGLU, norm_in=(sa, parts, c.eps))        # norm(x) -> gate/up
+            o.gemm_dk(g, L["w_down"], epi=EPI_RESID, resid=x, out=x, ssq_out=sb)           # x += mlp
+            a_in, norm = x, (sb, parts, c.eps)
+        o.gemm_dk(x, self.w["lm_head"], out=st.logits, norm_in=norm)                      # final norm deferred
+        o.sample(st.logits, st.temperature, st.seed, 0, out_tok=st.tokens, out_lp=st.lp, conf=st.conf,
+                 active=st.active, ctr=st.pos, pos=st.pos, lens=st.lens, hist=st.hist, start=st.start, eos=st.eos)
+        return st.tokens
 
     def _decode_step_fused_norms(self, st: "DecodeState", x: torch.Tensor) -> torch.Tensor:
         c, o, cache = self.cfg, self.ops, self.cache
@@ -427,6 +462,8 @@ class DecodeState:
         self.qkv = torch.zeros(B, (model.hl + 2 * model.kl) * c.head_dim, dtype=torch.bfloat16, device=dev)
         self.attn = torch.zeros(B, model.hl * c.head_dim, dtype=torch.bfloat16, device=dev)
         self.logits = torch.zeros(B, c.vocab // model.tp.size, dtype=torch.bfloat16, device=dev)  # this rank's slice
+        # gemm_dk deferred-norm partial sums [parts, 64] (a tuple: shared as-is by row views)
+        self.ssq = tuple(torch.zeros(512 * 64, dtype=torch.float32, device=dev) for _ in range(2))
         self.temperature, self.seed, self.eos = temperature, seed, tuple(eos)[:4]
         self.graph = None
 

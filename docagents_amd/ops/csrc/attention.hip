@@ -537,6 +537,17 @@ flash_attn_pipe_kernel(const bf16_t* __restrict__ q, const bf16_t* __restrict__ 
 // (b, kv head) to finish (atomic ticket in cnt[b * Hkv + hk], reset by that split so the counters
 // are zero again for the next launch / graph replay) merges all splits of its G heads — the
 // separate combine launch (~5 us per layer, most of a batch-1 decode attention) is gone.
+// Keys per split of a row. The grid's split count is fixed at capture (sized for the cache
+// capacity, max_len), but a row holds L <= max_len keys: balanced splits (the default) spread the
+// row's L keys over ALL its splits (64-key multiples) instead of filling the first ceil(L / chunk)
+// and leaving the rest idle — at batch 1 and 2.9k of 4k keys, 256 working workgroups instead of 192.
+// chunk_arg < 0 (da_set_decode_balance(0), A/B): fixed -chunk_arg keys per split.
+__device__ __forceinline__ int dec_chunk(int L, int nsplit, int chunk_arg) {
+  if (chunk_arg < 0) return -chunk_arg;
+  const int c = ((L + nsplit - 1) / nsplit + 63) & ~63;
+  return c < chunk_arg ? c : chunk_arg;
+}
+
 __device__ __forceinline__ void dec_store(float o, float M, float ls, int b, int h, int d, int H, int nsplit,
                                           int split, int D, float* po, float* pm, float* pl, bf16_t* out,
                                           int ldo) {
@@ -623,7 +634,7 @@ __global__ void __launch_bounds__(256)
 decode_attn_kernel(const bf16_t* __restrict__ q, int ldq, const bf16_t* __restrict__ kc,
                    const bf16_t* __restrict__ vc, const int* __restrict__ lens, const int* __restrict__ slot,
                    const int* __restrict__ pre,
-                   int H, int Hkv, int max_seq, int chunk, int nsplit, float scale_log2e,
+                   int H, int Hkv, int max_seq, int chunk_max, int nsplit, float scale_log2e,
                    float* __restrict__ po, float* __restrict__ pm, float* __restrict__ pl,
                    bf16_t* __restrict__ out, int ldo, int* __restrict__ cnt, DecRope rope) {
   constexpr int KT = 64;
@@ -650,6 +661,7 @@ decode_attn_kernel(const bf16_t* __restrict__ q, int ldq, const bf16_t* __restri
   stamp(0);
   const int L = lens[b];
   DA_ASSERT(L >= 0 && L <= max_seq && slot[b] >= 0);
+  const int chunk = dec_chunk(L, nsplit, chunk_max);
   const int kstart = split * chunk;
   const bool fr = rope.cs != nullptr;
   const bool own_new = fr && kstart <= L - 1 && L - 1 < kstart + chunk;  // this split holds key L-1
@@ -729,6 +741,9 @@ decode_attn_kernel(const bf16_t* __restrict__ q, int ldq, const bf16_t* __restri
     const bf16_t* kr = fr ? q + (size_t)b * ldq + (size_t)(H + hk) * D : hp;
     const bf16_t* vr = fr ? q + (size_t)b * ldq + (size_t)(H + Hkv + hk) * D : hp;
     const bf16_t rk1 = kr[d & ~1], rk2 = kr[d | 1], nv = vr[d];
+    // VAR bit 4: the prologue operands land BEFORE this workgroup's K/V requests join the chip-wide
+    // flood (otherwise they queue behind other workgroups' tiles: 3.6 us at batch 1, decode_trace)
+    if constexpr ((VAR & 16) != 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const int t0 = kstart + w * KT, t1 = t0 + 4 * KT;
     load_k(ka, t0); load_v(va, t0);
     load_k(kb2, t1); load_v(vb2, t1);
@@ -1005,7 +1020,7 @@ __global__ void __launch_bounds__(256)
 decode_attn_gqa_kernel(const bf16_t* __restrict__ q, int ldq, const bf16_t* __restrict__ kc,
                        const bf16_t* __restrict__ vc, const int* __restrict__ lens, const int* __restrict__ slot,
                    const int* __restrict__ pre,
-                       int H, int Hkv, int max_seq, int chunk, int nsplit, float scale_log2e,
+                       int H, int Hkv, int max_seq, int chunk_max, int nsplit, float scale_log2e,
                        float* __restrict__ po, float* __restrict__ pm, float* __restrict__ pl,
                        bf16_t* __restrict__ out, int ldo, int* __restrict__ cnt) {
   static_assert(D == 64 || D == 128, "GQA MFMA decode supports head dims 64 and 128");
@@ -1019,6 +1034,7 @@ decode_attn_gqa_kernel(const bf16_t* __restrict__ q, int ldq, const bf16_t* __re
   const int split = blockIdx.x, hk = blockIdx.y, b = blockIdx.z;
   const int L = lens[b];
   DA_ASSERT(L >= 0 && L <= max_seq && slot[b] >= 0);
+  const int chunk = dec_chunk(L, nsplit, chunk_max);
   const int kstart = split * chunk;
   const int kend = min(L, kstart + chunk);
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -1188,6 +1204,10 @@ static int launch_decode_v(int G, dim3 grid, hipStream_t s, const bf16_t* q, int
 // GQA groups (G >= 2) take the MFMA kernel: 1.8x (Llama-3-8B, G=4) to 5x (Llama-3-70B TP=8, G=8)
 // over the VALU path (profiles/decode_attn_gqa_mfma_r1.json). da_set_gqa_mfma(0) selects the VALU
 // path (kept for A/B measurements and as the numerics cross-check in tests).
+static int g_dec_qfirst = 0;  // prefetch variant: prologue operands before the K/V stream (A/B)
+DA_EXPORT void da_set_decode_qfirst(int v) { g_dec_qfirst = v; }
+static int g_dec_balance = 1;  // balanced splits (dec_chunk); 0 = fixed chunk per split (A/B)
+DA_EXPORT void da_set_decode_balance(int v) { g_dec_balance = v; }
 static int g_gqa_mfma = 1;
 DA_EXPORT void da_set_gqa_mfma(int v) { g_gqa_mfma = v; }
 // MHA decode with the next tile prefetched (VAR bit 2) when B * Hkv <= this (0 = never).
@@ -1215,6 +1235,8 @@ static int launch_decode(int G, dim3 grid, hipStream_t s, const bf16_t* q, int l
         return launch_decode_v<D, 15>(G, grid, s, q, ldq, kc, vc, lens, slot, pre, H, Hkv, max_seq, chunk, nsplit, sl2e, po, pm, pl, out, ldo, cnt, r);
       }
     }
+    if (g_dec_pft && (int)(grid.y * grid.z) <= g_dec_pft && g_dec_qfirst)
+      return launch_decode_v<D, 23>(G, grid, s, q, ldq, kc, vc, lens, slot, pre, H, Hkv, max_seq, chunk, nsplit, sl2e, po, pm, pl, out, ldo, cnt, rope);
     if (g_dec_pft && (int)(grid.y * grid.z) <= g_dec_pft)  // few (row, kv head) pairs: latency-bound
       return launch_decode_v<D, 7>(G, grid, s, q, ldq, kc, vc, lens, slot, pre, H, Hkv, max_seq, chunk, nsplit, sl2e, po, pm, pl, out, ldo, cnt, rope);
     return launch_decode_v<D, 3>(G, grid, s, q, ldq, kc, vc, lens, slot, pre, H, Hkv, max_seq, chunk, nsplit, sl2e, po, pm, pl, out, ldo, cnt, rope);
@@ -1263,6 +1285,7 @@ DA_EXPORT int da_decode_attn(const void* q, int ldq, const void* k_cache, const 
     return (int)hipErrorInvalidValue;
   const DecRope rope{(bf16_t*)k_cache, (bf16_t*)v_cache, (const float*)cos_sin, (const int*)pos, nullptr};
   if (B == 0) return 0;
+  if (!g_dec_balance) chunk = -chunk;  // kernels: negative = fixed keys per split (dec_chunk)
   const int G = H / Hkv;
   float* po = (float*)ws;
   float* pm = po + (size_t)B * H * nsplit * D;

@@ -83,12 +83,13 @@ gemm_bf16_kernel(GemmArgs p) {
   auto dload = [&](bf16x8_t (&xd)[DB ? 2 : 1][DB ? FN : 1], int kt) {
     if constexpr (DB) {
       const int k0 = kbeg + kt * BK + fg * 8;
+      // the two k halves of a row's 128-B line back to back (one line, two 64-B requests)
 #pragma unroll
-      for (int kk = 0; kk < 2; ++kk)
+      for (int j = 0; j < FN; ++j)
 #pragma unroll
-        for (int j = 0; j < FN; ++j) {
+        for (int kk = 0; kk < 2; ++kk) {
           const int n = min(n0 + wn * TN + j * 16 + fr, p.N - 1);
-          xd[kk][j] = __builtin_nontemporal_load((const bf16x8_t*)(p.W + (size_t)n * p.K + k0 + kk * 32));
+          xd[kk][j] = *(const bf16x8_t*)(p.W + (size_t)n * p.K + k0 + kk * 32);
         }
     }
   };

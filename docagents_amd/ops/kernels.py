@@ -61,6 +61,12 @@ _SIGS = {
     "da_set_flash_pipe": [c_int],
     "da_set_gemm_pf": [c_int],
     "da_set_gemm_db": [c_int],
+    "da_set_decode_balance": [c_int],
+    "da_gemm_dk": [c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
+                   c_int, c_void_p, c_int, c_int, c_float, c_void_p, c_void_p],
+    "da_gemm_dk_parts": [c_int],
+    "da_set_dk_rb": [c_int],
+    "da_set_decode_qfirst": [c_int],
     "da_set_gemv_u": [c_int],
     "da_set_gemv_ks": [c_int],
     "da_set_decode_pft": [c_int],
@@ -218,6 +224,8 @@ def gemm(a: torch.Tensor, w: torch.Tensor, bias=None, epi: int = EPI_NONE, resid
         ldr = resid.stride(0)
     if M == 0:
         return out
+    if (tile == 12 or (tile == 0 and splits <= 0)) and rms is None and dk_fusable(M, N, K, epi):
+        return gemm_dk(a, w, epi=epi, bias=bias, resid=resid, out=out)
     if tile == 0 and splits <= 0 and gemv_fusable(M, N, K, epi):
         tile, splits = 6, 1  # batch-1 decode: weight-streaming GEMV, one launch, no split-K workspace
     gamma, eps = (None, 0.0) if rms is None else rms  # rms = (gain or None for unit gain, eps > 0)
@@ -236,6 +244,58 @@ def gemm(a: torch.Tensor, w: torch.Tensor, bias=None, epi: int = EPI_NONE, resid
     rc = lib().da_gemm_bf16(_ptr(a), a.stride(0), _ptr(w), _ptr(out), out.stride(0), _ptr(bias), _ptr(resid), ldr,
                             M, N, K, epi, tile, splits, _ptr(ws), _ptr(gamma), float(eps), _stream())
     _check(rc, "gemm")
+    return out
+
+
+# Decode GEMMs with 2..64 rows: gemm_dk (csrc/gemm_dk.hip: K split across the 4 waves of a
+# workgroup and summed through LDS, no split-K partials, no reduce launch). False: the 64x128 /
+# 32x128 tiles + split-K + reduce (bench/ab_arms.py DA_DECODE_DK=0).
+DECODE_DK = True
+# above 32 rows the split-K tiles stay faster (bench/midm_chain.py, profiles/r3/dk/): the narrow
+# dk tiles re-read the activation block once per 16-64 weight rows
+DK_MAX_M = 32
+
+
+def dk_fusable(M: int, N: int, K: int, epi: int = EPI_NONE) -> bool:
+    """True when gemm() runs a decode-sized product on gemm_dk (no split-K)."""
+    return (DECODE_DK and 2 <= M <= DK_MAX_M and K % 256 == 0 and N % 16 == 0
+            and epi in (EPI_NONE, EPI_BIAS, EPI_RESID, EPI_SWIGLU) and (epi != EPI_SWIGLU or N % 32 == 0))
+
+
+def dk_parts(N: int) -> int:
+    """Row-norm partial sums an EPI_RESID gemm_dk of width N writes (the consumer's part count)."""
+    return int(lib().da_gemm_dk_parts(N))
+
+
+def gemm_dk(a, w, epi: int = EPI_NONE, bias=None, resid=None, out=None, norm_in=None, ssq_out=None):
+    """Decode-sized product (1 <= M <= 64) in one launch without split-K:
+    out = epi(rownorm(a) @ w^T). norm_in = (ssq, parts, eps): ``a`` is the raw residual stream and
+    each row is scaled by rsqrt(sum of ssq[:parts, row] / K + eps) first (bf16-rounded, as the
+    rmsnorm kernel would; RMSNorm gains folded into w). ssq_out (EPI_RESID only): fp32
+    [dk_parts(N), 64] receives the per-part sums of squares of the new rows, for the next consumer."""
+    _bf16_cuda(a, "a"); _bf16_cuda(w, "w")
+    M, K = a.shape
+    N = w.shape[0]
+    _req(1 <= M <= 64 and K % 256 == 0 and N % 16 == 0 and w.shape[1] == K, f"gemm_dk shape M={M} N={N} K={K}")
+    _req(a.stride(1) == 1 and a.stride(0) % 8 == 0 and w.is_contiguous(), "gemm_dk layout")
+    _req(a.data_ptr() % 16 == 0 and w.data_ptr() % 16 == 0, "operands must be 16-B aligned")
+    nout = N // 2 if epi == EPI_SWIGLU else N
+    if out is None:
+        out = torch.empty((M, nout), dtype=torch.bfloat16, device=a.device)
+    _req(out.shape == (M, nout) and out.stride(1) == 1 and out.stride(0) % 8 == 0, "bad out")
+    ldr = 0
+    if epi == EPI_RESID:
+        _req(resid is not None and resid.shape == (M, N) and resid.stride(1) == 1 and resid.stride(0) % 8 == 0,
+             "bad resid")
+        ldr = resid.stride(0)
+    ssq, parts, eps = (None, 0, 0.0) if norm_in is None else norm_in
+    if ssq is not None:
+        _req(ssq.dtype == torch.float32 and ssq.is_contiguous() and ssq.numel() >= parts * 64, "bad ssq_in")
+    if ssq_out is not None:
+        _req(epi == EPI_RESID and ssq_out.dtype == torch.float32 and ssq_out.is_contiguous()
+             and ssq_out.numel() >= dk_parts(N) * 64, "bad ssq_out")
+    _check(lib().da_gemm_dk(_ptr(a), a.stride(0), _ptr(w), _ptr(out), out.stride(0), _ptr(bias), _ptr(resid), ldr,
+                            M, N, K, epi, _ptr(ssq), parts, K, float(eps), _ptr(ssq_out), _stream()), "gemm_dk")
     return out
 
 

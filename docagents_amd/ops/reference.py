@@ -436,6 +436,41 @@ def quant_weight_fp8(w):
     return (wf / sw[:, None]).clamp(-448, 448).to(torch.float8_e4m3fn).contiguous(), sw.contiguous()
 
 
+DECODE_DK = True
+# above 32 rows the split-K tiles stay faster (bench/midm_chain.py, profiles/r3/dk/): the narrow
+# dk tiles re-read the activation block once per 16-64 weight rows
+DK_MAX_M = 32
+
+
+def dk_fusable(M, N, K, epi=EPI_NONE):
+    return (DECODE_DK and 2 <= M <= DK_MAX_M and K % 256 == 0 and N % 16 == 0
+            and epi in (EPI_NONE, EPI_BIAS, EPI_RESID, EPI_SWIGLU) and (epi != EPI_SWIGLU or N % 32 == 0))
+
+
+def dk_parts(N):
+    """gemm_dk.hip dk_bn for EPI_RESID: row-norm partial sums written per output tile."""
+    bn = 64 if N // 64 >= 192 else (32 if N // 32 >= 192 else 16)
+    return (N + bn - 1) // bn
+
+
+def gemm_dk(a, w, epi=EPI_NONE, bias=None, resid=None, out=None, norm_in=None, ssq_out=None):
+    """gemm_dk.hip: optional deferred row RMSNorm of ``a`` from partial sums of squares, then the
+    product + epilogue; EPI_RESID may also emit the new rows' per-part sums of squares."""
+    M, K = a.shape
+    N = w.shape[0]
+    x = a.float()
+    if norm_in is not None:
+        ssq, parts, eps = norm_in
+        inv = torch.rsqrt(ssq.view(-1, 64)[:parts, :M].sum(0) / K + eps)
+        x = (x * inv[:, None]).to(torch.bfloat16).float()
+    y = _epilogue(x @ w.float().t(), N, bias, epi, resid, out)
+    if ssq_out is not None:
+        parts = dk_parts(N)
+        sq = y.float().pow(2).view(M, parts, N // parts).sum(-1)
+        ssq_out.view(-1, 64)[:parts, :M] = sq.t()
+    return y
+
+
 def gemm_resid_norm(a, w, resid, gamma, eps, out=None, h_out=None, bias=None):
     y = gemm(a, w, bias=bias, epi=EPI_RESID, resid=resid)
     (resid if out is None else out).copy_(y)

@@ -275,6 +275,34 @@ def test_decode_attn_prefetch_variant(D, B, chunk):
     _close(outs[1], outs[0], atol=0.01)
 
 
+@pytest.mark.parametrize("H,Hkv,D", [(32, 32, 96), (32, 8, 128), (8, 2, 64)])
+@pytest.mark.parametrize("rope", [False, True])
+def test_decode_attn_balanced_splits(H, Hkv, D, rope):
+    """Balanced splits (a row's L keys spread over every split of the capacity-sized grid) and the
+    fixed-chunk layout both match the fp32 reference, including rows shorter than one split, rows
+    on a split boundary and a shared prefix, with the in-kernel merge (fused RoPE: MHA only)."""
+    if rope and H != Hkv:
+        pytest.skip("fused RoPE decode is MHA only")
+    torch.manual_seed(H + D + rope)
+    max_seq = 4096
+    lens_l = [2935, 1, 512, 4000, 63]
+    B = len(lens_l)
+    kc, vc = _rand(B + 2, Hkv, max_seq, D), _rand(B + 2, Hkv, max_seq, D)
+    q = _rand(B, (H + 2 * Hkv) * D)
+    lens = torch.tensor(lens_l, dtype=torch.int32, device=DEV)
+    slot = torch.arange(B, dtype=torch.int32, device=DEV) + 1
+    cs = R.rope_table(max_seq, D, 10000.0, device=DEV)
+    rp = (cs, lens - 1) if rope else None
+    ref = R.decode_attn(q.clone(), kc.clone(), vc.clone(), lens, slot, H, Hkv, D, rope=rp)
+    for bal in (1, 0):
+        K.lib().da_set_decode_balance(bal)
+        try:
+            got = K.decode_attn(q, kc.clone(), vc.clone(), lens, slot, H, Hkv, D, max_len=max_seq, chunk=512, rope=rp)
+        finally:
+            K.lib().da_set_decode_balance(1)
+        _close(got, ref, atol=0.02)
+
+
 @pytest.mark.parametrize("H,Hkv,D", [(32, 32, 96), (32, 8, 128), (8, 1, 128), (12, 6, 64)])
 def test_decode_attn(H, Hkv, D):
     torch.manual_seed(H * D)
@@ -684,3 +712,47 @@ def test_decode_attn_split_merge(fused, monkeypatch):
     ref = R.decode_attn(q, kc, vc, lens, slot, H, Hkv, D)
     for ch in (64, 512, 1152):
         _close(K.decode_attn(q, kc, vc, lens, slot, H, Hkv, D, max_len=S, chunk=ch), ref, atol=0.02)
+
+
+@pytest.mark.parametrize("M", [2, 16, 17, 33, 64])
+@pytest.mark.parametrize("N,Kd,epi", [(9216, 3072, 0), (3072, 3072, 4), (16384, 3072, 3), (3072, 8192, 4),
+                                      (32064, 3072, 0), (512, 256, 1), (1024, 512, 3)])
+def test_gemm_dk_matches_reference(M, N, Kd, epi):
+    """gemm_dk (K split inside the workgroup, no split-K partials) == the fp32 reference for every
+    epilogue and tile width (BN 16 / 32 / 64 from N), ragged M."""
+    torch.manual_seed(M * 7 + N + Kd)
+    a, w = _rand(M, Kd), _rand(N, Kd, scale=Kd ** -0.5)
+    bias = _rand(N) if epi == 1 else None
+    r = _rand(M, N) if epi == 4 else None
+    got = K.gemm_dk(a, w, epi=epi, bias=bias, resid=r)
+    _close(got, R.gemm(a, w, bias=bias, epi=epi, resid=r), atol=0.03)
+    if K.dk_fusable(M, N, Kd, epi):  # the auto route of gemm() takes gemm_dk for 2..32 rows
+        assert torch.equal(K.gemm(a, w, epi=epi, resid=r, bias=bias), got)
+
+
+@pytest.mark.parametrize("M", [3, 16, 40, 64])
+@pytest.mark.parametrize("H,F", [(3072, 8192), (4096, 14336)])
+def test_gemm_dk_deferred_norm_chain(M, H, F):
+    """Producer (EPI_RESID + per-part sums of squares) -> consumer (deferred RMSNorm of its A rows)
+    == residual add, rmsnorm kernel, plain GEMM; the sums match the fp32 row sums."""
+    torch.manual_seed(M + H)
+    a, wo = _rand(M, H), _rand(H, H, scale=H ** -0.5)
+    x = _rand(M, H)
+    wgu = _rand(2 * F, H, scale=H ** -0.5)
+    x_ref = x.clone()
+    ssq = torch.zeros(512 * 64, dtype=torch.float32, device=DEV)
+    parts = K.dk_parts(H)
+    K.gemm_dk(a, wo, epi=K.EPI_RESID, resid=x, out=x, ssq_out=ssq)
+    y = R.gemm(a, wo, epi=K.EPI_RESID, resid=x_ref)
+    _close(x, y, atol=0.03)
+    sums = ssq.view(-1, 64)[:parts, :M].sum(0)
+    _close(sums, x.float().pow(2).sum(-1), atol=1e-2 * H, rtol=1e-3)
+    g = K.gemm_dk(x, wgu, epi=K.EPI_SWIGLU, norm_in=(ssq, parts, 1e-5))
+    h = K.rmsnorm(x, torch.ones(H, dtype=torch.bfloat16, device=DEV), 1e-5)
+    _close(g, R.gemm(h, wgu, epi=K.EPI_SWIGLU), atol=0.03)
+    # R.gemm_dk (the CPU model path) agrees with the kernel
+    ssq_r = torch.zeros_like(ssq)
+    x2 = x_ref.clone()
+    R.gemm_dk(a, wo, epi=K.EPI_RESID, resid=x2, out=x2, ssq_out=ssq_r)
+    _close(ssq_r.view(-1, 64)[:parts, :M], ssq.view(-1, 64)[:parts, :M], atol=0.5, rtol=2e-2)
+    _close(R.gemm_dk(x, wgu, epi=K.EPI_SWIGLU, norm_in=(ssq, parts, 1e-5)), g, atol=0.03)
