@@ -16,6 +16,7 @@ from __future__ import annotations
 
 import json
 import os
+import socket
 
 import numpy as np
 import torch
@@ -234,8 +235,19 @@ def check_replicas(rank, world, port, out_path, tp: int = 1):
         faults.configure_delay({"engine.tick": float(os.environ.get("DA_TEST_SLOW_TICK", "3.0"))})
     plane = SearchPlane(eng.index, rank, world, plane_ctrl, plane_data).start()
     grp = EngineGroup(eng, rank, world, rep_ctrl, rep_data, tp_size=tp, plane=plane)
-    base = port + 1
-    urls = [f"tcp://127.0.0.1:{base + r}" for r in range(replicas)]
+    # replica endpoints: free ports picked by rank 0 (neighbours of the rendezvous port may already
+    # be taken by the process group's own connections)
+    ports = [0] * replicas
+    if rank == 0:
+        socks = [socket.socket() for _ in range(replicas)]
+        for sk in socks:
+            sk.bind(("127.0.0.1", 0))
+        ports = [sk.getsockname()[1] for sk in socks]
+        for sk in socks:
+            sk.close()
+    box = [ports]
+    dist.broadcast_object_list(box, src=0)
+    urls = [f"tcp://127.0.0.1:{p}" for p in box[0]]
     done_flag = out_path + ".done"
     if not grp.is_leader:
         grp.follower_loop()
