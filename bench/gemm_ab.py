@@ -99,10 +99,11 @@ def perf():
         w = ((torch.rand(N, Kd, device="cuda") * 2 - 1) * Kd ** -0.5).bfloat16()
         out = torch.empty(M, N // 2 if epi == "swiglu" else N, device="cuda", dtype=torch.bfloat16)
         flop = 2 * M * N * Kd
+        resid = (torch.rand(M, N, device="cuda") - 0.5).bfloat16() if epi == "resid" else None
         res = {a: [] for a in ARMS}
         for _ in range(ROUNDS):
             for a in ARMS:
-                res[a].append(round(rate(lambda: call(a, x, w, out, EPI[epi]), flop), 1))
+                res[a].append(round(rate(lambda: call(a, x, w, out, EPI[epi], resid=resid), flop), 1))
         print(json.dumps({"shape": [M, N, Kd, epi], **{a: max(v) for a, v in res.items()},
                           "rounds": res}), flush=True)
 

@@ -204,8 +204,8 @@ gemm_dk_kernel(DkArgs p) {
                          red[3][m][gc + 16 + e];
         v[e] = silu(gt) * up;
       }
-      if (m < Mb) {
-        const int oc = n0 / 2 + 16 * g + 8 * hh;
+      const int oc = n0 / 2 + 16 * g + 8 * hh;
+      if (m < Mb && oc < p.N / 2) {  // a ragged last tile (N % BN == 32) holds one gate/up group
         *(u32x4_t*)(p.C + (size_t)(m0 + m) * p.ldc + oc) =
             u32x4_t{pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3]), pack_bf2(v[4], v[5]), pack_bf2(v[6], v[7])};
       }

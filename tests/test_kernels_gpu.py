@@ -716,7 +716,7 @@ def test_decode_attn_split_merge(fused, monkeypatch):
 
 @pytest.mark.parametrize("M", [2, 16, 17, 33, 64])
 @pytest.mark.parametrize("N,Kd,epi", [(9216, 3072, 0), (3072, 3072, 4), (16384, 3072, 3), (3072, 8192, 4),
-                                      (32064, 3072, 0), (512, 256, 1), (1024, 512, 3)])
+                                      (32064, 3072, 0), (512, 256, 1), (1024, 512, 3), (12320, 512, 3)])
 def test_gemm_dk_matches_reference(M, N, Kd, epi):
     """gemm_dk (K split inside the workgroup, no split-K partials) == the fp32 reference for every
     epilogue and tile width (BN 16 / 32 / 64 from N), ragged M."""
