@@ -81,6 +81,9 @@ class Config:
     engine_cb_max_steps: int = field(default=16, metadata={"env": "ENGINE_CB_MAX_STEPS"})
     # CUs reserved for the latency lanes (query embeds + search plane); 0 = no partition
     engine_latency_cus: int = field(default=0, metadata={"env": "ENGINE_LATENCY_CUS"})
+    # the decode scheduler pauses between steps while question embeds run on the fast lane (their
+    # ~100 encoder launches then find free CUs instead of queueing behind decode replays)
+    engine_fast_yield: bool = field(default=False, metadata={"env": "ENGINE_FAST_YIELD"})
     engine_admit_tokens: int = field(default=0, metadata={"env": "ENGINE_ADMIT_TOKENS"})  # 0 -> 4 prefill chunks
     # --- new keys: durable vector shards (index/wal.py) ---
     index_dir: str = field(default="", metadata={"env": "INDEX_DIR"})  # "" -> DATA_DIR/index; "none" -> off

@@ -257,7 +257,7 @@ class EngineServer:
                  hard_timeout_s: float = 0.0, liveness_s: float = 30.0, profiler: StepProfiler | None = None,
                  continuous: bool = False, cb_steps: int = 1, checkpoint_s: float = 0.0,
                  cb_window_s: float = 0.003, fast_embed_max: int = 8, urls: list[str] | None = None,
-                 cb_max_steps: int = 16, lanes=None):
+                 cb_max_steps: int = 16, lanes=None, fast_yield: bool = False):
         self.group, self.log = group, log
         self.urls = urls or []  # every replica's listen URL (topology RPC), replica order
         # the fast lane: query-sized embeds on their own thread / high-priority stream / workspace
@@ -268,6 +268,12 @@ class EngineServer:
         self._fast_q: list = []
         self._fast_wake = asyncio.Event()
         self._fast_stream = fast_stream
+        # fast_yield: decode ticks end after the current step while question embeds are queued or
+        # running, and the next tick waits (bounded) for the lane to go idle
+        self.fast_yield = fast_yield
+        self._fast_running = 0
+        self._fast_idle = asyncio.Event()
+        self._fast_idle.set()
         self.checkpoint_s = checkpoint_s  # periodic shard snapshots when the shard is durable (0 = off)
         init = (lambda: torch.cuda.set_stream(main_stream)) if main_stream is not None else None
         self.gpu = cf.ThreadPoolExecutor(max_workers=1, thread_name_prefix="gpu", initializer=init)
@@ -287,7 +293,7 @@ class EngineServer:
         # decode steps per scheduler tick: cb_steps while requests wait for admission, up to
         # cb_max_steps otherwise (a one-rank replica also ends a long tick as soon as one arrives)
         self.cb_steps, self.cb_max_steps = cb_steps, max(cb_steps, cb_max_steps)
-        group.tick_stop = lambda: bool(self._cb_new)
+        group.tick_stop = lambda: bool(self._cb_new) or (self.fast_yield and bool(self._fast_q or self._fast_running))
         self.cb_window_s = cb_window_s
         self._cb_new: list = []
         self._cb_futs: dict = {}
@@ -393,6 +399,7 @@ class EngineServer:
         throughput scales with the burst instead of one encoder pass per question."""
         fut = asyncio.get_running_loop().create_future()
         self._fast_q.append((list(texts), bool(preprocess), fut))
+        self._fast_idle.clear()
         self._fast_wake.set()
         return await fut
 
@@ -400,6 +407,7 @@ class EngineServer:
         loop = asyncio.get_running_loop()
         while True:
             if not self._fast_q:
+                self._fast_idle.set()
                 self._fast_wake.clear()
                 await self._fast_wake.wait()
             pre = self._fast_q[0][1]
@@ -407,6 +415,7 @@ class EngineServer:
             self._fast_q = [r for r in self._fast_q if all(r is not t for t in take)]
             texts = [t for r in take for t in r[0]]
             t0 = time.perf_counter()
+            self._fast_running += 1
             try:
                 v = await loop.run_in_executor(self.fast, self._fast_embed, texts, pre)
             except Exception as e:  # noqa: BLE001 - fail this batch, keep the lane serving
@@ -414,6 +423,8 @@ class EngineServer:
                     if not f.done():
                         f.set_exception(e)
                 continue
+            finally:
+                self._fast_running -= 1
             st = self.stats.setdefault("embed_fast", {"batches": 0, "items": 0, "busy_s": 0.0})
             st["batches"] += 1
             st["items"] += len(texts)
@@ -449,6 +460,11 @@ class EngineServer:
                     # one tick and decodes in lockstep, instead of the first request's tick delaying
                     # everyone else's start by a whole tick
                     await asyncio.sleep(self.cb_window_s)
+            if self.fast_yield and not self._fast_idle.is_set():
+                try:  # question embeds first: they take ~2 ms on an uncontended GPU
+                    await asyncio.wait_for(self._fast_idle.wait(), 0.02)
+                except asyncio.TimeoutError:
+                    pass
             new, self._cb_new = self._cb_new, []
             t0 = time.perf_counter()
             try:

@@ -117,7 +117,7 @@ def main(argv=None) -> int:
         srv = EngineServer(grp, log, max_batch_items=cfg.max_batch * 4, step_timeout_s=cfg.engine_step_timeout,
                            hard_timeout_s=cfg.engine_hard_timeout, liveness_s=cfg.engine_liveness_s,
                            continuous=cfg.engine_continuous, cb_steps=cfg.engine_cb_steps,
-                           cb_max_steps=cfg.engine_cb_max_steps, lanes=lanes,
+                           cb_max_steps=cfg.engine_cb_max_steps, lanes=lanes, fast_yield=cfg.engine_fast_yield,
                            checkpoint_s=cfg.index_checkpoint_s, urls=urls)
         if cfg.engine_metrics_port:
             import prometheus_client
