@@ -99,6 +99,10 @@ def main():
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--breakdown", type=int, default=1, help="1: one extra untimed QA step with per-phase timing")
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--overlap", type=int, default=1,
+                    help="1: QA waves pipelined — the decode of step i on half of the CUs beside the prefill "
+                         "of step i + 1 (Engine.answer_overlapped); 0: one wave after the other")
+    ap.add_argument("--overlap-frac", type=float, default=0.5, help="decode lane's share of the CUs")
     a = ap.parse_args()
 
     info = init_from_env()
@@ -117,9 +121,11 @@ def main():
         from docagents_amd.models.llama import TPContext
         groups = [dist.new_group(list(range(g * TP, (g + 1) * TP))) for g in range(DP)]  # every rank creates every group
         tp_ctx = TPContext(R % TP, TP, groups[dp_rank])
+    overlap = bool(a.overlap) and TP == 1 and not a.no_graphs
     eng = Engine(a.enc, a.llm, dev, seed=a.seed, tp=tp_ctx, max_batch=a.batch, max_seq=4096, temperature=0.2,
                  max_new_tokens=a.max_new, summary_max_new=128, use_graphs=not a.no_graphs,
-                 index_kind=a.index_kind, ivf_lists=a.ivf_lists, ivf_probes=a.ivf_probes, enc_dtype=a.enc_dtype)
+                 index_kind=a.index_kind, ivf_lists=a.ivf_lists, ivf_probes=a.ivf_probes, enc_dtype=a.enc_dtype,
+                 overlap_waves=overlap)
     shard = ShardedIndex(eng.index, R, W)
     d = eng.dim
 
@@ -152,7 +158,8 @@ def main():
             per_dp.append(fs)
         return [f for r in range(W) for f in per_dp[r // TP]]  # rank order, identical within a TP group
 
-    def qa_step(step: int, B: int):
+    def qa_items(step: int, B: int):
+        """A QA step up to the answers: embed the questions, sharded search, context chunks."""
         qs = [tg.question() for _ in range(B)]
         filters = make_filters(step)
         qv = eng.embed(qs)
@@ -164,8 +171,25 @@ def main():
             sc = s_h[b][valid]
             quality = float(sc.mean()) if len(sc) else 0.0
             items.append((qs[b], [chunks.get(int(c)) for c in id_h[b][valid]], quality))
+        return items
+
+    def qa_step(step: int, B: int):
+        items = qa_items(step, B)
         res = eng.answer_many(items, a.max_new)
         return res, items
+
+    def qa_steps_overlapped(step0: int, n: int, B: int):
+        """n QA steps as pipelined waves: step i's embed + search + prefill run while step i - 1
+        decodes (every step's answers are complete when this returns)."""
+        waves = []
+
+        def next_items(i):
+            if i >= n:
+                return None
+            waves.append(qa_items(step0 + i, B))
+            return waves[-1]
+        res = eng.answer_overlapped(next_items, a.max_new, a.overlap_frac)
+        return res, waves
 
     # ---- QA throughput ----
     B_cur = a.batch
@@ -173,12 +197,20 @@ def main():
     for i in range(a.warmup):
         qa_step(i, a.batch)
         log(info, f"warmup step {i + 1}/{a.warmup} done")
+    if overlap:  # both decode states of the pipelined path captured before the timed steps
+        qa_steps_overlapped(50, 2, a.batch)
+        log(info, "overlapped warmup done")
     barrier(); torch.cuda.synchronize()
     t0 = time.perf_counter()
     plen = []
-    for i in range(a.steps):
-        res, items = qa_step(100 + i, a.batch)
-        plen.extend(len(eng.answer_prompt_ids(q, ch, a.max_new)) for q, ch, _ in items[:4])
+    if overlap:
+        _, waves = qa_steps_overlapped(100, a.steps, a.batch)
+        for items in waves:
+            plen.extend(len(eng.answer_prompt_ids(q, ch, a.max_new)) for q, ch, _ in items[:4])
+    else:
+        for i in range(a.steps):
+            res, items = qa_step(100 + i, a.batch)
+            plen.extend(len(eng.answer_prompt_ids(q, ch, a.max_new)) for q, ch, _ in items[:4])
     torch.cuda.synchronize(); barrier()
     dt = time.perf_counter() - t0
     dt_max = all_reduce_max(dt, dev)
@@ -320,6 +352,8 @@ def main():
         "config": {"model": f"{a.enc} embedder + {a.llm} QA", "global_batch": DP * a.batch,
                    "seq_len": int(np.mean(plen)) if plen else None,
                    "parallelism": (f"tp{TP} x dp{DP}" if TP > 1 else f"dp{W}") + f" + {W}-way sharded index",
+                   "qa_waves": f"pipelined (decode beside the next prefill, decode lane {a.overlap_frac:.2f} of the CUs)"
+                   if overlap else "sequential",
                    "index_kind": a.index_kind if a.index_kind == "flat" else
                    f"ivfflat(lists={a.ivf_lists}, probes={a.ivf_probes})",
                    "index_rows_per_gpu": a.index_rows, "top_k": a.top_k, "max_new_tokens": a.max_new,

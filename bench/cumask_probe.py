@@ -44,6 +44,7 @@ def main():
     ap.add_argument("--llm", default="phi3-mini")
     ap.add_argument("--skip-placement", action="store_true")
     ap.add_argument("--out", default="")
+    ap.add_argument("--expand", action="store_true", help="co-run, then move the prefill to the full chip")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
@@ -121,8 +122,51 @@ def main():
     tc = min(timed(lambda: (decode(p1), prefill(p2))) for _ in range(2))
     emit({"mode": "unmasked", "decode_ms": round(td, 1), "prefill_ms": round(tp, 1), "concurrent_ms": round(tc, 1),
           "serial_ms": round(td + tp, 1), "B": B, "ctx": a.ctx, "steps": a.steps}, a.out)
+    # co-run, then expand: the prefill starts on lane B beside the decode on lane A; before each
+    # layer it checks (host side, at most two layers issued ahead) whether the decode is done and
+    # then moves the rest of the prefill to a full-chip stream
+    def corun_expand(sa, sb):
+        done = torch.cuda.Event()
+        decode(sa)
+        done.record(sa)
+        evs = []
+        state = {"moved": False}
+
+        def hook(li):
+            if state["moved"]:
+                return
+            if len(evs) >= 2:
+                evs[-2].synchronize()
+            if done.query():
+                full.wait_stream(sb)
+                torch.cuda.set_stream(full)
+                state["moved"] = li
+                return
+            ev = torch.cuda.Event()
+            ev.record(sb)
+            evs.append(ev)
+        m.layer_hook = hook
+        try:
+            with torch.cuda.stream(sb), K.workspace_role("prefill"):
+                init_state(st_pf, slots_pf)
+                gen._prefill_into(st_pf, prompts, slots_pf, 0)
+        finally:
+            m.layer_hook = None
+        return state["moved"]
+
     for f in [float(x) for x in a.fracs.split(",")]:
         sa, sb = S.lane_streams(f, dev)
+        if a.expand:
+            timed(lambda: decode(sa)); timed(lambda: prefill(sb))
+            tdm = min(timed(lambda: decode(sa)) for _ in range(2))
+            tpm = min(timed(lambda: prefill(sb)) for _ in range(2))
+            moved = []
+            te = min(timed(lambda: moved.append(corun_expand(sa, sb))) for _ in range(3))
+            emit({"mode": "corun_expand", "frac_decode": f, "decode_masked_ms": round(tdm, 1),
+                  "prefill_masked_ms": round(tpm, 1), "corun_expand_ms": round(te, 1), "moved_at_layer": moved,
+                  "decode_full_ms": round(td, 1), "prefill_full_ms": round(tp, 1), "serial_full_ms": round(td + tp, 1),
+                  "speedup_vs_serial": round((td + tp) / te, 3)}, a.out)
+            continue
         timed(lambda: decode(sa)); timed(lambda: prefill(sb))
         tdm = min(timed(lambda: decode(sa)) for _ in range(2))
         tpm = min(timed(lambda: prefill(sb)) for _ in range(2))

@@ -34,7 +34,7 @@ class Engine:
                  max_new_tokens: int = 64, summary_max_new: int = 128, index_kind: str = "flat",
                  ivf_lists: int = 100, ivf_probes: int = 1, load_llm: bool = True, load_encoder: bool = True,
                  use_graphs: bool = True, embed_max_tokens: int = 65536, enc_dtype: str = "bf16",
-                 share_prefix: bool = True):
+                 share_prefix: bool = True, overlap_waves: bool = False):
         self.device = torch.device(device)
         self.lock = threading.RLock()      # the decoder / generator (one GPU thread drives it)
         self.enc_lock = threading.RLock()  # the encoder: the fast embed lane and the batcher share it
@@ -53,8 +53,9 @@ class Engine:
         if load_llm:
             self.decoder = LlamaDecoder(self.dec_cfg, self.device, seed=seed, tp=tp)
             # + 1 dummy slot (padded graph rows) + 2 prompt-head slots (ContinuousScheduler heads)
-            # + 1 for the wave path's kept prompt head (Generator.head)
-            self.decoder.alloc_cache(max_batch + 4, max_seq)
+            # + 1 for the wave path's kept prompt head (Generator.head); overlap_waves: a second
+            # wave's rows (answer_overlapped keeps two waves in flight)
+            self.decoder.alloc_cache((2 if overlap_waves else 1) * max_batch + 4, max_seq)
             self.gen = Generator(self.decoder, max_batch=max_batch, max_seq=max_seq, temperature=temperature,
                                  seed=seed, eos=sorted(self.chat.eos_ids), use_graphs=use_graphs,
                                  share_prefix=share_prefix)
@@ -163,6 +164,32 @@ class Engine:
             res = self.gen.generate(prompts, max_new)
         texts = self.chat.decode_many([r.tokens for r in res])
         return [(txt, float(quality) * r.mean_prob) for (_, _, quality), r, txt in zip(items, res, texts)]
+
+    def answer_overlapped(self, next_items, max_new: int | None = None, decode_frac: float = 0.5):
+        """Waves of answers, the decode of one beside the prefill of the next (Generator.
+        generate_overlapped; the engine must be built with overlap_waves=True). next_items(i) ->
+        the items of wave i (answer_many's items) or None after the last; it runs while the previous
+        wave decodes. decode_frac: the decode lane's share of the CUs (ops/streams.py lane_streams;
+        0.5 measured best, profiles/r3/corun_expand.jsonl). Returns one answer_many result per wave."""
+        from ..ops.streams import lane_streams
+        max_new = max_new or self.max_new_tokens
+        lanes = lane_streams(decode_frac, self.device)
+        waves: list = []
+
+        def next_prompts(i):
+            items = next_items(i)
+            if items is None:
+                return None
+            waves.append(items)
+            tails = self._ids_many([self._answer_tail(q) for q, _, _ in items])
+            return [self.answer_prompt_ids(q, ch, max_new, tail=t) for (q, ch, _), t in zip(items, tails)]
+        with self.lock:
+            res = self.gen.generate_overlapped(next_prompts, max_new, lanes)
+        out = []
+        for items, r in zip(waves, res):
+            texts = self.chat.decode_many([x.tokens for x in r])
+            out.append([(txt, float(q) * x.mean_prob) for (_, _, q), x, txt in zip(items, r, texts)])
+        return out
 
     # ------------------------------------------------------------------ continuous batching
     @property

@@ -11,6 +11,7 @@ from __future__ import annotations
 
 import collections
 import math
+import threading
 import time
 from types import SimpleNamespace
 
@@ -86,8 +87,8 @@ class Generator:
             self._head_slot = self.cache.acquire(1)[0]
         return self._head_slot
 
-    def _state(self, B: int, max_new: int) -> DecodeState:
-        key = (B, max_new)
+    def _state(self, B: int, max_new: int, lane: int = 0) -> DecodeState:
+        key = (B, max_new, lane)
         st = self.states.get(key)
         if st is None:
             st = DecodeState(self.model, B, max_new, self.temperature, self.seed, self.eos)
@@ -169,10 +170,23 @@ class Generator:
         return out
 
     def _generate_wave(self, prompts, max_new: int) -> list[GenResult]:
+        if not prompts:
+            return []
+        w = self._wave_begin(prompts, max_new)
+        try:
+            self._wave_decode(w)
+        except BaseException:
+            self.cache.release(w.slots)
+            raise
+        return self._wave_end(w)
+
+    def _wave_begin(self, prompts, max_new: int, lane: int = 0, head_build: bool = True) -> "_Wave":
+        """Set up the decode state of one wave (bucketed to B rows) and prefill it on the current
+        stream. lane: which of the generator's decode states of that bucket to use (two waves in
+        flight need two). head_build=False: never (re)build the shared prompt head (another wave
+        may be decoding against the kept head's slot) — a miss then prefills whole prompts."""
         m = self.model
         n = len(prompts)
-        if n == 0:
-            return []
         max_new = max(1, max_new)
         for p in prompts:
             if len(p) + max_new > self.cache.max_seq:
@@ -180,7 +194,7 @@ class Generator:
             if len(p) == 0:
                 raise ValueError("empty prompt")
         B = min(_bucket(n), self.max_batch) if self.use_graphs else n
-        st = self._state(B, max_new)
+        st = self._state(B, max_new, lane)
         slots = self.cache.acquire(n)
         try:
             self.stats["calls"] += 1
@@ -207,7 +221,7 @@ class Generator:
                 self.stats["head_cache_hits"] = self.stats.get("head_cache_hits", 0) + n
                 self.stats["shared_prefix_tokens"] += P * n
             else:
-                P = self.shared_prefix_len(prompts)
+                P = self.shared_prefix_len(prompts) if head_build else 0
                 hslot = None
             if P and hslot is None:
                 # the shared head once, then only the suffixes, attending to the head's keys in its
@@ -243,33 +257,45 @@ class Generator:
             if self.sync_phases:
                 torch.cuda.synchronize(dev)
                 self.stats["prefill_wall_s"] = self.stats.get("prefill_wall_s", 0.0) + time.perf_counter() - t_pf
-            t0 = time.perf_counter()
-            steps = max_new - 1
-            if steps > 0:
-                if self.use_graphs and st.graph is None:
-                    self._capture(st)
-                done = 0
-                while done < steps:
-                    k = min(self.check_every, steps - done)
-                    for _ in range(k):
-                        if st.graph is not None:
-                            st.graph.replay()
-                        else:
-                            m.decode_step(st)
-                        # padded rows never advance past the dummy slot's capacity
-                    done += k
-                    self.stats["decode_steps"] += k
-                    if done < steps and int(st.active[:n].sum().item()) == 0:
-                        break
-                    if B > n:
-                        st.pos[n:].zero_(); st.lens[n:].fill_(1)
-            hist = st.hist[:n].cpu().numpy()
-            conf = st.conf[:n].cpu().numpy()
-            self.stats["decode_s"] += time.perf_counter() - t0
-        finally:
+        except BaseException:
             self.cache.release(slots)
+            raise
+        return _Wave(st, n, B, slots, max_new - 1)
+
+    def _wave_decode(self, w: "_Wave"):
+        """The wave's decode steps on the current stream (graph replays; the host checks every
+        check_every steps whether every row has stopped)."""
+        m, st, n, B = self.model, w.st, w.n, w.B
+        t0 = time.perf_counter()
+        steps = w.steps
+        if steps > 0:
+            if self.use_graphs and st.graph is None:
+                self._capture(st)
+            done = 0
+            while done < steps:
+                k = min(self.check_every, steps - done)
+                for _ in range(k):
+                    if st.graph is not None:
+                        st.graph.replay()
+                    else:
+                        m.decode_step(st)
+                    # padded rows never advance past the dummy slot's capacity
+                done += k
+                self.stats["decode_steps"] += k
+                if done < steps and int(st.active[:n].sum().item()) == 0:
+                    break
+                if B > n:
+                    st.pos[n:].zero_(); st.lens[n:].fill_(1)
+        self.stats["decode_s"] += time.perf_counter() - t0
+
+    def _wave_end(self, w: "_Wave") -> list[GenResult]:
+        try:
+            hist = w.st.hist[:w.n].cpu().numpy()
+            conf = w.st.conf[:w.n].cpu().numpy()
+        finally:
+            self.cache.release(w.slots)
         res = []
-        for b in range(n):
+        for b in range(w.n):
             toks = [int(t) for t in hist[b] if t >= 0]
             # drop EOS from the text
             toks = [t for t in toks if t not in self.eos]
@@ -277,6 +303,96 @@ class Generator:
             res.append(GenResult(toks, float(conf[b, 0] / cnt) if cnt > 0 else 1.0, int(cnt)))
             self.stats["decode_tokens"] += int(cnt)
         return res
+
+    def generate_overlapped(self, next_prompts, max_new: int, lanes) -> list[list[GenResult]]:
+        """Waves of prompts with the decode of wave i running BESIDE the prefill of wave i + 1.
+
+        The decode of a wave is HBM-bound (KV-cache stream), the prefill MFMA-bound; plain
+        concurrent streams interleave them badly (profiles/r1 stream_overlap_probe), and a fixed CU
+        partition leaves the prefill on part of the chip after the decode ends
+        (profiles/r3/cumask_probe.jsonl). Here: the decode replays on the decode lane (a CU-masked
+        stream, ``lanes[0]``) from a helper thread; the next wave's prefill starts on the
+        complementary lane (``lanes[1]``) and, before each layer, moves to the full chip as soon as
+        the decode has finished (host check, at most two layers issued ahead). Tokens are identical
+        to ``generate`` wave by wave (same kernels, same sampler counters).
+
+        next_prompts(i) -> prompts of wave i, or None after the last; it runs on the host while the
+        previous wave decodes (its own kernels — question embeds, searches — go to the full chip).
+        Returns one result list per wave."""
+        dec_s, pf_s = lanes
+        full = torch.cuda.current_stream()
+        from ..ops import kernels as K
+        out: list[list[GenResult]] = []
+        prompts = next_prompts(0)
+        if not prompts:
+            return out
+        cur = self._wave_begin(prompts, max_new, lane=0)
+        i = 1
+        while cur is not None:
+            if self.use_graphs and cur.st.graph is None and cur.steps > 0:
+                self._capture(cur.st)  # never capture while another thread issues work
+            dec_s.wait_stream(torch.cuda.current_stream())
+            done = torch.cuda.Event()
+            err: list = []
+
+            def run_decode(w=cur):
+                try:
+                    with torch.cuda.stream(dec_s):
+                        self._wave_decode(w)
+                        done.record(dec_s)
+                except BaseException as e:  # noqa: BLE001 - re-raised on the caller's thread
+                    err.append(e)
+                    done.record(dec_s)
+            th = threading.Thread(target=run_decode, name="wave-decode", daemon=True)
+            th.start()
+            nxt = None
+            try:
+                prompts = next_prompts(i)
+                if prompts:
+                    issued: list = []
+                    state = {"moved": False}
+
+                    def hook(li):
+                        if state["moved"]:
+                            return
+                        if len(issued) >= 2:
+                            issued[-2].synchronize()
+                        if done.query():
+                            full.wait_stream(pf_s)
+                            torch.cuda.set_stream(full)
+                            state["moved"] = True
+                            return
+                        ev = torch.cuda.Event()
+                        ev.record(pf_s)
+                        issued.append(ev)
+                    pf_s.wait_stream(full)
+                    self.model.layer_hook = hook
+                    try:
+                        with torch.cuda.stream(pf_s), K.workspace_role("prefill"):
+                            nxt = self._wave_begin(prompts, max_new, lane=i % 2, head_build=False)
+                            end = torch.cuda.current_stream()
+                    finally:
+                        self.model.layer_hook = None
+                    full.wait_stream(end)
+            finally:
+                th.join()
+            full.wait_stream(dec_s)
+            if err:
+                self.cache.release(cur.slots)
+                if nxt is not None:
+                    self.cache.release(nxt.slots)
+                raise err[0]
+            out.append(self._wave_end(cur))
+            cur = nxt
+            i += 1
+        return out
+
+
+class _Wave:
+    __slots__ = ("st", "n", "B", "slots", "steps")
+
+    def __init__(self, st, n, B, slots, steps):
+        self.st, self.n, self.B, self.slots, self.steps = st, n, B, slots, steps
 
 
 class ContinuousScheduler:

@@ -205,6 +205,7 @@ class KVCache:
 
 class LlamaDecoder:
     unit_gains = False  # set by _fold_norm_gains
+    layer_hook = None   # prefill: called with the layer index before each layer (stream steering)
 
     def __init__(self, cfg: DecoderConfig, device="cuda", seed: int = 0, tp: TPContext | None = None,
                  weights: dict | None = None):
@@ -295,7 +296,10 @@ class LlamaDecoder:
         c, o, cache = self.cfg, self.ops, self.cache
         D, hl, kl = c.head_dim, self.hl, self.kl
         x = o.embed(ids, self.w["embed"])
+        hook = self.layer_hook
         for li, L in enumerate(self.w["layers"]):
+            if hook is not None:  # e.g. move the rest of a prefill to another (CU-masked) stream
+                hook(li)
             h = o.rmsnorm(x, L["ln_attn"], c.eps)
             # QKV projection + RoPE + KV-cache write in one kernel (gemm8p EPI_ROPE epilogue)
             qkv = o.gemm_rope(h, L["wqkv"], pos, self.cos_sin, hl, kl, D, slot_tok, cache.k(li), cache.v(li))

@@ -50,3 +50,66 @@ DA_EXPORT int da_placement_probe(void* out, int blocks, long long spin, void* st
   placement_kernel<<<blocks, 64, 0, (hipStream_t)stream>>>((unsigned*)out, spin);
   DA_LAUNCH_CHECK();
 }
+
+// ------------------------------------------------------------------------------------------
+// Read-bandwidth probe for a CU subset (bench/cumask_bw.py): how many bytes per second can the
+// CUs of a masked stream pull from HBM, by LDS-DMA into an LDS ring (mode 0: D 1-KB wave loads in
+// flight per wave, no registers held) or into registers (mode 1: U 1-KB loads per wave per round)?
+// The decode attention is bound by exactly this on a partition of the chip.
+typedef __attribute__((address_space(3))) void* probe_lds_t;
+typedef __attribute__((address_space(1))) const void* probe_g_t;
+
+template <int D>
+__global__ void __launch_bounds__(256) lds_stream_probe(const char* __restrict__ src, long long per_wg,
+                                                        unsigned* out) {
+  __shared__ __attribute__((aligned(16))) char ring[4][32][1024];  // 128 KB: 32 slots per wave
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const char* base = src + blockIdx.x * per_wg;
+  const long long n = per_wg / 4096;  // loads per wave
+  for (long long k = 0; k < n; ++k) {
+    __builtin_amdgcn_global_load_lds((probe_g_t)(base + (k * 4 + w) * 1024 + lane * 16),
+                                     (probe_lds_t)&ring[w][k & 31][0], 16, 0, 2);
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(D - 1) : "memory");
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (ring[w][lane & 31][lane] == 0x5a && lane == 63) out[blockIdx.x] = 1;  // keep the stream live
+}
+
+template <int U>
+__global__ void __launch_bounds__(256) reg_stream_probe(const char* __restrict__ src, long long per_wg,
+                                                        unsigned* out) {
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const char* base = src + blockIdx.x * per_wg;
+  const long long n = per_wg / 4096;
+  unsigned acc = 0;
+  for (long long k = 0; k < n; k += U) {
+    u32x4_t v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const long long kk = k + u < n ? k + u : n - 1;
+      v[u] = __builtin_nontemporal_load((const u32x4_t*)(base + (kk * 4 + w) * 1024 + lane * 16));
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) acc ^= v[u][0] ^ v[u][1] ^ v[u][2] ^ v[u][3];
+  }
+  if (acc == 0x12345678u) out[blockIdx.x] = acc;
+}
+
+// mode 0: LDS-DMA ring, depth 8 / 16 / 31; mode 1: registers, U = 8 / 16. per_wg % 4096 == 0.
+DA_EXPORT int da_stream_probe(const void* src, long long per_wg, int nwg, int mode, int depth, void* out,
+                              void* stream) {
+  if (nwg <= 0 || per_wg % 4096 || !src || !out) return (int)hipErrorInvalidValue;
+  hipStream_t s = (hipStream_t)stream;
+  const char* p = (const char*)src;
+  unsigned* o = (unsigned*)out;
+  if (mode == 0) {
+    if (depth >= 31) lds_stream_probe<31><<<nwg, 256, 0, s>>>(p, per_wg, o);
+    else if (depth >= 16) lds_stream_probe<16><<<nwg, 256, 0, s>>>(p, per_wg, o);
+    else lds_stream_probe<8><<<nwg, 256, 0, s>>>(p, per_wg, o);
+  } else {
+    if (depth >= 16) reg_stream_probe<16><<<nwg, 256, 0, s>>>(p, per_wg, o);
+    else reg_stream_probe<8><<<nwg, 256, 0, s>>>(p, per_wg, o);
+  }
+  DA_LAUNCH_CHECK();
+}
