@@ -99,9 +99,11 @@ def main():
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--breakdown", type=int, default=1, help="1: one extra untimed QA step with per-phase timing")
     ap.add_argument("--seed", type=int, default=0)
-    ap.add_argument("--overlap", type=int, default=1,
+    ap.add_argument("--overlap", type=int, default=0,
                     help="1: QA waves pipelined — the decode of step i on half of the CUs beside the prefill "
-                         "of step i + 1 (Engine.answer_overlapped); 0: one wave after the other")
+                         "of step i + 1 (Engine.answer_overlapped); 0 (default): one wave after the other. "
+                         "Same box: 30.2 vs 32.3 q/s (profiles/r3/overlap/): the co-run loses to the clock "
+                         "and HBM interference what the partition gains")
     ap.add_argument("--overlap-frac", type=float, default=0.5, help="decode lane's share of the CUs")
     a = ap.parse_args()
 
@@ -204,7 +206,10 @@ def main():
     t0 = time.perf_counter()
     plen = []
     if overlap:
+        eng.gen.stats.pop("overlap_moves", None); eng.gen.stats.pop("overlap_decode_join_s", None)
         _, waves = qa_steps_overlapped(100, a.steps, a.batch)
+        log(info, f"overlap: prefill moved to the full chip at (layer, s) {eng.gen.stats.get('overlap_moves')}, "
+                  f"decode joined after {eng.gen.stats.get('overlap_decode_join_s')} s")
         for items in waves:
             plen.extend(len(eng.answer_prompt_ids(q, ch, a.max_new)) for q, ch, _ in items[:4])
     else:

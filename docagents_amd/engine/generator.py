@@ -266,7 +266,7 @@ class Generator:
         """The wave's decode steps on the current stream (graph replays; the host checks every
         check_every steps whether every row has stopped)."""
         m, st, n, B = self.model, w.st, w.n, w.B
-        t0 = time.perf_counter()
+        w.t0 = time.perf_counter()  # decode_s runs to the results on the host (_wave_end)
         steps = w.steps
         if steps > 0:
             if self.use_graphs and st.graph is None:
@@ -286,12 +286,13 @@ class Generator:
                     break
                 if B > n:
                     st.pos[n:].zero_(); st.lens[n:].fill_(1)
-        self.stats["decode_s"] += time.perf_counter() - t0
 
     def _wave_end(self, w: "_Wave") -> list[GenResult]:
         try:
             hist = w.st.hist[:w.n].cpu().numpy()
             conf = w.st.conf[:w.n].cpu().numpy()
+            if w.t0 is not None:
+                self.stats["decode_s"] += time.perf_counter() - w.t0
         finally:
             self.cache.release(w.slots)
         res = []
@@ -333,6 +334,7 @@ class Generator:
                 self._capture(cur.st)  # never capture while another thread issues work
             dec_s.wait_stream(torch.cuda.current_stream())
             done = torch.cuda.Event()
+            recorded = threading.Event()  # an event never recorded reads as complete: gate on this
             err: list = []
 
             def run_decode(w=cur):
@@ -343,7 +345,10 @@ class Generator:
                 except BaseException as e:  # noqa: BLE001 - re-raised on the caller's thread
                     err.append(e)
                     done.record(dec_s)
+                finally:
+                    recorded.set()
             th = threading.Thread(target=run_decode, name="wave-decode", daemon=True)
+            t_w = time.perf_counter()
             th.start()
             nxt = None
             try:
@@ -357,10 +362,11 @@ class Generator:
                             return
                         if len(issued) >= 2:
                             issued[-2].synchronize()
-                        if done.query():
+                        if recorded.is_set() and done.query():
                             full.wait_stream(pf_s)
                             torch.cuda.set_stream(full)
                             state["moved"] = True
+                            self.stats.setdefault("overlap_moves", []).append((li, round(time.perf_counter() - t_w, 4)))
                             return
                         ev = torch.cuda.Event()
                         ev.record(pf_s)
@@ -376,6 +382,7 @@ class Generator:
                     full.wait_stream(end)
             finally:
                 th.join()
+            self.stats.setdefault("overlap_decode_join_s", []).append(round(time.perf_counter() - t_w, 4))
             full.wait_stream(dec_s)
             if err:
                 self.cache.release(cur.slots)
@@ -389,10 +396,11 @@ class Generator:
 
 
 class _Wave:
-    __slots__ = ("st", "n", "B", "slots", "steps")
+    __slots__ = ("st", "n", "B", "slots", "steps", "t0")
 
     def __init__(self, st, n, B, slots, steps):
         self.st, self.n, self.B, self.slots, self.steps = st, n, B, slots, steps
+        self.t0 = None
 
 
 class ContinuousScheduler:
