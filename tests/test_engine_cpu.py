@@ -531,3 +531,35 @@ def test_continuous_scheduler_runs_the_smallest_row_bucket():
     got3 = sched.run_all(prompts, 6)
     assert [r.tokens for r in got3] == want
     assert sched.stats["steps_by_bucket"].get(4, 0) > 0 and 8 not in sched.stats["steps_by_bucket"]
+
+
+def test_dk_decode_step_matches_fused_norm_step():
+    """The gemm_dk decode layer structure (norms deferred into the consuming GEMM from per-part sums
+    of squares, ops/reference.py gemm_dk) produces the same logits as the split-K + fused-norm
+    structure it replaces for 2..32 rows, within bf16 rounding, step after step."""
+    from docagents_amd.models.configs import decoder_config
+    from docagents_amd.models.llama import DecodeState, LlamaDecoder
+    from docagents_amd.ops import reference as R
+    torch.manual_seed(0)
+    m = LlamaDecoder(decoder_config("tiny-dec"), "cpu", seed=0)
+    m.alloc_cache(6, 256)
+    B = 4
+    assert m._dk_decode(B)
+    out = {}
+    for dk in (True, False):
+        R.DECODE_DK = dk
+        try:
+            assert m._dk_decode(B) == dk
+            st = DecodeState(m, B, 8, 0.0, 0, ())
+            st.slot.copy_(torch.arange(B, dtype=torch.int32))
+            st.lens.fill_(1); st.pos.zero_(); st.active.fill_(1); st.start.zero_()
+            st.tokens.copy_(torch.tensor([5, 77, 300, 1234], dtype=torch.int32))
+            logits = []
+            for _ in range(3):
+                m.decode_step(st)
+                logits.append(st.logits.float().clone())
+            out[dk] = logits
+        finally:
+            R.DECODE_DK = True
+    for a, b in zip(out[True], out[False]):
+        assert torch.allclose(a, b, atol=0.05, rtol=0.02), (a - b).abs().max()
