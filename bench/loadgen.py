@@ -279,7 +279,7 @@ async def _engine_stats(url: str) -> dict:
         st = dict(st["replicas"][0], replicas=len(st["replicas"]))
     r0 = st["ranks"][0] if st.get("ranks") else {}
     return {"exec": st.get("exec"), "batching": st.get("batching"), "gen": r0.get("gen"), "embed": r0.get("embed"),
-            "sched": r0.get("sched")}
+            "sched": r0.get("sched"), "rpc_mean_ms": st.get("rpc_mean_ms")}
 
 
 def diagnostics(base: int, parsers: int = 2, analyzers: int = 2, engine_url: str = "") -> dict:

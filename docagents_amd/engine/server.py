@@ -274,6 +274,7 @@ class EngineServer:
         self._fast_running = 0
         self._fast_idle = asyncio.Event()
         self._fast_idle.set()
+        self.rpc_ms: dict[str, list] = {}  # method -> [calls, total ms] (engine side)
         self.checkpoint_s = checkpoint_s  # periodic shard snapshots when the shard is durable (0 = off)
         init = (lambda: torch.cuda.set_stream(main_stream)) if main_stream is not None else None
         self.gpu = cf.ThreadPoolExecutor(max_workers=1, thread_name_prefix="gpu", initializer=init)
@@ -604,7 +605,8 @@ class EngineServer:
         if method == "stats":
             st = await self._gpu("stats", {})
             return {"ranks": st, "batching": self.stats,
-                    "exec": {k: {"n": n, "s": round(t, 4)} for k, (n, t) in self.exec_stats.items()}}
+                    "exec": {k: {"n": n, "s": round(t, 4)} for k, (n, t) in self.exec_stats.items()},
+                    "rpc_mean_ms": {k: round(t / max(1, n), 3) for k, (n, t) in self.rpc_ms.items()}}
         if method == "health":
             pl = self.group.plane
             return dict(self.watchdog.state(), live_ranks=self.live_ranks, world=self.group.world,
@@ -616,9 +618,17 @@ class EngineServer:
 
         async def handle(msg):
             rid = msg.get("id")
+            method = msg.get("method")
+            t0 = time.perf_counter()
             try:
-                res = await self.dispatch(msg.get("method"), msg.get("args") or {})
+                res = await self.dispatch(method, msg.get("args") or {})
                 out = {"id": rid, "result": res}
+                if method in ("embed", "embed_search", "search"):
+                    # engine-side latency of the query-path calls (receipt -> reply ready): with the
+                    # client's stage time it splits a slow query between the engine and the RPC hop
+                    r = self.rpc_ms.setdefault(method, [0, 0.0])
+                    r[0] += 1
+                    r[1] += (time.perf_counter() - t0) * 1000
             except Exception as e:  # noqa: BLE001
                 self.log.error("engine rpc failed", "method", msg.get("method"), "err", repr(e),
                                "trace_id", msg.get("trace", ""))
