@@ -84,6 +84,9 @@ class Config:
     # the decode scheduler pauses between steps while question embeds run on the fast lane (their
     # ~100 encoder launches then find free CUs instead of queueing behind decode replays)
     engine_fast_yield: bool = field(default=False, metadata={"env": "ENGINE_FAST_YIELD"})
+    # Python GIL switch interval of the engine process (ms; 0 = interpreter default 5 ms). 0.5 ms
+    # measured no better for the query path under load (profiles/r3/stack/*switch*)
+    engine_switch_interval_ms: float = field(default=0.0, metadata={"env": "ENGINE_SWITCH_INTERVAL_MS"})
     engine_admit_tokens: int = field(default=0, metadata={"env": "ENGINE_ADMIT_TOKENS"})  # 0 -> 4 prefill chunks
     # --- new keys: durable vector shards (index/wal.py) ---
     index_dir: str = field(default="", metadata={"env": "INDEX_DIR"})  # "" -> DATA_DIR/index; "none" -> off

@@ -52,6 +52,12 @@ def main(argv=None) -> int:
 
     cfg = load()
     log = new_logger(cfg.log_level)
+    if cfg.engine_switch_interval_ms > 0:
+        # the engine's threads (RPC loop, GPU thread, fast embed lane, search plane, tokenizers)
+        # hand the GIL back and forth several times per query (a shorter switch interval was
+        # measured for the loaded query path: no gain, profiles/r3/stack)
+        import sys
+        sys.setswitchinterval(cfg.engine_switch_interval_ms / 1000.0)
     info = init_from_env()
     world, rank = info.world, info.rank
     t = max(1, cfg.tp_size)
