@@ -322,12 +322,18 @@ class Generator:
         Returns one result list per wave."""
         dec_s, pf_s = lanes
         full = torch.cuda.current_stream()
-        from ..ops import kernels as K
         out: list[list[GenResult]] = []
         prompts = next_prompts(0)
         if not prompts:
             return out
         cur = self._wave_begin(prompts, max_new, lane=0)
+        try:
+            return self._overlap_loop(cur, next_prompts, max_new, dec_s, pf_s, full, out)
+        finally:
+            self.model.layer_hook = None
+
+    def _overlap_loop(self, cur, next_prompts, max_new, dec_s, pf_s, full, out):
+        from ..ops import kernels as K
         i = 1
         while cur is not None:
             if self.use_graphs and cur.st.graph is None and cur.steps > 0:
@@ -351,6 +357,7 @@ class Generator:
             t_w = time.perf_counter()
             th.start()
             nxt = None
+            failed = None
             try:
                 prompts = next_prompts(i)
                 if prompts:
@@ -380,15 +387,18 @@ class Generator:
                     finally:
                         self.model.layer_hook = None
                     full.wait_stream(end)
+            except BaseException as e:  # noqa: BLE001 - the decode thread is joined first
+                failed = e
             finally:
                 th.join()
             self.stats.setdefault("overlap_decode_join_s", []).append(round(time.perf_counter() - t_w, 4))
             full.wait_stream(dec_s)
-            if err:
+            if err or failed is not None:
+                torch.cuda.synchronize()
                 self.cache.release(cur.slots)
                 if nxt is not None:
                     self.cache.release(nxt.slots)
-                raise err[0]
+                raise err[0] if err else failed
             out.append(self._wave_end(cur))
             cur = nxt
             i += 1

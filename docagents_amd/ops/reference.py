@@ -466,8 +466,10 @@ def gemm_dk(a, w, epi=EPI_NONE, bias=None, resid=None, out=None, norm_in=None, s
     y = _epilogue(x @ w.float().t(), N, bias, epi, resid, out)
     if ssq_out is not None:
         parts = dk_parts(N)
-        sq = y.float().pow(2).view(M, parts, N // parts).sum(-1)
-        ssq_out.view(-1, 64)[:parts, :M] = sq.t()
+        bn = -(-N // parts)
+        y2 = y.float().pow(2)
+        sq = torch.stack([y2[:, i * bn:(i + 1) * bn].sum(-1) for i in range(parts)])  # [parts, M]
+        ssq_out.view(-1, 64)[:parts, :M] = sq
     return y
 
 
