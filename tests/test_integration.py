@@ -26,7 +26,7 @@ def free_port():
     return p
 
 
-def wait_http(url, timeout=60):
+def wait_http(url, timeout=180):  # generous: service start under a loaded CI box
     t0 = time.time()
     while time.time() - t0 < timeout:
         try:
