@@ -112,6 +112,15 @@ def _build_locked(stamp: Path, fp: str, debug: bool, verbose: bool) -> Path:
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"link failed:\n{r.stderr}")
+    # a kernel whose launch stub the host pass dropped (e.g. a template-dependent array extent in a
+    # builtin argument) links fine and fails only at dlopen on the GPU box: catch it here
+    nm = shutil.which("nm")
+    if nm:
+        u = subprocess.run([nm, "-D", "--undefined-only", str(tmp)], capture_output=True, text=True).stdout
+        stubs = [ln.split()[-1] for ln in u.splitlines() if "__device_stub__" in ln]
+        if stubs:
+            tmp.unlink(missing_ok=True)
+            raise RuntimeError(f"undefined kernel launch stubs: {stubs[:4]}")
     os.replace(tmp, LIB)
     stamp.write_text(fp)
     return LIB

@@ -308,7 +308,22 @@ flash_attn_v2_kernel(const bf16_t* __restrict__ q, const bf16_t* __restrict__ k,
 // so the softmax VALU work never waits on the MFMA results it follows (RAW) and the matrix pipe has
 // independent work while a wave is in its exp/max/pack stretch. Three LDS tile buffers: tile t
 // (P·V), t + 1 (S) and t + 2 (being written); one barrier per tile.
-template <int D>
+//
+// SPEC = true: speculative softmax against a deferred running max (guide T13). The round-2 form put
+// the S MFMAs of tile t + 1, the max / rescale branch and the exp / pack / P·V of tile t in separate
+// basic blocks, so the compiler could not interleave the softmax VALU of t with the S MFMAs of t + 1
+// (ISA: a 12-MFMA block with no VALU, then a 116-VALU + 32-exp block; the SIMD ran them back to back).
+// With SPEC, an unmasked tile (every key visible to every query of the wave) is one straight-line
+// block: S(t + 1) MFMAs interleaved with max(t), p = exp2(s·c - m_run·c) against the STALE running
+// max, row sums and the bf16 pack; only then one wave-uniform test: if any query's tile max exceeds
+// its running max by more than 2^SPEC_TAU in p (first tile of a wave, or a late spike) the tile is
+// redone the exact way — its S recomputed from the K tile still in LDS, then the ordinary
+// max / rescale / exp path — otherwise P·V follows. Masked tiles (causal diagonal, sequence end)
+// always take the exact path. p <= 2^SPEC_TAU keeps the fp32 sums and the bf16 P exact in relative
+// terms; the result is normalised by the same l, so only rounding differs from SPEC = false.
+constexpr float SPEC_TAU = 8.f;
+
+template <int D, bool SPEC>
 __global__ void __launch_bounds__(256, 2)
 flash_attn_pipe_kernel(const bf16_t* __restrict__ q, const bf16_t* __restrict__ k, const bf16_t* __restrict__ v,
                        int ldq, int ldk, int ldv, const int* __restrict__ cu, int H, int Hkv, int causal,
@@ -408,25 +423,55 @@ flash_attn_pipe_kernel(const bf16_t* __restrict__ q, const bf16_t* __restrict__ 
   // S^T of tile t: all K fragments, then the MFMAs (two independent accumulation chains)
   auto s_tile = [&](int t, f32x16_t (&sa)[2]) {
     const char* sK = buf_of(t);
-    bf16x8_t kfr[2][NDS];
-#pragma unroll
-    for (int hh = 0; hh < 2; ++hh)
-#pragma unroll
-      for (int ds = 0; ds < NDS; ++ds)
-        kfr[hh][ds] = *(const bf16x8_t*)(sK + (hh * 32 + qr) * C::KSTR + ds * 32 + hi * 16);
 #pragma unroll
     for (int hh = 0; hh < 2; ++hh)
 #pragma unroll
       for (int r = 0; r < 16; ++r) sa[hh][r] = 0.f;
+    if constexpr (SPEC) {
+      // one 32-key half at a time: 6 fragments (24 VGPRs) live instead of 12 beside the softmax of t
 #pragma unroll
-    for (int ds = 0; ds < NDS; ++ds)
+      for (int hh = 0; hh < 2; ++hh) {
+        bf16x8_t kfr[NDS];
 #pragma unroll
-      for (int hh = 0; hh < 2; ++hh) sa[hh] = mfma32(kfr[hh][ds], qf[ds], sa[hh]);
+        for (int ds = 0; ds < NDS; ++ds)
+          kfr[ds] = *(const bf16x8_t*)(sK + (hh * 32 + qr) * C::KSTR + ds * 32 + hi * 16);
+#pragma unroll
+        for (int ds = 0; ds < NDS; ++ds) sa[hh] = mfma32(kfr[ds], qf[ds], sa[hh]);
+      }
+    } else {
+      bf16x8_t kfr[2][NDS];
+#pragma unroll
+      for (int hh = 0; hh < 2; ++hh)
+#pragma unroll
+        for (int ds = 0; ds < NDS; ++ds)
+          kfr[hh][ds] = *(const bf16x8_t*)(sK + (hh * 32 + qr) * C::KSTR + ds * 32 + hi * 16);
+#pragma unroll
+      for (int ds = 0; ds < NDS; ++ds)
+#pragma unroll
+        for (int hh = 0; hh < 2; ++hh) sa[hh] = mfma32(kfr[hh][ds], qf[ds], sa[hh]);
+    }
+  };
+  // O^T += V^T P^T of tile t, P packed to bf16 (kc = 16-key step)
+  auto pv_tile = [&](int t, const u32x4_t (&pw)[4]) {
+    const char* sV = buf_of(t) + C::KBUF;
+#pragma unroll
+    for (int kc = 0; kc < 4; ++kc) {
+      const bf16x8_t pb = __builtin_bit_cast(bf16x8_t, pw[kc]);
+      const int g = lane >> 4, li = lane & 15;
+      const int row0 = kc * 16 + 4 * (g >> 1) + (li >> 2);
+#pragma unroll
+      for (int db = 0; db < NDB; ++db) {
+        const int col = db * 32 + 16 * (g & 1) + 4 * (li & 3);
+        const s16x4_t lo = lds_read_tr16(sV + row0 * C::VSTR + col * 2);
+        const s16x4_t hi8 = lds_read_tr16(sV + (row0 + 8) * C::VSTR + col * 2);
+        const bf16x8_t va = bf16x8_t{lo[0], lo[1], lo[2], lo[3], hi8[0], hi8[1], hi8[2], hi8[3]};
+        oacc[db] = mfma32(va, pb, oacc[db]);
+      }
+    }
   };
   // mask + online softmax + O^T += V^T P^T of tile t
   auto finish = [&](int t, f32x16_t (&sa)[2]) {
     const int kb = t * KT;
-    const char* sV = buf_of(t) + C::KBUF;
     if (kb + KT > Lk || (causal && kb + KT - 1 > P + wq0)) {
 #pragma unroll
       for (int hh = 0; hh < 2; ++hh)
@@ -462,23 +507,59 @@ flash_attn_pipe_kernel(const bf16_t* __restrict__ q, const bf16_t* __restrict__ 
         psum += pv;
       }
     l_part += psum;
+    u32x4_t pw[4];
 #pragma unroll
     for (int kc = 0; kc < 4; ++kc) {
       const int hh = kc >> 1, cb = (kc & 1) * 8;
-      const u32x4_t pw = u32x4_t{pack_bf2(sa[hh][cb], sa[hh][cb + 1]), pack_bf2(sa[hh][cb + 2], sa[hh][cb + 3]),
-                                 pack_bf2(sa[hh][cb + 4], sa[hh][cb + 5]), pack_bf2(sa[hh][cb + 6], sa[hh][cb + 7])};
-      const bf16x8_t pb = __builtin_bit_cast(bf16x8_t, pw);
-      const int g = lane >> 4, li = lane & 15;
-      const int row0 = kc * 16 + 4 * (g >> 1) + (li >> 2);
-#pragma unroll
-      for (int db = 0; db < NDB; ++db) {
-        const int col = db * 32 + 16 * (g & 1) + 4 * (li & 3);
-        const s16x4_t lo = lds_read_tr16(sV + row0 * C::VSTR + col * 2);
-        const s16x4_t hi8 = lds_read_tr16(sV + (row0 + 8) * C::VSTR + col * 2);
-        const bf16x8_t va = bf16x8_t{lo[0], lo[1], lo[2], lo[3], hi8[0], hi8[1], hi8[2], hi8[3]};
-        oacc[db] = mfma32(va, pb, oacc[db]);
-      }
+      pw[kc] = u32x4_t{pack_bf2(sa[hh][cb], sa[hh][cb + 1]), pack_bf2(sa[hh][cb + 2], sa[hh][cb + 3]),
+                       pack_bf2(sa[hh][cb + 4], sa[hh][cb + 5]), pack_bf2(sa[hh][cb + 6], sa[hh][cb + 7])};
     }
+    pv_tile(t, pw);
+  };
+  // unmasked tile with a deferred running max (SPEC; see above the kernel). The caller issues the S
+  // MFMAs of tile t + 1 just before, in the same basic block.
+  const float spec_thr = SPEC_TAU / c;  // raw-score headroom above the reference max
+  auto finish_spec = [&](int t, f32x16_t (&sa)[2]) {
+    float mx = fmaxf(sa[0][0], sa[0][1]);
+#pragma unroll
+    for (int r = 2; r < 16; ++r) mx = fmaxf(mx, sa[0][r]);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) mx = fmaxf(mx, sa[1][r]);
+    mx = max_xhalf(mx);
+    // the reference max moves only when the tile max overshoots it by SPEC_TAU (log2 units of p):
+    // p <= 2^SPEC_TAU; first tile: m_run = -inf -> m_new = mx, alpha = 0
+    const bool up = mx > m_run + spec_thr;
+    const float m_new = up ? mx : m_run;
+    const float alpha = exp2f((m_run - m_new) * c);
+    const float mcs = -m_new * c;
+    float psum = 0.f;
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float pv = __builtin_amdgcn_exp2f(fmaf(sa[hh][r], c, mcs));
+        sa[hh][r] = pv;
+        psum += pv;
+      }
+    u32x4_t pw[4];
+#pragma unroll
+    for (int kc = 0; kc < 4; ++kc) {
+      const int hh = kc >> 1, cb = (kc & 1) * 8;
+      pw[kc] = u32x4_t{pack_bf2(sa[hh][cb], sa[hh][cb + 1]), pack_bf2(sa[hh][cb + 2], sa[hh][cb + 3]),
+                       pack_bf2(sa[hh][cb + 4], sa[hh][cb + 5]), pack_bf2(sa[hh][cb + 6], sa[hh][cb + 7])};
+    }
+    l_part = l_part * alpha + psum;
+    m_run = m_new;
+    // materialise P and l here: otherwise the compiler sinks the exp / pack work past the branch
+    // into the P·V block, away from the S MFMAs of t + 1 it is meant to run beside
+#pragma unroll
+    for (int kc = 0; kc < 4; ++kc) asm volatile("" : "+v"(pw[kc]));
+    asm volatile("" : "+v"(l_part));
+    if (__any(up)) {  // rare after the first tiles: O moves to the new reference
+#pragma unroll
+      for (int i = 0; i < NDB; ++i) oacc[i] *= alpha;
+    }
+    pv_tile(t, pw);
   };
 
   load_tile(0);
@@ -492,8 +573,19 @@ flash_attn_pipe_kernel(const bf16_t* __restrict__ q, const bf16_t* __restrict__ 
   f32x16_t SA[2], SB[2];
   s_tile(0, SA);
   auto step = [&](int t, f32x16_t (&cur)[2], f32x16_t (&nxt)[2]) {
-    if (t + 1 < ntiles && (t + 1) * KT < wave_end) s_tile(t + 1, nxt);
-    if (t * KT < wave_end) finish(t, cur);
+    const int kb = t * KT;
+    const bool nx = t + 1 < ntiles && (t + 1) * KT < wave_end;
+    // unmasked for every query of this wave (the smallest query sees the tile's last key)
+    const bool clean = kb + KT <= Lk && (!causal || kb + KT - 1 <= P + wq0);
+    if (SPEC && nx && clean) {
+      s_tile(t + 1, nxt);
+      finish_spec(t, cur);
+    } else if (SPEC && clean && kb < wave_end) {
+      finish_spec(t, cur);
+    } else {
+      if (nx) s_tile(t + 1, nxt);
+      if (kb < wave_end) finish(t, cur);
+    }
     if (t + 2 < ntiles) store_tile(t + 2);   // its buffer (t - 1) % 3 was last read before the previous barrier
     if (t + 3 < ntiles) load_tile(t + 3);
     __syncthreads();
@@ -1363,30 +1455,35 @@ static int g_fa_qh = 0;
 DA_EXPORT void da_set_flash_qh(int v) { g_fa_qh = v; }
 // software-pipelined kernel (flash_attn_pipe, D <= 96, 4 waves x 32 queries): 0 = off, 1 = on,
 // 2 = auto: causal D = 96 (Phi-3 prefill 576 -> 656 TF/s; the short bidirectional BGE sequences,
-// 8 tiles, lose to its longer pipeline fill: 617 -> 531 at D = 64, profiles/r2/attn_bench_v5.txt)
+// 8 tiles, lose to its longer pipeline fill: 617 -> 531 at D = 64, profiles/r2/attn_bench_v5.txt);
+// 3 = on with the speculative softmax (SPEC; auto picks it: Phi-3 prefill 654 -> 689 TF/s,
+// profiles/r3/attn_bench_spec.txt)
 static int g_fa_pipe = 2;
 DA_EXPORT void da_set_flash_pipe(int v) { g_fa_pipe = v; }
 
+template <bool SPEC>
 static int launch_fa_pipe(const void* q, const void* k, const void* v, int ldq, int ldk, int ldv, const void* cu_seqlens,
                           int B, int max_seqlen, int H, int Hkv, int D, int causal, float sl2e, void* o, int ldo,
                           FaPrefix pre, hipStream_t s) {
   static bool attr_set = false;
   if (!attr_set) {
-    (void)hipFuncSetAttribute((const void*)flash_attn_pipe_kernel<96>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    (void)hipFuncSetAttribute((const void*)flash_attn_pipe_kernel<96, SPEC>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               3 * (FA2Cfg<96, 4, 1>::KBUF + FA2Cfg<96, 4, 1>::VBUF));
-    (void)hipFuncSetAttribute((const void*)flash_attn_pipe_kernel<64>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    (void)hipFuncSetAttribute((const void*)flash_attn_pipe_kernel<64, SPEC>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               3 * (FA2Cfg<64, 4, 1>::KBUF + FA2Cfg<64, 4, 1>::VBUF));
     attr_set = true;
   }
   dim3 grid((max_seqlen + 127) / 128, H, B);
 #define FA_ARGS (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, ldq, ldk, ldv, (const int*)cu_seqlens, H, Hkv, \
                 causal, sl2e, (bf16_t*)o, ldo, pre
+#define FA_SMEM(DD) 3 * (FA2Cfg<DD, 4, 1>::KBUF + FA2Cfg<DD, 4, 1>::VBUF)
   switch (D) {
-    case 32: flash_attn_pipe_kernel<32><<<grid, 256, 3 * (FA2Cfg<32, 4, 1>::KBUF + FA2Cfg<32, 4, 1>::VBUF), s>>>(FA_ARGS); break;
-    case 64: flash_attn_pipe_kernel<64><<<grid, 256, 3 * (FA2Cfg<64, 4, 1>::KBUF + FA2Cfg<64, 4, 1>::VBUF), s>>>(FA_ARGS); break;
-    case 96: flash_attn_pipe_kernel<96><<<grid, 256, 3 * (FA2Cfg<96, 4, 1>::KBUF + FA2Cfg<96, 4, 1>::VBUF), s>>>(FA_ARGS); break;
+    case 32: flash_attn_pipe_kernel<32, SPEC><<<grid, 256, FA_SMEM(32), s>>>(FA_ARGS); break;
+    case 64: flash_attn_pipe_kernel<64, SPEC><<<grid, 256, FA_SMEM(64), s>>>(FA_ARGS); break;
+    case 96: flash_attn_pipe_kernel<96, SPEC><<<grid, 256, FA_SMEM(96), s>>>(FA_ARGS); break;
     default: return (int)hipErrorInvalidValue;
   }
+#undef FA_SMEM
 #undef FA_ARGS
   return (int)hipGetLastError();
 }
@@ -1404,9 +1501,12 @@ DA_EXPORT int da_flash_attn_v2(const void* q, const void* k, const void* v, int 
   const float sl2e = scale * 1.4426950408889634f;
   hipStream_t s = (hipStream_t)stream;
   const FaPrefix pre{(const bf16_t*)pre_k, (const bf16_t*)pre_v, pre_hstride, pre_len, g_fa_rev};
-  const bool pipe = g_fa_pipe == 1 || (g_fa_pipe == 2 && causal && D == 96);
-  if (pipe && D <= 96 && g_fa_waves != 8 && g_fa_qh != 2)
-    return launch_fa_pipe(q, k, v, ldq, ldk, ldv, cu_seqlens, B, max_seqlen, H, Hkv, D, causal, sl2e, o, ldo, pre, s);
+  const bool pipe = g_fa_pipe == 1 || g_fa_pipe == 3 || (g_fa_pipe == 2 && causal && D == 96);
+  if (pipe && D <= 96 && g_fa_waves != 8 && g_fa_qh != 2) {
+    if (g_fa_pipe != 1)  // auto (causal D = 96) and 3: speculative softmax (654 -> 689 TF/s, attn_bench)
+      return launch_fa_pipe<true>(q, k, v, ldq, ldk, ldv, cu_seqlens, B, max_seqlen, H, Hkv, D, causal, sl2e, o, ldo, pre, s);
+    return launch_fa_pipe<false>(q, k, v, ldq, ldk, ldv, cu_seqlens, B, max_seqlen, H, Hkv, D, causal, sl2e, o, ldo, pre, s);
+  }
   const int qh = g_fa_qh ? g_fa_qh : 1;
   // auto: 4 waves, except D = 128 (Llama-3 prefill: 8 waves measured faster, profiles/r2/attn_bench_v4.txt)
   const bool w8 = g_fa_waves == 8 || (g_fa_waves == 0 && D == 128);

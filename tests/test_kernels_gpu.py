@@ -207,18 +207,25 @@ def test_flash_attn(D, causal, H, Hkv):
     _close(got, ref, atol=0.02)
 
 
-def test_flash_attn_spike():
-    # force a late rescale: one key dominates one query (online-softmax branch coverage)
-    H, Hkv, D = 2, 2, 64
+@pytest.mark.parametrize("D,pipe", [(64, None), (64, 3), (96, None), (96, 3), (96, 1)])
+def test_flash_attn_spike(D, pipe):
+    # force a late rescale: one key dominates one query (online-softmax branch coverage; with the
+    # speculative softmax (pipe 3) the deferred-max branch, whose overshoot threshold it exceeds)
+    H, Hkv = 2, 2
     L = 300
     qkv = _rand(L, 6 * D, scale=0.3)
     qkv[250, 2 * D:3 * D] = 4.0
     qkv[10, :D] = 4.0
     cu = torch.tensor([0, L], device=DEV, dtype=torch.int32)
     q, k, v = qkv[:, :2 * D], qkv[:, 2 * D:4 * D], qkv[:, 4 * D:]
-    for causal in (False, True):
-        _close(K.flash_attn_varlen(q, k, v, cu, L, H, Hkv, D, causal),
-               R.flash_attn_varlen(q, k, v, cu, L, H, Hkv, D, causal), atol=0.02)
+    if pipe is not None:
+        K.lib().da_set_flash_pipe(pipe)
+    try:
+        for causal in (False, True):
+            _close(K.flash_attn_varlen(q, k, v, cu, L, H, Hkv, D, causal),
+                   R.flash_attn_varlen(q, k, v, cu, L, H, Hkv, D, causal), atol=0.02)
+    finally:
+        K.lib().da_set_flash_pipe(K.FLASH_PIPE_DEFAULT)
 
 
 @pytest.mark.parametrize("D", [64, 96, 128])
@@ -553,7 +560,7 @@ def test_gemv_fused_rmsnorm(N, Kd, epi):
     _close(got, R.gemm(x, w, epi=epi, rms=(g, 1e-5)), atol=0.03)
 
 
-@pytest.mark.parametrize("nw,qh,pipe", [(4, 1, 0), (8, 1, 0), (4, 2, 0), (8, 2, 0), (4, 1, 1)])
+@pytest.mark.parametrize("nw,qh,pipe", [(4, 1, 0), (8, 1, 0), (4, 2, 0), (8, 2, 0), (4, 1, 1), (4, 1, 3)])
 @pytest.mark.parametrize("D,causal", [(64, False), (96, True), (128, True), (32, False), (64, True), (96, False)])
 def test_flash_attn_wave_shapes(nw, qh, pipe, D, causal):
     """Every workgroup shape (waves x 32-query halves per wave, and the software-pipelined kernel)
@@ -659,7 +666,7 @@ def test_gemm_mid_m(M):
 
 
 @pytest.mark.parametrize("H,Hkv,D,P", [(32, 32, 96, 261), (8, 2, 128, 64), (4, 4, 64, 1), (4, 2, 96, 130)])
-@pytest.mark.parametrize("nw,qh,pipe", [(4, 1, 0), (8, 1, 0), (4, 2, 0), (4, 1, 1)])
+@pytest.mark.parametrize("nw,qh,pipe", [(4, 1, 0), (8, 1, 0), (4, 2, 0), (4, 1, 1), (4, 1, 3)])
 def test_flash_attn_shared_prefix(H, Hkv, D, P, nw, qh, pipe):
     """Suffix queries attend to P shared-prefix keys held in a KV-cache slot + their own keys."""
     torch.manual_seed(H + D + P)
