@@ -50,13 +50,13 @@ def main():
         ref = torch.nn.functional.scaled_dot_product_attention(qq, kk, vv, is_causal=causal)
         ref = ref.transpose(1, 2).reshape(T, H * D).float()
         # arms: waves per workgroup x 32-query halves per wave
-        for nw, qh, pipe in ((4, 1, 0), (8, 1, 0), (4, 2, 0), (8, 2, 0), (4, 1, 1), (4, 1, 3)):
+        for nw, qh, pipe in ((4, 1, 0), (8, 1, 0), (4, 2, 0), (8, 2, 0), (4, 1, 1), (4, 1, 3), (4, 1, 4)):
             if (nw * qh > 8 and D > 64) or (pipe and D > 96):
                 continue
             K.lib().da_set_flash_waves(nw)
             K.lib().da_set_flash_qh(qh)
             K.lib().da_set_flash_pipe(pipe)
-            arm = f"w{nw}q{qh}" + ("" if not pipe else "pipe" if pipe == 1 else "spec")
+            arm = f"w{nw}q{qh}" + ("", "pipe", "", "spec", "dma")[pipe]
             t = timeit(lambda: K.flash_attn_varlen(q, k, v, cu, L, H, Hkv, D, causal))
             out = K.flash_attn_varlen(q, k, v, cu, L, H, Hkv, D, causal).float()
             r[arm] = {"ms": round(t, 3), "tflops": round(fl / t / 1e9, 1),

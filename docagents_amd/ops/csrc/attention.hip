@@ -315,15 +315,53 @@ flash_attn_v2_kernel(const bf16_t* __restrict__ q, const bf16_t* __restrict__ k,
 // (ISA: a 12-MFMA block with no VALU, then a 116-VALU + 32-exp block; the SIMD ran them back to back).
 // With SPEC, an unmasked tile (every key visible to every query of the wave) is one straight-line
 // block: S(t + 1) MFMAs interleaved with max(t), p = exp2(s·c - m_run·c) against the STALE running
-// max, row sums and the bf16 pack; only then one wave-uniform test: if any query's tile max exceeds
-// its running max by more than 2^SPEC_TAU in p (first tile of a wave, or a late spike) the tile is
-// redone the exact way — its S recomputed from the K tile still in LDS, then the ordinary
-// max / rescale / exp path — otherwise P·V follows. Masked tiles (causal diagonal, sequence end)
-// always take the exact path. p <= 2^SPEC_TAU keeps the fp32 sums and the bf16 P exact in relative
-// terms; the result is normalised by the same l, so only rounding differs from SPEC = false.
+// max, row sums and the bf16 pack. The reference max of a query moves only when its tile max
+// overshoots it by SPEC_TAU (log2 units of p; the first tile always does), branch-free per lane;
+// only the O rescale that such a move needs is a (rare, wave-uniform) branch before P·V. Masked
+// tiles (causal diagonal, sequence end) take the exact path. p <= 2^SPEC_TAU keeps the fp32 sums
+// and the bf16 P exact in relative terms; the result is normalised by the same l, so only rounding
+// differs from SPEC = false.
+//
+// DMA = true (D = 96, shared prefix a multiple of 64 keys): K / V tiles arrive by LDS-DMA
+// (buffer_load ... lds) instead of register staging, in rings that give each tile TWO steps of
+// latency cover (staging gave one, and a step is ~0.5 us against 1-2 us of loaded HBM / L2
+// latency): at the start of step t the wave issues K(t + 3) into the slot S(t) read in step t - 1
+// and V(t + 2) into the slot P·V(t - 1) read; before the step's barrier it waits for K(t + 2) and
+// V(t + 1) (vmcnt(6): the 3 + 3 pieces of step t may stay in flight). K rows are unpadded (192 B)
+// with 16-B chunk c of row r at slot c ^ ((r >> 2) & 3) — applied on the DMA source side — so the
+// 16 rows one ds_read_b128 lane group reads hit 16 distinct bank slots; V keeps its linear rows.
+// No staging registers, no ds_write, no per-tile address VALU. Past the last tile the pieces are
+// issued at an out-of-range offset (no memory traffic, zeros into a free slot): uniform counts.
 constexpr float SPEC_TAU = 8.f;
 
-template <int D, bool SPEC>
+// Three 1-KiB LDS-DMA pieces (buffer_load_dwordx4 ... lds) into LDS lds, lds + 1 KiB, lds + 2 KiB,
+// lane l's 16 B from rsrc + v_i + soff. Inline asm on purpose: through the builtin, hipcc treats the
+// transposed V reads (ds_read_b64_tr_b16) as possibly aliasing the DMA and drains vmcnt to 0 before
+// them, which would cancel the prefetch; these ops are invisible to its counters, and the kernel
+// waits for them with explicit vmcnt. No VGPR destination (register-safe); M0 is saved and
+// restored inside the statement; s_nop 4 covers an SGPR operand fresh from v_readfirstlane.
+__device__ __forceinline__ void dma3_lds(__amdgpu_buffer_rsrc_t rs, unsigned lds, unsigned v0, unsigned v1,
+                                         unsigned v2, int soff) {
+  unsigned keep;
+  asm volatile(
+      "s_nop 4\n\t"
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %5\n\t"
+      "s_nop 0\n\t"
+      "buffer_load_dwordx4 %1, %4, %6 offen lds\n\t"
+      "s_add_u32 m0, m0, 0x400\n\t"
+      "s_nop 0\n\t"
+      "buffer_load_dwordx4 %2, %4, %6 offen lds\n\t"
+      "s_add_u32 m0, m0, 0x400\n\t"
+      "s_nop 0\n\t"
+      "buffer_load_dwordx4 %3, %4, %6 offen lds\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(v0), "v"(v1), "v"(v2), "s"(rs), "s"(lds), "s"(soff)
+      : "memory", "scc");
+}
+
+template <int D, bool SPEC, bool DMA>
 __global__ void __launch_bounds__(256, 2)
 flash_attn_pipe_kernel(const bf16_t* __restrict__ q, const bf16_t* __restrict__ k, const bf16_t* __restrict__ v,
                        int ldq, int ldk, int ldv, const int* __restrict__ cu, int H, int Hkv, int causal,
@@ -332,6 +370,8 @@ flash_attn_pipe_kernel(const bf16_t* __restrict__ q, const bf16_t* __restrict__ 
   constexpr int KT = C::KT, NDS = D / 16, NDB = D / 32, CPR = C::CPR, LPT = C::LPT, NT = C::NT;
   constexpr bool EVEN = (KT * CPR) % NT == 0;
   static_assert(NDS <= 6, "pipelined flash: D <= 96");
+  static_assert(!DMA || (D == 96 && C::VSTR == D * 2), "DMA tiles: D = 96 (linear V rows)");
+  constexpr int KSTR = DMA ? D * 2 : C::KSTR, KBUF = KT * KSTR, TBUF = KBUF + C::VBUF;
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
   const int b = blockIdx.z, h = blockIdx.y;
@@ -366,6 +406,7 @@ flash_attn_pipe_kernel(const bf16_t* __restrict__ q, const bf16_t* __restrict__ 
   const bf16_t* vbase_p = v + (size_t)s0 * ldv + hk * D;
   const bf16_t* kpre = pre.k + hk * pre.hstride;
   const bf16_t* vpre = pre.v + hk * pre.hstride;
+  auto buf_of = [&](int t) { return smem + (t % 3) * TBUF; };
   u32x4_t kst[LPT], vst[LPT];
   unsigned koff[LPT], voff[LPT];
 #pragma unroll
@@ -375,6 +416,34 @@ flash_attn_pipe_kernel(const bf16_t* __restrict__ q, const bf16_t* __restrict__ 
     koff[i] = in ? (unsigned)(r * ldk * 2 + cc * 16) : 0x80000000u;
     voff[i] = in ? (unsigned)(r * ldv * 2 + cc * 16) : 0x80000000u;
   }
+  // DMA pieces: wave wid fills LDS 16-B positions (3 wid + i) * 64 + lane of a tile (768 = 64 rows x
+  // 12 chunks): row r, slot sl; K slot sl holds chunk sl ^ ((r >> 2) & 3), V slot sl chunk sl
+  unsigned dkr[3], dkc[3], dvc[3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const int pos = (wid * 3 + i) * 64 + lane, r = pos / 12, sl = pos % 12;
+    dkr[i] = r;
+    dkc[i] = (sl ^ ((r >> 2) & 3)) * 16;
+    dvc[i] = sl * 16;
+  }
+  // tile t's K (KV = false) or V pieces into slot t % 3; t >= ntiles: out of range, no traffic
+  auto dma_tile = [&](int t, bool is_v) {
+    const int k0 = t * KT;
+    const bf16_t* base = is_v ? vbase_p : kbase_p;
+    const bf16_t* pbase = is_v ? vpre : kpre;
+    const int ld = is_v ? ldv : ldk;
+    const bool own = k0 >= P;
+    const int o0 = k0 - P;
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(own ? base + (size_t)o0 * ld : pbase + (size_t)k0 * D), (short)0,
+        own ? max(L - o0, 0) * ld * 2 : (P - k0) * D * 2, 0x00020000);
+    const unsigned rstride = own ? ld * 2 : D * 2;
+    const int soff = t < ntiles ? 0 : 0x7ffffff0;
+    typedef __attribute__((address_space(3))) char lds_char;  // LDS byte offset, not the flat address
+    const unsigned dst = (unsigned)(size_t)(lds_char*)(buf_of(t) + (is_v ? KBUF : 0)) + wid * 3 * 1024;
+    dma3_lds(rs, __builtin_amdgcn_readfirstlane(dst), dkr[0] * rstride + (is_v ? dvc[0] : dkc[0]),
+             dkr[1] * rstride + (is_v ? dvc[1] : dkc[1]), dkr[2] * rstride + (is_v ? dvc[2] : dkc[2]), soff);
+  };
   auto load_tile = [&](int t) {
     const int k0 = t * KT;
     if (k0 >= P) {
@@ -407,7 +476,6 @@ flash_attn_pipe_kernel(const bf16_t* __restrict__ q, const bf16_t* __restrict__ 
       }
     }
   };
-  auto buf_of = [&](int t) { return smem + (t % 3) * (C::KBUF + C::VBUF); };
   auto store_tile = [&](int t) {
     char* sK = buf_of(t);
     char* sV = sK + C::KBUF;
@@ -419,6 +487,11 @@ flash_attn_pipe_kernel(const bf16_t* __restrict__ q, const bf16_t* __restrict__ 
         *(u32x4_t*)(sV + r * C::VSTR + cc * 16) = vst[i];
       }
     }
+  };
+  // byte offset of K fragment (32-key half hh, 16-dim step ds) of this lane in a K tile
+  auto kfrag = [&](int hh, int ds) -> int {
+    if constexpr (DMA) return (hh * 32 + qr) * KSTR + (((2 * ds + hi) ^ ((qr >> 2) & 3)) << 4);
+    else return (hh * 32 + qr) * KSTR + ds * 32 + hi * 16;
   };
   // S^T of tile t: all K fragments, then the MFMAs (two independent accumulation chains)
   auto s_tile = [&](int t, f32x16_t (&sa)[2]) {
@@ -434,7 +507,7 @@ flash_attn_pipe_kernel(const bf16_t* __restrict__ q, const bf16_t* __restrict__ 
         bf16x8_t kfr[NDS];
 #pragma unroll
         for (int ds = 0; ds < NDS; ++ds)
-          kfr[ds] = *(const bf16x8_t*)(sK + (hh * 32 + qr) * C::KSTR + ds * 32 + hi * 16);
+          kfr[ds] = *(const bf16x8_t*)(sK + kfrag(hh, ds));
 #pragma unroll
         for (int ds = 0; ds < NDS; ++ds) sa[hh] = mfma32(kfr[ds], qf[ds], sa[hh]);
       }
@@ -444,7 +517,7 @@ flash_attn_pipe_kernel(const bf16_t* __restrict__ q, const bf16_t* __restrict__ 
       for (int hh = 0; hh < 2; ++hh)
 #pragma unroll
         for (int ds = 0; ds < NDS; ++ds)
-          kfr[hh][ds] = *(const bf16x8_t*)(sK + (hh * 32 + qr) * C::KSTR + ds * 32 + hi * 16);
+          kfr[hh][ds] = *(const bf16x8_t*)(sK + kfrag(hh, ds));
 #pragma unroll
       for (int ds = 0; ds < NDS; ++ds)
 #pragma unroll
@@ -453,7 +526,7 @@ flash_attn_pipe_kernel(const bf16_t* __restrict__ q, const bf16_t* __restrict__ 
   };
   // O^T += V^T P^T of tile t, P packed to bf16 (kc = 16-key step)
   auto pv_tile = [&](int t, const u32x4_t (&pw)[4]) {
-    const char* sV = buf_of(t) + C::KBUF;
+    const char* sV = buf_of(t) + KBUF;
 #pragma unroll
     for (int kc = 0; kc < 4; ++kc) {
       const bf16x8_t pb = __builtin_bit_cast(bf16x8_t, pw[kc]);
@@ -562,17 +635,33 @@ flash_attn_pipe_kernel(const bf16_t* __restrict__ q, const bf16_t* __restrict__ 
     pv_tile(t, pw);
   };
 
-  load_tile(0);
-  store_tile(0);
-  if (ntiles > 1) {
-    load_tile(1);
-    store_tile(1);
-  }
-  __syncthreads();
-  if (ntiles > 2) load_tile(2);
   f32x16_t SA[2], SB[2];
-  s_tile(0, SA);
+  auto barrier = [&]() {  // LDS reads done + every wave here (no vmcnt drain: DMA stays in flight)
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  };
+  if constexpr (DMA) {
+    dma_tile(0, false); dma_tile(0, true); dma_tile(1, false); dma_tile(1, true); dma_tile(2, false);
+    asm volatile("s_waitcnt vmcnt(6)" ::: "memory");  // K0 V0 K1 landed (V1 K2 may fly)
+    barrier();
+    s_tile(0, SA);
+    barrier();  // every wave's S(0) reads are done before K(3) refills slot 0
+  } else {
+    load_tile(0);
+    store_tile(0);
+    if (ntiles > 1) {
+      load_tile(1);
+      store_tile(1);
+    }
+    __syncthreads();
+    if (ntiles > 2) load_tile(2);
+    s_tile(0, SA);
+  }
   auto step = [&](int t, f32x16_t (&cur)[2], f32x16_t (&nxt)[2]) {
+    if constexpr (DMA) {
+      dma_tile(t + 3, false);  // slot of K(t): read by S(t) in step t - 1
+      dma_tile(t + 2, true);   // slot of V(t - 1): read by P·V(t - 1) in step t - 1
+    }
     const int kb = t * KT;
     const bool nx = t + 1 < ntiles && (t + 1) * KT < wave_end;
     // unmasked for every query of this wave (the smallest query sees the tile's last key)
@@ -586,14 +675,20 @@ flash_attn_pipe_kernel(const bf16_t* __restrict__ q, const bf16_t* __restrict__ 
       if (nx) s_tile(t + 1, nxt);
       if (kb < wave_end) finish(t, cur);
     }
-    if (t + 2 < ntiles) store_tile(t + 2);   // its buffer (t - 1) % 3 was last read before the previous barrier
-    if (t + 3 < ntiles) load_tile(t + 3);
-    __syncthreads();
+    if constexpr (DMA) {
+      asm volatile("s_waitcnt vmcnt(6)" ::: "memory");  // K(t + 2), V(t + 1) landed
+      barrier();
+    } else {
+      if (t + 2 < ntiles) store_tile(t + 2);   // its buffer (t - 1) % 3 was last read before the previous barrier
+      if (t + 3 < ntiles) load_tile(t + 3);
+      __syncthreads();
+    }
   };
   for (int t = 0; t < ntiles; t += 2) {
     step(t, SA, SB);
     if (t + 1 < ntiles) step(t + 1, SB, SA);
   }
+  if constexpr (DMA) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // trailing no-traffic pieces
 
   const float l_tot = sum_xhalf(l_part);
   const float inv = l_tot > 0.f ? 1.f / l_tot : 0.f;
@@ -1456,34 +1551,44 @@ DA_EXPORT void da_set_flash_qh(int v) { g_fa_qh = v; }
 // software-pipelined kernel (flash_attn_pipe, D <= 96, 4 waves x 32 queries): 0 = off, 1 = on,
 // 2 = auto: causal D = 96 (Phi-3 prefill 576 -> 656 TF/s; the short bidirectional BGE sequences,
 // 8 tiles, lose to its longer pipeline fill: 617 -> 531 at D = 64, profiles/r2/attn_bench_v5.txt);
-// 3 = on with the speculative softmax (SPEC; auto picks it: Phi-3 prefill 654 -> 689 TF/s,
-// profiles/r3/attn_bench_spec.txt)
+// 3 = on with the speculative softmax (SPEC: Phi-3 prefill 654 -> 689 TF/s,
+// profiles/r3/attn_bench_spec.txt); 4 = SPEC with LDS-DMA K / V tiles (D = 96, prefix % 64 == 0,
+// else 3); auto = 4 for causal D = 96
 static int g_fa_pipe = 2;
 DA_EXPORT void da_set_flash_pipe(int v) { g_fa_pipe = v; }
 
-template <bool SPEC>
+template <int D, bool DMA>
+static constexpr int fa_pipe_smem() {
+  return 3 * ((DMA ? 64 * D * 2 : FA2Cfg<D, 4, 1>::KBUF) + FA2Cfg<D, 4, 1>::VBUF);
+}
+
+template <bool SPEC, bool DMA>
 static int launch_fa_pipe(const void* q, const void* k, const void* v, int ldq, int ldk, int ldv, const void* cu_seqlens,
                           int B, int max_seqlen, int H, int Hkv, int D, int causal, float sl2e, void* o, int ldo,
                           FaPrefix pre, hipStream_t s) {
   static bool attr_set = false;
   if (!attr_set) {
-    (void)hipFuncSetAttribute((const void*)flash_attn_pipe_kernel<96, SPEC>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              3 * (FA2Cfg<96, 4, 1>::KBUF + FA2Cfg<96, 4, 1>::VBUF));
-    (void)hipFuncSetAttribute((const void*)flash_attn_pipe_kernel<64, SPEC>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              3 * (FA2Cfg<64, 4, 1>::KBUF + FA2Cfg<64, 4, 1>::VBUF));
+    (void)hipFuncSetAttribute((const void*)flash_attn_pipe_kernel<96, SPEC, DMA>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, fa_pipe_smem<96, DMA>());
+    if constexpr (!DMA)
+      (void)hipFuncSetAttribute((const void*)flash_attn_pipe_kernel<64, SPEC, false>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, fa_pipe_smem<64, false>());
     attr_set = true;
   }
   dim3 grid((max_seqlen + 127) / 128, H, B);
 #define FA_ARGS (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, ldq, ldk, ldv, (const int*)cu_seqlens, H, Hkv, \
                 causal, sl2e, (bf16_t*)o, ldo, pre
-#define FA_SMEM(DD) 3 * (FA2Cfg<DD, 4, 1>::KBUF + FA2Cfg<DD, 4, 1>::VBUF)
-  switch (D) {
-    case 32: flash_attn_pipe_kernel<32, SPEC><<<grid, 256, FA_SMEM(32), s>>>(FA_ARGS); break;
-    case 64: flash_attn_pipe_kernel<64, SPEC><<<grid, 256, FA_SMEM(64), s>>>(FA_ARGS); break;
-    case 96: flash_attn_pipe_kernel<96, SPEC><<<grid, 256, FA_SMEM(96), s>>>(FA_ARGS); break;
-    default: return (int)hipErrorInvalidValue;
+  if constexpr (DMA) {
+    if (D != 96) return (int)hipErrorInvalidValue;
+    flash_attn_pipe_kernel<96, SPEC, true><<<grid, 256, fa_pipe_smem<96, true>(), s>>>(FA_ARGS);
+  } else {
+    switch (D) {
+      case 32: flash_attn_pipe_kernel<32, SPEC, false><<<grid, 256, fa_pipe_smem<32, false>(), s>>>(FA_ARGS); break;
+      case 64: flash_attn_pipe_kernel<64, SPEC, false><<<grid, 256, fa_pipe_smem<64, false>(), s>>>(FA_ARGS); break;
+      case 96: flash_attn_pipe_kernel<96, SPEC, false><<<grid, 256, fa_pipe_smem<96, false>(), s>>>(FA_ARGS); break;
+      default: return (int)hipErrorInvalidValue;
+    }
   }
-#undef FA_SMEM
 #undef FA_ARGS
   return (int)hipGetLastError();
 }
@@ -1501,11 +1606,16 @@ DA_EXPORT int da_flash_attn_v2(const void* q, const void* k, const void* v, int 
   const float sl2e = scale * 1.4426950408889634f;
   hipStream_t s = (hipStream_t)stream;
   const FaPrefix pre{(const bf16_t*)pre_k, (const bf16_t*)pre_v, pre_hstride, pre_len, g_fa_rev};
-  const bool pipe = g_fa_pipe == 1 || g_fa_pipe == 3 || (g_fa_pipe == 2 && causal && D == 96);
+  const bool pipe = g_fa_pipe == 1 || g_fa_pipe == 3 || g_fa_pipe == 4 || (g_fa_pipe == 2 && causal && D == 96);
   if (pipe && D <= 96 && g_fa_waves != 8 && g_fa_qh != 2) {
+    // LDS-DMA tiles (D = 96, prefix in whole 64-key tiles, 16-B aligned operands): modes 2 / 4
+    const bool dma = (g_fa_pipe == 2 || g_fa_pipe == 4) && D == 96 && pre_len % 64 == 0 &&
+                     ((uintptr_t)k | (uintptr_t)v | (uintptr_t)pre_k | (uintptr_t)pre_v) % 16 == 0;
+    if (dma)
+      return launch_fa_pipe<true, true>(q, k, v, ldq, ldk, ldv, cu_seqlens, B, max_seqlen, H, Hkv, D, causal, sl2e, o, ldo, pre, s);
     if (g_fa_pipe != 1)  // auto (causal D = 96) and 3: speculative softmax (654 -> 689 TF/s, attn_bench)
-      return launch_fa_pipe<true>(q, k, v, ldq, ldk, ldv, cu_seqlens, B, max_seqlen, H, Hkv, D, causal, sl2e, o, ldo, pre, s);
-    return launch_fa_pipe<false>(q, k, v, ldq, ldk, ldv, cu_seqlens, B, max_seqlen, H, Hkv, D, causal, sl2e, o, ldo, pre, s);
+      return launch_fa_pipe<true, false>(q, k, v, ldq, ldk, ldv, cu_seqlens, B, max_seqlen, H, Hkv, D, causal, sl2e, o, ldo, pre, s);
+    return launch_fa_pipe<false, false>(q, k, v, ldq, ldk, ldv, cu_seqlens, B, max_seqlen, H, Hkv, D, causal, sl2e, o, ldo, pre, s);
   }
   const int qh = g_fa_qh ? g_fa_qh : 1;
   // auto: 4 waves, except D = 128 (Llama-3 prefill: 8 waves measured faster, profiles/r2/attn_bench_v4.txt)

@@ -207,7 +207,7 @@ def test_flash_attn(D, causal, H, Hkv):
     _close(got, ref, atol=0.02)
 
 
-@pytest.mark.parametrize("D,pipe", [(64, None), (64, 3), (96, None), (96, 3), (96, 1)])
+@pytest.mark.parametrize("D,pipe", [(64, None), (64, 3), (96, None), (96, 3), (96, 1), (96, 4)])
 def test_flash_attn_spike(D, pipe):
     # force a late rescale: one key dominates one query (online-softmax branch coverage; with the
     # speculative softmax (pipe 3) the deferred-max branch, whose overshoot threshold it exceeds)
@@ -560,7 +560,7 @@ def test_gemv_fused_rmsnorm(N, Kd, epi):
     _close(got, R.gemm(x, w, epi=epi, rms=(g, 1e-5)), atol=0.03)
 
 
-@pytest.mark.parametrize("nw,qh,pipe", [(4, 1, 0), (8, 1, 0), (4, 2, 0), (8, 2, 0), (4, 1, 1), (4, 1, 3)])
+@pytest.mark.parametrize("nw,qh,pipe", [(4, 1, 0), (8, 1, 0), (4, 2, 0), (8, 2, 0), (4, 1, 1), (4, 1, 3), (4, 1, 4)])
 @pytest.mark.parametrize("D,causal", [(64, False), (96, True), (128, True), (32, False), (64, True), (96, False)])
 def test_flash_attn_wave_shapes(nw, qh, pipe, D, causal):
     """Every workgroup shape (waves x 32-query halves per wave, and the software-pipelined kernel)
@@ -665,8 +665,9 @@ def test_gemm_mid_m(M):
     _close(K.gemm(a, w, tile=1), ref, atol=0.03)
 
 
-@pytest.mark.parametrize("H,Hkv,D,P", [(32, 32, 96, 261), (8, 2, 128, 64), (4, 4, 64, 1), (4, 2, 96, 130)])
-@pytest.mark.parametrize("nw,qh,pipe", [(4, 1, 0), (8, 1, 0), (4, 2, 0), (4, 1, 1), (4, 1, 3)])
+@pytest.mark.parametrize("H,Hkv,D,P", [(32, 32, 96, 261), (8, 2, 128, 64), (4, 4, 64, 1), (4, 2, 96, 130),
+                                       (32, 32, 96, 256), (4, 2, 96, 64)])
+@pytest.mark.parametrize("nw,qh,pipe", [(4, 1, 0), (8, 1, 0), (4, 2, 0), (4, 1, 1), (4, 1, 3), (4, 1, 4)])
 def test_flash_attn_shared_prefix(H, Hkv, D, P, nw, qh, pipe):
     """Suffix queries attend to P shared-prefix keys held in a KV-cache slot + their own keys."""
     torch.manual_seed(H + D + P)
