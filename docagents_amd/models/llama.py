@@ -266,15 +266,17 @@ class LlamaDecoder:
         tp.all_reduce_(x)
         return x
 
-    def _logits(self, hlast, gather: bool = True):
+    def _logits(self, hlast, gather: bool = True, out=None):
         """Logits of the rows of ``hlast``: the full [B, V] (gather=True; an all-gather of the vocab
-        slices under TP) or this rank's slice [B, V/t] (gather=False: what ``sample`` consumes)."""
+        slices under TP) or this rank's slice [B, V/t] (gather=False: what ``sample`` consumes;
+        ``out`` receives it)."""
         o = self.ops
         if o.gemv_fusable(hlast.shape[0], self.w["lm_head"].shape[0], hlast.shape[1]):
-            logits = o.gemm(hlast.contiguous(), self.w["lm_head"], rms=(self._gain(self.w["norm"]), self.cfg.eps))
+            logits = o.gemm(hlast.contiguous(), self.w["lm_head"], rms=(self._gain(self.w["norm"]), self.cfg.eps),
+                            out=None if gather else out)
         else:
             h = o.rmsnorm(hlast, self.w["norm"], self.cfg.eps)
-            logits = o.gemm(h, self.w["lm_head"])
+            logits = o.gemm(h, self.w["lm_head"], out=None if gather else out)
         return self.tp.all_gather_cols(logits) if gather else logits
 
     def sample(self, logits, temperature: float, seed: int, step: int = 0, **kw):
@@ -330,8 +332,9 @@ class LlamaDecoder:
                 qkv = o.gemm(h, L["wqkv"], out=st.qkv)
             a = self._decode_attn(qkv, li, st)
             self._attn_out_and_mlp(L, a, x)
-        logits = self._logits(x, gather=False)
-        st.logits.copy_(logits)
+        logits = self._logits(x, gather=False, out=st.logits)  # straight into the state (no copy launch)
+        if logits.data_ptr() != st.logits.data_ptr():
+            st.logits.copy_(logits)
         self.sample(st.logits, st.temperature, st.seed, 0, out_tok=st.tokens, out_lp=st.lp, conf=st.conf,
                     active=st.active, ctr=st.pos, pos=st.pos, lens=st.lens, hist=st.hist, start=st.start, eos=st.eos)
         return st.tokens

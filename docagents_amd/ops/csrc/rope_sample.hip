@@ -206,6 +206,70 @@ sample_partial_kernel(const bf16_t* __restrict__ logits, int V, int ld, int v0, 
   }
 }
 
+// Small batches (the batch-1 decode step of the p50 path): one 1024-thread workgroup per row ran
+// two passes over the 32k-entry vocabulary on ONE CU, ~21 us of a ~1.9 ms step. Here the row is cut
+// into chunks of CL entries, one 256-thread workgroup per (chunk, row) produces the same 8-float
+// stats as a vocab-parallel rank (sample_partial_kernel), and sample_finalize_kernel with
+// ranks = chunks picks the token: the same token as sample_kernel (Gumbel noise keyed by the global
+// index, ties to the lower index), the logprob's log-sum-exp combined per chunk.
+constexpr int SAMPLE_CL = 1024;  // vocabulary entries per chunk: 4 per thread, kept in registers
+
+__global__ void __launch_bounds__(256)
+sample_chunk_kernel(const bf16_t* __restrict__ logits, int V, int ld, float temperature, unsigned seed,
+                    unsigned step, const int* __restrict__ ctr, float* __restrict__ stats) {
+  __shared__ float redf[16];
+  __shared__ float bestv[16];
+  __shared__ int besti[16];
+  const int c = blockIdx.x, b = blockIdx.y, NC = gridDim.x;
+  const int v0 = c * SAMPLE_CL;
+  const bf16_t* row = logits + (size_t)b * ld;
+  const float invT = temperature > 0.f ? 1.f / temperature : 0.f;
+  const unsigned rs = ctr ? (unsigned)ctr[b] : step;
+  const unsigned rkey = rs * 131071u + (unsigned)b;
+  float mx = -INFINITY, bv = -INFINITY, xs[4];
+  int bi = v0;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int v = v0 + threadIdx.x + 256 * i;
+    xs[i] = v < V ? bf2f(row[v]) : -INFINITY;
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {  // ascending v per thread: ties keep the lower index
+    const int v = v0 + threadIdx.x + 256 * i;
+    if (v >= V) continue;
+    mx = fmaxf(mx, xs[i]);
+    float score = xs[i];
+    if (temperature > 0.f) score = xs[i] * invT - __logf(-__logf(u01(seed, rkey, (unsigned)v)));
+    if (score > bv) { bv = score; bi = v; }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float ov = __shfl_xor(bv, o, 64);
+    const int oi = __shfl_xor(bi, o, 64);
+    if (ov > bv || (ov == bv && oi < bi)) { bv = ov; bi = oi; }
+  }
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  if (lane == 0) { bestv[wid] = bv; besti[wid] = bi; }
+  const float lmax = block_max(mx, redf);
+  float sacc = 0.f;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) sacc += (xs[i] == -INFINITY) ? 0.f : __expf(xs[i] - lmax);
+  sacc = block_sum(sacc, redf);
+  if (threadIdx.x == 0) {
+    float fv = bestv[0];
+    int fi = besti[0];
+    for (int i = 1; i < nw; ++i)
+      if (bestv[i] > fv || (bestv[i] == fv && besti[i] < fi)) { fv = bestv[i]; fi = besti[i]; }
+    float* o = stats + ((size_t)b * NC + c) * 8;
+    o[0] = fv;
+    o[1] = __int_as_float(fi);
+    o[2] = lmax;
+    o[3] = sacc;
+    o[4] = bf2f(row[fi]);
+    o[5] = o[6] = o[7] = 0.f;
+  }
+}
+
 // gathered: [B][ranks][8] (the per-rank stats, rank-major within a row). One thread per row.
 __global__ void __launch_bounds__(64)
 sample_finalize_kernel(const float* __restrict__ gathered, int B, int ranks, SampleArgs a) {
@@ -259,6 +323,28 @@ DA_EXPORT int da_sample_finalize(const void* gathered, int B, int ranks, void* o
   a.active = (int*)active; a.pos = (int*)pos; a.lens = (int*)lens; a.hist = (int*)hist; a.start = (const int*)start;
   a.hist_ld = hist_ld; a.eos0 = eos0; a.eos1 = eos1; a.eos2 = eos2; a.eos3 = eos3;
   sample_finalize_kernel<<<(B + 63) / 64, 64, 0, (hipStream_t)stream>>>((const float*)gathered, B, ranks, a);
+  DA_LAUNCH_CHECK();
+}
+
+// Chunked small-batch sampler (see sample_chunk_kernel): same arguments as da_sample plus a
+// workspace of >= B * ceil(V / 1024) * 8 floats.
+DA_EXPORT int da_sample_chunked(const void* logits, int B, int V, int ld, float temperature, unsigned seed,
+                                unsigned step, const void* ctr, void* ws, void* out_tok, void* out_lp, void* conf,
+                                void* active, void* pos, void* lens, void* hist, const void* start, int hist_ld,
+                                int eos0, int eos1, int eos2, int eos3, void* stream) {
+  if (hist && (!pos || !start)) return (int)hipErrorInvalidValue;
+  if (V <= 0 || ld < V || !ws) return (int)hipErrorInvalidValue;
+  if (B == 0) return 0;
+  const int NC = (V + SAMPLE_CL - 1) / SAMPLE_CL;
+  sample_chunk_kernel<<<dim3(NC, B), 256, 0, (hipStream_t)stream>>>((const bf16_t*)logits, V, ld, temperature,
+                                                                     seed, step, (const int*)ctr, (float*)ws);
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return (int)e;
+  SampleArgs a{};
+  a.out_tok = (int*)out_tok; a.out_lp = (float*)out_lp; a.conf = (float*)conf;
+  a.active = (int*)active; a.pos = (int*)pos; a.lens = (int*)lens; a.hist = (int*)hist; a.start = (const int*)start;
+  a.hist_ld = hist_ld; a.eos0 = eos0; a.eos1 = eos1; a.eos2 = eos2; a.eos3 = eos3;
+  sample_finalize_kernel<<<(B + 63) / 64, 64, 0, (hipStream_t)stream>>>((const float*)ws, B, NC, a);
   DA_LAUNCH_CHECK();
 }
 

@@ -81,6 +81,8 @@ _SIGS = {
     "da_topk_merge": [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p],
     "da_kmeans_accum": [c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p],
     "da_sample_partial": [c_void_p, c_int, c_int, c_int, c_int, c_float, c_uint, c_uint, c_void_p, c_void_p, c_void_p],
+    "da_sample_chunked": [c_void_p, c_int, c_int, c_int, c_float, c_uint, c_uint] + [c_void_p] * 10
+                         + [c_int] * 5 + [c_void_p],
     "da_sample_finalize": [c_void_p, c_int, c_int] + [c_void_p] * 8 + [c_int] * 5 + [c_void_p],
     "da_stream_create_cumask": [c_uint, ctypes.POINTER(c_uint), ctypes.POINTER(c_void_p)],
     "da_stream_get_cumask": [c_void_p, c_uint, ctypes.POINTER(c_uint)],
@@ -644,6 +646,21 @@ def decode_attn(q, k_cache, v_cache, lens, slot, H, Hkv, D, max_len: int, chunk:
     return out
 
 
+# rows up to which sample() cuts the vocabulary over many workgroups (0: always one per row)
+SAMPLE_CHUNKED_MAX_B = 8
+_SAMPLE_WS: dict = {}
+
+
+def _sample_ws(nfloats: int, device) -> torch.Tensor:
+    """Per-(device, workspace role) fp32 scratch of the chunked sampler. Grows by adding buffers and
+    never frees one: a captured decode graph keeps pointing at the buffer it was captured with."""
+    key = (device.index if device.index is not None else torch.cuda.current_device(), getattr(_ROLE, "name", "main"))
+    bufs = _SAMPLE_WS.setdefault(key, [])
+    if not bufs or bufs[-1].numel() < nfloats:
+        bufs.append(torch.empty(max(nfloats, 16384), dtype=torch.float32, device=device))
+    return bufs[-1]
+
+
 def sample(logits, temperature: float, seed: int, step: int = 0, out_tok=None, out_lp=None, conf=None,
            active=None, ctr=None, pos=None, lens=None, hist=None, start=None, eos=()):
     """Fused temperature sampler (see rope_sample.hip). Returns (tokens, logprobs)."""
@@ -666,6 +683,15 @@ def sample(logits, temperature: float, seed: int, step: int = 0, out_tok=None, o
         _req(pos is not None and start is not None, "hist needs pos and start")
         hist_ld = hist.shape[1]
     e = list(eos)[:4] + [-1] * (4 - min(4, len(eos)))
+    if B <= SAMPLE_CHUNKED_MAX_B and V >= 4096:
+        # few rows: the row is split over ceil(V / 1024) workgroups + a finalize launch (same token;
+        # the batch-1 sampler took ~21 us on one CU, rope_sample.hip sample_chunk_kernel)
+        ws = _sample_ws(B * ((V + 1023) // 1024) * 8, dev)
+        _check(lib().da_sample_chunked(_ptr(logits), B, V, logits.stride(0), float(temperature), seed & 0xffffffff,
+                                       step & 0xffffffff, _ptr(ctr), _ptr(ws), _ptr(out_tok), _ptr(out_lp),
+                                       _ptr(conf), _ptr(active), _ptr(pos), _ptr(lens), _ptr(hist), _ptr(start),
+                                       hist_ld, e[0], e[1], e[2], e[3], _stream()), "sample_chunked")
+        return out_tok, out_lp
     _check(lib().da_sample(_ptr(logits), B, V, logits.stride(0), float(temperature), seed & 0xffffffff,
                            step & 0xffffffff, _ptr(ctr), _ptr(out_tok), _ptr(out_lp), _ptr(conf), _ptr(active),
                            _ptr(pos), _ptr(lens), _ptr(hist), _ptr(start), hist_ld, e[0], e[1], e[2], e[3],

@@ -362,6 +362,42 @@ def test_sample_kernel_rng_matches_reference():
 
 
 @pytest.mark.parametrize("T", [0.0, 0.2, 1.0])
+@pytest.mark.parametrize("B,V", [(1, 32064), (3, 32064), (8, 128256), (2, 5000)])
+def test_sample_chunked_matches_one_workgroup_per_row(T, B, V):
+    """Small batches cut each row over ceil(V / 1024) workgroups + finalize (sample_chunk_kernel):
+    the same tokens and bookkeeping as one workgroup per row (sample_kernel), logprobs to rounding,
+    including a tie between chunks (the lower index wins)."""
+    torch.manual_seed(B * 7 + V)
+    logits = _rand(B, V, scale=3.0)
+    logits[0, 17] = logits[0, V - 3] = 60.0
+
+    def state():
+        return dict(out_tok=torch.zeros(B, dtype=torch.int32, device=DEV), out_lp=torch.zeros(B, device=DEV),
+                    conf=torch.zeros(B, 2, device=DEV),
+                    active=(torch.arange(B, device=DEV) % 5 != 3).int(),
+                    pos=torch.arange(B, dtype=torch.int32, device=DEV) + 40,
+                    lens=torch.arange(B, dtype=torch.int32, device=DEV) + 41,
+                    hist=torch.full((B, 8), -1, dtype=torch.int32, device=DEV),
+                    start=torch.full((B,), 39, dtype=torch.int32, device=DEV))
+    a, b = state(), state()
+    old = K.SAMPLE_CHUNKED_MAX_B
+    try:
+        K.SAMPLE_CHUNKED_MAX_B = 0
+        K.sample(logits, T, 99, 0, ctr=a["pos"], eos=(5,), **a)
+        K.SAMPLE_CHUNKED_MAX_B = 8
+        K.sample(logits, T, 99, 0, ctr=b["pos"], eos=(5,), **b)
+    finally:
+        K.SAMPLE_CHUNKED_MAX_B = old
+    torch.cuda.synchronize()
+    assert a["out_tok"][0].item() == 17 or T > 0
+    for k in a:
+        if k in ("out_lp", "conf"):
+            _close(a[k], b[k], atol=1e-4)
+        else:
+            assert torch.equal(a[k], b[k]), k
+
+
+@pytest.mark.parametrize("T", [0.0, 0.2, 1.0])
 @pytest.mark.parametrize("ranks", [2, 8])
 def test_sample_partial_finalize_matches_full_row(T, ranks):
     """Vocab-parallel sampling: per-slice 8-float summaries + finalize == the
