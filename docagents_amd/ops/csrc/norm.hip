@@ -64,6 +64,49 @@ __global__ void rmsnorm_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict_
   }
 }
 
+// Many-row RMSNorm (prefill chunks: 57k rows of 3072): one WAVE per row, NCH 16-B chunks per lane
+// (D = 64 * 8 * NCH), four rows per workgroup. The one-workgroup-per-row kernel above spends its
+// time in two block barriers per 6 KB row and, at D = 3072, leaves half its threads with one chunk
+// and half with two (4.2 TB/s measured in the QA prefill); here a row is a wave-level sum and every
+// lane issues all its loads up front. Same math and roundings as rmsnorm_kernel.
+template <int NCH>
+__global__ void __launch_bounds__(256)
+rmsnorm_rows_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ resid, const bf16_t* __restrict__ w,
+                    bf16_t* __restrict__ y, int M, int D, float eps, int ldx, int ldy) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (row >= M) return;  // whole wave: no barrier below
+  const bf16_t* xr = x + (size_t)row * ldx;
+  bf16_t* rr = resid ? resid + (size_t)row * D : nullptr;
+  float v[NCH][8];
+  float ss = 0.f;
+#pragma unroll
+  for (int i = 0; i < NCH; ++i) load8(xr + (i * 64 + lane) * 8, v[i]);
+  if (rr) {
+#pragma unroll
+    for (int i = 0; i < NCH; ++i) {
+      float r[8];
+      load8(rr + (i * 64 + lane) * 8, r);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[i][e] += r[e];
+      store8(rr + (i * 64 + lane) * 8, v[i]);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < NCH; ++i)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) ss += v[i][e] * v[i][e];
+  ss = wave_sum(ss);
+  const float inv = rsqrtf(ss / D + eps);
+#pragma unroll
+  for (int i = 0; i < NCH; ++i) {
+    float wv[8];
+    load8(w + (i * 64 + lane) * 8, wv);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[i][e] = v[i][e] * inv * wv[e];
+    store8(y + (size_t)row * ldy + (i * 64 + lane) * 8, v[i]);
+  }
+}
+
 // Optional fused fp8 output of a normalised row held in registers (v[i] = chunk threadIdx.x + i*blockDim):
 // per-row e4m3 quantisation exactly like quant_fp8_rows_kernel, so the next GEMM can run on fp8
 // without a separate quantisation pass over the activations.
@@ -311,6 +354,22 @@ DA_EXPORT int da_rmsnorm(const void* x, int ldx, void* resid, const void* w, voi
                          float eps, void* stream) {
   if (!d_ok(D) || ldx % 8 || ldy % 8) return (int)hipErrorInvalidValue;
   if (M == 0) return 0;
+  // many rows of a width that is whole 512-element wave slices: one wave per row
+  if (M >= 1024 && D % 512 == 0 && D / 512 <= 8) {
+    const dim3 grid((M + 3) / 4);
+#define RMS_ROWS(N) rmsnorm_rows_kernel<N><<<grid, 256, 0, (hipStream_t)stream>>>((const bf16_t*)x, (bf16_t*)resid, \
+                      (const bf16_t*)w, (bf16_t*)y, M, D, eps, ldx, ldy)
+    switch (D / 512) {
+      case 4: RMS_ROWS(4); break;
+      case 6: RMS_ROWS(6); break;
+      case 8: RMS_ROWS(8); break;
+      default: rmsnorm_kernel<<<M, row_threads(D), 0, (hipStream_t)stream>>>((const bf16_t*)x, (bf16_t*)resid,
+                                                                           (const bf16_t*)w, (bf16_t*)y, D, eps,
+                                                                           ldx, ldy);
+    }
+#undef RMS_ROWS
+    DA_LAUNCH_CHECK();
+  }
   rmsnorm_kernel<<<M, row_threads(D), 0, (hipStream_t)stream>>>((const bf16_t*)x, (bf16_t*)resid,
                                                                  (const bf16_t*)w, (bf16_t*)y, D, eps, ldx, ldy);
   DA_LAUNCH_CHECK();

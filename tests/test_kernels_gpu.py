@@ -145,6 +145,24 @@ def test_rmsnorm(D):
     _close(K.rmsnorm(x, w, 1e-5), R.rmsnorm(x, w, 1e-5), atol=0.02)
 
 
+@pytest.mark.parametrize("D", [2048, 3072, 4096, 2560])
+def test_rmsnorm_many_rows(D):
+    """>= 1024 rows of a width made of whole 512-element slices take the one-wave-per-row kernel
+    (2560: not a supported slice count, the per-row workgroup kernel); both vs the fp32 reference,
+    with and without the fused residual add, and row-strided input / output."""
+    M = 1500
+    x, w = _rand(M, D + 64)[:, :D], _rand(D)
+    r1 = _rand(M, D)
+    r2 = r1.clone()
+    got = K.rmsnorm(x, w, 1e-5, resid=r1)
+    _close(got, R.rmsnorm(x, w, 1e-5, resid=r2), atol=0.02)
+    _close(r1, r2, atol=0.01)
+    out = torch.zeros(M, D + 128, device=DEV, dtype=torch.bfloat16)
+    K.rmsnorm(x, w, 1e-5, out=out[:, :D])
+    _close(out[:, :D], R.rmsnorm(x, w, 1e-5), atol=0.02)
+    assert float(out[:, D:].abs().max()) == 0.0
+
+
 @pytest.mark.parametrize("D", [384, 768, 1024])
 def test_layernorm_and_embed(D):
     x, g, b = _rand(19, D), _rand(D), _rand(D)
