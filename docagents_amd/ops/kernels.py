@@ -646,8 +646,9 @@ def decode_attn(q, k_cache, v_cache, lens, slot, H, Hkv, D, max_len: int, chunk:
     return out
 
 
-# rows up to which sample() cuts the vocabulary over many workgroups (0: always one per row)
-SAMPLE_CHUNKED_MAX_B = 8
+# rows up to which sample() cuts the vocabulary over many workgroups (0: always one per row); at
+# batch 64 one workgroup per row leaves 192 CUs idle too
+SAMPLE_CHUNKED_MAX_B = 64
 _SAMPLE_WS: dict = {}
 
 

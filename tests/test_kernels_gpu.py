@@ -380,7 +380,7 @@ def test_sample_kernel_rng_matches_reference():
 
 
 @pytest.mark.parametrize("T", [0.0, 0.2, 1.0])
-@pytest.mark.parametrize("B,V", [(1, 32064), (3, 32064), (8, 128256), (2, 5000)])
+@pytest.mark.parametrize("B,V", [(1, 32064), (3, 32064), (8, 128256), (2, 5000), (64, 32064)])
 def test_sample_chunked_matches_one_workgroup_per_row(T, B, V):
     """Small batches cut each row over ceil(V / 1024) workgroups + finalize (sample_chunk_kernel):
     the same tokens and bookkeeping as one workgroup per row (sample_kernel), logprobs to rounding,
@@ -402,7 +402,7 @@ def test_sample_chunked_matches_one_workgroup_per_row(T, B, V):
     try:
         K.SAMPLE_CHUNKED_MAX_B = 0
         K.sample(logits, T, 99, 0, ctr=a["pos"], eos=(5,), **a)
-        K.SAMPLE_CHUNKED_MAX_B = 8
+        K.SAMPLE_CHUNKED_MAX_B = 64
         K.sample(logits, T, 99, 0, ctr=b["pos"], eos=(5,), **b)
     finally:
         K.SAMPLE_CHUNKED_MAX_B = old
