@@ -368,7 +368,7 @@ class LlamaDecoder:
         L = self.w["layers"][0]
         shapes = [(L["wqkv"], EPI_NONE), (L["wo"], EPI_RESID), (L["w_gu"], EPI_SWIGLU), (L["w_down"], EPI_RESID),
                   (self.w["lm_head"], EPI_NONE)]
-        return all(f(B, w.shape[0], w.shape[1], e) for w, e in shapes) and o.dk_parts(c.hidden) <= 512
+        return all(f(B, w.shape[0], w.shape[1], e) for w, e in shapes) and o.dk_parts(c.hidden, B) <= 512
 
     def _decode_step_dk(self, st: "DecodeState", x: torch.Tensor) -> torch.Tensor:
         """A layer = QKV, attention, O (+ residual, row sums of squares), gate/up + SwiGLU (norm
@@ -377,7 +377,7 @@ class LlamaDecoder:
         c, o = self.cfg, self.ops
         layers = self.w["layers"]
         sa, sb = st.ssq
-        parts = o.dk_parts(c.hidden)
+        parts = o.dk_parts(c.hidden, x.shape[0])
         a_in, norm = o.rmsnorm(x, layers[0]["ln_attn"], c.eps, out=st.h), None
         for li, L in enumerate(layers):
             qkv = o.gemm_dk(a_in, L["wqkv"], out=st.qkv, norm_in=norm)

@@ -257,16 +257,26 @@ gemm_bf16_kernel(GemmArgs p) {
 }
 
 // Split-K reduction + epilogue. One thread per 8 output elements (16-B stores).
+// ssq_in (nullable): deferred RMSNorm of the product's rows — the A rows were the raw residual
+// stream, so by linearity out[m, :] = inv[m] * (A W^T)[m, :], inv[m] = rsqrt(sum_p ssq_in[p][m] /
+// norm_k + eps) over the producer's `parts` row sums ([parts][64] floats; gains folded into W).
 __global__ void __launch_bounds__(256)
 gemm_splitk_reduce(const float* __restrict__ ws, int splits, int M, int N, int epi,
                    const bf16_t* __restrict__ bias, const bf16_t* __restrict__ resid, int ldr,
-                   bf16_t* __restrict__ C, int ldc) {
+                   bf16_t* __restrict__ C, int ldc, const float* __restrict__ ssq_in = nullptr, int parts = 0,
+                   int norm_k = 1, float eps = 0.f) {
   const int nout = (epi == EPI_SWIGLU) ? N / 2 : N;
   const int chunks = nout / 8;
   const size_t total = (size_t)M * chunks;
   for (size_t idx = blockIdx.x * (size_t)blockDim.x + threadIdx.x; idx < total;
        idx += (size_t)gridDim.x * blockDim.x) {
     const int m = (int)(idx / chunks), oc = (int)(idx % chunks) * 8;
+    float inv = 1.f;
+    if (ssq_in) {  // a handful of L2-resident floats per row (fixed summation order)
+      float ss = 0.f;
+      for (int q = 0; q < parts; ++q) ss += ssq_in[q * 64 + m];
+      inv = rsqrtf(ss / norm_k + eps);
+    }
     float v[8];
     if (epi == EPI_SWIGLU) {
       const int grp = oc / 16, within = oc % 16;
@@ -281,7 +291,7 @@ gemm_splitk_reduce(const float* __restrict__ ws, int splits, int M, int N, int e
         for (int e = 0; e < 8; ++e) { g[e] += row[gc + e]; u[e] += row[gc + 16 + e]; }
       }
 #pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] = silu(g[e]) * u[e];
+      for (int e = 0; e < 8; ++e) v[e] = silu(g[e] * inv) * (u[e] * inv);
     } else {
 #pragma unroll
       for (int e = 0; e < 8; ++e) v[e] = 0.f;
@@ -292,6 +302,8 @@ gemm_splitk_reduce(const float* __restrict__ ws, int splits, int M, int N, int e
         v[0] += a[0]; v[1] += a[1]; v[2] += a[2]; v[3] += a[3];
         v[4] += b[0]; v[5] += b[1]; v[6] += b[2]; v[7] += b[3];
       }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] *= inv;
       if (bias) {
 #pragma unroll
         for (int e = 0; e < 8; ++e) v[e] += bf2f(bias[oc + e]);
@@ -613,6 +625,81 @@ DA_EXPORT int da_gemm_resid_rmsnorm(const void* A, int lda, const void* W, void*
   splitk_reduce_resid_rmsnorm<<<M, 256, 0, s>>>((const float*)ws, splits, M, N, (const bf16_t*)bias,
                                                 (const bf16_t*)resid, ldr, (bf16_t*)C, ldc, (const bf16_t*)gamma, eps,
                                                 (bf16_t*)Hout, ldh);
+  DA_LAUNCH_CHECK();
+}
+
+// Split-K reduce of a residual-producing decode GEMM (33..64 rows) in the gemm_dk layer structure:
+// C = resid + sum of the partials (+ bias), and per-row sums of squares of the bf16 rows C holds,
+// one per 512-column part ([N / 512][64] floats: a consumer reads N / 512 floats per row). One wave
+// per (row, 512 columns): no norm here, so no workgroup has to see a whole row — 64 rows x 6
+// blocks instead of the 64 row-workgroups of splitk_reduce_resid_rmsnorm, whose 98 KB of partials
+// per row was read by one CU.
+__global__ void __launch_bounds__(64)
+splitk_reduce_resid_ssq(const float* __restrict__ ws, int splits, int M, int N, const bf16_t* __restrict__ bias,
+                        const bf16_t* __restrict__ resid, int ldr, bf16_t* __restrict__ C, int ldc,
+                        float* __restrict__ ssq_out) {
+  const int m = blockIdx.y, lane = threadIdx.x;
+  const int oc = blockIdx.x * 512 + lane * 8;
+  float v[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) v[e] = 0.f;
+#pragma unroll 8
+  for (int sp = 0; sp < splits; ++sp) {
+    const float* row = ws + ((size_t)sp * M + m) * N + oc;
+    const f32x4_t a = *(const f32x4_t*)row, b = *(const f32x4_t*)(row + 4);
+    v[0] += a[0]; v[1] += a[1]; v[2] += a[2]; v[3] += a[3];
+    v[4] += b[0]; v[5] += b[1]; v[6] += b[2]; v[7] += b[3];
+  }
+  const u32x4_t r = *(const u32x4_t*)(resid + (size_t)m * ldr + oc);
+  u32x4_t o;
+  float sq = 0.f;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const float lo = v[2 * e] + bf2f((bf16_t)(r[e] & 0xffff)) + (bias ? bf2f(bias[oc + 2 * e]) : 0.f);
+    const float hi = v[2 * e + 1] + bf2f((bf16_t)(r[e] >> 16)) + (bias ? bf2f(bias[oc + 2 * e + 1]) : 0.f);
+    o[e] = pack_bf2(lo, hi);
+    const float bl = bf2f((bf16_t)(o[e] & 0xffff)), bh = bf2f((bf16_t)(o[e] >> 16));
+    sq += bl * bl + bh * bh;  // what the stream now holds (bf16)
+  }
+  *(u32x4_t*)(C + (size_t)m * ldc + oc) = o;
+  sq = wave_sum(sq);
+  if (lane == 0) ssq_out[(size_t)blockIdx.x * 64 + m] = sq;
+}
+
+// gemm_dk's contract (DkArgs semantics, csrc/gemm_dk.hip) for 33..64 rows on the 64x128 split-K
+// tiles: epi NONE / BIAS / SWIGLU with an optional deferred norm of A's rows (ssq_in: the raw
+// residual stream as A, the row scale applied in the reduce), or EPI_RESID with optional per-part
+// sums of squares out (ssq_out: [N / 512][64]). splits >= 2 whenever a reduce is needed; ws holds
+// splits * M * N floats.
+DA_EXPORT int da_gemm_dk_splitk(const void* A, int lda, const void* W, void* C, int ldc, const void* bias,
+                                const void* resid, int ldr, int M, int N, int K, int epi, const float* ssq_in,
+                                int ssq_parts, int norm_k, float eps, float* ssq_out, void* ws, int splits,
+                                void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  if (M < 1 || M > 64 || K % 64 || N % 16 || lda % 8 || ldc % 8 || !ws || splits < 2 || (K / 64) % splits)
+    return (int)hipErrorInvalidValue;
+  if (epi == EPI_SWIGLU && N % 32) return (int)hipErrorInvalidValue;
+  if (epi == EPI_RESID && (!resid || ldr % 8 || ssq_in)) return (int)hipErrorInvalidValue;
+  if (ssq_out && (epi != EPI_RESID || N % 512)) return (int)hipErrorInvalidValue;
+  if (ssq_in && (ssq_parts < 1 || norm_k < 1 || !(eps > 0.f))) return (int)hipErrorInvalidValue;
+  if (epi != EPI_NONE && epi != EPI_BIAS && epi != EPI_SWIGLU && epi != EPI_RESID) return (int)hipErrorInvalidValue;
+  GemmArgs a{};
+  a.A = (const bf16_t*)A; a.W = (const bf16_t*)W; a.C = (bf16_t*)C;
+  a.ws = (float*)ws;
+  a.M = M; a.N = N; a.K = K; a.lda = lda; a.ldc = ldc; a.ldr = ldr; a.k_per_split = K / splits;
+  const int err = launch_decode_tile<64, 128>(a, EPI_PARTIAL, splits, s);
+  if (err) return err;
+  if (epi == EPI_RESID && ssq_out) {
+    splitk_reduce_resid_ssq<<<dim3(N / 512, M), 64, 0, s>>>((const float*)ws, splits, M, N, (const bf16_t*)bias,
+                                                            (const bf16_t*)resid, ldr, (bf16_t*)C, ldc, ssq_out);
+    DA_LAUNCH_CHECK();
+  }
+  const int nout = (epi == EPI_SWIGLU) ? N / 2 : N;
+  const size_t work = (size_t)M * (nout / 8);
+  const int blocks = (int)((work + 255) / 256);
+  gemm_splitk_reduce<<<blocks, 256, 0, s>>>((const float*)ws, splits, M, N, epi, (const bf16_t*)bias,
+                                             (const bf16_t*)resid, ldr, (bf16_t*)C, ldc, ssq_in, ssq_parts, norm_k,
+                                             eps);
   DA_LAUNCH_CHECK();
 }
 

@@ -65,6 +65,8 @@ _SIGS = {
     "da_gemm_dk": [c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
                    c_int, c_void_p, c_int, c_int, c_float, c_void_p, c_void_p],
     "da_gemm_dk_parts": [c_int],
+    "da_gemm_dk_splitk": [c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
+                          c_int, c_void_p, c_int, c_int, c_float, c_void_p, c_void_p, c_int, c_void_p],
     "da_set_dk_rb": [c_int],
     "da_set_decode_qfirst": [c_int],
     "da_set_gemv_u": [c_int],
@@ -253,9 +255,12 @@ def gemm(a: torch.Tensor, w: torch.Tensor, bias=None, epi: int = EPI_NONE, resid
 # workgroup and summed through LDS, no split-K partials, no reduce launch). False: the 64x128 /
 # 32x128 tiles + split-K + reduce (bench/ab_arms.py DA_DECODE_DK=0).
 DECODE_DK = True
-# above 32 rows the split-K tiles stay faster (bench/midm_chain.py, profiles/r3/dk/): the narrow
-# dk tiles re-read the activation block once per 16-64 weight rows
-DK_MAX_M = 32
+# 33..64 rows keep the gemm_dk layer structure (norms deferred into the consumer) on the split-K
+# tiles: the narrow dk tiles re-read the activation block once per 16-64 weight rows there
+# (bench/midm_chain.py, profiles/r3/dk/), so gemm_dk() routes those rows to da_gemm_dk_splitk
+# (reduce + residual + row sums of squares; the consumer's reduce applies the row scale)
+DK_MAX_M = 64
+DK_SPLITK_ABOVE = 32
 
 
 def dk_fusable(M: int, N: int, K: int, epi: int = EPI_NONE) -> bool:
@@ -264,8 +269,15 @@ def dk_fusable(M: int, N: int, K: int, epi: int = EPI_NONE) -> bool:
             and epi in (EPI_NONE, EPI_BIAS, EPI_RESID, EPI_SWIGLU) and (epi != EPI_SWIGLU or N % 32 == 0))
 
 
-def dk_parts(N: int) -> int:
-    """Row-norm partial sums an EPI_RESID gemm_dk of width N writes (the consumer's part count)."""
+def _dk_splitk(M: int, N: int) -> bool:
+    return DK_SPLITK_ABOVE < M <= 64 and N % 512 == 0
+
+
+def dk_parts(N: int, M: int = 0) -> int:
+    """Row-norm partial sums an EPI_RESID gemm_dk of width N and M rows writes (the consumer's part
+    count): one per dk output tile, or one per 512 columns on the 33..64-row split-K route."""
+    if _dk_splitk(M, N):
+        return N // 512
     return int(lib().da_gemm_dk_parts(N))
 
 
@@ -295,7 +307,17 @@ def gemm_dk(a, w, epi: int = EPI_NONE, bias=None, resid=None, out=None, norm_in=
         _req(ssq.dtype == torch.float32 and ssq.is_contiguous() and ssq.numel() >= parts * 64, "bad ssq_in")
     if ssq_out is not None:
         _req(epi == EPI_RESID and ssq_out.dtype == torch.float32 and ssq_out.is_contiguous()
-             and ssq_out.numel() >= dk_parts(N) * 64, "bad ssq_out")
+             and ssq_out.numel() >= dk_parts(N, M) * 64, "bad ssq_out")
+    if _dk_splitk(M, N) or (DK_SPLITK_ABOVE < M <= 64 and ssq_out is None):
+        splits = max(2, _auto_splits(M, N, K))
+        while (K // 64) % splits:
+            splits //= 2
+        splits = max(splits, 2)
+        ws = _workspace(splits * M * N * 4, a.device)
+        _check(lib().da_gemm_dk_splitk(_ptr(a), a.stride(0), _ptr(w), _ptr(out), out.stride(0), _ptr(bias), _ptr(resid),
+                                       ldr, M, N, K, epi, _ptr(ssq), parts, K, float(eps), _ptr(ssq_out), _ptr(ws),
+                                       splits, _stream()), "gemm_dk_splitk")
+        return out
     _check(lib().da_gemm_dk(_ptr(a), a.stride(0), _ptr(w), _ptr(out), out.stride(0), _ptr(bias), _ptr(resid), ldr,
                             M, N, K, epi, _ptr(ssq), parts, K, float(eps), _ptr(ssq_out), _stream()), "gemm_dk")
     return out

@@ -439,7 +439,8 @@ def quant_weight_fp8(w):
 DECODE_DK = True
 # above 32 rows the split-K tiles stay faster (bench/midm_chain.py, profiles/r3/dk/): the narrow
 # dk tiles re-read the activation block once per 16-64 weight rows
-DK_MAX_M = 32
+DK_MAX_M = 64
+DK_SPLITK_ABOVE = 32
 
 
 def dk_fusable(M, N, K, epi=EPI_NONE):
@@ -447,8 +448,11 @@ def dk_fusable(M, N, K, epi=EPI_NONE):
             and epi in (EPI_NONE, EPI_BIAS, EPI_RESID, EPI_SWIGLU) and (epi != EPI_SWIGLU or N % 32 == 0))
 
 
-def dk_parts(N):
-    """gemm_dk.hip dk_bn for EPI_RESID: row-norm partial sums written per output tile."""
+def dk_parts(N, M=0):
+    """gemm_dk.hip dk_bn for EPI_RESID: row-norm partial sums written per output tile; 33..64 rows
+    (the split-K route, gemm.hip splitk_reduce_resid_ssq): one per 512 columns."""
+    if DK_SPLITK_ABOVE < M <= 64 and N % 512 == 0:
+        return N // 512
     bn = 64 if N // 64 >= 192 else (32 if N // 32 >= 192 else 16)
     return (N + bn - 1) // bn
 
@@ -465,7 +469,7 @@ def gemm_dk(a, w, epi=EPI_NONE, bias=None, resid=None, out=None, norm_in=None, s
         x = (x * inv[:, None]).to(torch.bfloat16).float()
     y = _epilogue(x @ w.float().t(), N, bias, epi, resid, out)
     if ssq_out is not None:
-        parts = dk_parts(N)
+        parts = dk_parts(N, M)
         bn = -(-N // parts)
         y2 = y.float().pow(2)
         sq = torch.stack([y2[:, i * bn:(i + 1) * bn].sum(-1) for i in range(parts)])  # [parts, M]

@@ -803,7 +803,7 @@ def test_gemm_dk_deferred_norm_chain(M, H, F):
     wgu = _rand(2 * F, H, scale=H ** -0.5)
     x_ref = x.clone()
     ssq = torch.zeros(512 * 64, dtype=torch.float32, device=DEV)
-    parts = K.dk_parts(H)
+    parts = K.dk_parts(H, M)  # 33..64 rows: the split-K route's 512-column parts
     K.gemm_dk(a, wo, epi=K.EPI_RESID, resid=x, out=x, ssq_out=ssq)
     y = R.gemm(a, wo, epi=K.EPI_RESID, resid=x_ref)
     _close(x, y, atol=0.03)
