@@ -270,22 +270,33 @@ sample_chunk_kernel(const bf16_t* __restrict__ logits, int V, int ld, float temp
   }
 }
 
-// gathered: [B][ranks][8] (the per-rank stats, rank-major within a row). One thread per row.
+// gathered: [B][ranks][8] (the per-rank stats, rank-major within a row). One wave per row: lane r
+// takes ranks r, r + 64, ... (one thread walking up to 126 ranks serially was ~12 us of the
+// batch-1 step); winner = max score, ties to the lower index, as in sample_kernel.
 __global__ void __launch_bounds__(64)
 sample_finalize_kernel(const float* __restrict__ gathered, int B, int ranks, SampleArgs a) {
-  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  const int b = blockIdx.x, lane = threadIdx.x;
   if (b >= B) return;
   const float* g = gathered + (size_t)b * ranks * 8;
-  float fv = g[0], xb = g[4], gmax = g[2];
-  int fi = __float_as_int(g[1]);
-  for (int r = 1; r < ranks; ++r) {
+  float fv = -INFINITY, xb = 0.f, lm = -INFINITY;
+  int fi = 0x7fffffff;
+  for (int r = lane; r < ranks; r += 64) {
     const float* q = g + r * 8;
     const int qi = __float_as_int(q[1]);
     if (q[0] > fv || (q[0] == fv && qi < fi)) { fv = q[0]; fi = qi; xb = q[4]; }
-    gmax = fmaxf(gmax, q[2]);
+    lm = fmaxf(lm, q[2]);
   }
-  float s = 0.f;
-  for (int r = 0; r < ranks; ++r) s += g[r * 8 + 3] * __expf(g[r * 8 + 2] - gmax);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float ov = __shfl_xor(fv, o, 64), ox = __shfl_xor(xb, o, 64);
+    const int oi = __shfl_xor(fi, o, 64);
+    if (ov > fv || (ov == fv && oi < fi)) { fv = ov; fi = oi; xb = ox; }
+  }
+  const float gmax = wave_max(lm);
+  float sp = 0.f;
+  for (int r = lane; r < ranks; r += 64) sp += g[r * 8 + 3] * __expf(g[r * 8 + 2] - gmax);
+  const float s = wave_sum(sp);
+  if (lane != 0) return;
   const float lp = xb - gmax - __logf(s);
   const bool on = a.active ? a.active[b] != 0 : true;
   if (!on) return;
@@ -322,7 +333,7 @@ DA_EXPORT int da_sample_finalize(const void* gathered, int B, int ranks, void* o
   a.out_tok = (int*)out_tok; a.out_lp = (float*)out_lp; a.conf = (float*)conf;
   a.active = (int*)active; a.pos = (int*)pos; a.lens = (int*)lens; a.hist = (int*)hist; a.start = (const int*)start;
   a.hist_ld = hist_ld; a.eos0 = eos0; a.eos1 = eos1; a.eos2 = eos2; a.eos3 = eos3;
-  sample_finalize_kernel<<<(B + 63) / 64, 64, 0, (hipStream_t)stream>>>((const float*)gathered, B, ranks, a);
+  sample_finalize_kernel<<<B, 64, 0, (hipStream_t)stream>>>((const float*)gathered, B, ranks, a);
   DA_LAUNCH_CHECK();
 }
 
@@ -344,7 +355,7 @@ DA_EXPORT int da_sample_chunked(const void* logits, int B, int V, int ld, float 
   a.out_tok = (int*)out_tok; a.out_lp = (float*)out_lp; a.conf = (float*)conf;
   a.active = (int*)active; a.pos = (int*)pos; a.lens = (int*)lens; a.hist = (int*)hist; a.start = (const int*)start;
   a.hist_ld = hist_ld; a.eos0 = eos0; a.eos1 = eos1; a.eos2 = eos2; a.eos3 = eos3;
-  sample_finalize_kernel<<<(B + 63) / 64, 64, 0, (hipStream_t)stream>>>((const float*)ws, B, NC, a);
+  sample_finalize_kernel<<<B, 64, 0, (hipStream_t)stream>>>((const float*)ws, B, NC, a);
   DA_LAUNCH_CHECK();
 }
 
