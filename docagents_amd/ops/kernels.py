@@ -273,6 +273,19 @@ def _dk_splitk(M: int, N: int) -> bool:
     return DK_SPLITK_ABOVE < M <= 64 and N % 512 == 0
 
 
+def _dk_splits(N: int, K: int) -> int:
+    """Split-K of the 33..64-row route (64x128 tiles): the largest of 2, 3, 4, 6, 8, 12, 16 that keeps
+    the grid within one round of 256 workgroups and >= 4 K-steps of 64 per split; at least 2 (the
+    reduce carries the epilogue). 3 is the point of this list: the Phi-3 QKV projection (72 tiles)
+    18.7 us at 3 splits vs 21.8 at 2 and 25.7 at 4 (bench/splitk_m64.py, profiles/r3/splitk_m64.txt)."""
+    tiles, ks = (N + 127) // 128, K // 64
+    best = 2
+    for s in (2, 3, 4, 6, 8, 12, 16):
+        if ks % s == 0 and ks // s >= 4 and tiles * s <= 256:
+            best = s
+    return best if ks % best == 0 else 2
+
+
 def dk_parts(N: int, M: int = 0) -> int:
     """Row-norm partial sums an EPI_RESID gemm_dk of width N and M rows writes (the consumer's part
     count): one per dk output tile, or one per 512 columns on the 33..64-row split-K route."""
@@ -309,10 +322,7 @@ def gemm_dk(a, w, epi: int = EPI_NONE, bias=None, resid=None, out=None, norm_in=
         _req(epi == EPI_RESID and ssq_out.dtype == torch.float32 and ssq_out.is_contiguous()
              and ssq_out.numel() >= dk_parts(N, M) * 64, "bad ssq_out")
     if _dk_splitk(M, N) or (DK_SPLITK_ABOVE < M <= 64 and ssq_out is None):
-        splits = max(2, _auto_splits(M, N, K))
-        while (K // 64) % splits:
-            splits //= 2
-        splits = max(splits, 2)
+        splits = _dk_splits(N, K)
         ws = _workspace(splits * M * N * 4, a.device)
         _check(lib().da_gemm_dk_splitk(_ptr(a), a.stride(0), _ptr(w), _ptr(out), out.stride(0), _ptr(bias), _ptr(resid),
                                        ldr, M, N, K, epi, _ptr(ssq), parts, K, float(eps), _ptr(ssq_out), _ptr(ws),
