@@ -23,6 +23,8 @@ in-place all-reduce yields x + sum of partials.
 """
 from __future__ import annotations
 
+import os
+
 import numpy as np
 import torch
 
@@ -30,7 +32,9 @@ from ..ops import get_ops
 from ..ops.reference import interleave_gate_up, rope_table
 from .configs import DecoderConfig
 
-EPI_NONE, EPI_SWIGLU, EPI_RESID = 0, 3, 4
+EPI_NONE, EPI_SWIGLU, EPI_RESID, EPI_ROPE = 0, 3, 4, 6
+# DA_PREFILL_NORM_FUSE=0 keeps the separate RMSNorm kernels in the prefill (A/B measurements)
+_PREFILL_NORM_FUSE = os.environ.get("DA_PREFILL_NORM_FUSE", "1") != "0"
 # Decode step of MHA models: RoPE + KV-cache write folded into the attention kernel (False: separate
 # rope_cache launch; the GPU tests compare both).
 _FUSED_ROPE_DECODE = True
@@ -298,6 +302,9 @@ class LlamaDecoder:
         c, o, cache = self.cfg, self.ops, self.cache
         D, hl, kl = c.head_dim, self.hl, self.kl
         x = o.embed(ids, self.w["embed"])
+        if self._prefill_norms_fusable(x.shape[0]):
+            x = self._prefill_fused_norms(x, pos, slot_tok, cu, max_seqlen, prefix)
+            return self._logits(x.index_select(0, last_idx), gather=not local_logits)
         hook = self.layer_hook
         for li, L in enumerate(self.w["layers"]):
             if hook is not None:  # e.g. move the rest of a prefill to another (CU-masked) stream
@@ -311,6 +318,47 @@ class LlamaDecoder:
             del qkv, h
             x = self._attn_out_and_mlp(L, a, x)
         return self._logits(x.index_select(0, last_idx), gather=not local_logits)
+
+    def _prefill_norms_fusable(self, T: int) -> bool:
+        c = self.cfg
+        return (_PREFILL_NORM_FUSE and self.tp.size == 1 and self.unit_gains and c.hidden % 256 == 0
+                and self.ops.prefill_norm_fusable(T, c.hidden))
+
+    def _prefill_fused_norms(self, x, pos, slot_tok, cu, max_seqlen, prefix):
+        """Prefill with every RMSNorm after the first folded into the projections (csrc/gemm.hip
+        da_gemm8p_norm; gains already folded into the weights): the O / down projections (EPI_RESID)
+        also write the new residual rows' per-64-column sums of squares, and the next QKV (+ RoPE +
+        KV write) / gate-up (SwiGLU) projection reads the raw residual stream and scales its output
+        rows by rsqrt(mean square + eps) — no separate norm pass over x (2 per layer)."""
+        c, o, cache = self.cfg, self.ops, self.cache
+        D, hl, kl = c.head_dim, self.hl, self.kl
+        T, Hd = x.shape
+        parts = Hd // 64
+        ssq_attn = torch.empty(parts * T, dtype=torch.float32, device=x.device)
+        ssq_mlp = torch.empty_like(ssq_attn)
+        hook = self.layer_hook
+        for li, L in enumerate(self.w["layers"]):
+            if hook is not None:
+                hook(li)
+            rope = (pos, self.cos_sin, hl, kl, D, slot_tok, cache.k(li), cache.v(li))
+            if li == 0:
+                h = o.rmsnorm(x, L["ln_attn"], c.eps)
+                qkv = o.gemm_rope(h, L["wqkv"], pos, self.cos_sin, hl, kl, D, slot_tok, cache.k(li), cache.v(li))
+                del h
+            else:
+                qkv = o.gemm8p_norm(x, L["wqkv"], EPI_ROPE, norm_in=(ssq_attn, parts, c.eps), rope=rope)
+            pre = None if prefix is None else (cache.k(li)[prefix[0]], cache.v(li)[prefix[0]], prefix[1])
+            a = o.flash_attn_varlen(qkv[:, :hl * D], qkv[:, hl * D:(hl + kl) * D], qkv[:, (hl + kl) * D:], cu,
+                                    max_seqlen, hl, kl, D, causal=True, prefix=pre)
+            del qkv
+            o.gemm8p_norm(a, L["wo"], EPI_RESID, resid=x, out=x, ssq_out=ssq_mlp)
+            g = o.gemm8p_norm(x, L["w_gu"], EPI_SWIGLU, norm_in=(ssq_mlp, parts, c.eps))
+            o.gemm8p_norm(g, L["w_down"], EPI_RESID, resid=x, out=x, ssq_out=ssq_attn)
+            del a, g
+        if x.is_cuda:  # a layer hook may have moved the rest onto another stream: keep the sums alive there
+            for t in (ssq_attn, ssq_mlp):
+                t.record_stream(torch.cuda.current_stream())
+        return x
 
     # ------------------------------------------------------------- decode (graph-capturable)
     def decode_step(self, st: "DecodeState") -> torch.Tensor:

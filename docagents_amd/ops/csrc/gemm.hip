@@ -719,6 +719,38 @@ DA_EXPORT int da_gemm_rope(const void* A, int lda, const void* W, void* C, int l
   return launch_gemm8p(a, EPI_ROPE, (hipStream_t)stream, t256 >= 256 ? 256 : 128);
 }
 
+// Prefill projection on the phase-split kernel with the layer RMSNorms folded in (gemm.h GemmArgs
+// ssq_in / ssq_out): a consumer (QKV + RoPE + KV write, gate/up + SwiGLU) reads the raw residual
+// stream and scales its output rows by the norm from the producer's row sums; a producer (EPI_RESID:
+// O / down projection) writes those sums ([N / 64][M] floats). Same tile choice as da_gemm_bf16 /
+// da_gemm_rope. Rope args are used only by EPI_ROPE.
+DA_EXPORT int da_gemm8p_norm(const void* A, int lda, const void* W, void* C, int ldc, const void* bias,
+                             const void* resid, int ldr, int M, int N, int K, int epi, const float* ssq_in,
+                             int ssq_parts, int norm_k, float eps, float* ssq_out, const void* pos, const void* slot,
+                             const void* cos_sin, void* k_cache, void* v_cache, int H, int Hkv, int D, int max_seq,
+                             void* stream) {
+  if (K % 64 || K < 128 || N % 8 || lda % 8 || ldc % 8 || M < 256) return (int)hipErrorInvalidValue;
+  if (epi != EPI_ROPE && epi != EPI_SWIGLU && epi != EPI_RESID && epi != EPI_NONE && epi != EPI_BIAS)
+    return (int)hipErrorInvalidValue;
+  if (ssq_out && (epi != EPI_RESID || N % 256)) return (int)hipErrorInvalidValue;
+  if (epi == EPI_RESID && (!resid || ldr % 8 || ssq_in)) return (int)hipErrorInvalidValue;
+  if (ssq_in && (ssq_parts < 1 || norm_k < 1 || !(eps > 0.f))) return (int)hipErrorInvalidValue;
+  if (epi == EPI_ROPE && (N != (H + 2 * Hkv) * D || D % 8 || !pos || !slot || !cos_sin || !k_cache || !v_cache))
+    return (int)hipErrorInvalidValue;
+  if (epi == EPI_SWIGLU && N % 32) return (int)hipErrorInvalidValue;
+  GemmArgs a{};
+  a.A = (const bf16_t*)A; a.W = (const bf16_t*)W; a.C = (bf16_t*)C;
+  a.bias = (const bf16_t*)bias; a.resid = (const bf16_t*)resid;
+  a.M = M; a.N = N; a.K = K; a.lda = lda; a.ldc = ldc; a.ldr = ldr; a.k_per_split = K;
+  a.ssq_in = ssq_in; a.ssq_parts = ssq_parts; a.norm_k = norm_k; a.norm_eps = eps; a.ssq_out = ssq_out;
+  if (epi == EPI_ROPE)
+    a.rope = RopeArgs{(const int*)pos, (const int*)slot, (const float*)cos_sin, (bf16_t*)k_cache, (bf16_t*)v_cache,
+                      H, Hkv, D, max_seq};
+  const long t256 = (long)((M + 255) / 256) * ((N + 255) / 256);
+  const int bm = epi == EPI_ROPE ? (t256 >= 256 ? 256 : 128) : (t256 >= 128 ? 256 : 128);
+  return launch_gemm8p(a, epi, (hipStream_t)stream, bm);
+}
+
 // Tile selection: big tiles when the grid fills 256 CUs, skinny tiles (+ split-K) for decode-sized M.
 // tile: 0 = auto, 1 = 128x128, 2 = 64x128, 3 = 32x128, 4 / 7 = 256x256 phase-split (gemm8p),
 // 6 = GEMV (M = 1), 8 = 128x128 PF4, 9 = 128x64 PF4, 10 = 128x256 phase-split (gemm8p).

@@ -220,6 +220,28 @@ gemm8p_kernel(GemmArgs p) {
 #undef ISSUE_B
   __syncthreads();
 
+  // ---- deferred RMSNorm of A's rows (p.ssq_in): inv per tile row from the producer's 64-column
+  //      sums of squares, summed in a fixed order (part q by group q % G, then the groups)
+  __shared__ float snorm[4][BM], sinv[BM];
+  if (p.ssq_in) {
+    constexpr int G = 512 / BM;
+    const int r = tid % BM, grp = tid / BM, gm = m0 + r;
+    float ss = 0.f;
+    if (gm < p.M)
+      for (int q = grp; q < p.ssq_parts; q += G) ss += p.ssq_in[(size_t)q * p.M + gm];
+    snorm[grp][r] = ss;
+    __syncthreads();
+    if (tid < BM) {
+      float tot = 0.f;
+#pragma unroll
+      for (int g = 0; g < G; ++g) tot += snorm[g][tid];
+      sinv[tid] = rsqrtf(tot / p.norm_k + p.norm_eps);
+    }
+    __syncthreads();
+  }
+  // tile row of accumulator acc[ih][.][i][.][q]
+  auto arow = [&](int ih, int i, int q) { return ih * (BM / 2) + wg * QR + i * 16 + fg * 4 + q; };
+
   // ---- epilogue: registers -> (bias / GELU / SwiGLU) -> bf16 staging -> coalesced stores.
   //      Staged row lr = ih*QR + i*16 + fg*4 + q (tile row ih*BM/2 + wg*QR + (lr % QR)),
   //      staged column lc = jh*32 + j*16 + fr (tile column jh*128 + wn*32 + (lc & 31)).
@@ -235,7 +257,8 @@ gemm8p_kernel(GemmArgs p) {
         for (int i = 0; i < MI; ++i)
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
-            const float v = silu(acc[ih][jh][i][0][q]) * acc[ih][jh][i][1][q];
+            const float iv = p.ssq_in ? sinv[arow(ih, i, q)] : 1.f;
+            const float v = silu(acc[ih][jh][i][0][q] * iv) * (acc[ih][jh][i][1][q] * iv);
             *(bf16_t*)(st + (ih * QR + i * 16 + fg * 4 + q) * SROW + (jh * 16 + fr) * 2) = f2bf(v);
           }
   } else {
@@ -259,7 +282,8 @@ gemm8p_kernel(GemmArgs p) {
           for (int j = 0; j < 2; ++j)
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
-              float v = acc[ih][jh][i][j][q] + bv[jh][j];
+              const float iv = p.ssq_in ? sinv[arow(ih, i, q)] : 1.f;
+              float v = acc[ih][jh][i][j][q] * iv + bv[jh][j];
               if constexpr (EPI == EPI_GELU) v = gelu_erf(v);
               *(bf16_t*)(st + (ih * QR + i * 16 + fg * 4 + q) * SROW + (jh * 32 + j * 16 + fr) * 2) = f2bf(v);
             }
@@ -284,9 +308,13 @@ gemm8p_kernel(GemmArgs p) {
     rhead = rel / R.D;
     rd0 = rel % R.D;
   }
+  // EPI_RESID + ssq_out: the 8 lanes of a staged row (CPR = 8: two 32-column runs of this wave)
+  // also sum the squares of the bf16 values they store -> one part per (column tile, wave)
+  const bool ssq = EPI == EPI_RESID && p.ssq_out != nullptr;
   for (int lr = lane / CPR; lr < BM / 2; lr += RPI) {
     const int gm = m0 + (lr / QR) * (BM / 2) + wg * QR + (lr % QR);
-    if (gm >= p.M || gcol >= ncols) continue;
+    const bool ok = gm < p.M && gcol < ncols;
+    if (!ssq && !ok) continue;
     u32x4_t v = *(const u32x4_t*)(st + lr * SROW + (jh * HC + cc) * 2);
     if constexpr (EPI == EPI_ROPE) {
       // same bf16 roundings as GEMM -> rope_cache: rotate the bf16-rounded outputs in fp32
@@ -312,15 +340,29 @@ gemm8p_kernel(GemmArgs p) {
       }
     }
     if constexpr (EPI == EPI_RESID) {
-      const u32x4_t r = *(const u32x4_t*)(p.resid + (size_t)gm * p.ldr + gcol);
+      if (ok) {
+        const u32x4_t r = *(const u32x4_t*)(p.resid + (size_t)gm * p.ldr + gcol);
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const float lo = bf2f((bf16_t)(v[e] & 0xffff)) + bf2f((bf16_t)(r[e] & 0xffff));
-        const float hi = bf2f((bf16_t)(v[e] >> 16)) + bf2f((bf16_t)(r[e] >> 16));
-        v[e] = pack_bf2(lo, hi);
+        for (int e = 0; e < 4; ++e) {
+          const float lo = bf2f((bf16_t)(v[e] & 0xffff)) + bf2f((bf16_t)(r[e] & 0xffff));
+          const float hi = bf2f((bf16_t)(v[e] >> 16)) + bf2f((bf16_t)(r[e] >> 16));
+          v[e] = pack_bf2(lo, hi);
+        }
+      }
+      if (ssq) {
+        float sq = 0.f;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float lo = bf2f((bf16_t)(v[e] & 0xffff)), hi = bf2f((bf16_t)(v[e] >> 16));
+          sq += lo * lo + hi * hi;
+        }
+        if (!ok) sq = 0.f;
+#pragma unroll
+        for (int x = 1; x < CPR; x <<= 1) sq += __shfl_xor(sq, x, 64);
+        if (ch == 0 && gm < p.M) p.ssq_out[(size_t)((n0 / BN) * 4 + wn) * p.M + gm] = sq;
       }
     }
-    *(u32x4_t*)(p.C + (size_t)gm * p.ldc + gcol) = v;
+    if (ok) *(u32x4_t*)(p.C + (size_t)gm * p.ldc + gcol) = v;
   }
 }
 

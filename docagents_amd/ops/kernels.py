@@ -22,6 +22,7 @@ _LOCK = threading.Lock()
 _LIB_PATH = Path(__file__).resolve().parent / "_da_kernels.so"
 
 EPI_NONE, EPI_BIAS, EPI_GELU, EPI_SWIGLU, EPI_RESID = 0, 1, 2, 3, 4
+EPI_ROPE = 6  # gemm8p only: QKV + RoPE + KV-cache write
 # flash prefill kernel choice: 2 = auto (software-pipelined kernel for causal D = 96), 1 / 0 = force
 # on / off; must match g_fa_pipe's initial value in attention.hip (tests restore it after an A/B arm)
 FLASH_PIPE_DEFAULT = 2
@@ -35,6 +36,8 @@ _SIGS = {
                      c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_float, c_void_p],
     "da_gemm_rope": [c_void_p, c_int, c_void_p, c_void_p, c_int, c_int, c_int, c_int] + [c_void_p] * 5
                     + [c_int] * 4 + [c_void_p],
+    "da_gemm8p_norm": [c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
+                       c_int, c_void_p, c_int, c_int, c_float, c_void_p] + [c_void_p] * 5 + [c_int] * 4 + [c_void_p],
     "da_gemm_fp8": [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int,
                     c_int, c_int, c_int, c_int, c_void_p],
     "da_quant_fp8_rows": [c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p],
@@ -360,6 +363,47 @@ def gemm_rope(a, w, pos, cos_sin, H: int, Hkv: int, D: int, slot, k_cache, v_cac
     _check(lib().da_gemm_rope(_ptr(a), a.stride(0), _ptr(w), _ptr(out), out.stride(0), M, N, K, _ptr(pos), _ptr(slot),
                               _ptr(cos_sin), _ptr(k_cache), _ptr(v_cache), H, Hkv, D, k_cache.shape[2], _stream()),
            "gemm_rope")
+    return out
+
+
+def prefill_norm_fusable(M: int, K: int) -> bool:
+    """True when a prefill projection of M rows runs on the phase-split kernel, whose epilogues fold
+    the layer RMSNorms in (gemm8p_norm)."""
+    return M >= 640 and K % 64 == 0 and K >= 128
+
+
+def gemm8p_norm(a, w, epi: int, out=None, resid=None, bias=None, norm_in=None, ssq_out=None, rope=None):
+    """Prefill projection with the RMSNorms folded in (csrc/gemm.hip da_gemm8p_norm):
+    norm_in = (ssq [parts * M] fp32, parts, eps): ``a`` is the raw residual stream, each output row is
+    scaled by rsqrt(sum of its parts / K + eps) before the epilogue (gains folded into w);
+    ssq_out (EPI_RESID): fp32 [N // 64 * M] receives per-64-column sums of squares of the new rows.
+    rope = (pos, cos_sin, H, Hkv, D, slot, k_cache, v_cache) for EPI_ROPE (QKV + RoPE + KV write)."""
+    _bf16_cuda(a, "a"); _bf16_cuda(w, "w")
+    M, K = a.shape
+    N = w.shape[0]
+    _req(prefill_norm_fusable(M, K) and w.shape[1] == K and a.stride(1) == 1 and a.stride(0) % 8 == 0
+         and w.is_contiguous(), f"gemm8p_norm shape M={M} N={N} K={K}")
+    nout = N // 2 if epi == EPI_SWIGLU else N
+    if out is None:
+        out = torch.empty((M, nout), dtype=torch.bfloat16, device=a.device)
+    _req(out.shape == (M, nout) and out.stride(1) == 1 and out.stride(0) % 8 == 0, "bad out")
+    ldr = 0
+    if epi == EPI_RESID:
+        _req(resid is not None and resid.shape == (M, N) and resid.stride(1) == 1, "bad resid")
+        ldr = resid.stride(0)
+    ssq, parts, eps = (None, 0, 0.0) if norm_in is None else norm_in
+    if ssq is not None:
+        _req(ssq.dtype == torch.float32 and ssq.numel() >= parts * M, "bad ssq_in")
+    if ssq_out is not None:
+        _req(ssq_out.dtype == torch.float32 and ssq_out.numel() >= (N // 64) * M, "bad ssq_out")
+    pos = cs = slot = kc = vc = None
+    H = Hkv = D = max_seq = 0
+    if epi == EPI_ROPE:
+        pos, cs, H, Hkv, D, slot, kc, vc = rope
+        max_seq = kc.shape[2]
+    _check(lib().da_gemm8p_norm(_ptr(a), a.stride(0), _ptr(w), _ptr(out), out.stride(0), _ptr(bias), _ptr(resid), ldr,
+                                M, N, K, epi, _ptr(ssq), parts, K, float(eps), _ptr(ssq_out), _ptr(pos), _ptr(slot),
+                                _ptr(cs), _ptr(kc), _ptr(vc), H, Hkv, D, max_seq, _stream()), "gemm8p_norm")
     return out
 
 

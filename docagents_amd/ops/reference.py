@@ -13,6 +13,7 @@ import torch
 import torch.nn.functional as F
 
 EPI_NONE, EPI_BIAS, EPI_GELU, EPI_SWIGLU, EPI_RESID = 0, 1, 2, 3, 4
+EPI_ROPE = 6  # gemm8p only: QKV + RoPE + KV-cache write
 
 
 def gemv_fusable(M, N, K, epi=EPI_NONE):
@@ -132,6 +133,30 @@ def gemm_rope(a, w, pos, cos_sin, H, Hkv, D, slot, k_cache, v_cache, out=None):
     """QKV projection with RoPE on q / k and the k / v cache write fused (gemm + rope_cache)."""
     qkv = gemm(a, w, out=out)
     return rope_cache(qkv, pos, cos_sin, H, Hkv, D, slot=slot, k_cache=k_cache, v_cache=v_cache)
+
+
+def prefill_norm_fusable(M, K):
+    return M >= 640 and K % 64 == 0 and K >= 128
+
+
+def gemm8p_norm(a, w, epi, out=None, resid=None, bias=None, norm_in=None, ssq_out=None, rope=None):
+    """gemm.hip da_gemm8p_norm: rows of the raw ``a`` scaled by rsqrt(sum of the ssq parts / K + eps)
+    after the product (fp32), then the epilogue; EPI_RESID + ssq_out: per-64-column sums of squares
+    of the bf16 output rows ([N / 64][M]); EPI_ROPE: rope + KV write of the bf16 result."""
+    M, K = a.shape
+    N = w.shape[0]
+    y = a.float() @ w.float().t()
+    if norm_in is not None:
+        ssq, parts, eps = norm_in
+        y = y * torch.rsqrt(ssq.reshape(-1)[:parts * M].view(parts, M).sum(0) / K + eps)[:, None]
+    if epi == EPI_ROPE:
+        pos, cs, H, Hkv, D, slot, kc, vc = rope
+        qkv = _epilogue(y, N, bias, EPI_NONE, None, out)
+        return rope_cache(qkv, pos, cs, H, Hkv, D, slot=slot, k_cache=kc, v_cache=vc)
+    y = _epilogue(y, N, bias, epi, resid, out)
+    if ssq_out is not None:
+        ssq_out.reshape(-1)[:(N // 64) * M].view(N // 64, M)[:] = y.float().view(M, N // 64, 64).pow(2).sum(-1).t()
+    return y
 
 
 def rope_cache(qkv, pos, cos_sin, H, Hkv, D, slot=None, k_cache=None, v_cache=None, rotate_q=True):

@@ -107,6 +107,77 @@ def test_gemm_rope(M, H, Hkv, D):
     assert torch.equal(got, two) and torch.equal(kc, kc3) and torch.equal(vc, vc3)
 
 
+def _ssq_parts(x, parts):
+    """[parts, M] fp32 sums of squares of x's 64-column groups (what an EPI_RESID producer writes)."""
+    M, N = x.shape
+    return x.float().view(M, N // 64, 64).pow(2).sum(-1).t().contiguous()[:parts]
+
+
+@pytest.mark.parametrize("M", [640, 1000, 2304])
+@pytest.mark.parametrize("epi", [K.EPI_NONE, K.EPI_BIAS, K.EPI_SWIGLU, K.EPI_ROPE])
+def test_gemm8p_norm_consumer(M, epi):
+    """Deferred RMSNorm in the phase-split GEMM: raw rows in, output rows scaled by rsqrt(mean
+    square + eps) from the producer's 64-column sums == rmsnorm -> gemm (fp32 ref of the same op)."""
+    torch.manual_seed(M + epi)
+    Kd = 512
+    x = _rand(M, Kd, scale=3.0)
+    ssq = _ssq_parts(x, Kd // 64)
+    eps = 1e-5
+    h = R.rmsnorm(x, torch.ones(Kd, dtype=torch.bfloat16, device=DEV), eps)
+    if epi == K.EPI_ROPE:
+        H, Hkv, D = 8, 2, 64
+        N, L = (H + 2 * Hkv) * D, 4096
+        w = _rand(N, Kd, scale=Kd ** -0.5)
+        pos = torch.arange(M, device=DEV, dtype=torch.int32)
+        slot = torch.zeros(M, device=DEV, dtype=torch.int32)
+        cs = R.rope_table(L, D, 10000.0, device=DEV)
+        kc = torch.zeros(1, Hkv, L, D, device=DEV, dtype=torch.bfloat16)
+        vc, kc2, vc2 = torch.zeros_like(kc), kc.clone(), kc.clone()
+        got = K.gemm8p_norm(x, w, epi, norm_in=(ssq, Kd // 64, eps), rope=(pos, cs, H, Hkv, D, slot, kc, vc))
+        ref = R.gemm_rope(h, w, pos, cs, H, Hkv, D, slot, kc2, vc2)
+        _close(got, ref, atol=0.04)
+        _close(kc, kc2, atol=0.04)
+        _close(vc, vc2, atol=0.04)
+        return
+    N = 1536
+    w = _rand(N, Kd, scale=Kd ** -0.5)
+    bias = _rand(N) if epi == K.EPI_BIAS else None
+    got = K.gemm8p_norm(x, w, epi, bias=bias, norm_in=(ssq, Kd // 64, eps))
+    _close(got, R.gemm(h, w, bias=bias, epi=epi), atol=0.04)
+    _close(got, R.gemm8p_norm(x, w, epi, bias=bias, norm_in=(ssq, Kd // 64, eps)), atol=0.03)
+
+
+@pytest.mark.parametrize("M,N,Kd", [(640, 256, 512), (1000, 1024, 256), (3000, 3072, 1024)])
+def test_gemm8p_norm_producer(M, N, Kd):
+    """EPI_RESID + ssq_out: the output equals the plain residual GEMM bit for bit, and the
+    [N / 64][M] sums of squares equal those of the bf16 output rows."""
+    torch.manual_seed(M + N)
+    a, w, resid = _rand(M, Kd), _rand(N, Kd, scale=Kd ** -0.5), _rand(M, N)
+    ssq = torch.full(((N // 64) * M,), float("nan"), device=DEV)
+    got = K.gemm8p_norm(a, w, K.EPI_RESID, resid=resid, ssq_out=ssq)
+    plain = K.gemm(a, w, epi=K.EPI_RESID, resid=resid)
+    assert torch.equal(got, plain)
+    ref = _ssq_parts(got, N // 64)
+    assert torch.allclose(ssq.view(N // 64, M), ref, rtol=1e-4, atol=1e-3)
+
+
+def test_gemm8p_norm_in_place_chain():
+    """The prefill chain shape: O projection in place on x (resid = out = x) writing the sums, then
+    gate/up reading them — the SwiGLU rows equal rmsnorm(x_new) -> gemm."""
+    torch.manual_seed(5)
+    M, Hd, F = 1200, 768, 1024
+    x = _rand(M, Hd, scale=2.0)
+    a, wo = _rand(M, Hd), _rand(Hd, Hd, scale=Hd ** -0.5)
+    wgu = _rand(2 * F, Hd, scale=Hd ** -0.5)
+    ssq = torch.empty((Hd // 64) * M, device=DEV)
+    x_ref = R.gemm(a, wo, epi=K.EPI_RESID, resid=x)
+    K.gemm8p_norm(a, wo, K.EPI_RESID, resid=x, out=x, ssq_out=ssq)
+    _close(x, x_ref, atol=0.03)
+    g = K.gemm8p_norm(x, wgu, K.EPI_SWIGLU, norm_in=(ssq, Hd // 64, 1e-5))
+    h = R.rmsnorm(x, torch.ones(Hd, dtype=torch.bfloat16, device=DEV), 1e-5)
+    _close(g, R.gemm(h, wgu, epi=K.EPI_SWIGLU), atol=0.04)
+
+
 @pytest.mark.parametrize("M", [65, 128, 200])
 def test_gemm_mid_m_in_tree(M):
     """65..255 rows: the 64x128 weight-streaming tile over ceil(M/64) row blocks with split-K
