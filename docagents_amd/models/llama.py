@@ -33,8 +33,9 @@ from ..ops.reference import interleave_gate_up, rope_table
 from .configs import DecoderConfig
 
 EPI_NONE, EPI_SWIGLU, EPI_RESID, EPI_ROPE = 0, 3, 4, 6
-# DA_PREFILL_NORM_FUSE=0 keeps the separate RMSNorm kernels in the prefill (A/B measurements)
-_PREFILL_NORM_FUSE = os.environ.get("DA_PREFILL_NORM_FUSE", "1") != "0"
+# Prefill RMSNorms folded into the projections (_prefill_fused_norms); DA_PREFILL_NORM_FUSE=0/1
+# overrides the default (A/B measurements: profiles/r3/prefill_norm_fuse.txt)
+_PREFILL_NORM_FUSE = os.environ.get("DA_PREFILL_NORM_FUSE", "0") == "1"
 # Decode step of MHA models: RoPE + KV-cache write folded into the attention kernel (False: separate
 # rope_cache launch; the GPU tests compare both).
 _FUSED_ROPE_DECODE = True

@@ -28,9 +28,10 @@ struct GemmArgs {
   const bf16_t* gamma; float eps;    // GEMV only: fused RMSNorm of the input row (gamma != null)
   RopeArgs rope;                     // EPI_ROPE only
   // prefill RMSNorm folded into the phase-split GEMM (gemm8p; gains folded into W):
-  //   ssq_in: A holds the raw residual rows; out = epi(rsqrt(sum_p ssq_in[p][m] / norm_k + eps) * (A W^T))
-  //   ssq_out (EPI_RESID): per-row sums of squares of the bf16 output, one per 64 columns
-  //            ([N / 64][M] floats) — the next consumer's ssq_in
+  //   ssq_in: A holds the raw residual rows; out = epi(rsqrt(sum_p ssq_in[m][p] / norm_k + eps) * (A W^T))
+  //   ssq_out (EPI_RESID): per-row sums of squares of the bf16 output, one per 64 columns (part =
+  //            column tile * 4 + wave column: 2 x 32 columns, reference.gemm8p_ssq_parts)
+  //            ([M][N / 64] floats) — the next consumer's ssq_in
   const float* ssq_in; int ssq_parts; int norm_k; float norm_eps;
   float* ssq_out;
 };

@@ -722,7 +722,7 @@ DA_EXPORT int da_gemm_rope(const void* A, int lda, const void* W, void* C, int l
 // Prefill projection on the phase-split kernel with the layer RMSNorms folded in (gemm.h GemmArgs
 // ssq_in / ssq_out): a consumer (QKV + RoPE + KV write, gate/up + SwiGLU) reads the raw residual
 // stream and scales its output rows by the norm from the producer's row sums; a producer (EPI_RESID:
-// O / down projection) writes those sums ([N / 64][M] floats). Same tile choice as da_gemm_bf16 /
+// O / down projection) writes those sums ([M][N / 64] floats). Same tile choice as da_gemm_bf16 /
 // da_gemm_rope. Rope args are used only by EPI_ROPE.
 DA_EXPORT int da_gemm8p_norm(const void* A, int lda, const void* W, void* C, int ldc, const void* bias,
                              const void* resid, int ldr, int M, int N, int K, int epi, const float* ssq_in,

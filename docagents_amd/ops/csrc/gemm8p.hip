@@ -175,6 +175,29 @@ gemm8p_kernel(GemmArgs p) {
   //      (DMA order per wave: ... A0 B0 B1(t+1) | A1(t+1) | A0 B0 B1(t+2) | A1(t+2) ...)
   ISSUE_A(0, 0, 0); ISSUE_B(0, 0, 0); ISSUE_B(1, 0, 0); ISSUE_A(1, 0, 0);
   ISSUE_A(0, 1, 1); ISSUE_B(0, 1, 1); ISSUE_B(1, 1, 1);
+  // deferred RMSNorm of A's rows (p.ssq_in, [M][parts]): thread (row r, group grp) sums parts
+  // [grp, grp + 1) * parts / G of its row while the prologue DMA is in flight (one round of 16-B
+  // loads), kept in one register until the epilogue
+  constexpr int G = 512 / BM;
+  float ssn = 0.f;
+  if (p.ssq_in) {
+    const int r = tid % BM, grp = tid / BM;
+    const float* src = p.ssq_in + (size_t)min(m0 + r, p.M - 1) * p.ssq_parts;
+    if (p.ssq_parts % (4 * G) == 0) {
+      const int per = p.ssq_parts / G;
+      src += grp * per;
+      for (int q0 = 0; q0 < per; q0 += 32) {
+        f32x4_t v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+          v[u] = q0 + 4 * u < per ? *(const f32x4_t*)(src + q0 + 4 * u) : f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int u = 0; u < 8; ++u) ssn += (v[u][0] + v[u][1]) + (v[u][2] + v[u][3]);
+      }
+    } else {
+      for (int q = grp; q < p.ssq_parts; q += G) ssn += src[q];
+    }
+  }
   vmcnt<CNT_AB>();
   bar();
   if (wg) bar();  // G1 runs one barrier behind
@@ -220,16 +243,10 @@ gemm8p_kernel(GemmArgs p) {
 #undef ISSUE_B
   __syncthreads();
 
-  // ---- deferred RMSNorm of A's rows (p.ssq_in): inv per tile row from the producer's 64-column
-  //      sums of squares, summed in a fixed order (part q by group q % G, then the groups)
+  // ---- deferred RMSNorm: inv per tile row from the G partial sums (fixed order: deterministic)
   __shared__ float snorm[4][BM], sinv[BM];
   if (p.ssq_in) {
-    constexpr int G = 512 / BM;
-    const int r = tid % BM, grp = tid / BM, gm = m0 + r;
-    float ss = 0.f;
-    if (gm < p.M)
-      for (int q = grp; q < p.ssq_parts; q += G) ss += p.ssq_in[(size_t)q * p.M + gm];
-    snorm[grp][r] = ss;
+    snorm[tid / BM][tid % BM] = ssn;
     __syncthreads();
     if (tid < BM) {
       float tot = 0.f;
@@ -359,7 +376,7 @@ gemm8p_kernel(GemmArgs p) {
         if (!ok) sq = 0.f;
 #pragma unroll
         for (int x = 1; x < CPR; x <<= 1) sq += __shfl_xor(sq, x, 64);
-        if (ch == 0 && gm < p.M) p.ssq_out[(size_t)((n0 / BN) * 4 + wn) * p.M + gm] = sq;
+        if (ch == 0 && gm < p.M) p.ssq_out[(size_t)gm * (p.N / 64) + (n0 / BN) * 4 + wn] = sq;
       }
     }
     if (ok) *(u32x4_t*)(p.C + (size_t)gm * p.ldc + gcol) = v;

@@ -374,9 +374,9 @@ def prefill_norm_fusable(M: int, K: int) -> bool:
 
 def gemm8p_norm(a, w, epi: int, out=None, resid=None, bias=None, norm_in=None, ssq_out=None, rope=None):
     """Prefill projection with the RMSNorms folded in (csrc/gemm.hip da_gemm8p_norm):
-    norm_in = (ssq [parts * M] fp32, parts, eps): ``a`` is the raw residual stream, each output row is
+    norm_in = (ssq [M, parts] fp32, parts, eps): ``a`` is the raw residual stream, each output row is
     scaled by rsqrt(sum of its parts / K + eps) before the epilogue (gains folded into w);
-    ssq_out (EPI_RESID): fp32 [N // 64 * M] receives per-64-column sums of squares of the new rows.
+    ssq_out (EPI_RESID): fp32 [M, N // 64] receives per-64-column sums of squares of the new rows.
     rope = (pos, cos_sin, H, Hkv, D, slot, k_cache, v_cache) for EPI_ROPE (QKV + RoPE + KV write)."""
     _bf16_cuda(a, "a"); _bf16_cuda(w, "w")
     M, K = a.shape

@@ -139,23 +139,31 @@ def prefill_norm_fusable(M, K):
     return M >= 640 and K % 64 == 0 and K >= 128
 
 
+def gemm8p_ssq_parts(y):
+    """[M, N / 64] per-part sums of squares as gemm8p's EPI_RESID store loop forms them: part
+    (tile t, wave column wn) holds columns 256 t + 32 wn + [0, 32) and 256 t + 128 + 32 wn + [0, 32)
+    (a consumer only uses the sum over parts)."""
+    M, N = y.shape
+    return y.float().pow(2).view(M, N // 256, 2, 4, 32).sum((2, 4)).reshape(M, N // 64)
+
+
 def gemm8p_norm(a, w, epi, out=None, resid=None, bias=None, norm_in=None, ssq_out=None, rope=None):
     """gemm.hip da_gemm8p_norm: rows of the raw ``a`` scaled by rsqrt(sum of the ssq parts / K + eps)
     after the product (fp32), then the epilogue; EPI_RESID + ssq_out: per-64-column sums of squares
-    of the bf16 output rows ([N / 64][M]); EPI_ROPE: rope + KV write of the bf16 result."""
+    of the bf16 output rows ([M][N / 64], gemm8p_ssq_parts); EPI_ROPE: rope + KV write of the bf16 result."""
     M, K = a.shape
     N = w.shape[0]
     y = a.float() @ w.float().t()
     if norm_in is not None:
         ssq, parts, eps = norm_in
-        y = y * torch.rsqrt(ssq.reshape(-1)[:parts * M].view(parts, M).sum(0) / K + eps)[:, None]
+        y = y * torch.rsqrt(ssq.reshape(-1)[:parts * M].view(M, parts).sum(1) / K + eps)[:, None]
     if epi == EPI_ROPE:
         pos, cs, H, Hkv, D, slot, kc, vc = rope
         qkv = _epilogue(y, N, bias, EPI_NONE, None, out)
         return rope_cache(qkv, pos, cs, H, Hkv, D, slot=slot, k_cache=kc, v_cache=vc)
     y = _epilogue(y, N, bias, epi, resid, out)
     if ssq_out is not None:
-        ssq_out.reshape(-1)[:(N // 64) * M].view(N // 64, M)[:] = y.float().view(M, N // 64, 64).pow(2).sum(-1).t()
+        ssq_out.reshape(-1)[:(N // 64) * M].view(M, N // 64)[:] = gemm8p_ssq_parts(y)
     return y
 
 

@@ -108,9 +108,9 @@ def test_gemm_rope(M, H, Hkv, D):
 
 
 def _ssq_parts(x, parts):
-    """[parts, M] fp32 sums of squares of x's 64-column groups (what an EPI_RESID producer writes)."""
+    """[M, parts] fp32 sums of squares of x's 64-column groups (any partition: the consumer sums them)."""
     M, N = x.shape
-    return x.float().view(M, N // 64, 64).pow(2).sum(-1).t().contiguous()[:parts]
+    return x.float().view(M, N // 64, 64).pow(2).sum(-1)[:, :parts].contiguous()
 
 
 @pytest.mark.parametrize("M", [640, 1000, 2304])
@@ -150,15 +150,15 @@ def test_gemm8p_norm_consumer(M, epi):
 @pytest.mark.parametrize("M,N,Kd", [(640, 256, 512), (1000, 1024, 256), (3000, 3072, 1024)])
 def test_gemm8p_norm_producer(M, N, Kd):
     """EPI_RESID + ssq_out: the output equals the plain residual GEMM bit for bit, and the
-    [N / 64][M] sums of squares equal those of the bf16 output rows."""
+    [M][N / 64] sums of squares equal those of the bf16 output rows."""
     torch.manual_seed(M + N)
     a, w, resid = _rand(M, Kd), _rand(N, Kd, scale=Kd ** -0.5), _rand(M, N)
     ssq = torch.full(((N // 64) * M,), float("nan"), device=DEV)
     got = K.gemm8p_norm(a, w, K.EPI_RESID, resid=resid, ssq_out=ssq)
     plain = K.gemm(a, w, epi=K.EPI_RESID, resid=resid)
     assert torch.equal(got, plain)
-    ref = _ssq_parts(got, N // 64)
-    assert torch.allclose(ssq.view(N // 64, M), ref, rtol=1e-4, atol=1e-3)
+    ref = R.gemm8p_ssq_parts(got)
+    assert torch.allclose(ssq.view(M, N // 64), ref, rtol=1e-4, atol=1e-3)
 
 
 def test_gemm8p_norm_in_place_chain():

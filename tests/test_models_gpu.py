@@ -52,9 +52,11 @@ def test_decoder_prefill_matches_reference():
     assert torch.allclose(m.cache.buf.float(), r.cache.buf.float(), atol=0.05)
 
 
-def test_decoder_prefill_fused_norms():
+def test_decoder_prefill_fused_norms(monkeypatch):
     """>= 640 packed tokens: the prefill folds the layer RMSNorms into the projections (gemm8p_norm);
     logits and KV cache match the unfused GPU path and the fp32 reference."""
+    import docagents_amd.models.llama as llama
+    monkeypatch.setattr(llama, "_PREFILL_NORM_FUSE", True)
     cfg = decoder_config("tiny-dec")
     m = LlamaDecoder(cfg, "cuda", seed=11)
     u = LlamaDecoder(cfg, "cuda", weights=m.w)
