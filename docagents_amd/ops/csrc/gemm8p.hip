@@ -256,8 +256,16 @@ gemm8p_kernel(GemmArgs p) {
     }
     __syncthreads();
   }
-  // tile row of accumulator acc[ih][.][i][.][q]
-  auto arow = [&](int ih, int i, int q) { return ih * (BM / 2) + wg * QR + i * 16 + fg * 4 + q; };
+  // row scales of this thread's accumulator rows acc[ih][.][i][.][q] (tile row ih*BM/2 + wg*QR +
+  // i*16 + fg*4 + q), read once into registers (the K-loop fragments are dead here)
+  float rs[2][MI][4];
+#pragma unroll
+  for (int ih = 0; ih < 2; ++ih)
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        rs[ih][i][q] = p.ssq_in ? sinv[ih * (BM / 2) + wg * QR + i * 16 + fg * 4 + q] : 1.f;
 
   // ---- epilogue: registers -> (bias / GELU / SwiGLU) -> bf16 staging -> coalesced stores.
   //      Staged row lr = ih*QR + i*16 + fg*4 + q (tile row ih*BM/2 + wg*QR + (lr % QR)),
@@ -274,7 +282,7 @@ gemm8p_kernel(GemmArgs p) {
         for (int i = 0; i < MI; ++i)
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
-            const float iv = p.ssq_in ? sinv[arow(ih, i, q)] : 1.f;
+            const float iv = rs[ih][i][q];
             const float v = silu(acc[ih][jh][i][0][q] * iv) * (acc[ih][jh][i][1][q] * iv);
             *(bf16_t*)(st + (ih * QR + i * 16 + fg * 4 + q) * SROW + (jh * 16 + fr) * 2) = f2bf(v);
           }
@@ -299,8 +307,7 @@ gemm8p_kernel(GemmArgs p) {
           for (int j = 0; j < 2; ++j)
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
-              const float iv = p.ssq_in ? sinv[arow(ih, i, q)] : 1.f;
-              float v = acc[ih][jh][i][j][q] * iv + bv[jh][j];
+              float v = acc[ih][jh][i][j][q] * rs[ih][i][q] + bv[jh][j];
               if constexpr (EPI == EPI_GELU) v = gelu_erf(v);
               *(bf16_t*)(st + (ih * QR + i * 16 + fg * 4 + q) * SROW + (jh * 32 + j * 16 + fr) * 2) = f2bf(v);
             }
