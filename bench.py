@@ -2,13 +2,13 @@
 
 Metric / config from BASELINE.json: "QA queries/sec + p50 cache-miss latency; docs/min ingest at
 1/2/4/8 MI355X" on config 2: "BGE-base embedder + Phi-3-mini QA on 1xMI355X, 100k-chunk brute-force
-cosine in HBM" — here 100k chunks PER GPU (weak scaling: the index grows with N, every query is
-searched against every shard over RCCL/xGMI).
+cosine in HBM" — here 100k chunks PER GPU (weak scaling: the index grows with N; a query's
+documents are spread over all shards, so at N > 1 most searches read several ranks' shards).
 
 One timed step = every GPU serves B cache-miss queries end to end (the reference's query path,
 cmd/query/main.go:44-136, minus the cache hit): tokenize -> BGE-base encode (HIP kernels) ->
-all-gather query vectors -> fused cosine + doc-filter + threshold + top-k on every shard ->
-all-gather + merge top-k -> build the Answer prompt from the top-k chunks (pre-tokenized at ingest)
+search plane: query rows sent to the shards owning their filter documents -> fused cosine +
+doc-filter + threshold + top-k on each (vecsearch.hip) -> merge -> build the Answer prompt from the top-k chunks (pre-tokenized at ingest)
 -> Phi-3-mini prefill (~2.8k tokens/query) + decode MAX_NEW tokens at T=0.2 (HIP kernels, HIP
 graphs) -> confidence = avg similarity x mean token probability -> detokenize.
 
@@ -18,8 +18,14 @@ synthetic questions; each query filters on `--docs-per-query` random documents s
 shards. MIN_SIMILARITY is set to -1 so every query retrieves exactly top_k chunks (random weights
 make the reference's 0.7 floor meaningless; -1 is the MOST work per query, never less).
 
-Launch: python bench.py [--gpus 1 --steps 3 --warmup 1]  or, for N GPUs,
-        python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+Launch: python bench.py [--gpus N --steps K --warmup W]. With N > 1 and no WORLD_SIZE in the
+environment, this process launches N ranks itself (python -m torch.distributed.run, one rank per GPU)
+before anything touches the GPU, relays their output and exits with their status; under an external
+torchrun (WORLD_SIZE set) it is one rank, and WORLD_SIZE != --gpus is an error. Every rank is an
+independent replica (its own engine), the index is sharded one shard per rank, and every search goes
+through the production search plane (parallel/search_plane.py: routed to the shards that own the
+query's documents, point to point); the JSON line reports the process-group backend and the number
+of ranks that joined (ranks_seen, an all-reduce of ones).
 """
 from __future__ import annotations
 
@@ -27,17 +33,51 @@ import argparse
 import json
 import os
 import statistics
+import subprocess
 import sys
 import time
 
-import numpy as np
-import torch
+
+def _launch_ranks(argv: list[str]) -> int | None:
+    """Parent side of ``--gpus N``: None = run the bench in this process (we are a rank, or N = 1);
+    otherwise the exit status of N child ranks launched here. Imports nothing GPU-related and never
+    exec()s: the children are fresh processes (torch.distributed.run), this one only waits."""
+    ap = argparse.ArgumentParser(add_help=False)
+    ap.add_argument("--gpus", type=int, default=1)
+    a, _ = ap.parse_known_args(argv)
+    ws = os.environ.get("WORLD_SIZE")
+    if ws is not None:
+        if int(ws) != a.gpus:
+            print(f"[bench] WORLD_SIZE={ws} but --gpus {a.gpus}: refusing to report a different world",
+                  file=sys.stderr, flush=True)
+            return 2
+        return None
+    if a.gpus <= 1:
+        return None
+    import socket
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={a.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + list(argv)
+    print(f"[bench] launching {a.gpus} ranks: {' '.join(cmd)}", file=sys.stderr, flush=True)
+    return subprocess.call(cmd)
+
+
+if __name__ == "__main__":
+    _rc = _launch_ranks(sys.argv[1:])
+    if _rc is not None:
+        sys.exit(_rc)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
 from docagents_amd.engine.engine import Engine  # noqa: E402
 from docagents_amd.parallel.dist import (all_reduce_max, all_reduce_sum, barrier, init_from_env,  # noqa: E402
                                          shutdown)
+from docagents_amd.parallel.search_plane import SearchPlane, owner_of  # noqa: E402
 from docagents_amd.parallel.sharded_index import ShardedIndex  # noqa: E402
 from docagents_amd.engine.prompts import concatenate_chunks, dedup_overlap  # noqa: E402
 from docagents_amd.text.chunker import Options, chunk_text  # noqa: E402
@@ -124,11 +164,13 @@ def main():
         groups = [dist.new_group(list(range(g * TP, (g + 1) * TP))) for g in range(DP)]  # every rank creates every group
         tp_ctx = TPContext(R % TP, TP, groups[dp_rank])
     overlap = bool(a.overlap) and TP == 1 and not a.no_graphs
+    import torch.distributed as tdist
+    ctrl = tdist.new_group(backend="gloo") if W > 1 else None  # the search plane's address exchange
     eng = Engine(a.enc, a.llm, dev, seed=a.seed, tp=tp_ctx, max_batch=a.batch, max_seq=4096, temperature=0.2,
                  max_new_tokens=a.max_new, summary_max_new=128, use_graphs=not a.no_graphs,
                  index_kind=a.index_kind, ivf_lists=a.ivf_lists, ivf_probes=a.ivf_probes, enc_dtype=a.enc_dtype,
                  overlap_waves=overlap)
-    shard = ShardedIndex(eng.index, R, W)
+    shard = ShardedIndex(eng.index, R, W)  # IVF only: the k-means statistics all-reduce (C6)
     d = eng.dim
 
     # ---- synthetic 100k-chunk shard in HBM ----
@@ -138,35 +180,48 @@ def main():
     X = torch.randn((rows, d), device=dev, generator=g)
     X = torch.nn.functional.normalize(X, dim=-1).to(torch.bfloat16)
     ndocs = rows // a.chunks_per_doc
-    doc_ids = [f"d{R}-{i}" for i in range(ndocs)]
+    # document names that production routing (owner_of: hash(doc) % N) places on each rank's shard,
+    # so the plane routes every query row to the shards that really hold its documents
+    names = [[] for _ in range(W)]
+    i = 0
+    while min(len(n) for n in names) < ndocs:
+        for r in range(W):
+            nm = f"d{r}-{i}"
+            if len(names[r]) < ndocs and owner_of(nm, W) == r:
+                names[r].append(nm)
+        i += 1
+    doc_ids = names[R]
     ids = (np.int64(R) * 1_000_000_000 + np.arange(rows, dtype=np.int64))
     eng.index.add_bulk(doc_ids, [a.chunks_per_doc] * ndocs, ids, X)
     del X
     if a.index_kind == "ivfflat":
         shard.train(iters=10, sample=min(rows, 1 << 20))  # shared centroids: k-means stats all-reduced (C6)
+    plane = SearchPlane.start_world(eng.index, R, W, ctrl, device=dev, timeout_s=120.0)
     vocab_hi = eng.dec_tok.get_vocab_size()
     chunks = ChunkTokens(300, vocab_hi)
     tg = TextGen(seed=77 + dp_rank)  # the ranks of one TP group serve the same queries
 
     def make_filters(step: int):
-        rng = np.random.default_rng(10_000 + step)
-        per_dp = []
-        for _ in range(DP):
-            fs = []
-            for _ in range(B_cur):
-                rr = rng.integers(0, W, size=a.docs_per_query)
-                ii = rng.integers(0, ndocs, size=a.docs_per_query)
-                fs.append([f"d{x}-{y}" for x, y in zip(rr, ii)])
-            per_dp.append(fs)
-        return [f for r in range(W) for f in per_dp[r // TP]]  # rank order, identical within a TP group
+        """This rank's B query filters: docs_per_query random documents on random shards (the ranks
+        of one TP group serve the same queries)."""
+        rng = np.random.default_rng(10_000 + 7919 * step + dp_rank)
+        fs = []
+        for _ in range(B_cur):
+            rr = rng.integers(0, W, size=a.docs_per_query)
+            ii = rng.integers(0, ndocs, size=a.docs_per_query)
+            fs.append([names[x][y] for x, y in zip(rr, ii)])
+        return fs
+
+    def search(qv, filters):
+        """The production search path: submit to this rank's plane (routed to the owner shards)."""
+        return plane.submit(qv.float().cpu().numpy(), a.top_k, a.min_sim, filters).result()
 
     def qa_items(step: int, B: int):
         """A QA step up to the answers: embed the questions, sharded search, context chunks."""
         qs = [tg.question() for _ in range(B)]
         filters = make_filters(step)
         qv = eng.embed(qs)
-        s, gid = shard.search(qv, a.top_k, a.min_sim, filters)
-        s_h, id_h = s.cpu().numpy(), gid.cpu().numpy()
+        s_h, id_h = search(qv, filters)
         items = []
         for b in range(B):
             valid = id_h[b] >= 0
@@ -229,8 +284,7 @@ def main():
         filters = make_filters(seed)
         sy(); t = time.perf_counter()
         qv = eng.embed(qs); sy(); ph["embed"] = time.perf_counter() - t; t = time.perf_counter()
-        s_, gid = shard.search(qv, a.top_k, a.min_sim, filters)
-        s_h, id_h = s_.cpu().numpy(), gid.cpu().numpy(); ph["search"] = time.perf_counter() - t
+        s_h, id_h = search(qv, filters); ph["search"] = time.perf_counter() - t
         t = time.perf_counter()
         items = [(qs[b], [chunks.get(int(c)) for c in id_h[b][id_h[b] >= 0]], 0.5) for b in range(B)]
         prompts = [eng.answer_prompt_ids(q, ch, a.max_new) for q, ch, _ in items]
@@ -347,11 +401,12 @@ def main():
             xgmi = {"ok": False, "error": repr(e)[:200]}
         log(info, f"xgmi all-reduce check: {xgmi}")
 
+    ranks_seen = int(round(all_reduce_sum(1.0, dev)))  # every rank that reached the end of the run
     gen = eng.gen.stats
     out = {
         "metric": METRIC, "value": round(qps, 3), "unit": "queries/s", "n_gpus": W, "steps": a.steps,
         "warmup": a.warmup, "ms_per_step": round(dt_max / a.steps * 1000, 2), "higher_is_better": True,
-        "scaling": "weak", "vs_baseline": None,
+        "scaling": "weak", "vs_baseline": None, "dist_backend": info.backend, "ranks_seen": ranks_seen,
         "dtype": "bf16" if a.enc_dtype == "bf16" else "bf16 (fp8 e4m3 encoder GEMMs)",
         "data": "synthetic (random-init weights; random unit vectors for the background chunks; synthetic questions)",
         "config": {"model": f"{a.enc} embedder + {a.llm} QA", "global_batch": DP * a.batch,
@@ -377,8 +432,11 @@ def main():
     }
     if xgmi is not None:
         out["xgmi_allreduce_check"] = xgmi
+    out["search_plane"] = {k: (round(v, 3) if isinstance(v, float) else v) for k, v in plane.stats.items()}
     if R == 0:
         print(json.dumps(out), flush=True)
+    barrier()
+    plane.stop(timeout=2.0)
     shutdown()
 
 

@@ -491,14 +491,26 @@ class ContinuousScheduler:
                 self.gen._capture(st)
             t0 = time.perf_counter()
             ran = 0
+            # graph replays are asynchronous: without a bound the host would queue all k steps before
+            # stop() is ever consulted. With a stop callback at most 2 steps run ahead of the host
+            # (an event per step), so an arrival waits ~2 steps, and the GPU never idles.
+            ahead: collections.deque = collections.deque()
+            track = stop is not None and k > 1 and st.graph is not None
             while ran < k:
                 if st.graph is not None:
                     st.graph.replay()
                 else:
                     self.m.decode_step(st)
                 ran += 1
-                if stop is not None and ran < k and stop():
-                    break
+                if stop is not None and ran < k:
+                    if track:
+                        ev = torch.cuda.Event()
+                        ev.record()
+                        ahead.append(ev)
+                        if len(ahead) > 2:
+                            ahead.popleft().synchronize()
+                    if stop():
+                        break
             for r, left in enumerate(self.left):
                 if left is not None:
                     self.left[r] = max(0, left - ran)

@@ -14,6 +14,7 @@ from __future__ import annotations
 import asyncio
 import itertools
 import struct
+import time
 
 import msgpack
 import numpy as np
@@ -117,6 +118,10 @@ class EngineClient:
                     else:
                         fut.set_result(msg.get("result"))
         except (asyncio.IncompleteReadError, ConnectionError, OSError) as e:
+            # the next call reconnects (a restarted engine is picked up; a dead one fails fast)
+            w, self.writer = self.writer, None
+            if w is not None:
+                w.close()
             for f in self.pending.values():
                 if not f.done():
                     f.set_exception(ConnectionError(f"engine connection lost: {e}"))
@@ -128,10 +133,19 @@ class EngineClient:
         rid = next(self.ids)
         fut = asyncio.get_running_loop().create_future()
         self.pending[rid] = fut
-        async with self.lock:
-            self.writer.write(pack({"id": rid, "method": method, "args": args, "trace": trace}))
-            await self.writer.drain()
-        return await asyncio.wait_for(fut, self.timeout)
+        try:
+            async with self.lock:
+                if self.writer is None:
+                    raise ConnectionError(f"engine connection to {self.url} lost")
+                self.writer.write(pack({"id": rid, "method": method, "args": args, "trace": trace}))
+                await self.writer.drain()
+        except (ConnectionError, OSError) as e:
+            self.pending.pop(rid, None)
+            raise ConnectionError(f"engine at {self.url}: {e}") from e
+        try:
+            return await asyncio.wait_for(fut, self.timeout)
+        finally:
+            self.pending.pop(rid, None)
 
     async def close(self):
         if self.reader_task:
@@ -156,16 +170,22 @@ class EngineCluster:
       * ``index_docs`` / ``stats`` / ``checkpoint`` / ``ping`` fan out to every replica and merge;
       * everything else (embed, embed_search, search, answer, summarize) goes to the replica with
         the fewest calls in flight — the reference's queue-group load balancing
-        (internal/queue/nats.go:40-51) for the GPU engine.
-    A one-replica engine behaves exactly like a plain ``EngineClient``."""
+        (internal/queue/nats.go:40-51) for the GPU engine. These calls are idempotent (no engine
+        state changes), so a replica that is unreachable (or reports itself unhealthy) is skipped
+        for ``dead_s`` and the call is retried on the next live replica: replicas fail
+        independently, as the reference's queue-group workers do;
+      * ``health`` fans out: healthy only if every replica is, with the dead ones named.
+    ``stats`` has one shape for any replica count: ``{"replicas": [per-replica stats]}``."""
 
     ROUTED = ("index_add", "embed_index", "index_remove")
     FANOUT = ("index_docs", "stats", "checkpoint", "ping")
+    RETRYABLE = ("embed", "embed_search", "search", "answer", "summarize")
 
-    def __init__(self, url: str, timeout: float = 120.0):
-        self.url, self.timeout = url, timeout
+    def __init__(self, url: str, timeout: float = 120.0, dead_s: float = 2.0):
+        self.url, self.timeout, self.dead_s = url, timeout, dead_s
         self.clients: list[EngineClient] = []
         self.inflight: list[int] = []
+        self.dead_until: list[float] = []
         self.topology: dict = {"replicas": 1, "tp": 1, "world": 1}
         self._rr = 0
 
@@ -185,6 +205,7 @@ class EngineCluster:
                 u = f"tcp://{addr[0]}:{port}"
             self.clients.append(await EngineClient(u, self.timeout).connect(retries, delay))
         self.inflight = [0] * len(self.clients)
+        self.dead_until = [0.0] * len(self.clients)
         return self
 
     @property
@@ -194,11 +215,20 @@ class EngineCluster:
     def replica_of(self, doc_id: str) -> int:
         return _owner(str(doc_id), int(self.topology.get("world", 1))) // int(self.topology.get("tp", 1))
 
-    def _pick(self) -> int:
+    def _pick(self, exclude=()) -> int:
         n = len(self.clients)
-        best = min(range(n), key=lambda i: (self.inflight[i], (i - self._rr) % n))
+        now = time.monotonic()
+        cand = [i for i in range(n) if i not in exclude] or list(range(n))
+        best = min(cand, key=lambda i: (self.dead_until[i] > now, self.inflight[i], (i - self._rr) % n))
         self._rr = (best + 1) % n
         return best
+
+    @staticmethod
+    def _replica_down(e: BaseException) -> bool:
+        """A failure of the replica itself (not of the request): connection lost / refused, or the
+        engine's watchdog reporting it unhealthy."""
+        return isinstance(e, (ConnectionError, OSError, asyncio.TimeoutError)) or (
+            isinstance(e, RPCError) and "engine unhealthy" in str(e))
 
     async def _on(self, i: int, method: str, trace: str, args: dict):
         self.inflight[i] += 1
@@ -210,6 +240,11 @@ class EngineCluster:
     async def call(self, method: str, trace: str = "", **args):
         if self.writer_missing():
             await self.connect()
+        if method == "health":
+            return await self._health(trace)
+        if method == "stats":
+            return {"replicas": await asyncio.gather(*[self._on(i, method, trace, args)
+                                                       for i in range(len(self.clients))])}
         if len(self.clients) == 1:
             return await self._on(0, method, trace, args)
         if method in self.ROUTED:
@@ -228,7 +263,32 @@ class EngineCluster:
             if method == "ping":
                 return [r for p in parts for r in p]
             return {"replicas": parts}
-        return await self._on(self._pick(), method, trace, args)
+        if method not in self.RETRYABLE:
+            return await self._on(self._pick(), method, trace, args)
+        tried: list[int] = []
+        while True:
+            i = self._pick(tried)
+            tried.append(i)
+            try:
+                return await self._on(i, method, trace, args)
+            except Exception as e:  # noqa: BLE001
+                if not self._replica_down(e) or len(tried) >= len(self.clients):
+                    raise
+                self.dead_until[i] = time.monotonic() + self.dead_s
+
+    async def _health(self, trace: str = ""):
+        async def one(i):
+            try:
+                return await asyncio.wait_for(self.clients[i].call("health", trace=trace), min(self.timeout, 10.0))
+            except Exception as e:  # noqa: BLE001 - a dead replica is a health result, not an error
+                return {"ok": False, "replica": i, "error": f"{type(e).__name__}: {e}"}
+        parts = await asyncio.gather(*[one(i) for i in range(len(self.clients))])
+        if len(parts) == 1:
+            return parts[0]
+        dead = [i for i, p in enumerate(parts) if "error" in p]
+        down = sorted({r for p in parts for r in p.get("shards_down", [])})
+        return {"ok": all(bool(p.get("ok")) for p in parts), "replicas": parts, "dead_replicas": dead,
+                "shards_down": down}
 
     def writer_missing(self) -> bool:
         return not self.clients

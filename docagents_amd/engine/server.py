@@ -10,7 +10,8 @@ queues behind a decode tick or an admission prefill:
   * the GPU thread: the continuous scheduler's ticks, summaries, ingest embeds, index mutations;
   * the fast lane: query-sized embeds (the question of ``embed`` / ``embed_search``), on a
     high-priority stream with its own kernel workspace;
-  * the search plane (parallel/search_plane.py): sharded top-k rounds across every rank.
+  * the search plane (parallel/search_plane.py): a scan worker with its own stream serving this
+    rank's shard to every replica; searches are routed to the shards that own their documents.
 
 Multi-GPU (``torchrun --nproc-per-node N``, TP_SIZE = t): N / t independent replicas, replica r =
 ranks [r t, (r + 1) t) served by its leader on port base + r (``EngineGroup``); the vector index is
@@ -20,7 +21,6 @@ from __future__ import annotations
 
 import asyncio
 import concurrent.futures as cf
-import hashlib
 import time
 import traceback
 
@@ -30,11 +30,8 @@ import torch
 from ..text.preprocess import extract_summary
 from ..utils import faults, metrics
 from .observe import StepProfiler, Watchdog, device_memory
+from ..parallel.search_plane import owner_of  # noqa: F401 - re-exported (clients route by it)
 from .rpc import pack, parse_url, read_frame
-
-
-def owner_of(doc_id: str, world: int) -> int:
-    return int.from_bytes(hashlib.blake2b(doc_id.encode(), digest_size=8).digest(), "little") % max(1, world)
 
 
 class EngineGroup:
@@ -46,9 +43,11 @@ class EngineGroup:
     no command crosses replicas — decode ticks, admissions, embeds and ingest never wait for another
     replica. Within a replica the leader broadcasts each command to its TP followers over a gloo
     group (the TP ranks step one decoder together). The only cross-replica traffic is the sharded
-    search (parallel/search_plane.py, its own thread and stream on every rank) and ingest routing:
+    search (parallel/search_plane.py: point-to-point requests to the shards that own a search's
+    documents, served by a scan thread and stream of their own on every rank) and ingest routing:
     a document's vectors live on rank ``owner_of(doc_id, world)``, and clients send its index
-    mutations to that rank's replica (``EngineCluster.call``)."""
+    mutations to that rank's replica (``EngineCluster.call``). Index mutations order themselves
+    against concurrent scans on the device (index/flat.py ``writing`` / ``reading``)."""
 
     def __init__(self, engine, rank: int = 0, world: int = 1, ctrl_group=None, data_group=None, shard_log=None,
                  tp_size: int = 1, plane=None):
@@ -71,19 +70,15 @@ class EngineGroup:
     def tensor_parallel(self) -> bool:
         return self.tp_size > 1
 
-    def _wrote(self):
-        if self.plane is not None:
-            self.plane.note_write()
-
     def _put(self, doc_id, keys, vecs):
         """Replace ``doc_id``'s rows in this rank's shard (logged first when durable)."""
         idx = self.engine.index
         if self.shard_log is not None:
             self.shard_log.put(idx, doc_id, keys, vecs)
         else:
-            idx.remove_doc(doc_id)
-            idx.add(doc_id, keys, vecs)
-        self._wrote()
+            with idx.writing():  # one committed mutation: a scan sees the old rows or the new ones
+                idx.remove_doc(doc_id)
+                idx.add(doc_id, keys, vecs)
 
     def _upsert(self, doc_id, keys, vecs):
         """Per-chunk upsert of ``doc_id``'s rows (index_add = the reference's SaveEmbeddings,
@@ -94,9 +89,9 @@ class EngineGroup:
         else:
             from ..index.wal import validate
             validate(idx, keys, vecs)
-            idx.remove_keys(doc_id, keys)
-            idx.add(doc_id, keys, vecs)
-        self._wrote()
+            with idx.writing():
+                idx.remove_keys(doc_id, keys)
+                idx.add(doc_id, keys, vecs)
 
     def owner(self, doc_id: str) -> int:
         return owner_of(doc_id, self.world)
@@ -179,9 +174,8 @@ class EngineGroup:
         if cmd == "embed_index":
             # ingest without a vector round trip: the owner rank of each document
             # embeds its chunks and writes the unit-norm rows straight into its HBM shard; only the
-            # row counts travel back
-            for it in a["items"]:
-                self._check_routed(it[0])
+            # row counts travel back (routing was checked per request in EngineServer.dispatch, so a
+            # misrouted document fails alone, not the co-batched ingests of other clients)
             mine = [it for it in a["items"] if self.owner(it[0]) == self.rank]
             counts = {}
             if mine:
@@ -204,7 +198,6 @@ class EngineGroup:
                     n = self.shard_log.remove(e.index, a["doc_id"])
                 else:
                     n = e.index.remove_doc(a["doc_id"])
-                self._wrote()
             return sum(self._gather(n))
         if cmd == "index_docs":
             rows = {d: en.rows for d, en in e.index.docs.items() if en.rows}
@@ -223,7 +216,7 @@ class EngineGroup:
             d = e.describe()
             d["rank"], d["replica"] = self.rank, self.replica
             if self.plane is not None:
-                d["search_plane"] = dict(self.plane.stats, healthy=self.plane.healthy)
+                d["search_plane"] = dict(self.plane.stats, **self.plane.health())
             return self._gather(d)
         if cmd == "snapshot":
             from ..index.snapshot import save_index
@@ -232,7 +225,6 @@ class EngineGroup:
         if cmd == "restore":
             from ..index.snapshot import load_index
             load_index(e.index, f"{a['path']}.shard{self.rank}")
-            self._wrote()
             return len(e.index)
         if cmd == "ping":
             return self._gather(self.rank)
@@ -466,10 +458,15 @@ class EngineServer:
                     await asyncio.wait_for(self._fast_idle.wait(), 0.02)
                 except asyncio.TimeoutError:
                     pass
+            # short ticks while anything waits for admission (the requests taken now, or earlier ones
+            # the scheduler could not seat yet), long ticks otherwise; arrivals during a long tick
+            # end it through group.tick_stop (checked between steps, at most 2 steps queued ahead)
+            sched = getattr(self.group.engine, "scheduler", None)
+            waiting = bool(self._cb_new) or bool(getattr(sched, "pending", None))
+            steps = self.cb_steps if waiting else self.cb_max_steps
             new, self._cb_new = self._cb_new, []
             t0 = time.perf_counter()
             try:
-                steps = self.cb_steps if self._cb_new else self.cb_max_steps
                 done, busy = await self._gpu("cb_tick", {"items": new, "steps": steps})
             except Exception as e:  # noqa: BLE001 - fail the requests of this tick, keep serving
                 for tag, _ in new:
@@ -597,6 +594,7 @@ class EngineServer:
             s, ids = await self._search(args["vecs"], args["k"], args["min_sim"], args.get("filters"))
             return {"scores": s, "keys": ids}
         if method == "embed_index":
+            self.group._check_routed(str(args["doc_id"]))  # a misrouted document fails alone
             res = await self._enqueue("embed_index", [(str(args["doc_id"]), np.asarray(args["keys"], dtype=np.int64),
                                                        list(args["texts"]))])
             return {"rows": int(res[0]), "dim": int(self.group.engine.dim)}
@@ -609,8 +607,10 @@ class EngineServer:
                     "rpc_mean_ms": {k: round(t / max(1, n), 3) for k, (n, t) in self.rpc_ms.items()}}
         if method == "health":
             pl = self.group.plane
+            ph = pl.health() if pl is not None else {"ok": True, "shards_down": []}
             return dict(self.watchdog.state(), live_ranks=self.live_ranks, world=self.group.world,
-                        replica=self.group.replica, search_plane=bool(pl is None or pl.healthy))
+                        replica=self.group.replica, search_plane=bool(ph["ok"]),
+                        shards_down=list(ph["shards_down"]))
         raise ValueError(f"unknown method {method!r}")
 
     async def _client(self, reader, writer):

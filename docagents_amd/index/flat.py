@@ -10,6 +10,7 @@ Capacity grows geometrically; at 288 GB per GPU a 768-d bf16 shard holds ~180M r
 """
 from __future__ import annotations
 
+import contextlib
 import math
 import threading
 from dataclasses import dataclass, field
@@ -42,6 +43,56 @@ class FlatIndex:
         self.docs: dict[str, DocEntry] = {}
         self.slot_docs: list[str | None] = []
         self.lock = threading.RLock()
+        self._write_ev = None   # event after the last mutation's device work (None: nothing pending)
+        self._read_evs: dict = {}  # reader stream handle -> event after its last read
+        self._depth = 0
+
+    # ----------------------------------------------------------------- stream ordering
+    # Writers (add / add_bulk / remove_* / _grow / IVF train) and readers (search, gather_ids,
+    # snapshots) run on different HIP streams: the engine's GPU thread mutates, the search plane's
+    # stream scans. Host state (n, ranges, docs) changes under ``lock`` at once, the device copies
+    # later in stream order, so a reader that only took the lock could scan rows whose copy (or
+    # _grow zero-fill) has not run yet. Inside the lock every mutation therefore orders its stream
+    # after the previous write and every read still in flight, and records a write event as its
+    # last step; every read orders its stream after that event and records a read event for its
+    # stream. All device-side: no host synchronisation on either path. A committed mutation is
+    # atomic to readers, as a committed INSERT is in the reference (internal/store/postgres.go:176-201).
+    @contextlib.contextmanager
+    def writing(self):
+        with self.lock:
+            cuda = self.device.type == "cuda"
+            outer = self._depth == 0
+            self._depth += 1
+            if cuda and outer:
+                st = torch.cuda.current_stream(self.device)
+                if self._write_ev is not None:
+                    st.wait_event(self._write_ev)
+                for ev in self._read_evs.values():
+                    st.wait_event(ev)
+            try:
+                yield
+            finally:
+                self._depth -= 1
+                if cuda and outer:
+                    ev = torch.cuda.Event()
+                    ev.record(torch.cuda.current_stream(self.device))
+                    self._write_ev = ev
+                    self._read_evs.clear()  # this write is ordered after every one of them
+
+    @contextlib.contextmanager
+    def reading(self):
+        with self.lock:
+            cuda = self.device.type == "cuda"
+            if cuda and self._write_ev is not None:
+                torch.cuda.current_stream(self.device).wait_event(self._write_ev)
+            try:
+                yield
+            finally:
+                if cuda:
+                    st = torch.cuda.current_stream(self.device)
+                    ev = torch.cuda.Event()
+                    ev.record(st)
+                    self._read_evs[st.cuda_stream] = ev
 
     # ----------------------------------------------------------------- mutation
     def _grow(self, need: int):
@@ -57,6 +108,12 @@ class FlatIndex:
         ids[:self.n] = self.ids[:self.n]
         ids_t = torch.zeros(new, dtype=torch.int64, device=self.device)
         ids_t[:self.n] = self.ids_t[:self.n]
+        if self.device.type == "cuda":
+            # the copies above read the old buffers on this stream: the allocator must not hand
+            # them out again (to an allocation on their own stream) before those copies ran
+            st = torch.cuda.current_stream(self.device)
+            for old in (self.X, self.slots_t, self.ids_t):
+                old.record_stream(st)
         self.X, self.slots_t, self.ids, self.ids_t = X, s, ids, ids_t
 
     def doc_slot(self, doc_id: str) -> int:
@@ -75,7 +132,7 @@ class FlatIndex:
             return (self.n, self.n)
         if vecs.shape[1] != self.dim:
             raise ValueError(f"vector dim {vecs.shape[1]} != index dim {self.dim}")
-        with self.lock:
+        with self.writing():
             slot = self.doc_slot(doc_id)
             s0 = self.n
             self._grow(s0 + n)
@@ -91,7 +148,7 @@ class FlatIndex:
 
     def add_bulk(self, doc_ids: list[str], rows_per_doc: list[int], ids: np.ndarray, vecs: torch.Tensor):
         """Bulk load (benchmarks / snapshot restore): documents laid out back to back."""
-        with self.lock:
+        with self.writing():
             n = int(vecs.shape[0])
             s0 = self.n
             self._grow(s0 + n)
@@ -112,7 +169,7 @@ class FlatIndex:
 
     def remove_doc(self, doc_id: str) -> int:
         """Drop a document's rows from search (rows become unreachable; compacted on snapshot)."""
-        with self.lock:
+        with self.writing():
             e = self.docs.get(doc_id)
             if e is None:
                 return 0
@@ -128,7 +185,7 @@ class FlatIndex:
         IVF delta rows) have their ranges split around the dropped rows; rows tracked only by slot
         (IVF list-major rows) leave search through their slot. Returns the rows dropped."""
         keys = np.unique(np.asarray(keys, dtype=np.int64))
-        with self.lock:
+        with self.writing():
             e = self.docs.get(doc_id)
             if e is None or e.rows == 0 or keys.size == 0 or self.n == 0:
                 return 0
@@ -177,7 +234,7 @@ class FlatIndex:
         doc_filters: per-query list of document ids (None = all documents)."""
         Q = q.shape[0]
         q = q.to(device=self.device, dtype=self.X.dtype).contiguous()
-        with self.lock:
+        with self.reading():
             if self.n == 0 or Q == 0:
                 return (torch.full((Q, k), float("-inf"), device=self.device),
                         torch.full((Q, k), -1, dtype=torch.int32, device=self.device))
@@ -227,9 +284,17 @@ class FlatIndex:
     def gather_ids(self, rows: torch.Tensor) -> torch.Tensor:
         """Device: row indices (int32, -1 = none) -> external ids (int64, -1 = none). Indices are
         clamped into the id table before the gather (a bad row index must never read outside it)."""
-        r = rows.long()
-        ok = (r >= 0) & (r < self.n)
-        return torch.where(ok, self.ids_t[r.clamp(0, max(0, self.n - 1))], torch.full_like(r, -1))
+        with self.reading():
+            r = rows.long()
+            ok = (r >= 0) & (r < self.n)
+            return torch.where(ok, self.ids_t[r.clamp(0, max(0, self.n - 1))], torch.full_like(r, -1))
+
+    def search_ids(self, q: torch.Tensor, k: int, min_sim: float, doc_filters=None):
+        """search + gather_ids as ONE read: (scores fp32 [Q, k], external ids int64 [Q, k]) from the
+        same committed state of the shard."""
+        with self.reading():
+            s, rows = self.search(q, k, min_sim, doc_filters)
+            return s, self.gather_ids(rows)
 
     def row_ids(self, rows: np.ndarray) -> np.ndarray:
         out = np.full(rows.shape, -1, dtype=np.int64)
@@ -251,11 +316,12 @@ class FlatIndex:
         return sel.astype(np.int64), docs
 
     def state_dict(self) -> dict:
-        live = []
-        for d, e in self.docs.items():
-            for a, b in e.ranges:
-                live.append((d, a, b))
-        return {"dim": self.dim, "live": live, "X": self.X[:self.n].cpu(), "ids": self.ids[:self.n].copy()}
+        with self.reading():
+            live = []
+            for d, e in self.docs.items():
+                for a, b in e.ranges:
+                    live.append((d, a, b))
+            return {"dim": self.dim, "live": live, "X": self.X[:self.n].cpu(), "ids": self.ids[:self.n].copy()}
 
     def nbytes(self) -> int:
         return self.n * self.dim * self.X.element_size()

@@ -58,7 +58,7 @@ class IVFFlatIndex(FlatIndex):
         return C.to(torch.bfloat16).contiguous()
 
     def train(self, iters: int = 10, sample: int | None = None):
-        with self.lock:
+        with self.writing():
             n = self.n
             if n < self.lists:
                 return False
@@ -125,7 +125,7 @@ class IVFFlatIndex(FlatIndex):
         covers rows [c*chunk_rows, ...); must be deterministic: it is called twice per chunk).
         Documents are ``rows_per_doc`` consecutive generated rows named f"{doc_prefix}{i}"; external
         ids are id_base + generation index. Peak memory = the final index + one chunk."""
-        with self.lock:
+        with self.writing():
             if self.n:
                 raise RuntimeError("build_streaming needs an empty index")
             nch = (n_rows + chunk_rows - 1) // chunk_rows
@@ -184,7 +184,7 @@ class IVFFlatIndex(FlatIndex):
         return r
 
     def remove_doc(self, doc_id: str) -> int:
-        with self.lock:
+        with self.writing():
             e = self.docs.get(doc_id)
             if e is None or e.rows == 0:
                 return 0
@@ -196,6 +196,10 @@ class IVFFlatIndex(FlatIndex):
 
     def live_rows_by_doc(self):
         """(rows grouped by document, [(doc_id, n_rows)]) for snapshots."""
+        with self.reading():
+            return self._live_rows_by_doc()
+
+    def _live_rows_by_doc(self):
         n = self.n
         s = self.slots_t[:n].long()
         live = torch.nonzero(s >= 0).flatten()
@@ -206,7 +210,7 @@ class IVFFlatIndex(FlatIndex):
 
     # ------------------------------------------------------------------ search
     def search(self, q: torch.Tensor, k: int, min_sim: float, doc_filters=None):
-        with self.lock:
+        with self.reading():
             if self.centroids is None or self.n < self.lists:
                 if self.n >= self.lists and self.n >= 4 * self.lists:
                     self.train()

@@ -15,7 +15,7 @@ def save_index(index, path: str, extra_meta: dict | None = None, durable: bool =
     """Write the snapshot to ``path`` atomically (tmp file + rename); ``durable``: fsync the file
     before the rename and the directory after it, so the snapshot survives a power loss once this
     returns (the vector log deletes the generations it covers right after)."""
-    with index.lock:
+    with index.reading():
         sel, docs = index.live_rows_by_doc()
         docs = [[d, n] for d, n in docs]
         selt = torch.from_numpy(sel.astype(np.int64)).to(index.device)
@@ -59,7 +59,7 @@ def load_index(index, path: str) -> int:
         raise ValueError(f"snapshot dim {meta['dim']} != index dim {index.dim}")
     docs = json.loads(meta["docs"])
     X, ids = t["X"], t["ids"].numpy()
-    with index.lock:
+    with index.writing():
         index.add_bulk([d for d, _ in docs], [n for _, n in docs], ids, X)
         if "centroids" in t and hasattr(index, "_build_lists"):
             index.centroids = t["centroids"].to(index.device)

@@ -199,6 +199,14 @@ class ShardLog:
 
     @staticmethod
     def _apply(index, op, doc, keys, vecs):
+        writing = getattr(index, "writing", None)
+        if writing is None:
+            return ShardLog._apply_ops(index, op, doc, keys, vecs)
+        with writing():  # remove + add commit as ONE mutation for concurrent scans (index/flat.py)
+            return ShardLog._apply_ops(index, op, doc, keys, vecs)
+
+    @staticmethod
+    def _apply_ops(index, op, doc, keys, vecs):
         if op == OP_REMOVE:
             index.remove_doc(doc)
         elif op == OP_UPSERT:

@@ -113,3 +113,18 @@ DA_EXPORT int da_stream_probe(const void* src, long long per_wg, int nwg, int mo
   }
   DA_LAUNCH_CHECK();
 }
+
+// ------------------------------------------------------------------------------------------
+// A bounded device-side delay: one wave sleeping `iters` x s_sleep(127) (~8k cycles each). Tests
+// use it to hold a stream busy deterministically (a writer's copies queued behind it) so that a
+// reader on another stream provably overlaps the writer's pending work (index write/search race).
+__global__ void spin_kernel(int iters, int* out) {
+  for (int i = 0; i < iters; ++i) __builtin_amdgcn_s_sleep(127);
+  if (threadIdx.x == 0 && out) out[0] = iters;
+}
+
+DA_EXPORT int da_spin(int iters, void* out, void* stream) {
+  if (iters < 0 || iters > (1 << 20)) return (int)hipErrorInvalidValue;
+  spin_kernel<<<1, 64, 0, (hipStream_t)stream>>>(iters, (int*)out);
+  DA_LAUNCH_CHECK();
+}

@@ -94,6 +94,7 @@ _SIGS = {
     "da_stream_destroy": [c_void_p],
     "da_device_cu_count": [c_int, ctypes.POINTER(c_int)],
     "da_placement_probe": [c_void_p, c_int, c_longlong, c_void_p],
+    "da_spin": [c_int, c_void_p, c_void_p],
 }
 
 
@@ -904,3 +905,10 @@ def reserve_workspace(nbytes: int, device=None) -> None:
     so the captured kernels keep pointing at a live buffer."""
     dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
     _workspace(nbytes, dev)
+
+
+def spin(iters: int, device=None) -> None:
+    """Hold the current stream busy for ~``iters`` x 3.4 us (one wave of s_sleep; bounded to 2^20
+    iterations). Test helper: work queued behind it on this stream is provably still pending."""
+    _req(0 <= iters <= (1 << 20), "spin: 0 <= iters <= 2^20")
+    _check(lib().da_spin(int(iters), None, _stream()), "da_spin")

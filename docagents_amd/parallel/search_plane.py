@@ -1,37 +1,55 @@
-"""Sharded vector search as rounds across every rank, decoupled from the decode schedulers.
+"""Sharded vector search routed to the owner shards, point to point, with failures isolated per shard.
 
 The engine serves as independent data-parallel replicas (one per TP group, each with its own RPC
-endpoint and continuous-batching scheduler, no per-tick collective; engine/server.py), the way the
-reference scales its agents (docker-compose.yml:84-85,105-106; internal/queue/nats.go:40-51). The
-vector index, though, is sharded over ALL ranks (a document lives on rank hash(doc) % N), so a
-search needs every shard. That exchange runs here, on a thread and HIP stream of its own on every
-rank, so a search never waits for any replica's decode tick or admission prefill:
+endpoint and continuous-batching scheduler; engine/server.py), the way the reference scales its
+agents (docker-compose.yml:84-85,105-106; internal/queue/nats.go:40-51). The vector index is
+sharded over ALL ranks: a document's rows live on rank ``owner_of(doc_id, world)``. Every search in
+the reference is filtered by a required, non-empty document list (cmd/query/main.go:22,
+internal/store/postgres.go:239), so a search only needs the shards that own its filter's documents:
 
-    round:  all-gather (rows, k, stop) per rank            gloo, 24 B per rank (the poll)
-            all-gather filters / thresholds of the rows     gloo, msgpack bytes
-            C2 all-gather of the query vectors              data group (RCCL on GPUs, over xGMI)
-            fused scan + doc filter + floor + top-k on the local shard (vecsearch.hip)
-            C1 all-gather of packed (score, id) top-k       data group (RCCL)
-            topk_merge kernel -> each rank resolves the requests it submitted
+    submit(q, k, floor, filters)        any thread, any rank
+      route: rows -> owner ranks of their filter documents (no filter: every rank)
+      local part  -> this rank's scan worker                        (no socket)
+      remote part -> the owner's shard server: one msgpack frame    (TCP, persistent connection)
+    shard server (every rank): a scan worker thread with its own HIP stream and kernel workspace
+      drains every queued part (local and remote) as ONE fused scan + doc filter + floor + top-k
+      launch on the local shard (vecsearch.hip), replies [m, k] (score, external id) per part
+    merge on the submitter: per row, the owners' top-k lists -> the global top-k (ties: lower
+      rank, then lower position — the order of the all-gather merge of ShardedIndex)
 
-A rank with nothing to search still joins each round (its rows = 0) — a poll every ``poll_s``
-(1 ms while searches are flowing, ``idle_poll_s`` after a second without any). Results equal the
-single-index exact search (filter and floor applied before each shard's top-k; k / floor
-per request: the round runs max k / min floor and each request is cut back, which is exact because
-every row above a request's floor ranks above every row below it).
+Why not a collective here. A collective round (the previous design, and ``ShardedIndex`` for
+lock-step batch search) makes every search a world-wide rendezvous: every rank polls, an idle
+rank still joins every round, and ONE dead or hung rank stops search for every replica, because an
+RCCL communicator cannot lose a member. The reference's replicas fail independently. Here a search
+waits only for the shards it reads: a dead rank fails the searches that touch its documents (the
+health RPC names it) and nothing else; a restarted rank is reconnected on the next request. The
+bytes are tiny (a 768-d fp32 query is 3 KB, a top-5 reply 60 B) and the hop is host TCP on one
+node (~30-60 us), against a 15-20 ms question path. And it takes the search traffic off RCCL
+altogether: RCCL is issued by one thread per process (the GPU thread: TP all-reduces above the
+IPC limit, replica gathers), so no two threads ever drive two communicators concurrently.
+
+Exactness: the doc filter and the similarity floor are applied inside each shard BEFORE its top-k,
+and a document lives on exactly one shard, so the merged result equals the single-index exact
+search. Requests with different k / floor share a scan (max k, min floor; each part is cut back,
+which is exact because every row above a part's floor ranks above every row below it).
 """
 from __future__ import annotations
 
 import collections
 import concurrent.futures as cf
+import hashlib
+import socket
+import struct
 import threading
 import time
 
 import numpy as np
 import torch
-import torch.distributed as dist
 
-from .dist import pack_scores_ids, unpack_scores_ids
+
+def owner_of(doc_id: str, world: int) -> int:
+    """The rank whose shard holds ``doc_id``'s rows (stable across processes: blake2b, not hash())."""
+    return int.from_bytes(hashlib.blake2b(doc_id.encode(), digest_size=8).digest(), "little") % max(1, world)
 
 
 def merge_shard_topk(ops, S: torch.Tensor, G: torch.Tensor, k: int):
@@ -48,210 +66,485 @@ def merge_shard_topk(ops, S: torch.Tensor, G: torch.Tensor, k: int):
     return ms, mid
 
 
-class _Req:
-    __slots__ = ("vecs", "k", "thr", "filters", "fut")
+def merge_host(parts, n: int, k: int, world: int, thr: float):
+    """parts: {rank: (row index array [m], scores [m, k'], keys [m, k'])} -> (scores [n, k] fp32,
+    keys [n, k] int64), -inf / -1 padded, floor applied. Ties: lower rank, then lower position."""
+    S = np.full((n, world * k), -np.inf, dtype=np.float32)
+    G = np.full((n, world * k), -1, dtype=np.int64)
+    for r, (rows, s, g) in parts.items():
+        kk = min(k, s.shape[1])
+        S[rows, r * k:r * k + kk] = s[:, :kk]
+        G[rows, r * k:r * k + kk] = g[:, :kk]
+    S[G < 0] = -np.inf
+    order = np.argsort(-S, axis=1, kind="stable")[:, :k]
+    sc = np.take_along_axis(S, order, 1)
+    ky = np.take_along_axis(G, order, 1)
+    drop = ~(sc >= thr)
+    sc[drop], ky[drop] = -np.inf, -1
+    return sc, ky
 
-    def __init__(self, vecs, k, thr, filters, fut):
-        self.vecs, self.k, self.thr, self.filters, self.fut = vecs, k, thr, filters, fut
+
+# --------------------------------------------------------------------------- framing
+def _send_frame(sock, obj) -> None:
+    from ..engine.rpc import pack
+    sock.sendall(pack(obj))
+
+
+def _recv_exact(sock, n: int) -> bytes:
+    buf = bytearray()
+    while len(buf) < n:
+        b = sock.recv(n - len(buf))
+        if not b:
+            raise ConnectionError("peer closed the connection")
+        buf += b
+    return bytes(buf)
+
+
+def _recv_frame(sock):
+    from ..engine.rpc import unpack
+    n = struct.unpack(">I", _recv_exact(sock, 4))[0]
+    if n > (256 << 20):
+        raise ConnectionError(f"oversized search frame ({n} B)")
+    return unpack(_recv_exact(sock, n))
+
+
+class ShardUnavailable(RuntimeError):
+    pass
+
+
+class _Job:
+    """One part of a search on the local shard: rows [m, d] + per-row filters, and where the answer
+    goes (``reply(scores, keys)`` / ``fail(exc)``)."""
+    __slots__ = ("vecs", "k", "thr", "filters", "reply", "fail")
+
+    def __init__(self, vecs, k, thr, filters, reply, fail):
+        self.vecs, self.k, self.thr, self.filters, self.reply, self.fail = vecs, k, thr, filters, reply, fail
+
+
+class _Search:
+    """A submitted search waiting for its parts."""
+    __slots__ = ("n", "k", "thr", "left", "parts", "fut", "deadline", "lock", "ranks")
+
+    def __init__(self, n, k, thr, ranks, fut, deadline):
+        self.n, self.k, self.thr, self.fut, self.deadline = n, k, thr, fut, deadline
+        self.ranks = set(ranks)
+        self.left = len(self.ranks)
+        self.parts: dict = {}
+        self.lock = threading.Lock()
+
+
+class _Peer:
+    """Client side of one remote shard: a persistent connection, its reader thread, the pending
+    parts. A failed connection fails only its own pending parts; the next request reconnects
+    (at most once per ``retry_s``), so a restarted rank rejoins without any coordination."""
+
+    def __init__(self, plane, rank: int, addr):
+        self.plane, self.rank, self.addr = plane, rank, tuple(addr)
+        self.sock = None
+        self.lock = threading.Lock()
+        self.pending: dict = {}
+        self.down_since = None
+        self.last_try = 0.0
+        self.error = ""
+
+    def _connect(self):
+        now = time.monotonic()
+        if self.down_since is not None and now - self.last_try < self.plane.retry_s:
+            raise ShardUnavailable(f"search shard {self.rank} unavailable: {self.error}")
+        self.last_try = now
+        try:
+            s = socket.create_connection(self.addr, timeout=self.plane.connect_timeout_s)
+            s.settimeout(None)
+            s.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
+        except OSError as e:
+            self.down_since = self.down_since or now
+            self.error = repr(e)
+            raise ShardUnavailable(f"search shard {self.rank} unavailable: {e!r}") from e
+        self.sock = s
+        self.down_since, self.error = None, ""
+        threading.Thread(target=self._read_loop, args=(s,), name=f"plane-peer-{self.rank}", daemon=True).start()
+
+    def send(self, rid: int, msg: dict, on_reply, on_fail):
+        try:
+            with self.lock:
+                if self.sock is None:
+                    self._connect()
+                self.pending[rid] = (on_reply, on_fail)
+                sock = self.sock
+                _send_frame(sock, msg)
+        except ShardUnavailable as e:
+            on_fail(e)
+        except OSError as e:
+            self._down(sock, e)
+
+    def _read_loop(self, sock):
+        try:
+            while True:
+                msg = _recv_frame(sock)
+                with self.lock:
+                    cb = self.pending.pop(msg.get("id"), None)
+                if cb is None:
+                    continue
+                if "error" in msg:
+                    cb[1](RuntimeError(f"search shard {self.rank}: {msg['error']}"))
+                else:
+                    cb[0](msg["scores"], msg["keys"])
+        except Exception as e:  # noqa: BLE001 - EOF / reset / bad frame: this connection is done
+            self._down(sock, e)
+
+    def _down(self, sock, exc):
+        with self.lock:
+            if sock is not None and self.sock is not sock:
+                return  # an older connection
+            if self.sock is not None:
+                try:
+                    self.sock.close()
+                except OSError:
+                    pass
+            self.sock = None
+            if not self.plane._stop:
+                self.down_since = self.down_since or time.monotonic()
+                self.error = repr(exc)
+            pend, self.pending = self.pending, {}
+        err = ShardUnavailable(f"search shard {self.rank} unavailable: {exc!r}")
+        for _, fail in pend.values():
+            fail(err)
+
+    def close(self):
+        with self.lock:
+            if self.sock is not None:
+                try:
+                    self.sock.shutdown(socket.SHUT_RDWR)
+                    self.sock.close()
+                except OSError:
+                    pass
+                self.sock = None
 
 
 class SearchPlane:
-    """One per rank. ``submit`` from any thread; results arrive as concurrent futures."""
+    """One per rank: this rank's shard server + the client that routes searches to the owners.
 
-    def __init__(self, index, rank: int = 0, world: int = 1, ctrl_group=None, data_group=None, device=None,
-                 poll_s: float = 0.001, idle_poll_s: float = 0.005, max_rows: int = 1024, stream=None):
-        self.index, self.rank, self.world = index, rank, world
-        self.ctrl_group, self.data_group = ctrl_group, data_group
-        self.device = torch.device(device) if device is not None else torch.device("cpu")
-        self.poll_s, self.idle_poll_s, self.max_rows = poll_s, idle_poll_s, max_rows
-        self.q: collections.deque = collections.deque()
+    Single process: ``SearchPlane(index).start()``. Several ranks: ``listen()`` on every rank, one
+    address exchange at startup (``start_world`` does it with a single gloo all-gather — the only
+    collective the plane ever issues), ``connect(addrs)``, ``start()``."""
+
+    def __init__(self, index, rank: int = 0, world: int = 1, device=None, stream=None, owner=None,
+                 host: str = "127.0.0.1", port: int = 0, timeout_s: float = 30.0, max_rows: int = 1024,
+                 retry_s: float = 1.0, connect_timeout_s: float = 2.0):
+        self.index, self.rank, self.world = index, rank, max(1, world)
+        self.device = torch.device(device) if device is not None else getattr(index, "device", torch.device("cpu"))
+        self.stream = stream  # None: a high-priority stream created by the scan worker
+        self.owner = owner or (lambda d: owner_of(d, self.world))
+        self.host, self.port = host, port
+        self.timeout_s, self.max_rows = timeout_s, max_rows
+        self.retry_s, self.connect_timeout_s = retry_s, connect_timeout_s
+        self.addrs = None
+        self.peers: dict[int, _Peer] = {}
+        self.jobs: collections.deque = collections.deque()
         self.cv = threading.Condition()
-        self.stream = stream  # None: a high-priority stream created by the plane thread
-        self.write_event = None
+        self.searches: dict[int, _Search] = {}
+        self._ids = 0
+        self._ids_lock = threading.Lock()
         self._stop = False
-        self._thread = None
-        self._last_active = 0.0
-        self.healthy = True
+        self._threads: list[threading.Thread] = []
+        self._listener = None
+        self._conns: list = []
         self.error = ""
-        self.stats = {"rounds": 0, "empty_rounds": 0, "queries": 0, "busy_s": 0.0}
+        self.stats = {"searches": 0, "local_parts": 0, "remote_parts": 0, "served_remote": 0, "scans": 0,
+                      "rows": 0, "busy_s": 0.0, "failed": 0}
 
-    # ------------------------------------------------------------------ public
-    def submit(self, vecs: np.ndarray, k: int, min_sim: float, filters=None) -> cf.Future:
-        """vecs [n, d]; filters: None, or a list of n document-id lists (or one list for all rows)."""
+    # ------------------------------------------------------------------ lifecycle
+    def listen(self) -> tuple:
+        """Bind this rank's shard server; returns its (host, port)."""
+        if self._listener is None:
+            ls = socket.socket(socket.AF_INET, socket.SOCK_STREAM)
+            ls.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)
+            ls.bind((self.host, self.port))
+            ls.listen(64)
+            self._listener = ls
+        return self._listener.getsockname()[:2]
+
+    def connect(self, addrs) -> "SearchPlane":
+        """Every rank's shard-server address, rank order (connections open lazily)."""
+        self.addrs = [tuple(a) for a in addrs]
+        if len(self.addrs) != self.world:
+            raise ValueError(f"search plane: {len(self.addrs)} addresses for a world of {self.world}")
+        self.peers = {r: _Peer(self, r, a) for r, a in enumerate(self.addrs) if r != self.rank}
+        return self
+
+    def start(self) -> "SearchPlane":
+        if self.world > 1 and self.addrs is None:
+            raise RuntimeError("search plane: connect(addrs) before start() when world > 1")
+        for fn, name in ((self._scan_loop, "scan"), (self._housekeeping, "timer")):
+            t = threading.Thread(target=fn, name=f"plane-{name}-{self.rank}", daemon=True)
+            t.start()
+            self._threads.append(t)
+        if self._listener is not None:
+            t = threading.Thread(target=self._accept_loop, name=f"plane-accept-{self.rank}", daemon=True)
+            t.start()
+            self._threads.append(t)
+        return self
+
+    @classmethod
+    def start_world(cls, index, rank: int, world: int, group=None, **kw) -> "SearchPlane":
+        """listen + exchange addresses over ``group`` (gloo; one all_gather_object at startup) +
+        connect + start. Every rank of the world calls it."""
+        plane = cls(index, rank, world, **kw)
+        if world == 1:
+            return plane.start()
+        import torch.distributed as dist
+        addr = plane.listen()
+        addrs = [None] * world
+        dist.all_gather_object(addrs, list(addr), group=group)
+        return plane.connect(addrs).start()
+
+    def stop(self, timeout: float = 10.0) -> None:
+        self._stop = True
+        with self.cv:
+            self.cv.notify_all()
+        if self._listener is not None:
+            try:
+                self._listener.close()
+            except OSError:
+                pass
+        for p in self.peers.values():
+            p.close()
+        for c in list(self._conns):
+            try:
+                c.shutdown(socket.SHUT_RDWR)
+                c.close()
+            except OSError:
+                pass
+        for t in self._threads:
+            if t is not threading.current_thread():
+                t.join(timeout)
+        self._fail_all(RuntimeError("search plane stopped"))
+
+    @property
+    def healthy(self) -> bool:
+        """This rank's shard server is serving (peers being down is reported by ``health``)."""
+        return not self._stop and not self.error and all(t.is_alive() for t in self._threads)
+
+    def health(self) -> dict:
+        down = sorted(r for r, p in self.peers.items() if p.down_since is not None)
+        return {"ok": self.healthy, "shards_down": down,
+                "errors": {str(r): self.peers[r].error for r in down}}
+
+    # ------------------------------------------------------------------ submit / route / merge
+    def submit(self, vecs, k: int, min_sim: float, filters=None) -> cf.Future:
+        """vecs [n, d]; filters: None (every document), or one document-id list per row (or one list
+        for all rows). Future -> (scores fp32 [n, k], external ids int64 [n, k]), -inf / -1 padded."""
         vecs = np.ascontiguousarray(vecs, dtype=np.float32).reshape(-1, self.index.dim)
-        n = vecs.shape[0]
+        n, k, thr = vecs.shape[0], int(k), float(min_sim)
         if filters is not None:
             if len(filters) == 1 and n != 1:
                 filters = list(filters) * n
             if len(filters) != n:
                 raise ValueError("search: one document filter per query row (or one for all rows)")
-            filters = [None if f is None else list(f) for f in filters]
         fut: cf.Future = cf.Future()
-        if not self.healthy:
-            fut.set_exception(RuntimeError(f"search plane down: {self.error}"))
+        if self._stop or not self.healthy and self._threads:
+            fut.set_exception(RuntimeError(f"search plane down: {self.error or 'stopped'}"))
             return fut
-        with self.cv:
-            self.q.append(_Req(vecs, int(k), float(min_sim), filters, fut))
-            self.cv.notify()
+        # route: rank -> (rows, per-row filters restricted to that rank's documents)
+        route: dict[int, tuple[list, list]] = {}
+        for i in range(n):
+            f = None if filters is None else filters[i]
+            if f is None:
+                for r in range(self.world):
+                    rr = route.setdefault(r, ([], []))
+                    rr[0].append(i)
+                    rr[1].append(None)
+                continue
+            by: dict[int, list] = {}
+            for d in f:
+                by.setdefault(self.owner(str(d)), []).append(str(d))
+            for r, ds in by.items():
+                rr = route.setdefault(r, ([], []))
+                rr[0].append(i)
+                rr[1].append(ds)
+        self.stats["searches"] += 1
+        if not route:  # every row filters on nothing: nothing can match
+            fut.set_result((np.full((n, k), -np.inf, np.float32), np.full((n, k), -1, np.int64)))
+            return fut
+        with self._ids_lock:
+            self._ids += 1
+            sid = self._ids
+        srch = _Search(n, k, thr, route.keys(), fut, time.monotonic() + self.timeout_s)
+        self.searches[sid] = srch
+        for r, (rows, flt) in route.items():
+            rows_a = np.asarray(rows, dtype=np.int64)
+
+            def reply(s, g, r=r, rows_a=rows_a):
+                self._part_done(sid, r, (rows_a, np.asarray(s, np.float32), np.asarray(g, np.int64)), None)
+
+            def fail(exc, r=r):
+                self._part_done(sid, r, None, exc)
+            sub = vecs if len(rows) == n else vecs[rows_a]
+            if r == self.rank:
+                self.stats["local_parts"] += 1
+                self._enqueue(_Job(sub, k, thr, flt, reply, fail))
+            else:
+                self.stats["remote_parts"] += 1
+                self.peers[r].send(sid, {"id": sid, "vecs": sub, "k": k, "thr": thr, "filters": flt}, reply, fail)
         return fut
 
-    def note_write(self) -> None:
-        """Called by the thread that mutated the index (after the mutation was enqueued on its
-        stream): the next round's scan waits for it on the device."""
-        if self.device.type == "cuda":
-            ev = torch.cuda.Event()
-            ev.record()
-            self.write_event = ev
+    def _part_done(self, sid: int, rank: int, part, exc):
+        s = self.searches.get(sid)
+        if s is None:
+            return
+        with s.lock:
+            if s.fut.done() or rank not in s.ranks:
+                return
+            s.ranks.discard(rank)
+            if exc is not None:
+                self.searches.pop(sid, None)
+                self.stats["failed"] += 1
+                s.fut.set_exception(exc)
+                return
+            s.parts[rank] = part
+            if s.ranks:
+                return
+            self.searches.pop(sid, None)
+        try:
+            s.fut.set_result(merge_host(s.parts, s.n, s.k, self.world, s.thr))
+        except Exception as e:  # noqa: BLE001
+            s.fut.set_exception(e)
 
-    def start(self) -> "SearchPlane":
-        self._thread = threading.Thread(target=self._run, name=f"search-plane-{self.rank}", daemon=True)
-        self._thread.start()
-        return self
+    def _housekeeping(self):
+        """Fail searches whose parts did not come back within ``timeout_s`` (a hung shard), naming
+        the shards still pending."""
+        while not self._stop:
+            time.sleep(0.1)
+            now = time.monotonic()
+            for sid, s in list(self.searches.items()):
+                if now > s.deadline:
+                    pend = sorted(s.ranks)
+                    for r in pend:
+                        self._part_done(sid, r, None, TimeoutError(
+                            f"search shards {pend} did not answer within {self.timeout_s:.0f} s"))
 
-    def stop(self, timeout: float = 30.0) -> None:
-        """Leave the plane: this rank's next round carries the stop flag, and every rank exits the
-        round in which it sees one (so the whole engine stops searching together)."""
+    def _fail_all(self, exc):
+        for sid, s in list(self.searches.items()):
+            for r in list(s.ranks):
+                self._part_done(sid, r, None, exc)
         with self.cv:
-            self._stop = True
-            self.cv.notify()
-        if self._thread is not None:
-            self._thread.join(timeout)
+            jobs, self.jobs = list(self.jobs), collections.deque()
+        for j in jobs:
+            j.fail(exc)
 
-    # ------------------------------------------------------------------ rounds
-    def _run(self):
+    # ------------------------------------------------------------------ shard server
+    def _accept_loop(self):
+        while not self._stop:
+            try:
+                c, _ = self._listener.accept()
+            except OSError:
+                return
+            c.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
+            self._conns.append(c)
+            threading.Thread(target=self._serve_conn, args=(c,), name=f"plane-conn-{self.rank}", daemon=True).start()
+
+    def _serve_conn(self, c):
+        wlock = threading.Lock()
+
+        def send(obj):
+            try:
+                with wlock:
+                    _send_frame(c, obj)
+            except OSError:
+                pass  # the requester went away; its side fails its own pending parts
+        try:
+            while not self._stop:
+                msg = _recv_frame(c)
+                rid = msg.get("id")
+                try:
+                    vecs = np.ascontiguousarray(msg["vecs"], dtype=np.float32).reshape(-1, self.index.dim)
+                    flt = msg.get("filters")
+                    if flt is not None and len(flt) != vecs.shape[0]:
+                        raise ValueError("one filter per row")
+                    k = int(msg["k"])
+                    if not 0 < k <= 1024:
+                        raise ValueError(f"bad k {k}")
+                except Exception as e:  # noqa: BLE001 - a malformed request fails alone
+                    send({"id": rid, "error": f"bad request: {e}"})
+                    continue
+                self.stats["served_remote"] += 1
+                self._enqueue(_Job(vecs, k, float(msg["thr"]), flt,
+                                   lambda s, g, rid=rid: send({"id": rid, "scores": s, "keys": g}),
+                                   lambda e, rid=rid: send({"id": rid, "error": repr(e)})))
+        except Exception:  # noqa: BLE001 - EOF / reset: the requester's side handles it
+            pass
+        finally:
+            try:
+                c.close()
+            except OSError:
+                pass
+            try:
+                self._conns.remove(c)
+            except ValueError:
+                pass
+
+    def _enqueue(self, job: _Job):
+        with self.cv:
+            self.jobs.append(job)
+            self.cv.notify()
+
+    def _take(self) -> list[_Job]:
+        out, n = [], 0
+        with self.cv:
+            while not self.jobs and not self._stop:
+                self.cv.wait(0.5)
+            while self.jobs and (not out or n + self.jobs[0].vecs.shape[0] <= self.max_rows):
+                j = self.jobs.popleft()
+                out.append(j)
+                n += j.vecs.shape[0]
+        return out
+
+    def _scan_loop(self):
         if self.device.type == "cuda":
             torch.cuda.set_device(self.device)
             if self.stream is None:
                 self.stream = torch.cuda.Stream(device=self.device, priority=-1)
-        try:
-            while self._round():
-                pass
-        except Exception as e:  # noqa: BLE001 - a dead peer / collective timeout: fail loudly, stop
-            self.healthy = False
-            self.error = repr(e)
-        finally:
-            self._fail_pending(RuntimeError(f"search plane stopped{': ' + self.error if self.error else ''}"))
-
-    def _fail_pending(self, exc):
-        with self.cv:
-            while self.q:
-                r = self.q.popleft()
-                if not r.fut.done():
-                    r.fut.set_exception(exc)
-
-    def _take(self) -> list[_Req]:
-        out, n = [], 0
-        with self.cv:
-            while self.q and (not out or n + self.q[0].vecs.shape[0] <= self.max_rows):
-                r = self.q.popleft()
-                out.append(r)
-                n += r.vecs.shape[0]
-        return out
-
-    def _round(self) -> bool:
-        if self.world == 1:
-            with self.cv:
-                while not self.q and not self._stop:
-                    self.cv.wait(0.5)
-                if self._stop and not self.q:
-                    return False
+        while not self._stop:
             take = self._take()
-            if take:
-                self._serve(take, None)
-            return True
-        take = self._take()
-        n = sum(r.vecs.shape[0] for r in take)
-        hdr = torch.tensor([n, max((r.k for r in take), default=0), 1 if self._stop else 0], dtype=torch.int64)
-        allh = torch.empty(self.world * 3, dtype=torch.int64)
-        dist.all_gather_into_tensor(allh, hdr, group=self.ctrl_group)
-        allh = allh.view(self.world, 3)
-        if int(allh[:, 2].max()) > 0:
-            for r in take:
-                if not r.fut.done():
-                    r.fut.set_exception(RuntimeError("search plane stopping"))
-            return False
-        if int(allh[:, 0].sum()) == 0:
-            self.stats["empty_rounds"] += 1
-            idle = time.monotonic() - self._last_active > 1.0
-            with self.cv:
-                if not self.q and not self._stop:
-                    self.cv.wait(self.idle_poll_s if idle else self.poll_s)
-            return True
-        self._last_active = time.monotonic()
-        self._serve(take, allh)
-        return True
+            if not take:
+                continue
+            try:
+                self._scan(take)
+            except Exception as e:  # noqa: BLE001 - fail this batch's parts, keep serving
+                for j in take:
+                    j.fail(e)
 
-    def _serve(self, take: list[_Req], allh):
+    def _scan(self, take: list[_Job]):
+        """ONE fused scan for every queued part (local and remote) on this rank's shard."""
         t0 = time.perf_counter()
         idx, dev = self.index, self.index.device
-        d = idx.dim
+        K = max(j.k for j in take)
+        thr = min(j.thr for j in take)
+        Q = np.concatenate([j.vecs for j in take])
+        filters = [f for j in take for f in (j.filters if j.filters is not None else [None] * j.vecs.shape[0])]
+        nofilter = all(f is None for f in filters)
         stream_ctx = torch.cuda.stream(self.stream) if self.stream is not None else _nullctx()
-        # the scan kernels' scratch must not be the GPU thread's: its decode graph captured that
-        # workspace's pointer and runs concurrently with this thread (ops/kernels.py workspace_role)
         ws_ctx = _nullctx()
         if dev.type == "cuda":
+            # the scan kernels' scratch must not be the GPU thread's: its decode graph captured that
+            # workspace's pointer and runs concurrently with this thread (ops/kernels.py workspace_role)
             from ..ops.kernels import workspace_role
             ws_ctx = workspace_role("search")
         with stream_ctx, ws_ctx:
-            if self.write_event is not None and self.stream is not None:
-                self.stream.wait_event(self.write_event)
-            rows = [r.vecs.shape[0] for r in take]
-            mine_q = np.concatenate([r.vecs for r in take]) if take else np.zeros((0, d), np.float32)
-            mine_f = [f for r in take for f in (r.filters if r.filters is not None else [None] * r.vecs.shape[0])]
-            mine_thr = [r.thr for r in take for _ in range(r.vecs.shape[0])]
-            if allh is None:  # one rank: the local shard is the whole index
-                counts, K = [len(mine_q)], max(r.k for r in take)
-                filters, thr_all, Q = mine_f, mine_thr, torch.from_numpy(mine_q).to(dev)
-            else:
-                from .dist import all_gather_bytes
-                from ..engine.rpc import dumps, loads
-                counts = [int(x) for x in allh[:, 0].tolist()]
-                K = int(allh[:, 1].max())
-                parts = [loads(p) for p in all_gather_bytes(dumps([mine_f, mine_thr]), "cpu", self.ctrl_group)]
-                filters = [f for fs, _ in parts for f in fs]
-                thr_all = [t for _, ts in parts for t in ts]
-                maxn = max(counts)
-                pad = torch.zeros((maxn, d), dtype=torch.float32, device=self._data_dev())
-                if len(mine_q):
-                    pad[:len(mine_q)] = torch.from_numpy(mine_q).to(pad.device)
-                allq = torch.empty((self.world * maxn, d), dtype=torch.float32, device=pad.device)
-                dist.all_gather_into_tensor(allq, pad, group=self.data_group)             # C2
-                sel = torch.cat([torch.arange(r * maxn, r * maxn + c) for r, c in enumerate(counts)])
-                Q = allq.index_select(0, sel.to(allq.device)).to(dev)
-            thr = float(min(thr_all))
-            nofilter = all(f is None for f in filters)
-            with idx.lock:
-                s, rowsel = idx.search(Q, K, thr, None if nofilter else filters)
-                gid = idx.gather_ids(rowsel)
-                if self.stream is not None:
-                    self.stream.synchronize()  # the scan has read the shard before a writer may touch it
-            if allh is None:
-                ms, mid = s, gid
-            else:
-                P = pack_scores_ids(s, gid).to(self._data_dev())
-                allp = torch.empty((self.world,) + tuple(P.shape), dtype=P.dtype, device=P.device)
-                dist.all_gather_into_tensor(allp.view(-1, *P.shape[1:]), P, group=self.data_group)  # C1
-                S, G = unpack_scores_ids(allp.to(dev))                                       # [W, Qtot, K]
-                o = sum(counts[:self.rank])
-                S, G = S[:, o:o + counts[self.rank]].contiguous(), G[:, o:o + counts[self.rank]].contiguous()
-                ms, mid = merge_shard_topk(idx.ops, S, G, K) if counts[self.rank] else (S[0], G[0])
-            ms, mid = ms.float().cpu().numpy(), mid.cpu().numpy()
+            # search_ids orders this stream after the shard's last committed write (index/flat.py)
+            s, g = idx.search_ids(torch.from_numpy(Q).to(dev), K, thr, None if nofilter else filters)
+            s, g = s.float().cpu().numpy(), g.cpu().numpy()
         o = 0
-        for r, n in zip(take, rows):
-            sc, ky = ms[o:o + n, :r.k].copy(), mid[o:o + n, :r.k].copy()
-            drop = ~(sc >= r.thr)
+        for j in take:
+            m = j.vecs.shape[0]
+            sc, ky = s[o:o + m, :j.k].copy(), g[o:o + m, :j.k].copy()
+            drop = ~(sc >= j.thr)
             sc[drop], ky[drop] = -np.inf, -1
-            if not r.fut.done():
-                r.fut.set_result((sc, ky))
-            o += n
-        self.stats["rounds"] += 1
-        self.stats["queries"] += sum(rows)
+            j.reply(sc, ky)
+            o += m
+        self.stats["scans"] += 1
+        self.stats["rows"] += len(Q)
         self.stats["busy_s"] += time.perf_counter() - t0
-
-    def _data_dev(self):
-        if self.data_group is not None and dist.get_backend(self.data_group) == "gloo":
-            return torch.device("cpu")
-        return self.index.device if self.index.device.type == "cuda" else torch.device("cpu")
 
 
 class _nullctx:

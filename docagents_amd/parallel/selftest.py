@@ -227,13 +227,12 @@ def check_replicas(rank, world, port, out_path, tp: int = 1):
         if r == replica:
             rep_ctrl, rep_data = c, d
     plane_ctrl = dist.new_group(backend="gloo")
-    plane_data = dist.new_group(backend="gloo")
     tpc = TPContext(rank % tp, tp, rep_data) if tp > 1 else None
     eng = Engine("tiny-enc", "tiny-dec-tp8" if tp > 1 else "tiny-dec", "cpu", tp=tpc, max_batch=4, max_seq=512,
                  max_new_tokens=4, summary_max_new=4, use_graphs=False)
     if replica == 1:
         faults.configure_delay({"engine.tick": float(os.environ.get("DA_TEST_SLOW_TICK", "3.0"))})
-    plane = SearchPlane(eng.index, rank, world, plane_ctrl, plane_data).start()
+    plane = SearchPlane.start_world(eng.index, rank, world, plane_ctrl)
     grp = EngineGroup(eng, rank, world, rep_ctrl, rep_data, tp_size=tp, plane=plane)
     # replica endpoints: free ports picked by rank 0 (neighbours of the rendezvous port may already
     # be taken by the process group's own connections)
@@ -603,3 +602,135 @@ def check_tp_decoder_gpu(rank, world, port, out_path, wrong_order: bool = False)
 
 def check_tp_decoder_gpu_wrong_order(rank, world, port, out_path):
     check_tp_decoder_gpu(rank, world, port, out_path, wrong_order=True)
+
+
+def check_replica_failover(rank, world, port, out_path, victim: int | None = None):
+    """Replicas fail independently (the reference's queue-group workers, internal/queue/nats.go:40-51,
+    docker-compose.yml:84-85): ``world`` one-rank replicas serve the full stack as engine_main builds
+    it; once ingest is done the ``victim`` rank (default: the last) SIGKILLs itself. Then, driven by
+    rank 0 through ``EngineCluster``: searches over documents on live ranks must keep returning the
+    exact result, searches that need the dead shard must fail (naming it), answers must keep flowing
+    (retried away from the dead replica), and ``health`` must name the dead replica and shard.
+    Coordination after the kill uses files only: no collective can run with a dead member."""
+    import asyncio
+    import signal
+    import time as _t
+    _init(rank, world, port)
+    from ..engine.engine import Engine
+    from ..engine.rpc import EngineCluster
+    from ..engine.server import EngineGroup, EngineServer, owner_of
+    from ..utils.log import discard
+    from .search_plane import SearchPlane
+    victim = world - 1 if victim is None else victim
+    eng = Engine("tiny-enc", "tiny-dec", "cpu", max_batch=4, max_seq=512, max_new_tokens=4, summary_max_new=4,
+                 use_graphs=False)
+    plane = SearchPlane.start_world(eng.index, rank, world, None, timeout_s=10.0, retry_s=0.2)
+    grp = EngineGroup(eng, rank, world, plane=plane)
+    ports = [0] * world
+    if rank == 0:
+        socks = [socket.socket() for _ in range(world)]
+        for sk in socks:
+            sk.bind(("127.0.0.1", 0))
+        ports = [sk.getsockname()[1] for sk in socks]
+        for sk in socks:
+            sk.close()
+    box = [ports]
+    dist.broadcast_object_list(box, src=0)
+    urls = [f"tcp://127.0.0.1:{p}" for p in box[0]]
+    kill_flag, done_flag = out_path + ".kill", out_path + ".done"
+
+    async def serve():
+        srv = EngineServer(grp, discard(), continuous=True, cb_window_s=0.0, urls=urls, liveness_s=0)
+        await srv.start(urls[rank])
+        if rank == 0:
+            try:
+                verdict = await drive()
+            except Exception as e:  # noqa: BLE001 - reported, the test asserts on it
+                verdict = {"error": repr(e)}
+            with open(out_path, "w") as f:
+                json.dump(verdict, f)
+            open(done_flag, "w").close()
+        else:
+            while not os.path.exists(done_flag):
+                if rank == victim and os.path.exists(kill_flag):
+                    os.kill(os.getpid(), signal.SIGKILL)
+                await asyncio.sleep(0.02)
+        srv.server.close()
+
+    async def drive():
+        v = {}
+        cl = await EngineCluster(urls[0], timeout=30.0).connect(retries=200, delay=0.05)
+        docs, per = [], {}
+        i = 0
+        while min(per.get(r, 0) for r in range(world)) < 2:
+            d = f"fo-doc-{i}"
+            i += 1
+            o = owner_of(d, world)
+            if per.get(o, 0) < 2:
+                docs.append(d)
+                per[o] = per.get(o, 0) + 1
+        texts = {d: [f"chunk {j} of {d} on topic {i * 5 + j}" for j in range(3)] for i, d in enumerate(docs)}
+        await asyncio.gather(*[cl.call("embed_index", doc_id=d, keys=np.arange(3, dtype=np.int64) + 10 * i,
+                                       texts=texts[d]) for i, d in enumerate(docs)])
+        allt = [t for d in docs for t in texts[d]]
+        allv = (await cl.clients[0].call("embed", texts=allt, preprocess=True))["vecs"]
+        keys = np.array([10 * i + j for i, _ in enumerate(docs) for j in range(3)])
+        live = [d for d in docs if owner_of(d, world) != victim]
+        dead_docs = [d for d in docs if owner_of(d, world) == victim]
+
+        def exact(q, allowed, k):
+            m = np.array([d in allowed for d in docs for _ in range(3)])
+            sc = allv @ q
+            idx = np.where(m)[0]
+            order = idx[np.lexsort((idx, -sc[idx]))][:k]
+            return sc[order], keys[order]
+
+        def ok(res, q, allowed, k):
+            s_ref, _ = exact(q, allowed, k)
+            got = [x for x in res["keys"][0] if x >= 0]
+            return len(got) == len(s_ref) and np.allclose(np.sort(res["scores"][0][:len(got)]), np.sort(s_ref),
+                                                          atol=1e-2)
+        q = allv[4]
+        v["before_all_ok"] = ok(await cl.call("search", vecs=q[None], filters=[docs], k=5, min_sim=-1.0), q, docs, 5)
+        open(kill_flag, "w").close()
+        t0 = _t.perf_counter()
+        while _t.perf_counter() - t0 < 30:
+            h = await cl.call("health")
+            if victim in h.get("dead_replicas", []):
+                break
+            await asyncio.sleep(0.1)
+        v["dead_detected_s"] = round(_t.perf_counter() - t0, 3)
+        # searches over live shards, issued at every live replica
+        res = []
+        for r in range(world):
+            if r == victim:
+                continue
+            for b in range(3):
+                qq = allv[(3 * b + r) % len(allv)]
+                rr = await cl.clients[r].call("search", vecs=qq[None], filters=[live], k=4, min_sim=-1.0)
+                res.append(ok(rr, qq, live, 4))
+        v["live_searches_ok"] = bool(res) and all(res)
+        try:
+            await cl.clients[0].call("search", vecs=q[None], filters=[[live[0], dead_docs[0]]], k=4, min_sim=-1.0)
+            v["dead_search_failed"] = False
+        except Exception as e:  # noqa: BLE001
+            v["dead_search_failed"] = f"shard {victim}" in str(e)
+            v["dead_search_error"] = str(e)[:200]
+        answers = await asyncio.gather(*[cl.call("answer", items=[{"question": f"q{i}?", "context": "ctx",
+                                                                   "quality": 0.5}]) for i in range(2 * world)],
+                                       return_exceptions=True)
+        v["answers_ok"] = all(not isinstance(a, BaseException) and 0.0 <= a["results"][0][1] <= 0.5 + 1e-6
+                              for a in answers)
+        v["answer_errors"] = [repr(a)[:120] for a in answers if isinstance(a, BaseException)]
+        es = await cl.call("embed_search", texts=[allt[1]], filters=[live], k=3, min_sim=-1.0)
+        v["embed_search_ok"] = bool(ok(es, es["vecs"][0], live, 3))
+        h = await cl.call("health")
+        v["health_ok_flag"] = h["ok"]
+        v["dead_replicas"] = h.get("dead_replicas")
+        v["shards_down"] = h.get("shards_down")
+        await cl.close()
+        return v
+
+    asyncio.run(serve())
+    plane.stop(timeout=2.0)
+    os._exit(0)  # no collective teardown: the process group has a dead member

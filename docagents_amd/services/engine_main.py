@@ -7,7 +7,8 @@ collectives over xGMI, gloo groups carry the small control messages.
   TP_SIZE=t (divides the world; default 1): world / t independent replicas. Replica r = ranks
   [r t, (r + 1) t), served by its leader on port base + r (unix: path.r<r> for r > 0) with its own
   micro-batchers and continuous scheduler; TP followers step the decoder with their leader. The
-  vector index is sharded over every rank and searched through the search plane (all ranks).
+  vector index is sharded over every rank; a search goes point to point to the shards that own its
+  documents (parallel/search_plane.py), so a dead rank fails only the searches that need its shard.
   Agents connect to the base URL; ``EngineCluster`` discovers the other replicas (topology RPC),
   load-balances generation / embedding over them and routes index calls to the owner's replica.
 Durable shards (default): ``--index-dir DIR`` (INDEX_DIR, default DATA_DIR/index) holds each rank's
@@ -64,7 +65,7 @@ def main(argv=None) -> int:
     if world % t:
         raise SystemExit(f"TP_SIZE={t} must divide the world size {world}")
     replicas, replica = world // t, rank // t
-    rep_ctrl = rep_data = plane_ctrl = plane_data = None
+    rep_ctrl = rep_data = plane_ctrl = None
     tp = None
     dev = info.device
     if world > 1:
@@ -79,8 +80,7 @@ def main(argv=None) -> int:
             if r == replica:
                 rep_ctrl, rep_data = c, d
         to = datetime.timedelta(seconds=max(60.0, cfg.engine_step_timeout))
-        plane_ctrl = dist.new_group(backend="gloo", timeout=to)
-        plane_data = dist.new_group(timeout=to)
+        plane_ctrl = dist.new_group(backend="gloo", timeout=to)  # the plane's one address exchange
         if t > 1:
             tp = TPContext(rank % t, t, rep_data)
     eng = Engine(cfg.embed_arch, cfg.llm_arch, dev, seed=cfg.seed, tp=tp, max_batch=cfg.max_batch,
@@ -109,7 +109,9 @@ def main(argv=None) -> int:
         from ..ops.streams import serving_lanes
         lanes = serving_lanes(cfg.engine_latency_cus, dev)
         log.info("cu partition", "latency_cus", cfg.engine_latency_cus)
-    plane = SearchPlane(eng.index, rank, world, plane_ctrl, plane_data, device=dev, stream=lanes[2]).start()
+    plane = SearchPlane.start_world(eng.index, rank, world, plane_ctrl, device=dev, stream=lanes[2],
+                                    host=os.environ.get("ENGINE_PLANE_HOST", "127.0.0.1"),
+                                    timeout_s=max(5.0, min(60.0, cfg.engine_step_timeout)))
     grp = EngineGroup(eng, rank, world, rep_ctrl, rep_data, shard_log=shard_log, tp_size=t, plane=plane)
     if not grp.is_leader:
         grp.follower_loop()

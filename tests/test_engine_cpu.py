@@ -333,9 +333,9 @@ def test_engine_search_microbatch_matches_single_searches(eng):
         args = [dict(vecs=qs[i:i + 1], filters=None if f is None else [f], k=3, min_sim=-1.0)
                 for i, f in enumerate(flt)]
         alone = [await cl.call("search", **a) for a in args]
-        b0 = srv.group.plane.stats["rounds"]
+        b0 = srv.group.plane.stats["scans"]
         together = await asyncio.gather(*[cl.call("search", **a) for a in args])
-        assert srv.group.plane.stats["rounds"] - b0 < len(args)  # coalesced into plane rounds
+        assert srv.group.plane.stats["scans"] - b0 < len(args)  # coalesced into shared scans
         for x, y in zip(alone, together):
             assert np.array_equal(x["keys"], y["keys"]) and np.allclose(x["scores"], y["scores"])
         # a malformed search fails alone; the batcher keeps serving
