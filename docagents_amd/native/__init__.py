@@ -53,6 +53,28 @@ def build(target: str | None = None, force: bool = False) -> dict:
     return out
 
 
+SANITIZE_FLAGS = ["-O1", "-g", "-fno-omit-frame-pointer", "-fsanitize=address,undefined",
+                  "-fno-sanitize-recover=all"]
+
+
+def build_sanitized(dst: Path, extra: dict | None = None) -> dict:
+    """ASan + UBSan builds of the native servers (and of any ``extra`` {name: [sources]} test
+    drivers) into ``dst``: what tests/test_native_sanitized.py feeds malformed, partial, pipelined
+    and oversized protocol frames. Host code only."""
+    dst = Path(dst)
+    dst.mkdir(parents=True, exist_ok=True)
+    jobs = {"da-broker": [HERE / "broker.cpp"], "da-kvserver": [HERE / "kvserver.cpp"]}
+    jobs.update({k: [Path(x) for x in v] for k, v in (extra or {}).items()})
+    out = {}
+    for name, srcs in jobs.items():
+        cmd = [_cxx(), "-std=c++17", *SANITIZE_FLAGS, "-I", str(HERE), *map(str, srcs), "-o", str(dst / name)]
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"sanitized build of {name} failed:\n{r.stderr}")
+        out[name] = dst / name
+    return out
+
+
 def binary(name: str) -> Path:
     return build(name)[name]
 

@@ -70,6 +70,7 @@ struct Broker {
   std::string durable_prefix = "tasks.";
   int ack_wait_ms = 300000, max_deliver = 5;
   size_t max_parked = 1000000;
+  size_t max_payload = 64u << 20;  // advertised in INFO
   uint64_t n_pub = 0, n_msg = 0, n_redeliver = 0, n_dlq = 0, n_acks = 0;
   std::unordered_map<uint64_t, bool> verbose;
 
@@ -179,9 +180,10 @@ struct Broker {
     while (true) {
       size_t e = c.in.find("\r\n");
       if (e == std::string::npos) {
-        if (c.in.size() > (1u << 20)) { err(c, "Maximum Control Line Exceeded"); loop.close(c); }
+        if (c.in.size() > (1u << 20)) { err(c, "Maximum Control Line Exceeded"); c.in.clear(); loop.close(c); }
         return;
       }
+      if (e > (1u << 20)) { err(c, "Maximum Control Line Exceeded"); c.in.clear(); loop.close(c); return; }
       std::string line = c.in.substr(0, e);
       std::string verb = line.substr(0, line.find(' '));
       std::transform(verb.begin(), verb.end(), verb.begin(), ::toupper);
@@ -192,8 +194,20 @@ struct Broker {
         while (is >> t) a.push_back(t);
       }
       if (verb == "PUB") {
-        if (a.size() < 3) { err(c, "Unknown Protocol Operation"); c.in.erase(0, e + 2); continue; }
-        size_t n = strtoull(a.back().c_str(), nullptr, 10);
+        if (a.size() < 3 || a.size() > 4) { err(c, "Unknown Protocol Operation"); c.in.erase(0, e + 2); continue; }
+        // the size must be a plain decimal within max_payload (nats-server: "Maximum Payload
+        // Violation", then the connection is closed: the rest of the stream cannot be framed)
+        const std::string& ns = a.back();
+        size_t n = 0;
+        bool ok = !ns.empty() && ns.size() <= 10;
+        for (char ch : ns) ok = ok && ch >= '0' && ch <= '9';
+        if (ok) n = strtoull(ns.c_str(), nullptr, 10);
+        if (!ok || n > max_payload) {
+          err(c, ok ? "Maximum Payload Violation" : "Invalid Message Size");
+          c.in.clear();
+          loop.close(c);
+          return;
+        }
         if (c.in.size() < e + 2 + n + 2) return;  // wait for payload
         std::string data = c.in.substr(e + 2, n);
         c.in.erase(0, e + 2 + n + 2);

@@ -74,13 +74,38 @@ struct KV {
     }
   }
 
-  // parse one RESP array command (or inline command); returns false if incomplete
-  bool parse(Conn& c, std::vector<std::string>& args) {
+  // Limits of the stock server (redis.conf proto-max-bulk-len 512 MB; inline requests 64 KB;
+  // multibulk length 1M here): a frame outside them is a protocol error that closes the
+  // connection, as Redis does — the rest of the stream cannot be framed.
+  static constexpr long kMaxBulk = 512L << 20, kMaxArgs = 1L << 20;
+  static constexpr size_t kMaxInline = 64u << 10;
+
+  // strict decimal (optionally negative) between [p, e): false on anything else or overflow
+  static bool parse_long(const std::string& in, size_t p, size_t e, long& out) {
+    bool neg = p < e && in[p] == '-';
+    if (neg) ++p;
+    if (p >= e || e - p > 18) return false;
+    long v = 0;
+    for (size_t i = p; i < e; ++i) {
+      if (in[i] < '0' || in[i] > '9') return false;
+      v = v * 10 + (in[i] - '0');
+    }
+    out = neg ? -v : v;
+    return true;
+  }
+
+  // parse one RESP array command (or inline command): 1 = a command in args, 0 = incomplete,
+  // -1 = protocol error (replied; the caller closes the connection)
+  int parse(Conn& c, std::vector<std::string>& args) {
     std::string& in = c.in;
-    if (in.empty()) return false;
+    if (in.empty()) return 0;
     if (in[0] != '*') {  // inline
       size_t e = in.find("\r\n");
-      if (e == std::string::npos) return false;
+      if (e == std::string::npos) {
+        if (in.size() > kMaxInline) { reply_err(c, "ERR Protocol error: too big inline request"); return -1; }
+        return 0;
+      }
+      if (e > kMaxInline) { reply_err(c, "ERR Protocol error: too big inline request"); return -1; }
       std::string line = in.substr(0, e);
       in.erase(0, e + 2);
       size_t a = 0;
@@ -91,25 +116,54 @@ struct KV {
         if (b > a) args.push_back(line.substr(a, b - a));
         a = b;
       }
-      return true;
+      return 1;
     }
     size_t p = in.find("\r\n");
-    if (p == std::string::npos) return false;
-    long n = atol(in.c_str() + 1);
+    if (p == std::string::npos) {
+      if (in.size() > kMaxInline) { reply_err(c, "ERR Protocol error: too big multibulk header"); return -1; }
+      return 0;
+    }
+    long n = 0;
+    if (!parse_long(in, 1, p, n) || n > kMaxArgs) {
+      reply_err(c, "ERR Protocol error: invalid multibulk length");
+      return -1;
+    }
     size_t pos = p + 2;
     std::vector<std::string> out;
     for (long i = 0; i < n; ++i) {
-      if (pos >= in.size() || in[pos] != '$') return false;
+      if (pos >= in.size()) return 0;
+      if (in[pos] != '$') {
+        reply_err(c, std::string("ERR Protocol error: expected '$', got '") + in[pos] + "'");
+        return -1;
+      }
       size_t q = in.find("\r\n", pos);
-      if (q == std::string::npos) return false;
-      long len = atol(in.c_str() + pos + 1);
-      if (in.size() < q + 2 + (size_t)len + 2) return false;
+      if (q == std::string::npos) {
+        if (in.size() - pos > kMaxInline) { reply_err(c, "ERR Protocol error: invalid bulk length"); return -1; }
+        return 0;
+      }
+      long len = 0;
+      if (!parse_long(in, pos + 1, q, len) || len < 0 || len > kMaxBulk) {
+        reply_err(c, "ERR Protocol error: invalid bulk length");
+        return -1;
+      }
+      if (in.size() < q + 2 + (size_t)len + 2) return 0;
+      if (in.compare(q + 2 + (size_t)len, 2, "\r\n") != 0) {
+        reply_err(c, "ERR Protocol error: bulk not terminated by CRLF");
+        return -1;
+      }
       out.push_back(in.substr(q + 2, (size_t)len));
       pos = q + 2 + (size_t)len + 2;
     }
     in.erase(0, pos);
     args.swap(out);
-    return true;
+    return 1;
+  }
+
+  // now + v units, or -1 when that overflows (Redis: "invalid expire time")
+  static int64_t expire_at(long long v, int64_t unit_ms) {
+    const int64_t t = now_ms();
+    if (v <= 0 || v > (INT64_MAX - t) / unit_ms) return -1;
+    return t + v * unit_ms;
   }
 
   static std::string upper(std::string s) {
@@ -143,9 +197,8 @@ struct KV {
       for (size_t i = 3; i < a.size(); ++i) {
         std::string o = upper(a[i]);
         if ((o == "EX" || o == "PX") && i + 1 < a.size()) {
-          long long v = atoll(a[++i].c_str());
-          if (v <= 0) { reply_err(c, "ERR invalid expire time in 'set' command"); return; }
-          exp = now_ms() + (o == "EX" ? v * 1000 : v);
+          exp = expire_at(atoll(a[++i].c_str()), o == "EX" ? 1000 : 1);
+          if (exp < 0) { reply_err(c, "ERR invalid expire time in 'set' command"); return; }
         } else if (o == "NX") nx = true;
         else if (o == "XX") xx = true;
         else { reply_err(c, "ERR syntax error"); return; }
@@ -168,7 +221,15 @@ struct KV {
     } else if (cmd == "EXPIRE" && a.size() == 3) {
       Entry* e = lookup(a[1]);
       if (!e) { reply_int(c, 0); return; }
-      e->expire_ms = now_ms() + atoll(a[2].c_str()) * 1000;
+      const long long v = atoll(a[2].c_str());
+      if (v <= 0) {  // Redis: a non-positive TTL deletes the key
+        erase(db.find(a[1]));
+        reply_int(c, 1);
+        return;
+      }
+      const int64_t at = expire_at(v, 1000);
+      if (at < 0) { reply_err(c, "ERR invalid expire time in 'expire' command"); return; }
+      e->expire_ms = at;
       reply_int(c, 1);
     } else if ((cmd == "TTL" || cmd == "PTTL") && a.size() == 2) {
       Entry* e = lookup(a[1]);
@@ -233,7 +294,10 @@ int main(int argc, char** argv) {
   if (!kv.loop.listen_on(host, port)) { perror("listen"); return 1; }
   kv.loop.on_data = [&](Conn& c) {
     std::vector<std::string> a;
-    while (kv.parse(c, a)) {
+    while (true) {
+      const int r = kv.parse(c, a);
+      if (r < 0) { c.in.clear(); kv.loop.close(c); break; }
+      if (r == 0) break;
       kv.exec(c, a);
       a.clear();
       if (c.closing) break;

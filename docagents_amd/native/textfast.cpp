@@ -32,7 +32,7 @@ long da_word_offsets(const char* s, long n, int64_t* words, long cap) {
 
 // Builds all chunk texts (words joined by one space) into `out` (capacity out_cap bytes) and
 // writes per chunk [byte_off, byte_len, token_count] into `meta` (3 int64 per chunk).
-// Returns the number of chunks, or -1 if out/meta are too small.
+// Returns the number of chunks, -1 if out/meta are too small, -2 on malformed word spans.
 long da_chunk(const char* s, const int64_t* words, long nw, long max_tokens, long overlap, char* out,
               long out_cap, int64_t* meta, long meta_cap) {
   if (max_tokens <= 0) max_tokens = 400;
@@ -42,12 +42,14 @@ long da_chunk(const char* s, const int64_t* words, long nw, long max_tokens, lon
   if (step <= 0) step = max_tokens;
   long nc = 0, o = 0;
   for (long start = 0; start < nw; start += step) {
-    long end = start + max_tokens < nw ? start + max_tokens : nw;
+    // (no start + max_tokens: it overflows for a huge max_tokens)
+    long end = max_tokens < nw - start ? start + max_tokens : nw;
     if (nc >= meta_cap) return -1;
     long off = o;
     for (long k = start; k < end; ++k) {
       long len = words[2 * k + 1] - words[2 * k];
-      if (o + len + 1 > out_cap) return -1;
+      if (len < 0 || words[2 * k] < 0) return -2;  // not spans from da_word_offsets
+      if (len > out_cap - o - 1) return -1;
       if (k > start) out[o++] = ' ';
       memcpy(out + o, s + words[2 * k], (size_t)len);
       o += len;

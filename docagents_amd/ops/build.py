@@ -25,6 +25,7 @@ from pathlib import Path
 HERE = Path(__file__).resolve().parent
 CSRC = HERE / "csrc"
 LIB = HERE / "_da_kernels.so"
+LIB_DEBUG = HERE / "_da_kernels_debug.so"  # -O1 -g -DDA_DEBUG: device asserts on (DA_KERNELS_DEBUG=1 loads it)
 ARCH = os.environ.get("DA_OFFLOAD_ARCH", "gfx950")
 
 
@@ -67,20 +68,21 @@ def build(force: bool = False, debug: bool = False, verbose: bool = False) -> Pa
     """Compile (if stale) and return the path of the shared library. ``LAST_BUILD`` records what
     happened: mode "compiled" (hipcc ran, with the wall time) or "reused" (fingerprint match)."""
     import time
-    stamp = HERE / "_da_kernels.fingerprint"
+    lib = LIB_DEBUG if debug else LIB
+    stamp = HERE / ("_da_kernels_debug.fingerprint" if debug else "_da_kernels.fingerprint")
     fp = _fingerprint(debug)
     LAST_BUILD.clear()
-    LAST_BUILD.update({"lib": str(LIB), "fingerprint": fp[:16], "arch": ARCH, "debug": debug})
-    if LIB.exists() and stamp.exists() and stamp.read_text() == fp and not force:
+    LAST_BUILD.update({"lib": str(lib), "fingerprint": fp[:16], "arch": ARCH, "debug": debug})
+    if lib.exists() and stamp.exists() and stamp.read_text() == fp and not force:
         LAST_BUILD["mode"] = "reused"
-        return LIB
+        return lib
     # N ranks of one job import the package at once: one builds, the others wait and reuse it
     import fcntl
     with open(HERE / "_da_kernels.lock", "w") as lk:
         fcntl.flock(lk, fcntl.LOCK_EX)
-        if LIB.exists() and stamp.exists() and stamp.read_text() == fp and not force:
+        if lib.exists() and stamp.exists() and stamp.read_text() == fp and not force:
             LAST_BUILD["mode"] = "reused"
-            return LIB
+            return lib
         t0 = time.perf_counter()
         out = _build_locked(stamp, fp, debug, verbose)
         LAST_BUILD.update({"mode": "compiled", "compile_s": round(time.perf_counter() - t0, 1),
@@ -90,7 +92,8 @@ def build(force: bool = False, debug: bool = False, verbose: bool = False) -> Pa
 
 def _build_locked(stamp: Path, fp: str, debug: bool, verbose: bool) -> Path:
     hipcc = _hipcc()
-    objdir = HERE / "_build"
+    lib = LIB_DEBUG if debug else LIB
+    objdir = HERE / ("_build_debug" if debug else "_build")
     objdir.mkdir(exist_ok=True)
     flags = _flags(debug)
 
@@ -107,7 +110,7 @@ def _build_locked(stamp: Path, fp: str, debug: bool, verbose: bool) -> Path:
     workers = min(len(_sources()), int(os.environ.get("MAX_JOBS", "8")), 16)
     with cf.ThreadPoolExecutor(max_workers=max(1, workers)) as ex:
         objs = list(ex.map(compile_one, _sources()))
-    tmp = LIB.with_suffix(f".so.tmp{os.getpid()}")
+    tmp = lib.with_suffix(f".so.tmp{os.getpid()}")
     cmd = [hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", *map(str, objs), "-o", str(tmp)]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
@@ -121,9 +124,9 @@ def _build_locked(stamp: Path, fp: str, debug: bool, verbose: bool) -> Path:
         if stubs:
             tmp.unlink(missing_ok=True)
             raise RuntimeError(f"undefined kernel launch stubs: {stubs[:4]}")
-    os.replace(tmp, LIB)
+    os.replace(tmp, lib)
     stamp.write_text(fp)
-    return LIB
+    return lib
 
 
 def main() -> None:

@@ -19,7 +19,10 @@ import torch
 
 _LIB = None
 _LOCK = threading.Lock()
-_LIB_PATH = Path(__file__).resolve().parent / "_da_kernels.so"
+# DA_KERNELS_DEBUG=1: the -DDA_DEBUG build (device asserts: bounds / shape preconditions inside the
+# kernels; python -m docagents_amd.ops.build --debug) instead of the -O3 library
+_DEBUG = os.environ.get("DA_KERNELS_DEBUG", "0") == "1"
+_LIB_PATH = Path(__file__).resolve().parent / ("_da_kernels_debug.so" if _DEBUG else "_da_kernels.so")
 
 EPI_NONE, EPI_BIAS, EPI_GELU, EPI_SWIGLU, EPI_RESID = 0, 1, 2, 3, 4
 EPI_ROPE = 6  # gemm8p only: QKV + RoPE + KV-cache write
@@ -117,7 +120,7 @@ def lib() -> ctypes.CDLL:
         if os.environ.get("DA_BUILD_ON_IMPORT", "1") == "1":
             try:
                 from .build import build
-                build()
+                build(debug=_DEBUG)
             except Exception as e:  # noqa: BLE001 - fall through to the explicit check below
                 if not _LIB_PATH.exists():
                     raise KernelLibraryMissing(f"cannot build {_LIB_PATH}: {e}") from e
