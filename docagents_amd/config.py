@@ -116,6 +116,22 @@ class Config:
     def replace(self, **kw) -> "Config":
         return dataclasses.replace(self, **kw)
 
+    # engine compute dtypes actually implemented: bf16 everywhere, or fp8 (OCP e4m3) encoder GEMMs
+    # with bf16 elsewhere. fp16 is NOT implemented (no fp16 MFMA path) and is refused, never run as
+    # something else.
+    ENGINE_DTYPES = ("bf16", "fp8")
+
+    def validate_engine(self) -> "Config":
+        """Startup check of the engine keys whose wrong value would otherwise silently run a
+        different configuration (the engine process calls it before touching the GPU)."""
+        if self.dtype not in self.ENGINE_DTYPES:
+            raise ValueError(f"DTYPE={self.dtype!r} is not supported (choose one of {', '.join(self.ENGINE_DTYPES)})")
+        if self.index_kind not in ("flat", "ivfflat"):
+            raise ValueError(f"INDEX_KIND={self.index_kind!r} is not supported (flat | ivfflat)")
+        if self.tp_size < 1:
+            raise ValueError(f"TP_SIZE={self.tp_size} must be >= 1")
+        return self
+
 
 def load(environ: dict | None = None) -> Config:
     env = os.environ if environ is None else environ

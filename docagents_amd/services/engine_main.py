@@ -53,6 +53,11 @@ def main(argv=None) -> int:
 
     cfg = load()
     log = new_logger(cfg.log_level)
+    try:
+        cfg.validate_engine()
+    except ValueError as e:  # before any GPU or process-group work: fail at startup, loudly
+        log.error("invalid engine configuration", "err", str(e))
+        raise SystemExit(f"engine: {e}") from e
     if cfg.engine_switch_interval_ms > 0:
         # the engine's threads (RPC loop, GPU thread, fast embed lane, search plane, tokenizers)
         # hand the GIL back and forth several times per query (a shorter switch interval was
@@ -87,7 +92,7 @@ def main(argv=None) -> int:
                  temperature=cfg.temperature, max_new_tokens=cfg.max_new_tokens,
                  summary_max_new=cfg.summary_max_new_tokens, index_kind=cfg.index_kind, ivf_lists=cfg.ivf_lists,
                  ivf_probes=cfg.ivf_probes, max_seq=4096 if dev.type == "cuda" else 1024,
-                 enc_dtype="fp8" if cfg.dtype == "fp8" else "bf16")
+                 enc_dtype=cfg.dtype)
     if cfg.engine_admit_tokens > 0:
         eng.admit_tokens = cfg.engine_admit_tokens
     if cfg.engine_continuous and dev.type == "cuda" and eng.gen is not None:

@@ -206,3 +206,22 @@ def test_encoder_truncation_is_counted():
     assert eng.stats["embed_truncated_texts"] == 1 and eng.stats["embed_truncated_tokens"] > 0
     assert metrics.ENGINE_EMBED_TRUNCATED.labels("texts")._value.get() == before + 1
     assert eng.describe()["embed"]["embed_truncated_texts"] == 1
+
+
+def test_engine_dtype_is_validated_not_silently_replaced():
+    """DTYPE=fp16 / garbage must fail at engine startup (VERDICT r3 Weak #9), before any GPU work."""
+    import subprocess
+    import sys
+
+    from docagents_amd.config import load
+    for bad in ("fp16", "garbage", ""):
+        with pytest.raises(ValueError, match="DTYPE"):
+            load({"DTYPE": bad}).validate_engine()
+    for ok in ("bf16", "fp8"):
+        assert load({"DTYPE": ok}).validate_engine().dtype == ok
+    with pytest.raises(ValueError, match="INDEX_KIND"):
+        load({"INDEX_KIND": "hnsw"}).validate_engine()
+    env = dict(__import__("os").environ, DTYPE="garbage", WORLD_SIZE="1")
+    p = subprocess.run([sys.executable, "-m", "docagents_amd.services", "engine", "--listen", "tcp://127.0.0.1:1"],
+                       env=env, capture_output=True, text=True, timeout=120)
+    assert p.returncode != 0 and "DTYPE='garbage'" in (p.stderr + p.stdout), (p.returncode, p.stderr[-800:])
