@@ -149,6 +149,12 @@ def main():
 
     info = init_from_env()
     W, R = info.world, info.rank
+    if any(k.startswith("DA_") for k in os.environ):  # A/B arms (bench/ab_arms.py): only when asked
+        sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "bench"))
+        from ab_arms import apply_env_overrides
+        ab = apply_env_overrides()
+        if ab:
+            log(info, f"A/B overrides: {ab}")
     dev = info.device
     if dev.type != "cuda":
         raise SystemExit("bench.py needs a GPU (run it through gpurun)")

@@ -9,7 +9,9 @@ lives here now, for comparisons only:
 * ``swiglu_interleaved``: the standalone SwiGLU pass the BLAS arm needs (the in-tree GEMM fuses it);
 * ``apply_env_overrides``: kernel-schedule overrides (decode-tile prefetch depth, flash prefill
   shape, GEMV blocking, decode-attention prefetch) read from ``DA_*`` environment variables and
-  pushed into the library's setters, so a sweep can flip one knob per process.
+  pushed into the library's setters, and the model's alternative code paths (fused prefill norms,
+  the persistent batch-1 decode), so a sweep can flip one knob per process. ``bench.py`` applies
+  them too (nothing happens without a ``DA_*`` variable set).
 """
 from __future__ import annotations
 
@@ -41,6 +43,11 @@ def apply_env_overrides() -> dict:
     """Push every DA_* schedule override present in the environment into the library."""
     L = K.lib()
     done = {}
+    from docagents_amd.models import llama
+    for env, attr in (("DA_PREFILL_NORM_FUSE", "_PREFILL_NORM_FUSE"), ("DA_DECODE_B1", "_DECODE_B1")):
+        if os.environ.get(env) is not None:  # model-level code paths (default: llama.py)
+            setattr(llama, attr, os.environ[env] == "1")
+            done[env] = int(getattr(llama, attr))
     if os.environ.get("DA_DECODE_DK") is not None:  # decode GEMMs: gemm_dk (1) vs split-K tiles (0)
         K.DECODE_DK = os.environ["DA_DECODE_DK"] != "0"
         done["DA_DECODE_DK"] = int(K.DECODE_DK)

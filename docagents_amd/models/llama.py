@@ -23,8 +23,6 @@ in-place all-reduce yields x + sum of partials.
 """
 from __future__ import annotations
 
-import os
-
 import numpy as np
 import torch
 
@@ -33,12 +31,15 @@ from ..ops.reference import interleave_gate_up, rope_table
 from .configs import DecoderConfig
 
 EPI_NONE, EPI_SWIGLU, EPI_RESID, EPI_ROPE = 0, 3, 4, 6
-# Prefill RMSNorms folded into the projections (_prefill_fused_norms); DA_PREFILL_NORM_FUSE=0/1
-# overrides the default (A/B measurements: profiles/r3/prefill_norm_fuse.txt)
-_PREFILL_NORM_FUSE = os.environ.get("DA_PREFILL_NORM_FUSE", "0") == "1"
+# Prefill RMSNorms folded into the projections (_prefill_fused_norms): measured a net loss, off
+# (profiles/r3/prefill_norm_fuse/); bench/ab_arms.py flips it for A/B runs (DA_PREFILL_NORM_FUSE=1)
+_PREFILL_NORM_FUSE = False
 # Decode step of MHA models: RoPE + KV-cache write folded into the attention kernel (False: separate
 # rope_cache launch; the GPU tests compare both).
 _FUSED_ROPE_DECODE = True
+# Batch-1 decode as ONE persistent launch over all layers + the LM head (ops/csrc/decode_b1.hip);
+# bench/ab_arms.py selects the per-kernel path (5 launches per layer) for A/B runs (DA_DECODE_B1=0)
+_DECODE_B1 = True
 
 
 class TPContext:
@@ -366,6 +367,8 @@ class LlamaDecoder:
         c, o, cache = self.cfg, self.ops, self.cache
         D, hl, kl = c.head_dim, self.hl, self.kl
         x = o.embed(st.tokens, self.w["embed"], out=st.x)
+        if self._b1_decode(x.shape[0]):
+            return self._decode_step_b1(st, x)
         if self._dk_decode(x.shape[0]):
             return self._decode_step_dk(st, x)
         if self._norm_fusable(x.shape[0]):
@@ -400,6 +403,43 @@ class LlamaDecoder:
         o.rope_cache(qkv, st.pos, self.cos_sin, hl, kl, D, slot=st.slot, k_cache=cache.k(li), v_cache=cache.v(li))
         return o.decode_attn(qkv, cache.k(li), cache.v(li), st.lens, st.slot, hl, kl, D, max_len=cache.max_seq,
                              out=st.attn, pre=st.pre)
+
+    def _b1_decode(self, B: int) -> bool:
+        """Batch 1, one rank, MHA (the fused-RoPE attention), folded norm gains: the persistent
+        launch (every layer + the LM head; decode_b1.hip)."""
+        c, o = self.cfg, self.ops
+        return (_DECODE_B1 and B == 1 and self.tp.size == 1 and self.unit_gains and self.hl == self.kl
+                and _FUSED_ROPE_DECODE and hasattr(o, "decode_b1") and c.head_dim in (64, 96, 128)
+                and c.hidden % 512 == 0 and c.ffn % 512 == 0 and c.vocab % 16 == 0
+                and self.hl * c.head_dim == c.hidden and self.cache is not None)
+
+    def _b1_table(self) -> torch.Tensor:
+        """int64 [layers, 6] device table of the per-layer pointers the persistent launch reads
+        (weights never move; rebuilt if the KV cache is re-allocated)."""
+        cache = self.cache
+        key = cache.buf.data_ptr()
+        t = getattr(self, "_b1_ptrs", None)
+        if t is None or self._b1_key != key:
+            rows = [[L["wqkv"].data_ptr(), L["wo"].data_ptr(), L["w_gu"].data_ptr(), L["w_down"].data_ptr(),
+                     cache.k(li).data_ptr(), cache.v(li).data_ptr()] for li, L in enumerate(self.w["layers"])]
+            for L in self.w["layers"]:
+                for k in ("wqkv", "wo", "w_gu", "w_down"):
+                    if not L[k].is_contiguous():
+                        raise ValueError(f"decode_b1: {k} must be contiguous")
+            self._b1_ptrs = torch.tensor(rows, dtype=torch.int64, device=self.device)
+            self._b1_key = key
+        return self._b1_ptrs
+
+    def _decode_step_b1(self, st: "DecodeState", x: torch.Tensor) -> torch.Tensor:
+        """The whole batch-1 step in 3 launches: embedding, the persistent layers + LM head, the
+        sampler (was 5 per layer + 3)."""
+        c, o, cache = self.cfg, self.ops, self.cache
+        o.decode_b1(self._b1_table(), 0, c.layers, st.x.view(-1), st.qkv.view(-1), st.attn.view(-1), st.act.view(-1),
+                    st.lens, st.slot, st.pre, st.pos, self.cos_sin, self.hl, c.head_dim, c.ffn, cache.max_seq, c.eps,
+                    lm_head=self.w["lm_head"], logits=st.logits.view(-1))
+        o.sample(st.logits, st.temperature, st.seed, 0, out_tok=st.tokens, out_lp=st.lp, conf=st.conf,
+                 active=st.active, ctr=st.pos, pos=st.pos, lens=st.lens, hist=st.hist, start=st.start, eos=st.eos)
+        return st.tokens
 
     def _norm_fusable(self, B: int) -> bool:
         """Batched decode (1 < B <= 64, no TP): every RMSNorm rides on the split-K reduction of the
@@ -517,6 +557,7 @@ class DecodeState:
         self.h = torch.zeros(B, h, dtype=torch.bfloat16, device=dev)
         self.qkv = torch.zeros(B, (model.hl + 2 * model.kl) * c.head_dim, dtype=torch.bfloat16, device=dev)
         self.attn = torch.zeros(B, model.hl * c.head_dim, dtype=torch.bfloat16, device=dev)
+        self.act = torch.zeros(B, c.ffn, dtype=torch.bfloat16, device=dev)  # SwiGLU output (persistent batch-1 path)
         self.logits = torch.zeros(B, c.vocab // model.tp.size, dtype=torch.bfloat16, device=dev)  # this rank's slice
         # gemm_dk deferred-norm partial sums [parts, 64] (a tuple: shared as-is by row views)
         self.ssq = tuple(torch.zeros(512 * 64, dtype=torch.float32, device=dev) for _ in range(2))

@@ -115,16 +115,18 @@ DA_EXPORT int da_stream_probe(const void* src, long long per_wg, int nwg, int mo
 }
 
 // ------------------------------------------------------------------------------------------
-// A bounded device-side delay: one wave sleeping `iters` x s_sleep(127) (~8k cycles each). Tests
-// use it to hold a stream busy deterministically (a writer's copies queued behind it) so that a
-// reader on another stream provably overlaps the writer's pending work (index write/search race).
-__global__ void spin_kernel(int iters, int* out) {
-  for (int i = 0; i < iters; ++i) __builtin_amdgcn_s_sleep(127);
-  if (threadIdx.x == 0 && out) out[0] = iters;
+// A bounded device-side delay: one wave polling the 100 MHz wall clock (s_memrealtime) for `us`
+// microseconds. Tests use it to hold a stream busy deterministically (a writer's copies queued
+// behind it) so that a reader on another stream provably overlaps the writer's pending work (index
+// write/search race). Bounded to 10 s.
+__global__ void spin_kernel(long long ticks, int* out) {
+  const long long t0 = wall_clock64();
+  while (wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(8);
+  if (threadIdx.x == 0 && out) out[0] = 1;
 }
 
-DA_EXPORT int da_spin(int iters, void* out, void* stream) {
-  if (iters < 0 || iters > (1 << 20)) return (int)hipErrorInvalidValue;
-  spin_kernel<<<1, 64, 0, (hipStream_t)stream>>>(iters, (int*)out);
+DA_EXPORT int da_spin(int us, void* out, void* stream) {
+  if (us < 0 || us > 10000000) return (int)hipErrorInvalidValue;
+  spin_kernel<<<1, 64, 0, (hipStream_t)stream>>>((long long)us * 100, (int*)out);
   DA_LAUNCH_CHECK();
 }

@@ -98,6 +98,9 @@ _SIGS = {
     "da_device_cu_count": [c_int, ctypes.POINTER(c_int)],
     "da_placement_probe": [c_void_p, c_int, c_longlong, c_void_p],
     "da_spin": [c_int, c_void_p, c_void_p],
+    "da_decode_b1": [c_void_p, c_int, c_int] + [c_void_p] * 4 + [c_void_p] * 5 + [c_int] * 7 + [c_float, c_float]
+                    + [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p],
+    "da_decode_b1_occupancy": [c_int, ctypes.POINTER(c_int)],
 }
 
 
@@ -134,6 +137,8 @@ def lib() -> ctypes.CDLL:
             fn.restype = c_int
         L.da_topk_dense_ws.argtypes = [c_int, c_int, c_int, c_int]
         L.da_topk_dense_ws.restype = c_size_t
+        L.da_decode_b1_sync_bytes.argtypes = [c_int]
+        L.da_decode_b1_sync_bytes.restype = c_longlong
         _LIB = L
         return L
 
@@ -910,8 +915,93 @@ def reserve_workspace(nbytes: int, device=None) -> None:
     _workspace(nbytes, dev)
 
 
-def spin(iters: int, device=None) -> None:
-    """Hold the current stream busy for ~``iters`` x 3.4 us (one wave of s_sleep; bounded to 2^20
-    iterations). Test helper: work queued behind it on this stream is provably still pending."""
-    _req(0 <= iters <= (1 << 20), "spin: 0 <= iters <= 2^20")
-    _check(lib().da_spin(int(iters), None, _stream()), "da_spin")
+def spin(us: int, device=None) -> None:
+    """Hold the current stream busy for ``us`` microseconds (one wave polling the wall clock;
+    bounded to 10 s). Test helper: work queued behind it on this stream is provably still pending."""
+    _req(0 <= us <= 10_000_000, "spin: 0 <= us <= 1e7")
+    _check(lib().da_spin(int(us), None, _stream()), "da_spin")
+
+
+# ----------------------------------------------------------------------------------- batch-1 decode
+_B1_BUFS: dict = {}
+
+
+def _stream_cus(device) -> int:
+    """CUs the current stream may dispatch to (a CU-masked serving lane has fewer than the chip)."""
+    n = torch.cuda.get_device_properties(device).multi_processor_count
+    words = (n + 31) // 32
+    mask = (c_uint * words)()
+    if lib().da_stream_get_cumask(_stream(), words, mask) == 0:
+        bits = sum(bin(int(m)).count("1") for m in mask)
+        if 0 < bits <= n:
+            return bits
+    return n
+
+
+def decode_b1_grid(D: int, device) -> int:
+    """Workgroups of the persistent batch-1 decode launch: every one must be resident at once (they
+    wait on each other), so (CUs of the current stream) x (resident workgroups per CU)."""
+    occ = c_int(0)
+    _check(lib().da_decode_b1_occupancy(D, ctypes.byref(occ)), "decode_b1_occupancy")
+    _req(occ.value >= 1, "decode_b1: kernel does not fit on a CU")
+    return _stream_cus(device) * occ.value
+
+
+def decode_b1(layers, l0: int, l1: int, x, qkv, attn, act, lens, slot, pre, pos, cos_sin, H: int, D: int, F: int,
+              max_seq: int, eps: float, lm_head=None, logits=None, max_len: int | None = None, scale=None):
+    """Batch-1 decode of layers [l0, l1) as ONE persistent launch (ops/csrc/decode_b1.hip), plus the
+    LM head when ``lm_head`` is given (logits [1, V]). ``layers``: int64 device tensor [L, 6] of the
+    per-layer pointers (wqkv, wo, w_gu, w_down, k cache, v cache). x / qkv / attn / act: the decode
+    state's row buffers (x in: the token's embedding; out: the residual stream after the last
+    layer). Same split count as ``decode_attn`` at this capacity, same bits as the per-kernel path."""
+    dev = x.device
+    Hd = H * D
+    for t, n, nm in ((x, Hd, "x"), (qkv, 3 * Hd, "qkv"), (attn, Hd, "attn"), (act, F, "act")):
+        _bf16_cuda(t, nm)
+        _req(t.is_contiguous() and t.numel() == n, f"decode_b1: {nm} must be contiguous with {n} elements")
+    _i32(lens, "lens"); _i32(slot, "slot"); _i32(pos, "pos")
+    _req(lens.numel() == 1 and slot.numel() == 1 and pos.numel() == 1, "decode_b1: batch 1")
+    if pre is not None:
+        _i32(pre, "pre"); _req(pre.numel() == 2, "pre must be int32 [1, 2]")
+    _req(layers.dtype == torch.int64 and layers.is_cuda and layers.dim() == 2 and layers.shape[1] == 6
+         and 0 <= l0 < l1 <= layers.shape[0], "decode_b1: layer table")
+    _req(cos_sin.dtype == torch.float32 and cos_sin.is_contiguous() and cos_sin.shape[1] == D // 2, "cos_sin")
+    _req(Hd % 512 == 0 and F % 512 == 0 and D in (64, 96, 128), "decode_b1 shapes")
+    max_len = max_seq if max_len is None else max_len
+    want = max_len * Hd // D / 768  # decode_attn's auto chunk for B = 1
+    chunk = 512
+    while chunk < want and chunk < 4096:
+        chunk *= 2
+    nsplit = max(1, math.ceil(max_len / chunk))
+    V = 0
+    if lm_head is not None:
+        _bf16_cuda(lm_head, "lm_head")
+        V = lm_head.shape[0]
+        _req(lm_head.shape[1] == Hd and lm_head.is_contiguous() and V % 16 == 0, "lm_head")
+        _req(logits is not None and logits.numel() == V and logits.is_contiguous(), "logits")
+        _bf16_cuda(logits, "logits")
+    key = (dev.index, H, D, nsplit)
+    bufs = _B1_BUFS.get(key)
+    if bufs is None:  # kept for the process: a captured graph points at them
+        sb = int(lib().da_decode_b1_sync_bytes(H))
+        bufs = (torch.zeros(H * nsplit * (D + 2), dtype=torch.float32, device=dev),
+                torch.zeros((sb + 15) // 16 * 4, dtype=torch.int32, device=dev), decode_b1_grid(D, dev))
+        _B1_BUFS[key] = bufs
+    ws, sync, grid = bufs
+    scale = scale if scale is not None else 1.0 / math.sqrt(D)
+    _check(lib().da_decode_b1(_ptr(layers), l0, l1, _ptr(x), _ptr(qkv), _ptr(attn), _ptr(act), _ptr(lens), _ptr(slot),
+                              _ptr(pre), _ptr(pos), _ptr(cos_sin), Hd, H, D, F, max_seq, nsplit, chunk, float(eps),
+                              float(scale), _ptr(ws), _ptr(sync), _ptr(lm_head), _ptr(logits), V, grid, _stream()),
+           "decode_b1")
+
+
+def decode_b1_error(device=None) -> int:
+    """The persistent decode's error word of the last launch on ``device`` (0 = ok; else the code
+    of the wait that timed out). Reads device memory: synchronises."""
+    dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+    for (idx, *_), (_, sync, _) in _B1_BUFS.items():
+        if idx == dev.index:
+            v = int(sync[0].item())
+            if v:
+                return v
+    return 0

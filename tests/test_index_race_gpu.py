@@ -19,7 +19,7 @@ from docagents_amd.index.flat import FlatIndex  # noqa: E402
 from docagents_amd.index.ivf import IVFFlatIndex  # noqa: E402
 from docagents_amd.ops import kernels as K  # noqa: E402
 
-SPIN = 60000  # ~200 ms of one sleeping wave
+SPIN = 300_000  # 300 ms of one wave polling the wall clock
 
 
 def _unit(n, d, seed):
