@@ -48,6 +48,10 @@ def apply_env_overrides() -> dict:
         if os.environ.get(env) is not None:  # model-level code paths (default: llama.py)
             setattr(llama, attr, os.environ[env] == "1")
             done[env] = int(getattr(llama, attr))
+    if os.environ.get("DA_SPLITK_FUSED") is not None:  # 33..64-row decode: in-kernel split-K reduce
+        from docagents_amd.ops import reference as R
+        K.SPLITK_FUSED = R.SPLITK_FUSED = os.environ["DA_SPLITK_FUSED"] != "0"
+        done["DA_SPLITK_FUSED"] = int(K.SPLITK_FUSED)
     if os.environ.get("DA_DECODE_DK") is not None:  # decode GEMMs: gemm_dk (1) vs split-K tiles (0)
         K.DECODE_DK = os.environ["DA_DECODE_DK"] != "0"
         done["DA_DECODE_DK"] = int(K.DECODE_DK)

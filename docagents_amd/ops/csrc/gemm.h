@@ -10,6 +10,8 @@ enum Epi : int {
   EPI_RESID = 4,      // bias (optional) + residual add
   EPI_PARTIAL = 5,    // fp32 split-K partial to workspace
   EPI_ROPE = 6,       // QKV projection: RoPE (interleaved pairs) on q / k, k / v written to the KV cache
+  EPI_SPLITK = 7,     // decode tiles: split-K partials reduced IN the kernel by the tile's last split
+                      // (fuse_epi = the real epilogue; ssq_in / ssq_out as gemm_splitk_reduce)
 };
 
 // EPI_ROPE operands: output columns [H q heads | Hkv k heads | Hkv v heads] of D; token row m goes to
@@ -34,6 +36,9 @@ struct GemmArgs {
   //            ([M][N / 64] floats) — the next consumer's ssq_in
   const float* ssq_in; int ssq_parts; int norm_k; float norm_eps;
   float* ssq_out;
+  // EPI_SPLITK: per-tile arrival counters (zero before the launch, left zero after it) and the
+  // epilogue the last split applies (NONE / BIAS / SWIGLU / RESID)
+  int* cnt; int fuse_epi;
 };
 
 // 256x256 fp8 tile (gemm256.hip): A and W hold OCP e4m3 bytes (lda / K in elements = bytes),

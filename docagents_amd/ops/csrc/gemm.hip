@@ -15,6 +15,143 @@
 //  * split-K writes fp32 partials; gemm_splitk_reduce applies the same epilogue.
 #include "gemm.h"
 
+// ------------------------------------------------------------------------------------------
+// In-kernel split-K reduction for the decode tiles (33..64 rows): no reduce launch. Every split
+// writes its fp32 partial tile write-through (sc1: the tile's other splits run on other CUs /
+// XCDs, whose L2s are not coherent with this one), drains, and takes a ticket on the tile's
+// arrival counter; the LAST split of the tile sums every split's partial in split order (sc1
+// loads: the same fixed order as gemm_splitk_reduce, so results do not depend on arrival order)
+// and applies the epilogue: the deferred RMSNorm row scale (ssq_in), bias, SwiGLU (16-column
+// interleave) or residual (+ per-row sums of squares of the new rows over this tile's columns,
+// ssq_out [N / BN][64]: the next consumer's norm). It then zeroes the counter for the next launch
+// (cdna_hip_programming.md §6 Guideline 16 hand-off; MI355X_MICROARCH.md splitk-seam).
+__device__ __forceinline__ void st16_sc1(__amdgpu_buffer_rsrc_t r, unsigned off, const float* v) {
+  const u32x4_t x = {__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]), __float_as_uint(v[3])};
+  __builtin_amdgcn_raw_buffer_store_b128(x, r, off, 0, 16);
+}
+__device__ __forceinline__ f32x4_t ld16f_sc1(__amdgpu_buffer_rsrc_t r, unsigned off) {
+  const u32x4_t x = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 16);
+  return f32x4_t{__uint_as_float(x[0]), __uint_as_float(x[1]), __uint_as_float(x[2]), __uint_as_float(x[3])};
+}
+
+template <int TM, int TN, int SLD>
+__device__ __forceinline__ void splitk_fused_epilogue(const GemmArgs& p, const float* st, int row0, int col0,
+                                                      int tile_id, int tn, int lane, int wid) {
+  const int S = gridDim.z, z = blockIdx.z, M = p.M, N = p.N;
+  const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)p.ws, (short)0, (int)min((size_t)S * M * N * 4, (size_t)0x7ffffff0), 0x00020000);
+  constexpr int CPR = TN / 8, RPI = 64 / CPR;
+  {
+    const int cc = (lane % CPR) * 8, gn = col0 + cc;
+    for (int rr = lane / CPR; rr < TM; rr += RPI) {
+      const int gm = row0 + rr;
+      if (gm >= M || gn >= N) continue;
+      const unsigned off = (unsigned)((((size_t)z * M + gm) * N + gn) * 4);
+      st16_sc1(rw, off, st + rr * SLD + cc);
+      st16_sc1(rw, off + 16, st + rr * SLD + cc + 4);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  __shared__ int s_last;
+  if (threadIdx.x == 0) {
+    const int t = __hip_atomic_fetch_add(p.cnt + tile_id, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_last = t == S - 1;
+    if (s_last) __hip_atomic_store(p.cnt + tile_id, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  if (!s_last) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // the partial loads stay below the ticket
+  const int epi = p.fuse_epi;
+  auto row_scale = [&](int gm) -> float {
+    if (!p.ssq_in) return 1.f;
+    float ss = 0.f;
+    for (int q = 0; q < p.ssq_parts; ++q) ss += p.ssq_in[q * 64 + gm];
+    return rsqrtf(ss / p.norm_k + p.norm_eps);
+  };
+  if (epi == EPI_SWIGLU) {
+    // this wave's TN columns = TN / 32 (gate 16 | up 16) groups -> TN / 2 outputs per row
+    constexpr int OCPR = TN / 16, ORPI = 64 / OCPR;
+    const int oc = (lane % OCPR) * 8, grp = oc / 16, within = oc % 16;
+    const int gc = col0 + grp * 32 + within, gout = col0 / 2 + oc;
+    for (int rr = lane / OCPR; rr < TM; rr += ORPI) {
+      const int gm = row0 + rr;
+      if (gm >= M || gout >= N / 2) continue;
+      float g[8], u[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) { g[e] = 0.f; u[e] = 0.f; }
+      for (int sp = 0; sp < S; ++sp) {
+        const unsigned off = (unsigned)((((size_t)sp * M + gm) * N + gc) * 4);
+        const f32x4_t g0 = ld16f_sc1(rw, off), g1 = ld16f_sc1(rw, off + 16);
+        const f32x4_t u0 = ld16f_sc1(rw, off + 64), u1 = ld16f_sc1(rw, off + 80);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) { g[e] += g0[e]; g[4 + e] += g1[e]; u[e] += u0[e]; u[4 + e] += u1[e]; }
+      }
+      const float inv = row_scale(gm);
+      unsigned pk[4];
+#pragma unroll
+      for (int e = 0; e < 8; e += 2)
+        pk[e / 2] = pack_bf2(silu(g[e] * inv) * (u[e] * inv), silu(g[e + 1] * inv) * (u[e + 1] * inv));
+      *(u32x4_t*)(p.C + (size_t)gm * p.ldc + gout) = u32x4_t{pk[0], pk[1], pk[2], pk[3]};
+    }
+    return;
+  }
+  __shared__ float ssq_w[4][64];
+  const int cc = (lane % CPR) * 8, gn = col0 + cc;
+  for (int rr = lane / CPR; rr < TM; rr += RPI) {
+    const int gm = row0 + rr;
+    float sq = 0.f;
+    if (gm < M && gn < N) {
+      float v[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = 0.f;
+      for (int sp = 0; sp < S; ++sp) {
+        const unsigned off = (unsigned)((((size_t)sp * M + gm) * N + gn) * 4);
+        const f32x4_t a = ld16f_sc1(rw, off), b = ld16f_sc1(rw, off + 16);
+        v[0] += a[0]; v[1] += a[1]; v[2] += a[2]; v[3] += a[3];
+        v[4] += b[0]; v[5] += b[1]; v[6] += b[2]; v[7] += b[3];
+      }
+      const float inv = row_scale(gm);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] *= inv;
+      if (p.bias) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] += bf2f(p.bias[gn + e]);
+      }
+      if (epi == EPI_RESID) {
+        const u32x4_t r = *(const u32x4_t*)(p.resid + (size_t)gm * p.ldr + gn);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          v[2 * e] += bf2f((bf16_t)(r[e] & 0xffff));
+          v[2 * e + 1] += bf2f((bf16_t)(r[e] >> 16));
+        }
+      }
+      const u32x4_t o = {pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3]), pack_bf2(v[4], v[5]), pack_bf2(v[6], v[7])};
+      *(u32x4_t*)(p.C + (size_t)gm * p.ldc + gn) = o;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {  // what the stream now holds (bf16)
+        const float lo = bf2f((bf16_t)(o[e] & 0xffff)), hi = bf2f((bf16_t)(o[e] >> 16));
+        sq += lo * lo + hi * hi;
+      }
+    }
+    if (p.ssq_out) {  // the row's CPR chunks sit in CPR adjacent lanes
+#pragma unroll
+      for (int o = 1; o < CPR; o <<= 1) sq += __shfl_xor(sq, o, 64);
+      if (lane % CPR == 0) ssq_w[wid][rr] = sq;
+    }
+  }
+  if (p.ssq_out) {
+    __syncthreads();
+    const int t = threadIdx.x;
+    if (t < TM && row0 + t < M) {
+      float ss = 0.f;
+#pragma unroll
+      for (int w = 0; w < 4; ++w) ss += ssq_w[w][t];
+      p.ssq_out[(size_t)tn * 64 + row0 + t] = ss;
+    }
+  }
+}
+
 template <int BM, int BN, int WM, int WN, int EPI, int PF = 1, bool DB = false>
 __global__ void __launch_bounds__(256)
 gemm_bf16_kernel(GemmArgs p) {
@@ -192,6 +329,10 @@ gemm_bf16_kernel(GemmArgs p) {
   __syncthreads();
 
   const int row0 = m0 + wm * TM, col0 = n0 + wn * TN;
+  if constexpr (EPI == EPI_SPLITK) {
+    splitk_fused_epilogue<TM, TN, SLD>(p, st, row0, col0, tm * ntn + tn, tn, lane, wid);
+    return;
+  }
   if constexpr (EPI == EPI_SWIGLU) {
     // output tile TM x TN/2; chunk of 8 outputs; TN/16 chunks per row
     constexpr int CPR = TN / 16;
@@ -510,13 +651,19 @@ template <int BM, int BN, int WM, int WN, int PF = 1, bool DB = false>
 static int launch_tile(const GemmArgs& a, int epi, int splits, hipStream_t s) {
   const int ntm = (a.M + BM - 1) / BM, ntn = (a.N + BN - 1) / BN;
   dim3 grid(ntm * ntn, 1, splits), block(256);
-  switch (splits > 1 ? (int)EPI_PARTIAL : epi) {
+  switch (splits > 1 && epi != EPI_SPLITK ? (int)EPI_PARTIAL : epi) {
     case EPI_NONE: gemm_bf16_kernel<BM, BN, WM, WN, EPI_NONE, PF, DB><<<grid, block, 0, s>>>(a); break;
     case EPI_BIAS: gemm_bf16_kernel<BM, BN, WM, WN, EPI_BIAS, PF, DB><<<grid, block, 0, s>>>(a); break;
     case EPI_GELU: gemm_bf16_kernel<BM, BN, WM, WN, EPI_GELU, PF, DB><<<grid, block, 0, s>>>(a); break;
     case EPI_SWIGLU: gemm_bf16_kernel<BM, BN, WM, WN, EPI_SWIGLU, PF, DB><<<grid, block, 0, s>>>(a); break;
     case EPI_RESID: gemm_bf16_kernel<BM, BN, WM, WN, EPI_RESID, PF, DB><<<grid, block, 0, s>>>(a); break;
     case EPI_PARTIAL: gemm_bf16_kernel<BM, BN, WM, WN, EPI_PARTIAL, PF, DB><<<grid, block, 0, s>>>(a); break;
+    case EPI_SPLITK:
+      if constexpr (BM == 64 && WM == 1 && WN == 4) {
+        gemm_bf16_kernel<BM, BN, WM, WN, EPI_SPLITK, PF, DB><<<grid, block, 0, s>>>(a);
+        break;
+      }
+      return (int)hipErrorInvalidValue;
     default: return (int)hipErrorInvalidValue;
   }
   return (int)hipGetLastError();
@@ -701,6 +848,30 @@ DA_EXPORT int da_gemm_dk_splitk(const void* A, int lda, const void* W, void* C, 
                                              (const bf16_t*)resid, ldr, (bf16_t*)C, ldc, ssq_in, ssq_parts, norm_k,
                                              eps);
   DA_LAUNCH_CHECK();
+}
+
+// The same contract with the split-K reduction done by each tile's last split inside the tile
+// kernel (EPI_SPLITK): ONE launch, no reduce kernels. ssq_out is then [N / 128][64] (one part per
+// 128-column tile: dk_parts on this route). cnt: int32 [ceil(M/64) * N/128] zeros, left zero.
+DA_EXPORT int da_gemm_dk_splitk_fused(const void* A, int lda, const void* W, void* C, int ldc, const void* bias,
+                                      const void* resid, int ldr, int M, int N, int K, int epi, const float* ssq_in,
+                                      int ssq_parts, int norm_k, float eps, float* ssq_out, void* ws, int splits,
+                                      int* cnt, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  if (M < 1 || M > 64 || K % 64 || N % 128 || lda % 8 || ldc % 8 || !ws || !cnt || splits < 2 || (K / 64) % splits)
+    return (int)hipErrorInvalidValue;
+  if (epi == EPI_RESID && (!resid || ldr % 8 || ssq_in)) return (int)hipErrorInvalidValue;
+  if (ssq_out && epi != EPI_RESID) return (int)hipErrorInvalidValue;
+  if (ssq_in && (ssq_parts < 1 || norm_k < 1 || !(eps > 0.f))) return (int)hipErrorInvalidValue;
+  if (epi != EPI_NONE && epi != EPI_BIAS && epi != EPI_SWIGLU && epi != EPI_RESID) return (int)hipErrorInvalidValue;
+  if ((size_t)splits * M * N * 4 > (size_t)0x7ffffff0) return (int)hipErrorInvalidValue;
+  GemmArgs a{};
+  a.A = (const bf16_t*)A; a.W = (const bf16_t*)W; a.C = (bf16_t*)C;
+  a.bias = (const bf16_t*)bias; a.resid = (const bf16_t*)resid; a.ws = (float*)ws;
+  a.M = M; a.N = N; a.K = K; a.lda = lda; a.ldc = ldc; a.ldr = ldr; a.k_per_split = K / splits;
+  a.ssq_in = ssq_in; a.ssq_parts = ssq_parts; a.norm_k = norm_k; a.norm_eps = eps; a.ssq_out = ssq_out;
+  a.cnt = cnt; a.fuse_epi = epi;
+  return launch_decode_tile<64, 128>(a, EPI_SPLITK, splits, s);
 }
 
 // Prefill QKV projection with RoPE + KV-cache write fused into the epilogue (gemm8p EPI_ROPE);

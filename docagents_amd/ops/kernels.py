@@ -71,6 +71,9 @@ _SIGS = {
     "da_gemm_dk": [c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
                    c_int, c_void_p, c_int, c_int, c_float, c_void_p, c_void_p],
     "da_gemm_dk_parts": [c_int],
+    "da_gemm_dk_splitk_fused": [c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_int, c_int,
+                                c_int, c_int, c_void_p, c_int, c_int, c_float, c_void_p, c_void_p, c_int, c_void_p,
+                                c_void_p],
     "da_gemm_dk_splitk": [c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
                           c_int, c_void_p, c_int, c_int, c_float, c_void_p, c_void_p, c_int, c_void_p],
     "da_set_dk_rb": [c_int],
@@ -285,6 +288,22 @@ def _dk_splitk(M: int, N: int) -> bool:
     return DK_SPLITK_ABOVE < M <= 64 and N % 512 == 0
 
 
+# 33..64 rows: the split-K reduction runs inside the tile kernel (last split of each tile, EPI_SPLITK)
+# instead of separate reduce launches; 0 = the two-launch form (A/B: bench/ab_arms.py DA_SPLITK_FUSED)
+SPLITK_FUSED = True
+_SPLITK_CNT: dict = {}
+
+
+def _splitk_cnt(device) -> torch.Tensor:
+    """Per-(device, workspace role) tile arrival counters of the fused split-K tiles: zero, left zero
+    by every launch (the last split of a tile resets its counter); never freed (graphs keep it)."""
+    key = (device.index if device.index is not None else torch.cuda.current_device(), getattr(_ROLE, "name", "main"))
+    c = _SPLITK_CNT.get(key)
+    if c is None:
+        c = _SPLITK_CNT[key] = torch.zeros(4096, dtype=torch.int32, device=device)
+    return c
+
+
 def _dk_splits(N: int, K: int) -> int:
     """Split-K of the 33..64-row route (64x128 tiles): the largest of 2, 3, 4, 6, 8, 12, 16 that keeps
     the grid within one round of 256 workgroups and >= 4 K-steps of 64 per split; at least 2 (the
@@ -302,7 +321,7 @@ def dk_parts(N: int, M: int = 0) -> int:
     """Row-norm partial sums an EPI_RESID gemm_dk of width N and M rows writes (the consumer's part
     count): one per dk output tile, or one per 512 columns on the 33..64-row split-K route."""
     if _dk_splitk(M, N):
-        return N // 512
+        return N // 128 if SPLITK_FUSED else N // 512
     return int(lib().da_gemm_dk_parts(N))
 
 
@@ -336,6 +355,13 @@ def gemm_dk(a, w, epi: int = EPI_NONE, bias=None, resid=None, out=None, norm_in=
     if _dk_splitk(M, N) or (DK_SPLITK_ABOVE < M <= 64 and ssq_out is None):
         splits = _dk_splits(N, K)
         ws = _workspace(splits * M * N * 4, a.device)
+        if SPLITK_FUSED and N % 128 == 0:
+            _req((N // 128) <= 4096, "fused split-K: too many tiles")
+            _check(lib().da_gemm_dk_splitk_fused(_ptr(a), a.stride(0), _ptr(w), _ptr(out), out.stride(0), _ptr(bias),
+                                                 _ptr(resid), ldr, M, N, K, epi, _ptr(ssq), parts, K, float(eps),
+                                                 _ptr(ssq_out), _ptr(ws), splits, _ptr(_splitk_cnt(a.device)),
+                                                 _stream()), "gemm_dk_splitk_fused")
+            return out
         _check(lib().da_gemm_dk_splitk(_ptr(a), a.stride(0), _ptr(w), _ptr(out), out.stride(0), _ptr(bias), _ptr(resid),
                                        ldr, M, N, K, epi, _ptr(ssq), parts, K, float(eps), _ptr(ssq_out), _ptr(ws),
                                        splits, _stream()), "gemm_dk_splitk")

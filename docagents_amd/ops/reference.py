@@ -481,11 +481,15 @@ def dk_fusable(M, N, K, epi=EPI_NONE):
             and epi in (EPI_NONE, EPI_BIAS, EPI_RESID, EPI_SWIGLU) and (epi != EPI_SWIGLU or N % 32 == 0))
 
 
+SPLITK_FUSED = True  # mirrors kernels.SPLITK_FUSED (bench/ab_arms.py flips both)
+
+
 def dk_parts(N, M=0):
     """gemm_dk.hip dk_bn for EPI_RESID: row-norm partial sums written per output tile; 33..64 rows
-    (the split-K route, gemm.hip splitk_reduce_resid_ssq): one per 512 columns."""
+    (the split-K route): one per 128-column tile when the reduction runs in the tile kernel
+    (gemm.hip splitk_fused_epilogue), one per 512 columns with the reduce launch."""
     if DK_SPLITK_ABOVE < M <= 64 and N % 512 == 0:
-        return N // 512
+        return N // 128 if SPLITK_FUSED else N // 512
     bn = 64 if N // 64 >= 192 else (32 if N // 32 >= 192 else 16)
     return (N + bn - 1) // bn
 
