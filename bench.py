@@ -407,6 +407,34 @@ def main():
             xgmi = {"ok": False, "error": repr(e)[:200]}
         log(info, f"xgmi all-reduce check: {xgmi}")
 
+    rccl_search = None
+    if W > 1:
+        # C1 / C2 as RCCL collectives over xGMI (outside the timed steps): the same batch of searches
+        # through ShardedIndex (all-gather of every rank's query rows, local fused scan, ONE packed
+        # all-gather of the per-shard top-k, topk_merge kernel) and through the serving plane
+        # (owner-routed point to point): two transports, one exact answer
+        import torch.distributed as tdist
+        B_cur = a.batch
+        qs = [tg.question() for _ in range(a.batch)]
+        mine = make_filters(5000)
+        qv = eng.embed(qs)
+        s_p, id_p = search(qv, mine)
+        every = [None] * W
+        tdist.all_gather_object(every, mine, group=ctrl)
+        flt_all = [f for r in range(W) for f in every[r]]
+        shard.search(qv, a.top_k, a.min_sim, flt_all)  # warm the collectives
+        torch.cuda.synchronize(); barrier()
+        t_r = time.perf_counter()
+        s_r, id_r = shard.search(qv, a.top_k, a.min_sim, flt_all)
+        torch.cuda.synchronize()
+        ms_r = (time.perf_counter() - t_r) * 1000
+        s_r, id_r = s_r.float().cpu().numpy(), id_r.cpu().numpy()
+        agree = int(sum(1 for b in range(a.batch) if np.array_equal(id_r[b], id_p[b])))
+        close = bool(np.allclose(np.where(id_r >= 0, s_r, 0), np.where(id_p >= 0, s_p, 0), atol=1e-3))
+        rccl_search = {"backend": info.backend, "rows": a.batch, "rows_identical": agree,
+                       "scores_close": close, "ms": round(all_reduce_max(ms_r, dev), 3)}
+        log(info, f"RCCL all-gather search vs search plane: {rccl_search}")
+
     ranks_seen = int(round(all_reduce_sum(1.0, dev)))  # every rank that reached the end of the run
     gen = eng.gen.stats
     out = {
@@ -439,6 +467,8 @@ def main():
     if xgmi is not None:
         out["xgmi_allreduce_check"] = xgmi
     out["search_plane"] = {k: (round(v, 3) if isinstance(v, float) else v) for k, v in plane.stats.items()}
+    if rccl_search is not None:
+        out["rccl_search_check"] = rccl_search
     if R == 0:
         print(json.dumps(out), flush=True)
     barrier()

@@ -7,9 +7,9 @@
 // (profiles/r3/check6: ~58 us per layer for 262 MB, ~4.5 TB/s). Here one launch runs every phase of
 // every layer, and the seams between phases become counters in device memory:
 //
-//   P1 QKV      item = 16 rows (4 waves x 4)      publishes qkv rows, bumps head_cnt[head]
+//   P1 QKV      item = 12 rows (4 waves x 3)      publishes qkv rows, bumps head_cnt[head]
 //   P2 attn     item = (head, split)              waits head_cnt[h]; last split merges, bumps heads
-//   P3 O + x    item = 16 rows                    waits heads == H;  bumps o_cnt (per-XCD shards)
+//   P3 O + x    item = 12 rows                    waits heads == H;  bumps o_cnt (per-XCD shards)
 //   P4 gate/up  item = 16 rows (8 gate + 8 up)    waits o_cnt;       bumps gu_cnt
 //   P5 down + x item = 4 rows (K split over 2 waves) waits gu_cnt;   bumps dn_cnt (next layer's P1)
 //   P6 LM head  item = 16 rows (optional)         waits dn_cnt of the last layer
@@ -245,17 +245,28 @@ __device__ __forceinline__ bool gemv_item(const bf16_t* A, const bf16_t* W, bf16
       const int n = rows[r];
       if (n < N) st_bf(C + n, f2bf(acc[r] + bf2f(ld_bf(resid + n))));
     }
-  } else {
-    static_assert(R % 2 == 0, "EPI_NONE items store row pairs");
+  } else if constexpr (R % 2 == 0) {  // rows wg R .. + R - 1 start even: 4-B pairs
 #pragma unroll
     for (int r = 0; r < R; r += 2) {
       const int n = rows[r];
       if (n + 1 < N) st_u32(C + n, pack_bf2(acc[r], acc[r + 1]));
       else if (n < N) st_bf(C + n, f2bf(acc[r]));
     }
+  } else {
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+      if (rows[r] < N) st_bf(C + rows[r], f2bf(acc[r]));
   }
   return true;
 }
+
+// Rows per wave of the QKV / O items: 3 (12-row items) where the head width allows it — the Phi-3
+// QKV projection is then 768 items = exactly 3 per workgroup on 256 CUs and the O projection 256 =
+// one each (16-row items left a 2.25-item imbalance); 4 otherwise (items must not straddle heads).
+template <int D>
+struct B1Rows {
+  static constexpr int RQ = (D % 12 == 0) ? 3 : 4;
+};
 
 // ------------------------------------------------------------------ attention item (MHA, G = 1)
 // attention.hip decode_attn_kernel<D, 1, 7> (non-temporal K/V, V with K, next tile prefetched)
@@ -322,7 +333,8 @@ __device__ __forceinline__ bool attn_item(const B1Args& a, const B1Layer& Ly, in
     load_kv(kb2, kc, t1); load_kv(vb2, vc, t1);
   }
   // 2) q / new k / new v of head hk are P1 output of this launch
-  if (!wait_ge(a.sync, S_HEAD + hk, 1, (unsigned)(3 * D / 16) * (layer_i + 1), 0x100u + hk)) return false;
+  constexpr int IQ = 4 * B1Rows<D>::RQ;
+  if (!wait_ge(a.sync, S_HEAD + hk, 1, (unsigned)(3 * D / IQ) * (layer_i + 1), 0x100u + hk)) return false;
   {
     const bf16_t* row = a.qkv;
     const int qi = min(tid, D - 1), d = qi;
@@ -541,18 +553,19 @@ __global__ void __launch_bounds__(B1_NT, 1) decode_b1_kernel(B1Args a) {
   const int Hd = a.Hd, F = a.F, H = a.H;
   unsigned* sync = a.sync;
   const int shard = wg & 7;  // per-XCD shard of the fan-in counters (dispatch round-robins XCDs)
+  constexpr int RQ = B1Rows<D>::RQ, IQ = 4 * RQ;  // rows per wave / per item (QKV and O)
   // items per phase
-  const int nq = 3 * Hd / 16, no = Hd / 16, ngu = 2 * F / 16, ndn = Hd / 4, na = H * a.nsplit;
+  const int nq = 3 * Hd / IQ, no = Hd / IQ, ngu = 2 * F / 16, ndn = Hd / 4, na = H * a.nsplit;
   for (int li = a.l0; li < a.l1; ++li) {
     const B1Layer Ly = a.layers[li];
     const int lr = li - a.l0;  // layer index within this launch: counters are per launch
     // P1: QKV (input RMSNorm fused; gain folded into the weights)
     for (int vb = wg; vb < nq; vb += G) {
-      const bool ok = gemv_item<EPI_NONE, 4, 6, 1>(a.x, Ly.wqkv, a.qkv, nullptr, 3 * Hd, Hd, a.eps, vb, [&]() {
-        return lr == 0 || wait_ge(sync, S_DN, 8, (unsigned)ndn * lr, 0x200u + li);
+      const bool ok = gemv_item<EPI_NONE, RQ, 6, 1>(a.x, Ly.wqkv, a.qkv, nullptr, 3 * Hd, Hd, a.eps, vb, [&]() {
+        return lr == 0 || vb != wg || wait_ge(sync, S_DN, 8, (unsigned)ndn * lr, 0x200u + li);
       });
       if (!ok) return;
-      const int head = ((vb * 16) % Hd) / D;  // 16 rows of one section, inside one head
+      const int head = ((vb * IQ) % Hd) / D;  // IQ rows of one section, inside one head
       publish(sync + (S_HEAD + head) * CL, 1u);
     }
     // P2: attention (head, split) items; each waits for its own head only
@@ -562,7 +575,7 @@ __global__ void __launch_bounds__(B1_NT, 1) decode_b1_kernel(B1Args a) {
     // P3: O projection + residual (x += attn W_o^T)
     unsigned mine = 0;
     for (int vb = wg; vb < no; vb += G, ++mine) {
-      if (!gemv_item<EPI_RESID, 4, 6, 1>(a.attn, Ly.wo, a.x, a.x, Hd, Hd, 0.f, vb, [&]() {
+      if (!gemv_item<EPI_RESID, RQ, 6, 1>(a.attn, Ly.wo, a.x, a.x, Hd, Hd, 0.f, vb, [&]() {
             return vb != wg || wait_ge(sync, S_HEADS, 1, (unsigned)H * (lr + 1), 0x300u + li);
           }))
         return;
@@ -627,7 +640,7 @@ DA_EXPORT int da_decode_b1(const void* layers, int l0, int l1, void* x, void* qk
   if (!layers || !x || !qkv || !attn || !act || !lens || !slot || !pos || !cos_sin || !ws || !sync)
     return (int)hipErrorInvalidValue;
   if (l0 < 0 || l1 <= l0 || grid < 1 || nsplit < 1 || chunk < 64 || chunk % 64) return (int)hipErrorInvalidValue;
-  if (Hd != H * D || Hd % 512 || F % 512 || (3 * Hd) % 16 || D % 16 || F % 16 || Hd % 16) return (int)hipErrorInvalidValue;
+  if (Hd != H * D || Hd % 512 || F % 512 || D % 16 || F % 16) return (int)hipErrorInvalidValue;
   if ((long long)chunk * nsplit < 1 || H > 4096) return (int)hipErrorInvalidValue;
   if (lm_head && (!logits || V < 16 || V % 16)) return (int)hipErrorInvalidValue;
   hipStream_t s = (hipStream_t)stream;

@@ -950,6 +950,7 @@ def spin(us: int, device=None) -> None:
 
 # ----------------------------------------------------------------------------------- batch-1 decode
 _B1_BUFS: dict = {}
+_B1_GRID: dict = {}
 
 
 def _stream_cus(device) -> int:
@@ -1011,9 +1012,13 @@ def decode_b1(layers, l0: int, l1: int, x, qkv, attn, act, lens, slot, pre, pos,
     if bufs is None:  # kept for the process: a captured graph points at them
         sb = int(lib().da_decode_b1_sync_bytes(H))
         bufs = (torch.zeros(H * nsplit * (D + 2), dtype=torch.float32, device=dev),
-                torch.zeros((sb + 15) // 16 * 4, dtype=torch.int32, device=dev), decode_b1_grid(D, dev))
+                torch.zeros((sb + 15) // 16 * 4, dtype=torch.int32, device=dev))
         _B1_BUFS[key] = bufs
-    ws, sync, grid = bufs
+    ws, sync = bufs
+    gkey = (dev.index, D, torch.cuda.current_stream().cuda_stream)  # a CU-masked lane has fewer CUs
+    grid = _B1_GRID.get(gkey)
+    if grid is None:
+        grid = _B1_GRID[gkey] = decode_b1_grid(D, dev)
     scale = scale if scale is not None else 1.0 / math.sqrt(D)
     _check(lib().da_decode_b1(_ptr(layers), l0, l1, _ptr(x), _ptr(qkv), _ptr(attn), _ptr(act), _ptr(lens), _ptr(slot),
                               _ptr(pre), _ptr(pos), _ptr(cos_sin), Hd, H, D, F, max_seq, nsplit, chunk, float(eps),
@@ -1025,7 +1030,7 @@ def decode_b1_error(device=None) -> int:
     """The persistent decode's error word of the last launch on ``device`` (0 = ok; else the code
     of the wait that timed out). Reads device memory: synchronises."""
     dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
-    for (idx, *_), (_, sync, _) in _B1_BUFS.items():
+    for (idx, *_), (_, sync) in _B1_BUFS.items():
         if idx == dev.index:
             v = int(sync[0].item())
             if v:

@@ -36,11 +36,12 @@ class _PerKernel:
 
 def test_decode_b1_step_logits_bit_identical():
     a, b = _pair()
+    a.alloc_cache(2, 4096)
+    b.alloc_cache(2, 4096)
     assert a.unit_gains and a._b1_decode(1)
     prompt = [int(t) for t in np.random.default_rng(0).integers(5, 32000, size=777)]
     outs = []
     for m, persistent in ((a, True), (b, False)):
-        m.alloc_cache(2, 4096)
         g = Generator(m, max_batch=1, max_seq=4096, temperature=0.0, use_graphs=False)
         if persistent:
             r = g.generate([prompt], 3)
