@@ -134,8 +134,9 @@ def main():
     ap.add_argument("--index-kind", default="flat", choices=["flat", "ivfflat"])
     ap.add_argument("--ivf-lists", type=int, default=1024)
     ap.add_argument("--ivf-probes", type=int, default=16)
-    ap.add_argument("--enc-dtype", default="bf16", choices=["bf16", "fp8"],
-                    help="encoder GEMM dtype (fp8 = OCP e4m3 MFMA, BASELINE config 5)")
+    ap.add_argument("--enc-dtype", default="bf16", choices=["bf16", "fp16", "fp8"],
+                    help="encoder dtype: fp16 = the whole encoder on fp16 MFMA (BASELINE config 4), "
+                         "fp8 = OCP e4m3 MFMA GEMMs (BASELINE config 5)")
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--breakdown", type=int, default=1, help="1: one extra untimed QA step with per-phase timing")
     ap.add_argument("--seed", type=int, default=0)
@@ -441,7 +442,7 @@ def main():
         "metric": METRIC, "value": round(qps, 3), "unit": "queries/s", "n_gpus": W, "steps": a.steps,
         "warmup": a.warmup, "ms_per_step": round(dt_max / a.steps * 1000, 2), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dist_backend": info.backend, "ranks_seen": ranks_seen,
-        "dtype": "bf16" if a.enc_dtype == "bf16" else "bf16 (fp8 e4m3 encoder GEMMs)",
+        "dtype": {"bf16": "bf16", "fp16": "bf16 (fp16 encoder)", "fp8": "bf16 (fp8 e4m3 encoder GEMMs)"}[a.enc_dtype],
         "data": "synthetic (random-init weights; random unit vectors for the background chunks; synthetic questions)",
         "config": {"model": f"{a.enc} embedder + {a.llm} QA", "global_batch": DP * a.batch,
                    "seq_len": int(np.mean(plen)) if plen else None,

@@ -116,10 +116,10 @@ class Config:
     def replace(self, **kw) -> "Config":
         return dataclasses.replace(self, **kw)
 
-    # engine compute dtypes actually implemented: bf16 everywhere, or fp8 (OCP e4m3) encoder GEMMs
-    # with bf16 elsewhere. fp16 is NOT implemented (no fp16 MFMA path) and is refused, never run as
-    # something else.
-    ENGINE_DTYPES = ("bf16", "fp8")
+    # engine compute dtypes (the encoder's; the decoder is bf16): bf16 everywhere; fp16 encoder
+    # (f16 MFMA GEMMs + flash, fp16 LayerNorm: BASELINE config 4); fp8 (OCP e4m3) encoder GEMMs.
+    # Anything else is refused at startup, never run as something else.
+    ENGINE_DTYPES = ("bf16", "fp16", "fp8")
 
     def validate_engine(self) -> "Config":
         """Startup check of the engine keys whose wrong value would otherwise silently run a

@@ -31,19 +31,28 @@ class BertEncoder:
     LayerNorm kernels emit the per-token-quantised activations next to the bf16 rows, and the
     dequantisation is fused into the GEMM epilogue. Attention, the O / FFN-down projections
     (whose inputs would need a separate quantisation pass), pooling and the residual stream
-    stay bf16."""
+    stay bf16.
+
+    ``dtype="fp16"`` (BASELINE config 4 "BGE-large fp16 embedder"): every weight, activation and
+    the residual stream in fp16 — GEMMs on v_mfma_f32_16x16x32_f16, flash attention on the 32x32x16
+    f16 MFMA, fp16 LayerNorm / embeddings; fp32 accumulation; the pooled unit vectors come out fp32
+    (and bf16 for the index, its storage type)."""
 
     LINEAR = ("wqkv", "w1")
 
     def __init__(self, cfg: EncoderConfig, device="cuda", seed: int = 0, weights: dict | None = None,
                  dtype: str = "bf16"):
-        if dtype not in ("bf16", "fp8"):
-            raise ValueError(f"encoder dtype must be bf16 or fp8, got {dtype!r}")
+        if dtype not in ("bf16", "fp8", "fp16"):
+            raise ValueError(f"encoder dtype must be bf16, fp16 or fp8, got {dtype!r}")
         self.cfg = cfg
         self.device = torch.device(device)
         self.ops = get_ops(self.device)
         self.w = weights if weights is not None else self._random_init(seed)
         self.fp8 = dtype == "fp8"
+        self.fp16 = dtype == "fp16"
+        if self.fp16:  # one-time cast of the whole parameter set (an fp16 checkpoint loads as is)
+            self.w = {k: (v.to(torch.float16) if isinstance(v, torch.Tensor) else
+                          [{n: t.to(torch.float16) for n, t in L.items()} for L in v]) for k, v in self.w.items()}
         if self.fp8:
             for L in self.w["layers"]:
                 for n in self.LINEAR:
@@ -107,8 +116,11 @@ class BertEncoder:
 
     # ------------------------------------------------------------------ forward
     def forward(self, ids: torch.Tensor, positions: torch.Tensor, cu_seqlens: torch.Tensor, max_seqlen: int):
-        """ids/positions int32 [T] (packed), cu_seqlens int32 [B+1] -> hidden bf16 [T, H]."""
+        """ids/positions int32 [T] (packed), cu_seqlens int32 [B+1] -> hidden bf16 [T, H] (fp16 with
+        dtype="fp16")."""
         c, o, w = self.cfg, self.ops, self.w
+        if self.fp16:
+            return self._forward_f16(ids, positions, cu_seqlens, max_seqlen)
         h, nh, hd = c.hidden, c.heads, c.head_dim
         q8 = self.fp8
         xq = None
@@ -131,6 +143,21 @@ class BertEncoder:
                 x, *xq = x
         return x
 
+    def _forward_f16(self, ids, positions, cu_seqlens, max_seqlen):
+        c, o, w = self.cfg, self.ops, self.w
+        h, nh, hd = c.hidden, c.heads, c.head_dim
+        x = o.bert_embed_ln_f16(ids, positions, None, w["word"], w["pos"], w["type"], w["emb_ln_g"], w["emb_ln_b"],
+                                c.eps)
+        for L in w["layers"]:
+            qkv = o.gemm_f16(x, L["wqkv"], bias=L["bqkv"], epi=EPI_BIAS)
+            a = o.flash_attn_f16(qkv[:, :h], qkv[:, h:2 * h], qkv[:, 2 * h:], cu_seqlens, max_seqlen, nh, nh, hd)
+            x1 = o.gemm_f16(a, L["wo"], bias=L["bo"], epi=EPI_RESID, resid=x)
+            x = o.layernorm_f16(x1, L["ln1_g"], L["ln1_b"], c.eps)
+            f = o.gemm_f16(x, L["w1"], bias=L["b1"], epi=EPI_GELU)
+            x2 = o.gemm_f16(f, L["w2"], bias=L["b2"], epi=EPI_RESID, resid=x)
+            x = o.layernorm_f16(x2, L["ln2_g"], L["ln2_b"], c.eps)
+        return x
+
     def encode_packed(self, seqs: list[list[int]], out16: torch.Tensor | None = None) -> torch.Tensor:
         """Token-id sequences -> unit-norm embeddings. Returns bf16 [B, H] if out16 given else fp32."""
         lens = np.fromiter((len(s) for s in seqs), dtype=np.int64, count=len(seqs))
@@ -144,9 +171,10 @@ class BertEncoder:
         ids_t, pos_t, cu_t = h2d(flat, dev), h2d(pos, dev), h2d(cu, dev)
         hid = self.forward(ids_t, pos_t, cu_t, int(lens.max()))
         mode = 0 if self.cfg.pooling == "cls" else 1
+        pool = self.ops.pool_l2norm_f16 if self.fp16 else self.ops.pool_l2norm
         if out16 is not None:
-            return self.ops.pool_l2norm(hid, cu_t, mode, out16=out16)
-        return self.ops.pool_l2norm(hid, cu_t, mode)
+            return pool(hid, cu_t, mode, out16=out16)
+        return pool(hid, cu_t, mode)
 
     def flops_per_token(self, seqlen: int) -> float:
         c = self.cfg
@@ -154,7 +182,7 @@ class BertEncoder:
         return c.layers * (lin + 4 * seqlen * c.hidden)
 
     def param_bytes(self) -> int:
-        return 2 * self.cfg.param_count()
+        return 2 * self.cfg.param_count()  # bf16 and fp16 alike
 
 
 def pack_for_encoder(tok, texts: list[str], max_len: int, stats: dict | None = None) -> list[list[int]]:

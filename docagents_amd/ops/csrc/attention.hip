@@ -52,7 +52,7 @@ struct FaPrefix {
 // halves and each transposed V fragment the O MFMAs of both, so LDS read bytes per FLOP halve (at
 // QH = 1 the LDS reads of a tile take as long as its MFMAs); the two halves' softmax VALU work is
 // independent of the other half's MFMAs, so the scheduler overlaps them inside one wave.
-template <int D, int NW, int QH>
+template <int D, int NW, int QH, typename T = BF16T>
 __global__ void __launch_bounds__(64 * NW, QH == 1 ? 8 / NW : 1)
 flash_attn_v2_kernel(const bf16_t* __restrict__ q, const bf16_t* __restrict__ k, const bf16_t* __restrict__ v,
                      int ldq, int ldk, int ldv, const int* __restrict__ cu, int H, int Hkv, int causal,
@@ -196,7 +196,7 @@ flash_attn_v2_kernel(const bf16_t* __restrict__ q, const bf16_t* __restrict__ k,
 #pragma unroll
           for (int hh = 0; hh < 2; ++hh)
 #pragma unroll
-            for (int j = 0; j < QH; ++j) sacc[j][hh] = mfma32(kfr[hh][ds], qf[j][ds], sacc[j][hh]);
+            for (int j = 0; j < QH; ++j) sacc[j][hh] = T::mma32(kfr[hh][ds], qf[j][ds], sacc[j][hh]);
         // pin that order: the register-pressure scheduler otherwise re-serialises read -> MFMA pairs
         __builtin_amdgcn_sched_group_barrier(0x100, 2 * NDS, 0);       // DS reads
         __builtin_amdgcn_sched_group_barrier(0x008, 2 * NDS * QH, 0);  // MFMAs
@@ -210,7 +210,7 @@ flash_attn_v2_kernel(const bf16_t* __restrict__ q, const bf16_t* __restrict__ k,
 #pragma unroll
           for (int ds = 0; ds < NDS; ++ds)
 #pragma unroll
-            for (int j = 0; j < QH; ++j) sacc[j][hh] = mfma32(kfr[ds], qf[j][ds], sacc[j][hh]);
+            for (int j = 0; j < QH; ++j) sacc[j][hh] = T::mma32(kfr[ds], qf[j][ds], sacc[j][hh]);
           __builtin_amdgcn_sched_group_barrier(0x100, NDS, 0);
           __builtin_amdgcn_sched_group_barrier(0x008, NDS * QH, 0);
         }
@@ -261,10 +261,10 @@ flash_attn_v2_kernel(const bf16_t* __restrict__ q, const bf16_t* __restrict__ k,
         bf16x8_t pb[QH];
 #pragma unroll
         for (int j = 0; j < QH; ++j) {
-          const u32x4_t pw = u32x4_t{pack_bf2(sacc[j][hh][cb], sacc[j][hh][cb + 1]),
-                                     pack_bf2(sacc[j][hh][cb + 2], sacc[j][hh][cb + 3]),
-                                     pack_bf2(sacc[j][hh][cb + 4], sacc[j][hh][cb + 5]),
-                                     pack_bf2(sacc[j][hh][cb + 6], sacc[j][hh][cb + 7])};
+          const u32x4_t pw = u32x4_t{T::pack2(sacc[j][hh][cb], sacc[j][hh][cb + 1]),
+                                     T::pack2(sacc[j][hh][cb + 2], sacc[j][hh][cb + 3]),
+                                     T::pack2(sacc[j][hh][cb + 4], sacc[j][hh][cb + 5]),
+                                     T::pack2(sacc[j][hh][cb + 6], sacc[j][hh][cb + 7])};
           pb[j] = __builtin_bit_cast(bf16x8_t, pw);
         }
         const int g = lane >> 4, li = lane & 15;
@@ -276,7 +276,7 @@ flash_attn_v2_kernel(const bf16_t* __restrict__ q, const bf16_t* __restrict__ k,
           const s16x4_t hi8 = lds_read_tr16(sV + (row0 + 8) * C::VSTR + col * 2);
           const bf16x8_t va = bf16x8_t{lo[0], lo[1], lo[2], lo[3], hi8[0], hi8[1], hi8[2], hi8[3]};
 #pragma unroll
-          for (int j = 0; j < QH; ++j) oacc[j][db] = mfma32(va, pb[j], oacc[j][db]);
+          for (int j = 0; j < QH; ++j) oacc[j][db] = T::mma32(va, pb[j], oacc[j][db]);
         }
       }
     }
@@ -295,8 +295,8 @@ flash_attn_v2_kernel(const bf16_t* __restrict__ q, const bf16_t* __restrict__ k,
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
           const int d = db * 32 + 8 * g + 4 * hi;
-          *(u32x2_t*)(orow + d) = u32x2_t{pack_bf2(oacc[j][db][4 * g] * inv, oacc[j][db][4 * g + 1] * inv),
-                                          pack_bf2(oacc[j][db][4 * g + 2] * inv, oacc[j][db][4 * g + 3] * inv)};
+          *(u32x2_t*)(orow + d) = u32x2_t{T::pack2(oacc[j][db][4 * g] * inv, oacc[j][db][4 * g + 1] * inv),
+                                          T::pack2(oacc[j][db][4 * g + 2] * inv, oacc[j][db][4 * g + 3] * inv)};
         }
     }
   }
@@ -1511,6 +1511,26 @@ DA_EXPORT void da_set_flash_waves(int nw) { g_fa_waves = nw; }
 // causal flash: longest query blocks first (1, default) or grid order (0); A/B runs
 static int g_fa_rev = 1;
 DA_EXPORT void da_set_flash_rev(int v) { g_fa_rev = v ? 1 : 0; }
+
+// fp16 (the encoder's DTYPE=fp16): bidirectional or causal, no shared prefix, 4 waves x 32 queries
+DA_EXPORT int da_flash_attn_f16(const void* q, const void* k, const void* v, int ldq, int ldk, int ldv,
+                                const void* cu_seqlens, int B, int max_seqlen, int H, int Hkv, int D, int causal,
+                                float scale, void* o, int ldo, void* stream) {
+  if (H % Hkv || ldq % 8 || ldk % 8 || ldv % 8 || ldo % 4) return (int)hipErrorInvalidValue;
+  if (B == 0 || max_seqlen == 0) return 0;
+  const FaPrefix pre{nullptr, nullptr, 0, 0, g_fa_rev};
+  dim3 grid((max_seqlen + 127) / 128, H, B);
+  hipStream_t s = (hipStream_t)stream;
+#define FA_ARGS16 (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, ldq, ldk, ldv, (const int*)cu_seqlens, H, Hkv, \
+                  causal, scale * 1.4426950408889634f, (bf16_t*)o, ldo, pre
+  switch (D) {
+    case 64: flash_attn_v2_kernel<64, 4, 1, F16T><<<grid, 256, FA2Cfg<64, 4, 1>::SMEM, s>>>(FA_ARGS16); break;
+    case 96: flash_attn_v2_kernel<96, 4, 1, F16T><<<grid, 256, FA2Cfg<96, 4, 1>::SMEM, s>>>(FA_ARGS16); break;
+    default: return (int)hipErrorInvalidValue;
+  }
+#undef FA_ARGS16
+  return (int)hipGetLastError();
+}
 
 template <int NW, int QH>
 static int launch_fa2(const void* q, const void* k, const void* v, int ldq, int ldk, int ldv, const void* cu_seqlens,

@@ -57,6 +57,45 @@ __device__ __forceinline__ f32x16_t mfma32(const bf16x8_t& a, const bf16x8_t& b,
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
 }
 
+// ------------------------------------------------------------------------------------------
+// 16-bit element types of the kernels: bf16 (everything) and fp16 (the encoder's DTYPE=fp16 path:
+// GEMMs on v_mfma_f32_*_f16, flash attention, LayerNorm / embeddings / pooling). Both are stored as
+// raw 16-bit words and moved as bf16x8_t / u32x4_t registers; only the conversions and the MFMA
+// opcode depend on the type, so one kernel template serves both (fp32 accumulation either way).
+typedef __attribute__((ext_vector_type(8))) _Float16 f16x8_t;
+typedef __attribute__((ext_vector_type(2))) _Float16 f16x2_hw_t;
+
+struct BF16T {
+  static constexpr bool kF16 = false;
+  __device__ static __forceinline__ float to_f(uint16_t v) { return bf2f(v); }
+  __device__ static __forceinline__ uint16_t from_f(float f) { return f2bf(f); }
+  __device__ static __forceinline__ unsigned pack2(float lo, float hi) { return pack_bf2(lo, hi); }
+  __device__ static __forceinline__ f32x4_t mma16(const bf16x8_t& a, const bf16x8_t& b, const f32x4_t& c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+  }
+  __device__ static __forceinline__ f32x16_t mma32(const bf16x8_t& a, const bf16x8_t& b, const f32x16_t& c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+  }
+};
+
+struct F16T {
+  static constexpr bool kF16 = true;
+  __device__ static __forceinline__ float to_f(uint16_t v) { return (float)__builtin_bit_cast(_Float16, v); }
+  __device__ static __forceinline__ uint16_t from_f(float f) { return __builtin_bit_cast(uint16_t, (_Float16)f); }
+  __device__ static __forceinline__ unsigned pack2(float lo, float hi) {
+    const f16x2_hw_t r = {(_Float16)lo, (_Float16)hi};
+    return __builtin_bit_cast(unsigned, r);
+  }
+  __device__ static __forceinline__ f32x4_t mma16(const bf16x8_t& a, const bf16x8_t& b, const f32x4_t& c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8_t, a), __builtin_bit_cast(f16x8_t, b), c,
+                                                 0, 0, 0);
+  }
+  __device__ static __forceinline__ f32x16_t mma32(const bf16x8_t& a, const bf16x8_t& b, const f32x16_t& c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8_t, a), __builtin_bit_cast(f16x8_t, b), c,
+                                                 0, 0, 0);
+  }
+};
+
 // Exchange with lane l^32 (v_permlane32_swap, a VALU op — no LDS crossbar). Returns {own, partner}
 // in some order, so callers combine both halves symmetrically (max / sum).
 __device__ __forceinline__ float max_xhalf(float x) {

@@ -46,7 +46,7 @@ __device__ __forceinline__ void vmcnt() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-template <int EPI, int BM>
+template <int EPI, int BM, typename T = BF16T>
 __global__ void __launch_bounds__(512)
 gemm8p_kernel(GemmArgs p) {
   static_assert(BM == 256 || BM == 128, "BM");
@@ -164,7 +164,7 @@ gemm8p_kernel(GemmArgs p) {
 #pragma unroll
       for (int i = 0; i < MI; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) acc[IH][JH][i][j] = mfma16(ra[kk][i], rb[kk][j], acc[IH][JH][i][j]);
+        for (int j = 0; j < 2; ++j) acc[IH][JH][i][j] = T::mma16(ra[kk][i], rb[kk][j], acc[IH][JH][i][j]);
   };
   using I0 = std::integral_constant<int, 0>;
   using I1 = std::integral_constant<int, 1>;
@@ -284,7 +284,7 @@ gemm8p_kernel(GemmArgs p) {
           for (int q = 0; q < 4; ++q) {
             const float iv = rs[ih][i][q];
             const float v = silu(acc[ih][jh][i][0][q] * iv) * (acc[ih][jh][i][1][q] * iv);
-            *(bf16_t*)(st + (ih * QR + i * 16 + fg * 4 + q) * SROW + (jh * 16 + fr) * 2) = f2bf(v);
+            *(bf16_t*)(st + (ih * QR + i * 16 + fg * 4 + q) * SROW + (jh * 16 + fr) * 2) = T::from_f(v);
           }
   } else {
     float bv[2][2] = {{0.f, 0.f}, {0.f, 0.f}};
@@ -294,7 +294,7 @@ gemm8p_kernel(GemmArgs p) {
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
           const int gc = n0 + jh * 128 + wn * 32 + j * 16 + fr;
-          bv[jh][j] = gc < p.N ? bf2f(p.bias[gc]) : 0.f;
+          bv[jh][j] = gc < p.N ? T::to_f(p.bias[gc]) : 0.f;
         }
     }
 #pragma unroll
@@ -309,7 +309,7 @@ gemm8p_kernel(GemmArgs p) {
             for (int q = 0; q < 4; ++q) {
               float v = acc[ih][jh][i][j][q] * rs[ih][i][q] + bv[jh][j];
               if constexpr (EPI == EPI_GELU) v = gelu_erf(v);
-              *(bf16_t*)(st + (ih * QR + i * 16 + fg * 4 + q) * SROW + (jh * 32 + j * 16 + fr) * 2) = f2bf(v);
+              *(bf16_t*)(st + (ih * QR + i * 16 + fg * 4 + q) * SROW + (jh * 32 + j * 16 + fr) * 2) = T::from_f(v);
             }
   }
   __syncthreads();
@@ -368,16 +368,16 @@ gemm8p_kernel(GemmArgs p) {
         const u32x4_t r = *(const u32x4_t*)(p.resid + (size_t)gm * p.ldr + gcol);
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          const float lo = bf2f((bf16_t)(v[e] & 0xffff)) + bf2f((bf16_t)(r[e] & 0xffff));
-          const float hi = bf2f((bf16_t)(v[e] >> 16)) + bf2f((bf16_t)(r[e] >> 16));
-          v[e] = pack_bf2(lo, hi);
+          const float lo = T::to_f((bf16_t)(v[e] & 0xffff)) + T::to_f((bf16_t)(r[e] & 0xffff));
+          const float hi = T::to_f((bf16_t)(v[e] >> 16)) + T::to_f((bf16_t)(r[e] >> 16));
+          v[e] = T::pack2(lo, hi);
         }
       }
       if (ssq) {
         float sq = 0.f;
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          const float lo = bf2f((bf16_t)(v[e] & 0xffff)), hi = bf2f((bf16_t)(v[e] >> 16));
+          const float lo = T::to_f((bf16_t)(v[e] & 0xffff)), hi = T::to_f((bf16_t)(v[e] >> 16));
           sq += lo * lo + hi * hi;
         }
         if (!ok) sq = 0.f;
@@ -394,6 +394,16 @@ template <int BM>
 static int launch8p(const GemmArgs& a, int epi, hipStream_t s) {
   const int ntm = (a.M + BM - 1) / BM, ntn = (a.N + BN - 1) / BN;
   dim3 grid(ntm * ntn), block(512);
+  if (epi >= 100) {  // fp16 operands (the encoder's DTYPE=fp16): the BERT epilogues only
+    switch (epi - 100) {
+      case EPI_NONE: gemm8p_kernel<EPI_NONE, BM, F16T><<<grid, block, 0, s>>>(a); break;
+      case EPI_BIAS: gemm8p_kernel<EPI_BIAS, BM, F16T><<<grid, block, 0, s>>>(a); break;
+      case EPI_GELU: gemm8p_kernel<EPI_GELU, BM, F16T><<<grid, block, 0, s>>>(a); break;
+      case EPI_RESID: gemm8p_kernel<EPI_RESID, BM, F16T><<<grid, block, 0, s>>>(a); break;
+      default: return (int)hipErrorInvalidValue;
+    }
+    return (int)hipGetLastError();
+  }
   switch (epi) {
     case EPI_NONE: gemm8p_kernel<EPI_NONE, BM><<<grid, block, 0, s>>>(a); break;
     case EPI_BIAS: gemm8p_kernel<EPI_BIAS, BM><<<grid, block, 0, s>>>(a); break;
@@ -406,9 +416,26 @@ static int launch8p(const GemmArgs& a, int epi, hipStream_t s) {
   return (int)hipGetLastError();
 }
 
+// epi + 100: the same kernel on fp16 operands / output (v_mfma_f32_16x16x32_f16)
 int launch_gemm8p(const GemmArgs& a, int epi, hipStream_t s, int bm) {
   if (a.K < 128 || a.K % 64) return (int)hipErrorInvalidValue;
   // buffer resources span the tile's rows from its first one (num_records < 2 GiB)
   if ((size_t)bm * a.lda * 2 >= 0x7ffffff0ull || (size_t)256 * a.K * 2 >= 0x7ffffff0ull) return (int)hipErrorInvalidValue;
   return bm == 128 ? launch8p<128>(a, epi, s) : launch8p<256>(a, epi, s);
+}
+
+// fp16 GEMM for the encoder's DTYPE=fp16 path: C = epi(A W^T), A [M, K] / W [N, K] / C / bias /
+// resid fp16, fp32 accumulation; epi NONE / BIAS / GELU / RESID. Every M on the phase-split tile
+// (128-row tiles below half a chip of 256-row ones): the fp16 path has no decode-sized tiles.
+DA_EXPORT int da_gemm_f16(const void* A, int lda, const void* W, void* C, int ldc, const void* bias,
+                          const void* resid, int ldr, int M, int N, int K, int epi, void* stream) {
+  if (M < 1 || K % 64 || K < 128 || N % 8 || lda % 8 || ldc % 8) return (int)hipErrorInvalidValue;
+  if (epi != EPI_NONE && epi != EPI_BIAS && epi != EPI_GELU && epi != EPI_RESID) return (int)hipErrorInvalidValue;
+  if (epi == EPI_RESID && (!resid || ldr % 8)) return (int)hipErrorInvalidValue;
+  GemmArgs a{};
+  a.A = (const bf16_t*)A; a.W = (const bf16_t*)W; a.C = (bf16_t*)C;
+  a.bias = (const bf16_t*)bias; a.resid = (const bf16_t*)resid;
+  a.M = M; a.N = N; a.K = K; a.lda = lda; a.ldc = ldc; a.ldr = ldr; a.k_per_split = K;
+  const long t256 = (long)((M + 255) / 256) * ((N + 255) / 256);
+  return launch_gemm8p(a, 100 + epi, (hipStream_t)stream, t256 >= 128 ? 256 : 128);
 }

@@ -8,16 +8,18 @@
 
 #define MAXCH 8  // max 8-element chunks per thread (D <= 8 * 8 * 256 = 16384)
 
+template <typename T = BF16T>
 __device__ __forceinline__ void load8(const bf16_t* p, float* v) {
   u32x4_t u = *(const u32x4_t*)p;
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
-    v[2 * e] = bf2f((bf16_t)(u[e] & 0xffff));
-    v[2 * e + 1] = bf2f((bf16_t)(u[e] >> 16));
+    v[2 * e] = T::to_f((bf16_t)(u[e] & 0xffff));
+    v[2 * e + 1] = T::to_f((bf16_t)(u[e] >> 16));
   }
 }
+template <typename T = BF16T>
 __device__ __forceinline__ void store8(bf16_t* p, const float* v) {
-  *(u32x4_t*)p = u32x4_t{pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3]), pack_bf2(v[4], v[5]), pack_bf2(v[6], v[7])};
+  *(u32x4_t*)p = u32x4_t{T::pack2(v[0], v[1]), T::pack2(v[2], v[3]), T::pack2(v[4], v[5]), T::pack2(v[6], v[7])};
 }
 
 // RMSNorm with optional fused residual add:
@@ -139,6 +141,7 @@ __device__ __forceinline__ void store_row_fp8(float (&v)[MAXCH][8], int nch, int
 }
 
 // LayerNorm (BERT), optional residual input added first (x + resid), bias optional.
+template <typename T = BF16T>
 __global__ void layernorm_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ resid,
                                  const bf16_t* __restrict__ g, const bf16_t* __restrict__ b,
                                  bf16_t* __restrict__ y, int D, float eps, unsigned char* __restrict__ yq = nullptr,
@@ -152,10 +155,10 @@ __global__ void layernorm_kernel(const bf16_t* __restrict__ x, const bf16_t* __r
   for (int i = 0; i < MAXCH; ++i) {
     const int c = threadIdx.x + i * blockDim.x;
     if (c < nch) {
-      load8(x + (size_t)row * D + c * 8, v[i]);
+      load8<T>(x + (size_t)row * D + c * 8, v[i]);
       if (resid) {
         float r[8];
-        load8(resid + (size_t)row * D + c * 8, r);
+        load8<T>(resid + (size_t)row * D + c * 8, r);
 #pragma unroll
         for (int e = 0; e < 8; ++e) v[i][e] += r[e];
       }
@@ -180,17 +183,18 @@ __global__ void layernorm_kernel(const bf16_t* __restrict__ x, const bf16_t* __r
     const int c = threadIdx.x + i * blockDim.x;
     if (c < nch) {
       float gv[8], bv[8];
-      load8(g + c * 8, gv);
-      if (b) load8(b + c * 8, bv);
+      load8<T>(g + c * 8, gv);
+      if (b) load8<T>(b + c * 8, bv);
 #pragma unroll
       for (int e = 0; e < 8; ++e) v[i][e] = (v[i][e] - mean) * inv * gv[e] + (b ? bv[e] : 0.f);
-      store8(y + (size_t)row * D + c * 8, v[i]);
+      store8<T>(y + (size_t)row * D + c * 8, v[i]);
     }
   }
   if (yq) store_row_fp8(v, nch, row, yq, D, yscale, red);
 }
 
 // BERT embeddings: y = LN(word[ids[t]] + pos[positions[t]] + type[types ? types[t] : 0])
+template <typename T = BF16T>
 __global__ void bert_embed_ln_kernel(const int* __restrict__ ids, const int* __restrict__ positions,
                                      const int* __restrict__ types, const bf16_t* __restrict__ word,
                                      const bf16_t* __restrict__ pos, const bf16_t* __restrict__ type,
@@ -208,9 +212,9 @@ __global__ void bert_embed_ln_kernel(const int* __restrict__ ids, const int* __r
     const int c = threadIdx.x + i * blockDim.x;
     if (c < nch) {
       float a[8], p[8], t[8];
-      load8(word + wi * D + c * 8, a);
-      load8(pos + pi * D + c * 8, p);
-      load8(type + ti * D + c * 8, t);
+      load8<T>(word + wi * D + c * 8, a);
+      load8<T>(pos + pi * D + c * 8, p);
+      load8<T>(type + ti * D + c * 8, t);
 #pragma unroll
       for (int e = 0; e < 8; ++e) { v[i][e] = a[e] + p[e] + t[e]; s += v[i][e]; }
     }
@@ -232,11 +236,11 @@ __global__ void bert_embed_ln_kernel(const int* __restrict__ ids, const int* __r
     const int c = threadIdx.x + i * blockDim.x;
     if (c < nch) {
       float gv[8], bv[8];
-      load8(g + c * 8, gv);
-      load8(b + c * 8, bv);
+      load8<T>(g + c * 8, gv);
+      load8<T>(b + c * 8, bv);
 #pragma unroll
       for (int e = 0; e < 8; ++e) v[i][e] = (v[i][e] - mean) * inv * gv[e] + bv[e];
-      store8(y + (size_t)row * D + c * 8, v[i]);
+      store8<T>(y + (size_t)row * D + c * 8, v[i]);
     }
   }
   if (yq) store_row_fp8(v, nch, row, yq, D, yscale, red);
@@ -254,6 +258,7 @@ __global__ void embed_kernel(const int* __restrict__ ids, const bf16_t* __restri
 // Pooling + L2 normalisation (fp32 accumulate; zero vector left unchanged like the reference's
 // `normalize`). mode 0 = CLS (first token), 1 = mean over the sequence's tokens.
 // Output fp32 [B, D] and/or bf16 [B, D] (the index stores bf16).
+template <typename T = BF16T>
 __global__ void pool_l2norm_kernel(const bf16_t* __restrict__ h, const int* __restrict__ cu_seqlens,
                                    int D, int mode, float* __restrict__ out32,
                                    bf16_t* __restrict__ out16) {
@@ -268,13 +273,13 @@ __global__ void pool_l2norm_kernel(const bf16_t* __restrict__ h, const int* __re
     const int c = threadIdx.x + i * blockDim.x;
     if (c < nch) {
       if (mode == 0 || s1 <= s0) {
-        load8(h + (size_t)s0 * D + c * 8, v[i]);
+        load8<T>(h + (size_t)s0 * D + c * 8, v[i]);
       } else {
 #pragma unroll
         for (int e = 0; e < 8; ++e) v[i][e] = 0.f;
         for (int t = s0; t < s1; ++t) {
           float a[8];
-          load8(h + (size_t)t * D + c * 8, a);
+          load8<T>(h + (size_t)t * D + c * 8, a);
 #pragma unroll
           for (int e = 0; e < 8; ++e) v[i][e] += a[e];
         }
@@ -418,6 +423,38 @@ DA_EXPORT int da_quant_fp8_rows(const void* x, int ldx, int M, int K, void* out,
   if (M == 0) return 0;
   quant_fp8_rows_kernel<<<M, row_threads(K), 0, (hipStream_t)stream>>>((const bf16_t*)x, ldx, K, (unsigned char*)out,
                                                                        ldo, (float*)scale);
+  DA_LAUNCH_CHECK();
+}
+
+// fp16 forms (the encoder's DTYPE=fp16): LayerNorm and embeddings + LayerNorm read / write fp16
+// rows; pooling reads fp16 hidden states and writes fp32 and / or bf16 (the index storage type).
+DA_EXPORT int da_layernorm_f16(const void* x, const void* resid, const void* g, const void* b, void* y, int M, int D,
+                               float eps, void* stream) {
+  if (!d_ok(D)) return (int)hipErrorInvalidValue;
+  if (M == 0) return 0;
+  layernorm_kernel<F16T><<<M, row_threads(D), 0, (hipStream_t)stream>>>((const bf16_t*)x, (const bf16_t*)resid,
+                                                                         (const bf16_t*)g, (const bf16_t*)b,
+                                                                         (bf16_t*)y, D, eps);
+  DA_LAUNCH_CHECK();
+}
+
+DA_EXPORT int da_bert_embed_ln_f16(const void* ids, const void* positions, const void* types, const void* word,
+                                   const void* pos, const void* type, const void* g, const void* b, void* y, int T,
+                                   int D, float eps, void* stream) {
+  if (!d_ok(D)) return (int)hipErrorInvalidValue;
+  if (T == 0) return 0;
+  bert_embed_ln_kernel<F16T><<<T, row_threads(D), 0, (hipStream_t)stream>>>(
+      (const int*)ids, (const int*)positions, (const int*)types, (const bf16_t*)word, (const bf16_t*)pos,
+      (const bf16_t*)type, (const bf16_t*)g, (const bf16_t*)b, (bf16_t*)y, D, eps);
+  DA_LAUNCH_CHECK();
+}
+
+DA_EXPORT int da_pool_l2norm_f16(const void* h, const void* cu_seqlens, int B, int D, int mode, void* out32,
+                                 void* out16, void* stream) {
+  if (!d_ok(D)) return (int)hipErrorInvalidValue;
+  if (B == 0) return 0;
+  pool_l2norm_kernel<F16T><<<B, row_threads(D), 0, (hipStream_t)stream>>>((const bf16_t*)h, (const int*)cu_seqlens,
+                                                                           D, mode, (float*)out32, (bf16_t*)out16);
   DA_LAUNCH_CHECK();
 }
 

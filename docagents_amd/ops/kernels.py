@@ -104,6 +104,13 @@ _SIGS = {
     "da_decode_b1": [c_void_p, c_int, c_int] + [c_void_p] * 4 + [c_void_p] * 5 + [c_int] * 7 + [c_float, c_float]
                     + [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p],
     "da_decode_b1_occupancy": [c_int, ctypes.POINTER(c_int)],
+    "da_gemm_f16": [c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int,
+                    c_void_p],
+    "da_flash_attn_f16": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_int, c_int, c_int,
+                          c_int, c_int, c_float, c_void_p, c_int, c_void_p],
+    "da_layernorm_f16": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_float, c_void_p],
+    "da_bert_embed_ln_f16": [c_void_p] * 9 + [c_int, c_int, c_float, c_void_p],
+    "da_pool_l2norm_f16": [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p],
 }
 
 
@@ -1036,3 +1043,93 @@ def decode_b1_error(device=None) -> int:
             if v:
                 return v
     return 0
+
+
+# ----------------------------------------------------------------------------------- fp16 encoder
+# DTYPE=fp16 (BASELINE config 4's "fp16 embedder"): the encoder's GEMMs (v_mfma_f32_16x16x32_f16 on
+# the phase-split tile), flash attention (32x32x16 f16), LayerNorm / embeddings / pooling on fp16
+# rows; fp32 accumulation everywhere. Same kernels as bf16, instantiated on the fp16 element type.
+def _f16_cuda(t, name):
+    _req(t.is_cuda, f"{name} must be on GPU")
+    _req(t.dtype == torch.float16, f"{name} must be fp16, got {t.dtype}")
+
+
+def gemm_f16(a, w, bias=None, epi: int = EPI_NONE, resid=None, out=None) -> torch.Tensor:
+    """out = epi(a @ w^T) in fp16 (fp32 accumulate); epi NONE / BIAS / GELU / RESID."""
+    _f16_cuda(a, "a"); _f16_cuda(w, "w")
+    M, K = a.shape
+    N = w.shape[0]
+    _req(w.shape[1] == K and w.is_contiguous() and a.stride(1) == 1 and a.stride(0) % 8 == 0, "gemm_f16 layout")
+    _req(K % 64 == 0 and K >= 128 and N % 8 == 0, f"gemm_f16 shape N={N} K={K}")
+    _req(epi in (EPI_NONE, EPI_BIAS, EPI_GELU, EPI_RESID), "gemm_f16 epilogue")
+    if bias is not None:
+        _f16_cuda(bias, "bias"); _req(bias.numel() == N, "bias")
+    ldr = 0
+    if epi == EPI_RESID:
+        _f16_cuda(resid, "resid")
+        _req(resid.shape == (M, N) and resid.stride(1) == 1 and resid.stride(0) % 8 == 0, "resid")
+        ldr = resid.stride(0)
+    if out is None:
+        out = torch.empty((M, N), dtype=torch.float16, device=a.device)
+    _req(out.dtype == torch.float16 and out.shape == (M, N) and out.stride(1) == 1 and out.stride(0) % 8 == 0, "out")
+    _check(lib().da_gemm_f16(_ptr(a), a.stride(0), _ptr(w), _ptr(out), out.stride(0), _ptr(bias), _ptr(resid), ldr,
+                             M, N, K, epi, _stream()), "gemm_f16")
+    return out
+
+
+def flash_attn_f16(q, k, v, cu_seqlens, max_seqlen: int, H: int, Hkv: int, D: int, causal: bool = False,
+                   scale: float | None = None, out=None):
+    for t, n in ((q, "q"), (k, "k"), (v, "v")):
+        _f16_cuda(t, n)
+        _req(t.dim() == 2 and t.stride(1) == 1 and t.stride(0) % 8 == 0 and t.data_ptr() % 16 == 0, f"{n} layout")
+    _i32(cu_seqlens, "cu_seqlens")
+    _req(D in (64, 96) and H % Hkv == 0, "flash_attn_f16: D 64 / 96")
+    T = q.shape[0]
+    if out is None:
+        out = torch.empty((T, H * D), dtype=torch.float16, device=q.device)
+    scale = scale if scale is not None else 1.0 / math.sqrt(D)
+    _check(lib().da_flash_attn_f16(_ptr(q), _ptr(k), _ptr(v), q.stride(0), k.stride(0), v.stride(0), _ptr(cu_seqlens),
+                                   cu_seqlens.numel() - 1, int(max_seqlen), H, Hkv, D, int(causal), float(scale),
+                                   _ptr(out), out.stride(0), _stream()), "flash_attn_f16")
+    return out
+
+
+def layernorm_f16(x, g, b, eps: float, resid=None, out=None):
+    _f16_cuda(x, "x")
+    M, D = x.shape
+    _req(x.is_contiguous() and D % 8 == 0, "x must be contiguous, D % 8 == 0")
+    if resid is not None:
+        _f16_cuda(resid, "resid"); _req(resid.is_contiguous() and resid.shape == x.shape, "bad resid")
+    _f16_cuda(g, "g"); _f16_cuda(b, "b")
+    if out is None:
+        out = torch.empty_like(x)
+    _check(lib().da_layernorm_f16(_ptr(x), _ptr(resid), _ptr(g), _ptr(b), _ptr(out), M, D, float(eps), _stream()),
+           "layernorm_f16")
+    return out
+
+
+def bert_embed_ln_f16(ids, positions, types, word, pos, type_, g, b, eps: float, out=None):
+    _i32(ids, "ids"); _i32(positions, "positions")
+    for t, n in ((word, "word"), (pos, "pos"), (type_, "type"), (g, "g"), (b, "b")):
+        _f16_cuda(t, n)
+    T, D = ids.numel(), word.shape[1]
+    _req(positions.numel() == T and D % 8 == 0, "positions length / D")
+    if out is None:
+        out = torch.empty((T, D), dtype=torch.float16, device=ids.device)
+    _check(lib().da_bert_embed_ln_f16(_ptr(ids), _ptr(positions), _ptr(types), _ptr(word), _ptr(pos), _ptr(type_),
+                                      _ptr(g), _ptr(b), _ptr(out), T, D, float(eps), _stream()), "bert_embed_ln_f16")
+    return out
+
+
+def pool_l2norm_f16(h, cu_seqlens, mode: int = 0, out32=None, out16=None):
+    """fp16 hidden states -> unit-norm pooled rows, fp32 and / or bf16 (the index storage type)."""
+    _f16_cuda(h, "h"); _i32(cu_seqlens, "cu_seqlens")
+    B, D = cu_seqlens.numel() - 1, h.shape[1]
+    _req(h.is_contiguous() and D % 8 == 0, "h contiguous")
+    if out16 is not None:
+        _bf16_cuda(out16, "out16")
+    if out32 is None and out16 is None:
+        out32 = torch.empty((B, D), dtype=torch.float32, device=h.device)
+    _check(lib().da_pool_l2norm_f16(_ptr(h), _ptr(cu_seqlens), B, D, mode, _ptr(out32), _ptr(out16), _stream()),
+           "pool_l2norm_f16")
+    return out32 if out32 is not None else out16

@@ -45,6 +45,22 @@ def _epilogue(y, N, bias, epi, resid, out):
     return y
 
 
+def gemm_f16(a, w, bias=None, epi=EPI_NONE, resid=None, out=None):
+    """fp16 oracle of kernels.gemm_f16: fp32 product + epilogue, one fp16 rounding."""
+    y = a.float() @ w.float().t()
+    if bias is not None:
+        y = y + bias.float()
+    if epi == EPI_GELU:
+        y = F.gelu(y)
+    elif epi == EPI_RESID:
+        y = y + resid.float()
+    y = y.to(torch.float16)
+    if out is not None:
+        out.copy_(y)
+        return out
+    return y
+
+
 def interleave_gate_up(gate: torch.Tensor, up: torch.Tensor) -> torch.Tensor:
     """[F, K] gate + [F, K] up -> [2F, K] rows interleaved in 16-row groups (EPI_SWIGLU layout)."""
     Fd, K = gate.shape
@@ -522,3 +538,18 @@ def gemm_resid_norm(a, w, resid, gamma, eps, out=None, h_out=None, bias=None):
         h_out.copy_(h)
         return h_out
     return h
+
+
+# fp16 forms of the encoder ops (kernels.*_f16): these references keep the input dtype
+layernorm_f16 = layernorm
+bert_embed_ln_f16 = bert_embed_ln
+pool_l2norm_f16 = pool_l2norm
+
+
+def flash_attn_f16(q, k, v, cu_seqlens, max_seqlen, H, Hkv, D, causal=False, scale=None, out=None):
+    y = flash_attn_varlen(q.float(), k.float(), v.float(), cu_seqlens, max_seqlen, H, Hkv, D, causal, scale=scale)
+    y = y.to(torch.float16)
+    if out is not None:
+        out.copy_(y)
+        return out
+    return y

@@ -3,7 +3,7 @@
 set -u
 cd $GRAFT_REPO_ROOT
 OUT=gpurun_out/${1:-r4c}; mkdir -p $OUT
-timeout -k 10 600 python -u -m pytest tests/test_decode_b1_gpu.py tests/test_splitk_fused_gpu.py tests/test_index_race_gpu.py \
+timeout -k 10 600 python -u -m pytest tests/test_decode_b1_gpu.py tests/test_splitk_fused_gpu.py tests/test_index_race_gpu.py tests/test_fp16_encoder_gpu.py \
   -x -v --timeout 180 --timeout-method thread -p no:cacheprovider > $OUT/pytest_new.log 2>&1
 rc=$?; tail -12 $OUT/pytest_new.log; [ $rc -ne 0 ] && exit $rc
 timeout -k 10 900 python -u -m pytest tests/test_kernels_gpu.py tests/test_models_gpu.py tests/test_serving_gpu.py \

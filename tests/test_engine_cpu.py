@@ -563,3 +563,20 @@ def test_dk_decode_step_matches_fused_norm_step():
             R.DECODE_DK = True
     for a, b in zip(out[True], out[False]):
         assert torch.allclose(a, b, atol=0.05, rtol=0.02), (a - b).abs().max()
+
+
+def test_fp16_encoder_matches_bf16_encoder_cpu():
+    """DTYPE=fp16 (BASELINE config 4): the encoder on fp16 weights / activations gives the same unit
+    vectors as the bf16 one to rounding (CPU reference ops; the kernels: tests/test_models_gpu.py)."""
+    import copy
+
+    from docagents_amd.models.bert import BertEncoder
+    from docagents_amd.models.configs import encoder_config
+    cfg = encoder_config("tiny-enc")
+    a = BertEncoder(cfg, "cpu", seed=3)
+    b = BertEncoder(cfg, "cpu", weights=copy.deepcopy(a.w), dtype="fp16")
+    assert b.w["word"].dtype == torch.float16 and b.w["layers"][0]["wqkv"].dtype == torch.float16
+    seqs = [[101, 2000 + i, 3000 + 2 * i, 102] for i in range(5)] + [list(range(100, 140))]
+    va, vb = a.encode_packed(seqs), b.encode_packed(seqs)
+    cos = (va.float() * vb.float()).sum(-1)
+    assert cos.min() > 0.999, cos
