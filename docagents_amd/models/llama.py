@@ -405,12 +405,13 @@ class LlamaDecoder:
                              out=st.attn, pre=st.pre)
 
     def _b1_decode(self, B: int) -> bool:
-        """Batch 1, one rank, MHA (the fused-RoPE attention), folded norm gains: the persistent
-        launch (every layer + the LM head; decode_b1.hip)."""
+        """Batch 1, one rank, MHA (the fused-RoPE attention), folded norm gains, the Phi-3-mini
+        widths the launch is instantiated for: the persistent launch (every layer + the LM head;
+        decode_b1.hip)."""
         c, o = self.cfg, self.ops
         return (_DECODE_B1 and B == 1 and self.tp.size == 1 and self.unit_gains and self.hl == self.kl
                 and _FUSED_ROPE_DECODE and hasattr(o, "decode_b1") and c.head_dim in (64, 96, 128)
-                and c.hidden % 512 == 0 and c.ffn % 512 == 0 and c.vocab % 16 == 0
+                and c.hidden == 3072 and c.ffn == 8192 and c.vocab % 16 == 0  # the instantiated shape
                 and self.hl * c.head_dim == c.hidden and self.cache is not None)
 
     def _b1_table(self) -> torch.Tensor:

@@ -260,6 +260,135 @@ __device__ __forceinline__ bool gemv_item(const bf16_t* A, const bf16_t* W, bf16
   return true;
 }
 
+// All of this workgroup's items of one GEMV phase (vb = vb0, vb0 + stride, ...), software-pipelined:
+// the activation row (the same for every item of the phase) is loaded ONCE, after `wait`; each
+// item's weights are requested one item ahead (two register buffers), so the next item's weight
+// stream is in flight while this one's FMAs and stores run — the seam of gemv_item, where every
+// item starts from an empty pipe, happens once per phase instead of once per item. Needs one load
+// round per item: (K / 512) / KS == U. Same per-row FMA order and reductions as gemv_item.
+template <int EPI, int R, int U, int KS, typename Wait, typename After>
+__device__ __forceinline__ bool gemv_phase(const bf16_t* A, const bf16_t* W, bf16_t* C, const bf16_t* resid, int N,
+                                           int K, float eps, int vb0, int stride, int nvb, Wait&& wait,
+                                           After&& after) {
+  static_assert(EPI != EPI_SWIGLU || R == 4, "SwiGLU waves own 2 gate + 2 up rows");
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int ks = KS == 2 ? (w & 1) : 0;
+  const int kb0 = ks * U;  // (K / 512) == KS * U (host-checked)
+  if (nvb <= 0) return true;
+  auto rows_of = [&](int vb, int (&rows)[R]) {
+    const int wg = (vb * 4 + w) / KS;
+    if constexpr (EPI == EPI_SWIGLU) {
+      const int g = wg >> 3, t = wg & 7;
+#pragma unroll
+      for (int r = 0; r < R; ++r) rows[r] = g * 32 + 2 * t + (r & 1) + (r >> 1) * 16;
+    } else {
+#pragma unroll
+      for (int r = 0; r < R; ++r) rows[r] = wg * R + r;
+    }
+  };
+  auto issue = [&](int vb, u32x4_t (&wv)[U][R]) {
+    int rows[R];
+    rows_of(vb, rows);
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const bf16_t* wr = W + (size_t)min(rows[r], N - 1) * K + kb0 * 512 + lane * 8;
+#pragma unroll
+      for (int u = 0; u < U; ++u) wv[u][r] = __builtin_nontemporal_load((const u32x4_t*)(wr + u * 512));
+    }
+  };
+  u32x4_t wa[U][R], wb[U][R], av[U];
+  issue(vb0, wa);
+  if (!wait()) return false;
+  const __amdgpu_buffer_rsrc_t ra = rsrc(A, K * 2);
+#pragma unroll
+  for (int u = 0; u < U; ++u) av[u] = ld16_sc1(ra, (unsigned)((kb0 + u) * 512 + lane * 8) * 2u);
+  const bool rms = eps > 0.f;
+  auto finish = [&](int vb, const u32x4_t (&wv)[U][R]) {
+    float acc[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) acc[r] = 0.f;
+    float ss = 0.f;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      float a[8];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        a[2 * e] = bf2f((bf16_t)(av[u][e] & 0xffff));
+        a[2 * e + 1] = bf2f((bf16_t)(av[u][e] >> 16));
+      }
+      if (rms) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) ss = fmaf(a[2 * e], a[2 * e], fmaf(a[2 * e + 1], a[2 * e + 1], ss));
+      }
+#pragma unroll
+      for (int r = 0; r < R; ++r)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          acc[r] = fmaf(bf2f((bf16_t)(wv[u][r][e] & 0xffff)), a[2 * e], acc[r]);
+          acc[r] = fmaf(bf2f((bf16_t)(wv[u][r][e] >> 16)), a[2 * e + 1], acc[r]);
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r) acc[r] = wave_sum(acc[r]);
+    if (rms) ss = wave_sum(ss);
+    bool lead = true;
+    if constexpr (KS == 2) {
+      __shared__ float xch[4][R + 1];
+      if (lane == 0) {
+#pragma unroll
+        for (int r = 0; r < R; ++r) xch[w][r] = acc[r];
+        xch[w][R] = ss;
+      }
+      __syncthreads();
+      lead = ks == 0;
+      if (lead) {
+#pragma unroll
+        for (int r = 0; r < R; ++r) acc[r] += xch[w + 1][r];
+        ss += xch[w + 1][R];
+      }
+      __syncthreads();
+    }
+    if (rms) {
+      const float inv = rsqrtf(ss / K + eps);
+#pragma unroll
+      for (int r = 0; r < R; ++r) acc[r] *= inv;
+    }
+    if (lane != 0 || !lead) return;
+    int rows[R];
+    rows_of(vb, rows);
+    if constexpr (EPI == EPI_SWIGLU) {
+      const int wg = vb * 4 + w, g = wg >> 3, t = wg & 7;
+      const int o = g * 16 + 2 * t;
+      if (o < N / 2) st_u32(C + o, pack_bf2(silu(acc[0]) * acc[2], silu(acc[1]) * acc[3]));
+    } else if constexpr (EPI == EPI_RESID) {
+#pragma unroll
+      for (int r = 0; r < R; ++r)
+        if (rows[r] < N) st_bf(C + rows[r], f2bf(acc[r] + bf2f(ld_bf(resid + rows[r]))));
+    } else if constexpr (R % 2 == 0) {
+#pragma unroll
+      for (int r = 0; r < R; r += 2) {
+        const int n = rows[r];
+        if (n + 1 < N) st_u32(C + n, pack_bf2(acc[r], acc[r + 1]));
+        else if (n < N) st_bf(C + n, f2bf(acc[r]));
+      }
+    } else {
+#pragma unroll
+      for (int r = 0; r < R; ++r)
+        if (rows[r] < N) st_bf(C + rows[r], f2bf(acc[r]));
+    }
+  };
+  for (int i = 0; i < nvb; i += 2) {
+    if (i + 1 < nvb) issue(vb0 + (i + 1) * stride, wb);
+    finish(vb0 + i * stride, wa);
+    after(vb0 + i * stride);
+    if (i + 1 >= nvb) break;
+    if (i + 2 < nvb) issue(vb0 + (i + 2) * stride, wa);
+    finish(vb0 + (i + 1) * stride, wb);
+    after(vb0 + (i + 1) * stride);
+  }
+  return true;
+}
+
 // Rows per wave of the QKV / O items: 3 (12-row items) where the head width allows it — the Phi-3
 // QKV projection is then 768 items = exactly 3 per workgroup on 256 CUs and the O projection 256 =
 // one each (16-row items left a 2.25-item imbalance); 4 otherwise (items must not straddle heads).
@@ -559,57 +688,49 @@ __global__ void __launch_bounds__(B1_NT, 1) decode_b1_kernel(B1Args a) {
   for (int li = a.l0; li < a.l1; ++li) {
     const B1Layer Ly = a.layers[li];
     const int lr = li - a.l0;  // layer index within this launch: counters are per launch
-    // P1: QKV (input RMSNorm fused; gain folded into the weights)
-    for (int vb = wg; vb < nq; vb += G) {
-      const bool ok = gemv_item<EPI_NONE, RQ, 6, 1>(a.x, Ly.wqkv, a.qkv, nullptr, 3 * Hd, Hd, a.eps, vb, [&]() {
-        return lr == 0 || vb != wg || wait_ge(sync, S_DN, 8, (unsigned)ndn * lr, 0x200u + li);
-      });
-      if (!ok) return;
-      const int head = ((vb * IQ) % Hd) / D;  // IQ rows of one section, inside one head
-      publish(sync + (S_HEAD + head) * CL, 1u);
-    }
+    // P1: QKV (input RMSNorm fused; gain folded into the weights); each item publishes its head
+    auto nitems = [&](int n) { return wg < n ? (n - wg + G - 1) / G : 0; };
+    auto none = [](int) {};
+    if (!gemv_phase<EPI_NONE, RQ, 6, 1>(
+            a.x, Ly.wqkv, a.qkv, nullptr, 3 * Hd, Hd, a.eps, wg, G, nitems(nq),
+            [&]() { return lr == 0 || wait_ge(sync, S_DN, 8, (unsigned)ndn * lr, 0x200u + li); },
+            [&](int vb) { publish(sync + (S_HEAD + ((vb * IQ) % Hd) / D) * CL, 1u); }))
+      return;
     // P2: attention (head, split) items; each waits for its own head only
     for (int it = wg; it < na; it += G) {
       if (!attn_item<D>(a, Ly, it / a.nsplit, it % a.nsplit, lr)) return;
     }
     // P3: O projection + residual (x += attn W_o^T)
-    unsigned mine = 0;
-    for (int vb = wg; vb < no; vb += G, ++mine) {
-      if (!gemv_item<EPI_RESID, RQ, 6, 1>(a.attn, Ly.wo, a.x, a.x, Hd, Hd, 0.f, vb, [&]() {
-            return vb != wg || wait_ge(sync, S_HEADS, 1, (unsigned)H * (lr + 1), 0x300u + li);
-          }))
-        return;
-    }
-    publish(sync + (S_O + shard) * CL, mine);
-    // P4: gate/up + SwiGLU (norm fused)
-    mine = 0;
-    for (int vb = wg; vb < ngu; vb += G, ++mine) {
+    if (!gemv_phase<EPI_RESID, RQ, 6, 1>(
+            a.attn, Ly.wo, a.x, a.x, Hd, Hd, 0.f, wg, G, nitems(no),
+            [&]() { return wait_ge(sync, S_HEADS, 1, (unsigned)H * (lr + 1), 0x300u + li); }, none))
+      return;
+    publish(sync + (S_O + shard) * CL, (unsigned)nitems(no));
+    // P4: gate/up + SwiGLU (norm fused): 4 items of 96 KB each, one at a time (two buffers of
+    // 4 rows x 6 KiB per lane would not fit beside the activation row)
+    for (int vb = wg; vb < ngu; vb += G) {
       if (!gemv_item<EPI_SWIGLU, 4, 6, 1>(a.x, Ly.wgu, a.act, nullptr, 2 * F, Hd, a.eps, vb, [&]() {
             return vb != wg || wait_ge(sync, S_O, 8, (unsigned)no * (lr + 1), 0x400u + li);
           }))
         return;
     }
-    publish(sync + (S_GU + shard) * CL, mine);
+    publish(sync + (S_GU + shard) * CL, (unsigned)nitems(ngu));
     // P5: down projection + residual (K split over 2 waves)
-    mine = 0;
-    for (int vb = wg; vb < ndn; vb += G, ++mine) {
-      if (!gemv_item<EPI_RESID, 2, 8, 2>(a.act, Ly.wdown, a.x, a.x, Hd, F, 0.f, vb, [&]() {
-            return vb != wg || wait_ge(sync, S_GU, 8, (unsigned)ngu * (lr + 1), 0x500u + li);
-          }))
-        return;
-    }
-    publish(sync + (S_DN + shard) * CL, mine);
+    if (!gemv_phase<EPI_RESID, 2, 8, 2>(
+            a.act, Ly.wdown, a.x, a.x, Hd, F, 0.f, wg, G, nitems(ndn),
+            [&]() { return wait_ge(sync, S_GU, 8, (unsigned)ngu * (lr + 1), 0x500u + li); }, none))
+      return;
+    publish(sync + (S_DN + shard) * CL, (unsigned)nitems(ndn));
   }
   // P6: LM head (final RMSNorm fused) over the last layer's output
   if (a.lm_head) {
     const int nl = a.l1 - a.l0;
     const int nv = a.V / 16;
-    for (int vb = wg; vb < nv; vb += G) {
-      if (!gemv_item<EPI_NONE, 4, 6, 1>(a.x, a.lm_head, a.logits, nullptr, a.V, Hd, a.eps, vb, [&]() {
-            return vb != wg || wait_ge(sync, S_DN, 8, (unsigned)ndn * nl, 0x600u);
-          }))
-        return;
-    }
+    const int n6 = wg < nv ? (nv - wg + G - 1) / G : 0;
+    if (!gemv_phase<EPI_NONE, 4, 6, 1>(
+            a.x, a.lm_head, a.logits, nullptr, a.V, Hd, a.eps, wg, G, n6,
+            [&]() { return wait_ge(sync, S_DN, 8, (unsigned)ndn * nl, 0x600u); }, [](int) {}))
+      return;
   }
 }
 
@@ -641,6 +762,9 @@ DA_EXPORT int da_decode_b1(const void* layers, int l0, int l1, void* x, void* qk
     return (int)hipErrorInvalidValue;
   if (l0 < 0 || l1 <= l0 || grid < 1 || nsplit < 1 || chunk < 64 || chunk % 64) return (int)hipErrorInvalidValue;
   if (Hd != H * D || Hd % 512 || F % 512 || D % 16 || F % 16) return (int)hipErrorInvalidValue;
+  // one register round of weights per item: K = 6 x 512 (hidden) and 2 x 8 x 512 (FFN): the
+  // Phi-3-mini shape this launch is instantiated for (other models keep the per-kernel path)
+  if (Hd / 512 != 6 || F / 512 != 16) return (int)hipErrorInvalidValue;
   if ((long long)chunk * nsplit < 1 || H > 4096) return (int)hipErrorInvalidValue;
   if (lm_head && (!logits || V < 16 || V % 16)) return (int)hipErrorInvalidValue;
   hipStream_t s = (hipStream_t)stream;

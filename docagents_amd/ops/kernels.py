@@ -1000,7 +1000,7 @@ def decode_b1(layers, l0: int, l1: int, x, qkv, attn, act, lens, slot, pre, pos,
     _req(layers.dtype == torch.int64 and layers.is_cuda and layers.dim() == 2 and layers.shape[1] == 6
          and 0 <= l0 < l1 <= layers.shape[0], "decode_b1: layer table")
     _req(cos_sin.dtype == torch.float32 and cos_sin.is_contiguous() and cos_sin.shape[1] == D // 2, "cos_sin")
-    _req(Hd % 512 == 0 and F % 512 == 0 and D in (64, 96, 128), "decode_b1 shapes")
+    _req(Hd == 3072 and F == 8192 and D in (64, 96, 128), "decode_b1: instantiated for hidden 3072 / FFN 8192")
     max_len = max_seq if max_len is None else max_len
     want = max_len * Hd // D / 768  # decode_attn's auto chunk for B = 1
     chunk = 512
