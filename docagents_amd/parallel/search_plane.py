@@ -303,10 +303,13 @@ class SearchPlane:
         with self.cv:
             self.cv.notify_all()
         if self._listener is not None:
-            try:
-                self._listener.close()
-            except OSError:
-                pass
+            # shutdown first: close() alone neither wakes a thread blocked in accept() nor releases
+            # the port while that call holds the socket (a restarted rank could not rebind)
+            for fn in (lambda: self._listener.shutdown(socket.SHUT_RDWR), self._listener.close):
+                try:
+                    fn()
+                except OSError:
+                    pass
         for p in self.peers.values():
             p.close()
         for c in list(self._conns):

@@ -1,0 +1,119 @@
+"""The owner-routed search plane (parallel/search_plane.py) in one process, two ranks over real
+sockets: exact merged results, routing only to owner shards, a HUNG shard (accepts, never answers)
+failing only the searches that need it (by timeout, naming it), and a restarted shard rejoining
+without coordination."""
+import socket
+import threading
+import time
+
+import numpy as np
+import pytest
+import torch
+
+from docagents_amd.index.flat import FlatIndex
+from docagents_amd.parallel.search_plane import SearchPlane, ShardUnavailable, owner_of
+
+
+def _unit(n, d, seed):
+    x = np.random.default_rng(seed).standard_normal((n, d)).astype(np.float32)
+    return x / np.linalg.norm(x, axis=1, keepdims=True)
+
+
+def _docs(world, per, prefix="sp"):
+    out, i = {r: [] for r in range(world)}, 0
+    while min(len(v) for v in out.values()) < per:
+        d = f"{prefix}-{i}"
+        i += 1
+        r = owner_of(d, world)
+        if len(out[r]) < per:
+            out[r].append(d)
+    return out
+
+
+def _pair(timeout_s=2.0, retry_s=0.2):
+    d = 32
+    idx = [FlatIndex(d, "cpu"), FlatIndex(d, "cpu")]
+    planes = [SearchPlane(idx[r], r, 2, timeout_s=timeout_s, retry_s=retry_s) for r in range(2)]
+    addrs = [p.listen() for p in planes]
+    for p in planes:
+        p.connect(addrs).start()
+    docs = _docs(2, 4)
+    X = {}
+    for r in range(2):
+        for j, doc in enumerate(docs[r]):
+            v = _unit(3, d, 100 * r + j)
+            X[doc] = v
+            idx[r].add(doc, np.arange(3) + 1000 * r + 10 * j, torch.from_numpy(v))
+    return planes, idx, docs, X
+
+
+def _exact(q, docs, X, k):
+    rows = [(float(X[dd][i] @ q), dd, i) for dd in docs for i in range(3)]
+    return sorted((s for s, _, _ in rows), reverse=True)[:k]
+
+
+def test_plane_exact_and_routed():
+    planes, idx, docs, X = _pair()
+    try:
+        q = _unit(2, 32, 7)
+        flt = [docs[0][:2] + docs[1][:1], docs[0][2:3]]  # row 1 needs only rank 0's shard
+        s, keys = planes[1].submit(q, 4, -1.0, flt).result(10)
+        for b in range(2):
+            got = sorted(s[b][keys[b] >= 0].tolist(), reverse=True)
+            assert np.allclose(got, _exact(q[b], flt[b], X, 4), atol=2e-2)
+        st = planes[1].stats
+        assert st["remote_parts"] == 1 and st["local_parts"] == 1  # one request per owner shard
+        s2, k2 = planes[0].submit(q[:1], 3, -1.0, [docs[0]]).result(10)
+        assert planes[0].stats["remote_parts"] == 0  # all documents local: no network hop
+        assert (k2 >= 0).all()
+        # unknown / empty filter: nothing to match, no request sent
+        s3, k3 = planes[0].submit(q[:1], 3, -1.0, [[]]).result(10)
+        assert (k3 < 0).all()
+    finally:
+        for p in planes:
+            p.stop(timeout=2)
+
+
+def test_hung_shard_times_out_alone_and_restarted_shard_rejoins():
+    planes, idx, docs, X = _pair(timeout_s=1.0, retry_s=0.1)
+    q = _unit(1, 32, 9)
+    try:
+        # rank 1's shard server "hangs": replace it by a socket that accepts and never answers
+        addr = planes[0].addrs[1]
+        planes[0].peers[1].close()  # the peer process "died": its connections are gone
+        planes[1].stop(timeout=2)
+        time.sleep(0.2)
+        hung = socket.socket()
+        hung.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)
+        hung.bind(addr)
+        hung.listen(8)
+        conns = []
+        threading.Thread(target=lambda: conns.append(hung.accept()), daemon=True).start()
+        t0 = time.monotonic()
+        with pytest.raises(Exception) as ei:
+            planes[0].submit(q, 3, -1.0, [docs[0][:1] + docs[1][:1]]).result(10)
+        assert "[1]" in str(ei.value) or "shard 1" in str(ei.value), ei.value
+        assert time.monotonic() - t0 < 5
+        # searches that only need rank 0 are unaffected
+        s, k = planes[0].submit(q, 3, -1.0, [docs[0]]).result(10)
+        assert (k >= 0).all()
+        hung.close()
+        for c, _ in conns:
+            c.close()
+        # rank 1 comes back on the same address: the next request reconnects
+        planes[1] = SearchPlane(idx[1], 1, 2, port=addr[1], timeout_s=2.0)
+        planes[1].listen()
+        planes[1].connect(planes[0].addrs).start()
+        time.sleep(0.3)
+        deadline = time.monotonic() + 5
+        while True:
+            try:
+                s, k = planes[0].submit(q, 3, -1.0, [docs[1]]).result(10)
+                break
+            except (ShardUnavailable, TimeoutError):
+                assert time.monotonic() < deadline
+                time.sleep(0.2)
+        assert (k >= 0).all() and planes[0].health()["shards_down"] == []
+    finally:
+        for p in planes:
+            p.stop(timeout=2)
