@@ -1,6 +1,7 @@
 # BASELINE configs and rehearsals through bench.py on the box's one GPU: bash scripts/gpu_configs.sh CASE
 #   c3        Llama-3-8B summarizer + QA, PDF ingest (gateway PDF extraction in the timed ingest path)
 #   c4        BGE-large embedder, 1.25M-chunk shard (= 10M sharded 8-way), Phi-3-mini QA
+#   c4f16     the same with the embedder in fp16 (BASELINE config 4 "BGE-large fp16 embedder")
 #   llama70b  Llama-3-70B QA on one GPU (TP=1), BGE-large
 #   rank2     2 ranks sharing the GPU (gloo collectives): the multi-rank bench path
 #   tp2       Phi-3-mini TP=2 + IVFFlat, 2 ranks sharing the GPU (xGMI IPC all-reduce kernel, gloo)
@@ -21,6 +22,8 @@ run() {  # name timeout cmd...
 case ${1:-c4} in
   c3) run c3 900 python bench.py --llm llama3-8b --pdf-ingest ;;
   c4) run c4 600 python bench.py --enc bge-large --index-rows 1250000 --latency-reps 3 --ingest-docs 32 ;;
+  c4f16) run c4f16 600 python bench.py --enc bge-large --enc-dtype fp16 --index-rows 1250000 --latency-reps 3 \
+           --ingest-docs 32 ;;
   llama70b) run llama70b 1200 python bench.py --llm llama3-70b --enc bge-large --batch 16 --steps 2 --warmup 1 \
               --latency-reps 2 --ingest-docs 4 --ingest-batches 1 ;;
   rank2) DA_DIST_BACKEND=gloo run rank2 900 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
