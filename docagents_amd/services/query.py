@@ -143,11 +143,13 @@ async def query_handler(deps, body: bytes) -> Response:
     t3 = time.perf_counter()
     try:
         if getattr(deps.llm, "supports_chunks", False) and hasattr(deps.store, "chunks_by_keys") and results:
-            toks = await deps.store.chunks_by_keys([r.chunk.key for r in results])
-            chunks = []
-            for r in results:
-                blob = toks.get(r.chunk.key, (None, None))[1]
-                chunks.append((r.chunk.text, np.frombuffer(blob, dtype=np.int32).tolist() if blob else None))
+            if all(getattr(r, "tokens_loaded", False) for r in results):  # read with the hits
+                blobs = [r.tokens for r in results]
+            else:
+                toks = await deps.store.chunks_by_keys([r.chunk.key for r in results])
+                blobs = [toks.get(r.chunk.key, (None, None))[1] for r in results]
+            chunks = [(r.chunk.text, np.frombuffer(b, dtype=np.int32).tolist() if b else None)
+                      for r, b in zip(results, blobs)]
             answer, confidence = await deps.llm.answer_chunks(req.question, chunks, quality)
         else:
             answer, confidence = await deps.llm.answer(req.question, context, quality)

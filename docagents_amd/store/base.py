@@ -60,6 +60,10 @@ class SearchResult:
     chunk: Chunk
     score: float
     summary: Summary
+    # the chunk's decoder token ids (int32 bytes, None: never tokenized) when the store read them
+    # with the hit (tokens_loaded), so the Answer prompt needs no second lookup
+    tokens: bytes | None = None
+    tokens_loaded: bool = False
 
 
 class Store(Protocol):

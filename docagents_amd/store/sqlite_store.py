@@ -248,20 +248,29 @@ class CompositeStore:
         return vec, await self._results(hits)
 
     async def _results(self, hits) -> list[SearchResult]:
-        keys = [kk for kk, _ in hits]
-        found = await self.chunks_by_keys(keys)
+        """Chunks + their documents' summaries + decoder tokens of the hits in ONE query (one thread
+        hop): under load every extra hop is a GIL / executor round trip on the question's path."""
+        if not hits:
+            return []
+        keys = tuple(int(kk) for kk, _ in hits)
+        qs = ",".join("?" * len(keys))
+        rows = await self._run(
+            self.meta.q,
+            f"SELECT c.key, c.id, c.document_id, c.ord, c.text, c.token_count, c.dec_tokens, s.document_id, "
+            f"s.summary, s.key_points FROM chunks c LEFT JOIN summaries s ON s.document_id = c.document_id "
+            f"WHERE c.key IN ({qs})", keys)
+        found = {r[0]: r for r in rows}
         sums: dict[str, Summary] = {}
         out = []
         for key, score in hits:
-            if key not in found:
+            r = found.get(int(key))
+            if r is None:
                 continue
-            ch, _ = found[key]
-            if ch.document_id not in sums:
-                try:
-                    sums[ch.document_id] = await self.get_summary(ch.document_id)
-                except SummaryNotFound:
-                    sums[ch.document_id] = Summary(ch.document_id, "", [])
-            out.append(SearchResult(ch, float(score), sums[ch.document_id]))
+            doc = r[2]
+            if doc not in sums:
+                sums[doc] = Summary(doc, r[8], json.loads(r[9] or "[]")) if r[7] is not None else Summary(doc, "", [])
+            out.append(SearchResult(Chunk(r[1], doc, r[3], r[4], r[5], r[0]), float(score), sums[doc],
+                                    tokens=r[6], tokens_loaded=True))
         return out
 
     async def close(self):

@@ -159,3 +159,43 @@ def test_concurrent_pipeline_under_asyncio_debug(tmp_path, monkeypatch):
         warnings.simplefilter("error", RuntimeWarning)
         statuses = asyncio.run(go(), debug=True)
     assert statuses == ["ready"] * 12
+
+
+def test_search_results_resolved_in_one_query(tmp_path):
+    """top_k hits -> chunks + their document's summary (or an empty one) + decoder tokens, in hit
+    order, from ONE metadata query (store/sqlite_store.py _results)."""
+    import numpy as np
+
+    from docagents_amd.store.base import Chunk, Embedding, Summary
+
+    async def go():
+        meta = SqliteMeta(str(tmp_path / "m.sqlite3"))
+        store = CompositeStore(meta, SqliteVectors(meta), min_similarity=-1.0)
+        a = await store.create_document("a.txt")
+        b = await store.create_document("b.txt")
+        ca = await store.save_chunks(a.id, [Chunk(index=i, text=f"a{i}", token_count=1) for i in range(3)])
+        cb = await store.save_chunks(b.id, [Chunk(index=0, text="b0", token_count=1)])
+        await store.save_summary(a.id, Summary(a.id, "sum a", ["p1", "p2"]))
+        await store.save_chunk_tokens([(ca[1].id, [7, 8, 9])])
+        rng = np.random.default_rng(0)
+        vecs = {c.id: rng.standard_normal(16).astype(np.float32) for c in ca + cb}
+        vecs = {k: v / np.linalg.norm(v) for k, v in vecs.items()}
+        await store.save_embeddings([Embedding(cid, v, "m") for cid, v in vecs.items()])
+        calls = []
+        orig = meta.q
+        meta.q = lambda sql, args=(): (calls.append(sql), orig(sql, args))[1]
+        res = await store.top_k([a.id, b.id], vecs[ca[1].id], 4)
+        assert sum(1 for q in calls if "FROM chunks" in q or "FROM summaries" in q) == 1
+        assert res[0].chunk.id == ca[1].id and res[0].score > 0.99
+        assert {r.chunk.id for r in res} == {c.id for c in ca + cb}
+        for r in res:
+            assert r.tokens_loaded
+            if r.chunk.document_id == a.id:
+                assert (r.summary.summary, r.summary.key_points) == ("sum a", ["p1", "p2"])
+            else:
+                assert (r.summary.document_id, r.summary.summary, r.summary.key_points) == (b.id, "", [])
+        assert np.frombuffer(res[0].tokens, dtype=np.int32).tolist() == [7, 8, 9]
+        assert all(r.tokens is None for r in res[1:])
+        assert await store.top_k([a.id], vecs[ca[0].id], 0) == []
+        meta.close()
+    asyncio.run(go())
