@@ -165,6 +165,7 @@ class _Peer:
         threading.Thread(target=self._read_loop, args=(s,), name=f"plane-peer-{self.rank}", daemon=True).start()
 
     def send(self, rid: int, msg: dict, on_reply, on_fail):
+        sock = None
         try:
             with self.lock:
                 if self.sock is None:
@@ -176,6 +177,10 @@ class _Peer:
             on_fail(e)
         except OSError as e:
             self._down(sock, e)
+        except Exception as e:  # noqa: BLE001 - e.g. an unserialisable request: fails this part only
+            with self.lock:
+                self.pending.pop(rid, None)
+            on_fail(e)
 
     def _read_loop(self, sock):
         try:
@@ -425,6 +430,10 @@ class SearchPlane:
                     for r in pend:
                         self._part_done(sid, r, None, TimeoutError(
                             f"search shards {pend} did not answer within {self.timeout_s:.0f} s"))
+                        peer = self.peers.get(r)
+                        if peer is not None:  # a hung peer never replies: drop the callbacks (and rows)
+                            with peer.lock:
+                                peer.pending.pop(sid, None)
 
     def _fail_all(self, exc):
         for sid, s in list(self.searches.items()):

@@ -117,3 +117,30 @@ def test_hung_shard_times_out_alone_and_restarted_shard_rejoins():
     finally:
         for p in planes:
             p.stop(timeout=2)
+
+
+def test_timed_out_parts_leave_no_pending_callbacks():
+    planes, idx, docs, X = _pair(timeout_s=0.5, retry_s=0.1)
+    try:
+        addr = planes[0].addrs[1]
+        planes[0].peers[1].close()
+        planes[1].stop(timeout=2)
+        time.sleep(0.2)
+        hung = socket.socket()
+        hung.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)
+        hung.bind(addr)
+        hung.listen(8)
+        conns = []
+        threading.Thread(target=lambda: conns.append(hung.accept()), daemon=True).start()
+        q = _unit(1, 32, 3)
+        for _ in range(3):
+            with pytest.raises(TimeoutError):
+                planes[0].submit(q, 3, -1.0, [docs[1][:1]]).result(10)
+        time.sleep(0.3)
+        assert planes[0].peers[1].pending == {} and planes[0].searches == {}
+        hung.close()
+        for c, _ in conns:
+            c.close()
+    finally:
+        for p in planes:
+            p.stop(timeout=2)
