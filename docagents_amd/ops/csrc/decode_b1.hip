@@ -21,10 +21,14 @@
 //
 // Hand-off protocol (cdna_hip_programming.md §6 Guideline 16, table row 1 of MI355X_MICROARCH.md
 // § visibility): every handed-off byte (qkv, attention output, residual rows, SwiGLU output,
-// split partials) is STORED sc1 (write-through) and LOADED sc1 (buffer/global loads with the sc1
-// bit, never the scalar path); every storing wave drains (s_waitcnt vmcnt(0)) before the
-// workgroup barrier behind which ONE lane bumps the counter (agent-scope relaxed atomic add);
-// ONE wave polls the counter relaxed with s_sleep, then the workgroup barrier. Counters are
+// split partials) is STORED sc1 (write-through) and LOADED sc1 (global / buffer loads with the sc1
+// bit, never flat or scalar), in 4-, 8- or 16-B granules only — the sizes that row was measured
+// with — and each granule by ONE writer: a GEMV item's rows are gathered in LDS and leave as 8-B
+// words, an attention head's row as 16-B chunks, and 16-bit values are read as the 4-B word that
+// holds them (2-B sc1 stores from several workgroups into one line diverged after ~20 sampled
+// steps on the MI355X); every storing wave drains (s_waitcnt vmcnt(0)) before the workgroup
+// barrier behind which ONE lane bumps the counter (agent-scope relaxed atomic add); ONE wave polls
+// the counter relaxed with s_sleep, then the workgroup barrier. One workgroup per CU (occupancy 1). Counters are
 // cumulative over the launch (target = items x (layer + 1)) and zeroed by a memset node ahead of
 // every launch. Every spin is bounded: a timeout sets the error word, every workgroup leaves, and
 // the host raises (da_decode_b1_check) instead of hanging the GPU.
@@ -77,15 +81,23 @@ __device__ __forceinline__ unsigned ld_u32(const unsigned* p) {
   return __hip_atomic_load((unsigned*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 __device__ __forceinline__ float ld_f32(const float* p) { return __uint_as_float(ld_u32((const unsigned*)p)); }
-__device__ __forceinline__ bf16_t ld_bf(const bf16_t* p) {
-  return (bf16_t)__hip_atomic_load((unsigned short*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+__device__ __forceinline__ unsigned long long ld_u64(const void* p) {
+  return __hip_atomic_load((unsigned long long*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+// the two bf16 of the 4-B word holding element i (i even: low half)
+__device__ __forceinline__ unsigned ld_pair(const bf16_t* row, int i) { return ld_u32((const unsigned*)(row + (i & ~1))); }
+__device__ __forceinline__ bf16_t lo16(unsigned w) { return (bf16_t)(w & 0xffff); }
+__device__ __forceinline__ bf16_t hi16(unsigned w) { return (bf16_t)(w >> 16); }
 __device__ __forceinline__ void st_u32(void* p, unsigned v) {
   __hip_atomic_store((unsigned*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 __device__ __forceinline__ void st_f32(float* p, float v) { st_u32(p, __float_as_uint(v)); }
-__device__ __forceinline__ void st_bf(bf16_t* p, bf16_t v) {
-  __hip_atomic_store((unsigned short*)p, (unsigned short)v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+__device__ __forceinline__ void st_u64(void* p, unsigned long long v) {
+  __hip_atomic_store((unsigned long long*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// four fp32 results -> four bf16 in one 8-B word (element 0 lowest)
+__device__ __forceinline__ unsigned long long pack4(float a, float b, float c, float d) {
+  return (unsigned long long)pack_bf2(a, b) | ((unsigned long long)pack_bf2(c, d) << 32);
 }
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* base, int bytes) {
   return __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, bytes, 0x00020000);
@@ -93,6 +105,9 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* base, int byt
 // 16 B of handed-off data, sc1 (aux 16): bypasses this CU's L1, which other CUs' stores never refresh
 __device__ __forceinline__ u32x4_t ld16_sc1(__amdgpu_buffer_rsrc_t r, unsigned off) {
   return __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 16);
+}
+__device__ __forceinline__ void st16_sc1(__amdgpu_buffer_rsrc_t r, unsigned off, u32x4_t v) {
+  __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, 16);
 }
 
 __device__ __forceinline__ unsigned wave_sum_u(unsigned v) {
@@ -136,26 +151,22 @@ __device__ __forceinline__ bool wait_ge(unsigned* sync, int ctr_line, int nsh, u
 }
 
 // ------------------------------------------------------------------ GEMV item
-// gemm.hip gemv_kernel's body for one 4-wave item (vb), with (1) the first round's weight loads
-// issued before `wait` (the phase dependency) and (2) every activation / residual load and every
-// output store coherent (sc1). Same per-lane FMA order and wave reduction as gemv_kernel.
-// EPI_NONE: rows [wg R, wg R + R) -> C (R even: u32 pairs); EPI_SWIGLU: 2 gate + 2 up rows per wave
-// -> 2 outputs; EPI_RESID: C[n] = acc + resid[n] (resid may alias C: each row read before written).
+// gemm.hip gemv_kernel's body for one 4-wave gate/up + SwiGLU item (vb), with (1) the first round's
+// weight loads issued before `wait` (the phase dependency) and (2) the activation load and the
+// output store coherent (sc1). Same per-lane FMA order and wave reduction as gemv_kernel. Each wave
+// owns 2 gate + 2 up rows -> 2 adjacent outputs: one 4-B word, one writer.
 template <int EPI, int R, int U, int KS, typename Wait>
 __device__ __forceinline__ bool gemv_item(const bf16_t* A, const bf16_t* W, bf16_t* C, const bf16_t* resid, int N,
                                           int K, float eps, int vb, Wait&& wait) {
-  static_assert(EPI != EPI_SWIGLU || R == 4, "SwiGLU waves own 2 gate + 2 up rows");
+  static_assert(EPI == EPI_SWIGLU && R == 4, "the gate/up phase: 2 gate + 2 up rows per wave");
   const int lane = threadIdx.x & 63;
   const int wv = vb * 4 + (threadIdx.x >> 6);
   const int wg = wv / KS, ks = wv % KS;
   int rows[R];
-  if constexpr (EPI == EPI_SWIGLU) {
+  {
     const int g = wg >> 3, t = wg & 7;
 #pragma unroll
     for (int r = 0; r < R; ++r) rows[r] = g * 32 + 2 * t + (r & 1) + (r >> 1) * 16;
-  } else {
-#pragma unroll
-    for (int r = 0; r < R; ++r) rows[r] = wg * R + r;
   }
   const bf16_t* wr[R];
 #pragma unroll
@@ -235,28 +246,9 @@ __device__ __forceinline__ bool gemv_item(const bf16_t* A, const bf16_t* W, bf16
     for (int r = 0; r < R; ++r) acc[r] *= inv;
   }
   if (lane != 0 || !lead) return true;
-  if constexpr (EPI == EPI_SWIGLU) {
-    const int g = wg >> 3, t = wg & 7;
-    const int o = g * 16 + 2 * t;  // two adjacent outputs: one 4-B store
-    if (o < N / 2) st_u32(C + o, pack_bf2(silu(acc[0]) * acc[2], silu(acc[1]) * acc[3]));
-  } else if constexpr (EPI == EPI_RESID) {
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-      const int n = rows[r];
-      if (n < N) st_bf(C + n, f2bf(acc[r] + bf2f(ld_bf(resid + n))));
-    }
-  } else if constexpr (R % 2 == 0) {  // rows wg R .. + R - 1 start even: 4-B pairs
-#pragma unroll
-    for (int r = 0; r < R; r += 2) {
-      const int n = rows[r];
-      if (n + 1 < N) st_u32(C + n, pack_bf2(acc[r], acc[r + 1]));
-      else if (n < N) st_bf(C + n, f2bf(acc[r]));
-    }
-  } else {
-#pragma unroll
-    for (int r = 0; r < R; ++r)
-      if (rows[r] < N) st_bf(C + rows[r], f2bf(acc[r]));
-  }
+  const int g = wg >> 3, t = wg & 7;
+  const int o = g * 16 + 2 * t;  // two adjacent outputs: one 4-B store
+  if (o < N / 2) st_u32(C + o, pack_bf2(silu(acc[0]) * acc[2], silu(acc[1]) * acc[3]));
   return true;
 }
 
@@ -265,26 +257,26 @@ __device__ __forceinline__ bool gemv_item(const bf16_t* A, const bf16_t* W, bf16
 // item's weights are requested one item ahead (two register buffers), so the next item's weight
 // stream is in flight while this one's FMAs and stores run — the seam of gemv_item, where every
 // item starts from an empty pipe, happens once per phase instead of once per item. Needs one load
-// round per item: (K / 512) / KS == U. Same per-row FMA order and reductions as gemv_item.
+// round per item: (K / 512) / KS == U. Same per-row FMA order and reductions as gemv_kernel.
+// EPI_NONE / EPI_RESID: the item's NR = 4 R / KS contiguous rows are gathered in LDS (two buffers:
+// item parity) and lane 0 of wave 0 writes them as NR / 4 8-B words (RESID: after adding the
+// residual rows it reads the same way; resid may alias C) — N % NR == 0 (host-checked).
 template <int EPI, int R, int U, int KS, typename Wait, typename After>
 __device__ __forceinline__ bool gemv_phase(const bf16_t* A, const bf16_t* W, bf16_t* C, const bf16_t* resid, int N,
                                            int K, float eps, int vb0, int stride, int nvb, Wait&& wait,
                                            After&& after) {
-  static_assert(EPI != EPI_SWIGLU || R == 4, "SwiGLU waves own 2 gate + 2 up rows");
+  static_assert(EPI == EPI_NONE || EPI == EPI_RESID, "row outputs (the SwiGLU phase uses gemv_item)");
+  constexpr int NR = 4 / KS * R;  // rows per item
+  static_assert(NR % 4 == 0, "8-B output words");
+  __shared__ float s_out[2][NR];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int ks = KS == 2 ? (w & 1) : 0;
   const int kb0 = ks * U;  // (K / 512) == KS * U (host-checked)
   if (nvb <= 0) return true;
   auto rows_of = [&](int vb, int (&rows)[R]) {
     const int wg = (vb * 4 + w) / KS;
-    if constexpr (EPI == EPI_SWIGLU) {
-      const int g = wg >> 3, t = wg & 7;
 #pragma unroll
-      for (int r = 0; r < R; ++r) rows[r] = g * 32 + 2 * t + (r & 1) + (r >> 1) * 16;
-    } else {
-#pragma unroll
-      for (int r = 0; r < R; ++r) rows[r] = wg * R + r;
-    }
+    for (int r = 0; r < R; ++r) rows[r] = wg * R + r;
   };
   auto issue = [&](int vb, u32x4_t (&wv)[U][R]) {
     int rows[R];
@@ -303,7 +295,7 @@ __device__ __forceinline__ bool gemv_phase(const bf16_t* A, const bf16_t* W, bf1
 #pragma unroll
   for (int u = 0; u < U; ++u) av[u] = ld16_sc1(ra, (unsigned)((kb0 + u) * 512 + lane * 8) * 2u);
   const bool rms = eps > 0.f;
-  auto finish = [&](int vb, const u32x4_t (&wv)[U][R]) {
+  auto finish = [&](int vb, int par, const u32x4_t (&wv)[U][R]) {
     float acc[R];
 #pragma unroll
     for (int r = 0; r < R; ++r) acc[r] = 0.f;
@@ -353,37 +345,34 @@ __device__ __forceinline__ bool gemv_phase(const bf16_t* A, const bf16_t* W, bf1
 #pragma unroll
       for (int r = 0; r < R; ++r) acc[r] *= inv;
     }
-    if (lane != 0 || !lead) return;
-    int rows[R];
-    rows_of(vb, rows);
-    if constexpr (EPI == EPI_SWIGLU) {
-      const int wg = vb * 4 + w, g = wg >> 3, t = wg & 7;
-      const int o = g * 16 + 2 * t;
-      if (o < N / 2) st_u32(C + o, pack_bf2(silu(acc[0]) * acc[2], silu(acc[1]) * acc[3]));
-    } else if constexpr (EPI == EPI_RESID) {
+    if (lane == 0 && lead) {
 #pragma unroll
-      for (int r = 0; r < R; ++r)
-        if (rows[r] < N) st_bf(C + rows[r], f2bf(acc[r] + bf2f(ld_bf(resid + rows[r]))));
-    } else if constexpr (R % 2 == 0) {
+      for (int r = 0; r < R; ++r) s_out[par][(w / KS) * R + r] = acc[r];
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const int row0 = vb * NR;
+      if (row0 < N) {
 #pragma unroll
-      for (int r = 0; r < R; r += 2) {
-        const int n = rows[r];
-        if (n + 1 < N) st_u32(C + n, pack_bf2(acc[r], acc[r + 1]));
-        else if (n < N) st_bf(C + n, f2bf(acc[r]));
+        for (int c = 0; c < NR; c += 4) {
+          float v[4] = {s_out[par][c], s_out[par][c + 1], s_out[par][c + 2], s_out[par][c + 3]};
+          if constexpr (EPI == EPI_RESID) {
+            const unsigned long long rr = ld_u64(resid + row0 + c);
+            const unsigned r0 = (unsigned)rr, r1 = (unsigned)(rr >> 32);
+            v[0] += bf2f(lo16(r0)); v[1] += bf2f(hi16(r0)); v[2] += bf2f(lo16(r1)); v[3] += bf2f(hi16(r1));
+          }
+          st_u64(C + row0 + c, pack4(v[0], v[1], v[2], v[3]));
+        }
       }
-    } else {
-#pragma unroll
-      for (int r = 0; r < R; ++r)
-        if (rows[r] < N) st_bf(C + rows[r], f2bf(acc[r]));
     }
   };
   for (int i = 0; i < nvb; i += 2) {
     if (i + 1 < nvb) issue(vb0 + (i + 1) * stride, wb);
-    finish(vb0 + i * stride, wa);
+    finish(vb0 + i * stride, 0, wa);
     after(vb0 + i * stride);
     if (i + 1 >= nvb) break;
     if (i + 2 < nvb) issue(vb0 + (i + 2) * stride, wa);
-    finish(vb0 + (i + 1) * stride, wb);
+    finish(vb0 + (i + 1) * stride, 1, wb);
     after(vb0 + (i + 1) * stride);
   }
   return true;
@@ -423,6 +412,13 @@ __device__ __forceinline__ bool attn_item(const B1Args& a, const B1Layer& Ly, in
   __shared__ float swm[4], swl[4];
   __shared__ float skn[D], svn[D], ssn;
   __shared__ int s_last;
+  __shared__ __attribute__((aligned(16))) bf16_t s_ao[D];  // the head's output row, leaves as 16-B chunks
+  static_assert(D % 8 == 0 && D / 8 <= B1_NT, "16-B chunks of a head row");
+  const __amdgpu_buffer_rsrc_t r_attn = rsrc(a.attn + hk * D, D * 2);
+  auto store_head = [&]() {  // s_ao written by threads d < D; one writer per 16-B chunk
+    __syncthreads();
+    if (threadIdx.x < D / 8) st16_sc1(r_attn, threadIdx.x * 16u, *(const u32x4_t*)&s_ao[threadIdx.x * 8]);
+  };
 
   const int H = a.H, nsplit = a.nsplit, max_seq = a.max_seq;
   const int L = a.lens[0];
@@ -468,12 +464,14 @@ __device__ __forceinline__ bool attn_item(const B1Args& a, const B1Layer& Ly, in
     const bf16_t* row = a.qkv;
     const int qi = min(tid, D - 1), d = qi;
     const bf16_t* hp = row + hk * D;
-    const bf16_t rq1 = ld_bf(hp + (d & ~1)), rq2 = ld_bf(hp + (d | 1));
+    const unsigned wq = ld_pair(hp, d);
+    const bf16_t rq1 = lo16(wq), rq2 = hi16(wq);
     const float* csp = a.cs + ((size_t)(L - 1) * HALF + (d >> 1)) * 2;
     const f32x2_t rcs = *(const f32x2_t*)csp;
     const bf16_t* kr = row + (size_t)(H + hk) * D;
     const bf16_t* vr = row + (size_t)(2 * H + hk) * D;
-    const bf16_t rk1 = ld_bf(kr + (d & ~1)), rk2 = ld_bf(kr + (d | 1)), nv = ld_bf(vr + d);
+    const unsigned wk = ld_pair(kr, d), wv = ld_pair(vr, d);
+    const bf16_t rk1 = lo16(wk), rk2 = hi16(wk), nv = (d & 1) ? hi16(wv) : lo16(wv);
     const float pc = rcs[0], ps = rcs[1];
     if (tid < D) sq[d] = rot2(bf2f(rq1), bf2f(rq2), pc, ps, d) * a.sl2e;
     if (own_new && tid < D) {
@@ -621,12 +619,13 @@ __device__ __forceinline__ bool attn_item(const B1Args& a, const B1Layer& Ly, in
       ls += f;
     }
     if (nsplit == 1) {
-      st_bf(a.attn + hk * D + d, f2bf(ls > 0.f ? o / ls : 0.f));
+      s_ao[d] = f2bf(ls > 0.f ? o / ls : 0.f);
     } else {
       st_f32(a.po + pidx * D + d, o);
       if (d == 0) { st_f32(a.pm + pidx, M); st_f32(a.pl + pidx, ls); }
     }
   }
+  if (nsplit == 1) store_head();
   // this split's partial is out (sc1, drained) -> ticket; the last split of the head merges
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
@@ -668,8 +667,9 @@ __device__ __forceinline__ bool attn_item(const B1Args& a, const B1Layer& Ly, in
         }
         M = mx;
       }
-      st_bf(a.attn + hk * D + d, f2bf(lsum > 0.f ? o / lsum : 0.f));
+      s_ao[d] = f2bf(lsum > 0.f ? o / lsum : 0.f);
     }
+    store_head();
   }
   publish(a.sync + S_HEADS * CL, 1u);
   return true;

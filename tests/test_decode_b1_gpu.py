@@ -50,22 +50,26 @@ def test_decode_b1_step_logits_bit_identical():
                 r = g.generate([prompt], 3)
         outs.append(r[0])
     assert outs[0].tokens == outs[1].tokens
-    # one decode step from identical states: the logits must be the same bits
-    st = {}
-    for m, persistent in ((a, True), (b, False)):
-        s_ = LM.DecodeState(m, 1, 8, 0.0, 0)
-        s_.tokens.fill_(1234); s_.pos.fill_(500); s_.lens.fill_(501); s_.slot.fill_(1); s_.active.fill_(1)
-        if persistent:
-            m.decode_step(s_)
-        else:
-            with _PerKernel():
+    # one decode step from identical states at several context lengths (split layouts: 64-key
+    # splits up to 448-key ones, the new token in the first / a middle / the last split): the logits
+    # must be the same bits, repeatedly (a stale hand-off shows up as an occasional mismatch)
+    for rep, L in enumerate((501, 1500, 2777, 3000, 3583, 2777)):
+        st = {}
+        for m, persistent in ((a, True), (b, False)):
+            s_ = LM.DecodeState(m, 1, 8, 0.0, 0)
+            s_.tokens.fill_(1234 + rep); s_.pos.fill_(L - 1); s_.lens.fill_(L); s_.slot.fill_(1); s_.active.fill_(1)
+            if persistent:
                 m.decode_step(s_)
-        torch.cuda.synchronize()
-        st[persistent] = (s_.logits.clone(), s_.x.clone(), m.cache.buf[:, :, 1, :, 500].clone())
-    assert K.decode_b1_error() == 0
-    assert torch.equal(st[True][0], st[False][0]), (st[True][0].float() - st[False][0].float()).abs().max()
-    assert torch.equal(st[True][1], st[False][1])
-    assert torch.equal(st[True][2], st[False][2])  # the new token's k / v cache rows
+            else:
+                with _PerKernel():
+                    m.decode_step(s_)
+            torch.cuda.synchronize()
+            st[persistent] = (s_.logits.clone(), s_.x.clone(), m.cache.buf[:, :, 1, :, L - 1].clone())
+        assert K.decode_b1_error() == 0
+        d = (st[True][0].float() - st[False][0].float()).abs().max()
+        assert torch.equal(st[True][0], st[False][0]), (L, d)
+        assert torch.equal(st[True][1], st[False][1]), L
+        assert torch.equal(st[True][2], st[False][2]), L  # the new token's k / v cache rows
 
 
 @pytest.mark.parametrize("shared_head", [False, True])
