@@ -18,7 +18,7 @@ from dataclasses import dataclass, field
 import numpy as np
 import torch
 
-from ..ops import get_ops
+from ..ops import get_ops, h2d
 
 
 @dataclass
@@ -139,7 +139,7 @@ class FlatIndex:
             self.X[s0:s0 + n] = vecs.to(device=self.device, dtype=self.X.dtype)
             self.slots_t[s0:s0 + n] = slot
             self.ids[s0:s0 + n] = np.asarray(ids, dtype=np.int64)
-            self.ids_t[s0:s0 + n] = torch.from_numpy(self.ids[s0:s0 + n].copy()).to(self.device)
+            self.ids_t[s0:s0 + n] = h2d(self.ids[s0:s0 + n], self.device)
             self.n = s0 + n
             e = self.docs[doc_id]
             e.ranges.append((s0, s0 + n))
@@ -154,7 +154,7 @@ class FlatIndex:
             self._grow(s0 + n)
             self.X[s0:s0 + n] = vecs.to(device=self.device, dtype=self.X.dtype)
             self.ids[s0:s0 + n] = ids
-            self.ids_t[s0:s0 + n] = torch.from_numpy(np.asarray(ids, dtype=np.int64)).to(self.device)
+            self.ids_t[s0:s0 + n] = h2d(np.asarray(ids, dtype=np.int64), self.device)
             slots = np.empty(n, dtype=np.int32)
             r = s0
             for d, k in zip(doc_ids, rows_per_doc):
@@ -164,7 +164,7 @@ class FlatIndex:
                 e.ranges.append((r, r + k))
                 e.rows += k
                 r += k
-            self.slots_t[s0:s0 + n] = torch.from_numpy(slots).to(self.device)
+            self.slots_t[s0:s0 + n] = h2d(slots, self.device)
             self.n = s0 + n
 
     def remove_doc(self, doc_id: str) -> int:
@@ -190,7 +190,7 @@ class FlatIndex:
             if e is None or e.rows == 0 or keys.size == 0 or self.n == 0:
                 return 0
             n = self.n
-            kt = torch.from_numpy(keys).to(self.device)
+            kt = h2d(keys, self.device)
             s = self.slots_t[:n]
             sel = (s == e.slot) & torch.isin(self.ids_t[:n], kt)
             removed = int(sel.sum().item())
@@ -248,8 +248,8 @@ class FlatIndex:
             if maxrows * Q > 4 * self.n and self.dim % 32 == 0:
                 # wide filters: one MFMA dense scan + bitmap beats per-query range scans
                 return self._dense(X, q, k, min_sim, self.slots_t[:self.n], doc_filters)
-            rt = torch.tensor(ranges, dtype=torch.int32, device=self.device).view(-1, 2)
-            ot = torch.tensor(off, dtype=torch.int32, device=self.device)
+            rt = h2d(np.asarray(ranges, dtype=np.int32).reshape(-1, 2), self.device)
+            ot = h2d(np.asarray(off, dtype=np.int32), self.device)
             return self.ops.topk_ranges(X, q, rt, ot, k, min_sim, max_rows=maxrows)
 
     def _dense(self, X, q, k, min_sim, slots, doc_filters=None):
@@ -277,7 +277,7 @@ class FlatIndex:
                     e = self.docs.get(d)
                     if e is not None and e.rows:
                         bm[i, e.slot >> 5] |= np.uint32(1 << (e.slot & 31))
-        bitmap = torch.from_numpy(bm.view(np.int32)).to(self.device)
+        bitmap = h2d(bm.view(np.int32), self.device)
         slots = torch.where(slots < 0, torch.full_like(slots, guard), slots).contiguous()
         return self.ops.topk_dense(X, q, k, min_sim, slots=slots, bitmap=bitmap)
 

@@ -19,6 +19,7 @@ from __future__ import annotations
 import numpy as np
 import torch
 
+from ..ops import h2d
 from .flat import DocEntry, FlatIndex
 
 
@@ -236,8 +237,8 @@ class IVFFlatIndex(FlatIndex):
                 rr = np.stack([starts[valid], ends[valid]], axis=1).astype(np.int32)
                 ro = np.zeros(Q + 1, dtype=np.int32)
                 np.cumsum(valid.sum(axis=1), out=ro[1:])
-                rt = torch.from_numpy(rr).to(self.device)
-                ot = torch.from_numpy(ro).to(self.device)
+                rt = h2d(rr, self.device)
+                ot = h2d(ro, self.device)
                 s1, i1 = self.ops.topk_ranges(self.X, q, rt, ot, k, min_sim, max_rows=maxrows,
                                               slots=self.slots_t, bitmap=bitmap)
             else:
@@ -245,7 +246,7 @@ class IVFFlatIndex(FlatIndex):
                 i1 = torch.full((Q, k), -1, dtype=torch.int32, device=self.device)
             if self.n > self.trained_n:  # delta rows: exact scan
                 d0 = self.trained_n
-                rt = torch.tensor([[d0, self.n]] * Q, dtype=torch.int32, device=self.device)
+                rt = h2d(np.asarray([[d0, self.n]] * Q, dtype=np.int32), self.device)
                 ot = torch.arange(Q + 1, dtype=torch.int32, device=self.device)
                 s2, i2 = self.ops.topk_ranges(self.X, q, rt, ot, k, min_sim, max_rows=self.n - d0,
                                               slots=self.slots_t, bitmap=bitmap)
@@ -267,4 +268,4 @@ class IVFFlatIndex(FlatIndex):
                 e = self.docs.get(d)
                 if e is not None and e.rows:
                     bm[i, e.slot >> 5] |= np.uint32(1 << (e.slot & 31))
-        return torch.from_numpy(bm.view(np.int32)).to(self.device)
+        return h2d(bm.view(np.int32), self.device)
