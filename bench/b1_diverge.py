@@ -63,6 +63,17 @@ def run(arms: list[str], layers: int, steps: int):
         for li in (0, layers - 1):
             kv = [(m.cache.k(li)[s, :, pos], m.cache.v(li)[s, :, pos]) for m, s in zip(models, slots)]
             rec[f"kv{li}_equal"] = bool(torch.equal(kv[0][0], kv[1][0]) and torch.equal(kv[0][1], kv[1][1]))
+        # every layer's cache rows [0, L - 1): the first (layer, position, k|v) that differs
+        diff = None
+        for li in range(layers):
+            for nm in ("k", "v"):
+                ra = getattr(models[0].cache, nm)(li)[slots[0], :, :L - 1]
+                rb = getattr(models[1].cache, nm)(li)[slots[1], :, :L - 1]
+                ne = (ra != rb).any(dim=-1).any(dim=0).nonzero()
+                if ne.numel() and diff is None:
+                    diff = {"layer": li, "which": nm, "pos": int(ne[0]), "npos": int(ne.numel())}
+        rec["cache_first_diff"] = diff
+        rec["qkv_equal"] = bool(torch.equal(sa.qkv, sb.qkv))
         rec["b1_error"] = K.decode_b1_error()
         bad = not (rec["logits_equal"] and rec["x_equal"] and rec["token"][0] == rec["token"][1])
         if first_bad is None or after < 3:
@@ -75,6 +86,7 @@ def run(arms: list[str], layers: int, steps: int):
                 break
     print(json.dumps({"summary": True, "arms": arms, "first_mismatch_step": first_bad}), flush=True)
     LM._DECODE_B1 = True
+    K.decode_b1_error(reset=True)
 
 
 def main():

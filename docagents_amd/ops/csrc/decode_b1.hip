@@ -29,9 +29,12 @@
 // steps on the MI355X); every storing wave drains (s_waitcnt vmcnt(0)) before the workgroup
 // barrier behind which ONE lane bumps the counter (agent-scope relaxed atomic add); ONE wave polls
 // the counter relaxed with s_sleep, then the workgroup barrier. One workgroup per CU (occupancy 1). Counters are
-// cumulative over the launch (target = items x (layer + 1)) and zeroed by a memset node ahead of
-// every launch. Every spin is bounded: a timeout sets the error word, every workgroup leaves, and
-// the host raises (da_decode_b1_check) instead of hanging the GPU.
+// cumulative over the launch (target = items x (layer + 1)); the LAST workgroup to leave (an exit
+// ticket every workgroup takes after its final counter access) zeroes them for the next launch.
+// (A memset ahead of the launch is not enough under HIP-graph replay: measured, the second replay
+// started from the first one's counters, every wait passed at once and read stale rows.) Every
+// spin is bounded: a timeout sets the error word, every workgroup still takes its exit ticket, and
+// the host raises (decode_b1_error) instead of hanging the GPU.
 //
 // Numerics: each output element is computed by the same per-lane fp32 FMA sequence and wave
 // reduction as the separate kernels (gemm.hip gemv_kernel, attention.hip decode_attn_kernel
@@ -49,7 +52,7 @@ constexpr int CL = 32;              // words per counter line (128 B): one count
 constexpr unsigned SPIN_LIMIT = 1u << 21;  // polls of ~1 us: a wait gives up after a few seconds
 
 // sync block layout (unsigned words, each counter on its own 128-B line)
-enum : int { S_ERR = 0, S_HEADS = 1, S_O = 2, S_GU = 10, S_DN = 18, S_HEAD = 26 };  // x CL words
+enum : int { S_ERR = 0, S_EXIT = 1, S_HEADS = 2, S_O = 3, S_GU = 11, S_DN = 19, S_HEAD = 27 };  // x CL words
 // S_HEAD + h: qkv items published for head h; S_HEAD + H + h: split tickets of head h
 
 struct B1Layer {
@@ -677,7 +680,7 @@ __device__ __forceinline__ bool attn_item(const B1Args& a, const B1Layer& Ly, in
 
 // ------------------------------------------------------------------ the persistent kernel
 template <int D>
-__global__ void __launch_bounds__(B1_NT, 1) decode_b1_kernel(B1Args a) {
+__device__ __forceinline__ void b1_run(const B1Args& a) {
   const int G = gridDim.x, wg = blockIdx.x;
   const int Hd = a.Hd, F = a.F, H = a.H;
   unsigned* sync = a.sync;
@@ -734,6 +737,24 @@ __global__ void __launch_bounds__(B1_NT, 1) decode_b1_kernel(B1Args a) {
   }
 }
 
+template <int D>
+__global__ void __launch_bounds__(B1_NT, 1) decode_b1_kernel(B1Args a) {
+  b1_run<D>(a);
+  // exit ticket (also after an early exit on a timeout): the last workgroup out zeroes every
+  // counter line but the error word — all other workgroups are past their last counter access
+  __shared__ int s_lastout;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned old = __hip_atomic_fetch_add(a.sync + S_EXIT * CL, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_lastout = old == gridDim.x - 1;
+  }
+  __syncthreads();
+  if (s_lastout) {
+    for (int i = S_EXIT + (int)threadIdx.x; i < S_HEAD + 2 * a.H; i += B1_NT) st_u32(a.sync + i * CL, 0u);
+  }
+}
+
 }  // namespace
 
 // Resident workgroups per CU of the persistent kernel (occupancy query), for the grid size.
@@ -747,12 +768,13 @@ DA_EXPORT int da_decode_b1_occupancy(int D, int* out) {
   return (int)e;
 }
 
-// Bytes of the sync block for H heads (zeroed by every launch).
+// Bytes of the sync block for H heads (zero before the first launch; every launch leaves its counters
+// zero again, the error word excepted).
 DA_EXPORT long long da_decode_b1_sync_bytes(int H) { return (long long)(S_HEAD + 2 * H) * CL * 4; }
 
 // layers: device array of B1Layer (6 pointers each: wqkv, wo, wgu, wdown, kc, vc) for every layer;
 // runs layers [l0, l1). ws: H * nsplit * (D + 2) floats. sync: da_decode_b1_sync_bytes(H) bytes
-// (zeroed here by a memset on the stream: part of a captured graph). lm_head / logits / V: optional
+// (zero-initialised by the caller; see decode_b1_kernel's exit ticket). lm_head / logits / V: optional
 // final phase (null lm_head: skip). grid: resident workgroups (CUs of the stream x occupancy).
 DA_EXPORT int da_decode_b1(const void* layers, int l0, int l1, void* x, void* qkv, void* attn, void* act,
                            const void* lens, const void* slot, const void* pre, const void* pos, const void* cos_sin,
@@ -768,9 +790,6 @@ DA_EXPORT int da_decode_b1(const void* layers, int l0, int l1, void* x, void* qk
   if ((long long)chunk * nsplit < 1 || H > 4096) return (int)hipErrorInvalidValue;
   if (lm_head && (!logits || V < 16 || V % 16)) return (int)hipErrorInvalidValue;
   hipStream_t s = (hipStream_t)stream;
-  const size_t sbytes = (size_t)da_decode_b1_sync_bytes(H);
-  hipError_t e = hipMemsetAsync(sync, 0, sbytes, s);
-  if (e != hipSuccess) return (int)e;
   B1Args a{};
   a.layers = (const B1Layer*)layers; a.l0 = l0; a.l1 = l1;
   a.x = (bf16_t*)x; a.qkv = (bf16_t*)qkv; a.attn = (bf16_t*)attn; a.act = (bf16_t*)act;

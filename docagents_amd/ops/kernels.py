@@ -1033,16 +1033,19 @@ def decode_b1(layers, l0: int, l1: int, x, qkv, attn, act, lens, slot, pre, pos,
            "decode_b1")
 
 
-def decode_b1_error(device=None) -> int:
-    """The persistent decode's error word of the last launch on ``device`` (0 = ok; else the code
-    of the wait that timed out). Reads device memory: synchronises."""
+def decode_b1_error(device=None, reset: bool = False) -> int:
+    """The persistent decode's error word on ``device`` (0 = ok; else the code of the first wait that
+    timed out — it stays set, and makes every later launch leave at once, until ``reset``). Reads
+    device memory: synchronises."""
     dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+    err = 0
     for (idx, *_), (_, sync) in _B1_BUFS.items():
         if idx == dev.index:
             v = int(sync[0].item())
-            if v:
-                return v
-    return 0
+            err = err or v
+            if reset:
+                sync.zero_()
+    return err
 
 
 # ----------------------------------------------------------------------------------- fp16 encoder
