@@ -74,6 +74,11 @@ def run(arms: list[str], layers: int, steps: int):
                     diff = {"layer": li, "which": nm, "pos": int(ne[0]), "npos": int(ne.numel())}
         rec["cache_first_diff"] = diff
         rec["qkv_equal"] = bool(torch.equal(sa.qkv, sb.qkv))
+        rec["attn_equal"] = bool(torch.equal(sa.attn, sb.attn))  # the last layer's attention output
+        if not rec["attn_equal"]:
+            dh = (sa.attn.view(-1, cfg.head_dim) != sb.attn.view(-1, cfg.head_dim)).any(dim=1).nonzero().flatten()
+            rec["attn_heads_diff"] = dh.tolist()
+            rec["attn_maxdiff"] = float((sa.attn.float() - sb.attn.float()).abs().max())
         rec["b1_error"] = K.decode_b1_error()
         bad = not (rec["logits_equal"] and rec["x_equal"] and rec["token"][0] == rec["token"][1])
         if first_bad is None or after < 3:
