@@ -10,6 +10,13 @@
 //    (unnormalised O, running max, running sum) merged by decode_combine.
 #include "common.h"
 
+// Floating-point contraction only within one expression (a*b + c -> fma), never across statements:
+// with the HIP default (fast) the backend fuses differently depending on the surrounding code, and
+// the decode attention inlined into the persistent batch-1 kernel (decode_b1.hip) then differed from
+// decode_attn_kernel by one bf16 ulp on some heads (measured on the MI355X, bench/b1_diverge.py).
+// Both files pin the same rule, so the two compute the same bits by construction.
+#pragma clang fp contract(on)
+
 // ------------------------------------------------------------------------------------------
 // flash_attn_v2: 32x32x16 MFMA, 4 waves x 32 queries (128 queries per workgroup), 64-key tiles
 // double-buffered in LDS with register staging (tile t+1's global loads are in flight while tile t

@@ -45,6 +45,13 @@
 // occupancy query). Other streams' kernels only delay residency (they never wait on this one).
 #include "gemm.h"
 
+// Floating-point contraction only within one expression (a*b + c -> fma), never across statements:
+// with the HIP default (fast) the backend fuses differently depending on the surrounding code, and
+// the decode attention inlined into the persistent batch-1 kernel (decode_b1.hip) then differed from
+// decode_attn_kernel by one bf16 ulp on some heads (measured on the MI355X, bench/b1_diverge.py).
+// Both files pin the same rule, so the two compute the same bits by construction.
+#pragma clang fp contract(on)
+
 namespace {
 
 constexpr int B1_NT = 256;          // threads per workgroup (4 waves)
