@@ -90,7 +90,7 @@ def run(arms: list[str], layers: int, steps: int):
             if after > 3:
                 break
     print(json.dumps({"summary": True, "arms": arms, "first_mismatch_step": first_bad}), flush=True)
-    LM._DECODE_B1 = True
+    LM._DECODE_B1 = False  # the library default
     K.decode_b1_error(reset=True)
 
 

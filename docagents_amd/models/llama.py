@@ -37,9 +37,12 @@ _PREFILL_NORM_FUSE = False
 # Decode step of MHA models: RoPE + KV-cache write folded into the attention kernel (False: separate
 # rope_cache launch; the GPU tests compare both).
 _FUSED_ROPE_DECODE = True
-# Batch-1 decode as ONE persistent launch over all layers + the LM head (ops/csrc/decode_b1.hip);
-# bench/ab_arms.py selects the per-kernel path (5 launches per layer) for A/B runs (DA_DECODE_B1=0)
-_DECODE_B1 = True
+# Batch-1 decode as ONE persistent launch over all layers + the LM head (ops/csrc/decode_b1.hip).
+# Bit-identical to the per-kernel path (tests/test_decode_b1_gpu.py) but measured SLOWER on the
+# MI355X: 2.34 vs 2.06 ms per step (bench/b1_persistent_ab.py, profiles/r4/check_d_b1_fused_on/) — its four
+# chip-wide fan-ins per layer (~3-4 us each at 256 arrivals) cost more than the five launch
+# boundaries (~1.2 us each) they replace. Off by default; bench/ab_arms.py DA_DECODE_B1=1 selects it.
+_DECODE_B1 = False
 
 
 class TPContext:

@@ -497,7 +497,7 @@ def dk_fusable(M, N, K, epi=EPI_NONE):
             and epi in (EPI_NONE, EPI_BIAS, EPI_RESID, EPI_SWIGLU) and (epi != EPI_SWIGLU or N % 32 == 0))
 
 
-SPLITK_FUSED = True  # mirrors kernels.SPLITK_FUSED (bench/ab_arms.py flips both)
+SPLITK_FUSED = False  # mirrors kernels.SPLITK_FUSED (bench/ab_arms.py flips both)
 
 
 def dk_parts(N, M=0):

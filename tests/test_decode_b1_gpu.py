@@ -23,15 +23,28 @@ def _pair(layers=4, seed=21, max_seq=4096):
     return a, b
 
 
-class _PerKernel:
-    """Run a model with the persistent path switched off (the 5-launches-per-layer reference)."""
+class _Path:
+    """Run with the persistent path on or off (off: the 5-launches-per-layer reference)."""
+
+    def __init__(self, on: bool):
+        self.on = on
 
     def __enter__(self):
         self.old = LM._DECODE_B1
-        LM._DECODE_B1 = False
+        LM._DECODE_B1 = self.on
 
     def __exit__(self, *exc):
         LM._DECODE_B1 = self.old
+
+
+def _PerKernel():
+    return _Path(False)
+
+
+@pytest.fixture(autouse=True)
+def _persistent_on():
+    with _Path(True):  # the persistent launch is opt-in (off by default: slower on the MI355X)
+        yield
 
 
 def test_decode_b1_step_logits_bit_identical():
