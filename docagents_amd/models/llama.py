@@ -39,7 +39,7 @@ _PREFILL_NORM_FUSE = False
 _FUSED_ROPE_DECODE = True
 # Batch-1 decode as ONE persistent launch over all layers + the LM head (ops/csrc/decode_b1.hip).
 # Bit-identical to the per-kernel path (tests/test_decode_b1_gpu.py) but measured SLOWER on the
-# MI355X: 2.34 vs 2.06 ms per step (bench/b1_persistent_ab.py, profiles/r4/check_d_b1_fused_on/) — its four
+# MI355X: 2.34 vs 2.06 ms per step (bench/b1_persistent_ab.py, profiles/r4/check_d_b1_fused_on/, profiles/r4/check_d/) — its four
 # chip-wide fan-ins per layer (~3-4 us each at 256 arrivals) cost more than the five launch
 # boundaries (~1.2 us each) they replace. Off by default; bench/ab_arms.py DA_DECODE_B1=1 selects it.
 _DECODE_B1 = False

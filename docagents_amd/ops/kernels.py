@@ -298,7 +298,7 @@ def _dk_splitk(M: int, N: int) -> bool:
 # 33..64 rows: True = the split-K reduction inside the tile kernel (last split of each tile,
 # EPI_SPLITK) instead of separate reduce launches. Off: measured slower on the MI355X — the fused
 # tiles took 32.3 us each vs 16.0 us + the reduce launches' share (QA decode step 14.85 vs 13.35 ms,
-# profiles/r4/check_d_b1_fused_on/): the last arriver alone reads all S partial tiles of its tile cross-XCD
+# profiles/r4/check_d_b1_fused_on/, profiles/r4/check_d/): the last arriver alone reads all S partial tiles of its tile cross-XCD
 # (up to 8 x 32 KB per workgroup at the per-block hand-off rate), where the reduce launch spreads the
 # same bytes over the whole chip. Bit-identical either way (tests/test_splitk_fused_gpu.py);
 # bench/ab_arms.py DA_SPLITK_FUSED=1 selects it.
