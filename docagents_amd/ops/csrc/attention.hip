@@ -824,7 +824,7 @@ struct DecRope {
 };
 
 template <int D, int G, int VAR>
-__global__ void __launch_bounds__(256)
+__global__ void __launch_bounds__((VAR & 32) ? 512 : 256)
 decode_attn_kernel(const bf16_t* __restrict__ q, int ldq, const bf16_t* __restrict__ kc,
                    const bf16_t* __restrict__ vc, const int* __restrict__ lens, const int* __restrict__ slot,
                    const int* __restrict__ pre,
@@ -836,12 +836,15 @@ decode_attn_kernel(const bf16_t* __restrict__ q, int ldq, const bf16_t* __restri
   constexpr int GCD = (CPR % 16 == 0) ? 16 : ((CPR % 8 == 0) ? 8 : ((CPR % 4 == 0) ? 4 : 2));
   constexpr int NSET = CPR / GCD;                  // distinct dim-slots per lane
   constexpr bool SHFL = (64 % CPR) == 0;           // a key's chunks live in one wave-instruction
+  // VAR bit 5: 8 waves per workgroup (batch 1: a split's tiles all in flight at once, one per wave,
+  // instead of two back to back on each of 4 waves); else 4
+  constexpr int NWV = (VAR & 32) ? 8 : 4, NTH = 64 * NWV;
   __shared__ float sq[G][D];
-  __shared__ float sp[4][G][KT];
-  __shared__ float spart[SHFL ? 1 : 4][SHFL ? 1 : G * KT * CPR];
-  __shared__ float so[G == 1 ? 1 : 4][G][D];
-  __shared__ float sacc[G == 1 ? 4 * NSET * 64 * 8 : 1];
-  __shared__ float swm[4][G], swl[4][G];
+  __shared__ float sp[NWV][G][KT];
+  __shared__ float spart[SHFL ? 1 : NWV][SHFL ? 1 : G * KT * CPR];
+  __shared__ float so[G == 1 ? 1 : NWV][G][D];
+  __shared__ float sacc[G == 1 ? NWV * NSET * 64 * 8 : 1];
+  __shared__ float swm[NWV][G], swl[NWV][G];
 
   const int split = blockIdx.x, hk = blockIdx.y, b = blockIdx.z;
   constexpr bool TRACE = (VAR & 8) != 0;
@@ -938,7 +941,7 @@ decode_attn_kernel(const bf16_t* __restrict__ q, int ldq, const bf16_t* __restri
     // VAR bit 4: the prologue operands land BEFORE this workgroup's K/V requests join the chip-wide
     // flood (otherwise they queue behind other workgroups' tiles: 3.6 us at batch 1, decode_trace)
     if constexpr ((VAR & 16) != 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const int t0 = kstart + w * KT, t1 = t0 + 4 * KT;
+    const int t0 = kstart + w * KT, t1 = t0 + NWV * KT;
     load_k(ka, t0); load_v(va, t0);
     load_k(kb2, t1); load_v(vb2, t1);
     const float pc = fr ? rcs[0] : 1.f, ps = fr ? rcs[1] : 0.f;
@@ -957,11 +960,11 @@ decode_attn_kernel(const bf16_t* __restrict__ q, int ldq, const bf16_t* __restri
     }
   } else {
     if constexpr (PFT) {
-      const int t0 = kstart + w * KT, t1 = t0 + 4 * KT;
+      const int t0 = kstart + w * KT, t1 = t0 + NWV * KT;
       load_k(ka, t0); load_v(va, t0);
       load_k(kb2, t1); load_v(vb2, t1);
     }
-    for (int i = tid; i < G * D; i += 256) {
+    for (int i = tid; i < G * D; i += NTH) {
       const int g = i / D, d = i % D;
       const bf16_t* hp = q + (size_t)b * ldq + (hk * G + g) * D;
       sq[g][d] = (fr ? rot(hp, d, L - 1) : bf2f(hp[d])) * scale_log2e;
@@ -971,7 +974,7 @@ decode_attn_kernel(const bf16_t* __restrict__ q, int ldq, const bf16_t* __restri
     const bf16_t* kr = q + (size_t)b * ldq + (size_t)(H + hk) * D;
     const bf16_t* vr = q + (size_t)b * ldq + (size_t)(H + Hkv + hk) * D;
     const size_t crow = cbase + (size_t)(L - 1) * D;
-    for (int d = tid; d < D; d += 256) {
+    for (int d = tid; d < D; d += NTH) {
       const float kv = rot(kr, d, L - 1);
       skn[d] = kv;
       svn[d] = bf2f(vr[d]);
@@ -980,7 +983,7 @@ decode_attn_kernel(const bf16_t* __restrict__ q, int ldq, const bf16_t* __restri
     }
   }
   if constexpr (G > 1) {
-    for (int i = tid; i < 4 * G * D; i += 256) (&so[0][0][0])[i] = 0.f;
+    for (int i = tid; i < NWV * G * D; i += NTH) (&so[0][0][0])[i] = 0.f;
   }
   __syncthreads();
   stamp(1);
@@ -1089,20 +1092,20 @@ decode_attn_kernel(const bf16_t* __restrict__ q, int ldq, const bf16_t* __restri
   if constexpr (PFT) {  // two tiles in flight per wave: ka/va and kb2/vb2 alternate
     int t0 = kstart + w * KT;
     while (t0 < kend) {
-      const int t1 = t0 + 4 * KT;
+      const int t1 = t0 + NWV * KT;
       process(ka, va, t0);
       if (t0 == kstart + w * KT) stamp(7);
       if (t1 >= kend) break;
-      const int t2 = t1 + 4 * KT;
+      const int t2 = t1 + NWV * KT;
       if (t2 < kend) { load_k(ka, t2); load_v(va, t2); }
       process(kb2, vb2, t1);
       if (t2 >= kend) break;
-      const int t3 = t2 + 4 * KT;
+      const int t3 = t2 + NWV * KT;
       if (t3 < kend) { load_k(kb2, t3); load_v(vb2, t3); }
       t0 = t2;
     }
   } else {
-    for (int t0 = kstart + w * KT; t0 < kend; t0 += 4 * KT) {
+    for (int t0 = kstart + w * KT; t0 < kend; t0 += NWV * KT) {
       u32x4_t kv[CPR], vv[CPR];
       load_k(kv, t0);
       if constexpr (VEARLY) load_v(vv, t0);
@@ -1140,14 +1143,16 @@ decode_attn_kernel(const bf16_t* __restrict__ q, int ldq, const bf16_t* __restri
   }
   __syncthreads();
   stamp(12);
-  for (int i = tid; i < G * D; i += 256) {
+  for (int i = tid; i < G * D; i += NTH) {
     const int g = i / D, d = i % D;
     float M = fmaxf(fmaxf(swm[0][g], swm[1][g]), fmaxf(swm[2][g], swm[3][g]));
+#pragma unroll
+    for (int ww = 4; ww < NWV; ++ww) M = fmaxf(M, swm[ww][g]);
     if (own_new) M = fmaxf(M, ssn[g]);
     const float Mu = (M == -INFINITY) ? 0.f : M;
     float o = 0.f, ls = 0.f;
 #pragma unroll
-    for (int ww = 0; ww < 4; ++ww) {
+    for (int ww = 0; ww < NWV; ++ww) {
       const float f = exp2f(swm[ww][g] - Mu);
       float ow;
       if constexpr (G == 1) {
@@ -1382,7 +1387,7 @@ static int launch_decode_v(int G, dim3 grid, hipStream_t s, const bf16_t* q, int
                            const bf16_t* vc, const int* lens, const int* slot, const int* pre, int H, int Hkv, int max_seq, int chunk,
                            int nsplit, float sl2e, float* po, float* pm, float* pl, bf16_t* out, int ldo,
                            int* cnt, DecRope rope) {
-#define DEC(GG) decode_attn_kernel<D, GG, VAR><<<grid, 256, 0, s>>>(q, ldq, kc, vc, lens, slot, pre, H, Hkv, max_seq, \
+#define DEC(GG) decode_attn_kernel<D, GG, VAR><<<grid, (VAR & 32) ? 512 : 256, 0, s>>>(q, ldq, kc, vc, lens, slot, pre, H, Hkv, max_seq, \
                                                                      chunk, nsplit, sl2e, po, pm, pl, out, ldo, cnt, rope)
   switch (G) {
     case 1: DEC(1); break;
@@ -1407,6 +1412,9 @@ DA_EXPORT void da_set_gqa_mfma(int v) { g_gqa_mfma = v; }
 // MHA decode with the next tile prefetched (VAR bit 2) when B * Hkv <= this (0 = never).
 static int g_dec_pft = 32;
 DA_EXPORT void da_set_decode_pft(int v) { g_dec_pft = v; }
+// ... and with 8 waves per workgroup (VAR bit 5) when B * Hkv <= this (0 = never; A/B)
+static int g_dec_w8 = 0;
+DA_EXPORT void da_set_decode_w8(int v) { g_dec_w8 = v; }
 // Timeline probe (bench/decode_trace.py): non-null -> the MHA D=96 prefetch variant writes 8 wall-clock
 // stamps per workgroup here ([B][Hkv][nsplit][8]: start, prologue done, first tile done, tiles done,
 // partial stored, finished, last-split flag, CU id).
@@ -1431,6 +1439,8 @@ static int launch_decode(int G, dim3 grid, hipStream_t s, const bf16_t* q, int l
     }
     if (g_dec_pft && (int)(grid.y * grid.z) <= g_dec_pft && g_dec_qfirst)
       return launch_decode_v<D, 23>(G, grid, s, q, ldq, kc, vc, lens, slot, pre, H, Hkv, max_seq, chunk, nsplit, sl2e, po, pm, pl, out, ldo, cnt, rope);
+    if (g_dec_w8 && g_dec_pft && (int)(grid.y * grid.z) <= g_dec_w8)
+      return launch_decode_v<D, 39>(G, grid, s, q, ldq, kc, vc, lens, slot, pre, H, Hkv, max_seq, chunk, nsplit, sl2e, po, pm, pl, out, ldo, cnt, rope);
     if (g_dec_pft && (int)(grid.y * grid.z) <= g_dec_pft)  // few (row, kv head) pairs: latency-bound
       return launch_decode_v<D, 7>(G, grid, s, q, ldq, kc, vc, lens, slot, pre, H, Hkv, max_seq, chunk, nsplit, sl2e, po, pm, pl, out, ldo, cnt, rope);
     return launch_decode_v<D, 3>(G, grid, s, q, ldq, kc, vc, lens, slot, pre, H, Hkv, max_seq, chunk, nsplit, sl2e, po, pm, pl, out, ldo, cnt, rope);

@@ -318,10 +318,13 @@ def test_flash_attn_spike(D, pipe):
 
 
 @pytest.mark.parametrize("D", [64, 96, 128])
-@pytest.mark.parametrize("lens,chunk,pft", [([1000], 512, 32), ([1], 256, 32), ([513, 257, 64], 256, 0),
-                                            ([2944] * 5, 0, 0), ([65, 1024, 700], 64, 1024)])
-def test_decode_attn_fused_rope(D, lens, chunk, pft):
-    """Decode attention with RoPE + the new token's cache write folded in == rope_cache + attention."""
+@pytest.mark.parametrize("lens,chunk,pft,w8", [([1000], 512, 32, 0), ([1], 256, 32, 0), ([513, 257, 64], 256, 0, 0),
+                                               ([2944] * 5, 0, 0, 0), ([65, 1024, 700], 64, 1024, 0),
+                                               ([2935], 0, 32, 32), ([1], 256, 32, 32), ([1000, 3], 768, 32, 32),
+                                               ([4000, 64, 129], 512, 1024, 1024)])
+def test_decode_attn_fused_rope(D, lens, chunk, pft, w8):
+    """Decode attention with RoPE + the new token's cache write folded in == rope_cache + attention
+    (w8: the 8-waves-per-workgroup variant of the small-batch path)."""
     torch.manual_seed(D + len(lens) + chunk)
     H, slots, max_seq = 4, 6, 4096
     B = len(lens)
@@ -335,10 +338,12 @@ def test_decode_attn_fused_rope(D, lens, chunk, pft):
     K.rope_cache(qkv2, pos, cs, H, H, D, slot=slot, k_cache=kc2, v_cache=vc2)
     want = K.decode_attn(qkv2, kc2, vc2, L, slot, H, H, D, max_seq, chunk=chunk)
     K.lib().da_set_decode_pft(pft)
+    K.lib().da_set_decode_w8(w8)
     try:
         got = K.decode_attn(qkv, kc, vc, L, slot, H, H, D, max_seq, chunk=chunk, rope=(cs, pos))
     finally:
         K.lib().da_set_decode_pft(32)
+        K.lib().da_set_decode_w8(0)
     _close(got, want, atol=0.01)
     for b in range(B):
         s_, p_ = int(slot[b]), int(pos[b])
