@@ -1439,8 +1439,11 @@ static int launch_decode(int G, dim3 grid, hipStream_t s, const bf16_t* q, int l
     }
     if (g_dec_pft && (int)(grid.y * grid.z) <= g_dec_pft && g_dec_qfirst)
       return launch_decode_v<D, 23>(G, grid, s, q, ldq, kc, vc, lens, slot, pre, H, Hkv, max_seq, chunk, nsplit, sl2e, po, pm, pl, out, ldo, cnt, rope);
-    if (g_dec_w8 && g_dec_pft && (int)(grid.y * grid.z) <= g_dec_w8)
-      return launch_decode_v<D, 39>(G, grid, s, q, ldq, kc, vc, lens, slot, pre, H, Hkv, max_seq, chunk, nsplit, sl2e, po, pm, pl, out, ldo, cnt, rope);
+    if (g_dec_w8 && g_dec_pft && (int)(grid.y * grid.z) <= g_dec_w8) {  // MHA only (G = 1: LDS)
+      decode_attn_kernel<D, 1, 39><<<grid, 512, 0, s>>>(q, ldq, kc, vc, lens, slot, pre, H, Hkv, max_seq, chunk, nsplit,
+                                                         sl2e, po, pm, pl, out, ldo, cnt, rope);
+      return (int)hipGetLastError();
+    }
     if (g_dec_pft && (int)(grid.y * grid.z) <= g_dec_pft)  // few (row, kv head) pairs: latency-bound
       return launch_decode_v<D, 7>(G, grid, s, q, ldq, kc, vc, lens, slot, pre, H, Hkv, max_seq, chunk, nsplit, sl2e, po, pm, pl, out, ldo, cnt, rope);
     return launch_decode_v<D, 3>(G, grid, s, q, ldq, kc, vc, lens, slot, pre, H, Hkv, max_seq, chunk, nsplit, sl2e, po, pm, pl, out, ldo, cnt, rope);
