@@ -1413,7 +1413,7 @@ DA_EXPORT void da_set_gqa_mfma(int v) { g_gqa_mfma = v; }
 static int g_dec_pft = 32;
 DA_EXPORT void da_set_decode_pft(int v) { g_dec_pft = v; }
 // ... and with 8 waves per workgroup (VAR bit 5) when B * Hkv <= this (0 = never; A/B)
-static int g_dec_w8 = 0;
+static int g_dec_w8 = 0;  // measured 2x slower (profiles/r4/rejected_r4.txt): A/B only
 DA_EXPORT void da_set_decode_w8(int v) { g_dec_w8 = v; }
 // Timeline probe (bench/decode_trace.py): non-null -> the MHA D=96 prefetch variant writes 8 wall-clock
 // stamps per workgroup here ([B][Hkv][nsplit][8]: start, prologue done, first tile done, tiles done,
