@@ -39,6 +39,7 @@ struct GemmArgs {
   // EPI_SPLITK: per-tile arrival counters (zero before the launch, left zero after it) and the
   // epilogue the last split applies (NONE / BIAS / SWIGLU / RESID)
   int* cnt; int fuse_epi;
+  int group;  // gemm8p: row tiles per grouped-M band of the tile order (0: the default, 4)
 };
 
 // 256x256 fp8 tile (gemm256.hip): A and W hold OCP e4m3 bytes (lda / K in elements = bytes),

@@ -68,7 +68,7 @@ gemm8p_kernel(GemmArgs p) {
 
   const int ntm = (p.M + BM - 1) / BM, ntn = (p.N + BN - 1) / BN;
   const int t = xcd_remap(blockIdx.x, ntm * ntn);
-  constexpr int GROUP = 4;
+  const int GROUP = p.group > 0 ? p.group : 4;
   const int gid = t / (GROUP * ntn);
   const int first_m = gid * GROUP;
   const int gsz = min(ntm - first_m, GROUP);
@@ -390,8 +390,14 @@ gemm8p_kernel(GemmArgs p) {
   }
 }
 
+// grouped-M band height of the tile order (A/B: bench/gemm_group.py)
+static int g_8p_group = 0;
+DA_EXPORT void da_set_gemm8p_group(int v) { g_8p_group = v > 0 ? v : 0; }
+
 template <int BM>
-static int launch8p(const GemmArgs& a, int epi, hipStream_t s) {
+static int launch8p(const GemmArgs& a0, int epi, hipStream_t s) {
+  GemmArgs a = a0;
+  if (a.group <= 0) a.group = g_8p_group;
   const int ntm = (a.M + BM - 1) / BM, ntn = (a.N + BN - 1) / BN;
   dim3 grid(ntm * ntn), block(512);
   if (epi >= 100) {  // fp16 operands (the encoder's DTYPE=fp16): the BERT epilogues only
