@@ -1,5 +1,5 @@
 """Prefill GEMM (gemm8p, 256x256 tiles) vs the grouped-M band height of its tile order
-(da_set_gemm8p_group): Phi-3 prefill shapes, interleaved rounds, sustained TF/s on random
+(da_set_gemm8p_group; GRP="2,4" picks the arms): Phi-3 prefill shapes, interleaved rounds, sustained TF/s on random
 [-1, 1) operands. One JSON line per shape."""
 import json
 import os
@@ -11,7 +11,7 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from docagents_amd.ops import kernels as K  # noqa: E402
 
-GROUPS = [int(g) for g in os.environ.get("GROUPS", "1,2,4,8,16").split(",")]
+GROUPS = [int(g) for g in os.environ.get("GRP", "1,2,4,8,16").split(",")]
 ROUNDS = int(os.environ.get("ROUNDS", "3"))
 
 

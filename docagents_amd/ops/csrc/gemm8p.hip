@@ -390,7 +390,11 @@ gemm8p_kernel(GemmArgs p) {
   }
 }
 
-// grouped-M band height of the tile order (A/B: bench/gemm_group.py)
+// Grouped-M band height of the tile order: 0 = auto; else forced (A/B: bench/gemm_group.py).
+// Auto: 2-row-tile bands for the wide (N >= 8192) or deep (K >= 8192) prefill projections at
+// M >= 32k, 4 otherwise — measured on the MI355X at M = 65536 (profiles/r4/gemm_group.txt): QKV
+// 1358 vs 1322 TF/s, gate/up + SwiGLU 1334 vs 1316, down 1356 vs 1322; the O projection (3072 x
+// 3072) and smaller M keep 4 (1195 vs 1182, 1350 vs 1340).
 static int g_8p_group = 0;
 DA_EXPORT void da_set_gemm8p_group(int v) { g_8p_group = v > 0 ? v : 0; }
 
@@ -398,6 +402,7 @@ template <int BM>
 static int launch8p(const GemmArgs& a0, int epi, hipStream_t s) {
   GemmArgs a = a0;
   if (a.group <= 0) a.group = g_8p_group;
+  if (a.group <= 0) a.group = (a.M >= 32768 && (a.N >= 8192 || a.K >= 8192)) ? 2 : 4;
   const int ntm = (a.M + BM - 1) / BM, ntn = (a.N + BN - 1) / BN;
   dim3 grid(ntm * ntn), block(512);
   if (epi >= 100) {  // fp16 operands (the encoder's DTYPE=fp16): the BERT epilogues only
