@@ -36,7 +36,8 @@ ENV_SETTERS = {
     "DA_GEMV_U": "da_set_gemv_u",            # batch-1 GEMV K-blocks in flight per row
     "DA_GEMV_KS": "da_set_gemv_ks",          # batch-1 GEMV waves per long row
     "DA_DECODE_PFT": "da_set_decode_pft",    # MHA decode next-tile prefetch threshold
-    "DA_DECODE_W8": "da_set_decode_w8",      # ... with 8 waves per workgroup up to this many (row, kv head) pairs
+    "DA_DECODE_W8": "da_set_decode_w8",
+    "DA_GEMM8P_GROUP": "da_set_gemm8p_group",  # prefill GEMM tile-order band height (0 = auto)      # ... with 8 waves per workgroup up to this many (row, kv head) pairs
 }
 
 
