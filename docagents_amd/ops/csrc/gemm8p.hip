@@ -390,11 +390,11 @@ gemm8p_kernel(GemmArgs p) {
   }
 }
 
-// Grouped-M band height of the tile order: 0 = auto; else forced (A/B: bench/gemm_group.py).
-// Auto: 2-row-tile bands for the wide (N >= 8192) or deep (K >= 8192) prefill projections at
-// M >= 32k, 4 otherwise — measured on the MI355X at M = 65536 (profiles/r4/gemm_group.txt): QKV
-// 1358 vs 1322 TF/s, gate/up + SwiGLU 1334 vs 1316, down 1356 vs 1322; the O projection (3072 x
-// 3072) and smaller M keep 4 (1195 vs 1182, 1350 vs 1340).
+// Grouped-M band height of the tile order: 0 = 4 (default); else forced (A/B: bench/gemm_group.py,
+// bench/ab_arms.py DA_GEMM8P_GROUP). Isolated GEMMs at M = 65536 ran 1.4-2.7 % faster with 2-row
+// bands on the wide / deep projections (profiles/r4/gemm_group.txt), but the QA prefill of the bench
+// on one box ran 0.8 % SLOWER with them (1173-1175 vs 1163-1166 ms, profiles/r4/rejected_r4.txt):
+// back-to-back repeats of one GEMM keep its operands cache-warm; the real layer sequence does not.
 static int g_8p_group = 0;
 DA_EXPORT void da_set_gemm8p_group(int v) { g_8p_group = v > 0 ? v : 0; }
 
@@ -402,7 +402,7 @@ template <int BM>
 static int launch8p(const GemmArgs& a0, int epi, hipStream_t s) {
   GemmArgs a = a0;
   if (a.group <= 0) a.group = g_8p_group;
-  if (a.group <= 0) a.group = (a.M >= 32768 && (a.N >= 8192 || a.K >= 8192)) ? 2 : 4;
+  if (a.group <= 0) a.group = 4;
   const int ntm = (a.M + BM - 1) / BM, ntn = (a.N + BN - 1) / BN;
   dim3 grid(ntm * ntn), block(512);
   if (epi >= 100) {  // fp16 operands (the encoder's DTYPE=fp16): the BERT epilogues only
