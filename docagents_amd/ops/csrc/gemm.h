@@ -47,3 +47,5 @@ struct GemmArgs {
 int launch_gemm256(const GemmArgs& a, int epi, hipStream_t s, int fp8 = 1);
 // phase-split BMx256 bf16 kernel (gemm8p.hip), bm = 256 or 128; K % 64 == 0, K >= 128
 int launch_gemm8p(const GemmArgs& a, int epi, hipStream_t s, int bm = 256);
+// row-tile height (128 / 256) for a non-RoPE prefill product of M x N (gemm8p.hip)
+int gemm8p_pick_bm(int M, int N);

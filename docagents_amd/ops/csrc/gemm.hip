@@ -918,7 +918,7 @@ DA_EXPORT int da_gemm8p_norm(const void* A, int lda, const void* W, void* C, int
     a.rope = RopeArgs{(const int*)pos, (const int*)slot, (const float*)cos_sin, (bf16_t*)k_cache, (bf16_t*)v_cache,
                       H, Hkv, D, max_seq};
   const long t256 = (long)((M + 255) / 256) * ((N + 255) / 256);
-  const int bm = epi == EPI_ROPE ? (t256 >= 256 ? 256 : 128) : (t256 >= 128 ? 256 : 128);
+  const int bm = epi == EPI_ROPE ? (t256 >= 256 ? 256 : 128) : gemm8p_pick_bm(M, N);
   return launch_gemm8p(a, epi, (hipStream_t)stream, bm);
 }
 
@@ -942,15 +942,14 @@ DA_EXPORT int da_gemm_bf16(const void* A, int lda, const void* W, void* C, int l
   a.gamma = (const bf16_t*)rms_gamma; a.eps = rms_eps;
   if ((rms_gamma || rms_eps > 0.f) && tile != 6) return (int)hipErrorInvalidValue;  // fused RMSNorm: GEMV only
   if (tile == 0) {
-    const long t256 = (long)((M + 255) / 256) * ((N + 255) / 256);
     // decode-sized M: 32x128 / 64x128 weight-streaming tiles (+ split-K, chosen by the caller);
     // 65..639 rows: the 64x128 tile over ceil(M/64) row blocks; from 640 rows the phase-split
-    // kernel: 256-row tiles unless the grid is below half the chip, then 128-row tiles (32-layer
-    // Phi-3 chain and single-GEMM sweeps: bench/midm_chain.py, bench/gemm_ab.py, profiles/r2)
+    // kernel with the row-tile height of fewer workgroup waves (gemm8p_pick_bm; 32-layer Phi-3
+    // chain and single-GEMM sweeps: bench/midm_chain.py, bench/gemm_ab.py, profiles/r2, r3)
     if (M <= 32) tile = 3;
     else if (M < 640 || splits > 1) tile = 2;
     else if (K < 128) tile = 1;
-    else tile = (t256 >= 128) ? 7 : 10;
+    else tile = gemm8p_pick_bm(M, N) == 256 ? 7 : 10;
   }
   if (tile == 4 || tile == 7 || tile == 10) {
     if (splits != 1 || K < 128) return (int)hipErrorInvalidValue;

@@ -427,6 +427,31 @@ static int launch8p(const GemmArgs& a0, int epi, hipStream_t s) {
   return (int)hipGetLastError();
 }
 
+// Row-tile height for a non-RoPE prefill product: the one with fewer workgroup WAVES over the
+// chip's CUs, weighting a 128-row tile's time as 0.72 of a 256-row one (measured at M = 2930:
+// 128-row tiles took 0.61-0.73 of the 256-row tile time, profiles/r3/gemm_ab_batch1_prefill_tiles.txt).
+// At M ~ 2.6k (the batch-1 prefill of the p50 path) the O / down projections (N = 3072) then run
+// 252 128-row tiles in one wave instead of 132 256-row tiles on half the chip; QA-sized chunks
+// (M ~ 64k) keep 256. mode 0 (A/B, da_set_gemm8p_bm_rule): the round-3 rule, 256 rows once the
+// 256-row grid reaches half the chip.
+static int g_bm_rule = 1;
+DA_EXPORT void da_set_gemm8p_bm_rule(int v) { g_bm_rule = v; }
+
+int gemm8p_pick_bm(int M, int N) {
+  const long ntn = (N + 255) / 256;
+  const long t256 = (long)((M + 255) / 256) * ntn, t128 = (long)((M + 127) / 128) * ntn;
+  if (!g_bm_rule) return t256 >= 128 ? 256 : 128;
+  static int cus = 0;
+  if (cus <= 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+      cus = 256;
+  }
+  const long w256 = (t256 + cus - 1) / cus, w128 = (t128 + cus - 1) / cus;
+  return w128 * 72 < w256 * 100 ? 128 : 256;
+}
+
 // epi + 100: the same kernel on fp16 operands / output (v_mfma_f32_16x16x32_f16)
 int launch_gemm8p(const GemmArgs& a, int epi, hipStream_t s, int bm) {
   if (a.K < 128 || a.K % 64) return (int)hipErrorInvalidValue;
@@ -447,6 +472,5 @@ DA_EXPORT int da_gemm_f16(const void* A, int lda, const void* W, void* C, int ld
   a.A = (const bf16_t*)A; a.W = (const bf16_t*)W; a.C = (bf16_t*)C;
   a.bias = (const bf16_t*)bias; a.resid = (const bf16_t*)resid;
   a.M = M; a.N = N; a.K = K; a.lda = lda; a.ldc = ldc; a.ldr = ldr; a.k_per_split = K;
-  const long t256 = (long)((M + 255) / 256) * ((N + 255) / 256);
-  return launch_gemm8p(a, 100 + epi, (hipStream_t)stream, t256 >= 128 ? 256 : 128);
+  return launch_gemm8p(a, 100 + epi, (hipStream_t)stream, gemm8p_pick_bm(M, N));
 }

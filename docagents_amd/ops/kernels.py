@@ -83,6 +83,7 @@ _SIGS = {
     "da_set_decode_pft": [c_int],
     "da_set_decode_w8": [c_int],
     "da_set_gemm8p_group": [c_int],
+    "da_set_gemm8p_bm_rule": [c_int],
     "da_set_flash_rev": [c_int],
     "da_decode_attn": [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
                        c_int, c_int, c_int, c_float, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p,
