@@ -36,9 +36,10 @@ ENV_SETTERS = {
     "DA_GEMV_U": "da_set_gemv_u",            # batch-1 GEMV K-blocks in flight per row
     "DA_GEMV_KS": "da_set_gemv_ks",          # batch-1 GEMV waves per long row
     "DA_DECODE_PFT": "da_set_decode_pft",    # MHA decode next-tile prefetch threshold
-    "DA_DECODE_W8": "da_set_decode_w8",
+    "DA_DECODE_W8": "da_set_decode_w8",      # ... with 8 waves per workgroup up to this many (row, kv head) pairs
     "DA_GEMM8P_GROUP": "da_set_gemm8p_group",  # prefill GEMM tile-order band height (0 = auto)
-    "DA_GEMM8P_BM_RULE": "da_set_gemm8p_bm_rule",  # prefill row-tile height: 1 = fewest waves, 0 = round-3 rule      # ... with 8 waves per workgroup up to this many (row, kv head) pairs
+    "DA_GEMM8P_BM_RULE": "da_set_gemm8p_bm_rule",  # prefill row-tile height: 1 = fewest waves, 0 = round-3 rule
+    "DA_OMERGE_SHAPE": "da_set_omerge_shape",  # merged batch-1 O GEMV: waves per workgroup * 10 + rows per wave
 }
 
 
@@ -47,7 +48,8 @@ def apply_env_overrides() -> dict:
     L = K.lib()
     done = {}
     from docagents_amd.models import llama
-    for env, attr in (("DA_PREFILL_NORM_FUSE", "_PREFILL_NORM_FUSE"), ("DA_DECODE_B1", "_DECODE_B1")):
+    for env, attr in (("DA_PREFILL_NORM_FUSE", "_PREFILL_NORM_FUSE"), ("DA_DECODE_B1", "_DECODE_B1"),
+                      ("DA_O_MERGE", "_O_MERGE")):
         if os.environ.get(env) is not None:  # model-level code paths (default: llama.py)
             setattr(llama, attr, os.environ[env] == "1")
             done[env] = int(getattr(llama, attr))

@@ -43,6 +43,12 @@ _FUSED_ROPE_DECODE = True
 # chip-wide fan-ins per layer (~3-4 us each at 256 arrivals) cost more than the five launch
 # boundaries (~1.2 us each) they replace. Off by default; bench/ab_arms.py DA_DECODE_B1=1 selects it.
 _DECODE_B1 = False
+# Batch-1 decode: the attention's split merge folded into the O projection's input load
+# (attention.hip da_decode_attn_parts + gemm.hip da_gemv_omerge). Bit-identical (tests/
+# test_o_merge_gpu.py) but not faster on the MI355X: the attention loses its ticketed merge tail
+# (14.75 -> 12.38 us) and the O GEMV gains as much (5.26 -> 7.82 us: every workgroup merges the
+# whole 100 KB of partials; profiles/r4/o_merge/). Off; bench/ab_arms.py DA_O_MERGE=1 selects it.
+_O_MERGE = False
 
 
 class TPContext:
@@ -263,6 +269,10 @@ class LlamaDecoder:
         else:
             o.gemm(a, L["wo"], out=x)
         tp.all_reduce_(x)
+        return self._mlp(L, x)
+
+    def _mlp(self, L, x):
+        o, tp = self.ops, self.tp
         if o.gemv_fusable(x.shape[0], L["w_gu"].shape[0], x.shape[1], EPI_SWIGLU):  # batch 1: norm fused
             g = o.gemm(x, L["w_gu"], epi=EPI_SWIGLU, rms=(self._gain(L["ln_mlp"]), self.cfg.eps))
         else:
@@ -379,12 +389,18 @@ class LlamaDecoder:
         if self.tp.size > 1 and x.shape[0] > 1:
             return self._decode_step_tp_fused_norms(st, x)
         fuse = o.gemv_fusable(x.shape[0], self.w["layers"][0]["wqkv"].shape[0], x.shape[1])
+        omerge = self._o_merge(x.shape[0])
         for li, L in enumerate(self.w["layers"]):
             if fuse:  # batch 1: RMSNorm folded into the QKV GEMV (no separate norm launch)
                 qkv = o.gemm(x, L["wqkv"], out=st.qkv, rms=(self._gain(L["ln_attn"]), c.eps))
             else:
                 h = o.rmsnorm(x, L["ln_attn"], c.eps, out=st.h)
                 qkv = o.gemm(h, L["wqkv"], out=st.qkv)
+            if omerge:  # batch 1: attention -> split partials; the O GEMV merges them on its input load
+                parts = self._decode_attn(qkv, li, st, parts=True)
+                o.gemv_omerge(parts, L["wo"], resid=x, out=x, attn_out=st.attn)
+                self._mlp(L, x)
+                continue
             a = self._decode_attn(qkv, li, st)
             self._attn_out_and_mlp(L, a, x)
         logits = self._logits(x, gather=False, out=st.logits)  # straight into the state (no copy launch)
@@ -394,18 +410,29 @@ class LlamaDecoder:
                     active=st.active, ctr=st.pos, pos=st.pos, lens=st.lens, hist=st.hist, start=st.start, eos=st.eos)
         return st.tokens
 
-    def _decode_attn(self, qkv, li: int, st: "DecodeState"):
+    def _decode_attn(self, qkv, li: int, st: "DecodeState", parts: bool = False):
         """RoPE + new-token cache write + decode attention. MHA (Phi-3): one launch — the attention
         kernel rotates q / the new k itself and writes the new k / v to the cache; GQA: rope_cache,
-        then the MFMA decode kernel."""
+        then the MFMA decode kernel. parts=True (batch 1, _o_merge): the launch stops at the split
+        partials (ops.decode_attn_parts) for gemv_omerge."""
         c, o, cache = self.cfg, self.ops, self.cache
         D, hl, kl = c.head_dim, self.hl, self.kl
+        fn = o.decode_attn_parts if parts else o.decode_attn
+        kw = {} if parts else {"out": st.attn}
         if hl == kl and _FUSED_ROPE_DECODE:
-            return o.decode_attn(qkv, cache.k(li), cache.v(li), st.lens, st.slot, hl, kl, D, max_len=cache.max_seq,
-                                 out=st.attn, pre=st.pre, rope=(self.cos_sin, st.pos))
+            return fn(qkv, cache.k(li), cache.v(li), st.lens, st.slot, hl, kl, D, max_len=cache.max_seq,
+                      pre=st.pre, rope=(self.cos_sin, st.pos), **kw)
         o.rope_cache(qkv, st.pos, self.cos_sin, hl, kl, D, slot=st.slot, k_cache=cache.k(li), v_cache=cache.v(li))
-        return o.decode_attn(qkv, cache.k(li), cache.v(li), st.lens, st.slot, hl, kl, D, max_len=cache.max_seq,
-                             out=st.attn, pre=st.pre)
+        return fn(qkv, cache.k(li), cache.v(li), st.lens, st.slot, hl, kl, D, max_len=cache.max_seq, pre=st.pre, **kw)
+
+    def _o_merge(self, B: int) -> bool:
+        """Batch 1, one rank, the O projection a GEMV over the whole attention row, the launch split
+        (>= 2 splits at the cache capacity): attention partials merged by the O projection."""
+        c, o = self.cfg, self.ops
+        K = self.hl * c.head_dim
+        return (_O_MERGE and B == 1 and self.tp.size == 1 and hasattr(o, "gemv_omerge") and self.cache is not None
+                and K == c.hidden and K % 512 == 0 and K <= 4096 and c.head_dim % 8 == 0
+                and 2 <= o.decode_parts_splits(self.kl, self.cache.max_seq) <= 16)
 
     def _b1_decode(self, B: int) -> bool:
         """Batch 1, one rank, MHA (the fused-RoPE attention), folded norm gains, the Phi-3-mini

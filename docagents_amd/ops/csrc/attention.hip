@@ -1481,10 +1481,10 @@ DA_EXPORT int da_malloc_uncached(long long bytes, void** out) {
 
 // cos_sin / pos (both null, or both set): fused RoPE + new-token KV-cache write (MHA only; q is
 // then the raw qkv row, see DecRope).
-DA_EXPORT int da_decode_attn(const void* q, int ldq, const void* k_cache, const void* v_cache, const void* lens,
-                             const void* slot, const void* pre, int B, int H, int Hkv, int D, int max_seq, int chunk,
-                             int nsplit, float scale, void* ws, void* o, int ldo, void* counters, const void* cos_sin,
-                             const void* pos, void* stream) {
+static int decode_attn_impl(const void* q, int ldq, const void* k_cache, const void* v_cache, const void* lens,
+                            const void* slot, const void* pre, int B, int H, int Hkv, int D, int max_seq, int chunk,
+                            int nsplit, float scale, void* ws, void* o, int ldo, void* counters, const void* cos_sin,
+                            const void* pos, bool merge, void* stream) {
   bf16_t* out = (bf16_t*)o;
   int* cnt = (int*)counters;
   if (H % Hkv || chunk % 64 || nsplit < 1 || (long)chunk * nsplit < 1) return (int)hipErrorInvalidValue;
@@ -1514,7 +1514,7 @@ DA_EXPORT int da_decode_attn(const void* q, int ldq, const void* k_cache, const 
     default: return (int)hipErrorInvalidValue;
   }
   if (err) return err;
-  if (nsplit == 1 || cnt) return 0;
+  if (nsplit == 1 || cnt || !merge) return 0;
   dim3 cgrid(H, B);
   switch (D) {
     case 64: decode_combine_kernel<64><<<cgrid, 64, 0, s>>>(po, pm, pl, H, nsplit, (bf16_t*)o, ldo); break;
@@ -1522,6 +1522,28 @@ DA_EXPORT int da_decode_attn(const void* q, int ldq, const void* k_cache, const 
     case 128: decode_combine_kernel<128><<<cgrid, 128, 0, s>>>(po, pm, pl, H, nsplit, (bf16_t*)o, ldo); break;
   }
   DA_LAUNCH_CHECK();
+}
+
+DA_EXPORT int da_decode_attn(const void* q, int ldq, const void* k_cache, const void* v_cache, const void* lens,
+                             const void* slot, const void* pre, int B, int H, int Hkv, int D, int max_seq, int chunk,
+                             int nsplit, float scale, void* ws, void* o, int ldo, void* counters, const void* cos_sin,
+                             const void* pos, void* stream) {
+  return decode_attn_impl(q, ldq, k_cache, v_cache, lens, slot, pre, B, H, Hkv, D, max_seq, chunk, nsplit, scale, ws,
+                          o, ldo, counters, cos_sin, pos, true, stream);
+}
+
+// The same launch with the split merge left to the consumer (nsplit >= 2): the kernel ends at the
+// splits' fp32 partial stores in ws (layout as above: po [B][H][nsplit][D], pm / pl [B][H][nsplit])
+// and the batch-1 O projection merges them on its input load (gemm.hip da_gemv_omerge). No arrival
+// ticket and no last-split merge on the attention's critical path; ws is ordinary (cached) memory —
+// the launch boundary orders the partials before their reader.
+DA_EXPORT int da_decode_attn_parts(const void* q, int ldq, const void* k_cache, const void* v_cache, const void* lens,
+                                   const void* slot, const void* pre, int B, int H, int Hkv, int D, int max_seq,
+                                   int chunk, int nsplit, float scale, void* ws, const void* cos_sin, const void* pos,
+                                   void* stream) {
+  if (nsplit < 2 || !ws) return (int)hipErrorInvalidValue;
+  return decode_attn_impl(q, ldq, k_cache, v_cache, lens, slot, pre, B, H, Hkv, D, max_seq, chunk, nsplit, scale, ws,
+                          nullptr, 0, nullptr, cos_sin, pos, false, stream);
 }
 
 // Waves per workgroup: 0 = auto (4; 8 at D = 128), 4 / 8 force a shape (A/B runs). Round 1 picked 8

@@ -602,6 +602,195 @@ static int launch_gemv_r(const GemmArgs& a, int epi, hipStream_t s) {
   return (int)hipGetLastError();
 }
 
+// ------------------------------------------------------------------------------------------
+// Batch-1 decode O projection with the decode attention's split merge folded into its input load:
+//
+//   C[n] = resid[n] (+ bias[n]) + sum_k W[n][k] a[k],   a[h * D + d] = bf16(merge over the splits)
+//
+// The attention launch (attention.hip da_decode_attn_parts) then ends at its fp32 partial stores:
+// no arrival ticket and no last-split merge (uncached partial reads, one workgroup per head) on its
+// critical path. Each thread of a workgroup owns 8 consecutive elements of the row (one head: the
+// row is K / 8 <= NT chunks) and issues ALL of its partial loads (NS splits, clamped) before the
+// wave's weight rows: the partials come back first and are merged while the weight stream is still
+// landing (issued behind them, a CU's requests would queue behind ~100 KB of weights). The merged
+// bf16 row goes to LDS, then the same dot products as gemv_kernel (same fmaf order, same wave
+// reduction, same epilogue). The merge repeats attention.hip dec_finish's arithmetic expression for
+// expression (groups of 8 splits, online rescale) under the same contraction rule, so the row — and
+// the projection — are bit-identical to the ticketed in-kernel merge followed by gemv_kernel
+// (tests/test_o_merge_gpu.py).
+struct OMergeArgs {
+  const float* po; const float* pm; const float* pl;  // da_decode_attn_parts partials (row 0)
+  int nsplit, D;
+  bf16_t* a_out;  // nullable: workgroup 0 also stores the merged row (the attention output)
+};
+
+template <int NS>
+__device__ __forceinline__ void omerge_rows(const float (&ms)[NS], const float (&ls)[NS], const f32x4_t (&oa)[NS],
+                                            const f32x4_t (&ob)[NS], int nsplit, float (&out)[8]) {
+#pragma clang fp contract(on)
+  float M = -INFINITY, lsum = 0.f, acc[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) acc[e] = 0.f;
+#pragma unroll
+  for (int s0 = 0; s0 < NS; s0 += 8) {
+    if (s0 >= nsplit) break;
+    float mx = M;
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      if (s0 + j < nsplit) mx = fmaxf(mx, ms[s0 + j]);
+    const float mu = (mx == -INFINITY) ? 0.f : mx;
+    const float r = (M == -INFINITY) ? 0.f : exp2f(M - mu);
+    lsum *= r;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[e] *= r;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      if (s0 + j >= nsplit) continue;
+      const float f = exp2f(ms[s0 + j] - mu);
+      lsum += ls[s0 + j] * f;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        acc[e] += oa[s0 + j][e] * f;
+        acc[4 + e] += ob[s0 + j][e] * f;
+      }
+    }
+    M = mx;
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) out[e] = lsum > 0.f ? acc[e] / lsum : 0.f;
+}
+
+template <int NW, int R, int U, int NS>
+__global__ void __launch_bounds__(NW * 64)
+gemv_omerge_kernel(GemmArgs p, OMergeArgs m) {
+  __shared__ __attribute__((aligned(16))) bf16_t sa[U * 512];
+  const int lane = threadIdx.x & 63;
+  const int wv = blockIdx.x * NW + (threadIdx.x >> 6);
+  const int nkb = p.K / 512;  // 1..U: the whole row in one round of loads
+  // ---- this thread's chunk of the row: all NS splits' partials in flight first (clamped) ----
+  const int nch = p.K / 8;  // <= NW * 64 (host-checked)
+  const int c = min((int)threadIdx.x, nch - 1);
+  const int k0 = c * 8, h = k0 / m.D, d0 = k0 % m.D;
+  const size_t base = (size_t)h * m.nsplit;
+  float ms[NS], ls[NS];
+  f32x4_t oa[NS], ob[NS];
+#pragma unroll
+  for (int j = 0; j < NS; ++j) {
+    const int sp = min(j, m.nsplit - 1);
+    ms[j] = m.pm[base + sp];
+    ls[j] = m.pl[base + sp];
+    oa[j] = *(const f32x4_t*)(m.po + (base + sp) * m.D + d0);
+    ob[j] = *(const f32x4_t*)(m.po + (base + sp) * m.D + d0 + 4);
+  }
+  asm volatile("" ::: "memory");  // issue order: the partials, then the weight rows
+  int rows[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) rows[r] = wv * R + r;
+  u32x4_t wr[U][R];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int k = min(u, nkb - 1) * 512;
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+      wr[u][r] = __builtin_nontemporal_load((const u32x4_t*)(p.W + (size_t)min(rows[r], p.N - 1) * p.K + k + lane * 8));
+  }
+  {
+    float v[8];
+    omerge_rows<NS>(ms, ls, oa, ob, m.nsplit, v);
+    const u32x4_t o{pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3]), pack_bf2(v[4], v[5]), pack_bf2(v[6], v[7])};
+    if ((int)threadIdx.x < nch) {
+      *(u32x4_t*)(sa + k0) = o;
+      if (m.a_out && blockIdx.x == 0) *(u32x4_t*)(m.a_out + k0) = o;
+    }
+  }
+  __syncthreads();
+  if (rows[0] >= p.N) return;  // after the barrier: every wave helped merge
+  float acc[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) acc[r] = 0.f;
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    if (u >= nkb) break;
+    const u32x4_t av = *(const u32x4_t*)(sa + u * 512 + lane * 8);
+    float a[8];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      a[2 * e] = bf2f((bf16_t)(av[e] & 0xffff));
+      a[2 * e + 1] = bf2f((bf16_t)(av[e] >> 16));
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        acc[r] = fmaf(bf2f((bf16_t)(wr[u][r][e] & 0xffff)), a[2 * e], acc[r]);
+        acc[r] = fmaf(bf2f((bf16_t)(wr[u][r][e] >> 16)), a[2 * e + 1], acc[r]);
+      }
+  }
+#pragma unroll
+  for (int r = 0; r < R; ++r) acc[r] = wave_sum(acc[r]);
+  if (lane != 0) return;
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const int n = rows[r];
+    if (n >= p.N) continue;
+    float v = acc[r];
+    if (p.bias) v += bf2f(p.bias[n]);
+    if (p.resid) v += bf2f(p.resid[n]);
+    p.C[n] = f2bf(v);
+  }
+}
+
+// Workgroup shape of the merged O projection: waves per workgroup x rows per wave (every
+// workgroup merges the whole row, so fewer, fatter workgroups read fewer partial bytes; a thread
+// merges one 8-element chunk, so K <= 512 * waves). A/B knob.
+static int g_omerge_shape = 82;  // NW * 10 + R (82: 2.009 ms per batch-1 step, 81 2.042, 161 2.034)
+DA_EXPORT void da_set_omerge_shape(int v) { g_omerge_shape = v; }
+
+template <int NW, int R>
+static int launch_omerge(const GemmArgs& a, const OMergeArgs& mg, hipStream_t s) {
+  if (a.K > 512 * NW) return (int)hipErrorInvalidValue;  // one chunk of 8 per thread
+  const int grid = (a.N + NW * R - 1) / (NW * R), nkb = a.K / 512;
+#define OMK(U_, NS_) gemv_omerge_kernel<NW, R, U_, NS_><<<grid, NW * 64, 0, s>>>(a, mg)
+  if (mg.nsplit <= 8) {
+    if (nkb == 6) OMK(6, 8); else OMK(8, 8);
+  } else {
+    if constexpr (NW <= 8 && R == 1) {  // 16 splits' partials in registers: no spills at 8 x 1 only
+      if (nkb == 6) OMK(6, 16); else OMK(8, 16);
+    } else {
+      return (int)hipErrorInvalidValue;
+    }
+  }
+#undef OMK
+  return (int)hipGetLastError();
+}
+
+// C[N] = resid (nullable) + bias (nullable) + W[N, K] . merge(partials), one row (batch-1 decode).
+// ws = the da_decode_attn_parts workspace of B = 1: po [H][nsplit][D], then pm, pl [H][nsplit],
+// H = K / D. K % 512 == 0, K <= 4096, D % 8 == 0, 2 <= nsplit <= 16.
+DA_EXPORT int da_gemv_omerge(const void* ws, int nsplit, int D, const void* W, void* C, const void* resid,
+                             const void* bias, int N, int K, void* a_out, void* stream) {
+  if (!ws || nsplit < 2 || nsplit > 16 || D < 8 || D % 8 || K % 512 || K > 4096 || K % D || N < 1)
+    return (int)hipErrorInvalidValue;
+  const int H = K / D;
+  GemmArgs a{};
+  a.W = (const bf16_t*)W; a.C = (bf16_t*)C; a.resid = (const bf16_t*)resid; a.bias = (const bf16_t*)bias;
+  a.M = 1; a.N = N; a.K = K;
+  OMergeArgs mg{};
+  mg.po = (const float*)ws;
+  mg.pm = mg.po + (size_t)H * nsplit * D;
+  mg.pl = mg.pm + (size_t)H * nsplit;
+  mg.nsplit = nsplit; mg.D = D; mg.a_out = (bf16_t*)a_out;
+  hipStream_t s = (hipStream_t)stream;
+  // 9..16 splits: the 8-wave, 1-row shape (the only one whose registers hold 16 splits' partials)
+  const int shape = nsplit > 8 ? 81 : g_omerge_shape;
+  switch (shape) {
+    case 81: return launch_omerge<8, 1>(a, mg, s);
+    case 82: return launch_omerge<8, 2>(a, mg, s);
+    case 161: return launch_omerge<16, 1>(a, mg, s);
+    default: return (int)hipErrorInvalidValue;
+  }
+}
+
 // K-blocks (512 elements = 1 KiB per row) in flight per row: the whole row when it is short
 // (K = 3072: 6 blocks, one round of loads and no clamped duplicate loads), 8 per round otherwise.
 static int g_gemv_u = 0;  // 0 = auto; 4 = the fixed round-1 depth (A/B)

@@ -84,6 +84,11 @@ _SIGS = {
     "da_set_decode_w8": [c_int],
     "da_set_gemm8p_group": [c_int],
     "da_set_gemm8p_bm_rule": [c_int],
+    "da_set_omerge_shape": [c_int],
+    "da_decode_attn_parts": [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int,
+                             c_int, c_int, c_int, c_int, c_float, c_void_p, c_void_p, c_void_p, c_void_p],
+    "da_gemv_omerge": [c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p,
+                       c_void_p],
     "da_set_flash_rev": [c_int],
     "da_decode_attn": [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
                        c_int, c_int, c_int, c_float, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p,
@@ -723,35 +728,25 @@ def _uncached(tag: str, nbytes: int, device) -> _RawBuf:
     return bufs[-1]
 
 
-def decode_attn(q, k_cache, v_cache, lens, slot, H, Hkv, D, max_len: int, chunk: int = 0, scale=None, out=None,
-                pre=None, rope=None):
-    """q [B, >=H*D] (row stride any multiple of 8); lens/slot int32 [B]; max_len = max(lens) or the
-    cache capacity (host int, fixes the split count so the launch is graph-capturable).
-    chunk = keys per workgroup (0 = auto: enough workgroups to fill 256 CUs, 4 waves x 64-key tiles).
-    pre: optional int32 [B, 2] device tensor (P, prefix slot), P % 64 == 0: keys [0, P) of row b
-    are the batch's shared prompt head, stored once in the prefix slot (read through the cache).
-    rope = (cos_sin fp32 [max_pos, D/2, 2], pos int32 [B]), MHA only: q is the raw qkv row
-    [B, (H + 2 Hkv) D]; the kernel applies RoPE to q and the new token's k and writes that token's
-    k / v into the cache at pos (== lens - 1) — the decode step's rope_cache launch folded in."""
+def _decode_split(B: int, Hkv: int, max_len: int, chunk: int):
+    """(chunk, nsplit) of a decode-attention launch (static for a captured graph: from max_len)."""
     if chunk <= 0:
         # measured on MI355X (profiles/decode_attn_chunks_r1.txt): per-workgroup overhead dominates
         # small chunks; aim for ~768 workgroups, 512..4096 keys each
-        want = max_len * q.shape[0] * Hkv / 768
+        want = max_len * B * Hkv / 768
         chunk = 512
         while chunk < want and chunk < 4096:
             chunk *= 2
+    return chunk, max(1, math.ceil(max_len / chunk))
+
+
+def _decode_checks(q, k_cache, v_cache, lens, slot, H, Hkv, D, max_len, pre, rope):
     _bf16_cuda(q, "q"); _i32(lens, "lens"); _i32(slot, "slot")
     _req(D in (64, 96, 128), "head dim")
     _req((H // Hkv) in (1, 2, 4, 8) and H % Hkv == 0, "GQA group must be 1/2/4/8")
     B = q.shape[0]
     _req(k_cache.dim() == 4 and k_cache.shape[1] == Hkv and k_cache.shape[3] == D, "cache shape")
-    max_seq = k_cache.shape[2]
-    _req(max_len <= max_seq, "max_len > cache capacity")
-    nsplit = max(1, math.ceil(max_len / chunk))
-    ws = _workspace(B * H * nsplit * (D + 2) * 4, q.device)
-    if out is None:
-        out = torch.empty((B, H * D), dtype=torch.bfloat16, device=q.device)
-    scale = scale if scale is not None else 1.0 / math.sqrt(D)
+    _req(max_len <= k_cache.shape[2], "max_len > cache capacity")
     if pre is not None:
         _i32(pre, "pre"); _req(pre.shape == (B, 2) and pre.is_contiguous(), "pre must be int32 [B, 2]")
     cs = ps = None
@@ -762,13 +757,84 @@ def decode_attn(q, k_cache, v_cache, lens, slot, H, Hkv, D, max_len: int, chunk:
         _req(cs.dtype == torch.float32 and cs.is_contiguous() and cs.shape[1] == D // 2 and cs.shape[2] == 2, "cos_sin")
         _req(q.stride(1) == 1 and q.shape[1] >= (H + 2 * Hkv) * D, "fused RoPE decode needs the qkv row")
         _req(k_cache.is_contiguous() and v_cache.is_contiguous(), "caches must be contiguous")
+    return cs, ps
+
+
+def decode_attn(q, k_cache, v_cache, lens, slot, H, Hkv, D, max_len: int, chunk: int = 0, scale=None, out=None,
+                pre=None, rope=None):
+    """q [B, >=H*D] (row stride any multiple of 8); lens/slot int32 [B]; max_len = max(lens) or the
+    cache capacity (host int, fixes the split count so the launch is graph-capturable).
+    chunk = keys per workgroup (0 = auto: enough workgroups to fill 256 CUs, 4 waves x 64-key tiles).
+    pre: optional int32 [B, 2] device tensor (P, prefix slot), P % 64 == 0: keys [0, P) of row b
+    are the batch's shared prompt head, stored once in the prefix slot (read through the cache).
+    rope = (cos_sin fp32 [max_pos, D/2, 2], pos int32 [B]), MHA only: q is the raw qkv row
+    [B, (H + 2 Hkv) D]; the kernel applies RoPE to q and the new token's k and writes that token's
+    k / v into the cache at pos (== lens - 1) — the decode step's rope_cache launch folded in."""
+    cs, ps = _decode_checks(q, k_cache, v_cache, lens, slot, H, Hkv, D, max_len, pre, rope)
+    chunk, nsplit = _decode_split(q.shape[0], Hkv, max_len, chunk)
+    B = q.shape[0]
+    ws = _workspace(B * H * nsplit * (D + 2) * 4, q.device)
+    if out is None:
+        out = torch.empty((B, H * D), dtype=torch.bfloat16, device=q.device)
+    scale = scale if scale is not None else 1.0 / math.sqrt(D)
     cnt = None
     if _FUSED_COMBINE and nsplit > 1:
         cnt = _uncached("decode_cnt", B * Hkv * 4, q.device)
         ws = _uncached("decode_ws", B * H * nsplit * (D + 2) * 4, q.device)
     _check(lib().da_decode_attn(_ptr(q), q.stride(0), _ptr(k_cache), _ptr(v_cache), _ptr(lens), _ptr(slot), _ptr(pre), B, H,
-                                Hkv, D, max_seq, chunk, nsplit, float(scale), _ptr(ws), _ptr(out), out.stride(0), _ptr(cnt),
-                                _ptr(cs), _ptr(ps), _stream()), "decode_attn")
+                                Hkv, D, k_cache.shape[2], chunk, nsplit, float(scale), _ptr(ws), _ptr(out), out.stride(0),
+                                _ptr(cnt), _ptr(cs), _ptr(ps), _stream()), "decode_attn")
+    return out
+
+
+class DecodeParts:
+    """Split partials of a one-row decode attention whose merge is left to the O projection
+    (da_decode_attn_parts -> da_gemv_omerge): the workspace and its split count."""
+    __slots__ = ("ws", "nsplit", "H", "D")
+
+    def __init__(self, ws, nsplit: int, H: int, D: int):
+        self.ws, self.nsplit, self.H, self.D = ws, nsplit, H, D
+
+
+def decode_parts_splits(Hkv: int, max_len: int) -> int:
+    """Split count decode_attn_parts would use (>= 2 is required for the merged O projection)."""
+    return _decode_split(1, Hkv, max_len, 0)[1]
+
+
+def decode_attn_parts(q, k_cache, v_cache, lens, slot, H, Hkv, D, max_len: int, scale=None, pre=None,
+                      rope=None) -> DecodeParts:
+    """decode_attn for ONE row (batch-1 decode) without the split merge: the launch ends at the
+    splits' fp32 partials and ``gemv_omerge`` merges them on the O projection's input load (no
+    arrival ticket and no last-split merge on the attention's critical path). Same arguments as
+    decode_attn; needs >= 2 splits (decode_parts_splits)."""
+    cs, ps = _decode_checks(q, k_cache, v_cache, lens, slot, H, Hkv, D, max_len, pre, rope)
+    _req(q.shape[0] == 1, "decode_attn_parts: one row")
+    chunk, nsplit = _decode_split(1, Hkv, max_len, 0)
+    _req(2 <= nsplit <= 16, "decode_attn_parts: needs 2..16 splits")
+    ws = _workspace(H * nsplit * (D + 2) * 4, q.device)
+    scale = scale if scale is not None else 1.0 / math.sqrt(D)
+    _check(lib().da_decode_attn_parts(_ptr(q), q.stride(0), _ptr(k_cache), _ptr(v_cache), _ptr(lens), _ptr(slot),
+                                      _ptr(pre), 1, H, Hkv, D, k_cache.shape[2], chunk, nsplit, float(scale), _ptr(ws),
+                                      _ptr(cs), _ptr(ps), _stream()), "decode_attn_parts")
+    return DecodeParts(ws, nsplit, H, D)
+
+
+def gemv_omerge(parts: DecodeParts, w, resid=None, out=None, bias=None, attn_out=None):
+    """out[1, N] = resid + bias + merge(parts) @ w^T: the batch-1 O projection reading the decode
+    attention's split partials (bit-identical to decode_attn + gemm(EPI_RESID)). attn_out
+    (optional [1, H*D] bf16) also receives the merged attention row."""
+    _bf16_cuda(w, "w")
+    N, K = w.shape
+    _req(K == parts.H * parts.D and K % 512 == 0 and K <= 4096 and w.is_contiguous(), f"gemv_omerge shape N={N} K={K}")
+    if out is None:
+        out = torch.empty((1, N), dtype=torch.bfloat16, device=w.device)
+    _req(out.numel() == N and out.is_contiguous() and out.dtype == torch.bfloat16, "gemv_omerge out")
+    if resid is not None:
+        _req(resid.numel() == N and resid.is_contiguous() and resid.dtype == torch.bfloat16, "gemv_omerge resid")
+    if attn_out is not None:
+        _req(attn_out.numel() == K and attn_out.is_contiguous() and attn_out.dtype == torch.bfloat16, "attn_out")
+    _check(lib().da_gemv_omerge(_ptr(parts.ws), parts.nsplit, parts.D, _ptr(w), _ptr(out), _ptr(resid), _ptr(bias), N, K,
+                                _ptr(attn_out), _stream()), "gemv_omerge")
     return out
 
 

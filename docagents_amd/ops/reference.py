@@ -261,6 +261,81 @@ def decode_attn(q, k_cache, v_cache, lens, slot, H, Hkv, D, max_len=None, chunk=
     return res
 
 
+def _decode_split(B, Hkv, max_len, chunk=0):
+    """kernels._decode_split: (keys per split, split count) fixed by the cache capacity."""
+    if chunk <= 0:
+        want, chunk = max_len * B * Hkv / 768, 512
+        while chunk < want and chunk < 4096:
+            chunk *= 2
+    return chunk, max(1, math.ceil(max_len / chunk))
+
+
+def decode_parts_splits(Hkv, max_len):
+    return _decode_split(1, Hkv, max_len)[1]
+
+
+class DecodeParts:
+    """One row's split partials: unnormalised O [H, S, D], maxima (log2 domain) and sums [H, S]."""
+
+    def __init__(self, po, pm, pl, D):
+        self.po, self.pm, self.pl, self.D = po, pm, pl, D
+        self.H, self.nsplit = pm.shape
+
+
+def decode_attn_parts(q, k_cache, v_cache, lens, slot, H, Hkv, D, max_len=None, scale=None, pre=None, rope=None):
+    """decode_attn of one row stopped at the split partials (attention.hip da_decode_attn_parts):
+    the row's L keys spread over the launch's splits in 64-key multiples (dec_chunk), each split's
+    online-softmax state (O unnormalised, running max in the log2 domain, sum) in fp32."""
+    if rope is not None:
+        q = rope_cache(q.clone(), rope[1], rope[0], H, Hkv, D, slot=slot, k_cache=k_cache, v_cache=v_cache)
+    assert q.shape[0] == 1, "decode_attn_parts: one row"
+    chunk_arg, S = _decode_split(1, Hkv, max_len if max_len is not None else k_cache.shape[2])
+    assert S >= 2, "decode_attn_parts: needs >= 2 splits"
+    scale = scale if scale is not None else 1.0 / math.sqrt(D)
+    L, s = int(lens[0]), int(slot[0])
+    kk, vv = k_cache[s, :, :L].float(), v_cache[s, :, :L].float()
+    if pre is not None and int(pre[0, 0]) > 0:
+        P, ps = int(pre[0, 0]), int(pre[0, 1])
+        kk = torch.cat([k_cache[ps, :, :P].float(), kk[:, P:]], 1)
+        vv = torch.cat([v_cache[ps, :, :P].float(), vv[:, P:]], 1)
+    G = H // Hkv
+    kk, vv = kk.repeat_interleave(G, 0), vv.repeat_interleave(G, 0)
+    sc = (q[0, :H * D].float().view(H, 1, D) @ kk.transpose(1, 2))[:, 0] * (scale * 1.4426950408889634)  # [H, L]
+    c = min(((L + S - 1) // S + 63) & ~63, chunk_arg)
+    po = torch.zeros((H, S, D), dtype=torch.float32, device=q.device)
+    pm = torch.full((H, S), -math.inf, dtype=torch.float32, device=q.device)
+    pl = torch.zeros((H, S), dtype=torch.float32, device=q.device)
+    for j in range(S):
+        a, b = j * c, min(L, (j + 1) * c)
+        if a >= b:
+            continue
+        m = sc[:, a:b].max(dim=1).values
+        p = torch.exp2(sc[:, a:b] - m[:, None])
+        pm[:, j], pl[:, j] = m, p.sum(dim=1)
+        po[:, j] = (p[:, None, :] @ vv[:, a:b])[:, 0]
+    return DecodeParts(po, pm, pl, D)
+
+
+def merge_parts(parts):
+    """[1, H*D] fp32 attention row from the split partials (the combine every split-KV path runs)."""
+    M = parts.pm.max(dim=1, keepdim=True).values
+    Mu = torch.where(torch.isinf(M), torch.zeros_like(M), M)
+    f = torch.exp2(parts.pm - Mu)  # empty splits: exp2(-inf) = 0
+    lsum = (parts.pl * f).sum(dim=1)
+    o = (parts.po * f[:, :, None]).sum(dim=1) / torch.where(lsum > 0, lsum, torch.ones_like(lsum))[:, None]
+    return o.reshape(1, -1)
+
+
+def gemv_omerge(parts, w, resid=None, out=None, bias=None, attn_out=None):
+    """resid + bias + merge(parts) @ w^T, the merged row rounded to bf16 first (gemm.hip
+    da_gemv_omerge)."""
+    a = merge_parts(parts).to(torch.bfloat16)
+    if attn_out is not None:
+        attn_out.copy_(a.view_as(attn_out))
+    return gemm(a, w, bias=bias, epi=EPI_RESID if resid is not None else EPI_NONE,
+                resid=None if resid is None else resid.view(1, -1), out=out)
+
+
 def log_softmax_rows(logits):
     return torch.log_softmax(logits.float(), dim=-1)
 
