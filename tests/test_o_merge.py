@@ -61,3 +61,15 @@ def test_decoder_batch1_steps_same_with_merged_o_projection():
         finally:
             LM._O_MERGE = old
     assert torch.allclose(logits[True], logits[False], atol=3e-2), (logits[True] - logits[False]).abs().max()
+
+
+def test_split_count_rule_matches_the_kernels_module():
+    """reference._decode_split mirrors kernels._decode_split (the launch's split count is what the
+    O projection's merge is sized for)."""
+    from docagents_amd.ops import kernels as K
+    for B in (1, 2, 16, 64):
+        for Hkv in (8, 32):
+            for max_len in (256, 1000, 4096, 8192):
+                for chunk in (0, 256, 1024):
+                    assert K._decode_split(B, Hkv, max_len, chunk) == R._decode_split(B, Hkv, max_len, chunk)
+    assert K.decode_parts_splits(32, 4096) == R.decode_parts_splits(32, 4096) == 8
