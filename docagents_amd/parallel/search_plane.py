@@ -38,6 +38,7 @@ from __future__ import annotations
 import collections
 import concurrent.futures as cf
 import hashlib
+import queue
 import socket
 import struct
 import threading
@@ -112,6 +113,9 @@ class ShardUnavailable(RuntimeError):
     pass
 
 
+_REPLY_BACKLOG = 4096  # queued replies per requester connection before the shard drops it
+
+
 class _Job:
     """One part of a search on the local shard: rows [m, d] + per-row filters, and where the answer
     goes (``reply(scores, keys)`` / ``fail(exc)``)."""
@@ -141,7 +145,8 @@ class _Peer:
     def __init__(self, plane, rank: int, addr):
         self.plane, self.rank, self.addr = plane, rank, tuple(addr)
         self.sock = None
-        self.lock = threading.Lock()
+        self.lock = threading.Lock()   # sock / pending (the reader takes it per reply)
+        self.wlock = threading.Lock()  # one request frame at a time on the wire
         self.pending: dict = {}
         self.down_since = None
         self.last_try = 0.0
@@ -172,6 +177,9 @@ class _Peer:
                     self._connect()
                 self.pending[rid] = (on_reply, on_fail)
                 sock = self.sock
+            # the frame goes out under the write lock only: a send blocked on a slow shard's full
+            # receive buffer never holds up the reader thread that delivers this peer's replies
+            with self.wlock:
                 _send_frame(sock, msg)
         except ShardUnavailable as e:
             on_fail(e)
@@ -456,14 +464,34 @@ class SearchPlane:
             threading.Thread(target=self._serve_conn, args=(c,), name=f"plane-conn-{self.rank}", daemon=True).start()
 
     def _serve_conn(self, c):
-        wlock = threading.Lock()
+        # replies leave through this connection's own writer thread: the scan worker only queues
+        # them, so a requester that stops reading (its receive buffer full) blocks its own writer,
+        # never the shard's scans for everyone else; past _REPLY_BACKLOG queued replies the
+        # connection is dropped (that requester fails its own pending parts)
+        outq: queue.Queue = queue.Queue()
+        dead = threading.Event()
+
+        def writer():
+            while True:
+                obj = outq.get()
+                if obj is None or dead.is_set():
+                    return
+                try:
+                    _send_frame(c, obj)
+                except OSError:
+                    dead.set()
+                    _close(c)
+                    return
 
         def send(obj):
-            try:
-                with wlock:
-                    _send_frame(c, obj)
-            except OSError:
-                pass  # the requester went away; its side fails its own pending parts
+            if dead.is_set():
+                return
+            if outq.qsize() >= _REPLY_BACKLOG:
+                dead.set()
+                _close(c)
+                return
+            outq.put(obj)
+        threading.Thread(target=writer, name=f"plane-reply-{self.rank}", daemon=True).start()
         try:
             while not self._stop:
                 msg = _recv_frame(c)
@@ -486,10 +514,9 @@ class SearchPlane:
         except Exception:  # noqa: BLE001 - EOF / reset: the requester's side handles it
             pass
         finally:
-            try:
-                c.close()
-            except OSError:
-                pass
+            dead.set()
+            outq.put(None)
+            _close(c)
             try:
                 self._conns.remove(c)
             except ValueError:
@@ -557,6 +584,14 @@ class SearchPlane:
         self.stats["scans"] += 1
         self.stats["rows"] += len(Q)
         self.stats["busy_s"] += time.perf_counter() - t0
+
+
+def _close(sock):
+    for fn in (lambda: sock.shutdown(socket.SHUT_RDWR), sock.close):
+        try:
+            fn()
+        except OSError:
+            pass
 
 
 class _nullctx:

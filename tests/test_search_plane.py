@@ -144,3 +144,27 @@ def test_timed_out_parts_leave_no_pending_callbacks():
     finally:
         for p in planes:
             p.stop(timeout=2)
+
+
+def test_requester_that_stops_reading_does_not_stall_the_shard():
+    """A client that sends big searches and never reads the replies fills its socket buffers; the
+    shard's scan worker must keep serving everyone else (replies leave through a per-connection
+    writer thread, not the scan thread)."""
+    from docagents_amd.parallel.search_plane import _send_frame
+    planes, idx, docs, X = _pair(timeout_s=5.0)
+    stuck = socket.create_connection(planes[0].addrs[0])
+    stuck.setsockopt(socket.SOL_SOCKET, socket.SO_RCVBUF, 4096)
+    try:
+        big = _unit(512, 32, 11)
+        for i in range(8):  # 8 replies of 512 x 1024 (scores + keys) = ~6 MB each, never read
+            _send_frame(stuck, {"id": 10_000 + i, "vecs": big, "k": 1024, "thr": -1.0, "filters": None})
+        time.sleep(1.0)  # the shard has scanned them and is stuck writing to this client (old design)
+        q = _unit(1, 32, 12)
+        t0 = time.monotonic()
+        s, k = planes[1].submit(q, 3, -1.0, [docs[0][:2]]).result(10)  # a part served by rank 0
+        assert (k >= 0).all() and time.monotonic() - t0 < 3
+        assert planes[0].stats["served_remote"] >= 9
+    finally:
+        stuck.close()
+        for p in planes:
+            p.stop(timeout=2)
