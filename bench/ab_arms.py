@@ -49,7 +49,7 @@ def apply_env_overrides() -> dict:
     done = {}
     from docagents_amd.models import llama
     for env, attr in (("DA_PREFILL_NORM_FUSE", "_PREFILL_NORM_FUSE"), ("DA_DECODE_B1", "_DECODE_B1"),
-                      ("DA_O_MERGE", "_O_MERGE")):
+                      ("DA_O_MERGE", "_O_MERGE"), ("DA_QKV_FOLD", "_QKV_FOLD")):
         if os.environ.get(env) is not None:  # model-level code paths (default: llama.py)
             setattr(llama, attr, os.environ[env] == "1")
             done[env] = int(getattr(llama, attr))

@@ -49,6 +49,12 @@ _DECODE_B1 = False
 # (14.75 -> 12.38 us) and the O GEMV gains as much (5.26 -> 7.82 us: every workgroup merges the
 # whole 100 KB of partials; profiles/r4/o_merge/). Off; bench/ab_arms.py DA_O_MERGE=1 selects it.
 _O_MERGE = False
+# 33..64-row decode: the QKV projection's split-K reduce folded into the decode attention's prologue
+# (ops.gemm_dk_qkv_parts -> decode_attn reads the partials). Bit-identical (tests/
+# test_qkv_fold_gpu.py) but not faster on the MI355X: 14.85 vs 14.79 ms per batch-64 step
+# (bench/qkv_fold_ab.py, profiles/r4/qkv_fold/) — 2048 attention workgroups each rebuilding their
+# q / k / v from 3 splits cost what the reduce launch does. Off; bench/ab_arms.py DA_QKV_FOLD=1.
+_QKV_FOLD = False
 
 
 class TPContext:
@@ -490,6 +496,15 @@ class LlamaDecoder:
                   (self.w["lm_head"], EPI_NONE)]
         return all(f(B, w.shape[0], w.shape[1], e) for w, e in shapes) and o.dk_parts(c.hidden, B) <= 512
 
+    def _qkv_fold(self, B: int) -> bool:
+        """The QKV projection on the split-K route and MHA with the fused-RoPE attention (past the
+        small-batch prefetch variants, which read a bf16 row): its reduce runs in the attention's
+        prologue (_QKV_FOLD)."""
+        o = self.ops
+        w = self.w["layers"][0]["wqkv"]
+        return (_QKV_FOLD and hasattr(o, "gemm_dk_qkv_parts") and self.hl == self.kl and _FUSED_ROPE_DECODE
+                and o.qkv_parts_route(B, w.shape[0], w.shape[1]) and B * self.kl > 32)
+
     def _decode_step_dk(self, st: "DecodeState", x: torch.Tensor) -> torch.Tensor:
         """A layer = QKV, attention, O (+ residual, row sums of squares), gate/up + SwiGLU (norm
         deferred from those sums), down (+ residual, sums): 5 launches, no reduce launches, no
@@ -499,8 +514,12 @@ class LlamaDecoder:
         sa, sb = st.ssq
         parts = o.dk_parts(c.hidden, x.shape[0])
         a_in, norm = o.rmsnorm(x, layers[0]["ln_attn"], c.eps, out=st.h), None
+        fold = self._qkv_fold(x.shape[0])
         for li, L in enumerate(layers):
-            qkv = o.gemm_dk(a_in, L["wqkv"], out=st.qkv, norm_in=norm)
+            if fold:  # the split-K partials go straight to the attention (no reduce launch)
+                qkv = o.gemm_dk_qkv_parts(a_in, L["wqkv"], norm_in=norm)
+            else:
+                qkv = o.gemm_dk(a_in, L["wqkv"], out=st.qkv, norm_in=norm)
             a = self._decode_attn(qkv, li, st)
             o.gemm_dk(a, L["wo"], epi=EPI_RESID, resid=x, out=x, ssq_out=sa)               # x += o
             g = o.gemm_dk(x, L["w_gu"], epi=EPI_SWIGLU, norm_in=(sa, parts, c.eps))        # norm(x) -> gate/up

@@ -821,6 +821,14 @@ struct DecRope {
   const float* cs;      // [max_pos][D/2][2] (cos, sin)
   const int* pos;       // [B]
   unsigned long long* trace;  // VAR bit 3 only: per-workgroup wall-clock stamps (bench/decode_trace.py)
+  // QKV projection folded in (qp != null; MHA, no-prefetch path): row b's qkv element col is read
+  // from the projection's split-K partials instead of its reduced bf16 row —
+  // bf16((0 + p_0 + ... + p_{S-1}) * inv_b), inv_b = rsqrt(sum_q ssq[q][b] / norm_k + eps) (1 without
+  // ssq): the arithmetic of gemm.hip gemm_splitk_reduce (epilogue NONE, no bias), so the same bits
+  // as the reduce launch it replaces
+  const float* qp; const float* qp_ssq;
+  int qp_splits, qp_M, qp_N, qp_parts, qp_normk;
+  float qp_eps;
 };
 
 template <int D, int G, int VAR>
@@ -920,6 +928,20 @@ decode_attn_kernel(const bf16_t* __restrict__ q, int ldq, const bf16_t* __restri
     return rot2(bf2f(hp[d & ~1]), bf2f(hp[d | 1]), rope.cs[((size_t)p * HALF + i) * 2],
                 rope.cs[((size_t)p * HALF + i) * 2 + 1], d);
   };
+  // element col of row b's qkv row: the bf16 row, or rebuilt from the QKV split-K partials
+  float qinv = 1.f;
+  if (rope.qp != nullptr && rope.qp_ssq != nullptr)
+    qinv = rsqrtf(sum_strided(rope.qp_ssq + b, rope.qp_parts, 64) / rope.qp_normk + rope.qp_eps);
+  auto qel = [&](int col) -> bf16_t {
+    if (rope.qp == nullptr) return q[(size_t)b * ldq + col];
+    const float v = sum_strided(rope.qp + (size_t)b * rope.qp_N + col, rope.qp_splits, (size_t)rope.qp_M * rope.qp_N);
+    return f2bf(v * qinv);
+  };
+  auto rotc = [&](int col0, int d, int p) -> float {
+    const int i = d >> 1;
+    return rot2(bf2f(qel(col0 + (d & ~1))), bf2f(qel(col0 + (d | 1))), rope.cs[((size_t)p * HALF + i) * 2],
+                rope.cs[((size_t)p * HALF + i) * 2 + 1], d);
+  };
   // PFT (small batches): the prologue's operands (this thread's q element, its RoPE partner and
   // cos / sin, the new token's k / v element) are loaded FIRST, then the first two K/V tiles of the
   // wave are requested, unconditionally (an empty tile reads one line), so the compiler's counted
@@ -966,20 +988,37 @@ decode_attn_kernel(const bf16_t* __restrict__ q, int ldq, const bf16_t* __restri
     }
     for (int i = tid; i < G * D; i += NTH) {
       const int g = i / D, d = i % D;
-      const bf16_t* hp = q + (size_t)b * ldq + (hk * G + g) * D;
-      sq[g][d] = (fr ? rot(hp, d, L - 1) : bf2f(hp[d])) * scale_log2e;
+      if (rope.qp == nullptr) {
+        const bf16_t* hp = q + (size_t)b * ldq + (hk * G + g) * D;
+        sq[g][d] = (fr ? rot(hp, d, L - 1) : bf2f(hp[d])) * scale_log2e;
+      } else {
+        const int col0 = (hk * G + g) * D;
+        sq[g][d] = (fr ? rotc(col0, d, L - 1) : bf2f(qel(col0 + d))) * scale_log2e;
+      }
     }
   }
   if (own_new && !PRE) {
-    const bf16_t* kr = q + (size_t)b * ldq + (size_t)(H + hk) * D;
-    const bf16_t* vr = q + (size_t)b * ldq + (size_t)(H + Hkv + hk) * D;
     const size_t crow = cbase + (size_t)(L - 1) * D;
-    for (int d = tid; d < D; d += NTH) {
-      const float kv = rot(kr, d, L - 1);
-      skn[d] = kv;
-      svn[d] = bf2f(vr[d]);
-      rope.kc[crow + d] = f2bf(kv);  // for later steps (read back only after this launch)
-      rope.vc[crow + d] = vr[d];
+    if (rope.qp == nullptr) {
+      const bf16_t* kr = q + (size_t)b * ldq + (size_t)(H + hk) * D;
+      const bf16_t* vr = q + (size_t)b * ldq + (size_t)(H + Hkv + hk) * D;
+      for (int d = tid; d < D; d += NTH) {
+        const float kv = rot(kr, d, L - 1);
+        skn[d] = kv;
+        svn[d] = bf2f(vr[d]);
+        rope.kc[crow + d] = f2bf(kv);  // for later steps (read back only after this launch)
+        rope.vc[crow + d] = vr[d];
+      }
+    } else {
+      const int kcol = (H + hk) * D, vcol = (H + Hkv + hk) * D;
+      for (int d = tid; d < D; d += NTH) {
+        const float kv = rotc(kcol, d, L - 1);
+        const bf16_t nv = qel(vcol + d);
+        skn[d] = kv;
+        svn[d] = bf2f(nv);
+        rope.kc[crow + d] = f2bf(kv);
+        rope.vc[crow + d] = nv;
+      }
     }
   }
   if constexpr (G > 1) {
@@ -1481,16 +1520,25 @@ DA_EXPORT int da_malloc_uncached(long long bytes, void** out) {
 
 // cos_sin / pos (both null, or both set): fused RoPE + new-token KV-cache write (MHA only; q is
 // then the raw qkv row, see DecRope).
+struct QkvParts {  // the QKV projection's split-K partials (DecRope qp*): null ws = a bf16 qkv row
+  const float* ws; const float* ssq;
+  int splits, M, N, parts, normk;
+  float eps;
+};
+
 static int decode_attn_impl(const void* q, int ldq, const void* k_cache, const void* v_cache, const void* lens,
                             const void* slot, const void* pre, int B, int H, int Hkv, int D, int max_seq, int chunk,
                             int nsplit, float scale, void* ws, void* o, int ldo, void* counters, const void* cos_sin,
-                            const void* pos, bool merge, void* stream) {
+                            const void* pos, bool merge, void* stream, QkvParts qp = QkvParts{}) {
   bf16_t* out = (bf16_t*)o;
   int* cnt = (int*)counters;
   if (H % Hkv || chunk % 64 || nsplit < 1 || (long)chunk * nsplit < 1) return (int)hipErrorInvalidValue;
-  if ((cos_sin == nullptr) != (pos == nullptr) || (cos_sin && (H != Hkv || ldq < (H + 2 * Hkv) * D)))
+  if ((cos_sin == nullptr) != (pos == nullptr) ||
+      (cos_sin && (H != Hkv || (qp.ws ? qp.N : ldq) < (H + 2 * Hkv) * D)))
     return (int)hipErrorInvalidValue;
-  const DecRope rope{(bf16_t*)k_cache, (bf16_t*)v_cache, (const float*)cos_sin, (const int*)pos, nullptr};
+  DecRope rope{(bf16_t*)k_cache, (bf16_t*)v_cache, (const float*)cos_sin, (const int*)pos, nullptr};
+  rope.qp = qp.ws; rope.qp_ssq = qp.ssq; rope.qp_splits = qp.splits; rope.qp_M = qp.M; rope.qp_N = qp.N;
+  rope.qp_parts = qp.parts; rope.qp_normk = qp.normk; rope.qp_eps = qp.eps;
   if (B == 0) return 0;
   if (!g_dec_balance) chunk = -chunk;  // kernels: negative = fixed keys per split (dec_chunk)
   const int G = H / Hkv;
@@ -1544,6 +1592,26 @@ DA_EXPORT int da_decode_attn_parts(const void* q, int ldq, const void* k_cache, 
   if (nsplit < 2 || !ws) return (int)hipErrorInvalidValue;
   return decode_attn_impl(q, ldq, k_cache, v_cache, lens, slot, pre, B, H, Hkv, D, max_seq, chunk, nsplit, scale, ws,
                           nullptr, 0, nullptr, cos_sin, pos, false, stream);
+}
+
+// The same launch reading q and the new token's k / v from the QKV projection's split-K partials
+// (gemm.hip da_gemm_dk_splitk_parts: [splits][M][N] fp32, the deferred row norm from ssq [parts][64]
+// or none) instead of its reduced bf16 row: the 33..64-row decode's QKV reduce launch folded into
+// the attention's prologue, bit-identical. MHA with fused RoPE, B = M, and the no-prefetch variant
+// only (B * Hkv above the prefetch threshold).
+DA_EXPORT int da_decode_attn_qkvparts(const void* qkv_ws, int splits, int N, const void* ssq, int parts, int norm_k,
+                                      float eps, const void* k_cache, const void* v_cache, const void* lens,
+                                      const void* slot, const void* pre, int B, int H, int Hkv, int D, int max_seq,
+                                      int chunk, int nsplit, float scale, void* ws, void* o, int ldo, void* counters,
+                                      const void* cos_sin, const void* pos, void* stream) {
+  if (!qkv_ws || splits < 1 || !cos_sin || H != Hkv || B < 1 || B > 64) return (int)hipErrorInvalidValue;
+  if (ssq && (parts < 1 || norm_k < 1 || !(eps > 0.f))) return (int)hipErrorInvalidValue;
+  if ((g_dec_pft && B * Hkv <= g_dec_pft) || (g_dec_w8 && B * Hkv <= g_dec_w8))
+    return (int)hipErrorInvalidValue;  // the prefetch variants read q directly
+  if (g_dec_trace) return (int)hipErrorInvalidValue;
+  const QkvParts qp{(const float*)qkv_ws, (const float*)ssq, splits, B, N, ssq ? parts : 0, norm_k, eps};
+  return decode_attn_impl(nullptr, 0, k_cache, v_cache, lens, slot, pre, B, H, Hkv, D, max_seq, chunk, nsplit, scale,
+                          ws, o, ldo, counters, cos_sin, pos, true, stream, qp);
 }
 
 // Waves per workgroup: 0 = auto (4; 8 at D = 128), 4 / 8 force a shape (A/B runs). Round 1 picked 8

@@ -113,6 +113,22 @@ __device__ __forceinline__ s16x4_t lds_read_tr16(const void* p) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4_t*)(p));
 }
 
+// sum_{q < n} p[q * stride] in index order (((0 + p_0) + p_1) + ...), the loads issued 8 at a time:
+// a runtime-count loop of `s += p[q * stride]` waits for each load before the next add — one
+// memory round trip per term (the split-K reduce's deferred-norm sums were 6 in a row).
+__device__ __forceinline__ float sum_strided(const float* __restrict__ p, int n, size_t stride) {
+  float s = 0.f;
+  for (int q0 = 0; q0 < n; q0 += 8) {
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = p[(size_t)min(q0 + j, n - 1) * stride];
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      if (q0 + j < n) s += v[j];
+  }
+  return s;
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

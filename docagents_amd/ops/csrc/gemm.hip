@@ -65,8 +65,7 @@ __device__ __forceinline__ void splitk_fused_epilogue(const GemmArgs& p, const f
   const int epi = p.fuse_epi;
   auto row_scale = [&](int gm) -> float {
     if (!p.ssq_in) return 1.f;
-    float ss = 0.f;
-    for (int q = 0; q < p.ssq_parts; ++q) ss += p.ssq_in[q * 64 + gm];
+    const float ss = sum_strided(p.ssq_in + gm, p.ssq_parts, 64);
     return rsqrtf(ss / p.norm_k + p.norm_eps);
   };
   if (epi == EPI_SWIGLU) {
@@ -414,9 +413,7 @@ gemm_splitk_reduce(const float* __restrict__ ws, int splits, int M, int N, int e
     const int m = (int)(idx / chunks), oc = (int)(idx % chunks) * 8;
     float inv = 1.f;
     if (ssq_in) {  // a handful of L2-resident floats per row (fixed summation order)
-      float ss = 0.f;
-      for (int q = 0; q < parts; ++q) ss += ssq_in[q * 64 + m];
-      inv = rsqrtf(ss / norm_k + eps);
+      inv = rsqrtf(sum_strided(ssq_in + m, parts, 64) / norm_k + eps);
     }
     float v[8];
     if (epi == EPI_SWIGLU) {
@@ -1037,6 +1034,20 @@ DA_EXPORT int da_gemm_dk_splitk(const void* A, int lda, const void* W, void* C, 
                                              (const bf16_t*)resid, ldr, (bf16_t*)C, ldc, ssq_in, ssq_parts, norm_k,
                                              eps);
   DA_LAUNCH_CHECK();
+}
+
+// The 33..64-row split-K tiles alone (no reduce launch): ws receives splits x [M][N] fp32 partials
+// for a consumer that reduces them itself — the decode attention's prologue for the QKV projection
+// (attention.hip da_decode_attn_qkvparts: sum in split order, deferred row norm, bf16 — the
+// arithmetic of gemm_splitk_reduce). No epilogue: bias / SwiGLU / residual need the reduce.
+DA_EXPORT int da_gemm_dk_splitk_parts(const void* A, int lda, const void* W, int M, int N, int K, void* ws,
+                                      int splits, void* stream) {
+  if (M < 1 || M > 64 || K % 64 || N % 16 || lda % 8 || !ws || splits < 1 || (K / 64) % splits)
+    return (int)hipErrorInvalidValue;
+  GemmArgs a{};
+  a.A = (const bf16_t*)A; a.W = (const bf16_t*)W; a.ws = (float*)ws;
+  a.M = M; a.N = N; a.K = K; a.lda = lda; a.ldc = N; a.k_per_split = K / splits;
+  return launch_decode_tile<64, 128>(a, EPI_PARTIAL, splits, (hipStream_t)stream);
 }
 
 // The same contract with the split-K reduction done by each tile's last split inside the tile

@@ -85,6 +85,10 @@ _SIGS = {
     "da_set_gemm8p_group": [c_int],
     "da_set_gemm8p_bm_rule": [c_int],
     "da_set_omerge_shape": [c_int],
+    "da_gemm_dk_splitk_parts": [c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_void_p],
+    "da_decode_attn_qkvparts": [c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_float, c_void_p, c_void_p, c_void_p,
+                                c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_float, c_void_p,
+                                c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p],
     "da_decode_attn_parts": [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int,
                              c_int, c_int, c_int, c_int, c_float, c_void_p, c_void_p, c_void_p, c_void_p],
     "da_gemv_omerge": [c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p,
@@ -389,6 +393,45 @@ def gemm_dk(a, w, epi: int = EPI_NONE, bias=None, resid=None, out=None, norm_in=
     _check(lib().da_gemm_dk(_ptr(a), a.stride(0), _ptr(w), _ptr(out), out.stride(0), _ptr(bias), _ptr(resid), ldr,
                             M, N, K, epi, _ptr(ssq), parts, K, float(eps), _ptr(ssq_out), _stream()), "gemm_dk")
     return out
+
+
+class QKVParts:
+    """The 33..64-row QKV projection left as split-K partials (da_gemm_dk_splitk_parts) for the
+    decode attention to reduce in its prologue (decode_attn(q=QKVParts)): ws [splits][M][N] fp32 and
+    the deferred row norm (ssq [parts][64], eps; K = the norm width)."""
+    __slots__ = ("ws", "splits", "M", "N", "K", "ssq", "parts", "eps")
+
+    def __init__(self, ws, splits, M, N, K, ssq, parts, eps):
+        self.ws, self.splits, self.M, self.N, self.K = ws, splits, M, N, K
+        self.ssq, self.parts, self.eps = ssq, parts, eps
+
+    @property
+    def shape(self):
+        return (self.M, self.N)
+
+
+def qkv_parts_route(M: int, N: int, K: int) -> bool:
+    """True when gemm_dk(M x N x K) takes the split-K tiles whose reduce a consumer can absorb."""
+    return DECODE_DK and _dk_splitk(M, N) and K % 256 == 0 and not SPLITK_FUSED
+
+
+def gemm_dk_qkv_parts(a, w, norm_in=None) -> QKVParts:
+    """The QKV projection of a 33..64-row decode step without its reduce launch: the split-K
+    partials stay in the workspace for decode_attn to reduce (bit-identical to gemm_dk, which
+    reduces them in gemm_splitk_reduce). norm_in = gemm_dk's deferred RMSNorm (ssq, parts, eps)."""
+    _bf16_cuda(a, "a"); _bf16_cuda(w, "w")
+    M, K = a.shape
+    N = w.shape[0]
+    _req(qkv_parts_route(M, N, K) and w.shape[1] == K and w.is_contiguous(), f"gemm_dk_qkv_parts M={M} N={N} K={K}")
+    _req(a.stride(1) == 1 and a.stride(0) % 8 == 0, "gemm_dk_qkv_parts layout")
+    splits = _dk_splits(N, K)
+    ws = _workspace(splits * M * N * 4, a.device)
+    ssq, parts, eps = (None, 0, 0.0) if norm_in is None else norm_in
+    if ssq is not None:
+        _req(ssq.dtype == torch.float32 and ssq.is_contiguous() and ssq.numel() >= parts * 64, "bad ssq_in")
+    _check(lib().da_gemm_dk_splitk_parts(_ptr(a), a.stride(0), _ptr(w), M, N, K, _ptr(ws), splits, _stream()),
+           "gemm_dk_splitk_parts")
+    return QKVParts(ws, splits, M, N, K, ssq, parts, eps)
 
 
 # Every GEMM runs on the in-tree kernels: gemm8p (phase-split BMx256, csrc/gemm8p.hip) from 256
@@ -770,6 +813,9 @@ def decode_attn(q, k_cache, v_cache, lens, slot, H, Hkv, D, max_len: int, chunk:
     rope = (cos_sin fp32 [max_pos, D/2, 2], pos int32 [B]), MHA only: q is the raw qkv row
     [B, (H + 2 Hkv) D]; the kernel applies RoPE to q and the new token's k and writes that token's
     k / v into the cache at pos (== lens - 1) — the decode step's rope_cache launch folded in."""
+    if isinstance(q, QKVParts):
+        return _decode_attn_qkvparts(q, k_cache, v_cache, lens, slot, H, Hkv, D, max_len, chunk, scale, out, pre,
+                                     rope)
     cs, ps = _decode_checks(q, k_cache, v_cache, lens, slot, H, Hkv, D, max_len, pre, rope)
     chunk, nsplit = _decode_split(q.shape[0], Hkv, max_len, chunk)
     B = q.shape[0]
@@ -784,6 +830,38 @@ def decode_attn(q, k_cache, v_cache, lens, slot, H, Hkv, D, max_len: int, chunk:
     _check(lib().da_decode_attn(_ptr(q), q.stride(0), _ptr(k_cache), _ptr(v_cache), _ptr(lens), _ptr(slot), _ptr(pre), B, H,
                                 Hkv, D, k_cache.shape[2], chunk, nsplit, float(scale), _ptr(ws), _ptr(out), out.stride(0),
                                 _ptr(cnt), _ptr(cs), _ptr(ps), _stream()), "decode_attn")
+    return out
+
+
+def _decode_attn_qkvparts(qp: QKVParts, k_cache, v_cache, lens, slot, H, Hkv, D, max_len, chunk, scale, out, pre,
+                          rope):
+    """decode_attn with q / the new token's k and v reduced from the QKV projection's split-K
+    partials in the attention prologue (attention.hip da_decode_attn_qkvparts)."""
+    _req(rope is not None and H == Hkv and qp.N >= (H + 2 * Hkv) * D, "QKV partials: MHA with fused RoPE")
+    _i32(lens, "lens"); _i32(slot, "slot")
+    _req(D in (64, 96, 128) and k_cache.dim() == 4 and k_cache.shape[1] == Hkv and k_cache.shape[3] == D, "cache shape")
+    _req(max_len <= k_cache.shape[2] and k_cache.is_contiguous() and v_cache.is_contiguous(), "cache")
+    B = qp.M
+    _req(lens.numel() == B and slot.numel() == B, "lens / slot")
+    if pre is not None:
+        _i32(pre, "pre"); _req(pre.shape == (B, 2) and pre.is_contiguous(), "pre must be int32 [B, 2]")
+    cs, ps = rope
+    _i32(ps, "pos")
+    _req(cs.dtype == torch.float32 and cs.is_contiguous() and cs.shape[1] == D // 2 and cs.shape[2] == 2, "cos_sin")
+    chunk, nsplit = _decode_split(B, Hkv, max_len, chunk)
+    dev = k_cache.device
+    if out is None:
+        out = torch.empty((B, H * D), dtype=torch.bfloat16, device=dev)
+    scale = scale if scale is not None else 1.0 / math.sqrt(D)
+    ws = cnt = None
+    if nsplit > 1:  # never the attention's own workspace: the QKV partials live there
+        _req(_FUSED_COMBINE, "QKV partials: the in-kernel split merge")
+        cnt = _uncached("decode_cnt", B * Hkv * 4, dev)
+        ws = _uncached("decode_ws", B * H * nsplit * (D + 2) * 4, dev)
+    _check(lib().da_decode_attn_qkvparts(_ptr(qp.ws), qp.splits, qp.N, _ptr(qp.ssq), qp.parts, qp.K, float(qp.eps),
+                                         _ptr(k_cache), _ptr(v_cache), _ptr(lens), _ptr(slot), _ptr(pre), B, H, Hkv, D,
+                                         k_cache.shape[2], chunk, nsplit, float(scale), _ptr(ws), _ptr(out),
+                                         out.stride(0), _ptr(cnt), _ptr(cs), _ptr(ps), _stream()), "decode_attn_qkvparts")
     return out
 
 

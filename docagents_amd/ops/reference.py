@@ -235,7 +235,9 @@ def decode_attn(q, k_cache, v_cache, lens, slot, H, Hkv, D, max_len=None, chunk=
                 rope=None):
     """pre: optional int32 [B, 2] = (P, prefix slot): keys [0, P) of row b come from the prefix slot.
     rope = (cos_sin, pos): q is the raw qkv row; RoPE + the new token's cache write happen here
-    (rope_cache on a copy of the rows, then attention)."""
+    (rope_cache on a copy of the rows, then attention). q may be a QKVParts (gemm_dk_qkv_parts)."""
+    if isinstance(q, QKVParts):
+        q = q.qkv
     if rope is not None:
         q = rope_cache(q.clone(), rope[1], rope[0], H, Hkv, D, slot=slot, k_cache=k_cache, v_cache=v_cache)
     scale = scale if scale is not None else 1.0 / math.sqrt(D)
@@ -583,6 +585,23 @@ def dk_parts(N, M=0):
         return N // 128 if SPLITK_FUSED else N // 512
     bn = 64 if N // 64 >= 192 else (32 if N // 32 >= 192 else 16)
     return (N + bn - 1) // bn
+
+
+def qkv_parts_route(M, N, K):
+    """kernels.qkv_parts_route: the 33..64-row split-K route whose reduce the attention absorbs."""
+    return DECODE_DK and DK_SPLITK_ABOVE < M <= 64 and N % 512 == 0 and K % 256 == 0 and not SPLITK_FUSED
+
+
+class QKVParts:
+    """kernels.QKVParts stand-in: the oracle keeps the finished projection (there are no partials)."""
+
+    def __init__(self, qkv):
+        self.qkv = qkv
+        self.shape = qkv.shape
+
+
+def gemm_dk_qkv_parts(a, w, norm_in=None):
+    return QKVParts(gemm_dk(a, w, norm_in=norm_in))
 
 
 def gemm_dk(a, w, epi=EPI_NONE, bias=None, resid=None, out=None, norm_in=None, ssq_out=None):

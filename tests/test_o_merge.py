@@ -73,3 +73,32 @@ def test_split_count_rule_matches_the_kernels_module():
                 for chunk in (0, 256, 1024):
                     assert K._decode_split(B, Hkv, max_len, chunk) == R._decode_split(B, Hkv, max_len, chunk)
     assert K.decode_parts_splits(32, 4096) == R.decode_parts_splits(32, 4096) == 8
+
+
+def test_decoder_64_row_steps_same_with_qkv_fold():
+    """The 33..64-row decode with the QKV reduce folded into the attention (reference stand-ins:
+    the oracle keeps the finished projection) runs the same steps as the reduce-launch path."""
+    cfg = dataclasses.replace(decoder_config("tiny-dec-tp8"), layers=2, heads=8, kv_heads=8)  # MHA
+    m = LM.LlamaDecoder(cfg, "cpu", seed=5)
+    m.alloc_cache(36, 256)
+    B = 34
+    assert not LM._QKV_FOLD  # off by default (measured no faster on the MI355X)
+    logits = {}
+    for on in (True, False):
+        old = LM._QKV_FOLD
+        LM._QKV_FOLD = on
+        try:
+            assert m._qkv_fold(B) == on and not m._qkv_fold(8)
+            m.cache.buf.zero_()
+            st = LM.DecodeState(m, B, 8, 0.0, 0, ())
+            st.slot.copy_(torch.arange(B, dtype=torch.int32)); st.active.fill_(1); st.start.zero_()
+            st.lens.fill_(1); st.pos.zero_()
+            st.tokens.copy_(torch.arange(B, dtype=torch.int32) * 37 + 5)
+            out = []
+            for _ in range(3):
+                m.decode_step(st)
+                out.append(st.logits.float().clone())
+            logits[on] = torch.stack(out)
+        finally:
+            LM._QKV_FOLD = old
+    assert torch.equal(logits[True], logits[False])
