@@ -129,6 +129,34 @@ __device__ __forceinline__ float sum_strided(const float* __restrict__ p, int n,
   return s;
 }
 
+// v[e] = sum_{s < n} p[s * stride + e] (e < 8; p and stride 16-B aligned) in split order, the 16-B
+// loads of 8 splits issued together (clamped): split-K reduces over 2-3 splits otherwise ran a
+// remainder loop that waited for each split's loads before the next.
+__device__ __forceinline__ void sum_rows8(const float* __restrict__ p, int n, size_t stride, float (&v)[8]) {
+#pragma unroll
+  for (int e = 0; e < 8; ++e) v[e] = 0.f;
+  for (int s0 = 0; s0 < n; s0 += 8) {
+    f32x4_t a[8], b[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float* r = p + (size_t)min(s0 + j, n - 1) * stride;
+      a[j] = *(const f32x4_t*)r;
+      b[j] = *(const f32x4_t*)(r + 4);
+    }
+    // past n: + 0.f, an exact identity here (the sums start at +0 and never become -0), so the adds
+    // are unconditional and no load is sunk into a branch
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const bool in = s0 + j < n;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        v[e] += in ? a[j][e] : 0.f;
+        v[4 + e] += in ? b[j][e] : 0.f;
+      }
+    }
+  }
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

@@ -420,26 +420,12 @@ gemm_splitk_reduce(const float* __restrict__ ws, int splits, int M, int N, int e
       const int grp = oc / 16, within = oc % 16;
       const int gc = grp * 32 + within;
       float g[8], u[8];
-#pragma unroll
-      for (int e = 0; e < 8; ++e) { g[e] = 0.f; u[e] = 0.f; }
-#pragma unroll 4
-      for (int s = 0; s < splits; ++s) {
-        const float* row = ws + ((size_t)s * M + m) * N;
-#pragma unroll
-        for (int e = 0; e < 8; ++e) { g[e] += row[gc + e]; u[e] += row[gc + 16 + e]; }
-      }
+      sum_rows8(ws + (size_t)m * N + gc, splits, (size_t)M * N, g);
+      sum_rows8(ws + (size_t)m * N + gc + 16, splits, (size_t)M * N, u);
 #pragma unroll
       for (int e = 0; e < 8; ++e) v[e] = silu(g[e] * inv) * (u[e] * inv);
     } else {
-#pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] = 0.f;
-#pragma unroll 8
-      for (int s = 0; s < splits; ++s) {
-        const float* row = ws + ((size_t)s * M + m) * N + oc;
-        f32x4_t a = *(const f32x4_t*)row, b = *(const f32x4_t*)(row + 4);
-        v[0] += a[0]; v[1] += a[1]; v[2] += a[2]; v[3] += a[3];
-        v[4] += b[0]; v[5] += b[1]; v[6] += b[2]; v[7] += b[3];
-      }
+      sum_rows8(ws + (size_t)m * N + oc, splits, (size_t)M * N, v);
 #pragma unroll
       for (int e = 0; e < 8; ++e) v[e] *= inv;
       if (bias) {
@@ -898,15 +884,7 @@ splitk_reduce_resid_rmsnorm(const float* __restrict__ ws, int splits, int M, int
     const int c = threadIdx.x + 256 * i;
     if (c >= nch) continue;
     const int oc = c * 8;
-#pragma unroll
-    for (int e = 0; e < 8; ++e) v[i][e] = 0.f;
-#pragma unroll 8
-    for (int sp = 0; sp < splits; ++sp) {  // unrolled: 8 splits' loads in flight, not one at a time
-      const float* row = ws + ((size_t)sp * M + m) * N + oc;
-      const f32x4_t a = *(const f32x4_t*)row, b = *(const f32x4_t*)(row + 4);
-      v[i][0] += a[0]; v[i][1] += a[1]; v[i][2] += a[2]; v[i][3] += a[3];
-      v[i][4] += b[0]; v[i][5] += b[1]; v[i][6] += b[2]; v[i][7] += b[3];
-    }
+    sum_rows8(ws + (size_t)m * N + oc, splits, (size_t)M * N, v[i]);  // 8 splits' loads in flight
     const u32x4_t r = *(const u32x4_t*)(resid + (size_t)m * ldr + oc);
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
@@ -974,15 +952,7 @@ splitk_reduce_resid_ssq(const float* __restrict__ ws, int splits, int M, int N, 
   const int m = blockIdx.y, lane = threadIdx.x;
   const int oc = blockIdx.x * 512 + lane * 8;
   float v[8];
-#pragma unroll
-  for (int e = 0; e < 8; ++e) v[e] = 0.f;
-#pragma unroll 8
-  for (int sp = 0; sp < splits; ++sp) {
-    const float* row = ws + ((size_t)sp * M + m) * N + oc;
-    const f32x4_t a = *(const f32x4_t*)row, b = *(const f32x4_t*)(row + 4);
-    v[0] += a[0]; v[1] += a[1]; v[2] += a[2]; v[3] += a[3];
-    v[4] += b[0]; v[5] += b[1]; v[6] += b[2]; v[7] += b[3];
-  }
+  sum_rows8(ws + (size_t)m * N + oc, splits, (size_t)M * N, v);
   const u32x4_t r = *(const u32x4_t*)(resid + (size_t)m * ldr + oc);
   u32x4_t o;
   float sq = 0.f;
