@@ -1454,6 +1454,10 @@ DA_EXPORT void da_set_decode_pft(int v) { g_dec_pft = v; }
 // ... and with 8 waves per workgroup (VAR bit 5) when B * Hkv <= this (0 = never; A/B)
 static int g_dec_w8 = 0;  // measured 2x slower (profiles/r4/rejected_r4.txt): A/B only
 DA_EXPORT void da_set_decode_w8(int v) { g_dec_w8 = v; }
+// ... which 8-wave variant: 0 = two tiles in flight per wave (VAR 39: 256 VGPRs, spills), 1 = one
+// tile per wave, no prefetch (VAR 35: the 8 waves hold a split's tiles at once without spilling)
+static int g_dec_w8_var = 0;
+DA_EXPORT void da_set_decode_w8_var(int v) { g_dec_w8_var = v; }
 // Timeline probe (bench/decode_trace.py): non-null -> the MHA D=96 prefetch variant writes 8 wall-clock
 // stamps per workgroup here ([B][Hkv][nsplit][8]: start, prologue done, first tile done, tiles done,
 // partial stored, finished, last-split flag, CU id).
@@ -1479,8 +1483,12 @@ static int launch_decode(int G, dim3 grid, hipStream_t s, const bf16_t* q, int l
     if (g_dec_pft && (int)(grid.y * grid.z) <= g_dec_pft && g_dec_qfirst)
       return launch_decode_v<D, 23>(G, grid, s, q, ldq, kc, vc, lens, slot, pre, H, Hkv, max_seq, chunk, nsplit, sl2e, po, pm, pl, out, ldo, cnt, rope);
     if (g_dec_w8 && g_dec_pft && (int)(grid.y * grid.z) <= g_dec_w8) {  // MHA only (G = 1: LDS)
-      decode_attn_kernel<D, 1, 39><<<grid, 512, 0, s>>>(q, ldq, kc, vc, lens, slot, pre, H, Hkv, max_seq, chunk, nsplit,
-                                                         sl2e, po, pm, pl, out, ldo, cnt, rope);
+      if (g_dec_w8_var == 1)
+        decode_attn_kernel<D, 1, 35><<<grid, 512, 0, s>>>(q, ldq, kc, vc, lens, slot, pre, H, Hkv, max_seq, chunk,
+                                                           nsplit, sl2e, po, pm, pl, out, ldo, cnt, rope);
+      else
+        decode_attn_kernel<D, 1, 39><<<grid, 512, 0, s>>>(q, ldq, kc, vc, lens, slot, pre, H, Hkv, max_seq, chunk,
+                                                           nsplit, sl2e, po, pm, pl, out, ldo, cnt, rope);
       return (int)hipGetLastError();
     }
     if (g_dec_pft && (int)(grid.y * grid.z) <= g_dec_pft)  // few (row, kv head) pairs: latency-bound

@@ -82,6 +82,7 @@ _SIGS = {
     "da_set_gemv_ks": [c_int],
     "da_set_decode_pft": [c_int],
     "da_set_decode_w8": [c_int],
+    "da_set_decode_w8_var": [c_int],
     "da_set_gemm8p_group": [c_int],
     "da_set_gemm8p_bm_rule": [c_int],
     "da_set_omerge_shape": [c_int],
