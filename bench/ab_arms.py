@@ -32,7 +32,7 @@ ENV_SETTERS = {
     "DA_FLASH_PIPE": "da_set_flash_pipe",    # software-pipelined flash prefill on / off / auto
     "DA_FLASH_QH": "da_set_flash_qh",        # flash queries per wave: 1 = 32, 2 = 64
     "DA_FLASH_WAVES": "da_set_flash_waves",  # flash waves per workgroup
-    "DA_FLASH_REV": "da_set_flash_rev",      # causal flash longest-first dispatch
+    "DA_FLASH_REV": "da_set_flash_rev",      # flash dispatch: bit 0 causal longest-first, bit 1 XCD-grouped
     "DA_GEMV_U": "da_set_gemv_u",            # batch-1 GEMV K-blocks in flight per row
     "DA_GEMV_KS": "da_set_gemv_ks",          # batch-1 GEMV waves per long row
     "DA_DECODE_PFT": "da_set_decode_pft",    # MHA decode next-tile prefetch threshold

@@ -52,8 +52,34 @@ struct FaPrefix {
   const bf16_t* v;
   long long hstride;
   int len;
-  int rev;  // causal: dispatch query blocks longest-first (set by the launcher)
+  int rev;  // dispatch order (set by the launcher): bit 0 causal longest-first, bit 1 XCD-grouped
 };
+
+// The (query block, head, sequence) a flash workgroup works on, from its place in the dispatch
+// order. rev bit 0 (causal): the longest query blocks (most keys) first, so the kernel's tail is
+// made of short blocks (longest-processing-time-first packing). rev bit 1: the query blocks of one
+// (sequence, kv head) pair all run on one XCD. Workgroups are dealt round-robin over the 8 XCDs
+// (linear ids g and g + 8 share one: observed dispatch, relied on for speed only), and every block
+// of a pair re-reads that pair's K / V rows; grid order put a pair's blocks on all 8 XCDs, so each
+// XCD's L2 fetched the same rows. Grouped, the pair's rows are fetched into one L2 and re-read
+// there (pair-major per XCD: a few pairs' rows live at a time).
+struct FaBlock {
+  int qb, h, b;
+};
+__device__ __forceinline__ FaBlock fa_block(int rev, int causal, int G) {
+  const int X = gridDim.x, Y = gridDim.y, Z = gridDim.z;
+  const bool lpt = causal && (rev & 1);
+  if ((rev & 2) && G >= 1 && Y % G == 0 && ((Y / G) * Z) % 8 == 0) {
+    const int g = blockIdx.x + X * (blockIdx.y + Y * blockIdx.z);
+    const int xcd = g & 7, s = g >> 3;
+    const int per = X * G;                         // workgroups of one (sequence, kv head) pair
+    const int pair = (s / per) * 8 + xcd, r = s % per;
+    const int qi = r / G, gh = r % G;               // all G heads' longest blocks first
+    const int hkv = Y / G;
+    return FaBlock{lpt ? X - 1 - qi : qi, (pair % hkv) * G + gh, pair / hkv};
+  }
+  return FaBlock{lpt ? X - 1 - (int)blockIdx.x : (int)blockIdx.x, (int)blockIdx.y, (int)blockIdx.z};
+}
 
 // QH = 32-query halves per wave. QH = 2: each K fragment read from LDS feeds the S MFMAs of both
 // halves and each transposed V fragment the O MFMAs of both, so LDS read bytes per FLOP halve (at
@@ -69,11 +95,9 @@ flash_attn_v2_kernel(const bf16_t* __restrict__ q, const bf16_t* __restrict__ k,
   constexpr bool EVEN = (KT * CPR) % NT == 0;  // every thread stages exactly LPT chunks
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
-  const int b = blockIdx.z, h = blockIdx.y;
+  const FaBlock fb = fa_block(pre.rev, causal, H / Hkv);  // dispatch order: see fa_block
+  const int b = fb.b, h = fb.h, qb = fb.qb;
   const int s0 = cu[b], L = cu[b + 1] - s0;
-  // causal: the longest query blocks (most keys) are dispatched first, so the kernel's tail is
-  // made of short blocks (longest-processing-time-first packing); pre.rev = 0 keeps grid order
-  const int qb = (causal && pre.rev) ? (int)gridDim.x - 1 - (int)blockIdx.x : (int)blockIdx.x;
   const int q0 = qb * C::QB;
   if (q0 >= L) return;
   const int hk = h / (H / Hkv);
@@ -381,9 +405,9 @@ flash_attn_pipe_kernel(const bf16_t* __restrict__ q, const bf16_t* __restrict__ 
   constexpr int KSTR = DMA ? D * 2 : C::KSTR, KBUF = KT * KSTR, TBUF = KBUF + C::VBUF;
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
-  const int b = blockIdx.z, h = blockIdx.y;
+  const FaBlock fb = fa_block(pre.rev, causal, H / Hkv);  // dispatch order: see fa_block
+  const int b = fb.b, h = fb.h, qb = fb.qb;
   const int s0 = cu[b], L = cu[b + 1] - s0;
-  const int qb = (causal && pre.rev) ? (int)gridDim.x - 1 - (int)blockIdx.x : (int)blockIdx.x;
   const int q0 = qb * C::QB;
   if (q0 >= L) return;
   const int hk = h / (H / Hkv);
@@ -1627,8 +1651,8 @@ DA_EXPORT int da_decode_attn_qkvparts(const void* qkv_ws, int splits, int N, con
 static int g_fa_waves = 0;
 DA_EXPORT void da_set_flash_waves(int nw) { g_fa_waves = nw; }
 // causal flash: longest query blocks first (1, default) or grid order (0); A/B runs
-static int g_fa_rev = 1;
-DA_EXPORT void da_set_flash_rev(int v) { g_fa_rev = v ? 1 : 0; }
+static int g_fa_rev = 3;  // bit 0: causal longest-first; bit 1: XCD-grouped pairs (fa_block)
+DA_EXPORT void da_set_flash_rev(int v) { g_fa_rev = v & 3; }
 
 // fp16 (the encoder's DTYPE=fp16): bidirectional or causal, no shared prefix, 4 waves x 32 queries
 DA_EXPORT int da_flash_attn_f16(const void* q, const void* k, const void* v, int ldq, int ldk, int ldv,
