@@ -109,8 +109,17 @@ gemm_dk_kernel(DkArgs p) {
     __shared__ f32x4_t sq4[PL][RQ];
     const int rq = tid % RQ, pl = tid / RQ;
     f32x4_t a4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll 4
-    for (int q = pl; q < p.ssq_parts; q += PL) a4 += *(const f32x4_t*)(p.ssq_in + (size_t)q * 64 + m0 + 4 * rq);
+    // 8 parts' loads issued before their adds (clamped; + 0 past the end is exact: sums of squares
+    // are never -0): with ~192 parts on 64 part lanes, `#pragma unroll 4` left a 3-trip remainder
+    // loop that waited for each load in turn
+    for (int q0 = pl; q0 < p.ssq_parts; q0 += 8 * PL) {
+      f32x4_t v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        v[j] = *(const f32x4_t*)(p.ssq_in + (size_t)min(q0 + j * PL, p.ssq_parts - 1) * 64 + m0 + 4 * rq);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) a4 += (q0 + j * PL < p.ssq_parts) ? v[j] : f32x4_t{0.f, 0.f, 0.f, 0.f};
+    }
     sq4[pl][rq] = a4;
     __syncthreads();
     if (tid < BM) {

@@ -251,8 +251,21 @@ __global__ void embed_kernel(const int* __restrict__ ids, const bf16_t* __restri
                              bf16_t* __restrict__ y, int D) {
   const int row = blockIdx.x;
   const size_t id = (size_t)ids[row];
-  for (int c = threadIdx.x; c < D / 8; c += blockDim.x)
-    *(u32x4_t*)(y + (size_t)row * D + c * 8) = *(const u32x4_t*)(table + id * D + c * 8);
+  // up to 4 chunks per thread loaded before any store (D = 3072 on 256 threads was a load, a wait,
+  // a store and a second load: two table round trips in a row at the head of every decode step)
+  constexpr int U = 4;
+  const int nch = D / 8;
+  for (int c0 = threadIdx.x; c0 < nch; c0 += U * blockDim.x) {
+    u32x4_t v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      v[u] = *(const u32x4_t*)(table + id * D + (size_t)min(c0 + u * (int)blockDim.x, nch - 1) * 8);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int c = c0 + u * (int)blockDim.x;
+      if (c < nch) *(u32x4_t*)(y + (size_t)row * D + c * 8) = v[u];
+    }
+  }
 }
 
 // Pooling + L2 normalisation (fp32 accumulate; zero vector left unchanged like the reference's

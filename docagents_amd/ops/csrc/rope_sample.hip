@@ -80,6 +80,29 @@ struct SampleArgs {
   int* hist; const int* start; int hist_ld; int eos0, eos1, eos2, eos3;
 };
 
+// The sampler's per-row bookkeeping for the chosen token fi (logprob lp), one thread: token /
+// logprob out, confidence running sums, generated-token history, position / length advance, stop
+// on EOS or a full history. Every operand is read up front: as `x[b] += ...` statements behind the
+// active check they were a chain of dependent memory round trips at the end of every decode step.
+__device__ __forceinline__ void sample_bookkeep(const SampleArgs& a, int b, int fi, float lp) {
+  const int act = a.active ? a.active[b] : 1;
+  const float c0 = a.conf ? a.conf[2 * b] : 0.f, c1 = a.conf ? a.conf[2 * b + 1] : 0.f;
+  const int pos = a.pos ? a.pos[b] : 0, st = a.hist ? a.start[b] : 0, len = a.lens ? a.lens[b] : 0;
+  if (act == 0) return;
+  a.out_tok[b] = fi;
+  if (a.out_lp) a.out_lp[b] = lp;
+  if (a.conf) { a.conf[2 * b] = c0 + __expf(lp); a.conf[2 * b + 1] = c1 + 1.f; }
+  bool stop = (fi == a.eos0 || fi == a.eos1 || fi == a.eos2 || fi == a.eos3);
+  if (a.hist) {
+    const int gi = pos - st;
+    if (gi >= 0 && gi < a.hist_ld) a.hist[(size_t)b * a.hist_ld + gi] = fi;
+    if (gi + 1 >= a.hist_ld) stop = true;
+  }
+  if (a.pos) a.pos[b] = pos + 1;
+  if (a.lens) a.lens[b] = len + 1;
+  if (stop && a.active) a.active[b] = 0;
+}
+
 __global__ void __launch_bounds__(1024)
 sample_kernel(SampleArgs a) {
   __shared__ float redf[16];
@@ -130,22 +153,7 @@ sample_kernel(SampleArgs a) {
     int fi = besti[0];
     for (int i = 1; i < nw; ++i)
       if (bestv[i] > fv || (bestv[i] == fv && besti[i] < fi)) { fv = bestv[i]; fi = besti[i]; }
-    const float lp = bf2f(row[fi]) - gmax - __logf(s);
-    const bool on = a.active ? a.active[b] != 0 : true;
-    if (on) {
-      a.out_tok[b] = fi;
-      if (a.out_lp) a.out_lp[b] = lp;
-      if (a.conf) { a.conf[2 * b] += __expf(lp); a.conf[2 * b + 1] += 1.f; }
-      bool stop = (fi == a.eos0 || fi == a.eos1 || fi == a.eos2 || fi == a.eos3);
-      if (a.hist) {
-        const int gi = a.pos[b] - a.start[b];
-        if (gi >= 0 && gi < a.hist_ld) a.hist[(size_t)b * a.hist_ld + gi] = fi;
-        if (gi + 1 >= a.hist_ld) stop = true;
-      }
-      if (a.pos) a.pos[b] += 1;
-      if (a.lens) a.lens[b] += 1;
-      if (stop && a.active) a.active[b] = 0;
-    }
+    sample_bookkeep(a, b, fi, bf2f(row[fi]) - gmax - __logf(s));
   }
 }
 
@@ -297,21 +305,7 @@ sample_finalize_kernel(const float* __restrict__ gathered, int B, int ranks, Sam
   for (int r = lane; r < ranks; r += 64) sp += g[r * 8 + 3] * __expf(g[r * 8 + 2] - gmax);
   const float s = wave_sum(sp);
   if (lane != 0) return;
-  const float lp = xb - gmax - __logf(s);
-  const bool on = a.active ? a.active[b] != 0 : true;
-  if (!on) return;
-  a.out_tok[b] = fi;
-  if (a.out_lp) a.out_lp[b] = lp;
-  if (a.conf) { a.conf[2 * b] += __expf(lp); a.conf[2 * b + 1] += 1.f; }
-  bool stop = (fi == a.eos0 || fi == a.eos1 || fi == a.eos2 || fi == a.eos3);
-  if (a.hist) {
-    const int gi = a.pos[b] - a.start[b];
-    if (gi >= 0 && gi < a.hist_ld) a.hist[(size_t)b * a.hist_ld + gi] = fi;
-    if (gi + 1 >= a.hist_ld) stop = true;
-  }
-  if (a.pos) a.pos[b] += 1;
-  if (a.lens) a.lens[b] += 1;
-  if (stop && a.active) a.active[b] = 0;
+  sample_bookkeep(a, b, fi, xb - gmax - __logf(s));
 }
 
 DA_EXPORT int da_sample_partial(const void* logits, int B, int V, int ld, int v0, float temperature, unsigned seed,
