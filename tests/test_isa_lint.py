@@ -24,7 +24,9 @@ HOT_NO_SCRATCH = {  # mangled-name prefixes of the kernels the flagship bench ru
     "gemm_dk.hip": ["_Z14gemm_dk_kernel"],
 }
 NO_SERIAL_LOAD_LOOPS = {"gemm.hip": ["_Z18gemm_splitk_reduce", "_Z23splitk_reduce_resid_ssq",
-                                     "_Z27splitk_reduce_resid_rmsnorm"]}
+                                     "_Z27splitk_reduce_resid_rmsnorm"],
+                        "gemm_dk.hip": ["_Z14gemm_dk_kernel"],  # the deferred-norm sums
+                        "norm.hip": ["_Z12embed_kernel"]}       # the decode step's first launch
 
 
 def _asm(name, tmp_path):
