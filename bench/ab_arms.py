@@ -37,6 +37,7 @@ ENV_SETTERS = {
     "DA_GEMV_KS": "da_set_gemv_ks",          # batch-1 GEMV waves per long row
     "DA_DECODE_PFT": "da_set_decode_pft",    # MHA decode next-tile prefetch threshold
     "DA_DECODE_W8": "da_set_decode_w8",      # ... with 8 waves per workgroup up to this many (row, kv head) pairs
+    "DA_DECODE_W8_VAR": "da_set_decode_w8_var",  # ... 0: two tiles per wave (spills), 1: one tile per wave
     "DA_GEMM8P_GROUP": "da_set_gemm8p_group",  # prefill GEMM tile-order band height (0 = auto)
     "DA_GEMM8P_BM_RULE": "da_set_gemm8p_bm_rule",  # prefill row-tile height: 1 = fewest waves, 0 = round-3 rule
     "DA_OMERGE_SHAPE": "da_set_omerge_shape",  # merged batch-1 O GEMV: waves per workgroup * 10 + rows per wave
