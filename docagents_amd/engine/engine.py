@@ -247,34 +247,95 @@ class Engine:
                     owner.append((i, True))
         return windows, owner
 
-    def summary_reduce_prompts(self, partial: dict[int, list[str]], max_new: int | None = None):
-        """Reduce step: one prompt over the joined window summaries of each long text."""
-        head, tail, budget = self._summary_frame(max_new or self.summary_max_new)
-        keys = list(partial)
-        ids = self._ids_many(["\n".join(partial[i]) for i in keys])
-        return [(i, head + x[:budget] + tail) for i, x in zip(keys, ids)]
+    def _reduce_groups(self, parts: list[str], budget: int) -> list[list[int]]:
+        """One reduce level of one text: the summaries ``parts`` (window order), each tokenized on its
+        own, packed in order into groups whose joined tokens (newline separated) fit ``budget``.
+        Nothing is cut: a summary longer than half the budget is split into consecutive pieces of at
+        most half the budget, so any two neighbours fit one group, every group but the last holds at
+        least two pieces, and each level at least halves the pieces. Returns the groups' joined ids."""
+        nl = self._cached_ids("\n")
+        cap = (budget - len(nl)) // 2
+        if cap < 1:
+            raise ValueError(f"summary reduce: context budget {budget} too small to join two summaries")
+        pieces: list[list[int]] = []
+        for ids in self._ids_many(list(parts)):
+            if not ids:
+                continue
+            pieces.extend(ids[s:s + cap] for s in range(0, len(ids), cap))
+        groups: list[list[int]] = []
+        cur: list[int] = []
+        for pc in pieces:
+            if cur and len(cur) + len(nl) + len(pc) > budget:
+                groups.append(cur)
+                cur = []
+            cur = cur + nl + pc if cur else list(pc)
+        if cur or not groups:
+            groups.append(cur)
+        return groups
 
-    def summarize_many(self, texts: list[str], max_new: int | None = None) -> list[tuple[str, list[str]]]:
-        """Summarize each text; texts longer than the decoder context are summarized map-reduce:
-        window summaries (batched) then one reduce summary over them."""
+    def summary_plan(self, texts: list[str], max_new: int | None = None):
+        """Map-reduce summarization as a plan: a generator that yields lists of
+        prompts (token ids) and is sent back their generated texts in the same order; its return
+        value is the final raw summary of each text. The reference sends the whole document to a
+        128k-context model in one request (cmd/analysis/main.go:70-71, internal/llm/openai.go:40-62);
+        here a text longer than the decoder context is summarized per context-sized window (map),
+        then its window summaries are reduced LEVEL BY LEVEL: each level packs the previous level's
+        summaries, in order, into as few context-sized prompts as hold them all
+        (``_reduce_groups``), until one prompt holds them — every window reaches the final summary,
+        nothing is truncated. ``summarize_many`` drives it with the wave generator, the engine
+        server with the continuous scheduler."""
         max_new = max_new or self.summary_max_new
+        head, tail, budget = self._summary_frame(max_new)
         windows, owner = self.summary_windows(texts, max_new)
-        with self.lock:
-            res = self.gen.generate(windows, max_new)
-        partial: dict[int, list[str]] = {}
+        outs = yield windows
         final: dict[int, str] = {}
-        for (i, is_part), txt in zip(owner, self.chat.decode_many([r.tokens for r in res])):
+        pending: dict[int, list[str]] = {}
+        for (i, is_part), txt in zip(owner, outs):
             if is_part:
-                partial.setdefault(i, []).append(txt)
+                pending.setdefault(i, []).append(txt)
             else:
                 final[i] = txt
-        if partial:
-            red = self.summary_reduce_prompts(partial, max_new)
+        levels = 0
+        while pending:
+            levels += 1
+            if levels > 64:
+                raise RuntimeError("summary reduce did not converge")
+            prompts, pown = [], []  # pown[j] = (text index, final level?)
+            for i, parts in pending.items():
+                groups = self._reduce_groups(parts, budget)
+                for g in groups:
+                    prompts.append(head + g + tail)
+                    pown.append((i, len(groups) == 1))
+            outs = yield prompts
+            nxt: dict[int, list[str]] = {}
+            for (i, last), txt in zip(pown, outs):
+                if last:
+                    final[i] = txt
+                else:
+                    nxt.setdefault(i, []).append(txt)
+            pending = nxt
+        self.stats["summary_reduce_levels_max"] = max(self.stats.get("summary_reduce_levels_max", 0), levels)
+        return [final[i] for i in range(len(texts))]
+
+    @staticmethod
+    def summary_step(plan, outs=None):
+        """Advance a ``summary_plan``: ("prompts", [ids]) to generate next, or ("done", [text]).
+        (A plain call, so it can run on an executor thread: StopIteration must not cross a future.)"""
+        try:
+            return "prompts", (next(plan) if outs is None else plan.send(outs))
+        except StopIteration as e:
+            return "done", e.value
+
+    def summarize_many(self, texts: list[str], max_new: int | None = None) -> list[tuple[str, list[str]]]:
+        """Summarize each text (map-reduce over the decoder context for long ones: ``summary_plan``)."""
+        max_new = max_new or self.summary_max_new
+        plan = self.summary_plan(texts, max_new)
+        kind, val = self.summary_step(plan)
+        while kind == "prompts":
             with self.lock:
-                rres = self.gen.generate([p for _, p in red], max_new)
-            for (i, _), txt in zip(red, self.chat.decode_many([r.tokens for r in rres])):
-                final[i] = txt
-        return [extract_summary(final[i]) for i in range(len(texts))]
+                res = self.gen.generate(val, max_new)
+            kind, val = self.summary_step(plan, self.chat.decode_many([r.tokens for r in res]))
+        return [extract_summary(t) for t in val]
 
     # ------------------------------------------------------------------ introspection
     def describe(self) -> dict:

@@ -73,6 +73,15 @@ class Generator:
                        8 * max_batch * max(c.ffn * 2 // model.tp.size, c.vocab) * 4)
             kernels.reserve_workspace(need, model.device)
 
+    def close(self):
+        """Give this generator's KV slots (the padded rows' dummy slot, a kept prompt-head slot) back
+        to the model's cache and drop its decode states and graphs: several generators may take
+        turns on one model's cache (bench.py's TP decode arms)."""
+        held = [self.dummy_slot] + ([self._head_slot] if getattr(self, "_head_slot", None) is not None else [])
+        self.cache.release(held)
+        self._head_slot, self.head, self.dummy_slot = None, None, None
+        self.states.clear()
+
     # --------------------------------------------------------------------------------
     def _persistent_head_slot(self, held: int):
         """The KV slot that keeps the last wave's shared prompt head. Taken once, and only when it
@@ -211,7 +220,7 @@ class Generator:
             st.pos.copy_(ht[0]); st.lens.copy_(ht[1]); st.slot.copy_(ht[2]); st.active.copy_(ht[3])
             st.start.copy_(ht[4])
             st.tokens.zero_(); st.hist.fill_(-1); st.conf.zero_()
-            if self.sync_phases:
+            if self.sync_phases and self.is_cuda:
                 torch.cuda.synchronize(dev)
             t_pf = time.perf_counter()
             h = self.head if self.share_prefix else None
@@ -255,7 +264,8 @@ class Generator:
             if B > n:
                 st.pos[n:].zero_(); st.lens[n:].fill_(1)
             if self.sync_phases:
-                torch.cuda.synchronize(dev)
+                if self.is_cuda:
+                    torch.cuda.synchronize(dev)
                 self.stats["prefill_wall_s"] = self.stats.get("prefill_wall_s", 0.0) + time.perf_counter() - t_pf
         except BaseException:
             self.cache.release(slots)

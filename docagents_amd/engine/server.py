@@ -356,21 +356,13 @@ class EngineServer:
         Tokenization runs on a CPU thread, not on the GPU thread."""
         e = self.group.engine
         loop = asyncio.get_running_loop()
-        windows, owner = await loop.run_in_executor(self.cpu, e.summary_windows, texts)
-        res = await self._cb_submit([{"ids": w, "max_new": e.summary_max_new} for w in windows])
-        partial, final = {}, {}
-        for (i, is_part), (txt, _) in zip(owner, res):
-            if is_part:
-                partial.setdefault(i, []).append(txt)
-            else:
-                final[i] = txt
-        if partial:
-            red = await loop.run_in_executor(self.cpu, e.summary_reduce_prompts, partial)
-            rres = await self._cb_submit([{"ids": p, "max_new": e.summary_max_new} for _, p in red])
-            for (i, _), (txt, _) in zip(red, rres):
-                final[i] = txt
+        plan = e.summary_plan(texts, e.summary_max_new)
+        kind, val = await loop.run_in_executor(self.cpu, e.summary_step, plan)
+        while kind == "prompts":  # map windows, then every reduce level (engine.summary_plan)
+            res = await self._cb_submit([{"ids": p, "max_new": e.summary_max_new} for p in val])
+            kind, val = await loop.run_in_executor(self.cpu, e.summary_step, plan, [t for t, _ in res])
         metrics.ENGINE_ITEMS.labels("summarize").inc(len(texts))
-        return [extract_summary(final[i]) for i in range(len(texts))]
+        return [extract_summary(t) for t in val]
 
     def _fast_embed(self, texts, preprocess: bool) -> np.ndarray:
         """Runs on the fast-lane thread: the encoder on a high-priority stream with its own kernel

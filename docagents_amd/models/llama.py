@@ -60,8 +60,9 @@ _QKV_FOLD = False
 class TPContext:
     """Tensor-parallel process group (identity when size == 1)."""
 
-    def __init__(self, rank: int = 0, size: int = 1, group=None):
+    def __init__(self, rank: int = 0, size: int = 1, group=None, xgmi: bool = True):
         self.rank, self.size, self.group = rank, size, group
+        self.use_xgmi = xgmi  # False: every all-reduce / gather through torch.distributed (RCCL)
         self.xgmi = None  # XgmiAllReduce once setup_device() ran on a GPU
         self.xgmi_norm = None  # a second communicator for the fused all-reduce + RMSNorm (one row width)
 
@@ -69,7 +70,7 @@ class TPContext:
         """Collective (every TP rank): map the peers' all-reduce buffers over xGMI (GPU only).
         Decode-sized row-parallel outputs then take the one-/two-shot IPC kernel; anything else
         (and every CPU run) uses torch.distributed (RCCL / gloo)."""
-        if self.size > 1 and device.type == "cuda" and self.xgmi is None:
+        if self.size > 1 and device.type == "cuda" and self.xgmi is None and self.use_xgmi:
             from ..parallel.xgmi_allreduce import XgmiAllReduce
             self.xgmi = XgmiAllReduce.create(self.group, device)
             if self.xgmi is not None:

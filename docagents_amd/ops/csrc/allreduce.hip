@@ -258,8 +258,13 @@ DA_EXPORT int da_ar_signal_bytes() { return (int)sizeof(ArSignal); }
 DA_EXPORT int da_ar_max_blocks() { return AR_MAX_BLOCKS; }
 DA_EXPORT int da_ar_block_vecs() { return AR_TPB; }
 
-DA_EXPORT int da_ar_malloc(long long bytes, void** out) {
-  hipError_t e = hipMalloc(out, (size_t)bytes);
+// uncached != 0: hipDeviceMallocUncached (MTYPE UC). The signal block and the staging buffers are
+// written by one device and polled / read by its peers over xGMI; uncached pages keep a stale line
+// in any GPU's L2 from hiding a peer's flag or staged rows (coarse-grained hipMalloc memory gives no
+// such guarantee across devices; same-device IPC, as in the 1-GPU tests, could never show it).
+DA_EXPORT int da_ar_malloc(long long bytes, int uncached, void** out) {
+  hipError_t e = uncached ? hipExtMallocWithFlags(out, (size_t)bytes, hipDeviceMallocUncached)
+                          : hipMalloc(out, (size_t)bytes);
   if (e != hipSuccess) return (int)e;
   e = hipMemset(*out, 0, (size_t)bytes);
   if (e != hipSuccess) return (int)e;

@@ -1,0 +1,149 @@
+"""The multi-GPU mechanisms of the north star, timed (``bench.py`` at N > 1, after the headline).
+
+The headline (QA q/s with N data-parallel replicas) scales by replicas, as the reference does
+(docker-compose.yml:84-85,105-106), so on its own it says nothing about the fabric. These blocks
+time the collectives the north star names, each on all N ranks together:
+
+  rccl_search   C2 + C1 as RCCL collectives: ``ShardedIndex.search`` (all-gather of every rank's
+                query rows, local fused scan + filter + floor + top-k, ONE packed all-gather of the
+                per-shard top-k, topk_merge kernel) at B rows per rank, >= 20 timed calls; q/s over
+                the whole world, p50 / p90 ms per call, and the rows checked identical to the
+                serving plane's owner-routed answer for the same batch
+  tp_decode     the bench's decoder at TP = N over every rank (column / row-parallel layers,
+                vocab-parallel sampler): decode ms per step at batch 1 and batch B with the xGMI
+                IPC all-reduce (graph-replayed, as served) and with torch.distributed (RCCL on
+                GPUs) in its place, plus the per-decision agreement verdict of a TP = N decoder
+                with the unsharded one (parallel/tp_verify.py)
+  xgmi          the IPC all-reduce vs RCCL per call at 16 KB / 384 KB / 6 MB (xgmi_allreduce.py)
+
+Every block is collective: all ranks call it in the same order with the same shapes.
+"""
+from __future__ import annotations
+
+import statistics
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from .dist import all_reduce_max, barrier
+
+
+def _sync(dev):
+    if torch.device(dev).type == "cuda":
+        torch.cuda.synchronize(dev)
+
+
+def _pct(xs, q):
+    s = sorted(xs)
+    return s[min(len(s) - 1, int(round(q * (len(s) - 1))))]
+
+
+def rccl_search(shard, plane_search, embed, make_batch, k: int, min_sim: float, iters: int, ctrl, dev) -> dict:
+    """make_batch(i) -> (questions, this rank's per-row document filters). plane_search(qv, filters)
+    -> (scores, ids) through the serving plane. Returns the rccl_search block."""
+    W = shard.world
+    batches = []
+    for i in range(iters + 2):
+        qs, mine = make_batch(i)
+        qv = embed(qs)
+        every = [None] * W
+        dist.all_gather_object(every, mine, group=ctrl)
+        batches.append((qv, mine, [f for r in range(W) for f in every[r]]))
+    B = batches[0][0].shape[0]
+    # identity: the RCCL form and the plane's owner-routed form on the same batch
+    qv, mine, flt_all = batches[0]
+    s_p, id_p = plane_search(qv, mine)
+    s_r, id_r = shard.search(qv, k, min_sim, flt_all)
+    s_r, id_r = s_r.float().cpu().numpy(), id_r.cpu().numpy()
+    agree = int(sum(1 for b in range(B) if np.array_equal(id_r[b], id_p[b])))
+    close = bool(np.allclose(np.where(id_r >= 0, s_r, 0), np.where(id_p >= 0, s_p, 0), atol=1e-3))
+    shard.search(*batches[1][:1], k, min_sim, batches[1][2])  # warm
+    # throughput: back to back
+    _sync(dev); barrier()
+    t0 = time.perf_counter()
+    for qv, _, flt in batches[2:]:
+        shard.search(qv, k, min_sim, flt)
+    _sync(dev)
+    dt = all_reduce_max(time.perf_counter() - t0, dev)
+    # latency: one call at a time (every rank enters together: the call is collective)
+    lat = []
+    for qv, _, flt in batches[2:]:
+        _sync(dev)
+        t1 = time.perf_counter()
+        shard.search(qv, k, min_sim, flt)
+        _sync(dev)
+        lat.append(all_reduce_max(time.perf_counter() - t1, dev) * 1000)
+    return {"rows_per_rank": B, "iters": iters, "world": W, "qps": round(W * B * iters / dt, 1),
+            "ms_per_call_mean": round(dt / iters * 1000, 3), "p50_ms": round(statistics.median(lat), 3),
+            "p90_ms": round(_pct(lat, 0.9), 3), "rows_identical_to_plane": agree, "rows_checked": B,
+            "scores_close": close}
+
+
+def _round_up(x: int, m: int) -> int:
+    return -(-x // m) * m
+
+
+def tp_decode(dec_cfg, full_weights, rank: int, world: int, dev, prompts_by_b: dict, max_new: int,
+              rccl_graphs: bool = False, verdict: bool = True) -> dict:
+    """The decoder at TP = world over every rank, timed per decode step. prompts_by_b: {batch:
+    prompts} (the same on every rank). full_weights: the unsharded weights (identical on every rank:
+    seeded). Arms: the xGMI all-reduce graph-replayed (the served form) and eager, and
+    torch.distributed in its place (eager; graph-captured too when ``rccl_graphs``)."""
+    from ..engine.generator import Generator
+    from ..models.llama import LlamaDecoder, TPContext, shard_weights
+    backend = dist.get_backend()
+    tp = TPContext(rank, world, None)
+    model = LlamaDecoder(dec_cfg, dev, tp=tp, weights=shard_weights(dec_cfg, full_weights, rank, world))
+    maxB = max(prompts_by_b)
+    longest = max(len(p) for ps in prompts_by_b.values() for p in ps)
+    max_seq = min(dec_cfg.max_pos, _round_up(longest + max_new + 8, 256))
+    model.alloc_cache(maxB + 4, max_seq)
+    xg = (tp.xgmi, tp.xgmi_norm)
+    arms = []
+    if xg[0] is not None:
+        arms += [("xgmi_graph", True, True), ("xgmi_eager", True, False)]
+    arms.append((f"{'rccl' if backend == 'nccl' else backend}_eager", False, False))
+    if rccl_graphs and backend == "nccl":
+        arms.append(("rccl_graph", False, True))
+    out: dict = {"tp": world, "model": dec_cfg.name, "max_new_tokens": max_new,
+                 "prompt_tokens_mean": {str(b): round(float(np.mean([len(p) for p in ps])), 1)
+                                        for b, ps in prompts_by_b.items()},
+                 "xgmi_mapped": xg[0] is not None, "arms": {}}
+    for name, use_x, graphs in arms:
+        tp.xgmi, tp.xgmi_norm = xg if use_x else (None, None)
+        gen = Generator(model, max_batch=maxB, max_seq=max_seq, temperature=0.2, seed=0, use_graphs=graphs)
+        row = {"graphs": graphs}
+        try:
+            for b, prompts in sorted(prompts_by_b.items()):
+                gen.generate([p[:64] for p in prompts], max_new)  # warm: the decode graph of this bucket
+                gen.sync_phases = True
+                _sync(dev); barrier()
+                s0, n0, p0 = gen.stats["decode_s"], gen.stats["decode_steps"], gen.stats.get("prefill_wall_s", 0.0)
+                gen.generate(prompts, max_new)
+                gen.sync_phases = False
+                steps = max(1, gen.stats["decode_steps"] - n0)
+                row[f"b{b}_decode_ms_per_step"] = round(all_reduce_max((gen.stats["decode_s"] - s0) / steps, dev) * 1000, 3)
+                row[f"b{b}_prefill_ms"] = round(all_reduce_max(gen.stats["prefill_wall_s"] - p0, dev) * 1000, 2)
+        finally:
+            gen.close()
+        out["arms"][name] = row
+    tp.xgmi, tp.xgmi_norm = xg
+    if xg[0] is not None:
+        xg[0].check()
+        out["xgmi_calls"] = xg[0].calls + (xg[1].calls if xg[1] is not None else 0)
+        for c in xg:
+            if c is not None:
+                c.close()
+    del model
+    if verdict:
+        from .tp_verify import decision_verdict, verdict_ok
+        v = decision_verdict(rank, world, None, dev)
+        out["agreement"] = {"ok": verdict_ok(v), "arch": v["arch"], "decisions": v["decisions"],
+                            "checked": v["checked"], "checked_agree": v["checked_agree"],
+                            "prefix_ok": sum(v["prefix_ok"]), "prompts": len(v["prefix_ok"]),
+                            "max_logit_diff": round(v["max_logit_diff"], 5), "xgmi": v["xgmi"]}
+    if torch.device(dev).type == "cuda":
+        torch.cuda.empty_cache()
+    return out

@@ -6,8 +6,10 @@ xGMI link per neighbour; on a full-mesh MI355X node a one-shot kernel that reads
 buffers directly (IPC-mapped, 7 links concurrently) is latency-optimal for such messages, and a
 two-shot (reduce-scatter + all-gather through the same buffers) covers prefill-sized ones.
 
-Setup (once per communicator, NOT inside graph capture): every rank hipMallocs a staging buffer
-(2 x max_bytes, double-buffered by call parity) and a signal block, exports both with
+Setup (once per communicator, NOT inside graph capture): every rank allocates a staging buffer
+(2 x max_bytes, double-buffered by call parity) and a signal block in UNCACHED device memory
+(hipExtMallocWithFlags(..., hipDeviceMallocUncached): peers poll the flags and read the staged rows
+across devices, so no GPU may serve them from a stale L2 line), exports both with
 hipIpcGetMemHandle, exchanges the handles over the process group (all_gather_object), and opens
 the peers' handles. After that a call is one kernel launch with constant arguments, so it is
 captured into the decode HIP graph like any other kernel. Kernel: ops/csrc/allreduce.hip.
@@ -35,7 +37,7 @@ def _lib():
     L = K.lib()
     if not _BOUND:
         sigs = {
-            "da_ar_malloc": ([c_longlong, ctypes.POINTER(c_void_p)], c_int),
+            "da_ar_malloc": ([c_longlong, c_int, ctypes.POINTER(c_void_p)], c_int),
             "da_ar_free": ([c_void_p], c_int),
             "da_ar_ipc_handle": ([c_void_p, c_void_p], c_int),
             "da_ar_ipc_open": ([c_void_p, ctypes.POINTER(c_void_p)], c_int),
@@ -82,9 +84,9 @@ class XgmiAllReduce:
         self._opened: list[c_void_p] = []
         with torch.cuda.device(self.device):
             data, sig = c_void_p(), c_void_p()
-            _ok(L.da_ar_malloc(2 * self.max_bytes, byref(data)), "hipMalloc(staging)")
+            _ok(L.da_ar_malloc(2 * self.max_bytes, 1, byref(data)), "hipExtMallocWithFlags(staging, uncached)")
             self._own.append(data)
-            _ok(L.da_ar_malloc(L.da_ar_signal_bytes(), byref(sig)), "hipMalloc(signal)")
+            _ok(L.da_ar_malloc(L.da_ar_signal_bytes(), 1, byref(sig)), "hipExtMallocWithFlags(signal, uncached)")
             self._own.append(sig)
             hd, hs = ctypes.create_string_buffer(hb), ctypes.create_string_buffer(hb)
             _ok(L.da_ar_ipc_handle(data, hd), "hipIpcGetMemHandle(staging)")
@@ -191,12 +193,17 @@ class XgmiAllReduce:
         self._opened, self._own = [], []
 
 
-def verify_and_time(group=None, device=None, iters: int = 50) -> dict:
+def _size_name(nb: int) -> str:
+    return f"{nb >> 20}MB" if nb >= 1 << 20 and nb % (1 << 20) == 0 else f"{nb >> 10}KB"
+
+
+def verify_and_time(group=None, device=None, iters: int = 50,
+                    sizes: tuple = (16 << 10, 384 << 10, 6 << 20)) -> dict:
     """Cross-device evidence for C3 (run by bench.py on multi-GPU nodes, outside the timed steps):
     the IPC all-reduce against the exact rank-order fp32 sum for decode- and prefill-sized bf16
     messages (one-shot and two-shot), the fused all-reduce + RMSNorm against all-reduce followed by
-    the rmsnorm kernel (bit identity), and the time per call of a batch-64 Phi-3 row block
-    (64 x 3072 bf16) through this kernel vs RCCL ``all_reduce`` on the same group."""
+    the rmsnorm kernel (bit identity), and the time per call at each of ``sizes`` (bytes of bf16)
+    through this kernel vs RCCL ``all_reduce`` on the same group (RCCL only on the nccl backend)."""
     dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
     world, rank = dist.get_world_size(group), dist.get_rank(group)
     ar = XgmiAllReduce(group, dev, max_bytes=16 << 20)
@@ -225,9 +232,9 @@ def verify_and_time(group=None, device=None, iters: int = 50) -> dict:
     same = bool(torch.equal(x1, x2) and torch.equal(h1, h2))
     res["fused_norm_bit_identical"] = same
     res["ok"] &= same
-    # time per call, batch-64 row block: this kernel vs RCCL on the same group
-    x = torch.randn(64, 3072, device=dev).bfloat16()
-
+    # time per call: this kernel vs RCCL on the same group, at the TP message sizes (16 KB: a
+    # batch-1 Llama-3-70B row; 384 KB: a batch-64 Phi-3 row block, 64 x 3072; 6 MB: a two-shot
+    # prefill-sized block)
     def timed(fn):
         for _ in range(5):
             fn()
@@ -241,9 +248,15 @@ def verify_and_time(group=None, device=None, iters: int = 50) -> dict:
         torch.cuda.synchronize(dev)
         return s.elapsed_time(e) * 1000.0 / iters
 
-    res["us_per_call_64x3072_xgmi"] = round(timed(lambda: ar.all_reduce_(x)), 2)
-    if dist.get_backend(group) == "nccl":
-        res["us_per_call_64x3072_rccl"] = round(timed(lambda: dist.all_reduce(x, group=group)), 2)
+    rccl = dist.get_backend(group) == "nccl"
+    res["us_per_call"] = {}
+    for nb in sizes:
+        x = torch.randn(nb // 2, device=dev).bfloat16()
+        row = {"xgmi": round(timed(lambda: ar.all_reduce_(x)), 2), "twoshot": nb > ar.oneshot_max}
+        if rccl:
+            row["rccl"] = round(timed(lambda: dist.all_reduce(x, group=group)), 2)
+        res["us_per_call"][_size_name(nb)] = row
+    res["memory"] = "uncached (hipDeviceMallocUncached) staging + signals"
     ar.check()
     fused.check()
     ar.close()

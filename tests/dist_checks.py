@@ -1,6 +1,7 @@
-"""Multi-process correctness checks for the distributed paths (run with gloo on CPU in tests, or
-with RCCL on GPUs). Each ``check_*`` is a ``torch.multiprocessing.spawn`` target; rank 0 writes a
-JSON verdict to ``out_path``.
+"""Multi-process correctness checks for the distributed paths (test harness: run with gloo on CPU,
+or with GPU ranks through gpurun). Each ``check_*`` is a ``torch.multiprocessing.spawn`` target;
+rank 0 writes a JSON verdict to ``out_path``. Imported by the tests as ``dist_checks`` (tests/ is on
+sys.path under pytest, and spawned children inherit it).
 
   check_tp_decoder      TP=world LlamaDecoder (column/row-parallel + all-reduce, vocab-parallel
                         lm_head + all-gather) == the unsharded decoder (prefill logits, greedy tokens)
@@ -39,74 +40,14 @@ def _done(rank, out_path, verdict):
     dist.destroy_process_group()
 
 
-def _shuffled_shards(cfg, full, rank, world):
-    """NEGATIVE CONTROL: every rank loads its neighbour's shard (a wrong shard order). The checks
-    below must fail on it — tests assert they do."""
-    from ..models.llama import shard_weights
-    w = shard_weights(cfg, full, (rank + 1) % world, world)
-    return w
-
-
 def check_tp_decoder(rank, world, port, out_path, arch: str = "tiny-dec", wrong_order: bool = False):
-    """TP=world decoder vs the unsharded one on the same weights, per decision.
-
-    Teacher-forced on the unsharded model's greedy continuation, every generated step of every
-    prompt gives (gap = top-1 minus top-2 logit of the unsharded model, its argmax, the TP model's
-    argmax) and d = the max |logit difference| over all steps and the whole vocabulary (bf16
-    rounding noise of the partial sums only; a wrong-rank / stale-buffer bug is an O(1) error). A
-    decision with gap > 2 d cannot be flipped by that noise, so:
-
-    * ``checked`` = decisions with gap > 2 d; every one of them must have the same argmax in both
-      models (``checked_agree``), and they must be most decisions (a random-init model's logits are
-      bf16-quantised: top-1 / top-2 ties of 0-1 ulp exist, those steps are the unchecked ones);
-    * the free-running TP generation must equal the unsharded one up to the first unchecked step
-      of each prompt (``prefix_ok``): identical greedy tokens wherever rounding cannot decide;
-    * ``stable_prompts`` = prompts whose every step is checked (reported).
-
-    Random-init logits are flat AND bf16-quantised, so no weight scale makes every step decidable:
-    an LM-head or embedding scale multiplies gaps and noise alike (measured: stable prompts 0-3 of 8
-    at scales 1-16), hence the per-decision form. ``wrong_order`` runs the negative control."""
+    """TP=world decoder vs the unsharded one on the same weights, per decision
+    (docagents_amd/parallel/tp_verify.py: teacher-forced logit bound d, every decision with a top-1 /
+    top-2 gap above 2 d agreeing, identical free-running tokens up to each prompt's first undecidable
+    step). ``wrong_order`` runs the negative control (neighbour's shard)."""
     _init(rank, world, port)
-    from ..models.configs import decoder_config
-    from ..models.llama import LlamaDecoder, TPContext, random_weights, shard_weights
-    from ..engine.generator import Generator
-    cfg = decoder_config(arch)
-    full = random_weights(cfg, "cpu", seed=5)
-    ref = LlamaDecoder(cfg, "cpu", weights=full)
-    shard = (_shuffled_shards if wrong_order else shard_weights)(cfg, full, rank, world)
-    tp = LlamaDecoder(cfg, "cpu", tp=TPContext(rank, world, None), weights=shard)
-    prompts = [list(range(30 + 7 * i, 30 + 7 * i + n)) for i, n in enumerate((9, 33, 4, 17, 25, 6, 40, 12))]
-    steps = 8
-    a = Generator(ref, max_batch=8, max_seq=256, temperature=0.0, use_graphs=False).generate(prompts, steps)
-    b = Generator(tp, max_batch=8, max_seq=256, temperature=0.0, use_graphs=False).generate(prompts, steps)
-
-    def last_logits(m, seq):
-        t = torch.tensor(seq, dtype=torch.int32)
-        return m.prefill(t, torch.arange(len(seq), dtype=torch.int32), torch.zeros(len(seq), dtype=torch.int32),
-                         torch.tensor([0, len(seq)], dtype=torch.int32), len(seq),
-                         torch.tensor([len(seq) - 1]))[0].float()
-    d, dec = 0.0, []  # dec[i] = [(gap, ref argmax, tp argmax)] per step of prompt i
-    for p, x in zip(prompts, a):
-        steps_i = []
-        for t in range(len(x.tokens)):
-            lr, lt = last_logits(ref, p + x.tokens[:t]), last_logits(tp, p + x.tokens[:t])
-            d = max(d, float((lr - lt).abs().max()))
-            top = torch.topk(lr, 2)
-            steps_i.append((float(top.values[0] - top.values[1]), int(top.indices[0]), int(lt.argmax())))
-        dec.append(steps_i)
-    flat = [s_ for st in dec for s_ in st]
-    checked = [s_ for s_ in flat if s_[0] > 2 * d]
-    checked_agree = sum(1 for g, r_, t_ in checked if r_ == t_)
-    prefix_ok, stable = [], 0
-    for st, x, y in zip(dec, a, b):
-        n = next((j for j, s_ in enumerate(st) if s_[0] <= 2 * d), len(st))  # first undecidable step
-        stable += n == len(st)
-        prefix_ok.append(x.tokens[:n] == y.tokens[:n])  # tokens[t] is the decision of step t
-    probs = max(abs(x.mean_prob - y.mean_prob) for x, y in zip(a, b))
-    _done(rank, out_path, {"decisions": len(flat), "checked": len(checked), "checked_agree": checked_agree,
-                           "prefix_ok": prefix_ok, "stable_prompts": stable, "max_prob_diff": probs,
-                           "max_logit_diff": d, "gaps": [[round(s_[0], 4) for s_ in st] for st in dec],
-                           "tokens": [x.tokens for x in b]})
+    from docagents_amd.parallel.tp_verify import decision_verdict
+    _done(rank, out_path, decision_verdict(rank, world, None, "cpu", arch=arch, wrong_order=wrong_order))
 
 
 def check_tp8_decoder(rank, world, port, out_path):
@@ -125,8 +66,8 @@ def check_distributed_sampling(rank, world, port, out_path):
     logprobs (to fp32 rounding of the log-sum-exp regrouping), same bookkeeping (pos / hist / conf /
     active), greedy and at T = 0.2 / 1.0, on every rank."""
     _init(rank, world, port)
-    from ..models.llama import TPContext, tp_sample
-    from ..ops import reference as R
+    from docagents_amd.models.llama import TPContext, tp_sample
+    from docagents_amd.ops import reference as R
     B, V = 6, 32064 // 8 * 8
     g = torch.Generator().manual_seed(11)
     logits = (torch.randn(B, V, generator=g) * 3).bfloat16()
@@ -158,8 +99,8 @@ def check_distributed_sampling(rank, world, port, out_path):
 
 def check_sharded_index(rank, world, port, out_path):
     _init(rank, world, port)
-    from ..index.flat import FlatIndex
-    from .sharded_index import ShardedIndex
+    from docagents_amd.index.flat import FlatIndex
+    from docagents_amd.parallel.sharded_index import ShardedIndex
     d, per, B, k = 64, 120, 5, 7
     rng = np.random.default_rng(0)  # identical global data on every rank
     X = rng.standard_normal((world * per, d)).astype(np.float32)
@@ -211,13 +152,13 @@ def check_replicas(rank, world, port, out_path, tp: int = 1):
     import asyncio
     import time as _t
     _init(rank, world, port)
-    from ..engine.engine import Engine
-    from ..engine.rpc import EngineClient, EngineCluster
-    from ..engine.server import EngineGroup, EngineServer, owner_of
-    from ..models.llama import TPContext
-    from ..utils import faults
-    from ..utils.log import discard
-    from .search_plane import SearchPlane
+    from docagents_amd.engine.engine import Engine
+    from docagents_amd.engine.rpc import EngineClient, EngineCluster
+    from docagents_amd.engine.server import EngineGroup, EngineServer, owner_of
+    from docagents_amd.models.llama import TPContext
+    from docagents_amd.utils import faults
+    from docagents_amd.utils.log import discard
+    from docagents_amd.parallel.search_plane import SearchPlane
     replicas, replica = world // tp, rank // tp
     rep_ctrl = rep_data = None
     for r in range(replicas):
@@ -360,8 +301,8 @@ def check_replicas(rank, world, port, out_path, tp: int = 1):
 
 def check_ivf_kmeans(rank, world, port, out_path):
     _init(rank, world, port)
-    from ..index.ivf import IVFFlatIndex
-    from .sharded_index import ShardedIndex
+    from docagents_amd.index.ivf import IVFFlatIndex
+    from docagents_amd.parallel.sharded_index import ShardedIndex
     d, per = 32, 600
     rng = np.random.default_rng(1)
     centers = rng.standard_normal((8, d)).astype(np.float32)
@@ -397,7 +338,7 @@ def check_xgmi_allreduce(rank, world, port, out_path):
     of different sizes (exercises the per-workgroup counters and the staging parity). GPU ranks;
     the handle exchange rides a gloo group, so several ranks may share one GPU (1-GPU rehearsal)."""
     _init(rank, world, port)
-    from .xgmi_allreduce import XgmiAllReduce
+    from docagents_amd.parallel.xgmi_allreduce import XgmiAllReduce
     dev = torch.device("cuda", rank % torch.cuda.device_count())
     torch.cuda.set_device(dev)
     ar = XgmiAllReduce(None, dev, max_bytes=8 << 20, oneshot_max=256 << 10)
@@ -469,7 +410,7 @@ def check_xgmi_verify_and_time(rank, world, port, out_path):
     """The cross-device check bench.py runs on multi-GPU nodes (xgmi_allreduce.verify_and_time),
     rehearsed with ranks that may share one GPU."""
     _init(rank, world, port)
-    from .xgmi_allreduce import verify_and_time
+    from docagents_amd.parallel.xgmi_allreduce import verify_and_time
     dev = torch.device("cuda", rank % torch.cuda.device_count())
     torch.cuda.set_device(dev)
     _done(rank, out_path, verify_and_time(None, dev, iters=10))
@@ -480,8 +421,8 @@ def check_xgmi_allreduce_norm(rank, world, port, out_path):
     followed by the rmsnorm kernel: x and h must be BIT-identical, for several row widths / row
     counts, gamma given or unit, eager and HIP-graph replay. GPU ranks (may share one GPU)."""
     _init(rank, world, port)
-    from ..ops import kernels as K
-    from .xgmi_allreduce import XgmiAllReduce
+    from docagents_amd.ops import kernels as K
+    from docagents_amd.parallel.xgmi_allreduce import XgmiAllReduce
     dev = torch.device("cuda", rank % torch.cuda.device_count())
     torch.cuda.set_device(dev)
     plain = XgmiAllReduce(None, dev, max_bytes=8 << 20)
@@ -550,54 +491,13 @@ def check_xgmi_allreduce_norm(rank, world, port, out_path):
 
 def check_tp_decoder_gpu(rank, world, port, out_path, wrong_order: bool = False):
     """TP=world LlamaDecoder on GPU ranks (row-parallel outputs summed by the xGMI all-reduce kernel,
-    vocab-parallel logits gathered over it) vs the unsharded decoder on the same device, with the
-    per-decision verdict of check_tp_decoder: teacher-forced logit bound d, every decision with a
-    top-1 / top-2 gap above 2 d agreeing, identical free-running tokens up to each prompt's first
-    undecidable step. ``wrong_order``: negative control (neighbour's shard)."""
+    vocab-parallel sampling gathered over it) vs the unsharded decoder on the same device, with the
+    per-decision verdict of check_tp_decoder. ``wrong_order``: negative control."""
     _init(rank, world, port)
-    from ..engine.generator import Generator
-    from ..models.configs import decoder_config
-    from ..models.llama import LlamaDecoder, TPContext, random_weights, shard_weights
+    from docagents_amd.parallel.tp_verify import decision_verdict
     dev = torch.device("cuda", rank % torch.cuda.device_count())
     torch.cuda.set_device(dev)
-    cfg = decoder_config("tiny-dec")
-    full = random_weights(cfg, dev, seed=5)
-    ref = LlamaDecoder(cfg, dev, weights=full)
-    src = (rank + 1) % world if wrong_order else rank
-    tp = LlamaDecoder(cfg, dev, tp=TPContext(rank, world, None), weights=shard_weights(cfg, full, src, world))
-    prompts = [list(range(30 + 5 * i, 30 + 5 * i + n)) for i, n in enumerate((9, 33, 4, 120, 17, 64, 25, 7))]
-    steps = 8
-    a = Generator(ref, max_batch=8, max_seq=256, temperature=0.0, use_graphs=False).generate(prompts, steps)
-    b = Generator(tp, max_batch=8, max_seq=256, temperature=0.0, use_graphs=False).generate(prompts, steps)
-
-    def last_logits(m, seq):
-        t = torch.tensor(seq, dtype=torch.int32, device=dev)
-        return m.prefill(t, torch.arange(len(seq), dtype=torch.int32, device=dev),
-                         torch.zeros(len(seq), dtype=torch.int32, device=dev),
-                         torch.tensor([0, len(seq)], dtype=torch.int32, device=dev), len(seq),
-                         torch.tensor([len(seq) - 1], device=dev))[0].float()
-    ref.alloc_cache(1, 256)
-    tp.alloc_cache(1, 256)
-    d, dec = 0.0, []
-    for p, x in zip(prompts, a):
-        st = []
-        for t in range(len(x.tokens)):
-            lr, lt = last_logits(ref, p + x.tokens[:t]), last_logits(tp, p + x.tokens[:t])
-            d = max(d, float((lr - lt).abs().max()))
-            top = torch.topk(lr, 2)
-            st.append((float(top.values[0] - top.values[1]), int(top.indices[0]), int(lt.argmax())))
-        dec.append(st)
-    flat = [s_ for st in dec for s_ in st]
-    checked = [s_ for s_ in flat if s_[0] > 2 * d]
-    prefix_ok = []
-    for st, x, y in zip(dec, a, b):
-        n = next((j for j, s_ in enumerate(st) if s_[0] <= 2 * d), len(st))
-        prefix_ok.append(x.tokens[:n] == y.tokens[:n])
-    _done(rank, out_path, {"xgmi": tp.tp.xgmi is not None, "xgmi_calls": tp.tp.xgmi.calls if tp.tp.xgmi else 0,
-                           "decisions": len(flat), "checked": len(checked),
-                           "checked_agree": sum(1 for _, r_, t_ in checked if r_ == t_), "prefix_ok": prefix_ok,
-                           "max_logit_diff": d,
-                           "max_prob_diff": max(abs(p.mean_prob - q.mean_prob) for p, q in zip(a, b))})
+    _done(rank, out_path, decision_verdict(rank, world, None, dev, wrong_order=wrong_order))
 
 
 def check_tp_decoder_gpu_wrong_order(rank, world, port, out_path):
@@ -616,11 +516,11 @@ def check_replica_failover(rank, world, port, out_path, victim: int | None = Non
     import signal
     import time as _t
     _init(rank, world, port)
-    from ..engine.engine import Engine
-    from ..engine.rpc import EngineCluster
-    from ..engine.server import EngineGroup, EngineServer, owner_of
-    from ..utils.log import discard
-    from .search_plane import SearchPlane
+    from docagents_amd.engine.engine import Engine
+    from docagents_amd.engine.rpc import EngineCluster
+    from docagents_amd.engine.server import EngineGroup, EngineServer, owner_of
+    from docagents_amd.utils.log import discard
+    from docagents_amd.parallel.search_plane import SearchPlane
     victim = world - 1 if victim is None else victim
     eng = Engine("tiny-enc", "tiny-dec", "cpu", max_batch=4, max_seq=512, max_new_tokens=4, summary_max_new=4,
                  use_graphs=False)

@@ -1,0 +1,48 @@
+"""bench.py's JSON line at N > 1 (VERDICT r4 Next #1): after the data-parallel headline, the timed
+multi-GPU blocks — ``rccl_search`` (C1 + C2 as collectives, >= 3 timed sharded searches here, rows
+identical to the serving plane), ``tp_decode`` (the decoder at TP = N, decode ms per step at batch 1
+and batch B per all-reduce arm, the per-decision TP verdict) — plus the single-document ingest
+latency and the physical-GPU count. Rehearsed on CPU ranks (gloo, tiny configs): the schema and the
+verdicts are pinned here; the numbers come from the GPU node."""
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_bench_two_rank_json_schema():
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["OMP_NUM_THREADS"] = "2"
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--cpu-rehearsal",
+           "--enc", "tiny-enc", "--llm", "tiny-dec", "--batch", "2", "--steps", "1", "--warmup", "0",
+           "--latency-reps", "2", "--ingest-docs", "2", "--ingest-batches", "1", "--ingest-latency-reps", "2",
+           "--index-rows", "2000", "--multi-iters", "3", "--breakdown", "0", "--max-new", "4",
+           "--ingest-words", "300"]
+    p = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600, cwd=ROOT)
+    assert p.returncode == 0, p.stderr[-2000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout[-2000:]
+    out = json.loads(lines[0])
+    # driver contract + the physical-device count (two CPU ranks share this host: not two GPUs)
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
+              "scaling", "vs_baseline", "dtype", "data", "config"):
+        assert k in out, k
+    assert out["world_size"] == 2 and out["ranks_seen"] == 2
+    assert out["n_gpus"] == 1 and out["oversubscribed"] is True
+    # the reference's ingest number: per-document latency
+    assert out["ingest_single_doc_reps"] == 2 and out["ingest_single_doc_p50_ms"] > 0
+    # C1 + C2 over the collective backend, timed, identical rows to the plane
+    rs = out["rccl_search"]
+    assert rs["iters"] == 3 and rs["rows_per_rank"] == 2 and rs["world"] == 2, rs
+    assert rs["qps"] > 0 and rs["p50_ms"] > 0 and rs["p90_ms"] >= rs["p50_ms"], rs
+    assert rs["rows_identical_to_plane"] == rs["rows_checked"] == 2 and rs["scores_close"], rs
+    # TP = N decode per arm, batch 1 and batch B, plus the agreement verdict
+    td = out["tp_decode"]
+    assert td["tp"] == 2 and "error" not in td, td
+    assert td["arms"], td
+    for arm in td["arms"].values():
+        assert arm["b1_decode_ms_per_step"] > 0 and arm["b2_decode_ms_per_step"] > 0, td
+    ag = td["agreement"]
+    assert ag["ok"] and ag["checked_agree"] == ag["checked"] > 0, ag

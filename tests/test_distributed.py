@@ -6,7 +6,7 @@ import socket
 import pytest
 import torch.multiprocessing as mp
 
-from docagents_amd.parallel import selftest
+import dist_checks
 
 
 def _port():
@@ -25,26 +25,26 @@ def _run(fn, world, tmp_path):
 
 def _tp_verdict_ok(v) -> bool:
     """Every rounding-proof decision agrees, they are most decisions, and the free-running tokens
-    are identical up to each prompt's first rounding-decidable step (selftest.check_tp_decoder)."""
+    are identical up to each prompt's first rounding-decidable step (dist_checks.check_tp_decoder)."""
     return (v["max_logit_diff"] < 0.05 and v["checked"] >= 0.6 * v["decisions"]
             and v["checked_agree"] == v["checked"] and all(v["prefix_ok"]) and v["max_prob_diff"] < 1e-3)
 
 
 def test_tp2_decoder_matches_unsharded(tmp_path):
-    v = _run(selftest.check_tp_decoder, 2, tmp_path)
+    v = _run(dist_checks.check_tp_decoder, 2, tmp_path)
     assert _tp_verdict_ok(v), v
     assert v["checked"] >= 0.6 * v["decisions"] and v["decisions"] == 8 * 8, v
 
 
 def test_tp8_decoder_one_kv_head_per_rank_matches_unsharded(tmp_path):
     """TP=8 with 8 KV heads (one per rank, as Llama-3-70B at TP=8): identical greedy tokens."""
-    v = _run(selftest.check_tp8_decoder, 8, tmp_path)
+    v = _run(dist_checks.check_tp8_decoder, 8, tmp_path)
     assert _tp_verdict_ok(v), v
 
 
 def test_tp_decoder_check_bites_on_wrong_shard_order(tmp_path):
     """Negative control: ranks loading each other's shards must fail the same verdict."""
-    v = _run(selftest.check_tp_decoder_wrong_order, 2, tmp_path)
+    v = _run(dist_checks.check_tp_decoder_wrong_order, 2, tmp_path)
     assert not _tp_verdict_ok(v), v
     assert v["checked_agree"] < 0.5 * max(1, v["checked"]) or v["max_logit_diff"] > 0.05, v
 
@@ -52,13 +52,13 @@ def test_tp_decoder_check_bites_on_wrong_shard_order(tmp_path):
 @pytest.mark.parametrize("world", [2, 8])
 def test_distributed_sampling_matches_full_row_sampler(tmp_path, world):
     """vocab-parallel sampling (8 floats per row exchanged, not the logits)."""
-    v = _run(selftest.check_distributed_sampling, world, tmp_path)
+    v = _run(dist_checks.check_distributed_sampling, world, tmp_path)
     assert v["ok"], v
 
 
 @pytest.mark.parametrize("world", [2, 4, 8])
 def test_sharded_index_exact(tmp_path, world):
-    assert _run(selftest.check_sharded_index, world, tmp_path)["exact"]
+    assert _run(dist_checks.check_sharded_index, world, tmp_path)["exact"]
 
 
 def _replicas_ok(v, world, replicas):
@@ -73,11 +73,11 @@ def _replicas_ok(v, world, replicas):
 def test_eight_dp_replicas_never_block_on_each_other(tmp_path):
     """8 DP replicas (TP_SIZE=1): interleaved answer / embed / search / embed_search RPCs while one
     replica is stuck in slow decode ticks; searches still cover every shard through the plane."""
-    _replicas_ok(_run(selftest.check_replicas, 8, tmp_path), 8, 8)
+    _replicas_ok(_run(dist_checks.check_replicas, 8, tmp_path), 8, 8)
 
 
 def _check_replicas_tp2(rank, world, port, out_path):
-    selftest.check_replicas(rank, world, port, out_path, tp=2)
+    dist_checks.check_replicas(rank, world, port, out_path, tp=2)
 
 
 def test_tp2_x_dp4_serving(tmp_path):
@@ -87,6 +87,6 @@ def test_tp2_x_dp4_serving(tmp_path):
 
 @pytest.mark.parametrize("world", [2, 8])
 def test_ivf_distributed_kmeans(tmp_path, world):
-    v = _run(selftest.check_ivf_kmeans, world, tmp_path)
+    v = _run(dist_checks.check_ivf_kmeans, world, tmp_path)
     assert v["centroids_equal"], v
     assert v["recall"] >= 0.8, v

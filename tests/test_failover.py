@@ -6,7 +6,7 @@ import socket
 
 import torch.multiprocessing as mp
 
-from docagents_amd.parallel import selftest
+import dist_checks
 
 
 def _port():
@@ -21,7 +21,7 @@ def test_sigkilled_rank_fails_only_its_shard(tmp_path):
     world, port = 4, _port()
     out = str(tmp_path / "failover.json")
     ctx = mp.get_context("spawn")
-    procs = [ctx.Process(target=selftest.check_replica_failover, args=(r, world, port, out)) for r in range(world)]
+    procs = [ctx.Process(target=dist_checks.check_replica_failover, args=(r, world, port, out)) for r in range(world)]
     for p in procs:
         p.start()
     for p in procs:

@@ -7,7 +7,7 @@ import socket
 import pytest
 import torch.multiprocessing as mp
 
-from docagents_amd.parallel import selftest
+import dist_checks
 
 pytestmark = pytest.mark.gpu
 
@@ -22,7 +22,7 @@ def _port():
 
 def test_xgmi_allreduce_matches_rank_order_sum(tmp_path):
     out = tmp_path / "ar.json"
-    mp.spawn(selftest.check_xgmi_allreduce, args=(2, _port(), str(out)), nprocs=2, join=True)
+    mp.spawn(dist_checks.check_xgmi_allreduce, args=(2, _port(), str(out)), nprocs=2, join=True)
     v = json.loads(out.read_text())
     bad = [c for c in v["cases"] if not c["ok"]]
     assert v["ok"] and not bad, bad
@@ -32,7 +32,7 @@ def test_xgmi_allreduce_matches_rank_order_sum(tmp_path):
 def test_xgmi_allreduce_rmsnorm_bit_identical_to_unfused(tmp_path):
     """Fused all-reduce + RMSNorm epilogue == all-reduce kernel then rmsnorm kernel, bit for bit."""
     out = tmp_path / "arn.json"
-    mp.spawn(selftest.check_xgmi_allreduce_norm, args=(2, _port(), str(out)), nprocs=2, join=True)
+    mp.spawn(dist_checks.check_xgmi_allreduce_norm, args=(2, _port(), str(out)), nprocs=2, join=True)
     v = json.loads(out.read_text())
     bad = [c for c in v["cases"] if not c["ok"]]
     assert v["ok"] and not bad, bad
@@ -42,10 +42,12 @@ def test_xgmi_allreduce_rmsnorm_bit_identical_to_unfused(tmp_path):
 def test_bench_xgmi_cross_device_check_passes(tmp_path):
     """bench.py's multi-GPU C3 check (exact sums one-/two-shot, fused norm bit identity, timing)."""
     out = tmp_path / "vt.json"
-    mp.spawn(selftest.check_xgmi_verify_and_time, args=(2, _port(), str(out)), nprocs=2, join=True)
+    mp.spawn(dist_checks.check_xgmi_verify_and_time, args=(2, _port(), str(out)), nprocs=2, join=True)
     v = json.loads(out.read_text())
     assert v["ok"] and v["fused_norm_bit_identical"] and len(v["cases"]) == 3, v
-    assert any(c["twoshot"] for c in v["cases"]) and v["us_per_call_64x3072_xgmi"] > 0
+    assert any(c["twoshot"] for c in v["cases"]), v
+    assert set(v["us_per_call"]) == {"16KB", "384KB", "6MB"}, v
+    assert all(r["xgmi"] > 0 for r in v["us_per_call"].values()) and v["us_per_call"]["6MB"]["twoshot"], v
 
 
 def _tp_ok(v) -> bool:
@@ -54,10 +56,10 @@ def _tp_ok(v) -> bool:
 
 
 def test_tp2_decoder_gpu_uses_xgmi_allreduce(tmp_path):
-    """Per-decision TP verdict (parallel/selftest.py check_tp_decoder_gpu): teacher-forced logit bound,
+    """Per-decision TP verdict (tests/dist_checks.py check_tp_decoder_gpu): teacher-forced logit bound,
     every rounding-proof greedy decision identical, identical tokens up to the first undecidable step."""
     out = tmp_path / "tp.json"
-    mp.spawn(selftest.check_tp_decoder_gpu, args=(2, _port(), str(out)), nprocs=2, join=True)
+    mp.spawn(dist_checks.check_tp_decoder_gpu, args=(2, _port(), str(out)), nprocs=2, join=True)
     v = json.loads(out.read_text())
     assert v["xgmi"] and v["xgmi_calls"] > 0, v
     assert _tp_ok(v), v
@@ -65,6 +67,6 @@ def test_tp2_decoder_gpu_uses_xgmi_allreduce(tmp_path):
 
 def test_tp2_decoder_gpu_check_bites_on_wrong_shard_order(tmp_path):
     out = tmp_path / "tpw.json"
-    mp.spawn(selftest.check_tp_decoder_gpu_wrong_order, args=(2, _port(), str(out)), nprocs=2, join=True)
+    mp.spawn(dist_checks.check_tp_decoder_gpu_wrong_order, args=(2, _port(), str(out)), nprocs=2, join=True)
     v = json.loads(out.read_text())
     assert not _tp_ok(v), v
