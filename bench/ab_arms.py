@@ -7,11 +7,8 @@ lives here now, for comparisons only:
 * ``blas_gemm`` / ``blas_swiglu``: the platform BLAS (hipBLASLt through ``torch.mm``) for the same
   products, so ``bench/gemm_ab.py`` can time gemm8p against the vendor library on one box;
 * ``swiglu_interleaved``: the standalone SwiGLU pass the BLAS arm needs (the in-tree GEMM fuses it);
-* ``apply_env_overrides``: kernel-schedule overrides (decode-tile prefetch depth, flash prefill
-  shape, GEMV blocking, decode-attention prefetch) read from ``DA_*`` environment variables and
-  pushed into the library's setters, and the model's alternative code paths (fused prefill norms,
-  the persistent batch-1 decode), so a sweep can flip one knob per process. ``bench.py`` applies
-  them too (nothing happens without a ``DA_*`` variable set).
+* ``apply_env_overrides``: the model-level decode GEMM route read from ``DA_DECODE_DK``, so a
+  sweep can flip it per process. ``bench.py`` applies it too (nothing happens without it set).
 """
 from __future__ import annotations
 
@@ -23,49 +20,15 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from docagents_amd.ops import kernels as K  # noqa: E402
 
-ENV_SETTERS = {
-    "DA_GEMM_PF": "da_set_gemm_pf",          # decode-tile k-tiles in flight
-    "DA_DK_RB": "da_set_dk_rb",              # gemm_dk 33..64 rows: two 32-row blocks (1) / one 64-row block (0)
-    "DA_GEMM_DB": "da_set_gemm_db",          # decode tiles load W fragments straight to registers
-    "DA_DECODE_BALANCE": "da_set_decode_balance",  # decode attention: balanced vs fixed keys per split
-    "DA_DECODE_QFIRST": "da_set_decode_qfirst",    # batch-1 decode attention: prologue loads before K/V
-    "DA_FLASH_PIPE": "da_set_flash_pipe",    # software-pipelined flash prefill on / off / auto
-    "DA_FLASH_QH": "da_set_flash_qh",        # flash queries per wave: 1 = 32, 2 = 64
-    "DA_FLASH_WAVES": "da_set_flash_waves",  # flash waves per workgroup
-    "DA_FLASH_REV": "da_set_flash_rev",      # flash dispatch: bit 0 causal longest-first, bit 1 XCD-grouped
-    "DA_GEMV_U": "da_set_gemv_u",            # batch-1 GEMV K-blocks in flight per row
-    "DA_GEMV_KS": "da_set_gemv_ks",          # batch-1 GEMV waves per long row
-    "DA_DECODE_PFT": "da_set_decode_pft",    # MHA decode next-tile prefetch threshold
-    "DA_DECODE_W8": "da_set_decode_w8",      # ... with 8 waves per workgroup up to this many (row, kv head) pairs
-    "DA_DECODE_W8_VAR": "da_set_decode_w8_var",  # ... 0: two tiles per wave (spills), 1: one tile per wave
-    "DA_GEMM8P_GROUP": "da_set_gemm8p_group",  # prefill GEMM tile-order band height (0 = auto)
-    "DA_GEMM8P_BM_RULE": "da_set_gemm8p_bm_rule",  # prefill row-tile height: 1 = fewest waves, 0 = round-3 rule
-    "DA_OMERGE_SHAPE": "da_set_omerge_shape",  # merged batch-1 O GEMV: waves per workgroup * 10 + rows per wave
-}
-
-
 def apply_env_overrides() -> dict:
-    """Push every DA_* schedule override present in the environment into the library."""
-    L = K.lib()
+    """Model-level switches read from ``DA_*`` environment variables (one per process):
+    DA_DECODE_DK=0 routes 2..64-row decode GEMMs to the split-K tiles instead of gemm_dk. The kernel
+    schedule setters and the rejected decode / prefill arms of rounds 1-4 were removed from the
+    library (git history keeps them; profiles/r4/rejected_r4.txt has their numbers)."""
     done = {}
-    from docagents_amd.models import llama
-    for env, attr in (("DA_PREFILL_NORM_FUSE", "_PREFILL_NORM_FUSE"), ("DA_DECODE_B1", "_DECODE_B1"),
-                      ("DA_O_MERGE", "_O_MERGE"), ("DA_QKV_FOLD", "_QKV_FOLD")):
-        if os.environ.get(env) is not None:  # model-level code paths (default: llama.py)
-            setattr(llama, attr, os.environ[env] == "1")
-            done[env] = int(getattr(llama, attr))
-    if os.environ.get("DA_SPLITK_FUSED") is not None:  # 33..64-row decode: in-kernel split-K reduce
-        from docagents_amd.ops import reference as R
-        K.SPLITK_FUSED = R.SPLITK_FUSED = os.environ["DA_SPLITK_FUSED"] != "0"
-        done["DA_SPLITK_FUSED"] = int(K.SPLITK_FUSED)
     if os.environ.get("DA_DECODE_DK") is not None:  # decode GEMMs: gemm_dk (1) vs split-K tiles (0)
         K.DECODE_DK = os.environ["DA_DECODE_DK"] != "0"
         done["DA_DECODE_DK"] = int(K.DECODE_DK)
-    for env, fn in ENV_SETTERS.items():
-        v = os.environ.get(env)
-        if v is not None:
-            getattr(L, fn)(int(v))
-            done[env] = int(v)
     return done
 
 

@@ -1,5 +1,5 @@
-"""Prefill attention microbenchmark: flash_attn_v2 arms (4 / 8 waves per workgroup x 32 / 64 queries per wave)
-vs torch SDPA on MI355X shapes, each arm checked against SDPA."""
+"""Prefill attention microbenchmark: the production flash dispatch (ops.flash_attn_varlen: the pipelined
+causal D = 96 kernel, flash_attn_v2 otherwise) vs torch SDPA on MI355X shapes, checked against SDPA."""
 import argparse
 import os
 import sys
@@ -10,8 +10,6 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 from docagents_amd.ops import kernels as K  # noqa: E402
-from ab_arms import apply_env_overrides  # noqa: E402
-apply_env_overrides()  # DA_* schedule overrides for A/B sweeps
 
 
 def timeit(fn, iters=10):
@@ -33,7 +31,8 @@ def main():
     dev = torch.device("cuda")
     torch.manual_seed(0)
     res = {}
-    for name, B, L, H, Hkv, D, causal in [("phi3_prefill", 8, 2944, 32, 32, 96, True),
+    for name, B, L, H, Hkv, D, causal in [("phi3_qa_chunk", 22, 2938, 32, 32, 96, True),
+                                          ("phi3_prefill", 8, 2944, 32, 32, 96, True),
                                           ("bge_base", 64, 512, 12, 12, 64, False),
                                           ("bge_small", 64, 512, 12, 12, 32, False),
                                           ("llama3_prefill", 4, 4096, 32, 8, 128, True),
@@ -49,21 +48,10 @@ def main():
         vv = v.reshape(B, L, Hkv, D).transpose(1, 2).repeat_interleave(H // Hkv, 1)
         ref = torch.nn.functional.scaled_dot_product_attention(qq, kk, vv, is_causal=causal)
         ref = ref.transpose(1, 2).reshape(T, H * D).float()
-        # arms: waves per workgroup x 32-query halves per wave
-        for nw, qh, pipe in ((4, 1, 0), (8, 1, 0), (4, 2, 0), (8, 2, 0), (4, 1, 1), (4, 1, 3), (4, 1, 4)):
-            if (nw * qh > 8 and D > 64) or (pipe and D > 96):
-                continue
-            K.lib().da_set_flash_waves(nw)
-            K.lib().da_set_flash_qh(qh)
-            K.lib().da_set_flash_pipe(pipe)
-            arm = f"w{nw}q{qh}" + ("", "pipe", "", "spec", "dma")[pipe]
-            t = timeit(lambda: K.flash_attn_varlen(q, k, v, cu, L, H, Hkv, D, causal))
-            out = K.flash_attn_varlen(q, k, v, cu, L, H, Hkv, D, causal).float()
-            r[arm] = {"ms": round(t, 3), "tflops": round(fl / t / 1e9, 1),
-                      "max_err_vs_sdpa": round((out - ref).abs().max().item(), 4)}
-        K.lib().da_set_flash_waves(0)
-        K.lib().da_set_flash_qh(0)
-        K.lib().da_set_flash_pipe(K.FLASH_PIPE_DEFAULT)
+        t = timeit(lambda: K.flash_attn_varlen(q, k, v, cu, L, H, Hkv, D, causal))
+        out = K.flash_attn_varlen(q, k, v, cu, L, H, Hkv, D, causal).float()
+        r["ours"] = {"ms": round(t, 3), "tflops": round(fl / t / 1e9, 1),
+                     "max_err_vs_sdpa": round((out - ref).abs().max().item(), 4)}
         t = timeit(lambda: torch.nn.functional.scaled_dot_product_attention(qq, kk, vv, is_causal=causal))
         r["sdpa"] = {"ms": round(t, 3), "tflops": round(fl / t / 1e9, 1)}
         res[name] = r

@@ -1,5 +1,5 @@
 """One prefill-attention shape, repeated (for rocprofv3 PMC passes): phi3 (causal, D=96; phi3qa = the
-QA prefill chunk, 22 x 2938) or bge (D=64). DA_FLASH_REV selects the dispatch order."""
+QA prefill chunk, 22 x 2938) or bge (D=64)."""
 import os
 import sys
 
@@ -10,8 +10,6 @@ from docagents_amd.ops import kernels as K  # noqa: E402
 
 SHAPES = {"phi3": (8, 2944, 32, 32, 96, True), "phi3qa": (22, 2938, 32, 32, 96, True), "bge": (64, 512, 12, 12, 64, False)}
 B, L, H, Hkv, D, causal = SHAPES[os.environ.get("SHAPE", "phi3")]
-if os.environ.get("DA_FLASH_REV"):
-    K.lib().da_set_flash_rev(int(os.environ["DA_FLASH_REV"]))
 dev = torch.device("cuda")
 torch.manual_seed(0)
 T = B * L

@@ -72,13 +72,10 @@ def main():
                 res = {}
                 tile = K._decode_tile(M)
                 auto_s = K._auto_splits(M, N, Kd)
-                for pf in (1, 2, 4):
-                    K.lib().da_set_gemm_pf(pf)
-                    for sp in (1, 2, 4, 8, 16):
-                        if (Kd // 64) % sp or (pf == 2 and sp != auto_s):
-                            continue
-                        res[f"pf{pf}s{sp}"] = timed(runner(tile, sp), ncopy)
-                K.lib().da_set_gemm_pf(4)
+                for sp in (1, 2, 4, 8, 16):
+                    if (Kd // 64) % sp:
+                        continue
+                    res[f"s{sp}"] = timed(runner(tile, sp), ncopy)
                 best = min(res, key=res.get)
                 print(json.dumps({"model": model, "gemm": name, "M": M, "N": N, "K": Kd, "MB": round(by / 1e6, 1),
                                   "us": {k: round(v, 1) for k, v in res.items()}, "auto_splits": auto_s,

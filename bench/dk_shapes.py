@@ -1,7 +1,6 @@
 """Decode GEMMs at 33..64 rows, per Phi-3 layer shape (qkv, o + residual, gate/up + SwiGLU, down +
 residual), each over 32 distinct weight matrices captured in one graph (HBM-resident, like the
-decode chain): the split-K tiles + reduce ("splitk") vs gemm_dk arms selected by da_set_dk_rb
-(1 = two 32-row dk blocks, 0 = one 64-row dk block).
+decode chain): the split-K tiles + reduce ("splitk") vs gemm_dk (two 32-row blocks per n-tile).
 Prints us per GEMM and TB/s of weight bytes."""
 import json
 import os
@@ -29,15 +28,13 @@ def main():
             out = torch.empty(M, nout, device=dev, dtype=torch.bfloat16)
             K.reserve_workspace(8 * M * N * 4, dev)
             row = {}
-            for arm in ("splitk", "rb1", "rb0"):
+            for arm in ("splitk", "dk"):
                 def run():
                     for w in W:
                         if arm == "splitk":
                             K.gemm(x, w, epi=epi, resid=r, out=out, tile=2 if M > 32 else 3, splits=0)
                         else:
                             K.gemm_dk(x, w, epi=epi, resid=r, out=out)
-                if arm != "splitk":
-                    K.lib().da_set_dk_rb({"rb1": 1, "rb0": 0}[arm])
                 run(); torch.cuda.synchronize()
                 ref = out.clone()
                 graph = torch.cuda.CUDAGraph()
@@ -56,7 +53,6 @@ def main():
                 else:
                     row[arm]["maxdiff_vs_splitk"] = round((ref.float() - base.float()).abs().max().item(), 4)
                 del graph
-            K.lib().da_set_dk_rb(1)
             res[name] = row
             del W
         print(json.dumps(res), flush=True)

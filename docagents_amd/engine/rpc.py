@@ -173,7 +173,9 @@ class EngineCluster:
         (internal/queue/nats.go:40-51) for the GPU engine. These calls are idempotent (no engine
         state changes), so a replica that is unreachable (or reports itself unhealthy) is skipped
         for ``dead_s`` and the call is retried on the next live replica: replicas fail
-        independently, as the reference's queue-group workers do;
+        independently, as the reference's queue-group workers do. A client-side timeout is not a
+        dead replica: cheap calls (embed / search) are re-asked of another replica, generations
+        (answer / summarize) fail — nothing cancels them server-side, so a retry would double the work;
       * ``health`` fans out: healthy only if every replica is, with the dead ones named.
     ``stats`` has one shape for any replica count: ``{"replicas": [per-replica stats]}``."""
 
@@ -223,12 +225,17 @@ class EngineCluster:
         self._rr = (best + 1) % n
         return best
 
+    CHEAP = ("embed", "embed_search", "search")  # a timed-out one may be re-asked of another replica
+
     @staticmethod
     def _replica_down(e: BaseException) -> bool:
         """A failure of the replica itself (not of the request): connection lost / refused, or the
-        engine's watchdog reporting it unhealthy."""
-        return isinstance(e, (ConnectionError, OSError, asyncio.TimeoutError)) or (
-            isinstance(e, RPCError) and "engine unhealthy" in str(e))
+        engine's watchdog reporting it unhealthy. NOT a client-side timeout: a busy replica is
+        alive (marking it dead would steer load off live replicas and, for generations, re-run the
+        same work elsewhere while the first replica still computes it — a retry storm)."""
+        if isinstance(e, (asyncio.TimeoutError, TimeoutError)):
+            return False
+        return isinstance(e, (ConnectionError, OSError)) or (isinstance(e, RPCError) and "engine unhealthy" in str(e))
 
     async def _on(self, i: int, method: str, trace: str, args: dict):
         self.inflight[i] += 1
@@ -272,9 +279,12 @@ class EngineCluster:
             try:
                 return await self._on(i, method, trace, args)
             except Exception as e:  # noqa: BLE001
-                if not self._replica_down(e) or len(tried) >= len(self.clients):
+                if len(tried) >= len(self.clients):
                     raise
-                self.dead_until[i] = time.monotonic() + self.dead_s
+                if self._replica_down(e):
+                    self.dead_until[i] = time.monotonic() + self.dead_s
+                elif not (isinstance(e, (asyncio.TimeoutError, TimeoutError)) and method in self.CHEAP):
+                    raise  # a request error, or a timed-out generation: fail the call, retry nothing
 
     async def _health(self, trace: str = ""):
         async def one(i):

@@ -31,30 +31,9 @@ from ..ops.reference import interleave_gate_up, rope_table
 from .configs import DecoderConfig
 
 EPI_NONE, EPI_SWIGLU, EPI_RESID, EPI_ROPE = 0, 3, 4, 6
-# Prefill RMSNorms folded into the projections (_prefill_fused_norms): measured a net loss, off
-# (profiles/r3/prefill_norm_fuse/); bench/ab_arms.py flips it for A/B runs (DA_PREFILL_NORM_FUSE=1)
-_PREFILL_NORM_FUSE = False
 # Decode step of MHA models: RoPE + KV-cache write folded into the attention kernel (False: separate
 # rope_cache launch; the GPU tests compare both).
 _FUSED_ROPE_DECODE = True
-# Batch-1 decode as ONE persistent launch over all layers + the LM head (ops/csrc/decode_b1.hip).
-# Bit-identical to the per-kernel path (tests/test_decode_b1_gpu.py) but measured SLOWER on the
-# MI355X: 2.34 vs 2.06 ms per step (bench/b1_persistent_ab.py, profiles/r4/check_d_b1_fused_on/, profiles/r4/check_d/) — its four
-# chip-wide fan-ins per layer (~3-4 us each at 256 arrivals) cost more than the five launch
-# boundaries (~1.2 us each) they replace. Off by default; bench/ab_arms.py DA_DECODE_B1=1 selects it.
-_DECODE_B1 = False
-# Batch-1 decode: the attention's split merge folded into the O projection's input load
-# (attention.hip da_decode_attn_parts + gemm.hip da_gemv_omerge). Bit-identical (tests/
-# test_o_merge_gpu.py) but not faster on the MI355X: the attention loses its ticketed merge tail
-# (14.75 -> 12.38 us) and the O GEMV gains as much (5.26 -> 7.82 us: every workgroup merges the
-# whole 100 KB of partials; profiles/r4/o_merge/). Off; bench/ab_arms.py DA_O_MERGE=1 selects it.
-_O_MERGE = False
-# 33..64-row decode: the QKV projection's split-K reduce folded into the decode attention's prologue
-# (ops.gemm_dk_qkv_parts -> decode_attn reads the partials). Bit-identical (tests/
-# test_qkv_fold_gpu.py) but not faster on the MI355X: 14.85 vs 14.79 ms per batch-64 step
-# (bench/qkv_fold_ab.py, profiles/r4/qkv_fold/) — 2048 attention workgroups each rebuilding their
-# q / k / v from 3 splits cost what the reduce launch does. Off; bench/ab_arms.py DA_QKV_FOLD=1.
-_QKV_FOLD = False
 
 
 class TPContext:
@@ -324,9 +303,6 @@ class LlamaDecoder:
         c, o, cache = self.cfg, self.ops, self.cache
         D, hl, kl = c.head_dim, self.hl, self.kl
         x = o.embed(ids, self.w["embed"])
-        if self._prefill_norms_fusable(x.shape[0]):
-            x = self._prefill_fused_norms(x, pos, slot_tok, cu, max_seqlen, prefix)
-            return self._logits(x.index_select(0, last_idx), gather=not local_logits)
         hook = self.layer_hook
         for li, L in enumerate(self.w["layers"]):
             if hook is not None:  # e.g. move the rest of a prefill to another (CU-masked) stream
@@ -341,54 +317,11 @@ class LlamaDecoder:
             x = self._attn_out_and_mlp(L, a, x)
         return self._logits(x.index_select(0, last_idx), gather=not local_logits)
 
-    def _prefill_norms_fusable(self, T: int) -> bool:
-        c = self.cfg
-        return (_PREFILL_NORM_FUSE and self.tp.size == 1 and self.unit_gains and c.hidden % 256 == 0
-                and self.ops.prefill_norm_fusable(T, c.hidden))
-
-    def _prefill_fused_norms(self, x, pos, slot_tok, cu, max_seqlen, prefix):
-        """Prefill with every RMSNorm after the first folded into the projections (csrc/gemm.hip
-        da_gemm8p_norm; gains already folded into the weights): the O / down projections (EPI_RESID)
-        also write the new residual rows' per-64-column sums of squares, and the next QKV (+ RoPE +
-        KV write) / gate-up (SwiGLU) projection reads the raw residual stream and scales its output
-        rows by rsqrt(mean square + eps) — no separate norm pass over x (2 per layer)."""
-        c, o, cache = self.cfg, self.ops, self.cache
-        D, hl, kl = c.head_dim, self.hl, self.kl
-        T, Hd = x.shape
-        parts = Hd // 64
-        ssq_attn = torch.empty(parts * T, dtype=torch.float32, device=x.device)
-        ssq_mlp = torch.empty_like(ssq_attn)
-        hook = self.layer_hook
-        for li, L in enumerate(self.w["layers"]):
-            if hook is not None:
-                hook(li)
-            rope = (pos, self.cos_sin, hl, kl, D, slot_tok, cache.k(li), cache.v(li))
-            if li == 0:
-                h = o.rmsnorm(x, L["ln_attn"], c.eps)
-                qkv = o.gemm_rope(h, L["wqkv"], pos, self.cos_sin, hl, kl, D, slot_tok, cache.k(li), cache.v(li))
-                del h
-            else:
-                qkv = o.gemm8p_norm(x, L["wqkv"], EPI_ROPE, norm_in=(ssq_attn, parts, c.eps), rope=rope)
-            pre = None if prefix is None else (cache.k(li)[prefix[0]], cache.v(li)[prefix[0]], prefix[1])
-            a = o.flash_attn_varlen(qkv[:, :hl * D], qkv[:, hl * D:(hl + kl) * D], qkv[:, (hl + kl) * D:], cu,
-                                    max_seqlen, hl, kl, D, causal=True, prefix=pre)
-            del qkv
-            o.gemm8p_norm(a, L["wo"], EPI_RESID, resid=x, out=x, ssq_out=ssq_mlp)
-            g = o.gemm8p_norm(x, L["w_gu"], EPI_SWIGLU, norm_in=(ssq_mlp, parts, c.eps))
-            o.gemm8p_norm(g, L["w_down"], EPI_RESID, resid=x, out=x, ssq_out=ssq_attn)
-            del a, g
-        if x.is_cuda:  # a layer hook may have moved the rest onto another stream: keep the sums alive there
-            for t in (ssq_attn, ssq_mlp):
-                t.record_stream(torch.cuda.current_stream())
-        return x
-
     # ------------------------------------------------------------- decode (graph-capturable)
     def decode_step(self, st: "DecodeState") -> torch.Tensor:
         c, o, cache = self.cfg, self.ops, self.cache
         D, hl, kl = c.head_dim, self.hl, self.kl
         x = o.embed(st.tokens, self.w["embed"], out=st.x)
-        if self._b1_decode(x.shape[0]):
-            return self._decode_step_b1(st, x)
         if self._dk_decode(x.shape[0]):
             return self._decode_step_dk(st, x)
         if self._norm_fusable(x.shape[0]):
@@ -396,18 +329,12 @@ class LlamaDecoder:
         if self.tp.size > 1 and x.shape[0] > 1:
             return self._decode_step_tp_fused_norms(st, x)
         fuse = o.gemv_fusable(x.shape[0], self.w["layers"][0]["wqkv"].shape[0], x.shape[1])
-        omerge = self._o_merge(x.shape[0])
         for li, L in enumerate(self.w["layers"]):
             if fuse:  # batch 1: RMSNorm folded into the QKV GEMV (no separate norm launch)
                 qkv = o.gemm(x, L["wqkv"], out=st.qkv, rms=(self._gain(L["ln_attn"]), c.eps))
             else:
                 h = o.rmsnorm(x, L["ln_attn"], c.eps, out=st.h)
                 qkv = o.gemm(h, L["wqkv"], out=st.qkv)
-            if omerge:  # batch 1: attention -> split partials; the O GEMV merges them on its input load
-                parts = self._decode_attn(qkv, li, st, parts=True)
-                o.gemv_omerge(parts, L["wo"], resid=x, out=x, attn_out=st.attn)
-                self._mlp(L, x)
-                continue
             a = self._decode_attn(qkv, li, st)
             self._attn_out_and_mlp(L, a, x)
         logits = self._logits(x, gather=False, out=st.logits)  # straight into the state (no copy launch)
@@ -417,67 +344,18 @@ class LlamaDecoder:
                     active=st.active, ctr=st.pos, pos=st.pos, lens=st.lens, hist=st.hist, start=st.start, eos=st.eos)
         return st.tokens
 
-    def _decode_attn(self, qkv, li: int, st: "DecodeState", parts: bool = False):
+    def _decode_attn(self, qkv, li: int, st: "DecodeState"):
         """RoPE + new-token cache write + decode attention. MHA (Phi-3): one launch — the attention
         kernel rotates q / the new k itself and writes the new k / v to the cache; GQA: rope_cache,
-        then the MFMA decode kernel. parts=True (batch 1, _o_merge): the launch stops at the split
-        partials (ops.decode_attn_parts) for gemv_omerge."""
+        then the MFMA decode kernel."""
         c, o, cache = self.cfg, self.ops, self.cache
         D, hl, kl = c.head_dim, self.hl, self.kl
-        fn = o.decode_attn_parts if parts else o.decode_attn
-        kw = {} if parts else {"out": st.attn}
         if hl == kl and _FUSED_ROPE_DECODE:
-            return fn(qkv, cache.k(li), cache.v(li), st.lens, st.slot, hl, kl, D, max_len=cache.max_seq,
-                      pre=st.pre, rope=(self.cos_sin, st.pos), **kw)
+            return o.decode_attn(qkv, cache.k(li), cache.v(li), st.lens, st.slot, hl, kl, D, max_len=cache.max_seq,
+                                 pre=st.pre, rope=(self.cos_sin, st.pos), out=st.attn)
         o.rope_cache(qkv, st.pos, self.cos_sin, hl, kl, D, slot=st.slot, k_cache=cache.k(li), v_cache=cache.v(li))
-        return fn(qkv, cache.k(li), cache.v(li), st.lens, st.slot, hl, kl, D, max_len=cache.max_seq, pre=st.pre, **kw)
-
-    def _o_merge(self, B: int) -> bool:
-        """Batch 1, one rank, the O projection a GEMV over the whole attention row, the launch split
-        (>= 2 splits at the cache capacity): attention partials merged by the O projection."""
-        c, o = self.cfg, self.ops
-        K = self.hl * c.head_dim
-        return (_O_MERGE and B == 1 and self.tp.size == 1 and hasattr(o, "gemv_omerge") and self.cache is not None
-                and K == c.hidden and K % 512 == 0 and K <= 4096 and c.head_dim % 8 == 0
-                and 2 <= o.decode_parts_splits(self.kl, self.cache.max_seq) <= 16)
-
-    def _b1_decode(self, B: int) -> bool:
-        """Batch 1, one rank, MHA (the fused-RoPE attention), folded norm gains, the Phi-3-mini
-        widths the launch is instantiated for: the persistent launch (every layer + the LM head;
-        decode_b1.hip)."""
-        c, o = self.cfg, self.ops
-        return (_DECODE_B1 and B == 1 and self.tp.size == 1 and self.unit_gains and self.hl == self.kl
-                and _FUSED_ROPE_DECODE and hasattr(o, "decode_b1") and c.head_dim in (64, 96, 128)
-                and c.hidden == 3072 and c.ffn == 8192 and c.vocab % 16 == 0  # the instantiated shape
-                and self.hl * c.head_dim == c.hidden and self.cache is not None)
-
-    def _b1_table(self) -> torch.Tensor:
-        """int64 [layers, 6] device table of the per-layer pointers the persistent launch reads
-        (weights never move; rebuilt if the KV cache is re-allocated)."""
-        cache = self.cache
-        key = cache.buf.data_ptr()
-        t = getattr(self, "_b1_ptrs", None)
-        if t is None or self._b1_key != key:
-            rows = [[L["wqkv"].data_ptr(), L["wo"].data_ptr(), L["w_gu"].data_ptr(), L["w_down"].data_ptr(),
-                     cache.k(li).data_ptr(), cache.v(li).data_ptr()] for li, L in enumerate(self.w["layers"])]
-            for L in self.w["layers"]:
-                for k in ("wqkv", "wo", "w_gu", "w_down"):
-                    if not L[k].is_contiguous():
-                        raise ValueError(f"decode_b1: {k} must be contiguous")
-            self._b1_ptrs = torch.tensor(rows, dtype=torch.int64, device=self.device)
-            self._b1_key = key
-        return self._b1_ptrs
-
-    def _decode_step_b1(self, st: "DecodeState", x: torch.Tensor) -> torch.Tensor:
-        """The whole batch-1 step in 3 launches: embedding, the persistent layers + LM head, the
-        sampler (was 5 per layer + 3)."""
-        c, o, cache = self.cfg, self.ops, self.cache
-        o.decode_b1(self._b1_table(), 0, c.layers, st.x.view(-1), st.qkv.view(-1), st.attn.view(-1), st.act.view(-1),
-                    st.lens, st.slot, st.pre, st.pos, self.cos_sin, self.hl, c.head_dim, c.ffn, cache.max_seq, c.eps,
-                    lm_head=self.w["lm_head"], logits=st.logits.view(-1))
-        o.sample(st.logits, st.temperature, st.seed, 0, out_tok=st.tokens, out_lp=st.lp, conf=st.conf,
-                 active=st.active, ctr=st.pos, pos=st.pos, lens=st.lens, hist=st.hist, start=st.start, eos=st.eos)
-        return st.tokens
+        return o.decode_attn(qkv, cache.k(li), cache.v(li), st.lens, st.slot, hl, kl, D, max_len=cache.max_seq,
+                             pre=st.pre, out=st.attn)
 
     def _norm_fusable(self, B: int) -> bool:
         """Batched decode (1 < B <= 64, no TP): every RMSNorm rides on the split-K reduction of the
@@ -497,15 +375,6 @@ class LlamaDecoder:
                   (self.w["lm_head"], EPI_NONE)]
         return all(f(B, w.shape[0], w.shape[1], e) for w, e in shapes) and o.dk_parts(c.hidden, B) <= 512
 
-    def _qkv_fold(self, B: int) -> bool:
-        """The QKV projection on the split-K route and MHA with the fused-RoPE attention (past the
-        small-batch prefetch variants, which read a bf16 row): its reduce runs in the attention's
-        prologue (_QKV_FOLD)."""
-        o = self.ops
-        w = self.w["layers"][0]["wqkv"]
-        return (_QKV_FOLD and hasattr(o, "gemm_dk_qkv_parts") and self.hl == self.kl and _FUSED_ROPE_DECODE
-                and o.qkv_parts_route(B, w.shape[0], w.shape[1]) and B * self.kl > 32)
-
     def _decode_step_dk(self, st: "DecodeState", x: torch.Tensor) -> torch.Tensor:
         """A layer = QKV, attention, O (+ residual, row sums of squares), gate/up + SwiGLU (norm
         deferred from those sums), down (+ residual, sums): 5 launches, no reduce launches, no
@@ -515,12 +384,8 @@ class LlamaDecoder:
         sa, sb = st.ssq
         parts = o.dk_parts(c.hidden, x.shape[0])
         a_in, norm = o.rmsnorm(x, layers[0]["ln_attn"], c.eps, out=st.h), None
-        fold = self._qkv_fold(x.shape[0])
         for li, L in enumerate(layers):
-            if fold:  # the split-K partials go straight to the attention (no reduce launch)
-                qkv = o.gemm_dk_qkv_parts(a_in, L["wqkv"], norm_in=norm)
-            else:
-                qkv = o.gemm_dk(a_in, L["wqkv"], out=st.qkv, norm_in=norm)
+            qkv = o.gemm_dk(a_in, L["wqkv"], out=st.qkv, norm_in=norm)
             a = self._decode_attn(qkv, li, st)
             o.gemm_dk(a, L["wo"], epi=EPI_RESID, resid=x, out=x, ssq_out=sa)               # x += o
             g = o.gemm_dk(x, L["w_gu"], epi=EPI_SWIGLU, norm_in=(sa, parts, c.eps))        # norm(x) -> gate/up
@@ -608,7 +473,6 @@ class DecodeState:
         self.h = torch.zeros(B, h, dtype=torch.bfloat16, device=dev)
         self.qkv = torch.zeros(B, (model.hl + 2 * model.kl) * c.head_dim, dtype=torch.bfloat16, device=dev)
         self.attn = torch.zeros(B, model.hl * c.head_dim, dtype=torch.bfloat16, device=dev)
-        self.act = torch.zeros(B, c.ffn, dtype=torch.bfloat16, device=dev)  # SwiGLU output (persistent batch-1 path)
         self.logits = torch.zeros(B, c.vocab // model.tp.size, dtype=torch.bfloat16, device=dev)  # this rank's slice
         # gemm_dk deferred-norm partial sums [parts, 64] (a tuple: shared as-is by row views)
         self.ssq = tuple(torch.zeros(512 * 64, dtype=torch.float32, device=dev) for _ in range(2))

@@ -126,8 +126,8 @@ def textlib():
         L = ctypes.CDLL(str(binary("libda_text.so")))
         L.da_word_offsets.argtypes = [ctypes.c_char_p, ctypes.c_long, ctypes.c_void_p, ctypes.c_long]
         L.da_word_offsets.restype = ctypes.c_long
-        L.da_chunk.argtypes = [ctypes.c_char_p, ctypes.c_void_p, ctypes.c_long, ctypes.c_long, ctypes.c_long,
-                               ctypes.c_void_p, ctypes.c_long, ctypes.c_void_p, ctypes.c_long]
+        L.da_chunk.argtypes = [ctypes.c_char_p, ctypes.c_long, ctypes.c_void_p, ctypes.c_long, ctypes.c_long,
+                               ctypes.c_long, ctypes.c_void_p, ctypes.c_long, ctypes.c_void_p, ctypes.c_long]
         L.da_chunk.restype = ctypes.c_long
         _TEXT = L
     return _TEXT

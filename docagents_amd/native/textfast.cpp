@@ -33,7 +33,7 @@ long da_word_offsets(const char* s, long n, int64_t* words, long cap) {
 // Builds all chunk texts (words joined by one space) into `out` (capacity out_cap bytes) and
 // writes per chunk [byte_off, byte_len, token_count] into `meta` (3 int64 per chunk).
 // Returns the number of chunks, -1 if out/meta are too small, -2 on malformed word spans.
-long da_chunk(const char* s, const int64_t* words, long nw, long max_tokens, long overlap, char* out,
+long da_chunk(const char* s, long n, const int64_t* words, long nw, long max_tokens, long overlap, char* out,
               long out_cap, int64_t* meta, long meta_cap) {
   if (max_tokens <= 0) max_tokens = 400;
   if (overlap < 0) overlap = 0;
@@ -48,7 +48,8 @@ long da_chunk(const char* s, const int64_t* words, long nw, long max_tokens, lon
     long off = o;
     for (long k = start; k < end; ++k) {
       long len = words[2 * k + 1] - words[2 * k];
-      if (len < 0 || words[2 * k] < 0) return -2;  // not spans from da_word_offsets
+      // not spans of s from da_word_offsets (negative, reversed or past the n input bytes)
+      if (len < 0 || words[2 * k] < 0 || words[2 * k + 1] > n) return -2;
       if (len > out_cap - o - 1) return -1;
       if (k > start) out[o++] = ' ';
       memcpy(out + o, s + words[2 * k], (size_t)len);

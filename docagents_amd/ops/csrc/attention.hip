@@ -759,9 +759,7 @@ flash_attn_pipe_kernel(const bf16_t* __restrict__ q, const bf16_t* __restrict__ 
 // capacity, max_len), but a row holds L <= max_len keys: balanced splits (the default) spread the
 // row's L keys over ALL its splits (64-key multiples) instead of filling the first ceil(L / chunk)
 // and leaving the rest idle — at batch 1 and 2.9k of 4k keys, 256 working workgroups instead of 192.
-// chunk_arg < 0 (da_set_decode_balance(0), A/B): fixed -chunk_arg keys per split.
 __device__ __forceinline__ int dec_chunk(int L, int nsplit, int chunk_arg) {
-  if (chunk_arg < 0) return -chunk_arg;
   const int c = ((L + nsplit - 1) / nsplit + 63) & ~63;
   return c < chunk_arg ? c : chunk_arg;
 }
@@ -844,19 +842,10 @@ struct DecRope {
   bf16_t* vc;
   const float* cs;      // [max_pos][D/2][2] (cos, sin)
   const int* pos;       // [B]
-  unsigned long long* trace;  // VAR bit 3 only: per-workgroup wall-clock stamps (bench/decode_trace.py)
-  // QKV projection folded in (qp != null; MHA, no-prefetch path): row b's qkv element col is read
-  // from the projection's split-K partials instead of its reduced bf16 row —
-  // bf16((0 + p_0 + ... + p_{S-1}) * inv_b), inv_b = rsqrt(sum_q ssq[q][b] / norm_k + eps) (1 without
-  // ssq): the arithmetic of gemm.hip gemm_splitk_reduce (epilogue NONE, no bias), so the same bits
-  // as the reduce launch it replaces
-  const float* qp; const float* qp_ssq;
-  int qp_splits, qp_M, qp_N, qp_parts, qp_normk;
-  float qp_eps;
 };
 
 template <int D, int G, int VAR>
-__global__ void __launch_bounds__((VAR & 32) ? 512 : 256)
+__global__ void __launch_bounds__(256)
 decode_attn_kernel(const bf16_t* __restrict__ q, int ldq, const bf16_t* __restrict__ kc,
                    const bf16_t* __restrict__ vc, const int* __restrict__ lens, const int* __restrict__ slot,
                    const int* __restrict__ pre,
@@ -868,9 +857,9 @@ decode_attn_kernel(const bf16_t* __restrict__ q, int ldq, const bf16_t* __restri
   constexpr int GCD = (CPR % 16 == 0) ? 16 : ((CPR % 8 == 0) ? 8 : ((CPR % 4 == 0) ? 4 : 2));
   constexpr int NSET = CPR / GCD;                  // distinct dim-slots per lane
   constexpr bool SHFL = (64 % CPR) == 0;           // a key's chunks live in one wave-instruction
-  // VAR bit 5: 8 waves per workgroup (batch 1: a split's tiles all in flight at once, one per wave,
-  // instead of two back to back on each of 4 waves); else 4
-  constexpr int NWV = (VAR & 32) ? 8 : 4, NTH = 64 * NWV;
+  // 4 waves per workgroup (8, a split's tiles all in flight at once at batch 1, measured 2x slower:
+  // profiles/r4/rejected_r4.txt)
+  constexpr int NWV = 4, NTH = 64 * NWV;
   __shared__ float sq[G][D];
   __shared__ float sp[NWV][G][KT];
   __shared__ float spart[SHFL ? 1 : NWV][SHFL ? 1 : G * KT * CPR];
@@ -879,15 +868,6 @@ decode_attn_kernel(const bf16_t* __restrict__ q, int ldq, const bf16_t* __restri
   __shared__ float swm[NWV][G], swl[NWV][G];
 
   const int split = blockIdx.x, hk = blockIdx.y, b = blockIdx.z;
-  constexpr bool TRACE = (VAR & 8) != 0;
-  unsigned long long* const trw =
-      TRACE ? rope.trace + ((size_t)(b * gridDim.y + hk) * gridDim.x + split) * 16 : nullptr;
-  auto stamp = [&](int k) {
-    if constexpr (TRACE) {
-      if (threadIdx.x == 0) trw[k] = wall_clock64();
-    }
-  };
-  stamp(0);
   const int L = lens[b];
   DA_ASSERT(L >= 0 && L <= max_seq && slot[b] >= 0);
   const int chunk = dec_chunk(L, nsplit, chunk_max);
@@ -952,20 +932,6 @@ decode_attn_kernel(const bf16_t* __restrict__ q, int ldq, const bf16_t* __restri
     return rot2(bf2f(hp[d & ~1]), bf2f(hp[d | 1]), rope.cs[((size_t)p * HALF + i) * 2],
                 rope.cs[((size_t)p * HALF + i) * 2 + 1], d);
   };
-  // element col of row b's qkv row: the bf16 row, or rebuilt from the QKV split-K partials
-  float qinv = 1.f;
-  if (rope.qp != nullptr && rope.qp_ssq != nullptr)
-    qinv = rsqrtf(sum_strided(rope.qp_ssq + b, rope.qp_parts, 64) / rope.qp_normk + rope.qp_eps);
-  auto qel = [&](int col) -> bf16_t {
-    if (rope.qp == nullptr) return q[(size_t)b * ldq + col];
-    const float v = sum_strided(rope.qp + (size_t)b * rope.qp_N + col, rope.qp_splits, (size_t)rope.qp_M * rope.qp_N);
-    return f2bf(v * qinv);
-  };
-  auto rotc = [&](int col0, int d, int p) -> float {
-    const int i = d >> 1;
-    return rot2(bf2f(qel(col0 + (d & ~1))), bf2f(qel(col0 + (d | 1))), rope.cs[((size_t)p * HALF + i) * 2],
-                rope.cs[((size_t)p * HALF + i) * 2 + 1], d);
-  };
   // PFT (small batches): the prologue's operands (this thread's q element, its RoPE partner and
   // cos / sin, the new token's k / v element) are loaded FIRST, then the first two K/V tiles of the
   // wave are requested, unconditionally (an empty tile reads one line), so the compiler's counted
@@ -984,9 +950,6 @@ decode_attn_kernel(const bf16_t* __restrict__ q, int ldq, const bf16_t* __restri
     const bf16_t* kr = fr ? q + (size_t)b * ldq + (size_t)(H + hk) * D : hp;
     const bf16_t* vr = fr ? q + (size_t)b * ldq + (size_t)(H + Hkv + hk) * D : hp;
     const bf16_t rk1 = kr[d & ~1], rk2 = kr[d | 1], nv = vr[d];
-    // VAR bit 4: the prologue operands land BEFORE this workgroup's K/V requests join the chip-wide
-    // flood (otherwise they queue behind other workgroups' tiles: 3.6 us at batch 1, decode_trace)
-    if constexpr ((VAR & 16) != 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const int t0 = kstart + w * KT, t1 = t0 + NWV * KT;
     load_k(ka, t0); load_v(va, t0);
     load_k(kb2, t1); load_v(vb2, t1);
@@ -1012,44 +975,26 @@ decode_attn_kernel(const bf16_t* __restrict__ q, int ldq, const bf16_t* __restri
     }
     for (int i = tid; i < G * D; i += NTH) {
       const int g = i / D, d = i % D;
-      if (rope.qp == nullptr) {
-        const bf16_t* hp = q + (size_t)b * ldq + (hk * G + g) * D;
-        sq[g][d] = (fr ? rot(hp, d, L - 1) : bf2f(hp[d])) * scale_log2e;
-      } else {
-        const int col0 = (hk * G + g) * D;
-        sq[g][d] = (fr ? rotc(col0, d, L - 1) : bf2f(qel(col0 + d))) * scale_log2e;
-      }
+      const bf16_t* hp = q + (size_t)b * ldq + (hk * G + g) * D;
+      sq[g][d] = (fr ? rot(hp, d, L - 1) : bf2f(hp[d])) * scale_log2e;
     }
   }
   if (own_new && !PRE) {
     const size_t crow = cbase + (size_t)(L - 1) * D;
-    if (rope.qp == nullptr) {
-      const bf16_t* kr = q + (size_t)b * ldq + (size_t)(H + hk) * D;
-      const bf16_t* vr = q + (size_t)b * ldq + (size_t)(H + Hkv + hk) * D;
-      for (int d = tid; d < D; d += NTH) {
-        const float kv = rot(kr, d, L - 1);
-        skn[d] = kv;
-        svn[d] = bf2f(vr[d]);
-        rope.kc[crow + d] = f2bf(kv);  // for later steps (read back only after this launch)
-        rope.vc[crow + d] = vr[d];
-      }
-    } else {
-      const int kcol = (H + hk) * D, vcol = (H + Hkv + hk) * D;
-      for (int d = tid; d < D; d += NTH) {
-        const float kv = rotc(kcol, d, L - 1);
-        const bf16_t nv = qel(vcol + d);
-        skn[d] = kv;
-        svn[d] = bf2f(nv);
-        rope.kc[crow + d] = f2bf(kv);
-        rope.vc[crow + d] = nv;
-      }
+    const bf16_t* kr = q + (size_t)b * ldq + (size_t)(H + hk) * D;
+    const bf16_t* vr = q + (size_t)b * ldq + (size_t)(H + Hkv + hk) * D;
+    for (int d = tid; d < D; d += NTH) {
+      const float kv = rot(kr, d, L - 1);
+      skn[d] = kv;
+      svn[d] = bf2f(vr[d]);
+      rope.kc[crow + d] = f2bf(kv);  // for later steps (read back only after this launch)
+      rope.vc[crow + d] = vr[d];
     }
   }
   if constexpr (G > 1) {
     for (int i = tid; i < NWV * G * D; i += NTH) (&so[0][0][0])[i] = 0.f;
   }
   __syncthreads();
-  stamp(1);
   if (own_new && w == 0) {  // score of the new key for each query head of this kv head
 #pragma unroll
     for (int g = 0; g < G; ++g) {
@@ -1157,7 +1102,6 @@ decode_attn_kernel(const bf16_t* __restrict__ q, int ldq, const bf16_t* __restri
     while (t0 < kend) {
       const int t1 = t0 + NWV * KT;
       process(ka, va, t0);
-      if (t0 == kstart + w * KT) stamp(7);
       if (t1 >= kend) break;
       const int t2 = t1 + NWV * KT;
       if (t2 < kend) { load_k(ka, t2); load_v(va, t2); }
@@ -1174,10 +1118,6 @@ decode_attn_kernel(const bf16_t* __restrict__ q, int ldq, const bf16_t* __restri
       if constexpr (VEARLY) load_v(vv, t0);
       process(kv, vv, t0);
     }
-  }
-  stamp(2);
-  if constexpr (TRACE) {
-    if (lane == 0) trw[8 + w] = wall_clock64();
   }
   // ---- merge lanes -> per-wave O, then waves -> block partial ----
   // MHA (G = 1): every lane parks its accumulators in LDS with plain 16-B stores and the output
@@ -1205,7 +1145,6 @@ decode_attn_kernel(const bf16_t* __restrict__ q, int ldq, const bf16_t* __restri
     for (int g = 0; g < G; ++g) { swm[w][g] = m[g]; swl[w][g] = l[g]; }
   }
   __syncthreads();
-  stamp(12);
   for (int i = tid; i < G * D; i += NTH) {
     const int g = i / D, d = i % D;
     float M = fmaxf(fmaxf(swm[0][g], swm[1][g]), fmaxf(swm[2][g], swm[3][g]));
@@ -1245,17 +1184,8 @@ decode_attn_kernel(const bf16_t* __restrict__ q, int ldq, const bf16_t* __restri
     }
     dec_store(o, M, ls, b, hk * G + g, d, H, nsplit, split, D, po, pm, pl, out, ldo);
   }
-  stamp(3);
   __shared__ int s_last;
   dec_finish<D, G>(po, pm, pl, H, Hkv, nsplit, b, hk, cnt, out, ldo, &s_last);
-  if constexpr (TRACE) {
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      unsigned xcc;
-      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-      trw[4] = wall_clock64(); trw[5] = s_last; trw[6] = __smid() | ((unsigned long long)(xcc & 15) << 32);
-    }
-  }
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1450,7 +1380,7 @@ static int launch_decode_v(int G, dim3 grid, hipStream_t s, const bf16_t* q, int
                            const bf16_t* vc, const int* lens, const int* slot, const int* pre, int H, int Hkv, int max_seq, int chunk,
                            int nsplit, float sl2e, float* po, float* pm, float* pl, bf16_t* out, int ldo,
                            int* cnt, DecRope rope) {
-#define DEC(GG) decode_attn_kernel<D, GG, VAR><<<grid, (VAR & 32) ? 512 : 256, 0, s>>>(q, ldq, kc, vc, lens, slot, pre, H, Hkv, max_seq, \
+#define DEC(GG) decode_attn_kernel<D, GG, VAR><<<grid, 256, 0, s>>>(q, ldq, kc, vc, lens, slot, pre, H, Hkv, max_seq, \
                                                                      chunk, nsplit, sl2e, po, pm, pl, out, ldo, cnt, rope)
   switch (G) {
     case 1: DEC(1); break;
@@ -1464,72 +1394,34 @@ static int launch_decode_v(int G, dim3 grid, hipStream_t s, const bf16_t* q, int
 }
 
 // GQA groups (G >= 2) take the MFMA kernel: 1.8x (Llama-3-8B, G=4) to 5x (Llama-3-70B TP=8, G=8)
-// over the VALU path (profiles/decode_attn_gqa_mfma_r1.json). da_set_gqa_mfma(0) selects the VALU
-// path (kept for A/B measurements and as the numerics cross-check in tests).
-static int g_dec_qfirst = 0;  // prefetch variant: prologue operands before the K/V stream (A/B)
-DA_EXPORT void da_set_decode_qfirst(int v) { g_dec_qfirst = v; }
-static int g_dec_balance = 1;  // balanced splits (dec_chunk); 0 = fixed chunk per split (A/B)
-DA_EXPORT void da_set_decode_balance(int v) { g_dec_balance = v; }
-static int g_gqa_mfma = 1;
-DA_EXPORT void da_set_gqa_mfma(int v) { g_gqa_mfma = v; }
-// MHA decode with the next tile prefetched (VAR bit 2) when B * Hkv <= this (0 = never).
-static int g_dec_pft = 32;
-DA_EXPORT void da_set_decode_pft(int v) { g_dec_pft = v; }
-// ... and with 8 waves per workgroup (VAR bit 5) when B * Hkv <= this (0 = never; A/B)
-static int g_dec_w8 = 0;  // measured 2x slower (profiles/r4/rejected_r4.txt): A/B only
-DA_EXPORT void da_set_decode_w8(int v) { g_dec_w8 = v; }
-// ... which 8-wave variant: 0 = two tiles in flight per wave (VAR 39: 256 VGPRs, spills), 1 = one
-// tile per wave, no prefetch (VAR 35: the 8 waves hold a split's tiles at once without spilling)
-static int g_dec_w8_var = 0;
-DA_EXPORT void da_set_decode_w8_var(int v) { g_dec_w8_var = v; }
-// Timeline probe (bench/decode_trace.py): non-null -> the MHA D=96 prefetch variant writes 8 wall-clock
-// stamps per workgroup here ([B][Hkv][nsplit][8]: start, prologue done, first tile done, tiles done,
-// partial stored, finished, last-split flag, CU id).
-static unsigned long long* g_dec_trace = nullptr;
-DA_EXPORT void da_set_decode_trace(void* p) { g_dec_trace = (unsigned long long*)p; }
-
+// over the VALU path (profiles/decode_attn_gqa_mfma_r1.json); the VALU kernel covers the other
+// head dims. MHA (G = 1) decode prefetches each wave's next tile (VAR bit 2) when the launch has
+// few (row, kv head) pairs (B * Hkv <= 32: latency-bound), else streams with V issued with K.
+//
 // Measured on MI355X (profiles/decode_attn_variants_r1.json): non-temporal K/V loads + V issued with
 // K reach 6.5 TB/s for MHA (G = 1, Phi-3); with G >= 2 the extra V registers cost more occupancy
 // than they buy, so those keep V after the scores (nt loads only).
+constexpr int kDecPrefetchPairs = 32;
+
 template <int D>
 static int launch_decode(int G, dim3 grid, hipStream_t s, const bf16_t* q, int ldq, const bf16_t* kc,
                          const bf16_t* vc, const int* lens, const int* slot, const int* pre, int H, int Hkv, int max_seq, int chunk,
                          int nsplit, float sl2e, float* po, float* pm, float* pl, bf16_t* out, int ldo,
                          int* cnt, DecRope rope) {
   if (G == 1) {
-    if constexpr (D == 96) {
-      if (g_dec_trace) {
-        DecRope r = rope;
-        r.trace = g_dec_trace;
-        return launch_decode_v<D, 15>(G, grid, s, q, ldq, kc, vc, lens, slot, pre, H, Hkv, max_seq, chunk, nsplit, sl2e, po, pm, pl, out, ldo, cnt, r);
-      }
-    }
-    if (g_dec_pft && (int)(grid.y * grid.z) <= g_dec_pft && g_dec_qfirst)
-      return launch_decode_v<D, 23>(G, grid, s, q, ldq, kc, vc, lens, slot, pre, H, Hkv, max_seq, chunk, nsplit, sl2e, po, pm, pl, out, ldo, cnt, rope);
-    if (g_dec_w8 && g_dec_pft && (int)(grid.y * grid.z) <= g_dec_w8) {  // MHA only (G = 1: LDS)
-      if (g_dec_w8_var == 1)
-        decode_attn_kernel<D, 1, 35><<<grid, 512, 0, s>>>(q, ldq, kc, vc, lens, slot, pre, H, Hkv, max_seq, chunk,
-                                                           nsplit, sl2e, po, pm, pl, out, ldo, cnt, rope);
-      else
-        decode_attn_kernel<D, 1, 39><<<grid, 512, 0, s>>>(q, ldq, kc, vc, lens, slot, pre, H, Hkv, max_seq, chunk,
-                                                           nsplit, sl2e, po, pm, pl, out, ldo, cnt, rope);
-      return (int)hipGetLastError();
-    }
-    if (g_dec_pft && (int)(grid.y * grid.z) <= g_dec_pft)  // few (row, kv head) pairs: latency-bound
+    if ((int)(grid.y * grid.z) <= kDecPrefetchPairs)
       return launch_decode_v<D, 7>(G, grid, s, q, ldq, kc, vc, lens, slot, pre, H, Hkv, max_seq, chunk, nsplit, sl2e, po, pm, pl, out, ldo, cnt, rope);
     return launch_decode_v<D, 3>(G, grid, s, q, ldq, kc, vc, lens, slot, pre, H, Hkv, max_seq, chunk, nsplit, sl2e, po, pm, pl, out, ldo, cnt, rope);
   }
   if (rope.cs) return (int)hipErrorInvalidValue;  // fused RoPE: MHA kernel only
   if constexpr (D == 64 || D == 128) {
-    if (g_gqa_mfma) {
-      switch (G) {
-        case 2: decode_attn_gqa_kernel<D, 2><<<grid, 256, 0, s>>>(q, ldq, kc, vc, lens, slot, pre, H, Hkv, max_seq, chunk, nsplit, sl2e, po, pm, pl, out, ldo, cnt); break;
-        case 4: decode_attn_gqa_kernel<D, 4><<<grid, 256, 0, s>>>(q, ldq, kc, vc, lens, slot, pre, H, Hkv, max_seq, chunk, nsplit, sl2e, po, pm, pl, out, ldo, cnt); break;
-        case 8: decode_attn_gqa_kernel<D, 8><<<grid, 256, 0, s>>>(q, ldq, kc, vc, lens, slot, pre, H, Hkv, max_seq, chunk, nsplit, sl2e, po, pm, pl, out, ldo, cnt); break;
-        default: return (int)hipErrorInvalidValue;
-      }
-      return (int)hipGetLastError();
+    switch (G) {
+      case 2: decode_attn_gqa_kernel<D, 2><<<grid, 256, 0, s>>>(q, ldq, kc, vc, lens, slot, pre, H, Hkv, max_seq, chunk, nsplit, sl2e, po, pm, pl, out, ldo, cnt); break;
+      case 4: decode_attn_gqa_kernel<D, 4><<<grid, 256, 0, s>>>(q, ldq, kc, vc, lens, slot, pre, H, Hkv, max_seq, chunk, nsplit, sl2e, po, pm, pl, out, ldo, cnt); break;
+      case 8: decode_attn_gqa_kernel<D, 8><<<grid, 256, 0, s>>>(q, ldq, kc, vc, lens, slot, pre, H, Hkv, max_seq, chunk, nsplit, sl2e, po, pm, pl, out, ldo, cnt); break;
+      default: return (int)hipErrorInvalidValue;
     }
+    return (int)hipGetLastError();
   }
   return launch_decode_v<D, 1>(G, grid, s, q, ldq, kc, vc, lens, slot, pre, H, Hkv, max_seq, chunk, nsplit, sl2e, po, pm, pl, out, ldo, cnt, rope);
 }
@@ -1552,27 +1444,17 @@ DA_EXPORT int da_malloc_uncached(long long bytes, void** out) {
 
 // cos_sin / pos (both null, or both set): fused RoPE + new-token KV-cache write (MHA only; q is
 // then the raw qkv row, see DecRope).
-struct QkvParts {  // the QKV projection's split-K partials (DecRope qp*): null ws = a bf16 qkv row
-  const float* ws; const float* ssq;
-  int splits, M, N, parts, normk;
-  float eps;
-};
-
 static int decode_attn_impl(const void* q, int ldq, const void* k_cache, const void* v_cache, const void* lens,
                             const void* slot, const void* pre, int B, int H, int Hkv, int D, int max_seq, int chunk,
                             int nsplit, float scale, void* ws, void* o, int ldo, void* counters, const void* cos_sin,
-                            const void* pos, bool merge, void* stream, QkvParts qp = QkvParts{}) {
+                            const void* pos, void* stream) {
   bf16_t* out = (bf16_t*)o;
   int* cnt = (int*)counters;
   if (H % Hkv || chunk % 64 || nsplit < 1 || (long)chunk * nsplit < 1) return (int)hipErrorInvalidValue;
-  if ((cos_sin == nullptr) != (pos == nullptr) ||
-      (cos_sin && (H != Hkv || (qp.ws ? qp.N : ldq) < (H + 2 * Hkv) * D)))
+  if ((cos_sin == nullptr) != (pos == nullptr) || (cos_sin && (H != Hkv || ldq < (H + 2 * Hkv) * D)))
     return (int)hipErrorInvalidValue;
-  DecRope rope{(bf16_t*)k_cache, (bf16_t*)v_cache, (const float*)cos_sin, (const int*)pos, nullptr};
-  rope.qp = qp.ws; rope.qp_ssq = qp.ssq; rope.qp_splits = qp.splits; rope.qp_M = qp.M; rope.qp_N = qp.N;
-  rope.qp_parts = qp.parts; rope.qp_normk = qp.normk; rope.qp_eps = qp.eps;
+  DecRope rope{(bf16_t*)k_cache, (bf16_t*)v_cache, (const float*)cos_sin, (const int*)pos};
   if (B == 0) return 0;
-  if (!g_dec_balance) chunk = -chunk;  // kernels: negative = fixed keys per split (dec_chunk)
   const int G = H / Hkv;
   float* po = (float*)ws;
   float* pm = po + (size_t)B * H * nsplit * D;
@@ -1594,7 +1476,7 @@ static int decode_attn_impl(const void* q, int ldq, const void* k_cache, const v
     default: return (int)hipErrorInvalidValue;
   }
   if (err) return err;
-  if (nsplit == 1 || cnt || !merge) return 0;
+  if (nsplit == 1 || cnt) return 0;
   dim3 cgrid(H, B);
   switch (D) {
     case 64: decode_combine_kernel<64><<<cgrid, 64, 0, s>>>(po, pm, pl, H, nsplit, (bf16_t*)o, ldo); break;
@@ -1609,50 +1491,13 @@ DA_EXPORT int da_decode_attn(const void* q, int ldq, const void* k_cache, const 
                              int nsplit, float scale, void* ws, void* o, int ldo, void* counters, const void* cos_sin,
                              const void* pos, void* stream) {
   return decode_attn_impl(q, ldq, k_cache, v_cache, lens, slot, pre, B, H, Hkv, D, max_seq, chunk, nsplit, scale, ws,
-                          o, ldo, counters, cos_sin, pos, true, stream);
+                          o, ldo, counters, cos_sin, pos, stream);
 }
 
-// The same launch with the split merge left to the consumer (nsplit >= 2): the kernel ends at the
-// splits' fp32 partial stores in ws (layout as above: po [B][H][nsplit][D], pm / pl [B][H][nsplit])
-// and the batch-1 O projection merges them on its input load (gemm.hip da_gemv_omerge). No arrival
-// ticket and no last-split merge on the attention's critical path; ws is ordinary (cached) memory —
-// the launch boundary orders the partials before their reader.
-DA_EXPORT int da_decode_attn_parts(const void* q, int ldq, const void* k_cache, const void* v_cache, const void* lens,
-                                   const void* slot, const void* pre, int B, int H, int Hkv, int D, int max_seq,
-                                   int chunk, int nsplit, float scale, void* ws, const void* cos_sin, const void* pos,
-                                   void* stream) {
-  if (nsplit < 2 || !ws) return (int)hipErrorInvalidValue;
-  return decode_attn_impl(q, ldq, k_cache, v_cache, lens, slot, pre, B, H, Hkv, D, max_seq, chunk, nsplit, scale, ws,
-                          nullptr, 0, nullptr, cos_sin, pos, false, stream);
-}
-
-// The same launch reading q and the new token's k / v from the QKV projection's split-K partials
-// (gemm.hip da_gemm_dk_splitk_parts: [splits][M][N] fp32, the deferred row norm from ssq [parts][64]
-// or none) instead of its reduced bf16 row: the 33..64-row decode's QKV reduce launch folded into
-// the attention's prologue, bit-identical. MHA with fused RoPE, B = M, and the no-prefetch variant
-// only (B * Hkv above the prefetch threshold).
-DA_EXPORT int da_decode_attn_qkvparts(const void* qkv_ws, int splits, int N, const void* ssq, int parts, int norm_k,
-                                      float eps, const void* k_cache, const void* v_cache, const void* lens,
-                                      const void* slot, const void* pre, int B, int H, int Hkv, int D, int max_seq,
-                                      int chunk, int nsplit, float scale, void* ws, void* o, int ldo, void* counters,
-                                      const void* cos_sin, const void* pos, void* stream) {
-  if (!qkv_ws || splits < 1 || !cos_sin || H != Hkv || B < 1 || B > 64) return (int)hipErrorInvalidValue;
-  if (ssq && (parts < 1 || norm_k < 1 || !(eps > 0.f))) return (int)hipErrorInvalidValue;
-  if ((g_dec_pft && B * Hkv <= g_dec_pft) || (g_dec_w8 && B * Hkv <= g_dec_w8))
-    return (int)hipErrorInvalidValue;  // the prefetch variants read q directly
-  if (g_dec_trace) return (int)hipErrorInvalidValue;
-  const QkvParts qp{(const float*)qkv_ws, (const float*)ssq, splits, B, N, ssq ? parts : 0, norm_k, eps};
-  return decode_attn_impl(nullptr, 0, k_cache, v_cache, lens, slot, pre, B, H, Hkv, D, max_seq, chunk, nsplit, scale,
-                          ws, o, ldo, counters, cos_sin, pos, true, stream, qp);
-}
-
-// Waves per workgroup: 0 = auto (4; 8 at D = 128), 4 / 8 force a shape (A/B runs). Round 1 picked 8
-// for bidirectional encoders; with the buffer-loaded K/V tiles 4 waves are faster there too.
-static int g_fa_waves = 0;
-DA_EXPORT void da_set_flash_waves(int nw) { g_fa_waves = nw; }
-// causal flash: longest query blocks first (1, default) or grid order (0); A/B runs
-static int g_fa_rev = 3;  // bit 0: causal longest-first; bit 1: XCD-grouped pairs (fa_block)
-DA_EXPORT void da_set_flash_rev(int v) { g_fa_rev = v & 3; }
+// Dispatch order of the flash kernels (FaPrefix::rev, fa_block): causal longest query blocks first
+// and the query blocks of one (sequence, kv head) pair on one XCD (737 -> 778 TF/s on the Phi-3 QA
+// chunk, profiles/r4/flash_order/).
+constexpr int kFaDispatch = 3;
 
 // fp16 (the encoder's DTYPE=fp16): bidirectional or causal, no shared prefix, 4 waves x 32 queries
 DA_EXPORT int da_flash_attn_f16(const void* q, const void* k, const void* v, int ldq, int ldk, int ldv,
@@ -1660,7 +1505,7 @@ DA_EXPORT int da_flash_attn_f16(const void* q, const void* k, const void* v, int
                                 float scale, void* o, int ldo, void* stream) {
   if (H % Hkv || ldq % 8 || ldk % 8 || ldv % 8 || ldo % 4) return (int)hipErrorInvalidValue;
   if (B == 0 || max_seqlen == 0) return 0;
-  const FaPrefix pre{nullptr, nullptr, 0, 0, g_fa_rev};
+  const FaPrefix pre{nullptr, nullptr, 0, 0, kFaDispatch};
   dim3 grid((max_seqlen + 127) / 128, H, B);
   hipStream_t s = (hipStream_t)stream;
 #define FA_ARGS16 (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, ldq, ldk, ldv, (const int*)cu_seqlens, H, Hkv, \
@@ -1707,51 +1552,31 @@ static int launch_fa2(const void* q, const void* k, const void* v, int ldq, int 
   return (int)hipGetLastError();
 }
 
-// queries per wave: 0 = auto, 1 = 32 (round-1 shape), 2 = 64 (A/B runs)
-static int g_fa_qh = 0;
-DA_EXPORT void da_set_flash_qh(int v) { g_fa_qh = v; }
-// software-pipelined kernel (flash_attn_pipe, D <= 96, 4 waves x 32 queries): 0 = off, 1 = on,
-// 2 = auto: causal D = 96 (Phi-3 prefill 576 -> 656 TF/s; the short bidirectional BGE sequences,
-// 8 tiles, lose to its longer pipeline fill: 617 -> 531 at D = 64, profiles/r2/attn_bench_v5.txt);
-// 3 = on with the speculative softmax (SPEC: Phi-3 prefill 654 -> 689 TF/s,
-// profiles/r3/attn_bench_spec.txt); 4 = SPEC with LDS-DMA K / V tiles (D = 96, prefix % 64 == 0,
-// else 3); auto = 4 for causal D = 96
-static int g_fa_pipe = 2;
-DA_EXPORT void da_set_flash_pipe(int v) { g_fa_pipe = v; }
-
+// Causal D = 96 (the Phi-3 prefill) runs the software-pipelined kernel (flash_attn_pipe: 576 -> 656
+// TF/s; the short bidirectional BGE sequences, 8 tiles, lose to its longer pipeline fill, 617 -> 531
+// at D = 64, profiles/r2/attn_bench_v5.txt) with the speculative softmax (654 -> 689 TF/s,
+// profiles/r3/attn_bench_spec.txt) and LDS-DMA K / V tiles when the prefix is whole 64-key tiles and
+// the operands 16-B aligned (711 TF/s); every other shape the 4-wave flash_attn_v2_kernel (8 waves
+// at D = 128: Llama-3 prefill, profiles/r2/attn_bench_v4.txt).
 template <int D, bool DMA>
 static constexpr int fa_pipe_smem() {
   return 3 * ((DMA ? 64 * D * 2 : FA2Cfg<D, 4, 1>::KBUF) + FA2Cfg<D, 4, 1>::VBUF);
 }
 
-template <bool SPEC, bool DMA>
+template <bool DMA>
 static int launch_fa_pipe(const void* q, const void* k, const void* v, int ldq, int ldk, int ldv, const void* cu_seqlens,
-                          int B, int max_seqlen, int H, int Hkv, int D, int causal, float sl2e, void* o, int ldo,
+                          int B, int max_seqlen, int H, int Hkv, int causal, float sl2e, void* o, int ldo,
                           FaPrefix pre, hipStream_t s) {
   static bool attr_set = false;
   if (!attr_set) {
-    (void)hipFuncSetAttribute((const void*)flash_attn_pipe_kernel<96, SPEC, DMA>,
+    (void)hipFuncSetAttribute((const void*)flash_attn_pipe_kernel<96, true, DMA>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, fa_pipe_smem<96, DMA>());
-    if constexpr (!DMA)
-      (void)hipFuncSetAttribute((const void*)flash_attn_pipe_kernel<64, SPEC, false>,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, fa_pipe_smem<64, false>());
     attr_set = true;
   }
   dim3 grid((max_seqlen + 127) / 128, H, B);
-#define FA_ARGS (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, ldq, ldk, ldv, (const int*)cu_seqlens, H, Hkv, \
-                causal, sl2e, (bf16_t*)o, ldo, pre
-  if constexpr (DMA) {
-    if (D != 96) return (int)hipErrorInvalidValue;
-    flash_attn_pipe_kernel<96, SPEC, true><<<grid, 256, fa_pipe_smem<96, true>(), s>>>(FA_ARGS);
-  } else {
-    switch (D) {
-      case 32: flash_attn_pipe_kernel<32, SPEC, false><<<grid, 256, fa_pipe_smem<32, false>(), s>>>(FA_ARGS); break;
-      case 64: flash_attn_pipe_kernel<64, SPEC, false><<<grid, 256, fa_pipe_smem<64, false>(), s>>>(FA_ARGS); break;
-      case 96: flash_attn_pipe_kernel<96, SPEC, false><<<grid, 256, fa_pipe_smem<96, false>(), s>>>(FA_ARGS); break;
-      default: return (int)hipErrorInvalidValue;
-    }
-  }
-#undef FA_ARGS
+  flash_attn_pipe_kernel<96, true, DMA><<<grid, 256, fa_pipe_smem<96, DMA>(), s>>>(
+      (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, ldq, ldk, ldv, (const int*)cu_seqlens, H, Hkv, causal, sl2e,
+      (bf16_t*)o, ldo, pre);
   return (int)hipGetLastError();
 }
 
@@ -1767,25 +1592,12 @@ DA_EXPORT int da_flash_attn_v2(const void* q, const void* k, const void* v, int 
   if (B == 0 || max_seqlen == 0) return 0;
   const float sl2e = scale * 1.4426950408889634f;
   hipStream_t s = (hipStream_t)stream;
-  const FaPrefix pre{(const bf16_t*)pre_k, (const bf16_t*)pre_v, pre_hstride, pre_len, g_fa_rev};
-  const bool pipe = g_fa_pipe == 1 || g_fa_pipe == 3 || g_fa_pipe == 4 || (g_fa_pipe == 2 && causal && D == 96);
-  if (pipe && D <= 96 && g_fa_waves != 8 && g_fa_qh != 2) {
-    // LDS-DMA tiles (D = 96, prefix in whole 64-key tiles, 16-B aligned operands): modes 2 / 4
-    const bool dma = (g_fa_pipe == 2 || g_fa_pipe == 4) && D == 96 && pre_len % 64 == 0 &&
-                     ((uintptr_t)k | (uintptr_t)v | (uintptr_t)pre_k | (uintptr_t)pre_v) % 16 == 0;
-    if (dma)
-      return launch_fa_pipe<true, true>(q, k, v, ldq, ldk, ldv, cu_seqlens, B, max_seqlen, H, Hkv, D, causal, sl2e, o, ldo, pre, s);
-    if (g_fa_pipe != 1)  // auto (causal D = 96) and 3: speculative softmax (654 -> 689 TF/s, attn_bench)
-      return launch_fa_pipe<true, false>(q, k, v, ldq, ldk, ldv, cu_seqlens, B, max_seqlen, H, Hkv, D, causal, sl2e, o, ldo, pre, s);
-    return launch_fa_pipe<false, false>(q, k, v, ldq, ldk, ldv, cu_seqlens, B, max_seqlen, H, Hkv, D, causal, sl2e, o, ldo, pre, s);
+  const FaPrefix pre{(const bf16_t*)pre_k, (const bf16_t*)pre_v, pre_hstride, pre_len, kFaDispatch};
+  if (causal && D == 96) {
+    const bool dma = pre_len % 64 == 0 && ((uintptr_t)k | (uintptr_t)v | (uintptr_t)pre_k | (uintptr_t)pre_v) % 16 == 0;
+    if (dma) return launch_fa_pipe<true>(q, k, v, ldq, ldk, ldv, cu_seqlens, B, max_seqlen, H, Hkv, causal, sl2e, o, ldo, pre, s);
+    return launch_fa_pipe<false>(q, k, v, ldq, ldk, ldv, cu_seqlens, B, max_seqlen, H, Hkv, causal, sl2e, o, ldo, pre, s);
   }
-  const int qh = g_fa_qh ? g_fa_qh : 1;
-  // auto: 4 waves, except D = 128 (Llama-3 prefill: 8 waves measured faster, profiles/r2/attn_bench_v4.txt)
-  const bool w8 = g_fa_waves == 8 || (g_fa_waves == 0 && D == 128);
-  if (qh == 2) {
-    if (w8 && D <= 64) return launch_fa2<8, 2>(q, k, v, ldq, ldk, ldv, cu_seqlens, B, max_seqlen, H, Hkv, D, causal, sl2e, o, ldo, pre, s);
-    return launch_fa2<4, 2>(q, k, v, ldq, ldk, ldv, cu_seqlens, B, max_seqlen, H, Hkv, D, causal, sl2e, o, ldo, pre, s);
-  }
-  if (w8) return launch_fa2<8, 1>(q, k, v, ldq, ldk, ldv, cu_seqlens, B, max_seqlen, H, Hkv, D, causal, sl2e, o, ldo, pre, s);
+  if (D == 128) return launch_fa2<8, 1>(q, k, v, ldq, ldk, ldv, cu_seqlens, B, max_seqlen, H, Hkv, D, causal, sl2e, o, ldo, pre, s);
   return launch_fa2<4, 1>(q, k, v, ldq, ldk, ldv, cu_seqlens, B, max_seqlen, H, Hkv, D, causal, sl2e, o, ldo, pre, s);
 }

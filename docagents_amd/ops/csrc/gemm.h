@@ -10,8 +10,6 @@ enum Epi : int {
   EPI_RESID = 4,      // bias (optional) + residual add
   EPI_PARTIAL = 5,    // fp32 split-K partial to workspace
   EPI_ROPE = 6,       // QKV projection: RoPE (interleaved pairs) on q / k, k / v written to the KV cache
-  EPI_SPLITK = 7,     // decode tiles: split-K partials reduced IN the kernel by the tile's last split
-                      // (fuse_epi = the real epilogue; ssq_in / ssq_out as gemm_splitk_reduce)
 };
 
 // EPI_ROPE operands: output columns [H q heads | Hkv k heads | Hkv v heads] of D; token row m goes to
@@ -29,16 +27,6 @@ struct GemmArgs {
   const float* sa; const float* sw;  // fp8 path: per-row (A) and per-output-channel (W) scales
   const bf16_t* gamma; float eps;    // GEMV only: fused RMSNorm of the input row (gamma != null)
   RopeArgs rope;                     // EPI_ROPE only
-  // prefill RMSNorm folded into the phase-split GEMM (gemm8p; gains folded into W):
-  //   ssq_in: A holds the raw residual rows; out = epi(rsqrt(sum_p ssq_in[m][p] / norm_k + eps) * (A W^T))
-  //   ssq_out (EPI_RESID): per-row sums of squares of the bf16 output, one per 64 columns (part =
-  //            column tile * 4 + wave column: 2 x 32 columns, reference.gemm8p_ssq_parts)
-  //            ([M][N / 64] floats) — the next consumer's ssq_in
-  const float* ssq_in; int ssq_parts; int norm_k; float norm_eps;
-  float* ssq_out;
-  // EPI_SPLITK: per-tile arrival counters (zero before the launch, left zero after it) and the
-  // epilogue the last split applies (NONE / BIAS / SWIGLU / RESID)
-  int* cnt; int fuse_epi;
   int group;  // gemm8p: row tiles per grouped-M band of the tile order (0: the default, 4)
 };
 

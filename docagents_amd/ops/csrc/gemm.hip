@@ -15,162 +15,22 @@
 //  * split-K writes fp32 partials; gemm_splitk_reduce applies the same epilogue.
 #include "gemm.h"
 
-// ------------------------------------------------------------------------------------------
-// In-kernel split-K reduction for the decode tiles (33..64 rows): no reduce launch. Every split
-// writes its fp32 partial tile write-through (sc1: the tile's other splits run on other CUs /
-// XCDs, whose L2s are not coherent with this one), drains, and takes a ticket on the tile's
-// arrival counter; the LAST split of the tile sums every split's partial in split order (sc1
-// loads: the same fixed order as gemm_splitk_reduce, so results do not depend on arrival order)
-// and applies the epilogue: the deferred RMSNorm row scale (ssq_in), bias, SwiGLU (16-column
-// interleave) or residual (+ per-row sums of squares of the new rows over this tile's columns,
-// ssq_out [N / BN][64]: the next consumer's norm). It then zeroes the counter for the next launch
-// (cdna_hip_programming.md §6 Guideline 16 hand-off; MI355X_MICROARCH.md splitk-seam).
-__device__ __forceinline__ void st16_sc1(__amdgpu_buffer_rsrc_t r, unsigned off, const float* v) {
-  const u32x4_t x = {__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]), __float_as_uint(v[3])};
-  __builtin_amdgcn_raw_buffer_store_b128(x, r, off, 0, 16);
-}
-__device__ __forceinline__ f32x4_t ld16f_sc1(__amdgpu_buffer_rsrc_t r, unsigned off) {
-  const u32x4_t x = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 16);
-  return f32x4_t{__uint_as_float(x[0]), __uint_as_float(x[1]), __uint_as_float(x[2]), __uint_as_float(x[3])};
-}
-
-template <int TM, int TN, int SLD>
-__device__ __forceinline__ void splitk_fused_epilogue(const GemmArgs& p, const float* st, int row0, int col0,
-                                                      int tile_id, int tn, int lane, int wid) {
-  const int S = gridDim.z, z = blockIdx.z, M = p.M, N = p.N;
-  const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)p.ws, (short)0, (int)min((size_t)S * M * N * 4, (size_t)0x7ffffff0), 0x00020000);
-  constexpr int CPR = TN / 8, RPI = 64 / CPR;
-  {
-    const int cc = (lane % CPR) * 8, gn = col0 + cc;
-    for (int rr = lane / CPR; rr < TM; rr += RPI) {
-      const int gm = row0 + rr;
-      if (gm >= M || gn >= N) continue;
-      const unsigned off = (unsigned)((((size_t)z * M + gm) * N + gn) * 4);
-      st16_sc1(rw, off, st + rr * SLD + cc);
-      st16_sc1(rw, off + 16, st + rr * SLD + cc + 4);
-    }
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  __shared__ int s_last;
-  if (threadIdx.x == 0) {
-    const int t = __hip_atomic_fetch_add(p.cnt + tile_id, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    s_last = t == S - 1;
-    if (s_last) __hip_atomic_store(p.cnt + tile_id, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  __syncthreads();
-  if (!s_last) return;
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // the partial loads stay below the ticket
-  const int epi = p.fuse_epi;
-  auto row_scale = [&](int gm) -> float {
-    if (!p.ssq_in) return 1.f;
-    const float ss = sum_strided(p.ssq_in + gm, p.ssq_parts, 64);
-    return rsqrtf(ss / p.norm_k + p.norm_eps);
-  };
-  if (epi == EPI_SWIGLU) {
-    // this wave's TN columns = TN / 32 (gate 16 | up 16) groups -> TN / 2 outputs per row
-    constexpr int OCPR = TN / 16, ORPI = 64 / OCPR;
-    const int oc = (lane % OCPR) * 8, grp = oc / 16, within = oc % 16;
-    const int gc = col0 + grp * 32 + within, gout = col0 / 2 + oc;
-    for (int rr = lane / OCPR; rr < TM; rr += ORPI) {
-      const int gm = row0 + rr;
-      if (gm >= M || gout >= N / 2) continue;
-      float g[8], u[8];
-#pragma unroll
-      for (int e = 0; e < 8; ++e) { g[e] = 0.f; u[e] = 0.f; }
-      for (int sp = 0; sp < S; ++sp) {
-        const unsigned off = (unsigned)((((size_t)sp * M + gm) * N + gc) * 4);
-        const f32x4_t g0 = ld16f_sc1(rw, off), g1 = ld16f_sc1(rw, off + 16);
-        const f32x4_t u0 = ld16f_sc1(rw, off + 64), u1 = ld16f_sc1(rw, off + 80);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) { g[e] += g0[e]; g[4 + e] += g1[e]; u[e] += u0[e]; u[4 + e] += u1[e]; }
-      }
-      const float inv = row_scale(gm);
-      unsigned pk[4];
-#pragma unroll
-      for (int e = 0; e < 8; e += 2)
-        pk[e / 2] = pack_bf2(silu(g[e] * inv) * (u[e] * inv), silu(g[e + 1] * inv) * (u[e + 1] * inv));
-      *(u32x4_t*)(p.C + (size_t)gm * p.ldc + gout) = u32x4_t{pk[0], pk[1], pk[2], pk[3]};
-    }
-    return;
-  }
-  __shared__ float ssq_w[4][64];
-  const int cc = (lane % CPR) * 8, gn = col0 + cc;
-  for (int rr = lane / CPR; rr < TM; rr += RPI) {
-    const int gm = row0 + rr;
-    float sq = 0.f;
-    if (gm < M && gn < N) {
-      float v[8];
-#pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] = 0.f;
-      for (int sp = 0; sp < S; ++sp) {
-        const unsigned off = (unsigned)((((size_t)sp * M + gm) * N + gn) * 4);
-        const f32x4_t a = ld16f_sc1(rw, off), b = ld16f_sc1(rw, off + 16);
-        v[0] += a[0]; v[1] += a[1]; v[2] += a[2]; v[3] += a[3];
-        v[4] += b[0]; v[5] += b[1]; v[6] += b[2]; v[7] += b[3];
-      }
-      const float inv = row_scale(gm);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] *= inv;
-      if (p.bias) {
-#pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] += bf2f(p.bias[gn + e]);
-      }
-      if (epi == EPI_RESID) {
-        const u32x4_t r = *(const u32x4_t*)(p.resid + (size_t)gm * p.ldr + gn);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          v[2 * e] += bf2f((bf16_t)(r[e] & 0xffff));
-          v[2 * e + 1] += bf2f((bf16_t)(r[e] >> 16));
-        }
-      }
-      const u32x4_t o = {pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3]), pack_bf2(v[4], v[5]), pack_bf2(v[6], v[7])};
-      *(u32x4_t*)(p.C + (size_t)gm * p.ldc + gn) = o;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {  // what the stream now holds (bf16)
-        const float lo = bf2f((bf16_t)(o[e] & 0xffff)), hi = bf2f((bf16_t)(o[e] >> 16));
-        sq += lo * lo + hi * hi;
-      }
-    }
-    if (p.ssq_out) {  // the row's CPR chunks sit in CPR adjacent lanes
-#pragma unroll
-      for (int o = 1; o < CPR; o <<= 1) sq += __shfl_xor(sq, o, 64);
-      if (lane % CPR == 0) ssq_w[wid][rr] = sq;
-    }
-  }
-  if (p.ssq_out) {
-    __syncthreads();
-    const int t = threadIdx.x;
-    if (t < TM && row0 + t < M) {
-      float ss = 0.f;
-#pragma unroll
-      for (int w = 0; w < 4; ++w) ss += ssq_w[w][t];
-      p.ssq_out[(size_t)tn * 64 + row0 + t] = ss;
-    }
-  }
-}
-
-template <int BM, int BN, int WM, int WN, int EPI, int PF = 1, bool DB = false>
+template <int BM, int BN, int WM, int WN, int EPI, int PF = 1>
 __global__ void __launch_bounds__(256)
 gemm_bf16_kernel(GemmArgs p) {
   // PF = k-tiles in flight in registers. PF = 1: the classic register-staged double buffer (one
   // tile ahead). Decode-sized tiles (M <= 64) stream weights and are latency-bound at PF = 1 —
   // one 16-KB W tile per workgroup in flight, ~6 dependent HBM round trips per split — so they
   // keep PF tiles (up to 72 KB per workgroup) requested ahead of the MFMAs (Little's law).
-  // DB (direct B, decode tiles with WM = 1): each weight row is consumed by exactly one wave, so
-  // the wave loads its W fragments straight into the MFMA B-operand registers (lane l: row
-  // n0 + 16 j + (l & 15), k + 8 (l >> 4); 64 contiguous bytes per row per instruction) — no LDS
-  // write + read of the 16 KB W tile per k-tile; only the activation tile (shared by the 4 waves)
-  // goes through LDS.
+  // (Weight fragments loaded straight into the MFMA B registers, skipping LDS, lost on every arm
+  // measured: half-line requests, profiles/r3/rejected_r3.txt.)
   constexpr int BK = 64;
   constexpr int TM = BM / WM, TN = BN / WN;
   constexpr int FM = TM / 16, FN = TN / 16;
-  constexpr int A_BYTES = BM * BK * 2, B_BYTES = DB ? 0 : BN * BK * 2;
-  constexpr int LA = BM * 8 / 256, LB = DB ? 1 : BN * 8 / 256;  // 16-B loads per thread per tile
+  constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2;
+  constexpr int LA = BM * 8 / 256, LB = BN * 8 / 256;  // 16-B loads per thread per tile
   static_assert(WM * WN == 4, "4 waves");
   static_assert(LA >= 1 && LB >= 1, "tile too small");
-  static_assert(!DB || WM == 1, "direct B: one wave per weight column block");
   constexpr int STAGE_FLOATS = 4 * TM * (TN + 4);
   constexpr int LDS_MAIN = 2 * (A_BYTES + B_BYTES);
   constexpr int LDS_BYTES = LDS_MAIN > STAGE_FLOATS * 4 ? LDS_MAIN : STAGE_FLOATS * 4;
@@ -196,7 +56,6 @@ gemm_bf16_kernel(GemmArgs p) {
 
   // ---- global -> register staging (PF slots) ----
   u32x4_t ra[PF][LA], rb[PF][LB];
-  bf16x8_t rd[DB ? PF : 1][DB ? 2 : 1][DB ? FN : 1];  // DB: W fragments [slot][k half][n tile]
   const int fr = lane & 15, fg = lane >> 4;
   // Rows past M / N are clamped, not branched around: they only feed accumulators whose outputs
   // are never stored, and branch-free loads keep the compiler's vmcnt waits counted (a load
@@ -208,25 +67,10 @@ gemm_bf16_kernel(GemmArgs p) {
       const int idx = tid + 256 * i, r = idx >> 3, c = idx & 7;
       xa[i] = *(const u32x4_t*)(p.A + (size_t)min(m0 + r, p.M - 1) * p.lda + k0 + c * 8);
     }
-    if constexpr (!DB) {
 #pragma unroll
-      for (int i = 0; i < LB; ++i) {
-        const int idx = tid + 256 * i, r = idx >> 3, c = idx & 7;
-        xb[i] = *(const u32x4_t*)(p.W + (size_t)min(n0 + r, p.N - 1) * p.K + k0 + c * 8);
-      }
-    }
-  };
-  auto dload = [&](bf16x8_t (&xd)[DB ? 2 : 1][DB ? FN : 1], int kt) {
-    if constexpr (DB) {
-      const int k0 = kbeg + kt * BK + fg * 8;
-      // the two k halves of a row's 128-B line back to back (one line, two 64-B requests)
-#pragma unroll
-      for (int j = 0; j < FN; ++j)
-#pragma unroll
-        for (int kk = 0; kk < 2; ++kk) {
-          const int n = min(n0 + wn * TN + j * 16 + fr, p.N - 1);
-          xd[kk][j] = *(const bf16x8_t*)(p.W + (size_t)n * p.K + k0 + kk * 32);
-        }
+    for (int i = 0; i < LB; ++i) {
+      const int idx = tid + 256 * i, r = idx >> 3, c = idx & 7;
+      xb[i] = *(const u32x4_t*)(p.W + (size_t)min(n0 + r, p.N - 1) * p.K + k0 + c * 8);
     }
   };
   auto lstore = [&](const u32x4_t (&xa)[LA], const u32x4_t (&xb)[LB], int buf) {
@@ -237,12 +81,10 @@ gemm_bf16_kernel(GemmArgs p) {
       const int idx = tid + 256 * i, r = idx >> 3, c = idx & 7;
       *(u32x4_t*)(sa + r * 128 + ((c ^ ((r >> 1) & 7)) << 4)) = xa[i];
     }
-    if constexpr (!DB) {
 #pragma unroll
-      for (int i = 0; i < LB; ++i) {
-        const int idx = tid + 256 * i, r = idx >> 3, c = idx & 7;
-        *(u32x4_t*)(sb + r * 128 + ((c ^ ((r >> 1) & 7)) << 4)) = xb[i];
-      }
+    for (int i = 0; i < LB; ++i) {
+      const int idx = tid + 256 * i, r = idx >> 3, c = idx & 7;
+      *(u32x4_t*)(sb + r * 128 + ((c ^ ((r >> 1) & 7)) << 4)) = xb[i];
     }
   };
 
@@ -258,7 +100,6 @@ gemm_bf16_kernel(GemmArgs p) {
 #pragma unroll
   for (int u = 0; u < PF; ++u) {
     gload(ra[u], rb[u], min(u, kl));
-    dload(rd[DB ? u : 0], min(u, kl));
     asm volatile("" ::: "memory");  // keep issue order = tile order (counted waits stay short)
   }
   if (nk > 0) lstore(ra[0], rb[0], 0);
@@ -269,11 +110,8 @@ gemm_bf16_kernel(GemmArgs p) {
     for (int u = 0; u < PF; ++u) {
       const int kt = kt0 + u;
       const int cur = kt & 1;
-      // slot u held tile kt, already copied to LDS: refill it PF tiles ahead (DB: the W fragments
-      // of slot u are the MFMA operands of tile kt, refilled after the MFMAs below)
-      if constexpr (!DB) {
-        if (PF > 1 || kt + 1 < nk) gload(ra[u], rb[u], min(kt + PF, kl));
-      }
+      // slot u held tile kt, already copied to LDS: refill it PF tiles ahead
+      if (PF > 1 || kt + 1 < nk) gload(ra[u], rb[u], min(kt + PF, kl));
       if (kt < nk) {
         const char* sa = smem + cur * (A_BYTES + B_BYTES);
         const char* sb = sa + A_BYTES;
@@ -288,23 +126,13 @@ gemm_bf16_kernel(GemmArgs p) {
           }
 #pragma unroll
           for (int j = 0; j < FN; ++j) {
-            if constexpr (DB) {
-              bfr[j] = rd[DB ? u : 0][DB ? kk : 0][DB ? j : 0];
-            } else {
-              const int r = wn * TN + j * 16 + fr;
-              bfr[j] = *(const bf16x8_t*)(sb + r * 128 + ((c ^ ((r >> 1) & 7)) << 4));
-            }
+            const int r = wn * TN + j * 16 + fr;
+            bfr[j] = *(const bf16x8_t*)(sb + r * 128 + ((c ^ ((r >> 1) & 7)) << 4));
           }
 #pragma unroll
           for (int i = 0; i < FM; ++i)
 #pragma unroll
             for (int j = 0; j < FN; ++j) acc[i][j] = mfma16(af[i], bfr[j], acc[i][j]);
-        }
-      }
-      if constexpr (DB) {
-        if (PF > 1 || kt + 1 < nk) {
-          gload(ra[u], rb[u], min(kt + PF, kl));
-          dload(rd[DB ? u : 0], min(kt + PF, kl));
         }
       }
       if (kt >= nk) continue;
@@ -328,10 +156,6 @@ gemm_bf16_kernel(GemmArgs p) {
   __syncthreads();
 
   const int row0 = m0 + wm * TM, col0 = n0 + wn * TN;
-  if constexpr (EPI == EPI_SPLITK) {
-    splitk_fused_epilogue<TM, TN, SLD>(p, st, row0, col0, tm * ntn + tn, tn, lane, wid);
-    return;
-  }
   if constexpr (EPI == EPI_SWIGLU) {
     // output tile TM x TN/2; chunk of 8 outputs; TN/16 chunks per row
     constexpr int CPR = TN / 16;
@@ -585,204 +409,10 @@ static int launch_gemv_r(const GemmArgs& a, int epi, hipStream_t s) {
   return (int)hipGetLastError();
 }
 
-// ------------------------------------------------------------------------------------------
-// Batch-1 decode O projection with the decode attention's split merge folded into its input load:
-//
-//   C[n] = resid[n] (+ bias[n]) + sum_k W[n][k] a[k],   a[h * D + d] = bf16(merge over the splits)
-//
-// The attention launch (attention.hip da_decode_attn_parts) then ends at its fp32 partial stores:
-// no arrival ticket and no last-split merge (uncached partial reads, one workgroup per head) on its
-// critical path. Each thread of a workgroup owns 8 consecutive elements of the row (one head: the
-// row is K / 8 <= NT chunks) and issues ALL of its partial loads (NS splits, clamped) before the
-// wave's weight rows: the partials come back first and are merged while the weight stream is still
-// landing (issued behind them, a CU's requests would queue behind ~100 KB of weights). The merged
-// bf16 row goes to LDS, then the same dot products as gemv_kernel (same fmaf order, same wave
-// reduction, same epilogue). The merge repeats attention.hip dec_finish's arithmetic expression for
-// expression (groups of 8 splits, online rescale) under the same contraction rule, so the row — and
-// the projection — are bit-identical to the ticketed in-kernel merge followed by gemv_kernel
-// (tests/test_o_merge_gpu.py).
-struct OMergeArgs {
-  const float* po; const float* pm; const float* pl;  // da_decode_attn_parts partials (row 0)
-  int nsplit, D;
-  bf16_t* a_out;  // nullable: workgroup 0 also stores the merged row (the attention output)
-};
-
-template <int NS>
-__device__ __forceinline__ void omerge_rows(const float (&ms)[NS], const float (&ls)[NS], const f32x4_t (&oa)[NS],
-                                            const f32x4_t (&ob)[NS], int nsplit, float (&out)[8]) {
-#pragma clang fp contract(on)
-  float M = -INFINITY, lsum = 0.f, acc[8];
-#pragma unroll
-  for (int e = 0; e < 8; ++e) acc[e] = 0.f;
-#pragma unroll
-  for (int s0 = 0; s0 < NS; s0 += 8) {
-    if (s0 >= nsplit) break;
-    float mx = M;
-#pragma unroll
-    for (int j = 0; j < 8; ++j)
-      if (s0 + j < nsplit) mx = fmaxf(mx, ms[s0 + j]);
-    const float mu = (mx == -INFINITY) ? 0.f : mx;
-    const float r = (M == -INFINITY) ? 0.f : exp2f(M - mu);
-    lsum *= r;
-#pragma unroll
-    for (int e = 0; e < 8; ++e) acc[e] *= r;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      if (s0 + j >= nsplit) continue;
-      const float f = exp2f(ms[s0 + j] - mu);
-      lsum += ls[s0 + j] * f;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        acc[e] += oa[s0 + j][e] * f;
-        acc[4 + e] += ob[s0 + j][e] * f;
-      }
-    }
-    M = mx;
-  }
-#pragma unroll
-  for (int e = 0; e < 8; ++e) out[e] = lsum > 0.f ? acc[e] / lsum : 0.f;
-}
-
-template <int NW, int R, int U, int NS>
-__global__ void __launch_bounds__(NW * 64)
-gemv_omerge_kernel(GemmArgs p, OMergeArgs m) {
-  __shared__ __attribute__((aligned(16))) bf16_t sa[U * 512];
-  const int lane = threadIdx.x & 63;
-  const int wv = blockIdx.x * NW + (threadIdx.x >> 6);
-  const int nkb = p.K / 512;  // 1..U: the whole row in one round of loads
-  // ---- this thread's chunk of the row: all NS splits' partials in flight first (clamped) ----
-  const int nch = p.K / 8;  // <= NW * 64 (host-checked)
-  const int c = min((int)threadIdx.x, nch - 1);
-  const int k0 = c * 8, h = k0 / m.D, d0 = k0 % m.D;
-  const size_t base = (size_t)h * m.nsplit;
-  float ms[NS], ls[NS];
-  f32x4_t oa[NS], ob[NS];
-#pragma unroll
-  for (int j = 0; j < NS; ++j) {
-    const int sp = min(j, m.nsplit - 1);
-    ms[j] = m.pm[base + sp];
-    ls[j] = m.pl[base + sp];
-    oa[j] = *(const f32x4_t*)(m.po + (base + sp) * m.D + d0);
-    ob[j] = *(const f32x4_t*)(m.po + (base + sp) * m.D + d0 + 4);
-  }
-  asm volatile("" ::: "memory");  // issue order: the partials, then the weight rows
-  int rows[R];
-#pragma unroll
-  for (int r = 0; r < R; ++r) rows[r] = wv * R + r;
-  u32x4_t wr[U][R];
-#pragma unroll
-  for (int u = 0; u < U; ++u) {
-    const int k = min(u, nkb - 1) * 512;
-#pragma unroll
-    for (int r = 0; r < R; ++r)
-      wr[u][r] = __builtin_nontemporal_load((const u32x4_t*)(p.W + (size_t)min(rows[r], p.N - 1) * p.K + k + lane * 8));
-  }
-  {
-    float v[8];
-    omerge_rows<NS>(ms, ls, oa, ob, m.nsplit, v);
-    const u32x4_t o{pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3]), pack_bf2(v[4], v[5]), pack_bf2(v[6], v[7])};
-    if ((int)threadIdx.x < nch) {
-      *(u32x4_t*)(sa + k0) = o;
-      if (m.a_out && blockIdx.x == 0) *(u32x4_t*)(m.a_out + k0) = o;
-    }
-  }
-  __syncthreads();
-  if (rows[0] >= p.N) return;  // after the barrier: every wave helped merge
-  float acc[R];
-#pragma unroll
-  for (int r = 0; r < R; ++r) acc[r] = 0.f;
-#pragma unroll
-  for (int u = 0; u < U; ++u) {
-    if (u >= nkb) break;
-    const u32x4_t av = *(const u32x4_t*)(sa + u * 512 + lane * 8);
-    float a[8];
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      a[2 * e] = bf2f((bf16_t)(av[e] & 0xffff));
-      a[2 * e + 1] = bf2f((bf16_t)(av[e] >> 16));
-    }
-#pragma unroll
-    for (int r = 0; r < R; ++r)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        acc[r] = fmaf(bf2f((bf16_t)(wr[u][r][e] & 0xffff)), a[2 * e], acc[r]);
-        acc[r] = fmaf(bf2f((bf16_t)(wr[u][r][e] >> 16)), a[2 * e + 1], acc[r]);
-      }
-  }
-#pragma unroll
-  for (int r = 0; r < R; ++r) acc[r] = wave_sum(acc[r]);
-  if (lane != 0) return;
-#pragma unroll
-  for (int r = 0; r < R; ++r) {
-    const int n = rows[r];
-    if (n >= p.N) continue;
-    float v = acc[r];
-    if (p.bias) v += bf2f(p.bias[n]);
-    if (p.resid) v += bf2f(p.resid[n]);
-    p.C[n] = f2bf(v);
-  }
-}
-
-// Workgroup shape of the merged O projection: waves per workgroup x rows per wave (every
-// workgroup merges the whole row, so fewer, fatter workgroups read fewer partial bytes; a thread
-// merges one 8-element chunk, so K <= 512 * waves). A/B knob.
-static int g_omerge_shape = 82;  // NW * 10 + R (82: 2.009 ms per batch-1 step, 81 2.042, 161 2.034)
-DA_EXPORT void da_set_omerge_shape(int v) { g_omerge_shape = v; }
-
-template <int NW, int R>
-static int launch_omerge(const GemmArgs& a, const OMergeArgs& mg, hipStream_t s) {
-  if (a.K > 512 * NW) return (int)hipErrorInvalidValue;  // one chunk of 8 per thread
-  const int grid = (a.N + NW * R - 1) / (NW * R), nkb = a.K / 512;
-#define OMK(U_, NS_) gemv_omerge_kernel<NW, R, U_, NS_><<<grid, NW * 64, 0, s>>>(a, mg)
-  if (mg.nsplit <= 8) {
-    if (nkb == 6) OMK(6, 8); else OMK(8, 8);
-  } else {
-    if constexpr (NW <= 8 && R == 1) {  // 16 splits' partials in registers: no spills at 8 x 1 only
-      if (nkb == 6) OMK(6, 16); else OMK(8, 16);
-    } else {
-      return (int)hipErrorInvalidValue;
-    }
-  }
-#undef OMK
-  return (int)hipGetLastError();
-}
-
-// C[N] = resid (nullable) + bias (nullable) + W[N, K] . merge(partials), one row (batch-1 decode).
-// ws = the da_decode_attn_parts workspace of B = 1: po [H][nsplit][D], then pm, pl [H][nsplit],
-// H = K / D. K % 512 == 0, K <= 4096, D % 8 == 0, 2 <= nsplit <= 16.
-DA_EXPORT int da_gemv_omerge(const void* ws, int nsplit, int D, const void* W, void* C, const void* resid,
-                             const void* bias, int N, int K, void* a_out, void* stream) {
-  if (!ws || nsplit < 2 || nsplit > 16 || D < 8 || D % 8 || K % 512 || K > 4096 || K % D || N < 1)
-    return (int)hipErrorInvalidValue;
-  const int H = K / D;
-  GemmArgs a{};
-  a.W = (const bf16_t*)W; a.C = (bf16_t*)C; a.resid = (const bf16_t*)resid; a.bias = (const bf16_t*)bias;
-  a.M = 1; a.N = N; a.K = K;
-  OMergeArgs mg{};
-  mg.po = (const float*)ws;
-  mg.pm = mg.po + (size_t)H * nsplit * D;
-  mg.pl = mg.pm + (size_t)H * nsplit;
-  mg.nsplit = nsplit; mg.D = D; mg.a_out = (bf16_t*)a_out;
-  hipStream_t s = (hipStream_t)stream;
-  // 9..16 splits: the 8-wave, 1-row shape (the only one whose registers hold 16 splits' partials)
-  const int shape = nsplit > 8 ? 81 : g_omerge_shape;
-  switch (shape) {
-    case 81: return launch_omerge<8, 1>(a, mg, s);
-    case 82: return launch_omerge<8, 2>(a, mg, s);
-    case 161: return launch_omerge<16, 1>(a, mg, s);
-    default: return (int)hipErrorInvalidValue;
-  }
-}
-
 // K-blocks (512 elements = 1 KiB per row) in flight per row: the whole row when it is short
 // (K = 3072: 6 blocks, one round of loads and no clamped duplicate loads), 8 per round otherwise.
-static int g_gemv_u = 0;  // 0 = auto; 4 = the fixed round-1 depth (A/B)
-DA_EXPORT void da_set_gemv_u(int v) { g_gemv_u = v; }
-static int g_gemv_ks = 2;  // K split across 2 waves for long rows on narrow matrices (1 = off, A/B)
-DA_EXPORT void da_set_gemv_ks(int v) { g_gemv_ks = v == 1 ? 1 : 2; }
 static int gemv_u(int K, int /*R*/) {
   const int nkb = K / 512;
-  if (g_gemv_u) return g_gemv_u;
   if (nkb <= 4) return 4;
   if (nkb == 6) return 6;
   // 8, not the whole row at K = 8192: at U = 16 the compiler sinks the loads to their uses
@@ -815,54 +445,31 @@ static int launch_gemv(const GemmArgs& a, int epi, hipStream_t s) {
   if (a.N >= 16384) return launch_gemv_ru<4>(a, epi, s);
   if (a.N >= 8192) return launch_gemv_ru<2>(a, epi, s);
   // long rows on a narrow matrix (down projection, K = 8192): two waves per row, 8 blocks each
-  if (g_gemv_ks == 2 && a.K >= 8192 && a.K % 1024 == 0) return launch_gemv_r<1, 8, 2>(a, epi, s);
+  if (a.K >= 8192 && a.K % 1024 == 0) return launch_gemv_r<1, 8, 2>(a, epi, s);
   return launch_gemv_ru<1>(a, epi, s);
 }
 
-template <int BM, int BN, int WM, int WN, int PF = 1, bool DB = false>
+template <int BM, int BN, int WM, int WN, int PF = 1>
 static int launch_tile(const GemmArgs& a, int epi, int splits, hipStream_t s) {
   const int ntm = (a.M + BM - 1) / BM, ntn = (a.N + BN - 1) / BN;
   dim3 grid(ntm * ntn, 1, splits), block(256);
-  switch (splits > 1 && epi != EPI_SPLITK ? (int)EPI_PARTIAL : epi) {
-    case EPI_NONE: gemm_bf16_kernel<BM, BN, WM, WN, EPI_NONE, PF, DB><<<grid, block, 0, s>>>(a); break;
-    case EPI_BIAS: gemm_bf16_kernel<BM, BN, WM, WN, EPI_BIAS, PF, DB><<<grid, block, 0, s>>>(a); break;
-    case EPI_GELU: gemm_bf16_kernel<BM, BN, WM, WN, EPI_GELU, PF, DB><<<grid, block, 0, s>>>(a); break;
-    case EPI_SWIGLU: gemm_bf16_kernel<BM, BN, WM, WN, EPI_SWIGLU, PF, DB><<<grid, block, 0, s>>>(a); break;
-    case EPI_RESID: gemm_bf16_kernel<BM, BN, WM, WN, EPI_RESID, PF, DB><<<grid, block, 0, s>>>(a); break;
-    case EPI_PARTIAL: gemm_bf16_kernel<BM, BN, WM, WN, EPI_PARTIAL, PF, DB><<<grid, block, 0, s>>>(a); break;
-    case EPI_SPLITK:
-      if constexpr (BM == 64 && WM == 1 && WN == 4) {
-        gemm_bf16_kernel<BM, BN, WM, WN, EPI_SPLITK, PF, DB><<<grid, block, 0, s>>>(a);
-        break;
-      }
-      return (int)hipErrorInvalidValue;
+  switch (splits > 1 ? (int)EPI_PARTIAL : epi) {
+    case EPI_NONE: gemm_bf16_kernel<BM, BN, WM, WN, EPI_NONE, PF><<<grid, block, 0, s>>>(a); break;
+    case EPI_BIAS: gemm_bf16_kernel<BM, BN, WM, WN, EPI_BIAS, PF><<<grid, block, 0, s>>>(a); break;
+    case EPI_GELU: gemm_bf16_kernel<BM, BN, WM, WN, EPI_GELU, PF><<<grid, block, 0, s>>>(a); break;
+    case EPI_SWIGLU: gemm_bf16_kernel<BM, BN, WM, WN, EPI_SWIGLU, PF><<<grid, block, 0, s>>>(a); break;
+    case EPI_RESID: gemm_bf16_kernel<BM, BN, WM, WN, EPI_RESID, PF><<<grid, block, 0, s>>>(a); break;
+    case EPI_PARTIAL: gemm_bf16_kernel<BM, BN, WM, WN, EPI_PARTIAL, PF><<<grid, block, 0, s>>>(a); break;
     default: return (int)hipErrorInvalidValue;
   }
   return (int)hipGetLastError();
 }
 
-// Register prefetch depth of the decode tiles (64x128 / 32x128): 1, 2 or 4 (default 4);
-// da_set_gemm_pf for A/B runs.
-static int g_gemm_pf = 4;
-DA_EXPORT void da_set_gemm_pf(int v) { g_gemm_pf = (v == 1 || v == 2 || v == 8) ? v : 4; }
-// Direct-B decode tiles (W fragments straight to registers, gemm_bf16_kernel DB): A/B switch.
-static int g_gemm_db = 0;
-DA_EXPORT void da_set_gemm_db(int v) { g_gemm_db = v; }
-
+// Decode tiles (64x128 / 32x128): 4 k-tiles in flight per workgroup (register prefetch depth 4;
+// 1 / 2 / 8 measured slower, profiles/decode_gemm_prefetch_sweep_r1.jsonl).
 template <int BM, int BN>
 static int launch_decode_tile(const GemmArgs& a, int epi, int splits, hipStream_t s) {
-  if (g_gemm_db) {
-    switch (g_gemm_pf) {
-      case 2: return launch_tile<BM, BN, 1, 4, 2, true>(a, epi, splits, s);
-      case 8: return launch_tile<BM, BN, 1, 4, 8, true>(a, epi, splits, s);
-      default: return launch_tile<BM, BN, 1, 4, 4, true>(a, epi, splits, s);
-    }
-  }
-  switch (g_gemm_pf) {
-    case 1: return launch_tile<BM, BN, 1, 4, 1>(a, epi, splits, s);
-    case 2: return launch_tile<BM, BN, 1, 4, 2>(a, epi, splits, s);
-    default: return launch_tile<BM, BN, 1, 4, 4>(a, epi, splits, s);
-  }
+  return launch_tile<BM, BN, 1, 4, 4>(a, epi, splits, s);
 }
 
 // Split-K reduction fused with the residual add AND the next RMSNorm (decode layers, M <= 64):
@@ -1006,44 +613,6 @@ DA_EXPORT int da_gemm_dk_splitk(const void* A, int lda, const void* W, void* C, 
   DA_LAUNCH_CHECK();
 }
 
-// The 33..64-row split-K tiles alone (no reduce launch): ws receives splits x [M][N] fp32 partials
-// for a consumer that reduces them itself — the decode attention's prologue for the QKV projection
-// (attention.hip da_decode_attn_qkvparts: sum in split order, deferred row norm, bf16 — the
-// arithmetic of gemm_splitk_reduce). No epilogue: bias / SwiGLU / residual need the reduce.
-DA_EXPORT int da_gemm_dk_splitk_parts(const void* A, int lda, const void* W, int M, int N, int K, void* ws,
-                                      int splits, void* stream) {
-  if (M < 1 || M > 64 || K % 64 || N % 16 || lda % 8 || !ws || splits < 1 || (K / 64) % splits)
-    return (int)hipErrorInvalidValue;
-  GemmArgs a{};
-  a.A = (const bf16_t*)A; a.W = (const bf16_t*)W; a.ws = (float*)ws;
-  a.M = M; a.N = N; a.K = K; a.lda = lda; a.ldc = N; a.k_per_split = K / splits;
-  return launch_decode_tile<64, 128>(a, EPI_PARTIAL, splits, (hipStream_t)stream);
-}
-
-// The same contract with the split-K reduction done by each tile's last split inside the tile
-// kernel (EPI_SPLITK): ONE launch, no reduce kernels. ssq_out is then [N / 128][64] (one part per
-// 128-column tile: dk_parts on this route). cnt: int32 [ceil(M/64) * N/128] zeros, left zero.
-DA_EXPORT int da_gemm_dk_splitk_fused(const void* A, int lda, const void* W, void* C, int ldc, const void* bias,
-                                      const void* resid, int ldr, int M, int N, int K, int epi, const float* ssq_in,
-                                      int ssq_parts, int norm_k, float eps, float* ssq_out, void* ws, int splits,
-                                      int* cnt, void* stream) {
-  hipStream_t s = (hipStream_t)stream;
-  if (M < 1 || M > 64 || K % 64 || N % 128 || lda % 8 || ldc % 8 || !ws || !cnt || splits < 2 || (K / 64) % splits)
-    return (int)hipErrorInvalidValue;
-  if (epi == EPI_RESID && (!resid || ldr % 8 || ssq_in)) return (int)hipErrorInvalidValue;
-  if (ssq_out && epi != EPI_RESID) return (int)hipErrorInvalidValue;
-  if (ssq_in && (ssq_parts < 1 || norm_k < 1 || !(eps > 0.f))) return (int)hipErrorInvalidValue;
-  if (epi != EPI_NONE && epi != EPI_BIAS && epi != EPI_SWIGLU && epi != EPI_RESID) return (int)hipErrorInvalidValue;
-  if ((size_t)splits * M * N * 4 > (size_t)0x7ffffff0) return (int)hipErrorInvalidValue;
-  GemmArgs a{};
-  a.A = (const bf16_t*)A; a.W = (const bf16_t*)W; a.C = (bf16_t*)C;
-  a.bias = (const bf16_t*)bias; a.resid = (const bf16_t*)resid; a.ws = (float*)ws;
-  a.M = M; a.N = N; a.K = K; a.lda = lda; a.ldc = ldc; a.ldr = ldr; a.k_per_split = K / splits;
-  a.ssq_in = ssq_in; a.ssq_parts = ssq_parts; a.norm_k = norm_k; a.norm_eps = eps; a.ssq_out = ssq_out;
-  a.cnt = cnt; a.fuse_epi = epi;
-  return launch_decode_tile<64, 128>(a, EPI_SPLITK, splits, s);
-}
-
 // Prefill QKV projection with RoPE + KV-cache write fused into the epilogue (gemm8p EPI_ROPE);
 // M >= 256 (the phase-split kernel), N == (H + 2 Hkv) * D, D % 8 == 0.
 DA_EXPORT int da_gemm_rope(const void* A, int lda, const void* W, void* C, int ldc, int M, int N, int K,
@@ -1058,38 +627,6 @@ DA_EXPORT int da_gemm_rope(const void* A, int lda, const void* W, void* C, int l
                     H, Hkv, D, max_seq};
   const long t256 = (long)((M + 255) / 256) * ((N + 255) / 256);
   return launch_gemm8p(a, EPI_ROPE, (hipStream_t)stream, t256 >= 256 ? 256 : 128);
-}
-
-// Prefill projection on the phase-split kernel with the layer RMSNorms folded in (gemm.h GemmArgs
-// ssq_in / ssq_out): a consumer (QKV + RoPE + KV write, gate/up + SwiGLU) reads the raw residual
-// stream and scales its output rows by the norm from the producer's row sums; a producer (EPI_RESID:
-// O / down projection) writes those sums ([M][N / 64] floats). Same tile choice as da_gemm_bf16 /
-// da_gemm_rope. Rope args are used only by EPI_ROPE.
-DA_EXPORT int da_gemm8p_norm(const void* A, int lda, const void* W, void* C, int ldc, const void* bias,
-                             const void* resid, int ldr, int M, int N, int K, int epi, const float* ssq_in,
-                             int ssq_parts, int norm_k, float eps, float* ssq_out, const void* pos, const void* slot,
-                             const void* cos_sin, void* k_cache, void* v_cache, int H, int Hkv, int D, int max_seq,
-                             void* stream) {
-  if (K % 64 || K < 128 || N % 8 || lda % 8 || ldc % 8 || M < 256) return (int)hipErrorInvalidValue;
-  if (epi != EPI_ROPE && epi != EPI_SWIGLU && epi != EPI_RESID && epi != EPI_NONE && epi != EPI_BIAS)
-    return (int)hipErrorInvalidValue;
-  if (ssq_out && (epi != EPI_RESID || N % 256)) return (int)hipErrorInvalidValue;
-  if (epi == EPI_RESID && (!resid || ldr % 8 || ssq_in)) return (int)hipErrorInvalidValue;
-  if (ssq_in && (ssq_parts < 1 || norm_k < 1 || !(eps > 0.f))) return (int)hipErrorInvalidValue;
-  if (epi == EPI_ROPE && (N != (H + 2 * Hkv) * D || D % 8 || !pos || !slot || !cos_sin || !k_cache || !v_cache))
-    return (int)hipErrorInvalidValue;
-  if (epi == EPI_SWIGLU && N % 32) return (int)hipErrorInvalidValue;
-  GemmArgs a{};
-  a.A = (const bf16_t*)A; a.W = (const bf16_t*)W; a.C = (bf16_t*)C;
-  a.bias = (const bf16_t*)bias; a.resid = (const bf16_t*)resid;
-  a.M = M; a.N = N; a.K = K; a.lda = lda; a.ldc = ldc; a.ldr = ldr; a.k_per_split = K;
-  a.ssq_in = ssq_in; a.ssq_parts = ssq_parts; a.norm_k = norm_k; a.norm_eps = eps; a.ssq_out = ssq_out;
-  if (epi == EPI_ROPE)
-    a.rope = RopeArgs{(const int*)pos, (const int*)slot, (const float*)cos_sin, (bf16_t*)k_cache, (bf16_t*)v_cache,
-                      H, Hkv, D, max_seq};
-  const long t256 = (long)((M + 255) / 256) * ((N + 255) / 256);
-  const int bm = epi == EPI_ROPE ? (t256 >= 256 ? 256 : 128) : gemm8p_pick_bm(M, N);
-  return launch_gemm8p(a, epi, (hipStream_t)stream, bm);
 }
 
 // Tile selection: big tiles when the grid fills 256 CUs, skinny tiles (+ split-K) for decode-sized M.

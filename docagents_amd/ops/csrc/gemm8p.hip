@@ -175,29 +175,6 @@ gemm8p_kernel(GemmArgs p) {
   //      (DMA order per wave: ... A0 B0 B1(t+1) | A1(t+1) | A0 B0 B1(t+2) | A1(t+2) ...)
   ISSUE_A(0, 0, 0); ISSUE_B(0, 0, 0); ISSUE_B(1, 0, 0); ISSUE_A(1, 0, 0);
   ISSUE_A(0, 1, 1); ISSUE_B(0, 1, 1); ISSUE_B(1, 1, 1);
-  // deferred RMSNorm of A's rows (p.ssq_in, [M][parts]): thread (row r, group grp) sums parts
-  // [grp, grp + 1) * parts / G of its row while the prologue DMA is in flight (one round of 16-B
-  // loads), kept in one register until the epilogue
-  constexpr int G = 512 / BM;
-  float ssn = 0.f;
-  if (p.ssq_in) {
-    const int r = tid % BM, grp = tid / BM;
-    const float* src = p.ssq_in + (size_t)min(m0 + r, p.M - 1) * p.ssq_parts;
-    if (p.ssq_parts % (4 * G) == 0) {
-      const int per = p.ssq_parts / G;
-      src += grp * per;
-      for (int q0 = 0; q0 < per; q0 += 32) {
-        f32x4_t v[8];
-#pragma unroll
-        for (int u = 0; u < 8; ++u)
-          v[u] = q0 + 4 * u < per ? *(const f32x4_t*)(src + q0 + 4 * u) : f32x4_t{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int u = 0; u < 8; ++u) ssn += (v[u][0] + v[u][1]) + (v[u][2] + v[u][3]);
-      }
-    } else {
-      for (int q = grp; q < p.ssq_parts; q += G) ssn += src[q];
-    }
-  }
   vmcnt<CNT_AB>();
   bar();
   if (wg) bar();  // G1 runs one barrier behind
@@ -243,30 +220,6 @@ gemm8p_kernel(GemmArgs p) {
 #undef ISSUE_B
   __syncthreads();
 
-  // ---- deferred RMSNorm: inv per tile row from the G partial sums (fixed order: deterministic)
-  __shared__ float snorm[4][BM], sinv[BM];
-  if (p.ssq_in) {
-    snorm[tid / BM][tid % BM] = ssn;
-    __syncthreads();
-    if (tid < BM) {
-      float tot = 0.f;
-#pragma unroll
-      for (int g = 0; g < G; ++g) tot += snorm[g][tid];
-      sinv[tid] = rsqrtf(tot / p.norm_k + p.norm_eps);
-    }
-    __syncthreads();
-  }
-  // row scales of this thread's accumulator rows acc[ih][.][i][.][q] (tile row ih*BM/2 + wg*QR +
-  // i*16 + fg*4 + q), read once into registers (the K-loop fragments are dead here)
-  float rs[2][MI][4];
-#pragma unroll
-  for (int ih = 0; ih < 2; ++ih)
-#pragma unroll
-    for (int i = 0; i < MI; ++i)
-#pragma unroll
-      for (int q = 0; q < 4; ++q)
-        rs[ih][i][q] = p.ssq_in ? sinv[ih * (BM / 2) + wg * QR + i * 16 + fg * 4 + q] : 1.f;
-
   // ---- epilogue: registers -> (bias / GELU / SwiGLU) -> bf16 staging -> coalesced stores.
   //      Staged row lr = ih*QR + i*16 + fg*4 + q (tile row ih*BM/2 + wg*QR + (lr % QR)),
   //      staged column lc = jh*32 + j*16 + fr (tile column jh*128 + wn*32 + (lc & 31)).
@@ -282,8 +235,7 @@ gemm8p_kernel(GemmArgs p) {
         for (int i = 0; i < MI; ++i)
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
-            const float iv = rs[ih][i][q];
-            const float v = silu(acc[ih][jh][i][0][q] * iv) * (acc[ih][jh][i][1][q] * iv);
+            const float v = silu(acc[ih][jh][i][0][q]) * acc[ih][jh][i][1][q];
             *(bf16_t*)(st + (ih * QR + i * 16 + fg * 4 + q) * SROW + (jh * 16 + fr) * 2) = T::from_f(v);
           }
   } else {
@@ -307,7 +259,7 @@ gemm8p_kernel(GemmArgs p) {
           for (int j = 0; j < 2; ++j)
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
-              float v = acc[ih][jh][i][j][q] * rs[ih][i][q] + bv[jh][j];
+              float v = acc[ih][jh][i][j][q] + bv[jh][j];
               if constexpr (EPI == EPI_GELU) v = gelu_erf(v);
               *(bf16_t*)(st + (ih * QR + i * 16 + fg * 4 + q) * SROW + (jh * 32 + j * 16 + fr) * 2) = T::from_f(v);
             }
@@ -332,13 +284,9 @@ gemm8p_kernel(GemmArgs p) {
     rhead = rel / R.D;
     rd0 = rel % R.D;
   }
-  // EPI_RESID + ssq_out: the 8 lanes of a staged row (CPR = 8: two 32-column runs of this wave)
-  // also sum the squares of the bf16 values they store -> one part per (column tile, wave)
-  const bool ssq = EPI == EPI_RESID && p.ssq_out != nullptr;
   for (int lr = lane / CPR; lr < BM / 2; lr += RPI) {
     const int gm = m0 + (lr / QR) * (BM / 2) + wg * QR + (lr % QR);
-    const bool ok = gm < p.M && gcol < ncols;
-    if (!ssq && !ok) continue;
+    if (gm >= p.M || gcol >= ncols) continue;
     u32x4_t v = *(const u32x4_t*)(st + lr * SROW + (jh * HC + cc) * 2);
     if constexpr (EPI == EPI_ROPE) {
       // same bf16 roundings as GEMM -> rope_cache: rotate the bf16-rounded outputs in fp32
@@ -364,44 +312,25 @@ gemm8p_kernel(GemmArgs p) {
       }
     }
     if constexpr (EPI == EPI_RESID) {
-      if (ok) {
-        const u32x4_t r = *(const u32x4_t*)(p.resid + (size_t)gm * p.ldr + gcol);
+      const u32x4_t r = *(const u32x4_t*)(p.resid + (size_t)gm * p.ldr + gcol);
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const float lo = T::to_f((bf16_t)(v[e] & 0xffff)) + T::to_f((bf16_t)(r[e] & 0xffff));
-          const float hi = T::to_f((bf16_t)(v[e] >> 16)) + T::to_f((bf16_t)(r[e] >> 16));
-          v[e] = T::pack2(lo, hi);
-        }
-      }
-      if (ssq) {
-        float sq = 0.f;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const float lo = T::to_f((bf16_t)(v[e] & 0xffff)), hi = T::to_f((bf16_t)(v[e] >> 16));
-          sq += lo * lo + hi * hi;
-        }
-        if (!ok) sq = 0.f;
-#pragma unroll
-        for (int x = 1; x < CPR; x <<= 1) sq += __shfl_xor(sq, x, 64);
-        if (ch == 0 && gm < p.M) p.ssq_out[(size_t)gm * (p.N / 64) + (n0 / BN) * 4 + wn] = sq;
+      for (int e = 0; e < 4; ++e) {
+        const float lo = T::to_f((bf16_t)(v[e] & 0xffff)) + T::to_f((bf16_t)(r[e] & 0xffff));
+        const float hi = T::to_f((bf16_t)(v[e] >> 16)) + T::to_f((bf16_t)(r[e] >> 16));
+        v[e] = T::pack2(lo, hi);
       }
     }
-    if (ok) *(u32x4_t*)(p.C + (size_t)gm * p.ldc + gcol) = v;
+    *(u32x4_t*)(p.C + (size_t)gm * p.ldc + gcol) = v;
   }
 }
 
-// Grouped-M band height of the tile order: 0 = 4 (default); else forced (A/B: bench/gemm_group.py,
-// bench/ab_arms.py DA_GEMM8P_GROUP). Isolated GEMMs at M = 65536 ran 1.4-2.7 % faster with 2-row
-// bands on the wide / deep projections (profiles/r4/gemm_group.txt), but the QA prefill of the bench
-// on one box ran 0.8 % SLOWER with them (1173-1175 vs 1163-1166 ms, profiles/r4/rejected_r4.txt):
-// back-to-back repeats of one GEMM keep its operands cache-warm; the real layer sequence does not.
-static int g_8p_group = 0;
-DA_EXPORT void da_set_gemm8p_group(int v) { g_8p_group = v > 0 ? v : 0; }
-
+// Grouped-M band height of the tile order: 4 rows of tiles. (2-row bands ran isolated GEMMs at
+// M = 65536 1.4-2.7 % faster, profiles/r4/gemm_group.txt, but the bench's QA prefill 0.8 % slower,
+// profiles/r4/rejected_r4.txt: back-to-back repeats of one GEMM keep its operands cache-warm; the
+// real layer sequence does not.)
 template <int BM>
 static int launch8p(const GemmArgs& a0, int epi, hipStream_t s) {
   GemmArgs a = a0;
-  if (a.group <= 0) a.group = g_8p_group;
   if (a.group <= 0) a.group = 4;
   const int ntm = (a.M + BM - 1) / BM, ntn = (a.N + BN - 1) / BN;
   dim3 grid(ntm * ntn), block(512);
@@ -432,15 +361,11 @@ static int launch8p(const GemmArgs& a0, int epi, hipStream_t s) {
 // 128-row tiles took 0.61-0.73 of the 256-row tile time, profiles/r3/gemm_ab_batch1_prefill_tiles.txt).
 // At M ~ 2.6k (the batch-1 prefill of the p50 path) the O / down projections (N = 3072) then run
 // 252 128-row tiles in one wave instead of 132 256-row tiles on half the chip; QA-sized chunks
-// (M ~ 64k) keep 256. mode 0 (A/B, da_set_gemm8p_bm_rule): the round-3 rule, 256 rows once the
-// 256-row grid reaches half the chip.
-static int g_bm_rule = 1;
-DA_EXPORT void da_set_gemm8p_bm_rule(int v) { g_bm_rule = v; }
-
+// (M ~ 64k) keep 256 (the round-3 rule, 256 rows once the 256-row grid reached half the chip,
+// measured 65.5 vs 74.9 us per O projection at M ~ 2.6k: profiles/r4/bm_rule/).
 int gemm8p_pick_bm(int M, int N) {
   const long ntn = (N + 255) / 256;
   const long t256 = (long)((M + 255) / 256) * ntn, t128 = (long)((M + 127) / 128) * ntn;
-  if (!g_bm_rule) return t256 >= 128 ? 256 : 128;
   static int cus = 0;
   if (cus <= 0) {
     int dev = 0;

@@ -317,9 +317,6 @@ static int dk_launch1(const DkArgs& a, int epi, bool norm, hipStream_t s) {
   }
 }
 
-static int g_dk_rb = 1;  // 33..64 rows as two 32-row blocks (1) or one 64-row block (0), A/B
-DA_EXPORT void da_set_dk_rb(int v) { g_dk_rb = v; }
-
 // Number of ssq parts a RESID launch of width N writes (the consumer's ssq_parts).
 DA_EXPORT int da_gemm_dk_parts(int N) { return (N + dk_bn(N, EPI_RESID) - 1) / dk_bn(N, EPI_RESID); }
 
@@ -345,9 +342,7 @@ DA_EXPORT int da_gemm_dk(const void* A, int lda, const void* W, void* C, int ldc
   a.rb = 1;
   if (M <= 16) return dk_launch1<16>(a, epi, norm, s);
   if (M <= 32) return dk_launch1<32>(a, epi, norm, s);
-  if (g_dk_rb) {  // 33..64 rows: two 32-row blocks per n-tile (less A re-read per W byte)
-    a.rb = 2;
-    return dk_launch1<32>(a, epi, norm, s);
-  }
-  return dk_launch1<64>(a, epi, norm, s);
+  // 33..64 rows: two 32-row blocks per n-tile (less A re-read per W byte than one 64-row block)
+  a.rb = 2;
+  return dk_launch1<32>(a, epi, norm, s);
 }

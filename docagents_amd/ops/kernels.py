@@ -26,9 +26,6 @@ _LIB_PATH = Path(__file__).resolve().parent / ("_da_kernels_debug.so" if _DEBUG 
 
 EPI_NONE, EPI_BIAS, EPI_GELU, EPI_SWIGLU, EPI_RESID = 0, 1, 2, 3, 4
 EPI_ROPE = 6  # gemm8p only: QKV + RoPE + KV-cache write
-# flash prefill kernel choice: 2 = auto (software-pipelined kernel for causal D = 96), 1 / 0 = force
-# on / off; must match g_fa_pipe's initial value in attention.hip (tests restore it after an A/B arm)
-FLASH_PIPE_DEFAULT = 2
 
 c_longlong = ctypes.c_longlong
 c_void_p, c_int, c_float, c_uint, c_size_t = (ctypes.c_void_p, ctypes.c_int, ctypes.c_float,
@@ -39,8 +36,6 @@ _SIGS = {
                      c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_float, c_void_p],
     "da_gemm_rope": [c_void_p, c_int, c_void_p, c_void_p, c_int, c_int, c_int, c_int] + [c_void_p] * 5
                     + [c_int] * 4 + [c_void_p],
-    "da_gemm8p_norm": [c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
-                       c_int, c_void_p, c_int, c_int, c_float, c_void_p] + [c_void_p] * 5 + [c_int] * 4 + [c_void_p],
     "da_gemm_fp8": [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int,
                     c_int, c_int, c_int, c_int, c_void_p],
     "da_quant_fp8_rows": [c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p],
@@ -60,41 +55,12 @@ _SIGS = {
     "da_flash_attn_v2": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_int,
                          c_int, c_int, c_int, c_int, c_float, c_void_p, c_int, c_void_p, c_void_p, c_longlong,
                          c_int, c_void_p],
-    "da_set_gqa_mfma": [c_int],
     "da_malloc_uncached": [c_longlong, ctypes.POINTER(c_void_p)],
-    "da_set_flash_waves": [c_int],
-    "da_set_flash_qh": [c_int],
-    "da_set_flash_pipe": [c_int],
-    "da_set_gemm_pf": [c_int],
-    "da_set_gemm_db": [c_int],
-    "da_set_decode_balance": [c_int],
     "da_gemm_dk": [c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
                    c_int, c_void_p, c_int, c_int, c_float, c_void_p, c_void_p],
     "da_gemm_dk_parts": [c_int],
-    "da_gemm_dk_splitk_fused": [c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_int, c_int,
-                                c_int, c_int, c_void_p, c_int, c_int, c_float, c_void_p, c_void_p, c_int, c_void_p,
-                                c_void_p],
     "da_gemm_dk_splitk": [c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
                           c_int, c_void_p, c_int, c_int, c_float, c_void_p, c_void_p, c_int, c_void_p],
-    "da_set_dk_rb": [c_int],
-    "da_set_decode_qfirst": [c_int],
-    "da_set_gemv_u": [c_int],
-    "da_set_gemv_ks": [c_int],
-    "da_set_decode_pft": [c_int],
-    "da_set_decode_w8": [c_int],
-    "da_set_decode_w8_var": [c_int],
-    "da_set_gemm8p_group": [c_int],
-    "da_set_gemm8p_bm_rule": [c_int],
-    "da_set_omerge_shape": [c_int],
-    "da_gemm_dk_splitk_parts": [c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_void_p],
-    "da_decode_attn_qkvparts": [c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_float, c_void_p, c_void_p, c_void_p,
-                                c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_float, c_void_p,
-                                c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p],
-    "da_decode_attn_parts": [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int,
-                             c_int, c_int, c_int, c_int, c_float, c_void_p, c_void_p, c_void_p, c_void_p],
-    "da_gemv_omerge": [c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p,
-                       c_void_p],
-    "da_set_flash_rev": [c_int],
     "da_decode_attn": [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
                        c_int, c_int, c_int, c_float, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p,
                        c_void_p],
@@ -114,9 +80,6 @@ _SIGS = {
     "da_device_cu_count": [c_int, ctypes.POINTER(c_int)],
     "da_placement_probe": [c_void_p, c_int, c_longlong, c_void_p],
     "da_spin": [c_int, c_void_p, c_void_p],
-    "da_decode_b1": [c_void_p, c_int, c_int] + [c_void_p] * 4 + [c_void_p] * 5 + [c_int] * 7 + [c_float, c_float]
-                    + [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p],
-    "da_decode_b1_occupancy": [c_int, ctypes.POINTER(c_int)],
     "da_gemm_f16": [c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int,
                     c_void_p],
     "da_flash_attn_f16": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_int, c_int, c_int,
@@ -160,8 +123,6 @@ def lib() -> ctypes.CDLL:
             fn.restype = c_int
         L.da_topk_dense_ws.argtypes = [c_int, c_int, c_int, c_int]
         L.da_topk_dense_ws.restype = c_size_t
-        L.da_decode_b1_sync_bytes.argtypes = [c_int]
-        L.da_decode_b1_sync_bytes.restype = c_longlong
         _LIB = L
         return L
 
@@ -308,27 +269,6 @@ def _dk_splitk(M: int, N: int) -> bool:
     return DK_SPLITK_ABOVE < M <= 64 and N % 512 == 0
 
 
-# 33..64 rows: True = the split-K reduction inside the tile kernel (last split of each tile,
-# EPI_SPLITK) instead of separate reduce launches. Off: measured slower on the MI355X — the fused
-# tiles took 32.3 us each vs 16.0 us + the reduce launches' share (QA decode step 14.85 vs 13.35 ms,
-# profiles/r4/check_d_b1_fused_on/, profiles/r4/check_d/): the last arriver alone reads all S partial tiles of its tile cross-XCD
-# (up to 8 x 32 KB per workgroup at the per-block hand-off rate), where the reduce launch spreads the
-# same bytes over the whole chip. Bit-identical either way (tests/test_splitk_fused_gpu.py);
-# bench/ab_arms.py DA_SPLITK_FUSED=1 selects it.
-SPLITK_FUSED = False
-_SPLITK_CNT: dict = {}
-
-
-def _splitk_cnt(device) -> torch.Tensor:
-    """Per-(device, workspace role) tile arrival counters of the fused split-K tiles: zero, left zero
-    by every launch (the last split of a tile resets its counter); never freed (graphs keep it)."""
-    key = (device.index if device.index is not None else torch.cuda.current_device(), getattr(_ROLE, "name", "main"))
-    c = _SPLITK_CNT.get(key)
-    if c is None:
-        c = _SPLITK_CNT[key] = torch.zeros(4096, dtype=torch.int32, device=device)
-    return c
-
-
 def _dk_splits(N: int, K: int) -> int:
     """Split-K of the 33..64-row route (64x128 tiles): the largest of 2, 3, 4, 6, 8, 12, 16 that keeps
     the grid within one round of 256 workgroups and >= 4 K-steps of 64 per split; at least 2 (the
@@ -346,7 +286,7 @@ def dk_parts(N: int, M: int = 0) -> int:
     """Row-norm partial sums an EPI_RESID gemm_dk of width N and M rows writes (the consumer's part
     count): one per dk output tile, or one per 512 columns on the 33..64-row split-K route."""
     if _dk_splitk(M, N):
-        return N // 128 if SPLITK_FUSED else N // 512
+        return N // 512
     return int(lib().da_gemm_dk_parts(N))
 
 
@@ -380,13 +320,6 @@ def gemm_dk(a, w, epi: int = EPI_NONE, bias=None, resid=None, out=None, norm_in=
     if _dk_splitk(M, N) or (DK_SPLITK_ABOVE < M <= 64 and ssq_out is None):
         splits = _dk_splits(N, K)
         ws = _workspace(splits * M * N * 4, a.device)
-        if SPLITK_FUSED and N % 128 == 0:
-            _req((N // 128) <= 4096, "fused split-K: too many tiles")
-            _check(lib().da_gemm_dk_splitk_fused(_ptr(a), a.stride(0), _ptr(w), _ptr(out), out.stride(0), _ptr(bias),
-                                                 _ptr(resid), ldr, M, N, K, epi, _ptr(ssq), parts, K, float(eps),
-                                                 _ptr(ssq_out), _ptr(ws), splits, _ptr(_splitk_cnt(a.device)),
-                                                 _stream()), "gemm_dk_splitk_fused")
-            return out
         _check(lib().da_gemm_dk_splitk(_ptr(a), a.stride(0), _ptr(w), _ptr(out), out.stride(0), _ptr(bias), _ptr(resid),
                                        ldr, M, N, K, epi, _ptr(ssq), parts, K, float(eps), _ptr(ssq_out), _ptr(ws),
                                        splits, _stream()), "gemm_dk_splitk")
@@ -394,45 +327,6 @@ def gemm_dk(a, w, epi: int = EPI_NONE, bias=None, resid=None, out=None, norm_in=
     _check(lib().da_gemm_dk(_ptr(a), a.stride(0), _ptr(w), _ptr(out), out.stride(0), _ptr(bias), _ptr(resid), ldr,
                             M, N, K, epi, _ptr(ssq), parts, K, float(eps), _ptr(ssq_out), _stream()), "gemm_dk")
     return out
-
-
-class QKVParts:
-    """The 33..64-row QKV projection left as split-K partials (da_gemm_dk_splitk_parts) for the
-    decode attention to reduce in its prologue (decode_attn(q=QKVParts)): ws [splits][M][N] fp32 and
-    the deferred row norm (ssq [parts][64], eps; K = the norm width)."""
-    __slots__ = ("ws", "splits", "M", "N", "K", "ssq", "parts", "eps")
-
-    def __init__(self, ws, splits, M, N, K, ssq, parts, eps):
-        self.ws, self.splits, self.M, self.N, self.K = ws, splits, M, N, K
-        self.ssq, self.parts, self.eps = ssq, parts, eps
-
-    @property
-    def shape(self):
-        return (self.M, self.N)
-
-
-def qkv_parts_route(M: int, N: int, K: int) -> bool:
-    """True when gemm_dk(M x N x K) takes the split-K tiles whose reduce a consumer can absorb."""
-    return DECODE_DK and _dk_splitk(M, N) and K % 256 == 0 and not SPLITK_FUSED
-
-
-def gemm_dk_qkv_parts(a, w, norm_in=None) -> QKVParts:
-    """The QKV projection of a 33..64-row decode step without its reduce launch: the split-K
-    partials stay in the workspace for decode_attn to reduce (bit-identical to gemm_dk, which
-    reduces them in gemm_splitk_reduce). norm_in = gemm_dk's deferred RMSNorm (ssq, parts, eps)."""
-    _bf16_cuda(a, "a"); _bf16_cuda(w, "w")
-    M, K = a.shape
-    N = w.shape[0]
-    _req(qkv_parts_route(M, N, K) and w.shape[1] == K and w.is_contiguous(), f"gemm_dk_qkv_parts M={M} N={N} K={K}")
-    _req(a.stride(1) == 1 and a.stride(0) % 8 == 0, "gemm_dk_qkv_parts layout")
-    splits = _dk_splits(N, K)
-    ws = _workspace(splits * M * N * 4, a.device)
-    ssq, parts, eps = (None, 0, 0.0) if norm_in is None else norm_in
-    if ssq is not None:
-        _req(ssq.dtype == torch.float32 and ssq.is_contiguous() and ssq.numel() >= parts * 64, "bad ssq_in")
-    _check(lib().da_gemm_dk_splitk_parts(_ptr(a), a.stride(0), _ptr(w), M, N, K, _ptr(ws), splits, _stream()),
-           "gemm_dk_splitk_parts")
-    return QKVParts(ws, splits, M, N, K, ssq, parts, eps)
 
 
 # Every GEMM runs on the in-tree kernels: gemm8p (phase-split BMx256, csrc/gemm8p.hip) from 256
@@ -462,47 +356,6 @@ def gemm_rope(a, w, pos, cos_sin, H: int, Hkv: int, D: int, slot, k_cache, v_cac
     _check(lib().da_gemm_rope(_ptr(a), a.stride(0), _ptr(w), _ptr(out), out.stride(0), M, N, K, _ptr(pos), _ptr(slot),
                               _ptr(cos_sin), _ptr(k_cache), _ptr(v_cache), H, Hkv, D, k_cache.shape[2], _stream()),
            "gemm_rope")
-    return out
-
-
-def prefill_norm_fusable(M: int, K: int) -> bool:
-    """True when a prefill projection of M rows runs on the phase-split kernel, whose epilogues fold
-    the layer RMSNorms in (gemm8p_norm)."""
-    return M >= 640 and K % 64 == 0 and K >= 128
-
-
-def gemm8p_norm(a, w, epi: int, out=None, resid=None, bias=None, norm_in=None, ssq_out=None, rope=None):
-    """Prefill projection with the RMSNorms folded in (csrc/gemm.hip da_gemm8p_norm):
-    norm_in = (ssq [M, parts] fp32, parts, eps): ``a`` is the raw residual stream, each output row is
-    scaled by rsqrt(sum of its parts / K + eps) before the epilogue (gains folded into w);
-    ssq_out (EPI_RESID): fp32 [M, N // 64] receives per-64-column sums of squares of the new rows.
-    rope = (pos, cos_sin, H, Hkv, D, slot, k_cache, v_cache) for EPI_ROPE (QKV + RoPE + KV write)."""
-    _bf16_cuda(a, "a"); _bf16_cuda(w, "w")
-    M, K = a.shape
-    N = w.shape[0]
-    _req(prefill_norm_fusable(M, K) and w.shape[1] == K and a.stride(1) == 1 and a.stride(0) % 8 == 0
-         and w.is_contiguous(), f"gemm8p_norm shape M={M} N={N} K={K}")
-    nout = N // 2 if epi == EPI_SWIGLU else N
-    if out is None:
-        out = torch.empty((M, nout), dtype=torch.bfloat16, device=a.device)
-    _req(out.shape == (M, nout) and out.stride(1) == 1 and out.stride(0) % 8 == 0, "bad out")
-    ldr = 0
-    if epi == EPI_RESID:
-        _req(resid is not None and resid.shape == (M, N) and resid.stride(1) == 1, "bad resid")
-        ldr = resid.stride(0)
-    ssq, parts, eps = (None, 0, 0.0) if norm_in is None else norm_in
-    if ssq is not None:
-        _req(ssq.dtype == torch.float32 and ssq.numel() >= parts * M, "bad ssq_in")
-    if ssq_out is not None:
-        _req(ssq_out.dtype == torch.float32 and ssq_out.numel() >= (N // 64) * M, "bad ssq_out")
-    pos = cs = slot = kc = vc = None
-    H = Hkv = D = max_seq = 0
-    if epi == EPI_ROPE:
-        pos, cs, H, Hkv, D, slot, kc, vc = rope
-        max_seq = kc.shape[2]
-    _check(lib().da_gemm8p_norm(_ptr(a), a.stride(0), _ptr(w), _ptr(out), out.stride(0), _ptr(bias), _ptr(resid), ldr,
-                                M, N, K, epi, _ptr(ssq), parts, K, float(eps), _ptr(ssq_out), _ptr(pos), _ptr(slot),
-                                _ptr(cs), _ptr(kc), _ptr(vc), H, Hkv, D, max_seq, _stream()), "gemm8p_norm")
     return out
 
 
@@ -814,9 +667,6 @@ def decode_attn(q, k_cache, v_cache, lens, slot, H, Hkv, D, max_len: int, chunk:
     rope = (cos_sin fp32 [max_pos, D/2, 2], pos int32 [B]), MHA only: q is the raw qkv row
     [B, (H + 2 Hkv) D]; the kernel applies RoPE to q and the new token's k and writes that token's
     k / v into the cache at pos (== lens - 1) — the decode step's rope_cache launch folded in."""
-    if isinstance(q, QKVParts):
-        return _decode_attn_qkvparts(q, k_cache, v_cache, lens, slot, H, Hkv, D, max_len, chunk, scale, out, pre,
-                                     rope)
     cs, ps = _decode_checks(q, k_cache, v_cache, lens, slot, H, Hkv, D, max_len, pre, rope)
     chunk, nsplit = _decode_split(q.shape[0], Hkv, max_len, chunk)
     B = q.shape[0]
@@ -831,89 +681,6 @@ def decode_attn(q, k_cache, v_cache, lens, slot, H, Hkv, D, max_len: int, chunk:
     _check(lib().da_decode_attn(_ptr(q), q.stride(0), _ptr(k_cache), _ptr(v_cache), _ptr(lens), _ptr(slot), _ptr(pre), B, H,
                                 Hkv, D, k_cache.shape[2], chunk, nsplit, float(scale), _ptr(ws), _ptr(out), out.stride(0),
                                 _ptr(cnt), _ptr(cs), _ptr(ps), _stream()), "decode_attn")
-    return out
-
-
-def _decode_attn_qkvparts(qp: QKVParts, k_cache, v_cache, lens, slot, H, Hkv, D, max_len, chunk, scale, out, pre,
-                          rope):
-    """decode_attn with q / the new token's k and v reduced from the QKV projection's split-K
-    partials in the attention prologue (attention.hip da_decode_attn_qkvparts)."""
-    _req(rope is not None and H == Hkv and qp.N >= (H + 2 * Hkv) * D, "QKV partials: MHA with fused RoPE")
-    _i32(lens, "lens"); _i32(slot, "slot")
-    _req(D in (64, 96, 128) and k_cache.dim() == 4 and k_cache.shape[1] == Hkv and k_cache.shape[3] == D, "cache shape")
-    _req(max_len <= k_cache.shape[2] and k_cache.is_contiguous() and v_cache.is_contiguous(), "cache")
-    B = qp.M
-    _req(lens.numel() == B and slot.numel() == B, "lens / slot")
-    if pre is not None:
-        _i32(pre, "pre"); _req(pre.shape == (B, 2) and pre.is_contiguous(), "pre must be int32 [B, 2]")
-    cs, ps = rope
-    _i32(ps, "pos")
-    _req(cs.dtype == torch.float32 and cs.is_contiguous() and cs.shape[1] == D // 2 and cs.shape[2] == 2, "cos_sin")
-    chunk, nsplit = _decode_split(B, Hkv, max_len, chunk)
-    dev = k_cache.device
-    if out is None:
-        out = torch.empty((B, H * D), dtype=torch.bfloat16, device=dev)
-    scale = scale if scale is not None else 1.0 / math.sqrt(D)
-    ws = cnt = None
-    if nsplit > 1:  # never the attention's own workspace: the QKV partials live there
-        _req(_FUSED_COMBINE, "QKV partials: the in-kernel split merge")
-        cnt = _uncached("decode_cnt", B * Hkv * 4, dev)
-        ws = _uncached("decode_ws", B * H * nsplit * (D + 2) * 4, dev)
-    _check(lib().da_decode_attn_qkvparts(_ptr(qp.ws), qp.splits, qp.N, _ptr(qp.ssq), qp.parts, qp.K, float(qp.eps),
-                                         _ptr(k_cache), _ptr(v_cache), _ptr(lens), _ptr(slot), _ptr(pre), B, H, Hkv, D,
-                                         k_cache.shape[2], chunk, nsplit, float(scale), _ptr(ws), _ptr(out),
-                                         out.stride(0), _ptr(cnt), _ptr(cs), _ptr(ps), _stream()), "decode_attn_qkvparts")
-    return out
-
-
-class DecodeParts:
-    """Split partials of a one-row decode attention whose merge is left to the O projection
-    (da_decode_attn_parts -> da_gemv_omerge): the workspace and its split count."""
-    __slots__ = ("ws", "nsplit", "H", "D")
-
-    def __init__(self, ws, nsplit: int, H: int, D: int):
-        self.ws, self.nsplit, self.H, self.D = ws, nsplit, H, D
-
-
-def decode_parts_splits(Hkv: int, max_len: int) -> int:
-    """Split count decode_attn_parts would use (>= 2 is required for the merged O projection)."""
-    return _decode_split(1, Hkv, max_len, 0)[1]
-
-
-def decode_attn_parts(q, k_cache, v_cache, lens, slot, H, Hkv, D, max_len: int, scale=None, pre=None,
-                      rope=None) -> DecodeParts:
-    """decode_attn for ONE row (batch-1 decode) without the split merge: the launch ends at the
-    splits' fp32 partials and ``gemv_omerge`` merges them on the O projection's input load (no
-    arrival ticket and no last-split merge on the attention's critical path). Same arguments as
-    decode_attn; needs >= 2 splits (decode_parts_splits)."""
-    cs, ps = _decode_checks(q, k_cache, v_cache, lens, slot, H, Hkv, D, max_len, pre, rope)
-    _req(q.shape[0] == 1, "decode_attn_parts: one row")
-    chunk, nsplit = _decode_split(1, Hkv, max_len, 0)
-    _req(2 <= nsplit <= 16, "decode_attn_parts: needs 2..16 splits")
-    ws = _workspace(H * nsplit * (D + 2) * 4, q.device)
-    scale = scale if scale is not None else 1.0 / math.sqrt(D)
-    _check(lib().da_decode_attn_parts(_ptr(q), q.stride(0), _ptr(k_cache), _ptr(v_cache), _ptr(lens), _ptr(slot),
-                                      _ptr(pre), 1, H, Hkv, D, k_cache.shape[2], chunk, nsplit, float(scale), _ptr(ws),
-                                      _ptr(cs), _ptr(ps), _stream()), "decode_attn_parts")
-    return DecodeParts(ws, nsplit, H, D)
-
-
-def gemv_omerge(parts: DecodeParts, w, resid=None, out=None, bias=None, attn_out=None):
-    """out[1, N] = resid + bias + merge(parts) @ w^T: the batch-1 O projection reading the decode
-    attention's split partials (bit-identical to decode_attn + gemm(EPI_RESID)). attn_out
-    (optional [1, H*D] bf16) also receives the merged attention row."""
-    _bf16_cuda(w, "w")
-    N, K = w.shape
-    _req(K == parts.H * parts.D and K % 512 == 0 and K <= 4096 and w.is_contiguous(), f"gemv_omerge shape N={N} K={K}")
-    if out is None:
-        out = torch.empty((1, N), dtype=torch.bfloat16, device=w.device)
-    _req(out.numel() == N and out.is_contiguous() and out.dtype == torch.bfloat16, "gemv_omerge out")
-    if resid is not None:
-        _req(resid.numel() == N and resid.is_contiguous() and resid.dtype == torch.bfloat16, "gemv_omerge resid")
-    if attn_out is not None:
-        _req(attn_out.numel() == K and attn_out.is_contiguous() and attn_out.dtype == torch.bfloat16, "attn_out")
-    _check(lib().da_gemv_omerge(_ptr(parts.ws), parts.nsplit, parts.D, _ptr(w), _ptr(out), _ptr(resid), _ptr(bias), N, K,
-                                _ptr(attn_out), _stream()), "gemv_omerge")
     return out
 
 
@@ -1108,103 +875,6 @@ def spin(us: int, device=None) -> None:
     _check(lib().da_spin(int(us), None, _stream()), "da_spin")
 
 
-# ----------------------------------------------------------------------------------- batch-1 decode
-_B1_BUFS: dict = {}
-_B1_GRID: dict = {}
-
-
-def _stream_cus(device) -> int:
-    """CUs the current stream may dispatch to (a CU-masked serving lane has fewer than the chip)."""
-    n = torch.cuda.get_device_properties(device).multi_processor_count
-    words = (n + 31) // 32
-    mask = (c_uint * words)()
-    if lib().da_stream_get_cumask(_stream(), words, mask) == 0:
-        bits = sum(bin(int(m)).count("1") for m in mask)
-        if 0 < bits <= n:
-            return bits
-    return n
-
-
-def decode_b1_grid(D: int, device) -> int:
-    """Workgroups of the persistent batch-1 decode launch: every one must be resident at once (they
-    wait on each other), so (CUs of the current stream) x (resident workgroups per CU)."""
-    occ = c_int(0)
-    _check(lib().da_decode_b1_occupancy(D, ctypes.byref(occ)), "decode_b1_occupancy")
-    _req(occ.value >= 1, "decode_b1: kernel does not fit on a CU")
-    return _stream_cus(device) * occ.value
-
-
-def decode_b1(layers, l0: int, l1: int, x, qkv, attn, act, lens, slot, pre, pos, cos_sin, H: int, D: int, F: int,
-              max_seq: int, eps: float, lm_head=None, logits=None, max_len: int | None = None, scale=None):
-    """Batch-1 decode of layers [l0, l1) as ONE persistent launch (ops/csrc/decode_b1.hip), plus the
-    LM head when ``lm_head`` is given (logits [1, V]). ``layers``: int64 device tensor [L, 6] of the
-    per-layer pointers (wqkv, wo, w_gu, w_down, k cache, v cache). x / qkv / attn / act: the decode
-    state's row buffers (x in: the token's embedding; out: the residual stream after the last
-    layer). Same split count as ``decode_attn`` at this capacity, same bits as the per-kernel path."""
-    dev = x.device
-    Hd = H * D
-    for t, n, nm in ((x, Hd, "x"), (qkv, 3 * Hd, "qkv"), (attn, Hd, "attn"), (act, F, "act")):
-        _bf16_cuda(t, nm)
-        _req(t.is_contiguous() and t.numel() == n, f"decode_b1: {nm} must be contiguous with {n} elements")
-    _i32(lens, "lens"); _i32(slot, "slot"); _i32(pos, "pos")
-    _req(lens.numel() == 1 and slot.numel() == 1 and pos.numel() == 1, "decode_b1: batch 1")
-    if pre is not None:
-        _i32(pre, "pre"); _req(pre.numel() == 2, "pre must be int32 [1, 2]")
-    _req(layers.dtype == torch.int64 and layers.is_cuda and layers.dim() == 2 and layers.shape[1] == 6
-         and 0 <= l0 < l1 <= layers.shape[0], "decode_b1: layer table")
-    _req(cos_sin.dtype == torch.float32 and cos_sin.is_contiguous() and cos_sin.shape[1] == D // 2, "cos_sin")
-    _req(Hd == 3072 and F == 8192 and D in (64, 96, 128), "decode_b1: instantiated for hidden 3072 / FFN 8192")
-    max_len = max_seq if max_len is None else max_len
-    want = max_len * Hd // D / 768  # decode_attn's auto chunk for B = 1
-    chunk = 512
-    while chunk < want and chunk < 4096:
-        chunk *= 2
-    nsplit = max(1, math.ceil(max_len / chunk))
-    V = 0
-    if lm_head is not None:
-        _bf16_cuda(lm_head, "lm_head")
-        V = lm_head.shape[0]
-        _req(lm_head.shape[1] == Hd and lm_head.is_contiguous() and V % 16 == 0, "lm_head")
-        _req(logits is not None and logits.numel() == V and logits.is_contiguous(), "logits")
-        _bf16_cuda(logits, "logits")
-    key = (dev.index, H, D, nsplit)
-    bufs = _B1_BUFS.get(key)
-    if bufs is None:  # kept for the process: a captured graph points at them
-        sb = int(lib().da_decode_b1_sync_bytes(H))
-        bufs = (torch.zeros(H * nsplit * (D + 2), dtype=torch.float32, device=dev),
-                torch.zeros((sb + 15) // 16 * 4, dtype=torch.int32, device=dev))
-        _B1_BUFS[key] = bufs
-    ws, sync = bufs
-    gkey = (dev.index, D, torch.cuda.current_stream().cuda_stream)  # a CU-masked lane has fewer CUs
-    grid = _B1_GRID.get(gkey)
-    if grid is None:
-        grid = _B1_GRID[gkey] = decode_b1_grid(D, dev)
-    scale = scale if scale is not None else 1.0 / math.sqrt(D)
-    _check(lib().da_decode_b1(_ptr(layers), l0, l1, _ptr(x), _ptr(qkv), _ptr(attn), _ptr(act), _ptr(lens), _ptr(slot),
-                              _ptr(pre), _ptr(pos), _ptr(cos_sin), Hd, H, D, F, max_seq, nsplit, chunk, float(eps),
-                              float(scale), _ptr(ws), _ptr(sync), _ptr(lm_head), _ptr(logits), V, grid, _stream()),
-           "decode_b1")
-
-
-def decode_b1_error(device=None, reset: bool = False) -> int:
-    """The persistent decode's error word on ``device`` (0 = ok; else the code of the first wait that
-    timed out — it stays set, and makes every later launch leave at once, until ``reset``). Reads
-    device memory: synchronises."""
-    dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
-    err = 0
-    for (idx, *_), (_, sync) in _B1_BUFS.items():
-        if idx == dev.index:
-            v = int(sync[0].item())
-            err = err or v
-            if reset:
-                sync.zero_()
-    return err
-
-
-# ----------------------------------------------------------------------------------- fp16 encoder
-# DTYPE=fp16 (BASELINE config 4's "fp16 embedder"): the encoder's GEMMs (v_mfma_f32_16x16x32_f16 on
-# the phase-split tile), flash attention (32x32x16 f16), LayerNorm / embeddings / pooling on fp16
-# rows; fp32 accumulation everywhere. Same kernels as bf16, instantiated on the fp16 element type.
 def _f16_cuda(t, name):
     _req(t.is_cuda, f"{name} must be on GPU")
     _req(t.dtype == torch.float16, f"{name} must be fp16, got {t.dtype}")

@@ -151,38 +151,6 @@ def gemm_rope(a, w, pos, cos_sin, H, Hkv, D, slot, k_cache, v_cache, out=None):
     return rope_cache(qkv, pos, cos_sin, H, Hkv, D, slot=slot, k_cache=k_cache, v_cache=v_cache)
 
 
-def prefill_norm_fusable(M, K):
-    return M >= 640 and K % 64 == 0 and K >= 128
-
-
-def gemm8p_ssq_parts(y):
-    """[M, N / 64] per-part sums of squares as gemm8p's EPI_RESID store loop forms them: part
-    (tile t, wave column wn) holds columns 256 t + 32 wn + [0, 32) and 256 t + 128 + 32 wn + [0, 32)
-    (a consumer only uses the sum over parts)."""
-    M, N = y.shape
-    return y.float().pow(2).view(M, N // 256, 2, 4, 32).sum((2, 4)).reshape(M, N // 64)
-
-
-def gemm8p_norm(a, w, epi, out=None, resid=None, bias=None, norm_in=None, ssq_out=None, rope=None):
-    """gemm.hip da_gemm8p_norm: rows of the raw ``a`` scaled by rsqrt(sum of the ssq parts / K + eps)
-    after the product (fp32), then the epilogue; EPI_RESID + ssq_out: per-64-column sums of squares
-    of the bf16 output rows ([M][N / 64], gemm8p_ssq_parts); EPI_ROPE: rope + KV write of the bf16 result."""
-    M, K = a.shape
-    N = w.shape[0]
-    y = a.float() @ w.float().t()
-    if norm_in is not None:
-        ssq, parts, eps = norm_in
-        y = y * torch.rsqrt(ssq.reshape(-1)[:parts * M].view(M, parts).sum(1) / K + eps)[:, None]
-    if epi == EPI_ROPE:
-        pos, cs, H, Hkv, D, slot, kc, vc = rope
-        qkv = _epilogue(y, N, bias, EPI_NONE, None, out)
-        return rope_cache(qkv, pos, cs, H, Hkv, D, slot=slot, k_cache=kc, v_cache=vc)
-    y = _epilogue(y, N, bias, epi, resid, out)
-    if ssq_out is not None:
-        ssq_out.reshape(-1)[:(N // 64) * M].view(M, N // 64)[:] = gemm8p_ssq_parts(y)
-    return y
-
-
 def rope_cache(qkv, pos, cos_sin, H, Hkv, D, slot=None, k_cache=None, v_cache=None, rotate_q=True):
     T = qkv.shape[0]
     x = qkv.view(T, H + 2 * Hkv, D)
@@ -235,9 +203,7 @@ def decode_attn(q, k_cache, v_cache, lens, slot, H, Hkv, D, max_len=None, chunk=
                 rope=None):
     """pre: optional int32 [B, 2] = (P, prefix slot): keys [0, P) of row b come from the prefix slot.
     rope = (cos_sin, pos): q is the raw qkv row; RoPE + the new token's cache write happen here
-    (rope_cache on a copy of the rows, then attention). q may be a QKVParts (gemm_dk_qkv_parts)."""
-    if isinstance(q, QKVParts):
-        q = q.qkv
+    (rope_cache on a copy of the rows, then attention)."""
     if rope is not None:
         q = rope_cache(q.clone(), rope[1], rope[0], H, Hkv, D, slot=slot, k_cache=k_cache, v_cache=v_cache)
     scale = scale if scale is not None else 1.0 / math.sqrt(D)
@@ -261,81 +227,6 @@ def decode_attn(q, k_cache, v_cache, lens, slot, H, Hkv, D, max_len=None, chunk=
         out.copy_(res)
         return out
     return res
-
-
-def _decode_split(B, Hkv, max_len, chunk=0):
-    """kernels._decode_split: (keys per split, split count) fixed by the cache capacity."""
-    if chunk <= 0:
-        want, chunk = max_len * B * Hkv / 768, 512
-        while chunk < want and chunk < 4096:
-            chunk *= 2
-    return chunk, max(1, math.ceil(max_len / chunk))
-
-
-def decode_parts_splits(Hkv, max_len):
-    return _decode_split(1, Hkv, max_len)[1]
-
-
-class DecodeParts:
-    """One row's split partials: unnormalised O [H, S, D], maxima (log2 domain) and sums [H, S]."""
-
-    def __init__(self, po, pm, pl, D):
-        self.po, self.pm, self.pl, self.D = po, pm, pl, D
-        self.H, self.nsplit = pm.shape
-
-
-def decode_attn_parts(q, k_cache, v_cache, lens, slot, H, Hkv, D, max_len=None, scale=None, pre=None, rope=None):
-    """decode_attn of one row stopped at the split partials (attention.hip da_decode_attn_parts):
-    the row's L keys spread over the launch's splits in 64-key multiples (dec_chunk), each split's
-    online-softmax state (O unnormalised, running max in the log2 domain, sum) in fp32."""
-    if rope is not None:
-        q = rope_cache(q.clone(), rope[1], rope[0], H, Hkv, D, slot=slot, k_cache=k_cache, v_cache=v_cache)
-    assert q.shape[0] == 1, "decode_attn_parts: one row"
-    chunk_arg, S = _decode_split(1, Hkv, max_len if max_len is not None else k_cache.shape[2])
-    assert S >= 2, "decode_attn_parts: needs >= 2 splits"
-    scale = scale if scale is not None else 1.0 / math.sqrt(D)
-    L, s = int(lens[0]), int(slot[0])
-    kk, vv = k_cache[s, :, :L].float(), v_cache[s, :, :L].float()
-    if pre is not None and int(pre[0, 0]) > 0:
-        P, ps = int(pre[0, 0]), int(pre[0, 1])
-        kk = torch.cat([k_cache[ps, :, :P].float(), kk[:, P:]], 1)
-        vv = torch.cat([v_cache[ps, :, :P].float(), vv[:, P:]], 1)
-    G = H // Hkv
-    kk, vv = kk.repeat_interleave(G, 0), vv.repeat_interleave(G, 0)
-    sc = (q[0, :H * D].float().view(H, 1, D) @ kk.transpose(1, 2))[:, 0] * (scale * 1.4426950408889634)  # [H, L]
-    c = min(((L + S - 1) // S + 63) & ~63, chunk_arg)
-    po = torch.zeros((H, S, D), dtype=torch.float32, device=q.device)
-    pm = torch.full((H, S), -math.inf, dtype=torch.float32, device=q.device)
-    pl = torch.zeros((H, S), dtype=torch.float32, device=q.device)
-    for j in range(S):
-        a, b = j * c, min(L, (j + 1) * c)
-        if a >= b:
-            continue
-        m = sc[:, a:b].max(dim=1).values
-        p = torch.exp2(sc[:, a:b] - m[:, None])
-        pm[:, j], pl[:, j] = m, p.sum(dim=1)
-        po[:, j] = (p[:, None, :] @ vv[:, a:b])[:, 0]
-    return DecodeParts(po, pm, pl, D)
-
-
-def merge_parts(parts):
-    """[1, H*D] fp32 attention row from the split partials (the combine every split-KV path runs)."""
-    M = parts.pm.max(dim=1, keepdim=True).values
-    Mu = torch.where(torch.isinf(M), torch.zeros_like(M), M)
-    f = torch.exp2(parts.pm - Mu)  # empty splits: exp2(-inf) = 0
-    lsum = (parts.pl * f).sum(dim=1)
-    o = (parts.po * f[:, :, None]).sum(dim=1) / torch.where(lsum > 0, lsum, torch.ones_like(lsum))[:, None]
-    return o.reshape(1, -1)
-
-
-def gemv_omerge(parts, w, resid=None, out=None, bias=None, attn_out=None):
-    """resid + bias + merge(parts) @ w^T, the merged row rounded to bf16 first (gemm.hip
-    da_gemv_omerge)."""
-    a = merge_parts(parts).to(torch.bfloat16)
-    if attn_out is not None:
-        attn_out.copy_(a.view_as(attn_out))
-    return gemm(a, w, bias=bias, epi=EPI_RESID if resid is not None else EPI_NONE,
-                resid=None if resid is None else resid.view(1, -1), out=out)
 
 
 def log_softmax_rows(logits):
@@ -574,34 +465,13 @@ def dk_fusable(M, N, K, epi=EPI_NONE):
             and epi in (EPI_NONE, EPI_BIAS, EPI_RESID, EPI_SWIGLU) and (epi != EPI_SWIGLU or N % 32 == 0))
 
 
-SPLITK_FUSED = False  # mirrors kernels.SPLITK_FUSED (bench/ab_arms.py flips both)
-
-
 def dk_parts(N, M=0):
     """gemm_dk.hip dk_bn for EPI_RESID: row-norm partial sums written per output tile; 33..64 rows
-    (the split-K route): one per 128-column tile when the reduction runs in the tile kernel
-    (gemm.hip splitk_fused_epilogue), one per 512 columns with the reduce launch."""
+    (the split-K route): one per 512 columns (written by the reduce launch)."""
     if DK_SPLITK_ABOVE < M <= 64 and N % 512 == 0:
-        return N // 128 if SPLITK_FUSED else N // 512
+        return N // 512
     bn = 64 if N // 64 >= 192 else (32 if N // 32 >= 192 else 16)
     return (N + bn - 1) // bn
-
-
-def qkv_parts_route(M, N, K):
-    """kernels.qkv_parts_route: the 33..64-row split-K route whose reduce the attention absorbs."""
-    return DECODE_DK and DK_SPLITK_ABOVE < M <= 64 and N % 512 == 0 and K % 256 == 0 and not SPLITK_FUSED
-
-
-class QKVParts:
-    """kernels.QKVParts stand-in: the oracle keeps the finished projection (there are no partials)."""
-
-    def __init__(self, qkv):
-        self.qkv = qkv
-        self.shape = qkv.shape
-
-
-def gemm_dk_qkv_parts(a, w, norm_in=None):
-    return QKVParts(gemm_dk(a, w, norm_in=norm_in))
 
 
 def gemm_dk(a, w, epi=EPI_NONE, bias=None, resid=None, out=None, norm_in=None, ssq_out=None):

@@ -91,22 +91,29 @@ def _send_frame(sock, obj) -> None:
     sock.sendall(pack(obj))
 
 
-def _recv_exact(sock, n: int) -> bytes:
+def _recv_exact(sock, n: int, stopped=None) -> bytes:
+    """n bytes from ``sock``. A socket with a timeout (the requester side: its timeout bounds SENDS)
+    keeps waiting through idle timeouts, the partial frame kept, until ``stopped()``."""
     buf = bytearray()
     while len(buf) < n:
-        b = sock.recv(n - len(buf))
+        try:
+            b = sock.recv(n - len(buf))
+        except socket.timeout:
+            if stopped is not None and stopped():
+                raise ConnectionError("search plane stopped") from None
+            continue
         if not b:
             raise ConnectionError("peer closed the connection")
         buf += b
     return bytes(buf)
 
 
-def _recv_frame(sock):
+def _recv_frame(sock, stopped=None):
     from ..engine.rpc import unpack
-    n = struct.unpack(">I", _recv_exact(sock, 4))[0]
+    n = struct.unpack(">I", _recv_exact(sock, 4, stopped))[0]
     if n > (256 << 20):
         raise ConnectionError(f"oversized search frame ({n} B)")
-    return unpack(_recv_exact(sock, n))
+    return unpack(_recv_exact(sock, n, stopped))
 
 
 class ShardUnavailable(RuntimeError):
@@ -114,15 +121,19 @@ class ShardUnavailable(RuntimeError):
 
 
 _REPLY_BACKLOG = 4096  # queued replies per requester connection before the shard drops it
+_SEND_BACKLOG = 1024   # queued request frames per peer before new parts fail fast
+_QUEUED_ROWS_MAX = 1 << 16  # query rows queued on a shard before it refuses more (overload)
 
 
 class _Job:
     """One part of a search on the local shard: rows [m, d] + per-row filters, and where the answer
-    goes (``reply(scores, keys)`` / ``fail(exc)``)."""
-    __slots__ = ("vecs", "k", "thr", "filters", "reply", "fail")
+    goes (``reply(scores, keys)`` / ``fail(exc)``); ``deadline`` (monotonic s, None = none): past it
+    the requester has given up, so the scan worker drops the job instead of scanning it."""
+    __slots__ = ("vecs", "k", "thr", "filters", "reply", "fail", "deadline")
 
-    def __init__(self, vecs, k, thr, filters, reply, fail):
+    def __init__(self, vecs, k, thr, filters, reply, fail, deadline=None):
         self.vecs, self.k, self.thr, self.filters, self.reply, self.fail = vecs, k, thr, filters, reply, fail
+        self.deadline = deadline
 
 
 class _Search:
@@ -138,15 +149,19 @@ class _Search:
 
 
 class _Peer:
-    """Client side of one remote shard: a persistent connection, its reader thread, the pending
-    parts. A failed connection fails only its own pending parts; the next request reconnects
-    (at most once per ``retry_s``), so a restarted rank rejoins without any coordination."""
+    """Client side of one remote shard: a persistent connection, its writer and reader threads, the
+    pending parts. ``send`` never blocks its caller (the engine's event loop): it queues the frame
+    for the writer thread, which connects (bounded by connect_timeout_s) and sends (bounded by
+    send_timeout_s: a peer that accepts but stops reading is marked down when its receive buffer
+    stays full that long). A failed connection fails only its own pending parts; the next request
+    reconnects (at most once per ``retry_s``), so a restarted rank rejoins without coordination."""
 
     def __init__(self, plane, rank: int, addr):
         self.plane, self.rank, self.addr = plane, rank, tuple(addr)
         self.sock = None
         self.lock = threading.Lock()   # sock / pending (the reader takes it per reply)
-        self.wlock = threading.Lock()  # one request frame at a time on the wire
+        self.q: queue.Queue = queue.Queue(maxsize=_SEND_BACKLOG)
+        self.writer = None
         self.pending: dict = {}
         self.down_since = None
         self.last_try = 0.0
@@ -159,7 +174,7 @@ class _Peer:
         self.last_try = now
         try:
             s = socket.create_connection(self.addr, timeout=self.plane.connect_timeout_s)
-            s.settimeout(None)
+            s.settimeout(self.plane.send_timeout_s)  # bounds every sendall (the reader rides idle timeouts)
             s.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
         except OSError as e:
             self.down_since = self.down_since or now
@@ -170,30 +185,49 @@ class _Peer:
         threading.Thread(target=self._read_loop, args=(s,), name=f"plane-peer-{self.rank}", daemon=True).start()
 
     def send(self, rid: int, msg: dict, on_reply, on_fail):
-        sock = None
+        """Queue one request frame (never blocks: a full backlog fails the part at once)."""
+        with self.lock:
+            if self.writer is None:
+                self.writer = threading.Thread(target=self._write_loop, name=f"plane-send-{self.rank}", daemon=True)
+                self.writer.start()
         try:
-            with self.lock:
-                if self.sock is None:
-                    self._connect()
-                self.pending[rid] = (on_reply, on_fail)
-                sock = self.sock
-            # the frame goes out under the write lock only: a send blocked on a slow shard's full
-            # receive buffer never holds up the reader thread that delivers this peer's replies
-            with self.wlock:
+            self.q.put_nowait((rid, msg, on_reply, on_fail))
+        except queue.Full:
+            on_fail(ShardUnavailable(f"search shard {self.rank}: {_SEND_BACKLOG} requests already queued"))
+
+    def _write_loop(self):
+        while not self.plane._stop:
+            try:
+                item = self.q.get(timeout=0.5)
+            except queue.Empty:
+                continue
+            rid, msg, on_reply, on_fail = item
+            if self.plane._stop:
+                on_fail(RuntimeError("search plane stopped"))
+                continue
+            sock = None
+            try:
+                with self.lock:
+                    if self.sock is None:
+                        self._connect()
+                    self.pending[rid] = (on_reply, on_fail)
+                    sock = self.sock
+                # outside the lock: a send blocked on a slow shard's full receive buffer never holds
+                # up the reader thread that delivers this peer's replies
                 _send_frame(sock, msg)
-        except ShardUnavailable as e:
-            on_fail(e)
-        except OSError as e:
-            self._down(sock, e)
-        except Exception as e:  # noqa: BLE001 - e.g. an unserialisable request: fails this part only
-            with self.lock:
-                self.pending.pop(rid, None)
-            on_fail(e)
+            except ShardUnavailable as e:
+                on_fail(e)
+            except OSError as e:  # incl. socket.timeout: the shard stopped reading
+                self._down(sock, e)
+            except Exception as e:  # noqa: BLE001 - e.g. an unserialisable request: fails this part only
+                with self.lock:
+                    self.pending.pop(rid, None)
+                on_fail(e)
 
     def _read_loop(self, sock):
         try:
             while True:
-                msg = _recv_frame(sock)
+                msg = _recv_frame(sock, stopped=lambda: self.plane._stop or self.sock is not sock)
                 with self.lock:
                     cb = self.pending.pop(msg.get("id"), None)
                 if cb is None:
@@ -243,14 +277,14 @@ class SearchPlane:
 
     def __init__(self, index, rank: int = 0, world: int = 1, device=None, stream=None, owner=None,
                  host: str = "127.0.0.1", port: int = 0, timeout_s: float = 30.0, max_rows: int = 1024,
-                 retry_s: float = 1.0, connect_timeout_s: float = 2.0):
+                 retry_s: float = 1.0, connect_timeout_s: float = 2.0, send_timeout_s: float = 5.0):
         self.index, self.rank, self.world = index, rank, max(1, world)
         self.device = torch.device(device) if device is not None else getattr(index, "device", torch.device("cpu"))
         self.stream = stream  # None: a high-priority stream created by the scan worker
         self.owner = owner or (lambda d: owner_of(d, self.world))
         self.host, self.port = host, port
         self.timeout_s, self.max_rows = timeout_s, max_rows
-        self.retry_s, self.connect_timeout_s = retry_s, connect_timeout_s
+        self.retry_s, self.connect_timeout_s, self.send_timeout_s = retry_s, connect_timeout_s, send_timeout_s
         self.addrs = None
         self.peers: dict[int, _Peer] = {}
         self.jobs: collections.deque = collections.deque()
@@ -264,7 +298,8 @@ class SearchPlane:
         self._conns: list = []
         self.error = ""
         self.stats = {"searches": 0, "local_parts": 0, "remote_parts": 0, "served_remote": 0, "scans": 0,
-                      "rows": 0, "busy_s": 0.0, "failed": 0}
+                      "rows": 0, "busy_s": 0.0, "failed": 0, "refused": 0, "expired": 0}
+        self._queued_rows = 0
 
     # ------------------------------------------------------------------ lifecycle
     def listen(self) -> tuple:
@@ -401,7 +436,8 @@ class SearchPlane:
                 self._enqueue(_Job(sub, k, thr, flt, reply, fail))
             else:
                 self.stats["remote_parts"] += 1
-                self.peers[r].send(sid, {"id": sid, "vecs": sub, "k": k, "thr": thr, "filters": flt}, reply, fail)
+                self.peers[r].send(sid, {"id": sid, "vecs": sub, "k": k, "thr": thr, "filters": flt,
+                                         "ttl": self.timeout_s}, reply, fail)
         return fut
 
     def _part_done(self, sid: int, rank: int, part, exc):
@@ -449,6 +485,7 @@ class SearchPlane:
                 self._part_done(sid, r, None, exc)
         with self.cv:
             jobs, self.jobs = list(self.jobs), collections.deque()
+            self._queued_rows = 0
         for j in jobs:
             j.fail(exc)
 
@@ -508,9 +545,11 @@ class SearchPlane:
                     send({"id": rid, "error": f"bad request: {e}"})
                     continue
                 self.stats["served_remote"] += 1
+                ttl = msg.get("ttl")
                 self._enqueue(_Job(vecs, k, float(msg["thr"]), flt,
                                    lambda s, g, rid=rid: send({"id": rid, "scores": s, "keys": g}),
-                                   lambda e, rid=rid: send({"id": rid, "error": repr(e)})))
+                                   lambda e, rid=rid: send({"id": rid, "error": repr(e)}),
+                                   None if ttl is None else time.monotonic() + float(ttl)))
         except Exception:  # noqa: BLE001 - EOF / reset: the requester's side handles it
             pass
         finally:
@@ -523,19 +562,37 @@ class SearchPlane:
                 pass
 
     def _enqueue(self, job: _Job):
+        """Queue a part for the scan worker; a shard already holding _QUEUED_ROWS_MAX query rows
+        (its scan worker stalled: a GPU hang, a long IVF train) refuses it instead of growing."""
         with self.cv:
-            self.jobs.append(job)
-            self.cv.notify()
+            if self._queued_rows + job.vecs.shape[0] > _QUEUED_ROWS_MAX:
+                over = True
+            else:
+                over = False
+                self.jobs.append(job)
+                self._queued_rows += job.vecs.shape[0]
+                self.cv.notify()
+        if over:
+            self.stats["refused"] += 1
+            job.fail(ShardUnavailable(f"search shard {self.rank} overloaded ({_QUEUED_ROWS_MAX} rows queued)"))
 
     def _take(self) -> list[_Job]:
-        out, n = [], 0
+        out, n, expired = [], 0, []
         with self.cv:
             while not self.jobs and not self._stop:
                 self.cv.wait(0.5)
+            now = time.monotonic()
             while self.jobs and (not out or n + self.jobs[0].vecs.shape[0] <= self.max_rows):
                 j = self.jobs.popleft()
+                self._queued_rows -= j.vecs.shape[0]
+                if j.deadline is not None and now > j.deadline:
+                    expired.append(j)  # its requester has given up: do not scan it
+                    continue
                 out.append(j)
                 n += j.vecs.shape[0]
+        for j in expired:
+            self.stats["expired"] += 1
+            j.fail(TimeoutError("search part expired in the shard's queue"))
         return out
 
     def _scan_loop(self):

@@ -88,7 +88,7 @@ def chunk_text_native(text: str, opts: Options | None = None) -> list[Chunk]:
     nchunks = (max(0, nw - mx) + step - 1) // step + 1
     out = ctypes.create_string_buffer(len(b) * (mx // step + 2) + 16)
     meta = np.empty(3 * nchunks + 3, dtype=np.int64)
-    nc = L.da_chunk(b, words.ctypes.data, nw, opts.max_tokens, opts.overlap, out, len(out), meta.ctypes.data,
+    nc = L.da_chunk(b, len(b), words.ctypes.data, nw, opts.max_tokens, opts.overlap, out, len(out), meta.ctypes.data,
                     nchunks + 1)
     if nc < 0:
         raise RuntimeError("native chunker buffer too small")

@@ -72,7 +72,21 @@ int main(int argc, char** argv) {
     const long meta_cap = (rng() & 7) == 0 ? (long)(rng() % (ref.size() + 1)) : (long)ref.size() + 1;
     std::vector<char> out((size_t)out_cap + 1);
     std::vector<int64_t> meta(3 * (size_t)meta_cap + 3);
-    long nc = da_chunk(s.data(), words.data(), nw, maxt, ov, out.data(), out_cap, meta.data(), meta_cap);
+    if (nw > 0 && (rng() & 15) == 0) {
+      // malformed spans: one word's end past the input (or reversed): must be refused
+      // with -2 before any byte is copied from past the string (ASan would flag the read)
+      std::vector<int64_t> badw(words);
+      const long k = (long)(rng() % (unsigned long)nw);
+      if (rng() & 1) badw[2 * k + 1] = (int64_t)s.size() + 1 + (int64_t)(rng() % 4096);
+      else badw[2 * k] = badw[2 * k + 1] + 1;
+      std::vector<char> o2((size_t)s.size() * 8 + 4096);
+      std::vector<int64_t> m2(3 * (size_t)nw + 6);
+      const long r2 = da_chunk(s.data(), (long)s.size(), badw.data(), nw, maxt, ov, o2.data(), (long)o2.size() - 1,
+                               m2.data(), nw + 1);
+      if (r2 != -2 && r2 != -1) ++bad;
+    }
+    long nc = da_chunk(s.data(), (long)s.size(), words.data(), nw, maxt, ov, out.data(), out_cap, meta.data(),
+                       meta_cap);
     if (nc == -1) continue;  // undersized buffers: reported, nothing written past them (ASan checks)
     if (nc != (long)ref.size()) { ++bad; continue; }
     for (long c = 0; c < nc; ++c) {

@@ -113,3 +113,56 @@ def test_engine_main_replicas_route_balance_search_and_recover(tmp_path, tp):
     assert rows == {d: 2 for d in docs}
     np.testing.assert_array_equal(before["keys"], after["keys"])
     np.testing.assert_allclose(before["scores"], after["scores"], atol=1e-6)
+
+
+class _FakeReplica:
+    """An EngineClient stand-in: ``behaviour(method)`` returns a value or raises."""
+
+    def __init__(self, behaviour):
+        self.behaviour, self.calls = behaviour, []
+
+    async def call(self, method, trace="", **args):
+        self.calls.append(method)
+        return self.behaviour(method)
+
+
+def _cluster(*replicas):
+    from docagents_amd.engine.rpc import EngineCluster
+    cl = EngineCluster("tcp://127.0.0.1:1")
+    cl.clients = list(replicas)
+    cl.inflight = [0] * len(replicas)
+    cl.dead_until = [0.0] * len(replicas)
+    cl.topology = {"replicas": len(replicas), "tp": 1, "world": len(replicas)}
+    return cl
+
+
+def test_slow_but_alive_replica_is_not_marked_dead_and_generations_are_not_retried():
+    """a client-side timeout on a busy replica must not mark it dead for
+    dead_s or re-run a generation on another replica (nothing cancels the first one server-side).
+    Cheap calls (embed / search) may be re-asked of another replica; a connection failure still
+    fails over."""
+    import asyncio
+
+    def slow(method):
+        raise asyncio.TimeoutError()
+    fast = _FakeReplica(lambda m: f"ok-{m}")
+    busy = _FakeReplica(slow)
+
+    async def go():
+        cl = _cluster(busy, fast)
+        with pytest.raises(asyncio.TimeoutError):
+            cl._rr = 0
+            await cl.call("answer", question="q", context="c", quality=1.0)
+        assert fast.calls == [] and cl.dead_until == [0.0, 0.0]   # not retried, nobody marked dead
+        cl._rr = 0
+        assert await cl.call("embed", texts=["x"]) == "ok-embed"   # cheap: re-asked elsewhere
+        assert cl.dead_until == [0.0, 0.0] and fast.calls == ["embed"]
+
+        def gone(method):
+            raise ConnectionRefusedError("down")
+        dead = _FakeReplica(gone)
+        cl2 = _cluster(dead, fast)
+        cl2._rr = 0
+        assert await cl2.call("answer", question="q", context="c", quality=1.0) == "ok-answer"
+        assert cl2.dead_until[0] > 0  # a real failure: skipped for dead_s
+    asyncio.run(go())

@@ -17,10 +17,12 @@ from docagents_amd.ops import build as B
 
 HOT_NO_SCRATCH = {  # mangled-name prefixes of the kernels the flagship bench runs
     "attention.hip": ["_Z18decode_attn_kernelILi96ELi1ELi3EE", "_Z18decode_attn_kernelILi96ELi1ELi7EE",
-                      "_Z18decode_attn_kernelILi96ELi1ELi35EE", "_Z22flash_attn_pipe_kernelILi96ELb1ELb1EE",
+                      "_Z22flash_attn_pipe_kernelILi96ELb1ELb1EE",
                       "_Z20flash_attn_v2_kernelILi64ELi4ELi1E", "_Z20flash_attn_v2_kernelILi128ELi8ELi1E"],
-    "gemm.hip": ["_Z11gemv_kernel", "_Z16gemm_bf16_kernelILi64ELi128ELi1ELi4ELi5ELi4ELb0EE",
-                 "_Z18gemm_splitk_reduce", "_Z23splitk_reduce_resid_ssq", "_Z18gemv_omerge_kernel"],
+    "gemm.hip": ["_Z11gemv_kernel", "_Z16gemm_bf16_kernelILi64ELi128ELi1ELi4ELi5ELi4EE",
+                 "_Z16gemm_bf16_kernelILi32ELi128ELi1ELi4ELi5ELi4EE",
+                 "_Z18gemm_splitk_reduce", "_Z23splitk_reduce_resid_ssq"],
+    "gemm8p.hip": ["_Z13gemm8p_kernelILi6ELi256E", "_Z13gemm8p_kernelILi3ELi256E", "_Z13gemm8p_kernelILi4ELi256E"],
     "gemm_dk.hip": ["_Z14gemm_dk_kernel"],
 }
 NO_SERIAL_LOAD_LOOPS = {"gemm.hip": ["_Z18gemm_splitk_reduce", "_Z23splitk_reduce_resid_ssq",

@@ -107,77 +107,6 @@ def test_gemm_rope(M, H, Hkv, D):
     assert torch.equal(got, two) and torch.equal(kc, kc3) and torch.equal(vc, vc3)
 
 
-def _ssq_parts(x, parts):
-    """[M, parts] fp32 sums of squares of x's 64-column groups (any partition: the consumer sums them)."""
-    M, N = x.shape
-    return x.float().view(M, N // 64, 64).pow(2).sum(-1)[:, :parts].contiguous()
-
-
-@pytest.mark.parametrize("M", [640, 1000, 2304])
-@pytest.mark.parametrize("epi", [K.EPI_NONE, K.EPI_BIAS, K.EPI_SWIGLU, K.EPI_ROPE])
-def test_gemm8p_norm_consumer(M, epi):
-    """Deferred RMSNorm in the phase-split GEMM: raw rows in, output rows scaled by rsqrt(mean
-    square + eps) from the producer's 64-column sums == rmsnorm -> gemm (fp32 ref of the same op)."""
-    torch.manual_seed(M + epi)
-    Kd = 512
-    x = _rand(M, Kd, scale=3.0)
-    ssq = _ssq_parts(x, Kd // 64)
-    eps = 1e-5
-    h = R.rmsnorm(x, torch.ones(Kd, dtype=torch.bfloat16, device=DEV), eps)
-    if epi == K.EPI_ROPE:
-        H, Hkv, D = 8, 2, 64
-        N, L = (H + 2 * Hkv) * D, 4096
-        w = _rand(N, Kd, scale=Kd ** -0.5)
-        pos = torch.arange(M, device=DEV, dtype=torch.int32)
-        slot = torch.zeros(M, device=DEV, dtype=torch.int32)
-        cs = R.rope_table(L, D, 10000.0, device=DEV)
-        kc = torch.zeros(1, Hkv, L, D, device=DEV, dtype=torch.bfloat16)
-        vc, kc2, vc2 = torch.zeros_like(kc), kc.clone(), kc.clone()
-        got = K.gemm8p_norm(x, w, epi, norm_in=(ssq, Kd // 64, eps), rope=(pos, cs, H, Hkv, D, slot, kc, vc))
-        ref = R.gemm_rope(h, w, pos, cs, H, Hkv, D, slot, kc2, vc2)
-        _close(got, ref, atol=0.04)
-        _close(kc, kc2, atol=0.04)
-        _close(vc, vc2, atol=0.04)
-        return
-    N = 1536
-    w = _rand(N, Kd, scale=Kd ** -0.5)
-    bias = _rand(N) if epi == K.EPI_BIAS else None
-    got = K.gemm8p_norm(x, w, epi, bias=bias, norm_in=(ssq, Kd // 64, eps))
-    _close(got, R.gemm(h, w, bias=bias, epi=epi), atol=0.04)
-    _close(got, R.gemm8p_norm(x, w, epi, bias=bias, norm_in=(ssq, Kd // 64, eps)), atol=0.03)
-
-
-@pytest.mark.parametrize("M,N,Kd", [(640, 256, 512), (1000, 1024, 256), (3000, 3072, 1024)])
-def test_gemm8p_norm_producer(M, N, Kd):
-    """EPI_RESID + ssq_out: the output equals the plain residual GEMM bit for bit, and the
-    [M][N / 64] sums of squares equal those of the bf16 output rows."""
-    torch.manual_seed(M + N)
-    a, w, resid = _rand(M, Kd), _rand(N, Kd, scale=Kd ** -0.5), _rand(M, N)
-    ssq = torch.full(((N // 64) * M,), float("nan"), device=DEV)
-    got = K.gemm8p_norm(a, w, K.EPI_RESID, resid=resid, ssq_out=ssq)
-    plain = K.gemm(a, w, epi=K.EPI_RESID, resid=resid)
-    assert torch.equal(got, plain)
-    ref = R.gemm8p_ssq_parts(got)
-    assert torch.allclose(ssq.view(M, N // 64), ref, rtol=1e-4, atol=1e-3)
-
-
-def test_gemm8p_norm_in_place_chain():
-    """The prefill chain shape: O projection in place on x (resid = out = x) writing the sums, then
-    gate/up reading them — the SwiGLU rows equal rmsnorm(x_new) -> gemm."""
-    torch.manual_seed(5)
-    M, Hd, F = 1200, 768, 1024
-    x = _rand(M, Hd, scale=2.0)
-    a, wo = _rand(M, Hd), _rand(Hd, Hd, scale=Hd ** -0.5)
-    wgu = _rand(2 * F, Hd, scale=Hd ** -0.5)
-    ssq = torch.empty((Hd // 64) * M, device=DEV)
-    x_ref = R.gemm(a, wo, epi=K.EPI_RESID, resid=x)
-    K.gemm8p_norm(a, wo, K.EPI_RESID, resid=x, out=x, ssq_out=ssq)
-    _close(x, x_ref, atol=0.03)
-    g = K.gemm8p_norm(x, wgu, K.EPI_SWIGLU, norm_in=(ssq, Hd // 64, 1e-5))
-    h = R.rmsnorm(x, torch.ones(Hd, dtype=torch.bfloat16, device=DEV), 1e-5)
-    _close(g, R.gemm(h, wgu, epi=K.EPI_SWIGLU), atol=0.04)
-
-
 @pytest.mark.parametrize("M", [65, 128, 200])
 def test_gemm_mid_m_in_tree(M):
     """65..255 rows: the 64x128 weight-streaming tile over ceil(M/64) row blocks with split-K
@@ -296,10 +225,11 @@ def test_flash_attn(D, causal, H, Hkv):
     _close(got, ref, atol=0.02)
 
 
-@pytest.mark.parametrize("D,pipe", [(64, None), (64, 3), (96, None), (96, 3), (96, 1), (96, 4)])
-def test_flash_attn_spike(D, pipe):
-    # force a late rescale: one key dominates one query (online-softmax branch coverage; with the
-    # speculative softmax (pipe 3) the deferred-max branch, whose overshoot threshold it exceeds)
+@pytest.mark.parametrize("D", [64, 96])
+def test_flash_attn_spike(D):
+    # force a late rescale: one key dominates one query (online-softmax branch coverage; causal D = 96
+    # runs the speculative softmax of the pipelined kernel: the deferred-max branch, whose overshoot
+    # threshold it exceeds)
     H, Hkv = 2, 2
     L = 300
     qkv = _rand(L, 6 * D, scale=0.3)
@@ -307,27 +237,21 @@ def test_flash_attn_spike(D, pipe):
     qkv[10, :D] = 4.0
     cu = torch.tensor([0, L], device=DEV, dtype=torch.int32)
     q, k, v = qkv[:, :2 * D], qkv[:, 2 * D:4 * D], qkv[:, 4 * D:]
-    if pipe is not None:
-        K.lib().da_set_flash_pipe(pipe)
-    try:
-        for causal in (False, True):
-            _close(K.flash_attn_varlen(q, k, v, cu, L, H, Hkv, D, causal),
-                   R.flash_attn_varlen(q, k, v, cu, L, H, Hkv, D, causal), atol=0.02)
-    finally:
-        K.lib().da_set_flash_pipe(K.FLASH_PIPE_DEFAULT)
+    for causal in (False, True):
+        _close(K.flash_attn_varlen(q, k, v, cu, L, H, Hkv, D, causal),
+               R.flash_attn_varlen(q, k, v, cu, L, H, Hkv, D, causal), atol=0.02)
 
 
 @pytest.mark.parametrize("D", [64, 96, 128])
-@pytest.mark.parametrize("lens,chunk,pft,w8", [([1000], 512, 32, 0), ([1], 256, 32, 0), ([513, 257, 64], 256, 0, 0),
-                                               ([2944] * 5, 0, 0, 0), ([65, 1024, 700], 64, 1024, 0),
-                                               ([2935], 0, 32, 32), ([1], 256, 32, 32), ([1000, 3], 768, 32, 32),
-                                               ([4000, 64, 129], 512, 1024, 1024)])
-def test_decode_attn_fused_rope(D, lens, chunk, pft, w8):
-    """Decode attention with RoPE + the new token's cache write folded in == rope_cache + attention
-    (w8: the 8-waves-per-workgroup variant of the small-batch path)."""
+@pytest.mark.parametrize("lens,chunk", [([1000], 512), ([1], 256), ([513, 257, 64], 256), ([2944] * 5, 0),
+                                        ([65, 1024, 700], 64), ([2935], 0), ([1000, 3], 768),
+                                        ([300] * 9 + [1, 2000], 0), ([4000, 64, 129] * 4, 512)])
+def test_decode_attn_fused_rope(D, lens, chunk):
+    """Decode attention with RoPE + the new token's cache write folded in == rope_cache + attention,
+    on the small-batch (prefetching, B * Hkv <= 32) and the streaming (larger batches) variants."""
     torch.manual_seed(D + len(lens) + chunk)
-    H, slots, max_seq = 4, 6, 4096
     B = len(lens)
+    H, slots, max_seq = 4, B + 2, 4096
     kc, vc = _rand(slots, H, max_seq, D), _rand(slots, H, max_seq, D)
     qkv = _rand(B, 3 * H * D)
     L = torch.tensor(lens, dtype=torch.int32, device=DEV)
@@ -337,13 +261,7 @@ def test_decode_attn_fused_rope(D, lens, chunk, pft, w8):
     kc2, vc2, qkv2, qkv0 = kc.clone(), vc.clone(), qkv.clone(), qkv.clone()
     K.rope_cache(qkv2, pos, cs, H, H, D, slot=slot, k_cache=kc2, v_cache=vc2)
     want = K.decode_attn(qkv2, kc2, vc2, L, slot, H, H, D, max_seq, chunk=chunk)
-    K.lib().da_set_decode_pft(pft)
-    K.lib().da_set_decode_w8(w8)
-    try:
-        got = K.decode_attn(qkv, kc, vc, L, slot, H, H, D, max_seq, chunk=chunk, rope=(cs, pos))
-    finally:
-        K.lib().da_set_decode_pft(32)
-        K.lib().da_set_decode_w8(0)
+    got = K.decode_attn(qkv, kc, vc, L, slot, H, H, D, max_seq, chunk=chunk, rope=(cs, pos))
     _close(got, want, atol=0.01)
     for b in range(B):
         s_, p_ = int(slot[b]), int(pos[b])
@@ -357,31 +275,31 @@ def test_decode_attn_fused_rope(D, lens, chunk, pft, w8):
 @pytest.mark.parametrize("D", [64, 96, 128])
 @pytest.mark.parametrize("B,chunk", [(1, 512), (2, 256), (3, 1024), (1, 64)])
 def test_decode_attn_prefetch_variant(D, B, chunk):
-    """MHA decode with the next tile prefetched (small batches) == the plain variant."""
+    """MHA decode with the next tile prefetched (B rows alone: B * Hkv <= 32) == the streaming variant
+    (the same rows inside a batch padded past 32 (row, kv head) pairs)."""
     torch.manual_seed(D + B)
     H, slots, max_seq = 8, 4, 2048
     kc, vc = _rand(slots, H, max_seq, D), _rand(slots, H, max_seq, D)
     q = _rand(B, H * D)
     lens = torch.tensor([1000, 1537, 63][:B], dtype=torch.int32, device=DEV)
     slot = torch.tensor([2, 0, 3][:B], dtype=torch.int32, device=DEV)
-    outs = []
-    for pft in (0, 1024):
-        K.lib().da_set_decode_pft(pft)
-        try:
-            outs.append(K.decode_attn(q, kc, vc, lens, slot, H, H, D, max_seq, chunk=chunk))
-        finally:
-            K.lib().da_set_decode_pft(32)
+    pad = 8  # B + 8 rows x 8 heads > 32 pairs: the streaming variant
+    qp = torch.cat([q, _rand(pad, H * D)])
+    lp = torch.cat([lens, torch.full((pad,), 100, dtype=torch.int32, device=DEV)])
+    sp = torch.cat([slot, torch.zeros(pad, dtype=torch.int32, device=DEV)])
+    small = K.decode_attn(q, kc, vc, lens, slot, H, H, D, max_seq, chunk=chunk)
+    big = K.decode_attn(qp, kc, vc, lp, sp, H, H, D, max_seq, chunk=chunk)[:B]
     ref = R.decode_attn(q, kc, vc, lens, slot, H, H, D, max_seq)
-    _close(outs[1], ref, atol=0.02)
-    _close(outs[1], outs[0], atol=0.01)
+    _close(small, ref, atol=0.02)
+    _close(small, big, atol=0.01)
 
 
 @pytest.mark.parametrize("H,Hkv,D", [(32, 32, 96), (32, 8, 128), (8, 2, 64)])
 @pytest.mark.parametrize("rope", [False, True])
 def test_decode_attn_balanced_splits(H, Hkv, D, rope):
-    """Balanced splits (a row's L keys spread over every split of the capacity-sized grid) and the
-    fixed-chunk layout both match the fp32 reference, including rows shorter than one split, rows
-    on a split boundary and a shared prefix, with the in-kernel merge (fused RoPE: MHA only)."""
+    """Balanced splits (a row's L keys spread over every split of the capacity-sized grid) match the
+    fp32 reference, including rows shorter than one split and rows on a split boundary, with the
+    in-kernel merge (fused RoPE: MHA only)."""
     if rope and H != Hkv:
         pytest.skip("fused RoPE decode is MHA only")
     torch.manual_seed(H + D + rope)
@@ -395,13 +313,8 @@ def test_decode_attn_balanced_splits(H, Hkv, D, rope):
     cs = R.rope_table(max_seq, D, 10000.0, device=DEV)
     rp = (cs, lens - 1) if rope else None
     ref = R.decode_attn(q.clone(), kc.clone(), vc.clone(), lens, slot, H, Hkv, D, rope=rp)
-    for bal in (1, 0):
-        K.lib().da_set_decode_balance(bal)
-        try:
-            got = K.decode_attn(q, kc.clone(), vc.clone(), lens, slot, H, Hkv, D, max_len=max_seq, chunk=512, rope=rp)
-        finally:
-            K.lib().da_set_decode_balance(1)
-        _close(got, ref, atol=0.02)
+    got = K.decode_attn(q, kc.clone(), vc.clone(), lens, slot, H, Hkv, D, max_len=max_seq, chunk=512, rope=rp)
+    _close(got, ref, atol=0.02)
 
 
 @pytest.mark.parametrize("H,Hkv,D", [(32, 32, 96), (32, 8, 128), (8, 1, 128), (12, 6, 64)])
@@ -575,8 +488,9 @@ def test_kmeans_accum():
     assert torch.equal(c1, c2)
 
 
-@pytest.mark.parametrize("H,Hkv,D", [(32, 8, 128), (8, 1, 128), (16, 8, 64)])
-def test_decode_attn_gqa_mfma_matches_valu_path(H, Hkv, D):
+@pytest.mark.parametrize("H,Hkv,D", [(32, 8, 128), (8, 1, 128), (16, 8, 64), (8, 2, 96)])
+def test_decode_attn_gqa(H, Hkv, D):
+    """GQA decode: the MFMA kernel (D = 64 / 128) and the VALU kernel (other head dims) vs fp32."""
     torch.manual_seed(7)
     B, S = 4, 1500
     kc, vc = _rand(4, Hkv, S, D), _rand(4, Hkv, S, D)
@@ -584,12 +498,6 @@ def test_decode_attn_gqa_mfma_matches_valu_path(H, Hkv, D):
     slot = torch.tensor([3, 1, 0, 2], device=DEV, dtype=torch.int32)
     q = _rand(B, (H + 2 * Hkv) * D)
     a = K.decode_attn(q, kc, vc, lens, slot, H, Hkv, D, max_len=S)
-    K.lib().da_set_gqa_mfma(0)
-    try:
-        b = K.decode_attn(q, kc, vc, lens, slot, H, Hkv, D, max_len=S)
-    finally:
-        K.lib().da_set_gqa_mfma(1)
-    _close(a, b, atol=0.01)
     _close(a, R.decode_attn(q, kc, vc, lens, slot, H, Hkv, D), atol=0.02)
 
 
@@ -656,24 +564,19 @@ def test_gemv_batch1_decode(N, Kd, epi):
     assert torch.equal(auto, got)
 
 
-@pytest.mark.parametrize("ks", [1, 2])
 @pytest.mark.parametrize("N,Kd", [(3072, 8192), (1000, 16384), (8, 8192), (3072, 9216)])
 @pytest.mark.parametrize("epi", [K.EPI_NONE, K.EPI_BIAS, K.EPI_RESID])
-def test_gemv_long_rows_two_waves(ks, N, Kd, epi):
+def test_gemv_long_rows_two_waves(N, Kd, epi):
     """Batch-1 GEMV on narrow matrices with long rows (the K=8192 down projection): two waves split
-    each row's K range and combine through LDS (ks=2, the default) == one wave per row == fp32."""
+    each row's K range and combine through LDS == fp32 (plain and with the RMSNorm fused)."""
     torch.manual_seed(N + Kd + epi)
     a, w = _rand(1, Kd), _rand(N, Kd, scale=Kd ** -0.5)
     bias = _rand(N) if epi in (K.EPI_BIAS, K.EPI_RESID) else None
     resid = _rand(1, N) if epi == K.EPI_RESID else None
-    K.lib().da_set_gemv_ks(ks)
-    try:
-        got = K.gemm(a, w, bias=bias, epi=epi, resid=resid, tile=6, splits=1)
-        g = _rand(Kd) + 1.0
-        x = _rand(1, Kd, scale=3.0)
-        fused = K.gemm(x, w, epi=epi, bias=bias, resid=resid, rms=(g, 1e-5))
-    finally:
-        K.lib().da_set_gemv_ks(2)
+    got = K.gemm(a, w, bias=bias, epi=epi, resid=resid, tile=6, splits=1)
+    g = _rand(Kd) + 1.0
+    x = _rand(1, Kd, scale=3.0)
+    fused = K.gemm(x, w, epi=epi, bias=bias, resid=resid, rms=(g, 1e-5))
     _close(got, R.gemm(a, w, bias=bias, epi=epi, resid=resid), atol=0.03)
     _close(fused, R.gemm(x, w, bias=bias, epi=epi, resid=resid, rms=(g, 1e-5)), atol=0.03)
 
@@ -690,26 +593,18 @@ def test_gemv_fused_rmsnorm(N, Kd, epi):
     _close(got, R.gemm(x, w, epi=epi, rms=(g, 1e-5)), atol=0.03)
 
 
-@pytest.mark.parametrize("nw,qh,pipe", [(4, 1, 0), (8, 1, 0), (4, 2, 0), (8, 2, 0), (4, 1, 1), (4, 1, 3), (4, 1, 4)])
-@pytest.mark.parametrize("D,causal", [(64, False), (96, True), (128, True), (32, False), (64, True), (96, False)])
-def test_flash_attn_wave_shapes(nw, qh, pipe, D, causal):
-    """Every workgroup shape (waves x 32-query halves per wave, and the software-pipelined kernel)
-    against the fp32 reference."""
-    torch.manual_seed(D + nw + qh)
+@pytest.mark.parametrize("D,causal", [(64, False), (96, True), (128, True), (32, False), (64, True), (96, False),
+                                      (128, False), (32, True)])
+def test_flash_attn_dispatch_shapes(D, causal):
+    """Every kernel the flash dispatch picks (the pipelined causal D = 96 kernel, the 4-wave and the
+    8-wave D = 128 flash_attn_v2 shapes) against the fp32 reference, GQA, ragged lengths."""
+    torch.manual_seed(D + causal)
     lens = [1, 77, 300, 513]
     H, Hkv = 4, 2
     T = sum(lens)
     q, k, v = _rand(T, H * D), _rand(T, Hkv * D), _rand(T, Hkv * D)
     cu = torch.tensor([0] + list(np.cumsum(lens)), device=DEV, dtype=torch.int32)
-    K.lib().da_set_flash_waves(nw)
-    K.lib().da_set_flash_qh(qh)
-    K.lib().da_set_flash_pipe(pipe)
-    try:
-        got = K.flash_attn_varlen(q, k, v, cu, max(lens), H, Hkv, D, causal)
-    finally:
-        K.lib().da_set_flash_waves(0)
-        K.lib().da_set_flash_qh(0)
-        K.lib().da_set_flash_pipe(K.FLASH_PIPE_DEFAULT)
+    got = K.flash_attn_varlen(q, k, v, cu, max(lens), H, Hkv, D, causal)
     _close(got, R.flash_attn_varlen(q, k, v, cu, max(lens), H, Hkv, D, causal), atol=0.02)
 
 
@@ -726,53 +621,25 @@ def test_gemm_resid_rmsnorm_fused(M, N, Kd):
     _close(h, h_ref, atol=0.05)
 
 
-@pytest.mark.parametrize("pf", [1, 2, 4])
-@pytest.mark.parametrize("tile,M", [(2, 64), (2, 40), (3, 17)])
-@pytest.mark.parametrize("splits,Kd", [(1, 64), (1, 448), (2, 768), (4, 3072), (3, 576)])
-def test_gemm_decode_tile_prefetch(pf, tile, M, splits, Kd):
-    """Decode tiles with PF k-tiles in flight (incl. nk < PF and nk % PF != 0) match PF = 1."""
-    torch.manual_seed(pf * 100 + M + Kd)
-    N = 392
-    a, w, r = _rand(M, Kd), _rand(N, Kd, scale=Kd ** -0.5), _rand(M, N)
-    K.lib().da_set_gemm_pf(pf)
-    try:
-        got = K.gemm(a, w, epi=K.EPI_RESID, resid=r, tile=tile, splits=splits)
-    finally:
-        K.lib().da_set_gemm_pf(4)
-    _close(got, R.gemm(a, w, epi=K.EPI_RESID, resid=r), atol=0.03)
-
-
-@pytest.mark.parametrize("pf", [2, 4, 8])
 @pytest.mark.parametrize("tile,M", [(2, 64), (2, 40), (3, 17), (2, 130)])
 @pytest.mark.parametrize("splits,Kd,N", [(1, 64, 392), (1, 448, 392), (2, 768, 392), (4, 3072, 392), (3, 576, 392),
                                          (2, 3072, 9216)])
-def test_gemm_decode_tile_direct_b(pf, tile, M, splits, Kd, N):
-    """Direct-B decode tiles (W fragments loaded straight into MFMA registers, no LDS hop) are
-    bit-identical to the LDS-staged tiles (same fragments, same MFMA order) for every epilogue
-    route (plain, residual, SwiGLU, split-K partials + reduce, the fused reduce + RMSNorm)."""
-    torch.manual_seed(pf * 100 + M + Kd)
+def test_gemm_decode_tile(tile, M, splits, Kd, N):
+    """Decode tiles with 4 k-tiles in flight (incl. nk < 4 and nk % 4 != 0) for every epilogue route
+    (residual, SwiGLU, split-K partials + reduce, the fused reduce + RMSNorm) vs fp32."""
+    torch.manual_seed(M + Kd + N)
     a, w, r = _rand(M, Kd), _rand(N, Kd, scale=Kd ** -0.5), _rand(M, N)
     g = _rand(N) + 1.0
-
-    def run():
-        o1 = K.gemm(a, w, epi=K.EPI_RESID, resid=r, tile=tile, splits=splits)
-        o2 = K.gemm(a, w, epi=K.EPI_SWIGLU, tile=tile, splits=splits) if N % 32 == 0 else None
-        x = r.clone()
-        h = K.gemm_resid_norm(a, w, x, g, 1e-5, out=x, tile=tile, splits=splits) if M <= 64 and N <= 8192 else None
-        return o1, o2, x, h
-
-    K.lib().da_set_gemm_pf(pf)
-    try:
-        base = run()
-        K.lib().da_set_gemm_db(1)
-        got = run()
-    finally:
-        K.lib().da_set_gemm_db(0)
-        K.lib().da_set_gemm_pf(4)
-    for b, o in zip(base, got):
-        if b is not None:
-            assert torch.equal(b, o)
-    _close(got[0], R.gemm(a, w, epi=K.EPI_RESID, resid=r), atol=0.03)
+    _close(K.gemm(a, w, epi=K.EPI_RESID, resid=r, tile=tile, splits=splits), R.gemm(a, w, epi=K.EPI_RESID, resid=r),
+           atol=0.03)
+    if N % 32 == 0:
+        _close(K.gemm(a, w, epi=K.EPI_SWIGLU, tile=tile, splits=splits), R.gemm(a, w, epi=K.EPI_SWIGLU), atol=0.03)
+    if M <= 64 and N <= 8192:
+        x, xr = r.clone(), r.clone()
+        h = K.gemm_resid_norm(a, w, x, g, 1e-5, out=x, tile=tile, splits=splits)
+        hr = R.gemm_resid_norm(a, w, xr, g, 1e-5, out=xr)
+        _close(x, xr, atol=0.03)
+        _close(h, hr, atol=0.05)
 
 
 @pytest.mark.parametrize("M", [65, 128, 261, 1023])
@@ -797,9 +664,9 @@ def test_gemm_mid_m(M):
 
 @pytest.mark.parametrize("H,Hkv,D,P", [(32, 32, 96, 261), (8, 2, 128, 64), (4, 4, 64, 1), (4, 2, 96, 130),
                                        (32, 32, 96, 256), (4, 2, 96, 64)])
-@pytest.mark.parametrize("nw,qh,pipe", [(4, 1, 0), (8, 1, 0), (4, 2, 0), (4, 1, 1), (4, 1, 3), (4, 1, 4)])
-def test_flash_attn_shared_prefix(H, Hkv, D, P, nw, qh, pipe):
-    """Suffix queries attend to P shared-prefix keys held in a KV-cache slot + their own keys."""
+def test_flash_attn_shared_prefix(H, Hkv, D, P):
+    """Suffix queries attend to P shared-prefix keys held in a KV-cache slot + their own keys (causal
+    D = 96: the LDS-DMA pipelined kernel for whole 64-key prefixes, its register-staged form else)."""
     torch.manual_seed(H + D + P)
     lens = [1, 63, 64, 200, 7]
     T = sum(lens)
@@ -808,15 +675,7 @@ def test_flash_attn_shared_prefix(H, Hkv, D, P, nw, qh, pipe):
     cu = torch.tensor([0] + list(np.cumsum(lens)), device=DEV, dtype=torch.int32)
     kc, vc = _rand(3, Hkv, 512, D), _rand(3, Hkv, 512, D)
     pre = (kc[1], vc[1], P)
-    K.lib().da_set_flash_waves(nw)
-    K.lib().da_set_flash_qh(qh)
-    K.lib().da_set_flash_pipe(pipe)
-    try:
-        got = K.flash_attn_varlen(q, k, v, cu, max(lens), H, Hkv, D, True, prefix=pre)
-    finally:
-        K.lib().da_set_flash_waves(0)
-        K.lib().da_set_flash_qh(0)
-        K.lib().da_set_flash_pipe(K.FLASH_PIPE_DEFAULT)
+    got = K.flash_attn_varlen(q, k, v, cu, max(lens), H, Hkv, D, True, prefix=pre)
     ref = R.flash_attn_varlen(q, k, v, cu, max(lens), H, Hkv, D, True, prefix=pre)
     _close(got, ref, atol=0.02)
 

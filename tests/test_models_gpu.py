@@ -52,33 +52,6 @@ def test_decoder_prefill_matches_reference():
     assert torch.allclose(m.cache.buf.float(), r.cache.buf.float(), atol=0.05)
 
 
-def test_decoder_prefill_fused_norms(monkeypatch):
-    """>= 640 packed tokens: the prefill folds the layer RMSNorms into the projections (gemm8p_norm);
-    logits and KV cache match the unfused GPU path and the fp32 reference."""
-    import docagents_amd.models.llama as llama
-    monkeypatch.setattr(llama, "_PREFILL_NORM_FUSE", True)
-    cfg = decoder_config("tiny-dec")
-    m = LlamaDecoder(cfg, "cuda", seed=11)
-    u = LlamaDecoder(cfg, "cuda", weights=m.w)
-    u._prefill_norms_fusable = lambda T: False
-    r = LlamaDecoder(cfg, "cuda", weights=m.w)
-    r.ops = reference
-    prompts = [list(range(10, 10 + n)) for n in (300, 420, 77)]
-    flat, pos, cu, lens = pack_prompts(prompts)
-    assert m._prefill_norms_fusable(len(flat))
-    slot_tok = np.repeat(np.arange(3, dtype=np.int32), lens)
-    to = lambda x: torch.from_numpy(np.ascontiguousarray(x)).cuda()  # noqa: E731
-    last = to((cu[1:] - 1).astype(np.int64))
-    out = []
-    for d in (m, u, r):
-        d.alloc_cache(4, 512)
-        out.append(d.prefill(to(flat), to(pos), to(slot_tok), to(cu), int(lens.max()), last).float())
-    assert (out[0] - out[1]).abs().max() < 0.05
-    assert (out[0] - out[2]).abs().max() < 0.05
-    assert torch.allclose(m.cache.buf.float(), u.cache.buf.float(), atol=0.05)
-    assert torch.allclose(m.cache.buf.float(), r.cache.buf.float(), atol=0.05)
-
-
 def test_generate_graph_equals_eager_greedy():
     cfg = decoder_config("tiny-dec")
     m = LlamaDecoder(cfg, "cuda", seed=2)

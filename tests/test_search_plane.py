@@ -168,3 +168,62 @@ def test_requester_that_stops_reading_does_not_stall_the_shard():
         stuck.close()
         for p in planes:
             p.stop(timeout=2)
+
+
+def test_shard_that_accepts_but_never_reads_never_blocks_submit():
+    """a remote shard that accepts connections but never reads them (a stopped
+    process) fills the requester's send buffer. submit() must return at once (the frame goes out on
+    the peer's writer thread), the send times out and marks the shard down, the searches that need
+    it fail, and searches on other shards keep running meanwhile."""
+    d = 32
+    idx = FlatIndex(d, "cpu")
+    docs = _docs(2, 3)
+    for j, doc in enumerate(docs[0]):
+        idx.add(doc, np.arange(3) + 10 * j, torch.from_numpy(_unit(3, d, j)))
+    mute = socket.socket()
+    mute.setsockopt(socket.SOL_SOCKET, socket.SO_RCVBUF, 4096)  # accepted sockets inherit it
+    mute.bind(("127.0.0.1", 0))
+    mute.listen(8)
+    held = []
+    threading.Thread(target=lambda: held.append(mute.accept()), daemon=True).start()
+    plane = SearchPlane(idx, 0, 2, timeout_s=6.0, send_timeout_s=0.5, retry_s=0.1)
+    plane.listen()
+    plane.connect([plane.listen(), mute.getsockname()]).start()
+    try:
+        big = _unit(4096, d, 5)  # 512 KB of fp32 per request: the kernel buffers fill quickly
+        futs = []
+        t0 = time.monotonic()
+        for _ in range(6):
+            futs.append(plane.submit(big, 3, -1.0, [docs[1][:1]] * len(big)))
+        assert time.monotonic() - t0 < 1.0  # never blocked on the mute shard's socket
+        s, k = plane.submit(_unit(1, d, 6), 3, -1.0, [docs[0]]).result(5)  # local shard unaffected
+        assert (k >= 0).all()
+        errs = []
+        for f in futs:
+            with pytest.raises(Exception) as ei:
+                f.result(30)
+            errs.append(str(ei.value))
+        # the send timeout (buffers full) or the search deadline (frames buffered, never answered)
+        assert all("shard 1" in e or "[1]" in e for e in errs), errs[:3]
+    finally:
+        plane.stop(timeout=2)
+        mute.close()
+        for c, _ in held:
+            c.close()
+
+
+def test_shard_refuses_parts_past_its_queue_cap_and_drops_expired_ones(monkeypatch):
+    """a shard whose scan worker is stalled stops queueing after _QUEUED_ROWS_MAX
+    rows (the part fails at once) and drops queued parts whose requester deadline has passed."""
+    import docagents_amd.parallel.search_plane as SP
+    monkeypatch.setattr(SP, "_QUEUED_ROWS_MAX", 64)
+    idx = FlatIndex(32, "cpu")
+    plane = SearchPlane(idx, 0, 1, timeout_s=5.0)  # not started: nothing drains the queue
+    got = []
+    for i in range(3):
+        plane._enqueue(SP._Job(_unit(32, 32, i), 3, -1.0, None, lambda s, g: got.append("ok"),
+                               lambda e: got.append(repr(e)), deadline=time.monotonic() - 1 if i == 0 else None))
+    assert plane.stats["refused"] == 1 and "overloaded" in got[-1]
+    take = plane._take()  # the expired part is dropped (failed), the live one is scanned
+    assert len(take) == 1 and plane.stats["expired"] == 1 and "expired" in got[-1]
+    assert plane._queued_rows == 0
