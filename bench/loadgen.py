@@ -5,6 +5,9 @@ upload -> poll summary -> query), through the gateway:
 
   1. ingest: upload ``--docs`` synthetic documents (``--concurrency`` in flight), poll each
      summary until it is ready -> docs/min from the first upload to the last ready summary;
+  1b. unloaded ingest latency: ``--serial-docs`` more documents uploaded one at a time, each
+     polled (every 10 ms) until its summary reads 200 -> p50 / p90 upload -> summary readable, the
+     reference's only ingest number ("wait 2-3 seconds", README.md:346);
   2. unloaded cache-miss latency: ``--serial-queries`` unique questions sent one at a time
      (concurrency 1) -> p50 / p90 / p99 through gateway proxy -> query service -> engine, the
      number the reference publishes ("~2-3 seconds", README.md:590);
@@ -119,7 +122,8 @@ def _raw_hits(url: str, bodies: list[str]) -> list[float]:
 
 
 async def run(gw: str, docs: int, words: int, queries: int, concurrency: int, top_k: int, seed: int,
-              poll_s: float = 0.05, ingest_timeout: float = 600.0, query_url: str = "", serial: int = 50) -> dict:
+              poll_s: float = 0.05, ingest_timeout: float = 600.0, query_url: str = "", serial: int = 50,
+              serial_docs: int = 10) -> dict:
     tg = TextGen(seed=seed)
     texts = [tg.document(words) for _ in range(docs)]
     sem = asyncio.Semaphore(concurrency)
@@ -159,6 +163,20 @@ async def run(gw: str, docs: int, words: int, queries: int, concurrency: int, to
         timeline = {"uploads_accepted_s": _r(t_up - t0), "first_ready_s": _r(rt[0]) if rt else None,
                     "median_ready_s": _r(statistics.median(rt)) if rt else None,
                     "last_ready_s": _r(rt[-1]) if rt else None}
+
+        # ---- unloaded ingest latency: one document at a time, upload -> summary readable ----
+        serial_ingest = []
+        for i in range(serial_docs):
+            t_s = time.perf_counter()
+            body, ctype = multipart.build({}, {"file": (f"serial{i}.txt", tg.document(words).encode(), "text/plain")})
+            r = await client.post(gw + "/api/documents/upload", content=body, headers={"content-type": ctype})
+            r.raise_for_status()
+            did = r.json()["document_id"]
+            while time.perf_counter() - t_s < 120:
+                if (await client.get(f"{gw}/api/documents/{did}/summary")).status_code == 200:
+                    serial_ingest.append((time.perf_counter() - t_s) * 1000.0)
+                    break
+                await asyncio.sleep(0.01)
 
         # ---- queries ----
         qs = [f"What does {tg.word()} say about {tg.word()} and {tg.word()}?" for _ in range(queries)]
@@ -207,6 +225,10 @@ async def run(gw: str, docs: int, words: int, queries: int, concurrency: int, to
     return {
         "metric": "http_stack", "docs": docs, "docs_ready": len(ready), "words_per_doc": words,
         "ingest_docs_per_min": round(len(ready) / t_ingest * 60.0, 1) if t_ingest else None,
+        "serial_ingest_docs": len(serial_ingest),
+        "serial_ingest_p50_ms": _r(statistics.median(serial_ingest) if serial_ingest else None),
+        "serial_ingest_p90_ms": _r(_pct(serial_ingest, 90)),
+        "reference_ingest_ms": "2000-3000 (README.md:346, 'wait 2-3 seconds')",
         "serial_queries": len(serial_res), "serial_errors": sum(1 for st, _ in serial_res if st != 200),
         "serial_cache_miss_p50_ms": _r(statistics.median(serial_ok) if serial_ok else None),
         "serial_cache_miss_p90_ms": _r(_pct(serial_ok, 90)),
@@ -314,6 +336,7 @@ def main(argv=None):
     ap.add_argument("--words", type=int, default=2000)
     ap.add_argument("--queries", type=int, default=64)
     ap.add_argument("--serial-queries", type=int, default=50, help="unloaded (concurrency 1) cache-miss queries")
+    ap.add_argument("--serial-docs", type=int, default=10, help="unloaded single-document uploads (upload -> summary)")
     ap.add_argument("--concurrency", type=int, default=16)
     ap.add_argument("--top-k", type=int, default=5)
     ap.add_argument("--seed", type=int, default=7)
@@ -358,7 +381,7 @@ def main(argv=None):
     try:
         qurl = f"http://127.0.0.1:{int(gw.rsplit(':', 1)[1]) + 1}/api/query" if proc is not None else a.query_url
         out = asyncio.run(run(gw, a.docs, a.words, a.queries, a.concurrency, a.top_k, a.seed, query_url=qurl,
-                              serial=a.serial_queries))
+                              serial=a.serial_queries, serial_docs=a.serial_docs))
         out["topology"] = a.topology if proc is not None else "external"
         if proc is not None and a.topology == "deploy":
             eng = env.get("ENGINE_URL", "") if env.get("LLM_PROVIDER") == "engine" else ""

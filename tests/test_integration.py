@@ -139,9 +139,11 @@ def test_loadgen_against_spawned_stack(tmp_path):
     """bench/loadgen.py end to end on CPU with stub models (the same tool drives the GPU stack)."""
     env = dict(os.environ, LLM_PROVIDER="stub", EMBED_DIM="64", TMPDIR=str(tmp_path), LOG_LEVEL="error")
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench", "loadgen.py"), "--spawn", "--docs", "4",
-                        "--words", "500", "--queries", "6", "--concurrency", "3"],
+                        "--words", "500", "--queries", "6", "--concurrency", "3", "--serial-docs", "3"],
                        env=env, capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stderr[-2000:]
     out = json.loads(r.stdout.strip().splitlines()[-1])
     assert out["docs_ready"] == 4 and out["query_errors"] == 0
     assert out["cache_hit_p50_ms"] < out["cache_miss_p99_ms"] + 1000
+    # the reference's ingest number: one document at a time, upload -> summary readable
+    assert out["serial_ingest_docs"] == 3 and out["serial_ingest_p50_ms"] > 0
