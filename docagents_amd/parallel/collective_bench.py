@@ -52,13 +52,9 @@ def rccl_search(shard, plane_search, embed, make_batch, k: int, min_sim: float, 
         dist.all_gather_object(every, mine, group=ctrl)
         batches.append((qv, mine, [f for r in range(W) for f in every[r]]))
     B = batches[0][0].shape[0]
-    # identity: the RCCL form and the plane's owner-routed form on the same batch
     qv, mine, flt_all = batches[0]
-    s_p, id_p = plane_search(qv, mine)
     s_r, id_r = shard.search(qv, k, min_sim, flt_all)
     s_r, id_r = s_r.float().cpu().numpy(), id_r.cpu().numpy()
-    agree = int(sum(1 for b in range(B) if np.array_equal(id_r[b], id_p[b])))
-    close = bool(np.allclose(np.where(id_r >= 0, s_r, 0), np.where(id_p >= 0, s_p, 0), atol=1e-3))
     shard.search(*batches[1][:1], k, min_sim, batches[1][2])  # warm
     # throughput: back to back
     _sync(dev); barrier()
@@ -75,6 +71,14 @@ def rccl_search(shard, plane_search, embed, make_batch, k: int, min_sim: float, 
         shard.search(qv, k, min_sim, flt)
         _sync(dev)
         lat.append(all_reduce_max(time.perf_counter() - t1, dev) * 1000)
+    # identity with the serving plane's owner-routed answer for batch 0, after every collective of
+    # the block (a rank-local plane failure cannot desynchronise the ranks' collective sequence)
+    try:
+        s_p, id_p = plane_search(batches[0][0], batches[0][1])
+        agree = int(sum(1 for b in range(B) if np.array_equal(id_r[b], id_p[b])))
+        close = bool(np.allclose(np.where(id_r >= 0, s_r, 0), np.where(id_p >= 0, s_p, 0), atol=1e-3))
+    except Exception as e:  # noqa: BLE001
+        agree, close = -1, repr(e)[:200]
     return {"rows_per_rank": B, "iters": iters, "world": W, "qps": round(W * B * iters / dt, 1),
             "ms_per_call_mean": round(dt / iters * 1000, 3), "p50_ms": round(statistics.median(lat), 3),
             "p90_ms": round(_pct(lat, 0.9), 3), "rows_identical_to_plane": agree, "rows_checked": B,
@@ -111,7 +115,11 @@ def tp_decode(dec_cfg, full_weights, rank: int, world: int, dev, prompts_by_b: d
                  "prompt_tokens_mean": {str(b): round(float(np.mean([len(p) for p in ps])), 1)
                                         for b, ps in prompts_by_b.items()},
                  "xgmi_mapped": xg[0] is not None, "arms": {}}
+    xgmi_failed = ""
     for name, use_x, graphs in arms:
+        if use_x and xgmi_failed:
+            out["arms"][name] = {"skipped": xgmi_failed}
+            continue
         tp.xgmi, tp.xgmi_norm = xg if use_x else (None, None)
         gen = Generator(model, max_batch=maxB, max_seq=max_seq, temperature=0.2, seed=0, use_graphs=graphs)
         row = {"graphs": graphs}
@@ -128,10 +136,22 @@ def tp_decode(dec_cfg, full_weights, rank: int, world: int, dev, prompts_by_b: d
                 row[f"b{b}_prefill_ms"] = round(all_reduce_max(gen.stats["prefill_wall_s"] - p0, dev) * 1000, 2)
         finally:
             gen.close()
+        if use_x:  # any barrier timeout on any rank -> every rank skips the remaining xGMI arms
+            err = ""
+            try:
+                for c in xg:
+                    if c is not None:
+                        c.check()
+            except Exception as e:  # noqa: BLE001
+                err = repr(e)[:200]
+            errs: list = [None] * world
+            dist.all_gather_object(errs, err)
+            xgmi_failed = next((e for e in errs if e), "")
+            if xgmi_failed:
+                row["xgmi_error"] = xgmi_failed
         out["arms"][name] = row
     tp.xgmi, tp.xgmi_norm = xg
     if xg[0] is not None:
-        xg[0].check()
         out["xgmi_calls"] = xg[0].calls + (xg[1].calls if xg[1] is not None else 0)
         for c in xg:
             if c is not None:

@@ -67,7 +67,12 @@ class XgmiAllReduce:
     """One-shot / two-shot all-reduce through IPC-mapped peer buffers (one instance per group)."""
 
     def __init__(self, group=None, device=None, max_bytes: int = 32 << 20, oneshot_max: int = 512 << 10,
-                 grid: int = 0, timeout_ms: int = 5000):
+                 grid: int = 0, timeout_ms: int = 5000, probe_ms: int = 2000):
+        """Collective over ``group``, and symmetric: every rank takes part in every exchange whether
+        or not its own setup worked, and either every rank ends with a working communicator or every
+        rank raises (one rank on RCCL while its peers spin on xGMI flags would deadlock the group).
+        ``probe_ms`` > 0: one small all-reduce with that bounded wait checks the peers' flags and
+        staged rows are really visible across the devices before the communicator is used."""
         self.group = group
         self.world = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
@@ -76,50 +81,102 @@ class XgmiAllReduce:
         self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
         self.max_bytes = (max_bytes + 15) // 16 * 16
         self.oneshot_max = oneshot_max
-        L = _lib()
-        self.grid = grid or L.da_ar_max_blocks()
-        self.timeout = int(timeout_ms * L.da_ar_clock_khz())
-        hb = L.da_ar_ipc_handle_bytes()
         self._own: list[c_void_p] = []
         self._opened: list[c_void_p] = []
-        with torch.cuda.device(self.device):
-            data, sig = c_void_p(), c_void_p()
-            _ok(L.da_ar_malloc(2 * self.max_bytes, 1, byref(data)), "hipExtMallocWithFlags(staging, uncached)")
-            self._own.append(data)
-            _ok(L.da_ar_malloc(L.da_ar_signal_bytes(), 1, byref(sig)), "hipExtMallocWithFlags(signal, uncached)")
-            self._own.append(sig)
-            hd, hs = ctypes.create_string_buffer(hb), ctypes.create_string_buffer(hb)
-            _ok(L.da_ar_ipc_handle(data, hd), "hipIpcGetMemHandle(staging)")
-            _ok(L.da_ar_ipc_handle(sig, hs), "hipIpcGetMemHandle(signal)")
-            allh: list = [None] * self.world
-            dist.all_gather_object(allh, (hd.raw, hs.raw), group=group)
-            dptr, sptr = [], []
-            for r, (h_d, h_s) in enumerate(allh):
-                if r == self.rank:
-                    dptr.append(data.value)
-                    sptr.append(sig.value)
-                    continue
-                pd, ps = c_void_p(), c_void_p()
-                _ok(L.da_ar_ipc_open(ctypes.create_string_buffer(h_d, hb), byref(pd)), f"hipIpcOpenMemHandle(rank {r})")
-                self._opened.append(pd)
-                _ok(L.da_ar_ipc_open(ctypes.create_string_buffer(h_s, hb), byref(ps)), f"hipIpcOpenMemHandle(rank {r})")
-                self._opened.append(ps)
-                dptr.append(pd.value)
-                sptr.append(ps.value)
+        self.calls = 0
+        err, payload = "", None
+        try:
+            L = _lib()
+            self.grid = grid or L.da_ar_max_blocks()
+            self.khz = L.da_ar_clock_khz()
+            self.timeout = int(timeout_ms * self.khz)
+            hb = L.da_ar_ipc_handle_bytes()
+            with torch.cuda.device(self.device):
+                data, sig = c_void_p(), c_void_p()
+                _ok(L.da_ar_malloc(2 * self.max_bytes, 1, byref(data)), "hipExtMallocWithFlags(staging, uncached)")
+                self._own.append(data)
+                _ok(L.da_ar_malloc(L.da_ar_signal_bytes(), 1, byref(sig)), "hipExtMallocWithFlags(signal, uncached)")
+                self._own.append(sig)
+                hd, hs = ctypes.create_string_buffer(hb), ctypes.create_string_buffer(hb)
+                _ok(L.da_ar_ipc_handle(data, hd), "hipIpcGetMemHandle(staging)")
+                _ok(L.da_ar_ipc_handle(sig, hs), "hipIpcGetMemHandle(signal)")
+            payload = (hd.raw, hs.raw)
+        except Exception as e:  # noqa: BLE001 - reported to every rank below
+            err = f"local setup: {e}"
+        allh: list = [None] * self.world
+        dist.all_gather_object(allh, payload, group=group)
+        dptr, sptr = [], []
+        if not err and any(h is None for h in allh):
+            err = "a peer failed its local setup"
+        if not err:
+            try:
+                with torch.cuda.device(self.device):
+                    for r, (h_d, h_s) in enumerate(allh):
+                        if r == self.rank:
+                            dptr.append(data.value)
+                            sptr.append(sig.value)
+                            continue
+                        pd, ps = c_void_p(), c_void_p()
+                        _ok(L.da_ar_ipc_open(ctypes.create_string_buffer(h_d, hb), byref(pd)),
+                            f"hipIpcOpenMemHandle(rank {r})")
+                        self._opened.append(pd)
+                        _ok(L.da_ar_ipc_open(ctypes.create_string_buffer(h_s, hb), byref(ps)),
+                            f"hipIpcOpenMemHandle(rank {r})")
+                        self._opened.append(ps)
+                        dptr.append(pd.value)
+                        sptr.append(ps.value)
+            except Exception as e:  # noqa: BLE001
+                err = f"peer mapping: {e}"
+        self._agree(err)  # every peer mapped everywhere, or every rank raises
         self._data = (c_void_p * self.world)(*dptr)
         self._sig = (c_void_p * self.world)(*sptr)
         self._sig_self = sig
         dist.barrier(group=group)  # every peer mapped before anyone launches
-        self.calls = 0
+        if probe_ms > 0:
+            self._agree(self._probe(probe_ms))
+
+    def _agree(self, err: str) -> None:
+        """All ranks exchange their error string; any error anywhere -> every rank closes and raises."""
+        errs: list = [None] * self.world
+        dist.all_gather_object(errs, err, group=self.group)
+        bad = [f"rank {r}: {e}" for r, e in enumerate(errs) if e]
+        if bad:
+            self.close()
+            raise RuntimeError("; ".join(bad))
+
+    def _probe(self, probe_ms: int) -> str:
+        """One all-reduce of a known pattern with a short bounded wait: '' when the sum arrived and no
+        barrier timed out (flags and staged rows visible across the devices), else why not."""
+        saved = self.timeout
+        self.timeout = int(probe_ms * self.khz)
+        try:
+            # every workgroup of the grid takes part when the staging allows (fp32: 4 per 16-B vector)
+            n = max(4, min(self.grid * 256 * 4, self.max_bytes // 4) // 4 * 4)
+            t = torch.full((n,), float(self.rank + 1), dtype=torch.float32, device=self.device)
+            self.all_reduce_(t)
+            torch.cuda.synchronize(self.device)
+            want = self.world * (self.world + 1) / 2
+            err = ctypes.c_uint(0)
+            _ok(_lib().da_ar_read_err(self._sig_self, byref(err)), "read all-reduce error flag")
+            if err.value:
+                return "probe: a barrier timed out (peer flags not visible across devices)"
+            if not bool(torch.all(t == want)):
+                return "probe: wrong sum (staged rows not visible across devices)"
+            return ""
+        except Exception as e:  # noqa: BLE001
+            return f"probe: {e}"
+        finally:
+            self.timeout = saved
 
     @classmethod
     def create(cls, group=None, device=None, **kw):
-        """The communicator, or None (with the reason logged) when peer mapping is unavailable."""
+        """The communicator, or None on EVERY rank of the group (the reason logged) when peer mapping
+        is unavailable or the probe fails: the caller then uses RCCL on every rank."""
         if os.environ.get("DA_XGMI_AR", "1") == "0" or not torch.cuda.is_available():
             return None
         try:
             return cls(group, device, **kw)
-        except Exception as e:  # noqa: BLE001 - any setup failure means: use RCCL
+        except Exception as e:  # noqa: BLE001 - any setup failure means: use RCCL (symmetric, see __init__)
             import sys
             print(f"[xgmi-allreduce] disabled, using RCCL: {e}", file=sys.stderr, flush=True)
             return None
@@ -184,6 +241,8 @@ class XgmiAllReduce:
             raise RuntimeError("xGMI all-reduce barrier timed out (peer missing or call sequences diverged)")
 
     def close(self):
+        if not self._own and not self._opened:
+            return
         L = _lib()
         torch.cuda.synchronize(self.device)
         for p in self._opened:
