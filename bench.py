@@ -425,6 +425,14 @@ def main():
     # rank), the decoder at TP = N (xGMI all-reduce vs torch.distributed, batch 1 and B) with the
     # per-decision TP verdict, and the xGMI all-reduce vs RCCL per call at 16 KB / 384 KB / 6 MB.
     # Each block reports its own error instead of the bench failing.
+    # physical GPUs behind the ranks (a 1-GPU rehearsal of N ranks must not read as N GPUs)
+    import socket
+    where = [None] * W
+    if W > 1:
+        tdist.all_gather_object(where, (socket.gethostname(), dev.index), group=ctrl)
+    else:
+        where = [(socket.gethostname(), dev.index)]
+    n_phys = len(set(map(tuple, where)))
     multi: dict = {}
     if W > 1:
         from docagents_amd.parallel import collective_bench as CB
@@ -449,22 +457,17 @@ def main():
             return [eng.answer_prompt_ids(tq.question(), [chunks.get(int(c)) for c in rng.integers(0, 1 << 30, a.top_k)],
                                           a.max_new) for _ in range(B)]
         if TP == 1:  # (--tp > 1: the headline itself decodes tensor-parallel)
+            # ranks sharing one GPU (a rehearsal) make every IPC all-reduce wait for the card's other
+            # contexts (~23 ms per call at 8 ranks): a few decode steps there, the full budget on a node
+            tp_new = a.max_new if n_phys == W else min(a.max_new, 6)
             block("tp_decode", lambda: CB.tp_decode(
                 eng.dec_cfg, eng.decoder.w, R, W, dev, {1: tp_prompts(1, 1), a.batch: tp_prompts(a.batch, 2)},
-                a.max_new, rccl_graphs=os.environ.get("DA_BENCH_RCCL_GRAPH") == "1"))
+                tp_new, rccl_graphs=os.environ.get("DA_BENCH_RCCL_GRAPH") == "1", log=lambda m: log(info, m)))
         if dev.type == "cuda":
             from docagents_amd.parallel.xgmi_allreduce import verify_and_time
             block("xgmi_allreduce", lambda: verify_and_time(None, dev))
 
     ranks_seen = int(round(all_reduce_sum(1.0, dev)))  # every rank that reached the end of the run
-    # physical GPUs behind the ranks (a 1-GPU rehearsal of N ranks must not read as N GPUs)
-    import socket
-    where = [None] * W
-    if W > 1:
-        tdist.all_gather_object(where, (socket.gethostname(), dev.index), group=ctrl)
-    else:
-        where = [(socket.gethostname(), dev.index)]
-    n_phys = len(set(map(tuple, where)))
     gen = eng.gen.stats
     out = {
         "metric": METRIC, "value": round(qps, 3), "unit": "queries/s", "n_gpus": n_phys, "world_size": W,

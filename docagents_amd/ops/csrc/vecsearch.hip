@@ -121,6 +121,146 @@ topk_dense_kernel(const bf16_t* __restrict__ X, int N, int d, const int* __restr
   }
 }
 
+// ------------------------------------------------------------------------------------------------
+// Streaming dense scan (d % 128 == 0): the whole-shard pass of flat search, IVF coarse probing and
+// k-means assignment, built to run at HBM speed.
+//
+//  * Every wave is an independent worker over its own contiguous run of rows, 16 rows per MFMA
+//    tile, against the workgroup's 16 queries (B fragments from LDS, one copy per workgroup).
+//  * The rows stream from HBM through a ring of R groups (4 MFMA k-steps = 64 B per lane each)
+//    that runs across tile boundaries: group s + R is requested as soon as group s is consumed,
+//    so ~R * 4 KB per wave stay in flight (the old kernel issued one row load, waited, issued the
+//    next: 3.5 TB/s on a 10M x 1024 shard).
+//  * A tile's 16 x 16 scores are tested against each query's running k-th best (a register of
+//    the lanes that own that query): only a tile holding a row that beats it (early tiles, then
+//    rarely) takes the slow path — doc filter, floor, wave top-K merge into the wave's LDS list.
+//  * More than 16 queries: the grid's query blocks of one row block are dispatched to ONE XCD back
+//    to back, so the shard is read from HBM once and re-read from that XCD's L2 (batch 64 reads X
+//    once, not four times).
+// out [row blocks (padded to 8), Q, K]: one top-K list per workgroup (its 4 waves' lists merged),
+// merged by topk_merge_kernel.
+constexpr int TD_G = 4;  // MFMA k-steps (of 32) per load group: 64 B per lane
+
+// NG = d / 128 load groups per 16-row tile (3, 6, 8: d = 384, 768, 1024): the ring holds one whole
+// tile ahead (NG * 4 KB per wave in flight), every load of the loop body unconditional (clamped),
+// so the compiler's vmcnt waits stay counted.
+template <int NG>
+__global__ void __launch_bounds__(256)
+topk_dense_stream_kernel(const bf16_t* __restrict__ X, int N, const int* __restrict__ slots,
+                         const bf16_t* __restrict__ Qv, int Q, const unsigned* __restrict__ bitmap, int W, float thr,
+                         int K, int rows_per_wave, int nqb, float* __restrict__ out_s, int* __restrict__ out_i) {
+  constexpr int d = NG * 32 * TD_G;
+  constexpr int qstr = d * 2 + 16;
+  __shared__ __attribute__((aligned(16))) char sQ[16 * qstr];   // [16][d] bf16, rows padded by 16 B
+  __shared__ float best_all[4][16 * TK_MAX];
+  __shared__ int bidx_all[4][16 * TK_MAX];
+  __shared__ float sc_all[4][16 * 17];
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int fr = lane & 15, fg = lane >> 4;
+  // XCD-grouped block order: blocks b and b + 8 i share an XCD; the nqb query blocks of row block rb
+  // are b = (rb / 8) * 8 nqb + j * 8 + rb % 8
+  const int b = blockIdx.x, per = 8 * nqb;
+  const int grp = b / per, rem = b % per;
+  const int qb = rem / 8, rb = grp * 8 + rem % 8;
+  const int qbase = qb * 16, nq = min(16, Q - qbase);
+  for (int i = tid; i < 16 * (d / 8); i += 256) {
+    const int r = i / (d / 8), c = i % (d / 8);
+    u32x4_t v = u32x4_t{0, 0, 0, 0};
+    if (r < nq) v = *(const u32x4_t*)(Qv + (size_t)(qbase + r) * d + c * 8);
+    *(u32x4_t*)(sQ + r * qstr + c * 16) = v;
+  }
+  float* best = best_all[wid];
+  int* bidx = bidx_all[wid];
+  float* sc = sc_all[wid];
+  for (int i = lane; i < 16 * TK_MAX; i += 64) { best[i] = -INFINITY; bidx[i] = -1; }
+  __syncthreads();
+
+  const int wbeg = (int)min((long)N, ((long)rb * 4 + wid) * rows_per_wave);
+  const int wend = (int)min((long)N, (long)wbeg + rows_per_wave);
+  const int ntile = (wend - wbeg + 15) / 16;
+  const int lrow = N - 1;
+  auto gload = [&](u32x4_t (&v)[NG][TD_G], int t) {  // tile t's fragments (rows clamped)
+    const int row = min(wbeg + t * 16 + fr, lrow);
+    const bf16_t* p = X + (size_t)row * d + fg * 8;
+#pragma unroll
+    for (int g = 0; g < NG; ++g)
+#pragma unroll
+      for (int j = 0; j < TD_G; ++j) v[g][j] = __builtin_nontemporal_load((const u32x4_t*)(p + (g * TD_G + j) * 32));
+  };
+  u32x4_t ring[NG][TD_G];
+  gload(ring, 0);
+  float kth = -INFINITY;  // this lane's query (fr): its current k-th best score
+  const bool qok = fr < nq;
+  for (int t = 0; t < ntile; ++t) {
+    f32x4_t acc = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    const int row_next = min(wbeg + (t + 1) * 16 + fr, lrow);
+    const bf16_t* pn = X + (size_t)row_next * d + fg * 8;
+#pragma unroll
+    for (int g = 0; g < NG; ++g) {
+#pragma unroll
+      for (int j = 0; j < TD_G; ++j) {
+        const int kk = g * TD_G + j;
+        const bf16x8_t bq = *(const bf16x8_t*)(sQ + fr * qstr + kk * 64 + fg * 16);
+        acc = mfma16(__builtin_bit_cast(bf16x8_t, ring[g][j]), bq, acc);
+      }
+      // group g of the NEXT tile into the slot just consumed (one tile of loads stays in flight)
+#pragma unroll
+      for (int j = 0; j < TD_G; ++j)
+        ring[g][j] = __builtin_nontemporal_load((const u32x4_t*)(pn + (g * TD_G + j) * 32));
+    }
+    // ---- the tile is done: lane (fr, fg) holds rows fg*4 + i of query fr ----
+    const int row0 = wbeg + t * 16;
+    bool cand = false;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) cand |= qok && row0 + fg * 4 + i < wend && acc[i] >= thr && acc[i] > kth;
+    if (__ballot(cand)) {  // slow path (early tiles, then rarely): filter + merge into the wave's lists
+      const unsigned long long bal = __ballot(cand);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) sc[fr * 17 + fg * 4 + i] = acc[i];
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      const unsigned long long qmask = (bal | (bal >> 16) | (bal >> 32) | (bal >> 48)) & 0xffffull;
+      for (int q = 0; q < 16; ++q) {
+        if (!((qmask >> q) & 1ull)) continue;
+        float a = -INFINITY;
+        int ia = -1;
+        if (lane < 16) {
+          const int row = row0 + lane;
+          const float v = sc[q * 17 + lane];
+          bool ok = row < wend && v >= thr;
+          if (ok && slots) {  // removed rows (slot -1) never match; the bitmap filters documents
+            const int sl = slots[row];
+            ok = sl >= 0 &&
+                 (!bitmap || ((sl >> 5) < W && ((bitmap[(size_t)(qbase + q) * W + (sl >> 5)] >> (sl & 31)) & 1u)));
+          }
+          if (ok) { a = v; ia = row; }
+        }
+        wave_merge_topk(a, ia, best + q * TK_MAX, bidx + q * TK_MAX, K, lane);
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      kth = best[fr * TK_MAX + K - 1];
+    }
+  }
+  // the 4 waves' lists -> one per workgroup (wave 0 merges the others'), out [rb, Q, K]
+  __syncthreads();
+  if (wid == 0) {
+    for (int q = 0; q < nq; ++q)
+      for (int w = 1; w < 4; ++w)
+        wave_merge_topk(lane < K ? best_all[w][q * TK_MAX + lane] : -INFINITY,
+                        lane < K ? bidx_all[w][q * TK_MAX + lane] : -1, best + q * TK_MAX, bidx + q * TK_MAX, K, lane);
+    for (int i = lane; i < nq * K; i += 64) {
+      const int qq = i / K, j = i % K;
+      const size_t o = ((size_t)rb * Q + qbase + qq) * K + j;
+      out_s[o] = best[qq * TK_MAX + j];
+      out_i[o] = bidx[qq * TK_MAX + j];
+    }
+  }
+}
+
 // Per-query row ranges. ranges [R, 2] (start, end), range_off [Q+1]; rows_per_q_block rows of the
 // query's concatenated ranges per workgroup (grid = (splits, Q)). out [splits, Q, K].
 __global__ void __launch_bounds__(256)
@@ -275,6 +415,43 @@ DA_EXPORT int da_topk_dense(const void* X, int N, int d, const void* slots, cons
   int err = (int)hipGetLastError();
   if (err) return err;
   topk_merge_kernel<<<Q, 256, 0, s>>>(cs, ci, nblk, Q, K, (float*)out_s, (int*)out_i);
+  DA_LAUNCH_CHECK();
+}
+
+// The streaming scan (d = 384, 768 or 1024): ws holds (row blocks padded to 8) * 4 * Q * K candidate
+// pairs; rows_per_wave % 16 == 0. hipErrorInvalidValue for shapes it does not take (the caller
+// then uses da_topk_dense).
+DA_EXPORT size_t da_topk_stream_ws(int N, int Q, int K, int rows_per_wave) {
+  const long nrb = ((long)N + 4L * rows_per_wave - 1) / (4L * rows_per_wave);
+  const long nrb8 = (nrb + 7) / 8 * 8;
+  return (size_t)nrb8 * Q * K * 8;
+}
+
+DA_EXPORT int da_topk_dense_stream(const void* X, int N, int d, const void* slots, const void* Qv, int Q,
+                                   const void* bitmap, int W, float thr, int K, int rows_per_wave, void* ws,
+                                   void* out_s, void* out_i, void* stream) {
+  if ((d != 384 && d != 768 && d != 1024) || K < 1 || K > TK_MAX || rows_per_wave % 16 || rows_per_wave <= 0 ||
+      N < 1)
+    return (int)hipErrorInvalidValue;
+  if (Q == 0) return 0;
+  hipStream_t s = (hipStream_t)stream;
+  const long nrb = ((long)N + 4L * rows_per_wave - 1) / (4L * rows_per_wave);
+  const int nrb8 = (int)((nrb + 7) / 8 * 8);
+  const int nqb = (Q + 15) / 16;
+  if ((long)nrb8 * nqb > 0x7fffffffL) return (int)hipErrorInvalidValue;
+  float* cs = (float*)ws;
+  int* ci = (int*)(cs + (size_t)nrb8 * Q * K);
+#define TDS(NG) topk_dense_stream_kernel<NG><<<nrb8 * nqb, 256, 0, s>>>((const bf16_t*)X, N, (const int*)slots, \
+      (const bf16_t*)Qv, Q, (const unsigned*)bitmap, W, thr, K, rows_per_wave, nqb, cs, ci)
+  switch (d) {
+    case 384: TDS(3); break;
+    case 768: TDS(6); break;
+    default: TDS(8); break;
+  }
+#undef TDS
+  int err = (int)hipGetLastError();
+  if (err) return err;
+  topk_merge_kernel<<<Q, 256, 0, s>>>(cs, ci, nrb8, Q, K, (float*)out_s, (int*)out_i);
   DA_LAUNCH_CHECK();
 }
 

@@ -66,6 +66,8 @@ _SIGS = {
                        c_void_p],
     "da_topk_dense": [c_void_p, c_int, c_int, c_void_p, c_void_p, c_int, c_void_p, c_int, c_float, c_int,
                       c_int, c_void_p, c_void_p, c_void_p, c_void_p],
+    "da_topk_dense_stream": [c_void_p, c_int, c_int, c_void_p, c_void_p, c_int, c_void_p, c_int, c_float, c_int,
+                             c_int, c_void_p, c_void_p, c_void_p, c_void_p],
     "da_topk_ranges": [c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int,
                        c_float, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p],
     "da_topk_merge": [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p],
@@ -123,6 +125,8 @@ def lib() -> ctypes.CDLL:
             fn.restype = c_int
         L.da_topk_dense_ws.argtypes = [c_int, c_int, c_int, c_int]
         L.da_topk_dense_ws.restype = c_size_t
+        L.da_topk_stream_ws.argtypes = [c_int, c_int, c_int, c_int]
+        L.da_topk_stream_ws.restype = c_size_t
         _LIB = L
         return L
 
@@ -801,6 +805,17 @@ def topk_dense(X, Qv, K: int, thr: float, slots=None, bitmap=None, rows_per_bloc
         _req(slots is not None, "bitmap needs slots")
         _req(bitmap.dtype == torch.int32 and bitmap.is_contiguous() and bitmap.shape[0] == Q, "bitmap [Q, W] int32")
         W = bitmap.shape[1]
+    if d in (384, 768, 1024) and rows_per_block is None and N > 0 and Q <= 256:
+        # the streaming scan (search-sized batches over a big shard; k-means assignment, with the
+        # rows as the queries, keeps the query-major tiles below): ~16 waves of rows per CU over
+        # the chip (256 CUs), >= 64 rows each
+        rpw = max(64, math.ceil(N / (256 * 16) / 16) * 16)
+        ws = _workspace(int(lib().da_topk_stream_ws(N, Q, K, rpw)), X.device)
+        out_s = torch.empty((Q, K), dtype=torch.float32, device=X.device)
+        out_i = torch.empty((Q, K), dtype=torch.int32, device=X.device)
+        _check(lib().da_topk_dense_stream(_ptr(X), N, d, _ptr(slots), _ptr(Qv), Q, _ptr(bitmap), W, float(thr), K,
+                                          rpw, _ptr(ws), _ptr(out_s), _ptr(out_i), _stream()), "topk_dense_stream")
+        return out_s, out_i
     if rows_per_block is None:
         qt = math.ceil(Q / 16)
         nblk = max(1, min(math.ceil(N / 256), max(1, 1024 // qt)))

@@ -90,7 +90,7 @@ def _round_up(x: int, m: int) -> int:
 
 
 def tp_decode(dec_cfg, full_weights, rank: int, world: int, dev, prompts_by_b: dict, max_new: int,
-              rccl_graphs: bool = False, verdict: bool = True) -> dict:
+              rccl_graphs: bool = False, verdict: bool = True, log=None) -> dict:
     """The decoder at TP = world over every rank, timed per decode step. prompts_by_b: {batch:
     prompts} (the same on every rank). full_weights: the unsharded weights (identical on every rank:
     seeded). Arms: the xGMI all-reduce graph-replayed (the served form) and eager, and
@@ -150,6 +150,8 @@ def tp_decode(dec_cfg, full_weights, rank: int, world: int, dev, prompts_by_b: d
             if xgmi_failed:
                 row["xgmi_error"] = xgmi_failed
         out["arms"][name] = row
+        if log is not None:
+            log(f"tp_decode arm {name}: {row}")
     tp.xgmi, tp.xgmi_norm = xg
     if xg[0] is not None:
         out["xgmi_calls"] = xg[0].calls + (xg[1].calls if xg[1] is not None else 0)

@@ -438,8 +438,12 @@ def test_sample_partial_finalize_matches_full_row(T, ranks):
         assert int(b["out_tok"][0]) == 11
 
 
-@pytest.mark.parametrize("N,d,Q,Kk", [(1000, 768, 5, 5), (5000, 1024, 37, 20), (63, 768, 1, 3), (20000, 768, 16, 1)])
+@pytest.mark.parametrize("N,d,Q,Kk", [(1000, 768, 5, 5), (5000, 1024, 37, 20), (63, 768, 1, 3), (20000, 768, 16, 1),
+                                      (300000, 1024, 64, 10), (7000, 384, 3, 32), (4000, 512, 8, 5),
+                                      (3000, 768, 300, 4)])
 def test_topk_dense(N, d, Q, Kk):
+    """The streaming scan (d 384 / 768 / 1024, up to 256 queries) and the query-major tiles (other d,
+    k-means-sized batches) vs fp32: plain, filtered + floored, and with removed rows (slot -1)."""
     torch.manual_seed(N)
     X = torch.nn.functional.normalize(torch.randn(N, d, device=DEV), dim=-1).to(torch.bfloat16)
     Qv = torch.nn.functional.normalize(torch.randn(Q, d, device=DEV), dim=-1).to(torch.bfloat16)
@@ -459,6 +463,14 @@ def test_topk_dense(N, d, Q, Kk):
     rs, ri = R.topk_dense(X, Qv, Kk, 0.0, slots=slots, bitmap=bitmap)
     _close(s, rs, atol=2e-3)
     assert torch.equal(i.cpu(), ri.cpu()) or (s - rs).abs().max() < 2e-3
+    # removed rows (slot -1) never match, including the query's own row
+    slots2 = torch.zeros(N, dtype=torch.int32, device=DEV)
+    slots2[N // 2] = -1
+    slots2[::7] = -1
+    s, i = K.topk_dense(X, Qv, Kk, -1.0, slots=slots2)
+    rs, ri = R.topk_dense(X, Qv, Kk, -1.0, slots=slots2)
+    _close(s, rs, atol=2e-3)
+    assert not bool((i == N // 2).any()) and not bool(((i >= 0) & (i % 7 == 0)).any())
 
 
 def test_topk_ranges():
