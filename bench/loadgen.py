@@ -48,17 +48,32 @@ def _pct(xs, q):
     return xs[min(len(xs) - 1, int(round(q / 100.0 * (len(xs) - 1))))]
 
 
+def _ephemeral_range() -> tuple[int, int]:
+    try:
+        with open("/proc/sys/net/ipv4/ip_local_port_range") as f:
+            lo, hi = (int(x) for x in f.read().split())
+        return lo, hi
+    except (OSError, ValueError):
+        return 32768, 60999
+
+
 def _free_block(n: int = 40) -> int:
-    """A base port with [base, base + n) free (the deploy topology's port plan)."""
-    for _ in range(50):
-        base = _free_port()
-        if base + n >= 65000:
-            continue
+    """A base port with [base, base + n) free on every interface (the deploy topology's port plan),
+    BELOW the kernel's ephemeral range: the services' own outgoing connections take local ports from
+    that range, and one of them holding a planned port made a service fail to bind (a GPU-box stack
+    run whose query service restarted three times on 'address already in use')."""
+    import random
+    lo, hi = _ephemeral_range()
+    top = lo - n - 1 if lo - n - 1 > 10000 else 65000 - n
+    bottom = 10000 if top == lo - n - 1 else hi + 1
+    rng = random.Random(os.getpid() ^ int(time.time() * 1000))
+    for _ in range(200):
+        base = rng.randrange(bottom, top)
         ok = True
         for p in range(base, base + n):
             t = socket.socket()
             try:
-                t.bind(("127.0.0.1", p))
+                t.bind(("0.0.0.0", p))
             except OSError:
                 ok = False
             finally:

@@ -132,14 +132,19 @@ topk_dense_kernel(const bf16_t* __restrict__ X, int N, int d, const int* __restr
 //    so ~R * 4 KB per wave stay in flight (the old kernel issued one row load, waited, issued the
 //    next: 3.5 TB/s on a 10M x 1024 shard).
 //  * A tile's 16 x 16 scores are tested against each query's running k-th best (a register of
-//    the lanes that own that query): only a tile holding a row that beats it (early tiles, then
-//    rarely) takes the slow path — doc filter, floor, wave top-K merge into the wave's LDS list.
+//    the lanes that own that query). Rows that beat it pass the doc filter / floor and are APPENDED
+//    to the query's candidate buffer in LDS (positions from a 4-lane prefix sum, no atomics); only a
+//    buffer past TD_CB - 16 entries is merged into the wave's sorted top-K list (one wave merge per
+//    up to 48 candidates, and the k-th best rises at each merge). Merging every (tile, query) that
+//    had a candidate instead made 16 live queries VALU-bound: 10.8 ms vs 3.7 ms for one query on a
+//    10M x 1024 shard (profiles/r5/index/).
 //  * More than 16 queries: the grid's query blocks of one row block are dispatched to ONE XCD back
 //    to back, so the shard is read from HBM once and re-read from that XCD's L2 (batch 64 reads X
 //    once, not four times).
 // out [row blocks (padded to 8), Q, K]: one top-K list per workgroup (its 4 waves' lists merged),
 // merged by topk_merge_kernel.
-constexpr int TD_G = 4;  // MFMA k-steps (of 32) per load group: 64 B per lane
+constexpr int TD_G = 4;    // MFMA k-steps (of 32) per load group: 64 B per lane
+constexpr int TD_CB = 48;  // candidate buffer entries per (wave, query): a tile adds <= 16
 
 // NG = d / 128 load groups per 16-row tile (3, 6, 8: d = 384, 768, 1024): the ring holds one whole
 // tile ahead (NG * 4 KB per wave in flight), every load of the loop body unconditional (clamped),
@@ -154,7 +159,8 @@ topk_dense_stream_kernel(const bf16_t* __restrict__ X, int N, const int* __restr
   __shared__ __attribute__((aligned(16))) char sQ[16 * qstr];   // [16][d] bf16, rows padded by 16 B
   __shared__ float best_all[4][16 * TK_MAX];
   __shared__ int bidx_all[4][16 * TK_MAX];
-  __shared__ float sc_all[4][16 * 17];
+  __shared__ float cbs_all[4][16 * TD_CB];  // candidate buffers: score, row
+  __shared__ int cbi_all[4][16 * TD_CB];
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int fr = lane & 15, fg = lane >> 4;
@@ -172,7 +178,8 @@ topk_dense_stream_kernel(const bf16_t* __restrict__ X, int N, const int* __restr
   }
   float* best = best_all[wid];
   int* bidx = bidx_all[wid];
-  float* sc = sc_all[wid];
+  float* cbs = cbs_all[wid];
+  int* cbi = cbi_all[wid];
   for (int i = lane; i < 16 * TK_MAX; i += 64) { best[i] = -INFINITY; bidx[i] = -1; }
   __syncthreads();
 
@@ -191,7 +198,25 @@ topk_dense_stream_kernel(const bf16_t* __restrict__ X, int N, const int* __restr
   u32x4_t ring[NG][TD_G];
   gload(ring, 0);
   float kth = -INFINITY;  // this lane's query (fr): its current k-th best score
+  int cnt = 0;            // ... and the entries in its candidate buffer (same in its 4 lanes)
   const bool qok = fr < nq;
+  // merge the buffers of the queries set in `full` (bit q) into their top-K lists
+  auto flush = [&](unsigned long long full) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    for (int q = 0; q < 16; ++q) {
+      if (!((full >> q) & 1ull)) continue;
+      const int n = __shfl(cnt, q, 64);
+      const float a = lane < n ? cbs[q * TD_CB + lane] : -INFINITY;
+      const int ia = lane < n ? cbi[q * TD_CB + lane] : -1;
+      wave_merge_topk(a, ia, best + q * TK_MAX, bidx + q * TK_MAX, K, lane);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if ((full >> fr) & 1ull) { kth = best[fr * TK_MAX + K - 1]; cnt = 0; }
+  };
   for (int t = 0; t < ntile; ++t) {
     f32x4_t acc = f32x4_t{0.f, 0.f, 0.f, 0.f};
     const int row_next = min(wbeg + (t + 1) * 16 + fr, lrow);
@@ -210,40 +235,44 @@ topk_dense_stream_kernel(const bf16_t* __restrict__ X, int N, const int* __restr
         ring[g][j] = __builtin_nontemporal_load((const u32x4_t*)(pn + (g * TD_G + j) * 32));
     }
     // ---- the tile is done: lane (fr, fg) holds rows fg*4 + i of query fr ----
-    const int row0 = wbeg + t * 16;
+    const int row0 = wbeg + t * 16 + fg * 4;
     bool cand = false;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) cand |= qok && row0 + fg * 4 + i < wend && acc[i] >= thr && acc[i] > kth;
-    if (__ballot(cand)) {  // slow path (early tiles, then rarely): filter + merge into the wave's lists
-      const unsigned long long bal = __ballot(cand);
+    for (int i = 0; i < 4; ++i) cand |= qok && row0 + i < wend && acc[i] >= thr && acc[i] > kth;
+    if (__ballot(cand)) {  // early tiles, then rarely: filter, append to the buffers
+      bool keep[4];
+      int c = 0;
 #pragma unroll
-      for (int i = 0; i < 4; ++i) sc[fr * 17 + fg * 4 + i] = acc[i];
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      const unsigned long long qmask = (bal | (bal >> 16) | (bal >> 32) | (bal >> 48)) & 0xffffull;
-      for (int q = 0; q < 16; ++q) {
-        if (!((qmask >> q) & 1ull)) continue;
-        float a = -INFINITY;
-        int ia = -1;
-        if (lane < 16) {
-          const int row = row0 + lane;
-          const float v = sc[q * 17 + lane];
-          bool ok = row < wend && v >= thr;
-          if (ok && slots) {  // removed rows (slot -1) never match; the bitmap filters documents
-            const int sl = slots[row];
-            ok = sl >= 0 &&
-                 (!bitmap || ((sl >> 5) < W && ((bitmap[(size_t)(qbase + q) * W + (sl >> 5)] >> (sl & 31)) & 1u)));
-          }
-          if (ok) { a = v; ia = row; }
+      for (int i = 0; i < 4; ++i) {
+        const int row = row0 + i;
+        bool ok = qok && row < wend && acc[i] >= thr && acc[i] > kth;
+        if (ok && slots) {  // removed rows (slot -1) never match; the bitmap filters documents
+          const int sl = slots[row];
+          ok = sl >= 0 &&
+               (!bitmap || ((sl >> 5) < W && ((bitmap[(size_t)(qbase + fr) * W + (sl >> 5)] >> (sl & 31)) & 1u)));
         }
-        wave_merge_topk(a, ia, best + q * TK_MAX, bidx + q * TK_MAX, K, lane);
+        keep[i] = ok;
+        c += ok;
       }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      kth = best[fr * TK_MAX + K - 1];
+      // inclusive prefix over the query's 4 lanes (fr, fr + 16, fr + 32, fr + 48)
+      int p = c;
+      const int p1 = __shfl_up(p, 16, 64);
+      if (fg >= 1) p += p1;
+      const int p2 = __shfl_up(p, 32, 64);
+      if (fg >= 2) p += p2;
+      const int total = __shfl(p, 48 + fr, 64);
+      int pos = cnt + p - c;
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        if (keep[i]) { cbs[fr * TD_CB + pos] = acc[i]; cbi[fr * TD_CB + pos] = row0 + i; ++pos; }
+      cnt += total;
+      const unsigned long long full = __ballot(fg == 0 && cnt > TD_CB - 16);
+      if (full) flush(full);
     }
+  }
+  {
+    const unsigned long long rest = __ballot(fg == 0 && cnt > 0);
+    if (rest) flush(rest);
   }
   // the 4 waves' lists -> one per workgroup (wave 0 merges the others'), out [rb, Q, K]
   __syncthreads();

@@ -25,12 +25,24 @@ from __future__ import annotations
 import torch
 
 
-def decision_verdict(rank: int, world: int, group=None, device="cpu", arch: str = "tiny-dec",
+def verdict_arch(world: int) -> str:
+    """The miniature decoder the verdict runs at TP = ``world``: tiny-dec (4 heads / 2 KV heads) splits
+    two ways; from three ranks the Llama-3-70B-shaped tiny-dec-tp8 (16 heads / 8 KV heads)."""
+    from ..models.configs import decoder_config
+    for name in ("tiny-dec", "tiny-dec-tp8"):
+        c = decoder_config(name)
+        if c.heads % world == 0 and c.kv_heads % world == 0 and c.ffn % (16 * world) == 0 and c.vocab % world == 0:
+            return name
+    raise ValueError(f"no verdict decoder splits {world} ways")
+
+
+def decision_verdict(rank: int, world: int, group=None, device="cpu", arch: str | None = None,
                      wrong_order: bool = False, steps: int = 8) -> dict:
     from ..engine.generator import Generator
     from ..models.configs import decoder_config
     from ..models.llama import LlamaDecoder, TPContext, random_weights, shard_weights
     dev = torch.device(device)
+    arch = arch or verdict_arch(world)
     cfg = decoder_config(arch)
     full = random_weights(cfg, dev, seed=5)
     ref = LlamaDecoder(cfg, dev, weights=full)
