@@ -50,9 +50,11 @@ def test_bench_two_rank_json_schema():
 
 def test_verdict_decoder_splits_every_bench_world():
     """bench.py's TP verdict at N = 4 / 8 needs a decoder whose heads split that many ways (an 8-rank
-    rehearsal failed on tiny-dec's 4 heads before the choice depended on the world)."""
+    rehearsal failed on tiny-dec's 4 heads before the choice depended on the world, then on
+    tiny-dec-tp8's head dim 32)."""
     from docagents_amd.models.configs import decoder_config
     from docagents_amd.parallel.tp_verify import verdict_arch
     for w in (1, 2, 4, 8):
         c = decoder_config(verdict_arch(w))
         assert c.heads % w == 0 and c.kv_heads % w == 0 and c.ffn % (16 * w) == 0 and c.vocab % w == 0
+        assert c.hidden // c.heads in (64, 96, 128)  # a head dim the GPU decode-attention kernels take
