@@ -358,10 +358,10 @@ class LlamaDecoder:
                              pre=st.pre, out=st.attn)
 
     def _norm_fusable(self, B: int) -> bool:
-        """Batched decode (1 < B <= 64, no TP): every RMSNorm rides on the split-K reduction of the
-        projection before it (gemm_resid_norm), so a layer is 2 GEMM+reduce pairs, 2 plain GEMMs,
-        RoPE/cache and attention — no standalone norm launches."""
-        return self.tp.size == 1 and 1 < B <= 64 and self.cfg.hidden <= 8192 and self.cfg.hidden % 8 == 0
+        """Batched decode (1 < B <= 128, no TP; B <= 64 normally takes gemm_dk first): every RMSNorm
+        rides on the split-K reduction of the projection before it (gemm_resid_norm), so a layer is
+        2 GEMM+reduce pairs, 2 plain GEMMs, RoPE/cache and attention — no standalone norm launches."""
+        return self.tp.size == 1 and 1 < B <= 128 and self.cfg.hidden <= 8192 and self.cfg.hidden % 8 == 0
 
     def _dk_decode(self, B: int) -> bool:
         """Batched decode (2 <= B <= 64, no TP) on gemm_dk: every projection one launch without

@@ -531,14 +531,16 @@ DA_EXPORT int da_gemm_resid_rmsnorm(const void* A, int lda, const void* W, void*
   hipStream_t s = (hipStream_t)stream;
   if (K % 64 || N % 8 || N > 8192 || lda % 8 || ldc % 8 || ldh % 8 || !ws || !gamma || !resid || !Hout)
     return (int)hipErrorInvalidValue;
-  if (splits < 1 || (K / 64) % splits || M > 64) return (int)hipErrorInvalidValue;
+  if (splits < 1 || (K / 64) % splits || M > 128 || (M > 64 && tile != 9)) return (int)hipErrorInvalidValue;
   if (M == 0) return 0;
   GemmArgs a{};
   a.A = (const bf16_t*)A; a.W = (const bf16_t*)W; a.C = (bf16_t*)C;
   a.bias = nullptr; a.resid = nullptr; a.ws = (float*)ws;
   a.M = M; a.N = N; a.K = K; a.lda = lda; a.ldc = ldc; a.ldr = ldr; a.k_per_split = K / splits;
-  const int err = tile == 2 ? launch_decode_tile<64, 128>(a, EPI_PARTIAL, splits, s)
-                            : launch_decode_tile<32, 128>(a, EPI_PARTIAL, splits, s);
+  // tile 9 (65..128 rows): one 128x64 weight-streaming tile per 64 weight rows
+  const int err = tile == 9   ? launch_tile<128, 64, 2, 2, 4>(a, EPI_PARTIAL, splits, s)
+                  : tile == 2 ? launch_decode_tile<64, 128>(a, EPI_PARTIAL, splits, s)
+                              : launch_decode_tile<32, 128>(a, EPI_PARTIAL, splits, s);
   if (err) return err;
   splitk_reduce_resid_rmsnorm<<<M, 256, 0, s>>>((const float*)ws, splits, M, N, (const bf16_t*)bias,
                                                 (const bf16_t*)resid, ldr, (bf16_t*)C, ldc, (const bf16_t*)gamma, eps,

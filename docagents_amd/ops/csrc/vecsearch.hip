@@ -131,34 +131,169 @@ topk_dense_kernel(const bf16_t* __restrict__ X, int N, int d, const int* __restr
 //    that runs across tile boundaries: group s + R is requested as soon as group s is consumed,
 //    so ~R * 4 KB per wave stay in flight (the old kernel issued one row load, waited, issued the
 //    next: 3.5 TB/s on a 10M x 1024 shard).
-//  * A tile's 16 x 16 scores are tested against each query's running k-th best (a register of
-//    the lanes that own that query). Rows that beat it pass the doc filter / floor and are APPENDED
-//    to the query's candidate buffer in LDS (positions from a 4-lane prefix sum, no atomics); only a
-//    buffer past TD_CB - 16 entries is merged into the wave's sorted top-K list (one wave merge per
-//    up to 48 candidates, and the k-th best rises at each merge). Merging every (tile, query) that
-//    had a candidate instead made 16 live queries VALU-bound: 10.8 ms vs 3.7 ms for one query on a
-//    10M x 1024 shard (profiles/r5/index/).
-//  * More than 16 queries: the grid's query blocks of one row block are dispatched to ONE XCD back
-//    to back, so the shard is read from HBM once and re-read from that XCD's L2 (batch 64 reads X
-//    once, not four times).
-// out [row blocks (padded to 8), Q, K]: one top-K list per workgroup (its 4 waves' lists merged),
+//  * A tile's 16 x 16 scores are tested against each query's running k-th best; only rows that beat
+//    it do any top-K work (TdWave below).
+//  * Up to 16 queries (one query block): topk_dense_stream_kernel, every wave its own rows, the
+//    rows loaded non-temporally straight into the MFMA A registers.
+//  * 17..64 queries: topk_dense_mq_kernel, the workgroup's 4 waves = 4 query blocks over the SAME
+//    rows: each 16-row tile is read from HBM once into LDS and feeds all four waves (B fragments of
+//    a wave's 16 queries live in its registers). Query blocks as separate workgroups over the same
+//    rows, even dispatched back to back to one XCD, missed in L2 and read the shard once per block
+//    (batch 64: 12.1 ms vs 3.6 ms for batch 1, profiles/r5/index/).
+// out [row blocks (padded to 8), Q, K]: one unsorted top-K list per (workgroup, query), ordered and
 // merged by topk_merge_kernel.
 constexpr int TD_G = 4;    // MFMA k-steps (of 32) per load group: 64 B per lane
-constexpr int TD_CB = 48;  // candidate buffer entries per (wave, query): a tile adds <= 16
 
-// NT: streaming (non-temporal) row loads — one query block, every row read once. With several
-// query blocks the rows must stay in the XCD's L2 for the sibling blocks: non-temporal loads there
-// sent every block to HBM (batch 64 = 4 blocks read 80 GB for a 20 GB shard: 15.2 ms vs 3.6 ms).
-template <bool NT>
-__device__ __forceinline__ u32x4_t td_load(const u32x4_t* p) {
-  if constexpr (NT) return __builtin_nontemporal_load(p);
-  else return *p;
+// One wave's top-K state for its 16 queries over a run of 16-row tiles. Per query, 64 LDS slots:
+// [0, K) the current top-K (unsorted), then one candidate sub-buffer of SB slots for each of the
+// query's 4 lanes; the k-th best score sits in a register of those lanes.
+//  * tile(): a lane's rows that beat the k-th best pass the doc filter / floor and go to ITS
+//    sub-buffer at a lane-local count: no cross-lane traffic on the append path.
+//  * cut(): once a sub-buffer could overflow on the next tile, the query's list + buffered rows (one
+//    per lane, <= 64) are cut to the top K by a radix select on the ballot unit: 32 rounds of ballot
+//    + popcount on an order-preserving integer image of the score find the K-th largest (ties at
+//    the threshold go to the smaller row id), the winners are compacted into [0, K) by mbcnt. The
+//    sorted-list merge it replaces (K rounds of a 6-level shuffle argmax per (tile, query), then
+//    per 48 candidates) stalled the workgroup's load pipeline: 64 queries took 10.5 ms against
+//    3.7 ms with no candidate work (bench/scan_probe.py, profiles/r5/index/).
+// Lists leave unsorted; topk_merge_kernel orders them.
+constexpr int TD_SL = 64;  // LDS slots per (wave, query)
+
+__device__ __forceinline__ unsigned td_key(float v, int id) {  // larger = better; empty (id < 0) = 0
+  const unsigned u = __float_as_uint(v);
+  return id < 0 ? 0u : ((u & 0x80000000u) ? ~u : (u | 0x80000000u));
 }
+__device__ __forceinline__ float td_unkey(unsigned k) {
+  return k == 0u ? -INFINITY : __uint_as_float((k & 0x80000000u) ? (k & 0x7fffffffu) : ~k);
+}
+__device__ __forceinline__ void wave_sync_lds() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// The top K of the wave's 64 (v, id) (one per lane; id < 0 = empty) into cs/ci[0, K) of a list,
+// unsorted. Returns the K-th best score (-inf while fewer than K are real). Every lane must have
+// read what it passes before the call (the list slots are overwritten).
+__device__ __forceinline__ float td_cut(float v, int id, int K, int lane, float* cs, int* ci) {
+  const unsigned key = td_key(v, id);
+  unsigned T = 0;  // the K-th largest key (empty lanes have key 0)
+  int need = K;
+  bool act = true;
+  for (int bt = 31; bt >= 0; --bt) {
+    const bool one = (key >> bt) & 1u;
+    const int c1 = __popcll(__ballot(act && one));
+    if (c1 >= need) { T |= 1u << bt; act = act && one; }
+    else { need -= c1; act = act && !one; }
+  }
+  // winners: every key > T, then `need` of the keys == T (smallest row ids; empties: any)
+  unsigned long long sel = __ballot(key > T);
+  unsigned long long eq = __ballot(key == T);
+  need = K - __popcll(sel);
+  if (__popcll(eq) <= need || T == 0u) {
+    for (; need > 0 && eq; --need) { sel |= eq & (~eq + 1); eq &= eq - 1; }
+  } else {  // exact score ties at the threshold (rare): smallest row ids first
+    for (; need > 0; --need) {
+      int m = ((eq >> lane) & 1ull) ? id : 0x7fffffff;
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) m = min(m, __shfl_xor(m, o, 64));
+      const unsigned long long w = __ballot(((eq >> lane) & 1ull) && id == m);
+      sel |= w & (~w + 1);
+      eq &= ~(w & (~w + 1));
+    }
+  }
+  const int pos = __builtin_amdgcn_mbcnt_hi((unsigned)(sel >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)sel, 0u));
+  wave_sync_lds();
+  if ((sel >> lane) & 1ull) { cs[pos] = v; ci[pos] = id; }
+  wave_sync_lds();
+  return td_unkey(T);
+}
+
+struct TdWave {
+  float* cs; int* ci;  // [16][TD_SL] scores / rows
+  int K, SB, lane, fr, fg;
+  float kth;  // this lane's query (fr): its current k-th best score
+  int cnt;    // entries in this lane's sub-buffer
+
+  __device__ __forceinline__ void init(float* s, int* i, int k) {
+    cs = s; ci = i; K = k; SB = (TD_SL - k) / 4;  // K <= 32: SB >= 8
+    lane = threadIdx.x & 63; fr = lane & 15; fg = lane >> 4;
+    kth = -INFINITY; cnt = 0;
+    for (int j = lane; j < 16 * TD_SL; j += 64) { cs[j] = -INFINITY; ci[j] = -1; }
+  }
+  // cut the lists of the queries set in `full` (bit q) back to their top K
+  __device__ __forceinline__ void flush(const unsigned long long full) {
+    wave_sync_lds();
+    float kq = -INFINITY;  // lane q < 16: query q's new k-th best
+    for (unsigned long long left = full; left; left &= left - 1) {
+      const int q = __builtin_ctzll(left);
+      // lane j: list slot j (< K) or sub-buffer b = (j - K) / SB entry (j - K) % SB, live below the
+      // count of lane q + 16 b
+      const int b = lane < K ? 0 : min((lane - K) / SB, 3), e = lane < K ? 0 : lane - K - b * SB;
+      const int nb = __shfl(cnt, q + 16 * b, 64);
+      const bool live = lane < K || (lane < K + 4 * SB && e < nb);
+      const float v = live ? cs[q * TD_SL + lane] : -INFINITY;
+      const int id = live ? ci[q * TD_SL + lane] : -1;
+      const float t = td_cut(v, id, K, lane, cs + q * TD_SL, ci + q * TD_SL);
+      if (lane == q) kq = t;
+    }
+    const float kn = __shfl(kq, fr, 64);
+    if ((full >> fr) & 1ull) { kth = kn; cnt = 0; }
+  }
+  // a finished 16 x 16 tile: lane (fr, fg) holds rows row0 + i (row0 = tile base + 4 fg) of query fr
+  // (global query index qrow); rows from `end` on are padding
+  __device__ __forceinline__ void tile(const f32x4_t& acc, int row0, int end, bool qok, float thr,
+                                       const int* __restrict__ slots, const unsigned* __restrict__ bitmap, int W,
+                                       int qrow) {
+    bool cand = false;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) cand |= qok && row0 + i < end && acc[i] >= thr && acc[i] > kth;
+    if (!__ballot(cand)) return;  // the common case after the first tiles
+    float* bs = cs + fr * TD_SL + K + fg * SB;
+    int* bi = ci + fr * TD_SL + K + fg * SB;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row = row0 + i;
+      bool ok = qok && row < end && acc[i] >= thr && acc[i] > kth;
+      if (ok && slots) {  // removed rows (slot -1) never match; the bitmap filters documents
+        const int sl = slots[row];
+        ok = sl >= 0 && (!bitmap || ((sl >> 5) < W && ((bitmap[(size_t)qrow * W + (sl >> 5)] >> (sl & 31)) & 1u)));
+      }
+      if (ok) { bs[cnt] = acc[i]; bi[cnt] = row; ++cnt; }
+    }
+    // a lane's next tile adds <= 4: cut the queries with a sub-buffer past SB - 4
+    const unsigned long long over = __ballot(cnt > SB - 4);
+    if (over) flush((over | (over >> 16) | (over >> 32) | (over >> 48)) & 0xffffull);
+  }
+  // every list cut to its top K (unsorted) in slots [0, K)
+  __device__ __forceinline__ void finish() {
+    const unsigned long long rest = __ballot(cnt > 0);
+    if (rest) flush((rest | (rest >> 16) | (rest >> 32) | (rest >> 48)) & 0xffffull);
+  }
+  // merge another wave's finished lists (same 16 queries) into this wave's
+  __device__ __forceinline__ void absorb(const float* os, const int* oi, int nq) {
+    wave_sync_lds();
+    for (int q = 0; q < nq; ++q) {
+      const float v = lane < K ? cs[q * TD_SL + lane] : lane < 2 * K ? os[q * TD_SL + lane - K] : -INFINITY;
+      const int id = lane < K ? ci[q * TD_SL + lane] : lane < 2 * K ? oi[q * TD_SL + lane - K] : -1;
+      td_cut(v, id, K, lane, cs + q * TD_SL, ci + q * TD_SL);
+    }
+  }
+  // lists of queries [0, nq) -> out[o0 + q * K + j] (o0: this list's (part, first query) offset)
+  __device__ __forceinline__ void store(int nq, size_t o0, float* __restrict__ os, int* __restrict__ oi) {
+    wave_sync_lds();
+    for (int i = lane; i < nq * K; i += 64) {
+      const int q = i / K, j = i % K;
+      os[o0 + i] = cs[q * TD_SL + j];
+      oi[o0 + i] = ci[q * TD_SL + j];
+    }
+  }
+};
 
 // NG = d / 128 load groups per 16-row tile (3, 6, 8: d = 384, 768, 1024): the ring holds one whole
 // tile ahead (NG * 4 KB per wave in flight), every load of the loop body unconditional (clamped),
 // so the compiler's vmcnt waits stay counted.
-template <int NG, bool NT>
+template <int NG>
 __global__ void __launch_bounds__(256)
 topk_dense_stream_kernel(const bf16_t* __restrict__ X, int N, const int* __restrict__ slots,
                          const bf16_t* __restrict__ Qv, int Q, const unsigned* __restrict__ bitmap, int W, float thr,
@@ -166,10 +301,8 @@ topk_dense_stream_kernel(const bf16_t* __restrict__ X, int N, const int* __restr
   constexpr int d = NG * 32 * TD_G;
   constexpr int qstr = d * 2 + 16;
   __shared__ __attribute__((aligned(16))) char sQ[16 * qstr];   // [16][d] bf16, rows padded by 16 B
-  __shared__ float best_all[4][16 * TK_MAX];
-  __shared__ int bidx_all[4][16 * TK_MAX];
-  __shared__ float cbs_all[4][16 * TD_CB];  // candidate buffers: score, row
-  __shared__ int cbi_all[4][16 * TD_CB];
+  __shared__ float cs_all[4][16 * TD_SL];  // per wave: top-K lists + candidate buffers (TdWave)
+  __shared__ int ci_all[4][16 * TD_SL];
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int fr = lane & 15, fg = lane >> 4;
@@ -185,11 +318,8 @@ topk_dense_stream_kernel(const bf16_t* __restrict__ X, int N, const int* __restr
     if (r < nq) v = *(const u32x4_t*)(Qv + (size_t)(qbase + r) * d + c * 8);
     *(u32x4_t*)(sQ + r * qstr + c * 16) = v;
   }
-  float* best = best_all[wid];
-  int* bidx = bidx_all[wid];
-  float* cbs = cbs_all[wid];
-  int* cbi = cbi_all[wid];
-  for (int i = lane; i < 16 * TK_MAX; i += 64) { best[i] = -INFINITY; bidx[i] = -1; }
+  TdWave st;
+  st.init(cs_all[wid], ci_all[wid], K);
   __syncthreads();
 
   const int wbeg = (int)min((long)N, ((long)rb * 4 + wid) * rows_per_wave);
@@ -202,30 +332,11 @@ topk_dense_stream_kernel(const bf16_t* __restrict__ X, int N, const int* __restr
 #pragma unroll
     for (int g = 0; g < NG; ++g)
 #pragma unroll
-      for (int j = 0; j < TD_G; ++j) v[g][j] = td_load<NT>((const u32x4_t*)(p + (g * TD_G + j) * 32));
+      for (int j = 0; j < TD_G; ++j) v[g][j] = __builtin_nontemporal_load((const u32x4_t*)(p + (g * TD_G + j) * 32));
   };
   u32x4_t ring[NG][TD_G];
   gload(ring, 0);
-  float kth = -INFINITY;  // this lane's query (fr): its current k-th best score
-  int cnt = 0;            // ... and the entries in its candidate buffer (same in its 4 lanes)
   const bool qok = fr < nq;
-  // merge the buffers of the queries set in `full` (bit q) into their top-K lists
-  auto flush = [&](unsigned long long full) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    for (int q = 0; q < 16; ++q) {
-      if (!((full >> q) & 1ull)) continue;
-      const int n = __shfl(cnt, q, 64);
-      const float a = lane < n ? cbs[q * TD_CB + lane] : -INFINITY;
-      const int ia = lane < n ? cbi[q * TD_CB + lane] : -1;
-      wave_merge_topk(a, ia, best + q * TK_MAX, bidx + q * TK_MAX, K, lane);
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    if ((full >> fr) & 1ull) { kth = best[fr * TK_MAX + K - 1]; cnt = 0; }
-  };
   for (int t = 0; t < ntile; ++t) {
     f32x4_t acc = f32x4_t{0.f, 0.f, 0.f, 0.f};
     const int row_next = min(wbeg + (t + 1) * 16 + fr, lrow);
@@ -241,62 +352,103 @@ topk_dense_stream_kernel(const bf16_t* __restrict__ X, int N, const int* __restr
       // group g of the NEXT tile into the slot just consumed (one tile of loads stays in flight)
 #pragma unroll
       for (int j = 0; j < TD_G; ++j)
-        ring[g][j] = td_load<NT>((const u32x4_t*)(pn + (g * TD_G + j) * 32));
+        ring[g][j] = __builtin_nontemporal_load((const u32x4_t*)(pn + (g * TD_G + j) * 32));
     }
-    // ---- the tile is done: lane (fr, fg) holds rows fg*4 + i of query fr ----
-    const int row0 = wbeg + t * 16 + fg * 4;
-    bool cand = false;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) cand |= qok && row0 + i < wend && acc[i] >= thr && acc[i] > kth;
-    if (__ballot(cand)) {  // early tiles, then rarely: filter, append to the buffers
-      bool keep[4];
-      int c = 0;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int row = row0 + i;
-        bool ok = qok && row < wend && acc[i] >= thr && acc[i] > kth;
-        if (ok && slots) {  // removed rows (slot -1) never match; the bitmap filters documents
-          const int sl = slots[row];
-          ok = sl >= 0 &&
-               (!bitmap || ((sl >> 5) < W && ((bitmap[(size_t)(qbase + fr) * W + (sl >> 5)] >> (sl & 31)) & 1u)));
-        }
-        keep[i] = ok;
-        c += ok;
-      }
-      // inclusive prefix over the query's 4 lanes (fr, fr + 16, fr + 32, fr + 48)
-      int p = c;
-      const int p1 = __shfl_up(p, 16, 64);
-      if (fg >= 1) p += p1;
-      const int p2 = __shfl_up(p, 32, 64);
-      if (fg >= 2) p += p2;
-      const int total = __shfl(p, 48 + fr, 64);
-      int pos = cnt + p - c;
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-        if (keep[i]) { cbs[fr * TD_CB + pos] = acc[i]; cbi[fr * TD_CB + pos] = row0 + i; ++pos; }
-      cnt += total;
-      const unsigned long long full = __ballot(fg == 0 && cnt > TD_CB - 16);
-      if (full) flush(full);
-    }
+    st.tile(acc, wbeg + t * 16 + fg * 4, wend, qok, thr, slots, bitmap, W, qbase + fr);
   }
-  {
-    const unsigned long long rest = __ballot(fg == 0 && cnt > 0);
-    if (rest) flush(rest);
-  }
-  // the 4 waves' lists -> one per workgroup (wave 0 merges the others'), out [rb, Q, K]
+  st.finish();
+  // the 4 waves' lists -> one per workgroup (wave 0 absorbs the others'), out [rb, Q, K]
   __syncthreads();
   if (wid == 0) {
-    for (int q = 0; q < nq; ++q)
-      for (int w = 1; w < 4; ++w)
-        wave_merge_topk(lane < K ? best_all[w][q * TK_MAX + lane] : -INFINITY,
-                        lane < K ? bidx_all[w][q * TK_MAX + lane] : -1, best + q * TK_MAX, bidx + q * TK_MAX, K, lane);
-    for (int i = lane; i < nq * K; i += 64) {
-      const int qq = i / K, j = i % K;
-      const size_t o = ((size_t)rb * Q + qbase + qq) * K + j;
-      out_s[o] = best[qq * TK_MAX + j];
-      out_i[o] = bidx[qq * TK_MAX + j];
+    for (int w = 1; w < 4; ++w) st.absorb(cs_all[w], ci_all[w], nq);
+    st.store(nq, ((size_t)rb * Q + qbase) * K, out_s, out_i);
+  }
+}
+
+// 17..64 queries per workgroup (see above). rows_per_block rows per workgroup (multiple of 16), grid
+// = row blocks (padded to 8) x query groups of 64: the nqg groups of one row block are dispatched to
+// one XCD back to back. A tile: 16 rows x d, 16 B per thread per load (NG loads), TD_PF tiles in
+// flight in registers, written to one of two LDS buffers (16-B chunk c of row r at c ^ (r & 15): the
+// 16 rows one ds_read_b128 lane group reads hit 16 distinct slots), one barrier per tile.
+constexpr int TD_PF = 3;
+
+template <int NG>
+__global__ void __launch_bounds__(256, 1)
+topk_dense_mq_kernel(const bf16_t* __restrict__ X, int N, const int* __restrict__ slots,
+                     const bf16_t* __restrict__ Qv, int Q, const unsigned* __restrict__ bitmap, int W, float thr,
+                     int K, int rows_per_block, int nqg, float* __restrict__ out_s, int* __restrict__ out_i) {
+  constexpr int d = NG * 128, NK = d / 32, CPR = d / 8, RB = d * 2, TB = 16 * RB;
+  static_assert(16 * CPR == 256 * NG, "one 16-B load per thread per 128 columns");
+  __shared__ __attribute__((aligned(16))) char sX[2][TB];
+  __shared__ float cs_all[4][16 * TD_SL];
+  __shared__ int ci_all[4][16 * TD_SL];
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int fr = lane & 15, fg = lane >> 4;
+  const int b = blockIdx.x, per = 8 * nqg;
+  const int grp = b / per, rem = b % per;
+  const int qg = rem / 8, rb = grp * 8 + rem % 8;
+  const int qbase = (qg * 4 + wid) * 16, nq = max(0, min(16, Q - qbase));
+  const bool qok = fr < nq;
+  // this wave's B fragments: query qbase + fr, columns 32 kk + 8 fg .. + 8
+  bf16x8_t bq[NK];
+#pragma unroll
+  for (int kk = 0; kk < NK; ++kk)
+    bq[kk] = qok ? *(const bf16x8_t*)(Qv + (size_t)(qbase + fr) * d + kk * 32 + fg * 8)
+                 : bf16x8_t{0, 0, 0, 0, 0, 0, 0, 0};
+  TdWave st;
+  st.init(cs_all[wid], ci_all[wid], K);
+
+  const int rbeg = (int)min((long)N, (long)rb * rows_per_block);
+  const int rend = (int)min((long)N, (long)rbeg + rows_per_block);
+  const int ntile = (rend - rbeg + 15) / 16;
+  const int tl = max(ntile - 1, 0), lrow = N - 1;
+  auto gload = [&](u32x4_t (&v)[NG], int t) {  // tile t (rows clamped): thread's chunks tid + 256 i
+#pragma unroll
+    for (int i = 0; i < NG; ++i) {
+      const int idx = tid + 256 * i, r = idx / CPR, c = idx % CPR;
+      v[i] = __builtin_nontemporal_load((const u32x4_t*)(X + (size_t)min(rbeg + t * 16 + r, lrow) * d + c * 8));
+    }
+  };
+  auto lstore = [&](const u32x4_t (&v)[NG], int buf) {
+#pragma unroll
+    for (int i = 0; i < NG; ++i) {
+      const int idx = tid + 256 * i, r = idx / CPR, c = idx % CPR;
+      *(u32x4_t*)(&sX[buf][r * RB + ((c ^ (r & 15)) << 4)]) = v[i];
+    }
+  };
+  __syncthreads();  // the lists' initial values (before any load is in flight: this drains them)
+  u32x4_t ring[TD_PF][NG];
+#pragma unroll
+  for (int u = 0; u < TD_PF; ++u) {
+    gload(ring[u], min(u, tl));
+    asm volatile("" ::: "memory");  // issue order = tile order (counted waits)
+  }
+  // whole groups of TD_PF tiles (no exit inside the unrolled group: the ring keeps fixed registers);
+  // tiles past the end re-read the last one and mask every row
+  for (int t0 = 0; t0 < ntile; t0 += TD_PF) {
+#pragma unroll
+    for (int u = 0; u < TD_PF; ++u) {
+      const int t = t0 + u;
+      const int buf = t & 1;
+      lstore(ring[u], buf);
+      gload(ring[u], min(t + TD_PF, tl));  // clamped past the end: uniform counts
+      // tile t visible to every wave, and every wave is done with tile t - 2 (same buffer): a raw
+      // barrier (__syncthreads() would drain the loads in flight)
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      f32x4_t acc = f32x4_t{0.f, 0.f, 0.f, 0.f};
+      const char* xr = &sX[buf][fr * RB];
+#pragma unroll
+      for (int kk = 0; kk < NK; ++kk) {
+        const int c = kk * 4 + fg;
+        acc = mfma16(*(const bf16x8_t*)(xr + ((c ^ fr) << 4)), bq[kk], acc);
+      }
+      st.tile(acc, rbeg + t * 16 + fg * 4, rend, qok, thr, slots, bitmap, W, qbase + fr);
     }
   }
+  st.finish();
+  st.store(nq, ((size_t)rb * Q + qbase) * K, out_s, out_i);
 }
 
 // Per-query row ranges. ranges [R, 2] (start, end), range_off [Q+1]; rows_per_q_block rows of the
@@ -475,18 +627,18 @@ DA_EXPORT int da_topk_dense_stream(const void* X, int N, int d, const void* slot
   hipStream_t s = (hipStream_t)stream;
   const long nrb = ((long)N + 4L * rows_per_wave - 1) / (4L * rows_per_wave);
   const int nrb8 = (int)((nrb + 7) / 8 * 8);
-  const int nqb = (Q + 15) / 16;
-  if ((long)nrb8 * nqb > 0x7fffffffL) return (int)hipErrorInvalidValue;
+  const int nqb = (Q + 15) / 16, nqg = (Q + 63) / 64;  // query blocks of 16 / groups of 64
+  if ((long)nrb8 * nqg > 0x7fffffffL) return (int)hipErrorInvalidValue;
   float* cs = (float*)ws;
   int* ci = (int*)(cs + (size_t)nrb8 * Q * K);
-#define TDS(NG)                                                                                          \
-  do {                                                                                                   \
-    if (nqb == 1)                                                                                        \
-      topk_dense_stream_kernel<NG, true><<<nrb8 * nqb, 256, 0, s>>>((const bf16_t*)X, N, (const int*)slots, \
-          (const bf16_t*)Qv, Q, (const unsigned*)bitmap, W, thr, K, rows_per_wave, nqb, cs, ci);          \
-    else                                                                                                 \
-      topk_dense_stream_kernel<NG, false><<<nrb8 * nqb, 256, 0, s>>>((const bf16_t*)X, N, (const int*)slots, \
-          (const bf16_t*)Qv, Q, (const unsigned*)bitmap, W, thr, K, rows_per_wave, nqb, cs, ci);         \
+#define TDS(NG)                                                                                         \
+  do {                                                                                                  \
+    if (nqb == 1)                                                                                       \
+      topk_dense_stream_kernel<NG><<<nrb8, 256, 0, s>>>((const bf16_t*)X, N, (const int*)slots,         \
+          (const bf16_t*)Qv, Q, (const unsigned*)bitmap, W, thr, K, rows_per_wave, 1, cs, ci);           \
+    else                                                                                                \
+      topk_dense_mq_kernel<NG><<<nrb8 * nqg, 256, 0, s>>>((const bf16_t*)X, N, (const int*)slots,       \
+          (const bf16_t*)Qv, Q, (const unsigned*)bitmap, W, thr, K, 4 * rows_per_wave, nqg, cs, ci);    \
   } while (0)
   switch (d) {
     case 384: TDS(3); break;

@@ -241,7 +241,7 @@ def gemm(a: torch.Tensor, w: torch.Tensor, bias=None, epi: int = EPI_NONE, resid
     if splits <= 0:
         if tile == 0 and M < 640:
             tile = _decode_tile(M)
-        splits = _auto_splits(M, N, K) if tile in (0, 2, 3) else 1
+        splits = _auto_splits(M, N, K) if tile in (0, 2, 3) or (tile == 9 and M <= 128) else 1
     ws = None
     if splits > 1:
         ws = _workspace(splits * M * N * 4, a.device)
@@ -417,12 +417,12 @@ def gemm_fp8(aq, sa, wq, sw, bias=None, epi: int = EPI_NONE, resid=None, out=Non
 
 
 def gemm_resid_norm(a, w, resid, gamma, eps: float, out=None, h_out=None, bias=None, tile: int = 0, splits: int = 0):
-    """Decode layer tail (M <= 64): out = resid + a @ w^T (+ bias) — the new residual stream — and
+    """Decode layer tail (M <= 128): out = resid + a @ w^T (+ bias) — the new residual stream — and
     h_out = RMSNorm(out) * gamma, with the norm fused into the split-K reduction. Returns h_out."""
     _bf16_cuda(a, "a"); _bf16_cuda(w, "w"); _bf16_cuda(resid, "resid"); _bf16_cuda(gamma, "gamma")
     M, K = a.shape
     N = w.shape[0]
-    _req(M <= 64 and K % 64 == 0 and N % 8 == 0 and N <= 8192 and w.shape[1] == K, "gemm_resid_norm shape")
+    _req(M <= 128 and K % 64 == 0 and N % 8 == 0 and N <= 8192 and w.shape[1] == K, "gemm_resid_norm shape")
     _req(a.stride(1) == 1 and a.stride(0) % 8 == 0 and w.is_contiguous() and gamma.numel() == N, "layout")
     _req(resid.shape == (M, N) and resid.stride(1) == 1, "bad resid")
     out = resid if out is None else out
@@ -441,9 +441,14 @@ def gemm_resid_norm(a, w, resid, gamma, eps: float, out=None, h_out=None, bias=N
 
 
 def _decode_tile(M: int) -> int:
-    """Decode-sized M: 32x128 tiles up to 32 rows, 64x128 above (no wasted MFMA rows either way;
-    65..255 rows run the 64x128 tile over ceil(M/64) row blocks)."""
-    return 3 if M <= 32 else 2
+    """Decode-sized M: 32x128 tiles up to 32 rows, 64x128 to 64; 65..128 rows (a batch-128 decode
+    step) one 128x64 weight-streaming tile per 64 weight rows, so every weight byte is read by ONE
+    workgroup (32-layer Phi-3 chain at M = 96 / 128: 3.47 / 3.78 ms vs 3.73 / 4.10 ms on the 64x128
+    tile over two row blocks, profiles/r5/midm/); 129..639 rows the 64x128 tile over ceil(M/64)
+    row blocks."""
+    if M <= 32:
+        return 3
+    return 9 if 64 < M <= 128 else 2
 
 
 def _auto_splits(M: int, N: int, K: int) -> int:
@@ -455,8 +460,13 @@ def _auto_splits(M: int, N: int, K: int) -> int:
     Llama-3-8B shapes at M = 16 / 64, within 0.7 us on the rest)."""
     if M >= 640:
         return 1
-    tiles = math.ceil(M / (32 if _decode_tile(M) == 3 else 64)) * math.ceil(N / 128)
     ksteps = K // 64
+    if _decode_tile(M) == 9:  # 65..128 rows: 4 splits (the same chain sweep), fewer if K is short
+        s = 4
+        while s > 1 and (ksteps % s or ksteps // s < 4):
+            s //= 2
+        return s
+    tiles = math.ceil(M / (32 if _decode_tile(M) == 3 else 64)) * math.ceil(N / 128)
     # 65..639 rows run the 64x128 tile over ceil(M/64) row blocks (the row blocks of one weight tile
     # share it through L2): up to 4 workgroups per CU below 256 rows, 2.5 from 256 (32-layer Phi-3
     # chain, bench/midm_chain.py, profiles/r2/midm_chain.txt: split 4 best at M = 65 / 128, 2 at 192 /

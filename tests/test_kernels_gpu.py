@@ -109,8 +109,8 @@ def test_gemm_rope(M, H, Hkv, D):
 
 @pytest.mark.parametrize("M", [65, 128, 200])
 def test_gemm_mid_m_in_tree(M):
-    """65..255 rows: the 64x128 weight-streaming tile over ceil(M/64) row blocks with split-K
-    (auto), plain / SwiGLU / residual epilogues, vs the fp32 reference."""
+    """65..255 rows with split-K (auto): the 128x64 weight-streaming tile to 128 rows, the 64x128 tile
+    over ceil(M/64) row blocks above; plain / SwiGLU / residual epilogues, vs the fp32 reference."""
     torch.manual_seed(M)
     N, F, Kd = 3072, 1024, 3072
     a, w = _rand(M, Kd), _rand(N, Kd, scale=Kd ** -0.5)
@@ -440,9 +440,10 @@ def test_sample_partial_finalize_matches_full_row(T, ranks):
 
 @pytest.mark.parametrize("N,d,Q,Kk", [(1000, 768, 5, 5), (5000, 1024, 37, 20), (63, 768, 1, 3), (20000, 768, 16, 1),
                                       (300000, 1024, 64, 10), (7000, 384, 3, 32), (4000, 512, 8, 5),
-                                      (3000, 768, 300, 4)])
+                                      (3000, 768, 300, 4), (40000, 384, 100, 8), (2000, 768, 17, 3)])
 def test_topk_dense(N, d, Q, Kk):
-    """The streaming scan (d 384 / 768 / 1024, up to 256 queries) and the query-major tiles (other d,
+    """The streaming scans (d 384 / 768 / 1024: one query block per wave run up to 16 queries, four
+    query blocks sharing LDS tiles above, up to 256 queries) and the query-major tiles (other d,
     k-means-sized batches) vs fp32: plain, filtered + floored, and with removed rows (slot -1)."""
     torch.manual_seed(N)
     X = torch.nn.functional.normalize(torch.randn(N, d, device=DEV), dim=-1).to(torch.bfloat16)
@@ -620,7 +621,8 @@ def test_flash_attn_dispatch_shapes(D, causal):
     _close(got, R.flash_attn_varlen(q, k, v, cu, max(lens), H, Hkv, D, causal), atol=0.02)
 
 
-@pytest.mark.parametrize("M,N,Kd", [(2, 3072, 3072), (17, 3072, 8192), (64, 4096, 1024), (64, 8192, 512)])
+@pytest.mark.parametrize("M,N,Kd", [(2, 3072, 3072), (17, 3072, 8192), (64, 4096, 1024), (64, 8192, 512),
+                                    (65, 3072, 3072), (128, 3072, 8192), (100, 8192, 512)])
 def test_gemm_resid_rmsnorm_fused(M, N, Kd):
     torch.manual_seed(M + N)
     a, w = _rand(M, Kd), _rand(N, Kd, scale=Kd ** -0.5)
@@ -633,7 +635,7 @@ def test_gemm_resid_rmsnorm_fused(M, N, Kd):
     _close(h, h_ref, atol=0.05)
 
 
-@pytest.mark.parametrize("tile,M", [(2, 64), (2, 40), (3, 17), (2, 130)])
+@pytest.mark.parametrize("tile,M", [(2, 64), (2, 40), (3, 17), (2, 130), (9, 128), (9, 77)])
 @pytest.mark.parametrize("splits,Kd,N", [(1, 64, 392), (1, 448, 392), (2, 768, 392), (4, 3072, 392), (3, 576, 392),
                                          (2, 3072, 9216)])
 def test_gemm_decode_tile(tile, M, splits, Kd, N):
@@ -646,7 +648,7 @@ def test_gemm_decode_tile(tile, M, splits, Kd, N):
            atol=0.03)
     if N % 32 == 0:
         _close(K.gemm(a, w, epi=K.EPI_SWIGLU, tile=tile, splits=splits), R.gemm(a, w, epi=K.EPI_SWIGLU), atol=0.03)
-    if M <= 64 and N <= 8192:
+    if (M <= 64 or (tile == 9 and M <= 128)) and N <= 8192:
         x, xr = r.clone(), r.clone()
         h = K.gemm_resid_norm(a, w, x, g, 1e-5, out=x, tile=tile, splits=splits)
         hr = R.gemm_resid_norm(a, w, xr, g, 1e-5, out=xr)
