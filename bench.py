@@ -149,6 +149,11 @@ def main():
     ap.add_argument("--cpu-rehearsal", action="store_true",
                     help="tests only: run on CPU ranks (gloo) with tiny configs to pin the JSON schema; "
                          "the numbers are not a benchmark")
+    ap.add_argument("--search", default="auto", choices=["auto", "rccl", "plane"],
+                    help="QA-step search transport at N > 1: rccl = the lock-step sharded search (C2 all-gather "
+                         "of the query rows, every shard scans them, C1 all-gather of the per-shard top-k over "
+                         "RCCL / xGMI, device merge); plane = the serving search plane (owner-routed, host TCP); "
+                         "auto = rccl without TP, plane with TP (TP ranks share their queries)")
     ap.add_argument("--multi-iters", type=int, default=24,
                     help="N > 1: timed sharded searches of the rccl_search block (C1 + C2 over RCCL)")
     ap.add_argument("--ingest-latency-reps", type=int, default=10,
@@ -227,8 +232,18 @@ def main():
             fs.append([names[x][y] for x, y in zip(rr, ii)])
         return fs
 
+    use_rccl = W > 1 and (a.search == "rccl" or (a.search == "auto" and TP == 1))
+
     def search(qv, filters):
-        """The production search path: submit to this rank's plane (routed to the owner shards)."""
+        """The QA step's sharded search. rccl: every rank calls it with the same B at the same point of
+        the bench (the QA, latency and breakdown loops run in lock-step), so it is one collective
+        round — filters exchanged on the gloo control group, then ShardedIndex.search (C2 + local
+        scan + C1 over RCCL). plane: submit to this rank's search plane (routed to the owner shards)."""
+        if use_rccl:
+            flt_all = [None] * W
+            tdist.all_gather_object(flt_all, filters, group=ctrl)
+            sc, gid = shard.search(qv, a.top_k, a.min_sim, [f for fs in flt_all for f in fs])
+            return sc.float().cpu().numpy(), gid.cpu().numpy()
         return plane.submit(qv.float().cpu().numpy(), a.top_k, a.min_sim, filters).result()
 
     def qa_items(step: int, B: int):
@@ -484,7 +499,9 @@ def main():
                    "index_kind": a.index_kind if a.index_kind == "flat" else
                    f"ivfflat(lists={a.ivf_lists}, probes={a.ivf_probes})",
                    "index_rows_per_gpu": a.index_rows, "top_k": a.top_k, "max_new_tokens": a.max_new,
-                   "temperature": 0.2, "min_similarity": a.min_sim, "docs_per_query": a.docs_per_query},
+                   "temperature": 0.2, "min_similarity": a.min_sim, "docs_per_query": a.docs_per_query,
+                   "search_transport": "rccl all-gather (C2 query rows + C1 per-shard top-k), device merge"
+                   if use_rccl else ("search plane (owner-routed, host TCP)" if W > 1 else "local shard")},
         "p50_cache_miss_ms": round(p50, 2) if p50 else None,
         "p90_cache_miss_ms": round(p90, 2) if p90 else None, "latency_reps": len(lat),
         "reference_cache_miss_ms": REFERENCE_CACHE_MISS_MS,

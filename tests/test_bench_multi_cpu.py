@@ -31,6 +31,8 @@ def test_bench_two_rank_json_schema():
         assert k in out, k
     assert out["world_size"] == 2 and out["ranks_seen"] == 2
     assert out["n_gpus"] == 1 and out["oversubscribed"] is True
+    # the QA steps' search ran as the lock-step collective (C2 + C1), not over the host plane
+    assert out["config"]["search_transport"].startswith("rccl"), out["config"]
     # the reference's ingest number: per-document latency
     assert out["ingest_single_doc_reps"] == 2 and out["ingest_single_doc_p50_ms"] > 0
     # C1 + C2 over the collective backend, timed, identical rows to the plane

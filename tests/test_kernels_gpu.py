@@ -474,6 +474,24 @@ def test_topk_dense(N, d, Q, Kk):
     assert not bool((i == N // 2).any()) and not bool(((i >= 0) & (i % 7 == 0)).any())
 
 
+@pytest.mark.parametrize("Q", [3, 20, 64])
+def test_topk_dense_ties(Q):
+    """Exact score ties at the k-th place go to the smaller row id (the scans' radix-select cut and
+    the merge): 50 copies of one row, queried with that row, must return its 8 smallest ids."""
+    torch.manual_seed(Q)
+    N, d, Kk = 20000, 1024, 8
+    X = torch.nn.functional.normalize(torch.randn(N, d, device=DEV), dim=-1).to(torch.bfloat16)
+    X[7000:7050] = X[7000]
+    X[150:160] = X[7000]  # ten more copies in another row block, smaller ids
+    Qv = torch.nn.functional.normalize(torch.randn(Q, d, device=DEV), dim=-1).to(torch.bfloat16)
+    Qv[Q - 1] = X[7000]
+    s, i = K.topk_dense(X, Qv, Kk, -1.0)
+    assert i[Q - 1].tolist() == list(range(150, 158))
+    assert bool((s[Q - 1] == s[Q - 1, 0]).all())
+    rs, ri = R.topk_dense(X, Qv, Kk, -1.0)
+    _close(s, rs, atol=2e-3)
+
+
 def test_topk_ranges():
     torch.manual_seed(1)
     N, d, Q, Kk = 3000, 768, 4, 6
