@@ -304,15 +304,22 @@ class LlamaDecoder:
         D, hl, kl = c.head_dim, self.hl, self.kl
         x = o.embed(ids, self.w["embed"])
         hook = self.layer_hook
+        kv_from_cache = bool(getattr(o, "flash_kv_cache_ok", lambda *_: False)(D, True))
         for li, L in enumerate(self.w["layers"]):
             if hook is not None:  # e.g. move the rest of a prefill to another (CU-masked) stream
                 hook(li)
             h = o.rmsnorm(x, L["ln_attn"], c.eps)
-            # QKV projection + RoPE + KV-cache write in one kernel (gemm8p EPI_ROPE epilogue)
-            qkv = o.gemm_rope(h, L["wqkv"], pos, self.cos_sin, hl, kl, D, slot_tok, cache.k(li), cache.v(li))
+            # QKV projection + RoPE + KV-cache write in one kernel (gemm8p EPI_ROPE epilogue); where the
+            # attention reads its keys from the cache (Phi-3's D = 96), k / v go to the cache only
+            qkv = o.gemm_rope(h, L["wqkv"], pos, self.cos_sin, hl, kl, D, slot_tok, cache.k(li), cache.v(li),
+                              kv_out=not kv_from_cache)
             pre = None if prefix is None else (cache.k(li)[prefix[0]], cache.v(li)[prefix[0]], prefix[1])
-            a = o.flash_attn_varlen(qkv[:, :hl * D], qkv[:, hl * D:(hl + kl) * D], qkv[:, (hl + kl) * D:], cu,
-                                    max_seqlen, hl, kl, D, causal=True, prefix=pre)
+            if kv_from_cache:
+                a = o.flash_attn_varlen(qkv[:, :hl * D], None, None, cu, max_seqlen, hl, kl, D, causal=True,
+                                        prefix=pre, kv_cache=(cache.k(li), cache.v(li), slot_tok, pos))
+            else:
+                a = o.flash_attn_varlen(qkv[:, :hl * D], qkv[:, hl * D:(hl + kl) * D], qkv[:, (hl + kl) * D:], cu,
+                                        max_seqlen, hl, kl, D, causal=True, prefix=pre)
             del qkv, h
             x = self._attn_out_and_mlp(L, a, x)
         return self._logits(x.index_select(0, last_idx), gather=not local_logits)

@@ -53,6 +53,14 @@ struct FaPrefix {
   long long hstride;
   int len;
   int rev;  // dispatch order (set by the launcher): bit 0 causal longest-first, bit 1 XCD-grouped
+  // own keys from the KV cache (pipelined D = 96 kernel; null: from the k / v views): sequence b's
+  // keys at cache[kv_slot[cu[b]], hk, kv_pos[cu[b]] + j, :] (slot_stride = Hkv * max_seq * D,
+  // head stride hstride), rows D apart — the QKV epilogue then stores k / v to the cache only
+  const int* kv_slot;
+  const int* kv_pos;
+  const bf16_t* kc;
+  const bf16_t* vc;
+  long long slot_stride;
 };
 
 // The (query block, head, sequence) a flash workgroup works on, from its place in the dispatch
@@ -133,6 +141,11 @@ flash_attn_v2_kernel(const bf16_t* __restrict__ q, const bf16_t* __restrict__ k,
 
   const bf16_t* kbase_p = k + (size_t)s0 * ldk + hk * D;
   const bf16_t* vbase_p = v + (size_t)s0 * ldv + hk * D;
+  if (pre.kv_slot) {  // own keys in the cache (the launcher passes ldk = ldv = D)
+    const size_t off = (size_t)pre.kv_slot[s0] * pre.slot_stride + (size_t)hk * pre.hstride + (size_t)pre.kv_pos[s0] * D;
+    kbase_p = pre.kc + off;
+    vbase_p = pre.vc + off;
+  }
   const bf16_t* kpre = pre.k + hk * pre.hstride;
   const bf16_t* vpre = pre.v + hk * pre.hstride;
   u32x4_t kst[LPT], vst[LPT];
@@ -435,6 +448,11 @@ flash_attn_pipe_kernel(const bf16_t* __restrict__ q, const bf16_t* __restrict__ 
 
   const bf16_t* kbase_p = k + (size_t)s0 * ldk + hk * D;
   const bf16_t* vbase_p = v + (size_t)s0 * ldv + hk * D;
+  if (pre.kv_slot) {  // own keys in the cache (the launcher passes ldk = ldv = D)
+    const size_t off = (size_t)pre.kv_slot[s0] * pre.slot_stride + (size_t)hk * pre.hstride + (size_t)pre.kv_pos[s0] * D;
+    kbase_p = pre.kc + off;
+    vbase_p = pre.vc + off;
+  }
   const bf16_t* kpre = pre.k + hk * pre.hstride;
   const bf16_t* vpre = pre.v + hk * pre.hstride;
   auto buf_of = [&](int t) { return smem + (t % 3) * TBUF; };
@@ -1582,17 +1600,30 @@ static int launch_fa_pipe(const void* q, const void* k, const void* v, int ldq, 
 
 // pre_k / pre_v: shared-prefix K/V of KV head 0 in a cache slot (nullptr / pre_len 0: none),
 // pre_hstride: elements between KV heads there (max_seq * D).
+// kv_slot / kv_pos (nullable; per token, int32): the sequences' own keys are read from the KV cache
+// k_cache / v_cache [slots, Hkv, max_seq, D] (pre_hstride = max_seq * D) instead of k / v — causal
+// D = 96 only.
 DA_EXPORT int da_flash_attn_v2(const void* q, const void* k, const void* v, int ldq, int ldk, int ldv,
                                const void* cu_seqlens, int B, int max_seqlen, int H, int Hkv, int D, int causal,
                                float scale, void* o, int ldo, const void* pre_k, const void* pre_v,
-                               long long pre_hstride, int pre_len, void* stream) {
+                               long long pre_hstride, int pre_len, const void* kv_slot, const void* kv_pos,
+                               const void* k_cache, const void* v_cache, void* stream) {
+  const bool from_cache = kv_slot != nullptr;
+  if (from_cache) {
+    if (!causal || D != 96 || !kv_pos || !k_cache || !v_cache || pre_hstride < (long long)D ||
+        pre_hstride % D || ((uintptr_t)k_cache | (uintptr_t)v_cache) % 16)
+      return (int)hipErrorInvalidValue;
+    k = k_cache; v = v_cache; ldk = ldv = D;  // rows D apart inside a (slot, head) block
+  }
   if (H % Hkv || ldq % 8 || ldk % 8 || ldv % 8 || ldo % 4) return (int)hipErrorInvalidValue;
   if (pre_len < 0 || (pre_len > 0 && (!pre_k || !pre_v || pre_hstride < (long long)pre_len * D)))
     return (int)hipErrorInvalidValue;
   if (B == 0 || max_seqlen == 0) return 0;
   const float sl2e = scale * 1.4426950408889634f;
   hipStream_t s = (hipStream_t)stream;
-  const FaPrefix pre{(const bf16_t*)pre_k, (const bf16_t*)pre_v, pre_hstride, pre_len, kFaDispatch};
+  const FaPrefix pre{(const bf16_t*)pre_k, (const bf16_t*)pre_v, pre_hstride, pre_len, kFaDispatch,
+                     (const int*)kv_slot, (const int*)kv_pos, (const bf16_t*)k_cache, (const bf16_t*)v_cache,
+                     from_cache ? (long long)Hkv * pre_hstride : 0LL};
   if (causal && D == 96) {
     const bool dma = pre_len % 64 == 0 && ((uintptr_t)k | (uintptr_t)v | (uintptr_t)pre_k | (uintptr_t)pre_v) % 16 == 0;
     if (dma) return launch_fa_pipe<true>(q, k, v, ldq, ldk, ldv, cu_seqlens, B, max_seqlen, H, Hkv, causal, sl2e, o, ldo, pre, s);

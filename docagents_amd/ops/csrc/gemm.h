@@ -18,6 +18,7 @@ struct RopeArgs {
   const int* pos; const int* slot; const float* cs;
   bf16_t* kc; bf16_t* vc;
   int H, Hkv, D, max_seq;
+  int kv_out;  // 1: k / v columns also stored in C; 0: cache only (attention reads the cache)
 };
 
 struct GemmArgs {

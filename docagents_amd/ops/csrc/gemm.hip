@@ -616,17 +616,18 @@ DA_EXPORT int da_gemm_dk_splitk(const void* A, int lda, const void* W, void* C, 
 }
 
 // Prefill QKV projection with RoPE + KV-cache write fused into the epilogue (gemm8p EPI_ROPE);
-// M >= 256 (the phase-split kernel), N == (H + 2 Hkv) * D, D % 8 == 0.
+// M >= 256 (the phase-split kernel), N == (H + 2 Hkv) * D, D % 8 == 0. kv_out = 0: the k / v
+// columns of C are left unwritten (cache only).
 DA_EXPORT int da_gemm_rope(const void* A, int lda, const void* W, void* C, int ldc, int M, int N, int K,
                            const void* pos, const void* slot, const void* cos_sin, void* k_cache, void* v_cache,
-                           int H, int Hkv, int D, int max_seq, void* stream) {
+                           int H, int Hkv, int D, int max_seq, int kv_out, void* stream) {
   if (K % 64 || K < 128 || N % 8 || lda % 8 || ldc % 8 || D % 8 || M < 256) return (int)hipErrorInvalidValue;
   if (N != (H + 2 * Hkv) * D || !pos || !slot || !cos_sin || !k_cache || !v_cache) return (int)hipErrorInvalidValue;
   GemmArgs a{};
   a.A = (const bf16_t*)A; a.W = (const bf16_t*)W; a.C = (bf16_t*)C;
   a.M = M; a.N = N; a.K = K; a.lda = lda; a.ldc = ldc; a.k_per_split = K;
   a.rope = RopeArgs{(const int*)pos, (const int*)slot, (const float*)cos_sin, (bf16_t*)k_cache, (bf16_t*)v_cache,
-                    H, Hkv, D, max_seq};
+                    H, Hkv, D, max_seq, kv_out ? 1 : 0};
   const long t256 = (long)((M + 255) / 256) * ((N + 255) / 256);
   return launch_gemm8p(a, EPI_ROPE, (hipStream_t)stream, t256 >= 256 ? 256 : 128);
 }

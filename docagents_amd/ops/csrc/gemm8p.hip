@@ -28,7 +28,9 @@
 //  * Bijective XCD remap + grouped-M tile order; epilogue (bias / GELU / SwiGLU / residual) in
 //    registers, bf16 tile staged through LDS, 16-B coalesced row stores. EPI_ROPE (the prefill QKV
 //    projection): each 16-B chunk holds 4 interleaved rotary pairs of one head, rotated on its way
-//    out, and the k / v chunks are also stored into the KV cache — the rope_cache pass folded in.
+//    out, and the k / v chunks are also stored into the KV cache — the rope_cache pass folded in
+//    (kv_out = 0: ONLY into the cache; the prefill attention then reads its keys there, and the
+//    epilogue writes 2/3 fewer bytes of the QKV tile — the store tail is issue-bound).
 #include "gemm.h"
 
 #include <type_traits>
@@ -309,6 +311,7 @@ gemm8p_kernel(GemmArgs p) {
       if (rkind > 0) {
         bf16_t* cache = rkind == 1 ? R.kc : R.vc;
         *(u32x4_t*)(cache + (((size_t)R.slot[gm] * R.Hkv + rhead) * R.max_seq + ps) * R.D + rd0) = v;
+        if (!R.kv_out) continue;  // k / v live in the cache only: no second copy in C
       }
     }
     if constexpr (EPI == EPI_RESID) {

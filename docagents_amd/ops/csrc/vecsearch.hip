@@ -631,14 +631,19 @@ DA_EXPORT int da_topk_dense_stream(const void* X, int N, int d, const void* slot
   if ((long)nrb8 * nqg > 0x7fffffffL) return (int)hipErrorInvalidValue;
   float* cs = (float*)ws;
   int* ci = (int*)(cs + (size_t)nrb8 * Q * K);
+  // shared-tile kernel: one workgroup per CU over the whole shard (~N / 256 rows each; each
+  // workgroup pays the early top-K fill once), never more row blocks than the workspace holds
+  const int rpb = (int)max(4L * rows_per_wave, ((long)N + 256 * 16 - 1) / (256 * 16) * 16);
+  const long nrb_mq = ((long)N + rpb - 1) / rpb;
+  const int nrb8_mq = (int)((nrb_mq + 7) / 8 * 8);
 #define TDS(NG)                                                                                         \
   do {                                                                                                  \
     if (nqb == 1)                                                                                       \
       topk_dense_stream_kernel<NG><<<nrb8, 256, 0, s>>>((const bf16_t*)X, N, (const int*)slots,         \
           (const bf16_t*)Qv, Q, (const unsigned*)bitmap, W, thr, K, rows_per_wave, 1, cs, ci);           \
     else                                                                                                \
-      topk_dense_mq_kernel<NG><<<nrb8 * nqg, 256, 0, s>>>((const bf16_t*)X, N, (const int*)slots,       \
-          (const bf16_t*)Qv, Q, (const unsigned*)bitmap, W, thr, K, 4 * rows_per_wave, nqg, cs, ci);    \
+      topk_dense_mq_kernel<NG><<<nrb8_mq * nqg, 256, 0, s>>>((const bf16_t*)X, N, (const int*)slots,    \
+          (const bf16_t*)Qv, Q, (const unsigned*)bitmap, W, thr, K, rpb, nqg, cs, ci);                  \
   } while (0)
   switch (d) {
     case 384: TDS(3); break;
@@ -648,7 +653,7 @@ DA_EXPORT int da_topk_dense_stream(const void* X, int N, int d, const void* slot
 #undef TDS
   int err = (int)hipGetLastError();
   if (err) return err;
-  topk_merge_kernel<<<Q, 256, 0, s>>>(cs, ci, nrb8, Q, K, (float*)out_s, (int*)out_i);
+  topk_merge_kernel<<<Q, 256, 0, s>>>(cs, ci, nqb == 1 ? nrb8 : nrb8_mq, Q, K, (float*)out_s, (int*)out_i);
   DA_LAUNCH_CHECK();
 }
 

@@ -35,7 +35,7 @@ _SIGS = {
     "da_gemm_bf16": [c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int,
                      c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_float, c_void_p],
     "da_gemm_rope": [c_void_p, c_int, c_void_p, c_void_p, c_int, c_int, c_int, c_int] + [c_void_p] * 5
-                    + [c_int] * 4 + [c_void_p],
+                    + [c_int] * 5 + [c_void_p],
     "da_gemm_fp8": [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int,
                     c_int, c_int, c_int, c_int, c_void_p],
     "da_quant_fp8_rows": [c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p],
@@ -54,7 +54,7 @@ _SIGS = {
                  + [c_int] * 5 + [c_void_p],
     "da_flash_attn_v2": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_int,
                          c_int, c_int, c_int, c_int, c_float, c_void_p, c_int, c_void_p, c_void_p, c_longlong,
-                         c_int, c_void_p],
+                         c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
     "da_malloc_uncached": [c_longlong, ctypes.POINTER(c_void_p)],
     "da_gemm_dk": [c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
                    c_int, c_void_p, c_int, c_int, c_float, c_void_p, c_void_p],
@@ -339,10 +339,13 @@ def gemm_dk(a, w, epi: int = EPI_NONE, bias=None, resid=None, out=None, norm_in=
 # profiles/r2/ab_gemm8p_vs_hipblaslt.txt).
 
 
-def gemm_rope(a, w, pos, cos_sin, H: int, Hkv: int, D: int, slot, k_cache, v_cache, out=None) -> torch.Tensor:
+def gemm_rope(a, w, pos, cos_sin, H: int, Hkv: int, D: int, slot, k_cache, v_cache, out=None,
+              kv_out: bool = True) -> torch.Tensor:
     """Prefill QKV projection: qkv = a @ w^T with RoPE applied to the q / k heads and the token's
     k / v written to the KV cache (cache [slots, Hkv, max_seq, D]) — one kernel (gemm8p EPI_ROPE)
-    from 256 rows; shorter prefills run gemm + rope_cache (identical roundings)."""
+    from 256 rows; shorter prefills run gemm + rope_cache (identical roundings). kv_out=False: the
+    k / v columns of the result may be left unwritten (the attention reads the cache; see
+    flash_attn_varlen kv_cache) — only the q columns are defined."""
     _bf16_cuda(a, "a"); _bf16_cuda(w, "w"); _i32(pos, "pos"); _i32(slot, "slot")
     M, K = a.shape
     N = w.shape[0]
@@ -358,7 +361,8 @@ def gemm_rope(a, w, pos, cos_sin, H: int, Hkv: int, D: int, slot, k_cache, v_cac
         out = torch.empty((M, N), dtype=torch.bfloat16, device=a.device)
     _req(out.shape == (M, N) and out.stride(1) == 1 and out.stride(0) % 8 == 0, "bad out")
     _check(lib().da_gemm_rope(_ptr(a), a.stride(0), _ptr(w), _ptr(out), out.stride(0), M, N, K, _ptr(pos), _ptr(slot),
-                              _ptr(cos_sin), _ptr(k_cache), _ptr(v_cache), H, Hkv, D, k_cache.shape[2], _stream()),
+                              _ptr(cos_sin), _ptr(k_cache), _ptr(v_cache), H, Hkv, D, k_cache.shape[2], int(kv_out),
+                              _stream()),
            "gemm_rope")
     return out
 
@@ -575,11 +579,28 @@ def rope_cache(qkv, pos, cos_sin, H, Hkv, D, slot=None, k_cache=None, v_cache=No
     return qkv
 
 
+def flash_kv_cache_ok(D: int, causal: bool) -> bool:
+    """True when flash_attn_varlen can read the sequences' own keys from the KV cache (kv_cache=)."""
+    return causal and D == 96
+
+
 def flash_attn_varlen(q, k, v, cu_seqlens, max_seqlen: int, H: int, Hkv: int, D: int, causal: bool,
-                      scale: float | None = None, out=None, prefix=None):
+                      scale: float | None = None, out=None, prefix=None, kv_cache=None):
     """q/k/v: 2-D [T, *] views with head h at columns h*D (strided views into a packed qkv are fine).
     prefix = (k_pre, v_pre, P): shared-prefix keys of every sequence, one KV-cache slot's
-    [Hkv, max_seq, D] K and V (RoPE applied); query i of a sequence is key P + i."""
+    [Hkv, max_seq, D] K and V (RoPE applied); query i of a sequence is key P + i.
+    kv_cache = (k_cache, v_cache, slot, pos) (flash_kv_cache_ok only): the own keys of the sequence
+    starting at token t are k_cache[slot[t], :, pos[t] + j] (slot / pos int32 per token, as the QKV
+    projection wrote them); k / v are then ignored (None allowed)."""
+    kc = vc = ks = kpos = None
+    if kv_cache is not None:
+        kc, vc, ks, kpos = kv_cache
+        _req(flash_kv_cache_ok(D, causal), "kv_cache: causal D = 96 only")
+        _bf16_cuda(kc, "k_cache"); _bf16_cuda(vc, "v_cache"); _i32(ks, "slot"); _i32(kpos, "pos")
+        _req(kc.is_contiguous() and vc.is_contiguous() and kc.shape == vc.shape and kc.dim() == 4
+             and kc.shape[1] == Hkv and kc.shape[3] == D, "caches [slots, Hkv, max_seq, D]")
+        _req(ks.numel() >= q.shape[0] and kpos.numel() >= q.shape[0], "slot / pos per token")
+        k = v = q  # unused by the kernel in this mode
     for t, n in ((q, "q"), (k, "k"), (v, "v")):
         _bf16_cuda(t, n)
         _req(t.dim() == 2 and t.stride(1) == 1 and t.stride(0) % 8 == 0 and t.data_ptr() % 16 == 0, f"{n} layout")
@@ -600,9 +621,13 @@ def flash_attn_varlen(q, k, v, cu_seqlens, max_seqlen: int, H: int, Hkv: int, D:
         _req(kp.dim() == 3 and kp.shape == vp.shape and kp.shape[0] == Hkv and kp.shape[2] == D
              and kp.is_contiguous() and vp.is_contiguous() and 0 <= P <= kp.shape[1], "prefix K/V [Hkv, max_seq, D]")
         hstride = kp.shape[1] * D
+    if kc is not None:
+        _req(prefix is None or kp.shape[1] == kc.shape[2], "prefix and caches differ in max_seq")
+        hstride = kc.shape[2] * D
     _check(lib().da_flash_attn_v2(_ptr(q), _ptr(k), _ptr(v), q.stride(0), k.stride(0), v.stride(0),
                                   _ptr(cu_seqlens), B, int(max_seqlen), H, Hkv, D, int(causal), float(scale),
-                                  _ptr(out), out.stride(0), _ptr(kp), _ptr(vp), hstride, P, _stream()),
+                                  _ptr(out), out.stride(0), _ptr(kp), _ptr(vp), hstride, P, _ptr(ks), _ptr(kpos),
+                                  _ptr(kc), _ptr(vc), _stream()),
            "flash_attn_varlen")
     return out
 

@@ -145,7 +145,7 @@ def _rope_rows(x, cs):  # x [T, nh, D], cs [T, D/2, 2]; pairs (2i, 2i+1) rotated
     return torch.stack([x1 * c - x2 * s, x2 * c + x1 * s], dim=-1).flatten(-2)
 
 
-def gemm_rope(a, w, pos, cos_sin, H, Hkv, D, slot, k_cache, v_cache, out=None):
+def gemm_rope(a, w, pos, cos_sin, H, Hkv, D, slot, k_cache, v_cache, out=None, kv_out=True):
     """QKV projection with RoPE on q / k and the k / v cache write fused (gemm + rope_cache)."""
     qkv = gemm(a, w, out=out)
     return rope_cache(qkv, pos, cos_sin, H, Hkv, D, slot=slot, k_cache=k_cache, v_cache=v_cache)
@@ -165,9 +165,28 @@ def rope_cache(qkv, pos, cos_sin, H, Hkv, D, slot=None, k_cache=None, v_cache=No
     return qkv
 
 
-def flash_attn_varlen(q, k, v, cu_seqlens, max_seqlen, H, Hkv, D, causal, scale=None, out=None, prefix=None):
+def flash_kv_cache_ok(D: int, causal: bool) -> bool:
+    return causal
+
+
+def flash_attn_varlen(q, k, v, cu_seqlens, max_seqlen, H, Hkv, D, causal, scale=None, out=None, prefix=None,
+                      kv_cache=None):
     """prefix = (k_pre [Hkv, >=P, D], v_pre, P): every sequence's keys are the P shared prefix keys
-    followed by its own; query i sits at key position P + i (bottom-right causal)."""
+    followed by its own; query i sits at key position P + i (bottom-right causal).
+    kv_cache = (k_cache, v_cache, slot, pos): own keys of the sequence starting at token t read from
+    k_cache[slot[t], :, pos[t] + j] (k / v ignored)."""
+    if kv_cache is not None:
+        kc, vc, ks, kpos = kv_cache
+        T = q.shape[0]
+        cu = cu_seqlens.tolist()
+        k = torch.empty((T, Hkv * D), dtype=q.dtype, device=q.device)
+        v = torch.empty((T, Hkv * D), dtype=q.dtype, device=q.device)
+        for b in range(len(cu) - 1):
+            s0, s1 = cu[b], cu[b + 1]
+            if s1 > s0:
+                sl, p0 = int(ks[s0]), int(kpos[s0])
+                k[s0:s1] = kc[sl, :, p0:p0 + s1 - s0].transpose(0, 1).reshape(s1 - s0, Hkv * D)
+                v[s0:s1] = vc[sl, :, p0:p0 + s1 - s0].transpose(0, 1).reshape(s1 - s0, Hkv * D)
     scale = scale if scale is not None else 1.0 / math.sqrt(D)
     T = q.shape[0]
     res = torch.empty((T, H * D), dtype=q.dtype, device=q.device)

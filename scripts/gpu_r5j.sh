@@ -6,7 +6,7 @@ cd "${GRAFT_REPO_ROOT:-/root/repo}"
 O=gpurun_out/r5j
 mkdir -p $O
 timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_kernels_gpu.py \
-  -k "topk or gemm_decode_tile or resid_rmsnorm or mid_m" > $O/kern.log 2>&1 || { tail -30 $O/kern.log; exit 1; }
+  -k "topk or gemm_decode_tile or resid_rmsnorm or mid_m or gemm_rope or flash_attn or kv_from_cache" > $O/kern.log 2>&1 || { tail -30 $O/kern.log; exit 1; }
 tail -2 $O/kern.log
 timeout -k 10 300 python -u bench/scan_probe.py --qs 1,16,17,64 > $O/scan_probe.txt 2>&1 || { tail -20 $O/scan_probe.txt; exit 1; }
 cat $O/scan_probe.txt

@@ -712,6 +712,36 @@ def test_flash_attn_shared_prefix(H, Hkv, D, P):
     _close(got, ref, atol=0.02)
 
 
+@pytest.mark.parametrize("H,Hkv,P", [(32, 32, 0), (32, 32, 256), (8, 4, 64), (8, 2, 100)])
+def test_flash_attn_kv_from_cache(H, Hkv, P):
+    """The prefill as the model runs it for D = 96: the QKV epilogue writes k / v to the cache only
+    (kv_out=False: the q columns and the caches are bit-identical to kv_out=True), and the attention
+    reads each sequence's own keys from its cache slot at its first token's position — bit-identical
+    to the attention over the k / v columns, with and without a shared prefix in another slot."""
+    torch.manual_seed(H + P)
+    D, Kd, S, L = 96, 256, 6, 1024
+    lens = [300, 1, 64, 257, 90]
+    T = sum(lens)
+    N = (H + 2 * Hkv) * D
+    a, w = _rand(T, Kd), _rand(N, Kd, scale=Kd ** -0.5)
+    cu = torch.tensor([0] + list(np.cumsum(lens)), device=DEV, dtype=torch.int32)
+    slot = torch.cat([torch.full((n,), b, dtype=torch.int32) for b, n in enumerate(lens)]).to(DEV)
+    pos = torch.cat([torch.arange(P, P + n, dtype=torch.int32) for n in lens]).to(DEV)
+    cs = R.rope_table(L, D, 10000.0, device=DEV)
+    kc, vc = _rand(S, Hkv, L, D), _rand(S, Hkv, L, D)  # slot 5: the shared prefix's keys
+    kc2, vc2 = kc.clone(), vc.clone()
+    qkv = K.gemm_rope(a, w, pos, cs, H, Hkv, D, slot, kc, vc)
+    qkv2 = K.gemm_rope(a, w, pos, cs, H, Hkv, D, slot, kc2, vc2, kv_out=False)
+    assert torch.equal(qkv[:, :H * D], qkv2[:, :H * D]) and torch.equal(kc, kc2) and torch.equal(vc, vc2)
+    pre = (kc[5], vc[5], P) if P else None
+    q, k, v = qkv[:, :H * D], qkv[:, H * D:(H + Hkv) * D], qkv[:, (H + Hkv) * D:]
+    ref = K.flash_attn_varlen(q, k, v, cu, max(lens), H, Hkv, D, True, prefix=pre)
+    got = K.flash_attn_varlen(qkv2[:, :H * D], None, None, cu, max(lens), H, Hkv, D, True, prefix=pre,
+                              kv_cache=(kc2, vc2, slot, pos))
+    assert torch.equal(got, ref)
+    _close(got, R.flash_attn_varlen(q, k, v, cu, max(lens), H, Hkv, D, True, prefix=pre), atol=0.02)
+
+
 @pytest.mark.parametrize("H,Hkv,D", [(32, 32, 96), (32, 8, 128), (8, 1, 128), (12, 6, 64)])
 def test_decode_attn_shared_prefix(H, Hkv, D):
     """Rows whose keys [0, P) live in a shared prefix slot (pre = (P, slot)) vs the fp32 reference."""
