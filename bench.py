@@ -461,7 +461,7 @@ def main():
             try:
                 multi[name] = fn()
             except Exception as e:  # noqa: BLE001 - reported in the JSON line, the headline stands
-                multi[name] = {"ok": False, "error": repr(e)[:300]}
+                multi[name] = {"ok": False, "error": repr(e)[:1000]}
             multi[name]["wall_s"] = round(time.perf_counter() - t_b, 1)
             log(info, f"{name}: {multi[name]}")
 

@@ -56,6 +56,19 @@ class TPContext:
                 # decode-sized rows only (one-shot): 512 KB = 32 rows of Llama-3-70B's 8192
                 self.xgmi_norm = XgmiAllReduce.create(self.group, device, max_bytes=512 << 10)
 
+    def close(self) -> None:
+        """Collective (every TP rank): release the xGMI communicators once no rank uses them any more
+        (a process that builds several TP models, e.g. bench.py's N > 1 blocks, would otherwise keep
+        every model's IPC-exported buffers mapped on every peer)."""
+        comms = [c for c in (self.xgmi, self.xgmi_norm) if c is not None]
+        if not comms:
+            return
+        import torch.distributed as dist
+        dist.barrier(group=self.group)
+        for c in comms:
+            c.close()
+        self.xgmi = self.xgmi_norm = None
+
     def all_reduce_(self, t: torch.Tensor) -> torch.Tensor:
         if self.size > 1:
             if self.xgmi is not None and self.xgmi.takes(t):

@@ -273,6 +273,13 @@ DA_EXPORT int da_ar_malloc(long long bytes, int uncached, void** out) {
 
 DA_EXPORT int da_ar_free(void* p) { return (int)hipFree(p); }
 
+// Zero a pooled communicator buffer before its next use (signals / flags must start at 0).
+DA_EXPORT int da_ar_zero(void* p, long long bytes) {
+  const hipError_t e = hipMemset(p, 0, (size_t)bytes);
+  if (e != hipSuccess) return (int)e;
+  return (int)hipDeviceSynchronize();
+}
+
 DA_EXPORT int da_ar_ipc_handle(void* p, void* handle_out) {
   return (int)hipIpcGetMemHandle((hipIpcMemHandle_t*)handle_out, p);
 }

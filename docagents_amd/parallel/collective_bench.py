@@ -155,9 +155,7 @@ def tp_decode(dec_cfg, full_weights, rank: int, world: int, dev, prompts_by_b: d
     tp.xgmi, tp.xgmi_norm = xg
     if xg[0] is not None:
         out["xgmi_calls"] = xg[0].calls + (xg[1].calls if xg[1] is not None else 0)
-        for c in xg:
-            if c is not None:
-                c.close()
+    tp.close()
     del model
     if verdict:
         from .tp_verify import decision_verdict, verdict_ok

@@ -77,11 +77,13 @@ def decision_verdict(rank: int, world: int, group=None, device="cpu", arch: str 
         stable += n == len(st)
         prefix_ok.append(x.tokens[:n] == y.tokens[:n])  # tokens[t] is the decision of step t
     xg = tp.tp.xgmi
+    calls = xg.calls if xg is not None else 0
+    tp.tp.close()  # collective: the verdict's communicators are not left mapped on the peers
     return {"arch": arch, "world": world, "wrong_order": wrong_order,
             "decisions": len(flat), "checked": len(checked), "checked_agree": agree,
             "prefix_ok": prefix_ok, "stable_prompts": stable, "max_logit_diff": d,
             "max_prob_diff": max(abs(x.mean_prob - y.mean_prob) for x, y in zip(a, b)),
-            "xgmi": xg is not None, "xgmi_calls": xg.calls if xg is not None else 0,
+            "xgmi": xg is not None, "xgmi_calls": calls,
             "gaps": [[round(s_[0], 4) for s_ in st] for st in dec], "tokens": [y.tokens for y in b]}
 
 

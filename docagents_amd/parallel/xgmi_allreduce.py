@@ -39,6 +39,7 @@ def _lib():
         sigs = {
             "da_ar_malloc": ([c_longlong, c_int, ctypes.POINTER(c_void_p)], c_int),
             "da_ar_free": ([c_void_p], c_int),
+            "da_ar_zero": ([c_void_p, c_longlong], c_int),
             "da_ar_ipc_handle": ([c_void_p, c_void_p], c_int),
             "da_ar_ipc_open": ([c_void_p, ctypes.POINTER(c_void_p)], c_int),
             "da_ar_ipc_close": ([c_void_p], c_int),
@@ -56,6 +57,36 @@ def _lib():
         L.da_ar_clock_khz.restype = c_longlong
         _BOUND = True
     return L
+
+
+# Exported communicator buffers are pooled per (device, bytes), never freed: an uncached buffer
+# allocated after another exported one was freed can land inside the runtime's cached range of the
+# old one, and hipIpcGetMemHandle then refuses it (hipErrorInvalidValue on one rank of eight in an
+# 8-rank rehearsal that created a communicator after closing two). A pooled buffer keeps its IPC
+# handle and is zeroed before reuse.
+_POOL: dict = {}
+
+
+def _take(L, dev: torch.device, nbytes: int, hb: int, what: str):
+    """(ptr, handle bytes) of a zeroed, IPC-exported uncached buffer of nbytes on dev."""
+    key = (dev.index if dev.index is not None else torch.cuda.current_device(), nbytes)
+    if _POOL.get(key):
+        p, h = _POOL[key].pop()
+        _ok(L.da_ar_zero(p, nbytes), f"zero({what})")
+        return p, h
+    p = c_void_p()
+    _ok(L.da_ar_malloc(nbytes, 1, byref(p)), f"hipExtMallocWithFlags({what}, uncached)")
+    h = ctypes.create_string_buffer(hb)
+    rc = L.da_ar_ipc_handle(p, h)
+    if rc != 0:
+        L.da_ar_free(p)
+        _ok(rc, f"hipIpcGetMemHandle({what})")
+    return p, h.raw
+
+
+def _give(dev: torch.device, nbytes: int, item) -> None:
+    key = (dev.index if dev.index is not None else torch.cuda.current_device(), nbytes)
+    _POOL.setdefault(key, []).append(item)
 
 
 def _ok(rc: int, what: str):
@@ -81,7 +112,7 @@ class XgmiAllReduce:
         self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
         self.max_bytes = (max_bytes + 15) // 16 * 16
         self.oneshot_max = oneshot_max
-        self._own: list[c_void_p] = []
+        self._own: list = []  # (bytes, (ptr, handle)) taken from the pool
         self._opened: list[c_void_p] = []
         self.calls = 0
         err, payload = "", None
@@ -92,15 +123,12 @@ class XgmiAllReduce:
             self.timeout = int(timeout_ms * self.khz)
             hb = L.da_ar_ipc_handle_bytes()
             with torch.cuda.device(self.device):
-                data, sig = c_void_p(), c_void_p()
-                _ok(L.da_ar_malloc(2 * self.max_bytes, 1, byref(data)), "hipExtMallocWithFlags(staging, uncached)")
-                self._own.append(data)
-                _ok(L.da_ar_malloc(L.da_ar_signal_bytes(), 1, byref(sig)), "hipExtMallocWithFlags(signal, uncached)")
-                self._own.append(sig)
-                hd, hs = ctypes.create_string_buffer(hb), ctypes.create_string_buffer(hb)
-                _ok(L.da_ar_ipc_handle(data, hd), "hipIpcGetMemHandle(staging)")
-                _ok(L.da_ar_ipc_handle(sig, hs), "hipIpcGetMemHandle(signal)")
-            payload = (hd.raw, hs.raw)
+                nd, ns = 2 * self.max_bytes, L.da_ar_signal_bytes()
+                data, hd = _take(L, self.device, nd, hb, "staging")
+                self._own.append((nd, (data, hd)))
+                sig, hs = _take(L, self.device, ns, hb, "signal")
+                self._own.append((ns, (sig, hs)))
+            payload = (hd, hs)
         except Exception as e:  # noqa: BLE001 - reported to every rank below
             err = f"local setup: {e}"
         allh: list = [None] * self.world
@@ -139,7 +167,8 @@ class XgmiAllReduce:
         """All ranks exchange their error string; any error anywhere -> every rank closes and raises."""
         errs: list = [None] * self.world
         dist.all_gather_object(errs, err, group=self.group)
-        bad = [f"rank {r}: {e}" for r, e in enumerate(errs) if e]
+        # the ranks whose own setup failed first (the others only report "a peer failed ...")
+        bad = sorted((f"rank {r}: {e}" for r, e in enumerate(errs) if e), key=lambda m: "a peer failed" in m)
         if bad:
             self.close()
             raise RuntimeError("; ".join(bad))
@@ -247,8 +276,8 @@ class XgmiAllReduce:
         torch.cuda.synchronize(self.device)
         for p in self._opened:
             L.da_ar_ipc_close(p)
-        for p in self._own:
-            L.da_ar_free(p)
+        for nbytes, item in self._own:  # back to the pool (see _POOL)
+            _give(self.device, nbytes, item)
         self._opened, self._own = [], []
 
 
