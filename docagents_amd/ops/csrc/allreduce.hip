@@ -284,6 +284,19 @@ DA_EXPORT int da_ar_ipc_handle(void* p, void* handle_out) {
   return (int)hipIpcGetMemHandle((hipIpcMemHandle_t*)handle_out, p);
 }
 
+// Export the allocation that CONTAINS p: the runtime may hand out a buffer inside a larger block it
+// keeps (seen after other exported buffers were freed: hipIpcGetMemHandle refused the pointer on one
+// rank, or exported the block so that peers mapped its start, not the buffer). The importer adds
+// *offset_out to the pointer hipIpcOpenMemHandle returns.
+DA_EXPORT int da_ar_ipc_export(void* p, void* handle_out, long long* offset_out) {
+  hipDeviceptr_t base = nullptr;
+  size_t size = 0;
+  hipError_t e = hipMemGetAddressRange(&base, &size, (hipDeviceptr_t)p);
+  if (e != hipSuccess) return (int)e;
+  *offset_out = (long long)((char*)p - (char*)base);
+  return (int)hipIpcGetMemHandle((hipIpcMemHandle_t*)handle_out, (void*)base);
+}
+
 DA_EXPORT int da_ar_ipc_handle_bytes() { return (int)sizeof(hipIpcMemHandle_t); }
 
 DA_EXPORT int da_ar_ipc_open(const void* handle, void** out) {

@@ -9,9 +9,10 @@ two-shot (reduce-scatter + all-gather through the same buffers) covers prefill-s
 Setup (once per communicator, NOT inside graph capture): every rank allocates a staging buffer
 (2 x max_bytes, double-buffered by call parity) and a signal block in UNCACHED device memory
 (hipExtMallocWithFlags(..., hipDeviceMallocUncached): peers poll the flags and read the staged rows
-across devices, so no GPU may serve them from a stale L2 line), exports both with
-hipIpcGetMemHandle, exchanges the handles over the process group (all_gather_object), and opens
-the peers' handles. After that a call is one kernel launch with constant arguments, so it is
+across devices, so no GPU may serve them from a stale L2 line), exports the allocations holding
+them (hipMemGetAddressRange + hipIpcGetMemHandle; the buffer's offset inside travels with the
+handle), exchanges the handles over the process group (all_gather_object), and opens the peers'
+handles. Buffers are pooled per process, never freed (see _POOL). After that a call is one kernel launch with constant arguments, so it is
 captured into the decode HIP graph like any other kernel. Kernel: ops/csrc/allreduce.hip.
 
 Falls back to ``torch.distributed.all_reduce`` (RCCL) for tensors it does not take (dtype other
@@ -41,6 +42,7 @@ def _lib():
             "da_ar_free": ([c_void_p], c_int),
             "da_ar_zero": ([c_void_p, c_longlong], c_int),
             "da_ar_ipc_handle": ([c_void_p, c_void_p], c_int),
+            "da_ar_ipc_export": ([c_void_p, c_void_p, ctypes.POINTER(c_longlong)], c_int),
             "da_ar_ipc_open": ([c_void_p, ctypes.POINTER(c_void_p)], c_int),
             "da_ar_ipc_close": ([c_void_p], c_int),
             "da_ar_read_err": ([c_void_p, ctypes.POINTER(ctypes.c_uint)], c_int),
@@ -65,23 +67,30 @@ def _lib():
 # 8-rank rehearsal that created a communicator after closing two). A pooled buffer keeps its IPC
 # handle and is zeroed before reuse.
 _POOL: dict = {}
+_REFUSED: list = []
 
 
 def _take(L, dev: torch.device, nbytes: int, hb: int, what: str):
-    """(ptr, handle bytes) of a zeroed, IPC-exported uncached buffer of nbytes on dev."""
+    """(ptr, (handle bytes, offset)) of a zeroed, IPC-exported uncached buffer of nbytes on dev: the
+    handle names the allocation containing the buffer, which starts ``offset`` bytes into it."""
     key = (dev.index if dev.index is not None else torch.cuda.current_device(), nbytes)
     if _POOL.get(key):
         p, h = _POOL[key].pop()
         _ok(L.da_ar_zero(p, nbytes), f"zero({what})")
         return p, h
-    p = c_void_p()
-    _ok(L.da_ar_malloc(nbytes, 1, byref(p)), f"hipExtMallocWithFlags({what}, uncached)")
-    h = ctypes.create_string_buffer(hb)
-    rc = L.da_ar_ipc_handle(p, h)
-    if rc != 0:
-        L.da_ar_free(p)
-        _ok(rc, f"hipIpcGetMemHandle({what})")
-    return p, h.raw
+    rc = 0
+    for _ in range(4):
+        p = c_void_p()
+        _ok(L.da_ar_malloc(nbytes, 1, byref(p)), f"hipExtMallocWithFlags({what}, uncached)")
+        h, off = ctypes.create_string_buffer(hb), c_longlong(0)
+        rc = L.da_ar_ipc_export(p, h, byref(off))
+        if rc == 0:
+            return p, (h.raw, off.value)
+        # an allocation the runtime will not export (seen only with 8 ranks sharing one GPU, on one
+        # rank, for a buffer allocated late in the process): keep it (freeing it would hand the same
+        # range back) and allocate another
+        _REFUSED.append(p)
+    _ok(rc, f"hipIpcGetMemHandle({what})")
 
 
 def _give(dev: torch.device, nbytes: int, item) -> None:
@@ -136,6 +145,15 @@ class XgmiAllReduce:
         dptr, sptr = [], []
         if not err and any(h is None for h in allh):
             err = "a peer failed its local setup"
+        mapped: dict = {}
+
+        def open_once(h: bytes, r: int) -> int:
+            if h not in mapped:
+                p = c_void_p()
+                _ok(L.da_ar_ipc_open(ctypes.create_string_buffer(h, hb), byref(p)), f"hipIpcOpenMemHandle(rank {r})")
+                self._opened.append(p)
+                mapped[h] = p.value
+            return mapped[h]
         if not err:
             try:
                 with torch.cuda.device(self.device):
@@ -144,15 +162,10 @@ class XgmiAllReduce:
                             dptr.append(data.value)
                             sptr.append(sig.value)
                             continue
-                        pd, ps = c_void_p(), c_void_p()
-                        _ok(L.da_ar_ipc_open(ctypes.create_string_buffer(h_d, hb), byref(pd)),
-                            f"hipIpcOpenMemHandle(rank {r})")
-                        self._opened.append(pd)
-                        _ok(L.da_ar_ipc_open(ctypes.create_string_buffer(h_s, hb), byref(ps)),
-                            f"hipIpcOpenMemHandle(rank {r})")
-                        self._opened.append(ps)
-                        dptr.append(pd.value)
-                        sptr.append(ps.value)
+                        # the peer's buffers inside the mapped allocations (staging and signal
+                        # may share one: each allocation is opened once)
+                        dptr.append(open_once(h_d[0], r) + h_d[1])
+                        sptr.append(open_once(h_s[0], r) + h_s[1])
             except Exception as e:  # noqa: BLE001
                 err = f"peer mapping: {e}"
         self._agree(err)  # every peer mapped everywhere, or every rank raises
@@ -295,7 +308,7 @@ def verify_and_time(group=None, device=None, iters: int = 50,
     dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
     world, rank = dist.get_world_size(group), dist.get_rank(group)
     ar = XgmiAllReduce(group, dev, max_bytes=16 << 20)
-    res: dict = {"world": world, "ok": True, "cases": []}
+    res: dict = {"world": world, "ok": True, "cases": [], "export_refusals": len(_REFUSED)}
     for i, n in enumerate((64 * 3072, 1 << 20, 6 << 20)):
         xs = [torch.randn(n, generator=torch.Generator().manual_seed(7000 + 31 * i + r)).bfloat16()
               for r in range(world)]
