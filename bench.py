@@ -124,8 +124,8 @@ def main():
     ap.add_argument("--enc", default="bge-base")
     ap.add_argument("--llm", default="phi3-mini")
     ap.add_argument("--latency-reps", type=int, default=24, help="batch-1 cache-miss queries for p50 / p90")
-    ap.add_argument("--ingest-docs", type=int, default=64,
-                    help="docs per GPU per ingest batch (one engine batch, like the QA batch)")
+    ap.add_argument("--ingest-docs", type=int, default=None,
+                    help="docs per GPU per ingest batch (default: one engine batch, the QA --batch)")
     ap.add_argument("--ingest-batches", type=int, default=3,
                     help="timed ingest batches (distinct documents); docs/min is their median")
     ap.add_argument("--ingest-words", type=int, default=2000)
@@ -163,6 +163,8 @@ def main():
                     help="single-document ingest latency reps (upload -> summary readable, engine level)")
     a = ap.parse_args()
 
+    if a.ingest_docs is None:
+        a.ingest_docs = a.batch
     info = init_from_env()
     W, R = info.world, info.rank
     if any(k.startswith("DA_") for k in os.environ):  # A/B arms (bench/ab_arms.py): only when asked
