@@ -1,4 +1,4 @@
-"""Decode GEMMs (M <= 64): split-K LDS tile, register prefetch depth PF x split count. Timed the way the decoder runs them: one HIP graph of
+"""Decode GEMMs (M <= 128): split-K LDS tile (--tiles to compare tiles), register prefetch depth PF x split count. Timed the way the decoder runs them: one HIP graph of
 back-to-back calls, each on a different weight copy (>= 1 GiB of copies, so every call streams its
 weights cold from HBM as a decode step does). Times include the split-K reduction / fused epilogue
 exactly as the decoder calls it (o / down: resid + RMSNorm tail; gate/up: SwiGLU; qkv / LM head:
@@ -49,6 +49,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--shapes", default="phi3")
     ap.add_argument("--m", default="64,16")
+    ap.add_argument("--tiles", default="auto", help="comma list of gemm tiles (2 = 64x128, 9 = 128x64, ...) or auto")
     a = ap.parse_args()
     models = list(SHAPES) if a.shapes == "all" else a.shapes.split(",")
     for model in models:
@@ -70,12 +71,15 @@ def main():
                                    splits=splits)
                     return run
                 res = {}
-                tile = K._decode_tile(M)
                 auto_s = K._auto_splits(M, N, Kd)
-                for sp in (1, 2, 4, 8, 16):
-                    if (Kd // 64) % sp:
-                        continue
-                    res[f"s{sp}"] = timed(runner(tile, sp), ncopy)
+                tiles = [K._decode_tile(M)] if a.tiles == "auto" else [int(t) for t in a.tiles.split(",")]
+                for tile in tiles:
+                    if kind == "norm" and M > 64 and tile != 9:
+                        continue  # the fused reduce + norm runs on the 128x64 tile above 64 rows
+                    for sp in (1, 2, 4, 8, 16):
+                        if (Kd // 64) % sp:
+                            continue
+                        res[f"t{tile}s{sp}" if len(tiles) > 1 else f"s{sp}"] = timed(runner(tile, sp), ncopy)
                 best = min(res, key=res.get)
                 print(json.dumps({"model": model, "gemm": name, "M": M, "N": N, "K": Kd, "MB": round(by / 1e6, 1),
                                   "us": {k: round(v, 1) for k, v in res.items()}, "auto_splits": auto_s,

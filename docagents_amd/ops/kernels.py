@@ -240,7 +240,7 @@ def gemm(a: torch.Tensor, w: torch.Tensor, bias=None, epi: int = EPI_NONE, resid
             _bf16_cuda(gamma, "gamma"); _req(gamma.numel() == K, "gamma must be [K]")
     if splits <= 0:
         if tile == 0 and M < 640:
-            tile = _decode_tile(M)
+            tile = _decode_tile(M, N)
         splits = _auto_splits(M, N, K) if tile in (0, 2, 3) or (tile == 9 and M <= 128) else 1
     ws = None
     if splits > 1:
@@ -434,7 +434,7 @@ def gemm_resid_norm(a, w, resid, gamma, eps: float, out=None, h_out=None, bias=N
         h_out = torch.empty((M, N), dtype=torch.bfloat16, device=a.device)
     if M == 0:
         return h_out
-    tile = tile or _decode_tile(M)
+    tile = tile or (9 if M > 64 else _decode_tile(M))  # the fused reduce + norm: 128x64 tile above 64 rows
     if splits <= 0:
         splits = _auto_splits(M, N, K)
     ws = _workspace(splits * M * N * 4, a.device)
@@ -444,15 +444,18 @@ def gemm_resid_norm(a, w, resid, gamma, eps: float, out=None, h_out=None, bias=N
     return h_out
 
 
-def _decode_tile(M: int) -> int:
+def _decode_tile(M: int, N: int = 0) -> int:
     """Decode-sized M: 32x128 tiles up to 32 rows, 64x128 to 64; 65..128 rows (a batch-128 decode
-    step) one 128x64 weight-streaming tile per 64 weight rows, so every weight byte is read by ONE
-    workgroup (32-layer Phi-3 chain at M = 96 / 128: 3.47 / 3.78 ms vs 3.73 / 4.10 ms on the 64x128
-    tile over two row blocks, profiles/r5/midm/); 129..639 rows the 64x128 tile over ceil(M/64)
-    row blocks."""
+    step): N >= 8192 (QKV, gate/up, LM head: >= 128 weight tiles) the 64x128 tile over the two row
+    blocks without split-K, else one 128x64 weight-streaming tile per 64 weight rows with split-K
+    (profiles/r5/midm/decode_gemm_sweep_m128.txt, weights cold: QKV 28.0 vs 33.5 us, gate/up 30.5 vs
+    47.4 us at 128 rows vs the 128x64 tile at split 4; O / down best on the 128x64 tile at split 4);
+    129..639 rows the 64x128 tile over ceil(M/64) row blocks."""
     if M <= 32:
         return 3
-    return 9 if 64 < M <= 128 else 2
+    if 64 < M <= 128:
+        return 2 if N >= 8192 else 9
+    return 2
 
 
 def _auto_splits(M: int, N: int, K: int) -> int:
@@ -465,7 +468,9 @@ def _auto_splits(M: int, N: int, K: int) -> int:
     if M >= 640:
         return 1
     ksteps = K // 64
-    if _decode_tile(M) == 9:  # 65..128 rows: 4 splits (the same chain sweep), fewer if K is short
+    if 64 < M <= 128:  # (see _decode_tile) wide N: no split; else 4 splits, fewer if K is short
+        if N >= 8192:
+            return 1
         s = 4
         while s > 1 and (ksteps % s or ksteps // s < 4):
             s //= 2
