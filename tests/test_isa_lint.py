@@ -21,9 +21,11 @@ HOT_NO_SCRATCH = {  # mangled-name prefixes of the kernels the flagship bench ru
                       "_Z20flash_attn_v2_kernelILi64ELi4ELi1E", "_Z20flash_attn_v2_kernelILi128ELi8ELi1E"],
     "gemm.hip": ["_Z11gemv_kernel", "_Z16gemm_bf16_kernelILi64ELi128ELi1ELi4ELi5ELi4EE",
                  "_Z16gemm_bf16_kernelILi32ELi128ELi1ELi4ELi5ELi4EE",
+                 "_Z16gemm_bf16_kernelILi128ELi64ELi2ELi2ELi5ELi4EE",  # 65..128-row decode (O / down)
                  "_Z18gemm_splitk_reduce", "_Z23splitk_reduce_resid_ssq"],
     "gemm8p.hip": ["_Z13gemm8p_kernelILi6ELi256E", "_Z13gemm8p_kernelILi3ELi256E", "_Z13gemm8p_kernelILi4ELi256E"],
     "gemm_dk.hip": ["_Z14gemm_dk_kernel"],
+    "vecsearch.hip": ["_Z24topk_dense_stream_kernel", "_Z20topk_dense_mq_kernel"],  # the shard scans
 }
 NO_SERIAL_LOAD_LOOPS = {"gemm.hip": ["_Z18gemm_splitk_reduce", "_Z23splitk_reduce_resid_ssq",
                                      "_Z27splitk_reduce_resid_rmsnorm"],
