@@ -286,44 +286,86 @@ gemm8p_kernel(GemmArgs p) {
     rhead = rel / R.D;
     rd0 = rel % R.D;
   }
-  for (int lr = lane / CPR; lr < BM / 2; lr += RPI) {
-    const int gm = m0 + (lr / QR) * (BM / 2) + wg * QR + (lr % QR);
-    if (gm >= p.M || gcol >= ncols) continue;
-    u32x4_t v = *(const u32x4_t*)(st + lr * SROW + (jh * HC + cc) * 2);
+  // This lane's rows lr = lane / CPR + i * RPI, in batches of NB whose global loads (residual rows;
+  // RoPE positions, slots, then cos / sin) are all issued before any is waited for: the one-row-at-
+  // a-time loop waited a memory round trip per row for those loads (16 per tile per wave, ISA:
+  // global_load + s_waitcnt vmcnt(0) each iteration).
+  constexpr int NI = (BM / 2) / RPI;
+  constexpr int NB = NI < 8 ? NI : 8;
+  const int lr0 = lane / CPR;
+  const bool col_ok = gcol < ncols;
+  for (int i0 = 0; i0 < NI; i0 += NB) {
+    int gmv[NB];
+    u32x4_t vv[NB];
+    [[maybe_unused]] u32x4_t rr[NB];
+    [[maybe_unused]] int psv[NB], slv[NB];
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+      const int lr = lr0 + (i0 + i) * RPI;
+      gmv[i] = m0 + (lr / QR) * (BM / 2) + wg * QR + (lr % QR);
+      const int gmc = min(gmv[i], p.M - 1);  // loads of rows past M read a valid row, never stored
+      vv[i] = *(const u32x4_t*)(st + lr * SROW + (jh * HC + cc) * 2);
+      if constexpr (EPI == EPI_RESID)
+        rr[i] = *(const u32x4_t*)(p.resid + (size_t)gmc * p.ldr + (col_ok ? gcol : 0));
+      if constexpr (EPI == EPI_ROPE) {
+        psv[i] = p.rope.pos[gmc];
+        slv[i] = p.rope.slot[gmc];
+      }
+    }
     if constexpr (EPI == EPI_ROPE) {
       // same bf16 roundings as GEMM -> rope_cache: rotate the bf16-rounded outputs in fp32
       const RopeArgs& R = p.rope;
-      const int ps = R.pos[gm];
-      DA_ASSERT(ps >= 0 && ps < R.max_seq && R.slot[gm] >= 0);
+      const int half = R.D / 2, i0c = rd0 / 2;
+      f32x4_t c01[NB], c23[NB];
       if (rkind < 2) {
-        const int half = R.D / 2, i0 = rd0 / 2;
-        const f32x4_t c01 = *(const f32x4_t*)(R.cs + ((size_t)ps * half + i0) * 2);
-        const f32x4_t c23 = *(const f32x4_t*)(R.cs + ((size_t)ps * half + i0) * 2 + 4);
-        const float ccs[4] = {c01[0], c01[2], c23[0], c23[2]}, sns[4] = {c01[1], c01[3], c23[1], c23[3]};
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const float x1 = bf2f((bf16_t)(v[e] & 0xffff)), x2 = bf2f((bf16_t)(v[e] >> 16));
-          const float o1 = x1 * ccs[e] - x2 * sns[e];
-          const float o2 = x2 * ccs[e] + x1 * sns[e];
-          v[e] = pack_bf2(o1, o2);
+        for (int i = 0; i < NB; ++i) {
+          const int ps = min(max(psv[i], 0), R.max_seq - 1);
+          c01[i] = *(const f32x4_t*)(R.cs + ((size_t)ps * half + i0c) * 2);
+          c23[i] = *(const f32x4_t*)(R.cs + ((size_t)ps * half + i0c) * 2 + 4);
         }
       }
-      if (rkind > 0) {
-        bf16_t* cache = rkind == 1 ? R.kc : R.vc;
-        *(u32x4_t*)(cache + (((size_t)R.slot[gm] * R.Hkv + rhead) * R.max_seq + ps) * R.D + rd0) = v;
-        if (!R.kv_out) continue;  // k / v live in the cache only: no second copy in C
-      }
-    }
-    if constexpr (EPI == EPI_RESID) {
-      const u32x4_t r = *(const u32x4_t*)(p.resid + (size_t)gm * p.ldr + gcol);
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const float lo = T::to_f((bf16_t)(v[e] & 0xffff)) + T::to_f((bf16_t)(r[e] & 0xffff));
-        const float hi = T::to_f((bf16_t)(v[e] >> 16)) + T::to_f((bf16_t)(r[e] >> 16));
-        v[e] = T::pack2(lo, hi);
+      for (int i = 0; i < NB; ++i) {
+        const int gm = gmv[i];
+        if (gm >= p.M || !col_ok) continue;
+        u32x4_t v = vv[i];
+        DA_ASSERT(psv[i] >= 0 && psv[i] < R.max_seq && slv[i] >= 0);
+        if (rkind < 2) {
+          const float ccs[4] = {c01[i][0], c01[i][2], c23[i][0], c23[i][2]};
+          const float sns[4] = {c01[i][1], c01[i][3], c23[i][1], c23[i][3]};
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float x1 = bf2f((bf16_t)(v[e] & 0xffff)), x2 = bf2f((bf16_t)(v[e] >> 16));
+            const float o1 = x1 * ccs[e] - x2 * sns[e];
+            const float o2 = x2 * ccs[e] + x1 * sns[e];
+            v[e] = pack_bf2(o1, o2);
+          }
+        }
+        if (rkind > 0) {
+          bf16_t* cache = rkind == 1 ? R.kc : R.vc;
+          *(u32x4_t*)(cache + (((size_t)slv[i] * R.Hkv + rhead) * R.max_seq + psv[i]) * R.D + rd0) = v;
+          if (!R.kv_out) continue;  // k / v live in the cache only: no second copy in C
+        }
+        *(u32x4_t*)(p.C + (size_t)gm * p.ldc + gcol) = v;
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < NB; ++i) {
+        const int gm = gmv[i];
+        if (gm >= p.M || !col_ok) continue;
+        u32x4_t v = vv[i];
+        if constexpr (EPI == EPI_RESID) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float lo = T::to_f((bf16_t)(v[e] & 0xffff)) + T::to_f((bf16_t)(rr[i][e] & 0xffff));
+            const float hi = T::to_f((bf16_t)(v[e] >> 16)) + T::to_f((bf16_t)(rr[i][e] >> 16));
+            v[e] = T::pack2(lo, hi);
+          }
+        }
+        *(u32x4_t*)(p.C + (size_t)gm * p.ldc + gcol) = v;
       }
     }
-    *(u32x4_t*)(p.C + (size_t)gm * p.ldc + gcol) = v;
   }
 }
 
