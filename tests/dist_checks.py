@@ -416,6 +416,34 @@ def check_xgmi_verify_and_time(rank, world, port, out_path):
     _done(rank, out_path, verify_and_time(None, dev, iters=10))
 
 
+def check_xgmi_reuse(rank, world, port, out_path):
+    """Communicators created, used and closed repeatedly in one process, as bench.py's N > 1 blocks
+    do (TP model + its norm communicator, closed; the verdict's pair, closed; a third size): every
+    all-reduce exact, the pooled buffers reused for a size seen before."""
+    _init(rank, world, port)
+    import docagents_amd.parallel.xgmi_allreduce as X
+    dev = torch.device("cuda", rank % torch.cuda.device_count())
+    torch.cuda.set_device(dev)
+    verdict = {"rounds": [], "ok": True}
+    for rnd, sizes in enumerate([(32 << 20, 512 << 10), (32 << 20, 512 << 10), (16 << 20,), (32 << 20,)]):
+        comms = [X.XgmiAllReduce(None, dev, max_bytes=b) for b in sizes]
+        for i, c in enumerate(comms):
+            n = 64 * 3072 + 8 * i
+            x = torch.full((n,), float(rank + 1 + rnd), dtype=torch.float32, device=dev)
+            c.all_reduce_(x)
+            torch.cuda.synchronize(dev)
+            want = sum(r + 1 + rnd for r in range(world))
+            ok = bool((x == want).all())
+            verdict["rounds"].append({"round": rnd, "max_bytes": sizes[i], "ok": ok})
+            verdict["ok"] &= ok
+        dist.barrier()
+        for c in comms:
+            c.close()
+    verdict["pooled_sizes"] = sorted(k[1] for k in X._POOL)
+    verdict["pooled_buffers"] = sum(len(v) for v in X._POOL.values())
+    _done(rank, out_path, verdict)
+
+
 def check_xgmi_allreduce_norm(rank, world, port, out_path):
     """C3 with the RMSNorm in the all-reduce's epilogue (one launch) vs the all-reduce kernel
     followed by the rmsnorm kernel: x and h must be BIT-identical, for several row widths / row

@@ -50,6 +50,19 @@ def test_bench_xgmi_cross_device_check_passes(tmp_path):
     assert all(r["xgmi"] > 0 for r in v["us_per_call"].values()) and v["us_per_call"]["6MB"]["twoshot"], v
 
 
+def test_xgmi_communicators_recreated_in_one_process(tmp_path):
+    """Create / use / close communicators repeatedly (bench.py's N > 1 sequence): exact sums every
+    round, and the exported buffers pooled and reused instead of freed (an uncached buffer allocated
+    after an exported one was freed could not be exported on an 8-rank rehearsal)."""
+    out = tmp_path / "reuse.json"
+    mp.spawn(dist_checks.check_xgmi_reuse, args=(2, _port(), str(out)), nprocs=2, join=True)
+    v = json.loads(out.read_text())
+    assert v["ok"], v
+    # three staging sizes (2 x 32 MB, 2 x 512 KB, 2 x 16 MB) and the two signal blocks that were
+    # live at once: rounds 2 and 4 reused round 1's buffers, round 3 one signal block
+    assert v["pooled_buffers"] == 3 + 2, v
+
+
 def _tp_ok(v) -> bool:
     return (v["max_logit_diff"] < 0.05 and v["checked"] >= 0.6 * v["decisions"]
             and v["checked_agree"] == v["checked"] and all(v["prefix_ok"]) and v["max_prob_diff"] < 1e-3)
