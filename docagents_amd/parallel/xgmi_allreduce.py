@@ -124,6 +124,24 @@ class XgmiAllReduce:
         self._own: list = []  # (bytes, (ptr, handle)) taken from the pool
         self._opened: list[c_void_p] = []
         self.calls = 0
+        # The probe names the ranks whose staged rows no peer saw (an export that mapped other
+        # memory: seen once on an 8-rank rehearsal sharing one GPU); those ranks set their buffers
+        # aside and every rank sets up again, up to twice.
+        for attempt in range(3):
+            self._setup(grid, timeout_ms)  # every peer mapped everywhere, or every rank raises
+            if probe_ms <= 0:
+                return
+            res: list = [None] * self.world
+            dist.all_gather_object(res, self._probe(probe_ms), group=self.group)
+            if not any(e for e, _ in res):
+                return
+            unseen = set.intersection(*(set(m) | {r} for r, (_, m) in enumerate(res)))
+            if not unseen or attempt == 2:
+                self.close()
+                raise RuntimeError("; ".join(f"rank {r}: {e}" for r, (e, _) in enumerate(res) if e))
+            self.close(quarantine=self.rank in unseen)
+
+    def _setup(self, grid: int, timeout_ms: int) -> None:
         err, payload = "", None
         try:
             L = _lib()
@@ -141,7 +159,7 @@ class XgmiAllReduce:
         except Exception as e:  # noqa: BLE001 - reported to every rank below
             err = f"local setup: {e}"
         allh: list = [None] * self.world
-        dist.all_gather_object(allh, payload, group=group)
+        dist.all_gather_object(allh, payload, group=self.group)
         dptr, sptr = [], []
         if not err and any(h is None for h in allh):
             err = "a peer failed its local setup"
@@ -172,9 +190,7 @@ class XgmiAllReduce:
         self._data = (c_void_p * self.world)(*dptr)
         self._sig = (c_void_p * self.world)(*sptr)
         self._sig_self = sig
-        dist.barrier(group=group)  # every peer mapped before anyone launches
-        if probe_ms > 0:
-            self._agree(self._probe(probe_ms))
+        dist.barrier(group=self.group)  # every peer mapped before anyone launches
 
     def _agree(self, err: str) -> None:
         """All ranks exchange their error string; any error anywhere -> every rank closes and raises."""
@@ -186,27 +202,33 @@ class XgmiAllReduce:
             self.close()
             raise RuntimeError("; ".join(bad))
 
-    def _probe(self, probe_ms: int) -> str:
-        """One all-reduce of a known pattern with a short bounded wait: '' when the sum arrived and no
-        barrier timed out (flags and staged rows visible across the devices), else why not."""
+    def _probe(self, probe_ms: int) -> tuple:
+        """One all-reduce of rank r's 2^r with a short bounded wait: ('', []) when the exact sum
+        arrived and no barrier timed out (flags and staged rows visible across the devices), else
+        (why, the ranks whose rows this rank did not see)."""
         saved = self.timeout
         self.timeout = int(probe_ms * self.khz)
         try:
             # every workgroup of the grid takes part when the staging allows (fp32: 4 per 16-B vector)
             n = max(4, min(self.grid * 256 * 4, self.max_bytes // 4) // 4 * 4)
-            t = torch.full((n,), float(self.rank + 1), dtype=torch.float32, device=self.device)
+            t = torch.full((n,), float(1 << self.rank), dtype=torch.float32, device=self.device)
             self.all_reduce_(t)
             torch.cuda.synchronize(self.device)
-            want = self.world * (self.world + 1) / 2
+            want = (1 << self.world) - 1
             err = ctypes.c_uint(0)
             _ok(_lib().da_ar_read_err(self._sig_self, byref(err)), "read all-reduce error flag")
             if err.value:
-                return "probe: a barrier timed out (peer flags not visible across devices)"
+                return "probe: a barrier timed out (peer flags not visible across devices)", []
             if not bool(torch.all(t == want)):
-                return "probe: wrong sum (staged rows not visible across devices)"
-            return ""
+                got = t.cpu()
+                seen = want
+                for v in got.unique().tolist():  # sums of whole powers of two name the ranks seen
+                    seen &= int(v) if float(v).is_integer() and 0 <= v <= want else 0
+                missing = [r for r in range(self.world) if not (seen >> r) & 1]
+                return f"probe: wrong sum (staged rows of ranks {missing} not visible)", missing
+            return "", []
         except Exception as e:  # noqa: BLE001
-            return f"probe: {e}"
+            return f"probe: {e}", []
         finally:
             self.timeout = saved
 
@@ -282,7 +304,9 @@ class XgmiAllReduce:
         if err.value:
             raise RuntimeError("xGMI all-reduce barrier timed out (peer missing or call sequences diverged)")
 
-    def close(self):
+    def close(self, quarantine: bool = False):
+        """Unmap the peers and return this rank's buffers to the pool (quarantine: set them aside,
+        never reused — the probe found peers could not see them)."""
         if not self._own and not self._opened:
             return
         L = _lib()
@@ -290,7 +314,10 @@ class XgmiAllReduce:
         for p in self._opened:
             L.da_ar_ipc_close(p)
         for nbytes, item in self._own:  # back to the pool (see _POOL)
-            _give(self.device, nbytes, item)
+            if quarantine:
+                _REFUSED.append(item[0])
+            else:
+                _give(self.device, nbytes, item)
         self._opened, self._own = [], []
 
 
@@ -307,7 +334,10 @@ def verify_and_time(group=None, device=None, iters: int = 50,
     through this kernel vs RCCL ``all_reduce`` on the same group (RCCL only on the nccl backend)."""
     dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
     world, rank = dist.get_world_size(group), dist.get_rank(group)
-    ar = XgmiAllReduce(group, dev, max_bytes=16 << 20)
+    # the TP communicators' sizes (32 MB, 512 KB): the pooled buffers of an earlier TP model are
+    # reused rather than a fresh buffer exported late in the process (on an 8-rank rehearsal sharing
+    # one GPU a late 32 MB export mapped other memory on one rank: the probe caught it)
+    ar = XgmiAllReduce(group, dev)
     res: dict = {"world": world, "ok": True, "cases": [], "export_refusals": len(_REFUSED)}
     for i, n in enumerate((64 * 3072, 1 << 20, 6 << 20)):
         xs = [torch.randn(n, generator=torch.Generator().manual_seed(7000 + 31 * i + r)).bfloat16()
