@@ -196,7 +196,9 @@ __device__ __forceinline__ float gelu_erf(float x) {
   return 0.5f * x * (1.f + erff(x * 0.70710678118654752f));
 }
 
-__device__ __forceinline__ float silu(float x) { return x / (1.f + __expf(-x)); }
+// x * sigmoid(x) with the hardware reciprocal (1 ulp) instead of an IEEE division (a 10-instruction
+// scale / fma / fixup sequence per element): every caller rounds the result to bf16.
+__device__ __forceinline__ float silu(float x) { return x * __builtin_amdgcn_rcpf(1.f + __expf(-x)); }
 
 // Bijective XCD-aware remap of a flat workgroup id (cdna_hip_programming.md §5,
 // "XCD swizzle must be bijective"): blocks that share an XCD (b % 8) get a

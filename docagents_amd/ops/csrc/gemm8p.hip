@@ -166,7 +166,7 @@ gemm8p_kernel(GemmArgs p) {
 #pragma unroll
       for (int i = 0; i < MI; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) acc[IH][JH][i][j] = T::mma16(ra[kk][i], rb[kk][j], acc[IH][JH][i][j]);
+        for (int j = 0; j < 2; ++j) acc[IH][JH][i][j] = T::mma16(rb[kk][j], ra[kk][i], acc[IH][JH][i][j]);
   };
   using I0 = std::integral_constant<int, 0>;
   using I1 = std::integral_constant<int, 1>;
@@ -223,33 +223,39 @@ gemm8p_kernel(GemmArgs p) {
   __syncthreads();
 
   // ---- epilogue: registers -> (bias / GELU / SwiGLU) -> bf16 staging -> coalesced stores.
-  //      Staged row lr = ih*QR + i*16 + fg*4 + q (tile row ih*BM/2 + wg*QR + (lr % QR)),
-  //      staged column lc = jh*32 + j*16 + fr (tile column jh*128 + wn*32 + (lc & 31)).
+  //      Staged row lr = ih*QR + i*16 + fr (tile row ih*BM/2 + wg*QR + (lr % QR)), staged
+  //      columns lc = jh*32 + j*16 + 4 fg .. + 3 (tile columns jh*128 + wn*32 + (lc & 31)).
   char* st = smem + wid * (BM / 2) * SROW;
+  // The MFMAs run with W as the A operand (D^T): lane (fr, fg) holds output row i*16 + fr of its
+  // 16 x 16 block and the 4 CONSECUTIVE output columns 4 fg .. 4 fg + 3, so a lane stages 8 B per
+  // block (one ds_write_b64 of 4 packed bf16) instead of 4 separate 2-byte writes.
   if constexpr (EPI == EPI_SWIGLU) {
-    // W rows interleaved in 16-row (gate, up) groups: j = 0 is gate, j = 1 is up of output
-    // columns (n0 + jh*128 + wn*32) / 2 + fr
+    // W rows interleaved in 16-row (gate, up) groups: j = 0 is gate, j = 1 is up of output columns
+    // (n0 + jh*128 + wn*32) / 2 + 4 fg + q
 #pragma unroll
     for (int ih = 0; ih < 2; ++ih)
 #pragma unroll
       for (int jh = 0; jh < 2; ++jh)
 #pragma unroll
-        for (int i = 0; i < MI; ++i)
+        for (int i = 0; i < MI; ++i) {
+          float v[4];
 #pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            const float v = silu(acc[ih][jh][i][0][q]) * acc[ih][jh][i][1][q];
-            *(bf16_t*)(st + (ih * QR + i * 16 + fg * 4 + q) * SROW + (jh * 16 + fr) * 2) = T::from_f(v);
-          }
+          for (int q = 0; q < 4; ++q) v[q] = silu(acc[ih][jh][i][0][q]) * acc[ih][jh][i][1][q];
+          *(u32x2_t*)(st + (ih * QR + i * 16 + fr) * SROW + (jh * 16 + fg * 4) * 2) =
+              u32x2_t{T::pack2(v[0], v[1]), T::pack2(v[2], v[3])};
+        }
   } else {
-    float bv[2][2] = {{0.f, 0.f}, {0.f, 0.f}};
+    float bv[2][2][4] = {};
     if (p.bias) {
 #pragma unroll
       for (int jh = 0; jh < 2; ++jh)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          const int gc = n0 + jh * 128 + wn * 32 + j * 16 + fr;
-          bv[jh][j] = gc < p.N ? T::to_f(p.bias[gc]) : 0.f;
-        }
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const int gc = n0 + jh * 128 + wn * 32 + j * 16 + fg * 4 + q;
+            bv[jh][j][q] = gc < p.N ? T::to_f(p.bias[gc]) : 0.f;
+          }
     }
 #pragma unroll
     for (int ih = 0; ih < 2; ++ih)
@@ -258,13 +264,16 @@ gemm8p_kernel(GemmArgs p) {
 #pragma unroll
         for (int i = 0; i < MI; ++i)
 #pragma unroll
-          for (int j = 0; j < 2; ++j)
+          for (int j = 0; j < 2; ++j) {
+            float v[4];
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
-              float v = acc[ih][jh][i][j][q] + bv[jh][j];
-              if constexpr (EPI == EPI_GELU) v = gelu_erf(v);
-              *(bf16_t*)(st + (ih * QR + i * 16 + fg * 4 + q) * SROW + (jh * 32 + j * 16 + fr) * 2) = T::from_f(v);
+              v[q] = acc[ih][jh][i][j][q] + bv[jh][j][q];
+              if constexpr (EPI == EPI_GELU) v[q] = gelu_erf(v[q]);
             }
+            *(u32x2_t*)(st + (ih * QR + i * 16 + fr) * SROW + (jh * 32 + j * 16 + fg * 4) * 2) =
+                u32x2_t{T::pack2(v[0], v[1]), T::pack2(v[2], v[3])};
+          }
   }
   __syncthreads();
   constexpr bool SW = (EPI == EPI_SWIGLU);
