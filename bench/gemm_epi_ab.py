@@ -13,7 +13,10 @@ from docagents_amd.ops import kernels as K  # noqa: E402
 from docagents_amd.ops import reference as R  # noqa: E402
 
 if os.environ.get("DA_LIB"):
+    import ctypes
     K._LIB_PATH = Path(os.environ["DA_LIB"])
+    _probe = ctypes.CDLL(str(K._LIB_PATH))  # an older library lacks newer exports: do not bind those
+    K._SIGS = {n: a for n, a in K._SIGS.items() if hasattr(_probe, n)}
 
 
 def timed(fn, reps=20):
@@ -53,7 +56,7 @@ def main():
     w3 = (torch.randn(16384, Kd, device=dev, generator=g) * Kd ** -0.5).to(torch.bfloat16)
     c3 = torch.empty(M, 8192, device=dev, dtype=torch.bfloat16)
     out["swiglu_16384"] = timed(lambda: K.gemm(a, w3, epi=K.EPI_SWIGLU, out=c3))
-    print(json.dumps({"lib": os.environ.get("DA_LIB", "in-tree"), "ms": {k: round(v, 4) for k, v in out.items()}}),
+    print(json.dumps({"lib": os.environ.get("DA_LIB", "in-tree"), "persist": os.environ.get("DA_GEMM8P_PERSIST", "default"), "ms": {k: round(v, 4) for k, v in out.items()}}),
           flush=True)
 
 

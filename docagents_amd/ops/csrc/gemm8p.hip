@@ -31,8 +31,12 @@
 //    out, and the k / v chunks are also stored into the KV cache — the rope_cache pass folded in
 //    (kv_out = 0: ONLY into the cache; the prefill attention then reads its keys there, and the
 //    epilogue writes 2/3 fewer bytes of the QKV tile — the store tail is issue-bound).
+//  * PERSIST: one workgroup per CU walks tile ids b, b + G, ... (G a multiple of 8: each id stays on
+//    the workgroup's XCD); the staged rows go to registers, then the next tile's prologue DMA is
+//    issued before this tile's stores (profiles/r5/gemm_persist/: +0.3..1 %, not for EPI_ROPE).
 #include "gemm.h"
 
+#include <cstdlib>
 #include <type_traits>
 
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
@@ -48,7 +52,7 @@ __device__ __forceinline__ void vmcnt() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-template <int EPI, int BM, typename T = BF16T>
+template <int EPI, int BM, typename T = BF16T, bool PERSIST = false>
 __global__ void __launch_bounds__(512)
 gemm8p_kernel(GemmArgs p) {
   static_assert(BM == 256 || BM == 128, "BM");
@@ -68,40 +72,52 @@ gemm8p_kernel(GemmArgs p) {
   const int wg = wid >> 2, wn = wid & 3;
   const int fr = lane & 15, fg = lane >> 4;
 
-  const int ntm = (p.M + BM - 1) / BM, ntn = (p.N + BN - 1) / BN;
-  const int t = xcd_remap(blockIdx.x, ntm * ntn);
+  const int ntm = (p.M + BM - 1) / BM, ntn = (p.N + BN - 1) / BN, ntiles = ntm * ntn;
   const int GROUP = p.group > 0 ? p.group : 4;
-  const int gid = t / (GROUP * ntn);
-  const int first_m = gid * GROUP;
-  const int gsz = min(ntm - first_m, GROUP);
-  const int tin = t % (GROUP * ntn);
-  const int m0 = (first_m + tin % gsz) * BM, n0 = (tin / gsz) * BN;
+  // tile id -> (m0, n0): bijective XCD remap, then grouped-M order. PERSIST: workgroup b runs ids
+  // b, b + G, b + 2G, ... (G = gridDim.x, a multiple of 8, so every id it runs maps to its own XCD)
+  auto tile_of = [&](int id, int& m0_, int& n0_) __attribute__((always_inline)) {
+    const int t = xcd_remap(id, ntiles);
+    const int gid = t / (GROUP * ntn);
+    const int first_m = gid * GROUP;
+    const int gsz = min(ntm - first_m, GROUP);
+    const int tin = t % (GROUP * ntn);
+    m0_ = (first_m + tin % gsz) * BM;
+    n0_ = (tin / gsz) * BN;
+  };
+  int id = blockIdx.x, m0, n0;
+  tile_of(id, m0, n0);
 
   // ---- LDS-DMA sources: buffer resources at the tile's first A row / W row; wave w fills rows
   //      (NA*w + j) * 8 + lane / 8 of each A half-tile and (2w + j) * 8 + lane / 8 of each B half,
   //      16-B chunk (lane & 7) ^ ((row >> 1) & 7). Rows past M / N are clamped: they only feed
   //      outputs that are never stored.
-  const __amdgpu_buffer_rsrc_t rsa = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)((const char*)p.A + (size_t)m0 * p.lda * 2), (short)0, 0x7ffffff0, 0x00020000);
-  const __amdgpu_buffer_rsrc_t rsw = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)((const char*)p.W + (size_t)n0 * p.K * 2), (short)0, 0x7ffffff0, 0x00020000);
+  __amdgpu_buffer_rsrc_t rsa, rsw;
   unsigned aoffs[2][2], boffs[2][2];  // (fixed extents: a template-dependent array extent in a builtin argument makes hipcc's host pass drop the launch stub)
+  auto sources = [&](int m0_, int n0_) __attribute__((always_inline)) {
+    int sl = lane;  // (laundered like the epilogue's lane indices: recomputed per tile, not hoisted)
+    if constexpr (PERSIST) asm volatile("" : "+v"(sl));
+    rsa = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)((const char*)p.A + (size_t)m0_ * p.lda * 2), (short)0, 0x7ffffff0, 0x00020000);
+    rsw = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)((const char*)p.W + (size_t)n0_ * p.K * 2), (short)0, 0x7ffffff0, 0x00020000);
 #pragma unroll
-  for (int j = 0; j < NA; ++j) {
-    const int r = (wid * NA + j) * 8 + (lane >> 3);
-    const int c = (lane & 7) ^ ((r >> 1) & 7);
+    for (int j = 0; j < NA; ++j) {
+      const int r = (wid * NA + j) * 8 + (sl >> 3);
+      const int c = (sl & 7) ^ ((r >> 1) & 7);
 #pragma unroll
-    for (int h = 0; h < 2; ++h)
-      aoffs[h][j] = (unsigned)(min(m0 + h * (BM / 2) + r, p.M - 1) - m0) * (unsigned)(p.lda * 2) + c * 16;
-  }
+      for (int h = 0; h < 2; ++h)
+        aoffs[h][j] = (unsigned)(min(m0_ + h * (BM / 2) + r, p.M - 1) - m0_) * (unsigned)(p.lda * 2) + c * 16;
+    }
 #pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int r = (wid * 2 + j) * 8 + (lane >> 3);
-    const int c = (lane & 7) ^ ((r >> 1) & 7);
+    for (int j = 0; j < 2; ++j) {
+      const int r = (wid * 2 + j) * 8 + (sl >> 3);
+      const int c = (sl & 7) ^ ((r >> 1) & 7);
 #pragma unroll
-    for (int h = 0; h < 2; ++h)
-      boffs[h][j] = (unsigned)(min(n0 + h * 128 + r, p.N - 1) - n0) * (unsigned)(p.K * 2) + c * 16;
-  }
+      for (int h = 0; h < 2; ++h)
+        boffs[h][j] = (unsigned)(min(n0_ + h * 128 + r, p.N - 1) - n0_) * (unsigned)(p.K * 2) + c * 16;
+    }
+  };
 #define ISSUE_A(H, KT, B)                                                                               \
   do {                                                                                                  \
     char* d_ = smem + (B) * BUF + ((H) ? OFF_A1 : OFF_A0) + wid * NA * 1024;                            \
@@ -114,6 +130,12 @@ gemm8p_kernel(GemmArgs p) {
     _Pragma("unroll") for (int j_ = 0; j_ < 2; ++j_)                                                    \
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rsw, (lds_ptr_t)(d_ + j_ * 1024), 16, boffs[H][j_], (KT) * 128, 0, 0); \
   } while (0)
+  // prologue DMA: all of K-tile 0 and A0 B0 B1 of K-tile 1
+  //   (DMA order per wave: ... A0 B0 B1(t+1) | A1(t+1) | A0 B0 B1(t+2) | A1(t+2) ...)
+  auto prologue = [&]() __attribute__((always_inline)) {
+    ISSUE_A(0, 0, 0); ISSUE_B(0, 0, 0); ISSUE_B(1, 0, 0); ISSUE_A(1, 0, 0);
+    ISSUE_A(0, 1, 1); ISSUE_B(0, 1, 1); ISSUE_B(1, 1, 1);
+  };
 
   // ---- fragment read offsets: row wg*QR + i*16 + fr of an A half (wn*32 + j*16 + fr of a B half),
   //      16-B chunk kk*4 + fg, swizzled by ((row >> 1) & 7) = fr >> 1 (i*16, wg*QR, wn*32 keep it).
@@ -128,15 +150,6 @@ gemm8p_kernel(GemmArgs p) {
   }
 
   f32x4_t acc[2][2][MI][2];
-#pragma unroll
-  for (int a = 0; a < 2; ++a)
-#pragma unroll
-    for (int b = 0; b < 2; ++b)
-#pragma unroll
-      for (int i = 0; i < MI; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j) acc[a][b][i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-
   bf16x8_t ra[2][MI], rb0[2][2], rb1[2][2];
   auto read_a = [&](const char* base) __attribute__((always_inline)) {
 #pragma unroll
@@ -171,16 +184,6 @@ gemm8p_kernel(GemmArgs p) {
   using I0 = std::integral_constant<int, 0>;
   using I1 = std::integral_constant<int, 1>;
 
-  const int nk = p.K / 64;  // >= 2 (host-checked)
-
-  // ---- prologue: all of tile 0 and A0 B0 B1 of tile 1 in flight; wait for A0 B0 B1 of tile 0
-  //      (DMA order per wave: ... A0 B0 B1(t+1) | A1(t+1) | A0 B0 B1(t+2) | A1(t+2) ...)
-  ISSUE_A(0, 0, 0); ISSUE_B(0, 0, 0); ISSUE_B(1, 0, 0); ISSUE_A(1, 0, 0);
-  ISSUE_A(0, 1, 1); ISSUE_B(0, 1, 1); ISSUE_B(1, 1, 1);
-  vmcnt<CNT_AB>();
-  bar();
-  if (wg) bar();  // G1 runs one barrier behind
-
   //   phase A waits A1(t)         : A0 B0 B1(t+1), A1(t+1) newer -> CNT_AB (0 in the last tile)
   //   phase B waits A0 B0 B1(t+1) : A1(t+1), A0 B0 B1(t+2) newer -> CNT_AB (NA when t+2 does not exist)
   auto ktile = [&](int kt, auto fill_tag, auto next_tag) __attribute__((always_inline)) {
@@ -213,104 +216,130 @@ gemm8p_kernel(GemmArgs p) {
   };
   using T_ = std::true_type;
   using F_ = std::false_type;
-  int kt = 0;
-  for (; kt < nk - 2; ++kt) ktile(kt, T_{}, T_{});
-  ktile(kt, F_{}, T_{});
-  ktile(kt + 1, F_{}, F_{});
-  if (!wg) bar();  // re-align the groups
-#undef ISSUE_A
-#undef ISSUE_B
-  __syncthreads();
+  const int nk = p.K / 64;  // >= 2 (host-checked)
 
-  // ---- epilogue: registers -> (bias / GELU / SwiGLU) -> bf16 staging -> coalesced stores.
-  //      Staged row lr = ih*QR + i*16 + fr (tile row ih*BM/2 + wg*QR + (lr % QR)), staged
-  //      columns lc = jh*32 + j*16 + 4 fg .. + 3 (tile columns jh*128 + wn*32 + (lc & 31)).
-  char* st = smem + wid * (BM / 2) * SROW;
-  // The MFMAs run with W as the A operand (D^T): lane (fr, fg) holds output row i*16 + fr of its
-  // 16 x 16 block and the 4 CONSECUTIVE output columns 4 fg .. 4 fg + 3, so a lane stages 8 B per
-  // block (one ds_write_b64 of 4 packed bf16) instead of 4 separate 2-byte writes.
-  if constexpr (EPI == EPI_SWIGLU) {
-    // W rows interleaved in 16-row (gate, up) groups: j = 0 is gate, j = 1 is up of output columns
-    // (n0 + jh*128 + wn*32) / 2 + 4 fg + q
-#pragma unroll
-    for (int ih = 0; ih < 2; ++ih)
-#pragma unroll
-      for (int jh = 0; jh < 2; ++jh)
-#pragma unroll
-        for (int i = 0; i < MI; ++i) {
-          float v[4];
-#pragma unroll
-          for (int q = 0; q < 4; ++q) v[q] = silu(acc[ih][jh][i][0][q]) * acc[ih][jh][i][1][q];
-          *(u32x2_t*)(st + (ih * QR + i * 16 + fr) * SROW + (jh * 16 + fg * 4) * 2) =
-              u32x2_t{T::pack2(v[0], v[1]), T::pack2(v[2], v[3])};
-        }
-  } else {
-    float bv[2][2][4] = {};
-    if (p.bias) {
-#pragma unroll
-      for (int jh = 0; jh < 2; ++jh)
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            const int gc = n0 + jh * 128 + wn * 32 + j * 16 + fg * 4 + q;
-            bv[jh][j][q] = gc < p.N ? T::to_f(p.bias[gc]) : 0.f;
-          }
-    }
-#pragma unroll
-    for (int ih = 0; ih < 2; ++ih)
-#pragma unroll
-      for (int jh = 0; jh < 2; ++jh)
-#pragma unroll
-        for (int i = 0; i < MI; ++i)
-#pragma unroll
-          for (int j = 0; j < 2; ++j) {
-            float v[4];
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-              v[q] = acc[ih][jh][i][j][q] + bv[jh][j][q];
-              if constexpr (EPI == EPI_GELU) v[q] = gelu_erf(v[q]);
-            }
-            *(u32x2_t*)(st + (ih * QR + i * 16 + fr) * SROW + (jh * 32 + j * 16 + fg * 4) * 2) =
-                u32x2_t{T::pack2(v[0], v[1]), T::pack2(v[2], v[3])};
-          }
-  }
-  __syncthreads();
   constexpr bool SW = (EPI == EPI_SWIGLU);
   constexpr int HC = SW ? 16 : 32;   // staged columns per jh half (one contiguous global run)
   constexpr int CPR = 2 * HC / 8;    // 16-B chunks per staged row
   constexpr int RPI = 64 / CPR;      // rows per store instruction
-  const int ch = lane % CPR;
-  const int jh = ch / (HC / 8);
-  const int cc = (ch % (HC / 8)) * 8;
-  const int gcol = (SW ? n0 / 2 : n0) + jh * (SW ? 64 : 128) + wn * HC + cc;
-  const int ncols = SW ? p.N / 2 : p.N;
-  // EPI_ROPE: this lane's 8 columns lie in one head (D % 8 == 0) and hold 4 whole rotary pairs
-  [[maybe_unused]] int rkind = 0, rhead = 0, rd0 = 0;
-  if constexpr (EPI == EPI_ROPE) {
-    const RopeArgs& R = p.rope;
-    const int qw = R.H * R.D, kw = R.Hkv * R.D;
-    rkind = gcol < qw ? 0 : (gcol < qw + kw ? 1 : 2);
-    const int rel = gcol - (rkind == 0 ? 0 : (rkind == 1 ? qw : qw + kw));
-    rhead = rel / R.D;
-    rd0 = rel % R.D;
-  }
-  // This lane's rows lr = lane / CPR + i * RPI, in batches of NB whose global loads (residual rows;
-  // RoPE positions, slots, then cos / sin) are all issued before any is waited for: the one-row-at-
-  // a-time loop waited a memory round trip per row for those loads (16 per tile per wave, ISA:
-  // global_load + s_waitcnt vmcnt(0) each iteration).
-  constexpr int NI = (BM / 2) / RPI;
+  constexpr int NI = (BM / 2) / RPI; // staged rows per lane
   constexpr int NB = NI < 8 ? NI : 8;
-  const int lr0 = lane / CPR;
-  const bool col_ok = gcol < ncols;
-  for (int i0 = 0; i0 < NI; i0 += NB) {
-    int gmv[NB];
-    u32x4_t vv[NB];
-    [[maybe_unused]] u32x4_t rr[NB];
-    [[maybe_unused]] int psv[NB], slv[NB];
+  const int ncols = SW ? p.N / 2 : p.N;
+
+  sources(m0, n0);
+  prologue();
+  bool first = true;
+  for (;;) {
+    // wait for A0 B0 B1 of K-tile 0. A persistent workgroup's later tiles wait for everything it
+    // has in flight: the previous tile's output stores were issued after this tile's prologue DMA,
+    // and loads and stores need not retire in issue order.
+    if (first) vmcnt<CNT_AB>();
+    else vmcnt<0>();
+    first = false;
+    bar();
+    if (wg) bar();  // G1 runs one barrier behind
 #pragma unroll
-    for (int i = 0; i < NB; ++i) {
-      const int lr = lr0 + (i0 + i) * RPI;
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int i = 0; i < MI; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) acc[a][b][i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    int kt = 0;
+    for (; kt < nk - 2; ++kt) ktile(kt, T_{}, T_{});
+    ktile(kt, F_{}, T_{});
+    ktile(kt + 1, F_{}, F_{});
+    if (!wg) bar();  // re-align the groups
+    __syncthreads();
+
+    // lane-derived epilogue indices from a copy of the lane id the compiler cannot see through, so
+    // they are recomputed here rather than hoisted out of the tile loop (live across the K-loop
+    // they pushed a persistent instance past 256 VGPRs into scratch)
+    int el = lane;
+    if constexpr (PERSIST) asm volatile("" : "+v"(el));
+    const int efr = el & 15, efg = el >> 4;
+    const int ch = el % CPR;
+    const int jh = ch / (HC / 8);
+    const int cc = (ch % (HC / 8)) * 8;
+    const int lr0 = el / CPR;
+    // ---- epilogue: registers -> (bias / GELU / SwiGLU) -> bf16 staging -> coalesced stores.
+    //      Staged row lr = ih*QR + i*16 + efr (tile row ih*BM/2 + wg*QR + (lr % QR)), staged
+    //      columns lc = jh*32 + j*16 + 4 efg .. + 3 (tile columns jh*128 + wn*32 + (lc & 31)).
+    char* st = smem + wid * (BM / 2) * SROW;
+    // The MFMAs run with W as the A operand (D^T): lane (efr, efg) holds output row i*16 + efr of its
+    // 16 x 16 block and the 4 CONSECUTIVE output columns 4 efg .. 4 efg + 3, so a lane stages 8 B per
+    // block (one ds_write_b64 of 4 packed bf16) instead of 4 separate 2-byte writes.
+    if constexpr (EPI == EPI_SWIGLU) {
+      // W rows interleaved in 16-row (gate, up) groups: j = 0 is gate, j = 1 is up of output columns
+      // (n0 + jh*128 + wn*32) / 2 + 4 efg + q
+#pragma unroll
+      for (int ih = 0; ih < 2; ++ih)
+#pragma unroll
+        for (int jh_ = 0; jh_ < 2; ++jh_)
+#pragma unroll
+          for (int i = 0; i < MI; ++i) {
+            float v[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) v[q] = silu(acc[ih][jh_][i][0][q]) * acc[ih][jh_][i][1][q];
+            *(u32x2_t*)(st + (ih * QR + i * 16 + efr) * SROW + (jh_ * 16 + efg * 4) * 2) =
+                u32x2_t{T::pack2(v[0], v[1]), T::pack2(v[2], v[3])};
+          }
+    } else {
+      float bv[2][2][4] = {};
+      if (p.bias) {
+#pragma unroll
+        for (int jh_ = 0; jh_ < 2; ++jh_)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              const int gc = n0 + jh_ * 128 + wn * 32 + j * 16 + efg * 4 + q;
+              bv[jh_][j][q] = gc < p.N ? T::to_f(p.bias[gc]) : 0.f;
+            }
+      }
+#pragma unroll
+      for (int ih = 0; ih < 2; ++ih)
+#pragma unroll
+        for (int jh_ = 0; jh_ < 2; ++jh_)
+#pragma unroll
+          for (int i = 0; i < MI; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+              float v[4];
+#pragma unroll
+              for (int q = 0; q < 4; ++q) {
+                v[q] = acc[ih][jh_][i][j][q] + bv[jh_][j][q];
+                if constexpr (EPI == EPI_GELU) v[q] = gelu_erf(v[q]);
+              }
+              *(u32x2_t*)(st + (ih * QR + i * 16 + efr) * SROW + (jh_ * 32 + j * 16 + efg * 4) * 2) =
+                  u32x2_t{T::pack2(v[0], v[1]), T::pack2(v[2], v[3])};
+            }
+    }
+    __syncthreads();
+    const int gcol = (SW ? n0 / 2 : n0) + jh * (SW ? 64 : 128) + wn * HC + cc;
+    const bool col_ok = gcol < ncols;
+    // EPI_ROPE: this lane's 8 columns lie in one head (D % 8 == 0) and hold 4 whole rotary pairs
+    [[maybe_unused]] int rkind = 0, rhead = 0, rd0 = 0;
+    if constexpr (EPI == EPI_ROPE) {
+      const RopeArgs& R = p.rope;
+      const int qw = R.H * R.D, kw = R.Hkv * R.D;
+      rkind = gcol < qw ? 0 : (gcol < qw + kw ? 1 : 2);
+      const int rel = gcol - (rkind == 0 ? 0 : (rkind == 1 ? qw : qw + kw));
+      rhead = rel / R.D;
+      rd0 = rel % R.D;
+    }
+    // This lane's rows lr = lane / CPR + i * RPI: the staged values of all of them go to registers
+    // first (a persistent workgroup then refills the buffers with the next tile's prologue DMA
+    // while this tile's stores drain), with their residual rows / RoPE positions and slots issued
+    // alongside; RoPE cos / sin follow in batches of NB, all issued before any is waited for.
+    int gmv[NI];
+    u32x4_t vv[NI];
+    [[maybe_unused]] u32x4_t rr[EPI == EPI_RESID ? NI : 1];
+    [[maybe_unused]] int psv[EPI == EPI_ROPE ? NI : 1], slv[EPI == EPI_ROPE ? NI : 1];
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const int lr = lr0 + i * RPI;
       gmv[i] = m0 + (lr / QR) * (BM / 2) + wg * QR + (lr % QR);
       const int gmc = min(gmv[i], p.M - 1);  // loads of rows past M read a valid row, never stored
       vv[i] = *(const u32x4_t*)(st + lr * SROW + (jh * HC + cc) * 2);
@@ -321,90 +350,157 @@ gemm8p_kernel(GemmArgs p) {
         slv[i] = p.rope.slot[gmc];
       }
     }
-    if constexpr (EPI == EPI_ROPE) {
-      // same bf16 roundings as GEMM -> rope_cache: rotate the bf16-rounded outputs in fp32
-      const RopeArgs& R = p.rope;
-      const int half = R.D / 2, i0c = rd0 / 2;
-      f32x4_t c01[NB], c23[NB];
-      if (rkind < 2) {
-#pragma unroll
-        for (int i = 0; i < NB; ++i) {
-          const int ps = min(max(psv[i], 0), R.max_seq - 1);
-          c01[i] = *(const f32x4_t*)(R.cs + ((size_t)ps * half + i0c) * 2);
-          c23[i] = *(const f32x4_t*)(R.cs + ((size_t)ps * half + i0c) * 2 + 4);
-        }
-      }
-#pragma unroll
-      for (int i = 0; i < NB; ++i) {
-        const int gm = gmv[i];
-        if (gm >= p.M || !col_ok) continue;
-        u32x4_t v = vv[i];
-        DA_ASSERT(psv[i] >= 0 && psv[i] < R.max_seq && slv[i] >= 0);
-        if (rkind < 2) {
-          const float ccs[4] = {c01[i][0], c01[i][2], c23[i][0], c23[i][2]};
-          const float sns[4] = {c01[i][1], c01[i][3], c23[i][1], c23[i][3]};
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const float x1 = bf2f((bf16_t)(v[e] & 0xffff)), x2 = bf2f((bf16_t)(v[e] >> 16));
-            const float o1 = x1 * ccs[e] - x2 * sns[e];
-            const float o2 = x2 * ccs[e] + x1 * sns[e];
-            v[e] = pack_bf2(o1, o2);
-          }
-        }
-        if (rkind > 0) {
-          bf16_t* cache = rkind == 1 ? R.kc : R.vc;
-          *(u32x4_t*)(cache + (((size_t)slv[i] * R.Hkv + rhead) * R.max_seq + psv[i]) * R.D + rd0) = v;
-          if (!R.kv_out) continue;  // k / v live in the cache only: no second copy in C
-        }
-        *(u32x4_t*)(p.C + (size_t)gm * p.ldc + gcol) = v;
-      }
-    } else {
-#pragma unroll
-      for (int i = 0; i < NB; ++i) {
-        const int gm = gmv[i];
-        if (gm >= p.M || !col_ok) continue;
-        u32x4_t v = vv[i];
-        if constexpr (EPI == EPI_RESID) {
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const float lo = T::to_f((bf16_t)(v[e] & 0xffff)) + T::to_f((bf16_t)(rr[i][e] & 0xffff));
-            const float hi = T::to_f((bf16_t)(v[e] >> 16)) + T::to_f((bf16_t)(rr[i][e] >> 16));
-            v[e] = T::pack2(lo, hi);
-          }
-        }
-        *(u32x4_t*)(p.C + (size_t)gm * p.ldc + gcol) = v;
+    const int nid = id + (int)gridDim.x;
+    const bool more = PERSIST && nid < ntiles;
+    int nm0 = 0, nn0 = 0;
+    if constexpr (PERSIST) {
+      lgkm0();
+      bar();  // every wave holds its staged rows: both operand buffers are free
+      if (more) {
+        tile_of(nid, nm0, nn0);
+        sources(nm0, nn0);
+        prologue();
       }
     }
+#pragma unroll
+    for (int i0 = 0; i0 < NI; i0 += NB) {
+      if constexpr (EPI == EPI_ROPE) {
+        // same bf16 roundings as GEMM -> rope_cache: rotate the bf16-rounded outputs in fp32
+        const RopeArgs& R = p.rope;
+        const int half = R.D / 2, i0c = rd0 / 2;
+        f32x4_t c01[NB], c23[NB];
+        if (rkind < 2) {
+#pragma unroll
+          for (int i = 0; i < NB; ++i) {
+            const int ps = min(max(psv[i0 + i], 0), R.max_seq - 1);
+            c01[i] = *(const f32x4_t*)(R.cs + ((size_t)ps * half + i0c) * 2);
+            c23[i] = *(const f32x4_t*)(R.cs + ((size_t)ps * half + i0c) * 2 + 4);
+          }
+        }
+#pragma unroll
+        for (int i = 0; i < NB; ++i) {
+          const int gm = gmv[i0 + i];
+          if (gm >= p.M || !col_ok) continue;
+          u32x4_t v = vv[i0 + i];
+          const int ps = psv[i0 + i], sl = slv[i0 + i];
+          DA_ASSERT(ps >= 0 && ps < R.max_seq && sl >= 0);
+          if (rkind < 2) {
+            const float ccs[4] = {c01[i][0], c01[i][2], c23[i][0], c23[i][2]};
+            const float sns[4] = {c01[i][1], c01[i][3], c23[i][1], c23[i][3]};
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const float x1 = bf2f((bf16_t)(v[e] & 0xffff)), x2 = bf2f((bf16_t)(v[e] >> 16));
+              const float o1 = x1 * ccs[e] - x2 * sns[e];
+              const float o2 = x2 * ccs[e] + x1 * sns[e];
+              v[e] = pack_bf2(o1, o2);
+            }
+          }
+          if (rkind > 0) {
+            bf16_t* cache = rkind == 1 ? R.kc : R.vc;
+            *(u32x4_t*)(cache + (((size_t)sl * R.Hkv + rhead) * R.max_seq + ps) * R.D + rd0) = v;
+            if (!R.kv_out) continue;  // k / v live in the cache only: no second copy in C
+          }
+          *(u32x4_t*)(p.C + (size_t)gm * p.ldc + gcol) = v;
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < NB; ++i) {
+          const int gm = gmv[i0 + i];
+          if (gm >= p.M || !col_ok) continue;
+          u32x4_t v = vv[i0 + i];
+          if constexpr (EPI == EPI_RESID) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const float lo = T::to_f((bf16_t)(v[e] & 0xffff)) + T::to_f((bf16_t)(rr[i0 + i][e] & 0xffff));
+              const float hi = T::to_f((bf16_t)(v[e] >> 16)) + T::to_f((bf16_t)(rr[i0 + i][e] >> 16));
+              v[e] = T::pack2(lo, hi);
+            }
+          }
+          *(u32x4_t*)(p.C + (size_t)gm * p.ldc + gcol) = v;
+        }
+      }
+    }
+    if (!more) break;
+    id = nid; m0 = nm0; n0 = nn0;
   }
+#undef ISSUE_A
+#undef ISSUE_B
 }
 
 // Grouped-M band height of the tile order: 4 rows of tiles. (2-row bands ran isolated GEMMs at
 // M = 65536 1.4-2.7 % faster, profiles/r4/gemm_group.txt, but the bench's QA prefill 0.8 % slower,
 // profiles/r4/rejected_r4.txt: back-to-back repeats of one GEMM keep its operands cache-warm; the
 // real layer sequence does not.)
+static int num_cus() {
+  static int cus = 0;
+  if (cus <= 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+      cus = 256;
+  }
+  return cus;
+}
+
+// Persistent tile loop (a grid of one workgroup per CU, a multiple of 8 so a workgroup's tiles
+// stay on its XCD) when the product has more tiles than CUs: the next tile's prologue DMA is in
+// flight while this tile's stores drain, instead of a workgroup retiring and the next one paying
+// launch + prologue latency (profiles/r5/gemm_epilogue/: prologue + launch ~4 % of a prefill GEMM).
+// DA_GEMM8P_PERSIST=0 turns it off.
+static int g_persist = -1;
+static bool persist_on() {
+  if (g_persist < 0) {
+    const char* e = getenv("DA_GEMM8P_PERSIST");
+    g_persist = (e && e[0] == '0') ? 0 : 1;
+  }
+  return g_persist == 1;
+}
+
+// on = 0 / 1 sets the persistent tile loop off / on for later launches, -1 only queries; returns
+// the previous setting (tests run one product both ways and compare bit for bit)
+DA_EXPORT int da_gemm8p_persist(int on) {
+  const int prev = persist_on() ? 1 : 0;
+  if (on == 0 || on == 1) g_persist = on;
+  return prev;
+}
+
+template <int EPI, int BM, typename T>
+static void launch8p_epi(const GemmArgs& a, int ntiles, hipStream_t s) {
+  const int cus = num_cus();
+  // (not EPI_ROPE: its per-row positions / slots / cos-sin next to the tile loop's state spill past
+  // 256 VGPRs, and the persistent QKV projection measured 4 % slower, profiles/r5/gemm_persist/)
+  if constexpr (EPI != EPI_ROPE) {
+    if (persist_on() && ntiles > cus && cus >= 8) {
+      gemm8p_kernel<EPI, BM, T, true><<<dim3(cus & ~7), dim3(512), 0, s>>>(a);
+      return;
+    }
+  }
+  gemm8p_kernel<EPI, BM, T, false><<<dim3(ntiles), dim3(512), 0, s>>>(a);
+}
+
 template <int BM>
 static int launch8p(const GemmArgs& a0, int epi, hipStream_t s) {
   GemmArgs a = a0;
   if (a.group <= 0) a.group = 4;
   const int ntm = (a.M + BM - 1) / BM, ntn = (a.N + BN - 1) / BN;
-  dim3 grid(ntm * ntn), block(512);
+  const int nt = ntm * ntn;
   if (epi >= 100) {  // fp16 operands (the encoder's DTYPE=fp16): the BERT epilogues only
     switch (epi - 100) {
-      case EPI_NONE: gemm8p_kernel<EPI_NONE, BM, F16T><<<grid, block, 0, s>>>(a); break;
-      case EPI_BIAS: gemm8p_kernel<EPI_BIAS, BM, F16T><<<grid, block, 0, s>>>(a); break;
-      case EPI_GELU: gemm8p_kernel<EPI_GELU, BM, F16T><<<grid, block, 0, s>>>(a); break;
-      case EPI_RESID: gemm8p_kernel<EPI_RESID, BM, F16T><<<grid, block, 0, s>>>(a); break;
+      case EPI_NONE: launch8p_epi<EPI_NONE, BM, F16T>(a, nt, s); break;
+      case EPI_BIAS: launch8p_epi<EPI_BIAS, BM, F16T>(a, nt, s); break;
+      case EPI_GELU: launch8p_epi<EPI_GELU, BM, F16T>(a, nt, s); break;
+      case EPI_RESID: launch8p_epi<EPI_RESID, BM, F16T>(a, nt, s); break;
       default: return (int)hipErrorInvalidValue;
     }
     return (int)hipGetLastError();
   }
   switch (epi) {
-    case EPI_NONE: gemm8p_kernel<EPI_NONE, BM><<<grid, block, 0, s>>>(a); break;
-    case EPI_BIAS: gemm8p_kernel<EPI_BIAS, BM><<<grid, block, 0, s>>>(a); break;
-    case EPI_GELU: gemm8p_kernel<EPI_GELU, BM><<<grid, block, 0, s>>>(a); break;
-    case EPI_SWIGLU: gemm8p_kernel<EPI_SWIGLU, BM><<<grid, block, 0, s>>>(a); break;
-    case EPI_RESID: gemm8p_kernel<EPI_RESID, BM><<<grid, block, 0, s>>>(a); break;
-    case EPI_ROPE: gemm8p_kernel<EPI_ROPE, BM><<<grid, block, 0, s>>>(a); break;
+    case EPI_NONE: launch8p_epi<EPI_NONE, BM, BF16T>(a, nt, s); break;
+    case EPI_BIAS: launch8p_epi<EPI_BIAS, BM, BF16T>(a, nt, s); break;
+    case EPI_GELU: launch8p_epi<EPI_GELU, BM, BF16T>(a, nt, s); break;
+    case EPI_SWIGLU: launch8p_epi<EPI_SWIGLU, BM, BF16T>(a, nt, s); break;
+    case EPI_RESID: launch8p_epi<EPI_RESID, BM, BF16T>(a, nt, s); break;
+    case EPI_ROPE: launch8p_epi<EPI_ROPE, BM, BF16T>(a, nt, s); break;
     default: return (int)hipErrorInvalidValue;
   }
   return (int)hipGetLastError();
@@ -420,13 +516,7 @@ static int launch8p(const GemmArgs& a0, int epi, hipStream_t s) {
 int gemm8p_pick_bm(int M, int N) {
   const long ntn = (N + 255) / 256;
   const long t256 = (long)((M + 255) / 256) * ntn, t128 = (long)((M + 127) / 128) * ntn;
-  static int cus = 0;
-  if (cus <= 0) {
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
-      cus = 256;
-  }
+  const int cus = num_cus();
   const long w256 = (t256 + cus - 1) / cus, w128 = (t128 + cus - 1) / cus;
   return w128 * 72 < w256 * 100 ? 128 : 256;
 }

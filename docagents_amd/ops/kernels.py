@@ -82,6 +82,7 @@ _SIGS = {
     "da_device_cu_count": [c_int, ctypes.POINTER(c_int)],
     "da_placement_probe": [c_void_p, c_int, c_longlong, c_void_p],
     "da_spin": [c_int, c_void_p, c_void_p],
+    "da_gemm8p_persist": [c_int],
     "da_gemm_f16": [c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int,
                     c_void_p],
     "da_flash_attn_f16": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_int, c_int, c_int,
@@ -928,6 +929,12 @@ def spin(us: int, device=None) -> None:
     bounded to 10 s). Test helper: work queued behind it on this stream is provably still pending."""
     _req(0 <= us <= 10_000_000, "spin: 0 <= us <= 1e7")
     _check(lib().da_spin(int(us), None, _stream()), "da_spin")
+
+
+def gemm8p_persist(on: int = -1) -> int:
+    """Persistent tile loop of the prefill GEMM (one workgroup per CU walking its XCD's tiles) on
+    (1) / off (0) for later launches; -1 only queries. Returns the previous setting."""
+    return int(lib().da_gemm8p_persist(int(on)))
 
 
 def _f16_cuda(t, name):

@@ -23,7 +23,8 @@ def _h(*shape, scale=1.0):
     return (torch.randn(*shape, device=DEV) * scale).to(torch.float16)
 
 
-@pytest.mark.parametrize("M,N,Kd", [(1, 1024, 1024), (77, 3072, 1024), (640, 1024, 4096), (2048, 3072, 1024)])
+@pytest.mark.parametrize("M,N,Kd", [(1, 1024, 1024), (77, 3072, 1024), (640, 1024, 4096), (2048, 3072, 1024),
+                                    (8192, 3072, 1024)])
 @pytest.mark.parametrize("epi", [K.EPI_NONE, K.EPI_BIAS, K.EPI_GELU, K.EPI_RESID])
 def test_gemm_f16_matches_fp32(M, N, Kd, epi):
     torch.manual_seed(M + N + epi)

@@ -78,6 +78,29 @@ def test_gemm8p_tile(M, N, Kd, epi, tile):
     _close(got, ref, atol=0.04)
 
 
+@pytest.mark.parametrize("M,N,Kd", [(4100, 4104, 256), (2304, 9216, 192)])
+@pytest.mark.parametrize("epi", [K.EPI_NONE, K.EPI_BIAS, K.EPI_GELU, K.EPI_RESID, K.EPI_SWIGLU])
+@pytest.mark.parametrize("tile", [7, 10])
+def test_gemm8p_persistent(M, N, Kd, epi, tile):
+    """More tiles than CUs: the persistent tile loop (workgroups running 1-3 tiles each, ragged M / N)
+    vs the fp32 reference, and bit-identical to one workgroup per tile."""
+    torch.manual_seed(M + N + epi + tile)
+    if epi == K.EPI_SWIGLU:
+        N = (N // 32) * 32
+    a, w = _rand(M, Kd), _rand(N, Kd, scale=Kd ** -0.5)
+    bias = _rand(N) if epi in (K.EPI_BIAS, K.EPI_GELU, K.EPI_RESID) else None
+    resid = _rand(M, N) if epi == K.EPI_RESID else None
+    prev = K.gemm8p_persist(1)
+    try:
+        got = K.gemm(a, w, bias=bias, epi=epi, resid=resid, tile=tile, splits=1)
+        K.gemm8p_persist(0)
+        one = K.gemm(a, w, bias=bias, epi=epi, resid=resid, tile=tile, splits=1)
+    finally:
+        K.gemm8p_persist(prev)
+    _close(got, R.gemm(a, w, bias=bias, epi=epi, resid=resid), atol=0.04)
+    assert torch.equal(got, one)
+
+
 @pytest.mark.parametrize("M", [256, 700, 3000])
 @pytest.mark.parametrize("H,Hkv,D", [(32, 32, 96), (8, 2, 128), (4, 4, 64)])
 def test_gemm_rope(M, H, Hkv, D):
