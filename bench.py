@@ -159,6 +159,9 @@ def main():
                          "auto = rccl without TP, plane with TP (TP ranks share their queries)")
     ap.add_argument("--multi-iters", type=int, default=24,
                     help="N > 1: timed sharded searches of the rccl_search block (C1 + C2 over RCCL)")
+    ap.add_argument("--serving-requests", type=int, default=256,
+                    help="N > 1: single-question searches per rank of the serving_search block (the owner-routed "
+                         "plane vs SEARCH_TRANSPORT=rccl lock-step rounds); 0 skips it")
     ap.add_argument("--ingest-latency-reps", type=int, default=10,
                     help="single-document ingest latency reps (upload -> summary readable, engine level)")
     a = ap.parse_args()
@@ -470,6 +473,31 @@ def main():
         block("rccl_search", lambda: CB.rccl_search(
             shard, search, eng.embed, lambda i: ([tg.question() for _ in range(a.batch)], make_filters(5000 + i)),
             a.top_k, a.min_sim, a.multi_iters, ctrl, dev))
+
+        def serving_search():
+            """The serving transports side by side: the owner-routed plane (host TCP, the default) and
+            SEARCH_TRANSPORT=rccl (lock-step rounds of RCCL all-gathers; parallel/collective_plane.py)."""
+            import datetime
+
+            from docagents_amd.parallel.collective_plane import CollectiveSearchPlane
+            cctrl = tdist.new_group(backend="gloo", timeout=datetime.timedelta(seconds=120))
+            cdata = tdist.new_group(backend=info.backend)
+            cplane = CollectiveSearchPlane(eng.index, R, W, cdata, cctrl, device=dev, timeout_s=120.0).start()
+            try:
+                qv = eng.embed([tg.question() for _ in range(a.serving_requests)]).float().cpu().numpy()
+                flt = []
+                while len(flt) < len(qv):
+                    flt.extend(make_filters(9000 + len(flt)))
+                reqs = [(qv[i:i + 1], flt[i]) for i in range(len(qv))]
+                res = CB.serving_search({"plane": plane, "rccl": cplane}, reqs, a.top_k, a.min_sim, ctrl, dev)
+                res["rounds"] = cplane.stats["rounds"]
+                res["rccl_transport"] = cplane.stats["transport"]
+                return res
+            finally:
+                tdist.barrier(group=ctrl)  # every rank done submitting before the rounds stop
+                cplane.stop(timeout=10.0)
+        if a.serving_requests > 0:
+            block("serving_search", serving_search)
 
         def tp_prompts(B, salt):
             rng = np.random.default_rng(4242 + salt)  # the same prompts on every rank

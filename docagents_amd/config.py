@@ -88,6 +88,11 @@ class Config:
     # measured no better for the query path under load (profiles/r3/stack/*switch*)
     engine_switch_interval_ms: float = field(default=0.0, metadata={"env": "ENGINE_SWITCH_INTERVAL_MS"})
     engine_admit_tokens: int = field(default=0, metadata={"env": "ENGINE_ADMIT_TOKENS"})  # 0 -> 4 prefill chunks
+    # serving search transport over the sharded index: "plane" (point to point to the owner shards,
+    # failures isolated per shard; parallel/search_plane.py) or "rccl" (lock-step rounds of RCCL
+    # all-gathers over xGMI; parallel/collective_plane.py; TP_SIZE=1 only)
+    search_transport: str = field(default="plane", metadata={"env": "SEARCH_TRANSPORT"})
+    search_round_idle_ms: float = field(default=2.0, metadata={"env": "SEARCH_ROUND_IDLE_MS"})
     # --- new keys: durable vector shards (index/wal.py) ---
     index_dir: str = field(default="", metadata={"env": "INDEX_DIR"})  # "" -> DATA_DIR/index; "none" -> off
     index_checkpoint_s: float = field(default=300.0, metadata={"env": "INDEX_CHECKPOINT_S"})
@@ -130,6 +135,12 @@ class Config:
             raise ValueError(f"INDEX_KIND={self.index_kind!r} is not supported (flat | ivfflat)")
         if self.tp_size < 1:
             raise ValueError(f"TP_SIZE={self.tp_size} must be >= 1")
+        if self.search_transport not in ("plane", "rccl"):
+            raise ValueError(f"SEARCH_TRANSPORT={self.search_transport!r} is not supported (plane | rccl)")
+        if self.search_transport == "rccl" and self.tp_size > 1:
+            # the rounds' RCCL calls run on their own thread; with TP the GPU thread drives the TP
+            # communicator at the same time (two communicators from two threads can deadlock)
+            raise ValueError("SEARCH_TRANSPORT=rccl needs TP_SIZE=1")
         return self
 
 

@@ -85,6 +85,45 @@ def rccl_search(shard, plane_search, embed, make_batch, k: int, min_sim: float, 
             "scores_close": close}
 
 
+def serving_search(planes: dict, reqs: list, k: int, min_sim: float, ctrl, dev, inflight: int = 64) -> dict:
+    """The two serving search transports under a serving load. planes: {name: plane} — "plane" (the
+    owner-routed point-to-point SearchPlane) and "rccl" (CollectiveSearchPlane: lock-step rounds of
+    RCCL all-gathers); reqs: this rank's single-question searches [(vec [1, d], document filter)].
+    Every rank submits its requests ``inflight`` at a time through one transport, then the next.
+    Per transport: aggregate searches/s over the ranks (wall = max over ranks), p50 / p90 of a
+    search's submit -> result time; and whether both transports returned the same ids for every
+    request. The barriers run on the gloo ``ctrl`` group: the collective transport's round thread
+    drives RCCL meanwhile, and no second thread may (two communicators from two threads)."""
+    W = dist.get_world_size()
+    out, ids = {}, {}
+    for name, pl in planes.items():
+        pl.submit(reqs[0][0], k, min_sim, [reqs[0][1]]).result(120)  # warm (connections / first round)
+        dist.barrier(group=ctrl)
+        lat, got = [], []
+        t0 = time.perf_counter()
+        for w0 in range(0, len(reqs), inflight):
+            wave = []
+            for v, f in reqs[w0:w0 + inflight]:
+                done = {}
+                fut = pl.submit(v, k, min_sim, [f])
+                fut.add_done_callback(lambda _f, d=done: d.setdefault("t", time.perf_counter()))
+                wave.append((time.perf_counter(), fut, done))
+            for ts, fut, done in wave:
+                _, g = fut.result(120)
+                lat.append((done.get("t", time.perf_counter()) - ts) * 1000)
+                got.append(np.asarray(g).reshape(-1))
+        dt = all_reduce_max(time.perf_counter() - t0, dev)
+        ids[name] = got
+        out[name] = {"searches_per_s": round(W * len(reqs) / dt, 1), "p50_ms": round(statistics.median(lat), 3),
+                     "p90_ms": round(_pct(lat, 0.9), 3)}
+    if len(ids) == 2:
+        a, b = ids.values()
+        out["ids_identical"] = int(all_reduce_max(float(sum(1 for x, y in zip(a, b) if not np.array_equal(x, y))),
+                                                  dev)) == 0
+    out.update({"requests_per_rank": len(reqs), "inflight_per_rank": inflight, "world": W})
+    return out
+
+
 def _round_up(x: int, m: int) -> int:
     return -(-x // m) * m
 

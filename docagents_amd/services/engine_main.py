@@ -9,6 +9,8 @@ collectives over xGMI, gloo groups carry the small control messages.
   micro-batchers and continuous scheduler; TP followers step the decoder with their leader. The
   vector index is sharded over every rank; a search goes point to point to the shards that own its
   documents (parallel/search_plane.py), so a dead rank fails only the searches that need its shard.
+  SEARCH_TRANSPORT=rccl (TP_SIZE=1): every rank's searches travel instead in lock-step rounds of
+  RCCL all-gathers over xGMI (parallel/collective_plane.py; one hung rank then stops search on all).
   Agents connect to the base URL; ``EngineCluster`` discovers the other replicas (topology RPC),
   load-balances generation / embedding over them and routes index calls to the owner's replica.
 Durable shards (default): ``--index-dir DIR`` (INDEX_DIR, default DATA_DIR/index) holds each rank's
@@ -70,7 +72,7 @@ def main(argv=None) -> int:
     if world % t:
         raise SystemExit(f"TP_SIZE={t} must divide the world size {world}")
     replicas, replica = world // t, rank // t
-    rep_ctrl = rep_data = plane_ctrl = None
+    rep_ctrl = rep_data = plane_ctrl = search_ctrl = search_data = None
     tp = None
     dev = info.device
     if world > 1:
@@ -86,6 +88,12 @@ def main(argv=None) -> int:
                 rep_ctrl, rep_data = c, d
         to = datetime.timedelta(seconds=max(60.0, cfg.engine_step_timeout))
         plane_ctrl = dist.new_group(backend="gloo", timeout=to)  # the plane's one address exchange
+        if cfg.search_transport == "rccl":
+            # the collective transport's round control (gloo; its timeout bounds a round with a hung
+            # peer) and data (RCCL over xGMI on GPU ranks) groups
+            sto = datetime.timedelta(seconds=max(10.0, min(60.0, cfg.engine_step_timeout)))
+            search_ctrl = dist.new_group(backend="gloo", timeout=sto)
+            search_data = dist.new_group(backend="nccl" if dev.type == "cuda" else "gloo")
         if t > 1:
             tp = TPContext(rank % t, t, rep_data)
     eng = Engine(cfg.embed_arch, cfg.llm_arch, dev, seed=cfg.seed, tp=tp, max_batch=cfg.max_batch,
@@ -114,9 +122,16 @@ def main(argv=None) -> int:
         from ..ops.streams import serving_lanes
         lanes = serving_lanes(cfg.engine_latency_cus, dev)
         log.info("cu partition", "latency_cus", cfg.engine_latency_cus)
-    plane = SearchPlane.start_world(eng.index, rank, world, plane_ctrl, device=dev, stream=lanes[2],
-                                    host=os.environ.get("ENGINE_PLANE_HOST", "127.0.0.1"),
-                                    timeout_s=max(5.0, min(60.0, cfg.engine_step_timeout)))
+    if cfg.search_transport == "rccl" and world > 1:
+        from ..parallel.collective_plane import CollectiveSearchPlane
+        plane = CollectiveSearchPlane(eng.index, rank, world, search_data, search_ctrl, device=dev, stream=lanes[2],
+                                      timeout_s=max(5.0, min(60.0, cfg.engine_step_timeout)),
+                                      idle_s=cfg.search_round_idle_ms / 1000.0).start()
+    else:
+        plane = SearchPlane.start_world(eng.index, rank, world, plane_ctrl, device=dev, stream=lanes[2],
+                                        host=os.environ.get("ENGINE_PLANE_HOST", "127.0.0.1"),
+                                        timeout_s=max(5.0, min(60.0, cfg.engine_step_timeout)))
+    log.info("search transport", "kind", cfg.search_transport if world > 1 else "local")
     grp = EngineGroup(eng, rank, world, rep_ctrl, rep_data, shard_log=shard_log, tp_size=t, plane=plane)
     if not grp.is_leader:
         grp.follower_loop()

@@ -1,6 +1,7 @@
 """bench.py's JSON line at N > 1 (VERDICT r4 Next #1): after the data-parallel headline, the timed
 multi-GPU blocks — ``rccl_search`` (C1 + C2 as collectives, >= 3 timed sharded searches here, rows
-identical to the serving plane), ``tp_decode`` (the decoder at TP = N, decode ms per step at batch 1
+identical to the serving plane), ``serving_search`` (the owner-routed serving plane vs the
+SEARCH_TRANSPORT=rccl collective rounds under a serving load, same ids), ``tp_decode`` (the decoder at TP = N, decode ms per step at batch 1
 and batch B per all-reduce arm, the per-decision TP verdict) — plus the single-document ingest
 latency and the physical-GPU count. Rehearsed on CPU ranks (gloo, tiny configs): the schema and the
 verdicts are pinned here; the numbers come from the GPU node."""
@@ -19,7 +20,7 @@ def test_bench_two_rank_json_schema():
            "--enc", "tiny-enc", "--llm", "tiny-dec", "--batch", "2", "--steps", "1", "--warmup", "0",
            "--latency-reps", "2", "--ingest-docs", "2", "--ingest-batches", "1", "--ingest-latency-reps", "2",
            "--index-rows", "2000", "--multi-iters", "3", "--breakdown", "0", "--max-new", "4",
-           "--ingest-words", "300"]
+           "--ingest-words", "300", "--serving-requests", "12"]
     p = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600, cwd=ROOT)
     assert p.returncode == 0, p.stderr[-2000:]
     lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
@@ -40,6 +41,12 @@ def test_bench_two_rank_json_schema():
     assert rs["iters"] == 3 and rs["rows_per_rank"] == 2 and rs["world"] == 2, rs
     assert rs["qps"] > 0 and rs["p50_ms"] > 0 and rs["p90_ms"] >= rs["p50_ms"], rs
     assert rs["rows_identical_to_plane"] == rs["rows_checked"] == 2 and rs["scores_close"], rs
+    # the serving transports under load: owner-routed plane vs lock-step collective rounds, same ids
+    ss = out["serving_search"]
+    assert "error" not in ss, ss
+    assert ss["requests_per_rank"] == 12 and ss["ids_identical"] is True and ss["rounds"] >= 1, ss
+    for t in ("plane", "rccl"):
+        assert ss[t]["searches_per_s"] > 0 and ss[t]["p90_ms"] >= ss[t]["p50_ms"] > 0, ss
     # TP = N decode per arm, batch 1 and batch B, plus the agreement verdict
     td = out["tp_decode"]
     assert td["tp"] == 2 and "error" not in td, td

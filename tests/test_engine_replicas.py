@@ -36,8 +36,9 @@ def _port_block(n: int) -> int:
     raise RuntimeError("no free port block")
 
 
-def _start(tmp_path, base, world, tp):
+def _start(tmp_path, base, world, tp, transport="plane"):
     env = dict(os.environ, EMBED_ARCH="tiny-enc", LLM_ARCH="tiny-dec-tp8", TP_SIZE=str(tp), ENGINE_CONTINUOUS="1",
+               SEARCH_TRANSPORT=transport,
                INDEX_DIR=str(tmp_path / "index"), INDEX_CHECKPOINT_S="0", ENGINE_LIVENESS_INTERVAL="0",
                DATA_DIR=str(tmp_path), CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="", PYTHONPATH=ROOT,
                OMP_NUM_THREADS="1", ENGINE_MAX_BATCH="4", MAX_NEW_TOKENS="4", SUMMARY_MAX_NEW_TOKENS="4")
@@ -58,8 +59,10 @@ def _stop(p):
             p.wait(10)
 
 
-@pytest.mark.parametrize("tp", [1, 2])
-def test_engine_main_replicas_route_balance_search_and_recover(tmp_path, tp):
+@pytest.mark.parametrize("tp,transport", [(1, "plane"), (2, "plane"), (1, "rccl")])
+def test_engine_main_replicas_route_balance_search_and_recover(tmp_path, tp, transport):
+    """transport "rccl": the searches travel in the lock-step collective rounds
+    (parallel/collective_plane.py; gloo on these CPU ranks) instead of point to point."""
     from docagents_amd.engine.rpc import EngineCluster
     from docagents_amd.engine.server import owner_of
     world = 4
@@ -84,20 +87,28 @@ def test_engine_main_replicas_route_balance_search_and_recover(tmp_path, tp):
         assert {owner_of(d, world) for d in docs} == set(range(world))
         q = (await cl.call("embed", texts=["doc-3 part 1 text"], preprocess=True))["vecs"]
         s = await cl.call("search", vecs=q, filters=[docs], k=3, min_sim=-1.0)
+        assert (np.asarray(s["keys"]) >= 0).all()
+        h = await cl.call("health")
+        assert h["ok"] and not h.get("shards_down")
         ans = await asyncio.gather(*[cl.call("answer", items=[{"question": f"q{i}?", "context": "ctx",
                                                               "quality": 1.0}]) for i in range(2 * cl.replicas)])
         assert all(len(a["results"]) == 1 for a in ans)
         st = await cl.call("stats")
         assert len(st["replicas"]) == cl.replicas
+        planes = [r["search_plane"] for rep in st["replicas"] for r in rep["ranks"]]
+        if transport == "rccl":  # every rank joined the rounds that carried the search
+            assert len(planes) == world and all(p["transport"] == "gloo" and p["rounds"] >= 1 for p in planes)
+        else:
+            assert all("transport" not in p for p in planes)
         await cl.close()
         return q, s
 
-    p = _start(tmp_path, base, world, tp)
+    p = _start(tmp_path, base, world, tp, transport)
     try:
         q, before = asyncio.run(phase1())
     finally:
         _stop(p)
-    p = _start(tmp_path, base, world, tp)
+    p = _start(tmp_path, base, world, tp, transport)
 
     async def phase2():
         cl = await EngineCluster(f"tcp://127.0.0.1:{base}").connect(retries=400, delay=0.25)
