@@ -482,7 +482,10 @@ def main():
             from docagents_amd.parallel.collective_plane import CollectiveSearchPlane
             cctrl = tdist.new_group(backend="gloo", timeout=datetime.timedelta(seconds=120))
             cdata = tdist.new_group(backend=info.backend)
-            cplane = CollectiveSearchPlane(eng.index, R, W, cdata, cctrl, device=dev, timeout_s=120.0).start()
+            # the plane's scan stream, not a new one: ranks sharing one GPU (a rehearsal) each add a
+            # hardware queue per stream, and oversubscribed queues are time-sliced
+            cplane = CollectiveSearchPlane(eng.index, R, W, cdata, cctrl, device=dev, stream=plane.stream,
+                                           timeout_s=120.0).start()
             try:
                 qv = eng.embed([tg.question() for _ in range(a.serving_requests)]).float().cpu().numpy()
                 flt = []
