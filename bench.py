@@ -474,6 +474,24 @@ def main():
             shard, search, eng.embed, lambda i: ([tg.question() for _ in range(a.batch)], make_filters(5000 + i)),
             a.top_k, a.min_sim, a.multi_iters, ctrl, dev))
 
+        def tp_prompts(B, salt):
+            rng = np.random.default_rng(4242 + salt)  # the same prompts on every rank
+            tq = TextGen(seed=4242 + salt)
+            return [eng.answer_prompt_ids(tq.question(), [chunks.get(int(c)) for c in rng.integers(0, 1 << 30, a.top_k)],
+                                          a.max_new) for _ in range(B)]
+        if TP == 1:  # (--tp > 1: the headline itself decodes tensor-parallel)
+            # ranks sharing one GPU (a rehearsal) make every IPC all-reduce wait for the card's other
+            # contexts (~23 ms per call at 8 ranks): a few decode steps there, the full budget on a node
+            tp_new = a.max_new if n_phys == W else min(a.max_new, 6)
+            block("tp_decode", lambda: CB.tp_decode(
+                eng.dec_cfg, eng.decoder.w, R, W, dev, {1: tp_prompts(1, 1), a.batch: tp_prompts(a.batch, 2)},
+                tp_new, rccl_graphs=os.environ.get("DA_BENCH_RCCL_GRAPH") == "1", log=lambda m: log(info, m)))
+        if dev.type == "cuda":
+            from docagents_amd.parallel.xgmi_allreduce import verify_and_time
+            block("xgmi_allreduce", lambda: verify_and_time(None, dev))
+
+        # last: on ranks sharing one GPU (a rehearsal) the search streams' high-priority queues,
+        # once used, slowed every later block 2-3x (profiles/r5/rank8_gloo/serving_search_order/)
         def serving_search():
             """The serving transports side by side: the owner-routed plane (host TCP, the default) and
             SEARCH_TRANSPORT=rccl (lock-step rounds of RCCL all-gathers; parallel/collective_plane.py)."""
@@ -501,22 +519,6 @@ def main():
                 cplane.stop(timeout=10.0)
         if a.serving_requests > 0:
             block("serving_search", serving_search)
-
-        def tp_prompts(B, salt):
-            rng = np.random.default_rng(4242 + salt)  # the same prompts on every rank
-            tq = TextGen(seed=4242 + salt)
-            return [eng.answer_prompt_ids(tq.question(), [chunks.get(int(c)) for c in rng.integers(0, 1 << 30, a.top_k)],
-                                          a.max_new) for _ in range(B)]
-        if TP == 1:  # (--tp > 1: the headline itself decodes tensor-parallel)
-            # ranks sharing one GPU (a rehearsal) make every IPC all-reduce wait for the card's other
-            # contexts (~23 ms per call at 8 ranks): a few decode steps there, the full budget on a node
-            tp_new = a.max_new if n_phys == W else min(a.max_new, 6)
-            block("tp_decode", lambda: CB.tp_decode(
-                eng.dec_cfg, eng.decoder.w, R, W, dev, {1: tp_prompts(1, 1), a.batch: tp_prompts(a.batch, 2)},
-                tp_new, rccl_graphs=os.environ.get("DA_BENCH_RCCL_GRAPH") == "1", log=lambda m: log(info, m)))
-        if dev.type == "cuda":
-            from docagents_amd.parallel.xgmi_allreduce import verify_and_time
-            block("xgmi_allreduce", lambda: verify_and_time(None, dev))
 
     ranks_seen = int(round(all_reduce_sum(1.0, dev)))  # every rank that reached the end of the run
     gen = eng.gen.stats
