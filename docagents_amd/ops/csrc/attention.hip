@@ -794,7 +794,11 @@ __device__ __forceinline__ void dec_store(float o, float M, float ls, int b, int
   if (d == 0) { pm[pidx] = M; pl[pidx] = ls; }
 }
 
-template <int D, int G>
+// XC (same-XCD exchange): every split of (b, kv head) ran on ONE XCD (the launch's workgroup ->
+// XCD round-robin, see decode_attn_kernel), so partials and tickets live in ordinary (cached)
+// memory: the stores reach that XCD's L2, the ticket is an L2 atomic and the merging split reads
+// the partials from L2 (agent-scope loads: past its L1) — L2 round trips instead of uncached ones.
+template <int D, int G, bool XC = false>
 __device__ __forceinline__ void dec_finish(const float* po, const float* pm, const float* pl, int H, int Hkv,
                                            int nsplit, int b, int hk, int* cnt, bf16_t* out, int ldo, int* s_last) {
   if (nsplit == 1 || cnt == nullptr) return;  // no counters: the host launches decode_combine_kernel
@@ -806,12 +810,20 @@ __device__ __forceinline__ void dec_finish(const float* po, const float* pm, con
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (tid == 0) {
-    const int old = atomicAdd(&cnt[b * Hkv + hk], 1);
+    int* c = &cnt[b * Hkv + hk];
+    const int old = XC ? __hip_atomic_fetch_add(c, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : atomicAdd(c, 1);
     *s_last = old == nsplit - 1;
-    if (*s_last) cnt[b * Hkv + hk] = 0;
+    if (*s_last) {
+      if constexpr (XC) __hip_atomic_store(c, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      else *c = 0;
+    }
   }
   __syncthreads();
   if (!*s_last) return;
+  auto ld = [](const float* p) -> float {
+    if constexpr (XC) return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else return *p;
+  };
   // One online pass over the splits, 8 splits' (m, l, o) loads issued per step: the partials sit in
   // uncached memory (~1-2 us per round trip), so a max pass + a sum pass that each walk the splits
   // one dependent load at a time cost ~2 x nsplit round trips — most of a batch-1 decode attention.
@@ -824,9 +836,9 @@ __device__ __forceinline__ void dec_finish(const float* po, const float* pm, con
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const int s = min(s0 + j, nsplit - 1);
-        ms[j] = pm[base + s];
-        ls[j] = pl[base + s];
-        os[j] = po[(base + s) * D + d];
+        ms[j] = ld(pm + base + s);
+        ls[j] = ld(pl + base + s);
+        os[j] = ld(po + (base + s) * D + d);
       }
       float mx = M;
 #pragma unroll
@@ -885,7 +897,19 @@ decode_attn_kernel(const bf16_t* __restrict__ q, int ldq, const bf16_t* __restri
   __shared__ float sacc[G == 1 ? NWV * NSET * 64 * 8 : 1];
   __shared__ float swm[NWV][G], swl[NWV][G];
 
-  const int split = blockIdx.x, hk = blockIdx.y, b = blockIdx.z;
+  // VAR bit3 (XC): workgroup w of the launch runs on XCD w % 8 (round-robin dispatch; the host
+  // enables XC only after a placement probe confirmed it), so (b, kv head) pair p takes the nsplit
+  // workgroups w = 8 * (nsplit * (p / 8) + split) + p % 8: all of its splits on one XCD, their
+  // partials exchanged through that XCD's L2 (dec_finish<XC>). Needs (B * Hkv) % 8 == 0.
+  constexpr bool XC = (VAR & 8) != 0;
+  int split = blockIdx.x, hk = blockIdx.y, b = blockIdx.z;
+  if constexpr (XC) {
+    const int wl = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+    const int s8 = wl >> 3, pair = (s8 / nsplit) * 8 + (wl & 7);
+    split = s8 % nsplit;
+    hk = pair % Hkv;
+    b = pair / Hkv;
+  }
   const int L = lens[b];
   DA_ASSERT(L >= 0 && L <= max_seq && slot[b] >= 0);
   const int chunk = dec_chunk(L, nsplit, chunk_max);
@@ -1203,7 +1227,7 @@ decode_attn_kernel(const bf16_t* __restrict__ q, int ldq, const bf16_t* __restri
     dec_store(o, M, ls, b, hk * G + g, d, H, nsplit, split, D, po, pm, pl, out, ldo);
   }
   __shared__ int s_last;
-  dec_finish<D, G>(po, pm, pl, H, Hkv, nsplit, b, hk, cnt, out, ldo, &s_last);
+  dec_finish<D, G, XC>(po, pm, pl, H, Hkv, nsplit, b, hk, cnt, out, ldo, &s_last);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1425,7 +1449,12 @@ template <int D>
 static int launch_decode(int G, dim3 grid, hipStream_t s, const bf16_t* q, int ldq, const bf16_t* kc,
                          const bf16_t* vc, const int* lens, const int* slot, const int* pre, int H, int Hkv, int max_seq, int chunk,
                          int nsplit, float sl2e, float* po, float* pm, float* pl, bf16_t* out, int ldo,
-                         int* cnt, DecRope rope) {
+                         int* cnt, DecRope rope, int xc) {
+  if (xc) {  // same-XCD split exchange (cached ws / counters): the prefetching MHA form only
+    if (G != 1 || (int)(grid.y * grid.z) > kDecPrefetchPairs || (grid.y * grid.z) % 8 || !cnt || nsplit < 2)
+      return (int)hipErrorInvalidValue;
+    return launch_decode_v<D, 15>(G, grid, s, q, ldq, kc, vc, lens, slot, pre, H, Hkv, max_seq, chunk, nsplit, sl2e, po, pm, pl, out, ldo, cnt, rope);
+  }
   if (G == 1) {
     if ((int)(grid.y * grid.z) <= kDecPrefetchPairs)
       return launch_decode_v<D, 7>(G, grid, s, q, ldq, kc, vc, lens, slot, pre, H, Hkv, max_seq, chunk, nsplit, sl2e, po, pm, pl, out, ldo, cnt, rope);
@@ -1465,7 +1494,7 @@ DA_EXPORT int da_malloc_uncached(long long bytes, void** out) {
 static int decode_attn_impl(const void* q, int ldq, const void* k_cache, const void* v_cache, const void* lens,
                             const void* slot, const void* pre, int B, int H, int Hkv, int D, int max_seq, int chunk,
                             int nsplit, float scale, void* ws, void* o, int ldo, void* counters, const void* cos_sin,
-                            const void* pos, void* stream) {
+                            const void* pos, int xc, void* stream) {
   bf16_t* out = (bf16_t*)o;
   int* cnt = (int*)counters;
   if (H % Hkv || chunk % 64 || nsplit < 1 || (long)chunk * nsplit < 1) return (int)hipErrorInvalidValue;
@@ -1483,13 +1512,13 @@ static int decode_attn_impl(const void* q, int ldq, const void* k_cache, const v
   int err;
   switch (D) {
     case 64: err = launch_decode<64>(G, grid, s, (const bf16_t*)q, ldq, (const bf16_t*)k_cache, (const bf16_t*)v_cache,
-                                     (const int*)lens, (const int*)slot, (const int*)pre, H, Hkv, max_seq, chunk, nsplit, sl2e, po, pm, pl, out, ldo, cnt, rope);
+                                     (const int*)lens, (const int*)slot, (const int*)pre, H, Hkv, max_seq, chunk, nsplit, sl2e, po, pm, pl, out, ldo, cnt, rope, xc);
       break;
     case 96: err = launch_decode<96>(G, grid, s, (const bf16_t*)q, ldq, (const bf16_t*)k_cache, (const bf16_t*)v_cache,
-                                     (const int*)lens, (const int*)slot, (const int*)pre, H, Hkv, max_seq, chunk, nsplit, sl2e, po, pm, pl, out, ldo, cnt, rope);
+                                     (const int*)lens, (const int*)slot, (const int*)pre, H, Hkv, max_seq, chunk, nsplit, sl2e, po, pm, pl, out, ldo, cnt, rope, xc);
       break;
     case 128: err = launch_decode<128>(G, grid, s, (const bf16_t*)q, ldq, (const bf16_t*)k_cache, (const bf16_t*)v_cache,
-                                       (const int*)lens, (const int*)slot, (const int*)pre, H, Hkv, max_seq, chunk, nsplit, sl2e, po, pm, pl, out, ldo, cnt, rope);
+                                       (const int*)lens, (const int*)slot, (const int*)pre, H, Hkv, max_seq, chunk, nsplit, sl2e, po, pm, pl, out, ldo, cnt, rope, xc);
       break;
     default: return (int)hipErrorInvalidValue;
   }
@@ -1504,12 +1533,14 @@ static int decode_attn_impl(const void* q, int ldq, const void* k_cache, const v
   DA_LAUNCH_CHECK();
 }
 
+// xc = 1: same-XCD split exchange (ws / counters in ordinary device memory; the caller has checked
+// the launch's workgroup -> XCD round-robin with the placement probe). 0: uncached ws / counters.
 DA_EXPORT int da_decode_attn(const void* q, int ldq, const void* k_cache, const void* v_cache, const void* lens,
                              const void* slot, const void* pre, int B, int H, int Hkv, int D, int max_seq, int chunk,
                              int nsplit, float scale, void* ws, void* o, int ldo, void* counters, const void* cos_sin,
-                             const void* pos, void* stream) {
+                             const void* pos, int xc, void* stream) {
   return decode_attn_impl(q, ldq, k_cache, v_cache, lens, slot, pre, B, H, Hkv, D, max_seq, chunk, nsplit, scale, ws,
-                          o, ldo, counters, cos_sin, pos, stream);
+                          o, ldo, counters, cos_sin, pos, xc, stream);
 }
 
 // Dispatch order of the flash kernels (FaPrefix::rev, fa_block): causal longest query blocks first

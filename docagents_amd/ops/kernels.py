@@ -63,7 +63,7 @@ _SIGS = {
                           c_int, c_void_p, c_int, c_int, c_float, c_void_p, c_void_p, c_int, c_void_p],
     "da_decode_attn": [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
                        c_int, c_int, c_int, c_float, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p,
-                       c_void_p],
+                       c_int, c_void_p],
     "da_topk_dense": [c_void_p, c_int, c_int, c_void_p, c_void_p, c_int, c_void_p, c_int, c_float, c_int,
                       c_int, c_void_p, c_void_p, c_void_p, c_void_p],
     "da_topk_dense_stream": [c_void_p, c_int, c_int, c_void_p, c_void_p, c_int, c_void_p, c_int, c_float, c_int,
@@ -682,6 +682,50 @@ def _decode_split(B: int, Hkv: int, max_len: int, chunk: int):
     return chunk, max(1, math.ceil(max_len / chunk))
 
 
+# Same-XCD split exchange of the batch-1..small-batch MHA decode attention (attention.hip, VAR bit 3):
+# all splits of a (row, kv head) pair on one XCD, their partials and ticket in cached memory (L2
+# round trips instead of uncached ones). It relies on the launch's workgroup -> XCD round-robin, so
+# it is used only after the placement probe confirmed that on this device, and never once a
+# CU-masked stream exists in the process (a masked queue need not dispatch round-robin over XCDs;
+# ops/streams.py sets MASKED_STREAMS). DA_DECODE_XC=0 turns it off.
+DECODE_XC = os.environ.get("DA_DECODE_XC", "1") != "0"
+MASKED_STREAMS = False
+_XC_PROBE: dict = {}
+
+
+def decode_xc_ok(device) -> bool:
+    """True when every workgroup w of a launch runs on XCD w % 8 here (placement probe, once per
+    device; not during a graph capture, where the answer stays unknown = False)."""
+    if not DECODE_XC or MASKED_STREAMS:
+        return False
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    if idx in _XC_PROBE:
+        return _XC_PROBE[idx]
+    if torch.cuda.is_current_stream_capturing():
+        return False
+    n = 1024
+    out = torch.zeros(n * 4, dtype=torch.int32, device=device)
+    _check(lib().da_placement_probe(_ptr(out), n, 0, _stream()), "placement_probe")
+    xcc = out.view(n, 4)[:, 0].cpu().numpy()
+    ok = bool(len(set(xcc.tolist())) == 8 and all(len(set(xcc[r::8].tolist())) == 1 for r in range(8)))
+    _XC_PROBE[idx] = ok
+    return ok
+
+
+_COUNTERS: dict = {}
+
+
+def _cached_counters(tag: str, n: int, device) -> torch.Tensor:
+    """Zeroed int32 counters in ordinary device memory that stay allocated (captured graphs keep the
+    pointer; the kernels leave them zero)."""
+    key = (tag, device.index if device.index is not None else torch.cuda.current_device(),
+           getattr(_ROLE, "name", "main"))  # per workspace role, like the uncached ones: concurrent lanes
+    bufs = _COUNTERS.setdefault(key, [])
+    if not bufs or bufs[-1].numel() < n:
+        bufs.append(torch.zeros(max(n, 1024), dtype=torch.int32, device=device))
+    return bufs[-1]
+
+
 def _decode_checks(q, k_cache, v_cache, lens, slot, H, Hkv, D, max_len, pre, rope):
     _bf16_cuda(q, "q"); _i32(lens, "lens"); _i32(slot, "slot")
     _req(D in (64, 96, 128), "head dim")
@@ -720,12 +764,17 @@ def decode_attn(q, k_cache, v_cache, lens, slot, H, Hkv, D, max_len: int, chunk:
         out = torch.empty((B, H * D), dtype=torch.bfloat16, device=q.device)
     scale = scale if scale is not None else 1.0 / math.sqrt(D)
     cnt = None
+    xc = 0
     if _FUSED_COMBINE and nsplit > 1:
-        cnt = _uncached("decode_cnt", B * Hkv * 4, q.device)
-        ws = _uncached("decode_ws", B * H * nsplit * (D + 2) * 4, q.device)
+        if H == Hkv and B * Hkv <= 32 and (B * Hkv) % 8 == 0 and decode_xc_ok(q.device):
+            xc = 1  # same-XCD exchange: ws (the role workspace) and counters in cached memory
+            cnt = _cached_counters("decode_cnt_xc", B * Hkv, q.device)
+        else:
+            cnt = _uncached("decode_cnt", B * Hkv * 4, q.device)
+            ws = _uncached("decode_ws", B * H * nsplit * (D + 2) * 4, q.device)
     _check(lib().da_decode_attn(_ptr(q), q.stride(0), _ptr(k_cache), _ptr(v_cache), _ptr(lens), _ptr(slot), _ptr(pre), B, H,
                                 Hkv, D, k_cache.shape[2], chunk, nsplit, float(scale), _ptr(ws), _ptr(out), out.stride(0),
-                                _ptr(cnt), _ptr(cs), _ptr(ps), _stream()), "decode_attn")
+                                _ptr(cnt), _ptr(cs), _ptr(ps), xc, _stream()), "decode_attn")
     return out
 
 

@@ -61,6 +61,7 @@ def masked_stream(bits: list[int], device=None, tag: str = "") -> torch.cuda.Ext
     if not bits or max(bits) >= n:
         raise ValueError(f"CU mask bits must be a non-empty subset of 0..{n - 1}")
     words = mask_words(bits, n)
+    K.MASKED_STREAMS = True  # no same-XCD decode exchange from now on (kernels.decode_xc_ok)
     arr = (ctypes.c_uint * len(words))(*words)
     p = ctypes.c_void_p()
     with torch.cuda.device(dev):

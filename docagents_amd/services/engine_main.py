@@ -96,6 +96,13 @@ def main(argv=None) -> int:
             search_data = dist.new_group(backend="nccl" if dev.type == "cuda" else "gloo")
         if t > 1:
             tp = TPContext(rank % t, t, rep_data)
+    # CU-masked lanes before any decode graph is captured: the kernels pick launch forms that assume
+    # round-robin XCD dispatch only while no masked stream exists (ops/kernels.py decode_xc_ok)
+    lanes = (None, None, None)
+    if dev.type == "cuda" and cfg.engine_latency_cus > 0:
+        from ..ops.streams import serving_lanes
+        lanes = serving_lanes(cfg.engine_latency_cus, dev)
+        log.info("cu partition", "latency_cus", cfg.engine_latency_cus)
     eng = Engine(cfg.embed_arch, cfg.llm_arch, dev, seed=cfg.seed, tp=tp, max_batch=cfg.max_batch,
                  temperature=cfg.temperature, max_new_tokens=cfg.max_new_tokens,
                  summary_max_new=cfg.summary_max_new_tokens, index_kind=cfg.index_kind, ivf_lists=cfg.ivf_lists,
@@ -117,11 +124,6 @@ def main(argv=None) -> int:
         n = load_index(eng.index, f"{a.snapshot}.shard{rank}")
         log.info("restored index shard", "rank", rank, "rows", n)
     from ..parallel.search_plane import SearchPlane
-    lanes = (None, None, None)
-    if dev.type == "cuda" and cfg.engine_latency_cus > 0:
-        from ..ops.streams import serving_lanes
-        lanes = serving_lanes(cfg.engine_latency_cus, dev)
-        log.info("cu partition", "latency_cus", cfg.engine_latency_cus)
     if cfg.search_transport == "rccl" and world > 1:
         from ..parallel.collective_plane import CollectiveSearchPlane
         plane = CollectiveSearchPlane(eng.index, rank, world, search_data, search_ctrl, device=dev, stream=lanes[2],

@@ -340,6 +340,39 @@ def test_decode_attn_balanced_splits(H, Hkv, D, rope):
     _close(got, ref, atol=0.02)
 
 
+def test_decode_xc_probe_round_robin():
+    """The placement probe behind the same-XCD decode exchange: on an SPX MI355X a launch's workgroup w
+    runs on XCD w % 8 (8 distinct XCC ids, one per residue)."""
+    assert K.decode_xc_ok(torch.device(DEV))
+
+
+@pytest.mark.parametrize("B,H,rope", [(1, 32, False), (1, 32, True), (2, 16, True), (4, 8, False)])
+@pytest.mark.parametrize("lens0", [2937, 64, 1])
+def test_decode_attn_same_xcd_exchange(B, H, rope, lens0, monkeypatch):
+    """Splits merged through one XCD's L2 (cached partials + L2 ticket) == the uncached cross-XCD merge,
+    bit for bit, and vs the fp32 reference; repeated launches (the counters must return to zero)."""
+    torch.manual_seed(B * H + lens0)
+    D, max_seq = 96, 4096
+    kc, vc = _rand(B + 1, H, max_seq, D), _rand(B + 1, H, max_seq, D)
+    q = _rand(B, 3 * H * D)
+    lens = torch.tensor([lens0, 1500, 333, 4000][:B], dtype=torch.int32, device=DEV)
+    slot = torch.arange(B, dtype=torch.int32, device=DEV) + 1
+    cs = R.rope_table(max_seq, D, 10000.0, device=DEV)
+    rp = (cs, lens - 1) if rope else None
+    assert K.decode_xc_ok(torch.device(DEV)) and (B * H) % 8 == 0 and B * H <= 32
+    outs = {}
+    for xc in (True, False):
+        monkeypatch.setattr(K, "DECODE_XC", xc)
+        k2, v2 = kc.clone(), vc.clone()
+        outs[xc] = [K.decode_attn(q, k2, v2, lens, slot, H, H, D, max_len=max_seq, rope=rp) for _ in range(3)]
+        outs[xc].append((k2, v2))
+    for i in range(3):
+        assert torch.equal(outs[True][i], outs[False][i]) and torch.equal(outs[True][i], outs[True][0])
+    assert torch.equal(outs[True][3][0], outs[False][3][0]) and torch.equal(outs[True][3][1], outs[False][3][1])
+    ref = R.decode_attn(q.clone(), kc.clone(), vc.clone(), lens, slot, H, H, D, rope=rp)
+    _close(outs[True][0], ref, atol=0.02)
+
+
 @pytest.mark.parametrize("H,Hkv,D", [(32, 32, 96), (32, 8, 128), (8, 1, 128), (12, 6, 64)])
 def test_decode_attn(H, Hkv, D):
     torch.manual_seed(H * D)
