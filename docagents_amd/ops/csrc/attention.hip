@@ -10,6 +10,8 @@
 //    (unnormalised O, running max, running sum) merged by decode_combine.
 #include "common.h"
 
+#include <cstdlib>
+
 // Floating-point contraction only within one expression (a*b + c -> fma), never across statements:
 // with the HIP default (fast) the backend fuses differently depending on the surrounding code, and
 // the decode attention inlined into the persistent batch-1 kernel (decode_b1.hip) then differed from
@@ -1310,7 +1312,8 @@ decode_attn_gqa_kernel(const bf16_t* __restrict__ q, int ldq, const bf16_t* __re
       const int P = i * 64 + lane, row = P / NS, sl = P % NS;
       const int c = sl ^ vswz<D>(row);
       const int key = min(row, nk - 1);
-      __builtin_amdgcn_global_load_lds((gptr_t)(vb + (size_t)key * D + c * 8), (lds_ptr_t)(myv + i * 1024), 16, 0, 0);
+      // aux 2 = nt (read once per step; see decode_attn_mfma1_kernel)
+      __builtin_amdgcn_global_load_lds((gptr_t)(vb + (size_t)key * D + c * 8), (lds_ptr_t)(myv + i * 1024), 16, 0, 2);
     }
     // ---- S^T = K Q^T ----
     f32x4_t sacc[4];
@@ -1398,6 +1401,235 @@ decode_attn_gqa_kernel(const bf16_t* __restrict__ q, int ldq, const bf16_t* __re
   dec_finish<D, G>(po, pm, pl, H, Hkv, nsplit, b, hk, cnt, out, ldo, &s_last);
 }
 
+// MHA decode attention on MFMA for few (row, kv head) pairs (batch 1..: the p50 path). The VALU
+// kernel (decode_attn_kernel, G = 1) spends ~2k VALU cycles per 64-key tile on its dot products, so
+// at batch 1 — 32 pairs, a few tiles per wave — it is issue-bound, not HBM-bound (profiles/r5/
+// decode_mfma1/: 2.9 TB/s even with the K/V in the MALL). Here the single query is the N = 16 side of
+// v_mfma_f32_16x16x32_bf16 (column 0 live, 15 zero), exactly the GQA kernel's data path with G = 1:
+// K rows straight into registers (non-temporal), the V tile by LDS-DMA into a wave-private region
+// (XOR chunk swizzle within groups of 4 chunks, so D = 96's 12 chunks per row stay in the row),
+// S^T = K Q^T, softmax over column 0, O^T += V^T P^T with transposed LDS reads. chunk <= 512 keys per
+// split (host-checked) gives every wave at most TWO tiles, and both are requested before any is
+// waited for: one HBM round trip per workgroup. XC: same-XCD split exchange (see dec_finish).
+template <int D>
+__device__ __forceinline__ int vswz1(int r) {
+  return D == 96 ? ((r >> 1) & 3) : vswz<D>(r);
+}
+
+// RP: fused RoPE + new-token KV write (DecRope, as decode_attn_kernel): q is the raw qkv row; q is
+// rotated into LDS while the tiles fly, key L - 1 enters as one extra online-softmax term of the
+// split that holds it (taken from the qkv row, written into the cache for later steps).
+template <int D, bool XC, bool RP>
+__global__ void __launch_bounds__(256)
+decode_attn_mfma1_kernel(const bf16_t* __restrict__ q, int ldq, const bf16_t* __restrict__ kc,
+                         const bf16_t* __restrict__ vc, const int* __restrict__ lens, const int* __restrict__ slot,
+                         const int* __restrict__ pre, int H, int Hkv, int max_seq, int chunk_max, int nsplit,
+                         float scale_log2e, float* __restrict__ po, float* __restrict__ pm, float* __restrict__ pl,
+                         bf16_t* __restrict__ out, int ldo, int* __restrict__ cnt, DecRope rope) {
+  static_assert(D == 64 || D == 96 || D == 128, "head dim");
+  constexpr int KT = 64, NDS = D / 32, NDT = D / 16, NS = D / 8;
+  constexpr int VBYTES = KT * D * 2, NDMA = VBYTES / 1024;
+  typedef __attribute__((address_space(3))) void* lds_ptr_t;
+  typedef __attribute__((address_space(1))) const void* gptr_t;
+  __shared__ __attribute__((aligned(16))) char sv[4 * 2 * VBYTES];  // two tiles per wave
+  __shared__ float swm[4], swl[4];
+
+  int split = blockIdx.x, hk = blockIdx.y, b = blockIdx.z;
+  if constexpr (XC) {  // the same-XCD mapping of decode_attn_kernel
+    const int wl = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+    const int s8 = wl >> 3, pair = (s8 / nsplit) * 8 + (wl & 7);
+    split = s8 % nsplit;
+    hk = pair % Hkv;
+    b = pair / Hkv;
+  }
+  const int L = lens[b];
+  DA_ASSERT(L >= 0 && L <= max_seq && slot[b] >= 0);
+  const int chunk = dec_chunk(L, nsplit, chunk_max);
+  DA_ASSERT(chunk <= 8 * KT);
+  const int kstart = split * chunk;
+  const bool own_new = RP && kstart <= L - 1 && L - 1 < kstart + chunk;  // this split holds key L - 1
+  const int kend = min(RP ? L - 1 : L, kstart + chunk);                  // RP: key L - 1 from the qkv row
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int fr = lane & 15, fg = lane >> 4;
+  const size_t cbase = ((size_t)slot[b] * Hkv + hk) * (size_t)max_seq * D;
+  const int P = pre ? pre[2 * b] : 0;  // shared-prefix keys [0, P) live in slot pre[2b + 1]
+  const size_t pbase = P ? ((size_t)pre[2 * b + 1] * Hkv + hk) * (size_t)max_seq * D : cbase;
+  DA_ASSERT(P % 64 == 0 && P <= L);
+  DA_ASSERT(!RP || rope.pos[b] == L - 1);
+
+  // ---- both tiles of this wave requested up front (branch-free: an empty tile reads key 0 of
+  //      the row's own slot, valid memory whose scores are masked) ----
+  const int ta = kstart + w * KT, tb = ta + 4 * KT;
+  u32x4_t kr[2][4][NDS];
+  auto issue = [&](int j, int t0) {
+    const int nk = kend - t0;
+    const bool shared = t0 < P;
+    const bf16_t* kb = nk > 0 ? kc + (shared ? pbase : cbase) + (size_t)t0 * D : kc + cbase;
+    const bf16_t* vb = nk > 0 ? vc + (shared ? pbase : cbase) + (size_t)t0 * D : vc + cbase;
+    const int last = nk > 0 ? min(KT, nk) - 1 : 0;
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int ds = 0; ds < NDS; ++ds) {
+        const int key = min(16 * t + fr, last);
+        kr[j][t][ds] = __builtin_nontemporal_load((const u32x4_t*)(kb + (size_t)key * D + ds * 32 + fg * 8));
+      }
+    char* myv = sv + (w * 2 + j) * VBYTES;
+#pragma unroll
+    for (int i = 0; i < NDMA; ++i) {
+      const int pc = i * 64 + lane, row = pc / NS, sl = pc % NS;
+      const int c = sl ^ vswz1<D>(row);
+      const int key = min(row, last);
+      // aux 2 = nt: the KV stream is read once per step; allocating it in L2 / MALL cost the GEMVs
+      // that follow ~3 % (their weights lose cache residency): profiles/r5/decode_mfma1/
+      __builtin_amdgcn_global_load_lds((gptr_t)(vb + (size_t)key * D + c * 8), (lds_ptr_t)(myv + i * 1024), 16, 0, 2);
+    }
+  };
+  issue(0, ta);
+  issue(1, tb);
+
+  bf16x8_t qf[NDS];
+  [[maybe_unused]] __shared__ __attribute__((aligned(16))) bf16_t sqb[RP ? D : 1];
+  [[maybe_unused]] __shared__ float skn[RP ? D : 1], svn[RP ? D : 1];
+  [[maybe_unused]] __shared__ float ssn;
+  if constexpr (RP) {
+    // rotate q (and the new key) at position L - 1, rounded to bf16 like the rope_cache kernel
+    constexpr int HALF = D / 2;
+    const bf16_t* qrow = q + (size_t)b * ldq;
+    if (tid < D) {
+      const int d = tid, i = d >> 1;
+      const float c = rope.cs[((size_t)(L - 1) * HALF + i) * 2], sn = rope.cs[((size_t)(L - 1) * HALF + i) * 2 + 1];
+      auto rot = [&](const bf16_t* hp) {
+        const float x1 = bf2f(hp[d & ~1]), x2 = bf2f(hp[d | 1]);
+        return f2bf((d & 1) ? x2 * c + x1 * sn : x1 * c - x2 * sn);
+      };
+      sqb[d] = rot(qrow + hk * D);
+      if (own_new) {
+        const bf16_t kn = rot(qrow + (size_t)(H + hk) * D), vn = qrow[(size_t)(H + Hkv + hk) * D + d];
+        skn[d] = bf2f(kn);
+        svn[d] = bf2f(vn);
+        const size_t crow = cbase + (size_t)(L - 1) * D;
+        rope.kc[crow + d] = kn;  // for later steps (read back only after this launch)
+        rope.vc[crow + d] = vn;
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int ds = 0; ds < NDS; ++ds)
+      qf[ds] = fr == 0 ? *(const bf16x8_t*)(sqb + ds * 32 + fg * 8) : bf16x8_t{0, 0, 0, 0, 0, 0, 0, 0};
+    if (own_new && w == 0) {  // score of the new key (log2 units)
+      float part = 0.f;
+      for (int d = lane; d < D; d += 64) part += bf2f(sqb[d]) * skn[d];
+      part = wave_sum(part);
+      if (lane == 0) ssn = part * scale_log2e;
+    }
+  } else {
+#pragma unroll
+    for (int ds = 0; ds < NDS; ++ds)
+      qf[ds] = fr == 0 ? *(const bf16x8_t*)(q + (size_t)b * ldq + hk * D + ds * 32 + fg * 8)
+                       : bf16x8_t{0, 0, 0, 0, 0, 0, 0, 0};
+  }
+  f32x4_t oacc[NDT];
+#pragma unroll
+  for (int i = 0; i < NDT; ++i) oacc[i] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  float m_run = -INFINITY, l_part = 0.f;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // both tiles' K registers and V regions landed
+
+  auto process = [&](int j, int t0) {
+    const int nk = kend - t0;
+    f32x4_t sacc[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      sacc[t] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ds = 0; ds < NDS; ++ds) sacc[t] = mfma16(__builtin_bit_cast(bf16x8_t, kr[j][t][ds]), qf[ds], sacc[t]);
+    }
+    float mx = -INFINITY;
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int key = 16 * t + 4 * fg + i;
+        const float sc = key < nk ? sacc[t][i] * scale_log2e : -INFINITY;
+        sacc[t][i] = sc;
+        mx = fmaxf(mx, sc);
+      }
+    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+    mx = max_xhalf(mx);
+    const float m_new = fmaxf(m_run, mx);
+    const float m_use = (m_new == -INFINITY) ? 0.f : m_new;
+    const float alpha = exp2f(m_run - m_use);
+    m_run = m_new;
+    float psum = 0.f;
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float p = __builtin_amdgcn_exp2f(sacc[t][i] - m_use);
+        sacc[t][i] = p;
+        psum += p;
+      }
+    l_part = l_part * alpha + psum;
+#pragma unroll
+    for (int i = 0; i < NDT; ++i) oacc[i] *= alpha;
+    const char* myv = sv + (w * 2 + j) * VBYTES;
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      const u32x4_t pw = u32x4_t{pack_bf2(sacc[2 * c][0], sacc[2 * c][1]), pack_bf2(sacc[2 * c][2], sacc[2 * c][3]),
+                                 pack_bf2(sacc[2 * c + 1][0], sacc[2 * c + 1][1]),
+                                 pack_bf2(sacc[2 * c + 1][2], sacc[2 * c + 1][3])};
+      const bf16x8_t pb = __builtin_bit_cast(bf16x8_t, pw);
+      const int q4 = fr >> 2, p4 = fr & 3;
+#pragma unroll
+      for (int dt = 0; dt < NDT; ++dt) {
+        const int col = dt * 16 + 4 * p4;
+        const int r0 = 32 * c + 4 * fg + q4, r1 = r0 + 16;
+        const s16x4_t lo = lds_read_tr16(myv + r0 * (D * 2) + (((col >> 3) ^ vswz1<D>(r0)) << 4) + (col & 7) * 2);
+        const s16x4_t hi = lds_read_tr16(myv + r1 * (D * 2) + (((col >> 3) ^ vswz1<D>(r1)) << 4) + (col & 7) * 2);
+        const bf16x8_t va = bf16x8_t{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        oacc[dt] = mfma16(va, pb, oacc[dt]);
+      }
+    }
+  };
+  if (ta < kend) process(0, ta);
+  if (tb < kend) process(1, tb);
+
+  // ---- merge the 4 waves (query column 0: lanes fr == 0) through LDS ----
+  float l_tot = l_part + __shfl_xor(l_part, 16, 64);
+  l_tot = sum_xhalf(l_tot);
+  if (lane == 0) { swm[w] = m_run; swl[w] = l_tot; }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __syncthreads();  // every wave is done with its V regions
+  float* so = (float*)sv;  // [4][D]: column 0 of each wave's O^T
+  if (fr == 0) {
+#pragma unroll
+    for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) so[w * D + dt * 16 + 4 * fg + i] = oacc[dt][i];
+  }
+  __syncthreads();
+  for (int d = tid; d < D; d += 256) {
+    float M = fmaxf(fmaxf(swm[0], swm[1]), fmaxf(swm[2], swm[3]));
+    if (own_new) M = fmaxf(M, ssn);
+    const float Mu = (M == -INFINITY) ? 0.f : M;
+    float o = 0.f, ls = 0.f;
+#pragma unroll
+    for (int ww = 0; ww < 4; ++ww) {
+      const float f = exp2f(swm[ww] - Mu);
+      o += so[ww * D + d] * f;
+      ls += swl[ww] * f;
+    }
+    if (own_new) {  // the new token's key: weight exp2(s - M), value straight from the qkv row
+      const float f = exp2f(ssn - Mu);
+      o += svn[d] * f;
+      ls += f;
+    }
+    dec_store(o, M, ls, b, hk, d, H, nsplit, split, D, po, pm, pl, out, ldo);
+  }
+  __shared__ int s_last;
+  dec_finish<D, 1, XC>(po, pm, pl, H, Hkv, nsplit, b, hk, cnt, out, ldo, &s_last);
+}
+
 template <int D>
 __global__ void decode_combine_kernel(const float* __restrict__ po, const float* __restrict__ pm,
                                       const float* __restrict__ pl, int H, int nsplit, bf16_t* __restrict__ o,
@@ -1450,6 +1682,20 @@ static int launch_decode(int G, dim3 grid, hipStream_t s, const bf16_t* q, int l
                          const bf16_t* vc, const int* lens, const int* slot, const int* pre, int H, int Hkv, int max_seq, int chunk,
                          int nsplit, float sl2e, float* po, float* pm, float* pl, bf16_t* out, int ldo,
                          int* cnt, DecRope rope, int xc) {
+  static int mfma1 = -1;
+  if (mfma1 < 0) {
+    const char* e = getenv("DA_DECODE_MFMA1");
+    mfma1 = (e && e[0] == '0') ? 0 : 1;
+  }
+  if (mfma1 && G == 1 && (int)(grid.y * grid.z) <= kDecPrefetchPairs && chunk <= 512) {
+    if (xc && ((grid.y * grid.z) % 8 || !cnt || nsplit < 2)) return (int)hipErrorInvalidValue;
+#define M1(XCV, RPV) decode_attn_mfma1_kernel<D, XCV, RPV><<<grid, 256, 0, s>>>(q, ldq, kc, vc, lens, slot, pre, H, Hkv, \
+                         max_seq, chunk, nsplit, sl2e, po, pm, pl, out, ldo, cnt, rope)
+    if (xc) { if (rope.cs) M1(true, true); else M1(true, false); }
+    else { if (rope.cs) M1(false, true); else M1(false, false); }
+#undef M1
+    return (int)hipGetLastError();
+  }
   if (xc) {  // same-XCD split exchange (cached ws / counters): the prefetching MHA form only
     if (G != 1 || (int)(grid.y * grid.z) > kDecPrefetchPairs || (grid.y * grid.z) % 8 || !cnt || nsplit < 2)
       return (int)hipErrorInvalidValue;
