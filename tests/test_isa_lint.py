@@ -17,6 +17,7 @@ from docagents_amd.ops import build as B
 
 HOT_NO_SCRATCH = {  # mangled-name prefixes of the kernels the flagship bench runs
     "attention.hip": ["_Z18decode_attn_kernelILi96ELi1ELi3EE", "_Z18decode_attn_kernelILi96ELi1ELi7EE",
+                      "_Z18decode_attn_kernelILi96ELi1ELi15EE", "_Z24decode_attn_mfma1_kernelILi96E",
                       "_Z22flash_attn_pipe_kernelILi96ELb1ELb1EE",
                       "_Z20flash_attn_v2_kernelILi64ELi4ELi1E", "_Z20flash_attn_v2_kernelILi128ELi8ELi1E"],
     "gemm.hip": ["_Z11gemv_kernel", "_Z16gemm_bf16_kernelILi64ELi128ELi1ELi4ELi5ELi4EE",
