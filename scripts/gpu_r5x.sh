@@ -3,7 +3,7 @@
 # GPU with the serving_search block (owner-routed plane vs lock-step collective rounds).
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
-O=gpurun_out/r5x
+O=gpurun_out/${TAG:-r5x}
 mkdir -p $O
 timeout -k 10 300 python -u -m pytest -x -v --timeout 200 --timeout-method thread tests/test_collective_plane.py \
   > $O/cplane.log 2>&1 || { tail -30 $O/cplane.log; exit 1; }
