@@ -186,15 +186,20 @@ gemm8p_kernel(GemmArgs p) {
 
   //   phase A waits A1(t)         : A0 B0 B1(t+1), A1(t+1) newer -> CNT_AB (0 in the last tile)
   //   phase B waits A0 B0 B1(t+1) : A1(t+1), A0 B0 B1(t+2) newer -> CNT_AB (NA when t+2 does not exist)
-  auto ktile = [&](int kt, auto fill_tag, auto next_tag) __attribute__((always_inline)) {
+  // X: store instructions the previous tile of a persistent workgroup issued between this tile's
+  // prologue DMA and K-tile 0 (X > 0 only for kt = 0): they are younger than the half-tiles kt = 0
+  // waits for, so its counted waits let them stay in flight — the stores drain under the MFMAs of
+  // K-tile 0 instead of before them (vmcnt retires loads, stores and LDS-DMA in issue order)
+  auto ktile = [&](int kt, auto fill_tag, auto next_tag, auto x_tag) __attribute__((always_inline)) {
     constexpr bool FILL = decltype(fill_tag)::value;  // tile kt + 2 exists
     constexpr bool NEXT = decltype(next_tag)::value;  // tile kt + 1 exists
+    constexpr int X = decltype(x_tag)::value;
     const int b = kt & 1;
     const char* base = smem + b * BUF;
     read_a(base + OFF_A0);
     read_b(rb0, base + OFF_B0);
     read_b(rb1, base + OFF_B1);
-    if constexpr (NEXT) { ISSUE_A(1, kt + 1, b ^ 1); vmcnt<CNT_AB>(); }
+    if constexpr (NEXT) { ISSUE_A(1, kt + 1, b ^ 1); vmcnt<CNT_AB + X>(); }
     else { vmcnt<0>(); }
     lgkm0();
     bar();
@@ -204,8 +209,8 @@ gemm8p_kernel(GemmArgs p) {
     __builtin_amdgcn_s_setprio(0);
     bar();
     read_a(base + OFF_A1);
-    if constexpr (FILL) { ISSUE_A(0, kt + 2, b); ISSUE_B(0, kt + 2, b); ISSUE_B(1, kt + 2, b); vmcnt<CNT_AB>(); }
-    else if constexpr (NEXT) { vmcnt<NA>(); }
+    if constexpr (FILL) { ISSUE_A(0, kt + 2, b); ISSUE_B(0, kt + 2, b); ISSUE_B(1, kt + 2, b); vmcnt<CNT_AB + X>(); }
+    else if constexpr (NEXT) { vmcnt<NA + X>(); }
     lgkm0();
     bar();
     __builtin_amdgcn_s_setprio(1);
@@ -226,16 +231,20 @@ gemm8p_kernel(GemmArgs p) {
   constexpr int NB = NI < 8 ? NI : 8;
   const int ncols = SW ? p.N / 2 : p.N;
 
+  // stores per lane of a persistent tile's epilogue (non-RoPE: one unconditional buffer store per
+  // staged row; rows past M / columns past N fall outside the store's buffer range and are dropped)
+  constexpr int XS = (PERSIST && EPI != EPI_ROPE) ? NI : 0;
+  using X0 = std::integral_constant<int, 0>;
+  using XN = std::integral_constant<int, XS>;
+
   sources(m0, n0);
   prologue();
   bool first = true;
   for (;;) {
-    // wait for A0 B0 B1 of K-tile 0. A persistent workgroup's later tiles wait for everything it
-    // has in flight: the previous tile's output stores were issued after this tile's prologue DMA,
-    // and loads and stores need not retire in issue order.
+    // wait for A0 B0 B1 of K-tile 0; on a persistent workgroup's later tiles the previous tile's
+    // XS stores (issued after this tile's prologue DMA) may stay in flight
     if (first) vmcnt<CNT_AB>();
-    else vmcnt<0>();
-    first = false;
+    else vmcnt<CNT_AB + XS>();
     bar();
     if (wg) bar();  // G1 runs one barrier behind
 #pragma unroll
@@ -246,10 +255,17 @@ gemm8p_kernel(GemmArgs p) {
         for (int i = 0; i < MI; ++i)
 #pragma unroll
           for (int j = 0; j < 2; ++j) acc[a][b][i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-    int kt = 0;
-    for (; kt < nk - 2; ++kt) ktile(kt, T_{}, T_{});
-    ktile(kt, F_{}, T_{});
-    ktile(kt + 1, F_{}, F_{});
+    if (nk > 2) {
+      if (first) ktile(0, T_{}, T_{}, X0{});
+      else ktile(0, T_{}, T_{}, XN{});
+      for (int kt = 1; kt < nk - 2; ++kt) ktile(kt, T_{}, T_{}, X0{});
+      ktile(nk - 2, F_{}, T_{}, X0{});
+    } else {  // nk == 2: K-tile 0 is also the last-but-one
+      if (first) ktile(0, F_{}, T_{}, X0{});
+      else ktile(0, F_{}, T_{}, XN{});
+    }
+    ktile(nk - 1, F_{}, F_{}, X0{});
+    first = false;
     if (!wg) bar();  // re-align the groups
     __syncthreads();
 
@@ -350,6 +366,12 @@ gemm8p_kernel(GemmArgs p) {
         slv[i] = p.rope.slot[gmc];
       }
     }
+    // output rows m0 .. M - 1 of this tile (num_records clamped below 2 GiB: a tile's rows are far
+    // inside it, rows past M fall outside it)
+    [[maybe_unused]] __amdgpu_buffer_rsrc_t rsc;
+    if constexpr (XS > 0)
+      rsc = __builtin_amdgcn_make_buffer_rsrc((void*)(p.C + (size_t)m0 * p.ldc), (short)0,
+                                              (int)min((long long)(p.M - m0) * p.ldc * 2, 0x7ffffff0ll), 0x00020000);
     const int nid = id + (int)gridDim.x;
     const bool more = PERSIST && nid < ntiles;
     int nm0 = 0, nn0 = 0;
@@ -406,7 +428,7 @@ gemm8p_kernel(GemmArgs p) {
 #pragma unroll
         for (int i = 0; i < NB; ++i) {
           const int gm = gmv[i0 + i];
-          if (gm >= p.M || !col_ok) continue;
+          if (XS == 0 && (gm >= p.M || !col_ok)) continue;
           u32x4_t v = vv[i0 + i];
           if constexpr (EPI == EPI_RESID) {
 #pragma unroll
@@ -416,7 +438,14 @@ gemm8p_kernel(GemmArgs p) {
               v[e] = T::pack2(lo, hi);
             }
           }
-          *(u32x4_t*)(p.C + (size_t)gm * p.ldc + gcol) = v;
+          if constexpr (XS > 0) {
+            // exactly one store instruction per row, whatever the row / column (the counted waits
+            // of the next tile's K-tile 0 rely on it): out-of-range ones land past num_records
+            const unsigned off = col_ok ? (unsigned)((gm - m0) * p.ldc + gcol) * 2u : 0x80000000u;
+            __builtin_amdgcn_raw_buffer_store_b128(v, rsc, off, 0, 0);
+          } else {
+            *(u32x4_t*)(p.C + (size_t)gm * p.ldc + gcol) = v;
+          }
         }
       }
     }

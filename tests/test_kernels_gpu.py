@@ -78,12 +78,13 @@ def test_gemm8p_tile(M, N, Kd, epi, tile):
     _close(got, ref, atol=0.04)
 
 
-@pytest.mark.parametrize("M,N,Kd", [(4100, 4104, 256), (2304, 9216, 192)])
+@pytest.mark.parametrize("M,N,Kd", [(4100, 4104, 256), (2304, 9216, 192), (3000, 9216, 128), (2600, 3072, 3072)])
 @pytest.mark.parametrize("epi", [K.EPI_NONE, K.EPI_BIAS, K.EPI_GELU, K.EPI_RESID, K.EPI_SWIGLU])
 @pytest.mark.parametrize("tile", [7, 10])
 def test_gemm8p_persistent(M, N, Kd, epi, tile):
-    """More tiles than CUs: the persistent tile loop (workgroups running 1-3 tiles each, ragged M / N)
-    vs the fp32 reference, and bit-identical to one workgroup per tile."""
+    """More tiles than CUs: the persistent tile loop (workgroups running 1-3 tiles each, ragged M / N;
+    K = 128 / 192 / 256 / 3072: every K-loop shape of the first K-tile whose counted waits let the
+    previous tile's stores fly) vs the fp32 reference, and bit-identical to one workgroup per tile."""
     torch.manual_seed(M + N + epi + tile)
     if epi == K.EPI_SWIGLU:
         N = (N // 32) * 32
