@@ -47,6 +47,8 @@ class Engine:
         self.max_new_tokens = max_new_tokens
         self.summary_max_new = summary_max_new
         self.embed_max_tokens = embed_max_tokens
+        # one short text (a question) through the encoder's captured length-bucket graphs
+        self.enc_graphs = use_graphs and self.device.type == "cuda"
         self.encoder = BertEncoder(self.enc_cfg, self.device, seed=seed, dtype=enc_dtype) if load_encoder else None
         self.decoder = None
         self.gen = None
@@ -87,6 +89,13 @@ class Engine:
             from ..utils import metrics
             metrics.ENGINE_EMBED_TRUNCATED.labels("texts").inc(self.stats["embed_truncated_texts"] - trunc0[0])
             metrics.ENGINE_EMBED_TRUNCATED.labels("tokens").inc(self.stats["embed_truncated_tokens"] - trunc0[1])
+        if n == 1 and self.enc_graphs:
+            with self.enc_lock:
+                out[0] = self.encoder.encode_one(seqs[0])[0].to(out_dtype)
+            self.stats["embed_tokens"] += len(seqs[0])
+            self.stats["embed_texts"] += 1
+            self.stats["embed_s"] += time.perf_counter() - t0
+            return out
         order = np.argsort([-len(s) for s in seqs], kind="stable")
         with self.enc_lock:
             i = 0

@@ -195,6 +195,28 @@ def test_bge_base_width_encoder_vs_reference():
     assert torch.allclose(a.float(), b.float(), atol=3e-2)
 
 
+@pytest.mark.parametrize("arch", ["tiny-enc", "bge-base"])
+def test_encoder_one_sequence_graphs_match_eager(arch):
+    """encode_one (length-bucket HIP graphs, padded rows past the real length) == the eager packed
+    path and the fp32 reference, across bucket edges, repeated replays and both pooling inputs."""
+    import dataclasses
+    cfg = encoder_config(arch)
+    if arch == "bge-base":
+        cfg = dataclasses.replace(cfg, layers=2)
+    enc = BertEncoder(cfg, "cuda", seed=5)
+    ref = BertEncoder(cfg, "cuda", weights=enc.w)
+    ref.ops = reference
+    for n in (1, 2, 15, 16, 17, 31, 33, 64, 100, 128, 129, 20, 1):
+        seq = [int(t) for t in np.random.default_rng(n).integers(5, cfg.vocab - 1, size=n)]
+        g = enc.encode_one(seq)
+        e = enc.encode_packed([seq])
+        r = ref.encode_packed([seq]).to(g.device)
+        assert g.shape == e.shape == (1, cfg.hidden)
+        assert float((g.float() * e.float()).sum()) > 0.9995, n
+        assert torch.allclose(g.float(), r.float(), atol=3e-2), n
+    assert set(enc._g) == set(BertEncoder.GRAPH_BUCKETS)
+
+
 def test_generate_batch_above_64_graph_equals_eager():
     """Decode batches above 64 rows (mid-M weight-streaming tiles with split-K inside the captured
     graph): graph replay == eager, token for token, and near-argmax under the fp32 reference."""
