@@ -47,9 +47,12 @@ class Engine:
         self.max_new_tokens = max_new_tokens
         self.summary_max_new = summary_max_new
         self.embed_max_tokens = embed_max_tokens
-        # one short text (a question) through the encoder's captured length-bucket graphs
+        # one short text (a question) through the encoder's captured length-bucket graphs,
+        # captured here at startup rather than under the first request
         self.enc_graphs = use_graphs and self.device.type == "cuda"
         self.encoder = BertEncoder(self.enc_cfg, self.device, seed=seed, dtype=enc_dtype) if load_encoder else None
+        if self.encoder is not None and self.enc_graphs:
+            self.encoder.prepare_graphs()
         self.decoder = None
         self.gen = None
         if load_llm:

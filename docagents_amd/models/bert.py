@@ -203,10 +203,22 @@ class BertEncoder:
                     pool(self.forward(ids, pos, cu, T), cu, mode)
                 side.synchronize()
                 g = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g, stream=side):
+                # thread_local: a capture must not trip over the serving threads' own CUDA calls
+                with torch.cuda.graph(g, stream=side, capture_error_mode="thread_local"):
                     out = pool(self.forward(ids, pos, cu, T), cu, mode)
                 self._g[T] = (g, ids, cu, out)
         torch.cuda.current_stream(dev).wait_stream(side)
+
+    def prepare_graphs(self) -> None:
+        """Capture the length-bucket graphs now (the engine does it at startup, before serving). A
+        capture that fails leaves the eager path in charge (``_g`` empty), loudly."""
+        if self.device.type == "cuda" and getattr(self, "_g", None) is None:
+            try:
+                self._capture_small()
+            except Exception as e:  # noqa: BLE001 - the eager encoder still serves
+                import logging
+                logging.getLogger(__name__).warning("encoder graph capture failed, eager path: %r", e)
+                self._g = {}
 
     def encode_one(self, seq: list[int]) -> torch.Tensor:
         """One token sequence -> unit-norm embedding fp32 [1, H]: a captured graph when it fits a
@@ -216,8 +228,10 @@ class BertEncoder:
                 torch.cuda.is_current_stream_capturing():
             return self.encode_packed([seq])
         if getattr(self, "_g", None) is None:
-            self._capture_small()
+            self.prepare_graphs()
         T = next(b for b in self.GRAPH_BUCKETS if b >= L)
+        if T not in self._g:
+            return self.encode_packed([seq])
         g, ids, cu, out = self._g[T]
         host = torch.zeros(T + 2, dtype=torch.int32)
         host[:L] = torch.tensor(seq, dtype=torch.int32)

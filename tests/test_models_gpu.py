@@ -195,26 +195,32 @@ def test_bge_base_width_encoder_vs_reference():
     assert torch.allclose(a.float(), b.float(), atol=3e-2)
 
 
-@pytest.mark.parametrize("arch", ["tiny-enc", "bge-base"])
-def test_encoder_one_sequence_graphs_match_eager(arch):
+@pytest.mark.parametrize("arch,dtype", [("tiny-enc", "bf16"), ("bge-base", "bf16"), ("tiny-enc", "fp16"),
+                                        ("tiny-enc", "fp8")])
+def test_encoder_one_sequence_graphs_match_eager(arch, dtype):
     """encode_one (length-bucket HIP graphs, padded rows past the real length) == the eager packed
-    path and the fp32 reference, across bucket edges, repeated replays and both pooling inputs."""
+    path (and, bf16, the fp32 reference) across bucket edges and repeated replays; the capture works
+    for every encoder dtype (the engine captures at startup)."""
     import dataclasses
     cfg = encoder_config(arch)
     if arch == "bge-base":
         cfg = dataclasses.replace(cfg, layers=2)
-    enc = BertEncoder(cfg, "cuda", seed=5)
-    ref = BertEncoder(cfg, "cuda", weights=enc.w)
-    ref.ops = reference
+    enc = BertEncoder(cfg, "cuda", seed=5, dtype=dtype)
+    enc.prepare_graphs()
+    assert set(enc._g) == set(BertEncoder.GRAPH_BUCKETS)
+    ref = None
+    if dtype == "bf16":
+        ref = BertEncoder(cfg, "cuda", weights=enc.w)
+        ref.ops = reference
     for n in (1, 2, 15, 16, 17, 31, 33, 64, 100, 128, 129, 20, 1):
         seq = [int(t) for t in np.random.default_rng(n).integers(5, cfg.vocab - 1, size=n)]
         g = enc.encode_one(seq)
         e = enc.encode_packed([seq])
-        r = ref.encode_packed([seq]).to(g.device)
         assert g.shape == e.shape == (1, cfg.hidden)
-        assert float((g.float() * e.float()).sum()) > 0.9995, n
-        assert torch.allclose(g.float(), r.float(), atol=3e-2), n
-    assert set(enc._g) == set(BertEncoder.GRAPH_BUCKETS)
+        assert float((g.float() * e.float()).sum()) > 0.999, n
+        if ref is not None:
+            r = ref.encode_packed([seq]).to(g.device)
+            assert torch.allclose(g.float(), r.float(), atol=3e-2), n
 
 
 def test_generate_batch_above_64_graph_equals_eager():
