@@ -43,6 +43,7 @@ from .dist import all_gather_rows, pack_scores_ids, unpack_scores_ids
 from .search_plane import _nullctx, merge_shard_topk
 
 _log = logging.getLogger(__name__)
+_SCAN_FAILED = -2  # id marking every entry of a shard's lists whose scan failed in a round
 
 
 class _Pending:
@@ -236,7 +237,15 @@ class CollectiveSearchPlane:
         with stream_ctx, ws_ctx:
             q = torch.from_numpy(Q).to(dev)
             qs = all_gather_rows(q, self.data_group) if W > 1 else q                       # C2
-            s, g = idx.search_ids(qs, K, thr, filters_all)
+            scan_err = None
+            try:
+                s, g = idx.search_ids(qs, K, thr, filters_all)
+            except Exception as e:  # noqa: BLE001 - this shard's scan failed: the round goes on
+                # (the collectives stay in lock-step); every id of its lists carries the failure
+                scan_err = e
+                _log.error("search shard %d: scan failed in a round: %r", self.rank, e)
+                s = torch.full((W * B, K), float("-inf"), device=qs.device)
+                g = torch.full((W * B, K), _SCAN_FAILED, dtype=torch.int64, device=qs.device)
             if W > 1:
                 P = all_gather_rows(pack_scores_ids(s, g), self.data_group)                 # C1
                 S, G = unpack_scores_ids(P)
@@ -245,8 +254,19 @@ class CollectiveSearchPlane:
                 if n == 0:  # an idle rank joins the collectives and has nothing to merge
                     return self._count(0, W * B, t0)
                 mine = slice(self.rank * B, self.rank * B + n)
+                failed = [r for r in range(W) if bool((G[r, mine] == _SCAN_FAILED).any())]
+                if failed:
+                    exc = RuntimeError(f"search shards {failed} failed their scan in this round")
+                    for p in take:
+                        _settle(p.fut, exc=exc)
+                    self.stats["failed"] += len(take)
+                    return self._count(n, W * B, t0)
                 s, g = merge_shard_topk(idx.ops, S[:, mine].contiguous(), G[:, mine].contiguous(), K)
             else:
+                if scan_err is not None:
+                    for p in take:
+                        _settle(p.fut, exc=RuntimeError(f"search shard scan failed: {scan_err!r}"))
+                    return self._count(n, W * B, t0)
                 s, g = s[:n], g[:n]
             s, g = s.float().cpu().numpy(), g.cpu().numpy()
         o = 0

@@ -117,6 +117,44 @@ def _dead_rank(rank, world, port):
     os._exit(0)  # the process group lost a member: skip its teardown
 
 
+def _scan_fail_rank(rank, world, port):
+    plane, docs, X, ids = _setup(rank, world, port)
+    try:
+        if rank == 1:  # this shard's scans raise for one round only
+            real = plane.index.search_ids
+            calls = {"n": 0}
+
+            def flaky(*a, **kw):
+                calls["n"] += 1
+                if calls["n"] == 1:
+                    raise RuntimeError("injected scan failure")
+                return real(*a, **kw)
+            plane.index.search_ids = flaky
+        dist.barrier()
+        if rank == 0:
+            q = _unit(2, D, 11)
+            with pytest.raises(RuntimeError, match="failed their scan"):
+                plane.submit(q, 3, -1.0, [docs, docs]).result(20)
+            s, g = plane.submit(q, 3, -1.0, [docs, docs]).result(20)  # the next round is whole again
+            es, eg = _exact(q[0], docs, X, ids, 3, -1.0)
+            assert np.allclose(s[0], es, atol=2e-2) and sorted(g[0].tolist()) == sorted(eg)
+        dist.barrier()
+        assert plane.health()["ok"]  # a failed scan does not end the transport
+        if rank == world - 1:
+            plane.stop()
+        else:
+            t0 = time.monotonic()
+            while plane.healthy and time.monotonic() - t0 < 10:
+                time.sleep(0.01)
+            plane.stop()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_collective_plane_failed_scan_fails_its_round_only():
+    mp.spawn(_scan_fail_rank, args=(2, _free_port()), nprocs=2, join=True)
+
+
 def test_collective_plane_exact_and_coordinated_stop():
     mp.spawn(_exact_rank, args=(3, _free_port()), nprocs=3, join=True)
 
