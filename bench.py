@@ -106,6 +106,30 @@ class ChunkTokens:
         return self.pool[o:o + n].tolist()
 
 
+def shard_vectors(rank: int, rows: int, d: int, dev) -> torch.Tensor:
+    """Rank ``rank``'s synthetic background chunks: seeded random unit vectors [rows, d] bf16
+    (bench/sharded_recall.py regenerates every shard from the same seeds)."""
+    g = torch.Generator(device=dev)
+    g.manual_seed(1000 + rank)
+    X = torch.randn((rows, d), device=dev, generator=g)
+    return torch.nn.functional.normalize(X, dim=-1).to(torch.bfloat16)
+
+
+def doc_names(world: int, ndocs: int) -> list[list[str]]:
+    """Per rank, ``ndocs`` document names that production routing (owner_of: hash(doc) % N) places
+    on that rank's shard, so the plane routes every query row to the shards that hold its documents.
+    Document j of a rank owns rows [j * chunks_per_doc, (j + 1) * chunks_per_doc) of its shard."""
+    names = [[] for _ in range(world)]
+    i = 0
+    while min(len(n) for n in names) < ndocs:
+        for r in range(world):
+            nm = f"d{r}-{i}"
+            if len(names[r]) < ndocs and owner_of(nm, world) == r:
+                names[r].append(nm)
+        i += 1
+    return names
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -164,6 +188,15 @@ def main():
                          "plane vs SEARCH_TRANSPORT=rccl lock-step rounds); 0 skips it")
     ap.add_argument("--ingest-latency-reps", type=int, default=10,
                     help="single-document ingest latency reps (upload -> summary readable, engine level)")
+    ap.add_argument("--tp70b", default="auto", choices=["auto", "on", "off"],
+                    help="N > 1: the tp_decode_70b block (BASELINE config 5's QA model, Llama-3-70B, built "
+                         "directly as TP = N shards: xGMI graph vs RCCL graph decode); auto = at N = 8")
+    ap.add_argument("--tp70b-batches", default="1,16", help="tp_decode_70b: decode batches timed")
+    ap.add_argument("--tp70b-arch", default="llama3-70b",
+                    help="tp_decode_70b's decoder (tests: a miniature of the same TP = 8 layout on CPU ranks)")
+    ap.add_argument("--multi-budget-s", type=float, default=1500.0,
+                    help="N > 1: wall budget of the multi-GPU blocks; past it every rank ends the run and rank 0 "
+                         "prints the JSON line with the blocks done so far (a hung collective cannot eat the headline)")
     a = ap.parse_args()
 
     if a.ingest_docs is None:
@@ -202,22 +235,10 @@ def main():
     d = eng.dim
 
     # ---- synthetic 100k-chunk shard in HBM ----
-    g = torch.Generator(device=dev)
-    g.manual_seed(1000 + R)
     rows = a.index_rows
-    X = torch.randn((rows, d), device=dev, generator=g)
-    X = torch.nn.functional.normalize(X, dim=-1).to(torch.bfloat16)
+    X = shard_vectors(R, rows, d, dev)
     ndocs = rows // a.chunks_per_doc
-    # document names that production routing (owner_of: hash(doc) % N) places on each rank's shard,
-    # so the plane routes every query row to the shards that really hold its documents
-    names = [[] for _ in range(W)]
-    i = 0
-    while min(len(n) for n in names) < ndocs:
-        for r in range(W):
-            nm = f"d{r}-{i}"
-            if len(names[r]) < ndocs and owner_of(nm, W) == r:
-                names[r].append(nm)
-        i += 1
+    names = doc_names(W, ndocs)
     doc_ids = names[R]
     ids = (np.int64(R) * 1_000_000_000 + np.arange(rows, dtype=np.int64))
     eng.index.add_bulk(doc_ids, [a.chunks_per_doc] * ndocs, ids, X)
@@ -443,11 +464,7 @@ def main():
             ingest(batches[0], "b", ph=ingest_phases)
             log(info, f"ingest batch phases (ms): {ingest_phases}")
 
-    # ---- the multi-GPU mechanisms, timed (N > 1; after the headline, every rank together) ----
-    # parallel/collective_bench.py: C1 + C2 as RCCL collectives (>= 20 sharded searches of B rows per
-    # rank), the decoder at TP = N (xGMI all-reduce vs torch.distributed, batch 1 and B) with the
-    # per-decision TP verdict, and the xGMI all-reduce vs RCCL per call at 16 KB / 384 KB / 6 MB.
-    # Each block reports its own error instead of the bench failing.
+    # ---- the headline's JSON (the N > 1 blocks below add to it) ----
     # physical GPUs behind the ranks (a 1-GPU rehearsal of N ranks must not read as N GPUs)
     import socket
     where = [None] * W
@@ -456,77 +473,16 @@ def main():
     else:
         where = [(socket.gethostname(), dev.index)]
     n_phys = len(set(map(tuple, where)))
-    multi: dict = {}
-    if W > 1:
-        from docagents_amd.parallel import collective_bench as CB
-        B_cur = a.batch
-
-        def block(name, fn):
-            t_b = time.perf_counter()
-            try:
-                multi[name] = fn()
-            except Exception as e:  # noqa: BLE001 - reported in the JSON line, the headline stands
-                multi[name] = {"ok": False, "error": repr(e)[:1000]}
-            multi[name]["wall_s"] = round(time.perf_counter() - t_b, 1)
-            log(info, f"{name}: {multi[name]}")
-
-        block("rccl_search", lambda: CB.rccl_search(
-            shard, search, eng.embed, lambda i: ([tg.question() for _ in range(a.batch)], make_filters(5000 + i)),
-            a.top_k, a.min_sim, a.multi_iters, ctrl, dev))
-
-        def tp_prompts(B, salt):
-            rng = np.random.default_rng(4242 + salt)  # the same prompts on every rank
-            tq = TextGen(seed=4242 + salt)
-            return [eng.answer_prompt_ids(tq.question(), [chunks.get(int(c)) for c in rng.integers(0, 1 << 30, a.top_k)],
-                                          a.max_new) for _ in range(B)]
-        if TP == 1:  # (--tp > 1: the headline itself decodes tensor-parallel)
-            # ranks sharing one GPU (a rehearsal) make every IPC all-reduce wait for the card's other
-            # contexts (~23 ms per call at 8 ranks): a few decode steps there, the full budget on a node
-            tp_new = a.max_new if n_phys == W else min(a.max_new, 6)
-            block("tp_decode", lambda: CB.tp_decode(
-                eng.dec_cfg, eng.decoder.w, R, W, dev, {1: tp_prompts(1, 1), a.batch: tp_prompts(a.batch, 2)},
-                tp_new, rccl_graphs=os.environ.get("DA_BENCH_RCCL_GRAPH") == "1", log=lambda m: log(info, m)))
-        if dev.type == "cuda":
-            from docagents_amd.parallel.xgmi_allreduce import verify_and_time
-            block("xgmi_allreduce", lambda: verify_and_time(None, dev))
-
-        # last: on ranks sharing one GPU (a rehearsal) the search streams' high-priority queues,
-        # once used, slowed every later block 2-3x (profiles/r5/rank8_gloo/serving_search_order/)
-        def serving_search():
-            """The serving transports side by side: the owner-routed plane (host TCP, the default) and
-            SEARCH_TRANSPORT=rccl (lock-step rounds of RCCL all-gathers; parallel/collective_plane.py)."""
-            import datetime
-
-            from docagents_amd.parallel.collective_plane import CollectiveSearchPlane
-            cctrl = tdist.new_group(backend="gloo", timeout=datetime.timedelta(seconds=120))
-            cdata = tdist.new_group(backend=info.backend)
-            # the plane's scan stream, not a new one: ranks sharing one GPU (a rehearsal) each add a
-            # hardware queue per stream, and oversubscribed queues are time-sliced
-            cplane = CollectiveSearchPlane(eng.index, R, W, cdata, cctrl, device=dev, stream=plane.stream,
-                                           timeout_s=120.0).start()
-            try:
-                qv = eng.embed([tg.question() for _ in range(a.serving_requests)]).float().cpu().numpy()
-                flt = []
-                while len(flt) < len(qv):
-                    flt.extend(make_filters(9000 + len(flt)))
-                reqs = [(qv[i:i + 1], flt[i]) for i in range(len(qv))]
-                res = CB.serving_search({"plane": plane, "rccl": cplane}, reqs, a.top_k, a.min_sim, ctrl, dev)
-                res["rounds"] = cplane.stats["rounds"]
-                res["rccl_transport"] = cplane.stats["transport"]
-                return res
-            finally:
-                tdist.barrier(group=ctrl)  # every rank done submitting before the rounds stop
-                cplane.stop(timeout=10.0)
-        if a.serving_requests > 0:
-            block("serving_search", serving_search)
-
-    ranks_seen = int(round(all_reduce_sum(1.0, dev)))  # every rank that reached the end of the run
-    gen = eng.gen.stats
+    is_cuda = dev.type == "cuda"
+    gen = dict(eng.gen.stats)
+    from docagents_amd.parallel import hbm_plan as HP
+    plan = HP.bench_plan(HP.BenchArgs(enc=a.enc, llm=a.llm, batch=a.batch, max_new=a.max_new, index_rows=a.index_rows,
+                                      enc_dtype=a.enc_dtype, tp=TP, overlap=overlap), W)
     out = {
         "metric": METRIC, "value": round(qps, 3), "unit": "queries/s", "n_gpus": n_phys, "world_size": W,
         "oversubscribed": n_phys < W, "steps": a.steps,
         "warmup": a.warmup, "ms_per_step": round(dt_max / a.steps * 1000, 2), "higher_is_better": True,
-        "scaling": "weak", "vs_baseline": None, "dist_backend": info.backend, "ranks_seen": ranks_seen,
+        "scaling": "weak", "vs_baseline": None, "dist_backend": info.backend, "ranks_seen": None,
         "dtype": {"bf16": "bf16", "fp16": "bf16 (fp16 encoder)", "fp8": "bf16 (fp8 e4m3 encoder GEMMs)"}[a.enc_dtype],
         "data": "synthetic (random-init weights; random unit vectors for the background chunks; synthetic questions)",
         "config": {"model": f"{a.enc} embedder + {a.llm} QA", "global_batch": DP * a.batch,
@@ -556,14 +512,146 @@ def main():
         "qa_step_phase_ms": phases or None,
         "latency_phase_ms": lat_phases or None,
         "ingest_phase_ms": ingest_phases or None,
+        # per-rank HBM: the plan (parallel/hbm_plan.py, per phase) and what the caching allocator peaked at
+        "hbm_plan_gb": HP.plan_gb(plan),
+        "hbm_peak_gb": {"headline": round(torch.cuda.max_memory_allocated(dev) / 1e9, 1)} if is_cuda else None,
     }
     out["search_plane"] = {k: (round(v, 3) if isinstance(v, float) else v) for k, v in plane.stats.items()}
+
+    # ---- the multi-GPU mechanisms, timed (N > 1; after the headline, every rank together) ----
+    # parallel/collective_bench.py: C1 + C2 as RCCL collectives (>= 20 sharded searches of B rows per
+    # rank), the decoder at TP = N (xGMI all-reduce vs torch.distributed, eager and graph-captured, batch
+    # 1 and B) with the per-decision TP verdict, Llama-3-70B at TP = 8 (BASELINE config 5's QA model),
+    # and the xGMI all-reduce vs RCCL per call at 16 KB / 384 KB / 6 MB. Each block reports its own
+    # error instead of the bench failing; a watchdog ends the run with the blocks done so far if the
+    # blocks overrun --multi-budget-s (a hung collective).
+    multi: dict = {}
+    if W > 1:
+        from docagents_amd.parallel import collective_bench as CB
+        B_cur = a.batch
+
+        def tp_prompts(B, salt):
+            rng = np.random.default_rng(4242 + salt)  # the same prompts on every rank
+            tq = TextGen(seed=4242 + salt)
+            return [eng.answer_prompt_ids(tq.question(), [chunks.get(int(c)) for c in rng.integers(0, 1 << 30, a.top_k)],
+                                          a.max_new) for _ in range(B)]
+        tp70_batches = sorted({int(x) for x in a.tp70b_batches.split(",") if x.strip()})
+        run70 = TP == 1 and (a.tp70b == "on" or (a.tp70b == "auto" and W == HP.TP70B_WORLD))
+        td_prompts = {1: tp_prompts(1, 1), a.batch: tp_prompts(a.batch, 2)} if TP == 1 else {}
+        p70 = {b: tp_prompts(b, 10 + b) for b in tp70_batches} if run70 else {}
+        # the headline's decoder KV cache (213 GB at the default size) and graphs go before the TP
+        # decoders are built: both would not fit one GPU (parallel/hbm_plan.py)
+        eng.release_decoder()
+        import threading
+        current = {"block": None}
+
+        def watchdog():
+            if done_ev.wait(a.multi_budget_s):
+                return
+            out.update(multi)
+            out["multi_timeout"] = {"block": current["block"], "budget_s": a.multi_budget_s}
+            if R == 0:
+                print(json.dumps(out), flush=True)
+            print(f"[bench] rank {R}: multi-GPU blocks overran {a.multi_budget_s:.0f} s in {current['block']}; "
+                  "ending the run", file=sys.stderr, flush=True)
+            os._exit(0)
+        done_ev = threading.Event()
+        threading.Thread(target=watchdog, daemon=True, name="bench-watchdog").start()
+
+        def block(name, fn):
+            current["block"] = name
+            if is_cuda:
+                torch.cuda.synchronize(dev)
+                torch.cuda.reset_peak_memory_stats(dev)
+                base = torch.cuda.memory_allocated(dev)
+            t_b = time.perf_counter()
+            try:
+                multi[name] = fn()
+            except Exception as e:  # noqa: BLE001 - reported in the JSON line, the headline stands
+                multi[name] = {"ok": False, "error": repr(e)[:1000]}
+            multi[name]["wall_s"] = round(time.perf_counter() - t_b, 1)
+            if is_cuda:
+                multi[name]["hbm_peak_gb"] = round(torch.cuda.max_memory_allocated(dev) / 1e9, 1)
+                multi[name]["hbm_held_before_gb"] = round(base / 1e9, 1)
+                out["hbm_peak_gb"][name] = multi[name]["hbm_peak_gb"]
+                torch.cuda.empty_cache()
+            log(info, f"{name}: {multi[name]}")
+
+        block("rccl_search", lambda: CB.rccl_search(
+            shard, search, eng.embed, lambda i: ([tg.question() for _ in range(a.batch)], make_filters(5000 + i)),
+            a.top_k, a.min_sim, a.multi_iters, ctrl, dev))
+
+        # ranks sharing one GPU (a rehearsal) make every IPC all-reduce wait for the card's other
+        # contexts (~23 ms per call at 8 ranks): a few decode steps there, the full budget on a node
+        tp_new = a.max_new if n_phys == W else min(a.max_new, 6)
+        if TP == 1:  # (--tp > 1: the headline itself decodes tensor-parallel)
+            block("tp_decode", lambda: CB.tp_decode(
+                eng.dec_cfg, eng.decoder.w, R, W, dev, td_prompts, tp_new, log=lambda m: log(info, m)))
+        if run70:
+            # BASELINE config 5's QA model on the fabric: Llama-3-70B built directly as TP = N shards
+            # (seeded per shard), the served form (xGMI all-reduce, graph-replayed) vs the fallback
+            # (RCCL all-reduce captured in the graph); gloo rehearsals: the host all-reduce, eager
+            from docagents_amd.models.configs import decoder_config
+            arms70 = ("xgmi_graph", "rccl_graph") if info.backend == "nccl" else ("xgmi_graph", f"{info.backend}_eager")
+            block("tp_decode_70b", lambda: CB.tp_decode(
+                decoder_config(a.tp70b_arch), None, R, W, dev, p70, tp_new, verdict=False, seed=a.seed + 70,
+                arms=arms70, log=lambda m: log(info, m)))
+        if is_cuda:
+            from docagents_amd.parallel.xgmi_allreduce import verify_and_time
+            block("xgmi_allreduce", lambda: verify_and_time(None, dev))
+
+        # last: on ranks sharing one GPU (a rehearsal) the search streams' high-priority queues,
+        # once used, slowed every later block 2-3x (profiles/r5/rank8_gloo/serving_search_order/)
+        def serving_search():
+            """The serving transports side by side: the owner-routed plane (host TCP, the default) and
+            SEARCH_TRANSPORT=rccl (lock-step rounds of RCCL all-gathers; parallel/collective_plane.py)."""
+            import datetime
+
+            from docagents_amd.parallel.collective_plane import CollectiveSearchPlane
+            cctrl = tdist.new_group(backend="gloo", timeout=datetime.timedelta(seconds=120))
+            cdata = tdist.new_group(backend=info.backend)
+            # the plane's scan stream, not a new one: ranks sharing one GPU (a rehearsal) each add a
+            # hardware queue per stream, and oversubscribed queues are time-sliced
+            cplane = CollectiveSearchPlane(eng.index, R, W, cdata, cctrl, device=dev, stream=plane.stream,
+                                           timeout_s=120.0).start()
+            try:
+                qv = eng.embed([tg.question() for _ in range(a.serving_requests)]).float().cpu().numpy()
+                flt = []
+                while len(flt) < len(qv):
+                    flt.extend(make_filters(9000 + len(flt)))
+                reqs = [(qv[i:i + 1], flt[i]) for i in range(len(qv))]
+                res = CB.serving_search({"plane": plane, "rccl": cplane}, reqs, a.top_k, a.min_sim, ctrl, dev)
+                res["rounds"] = cplane.stats["rounds"]
+                res["idle_gathers"] = cplane.stats.get("idle_gathers")
+                res["rccl_transport"] = cplane.stats["transport"]
+                return res
+            finally:
+                tdist.barrier(group=ctrl)  # every rank done submitting before the rounds stop
+                cplane.stop(timeout=10.0)
+        if a.serving_requests > 0:
+            block("serving_search", serving_search)
+        done_ev.set()
+
+    out["ranks_seen"] = int(round(all_reduce_sum(1.0, dev)))  # every rank that reached the end of the run
     out.update(multi)
     if R == 0:
         print(json.dumps(out), flush=True)
     barrier()
     plane.stop(timeout=2.0)
-    shutdown()
+    if W == 1:
+        shutdown()
+        return
+    # N > 1: every rank is done and past the barrier; end without the interpreter's teardown. An
+    # 8-rank run on the box aborted one rank AFTER the JSON line with "terminate called without an
+    # active exception" (a native thread destroyed joinable at exit: profiles/r6/
+    # rehearsal_config5_llama70b_tp8_fp8enc_ivf_8rank_1gpu.err.txt), which turns the launcher's
+    # status into a failure for a run whose every result is in
+    barrier()
+    if dev.type == "cuda":
+        torch.cuda.synchronize(dev)
+    sys.stdout.flush()
+    sys.stderr.flush()
+    os._exit(0)
 
 
 if __name__ == "__main__":

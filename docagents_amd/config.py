@@ -93,6 +93,9 @@ class Config:
     # all-gathers over xGMI; parallel/collective_plane.py; TP_SIZE=1 only)
     search_transport: str = field(default="plane", metadata={"env": "SEARCH_TRANSPORT"})
     search_round_idle_ms: float = field(default=2.0, metadata={"env": "SEARCH_ROUND_IDLE_MS"})
+    # an idle collective transport backs off from SEARCH_ROUND_IDLE_MS to this between control
+    # gathers (<= 1000 / this gathers per second per rank while nothing is searched)
+    search_round_idle_max_ms: float = field(default=50.0, metadata={"env": "SEARCH_ROUND_IDLE_MAX_MS"})
     # --- new keys: durable vector shards (index/wal.py) ---
     index_dir: str = field(default="", metadata={"env": "INDEX_DIR"})  # "" -> DATA_DIR/index; "none" -> off
     index_checkpoint_s: float = field(default=300.0, metadata={"env": "INDEX_CHECKPOINT_S"})

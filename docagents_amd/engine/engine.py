@@ -349,6 +349,27 @@ class Engine:
             kind, val = self.summary_step(plan, self.chat.decode_many([r.tokens for r in res]))
         return [extract_summary(t) for t in val]
 
+    def release_decoder(self) -> dict:
+        """Drop the decoder's KV cache, decode states and captured graphs (the weights stay: the
+        N > 1 bench blocks shard them). Returns the generator's final stats. After this the engine
+        can still embed and search but no longer generate. bench.py calls it before building the
+        tensor-parallel decoders of its N > 1 blocks, whose caches would not fit beside this one
+        (parallel/hbm_plan.py: 213 GB for 132 x 4096 Phi-3 slots)."""
+        if self.gen is None:
+            return {}
+        with self.lock:
+            stats = dict(self.gen.stats)
+            if getattr(self, "_sched", None) is not None:
+                self._sched = None
+            self.gen.close()
+            self.gen = None
+            if self.decoder is not None:
+                self.decoder.cache = None
+        if self.device.type == "cuda":
+            torch.cuda.synchronize(self.device)
+            torch.cuda.empty_cache()  # the xGMI buffers are hipMalloc'd outside the caching allocator
+        return stats
+
     # ------------------------------------------------------------------ introspection
     def describe(self) -> dict:
         d = {"encoder": self.enc_cfg.name, "decoder": self.dec_cfg.name, "device": str(self.device),

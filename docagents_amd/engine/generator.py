@@ -67,11 +67,15 @@ class Generator:
         self.sync_phases = False
         if self.is_cuda:
             from ..ops import kernels
-            c = model.cfg
-            nsplit = math.ceil(self.cache.max_seq / 256)
-            need = max(max_batch * model.hl * nsplit * (c.head_dim + 2) * 4,
-                       8 * max_batch * max(c.ffn * 2 // model.tp.size, c.vocab) * 4)
-            kernels.reserve_workspace(need, model.device)
+            kernels.reserve_workspace(self.workspace_bytes(model.cfg, model.hl, model.tp.size, max_batch,
+                                                           self.cache.max_seq), model.device)
+
+    @staticmethod
+    def workspace_bytes(cfg, heads_local: int, tp: int, max_batch: int, max_seq: int) -> int:
+        """The shared split-KV / split-K workspace a generator reserves (parallel/hbm_plan.py)."""
+        nsplit = math.ceil(max_seq / 256)
+        return max(max_batch * heads_local * nsplit * (cfg.head_dim + 2) * 4,
+                   8 * max_batch * max(cfg.ffn * 2 // tp, cfg.vocab) * 4)
 
     def close(self):
         """Give this generator's KV slots (the padded rows' dummy slot, a kept prompt-head slot) back

@@ -57,6 +57,9 @@ class BertEncoder:
             for L in self.w["layers"]:
                 for n in self.LINEAR:
                     L[n + "_q"], L[n + "_s"] = self.ops.quant_weight_fp8(L[n])
+        import threading
+        self._g_lock = threading.Lock()  # encode_one: the captured graphs' static buffers
+        self._g_done = None              # event: the last graph use's output copied out
 
     def _linear(self, x, L, name, bias, epi, resid=None, xq=None):
         """fp8 path: ``xq = (q, scale)`` when the producer (a LayerNorm) already emitted the
@@ -236,11 +239,23 @@ class BertEncoder:
         host = torch.zeros(T + 2, dtype=torch.int32)
         host[:L] = torch.tensor(seq, dtype=torch.int32)
         host[T + 1] = L
-        dev = h2d(host.numpy(), self.device)
-        ids.copy_(dev[:T])
-        cu.copy_(dev[T:])
-        g.replay()
-        return out.clone()
+        # The graphs' static buffers (ids / cu / out and the enc_graph workspace) are shared by every
+        # caller, and callers run on streams of their own (the fast embed lane, the GPU thread).
+        # Host order is not device order: each use waits on the device for the previous use's
+        # clone (event chain) before its copies overwrite the inputs.
+        with self._g_lock:
+            cur = torch.cuda.current_stream(self.device)
+            if self._g_done is not None:
+                cur.wait_event(self._g_done)
+            dev = h2d(host.numpy(), self.device)
+            ids.copy_(dev[:T])
+            cu.copy_(dev[T:])
+            g.replay()
+            res = out.clone()
+            if self._g_done is None:
+                self._g_done = torch.cuda.Event()
+            self._g_done.record(cur)
+        return res
 
     def flops_per_token(self, seqlen: int) -> float:
         c = self.cfg

@@ -128,29 +128,59 @@ def _round_up(x: int, m: int) -> int:
     return -(-x // m) * m
 
 
+def hbm_check(need: int, what: str, dev, margin: int = 8 << 30) -> None:
+    """Refuse an allocation of ``need`` bytes that would not fit the device's free memory (less a
+    margin for the runtime and RCCL): the block then reports a clear error instead of an OOM
+    half-way through its collectives."""
+    if torch.device(dev).type != "cuda":
+        return
+    free, total = torch.cuda.mem_get_info(dev)
+    if need + margin > free:
+        raise MemoryError(f"{what}: needs {need / 1e9:.1f} GB + {margin / 1e9:.0f} GB margin, "
+                          f"{free / 1e9:.1f} of {total / 1e9:.1f} GB free")
+
+
 def tp_decode(dec_cfg, full_weights, rank: int, world: int, dev, prompts_by_b: dict, max_new: int,
-              rccl_graphs: bool = False, verdict: bool = True, log=None) -> dict:
+              rccl_graphs: bool | None = None, verdict: bool = True, log=None, seed: int = 0,
+              arms: tuple | None = None) -> dict:
     """The decoder at TP = world over every rank, timed per decode step. prompts_by_b: {batch:
     prompts} (the same on every rank). full_weights: the unsharded weights (identical on every rank:
-    seeded). Arms: the xGMI all-reduce graph-replayed (the served form) and eager, and
-    torch.distributed in its place (eager; graph-captured too when ``rccl_graphs``)."""
+    seeded), or None to build this rank's shard directly from ``seed`` (Llama-3-70B: never the
+    140 GB unsharded model on a rank). Arms: the xGMI all-reduce graph-replayed (the served form)
+    and eager, and torch.distributed in its place, eager and graph-captured (``rccl_graph``: the
+    form serving falls back to when the xGMI probe fails, models/llama.py TPContext.all_reduce_;
+    on by default with RCCL). ``arms``: only these arm names."""
     from ..engine.generator import Generator
-    from ..models.llama import LlamaDecoder, TPContext, shard_weights
+    from ..models.llama import KVCache, LlamaDecoder, TPContext, random_weights, shard_weights
     backend = dist.get_backend()
-    tp = TPContext(rank, world, None)
-    model = LlamaDecoder(dec_cfg, dev, tp=tp, weights=shard_weights(dec_cfg, full_weights, rank, world))
+    if rccl_graphs is None:
+        rccl_graphs = backend == "nccl"
     maxB = max(prompts_by_b)
     longest = max(len(p) for ps in prompts_by_b.values() for p in ps)
     max_seq = min(dec_cfg.max_pos, _round_up(longest + max_new + 8, 256))
+    from .hbm_plan import decoder_weight_bytes
+    hbm_check(KVCache.bytes_for(dec_cfg, maxB + 4, max_seq, world)
+              + (decoder_weight_bytes(dec_cfg, world) if full_weights is None else 0),
+              f"tp_decode {dec_cfg.name} TP={world} ({maxB + 4} slots x {max_seq})", dev)
+    tp = TPContext(rank, world, None)
+    w = (random_weights(dec_cfg, dev, seed, rank, world) if full_weights is None
+         else shard_weights(dec_cfg, full_weights, rank, world))
+    model = LlamaDecoder(dec_cfg, dev, tp=tp, weights=w)
+    del w
     model.alloc_cache(maxB + 4, max_seq)
     xg = (tp.xgmi, tp.xgmi_norm)
-    arms = []
+    run = []
     if xg[0] is not None:
-        arms += [("xgmi_graph", True, True), ("xgmi_eager", True, False)]
-    arms.append((f"{'rccl' if backend == 'nccl' else backend}_eager", False, False))
+        run += [("xgmi_graph", True, True), ("xgmi_eager", True, False)]
+    run.append((f"{'rccl' if backend == 'nccl' else backend}_eager", False, False))
     if rccl_graphs and backend == "nccl":
-        arms.append(("rccl_graph", False, True))
+        run.append(("rccl_graph", False, True))
+    if arms is not None:
+        run = [r for r in run if r[0] in arms]
+    arms = run
     out: dict = {"tp": world, "model": dec_cfg.name, "max_new_tokens": max_new,
+                 "weights_gb_per_rank": round(decoder_weight_bytes(dec_cfg, world) / 1e9, 2),
+                 "kv_slots": maxB + 4, "kv_max_seq": max_seq,
                  "prompt_tokens_mean": {str(b): round(float(np.mean([len(p) for p in ps])), 1)
                                         for b, ps in prompts_by_b.items()},
                  "xgmi_mapped": xg[0] is not None, "arms": {}}

@@ -8,7 +8,10 @@ round, the query rows and the per-shard top-k lists as two RCCL all-gathers.
     round thread (one per rank, its own HIP stream and scan workspace), forever:
       take this rank's queued searches (<= max_rows rows)
       M   all_gather_object over the gloo control group: (rows, k, floor, filters, stop) per rank
-          every rank idle -> wait up to idle_s for work, next round
+          every rank idle -> wait for work, next round; the wait backs off from idle_s to
+          idle_max_s (x2 per idle round), so an idle world does <= 1 / idle_max_s control
+          gathers per second per rank, and a search that arrives wakes its own rank at once
+          (its peers join within idle_max_s)
       C2  all-gather of the zero-padded query rows              [W * B, d]       (RCCL)
           ONE fused scan + doc filter + floor + top-k of every rank's rows on the local shard
       C1  all-gather of the packed (score, id) top-k lists      [W, W * B, k, 2] (RCCL)
@@ -69,12 +72,14 @@ class CollectiveSearchPlane:
     collective rounds. Every rank of ``ctrl_group`` / ``data_group`` must construct and start one."""
 
     def __init__(self, index, rank: int = 0, world: int = 1, data_group=None, ctrl_group=None, device=None,
-                 stream=None, timeout_s: float = 30.0, max_rows: int = 1024, idle_s: float = 0.002):
+                 stream=None, timeout_s: float = 30.0, max_rows: int = 1024, idle_s: float = 0.002,
+                 idle_max_s: float = 0.05):
         self.index, self.rank, self.world = index, rank, max(1, world)
         self.data_group, self.ctrl_group = data_group, ctrl_group
         self.device = torch.device(device) if device is not None else getattr(index, "device", torch.device("cpu"))
         self.stream = stream
         self.timeout_s, self.max_rows, self.idle_s = timeout_s, max_rows, idle_s
+        self.idle_max_s = max(idle_s, idle_max_s)
         self.pending: collections.deque = collections.deque()
         self.inflight: list[_Pending] = []
         self.cv = threading.Condition()
@@ -82,8 +87,8 @@ class CollectiveSearchPlane:
         self._threads: list[threading.Thread] = []
         self.error = ""
         self.stopped_by = None
-        self.stats = {"searches": 0, "rounds": 0, "idle_rounds": 0, "rows": 0, "round_rows": 0, "busy_s": 0.0,
-                      "failed": 0, "expired": 0, "transport": "rccl" if self._nccl() else "gloo"}
+        self.stats = {"searches": 0, "rounds": 0, "idle_rounds": 0, "idle_gathers": 0, "rows": 0, "round_rows": 0,
+                      "busy_s": 0.0, "failed": 0, "expired": 0, "local_failures": 0, "transport": "rccl" if self._nccl() else "gloo"}
 
     def _nccl(self) -> bool:
         return (self.world > 1 and dist.is_initialized()
@@ -168,11 +173,12 @@ class CollectiveSearchPlane:
             if self.stream is None:
                 self.stream = torch.cuda.Stream(device=self.device, priority=-1)
         take: list[_Pending] = []
+        wait = self.idle_s
         try:
             while True:
                 with self.cv:
                     if not self.pending and not self._stop:
-                        self.cv.wait(self.idle_s)
+                        self.cv.wait(wait)
                     stopping = self._stop
                 take = [] if stopping else self._take()
                 rows = sum(p.vecs.shape[0] for p in take)
@@ -193,10 +199,16 @@ class CollectiveSearchPlane:
                     exc = RuntimeError(f"search transport stopped by rank {stop_ranks[0]}")
                     for p in take:
                         _settle(p.fut, exc=exc)
+                    # and every search still queued here (submitted during the gather, or left out
+                    # by max_rows): no round will run them
+                    self._fail_all(exc)
                     break
                 if max(m["n"] for m in metas) == 0:
                     self.stats["idle_rounds"] += 1
+                    self.stats["idle_gathers"] += 1
+                    wait = min(self.idle_max_s, wait * 2)
                     continue
+                wait = self.idle_s
                 self._round(take, metas)
                 take = []
                 with self.cv:
@@ -217,8 +229,13 @@ class CollectiveSearchPlane:
         thr = min(m["thr"] for m in live)
         n = metas[self.rank]["n"]
         Q = np.zeros((B, idx.dim), dtype=np.float32)
-        if n:
-            Q[:n] = np.concatenate([p.vecs for p in take])
+        local_err = None  # a failure of this rank's own work fails only its searches of this round:
+        # the rank still joins every collective (its peers are already in them) and the next rounds
+        try:
+            if n:
+                Q[:n] = np.concatenate([p.vecs for p in take])
+        except Exception as e:  # noqa: BLE001
+            local_err = e
         # every rank's rows in rank order, B per rank; padded rows filter on no document
         if all(m["n"] == B and m["filters"] is None for m in metas):
             filters_all = None
@@ -253,22 +270,33 @@ class CollectiveSearchPlane:
                 G = G.reshape(W, W * B, K)
                 if n == 0:  # an idle rank joins the collectives and has nothing to merge
                     return self._count(0, W * B, t0)
-                mine = slice(self.rank * B, self.rank * B + n)
-                failed = [r for r in range(W) if bool((G[r, mine] == _SCAN_FAILED).any())]
-                if failed:
-                    exc = RuntimeError(f"search shards {failed} failed their scan in this round")
-                    for p in take:
-                        _settle(p.fut, exc=exc)
-                    self.stats["failed"] += len(take)
-                    return self._count(n, W * B, t0)
-                s, g = merge_shard_topk(idx.ops, S[:, mine].contiguous(), G[:, mine].contiguous(), K)
-            else:
-                if scan_err is not None:
-                    for p in take:
-                        _settle(p.fut, exc=RuntimeError(f"search shard scan failed: {scan_err!r}"))
-                    return self._count(n, W * B, t0)
-                s, g = s[:n], g[:n]
-            s, g = s.float().cpu().numpy(), g.cpu().numpy()
+            # past the collectives: everything below is this rank's own (merge, copy back, settle)
+            try:
+                if local_err is not None:
+                    raise local_err
+                if W > 1:
+                    mine = slice(self.rank * B, self.rank * B + n)
+                    failed = [r for r in range(W) if bool((G[r, mine] == _SCAN_FAILED).any())]
+                    if failed:
+                        exc = RuntimeError(f"search shards {failed} failed their scan in this round")
+                        for p in take:
+                            _settle(p.fut, exc=exc)
+                        self.stats["failed"] += len(take)
+                        return self._count(n, W * B, t0)
+                    s, g = merge_shard_topk(idx.ops, S[:, mine].contiguous(), G[:, mine].contiguous(), K)
+                else:
+                    if scan_err is not None:
+                        for p in take:
+                            _settle(p.fut, exc=RuntimeError(f"search shard scan failed: {scan_err!r}"))
+                        return self._count(n, W * B, t0)
+                    s, g = s[:n], g[:n]
+                s, g = s.float().cpu().numpy(), g.cpu().numpy()
+            except Exception as e:  # noqa: BLE001
+                _log.error("search rank %d: local merge failed in a round: %r", self.rank, e)
+                self.stats["local_failures"] += 1
+                for p in take:
+                    _settle(p.fut, exc=RuntimeError(f"search round failed on rank {self.rank}: {e!r}"))
+                return self._count(n, W * B, t0)
         o = 0
         for p in take:
             m = p.vecs.shape[0]

@@ -128,7 +128,8 @@ def main(argv=None) -> int:
         from ..parallel.collective_plane import CollectiveSearchPlane
         plane = CollectiveSearchPlane(eng.index, rank, world, search_data, search_ctrl, device=dev, stream=lanes[2],
                                       timeout_s=max(5.0, min(60.0, cfg.engine_step_timeout)),
-                                      idle_s=cfg.search_round_idle_ms / 1000.0).start()
+                                      idle_s=cfg.search_round_idle_ms / 1000.0,
+                                      idle_max_s=cfg.search_round_idle_max_ms / 1000.0).start()
     else:
         plane = SearchPlane.start_world(eng.index, rank, world, plane_ctrl, device=dev, stream=lanes[2],
                                         host=os.environ.get("ENGINE_PLANE_HOST", "127.0.0.1"),

@@ -6,6 +6,10 @@
 #   rank2     2 ranks sharing the GPU (gloo collectives): the multi-rank bench path
 #   tp2       Phi-3-mini TP=2 + IVFFlat, 2 ranks sharing the GPU (xGMI IPC all-reduce kernel, gloo)
 #   c5        BASELINE config 5 layout: Llama-3-70B TP=8 + fp8 encoder + IVFFlat, 8 ranks sharing the GPU
+#   r2 / r8   the driver's N > 1 bench path rehearsed with 2 / 8 ranks sharing the GPU (gloo; small batch):
+#             every block (rccl_search, tp_decode, tp_decode_70b at 8, xgmi_allreduce, serving_search)
+#   c4full    BASELINE config 4 at its real total size: 8 ranks x 1.25M rows (10M), BGE-large fp16, the
+#             rccl-form sharded search in the QA step; then recall vs one exact 10M-row index
 #   index     vector index microbenchmarks (flat / IVFFlat, up to 100M x 1024 rows)
 #   xgmi      IPC all-reduce GPU tests (2 ranks sharing the GPU)
 set -u
@@ -36,6 +40,20 @@ case ${1:-c4} in
         --master-addr 127.0.0.1 --master-port 29535 bench.py --gpus 8 --llm llama3-70b --tp 8 --enc bge-large \
         --enc-dtype fp8 --index-kind ivfflat --batch 2 --steps 1 --warmup 1 --latency-reps 1 --ingest-docs 0 \
         --max-new 8 --breakdown 0 ;;  # gloo TP all-reduces through the host: a path check, not a perf number
+  r2) DA_DIST_BACKEND=gloo run r2 900 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
+        --master-addr 127.0.0.1 --master-port 29536 bench.py --gpus 2 --steps 2 --warmup 1 --batch 4 \
+        --latency-reps 2 --ingest-docs 4 --ingest-batches 1 --ingest-latency-reps 2 ;;
+  r8) DA_DIST_BACKEND=gloo run r8 1100 python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 \
+        --master-addr 127.0.0.1 --master-port 29537 bench.py --gpus 8 --steps 1 --warmup 1 --batch 4 \
+        --latency-reps 1 --ingest-docs 2 --ingest-batches 1 --ingest-latency-reps 1 --max-new 8 \
+        --tp70b-batches 1,2 --breakdown 0 ;;
+  c4full) DA_DIST_BACKEND=gloo run c4full 900 python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 \
+            --master-addr 127.0.0.1 --master-port 29538 bench.py --gpus 8 --enc bge-large --enc-dtype fp16 \
+            --index-rows 1250000 --batch 4 --steps 2 --warmup 1 --latency-reps 2 --ingest-docs 0 --max-new 8 \
+            --breakdown 0 --tp70b off --search rccl \
+          && DA_DIST_BACKEND=gloo run c4recall 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 \
+            --master-addr 127.0.0.1 --master-port 29539 bench/sharded_recall.py --rows 1250000 --dim 1024 \
+            --queries 64 ;;
   index) run index_flat 600 python bench/index_bench.py --kind flat --rows 10000000 --dim 1024 \
            && run index_ivf 900 python bench/index_bench.py --kind ivfflat --rows 10000000 --dim 1024 --lists 4096 \
               --probes 4,16,64 ;;

@@ -20,7 +20,9 @@ def test_bench_two_rank_json_schema():
            "--enc", "tiny-enc", "--llm", "tiny-dec", "--batch", "2", "--steps", "1", "--warmup", "0",
            "--latency-reps", "2", "--ingest-docs", "2", "--ingest-batches", "1", "--ingest-latency-reps", "2",
            "--index-rows", "2000", "--multi-iters", "3", "--breakdown", "0", "--max-new", "4",
-           "--ingest-words", "300", "--serving-requests", "12"]
+           "--ingest-words", "300", "--serving-requests", "12",
+           # the 70B block's code path on a miniature of its TP = 8 layout
+           "--tp70b", "on", "--tp70b-arch", "tiny-dec-tp8", "--tp70b-batches", "1,2"]
     p = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600, cwd=ROOT)
     assert p.returncode == 0, p.stderr[-2000:]
     lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
@@ -55,6 +57,17 @@ def test_bench_two_rank_json_schema():
         assert arm["b1_decode_ms_per_step"] > 0 and arm["b2_decode_ms_per_step"] > 0, td
     ag = td["agreement"]
     assert ag["ok"] and ag["checked_agree"] == ag["checked"] > 0, ag
+    # gloo has no graph-captured collective arm; every arm timed both batches
+    assert "rccl_graph" not in td["arms"] and "gloo_eager" in td["arms"], td
+    # BASELINE config 5's QA model block: built as TP = N shards (no unsharded weights), timed per batch
+    t7 = out["tp_decode_70b"]
+    assert "error" not in t7 and t7["tp"] == 2 and t7["model"] == "tiny-dec-tp8", t7
+    assert "agreement" not in t7 and list(t7["arms"]) == ["gloo_eager"], t7
+    for arm in t7["arms"].values():
+        assert arm["b1_decode_ms_per_step"] > 0 and arm["b2_decode_ms_per_step"] > 0 and arm["b2_prefill_ms"] > 0, t7
+    # per-rank HBM plan per phase (parallel/hbm_plan.py); peaks are GPU-only
+    assert set(out["hbm_plan_gb"]) == {"headline", "tp_decode"}, out["hbm_plan_gb"]
+    assert out["hbm_peak_gb"] is None and "multi_timeout" not in out
 
 
 def test_verdict_decoder_splits_every_bench_world():

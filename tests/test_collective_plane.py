@@ -151,6 +151,111 @@ def _scan_fail_rank(rank, world, port):
         dist.destroy_process_group()
 
 
+def _idle_rank(rank, world, port):
+    """An idle world backs off: <= 25 control gathers per second per rank; the first search after
+    the idle period still completes in < 100 ms (its peers join within idle_max_s = 50 ms)."""
+    plane, docs, X, ids = _setup(rank, world, port)
+    try:
+        dist.barrier()
+        time.sleep(0.3)  # past the backoff ramp (2, 4, ..., 50 ms)
+        g0, t0 = plane.stats["idle_gathers"], time.monotonic()
+        time.sleep(2.0)
+        rate = (plane.stats["idle_gathers"] - g0) / (time.monotonic() - t0)
+        assert rate <= 25, rate
+        if rank == 0:
+            t1 = time.perf_counter()
+            s, g = plane.submit(_unit(1, D, 9), 3, -1.0, [docs]).result(20)
+            ms = (time.perf_counter() - t1) * 1000
+            assert ms < 100, ms
+            es, eg = _exact(_unit(1, D, 9)[0], docs, X, ids, 3, -1.0)
+            assert sorted(g[0].tolist()) == sorted(eg)
+        dist.barrier()
+        if rank == world - 1:
+            plane.stop()
+        else:
+            t0 = time.monotonic()
+            while plane.healthy and time.monotonic() - t0 < 10:
+                time.sleep(0.01)
+            plane.stop()
+    finally:
+        dist.destroy_process_group()
+
+
+def _stop_fails_queued_rank(rank, world, port):
+    """A peer's stop fails the searches still QUEUED here (left out of the last round), at once —
+    not when their deadline passes."""
+    plane, docs, X, ids = _setup(rank, world, port)
+    try:
+        fut = None
+        if rank == 0:
+            plane._take = lambda: []  # this rank never takes its work: it stays queued
+            fut = plane.submit(_unit(1, D, 5), 3, -1.0, [docs])
+        dist.barrier()
+        if rank == world - 1:
+            time.sleep(0.2)
+            plane.stop()
+        if rank == 0:
+            t0 = time.monotonic()
+            with pytest.raises(RuntimeError, match="stopped by rank"):
+                fut.result(8)
+            assert time.monotonic() - t0 < 5  # well before the 10 s search deadline
+            plane.stop()
+        elif rank != world - 1:
+            plane.stop()
+    finally:
+        dist.destroy_process_group()
+
+
+def _local_fail_rank(rank, world, port):
+    """A failure in one rank's own post-collective work (the merge) fails that round's searches on
+    that rank only; the transport stays up and the next round is exact."""
+    from docagents_amd.parallel import collective_plane as CP
+    plane, docs, X, ids = _setup(rank, world, port)
+    try:
+        if rank == 0:
+            real = CP.merge_shard_topk
+            calls = {"n": 0}
+
+            def flaky(*a, **kw):
+                calls["n"] += 1
+                if calls["n"] == 1:
+                    raise RuntimeError("injected merge failure")
+                return real(*a, **kw)
+            CP.merge_shard_topk = flaky
+        dist.barrier()
+        if rank == 0:
+            q = _unit(1, D, 13)
+            with pytest.raises(RuntimeError, match="injected merge failure"):
+                plane.submit(q, 3, -1.0, [docs]).result(20)
+            s, g = plane.submit(q, 3, -1.0, [docs]).result(20)
+            es, eg = _exact(q[0], docs, X, ids, 3, -1.0)
+            assert sorted(g[0].tolist()) == sorted(eg)
+            assert plane.stats["local_failures"] == 1
+        dist.barrier()
+        assert plane.health()["ok"]
+        if rank == world - 1:
+            plane.stop()
+        else:
+            t0 = time.monotonic()
+            while plane.healthy and time.monotonic() - t0 < 10:
+                time.sleep(0.01)
+            plane.stop()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_collective_plane_idle_backoff_and_wake():
+    mp.spawn(_idle_rank, args=(3, _free_port()), nprocs=3, join=True)
+
+
+def test_collective_plane_peer_stop_fails_queued_searches():
+    mp.spawn(_stop_fails_queued_rank, args=(3, _free_port()), nprocs=3, join=True)
+
+
+def test_collective_plane_local_failure_fails_its_round_only():
+    mp.spawn(_local_fail_rank, args=(2, _free_port()), nprocs=2, join=True)
+
+
 def test_collective_plane_failed_scan_fails_its_round_only():
     mp.spawn(_scan_fail_rank, args=(2, _free_port()), nprocs=2, join=True)
 

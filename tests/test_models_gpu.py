@@ -223,6 +223,44 @@ def test_encoder_one_sequence_graphs_match_eager(arch, dtype):
             assert torch.allclose(g.float(), r.float(), atol=3e-2), n
 
 
+def test_encoder_one_sequence_graphs_two_streams_concurrent():
+    """Two threads on two streams (the engine's fast embed lane and its GPU thread) call encode_one at
+    once; the captured graphs share their static ids / cu / out buffers, so without device-side
+    ordering one caller's input copy lands during the other's replay. Each thread's
+    stream is first held busy (ops.spin) so the two streams' graph uses overlap on the device. Every
+    result must equal the eager path for its own sequence."""
+    import dataclasses
+    import threading
+
+    from docagents_amd.ops import kernels
+    cfg = dataclasses.replace(encoder_config("bge-base"), layers=2)
+    enc = BertEncoder(cfg, "cuda", seed=6)
+    enc.prepare_graphs()
+    rng = np.random.default_rng(11)
+    seqs = [[int(t) for t in rng.integers(5, cfg.vocab - 1, size=int(n))] for n in rng.integers(3, 120, size=64)]
+    want = [enc.encode_packed([s]).float() for s in seqs]
+    torch.cuda.synchronize()
+    got = [None] * len(seqs)
+    lock = threading.Lock()  # the engine's enc_lock: host-side enqueue order only
+
+    def worker(which):
+        st = torch.cuda.Stream()
+        with torch.cuda.stream(st):
+            for i in range(which, len(seqs), 2):
+                with lock:
+                    kernels.spin(200 if i % 4 < 2 else 0)
+                    got[i] = enc.encode_one(seqs[i])
+        st.synchronize()
+    ts = [threading.Thread(target=worker, args=(w,)) for w in (0, 1)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    torch.cuda.synchronize()
+    bad = [i for i in range(len(seqs)) if float((got[i].float() * want[i]).sum()) < 0.999]
+    assert not bad, bad
+
+
 def test_generate_batch_above_64_graph_equals_eager():
     """Decode batches above 64 rows (mid-M weight-streaming tiles with split-K inside the captured
     graph): graph replay == eager, token for token, and near-argmax under the fp32 reference."""
