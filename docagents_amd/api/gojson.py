@@ -78,7 +78,8 @@ _HTML = ("<", ">", "&", "\u2028", "\u2029")
 
 def _str(s: str) -> str:
     """C-accelerated JSON string escaping plus Go's HTML-safe escapes; lone surrogates (invalid
-    UTF-8 in Go) take the slow path, which writes U+FFFD like Go."""
+    UTF-8 in Go: text/preprocess.py truncate_preview keeps one per byte) take the slow path, which
+    writes the ``\\ufffd`` escape for each, like Go."""
     if _SURR.search(s):
         return _str_slow(s)
     out = _encode_basestring(s)
@@ -97,7 +98,7 @@ def _str_slow(s: str) -> str:
         elif ord(ch) < 0x20:
             out.append(f"\\u{ord(ch):04x}")
         elif 0xD800 <= ord(ch) <= 0xDFFF:
-            out.append("�")
+            out.append("\\ufffd")  # encoding/json: the escape, once per invalid byte
         else:
             out.append(ch)
     out.append('"')

@@ -1,4 +1,5 @@
 """Prompts, verbatim from the reference (internal/llm/openai.go:47 and :71-78, :82)."""
+from ..text.preprocess import go_fields
 
 SUMMARIZE_SYSTEM = ("You are a concise assistant. First provide a brief summary paragraph, then list the key "
                     "points as bullet points (using - or *).")
@@ -36,7 +37,7 @@ def dedup_overlap(chunk_texts: list[str], max_overlap: int) -> list[str]:
     out: list[str] = []
     prev: list[str] = []
     for i, t in enumerate(chunk_texts):
-        words = t.split()
+        words = go_fields(t)
         k = 0
         if i > 0 and max_overlap > 0:
             for n in range(min(max_overlap, len(prev), len(words)), 0, -1):

@@ -5,9 +5,11 @@
 #include <stdint.h>
 #include <string.h>
 
+// Go's unicode.IsSpace over ASCII (the only input this path takes): exactly these six. Not
+// U+001C..U+001F (Python's str.split() cuts there, strings.Fields does not); 0x85 / 0xA0 are
+// not ASCII (and as single bytes of UTF-8 text they are continuation bytes, never whitespace).
 static inline bool is_ws(unsigned char c) {
-  return c == ' ' || c == '\t' || c == '\n' || c == '\r' || c == '\v' || c == '\f' || c == 0x1c || c == 0x1d ||
-         c == 0x1e || c == 0x1f || c == 0x85 || c == 0xa0;
+  return c == ' ' || c == '\t' || c == '\n' || c == '\r' || c == '\v' || c == '\f';
 }
 
 extern "C" {

@@ -10,6 +10,8 @@ from __future__ import annotations
 
 from dataclasses import dataclass
 
+from .preprocess import go_fields
+
 
 @dataclass
 class Options:
@@ -47,9 +49,8 @@ def chunk_spans(n_words: int, max_tokens: int, overlap: int) -> list[tuple[int, 
 
 
 def fields(text: str) -> list[str]:
-    # Python's str.split() with no argument splits on Unicode whitespace runs and drops empties,
-    # matching Go's strings.Fields (unicode.IsSpace) for all practical inputs.
-    return text.split()
+    """Go's strings.Fields (unicode.IsSpace; not U+001C..U+001F, which str.split() would cut at)."""
+    return go_fields(text)
 
 
 def chunk_text(text: str, opts: Options | None = None) -> list[Chunk]:

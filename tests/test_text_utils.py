@@ -226,3 +226,41 @@ def test_engine_dtype_is_validated_not_silently_replaced():
     p = subprocess.run([sys.executable, "-m", "docagents_amd.services", "engine", "--listen", "tcp://127.0.0.1:1"],
                        env=env, capture_output=True, text=True, timeout=120)
     assert p.returncode != 0 and "DTYPE='garbage'" in (p.stderr + p.stdout), (p.returncode, p.stderr[-800:])
+
+
+def test_go_whitespace_semantics_in_chunker_and_trim():
+    """strings.Fields / TrimSpace use unicode.IsSpace, which excludes U+001C..U+001F (Python's
+    str.split() / strip() cut there): "a\\x1eb" is ONE word for the reference
+    (internal/chunker/chunker.go:30), in the Python and the native path alike."""
+    from docagents_amd.text.chunker import Options, chunk_text, chunk_text_native
+    from docagents_amd.text.preprocess import go_fields, go_trim_space
+    text = "a\x1eb c\x1fd\x1c 　e\x85f\xa0g"
+    assert go_fields(text) == ["a\x1eb", "c\x1fd\x1c", "e", "f", "g"]
+    cs = chunk_text(text, Options(2, 0))
+    assert [(c.text, c.token_count) for c in cs] == [("a\x1eb c\x1fd\x1c", 2), ("e f", 2), ("g", 1)]
+    words = " ".join(f"w{i}\x1ex{i}" for i in range(30000))  # > 64 KiB of ASCII: the native path
+    try:
+        nat = chunk_text_native(words, Options(400, 80))
+    except Exception:  # noqa: BLE001 - native library not built here: the Python path is the contract
+        nat = None
+    py = chunk_text(words, Options(400, 80))
+    assert py[0].token_count == 400 and py[0].text.split(" ")[0] == "w0\x1ex0"
+    if nat is not None:
+        assert [(c.text, c.token_count) for c in nat] == [(c.text, c.token_count) for c in py]
+    assert go_trim_space("\x1e x  ") == "\x1e x"
+    s, kp = extract_summary("\x1fSummary\x1f\n- point\x1e")
+    assert s == "\x1fSummary\x1f" and kp == ["point\x1e"]
+
+
+def test_preview_cut_inside_a_rune_matches_go_json_bytes():
+    """cmd/query/main.go:186-195 slices the preview's BYTES; encoding/json then writes one \\ufffd
+    escape per invalid byte. A cut after 2 of the 3 bytes of U+20AC gives two escapes; a cut after
+    1 byte gives one; a genuine U+FFFD in the text stays a raw rune."""
+    from docagents_amd.api.gojson import dumps_compact
+    s2 = "a" * 148 + "€" + "b" * 20
+    t2 = truncate_preview(s2, 150)
+    assert dumps_compact(t2).encode() == b'"' + b"a" * 148 + b"\\ufffd\\ufffd..." + b'"'
+    s1 = "a" * 149 + "€" + "b" * 20
+    assert dumps_compact(truncate_preview(s1, 150)).encode() == b'"' + b"a" * 149 + b"\\ufffd..." + b'"'
+    ok = "�" + "c" * 10
+    assert dumps_compact(truncate_preview(ok, 150)).encode() == b'"' + "�".encode() + b"c" * 10 + b'"'
