@@ -88,6 +88,12 @@ class Config:
     # measured no better for the query path under load (profiles/r3/stack/*switch*)
     engine_switch_interval_ms: float = field(default=0.0, metadata={"env": "ENGINE_SWITCH_INTERVAL_MS"})
     engine_admit_tokens: int = field(default=0, metadata={"env": "ENGINE_ADMIT_TOKENS"})  # 0 -> 4 prefill chunks
+    # grouped admission under load (engine/server.py _admit_ready): while >= ENGINE_ADMIT_HOLD_FRAC of
+    # the decode rows are busy, arrivals wait until ENGINE_ADMIT_MIN of them (or the free rows) are
+    # ready, or the oldest waited ENGINE_ADMIT_WAIT_MS; ENGINE_ADMIT_MIN=1 admits every arrival at once
+    engine_admit_min: int = field(default=16, metadata={"env": "ENGINE_ADMIT_MIN"})
+    engine_admit_wait_ms: float = field(default=150.0, metadata={"env": "ENGINE_ADMIT_WAIT_MS"})
+    engine_admit_hold_frac: float = field(default=0.25, metadata={"env": "ENGINE_ADMIT_HOLD_FRAC"})
     # serving search transport over the sharded index: "plane" (point to point to the owner shards,
     # failures isolated per shard; parallel/search_plane.py) or "rccl" (lock-step rounds of RCCL
     # all-gathers over xGMI; parallel/collective_plane.py; TP_SIZE=1 only)

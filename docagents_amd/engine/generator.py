@@ -490,6 +490,11 @@ class ContinuousScheduler:
     def n_active(self) -> int:
         return sum(r is not None for r in self.rows)
 
+    def steps_to_free(self) -> int:
+        """Decode steps until the first running row reaches its token budget (1 when none runs)."""
+        left = [x for x in self.left if x is not None]
+        return max(1, min(left)) if left else 1
+
     def tick(self, steps: int | None = None, stop=None) -> list:
         """Admit what fits, run up to ``steps`` decode steps, return [(tag, GenResult)] of finished
         rows. The steps are capped by the largest remaining token budget of the running rows (no

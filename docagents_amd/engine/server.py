@@ -249,7 +249,8 @@ class EngineServer:
                  hard_timeout_s: float = 0.0, liveness_s: float = 30.0, profiler: StepProfiler | None = None,
                  continuous: bool = False, cb_steps: int = 1, checkpoint_s: float = 0.0,
                  cb_window_s: float = 0.003, fast_embed_max: int = 8, urls: list[str] | None = None,
-                 cb_max_steps: int = 16, lanes=None, fast_yield: bool = False):
+                 cb_max_steps: int = 16, lanes=None, fast_yield: bool = False, admit_min: int = 16,
+                 admit_wait_s: float = 0.15, admit_hold_frac: float = 0.25):
         self.group, self.log = group, log
         self.urls = urls or []  # every replica's listen URL (topology RPC), replica order
         # the fast lane: query-sized embeds on their own thread / high-priority stream / workspace
@@ -286,7 +287,14 @@ class EngineServer:
         # decode steps per scheduler tick: cb_steps while requests wait for admission, up to
         # cb_max_steps otherwise (a one-rank replica also ends a long tick as soon as one arrives)
         self.cb_steps, self.cb_max_steps = cb_steps, max(cb_steps, cb_max_steps)
-        group.tick_stop = lambda: bool(self._cb_new) or (self.fast_yield and bool(self._fast_q or self._fast_running))
+        # grouped admission under load: while at least admit_hold_frac of the decode rows are busy,
+        # arrivals are held until admit_min of them (or as many as there are free rows) are waiting,
+        # or the oldest has waited admit_wait_s, and then prefill together. One admission per
+        # arrival (a 1-prompt prefill, a tick cut short and a reap sync each) is what made a
+        # 128-row batch lose to a 64-row one in the deploy stack (profiles/r5/rejected_r5.txt)
+        self.admit_min, self.admit_wait_s, self.admit_hold_frac = max(1, admit_min), admit_wait_s, admit_hold_frac
+        self._cb_oldest = 0.0  # arrival time of the oldest held request
+        group.tick_stop = lambda: self._admit_ready() or (self.fast_yield and bool(self._fast_q or self._fast_running))
         self.cb_window_s = cb_window_s
         self._cb_new: list = []
         self._cb_futs: dict = {}
@@ -340,6 +348,8 @@ class EngineServer:
     async def _cb_submit(self, items):
         futs = []
         loop = asyncio.get_running_loop()
+        if not self._cb_new:
+            self._cb_oldest = time.monotonic()
         for it in items:
             self._cb_tag += 1
             f = loop.create_future()
@@ -433,6 +443,24 @@ class EngineServer:
         st["busy_s"] += time.perf_counter() - t0
         return s, ids
 
+    def _admit_ready(self) -> bool:
+        """Whether the held arrivals go to the scheduler now (the grouped-admission rule above).
+        Called on the event loop and, as the tick's stop callback, on the GPU thread between decode
+        steps (plain reads of counters the GPU thread itself updates)."""
+        n = len(self._cb_new)
+        if n == 0:
+            return False
+        sched = getattr(self.group.engine, "_sched", None)
+        if self.admit_min <= 1 or sched is None:
+            return True
+        active = sched.n_active
+        if active < self.admit_hold_frac * sched.B:
+            return True  # light load: latency first
+        free = sched.B - active - len(sched.pending)
+        if free <= 0:
+            return False  # no row to seat them: the tick runs until rows free (steps_to_free)
+        return n >= min(self.admit_min, free) or time.monotonic() - self._cb_oldest >= self.admit_wait_s
+
     async def _cb_loop(self):
         """Tick the decode scheduler while it has work; new answers join at the next tick."""
         busy = False
@@ -454,9 +482,18 @@ class EngineServer:
             # the scheduler could not seat yet), long ticks otherwise; arrivals during a long tick
             # end it through group.tick_stop (checked between steps, at most 2 steps queued ahead)
             sched = getattr(self.group.engine, "scheduler", None)
-            waiting = bool(self._cb_new) or bool(getattr(sched, "pending", None))
-            steps = self.cb_steps if waiting else self.cb_max_steps
-            new, self._cb_new = self._cb_new, []
+            if self._admit_ready():
+                new, self._cb_new = self._cb_new, []
+            else:
+                new = []
+            held = bool(self._cb_new)
+            waiting = bool(new) or bool(getattr(sched, "pending", None))
+            if held or (waiting and sched is not None and sched.n_active >= sched.B):
+                # requests wait for rows (or for their group): run until the first rows free up, or
+                # until the held group is ready (tick_stop), not one step at a time
+                steps = max(self.cb_steps, min(self.cb_max_steps, sched.steps_to_free()))
+            else:
+                steps = self.cb_steps if waiting else self.cb_max_steps
             t0 = time.perf_counter()
             try:
                 done, busy = await self._gpu("cb_tick", {"items": new, "steps": steps})

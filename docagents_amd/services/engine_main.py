@@ -149,6 +149,8 @@ def main(argv=None) -> int:
                            hard_timeout_s=cfg.engine_hard_timeout, liveness_s=cfg.engine_liveness_s,
                            continuous=cfg.engine_continuous, cb_steps=cfg.engine_cb_steps,
                            cb_max_steps=cfg.engine_cb_max_steps, lanes=lanes, fast_yield=cfg.engine_fast_yield,
+                           admit_min=cfg.engine_admit_min, admit_wait_s=cfg.engine_admit_wait_ms / 1000.0,
+                           admit_hold_frac=cfg.engine_admit_hold_frac,
                            checkpoint_s=cfg.index_checkpoint_s, urls=urls)
         if cfg.engine_metrics_port:
             import prometheus_client
