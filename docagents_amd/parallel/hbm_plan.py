@@ -13,6 +13,8 @@ Every term is the allocation the code makes, by the formula it makes it with:
   prefill transient   one ``max_prefill_tokens`` chunk of activations (x, h, qkv, attention out,
                       gate/up out) — freed between chunks, counted once
   index shard         ``FlatIndex``: rows x (dim bf16 + slot int32 + id int64), x 1.5 growth slack
+  index build         ``bench.shard_vectors``: the fp32 draw and its normalised copy, then bf16
+                      (setup only: before the first prefill)
   encoder             parameters (+ a second copy for the fp8 / fp16 forms)
   xGMI communicators  2 x (2 x max_bytes staging) + signals per communicator
 Reference: the reference sizes nothing (hosted OpenAI / Postgres); docker-compose.yml:84-85,105-106
@@ -65,6 +67,10 @@ def index_bytes(rows: int, dim: int) -> int:
     return int(rows * (dim * 2 + 4 + 8) * 1.5)
 
 
+def index_build_bytes(rows: int, dim: int) -> int:
+    return rows * dim * (4 + 4 + 2)
+
+
 def xgmi_bytes(max_bytes: int = 32 << 20, norm_bytes: int = 512 << 10) -> int:
     return 2 * max_bytes + 2 * norm_bytes + (4 << 20)
 
@@ -90,6 +96,7 @@ class BenchArgs:
     tp: int = 1
     overlap: bool = False
     max_seq: int = 4096
+    tp70b: bool | None = None  # None: bench.py's "auto" (on at N = 8)
 
 
 def bench_plan(a: BenchArgs, world: int, release_engine_kv: bool = True) -> dict:
@@ -107,6 +114,9 @@ def bench_plan(a: BenchArgs, world: int, release_engine_kv: bool = True) -> dict
     }
     engine_kv = kv_bytes(dec, slots, eng_seq, tp)
     phases: dict = {}
+    setup = dict(resident)
+    setup.update({"engine_kv": engine_kv, "index_build": index_build_bytes(a.index_rows, enc.hidden)})
+    phases["setup"] = setup
     head = dict(resident)
     head.update({"engine_kv": engine_kv, "workspace": workspace_bytes(dec, a.batch, eng_seq, tp),
                  "prefill_transient": prefill_transient_bytes(dec, tp)})
@@ -125,7 +135,7 @@ def bench_plan(a: BenchArgs, world: int, release_engine_kv: bool = True) -> dict
                   "prefill_transient": prefill_transient_bytes(dec, world)})
         p["workspace"] = max(kept["workspace"], workspace_bytes(dec, a.batch, td_seq, world))
         phases["tp_decode"] = p
-    if world == TP70B_WORLD and tp == 1:
+    if tp == 1 and world > 1 and (a.tp70b if a.tp70b is not None else world == TP70B_WORLD):
         big = decoder_config("llama3-70b")
         td_seq = tp_decode_max_seq(big, eng_seq - a.max_new - 8, a.max_new)
         p = dict(kept)

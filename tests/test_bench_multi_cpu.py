@@ -66,7 +66,7 @@ def test_bench_two_rank_json_schema():
     for arm in t7["arms"].values():
         assert arm["b1_decode_ms_per_step"] > 0 and arm["b2_decode_ms_per_step"] > 0 and arm["b2_prefill_ms"] > 0, t7
     # per-rank HBM plan per phase (parallel/hbm_plan.py); peaks are GPU-only
-    assert set(out["hbm_plan_gb"]) == {"headline", "tp_decode"}, out["hbm_plan_gb"]
+    assert set(out["hbm_plan_gb"]) == {"setup", "headline", "tp_decode", "tp_decode_70b"}, out["hbm_plan_gb"]
     assert out["hbm_peak_gb"] is None and "multi_timeout" not in out
 
 

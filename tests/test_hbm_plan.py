@@ -17,7 +17,7 @@ GB = 1e9
 def test_default_bench_fits_every_world(world):
     phases = HP.bench_plan(HP.BenchArgs(), world)
     assert HP.check(phases) == [], HP.plan_gb(phases)
-    want = {"headline"} | ({"tp_decode"} if world > 1 else set()) | ({"tp_decode_70b"} if world == 8 else set())
+    want = {"setup", "headline"} | ({"tp_decode"} if world > 1 else set()) | ({"tp_decode_70b"} if world == 8 else set())
     assert set(phases) == want
 
 
@@ -53,3 +53,12 @@ def test_kv_formula_matches_allocation():
     c = KVCache(cfg, 5, 256, 2, "cpu")
     assert c.buf.numel() * c.buf.element_size() == HP.kv_bytes(cfg, 5, 256, 2)
     assert c.buf.dtype == torch.bfloat16
+
+
+def test_setup_phase_counts_the_index_build():
+    """The config-4 rehearsal's per-rank peak (34.0 GB, profiles/r6/rehearsal_config4_*) came from
+    building a 1.25M x 1024 shard (fp32 draw + normalised copy), not from the QA step."""
+    a = HP.BenchArgs(enc="bge-large", enc_dtype="fp16", batch=4, index_rows=1_250_000, max_new=8, tp70b=False)
+    p = HP.bench_plan(a, 8)
+    assert "tp_decode_70b" not in p
+    assert p["setup"]["total"] >= 34.0e9 > p["headline"]["total"]
