@@ -31,6 +31,7 @@ import socket
 import statistics
 import subprocess
 import sys
+import threading
 import time
 
 import httpx
@@ -39,6 +40,34 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 from docagents_amd.text import multipart  # noqa: E402
 from docagents_amd.text.synthetic import TextGen  # noqa: E402
+from docagents_amd.utils import timeline as req_timeline  # noqa: E402
+
+
+def _cpu_sampler(stop, out: dict, every: float = 0.5):
+    """Sample the CPU use (cores) of this process and its descendants until ``stop``; ``out`` gets
+    {"<name>#<pid>": {"mean": m, "max": x}} keyed by the service name from the command line."""
+    import psutil
+    me = psutil.Process()
+    seen: dict = {}
+    samples: dict = {}
+    while not stop.is_set():
+        for p in [me] + me.children(recursive=True):
+            try:
+                if p.pid not in seen:
+                    seen[p.pid] = p
+                    p.cpu_percent(None)  # prime
+                    continue
+                v = seen[p.pid].cpu_percent(None) / 100.0
+                cmd = p.cmdline()
+                name = next((c for c in reversed(cmd) if c in ("gateway", "query", "engine", "parser", "analysis",
+                                                              "broker", "kvcache", "all")), os.path.basename(cmd[-1]) if cmd else "?")
+                samples.setdefault(f"{name}#{p.pid}", []).append(v)
+            except (psutil.NoSuchProcess, psutil.AccessDenied, IndexError):
+                pass
+        stop.wait(every)
+    for k, xs in samples.items():
+        if xs and max(xs) > 0.05:
+            out[k] = {"mean": round(sum(xs) / len(xs), 2), "max": round(max(xs), 2)}
 
 
 def _pct(xs, q):
@@ -143,6 +172,12 @@ async def run(gw: str, docs: int, words: int, queries: int, concurrency: int, to
     texts = [tg.document(words) for _ in range(docs)]
     sem = asyncio.Semaphore(concurrency)
     limits = httpx.Limits(max_connections=concurrency * 2, max_keepalive_connections=concurrency * 2)
+    # queries: the pooled keep-alive client the gateway itself uses (api/proxy.py). At 128 in flight
+    # httpx saturated this process's core and queued requests ~1.3-2.4 s before they reached the
+    # gateway (bench/timeline_report.py: loadgen_to_gateway; a stub LLM with fixed 2 s answers
+    # showed it without any GPU), which is the harness, not the stack
+    from docagents_amd.api.proxy import PooledHTTPClient
+    qclient = PooledHTTPClient(timeout=120.0, max_idle=concurrency * 2)
     async with httpx.AsyncClient(timeout=120.0, limits=limits) as client:
         await _wait_ready(client, gw + "/healthz")
 
@@ -202,10 +237,17 @@ async def run(gw: str, docs: int, words: int, queries: int, concurrency: int, to
 
         async def ask(body):
             async with sem:
+                if req_timeline.enabled():
+                    req_timeline.mark("l_send", q=json.loads(body)["question"])
                 t = time.perf_counter()
-                r = await client.post(gw + "/api/query", content=body, headers={"content-type": "application/json"})
+                try:
+                    status, _ = await qclient.post(gw + "/api/query", body.encode(), {"Content-Type": "application/json"})
+                except Exception:  # noqa: BLE001 - counted as an error, like a failed response
+                    status = 599
                 dt = (time.perf_counter() - t) * 1000.0
-            return r.status_code, dt
+                if req_timeline.enabled():
+                    req_timeline.mark("l_recv", q=json.loads(body)["question"], status=status)
+            return status, dt
 
         # ---- unloaded cache misses: one request in flight ----
         sq = [json.dumps({"question": f"Serial question {i}: what about {tg.word()} and {tg.word()}?",
@@ -219,8 +261,14 @@ async def run(gw: str, docs: int, words: int, queries: int, concurrency: int, to
         serial_stages = _stage_delta(before, _stage_sums(mbase)) if mbase else {}
 
         t1 = time.perf_counter()
+        cpu_stop = threading.Event()
+        cpu_out: dict = {}
+        cpu_thr = threading.Thread(target=_cpu_sampler, args=(cpu_stop, cpu_out), daemon=True)
+        cpu_thr.start()
         miss = await asyncio.gather(*[ask(b) for b in bodies])
         t_miss = time.perf_counter() - t1
+        cpu_stop.set()
+        cpu_thr.join(5)
         hit = []
         for b in bodies:  # sequential: per-request latency of a cache hit, not throughput
             hit.append(await ask(b))
@@ -259,6 +307,9 @@ async def run(gw: str, docs: int, words: int, queries: int, concurrency: int, to
         "cache_hit_query_service_raw_p50_ms": _r(statistics.median(raw_q) if raw_q else None),
         "cache_hit_handler_mean_ms": _r(handler_ms),
         "concurrency": concurrency, "top_k": top_k, "ingest_timeline": timeline,
+        # CPU use of every process of the stack (and this one) while the concurrent queries ran,
+        # in cores (1.0 = one core busy): a saturated single-threaded front end shows as ~1.0
+        "cpu_cores_during_queries": cpu_out,
     }
 
 

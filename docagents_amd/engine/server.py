@@ -28,7 +28,7 @@ import numpy as np
 import torch
 
 from ..text.preprocess import extract_summary
-from ..utils import faults, metrics
+from ..utils import faults, metrics, timeline
 from .observe import StepProfiler, Watchdog, device_memory
 from ..parallel.search_plane import owner_of  # noqa: F401 - re-exported (clients route by it)
 from .rpc import pack, parse_url, read_frame
@@ -484,6 +484,8 @@ class EngineServer:
             sched = getattr(self.group.engine, "scheduler", None)
             if self._admit_ready():
                 new, self._cb_new = self._cb_new, []
+                if timeline.enabled() and new:
+                    timeline.mark("e_admit", q=[it.get("question") for _, it in new], n_active=getattr(sched, "n_active", 0))
             else:
                 new = []
             held = bool(self._cb_new)
@@ -510,6 +512,9 @@ class EngineServer:
             st["busy_s"] += time.perf_counter() - t0
             if new:
                 metrics.ENGINE_BATCH_SIZE.labels("answer_cb_admit").observe(len(new))
+            if timeline.enabled():
+                timeline.mark("e_tick", steps=steps, admitted=len(new), done=len(done), dt=time.perf_counter() - t0,
+                              n_active=getattr(sched, "n_active", 0))
             for tag, ans, conf in done:
                 f = self._cb_futs.pop(tag, None)
                 if f is not None and not f.done():
@@ -614,10 +619,16 @@ class EngineServer:
                 res = await self._enqueue("summarize", list(args["texts"]))
             return {"results": [[s, list(kp)] for s, kp in res]}
         if method == "answer":
+            if timeline.enabled():
+                for it in args["items"]:
+                    timeline.mark("e_answer_rx", q=it.get("question"))
             if self.continuous:
                 res = await self._cb_submit(list(args["items"]))
             else:
                 res = await self._enqueue("answer", list(args["items"]))
+            if timeline.enabled():
+                for it in args["items"]:
+                    timeline.mark("e_answer_tx", q=it.get("question"))
             return {"results": [[a, float(c)] for a, c in res]}
         if method == "search":
             s, ids = await self._search(args["vecs"], args["k"], args["min_sim"], args.get("filters"))

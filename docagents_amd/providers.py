@@ -9,6 +9,8 @@ internal/llm/llm.go:6-9).
 """
 from __future__ import annotations
 
+import os
+
 import asyncio
 import hashlib
 
@@ -92,6 +94,9 @@ class StubLLM:
         return extract_summary(content)
 
     async def answer(self, question: str, context: str, quality: float):
+        delay = float(os.environ.get("DA_STUB_ANSWER_S", "0") or 0)  # load tests: a model-like answer time
+        if delay > 0:
+            await asyncio.sleep(delay)
         if not context.strip():
             return "I don't have enough information to answer this question", float(quality) * 0.9
         first = context.strip().split("\n")[0][:200]

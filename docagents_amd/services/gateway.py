@@ -27,6 +27,7 @@ from ..queue.task import TASK_PARSE, Task, enqueue_with_retry
 from ..store.base import STATUS_FAILED
 from ..text import multipart
 from ..text.pdf import extract_text as pdf_text
+from ..utils import timeline
 
 ALLOWED_TYPES = {"text/plain", "application/pdf"}
 INLINE_PAYLOAD_MAX = 256 * 1024
@@ -130,6 +131,13 @@ async def query_proxy(deps, request: Request) -> Response:
     """main.go:180-207: forward the body verbatim; status + body back, Content-Type forced."""
     from ..api.proxy import PooledHTTPClient
     body = await request.body()
+    q = None
+    if timeline.enabled():
+        try:
+            q = json.loads(body).get("question")
+        except (ValueError, AttributeError):
+            pass
+        timeline.mark("g_rx", q=q)
     client = deps.extras.get("http")
     if client is None:
         client = PooledHTTPClient(timeout=60.0)
@@ -139,6 +147,8 @@ async def query_proxy(deps, request: Request) -> Response:
                                             {"Content-Type": "application/json", "X-Request-Id": request_id(request)})
     except Exception as e:  # noqa: BLE001
         return fail(deps.log, "query service unavailable", e, 503)
+    if q is not None:
+        timeline.mark("g_tx", q=q)
     return Response(content, status_code=status, media_type="application/json")
 
 

@@ -23,6 +23,7 @@ from ..cache.cache import QueryResult, Source
 from ..cache.keys import generate_cache_key
 from ..providers import EmbedError
 from ..text.preprocess import preprocess_text, truncate_preview
+from ..utils import timeline
 
 try:
     from prometheus_client import Counter, Histogram
@@ -82,6 +83,8 @@ async def query_handler(deps, body: bytes) -> Response:
     if req.top_k == 0:
         req.top_k = 5
     t0 = time.perf_counter()
+    if timeline.enabled():
+        timeline.mark("q_start", q=req.question)
     key = generate_cache_key(req.question, req.document_ids, req.top_k)
     try:
         cached = await deps.cache.get_query_result(key)
@@ -141,6 +144,8 @@ async def query_handler(deps, body: bytes) -> Response:
     context = build_context(results)
     quality = calculate_avg_similarity(results)
     t3 = time.perf_counter()
+    if timeline.enabled():
+        timeline.mark("q_answer_sent", q=req.question)
     try:
         if getattr(deps.llm, "supports_chunks", False) and hasattr(deps.store, "chunks_by_keys") and results:
             if all(getattr(r, "tokens_loaded", False) for r in results):  # read with the hits
@@ -156,12 +161,16 @@ async def query_handler(deps, body: bytes) -> Response:
     except Exception as e:  # noqa: BLE001
         return fail(log, "llm failed", e, 500)
     _obs("answer", t3)
+    if timeline.enabled():
+        timeline.mark("q_answer_rx", q=req.question)
     sources = build_sources(results)
     try:
         await deps.cache.set_query_result(key, QueryResult(answer, confidence, sources), ttl)
     except Exception as e:  # noqa: BLE001
         log.warn("failed to cache result", "err", e)
     _obs("cache_miss_total", t0)
+    if timeline.enabled():
+        timeline.mark("q_end", q=req.question)
     return write_json(200, _resp(answer, sources, confidence, False))
 
 

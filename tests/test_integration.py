@@ -147,3 +147,24 @@ def test_loadgen_against_spawned_stack(tmp_path):
     assert out["cache_hit_p50_ms"] < out["cache_miss_p99_ms"] + 1000
     # the reference's ingest number: one document at a time, upload -> summary readable
     assert out["serial_ingest_docs"] == 3 and out["serial_ingest_p50_ms"] > 0
+
+
+def test_request_timeline_report(tmp_path):
+    """DA_REQ_TIMELINE events joined by question (bench/timeline_report.py): segment means and the
+    in-flight counts per stage."""
+    sys.path.insert(0, os.path.join(ROOT, "bench"))
+    import timeline_report as TR
+    ev = []
+    for i in range(4):
+        q, b = f"q{i}", 100.0 + i * 0.1
+        ev += [{"e": "l_send", "t": b, "q": q}, {"e": "q_start", "t": b + 0.01, "q": q},
+               {"e": "q_answer_sent", "t": b + 0.02, "q": q}, {"e": "e_answer_rx", "t": b + 0.021, "q": q},
+               {"e": "e_admit", "t": b + 0.1, "q": [q]}, {"e": "e_answer_tx", "t": b + 1.0, "q": q},
+               {"e": "q_answer_rx", "t": b + 1.001, "q": q}, {"e": "q_end", "t": b + 1.002, "q": q},
+               {"e": "l_recv", "t": b + 1.01, "q": q}]
+    ev.append({"e": "e_tick", "t": 100.5, "steps": 8, "admitted": 2, "done": 0, "dt": 0.2, "n_active": 4})
+    out = TR.report(sorted(ev, key=lambda e: e["t"]))
+    assert out["gateway_in"]["n"] == 4 and abs(out["gateway_in"]["mean_ms"] - 10) < 0.1
+    assert abs(out["held"]["mean_ms"] - 79) < 0.1 and abs(out["in_engine"]["mean_ms"] - 900) < 0.1
+    assert out["ticks"]["mean_active_rows_time_weighted"] == 4.0
+    assert out["inflight_mean"]["loadgen"] > out["inflight_mean"]["engine_admitted"] > 0
