@@ -600,6 +600,9 @@ class EngineServer:
             vecs = await self._enqueue("embed" if pre else "embed_raw", texts, pre)
             return {"vecs": np.asarray(vecs, dtype=np.float32)}
         if method == "embed_search":
+            tl = timeline.enabled()
+            if tl:
+                timeline.mark("e_es_rx", t_text=args["texts"][0] if args.get("texts") else None)
             # the query path in one call (cmd/query/main.go:87-105): embed the question on the fast
             # lane, search every shard through the plane; the vector comes back for the embedding
             # cache. texts: already preprocessed (the client checked they are non-empty).
@@ -611,6 +614,8 @@ class EngineServer:
                 s, ids = await self._search(v, args["k"], args["min_sim"], args.get("filters"))
             except Exception as e:  # noqa: BLE001
                 raise RuntimeError(f"embed_search/search: {e}") from e
+            if tl:
+                timeline.mark("e_es_tx", t_text=args["texts"][0] if args.get("texts") else None)
             return {"vecs": np.asarray(v, dtype=np.float32), "scores": s, "keys": ids}
         if method == "summarize":
             if self.continuous:

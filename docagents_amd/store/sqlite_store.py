@@ -22,6 +22,7 @@ import uuid
 import numpy as np
 
 from ..utils import faults
+from ..utils import timeline
 from .base import (STATUS_PROCESSING, Chunk, Document, DocumentNotFound, Embedding, SearchResult, Summary,
                    SummaryNotFound)
 
@@ -50,7 +51,25 @@ class SqliteMeta:
         self.conn.execute("PRAGMA synchronous=NORMAL")
         self.conn.execute("PRAGMA foreign_keys=ON")
         self.lock = threading.RLock()
+        # reads (q) run on a per-thread read-only connection: WAL lets readers run beside each other
+        # and beside the writer, so the query path's chunk lookups (one per question, from the
+        # executor threads) do not queue on the writer's lock under load (a 128-request burst
+        # queued ~30 ms there). ":memory:" databases are per-connection: they keep the one connection
+        self._tl = threading.local()
+        self._readers: list = []
         self._migrate()
+
+    def _reader(self):
+        if self.path == ":memory:":
+            return None
+        c = getattr(self._tl, "conn", None)
+        if c is None:
+            c = sqlite3.connect(self.path, check_same_thread=False, timeout=30.0, isolation_level=None)
+            c.execute("PRAGMA query_only=ON")
+            self._tl.conn = c
+            with self.lock:
+                self._readers.append(c)
+        return c
 
     def _migrate(self):
         with self.lock:
@@ -65,6 +84,9 @@ class SqliteMeta:
                 raise
 
     def q(self, sql, args=()):
+        c = self._reader()
+        if c is not None:
+            return c.execute(sql, args).fetchall()
         with self.lock:
             return self.conn.execute(sql, args).fetchall()
 
@@ -74,6 +96,9 @@ class SqliteMeta:
 
     def close(self):
         with self.lock:
+            for c in self._readers:
+                c.close()
+            self._readers.clear()
             self.conn.close()
 
 
@@ -244,7 +269,11 @@ class CompositeStore:
         """Embed the (preprocessed) question AND search in ONE engine call (the question vector never
         leaves the engine between the two; cmd/query/main.go:87-105). Returns (vector, results)."""
         thr = self.min_similarity if min_similarity is None else min_similarity
+        if timeline.enabled():
+            timeline.mark("q_es_sent", t_text=text)
         vec, hits = await self.vectors.embed_search(text, list(doc_ids), k, thr)
+        if timeline.enabled():
+            timeline.mark("q_es_rx", t_text=text)
         return vec, await self._results(hits)
 
     async def _results(self, hits) -> list[SearchResult]:
