@@ -28,6 +28,14 @@ from . import prompts as P
 from .generator import Generator
 
 
+class Prompts(list):
+    """A level of a summary plan: its prompts, and the tokens to generate for each (``max_new``)."""
+
+    def __init__(self, prompts, max_new: int):
+        super().__init__(prompts)
+        self.max_new = max_new
+
+
 class Engine:
     def __init__(self, embed_arch: str = "bge-base", llm_arch: str = "phi3-mini", device="cuda", seed: int = 0,
                  tp: TPContext | None = None, max_batch: int = 64, max_seq: int = 4096, temperature: float = 0.2,
@@ -297,9 +305,19 @@ class Engine:
         nothing is truncated. ``summarize_many`` drives it with the wave generator, the engine
         server with the continuous scheduler."""
         max_new = max_new or self.summary_max_new
-        head, tail, budget = self._summary_frame(max_new)
+        head, tail, _ = self._summary_frame(max_new)
+        # reduce levels converge only if a generated summary (re-tokenized) fits half a reduce
+        # prompt's budget: with budget = max_seq - new - 8 - head - tail, that needs
+        # new <= (budget - 1) / 2, i.e. 3 * new <= max_seq - 9 - head - tail. A max_new above that
+        # (a short context, a long summary setting) generates the reduce levels with the largest
+        # budget that converges (10 % slack for re-tokenization) instead of never converging
+        fit = int(0.9 * (self.gen.cache.max_seq - 9 - len(head) - len(tail)) // 3)
+        if fit < 1:
+            raise ValueError(f"summary reduce: decoder context {self.gen.cache.max_seq} too small")
+        reduce_new = min(max_new, fit)
+        budget = self.context_budget(reduce_new) - len(head) - len(tail)
         windows, owner = self.summary_windows(texts, max_new)
-        outs = yield windows
+        outs = yield Prompts(windows, max_new)
         final: dict[int, str] = {}
         pending: dict[int, list[str]] = {}
         for (i, is_part), txt in zip(owner, outs):
@@ -318,7 +336,7 @@ class Engine:
                 for g in groups:
                     prompts.append(head + g + tail)
                     pown.append((i, len(groups) == 1))
-            outs = yield prompts
+            outs = yield Prompts(prompts, reduce_new)
             nxt: dict[int, list[str]] = {}
             for (i, last), txt in zip(pown, outs):
                 if last:
@@ -345,7 +363,7 @@ class Engine:
         kind, val = self.summary_step(plan)
         while kind == "prompts":
             with self.lock:
-                res = self.gen.generate(val, max_new)
+                res = self.gen.generate(val, getattr(val, "max_new", max_new))
             kind, val = self.summary_step(plan, self.chat.decode_many([r.tokens for r in res]))
         return [extract_summary(t) for t in val]
 

@@ -369,7 +369,7 @@ class EngineServer:
         plan = e.summary_plan(texts, e.summary_max_new)
         kind, val = await loop.run_in_executor(self.cpu, e.summary_step, plan)
         while kind == "prompts":  # map windows, then every reduce level (engine.summary_plan)
-            res = await self._cb_submit([{"ids": p, "max_new": e.summary_max_new} for p in val])
+            res = await self._cb_submit([{"ids": p, "max_new": getattr(val, "max_new", e.summary_max_new)} for p in val])
             kind, val = await loop.run_in_executor(self.cpu, e.summary_step, plan, [t for t, _ in res])
         metrics.ENGINE_ITEMS.labels("summarize").inc(len(texts))
         return [extract_summary(t) for t in val]

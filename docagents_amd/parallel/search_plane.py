@@ -184,14 +184,17 @@ class _Peer:
         self.down_since, self.error = None, ""
         threading.Thread(target=self._read_loop, args=(s,), name=f"plane-peer-{self.rank}", daemon=True).start()
 
-    def send(self, rid: int, msg: dict, on_reply, on_fail):
-        """Queue one request frame (never blocks: a full backlog fails the part at once)."""
+    def send(self, rid: int, msg: dict, on_reply, on_fail, deadline: float | None = None):
+        """Queue one request frame (never blocks: a full backlog fails the part at once).
+        ``deadline`` (monotonic s): the search's own; a frame still queued past it is dropped, and
+        the frame carries what is left of it as its ``ttl`` (the shard then expires the part on time
+        however long it waited in this backlog)."""
         with self.lock:
             if self.writer is None:
                 self.writer = threading.Thread(target=self._write_loop, name=f"plane-send-{self.rank}", daemon=True)
                 self.writer.start()
         try:
-            self.q.put_nowait((rid, msg, on_reply, on_fail))
+            self.q.put_nowait((rid, msg, on_reply, on_fail, deadline))
         except queue.Full:
             on_fail(ShardUnavailable(f"search shard {self.rank}: {_SEND_BACKLOG} requests already queued"))
 
@@ -201,10 +204,17 @@ class _Peer:
                 item = self.q.get(timeout=0.5)
             except queue.Empty:
                 continue
-            rid, msg, on_reply, on_fail = item
+            rid, msg, on_reply, on_fail, deadline = item
             if self.plane._stop:
                 on_fail(RuntimeError("search plane stopped"))
                 continue
+            if deadline is not None:
+                left = deadline - time.monotonic()
+                if left <= 0:
+                    self.plane.stats["expired"] += 1
+                    on_fail(TimeoutError(f"search part for shard {self.rank} expired in the send backlog"))
+                    continue
+                msg["ttl"] = left
             sock = None
             try:
                 with self.lock:
@@ -437,7 +447,7 @@ class SearchPlane:
             else:
                 self.stats["remote_parts"] += 1
                 self.peers[r].send(sid, {"id": sid, "vecs": sub, "k": k, "thr": thr, "filters": flt,
-                                         "ttl": self.timeout_s}, reply, fail)
+                                         "ttl": self.timeout_s}, reply, fail, deadline=srch.deadline)
         return fut
 
     def _part_done(self, sid: int, rank: int, part, exc):

@@ -79,6 +79,28 @@ def test_summarize_reduce_is_recursive_and_never_truncates():
     assert len(calls[-1][0]) == 1  # the last level is one prompt: the final summary
 
 
+def test_summarize_reduce_converges_with_a_large_max_new():
+    """with max_new above ~max_seq / 3 a generated summary no longer fits half a reduce
+    prompt, and each level used to yield as many prompts as the last until the 64-level guard. The
+    reduce levels now generate with the largest budget that converges; the map windows keep max_new."""
+    from docagents_amd.text.synthetic import TextGen
+    e = Engine("tiny-enc", "tiny-dec", "cpu", max_batch=16, max_seq=512, max_new_tokens=4, summary_max_new=300,
+               temperature=0.0, use_graphs=False)
+    doc = TextGen(seed=5).document(3000)
+    news = []
+    orig = e.gen.generate
+
+    def spy(prompts, max_new):
+        news.append((len(prompts), max_new))
+        assert all(len(p) + max_new <= 512 for p in prompts)
+        return orig(prompts, max_new)
+    e.gen.generate = spy
+    (summary, _), = e.summarize_many([doc])
+    assert news[0][1] == 300 and len(news) >= 2, news   # map windows at max_new, then reduce levels
+    assert all(n < 300 for _, n in news[1:]) and news[-1][0] == 1, news
+    assert e.stats["summary_reduce_levels_max"] < 64
+
+
 def _unit(n, d, seed=0):
     x = np.random.default_rng(seed).standard_normal((n, d)).astype(np.float32)
     return torch.from_numpy(x / np.linalg.norm(x, axis=1, keepdims=True))

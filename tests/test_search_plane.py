@@ -227,3 +227,41 @@ def test_shard_refuses_parts_past_its_queue_cap_and_drops_expired_ones(monkeypat
     take = plane._take()  # the expired part is dropped (failed), the live one is scanned
     assert len(take) == 1 and plane.stats["expired"] == 1 and "expired" in got[-1]
     assert plane._queued_rows == 0
+
+
+def test_send_backlog_honours_the_search_deadline():
+    """a frame that waited in a peer's send backlog past its search's deadline is dropped
+    there (never scanned for a requester that gave up), and a frame that is sent carries what is
+    LEFT of the deadline as its ttl, not the full timeout."""
+    import threading
+    import time
+    from types import SimpleNamespace
+
+    from docagents_amd.parallel.search_plane import _Peer
+    plane = SimpleNamespace(_stop=False, stats={"expired": 0}, retry_s=5.0, connect_timeout_s=0.2, send_timeout_s=0.2)
+    srv = socket.socket()
+    srv.bind(("127.0.0.1", 0))
+    srv.listen(1)
+    got = {}
+    done = threading.Event()
+
+    def accept():
+        c, _ = srv.accept()
+        got["conn"] = c
+        done.set()
+    threading.Thread(target=accept, daemon=True).start()
+    peer = _Peer(plane, 1, srv.getsockname())
+    fails = []
+    peer.send(1, {"id": 1}, lambda *a: None, fails.append, deadline=time.monotonic() - 0.01)
+    msg = {"id": 2, "ttl": 30.0}
+    peer.send(2, msg, lambda *a: None, fails.append, deadline=time.monotonic() + 10.0)
+    assert done.wait(5)
+    t0 = time.monotonic()
+    while "ttl" in msg and msg["ttl"] == 30.0 and time.monotonic() - t0 < 5:
+        time.sleep(0.01)
+    assert len(fails) == 1 and isinstance(fails[0], TimeoutError), fails
+    assert plane.stats["expired"] == 1
+    assert 9.0 < msg["ttl"] <= 10.0  # the remaining time, not the full 30 s
+    plane._stop = True
+    got["conn"].close()
+    srv.close()
