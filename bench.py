@@ -194,8 +194,8 @@ def main():
     ap.add_argument("--tp70b-batches", default="1,16", help="tp_decode_70b: decode batches timed")
     ap.add_argument("--tp70b-arch", default="llama3-70b",
                     help="tp_decode_70b's decoder (tests: a miniature of the same TP = 8 layout on CPU ranks)")
-    ap.add_argument("--multi-budget-s", type=float, default=1500.0,
-                    help="N > 1: wall budget of the multi-GPU blocks; past it every rank ends the run and rank 0 "
+    ap.add_argument("--block-budget-s", type=float, default=360.0,
+                    help="N > 1: wall budget of each multi-GPU block; past it every rank ends the run and rank 0 "
                          "prints the JSON line with the blocks done so far (a hung collective cannot eat the headline)")
     a = ap.parse_args()
 
@@ -524,8 +524,9 @@ def main():
     # rank), the decoder at TP = N (xGMI all-reduce vs torch.distributed, eager and graph-captured, batch
     # 1 and B) with the per-decision TP verdict, Llama-3-70B at TP = 8 (BASELINE config 5's QA model),
     # and the xGMI all-reduce vs RCCL per call at 16 KB / 384 KB / 6 MB. Each block reports its own
-    # error instead of the bench failing; a watchdog ends the run with the blocks done so far if the
-    # blocks overrun --multi-budget-s (a hung collective).
+    # error instead of the bench failing; a watchdog ends the run with the blocks done so far if a
+    # block overruns --block-budget-s (a hung collective). The graph-captured RCCL arms (the served
+    # TP fallback) run last, in blocks of their own: the one form that has never run on a node.
     multi: dict = {}
     if W > 1:
         from docagents_amd.parallel import collective_bench as CB
@@ -544,28 +545,32 @@ def main():
         # decoders are built: both would not fit one GPU (parallel/hbm_plan.py)
         eng.release_decoder()
         import threading
-        current = {"block": None}
+        current = {"block": None, "t0": time.monotonic()}
 
         def watchdog():
-            if done_ev.wait(a.multi_budget_s):
-                return
-            out.update(multi)
-            out["multi_timeout"] = {"block": current["block"], "budget_s": a.multi_budget_s}
-            if R == 0:
-                print(json.dumps(out), flush=True)
-            print(f"[bench] rank {R}: multi-GPU blocks overran {a.multi_budget_s:.0f} s in {current['block']}; "
-                  "ending the run", file=sys.stderr, flush=True)
-            os._exit(0)
+            while not done_ev.wait(1.0):
+                if time.monotonic() - current["t0"] <= a.block_budget_s:
+                    continue
+                out.update(multi)
+                out["multi_timeout"] = {"block": current["block"], "budget_s": a.block_budget_s}
+                if R == 0:
+                    print(json.dumps(out), flush=True)
+                print(f"[bench] rank {R}: block {current['block']} overran {a.block_budget_s:.0f} s; ending the run",
+                      file=sys.stderr, flush=True)
+                os._exit(0)
         done_ev = threading.Event()
         threading.Thread(target=watchdog, daemon=True, name="bench-watchdog").start()
 
         def block(name, fn):
-            current["block"] = name
+            current["block"], current["t0"] = name, time.monotonic()
             if is_cuda:
                 torch.cuda.synchronize(dev)
                 torch.cuda.reset_peak_memory_stats(dev)
                 base = torch.cuda.memory_allocated(dev)
             t_b = time.perf_counter()
+            hang = os.environ.get("DA_BENCH_HANG_BLOCK", "")  # tests: a block that never returns
+            if hang == name:
+                time.sleep(3600)
             try:
                 multi[name] = fn()
             except Exception as e:  # noqa: BLE001 - reported in the JSON line, the headline stands
@@ -587,13 +592,15 @@ def main():
         tp_new = a.max_new if n_phys == W else min(a.max_new, 6)
         if TP == 1:  # (--tp > 1: the headline itself decodes tensor-parallel)
             block("tp_decode", lambda: CB.tp_decode(
-                eng.dec_cfg, eng.decoder.w, R, W, dev, td_prompts, tp_new, log=lambda m: log(info, m)))
+                eng.dec_cfg, eng.decoder.w, R, W, dev, td_prompts, tp_new, rccl_graphs=False,
+                log=lambda m: log(info, m)))
         if run70:
             # BASELINE config 5's QA model on the fabric: Llama-3-70B built directly as TP = N shards
-            # (seeded per shard), the served form (xGMI all-reduce, graph-replayed) vs the fallback
-            # (RCCL all-reduce captured in the graph); gloo rehearsals: the host all-reduce, eager
+            # (seeded per shard), the served form (xGMI all-reduce, graph-replayed) vs the collective
+            # library eager; the graph-captured RCCL fallback in the last block
             from docagents_amd.models.configs import decoder_config
-            arms70 = ("xgmi_graph", "rccl_graph") if info.backend == "nccl" else ("xgmi_graph", f"{info.backend}_eager")
+            coll = "rccl" if info.backend == "nccl" else info.backend
+            arms70 = ("xgmi_graph", f"{coll}_eager")
             block("tp_decode_70b", lambda: CB.tp_decode(
                 decoder_config(a.tp70b_arch), None, R, W, dev, p70, tp_new, verdict=False, seed=a.seed + 70,
                 arms=arms70, log=lambda m: log(info, m)))
@@ -631,6 +638,16 @@ def main():
                 cplane.stop(timeout=10.0)
         if a.serving_requests > 0:
             block("serving_search", serving_search)
+        if info.backend == "nccl" and TP == 1:
+            # the served TP fallback when the xGMI probe fails (models/llama.py TPContext.all_reduce_:
+            # torch.distributed captured in the decode graph), Phi-3 and, at N = 8, Llama-3-70B
+            block("tp_decode_rccl_graph", lambda: CB.tp_decode(
+                eng.dec_cfg, eng.decoder.w, R, W, dev, td_prompts, tp_new, rccl_graphs=True, verdict=False,
+                arms=("rccl_graph",), log=lambda m: log(info, m)))
+            if run70:
+                block("tp_decode_70b_rccl_graph", lambda: CB.tp_decode(
+                    decoder_config(a.tp70b_arch), None, R, W, dev, p70, tp_new, rccl_graphs=True, verdict=False,
+                    seed=a.seed + 70, arms=("rccl_graph",), log=lambda m: log(info, m)))
         done_ev.set()
 
     out["ranks_seen"] = int(round(all_reduce_sum(1.0, dev)))  # every rank that reached the end of the run

@@ -80,3 +80,22 @@ def test_verdict_decoder_splits_every_bench_world():
         c = decoder_config(verdict_arch(w))
         assert c.heads % w == 0 and c.kv_heads % w == 0 and c.ffn % (16 * w) == 0 and c.vocab % w == 0
         assert c.hidden // c.heads in (64, 96, 128)  # a head dim the GPU decode-attention kernels take
+
+
+def test_bench_watchdog_ends_a_hung_block_with_the_json_line():
+    """A multi-GPU block that never returns (a hung collective) must not cost the run its headline:
+    past --block-budget-s every rank ends, rank 0 having printed the one JSON line with the blocks
+    done so far and the block that hung; the launcher's status stays 0."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(OMP_NUM_THREADS="2", DA_BENCH_HANG_BLOCK="tp_decode")
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--cpu-rehearsal",
+           "--enc", "tiny-enc", "--llm", "tiny-dec", "--batch", "2", "--steps", "1", "--warmup", "0",
+           "--latency-reps", "1", "--ingest-docs", "0", "--index-rows", "2000", "--multi-iters", "2",
+           "--breakdown", "0", "--max-new", "4", "--serving-requests", "4", "--block-budget-s", "3"]
+    p = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600, cwd=ROOT)
+    assert p.returncode == 0, p.stderr[-2000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout[-2000:]
+    out = json.loads(lines[0])
+    assert out["value"] > 0 and out["multi_timeout"]["block"] == "tp_decode", out.get("multi_timeout")
+    assert "rccl_search" in out and "serving_search" not in out
