@@ -45,7 +45,7 @@ def local_engine(cfg: Config):
         from .engine.engine import Engine
         dev = "cuda" if torch.cuda.is_available() else "cpu"
         _ENGINES[key] = Engine(cfg.embed_arch, cfg.llm_arch, dev, seed=cfg.seed, max_batch=cfg.max_batch,
-                               temperature=cfg.temperature, max_new_tokens=cfg.max_new_tokens,
+                               kv_cache_gb=cfg.kv_cache_gb, temperature=cfg.temperature, max_new_tokens=cfg.max_new_tokens,
                                summary_max_new=cfg.summary_max_new_tokens, index_kind=cfg.index_kind,
                                ivf_lists=cfg.ivf_lists, ivf_probes=cfg.ivf_probes,
                                enc_dtype="fp8" if cfg.dtype == "fp8" else "bf16",

@@ -64,7 +64,10 @@ class Config:
     temperature: float = field(default=0.2, metadata={"env": "LLM_TEMPERATURE"})
     weights_path: str = field(default="", metadata={"env": "WEIGHTS_PATH"})
     seed: int = field(default=0, metadata={"env": "SEED"})
-    max_batch: int = field(default=64, metadata={"env": "ENGINE_MAX_BATCH"})
+    # decode rows of an engine replica; 0 = auto: the largest power of two <= 128 whose KV cache fits
+    # KV_CACHE_GB (0: the free HBM after the weights less 48 GB). Deploy stack, 128 in flight:
+    # 128 rows 40.6 q/s vs 64 rows 38.3 (profiles/r6/stack)
+    max_batch: int = field(default=0, metadata={"env": "ENGINE_MAX_BATCH"})
     kv_cache_gb: float = field(default=0.0, metadata={"env": "KV_CACHE_GB"})  # 0 -> auto
     fault_spec: str = field(default="", metadata={"env": "DA_FAULT"})
     # --- new keys: engine supervision / observability ---

@@ -42,7 +42,7 @@ class Engine:
                  max_new_tokens: int = 64, summary_max_new: int = 128, index_kind: str = "flat",
                  ivf_lists: int = 100, ivf_probes: int = 1, load_llm: bool = True, load_encoder: bool = True,
                  use_graphs: bool = True, embed_max_tokens: int = 65536, enc_dtype: str = "bf16",
-                 share_prefix: bool = True, overlap_waves: bool = False):
+                 share_prefix: bool = True, overlap_waves: bool = False, kv_cache_gb: float = 0.0):
         self.device = torch.device(device)
         self.lock = threading.RLock()      # the decoder / generator (one GPU thread drives it)
         self.enc_lock = threading.RLock()  # the encoder: the fast embed lane and the batcher share it
@@ -65,6 +65,8 @@ class Engine:
         self.gen = None
         if load_llm:
             self.decoder = LlamaDecoder(self.dec_cfg, self.device, seed=seed, tp=tp)
+            if max_batch <= 0:
+                max_batch = self.auto_batch(max_seq, overlap_waves, kv_gb=kv_cache_gb)
             # + 1 dummy slot (padded graph rows) + 2 prompt-head slots (ContinuousScheduler heads)
             # + 1 for the wave path's kept prompt head (Generator.head); overlap_waves: a second
             # wave's rows (answer_overlapped keeps two waves in flight)
@@ -77,6 +79,28 @@ class Engine:
         self._prefix_cache: dict[str, list[int]] = {}
         self.stats = {"embed_texts": 0, "embed_tokens": 0, "embed_s": 0.0, "embed_truncated_texts": 0,
                       "embed_truncated_tokens": 0}
+
+    AUTO_BATCH_MAX = 128            # decode rows: the deploy stack's measured best (profiles/r6/stack)
+    AUTO_RESERVE_BYTES = 48 << 30  # HBM left beside the KV cache: index growth, activations, graphs
+
+    def auto_batch(self, max_seq: int, overlap: bool = False, kv_gb: float = 0.0) -> int:
+        """``max_batch=0``: the largest power-of-two decode batch (<= AUTO_BATCH_MAX) whose KV cache
+        (batch + 4 slots x max_seq, this rank's kv heads) fits ``kv_gb`` GB, or the device's free
+        HBM after the weights less AUTO_RESERVE_BYTES. Phi-3-mini on an MI355X: 128 (213 GB of
+        KV); Llama-3-70B on one GPU: 16. CPU: 64."""
+        from ..models.llama import KVCache
+        if self.device.type != "cuda" and kv_gb <= 0:
+            return 64
+        per = KVCache.bytes_for(self.dec_cfg, 1, min(max_seq, self.dec_cfg.max_pos), self.decoder.tp.size)
+        if kv_gb > 0:
+            budget = int(kv_gb * 1e9)
+        else:
+            free, _ = torch.cuda.mem_get_info(self.device)
+            budget = free - self.AUTO_RESERVE_BYTES
+        b = self.AUTO_BATCH_MAX
+        while b > 1 and ((2 if overlap else 1) * b + 4) * per > budget:
+            b //= 2
+        return b
 
     @property
     def dim(self) -> int:

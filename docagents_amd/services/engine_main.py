@@ -104,6 +104,7 @@ def main(argv=None) -> int:
         lanes = serving_lanes(cfg.engine_latency_cus, dev)
         log.info("cu partition", "latency_cus", cfg.engine_latency_cus)
     eng = Engine(cfg.embed_arch, cfg.llm_arch, dev, seed=cfg.seed, tp=tp, max_batch=cfg.max_batch,
+                 kv_cache_gb=cfg.kv_cache_gb,
                  temperature=cfg.temperature, max_new_tokens=cfg.max_new_tokens,
                  summary_max_new=cfg.summary_max_new_tokens, index_kind=cfg.index_kind, ivf_lists=cfg.ivf_lists,
                  ivf_probes=cfg.ivf_probes, max_seq=4096 if dev.type == "cuda" else 1024,
@@ -145,7 +146,7 @@ def main(argv=None) -> int:
     urls = [replica_url(a.listen, r) for r in range(replicas)]
 
     async def serve():
-        srv = EngineServer(grp, log, max_batch_items=cfg.max_batch * 4, step_timeout_s=cfg.engine_step_timeout,
+        srv = EngineServer(grp, log, max_batch_items=max(1, eng.gen.max_batch if eng.gen is not None else 64) * 4, step_timeout_s=cfg.engine_step_timeout,
                            hard_timeout_s=cfg.engine_hard_timeout, liveness_s=cfg.engine_liveness_s,
                            continuous=cfg.engine_continuous, cb_steps=cfg.engine_cb_steps,
                            cb_max_steps=cfg.engine_cb_max_steps, lanes=lanes, fast_yield=cfg.engine_fast_yield,

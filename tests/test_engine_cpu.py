@@ -688,3 +688,21 @@ def test_scheduler_steps_to_free():
     assert sch.steps_to_free() == 1  # "b": budget 3, one token at prefill, one step run
     while sch.busy():
         sch.tick()
+
+
+def test_auto_decode_batch_from_the_kv_budget():
+    """ENGINE_MAX_BATCH=0 (the default): the largest power-of-two batch <= 128 whose KV cache
+    (batch + 4 slots) fits KV_CACHE_GB, 64 on a CPU without a budget."""
+    from docagents_amd.models.configs import decoder_config
+    from docagents_amd.models.llama import KVCache
+    e = Engine("tiny-enc", "tiny-dec", "cpu", max_batch=0, max_seq=256, max_new_tokens=4, use_graphs=False)
+    assert e.gen.max_batch == 64
+    per = KVCache.bytes_for(decoder_config("tiny-dec"), 1, 256)
+    assert e.auto_batch(256, kv_gb=(36 * per) / 1e9) == 32          # 32 + 4 slots fit, 64 + 4 do not
+    assert e.auto_batch(256, kv_gb=1e6) == Engine.AUTO_BATCH_MAX
+    # MI355X: Phi-3-mini (7.6 GB of weights) leaves ~280 GB free -> 128 rows = 213 GB of KV within
+    # 280 GB less the reserve; Llama-3-70B TP=1 (141 GB of weights) leaves room for 64 rows only
+    free_phi, free_70b = 280e9, 288e9 - 141e9
+    assert KVCache.bytes_for(decoder_config("phi3-mini"), 132, 4096) <= free_phi - Engine.AUTO_RESERVE_BYTES
+    per70 = KVCache.bytes_for(decoder_config("llama3-70b"), 1, 4096)
+    assert 68 * per70 <= free_70b - Engine.AUTO_RESERVE_BYTES < 132 * per70
