@@ -14,6 +14,7 @@ Providers:
 from __future__ import annotations
 
 import asyncio
+import collections
 import json
 import time
 from dataclasses import dataclass, field
@@ -133,17 +134,24 @@ def _resp_cmd(*parts) -> bytes:
 
 
 class KVCache:
-    """Minimal asyncio RESP client (GET/SET EX/DEL/SCAN/PING/AUTH)."""
+    """Minimal asyncio RESP client (GET/SET EX/DEL/SCAN/PING/AUTH), pipelined: a command is written
+    as soon as it is issued and its reply matched in FIFO order by one reader task (RESP answers in
+    request order), so concurrent requests share the connection without waiting for each other's
+    round trips — the reference's go-redis pools connections for the same reason. A command that
+    times out keeps its place in the FIFO (its late reply is read and dropped)."""
 
     def __init__(self, addr: str = "localhost:6379", password: str = "", timeout: float = 5.0):
         host, _, port = addr.rpartition(":")
         self.host, self.port = host or "localhost", int(port or 6379)
         self.password, self.timeout = password, timeout
         self.reader = self.writer = None
-        self.lock = asyncio.Lock()
+        self.lock = asyncio.Lock()  # write order == FIFO order
+        self._fifo: collections.deque = collections.deque()
+        self._reader_task = None
 
     async def connect(self):
         self.reader, self.writer = await asyncio.wait_for(asyncio.open_connection(self.host, self.port), self.timeout)
+        self._reader_task = asyncio.ensure_future(self._read_loop(self.reader))
         if self.password:
             await self._cmd("AUTH", self.password)
         r = await self._cmd("PING")
@@ -151,35 +159,60 @@ class KVCache:
             raise RespError(f"unexpected PING reply {r!r}")
         return self
 
-    async def _read(self):
-        line = await self.reader.readline()
+    async def _read(self, reader):
+        line = await reader.readline()
         if not line:
             raise ConnectionError("kv connection closed")
         t, rest = line[:1], line[1:-2]
         if t == b"+":
             return rest
         if t == b"-":
-            raise RespError(rest.decode())
+            return RespError(rest.decode())  # this command's error, not the connection's
         if t == b":":
             return int(rest)
         if t == b"$":
             n = int(rest)
             if n < 0:
                 return None
-            data = await self.reader.readexactly(n + 2)
+            data = await reader.readexactly(n + 2)
             return data[:-2]
         if t == b"*":
             n = int(rest)
-            return None if n < 0 else [await self._read() for _ in range(n)]
-        raise RespError(f"bad RESP type {t!r}")
+            return None if n < 0 else [await self._read(reader) for _ in range(n)]
+        raise ConnectionError(f"bad RESP type {t!r}")
+
+    async def _read_loop(self, reader):
+        try:
+            while True:
+                v = await self._read(reader)
+                fut = self._fifo.popleft() if self._fifo else None
+                if fut is None or fut.done():
+                    continue  # timed out / cancelled: its reply is dropped, the order kept
+                if isinstance(v, RespError):
+                    fut.set_exception(v)
+                else:
+                    fut.set_result(v)
+        except (ConnectionError, asyncio.IncompleteReadError, OSError, ValueError) as e:
+            err = e if isinstance(e, ConnectionError) else ConnectionError(f"kv connection lost: {e!r}")
+            w, self.writer = self.writer, None
+            if w is not None:
+                w.close()
+            while self._fifo:
+                f = self._fifo.popleft()
+                if not f.done():
+                    f.set_exception(err)
 
     async def _cmd(self, *parts):
+        fut = asyncio.get_running_loop().create_future()
         async with self.lock:
             if self.writer is None:
                 raise ConnectionError("not connected")
+            self._fifo.append(fut)
             self.writer.write(_resp_cmd(*parts))
-            await self.writer.drain()
-            return await asyncio.wait_for(self._read(), self.timeout)
+        w = self.writer
+        if w is not None:
+            await w.drain()
+        return await asyncio.wait_for(fut, self.timeout)
 
     async def get_query_result(self, key: str):
         faults.maybe_fail("cache.get")
@@ -212,6 +245,9 @@ class KVCache:
             await self._cmd("DEL", *keys)
 
     async def close(self):
+        if self._reader_task is not None:
+            self._reader_task.cancel()
+            self._reader_task = None
         if self.writer is not None:
             self.writer.close()
             try:

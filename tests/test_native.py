@@ -172,3 +172,22 @@ def test_kernel_debug_build_compiles(tmp_path):
     r = subprocess.run([hipcc, *B._flags(True), "-c", str(src), "-o", str(tmp_path / "dbg.o")],
                        capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stderr[-2000:]
+
+
+def test_kvserver_client_pipelines_concurrent_commands(kvserver):
+    """The RESP client pipelines: 300 concurrent SET / GET from one connection (replies matched in
+    FIFO order), an error reply fails only its own command, and a closed server fails every
+    pending command instead of hanging it."""
+    async def go():
+        c = await KVCache(kvserver, "pw").connect()
+
+        async def one(i):
+            await c._cmd("SET", f"pk{i}", f"v{i}", "EX", 100)
+            return await c._cmd("GET", f"pk{i}")
+        got = await asyncio.gather(*[one(i) for i in range(300)])
+        assert got == [f"v{i}".encode() for i in range(300)]
+        res = await asyncio.gather(c._cmd("GET", "pk1"), c._cmd("NOSUCHCMD"), c._cmd("GET", "pk2"),
+                                   return_exceptions=True)
+        assert res[0] == b"v1" and isinstance(res[1], Exception) and res[2] == b"v2", res
+        await c.close()
+    asyncio.run(go())
