@@ -23,15 +23,22 @@ def load(d):
         with open(f) as fh:
             for ln in fh:
                 try:
-                    ev.append(json.loads(ln))
+                    e = json.loads(ln)
                 except ValueError:
-                    pass
+                    continue
+                e["src"] = os.path.basename(f).split(".")[0]
+                ev.append(e)
     return sorted(ev, key=lambda e: e["t"])
 
 
 def report(ev):
     per: dict = {}
     ticks = []
+    by_text: dict = {}  # embed_search events carry the preprocessed question text
+    for e in ev:
+        if "t_text" in e:
+            by_text.setdefault(e["t_text"], {}).setdefault(e["e"], e["t"])
+    es = [r for r in by_text.values() if {"q_es_sent", "e_es_rx", "e_es_tx", "q_es_rx"} <= set(r)]
     for e in ev:
         k = e["e"]
         if k == "e_admit":
@@ -39,10 +46,11 @@ def report(ev):
                 per.setdefault(q, {}).setdefault("e_admit", e["t"])
         elif k == "e_tick":
             ticks.append(e)
-        elif "q" in e:
+        elif "q" in e and e["q"] is not None:
             per.setdefault(e["q"], {}).setdefault(k, e["t"])
     segs = [("loadgen_to_gateway", "l_send", "g_rx"), ("gateway_to_query", "g_rx", "q_start"),
-            ("gateway_in", "l_send", "q_start"), ("pre_answer", "q_start", "q_answer_sent"),
+            ("gateway_in", "l_send", "q_start"), ("pre_answer", "q_start", "q_answer_sent"), ("search_stage", "q_start", "q_searched"),
+            ("embed_cache_set", "q_searched", "q_embed_cached"), ("to_answer", "q_embed_cached", "q_answer_sent"),
             ("rpc_out", "q_answer_sent", "e_answer_rx"), ("held", "e_answer_rx", "e_admit"),
             ("in_engine", "e_admit", "e_answer_tx"), ("rpc_back", "e_answer_tx", "q_answer_rx"),
             ("post_answer", "q_answer_rx", "q_end"), ("query_to_gateway", "q_end", "g_tx"), ("gateway_to_loadgen", "g_tx", "l_recv"),
@@ -55,6 +63,20 @@ def report(ev):
         if xs:
             out[name] = {"n": len(xs), "mean_ms": round(statistics.mean(xs), 2), "p50_ms": round(xs[len(xs) // 2], 2),
                          "p99_ms": round(xs[min(len(xs) - 1, int(0.99 * len(xs)))], 2)}
+    for name, a, b in (("es_rpc_in", "q_es_sent", "e_es_rx"), ("es_engine", "e_es_rx", "e_es_tx"),
+                       ("es_rpc_back", "e_es_tx", "q_es_rx"), ("es_total", "q_es_sent", "q_es_rx"),
+                       ("chunk_rows", "q_es_rx", "q_results")):
+        xs = sorted((r[b] - r[a]) * 1000 for r in es)
+        if xs:
+            out[name] = {"n": len(xs), "mean_ms": round(statistics.mean(xs), 2), "p50_ms": round(xs[len(xs) // 2], 2),
+                         "p99_ms": round(xs[min(len(xs) - 1, int(0.99 * len(xs)))], 2)}
+    lags: dict = {}
+    for e in ev:
+        if e["e"] == "loop_lag":
+            lags.setdefault(e["src"], []).append(e["ms"])
+    if lags:
+        out["loop_stalls"] = {src: {"n": len(x), "total_ms": round(sum(x), 1), "max_ms": max(x)}
+                              for src, x in lags.items()}
     if full:
         t0 = min(r["l_send"] for r in full)
         t1 = max(r["l_recv"] for r in full)

@@ -119,10 +119,14 @@ async def query_handler(deps, body: bytes) -> Response:
             msg = "search failed" if "embed_search/search:" in str(e) else "failed to embed question"
             return fail(log, msg, e, 500)
         _obs("embed_search", t1)
+        if timeline.enabled():
+            timeline.mark("q_searched", q=req.question)
         try:
             await deps.cache.set_embedding(req.question, vec, ttl)
         except Exception as e:  # noqa: BLE001
             log.warn("failed to cache embedding", "err", e)
+        if timeline.enabled():
+            timeline.mark("q_embed_cached", q=req.question)
     if vec is None:
         t1 = time.perf_counter()
         try:

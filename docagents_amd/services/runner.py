@@ -136,9 +136,25 @@ async def startup_sweep(deps):
         deps.log.warn("startup sweep failed", "err", e)
 
 
+async def _loop_lag_monitor(every: float = 0.005):
+    """DA_REQ_TIMELINE: record event-loop stalls (a 5 ms sleep that took > 10 ms) as timeline events,
+    so a slow hop inside a service can be told apart from a blocked loop."""
+    from ..utils import timeline
+    loop = asyncio.get_running_loop()
+    while True:
+        t = loop.time()
+        await asyncio.sleep(every)
+        lag = loop.time() - t - every
+        if lag > 0.005:
+            timeline.mark("loop_lag", ms=round(lag * 1000, 2))
+
+
 async def run_http_service(name: str):
     from ..app import build
+    from ..utils import timeline
     deps = await build(name)
+    if timeline.enabled():
+        asyncio.ensure_future(_loop_lag_monitor())
     if name == "gateway":
         from .gateway import build_app
         deps.log.info("gateway listening", "addr", f":{deps.config.port}")

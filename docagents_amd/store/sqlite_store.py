@@ -274,7 +274,10 @@ class CompositeStore:
         vec, hits = await self.vectors.embed_search(text, list(doc_ids), k, thr)
         if timeline.enabled():
             timeline.mark("q_es_rx", t_text=text)
-        return vec, await self._results(hits)
+        res = await self._results(hits)
+        if timeline.enabled():
+            timeline.mark("q_results", t_text=text)
+        return vec, res
 
     async def _results(self, hits) -> list[SearchResult]:
         """Chunks + their documents' summaries + decoder tokens of the hits in ONE query (one thread
