@@ -144,6 +144,8 @@ def test_loadgen_against_spawned_stack(tmp_path):
     assert r.returncode == 0, r.stderr[-2000:]
     out = json.loads(r.stdout.strip().splitlines()[-1])
     assert out["docs_ready"] == 4 and out["query_errors"] == 0
+    # partial hits: the embedding cache answers, search + answer run again
+    assert out["serial_partial_hit_queries"] >= 1 and out["serial_partial_hit_p50_ms"] > 0
     assert out["cache_hit_p50_ms"] < out["cache_miss_p99_ms"] + 1000
     # the reference's ingest number: one document at a time, upload -> summary readable
     assert out["serial_ingest_docs"] == 3 and out["serial_ingest_p50_ms"] > 0
