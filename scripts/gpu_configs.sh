@@ -6,7 +6,7 @@
 #   rank2     2 ranks sharing the GPU (gloo collectives): the multi-rank bench path
 #   tp2       Phi-3-mini TP=2 + IVFFlat, 2 ranks sharing the GPU (xGMI IPC all-reduce kernel, gloo)
 #   c5        BASELINE config 5 layout: Llama-3-70B TP=8 + fp8 encoder + IVFFlat, 8 ranks sharing the GPU
-#   r2 / r8   the driver's N > 1 bench path rehearsed with 2 / 8 ranks sharing the GPU (gloo; small batch):
+#   r2/r4/r8  the driver's N > 1 bench path rehearsed with 2 / 4 / 8 ranks sharing the GPU (gloo; small batch):
 #             every block (rccl_search, tp_decode, tp_decode_70b at 8, xgmi_allreduce, serving_search)
 #   c4full    BASELINE config 4 at its real total size: 8 ranks x 1.25M rows (10M), BGE-large fp16, the
 #             rccl-form sharded search in the QA step; then recall vs one exact 10M-row index
@@ -43,6 +43,9 @@ case ${1:-c4} in
   r2) DA_DIST_BACKEND=gloo run r2 900 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
         --master-addr 127.0.0.1 --master-port 29536 bench.py --gpus 2 --steps 2 --warmup 1 --batch 4 \
         --latency-reps 2 --ingest-docs 4 --ingest-batches 1 --ingest-latency-reps 2 ;;
+  r4) DA_DIST_BACKEND=gloo run r4 900 python -m torch.distributed.run --nnodes=1 --nproc-per-node 4 \
+        --master-addr 127.0.0.1 --master-port 29540 bench.py --gpus 4 --steps 1 --warmup 1 --batch 4 \
+        --latency-reps 1 --ingest-docs 2 --ingest-batches 1 --ingest-latency-reps 1 --max-new 8 --breakdown 0 ;;
   r8) DA_DIST_BACKEND=gloo run r8 1100 python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 \
         --master-addr 127.0.0.1 --master-port 29537 bench.py --gpus 8 --steps 1 --warmup 1 --batch 4 \
         --latency-reps 1 --ingest-docs 2 --ingest-batches 1 --ingest-latency-reps 1 --max-new 8 \
