@@ -73,3 +73,25 @@ def test_decode_fast_embed_and_search_plane_co_run_exactly():
     assert plane.healthy
     plane.stop()
     assert threading.active_count() >= 1
+
+
+def test_release_decoder_returns_the_kv_cache_to_the_device():
+    """bench.py's N > 1 blocks build TP decoders only after Engine.release_decoder: the KV cache
+    (sized by parallel/hbm_plan.kv_bytes, the formula the plan uses) must really go back to the
+    device, the weights stay (the TP blocks shard them) and embeds still work."""
+    import torch
+
+    from docagents_amd.engine.engine import Engine
+    from docagents_amd.parallel.hbm_plan import kv_bytes
+    eng = Engine("tiny-enc", "tiny-dec", "cuda:0", max_batch=8, max_seq=4096, max_new_tokens=4)
+    eng.answer_many([("q?", [[5, 6, 7]], 0.5)], 4)  # a captured decode graph holds the cache too
+    torch.cuda.synchronize()
+    before = torch.cuda.memory_allocated()
+    want = kv_bytes(eng.dec_cfg, 8 + 4, 4096)
+    stats = eng.release_decoder()
+    after = torch.cuda.memory_allocated()
+    assert stats["decode_steps"] > 0 and eng.gen is None and eng.decoder.cache is None
+    assert before - after >= want, (before, after, want)
+    assert eng.decoder.w["layers"], "weights are kept"
+    v = eng.embed(["still embeds"])
+    assert v.shape == (1, eng.dim)
