@@ -554,7 +554,12 @@ def main():
                 out.update(multi)
                 out["multi_timeout"] = {"block": current["block"], "budget_s": a.block_budget_s}
                 if R == 0:
-                    print(json.dumps(out), flush=True)
+                    try:
+                        line = json.dumps(out)
+                    except Exception:  # noqa: BLE001 - a dict the main thread was writing: the headline keys
+                        line = json.dumps({k: out[k] for k in list(out) if k not in multi} |
+                                          {"multi_timeout": out["multi_timeout"]}, default=str)
+                    print(line, flush=True)
                 print(f"[bench] rank {R}: block {current['block']} overran {a.block_budget_s:.0f} s; ending the run",
                       file=sys.stderr, flush=True)
                 os._exit(0)

@@ -14,6 +14,9 @@ time the collectives the north star names, each on all N ranks together:
                 IPC all-reduce (graph-replayed, as served) and with torch.distributed (RCCL on
                 GPUs) in its place, plus the per-decision agreement verdict of a TP = N decoder
                 with the unsharded one (parallel/tp_verify.py)
+  tp_decode_70b the same timing for Llama-3-70B at TP = 8 (BASELINE config 5's QA model), each rank
+                building only its shard from a per-shard seed (``tp_decode(..., full_weights=None)``)
+  *_rccl_graph  the served TP fallback: torch.distributed all-reduces captured in the decode graph
   xgmi          the IPC all-reduce vs RCCL per call at 16 KB / 384 KB / 6 MB (xgmi_allreduce.py)
 
 Every block is collective: all ranks call it in the same order with the same shapes.
@@ -131,13 +134,19 @@ def _round_up(x: int, m: int) -> int:
 def hbm_check(need: int, what: str, dev, margin: int = 8 << 30) -> None:
     """Refuse an allocation of ``need`` bytes that would not fit the device's free memory (less a
     margin for the runtime and RCCL): the block then reports a clear error instead of an OOM
-    half-way through its collectives."""
-    if torch.device(dev).type != "cuda":
-        return
-    free, total = torch.cuda.mem_get_info(dev)
-    if need + margin > free:
-        raise MemoryError(f"{what}: needs {need / 1e9:.1f} GB + {margin / 1e9:.0f} GB margin, "
-                          f"{free / 1e9:.1f} of {total / 1e9:.1f} GB free")
+    half-way through its collectives. Collective: every rank refuses if any rank must (a rank that
+    raised alone would leave its peers inside the next collective)."""
+    short = ""
+    if torch.device(dev).type == "cuda":
+        free, total = torch.cuda.mem_get_info(dev)
+        if need + margin > free:
+            short = (f"{what}: needs {need / 1e9:.1f} GB + {margin / 1e9:.0f} GB margin, "
+                     f"{free / 1e9:.1f} of {total / 1e9:.1f} GB free")
+    if dist.is_initialized() and dist.get_world_size() > 1:
+        if all_reduce_max(1.0 if short else 0.0, dev) > 0 and not short:
+            short = f"{what}: another rank lacks the memory"
+    if short:
+        raise MemoryError(short)
 
 
 def tp_decode(dec_cfg, full_weights, rank: int, world: int, dev, prompts_by_b: dict, max_new: int,
