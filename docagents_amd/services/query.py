@@ -7,6 +7,7 @@ probability of the answer (llm/openai.go:101-102); preview = first 150 bytes cut
 """
 from __future__ import annotations
 
+import asyncio
 import time
 import uuid
 
@@ -66,6 +67,23 @@ def build_sources(results) -> list[Source]:
     return [Source(r.chunk.id, float(np.float32(r.score)), truncate_preview(r.chunk.text, 150)) for r in results]
 
 
+_BG: set = set()
+
+
+def _background(coro):
+    """Run ``coro`` without awaiting it (a reference is kept until it finishes)."""
+    t = asyncio.ensure_future(coro)
+    _BG.add(t)
+    t.add_done_callback(_BG.discard)
+
+
+async def _set_embedding(deps, question, vec, ttl, log):
+    try:
+        await deps.cache.set_embedding(question, vec, ttl)
+    except Exception as e:  # noqa: BLE001
+        log.warn("failed to cache embedding", "err", e)
+
+
 def _resp(answer, sources, confidence, cached):
     return {"answer": answer, "sources": [s.to_json() for s in sources], "confidence": F32(confidence),
             "cached": cached}
@@ -121,10 +139,10 @@ async def query_handler(deps, body: bytes) -> Response:
         _obs("embed_search", t1)
         if timeline.enabled():
             timeline.mark("q_searched", q=req.question)
-        try:
-            await deps.cache.set_embedding(req.question, vec, ttl)
-        except Exception as e:  # noqa: BLE001
-            log.warn("failed to cache embedding", "err", e)
+        # not awaited: the answer does not need it, and the cache client is pipelined over one
+        # connection, so this SET still reaches the cache before the query-result SET below (the
+        # reference's visibility: both are in the cache when the response is written)
+        _background(_set_embedding(deps, req.question, vec, ttl, log))
         if timeline.enabled():
             timeline.mark("q_embed_cached", q=req.question)
     if vec is None:

@@ -123,6 +123,8 @@ class CompositeStore:
         # one engine step that writes the rows into HBM directly (embed_and_save)
         self.direct_embed = direct_embed and hasattr(vectors, "embed_index")
 
+    INLINE_LOOKUP_KEYS = 32  # _results: the question path's chunk lookup runs inline up to this many keys
+
     async def _run(self, fn, *a):
         return await asyncio.to_thread(fn, *a)
 
@@ -286,11 +288,16 @@ class CompositeStore:
             return []
         keys = tuple(int(kk) for kk, _ in hits)
         qs = ",".join("?" * len(keys))
-        rows = await self._run(
-            self.meta.q,
-            f"SELECT c.key, c.id, c.document_id, c.ord, c.text, c.token_count, c.dec_tokens, s.document_id, "
-            f"s.summary, s.key_points FROM chunks c LEFT JOIN summaries s ON s.document_id = c.document_id "
-            f"WHERE c.key IN ({qs})", keys)
+        sql = (f"SELECT c.key, c.id, c.document_id, c.ord, c.text, c.token_count, c.dec_tokens, s.document_id, "
+               f"s.summary, s.key_points FROM chunks c LEFT JOIN summaries s ON s.document_id = c.document_id "
+               f"WHERE c.key IN ({qs})")
+        if len(keys) <= self.INLINE_LOOKUP_KEYS and self.meta.path != ":memory:":
+            # a top-k's rows by primary key: ~0.1 ms in SQLite, cheaper inline (the event loop's own
+            # read-only connection) than a thread-pool round trip, which under 128 in-flight queries
+            # cost ~36 ms (profiles/r6/stack: chunk_rows)
+            rows = self.meta.q(sql, keys)
+        else:
+            rows = await self._run(self.meta.q, sql, keys)
         found = {r[0]: r for r in rows}
         sums: dict[str, Summary] = {}
         out = []
