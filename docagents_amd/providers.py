@@ -119,7 +119,8 @@ class LocalLLM:
         return await asyncio.to_thread(self.engine.answer_text, question, context, quality)
 
     async def answer_chunks(self, question: str, chunks, quality: float):
-        ids = [tok if tok is not None else self.engine._ids(txt) for txt, tok in chunks]
+        ids = [(tok.tolist() if isinstance(tok, np.ndarray) else tok) if tok is not None else self.engine._ids(txt)
+               for txt, tok in chunks]
         return (await asyncio.to_thread(self.engine.answer_many, [(question, ids, quality)]))[0]
 
 

@@ -175,7 +175,9 @@ async def query_handler(deps, body: bytes) -> Response:
             else:
                 toks = await deps.store.chunks_by_keys([r.chunk.key for r in results])
                 blobs = [toks.get(r.chunk.key, (None, None))[1] for r in results]
-            chunks = [(r.chunk.text, np.frombuffer(b, dtype=np.int32).tolist() if b else None)
+            # token ids stay an int32 array (the engine RPC ships it as one buffer): no per-token
+            # Python ints on the query path
+            chunks = [(r.chunk.text, np.frombuffer(b, dtype=np.int32) if b else None)
                       for r, b in zip(results, blobs)]
             answer, confidence = await deps.llm.answer_chunks(req.question, chunks, quality)
         else:

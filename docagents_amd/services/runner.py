@@ -155,6 +155,11 @@ async def run_http_service(name: str):
     deps = await build(name)
     if timeline.enabled():
         asyncio.ensure_future(_loop_lag_monitor())
+    # everything built at startup (modules, config, clients) to the permanent generation: full
+    # collections under load then scan only what requests allocate
+    import gc
+    gc.collect()
+    gc.freeze()
     if name == "gateway":
         from .gateway import build_app
         deps.log.info("gateway listening", "addr", f":{deps.config.port}")
