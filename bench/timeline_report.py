@@ -64,7 +64,8 @@ def report(ev):
             out[name] = {"n": len(xs), "mean_ms": round(statistics.mean(xs), 2), "p50_ms": round(xs[len(xs) // 2], 2),
                          "p99_ms": round(xs[min(len(xs) - 1, int(0.99 * len(xs)))], 2)}
     for name, a, b in (("es_rpc_in", "q_es_sent", "e_es_rx"), ("es_engine", "e_es_rx", "e_es_tx"),
-                       ("es_rpc_back", "e_es_tx", "q_es_rx"), ("es_total", "q_es_sent", "q_es_rx"),
+                       ("es_rpc_back", "e_es_tx", "q_es_rx"), ("es_embed", "e_es_rx", "e_es_embedded"),
+                       ("es_search", "e_es_embedded", "e_es_tx"), ("es_total", "q_es_sent", "q_es_rx"),
                        ("chunk_rows", "q_es_rx", "q_results")):
         xs = sorted((r[b] - r[a]) * 1000 for r in es)
         if xs:

@@ -610,6 +610,8 @@ class EngineServer:
                 v = await self._embed_fast(list(args["texts"]), bool(args.get("preprocess", False)))
             except Exception as e:  # noqa: BLE001 - the client maps the tag to the reference's message
                 raise RuntimeError(f"embed_search/embed: {e}") from e
+            if tl:
+                timeline.mark("e_es_embedded", t_text=args["texts"][0] if args.get("texts") else None)
             try:
                 s, ids = await self._search(v, args["k"], args["min_sim"], args.get("filters"))
             except Exception as e:  # noqa: BLE001

@@ -158,6 +158,10 @@ def main(argv=None) -> int:
             prometheus_client.start_http_server(cfg.engine_metrics_port)
             log.info("engine metrics listening", "port", cfg.engine_metrics_port)
         server = await srv.start(urls[replica])
+        from ..utils import timeline
+        if timeline.enabled():
+            from .runner import _loop_lag_monitor
+            asyncio.ensure_future(_loop_lag_monitor())
         log.info("engine listening", "addr", urls[replica], "replica", replica, "replicas", replicas,
                  "world", world, "device", str(dev), "encoder", cfg.embed_arch, "decoder", cfg.llm_arch, "tp", t)
         stop = asyncio.Event()
