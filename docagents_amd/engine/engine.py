@@ -131,6 +131,15 @@ class Engine:
             self.stats["embed_texts"] += 1
             self.stats["embed_s"] += time.perf_counter() - t0
             return out
+        if self.enc_graphs and n <= 64:  # a micro-batch of questions: one captured graph
+            with self.enc_lock:
+                v = self.encoder.encode_batch(seqs)
+            if v is not None:
+                out.copy_(v.to(out_dtype))
+                self.stats["embed_tokens"] += sum(len(q) for q in seqs)
+                self.stats["embed_texts"] += n
+                self.stats["embed_s"] += time.perf_counter() - t0
+                return out
         order = np.argsort([-len(s) for s in seqs], kind="stable")
         with self.enc_lock:
             i = 0

@@ -186,6 +186,13 @@ class BertEncoder:
     # GEMMs / norms process them (their rows are independent) and flash attention and the pooling
     # read the real length from cu_seqlens, so row 0..L-1 see exactly the unpadded computation.
     GRAPH_BUCKETS = (16, 32, 64, 128)
+    # small batches of short texts (the fast embed lane's micro-batches of questions): one graph per
+    # (sequences, padded tokens) bucket; sequences packed back to back, then padding rows, padded
+    # sequences of length 0 (cu repeats the real total); every real length <= BATCH_MAX_LEN, which is
+    # the max_seqlen the graphs were captured with. Measured: a lane batch took ~5 ms of launches
+    # from Python beside the decode thread (profiles/r6/stack: es_embed)
+    BATCH_BUCKETS = ((2, 64), (4, 128), (8, 256), (16, 512), (32, 1024), (64, 2048))
+    BATCH_MAX_LEN = 128
 
     def _capture_small(self):
         from ..ops.kernels import workspace_role
@@ -210,6 +217,21 @@ class BertEncoder:
                 with torch.cuda.graph(g, stream=side, capture_error_mode="thread_local"):
                     out = pool(self.forward(ids, pos, cu, T), cu, mode)
                 self._g[T] = (g, ids, cu, out)
+            self._gb = {}
+            shared = torch.cuda.graph_pool_handle()  # replays are serialised (lock + event chain)
+            Lc = self.BATCH_MAX_LEN
+            for nb, T in sorted(self.BATCH_BUCKETS, reverse=True):
+                ids = torch.zeros(T, dtype=torch.int32, device=dev)
+                pos = torch.zeros(T, dtype=torch.int32, device=dev)
+                step = min(Lc, (T - 1) // nb)
+                cu = torch.tensor([i * step for i in range(nb + 1)], dtype=torch.int32, device=dev)
+                for _ in range(2):
+                    pool(self.forward(ids, pos, cu, Lc), cu, mode)
+                side.synchronize()
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g, pool=shared, stream=side, capture_error_mode="thread_local"):
+                    out = pool(self.forward(ids, pos, cu, Lc), cu, mode)
+                self._gb[nb] = (T, g, ids, pos, cu, out)
         torch.cuda.current_stream(dev).wait_stream(side)
 
     def prepare_graphs(self) -> None:
@@ -252,6 +274,44 @@ class BertEncoder:
             cu.copy_(dev[T:])
             g.replay()
             res = out.clone()
+            if self._g_done is None:
+                self._g_done = torch.cuda.Event()
+            self._g_done.record(cur)
+        return res
+
+    def encode_batch(self, seqs: list[list[int]]) -> torch.Tensor | None:
+        """2..64 short sequences -> unit-norm embeddings fp32 [n, H] through a captured batch
+        graph, or None when they fit no bucket (the caller runs the eager packed path)."""
+        n = len(seqs)
+        if self.device.type != "cuda" or n < 2 or torch.cuda.is_current_stream_capturing():
+            return None
+        if getattr(self, "_g", None) is None:
+            self.prepare_graphs()
+        lens = [len(q) for q in seqs]
+        tot = sum(lens)
+        if min(lens) == 0 or max(lens) > min(self.BATCH_MAX_LEN, self.cfg.max_pos):
+            return None
+        b = next((nb for nb, T in self.BATCH_BUCKETS if nb >= n and T > tot and nb in getattr(self, "_gb", {})), None)
+        if b is None:
+            return None
+        T, g, ids, pos, cu, out = self._gb[b]
+        host = np.zeros(2 * T + b + 1, dtype=np.int32)
+        host[:tot] = np.fromiter((t for q in seqs for t in q), dtype=np.int32, count=tot)
+        c = np.zeros(n + 1, dtype=np.int64)
+        np.cumsum(lens, out=c[1:])
+        host[T:T + tot] = np.arange(tot) - np.repeat(c[:-1], lens)
+        host[2 * T:2 * T + n + 1] = c
+        host[2 * T + n + 1:] = tot  # padded sequences: length 0
+        with self._g_lock:  # the same device-side ordering as encode_one (shared workspace)
+            cur = torch.cuda.current_stream(self.device)
+            if self._g_done is not None:
+                cur.wait_event(self._g_done)
+            d = h2d(host, self.device)
+            ids.copy_(d[:T])
+            pos.copy_(d[T:2 * T])
+            cu.copy_(d[2 * T:])
+            g.replay()
+            res = out[:n].clone()
             if self._g_done is None:
                 self._g_done = torch.cuda.Event()
             self._g_done.record(cur)

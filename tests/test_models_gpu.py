@@ -223,6 +223,35 @@ def test_encoder_one_sequence_graphs_match_eager(arch, dtype):
             assert torch.allclose(g.float(), r.float(), atol=3e-2), n
 
 
+@pytest.mark.parametrize("arch,dtype", [("tiny-enc", "bf16"), ("bge-base", "bf16"), ("tiny-enc", "fp16"),
+                                        ("tiny-enc", "fp8")])
+def test_encoder_batch_graphs_match_eager(arch, dtype):
+    """encode_batch (the fast lane's micro-batches through captured (sequences, tokens) bucket graphs:
+    sequences packed, padding rows, zero-length padded sequences) == the eager packed path row by
+    row, at every bucket edge; batches that fit no bucket return None (the caller goes eager)."""
+    import dataclasses
+    cfg = encoder_config(arch)
+    if arch == "bge-base":
+        cfg = dataclasses.replace(cfg, layers=2)
+    enc = BertEncoder(cfg, "cuda", seed=7, dtype=dtype)
+    enc.prepare_graphs()
+    assert set(enc._gb) == {nb for nb, _ in BertEncoder.BATCH_BUCKETS}
+    rng = np.random.default_rng(3)
+    for n, lo, hi in [(2, 1, 30), (3, 5, 40), (4, 20, 31), (7, 3, 36), (16, 10, 31), (17, 2, 30), (33, 1, 31),
+                      (64, 20, 31), (5, 100, 128)]:
+        seqs = [[int(t) for t in rng.integers(5, cfg.vocab - 1, size=int(m))] for m in rng.integers(lo, hi + 1, size=n)]
+        got = enc.encode_batch(seqs)
+        if sum(map(len, seqs)) >= dict(BertEncoder.BATCH_BUCKETS)[64]:
+            assert got is None
+            continue
+        assert got is not None and got.shape == (n, cfg.hidden), (n, lo, hi)
+        want = enc.encode_packed(seqs)
+        cos = (got.float() * want.float()).sum(-1)
+        assert float(cos.min()) > 0.999, (n, lo, hi, cos.min())
+    assert enc.encode_batch([[5] * 129, [6] * 3]) is None  # longer than the captured max_seqlen
+    assert enc.encode_batch([[5] * 40] * 65) is None       # more sequences than the largest bucket
+
+
 def test_encoder_one_sequence_graphs_two_streams_concurrent():
     """Two threads on two streams (the engine's fast embed lane and its GPU thread) call encode_one at
     once; the captured graphs share their static ids / cu / out buffers, so without device-side
