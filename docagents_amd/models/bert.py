@@ -195,43 +195,45 @@ class BertEncoder:
     BATCH_MAX_LEN = 128
 
     def _capture_small(self):
-        from ..ops.kernels import workspace_role
-        self._g = {}
+        from ..ops import kernels as K
+        self._g, self._gb = {}, {}
         dev = self.device
         mode = 0 if self.cfg.pooling == "cls" else 1
         pool = self.ops.pool_l2norm_f16 if self.fp16 else self.ops.pool_l2norm
         side = torch.cuda.Stream(device=dev)
         side.wait_stream(torch.cuda.current_stream(dev))
-        # largest bucket first, in a workspace role of their own: the scratch the first capture
-        # sizes is the scratch every later one reuses (a grown workspace would free captured memory)
-        with torch.cuda.stream(side), workspace_role("enc_graph"):
-            for T in sorted(self.GRAPH_BUCKETS, reverse=True):
+        Lc = self.BATCH_MAX_LEN
+        # (key, T, max_seqlen, cu): the one-sequence length buckets and the batch buckets
+        shapes = [(("one", T), T, T, [0, T]) for T in self.GRAPH_BUCKETS]
+        for nb, T in self.BATCH_BUCKETS:
+            step = min(Lc, (T - 1) // nb)
+            shapes.append((("batch", nb), T, Lc, [i * step for i in range(nb + 1)]))
+        bufs = {}
+        # In a workspace role of their own, and EVERY shape warmed before the first capture: the
+        # split-K scratch only grows, and a growth after a capture would free the memory that graph
+        # captured (an illegal address at its next replay). The scratch is checked unchanged below.
+        with torch.cuda.stream(side), K.workspace_role("enc_graph"):
+            for key, T, ms, cu_l in shapes:
                 ids = torch.zeros(T, dtype=torch.int32, device=dev)
-                pos = torch.arange(T, dtype=torch.int32, device=dev)
-                cu = torch.tensor([0, T], dtype=torch.int32, device=dev)
-                for _ in range(2):  # warm: allocations and workspaces before capture
-                    pool(self.forward(ids, pos, cu, T), cu, mode)
-                side.synchronize()
+                pos = torch.arange(T, dtype=torch.int32, device=dev) if key[0] == "one" else \
+                    torch.zeros(T, dtype=torch.int32, device=dev)
+                cu = torch.tensor(cu_l, dtype=torch.int32, device=dev)
+                for _ in range(2):  # warm: allocations and workspaces before any capture
+                    pool(self.forward(ids, pos, cu, ms), cu, mode)
+                bufs[key] = (T, ms, ids, pos, cu)
+            side.synchronize()
+            ws0 = K.workspace_buffer(dev)
+            for key, (T, ms, ids, pos, cu) in sorted(bufs.items(), key=lambda kv: -kv[1][0]):
                 g = torch.cuda.CUDAGraph()
                 # thread_local: a capture must not trip over the serving threads' own CUDA calls
                 with torch.cuda.graph(g, stream=side, capture_error_mode="thread_local"):
-                    out = pool(self.forward(ids, pos, cu, T), cu, mode)
-                self._g[T] = (g, ids, cu, out)
-            self._gb = {}
-            shared = torch.cuda.graph_pool_handle()  # replays are serialised (lock + event chain)
-            Lc = self.BATCH_MAX_LEN
-            for nb, T in sorted(self.BATCH_BUCKETS, reverse=True):
-                ids = torch.zeros(T, dtype=torch.int32, device=dev)
-                pos = torch.zeros(T, dtype=torch.int32, device=dev)
-                step = min(Lc, (T - 1) // nb)
-                cu = torch.tensor([i * step for i in range(nb + 1)], dtype=torch.int32, device=dev)
-                for _ in range(2):
-                    pool(self.forward(ids, pos, cu, Lc), cu, mode)
-                side.synchronize()
-                g = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g, pool=shared, stream=side, capture_error_mode="thread_local"):
-                    out = pool(self.forward(ids, pos, cu, Lc), cu, mode)
-                self._gb[nb] = (T, g, ids, pos, cu, out)
+                    out = pool(self.forward(ids, pos, cu, ms), cu, mode)
+                if key[0] == "one":
+                    self._g[T] = (g, ids, cu, out)
+                else:
+                    self._gb[key[1]] = (T, g, ids, pos, cu, out)
+            if K.workspace_buffer(dev) is not ws0:
+                raise RuntimeError("encoder graph capture grew the enc_graph workspace")
         torch.cuda.current_stream(dev).wait_stream(side)
 
     def prepare_graphs(self) -> None:
@@ -243,7 +245,7 @@ class BertEncoder:
             except Exception as e:  # noqa: BLE001 - the eager encoder still serves
                 import logging
                 logging.getLogger(__name__).warning("encoder graph capture failed, eager path: %r", e)
-                self._g = {}
+                self._g, self._gb = {}, {}
 
     def encode_one(self, seq: list[int]) -> torch.Tensor:
         """One token sequence -> unit-norm embedding fp32 [1, H]: a captured graph when it fits a

@@ -182,6 +182,15 @@ def workspace_role(name: str):
         _ROLE.name = prev
 
 
+def workspace_buffer(device):
+    """The current role's workspace tensor on ``device`` (None before its first use): callers that
+    capture graphs check it is the same object after their captures (a grown workspace frees the
+    buffer earlier captures point at)."""
+    device = torch.device(device)
+    key = (device.index if device.index is not None else torch.cuda.current_device(), getattr(_ROLE, "name", "main"))
+    return _WS.get(key)
+
+
 def _workspace(nbytes: int, device) -> torch.Tensor:
     key = (device.index if device.index is not None else torch.cuda.current_device(), getattr(_ROLE, "name", "main"))
     buf = _WS.get(key)
