@@ -36,5 +36,7 @@ struct GemmArgs {
 int launch_gemm256(const GemmArgs& a, int epi, hipStream_t s, int fp8 = 1);
 // phase-split BMx256 bf16 kernel (gemm8p.hip), bm = 256 or 128; K % 64 == 0, K >= 128
 int launch_gemm8p(const GemmArgs& a, int epi, hipStream_t s, int bm = 256);
+// four-wave 256x256 kernel (gemm4w.hip, 128x128 per wave; the tile-13 A/B arm), bf16, no EPI_ROPE
+int launch_gemm4w(const GemmArgs& a, int epi, hipStream_t s);
 // row-tile height (128 / 256) for a non-RoPE prefill product of M x N (gemm8p.hip)
 int gemm8p_pick_bm(int M, int N);

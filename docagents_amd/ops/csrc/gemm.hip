@@ -634,7 +634,8 @@ DA_EXPORT int da_gemm_rope(const void* A, int lda, const void* W, void* C, int l
 
 // Tile selection: big tiles when the grid fills 256 CUs, skinny tiles (+ split-K) for decode-sized M.
 // tile: 0 = auto, 1 = 128x128, 2 = 64x128, 3 = 32x128, 4 / 7 = 256x256 phase-split (gemm8p),
-// 6 = GEMV (M = 1), 8 = 128x128 PF4, 9 = 128x64 PF4, 10 = 128x256 phase-split (gemm8p).
+// 6 = GEMV (M = 1), 8 = 128x128 PF4, 9 = 128x64 PF4, 10 = 128x256 phase-split (gemm8p),
+// 13 = 256x256 four-wave (gemm4w).
 DA_EXPORT int da_gemm_bf16(const void* A, int lda, const void* W, void* C, int ldc,
                            const void* bias, const void* resid, int ldr,
                            int M, int N, int K, int epi, int tile, int splits, void* ws,
@@ -664,6 +665,10 @@ DA_EXPORT int da_gemm_bf16(const void* A, int lda, const void* W, void* C, int l
   if (tile == 4 || tile == 7 || tile == 10) {
     if (splits != 1 || K < 128) return (int)hipErrorInvalidValue;
     return launch_gemm8p(a, epi, s, tile == 10 ? 128 : 256);
+  }
+  if (tile == 13) {
+    if (splits != 1 || K < 128) return (int)hipErrorInvalidValue;
+    return launch_gemm4w(a, epi, s);
   }
   if (tile == 6) return launch_gemv(a, epi, s);
   int err;

@@ -83,6 +83,7 @@ _SIGS = {
     "da_placement_probe": [c_void_p, c_int, c_longlong, c_void_p],
     "da_spin": [c_int, c_void_p, c_void_p],
     "da_gemm8p_persist": [c_int],
+    "da_gemm4w_variant": [c_int],
     "da_gemm_f16": [c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int,
                     c_void_p],
     "da_flash_attn_f16": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_int, c_int, c_int,
@@ -993,6 +994,13 @@ def gemm8p_persist(on: int = -1) -> int:
     """Persistent tile loop of the prefill GEMM (one workgroup per CU walking its XCD's tiles) on
     (1) / off (0) for later launches; -1 only queries. Returns the previous setting."""
     return int(lib().da_gemm8p_persist(int(on)))
+
+
+def gemm4w_variant(v: int = -1) -> int:
+    """Schedule of the four-wave 256x256 kernel (tile 13, csrc/gemm4w.hip): 0 = three fragment sets
+    where K / 64 is even and >= 4 (default), 1 = two sets always; -1 only queries. Returns the
+    previous setting."""
+    return int(lib().da_gemm4w_variant(int(v)))
 
 
 def _f16_cuda(t, name):
