@@ -1,7 +1,7 @@
 """gemm4w (four-wave 256x256, csrc/gemm4w.hip) schedule variants vs gemm8p (tile 7) vs hipBLASLt.
 
 python bench/gemm4w_ab.py [arms] — arms: "7", "blas", "13:<v>" (v = kernels.gemm4w_variant:
-0 three fragment sets, 1 two). Checks every 13:* arm against an fp32 reference first, then prints sustained TF/s per shape (interleaved
+0 three fragment sets + two barriers per K-tile, 1 two sets, 2 three sets + one barrier). Checks every 13:* arm against an fp32 reference first, then prints sustained TF/s per shape (interleaved
 rounds, random operands)."""
 import json
 import os
@@ -15,7 +15,7 @@ from docagents_amd.ops import kernels as K  # noqa: E402
 from ab_arms import blas_gemm  # noqa: E402
 from gemm_ab import rate  # noqa: E402
 
-ARMS = (sys.argv[1] if len(sys.argv) > 1 else "7,13:0,13:1,blas").split(",")
+ARMS = (sys.argv[1] if len(sys.argv) > 1 else "7,13:0,13:1,13:2,blas").split(",")
 ROUNDS = int(os.environ.get("ROUNDS", "3"))
 SHAPES = [(32768, 9216, 3072), (32768, 3072, 8192), (32768, 3072, 3072), (8192, 8192, 8192), (2930, 9216, 3072)]
 

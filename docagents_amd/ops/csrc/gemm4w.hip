@@ -11,22 +11,23 @@
 // stream itself:
 //  * fragment register sets, written in issue order (the MFMAs are asm volatile, so every LDS read /
 //    DMA stays where it is written and hipcc counts the lgkmcnt each MFMA's operands need).
-//    SCHED 2 (K / 64 even and >= 4): THREE sets, ONE barrier per K-tile between its halves:
-//        half 1 of tile t: 64 MFMAs on set 0 (k-half 0 of t), nothing else
-//        [vmcnt(0) lgkmcnt(0) barrier]  -> stage t+1 landed for every wave; stage t was fully read
-//                                          before this barrier's half began (no LDS drain here)
-//        half 2 of tile t: 64 MFMAs on set S1(t) (k-half 1 of t) | per 4 MFMAs: one DMA of tile
-//                          t+2 -> stage t & 1, reads of k-halves 0 / 1 of t+1 -> set 0 / S1(t+1)
-//    with S1 alternating between sets 1 and 2 (a 2-tile unrolled loop). SCHED 0 (any K): two sets,
-//    half 1 reads k-half 1 of t beside its MFMAs, half 2 reads k-half 0 of t+1 beside the DMA.
-//    hipcc adds no vmcnt for LDS-DMA before a ds_read (checked on gemm8p's ISA): the explicit
-//    waits are the only ones.
-//  * measured (bench/gemm4w_ab.py, profiles/r6/gemm4w/): SCHED 2 reaches 1390-1424 TF/s at
-//    32768x9216x3072, 5-7 % BELOW gemm8p and 9-10 % below hipBLASLt; SCHED 0 1370; DMAs packed
-//    into the first MFMA slots 1297 (VMEM issue back-pressure), 8- / 2-row tile bands no gain.
-//    With one wave per SIMD each K-tile's barrier idles the MFMA pipe (PMC: SQ_WAIT_ANY 12 % of
-//    wave cycles vs hipBLASLt's 6 %), which gemm8p's offset wave groups hide; so production GEMMs
-//    stay on gemm8p and this kernel is the tile-13 A/B arm of that finding.
+//    SCHED 3 (default; K / 64 even and >= 4): THREE sets, TWO barriers per K-tile:
+//        [lgkmcnt(0) barrier B]  -> every wave has read stage t & 1 (reads came in half 2 of t-1)
+//        half 1 of tile t: 64 MFMAs on set 0 (k-half 0 of t) | DMAs 0-7 of tile t+2 -> stage t & 1
+//        [vmcnt(8) barrier M]    -> stage t+1 landed for every wave (tile t+2's 8 DMAs still fly)
+//        half 2 of tile t: 64 MFMAs on set S1(t) (k-half 1 of t) | 32 reads of tile t+1 -> set 0 /
+//                          S1(t+1) in the first 32 MFMA slots | DMAs 8-15 of tile t+2
+//    with S1 alternating between sets 1 and 2 (a 2-tile unrolled loop); one DMA per 8 MFMAs over
+//    the whole tile. SCHED 2: the same three sets with ONE barrier (M) per tile, so all 16 DMAs of
+//    a tile go out in half 2. SCHED 0 (any K): two sets, one barrier; half 1 reads k-half 1 of t
+//    beside its MFMAs, half 2 reads k-half 0 of t+1 beside the DMA. hipcc adds no vmcnt for
+//    LDS-DMA before a ds_read (checked on gemm8p's ISA): the explicit waits are the only ones.
+//  * measured (bench/gemm4w_ab.py, profiles/r6/gemm4w/), 32768x9216x3072: SCHED 3 1462-1472 TF/s,
+//    1.5-2 % below gemm8p (1485-1500) and 4-6 % below hipBLASLt (1527-1558); SCHED 2 1390-1424,
+//    SCHED 0 1370. The one-wave-per-SIMD issue stream stalls on LDS-DMA issue back-pressure (16
+//    DMAs per wave in half a tile: 1297 when packed into 16 MFMA slots, +3.6 % when spread over
+//    the whole tile at the price of a second barrier); gemm8p's two wave groups per SIMD cover
+//    each other's stalls. Production GEMMs stay on gemm8p; this kernel is the tile-13 A/B arm.
 //  * LDS: two stages of A 256x64 + W 256x64 bf16 (2 x 64 KiB), loaded by LDS-DMA
 //    (buffer_load ... lds, 1 KiB per wave-instruction, 16 per wave per K-tile) with the XOR swizzle
 //    of gemm8p (16-B chunk c of row r at chunk c ^ ((r >> 1) & 7), applied on the per-lane SOURCE
@@ -42,9 +43,9 @@
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 
 // v_mfma_f32_16x16x32_bf16 (f16 for T = F16T) as asm with the accumulator tied in an AGPR
-// ("+a": D = C, the register never moves). hipcc's own 16x16x32 with 256 accumulators per lane allocates D apart
-// from C and copies every result back with v_accvgpr_mov (0.9-1.4 copies per MFMA in the K-loop,
-// measured on this kernel's ISA); the 32x32x16 form allocates cleanly but runs ~12 % fewer FLOP/s
+// ("+a": D = C, the register never moves). hipcc's own 16x16x32 with 256 accumulators per lane
+// allocates D apart from C and copies every result back with v_accvgpr_mov (0.9-1.4 copies per
+// MFMA in the K-loop, measured on this kernel's ISA); the 32x32x16 form allocates cleanly but runs ~12 % fewer FLOP/s
 // on random data (MI355X_MICROARCH.md, MFMA shape and clock). Z: C = 0 (no accumulator read).
 // Wait states: operands come from ds_read (no VALU -> MFMA operand hazard); accumulators are
 // read only after the K-loop's closing s_nop.
@@ -116,7 +117,7 @@ gemm4w_kernel(GemmArgs p) {
   }
   // fragment register sets: SCHED 0 uses sets 0 and 1 (= k-halves 0 and 1 of the tile), SCHED 2
   // a third one (set 0 = k-half 0 of every tile, k-half 1 alternates between sets 1 and 2)
-  constexpr int NSET = SCHED == 2 ? 3 : 2;
+  constexpr int NSET = SCHED >= 2 ? 3 : 2;  // SCHED 2 / 3: three
   bf16x8_t fa[NSET][8], fw[NSET][8];
   f32x4_t acc[8][8];
   auto lds16 = [&](const char* q) __attribute__((always_inline)) { return *(const bf16x8_t*)q; };
@@ -183,6 +184,40 @@ gemm4w_kernel(GemmArgs p) {
   // (no LDS drain at the barrier). S1 / S1N: the sets holding k-half 1 of tiles kt / kt + 1.
   auto ktile3 = [&](int kt, auto fill_t, auto next_t, auto z_t, auto s1_t, auto s1n_t) __attribute__((always_inline)) {
     constexpr bool FILL = decltype(fill_t)::value, NEXT = decltype(next_t)::value;
+    if constexpr (SCHED == 3) {
+      // two barriers per K-tile, the DMA of tile kt + 2 spread over both halves (one per 8 MFMAs):
+      // B (tile start): every wave has read stage kt & 1 (its reads came in half 2 of tile kt - 1)
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+#pragma unroll
+      for (int n = 0; n < 64; ++n) {
+        if (FILL && n % 8 == 0) dma(n / 8, kt + 2, kt & 1);
+        mma(I0{}, z_t, n);
+      }
+      if constexpr (NEXT) {
+        // M (mid-tile): stage kt + 1 landed for every wave (the 8 DMAs of tile kt + 2 just issued
+        // may stay in flight)
+        if constexpr (FILL) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        const char* nxt = smem + ((kt + 1) & 1) * STG;
+        // read r (< 32: even -> k-half 0 frag r / 2 into set 0, odd -> k-half 1 into set S1N)
+        auto rd = [&](int r) __attribute__((always_inline)) {
+          if (r % 2 == 0) read_frag(I0{}, I0{}, r / 2, nxt);
+          else read_frag(s1n_t, I1{}, r / 2, nxt);
+        };
+#pragma unroll
+        for (int n = 0; n < 64; ++n) {
+          if (n < 32) rd(n);  // one per MFMA, first half
+          if (FILL && n % 8 == 0) dma(8 + n / 8, kt + 2, kt & 1);
+          mma(s1_t, F_{}, n);
+        }
+      } else {
+#pragma unroll
+        for (int n = 0; n < 64; ++n) mma(s1_t, F_{}, n);
+      }
+      return;
+    }
 #pragma unroll
     for (int n = 0; n < 64; ++n) mma(I0{}, z_t, n);
     stage_sync();
@@ -209,7 +244,7 @@ gemm4w_kernel(GemmArgs p) {
   for (int g = 0; g < 16; ++g) dma(g, 1, 1);
   asm volatile("s_waitcnt vmcnt(16)" ::: "memory");  // tile 0 (this wave's part); tile 1 in flight
   __builtin_amdgcn_s_barrier();
-  if constexpr (SCHED == 2) {
+  if constexpr (SCHED >= 2) {
 #pragma unroll
     for (int g = 0; g < 16; ++g) {
       read_frag(I0{}, I0{}, g, smem);
@@ -315,8 +350,8 @@ gemm4w_kernel(GemmArgs p) {
   }
 }
 
-// Schedule: SCHED 2 (three fragment sets) when K / 64 is even and >= 4, else SCHED 0;
-// da_gemm4w_variant(1) forces SCHED 0 (bench/gemm4w_ab.py A/B)
+// Schedule where K / 64 is even and >= 4: SCHED 3 (default), or via da_gemm4w_variant (the A/B of
+// bench/gemm4w_ab.py): 1 = SCHED 0, 2 = SCHED 2. Other K: SCHED 0.
 static int g_4w_variant = 0;
 DA_EXPORT int da_gemm4w_variant(int v) {
   const int prev = g_4w_variant;
@@ -327,7 +362,9 @@ DA_EXPORT int da_gemm4w_variant(int v) {
 template <int EPI, typename T>
 static void launch4w_e(const GemmArgs& a, int nt, hipStream_t s) {
   const int nk = a.K / 64;
-  if (g_4w_variant == 0 && nk >= 4 && nk % 2 == 0) gemm4w_kernel<EPI, T, 2><<<dim3(nt), dim3(256), 0, s>>>(a);
+  const bool three = nk >= 4 && nk % 2 == 0;
+  if (three && g_4w_variant == 0) gemm4w_kernel<EPI, T, 3><<<dim3(nt), dim3(256), 0, s>>>(a);
+  else if (three && g_4w_variant == 2) gemm4w_kernel<EPI, T, 2><<<dim3(nt), dim3(256), 0, s>>>(a);
   else gemm4w_kernel<EPI, T, 0><<<dim3(nt), dim3(256), 0, s>>>(a);
 }
 

@@ -997,9 +997,9 @@ def gemm8p_persist(on: int = -1) -> int:
 
 
 def gemm4w_variant(v: int = -1) -> int:
-    """Schedule of the four-wave 256x256 kernel (tile 13, csrc/gemm4w.hip): 0 = three fragment sets
-    where K / 64 is even and >= 4 (default), 1 = two sets always; -1 only queries. Returns the
-    previous setting."""
+    """Schedule of the four-wave 256x256 kernel (tile 13, csrc/gemm4w.hip) where K / 64 is even and
+    >= 4: 0 = three fragment sets, two barriers per K-tile (default), 1 = two sets, 2 = three sets,
+    one barrier; -1 only queries. Returns the previous setting."""
     return int(lib().da_gemm4w_variant(int(v)))
 
 

@@ -83,9 +83,9 @@ def test_gemm8p_tile(M, N, Kd, epi, tile):
 @pytest.mark.parametrize("epi", [K.EPI_NONE, K.EPI_BIAS, K.EPI_GELU, K.EPI_RESID, K.EPI_SWIGLU])
 def test_gemm4w_tile(M, N, Kd, epi):
     """Four-wave 256x256 kernel (tile 13, the A/B arm of csrc/gemm4w.hip; asm MFMAs with AGPR
-    accumulators): both schedules (three fragment sets at K / 64 even >= 4, two sets otherwise /
-    forced) on every epilogue and ragged M / N vs the fp32 reference, and bit-identical to each
-    other (same MFMA order per accumulator)."""
+    accumulators): its schedules (three fragment sets with two / one barriers per K-tile at K / 64
+    even >= 4, two sets otherwise or forced) on every epilogue and ragged M / N vs the fp32
+    reference, and bit-identical to each other (same MFMA order per accumulator)."""
     torch.manual_seed(M + N + epi + 13)
     if epi == K.EPI_SWIGLU:
         N = (N // 32) * 32
@@ -95,12 +95,15 @@ def test_gemm4w_tile(M, N, Kd, epi):
     prev = K.gemm4w_variant(0)
     try:
         got = K.gemm(a, w, bias=bias, epi=epi, resid=resid, tile=13, splits=1)
-        K.gemm4w_variant(1)
-        two = K.gemm(a, w, bias=bias, epi=epi, resid=resid, tile=13, splits=1)
+        others = []
+        for v in (1, 2):
+            K.gemm4w_variant(v)
+            others.append(K.gemm(a, w, bias=bias, epi=epi, resid=resid, tile=13, splits=1))
     finally:
         K.gemm4w_variant(prev)
     _close(got, R.gemm(a, w, bias=bias, epi=epi, resid=resid), atol=0.04)
-    assert torch.equal(got, two)
+    for o in others:
+        assert torch.equal(got, o)
 
 
 @pytest.mark.parametrize("M,N,Kd", [(4100, 4104, 256), (2304, 9216, 192), (3000, 9216, 128), (2600, 3072, 3072)])
