@@ -8,7 +8,6 @@ import json
 import math
 import os
 import sys
-import time
 
 import torch
 

@@ -153,7 +153,7 @@ def check_replicas(rank, world, port, out_path, tp: int = 1):
     import time as _t
     _init(rank, world, port)
     from docagents_amd.engine.engine import Engine
-    from docagents_amd.engine.rpc import EngineClient, EngineCluster
+    from docagents_amd.engine.rpc import EngineCluster
     from docagents_amd.engine.server import EngineGroup, EngineServer, owner_of
     from docagents_amd.models.llama import TPContext
     from docagents_amd.utils import faults

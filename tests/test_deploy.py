@@ -11,7 +11,6 @@ import sys
 import time
 
 import httpx
-import pytest
 
 from docagents_amd.text import multipart
 

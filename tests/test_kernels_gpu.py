@@ -1,5 +1,4 @@
 """Numerics of every gfx950 HIP kernel vs the plain-PyTorch fp32 reference of the same op."""
-import math
 
 import numpy as np
 

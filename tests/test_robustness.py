@@ -5,7 +5,6 @@ processed exactly once, chunks never duplicated by a retried parse), injected fa
 import asyncio
 import datetime as dt
 import json
-import uuid
 
 from docagents_amd.app import Deps
 from docagents_amd.config import Config

@@ -9,7 +9,7 @@ import pytest
 from starlette.testclient import TestClient
 
 from docagents_amd.app import Deps
-from docagents_amd.cache.cache import MemoryCache, QueryResult
+from docagents_amd.cache.cache import MemoryCache
 from docagents_amd.config import Config
 from docagents_amd.services import analysis, gateway, parser, query
 from docagents_amd.store.base import Chunk, Document, SearchResult, Summary, SummaryNotFound

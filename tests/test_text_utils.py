@@ -10,7 +10,7 @@ import pytest
 
 from docagents_amd.cache.cache import MemoryCache, NoOpCache, QueryResult, Source
 from docagents_amd.cache.keys import generate_cache_key, generate_embedding_key
-from docagents_amd.config import Config, load
+from docagents_amd.config import load
 from docagents_amd.text.chunker import Options, chunk_spans, chunk_text
 from docagents_amd.text.preprocess import extract_summary, preprocess_text, truncate_preview
 from docagents_amd.utils.log import new as new_logger, parse_level
