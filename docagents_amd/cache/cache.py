@@ -138,7 +138,12 @@ class KVCache:
     as soon as it is issued and its reply matched in FIFO order by one reader task (RESP answers in
     request order), so concurrent requests share the connection without waiting for each other's
     round trips — the reference's go-redis pools connections for the same reason. A command that
-    times out keeps its place in the FIFO (its late reply is read and dropped)."""
+    times out keeps its place in the FIFO (its late reply is read and dropped). A lost connection
+    fails the commands in flight; the next command reconnects (go-redis's behaviour), at most one
+    attempt per ``RECONNECT_S`` so a dead server costs the callers a fast error, not a connect
+    timeout each."""
+
+    RECONNECT_S = 1.0
 
     def __init__(self, addr: str = "localhost:6379", password: str = "", timeout: float = 5.0):
         host, _, port = addr.rpartition(":")
@@ -148,6 +153,8 @@ class KVCache:
         self.lock = asyncio.Lock()  # write order == FIFO order
         self._fifo: collections.deque = collections.deque()
         self._reader_task = None
+        self._last_attempt = 0.0
+        self.reconnects = 0
 
     async def connect(self):
         self.reader, self.writer = await asyncio.wait_for(asyncio.open_connection(self.host, self.port), self.timeout)
@@ -202,11 +209,29 @@ class KVCache:
                 if not f.done():
                     f.set_exception(err)
 
+    async def _reconnect_locked(self):
+        """(self.lock held) open a new connection after a loss; AUTH goes first in its FIFO."""
+        now = time.monotonic()
+        if self._last_attempt and now - self._last_attempt < self.RECONNECT_S:
+            raise ConnectionError("kv cache not connected (reconnect backoff)")
+        self._last_attempt = now
+        reader, writer = await asyncio.wait_for(asyncio.open_connection(self.host, self.port), self.timeout)
+        self.reader, self.writer = reader, writer
+        self._reader_task = asyncio.ensure_future(self._read_loop(reader))
+        self.reconnects += 1
+        if self.password:
+            auth = asyncio.get_running_loop().create_future()
+            auth.add_done_callback(lambda f: f.cancelled() or f.exception())  # a bad AUTH fails the next command
+            self._fifo.append(auth)
+            writer.write(_resp_cmd("AUTH", self.password))
+
     async def _cmd(self, *parts):
         fut = asyncio.get_running_loop().create_future()
         async with self.lock:
             if self.writer is None:
-                raise ConnectionError("not connected")
+                if self.reader is None:
+                    raise ConnectionError("not connected")
+                await self._reconnect_locked()
             self._fifo.append(fut)
             self.writer.write(_resp_cmd(*parts))
         w = self.writer
@@ -255,3 +280,4 @@ class KVCache:
             except Exception:  # noqa: BLE001
                 pass
             self.writer = None
+        self.reader = None  # closed on purpose: no reconnect

@@ -174,6 +174,43 @@ def test_kernel_debug_build_compiles(tmp_path):
     assert r.returncode == 0, r.stderr[-2000:]
 
 
+def test_kvserver_client_reconnects_after_server_restart():
+    """A KV server restart (same address) costs the client the commands in flight, not the cache:
+    the next command after the backoff reconnects (AUTH first) and the cache works again; while the
+    server is down, commands fail fast instead of hanging."""
+    port = free_port()
+    cmd = [str(binary("da-kvserver")), "--listen", f"127.0.0.1:{port}", "--requirepass", "pw"]
+    p = subprocess.Popen(cmd, stderr=subprocess.DEVNULL)
+    wait_port(port)
+
+    async def go():
+        nonlocal p
+        c = await KVCache(f"127.0.0.1:{port}", "pw", timeout=2.0).connect()
+        c.RECONNECT_S = 0.2
+        await c._cmd("SET", "a", "1", "EX", 100)
+        p.kill()
+        p.wait()
+        with pytest.raises(Exception):
+            await c._cmd("GET", "a")  # the loss surfaces on the command in flight
+        t0 = time.monotonic()
+        with pytest.raises(Exception):
+            await c._cmd("GET", "a")  # server down: a fast failure
+        assert time.monotonic() - t0 < 1.5
+        p = subprocess.Popen(cmd, stderr=subprocess.DEVNULL)
+        wait_port(port)
+        await asyncio.sleep(0.3)  # past the backoff
+        assert await c._cmd("GET", "a") is None  # a fresh server: reconnected, authenticated
+        await c._cmd("SET", "b", "2", "EX", 100)
+        assert await c._cmd("GET", "b") == b"2"
+        assert c.reconnects >= 1
+        await c.close()
+    try:
+        asyncio.run(go())
+    finally:
+        p.kill()
+        p.wait()
+
+
 def test_kvserver_client_pipelines_concurrent_commands(kvserver):
     """The RESP client pipelines: 300 concurrent SET / GET from one connection (replies matched in
     FIFO order), an error reply fails only its own command, and a closed server fails every
