@@ -478,7 +478,7 @@ def main():
     from docagents_amd.parallel import hbm_plan as HP
     plan = HP.bench_plan(HP.BenchArgs(enc=a.enc, llm=a.llm, batch=a.batch, max_new=a.max_new, index_rows=a.index_rows,
                                       enc_dtype=a.enc_dtype, tp=TP, overlap=overlap,
-                                      tp70b={"on": True, "off": False}.get(a.tp70b)), W)
+                                      tp70b={"on": True, "off": False}.get(a.tp70b), ingest=a.ingest_docs > 0), W)
     out = {
         "metric": METRIC, "value": round(qps, 3), "unit": "queries/s", "n_gpus": n_phys, "world_size": W,
         "oversubscribed": n_phys < W, "steps": a.steps,

@@ -12,11 +12,18 @@ Every term is the allocation the code makes, by the formula it makes it with:
   decode workspace    ``Generator.workspace_bytes`` (split-K / split-KV partials)
   prefill transient   one ``max_prefill_tokens`` chunk of activations (x, h, qkv, attention out,
                       gate/up out) — freed between chunks, counted once
-  index shard         ``FlatIndex``: rows x (dim bf16 + slot int32 + id int64), x 1.5 growth slack
+  index shard         ``FlatIndex``: rows x (dim bf16 + slot int32 + id int64), built at exactly ``rows``;
+                      with ingest the first add grows it 1.5x and the copy holds old + new: +1.5x in
+                      the headline, +0.5x after it (config 4 at 1.25M x 1024 peaked 3.3 GB over a
+                      plan without the copy)
   index build         ``bench.shard_vectors``: the fp32 draw and its normalised copy, then bf16
                       (setup only: before the first prefill)
   encoder             parameters (+ a second copy for the fp8 / fp16 forms)
   xGMI communicators  2 x (2 x max_bytes staging) + signals per communicator
+  runtime             RUNTIME_BYTES for what no formula above sizes: the captured graphs' private
+                      pools (decode buckets, encoder buckets), RoPE tables, sampler / prompt buffers,
+                      the allocator's block rounding (config 4 fp16 at 1.25M rows measured 0.7 GB
+                      over the formula terms)
 Reference: the reference sizes nothing (hosted OpenAI / Postgres); docker-compose.yml:84-85,105-106
 scales replicas, which is the headline's data-parallel layout here.
 """
@@ -30,6 +37,7 @@ GB = 1e9
 HBM_BYTES = 288 * GB
 PLAN_LIMIT_BYTES = 270 * GB  # what a phase may hold: the rest is the runtime, RCCL and fragmentation
 MAX_PREFILL_TOKENS = 65536   # Generator.max_prefill_tokens default
+RUNTIME_BYTES = 2 * GB       # graph pools, tables, small buffers, allocator rounding (every phase)
 TP70B_BATCHES = (1, 16)      # tp_decode_70b: decode batches timed
 TP70B_WORLD = 8              # tp_decode_70b runs at N = 8 (BASELINE config 5: Llama-3-70B TP=8)
 
@@ -64,7 +72,7 @@ def encoder_bytes(cfg: EncoderConfig, enc_dtype: str = "bf16") -> int:
 
 
 def index_bytes(rows: int, dim: int) -> int:
-    return int(rows * (dim * 2 + 4 + 8) * 1.5)
+    return rows * (dim * 2 + 4 + 8)
 
 
 def index_build_bytes(rows: int, dim: int) -> int:
@@ -97,6 +105,7 @@ class BenchArgs:
     overlap: bool = False
     max_seq: int = 4096
     tp70b: bool | None = None  # None: bench.py's "auto" (on at N = 8)
+    ingest: bool = True        # --ingest-docs > 0: documents are added to the index (it grows)
 
 
 def bench_plan(a: BenchArgs, world: int, release_engine_kv: bool = True) -> dict:
@@ -108,6 +117,7 @@ def bench_plan(a: BenchArgs, world: int, release_engine_kv: bool = True) -> dict
     eng_seq = min(a.max_seq, dec.max_pos)
     slots = (2 if a.overlap else 1) * a.batch + 4  # Engine: alloc_cache((2 if overlap) * max_batch + 4)
     resident = {  # held by the engine for the whole run
+        "runtime": RUNTIME_BYTES,
         "encoder": encoder_bytes(enc, a.enc_dtype),
         "decoder_weights": decoder_weight_bytes(dec, tp),
         "index": index_bytes(a.index_rows, enc.hidden),
@@ -120,8 +130,12 @@ def bench_plan(a: BenchArgs, world: int, release_engine_kv: bool = True) -> dict
     head = dict(resident)
     head.update({"engine_kv": engine_kv, "workspace": workspace_bytes(dec, a.batch, eng_seq, tp),
                  "prefill_transient": prefill_transient_bytes(dec, tp)})
+    if a.ingest:  # FlatIndex._grow at the first add: the 1.5x copy beside the old buffer
+        head["index_growth"] = int(1.5 * resident["index"])
     phases["headline"] = head
     kept = dict(resident)
+    if a.ingest:
+        kept["index_growth"] = int(0.5 * resident["index"])
     if not release_engine_kv:
         kept["engine_kv"] = engine_kv
     kept["workspace"] = head["workspace"]  # the shared workspace only grows

@@ -58,7 +58,21 @@ def test_kv_formula_matches_allocation():
 def test_setup_phase_counts_the_index_build():
     """The config-4 rehearsal's per-rank peak (34.0 GB, profiles/r6/rehearsal_config4_*) came from
     building a 1.25M x 1024 shard (fp32 draw + normalised copy), not from the QA step."""
-    a = HP.BenchArgs(enc="bge-large", enc_dtype="fp16", batch=4, index_rows=1_250_000, max_new=8, tp70b=False)
+    a = HP.BenchArgs(enc="bge-large", enc_dtype="fp16", batch=4, index_rows=1_250_000, max_new=8, tp70b=False,
+                     ingest=False)
     p = HP.bench_plan(a, 8)
     assert "tp_decode_70b" not in p
     assert p["setup"]["total"] >= 34.0e9 > p["headline"]["total"]
+
+
+def test_index_growth_and_runtime_cover_the_measured_config4_peak():
+    """BASELINE config 4 on one GPU (BGE-large fp16, 1.25M x 1024 shard, with ingest) measured a
+    233.8 GB headline peak (profiles/r6/configs/bench_config4_bge_large_fp16_1p25m_r6_head.json): the plan counts the shard's
+    growth copy at the first ingest and the runtime slack, so it bounds that peak; without ingest
+    the shard never grows."""
+    a = HP.BenchArgs(enc="bge-large", enc_dtype="fp16", index_rows=1_250_000)
+    p = HP.bench_plan(a, 1)["headline"]
+    assert p["total"] >= 233.8e9 and p["index_growth"] == int(1.5 * p["index"])
+    assert HP.check(HP.bench_plan(a, 1)) == []
+    q = HP.bench_plan(HP.BenchArgs(enc="bge-large", enc_dtype="fp16", index_rows=1_250_000, ingest=False), 1)
+    assert "index_growth" not in q["headline"]
