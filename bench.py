@@ -7,10 +7,14 @@ documents are spread over all shards, so at N > 1 most searches read several ran
 
 One timed step = every GPU serves B cache-miss queries end to end (the reference's query path,
 cmd/query/main.go:44-136, minus the cache hit): tokenize -> BGE-base encode (HIP kernels) ->
-search plane: query rows sent to the shards owning their filter documents -> fused cosine +
-doc-filter + threshold + top-k on each (vecsearch.hip) -> merge -> build the Answer prompt from the top-k chunks (pre-tokenized at ingest)
--> Phi-3-mini prefill (~2.8k tokens/query) + decode MAX_NEW tokens at T=0.2 (HIP kernels, HIP
-graphs) -> confidence = avg similarity x mean token probability -> detokenize.
+search (N = 1: the local shard through the search plane; N > 1: the lock-step RCCL sharded search,
+C2 all-gather of the query rows, every shard scans them, C1 all-gather of the per-shard top-k,
+device merge; ``--search plane`` keeps the point-to-point plane) -> fused cosine + doc-filter +
+threshold + top-k on each shard (vecsearch.hip) -> build the Answer prompt from the top-k chunks
+(pre-tokenized at ingest) -> Phi-3-mini prefill (~2.9k tokens/query) + decode MAX_NEW tokens at
+T=0.2 (HIP kernels, HIP graphs) -> confidence = avg similarity x mean token probability ->
+detokenize. After the timed steps at N > 1, the multi-GPU blocks (parallel/collective_bench.py)
+time the fabric mechanisms into the same JSON line.
 
 Synthetic data (no network): random-init weights of the named architectures, random unit vectors
 for the 100k background chunks per GPU (their token ids drawn from the locally trained BPE vocab),
@@ -22,10 +26,9 @@ Launch: python bench.py [--gpus N --steps K --warmup W]. With N > 1 and no WORLD
 environment, this process launches N ranks itself (python -m torch.distributed.run, one rank per GPU)
 before anything touches the GPU, relays their output and exits with their status; under an external
 torchrun (WORLD_SIZE set) it is one rank, and WORLD_SIZE != --gpus is an error. Every rank is an
-independent replica (its own engine), the index is sharded one shard per rank, and every search goes
-through the production search plane (parallel/search_plane.py: routed to the shards that own the
-query's documents, point to point); the JSON line reports the process-group backend and the number
-of ranks that joined (ranks_seen, an all-reduce of ones).
+independent replica (its own engine) and the index is sharded one shard per rank; the JSON line
+reports the process-group backend and the number of ranks that joined (ranks_seen, an all-reduce of
+ones).
 """
 from __future__ import annotations
 
