@@ -43,6 +43,16 @@ from docagents_amd.text.synthetic import TextGen  # noqa: E402
 from docagents_amd.utils import timeline as req_timeline  # noqa: E402
 
 
+def _tenths(done_at: list[float], span: float) -> list[float] | None:
+    """Completions per tenth of a run of ``span`` seconds, as q/s (done_at: seconds from its start)."""
+    if span <= 0:
+        return None
+    n = [0] * 10
+    for x in done_at:
+        n[min(9, max(0, int(x * 10 / span)))] += 1
+    return [round(c / (span / 10), 1) for c in n]
+
+
 def _cpu_sampler(stop, out: dict, every: float = 0.5):
     """Sample the CPU use (cores) of this process and its descendants until ``stop``; ``out`` gets
     {"<name>#<pid>": {"mean": m, "max": x}} keyed by the service name from the command line."""
@@ -274,7 +284,13 @@ async def run(gw: str, docs: int, words: int, queries: int, concurrency: int, to
         cpu_out: dict = {}
         cpu_thr = threading.Thread(target=_cpu_sampler, args=(cpu_stop, cpu_out), daemon=True)
         cpu_thr.start()
-        miss = await asyncio.gather(*[ask(b) for b in bodies])
+        miss_done: list[float] = []
+
+        async def ask_loaded(b):
+            r = await ask(b)
+            miss_done.append(time.perf_counter() - t1)
+            return r
+        miss = await asyncio.gather(*[ask_loaded(b) for b in bodies])
         t_miss = time.perf_counter() - t1
         cpu_stop.set()
         cpu_thr.join(5)
@@ -312,6 +328,8 @@ async def run(gw: str, docs: int, words: int, queries: int, concurrency: int, to
         "serial_stage_mean_ms": serial_stages,
         "queries": queries, "query_errors": sum(1 for st, _ in miss if st != 200),
         "qa_qps": round(len(miss_ok) / t_miss, 2) if t_miss > 0 else None,
+        # completions per tenth of the loaded run (q/s): flat = steady state (a soak shows no drift)
+        "qa_qps_tenths": _tenths(miss_done, t_miss),
         "cache_miss_p50_ms": _r(statistics.median(miss_ok) if miss_ok else None),
         "cache_miss_p99_ms": _r(_pct(miss_ok, 99)),
         "cache_hit_p50_ms": _r(statistics.median(hit_ok) if hit_ok else None),
