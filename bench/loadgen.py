@@ -290,7 +290,15 @@ async def run(gw: str, docs: int, words: int, queries: int, concurrency: int, to
             r = await ask(b)
             miss_done.append(time.perf_counter() - t1)
             return r
+
+        async def progress():  # a long (soak) run reports every 30 s
+            while True:
+                await asyncio.sleep(30)
+                print(f"[loadgen] {len(miss_done)}/{len(bodies)} queries done, "
+                      f"{time.perf_counter() - t1:.0f} s", file=sys.stderr, flush=True)
+        prog = asyncio.ensure_future(progress())
         miss = await asyncio.gather(*[ask_loaded(b) for b in bodies])
+        prog.cancel()
         t_miss = time.perf_counter() - t1
         cpu_stop.set()
         cpu_thr.join(5)
